@@ -1,0 +1,173 @@
+"""Model geometry + TF-variable table of the executed graph (oracle copy) — TEST INFRASTRUCTURE.
+
+Restates the variable scopes/creation order of the reference so that the
+product's C-ABI layout (``svae_param_layout``) can be checked against it:
+
+* ``phi/inference_step_t``            — inference_ladder (sequential_vae.py:1573-1609)
+* ``theta/generative_encoder_step_t`` — compute_encodings (sequential_vae.py:1757-1775), t >= 1
+* ``theta/generative_step_t``         — split_latent + generator_ladder (sequential_vae.py:1683-1727)
+
+Names follow tf.contrib.layers' default scope naming (``Conv``, ``Conv_1``,
+``BatchNorm``, ``fully_connected_2``, ``Conv2d_transpose_3`` …).  ``dead`` marks
+variables created by the reference but never on the executed path (the last
+inference level's conv + fc_bn_lrelu, sequential_vae.py:1602-1605, whose output
+is unused because the level-3 heads read ``ladder``); ``zero_grad`` marks the
+conv/FC biases that sit in front of a BatchNorm (their gradient is identically
+zero: BN subtracts the batch mean).
+"""
+import numpy as np
+
+PRESETS = {
+    # sequential_vae.py:201-258 defaults == netname c_inhomog (:727) / sequential_vae_celebA_inhomog (:671)
+    "celeba": dict(H=64, W=64, C=3, levels=4, filter_sizes=[3, 32, 64, 128, 384, 512],
+                   latent_dims=[3, 3, 3, 3], mc_steps=8, batch=128, range=(-1.0, 1.0)),
+    # sequential_vae_lsun (:712-714)
+    "lsun": dict(H=64, W=64, C=3, levels=4, filter_sizes=[3, 32, 64, 128, 384, 512],
+                 latent_dims=[20, 30, 30, 30], mc_steps=8, batch=256, range=(-1.0, 1.0)),
+    # m_* 3-level geometry (:842-848), latent [8,8,8] (:815), one step
+    "mnist_1step": dict(H=32, W=32, C=1, levels=3, filter_sizes=[1, 64, 128, 192, 256],
+                        latent_dims=[8, 8, 8], mc_steps=1, batch=64, range=(0.0, 1.0)),
+    # small geometry for fast parity tests (same code path as celeba: 4 levels)
+    "tiny": dict(H=32, W=32, C=3, levels=4, filter_sizes=[3, 8, 8, 16, 24, 16],
+                 latent_dims=[2, 2, 3, 2], mc_steps=3, batch=4, range=(-1.0, 1.0)),
+}
+
+DEFAULTS = dict(intermediate_reconstruction=True, first_step_loss_coeff=1.0,
+                latent_prior_stddev=1.0, latent_mean_clip=float("inf"),
+                min_highway=0.0, max_highway=1.0)
+
+
+def make_config(preset="celeba", **over):
+    cfg = dict(DEFAULTS)
+    cfg.update(PRESETS[preset])
+    cfg.update(over)
+    L = cfg["levels"]
+    cfg["image_sizes"] = [cfg["H"] // (2 ** i) for i in range(L + 1)]
+    cfg["latent_dim"] = int(sum(cfg["latent_dims"]))
+    assert len(cfg["filter_sizes"]) == L + 2 and len(cfg["latent_dims"]) == L
+    return cfg
+
+
+class _Scope:
+    def __init__(self, prefix, out):
+        self.prefix, self.out = prefix, out
+        self.cnt = {}
+
+    def _name(self, kind):
+        i = self.cnt.get(kind, 0)
+        self.cnt[kind] = i + 1
+        return kind if i == 0 else "%s_%d" % (kind, i)
+
+    def add(self, kind, entries, dead=False):
+        base = self._name(kind)
+        names = []
+        for suffix, shape, init, zero_grad in entries:
+            n = "%s/%s/%s" % (self.prefix, base, suffix)
+            self.out.append(dict(name=n, shape=tuple(int(s) for s in shape), init=init,
+                                 dead=dead, zero_grad=zero_grad or dead))
+            names.append(n)
+        return names
+
+    # abstract_network.py:17-24 / 55-71
+    def conv_bn(self, shape, transpose=False, dead=False):
+        kind = "Conv2d_transpose" if transpose else "Conv"
+        cout = shape[2] if transpose else shape[3]
+        w, b = self.add(kind, [("weights", shape, "normal0.02", False), ("biases", (cout,), "zeros", True)], dead)
+        (beta,) = self.add("BatchNorm", [("beta", (cout,), "zeros", False)], dead)
+        return dict(w=w, b=b, beta=beta)
+
+    def fc_bn(self, nin, nout, dead=False):
+        w, b = self.add("fully_connected", [("weights", (nin, nout), "normal0.02", False),
+                                            ("biases", (nout,), "zeros", True)], dead)
+        (beta,) = self.add("BatchNorm", [("beta", (nout,), "zeros", False)], dead)
+        return dict(w=w, b=b, beta=beta)
+
+    def fc(self, nin, nout):  # layers.fully_connected default init (xavier)
+        w, b = self.add("fully_connected", [("weights", (nin, nout), "glorot", False),
+                                            ("biases", (nout,), "zeros", False)])
+        return dict(w=w, b=b)
+
+    def convt_plain(self, shape):  # conv2d_t with default (xavier) init, sequential_vae.py:1720,1727
+        w, b = self.add("Conv2d_transpose", [("weights", shape, "glorot", False),
+                                             ("biases", (shape[2],), "zeros", False)])
+        return dict(w=w, b=b)
+
+
+def build_params(cfg):
+    """Returns (table, struct): ``table`` is the ordered variable list, ``struct``
+    the per-step name map used by model.py / torch_twin.py."""
+    L, F, D, S = cfg["levels"], cfg["filter_sizes"], cfg["latent_dims"], cfg["image_sizes"]
+    C = cfg["C"]
+    table, struct = [], []
+    for t in range(cfg["mc_steps"]):
+        st = {}
+        # ---- phi: inference_ladder (sequential_vae.py:1585-1609)
+        sc = _Scope("phi/inference_step_%d" % t, table)
+        inf = []
+        cin = F[0]
+        for lvl in range(L - 1):
+            a = sc.conv_bn((4, 4, cin, F[lvl + 1]))
+            b = sc.conv_bn((4, 4, F[lvl + 1], F[lvl + 1]))
+            nflat = S[lvl + 1] * S[lvl + 1] * F[lvl + 1]
+            hm = sc.fc(nflat, D[lvl])
+            hs = sc.fc(nflat, D[lvl])
+            inf.append(dict(a=a, b=b, mean=hm, std=hs))
+            cin = F[lvl + 1]
+        dead_conv = sc.conv_bn((4, 4, F[L - 1], F[L - 1]), dead=True)
+        dead_fc = sc.fc_bn(S[L] * S[L] * F[L - 1], F[L], dead=True)
+        nflat = S[L - 1] * S[L - 1] * F[L - 1]
+        hm = sc.fc(nflat, D[L - 1])
+        hs = sc.fc(nflat, D[L - 1])
+        st["inference"] = dict(levels=inf, last_mean=hm, last_std=hs, dead=[dead_conv, dead_fc])
+        # ---- theta: compute_encodings (sequential_vae.py:1764-1775), only for t >= 1
+        if t >= 1:
+            sc = _Scope("theta/generative_encoder_step_%d" % t, table)
+            enc = []
+            cin = F[0]
+            for lvl in range(L - 1):
+                a = sc.conv_bn((4, 4, cin, F[lvl + 1]))
+                b = sc.conv_bn((4, 4, F[lvl + 1], F[lvl + 1]))
+                enc.append(dict(a=a, b=b))
+                cin = F[lvl + 1]
+            c = sc.conv_bn((4, 4, F[L - 1], F[L - 1]))
+            fcl = sc.fc_bn(S[L] * S[L] * F[L - 1], F[L])
+            st["encoder"] = dict(levels=enc, last_conv=c, last_fc=fcl)
+        # ---- theta: split_latent + generator_ladder (sequential_vae.py:1689-1727)
+        sc = _Scope("theta/generative_step_%d" % t, table)
+        split = []
+        for i in range(L - 1):
+            split.append(sc.fc_bn(D[i], S[i + 1] * S[i + 1] * F[i + 1]))
+        split.append(sc.fc_bn(D[L - 1], F[L + 1]))
+        top_in = F[L + 1] + (F[L] if t >= 1 else 0)
+        top = sc.fc_bn(top_in, S[L] * S[L] * F[L])
+        dec = []
+        cin = F[L]
+        for lvl in range(L - 2, -1, -1):
+            s2 = sc.conv_bn((4, 4, F[lvl + 1], cin), transpose=True)
+            s1 = sc.conv_bn((4, 4, F[lvl + 1], 2 * F[lvl + 1]), transpose=True)
+            dec.append(dict(level=lvl, s2=s2, s1=s1))
+            cin = F[lvl + 1]
+        out = sc.convt_plain((4, 4, C, F[1]))
+        ratio = sc.convt_plain((4, 4, 1, F[1])) if t >= 1 else None
+        st["generator"] = dict(split=split, top=top, levels=dec, out=out, ratio=ratio)
+        struct.append(st)
+    return table, struct
+
+
+def init_params(cfg, seed=0, dtype=np.float64):
+    from .weightgen import generate
+    table, struct = build_params(cfg)
+    params = {p["name"]: generate(p["name"], p["shape"], p["init"], seed).astype(dtype) for p in table}
+    return table, struct, params
+
+
+def make_inputs(cfg, batch=None, seed_x=0, seed_eps=1):
+    """Synthetic batch of SURVEY §8d: x ~ U[range] (PCG64 seed 0), target = x,
+    eps ~ N(0,1) [T,B,Dz] (PCG64 seed 1)."""
+    B = batch or cfg["batch"]
+    lo, hi = cfg["range"]
+    rx = np.random.default_rng(seed_x)
+    x = rx.uniform(lo, hi, size=(B, cfg["H"], cfg["W"], cfg["C"])).astype(np.float32)
+    re = np.random.default_rng(seed_eps)
+    eps = re.standard_normal(size=(cfg["mc_steps"], B, cfg["latent_dim"])).astype(np.float32)
+    return x, x.copy(), eps

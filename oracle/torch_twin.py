@@ -1,0 +1,160 @@
+"""PyTorch-CPU autograd twin of the Sequential-VAE training subgraph — TEST INFRASTRUCTURE.
+
+Second, independent restatement of the executed graph (sequential_vae.py:877-1212,
+1537-1842; abstract_network.py:8-71), NCHW internally with explicit NHWC
+flatten order for every FC input.  Used (a) to cross-check oracle/model.py and
+(b) as the CPU throughput baseline in bench.py (``cpu_baseline.kind = "port"``):
+the reference's own TF-CPU path cannot run here (no TensorFlow).
+"""
+import torch
+import torch.nn.functional as Fn
+
+
+def _same(n_in, k, s):
+    n_out = -(-n_in // s)
+    total = max((n_out - 1) * s + k - n_in, 0)
+    return n_out, total // 2, total - total // 2
+
+
+def conv2d_same(x, w_tf, s):
+    """TF conv2d SAME; w_tf [kh,kw,Cin,Cout]; x NCHW."""
+    k = w_tf.shape[0]
+    _, pb, pa = _same(x.shape[2], k, s)
+    xp = Fn.pad(x, (pb, pa, pb, pa))
+    return Fn.conv2d(xp, w_tf.permute(3, 2, 0, 1), stride=s)
+
+
+def conv2d_t_same(x, w_tf, s):
+    """TF conv2d_transpose SAME; w_tf [kh,kw,Cout,Cin]; out = full[pb : pb + H*s]."""
+    k = w_tf.shape[0]
+    Ho = x.shape[2] * s
+    _, pb, _ = _same(Ho, k, s)
+    full = Fn.conv_transpose2d(x, w_tf.permute(3, 2, 0, 1), stride=s)
+    return full[:, :, pb:pb + Ho, pb:pb + Ho]
+
+
+def bn_train(x, beta, eps=1e-3):
+    dims = [0, 2, 3] if x.dim() == 4 else [0]
+    m = x.mean(dim=dims, keepdim=True)
+    v = ((x - m) ** 2).mean(dim=dims, keepdim=True)
+    shape = [1, -1, 1, 1] if x.dim() == 4 else [1, -1]
+    return (x - m) / torch.sqrt(v + eps) + beta.view(shape)
+
+
+def lrelu(x):
+    return torch.maximum(torch.minimum(x * 0.1, torch.zeros_like(x)), x)
+
+
+def nhwc_flatten(x):
+    return x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)
+
+
+def nhwc_unflatten(x, S, C):
+    return x.reshape(x.shape[0], S, S, C).permute(0, 3, 1, 2)
+
+
+class Twin:
+    def __init__(self, cfg, struct, params, dtype=torch.float32, requires_grad=True):
+        self.cfg, self.struct = cfg, struct
+        self.P = {k: torch.tensor(v, dtype=dtype, requires_grad=requires_grad) for k, v in params.items()}
+        self.dtype = dtype
+
+    def _cba(self, x, lay, s, act, transpose=False, residual=None):
+        P = self.P
+        y = (conv2d_t_same if transpose else conv2d_same)(x, P[lay["w"]], s)
+        y = y + P[lay["b"]].view(1, -1, 1, 1)
+        y = bn_train(y, P[lay["beta"]])
+        if residual is not None:
+            y = y + residual
+        if act == "lrelu":
+            y = lrelu(y)
+        elif act == "relu":
+            y = torch.relu(y)
+        return y
+
+    def _fcbn(self, x, lay):
+        P = self.P
+        return lrelu(bn_train(x @ P[lay["w"]] + P[lay["b"]], P[lay["beta"]]))
+
+    def _fc(self, x, lay):
+        return x @ self.P[lay["w"]] + self.P[lay["b"]]
+
+    def inference(self, st, x):
+        L, clip = self.cfg["levels"], self.cfg["latent_mean_clip"]
+        cur, means, stds, ladder = x, [], [], None
+        for lvl in range(L - 1):
+            lv = st["levels"][lvl]
+            cur = self._cba(self._cba(cur, lv["a"], 2, "lrelu"), lv["b"], 1, "lrelu")
+            ladder = nhwc_flatten(cur)
+            means.append(self._fc(ladder, lv["mean"]).clamp(-clip, clip))
+            stds.append(torch.sigmoid(self._fc(ladder, lv["std"])))
+        means.append(self._fc(ladder, st["last_mean"]).clamp(-clip, clip))
+        stds.append(torch.sigmoid(self._fc(ladder, st["last_std"])))
+        return torch.cat(means, 1), torch.cat(stds, 1)
+
+    def encodings(self, st, xprev):
+        L = self.cfg["levels"]
+        cur, encs = xprev, [xprev]
+        for lvl in range(L - 1):
+            lv = st["levels"][lvl]
+            cur = self._cba(self._cba(cur, lv["a"], 2, "lrelu"), lv["b"], 1, "lrelu")
+            encs.append(cur)
+        cur = nhwc_flatten(self._cba(cur, st["last_conv"], 2, "lrelu"))
+        encs.append(self._fcbn(cur, st["last_fc"]))
+        return encs
+
+    def generator(self, st, xprev, z, enc_st):
+        cfg = self.cfg
+        L, F, S = cfg["levels"], cfg["filter_sizes"], cfg["image_sizes"]
+        encs = self.encodings(enc_st, xprev) if xprev is not None else None
+        parts = torch.split(z, cfg["latent_dims"], dim=1)
+        lad = [nhwc_unflatten(self._fcbn(parts[i], st["split"][i]), S[i + 1], F[i + 1]) for i in range(L - 1)]
+        lad.append(self._fcbn(parts[L - 1], st["split"][L - 1]))
+        cur = torch.cat([encs[L], lad[L - 1]], 1) if encs is not None else lad[L - 1]
+        cur = nhwc_unflatten(self._fcbn(cur, st["top"]), S[L], F[L])
+        for dl in st["levels"]:
+            lvl = dl["level"]
+            res = encs[lvl + 1] if encs is not None else None
+            d = self._cba(cur, dl["s2"], 2, "relu", transpose=True, residual=res)
+            cur = self._cba(torch.cat([d, lad[lvl]], 1), dl["s1"], 1, "relu", transpose=True)
+        lo, hi = cfg["range"]
+        P = self.P
+        o = torch.sigmoid(conv2d_t_same(cur, P[st["out"]["w"]], 2) + P[st["out"]["b"]].view(1, -1, 1, 1))
+        out = (hi - lo) * o + lo
+        if encs is not None:
+            r = torch.sigmoid(conv2d_t_same(cur, P[st["ratio"]["w"]], 2) + P[st["ratio"]["b"]].view(1, -1, 1, 1))
+            r = cfg["min_highway"] + (cfg["max_highway"] - cfg["min_highway"]) * r.expand(-1, cfg["C"], -1, -1)
+            out = r * out + (1 - r) * encs[0]
+        return out
+
+    def step(self, x_nhwc, target_nhwc, eps, reg_coeff=1.0, backward=True):
+        cfg = self.cfg
+        x = torch.as_tensor(x_nhwc, dtype=self.dtype).permute(0, 3, 1, 2)
+        tgt = torch.as_tensor(target_nhwc, dtype=self.dtype).permute(0, 3, 1, 2)
+        eps = torch.as_tensor(eps, dtype=self.dtype)
+        Tn, p2 = cfg["mc_steps"], cfg["latent_prior_stddev"] ** 2
+        loss, prev, recs, kls, xhats = 0.0, None, [], [], []
+        for t in range(Tn):
+            st = self.struct[t]
+            mu, sig = self.inference(st["inference"], x)
+            z = mu + sig * eps[t]
+            xh = self.generator(st["generator"], prev, z, st.get("encoder"))
+            rec = ((xh - tgt) ** 2).mean()
+            kl = (-0.5 - torch.log(sig) + 0.5 * sig ** 2 / p2 + 0.5 * mu ** 2 / p2).mean(1).mean()
+            c = cfg["first_step_loss_coeff"] if t == 0 else 1.0
+            if cfg["intermediate_reconstruction"] or t == Tn - 1:
+                loss = loss + 16.0 * c * rec
+            loss = loss + reg_coeff * c * kl
+            recs.append(rec.detach())
+            kls.append(kl.detach())
+            xhats.append(xh.detach().permute(0, 2, 3, 1))
+            prev = xh
+        out = dict(loss=float(loss), final_loss=float(recs[-1]), recon=[float(r) for r in recs],
+                   kl=[float(k) for k in kls], xhat=[h.numpy() for h in xhats])
+        if backward:
+            for p in self.P.values():
+                p.grad = None
+            loss.backward()
+            out["grads"] = {k: (p.grad.numpy() if p.grad is not None else torch.zeros_like(p).numpy())
+                            for k, p in self.P.items()}
+        return out
