@@ -1,0 +1,120 @@
+/* libsvae_hip.so — C ABI of the MI355X Sequential-VAE training-step engine.
+ *
+ * Drop-in boundary.  The reference has no FFI: its path sits
+ * behind the Python methods
+ *     SequentialVAE.train(input_batch, batch_target) -> float   sequential_vae.py:1341-1375
+ *     SequentialVAE.test(input_batch) -> ndarray[B,H,W,C]        sequential_vae.py:1381-1391
+ * which run  sess.run([train_op, loss, final_loss])  (sequential_vae.py:1365) over the
+ * graph built by construct_network (sequential_vae.py:877-984).  The Python mirror of that
+ * interface (sequential-variational-autoencoder_amd/sequential_vae.py) binds the entry points
+ * below through ctypes; the binding a maintainer would add is shown in INTEGRATION.md.
+ *
+ * Conventions: every function returns 0 on success or a negative svae_status; the
+ * message is available from svae_last_error(ctx) (ctx may be NULL for create/layout
+ * errors).  No function calls exit().  All device work is enqueued on the caller's
+ * stream (hipStream_t passed as void*); no call allocates or synchronises on the hot
+ * path.  Tensors are NHWC fp32, row-major.
+ */
+#ifndef SVAE_HIP_H
+#define SVAE_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum svae_status {
+  SVAE_OK = 0,
+  SVAE_EBADCONFIG = -1, /* config rejected (sequential_vae.py:861-862, :1617-1627 analogue) */
+  SVAE_EBADARG = -2,    /* null pointer / unbound buffers / bad index */
+  SVAE_EHIP = -3,       /* HIP runtime error */
+  SVAE_ENOMEM = -4      /* device allocation failed */
+};
+
+/* Geometry + hyper-parameters of one SequentialVAE (sequential_vae.py:201-258, netname
+ * overrides :281-862).  Only the executed-path knobs of the BASELINE configs. */
+typedef struct svae_config {
+  int32_t batch;            /* per-GPU batch B (BN statistics are per shard) */
+  int32_t height, width, channels;   /* dataset.data_dims */
+  int32_t levels;           /* vlae_levels L */
+  int32_t mc_steps;         /* T */
+  int32_t filter_sizes[10]; /* L+2 entries */
+  int32_t latent_dims[8];   /* L entries */
+  int32_t intermediate_reconstruction;
+  float first_step_loss_coeff;
+  float latent_prior_stddev;
+  float latent_mean_clip;   /* +inf = no clip */
+  float range_lo, range_hi; /* dataset.range */
+  float min_highway, max_highway;
+  int32_t dtype;            /* 0 = fp32 (parity) */
+} svae_config;
+
+typedef struct svae_param_desc {
+  char name[96];            /* TF variable name, e.g. "phi/inference_step_0/Conv/weights" */
+  int32_t ndim;
+  int32_t shape[4];         /* TF shape: conv [kh,kw,Cin,Cout], conv-T [kh,kw,Cout,Cin], FC [in,out] */
+  int64_t offset;           /* element offset in the flat parameter / gradient buffers */
+  int32_t init;             /* 0 zeros, 1 normal(0,0.02), 2 glorot-uniform */
+  int32_t flags;            /* bit0: dead (never on the executed path), bit1: gradient identically 0 */
+} svae_param_desc;
+
+typedef struct svae_ctx svae_ctx;
+
+/* Buffers readable through svae_copy_out. */
+enum svae_buffer {
+  SVAE_BUF_XHAT = 0,     /* training_mles[t]  [B,H,W,C] (sequential_vae.py:962) */
+  SVAE_BUF_MU = 1,       /* latent mean (pre-clip) [B,Dz] */
+  SVAE_BUF_SIGMA = 2,    /* latent stddev [B,Dz] */
+  SVAE_BUF_Z = 3,        /* latent sample [B,Dz] */
+  SVAE_BUF_STEP_STATS = 4, /* [T][2] = (mean_b recon_t, mean_b KL_t)   (:1163-1164) */
+  SVAE_BUF_REC_IMG = 5,  /* [B] per-image recon of step t */
+  SVAE_BUF_KL_IMG = 6    /* [B] per-image KL of step t */
+};
+
+/* Parameter table (pure host; callable without a GPU).  Live (trainable, non-zero-grad)
+ * tensors occupy [0, n_live); dead / pre-BN-bias tensors the tail [n_live, n_total). */
+int svae_param_count(const svae_config* cfg, int64_t* n_total, int64_t* n_live, int32_t* n_tensors);
+int svae_param_layout(const svae_config* cfg, svae_param_desc* out, int32_t cap);
+
+/* Context: owns the activation arena (sized for cfg->batch) and Adam state. */
+int svae_create(const svae_config* cfg, int device, svae_ctx** out);
+int svae_destroy(svae_ctx* ctx);
+const char* svae_last_error(const svae_ctx* ctx);
+/* Borrow caller-owned flat fp32 buffers (n_total elements each). */
+int svae_bind(svae_ctx* ctx, float* params, float* grads);
+int64_t svae_workspace_bytes(const svae_ctx* ctx);
+
+/* Forward of the whole chain: x, target [B,H,W,C]; eps [T,B,Dz] or NULL (device Philox).
+ * reg_coeff as fed at sequential_vae.py:1357. */
+int svae_forward(svae_ctx* ctx, const float* x, const float* target, const float* eps, float reg_coeff,
+                 void* stream);
+/* d self.loss / d every variable (sequential_vae.py:1273) into the bound gradient buffer. */
+int svae_backward(svae_ctx* ctx, void* stream);
+/* clip(+-clip) + TF Adam on the live region (sequential_vae.py:1274-1276); step >= 1. */
+int svae_adam(svae_ctx* ctx, float lr, int64_t step, float clip, void* stream);
+/* Copy an internal buffer (device -> caller device pointer). */
+int svae_copy_out(svae_ctx* ctx, int which, int step, float* dst, int64_t n, void* stream);
+
+/* ---- per-op entry points (kernel-level parity tests) ---- */
+/* TF-SAME conv2d (transpose=0, W [4,4,Cin,Cout]) or conv2d_transpose (transpose=1,
+ * W [4,4,Cout,Cin]) forward on x [N,H,H,Cin]; stride 1|2. */
+int svae_op_conv(const float* x, int n, int h, int cin, const float* w, int cout, int stride, int transpose,
+                 float* y, void* stream);
+/* input gradient and weight gradient of the same op */
+int svae_op_conv_dgrad(const float* dy, int n, int h, int cin, const float* w, int cout, int stride, int transpose,
+                       float* dx, void* stream);
+int svae_op_conv_wgrad(const float* x, int n, int h, int cin, const float* dy, int cout, int stride, int transpose,
+                       float* dw, void* scratch, int64_t scratch_bytes, void* stream);
+/* training BN (+act 0 none,1 relu,2 lrelu) over rows of x [rows,C] */
+int svae_op_bn_act(const float* x, int64_t rows, int c, const float* beta, int act, float* y, float* mean,
+                   float* invstd, void* scratch, int64_t scratch_bytes, void* stream);
+int svae_op_bn_act_bwd(const float* dy, const float* y, const float* x, int64_t rows, int c, const float* mean,
+                       const float* invstd, int act, float* dx, float* dbeta, void* scratch, int64_t scratch_bytes,
+                       void* stream);
+/* y[B,N] = x[B,K] @ w[K,N]  (fully_connected, no bias) */
+int svae_op_fc(const float* x, int b, int k, const float* w, int nout, float* y, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,102 @@
+"""ctypes binding of libsvae_hip.so (the C ABI declared in include/svae_hip.h).
+
+The library is loaded after ``torch`` so that its ``libamdhip64.so.7`` dependency
+resolves to the HIP runtime torch already mapped (one runtime per process: device
+pointers from torch tensors are valid inside the library).  There is no fallback:
+if the library is missing or fails to load, every entry point raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be imported before the HIP library is mapped)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsvae_hip.so")
+
+_c_float_p = ctypes.POINTER(ctypes.c_float)
+
+
+class SvaeConfig(ctypes.Structure):
+    _fields_ = [
+        ("batch", ctypes.c_int32), ("height", ctypes.c_int32), ("width", ctypes.c_int32),
+        ("channels", ctypes.c_int32), ("levels", ctypes.c_int32), ("mc_steps", ctypes.c_int32),
+        ("filter_sizes", ctypes.c_int32 * 10), ("latent_dims", ctypes.c_int32 * 8),
+        ("intermediate_reconstruction", ctypes.c_int32),
+        ("first_step_loss_coeff", ctypes.c_float), ("latent_prior_stddev", ctypes.c_float),
+        ("latent_mean_clip", ctypes.c_float), ("range_lo", ctypes.c_float), ("range_hi", ctypes.c_float),
+        ("min_highway", ctypes.c_float), ("max_highway", ctypes.c_float), ("dtype", ctypes.c_int32),
+    ]
+
+
+class SvaeParamDesc(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 96), ("ndim", ctypes.c_int32), ("shape", ctypes.c_int32 * 4),
+                ("offset", ctypes.c_int64), ("init", ctypes.c_int32), ("flags", ctypes.c_int32)]
+
+
+BUF_XHAT, BUF_MU, BUF_SIGMA, BUF_Z, BUF_STEP_STATS, BUF_REC_IMG, BUF_KL_IMG = range(7)
+ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the library; raises if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("libsvae_hip.so not built (%s); run __graft_entry__.build() or "
+                           "python sequential-variational-autoencoder_amd/build.py" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64, f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float
+    cfgp = ctypes.POINTER(SvaeConfig)
+    sig = {
+        "svae_param_count": ([cfgp, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i32)], i32),
+        "svae_param_layout": ([cfgp, ctypes.POINTER(SvaeParamDesc), i32], i32),
+        "svae_create": ([cfgp, i32, ctypes.POINTER(vp)], i32),
+        "svae_destroy": ([vp], i32),
+        "svae_last_error": ([vp], ctypes.c_char_p),
+        "svae_bind": ([vp, vp, vp], i32),
+        "svae_workspace_bytes": ([vp], i64),
+        "svae_forward": ([vp, vp, vp, vp, f32, vp], i32),
+        "svae_backward": ([vp, vp], i32),
+        "svae_adam": ([vp, f32, i64, f32, vp], i32),
+        "svae_copy_out": ([vp, i32, i32, vp, i64, vp], i32),
+        "svae_op_conv": ([vp, i32, i32, i32, vp, i32, i32, i32, vp, vp], i32),
+        "svae_op_conv_dgrad": ([vp, i32, i32, i32, vp, i32, i32, i32, vp, vp], i32),
+        "svae_op_conv_wgrad": ([vp, i32, i32, i32, vp, i32, i32, i32, vp, vp, i64, vp], i32),
+        "svae_op_bn_act": ([vp, i64, i32, vp, i32, vp, vp, vp, vp, i64, vp], i32),
+        "svae_op_bn_act_bwd": ([vp, vp, vp, i64, i32, vp, vp, i32, vp, vp, vp, i64, vp], i32),
+        "svae_op_fc": ([vp, i32, i32, vp, i32, vp, vp], i32),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+EXPORTED = ["svae_param_count", "svae_param_layout", "svae_create", "svae_destroy", "svae_last_error",
+            "svae_bind", "svae_workspace_bytes", "svae_forward", "svae_backward", "svae_adam", "svae_copy_out",
+            "svae_op_conv", "svae_op_conv_dgrad", "svae_op_conv_wgrad", "svae_op_bn_act",
+            "svae_op_bn_act_bwd", "svae_op_fc"]
+
+
+def check(rc, ctx=None):
+    if rc != 0:
+        msg = lib().svae_last_error(ctx)
+        raise RuntimeError("libsvae_hip error %d: %s" % (rc, msg.decode() if msg else "?"))
+
+
+def ptr(t):
+    """Raw device (or host) pointer of a contiguous tensor, or None."""
+    if t is None:
+        return None
+    assert t.is_contiguous(), "tensor must be contiguous"
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)

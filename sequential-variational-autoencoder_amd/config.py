@@ -1,0 +1,91 @@
+"""Typed configuration of the Sequential-VAE path (replaces the netname if/elif chain).
+
+Only the geometry / loss knobs of the executed path of the BASELINE configs are
+modelled: sequential_vae.py:201-258 defaults plus the netname
+overrides for ``c_inhomog`` (:727) / ``sequential_vae_celebA_inhomog`` (:671),
+``sequential_vae_lsun`` (:712-714) and the MNIST ``m_*`` geometry (:842-848).
+Unknown presets raise ``KeyError`` instead of ``exit(-1)`` (:860-862).
+"""
+import math
+from dataclasses import dataclass, field, replace
+from typing import List, Tuple
+
+from . import _lib
+
+
+@dataclass
+class SVAEConfig:
+    batch: int = 128
+    height: int = 64
+    width: int = 64
+    channels: int = 3
+    levels: int = 4                                   # vlae_levels (:204)
+    filter_sizes: List[int] = field(default_factory=lambda: [3, 32, 64, 128, 384, 512])  # :209
+    latent_dims: List[int] = field(default_factory=lambda: [3, 3, 3, 3])                 # :205
+    mc_steps: int = 8                                 # :219
+    intermediate_reconstruction: bool = True          # :221
+    first_step_loss_coeff: float = 1.0                # :227
+    latent_prior_stddev: float = 1.0                  # :232
+    latent_mean_clip: float = math.inf                # :230
+    range: Tuple[float, float] = (-1.0, 1.0)          # dataset.range (dataset_celeba.py:29)
+    min_highway: float = 0.0                          # :244
+    max_highway: float = 1.0                          # :243
+    learning_rate: float = 2e-4                       # :253
+    learning_rate_decay: float = 1.0                  # :252
+    reg_coeff_rate: float = 5000.0                    # :254
+    clip_grad_value: float = 10.0                     # :259
+    dtype: str = "fp32"
+
+    @property
+    def latent_dim(self):
+        return int(sum(self.latent_dims))
+
+    @property
+    def image_sizes(self):
+        return [self.height >> i for i in range(self.levels + 1)]
+
+    def to_c(self):
+        c = _lib.SvaeConfig()
+        c.batch, c.height, c.width, c.channels = self.batch, self.height, self.width, self.channels
+        c.levels, c.mc_steps = self.levels, self.mc_steps
+        for i, f in enumerate(self.filter_sizes):
+            c.filter_sizes[i] = f
+        for i, d in enumerate(self.latent_dims):
+            c.latent_dims[i] = d
+        c.intermediate_reconstruction = int(self.intermediate_reconstruction)
+        c.first_step_loss_coeff = self.first_step_loss_coeff
+        c.latent_prior_stddev = self.latent_prior_stddev
+        c.latent_mean_clip = self.latent_mean_clip
+        c.range_lo, c.range_hi = self.range
+        c.min_highway, c.max_highway = self.min_highway, self.max_highway
+        c.dtype = {"fp32": 0}[self.dtype]
+        return c
+
+    def as_dict(self):
+        """Plain-dict view (the layout the oracle's make_config produces)."""
+        return dict(H=self.height, W=self.width, C=self.channels, levels=self.levels,
+                    filter_sizes=list(self.filter_sizes), latent_dims=list(self.latent_dims),
+                    mc_steps=self.mc_steps, batch=self.batch, range=tuple(self.range),
+                    intermediate_reconstruction=self.intermediate_reconstruction,
+                    first_step_loss_coeff=self.first_step_loss_coeff,
+                    latent_prior_stddev=self.latent_prior_stddev, latent_mean_clip=self.latent_mean_clip,
+                    min_highway=self.min_highway, max_highway=self.max_highway,
+                    image_sizes=self.image_sizes, latent_dim=self.latent_dim)
+
+
+PRESETS = {
+    "celeba": SVAEConfig(),
+    "lsun": SVAEConfig(batch=256, latent_dims=[20, 30, 30, 30]),
+    "mnist_1step": SVAEConfig(batch=64, height=32, width=32, channels=1, levels=3,
+                              filter_sizes=[1, 64, 128, 192, 256], latent_dims=[8, 8, 8], mc_steps=1,
+                              range=(0.0, 1.0)),
+    "tiny": SVAEConfig(batch=4, height=32, width=32, channels=3, levels=4, filter_sizes=[3, 8, 8, 16, 24, 16],
+                       latent_dims=[2, 2, 3, 2], mc_steps=3),
+}
+# reference netnames that map onto the presets (sequential_vae.py:671, :712, :727)
+NETNAMES = {"c_inhomog": "celeba", "sequential_vae_celebA_inhomog": "celeba", "sequential_vae_lsun": "lsun"}
+
+
+def preset(name, **over):
+    name = NETNAMES.get(name, name)
+    return replace(PRESETS[name], **over)

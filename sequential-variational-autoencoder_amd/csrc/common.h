@@ -1,0 +1,48 @@
+// Shared device/host definitions for the Sequential-VAE HIP engine (gfx950 / CDNA4).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define SVAE_WAVE 64
+
+enum SvaeAct { ACT_NONE = 0, ACT_RELU = 1, ACT_LRELU = 2, ACT_SIGMOID = 3 };
+
+// Gather modes of the implicit-GEMM kernels (see DESIGN.md "conv as gather-GEMM").
+//  DENSE : row p reads A[p]                      (fully connected layers)
+//  CONV  : iy = oy*s - pad + ky                   (TF SAME conv2d, conv-T dgrad)
+//  CONVT : oy + pad = iy*s + ky                   (TF SAME conv2d_transpose, conv dgrad);
+//          stride 2 is split into 4 output-parity classes with 2x2 taps each.
+enum GatherMode { GM_DENSE = 0, GM_CONV = 1, GM_CONVT = 2 };
+
+struct ConvGeom {
+  int mode;
+  int nimg;
+  int Hi, Wi;   // spatial dims of the gathered operand
+  int Ho, Wo;   // spatial dims of the row space (output pixels)
+  int stride, pad, ksz;
+};
+
+__device__ __forceinline__ float lrelu_f(float x) { return fmaxf(fminf(0.1f * x, 0.f), x); }
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float act_f(float x, int act) {
+  if (act == ACT_RELU) return fmaxf(x, 0.f);
+  if (act == ACT_LRELU) return lrelu_f(x);
+  if (act == ACT_SIGMOID) return sigmoid_f(x);
+  return x;
+}
+// derivative of relu/lrelu expressed through the activation OUTPUT y (y>0 <=> pre>0);
+// TF tie rules: relu'(0)=0, lrelu'(0)=0.1 (abstract_network.py:8-10).
+__device__ __forceinline__ float dact_from_y(float y, int act) {
+  if (act == ACT_RELU) return y > 0.f ? 1.f : 0.f;
+  if (act == ACT_LRELU) return y > 0.f ? 1.f : 0.1f;
+  return 1.f;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}

@@ -1,0 +1,1289 @@
+// Sequential-VAE training-step engine: parameter layout, activation arena, and the
+// forward / backward schedule of the executed training subgraph
+// (sequential_vae.py:877-1212, 1537-1842; abstract_network.py:8-71).
+//
+// The chain is unrolled exactly as construct_network does (:934-975); the backward is
+// written out by hand in reverse order (there is no autodiff here).  The T recognition
+// ladders depend only on x, so they run as ONE batched launch per layer (blockIdx.z =
+// step) with their parameters laid out at a constant per-step stride.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+#include "svae_hip.h"
+
+namespace {
+
+enum Init { INIT_ZERO = 0, INIT_NORMAL = 1, INIT_GLOROT = 2 };
+enum Region { R_PHI = 0, R_THETA = 1, R_FROZEN = 2 };
+
+struct PDesc {
+  std::string name;
+  std::vector<int> shape;
+  int init;
+  bool dead, zero_grad;
+  int region, step;
+  long long size, offset;
+};
+
+struct ConvL {
+  int w = -1, beta = -1;  // desc indices (resolved to offsets later)
+  long long ow = 0, obeta = 0;
+  int cin = 0, cout = 0, stride = 1, hin = 0, hout = 0;
+  bool tr = false;
+};
+struct FcL {
+  int w = -1, beta = -1;
+  long long ow = 0, obeta = 0;
+  int nin = 0, nout = 0;
+};
+struct HeadL {
+  int wm = -1, bm = -1, ws = -1, bs = -1;
+  long long owm = 0, obm = 0, ows = 0, obs = 0;
+  int nin = 0, d = 0, off = 0, src_level = 0;
+};
+struct InfStep {
+  ConvL a[8], b[8];
+  HeadL head[8];
+};
+struct EncStep {
+  ConvL a[8], b[8];
+  ConvL c;
+  FcL fc;
+};
+struct GenStep {
+  FcL split[8];
+  FcL top;
+  ConvL s2[8], s1[8];  // indexed by level
+  int wout = -1, bout = -1, wratio = -1, bratio = -1;
+  long long owout = 0, obout = 0, owratio = 0, obratio = 0;
+};
+
+struct Geo {
+  int B, H, W, C, L, T;
+  int F[10], D[8], S[10];
+  int Dz;
+  bool interm;
+  float c_first, prior, clipv, lo, hi, minh, maxh;
+};
+
+bool make_geo(const svae_config* c, Geo& g, std::string& err) {
+  if (!c) { err = "null config"; return false; }
+  g.B = c->batch; g.H = c->height; g.W = c->width; g.C = c->channels;
+  g.L = c->levels; g.T = c->mc_steps;
+  if (g.L < 2 || g.L > 7) { err = "levels must be in [2,7]"; return false; }
+  if (g.T < 1 || g.T > 64) { err = "mc_steps must be in [1,64]"; return false; }
+  if (g.H != g.W) { err = "square images only (sequential_vae.py:1701)"; return false; }
+  if (g.C < 1 || g.C > 3) { err = "channels must be 1..3"; return false; }
+  if (g.B < 2) { err = "batch >= 2 required (training BatchNorm over the batch)"; return false; }
+  for (int i = 0; i < g.L + 2; ++i) {
+    g.F[i] = c->filter_sizes[i];
+    if (g.F[i] <= 0) { err = "filter_sizes must be positive"; return false; }
+  }
+  if (g.F[0] != g.C) { err = "filter_sizes[0] must equal channels"; return false; }
+  g.Dz = 0;
+  for (int i = 0; i < g.L; ++i) {
+    g.D[i] = c->latent_dims[i];
+    if (g.D[i] <= 0 || g.D[i] > 32) { err = "latent_dims must be in [1,32]"; return false; }
+    g.Dz += g.D[i];
+  }
+  for (int i = 0; i <= g.L; ++i) {
+    g.S[i] = g.H >> i;
+    if ((g.S[i] << i) != g.H || g.S[i] < 1) { err = "image size must be divisible by 2^levels"; return false; }
+  }
+  for (int i = 1; i <= g.L; ++i)
+    if (g.F[i] % 4) { err = "filter_sizes[1..L] must be multiples of 4"; return false; }
+  if (g.F[g.L + 1] % 4) { err = "filter_sizes[L+1] must be a multiple of 4"; return false; }
+  g.interm = c->intermediate_reconstruction != 0;
+  g.c_first = c->first_step_loss_coeff;
+  g.prior = c->latent_prior_stddev;
+  g.clipv = c->latent_mean_clip;
+  g.lo = c->range_lo; g.hi = c->range_hi;
+  g.minh = c->min_highway; g.maxh = c->max_highway;
+  if (c->dtype != 0) { err = "only dtype 0 (fp32) is implemented"; return false; }
+  return true;
+}
+
+// tf.contrib.layers default scope naming (Conv, Conv_1, ..., BatchNorm_3, fully_connected_2)
+struct Scope {
+  std::string prefix;
+  std::vector<PDesc>* out;
+  int region, step;
+  int n_conv = 0, n_convt = 0, n_bn = 0, n_fc = 0;
+  static std::string nm(const char* k, int i) { return i == 0 ? std::string(k) : std::string(k) + "_" + std::to_string(i); }
+  int add(const std::string& layer, const char* suffix, std::vector<int> shape, int init, bool dead, bool zg) {
+    PDesc d;
+    d.name = prefix + "/" + layer + "/" + suffix;
+    d.shape = shape;
+    d.init = init;
+    d.dead = dead;
+    d.zero_grad = zg || dead;
+    d.region = (dead || zg) ? R_FROZEN : region;
+    d.step = step;
+    d.size = 1;
+    for (int s : shape) d.size *= s;
+    d.offset = -1;
+    out->push_back(d);
+    return (int)out->size() - 1;
+  }
+  ConvL conv_bn(int cin, int cout, int stride, int hin, bool tr, bool dead = false) {
+    ConvL c;
+    std::string ln = tr ? nm("Conv2d_transpose", n_convt++) : nm("Conv", n_conv++);
+    if (tr) c.w = add(ln, "weights", {4, 4, cout, cin}, INIT_NORMAL, dead, false);
+    else c.w = add(ln, "weights", {4, 4, cin, cout}, INIT_NORMAL, dead, false);
+    add(ln, "biases", {cout}, INIT_ZERO, dead, true);
+    c.beta = add(nm("BatchNorm", n_bn++), "beta", {cout}, INIT_ZERO, dead, false);
+    c.cin = cin; c.cout = cout; c.stride = stride; c.hin = hin; c.tr = tr;
+    c.hout = tr ? hin * stride : hin / stride;
+    return c;
+  }
+  FcL fc_bn(int nin, int nout, bool dead = false) {
+    FcL f;
+    std::string ln = nm("fully_connected", n_fc++);
+    f.w = add(ln, "weights", {nin, nout}, INIT_NORMAL, dead, false);
+    add(ln, "biases", {nout}, INIT_ZERO, dead, true);
+    f.beta = add(nm("BatchNorm", n_bn++), "beta", {nout}, INIT_ZERO, dead, false);
+    f.nin = nin; f.nout = nout;
+    return f;
+  }
+  void fc(int nin, int nout, int& w, int& b) {
+    std::string ln = nm("fully_connected", n_fc++);
+    w = add(ln, "weights", {nin, nout}, INIT_GLOROT, false, false);
+    b = add(ln, "biases", {nout}, INIT_ZERO, false, false);
+  }
+  void convt_plain(int cin, int cout, int& w, int& b) {
+    std::string ln = nm("Conv2d_transpose", n_convt++);
+    w = add(ln, "weights", {4, 4, cout, cin}, INIT_GLOROT, false, false);
+    b = add(ln, "biases", {cout}, INIT_ZERO, false, false);
+  }
+};
+
+struct Model {
+  Geo g;
+  std::vector<PDesc> descs;
+  std::vector<InfStep> inf;
+  std::vector<EncStep> enc;
+  std::vector<GenStep> gen;
+  long long n_total = 0, n_live = 0, phi_stride = 0;
+
+  long long off(int idx) const { return idx < 0 ? -1 : descs[idx].offset; }
+
+  void build() {
+    const int L = g.L;
+    const int* F = g.F;
+    const int* S = g.S;
+    inf.assign(g.T, InfStep());
+    enc.assign(g.T, EncStep());
+    gen.assign(g.T, GenStep());
+    for (int t = 0; t < g.T; ++t) {
+      // phi/inference_step_t  (sequential_vae.py:1579-1609)
+      Scope sc{"phi/inference_step_" + std::to_string(t), &descs, R_PHI, t};
+      InfStep& I = inf[t];
+      int cin = F[0];
+      int off = 0;
+      for (int lvl = 0; lvl < L - 1; ++lvl) {
+        I.a[lvl] = sc.conv_bn(cin, F[lvl + 1], 2, S[lvl], false);
+        I.b[lvl] = sc.conv_bn(F[lvl + 1], F[lvl + 1], 1, S[lvl + 1], false);
+        HeadL& h = I.head[lvl];
+        h.nin = S[lvl + 1] * S[lvl + 1] * F[lvl + 1];
+        h.d = g.D[lvl];
+        h.off = off;
+        h.src_level = lvl;
+        off += h.d;
+        sc.fc(h.nin, h.d, h.wm, h.bm);
+        sc.fc(h.nin, h.d, h.ws, h.bs);
+        cin = F[lvl + 1];
+      }
+      sc.conv_bn(F[L - 1], F[L - 1], 2, S[L - 1], false, /*dead=*/true);   // :1602 (dead)
+      sc.fc_bn(S[L] * S[L] * F[L - 1], F[L], /*dead=*/true);              // :1605 (dead)
+      HeadL& h = I.head[L - 1];                                            // :1607-1609 read `ladder`
+      h.nin = S[L - 1] * S[L - 1] * F[L - 1];
+      h.d = g.D[L - 1];
+      h.off = off;
+      h.src_level = L - 2;
+      sc.fc(h.nin, h.d, h.wm, h.bm);
+      sc.fc(h.nin, h.d, h.ws, h.bs);
+      // theta/generative_encoder_step_t  (:1764-1775)
+      if (t >= 1) {
+        Scope se{"theta/generative_encoder_step_" + std::to_string(t), &descs, R_THETA, t};
+        EncStep& E = enc[t];
+        cin = F[0];
+        for (int lvl = 0; lvl < L - 1; ++lvl) {
+          E.a[lvl] = se.conv_bn(cin, F[lvl + 1], 2, S[lvl], false);
+          E.b[lvl] = se.conv_bn(F[lvl + 1], F[lvl + 1], 1, S[lvl + 1], false);
+          cin = F[lvl + 1];
+        }
+        E.c = se.conv_bn(F[L - 1], F[L - 1], 2, S[L - 1], false);
+        E.fc = se.fc_bn(S[L] * S[L] * F[L - 1], F[L]);
+      }
+      // theta/generative_step_t  (:1689-1727, split_latent :1796-1806)
+      Scope sg{"theta/generative_step_" + std::to_string(t), &descs, R_THETA, t};
+      GenStep& G = gen[t];
+      for (int i = 0; i < L - 1; ++i) G.split[i] = sg.fc_bn(g.D[i], S[i + 1] * S[i + 1] * F[i + 1]);
+      G.split[L - 1] = sg.fc_bn(g.D[L - 1], F[L + 1]);
+      G.top = sg.fc_bn(F[L + 1] + (t >= 1 ? F[L] : 0), S[L] * S[L] * F[L]);
+      cin = F[L];
+      for (int lvl = L - 2; lvl >= 0; --lvl) {
+        G.s2[lvl] = sg.conv_bn(cin, F[lvl + 1], 2, S[lvl + 2], true);
+        G.s1[lvl] = sg.conv_bn(2 * F[lvl + 1], F[lvl + 1], 1, S[lvl + 1], true);
+        cin = F[lvl + 1];
+      }
+      sg.convt_plain(F[1], g.C, G.wout, G.bout);
+      if (t >= 1) sg.convt_plain(F[1], 1, G.wratio, G.bratio);
+    }
+    // offsets: live phi blocks (uniform per-step stride), live theta blocks, frozen tail
+    long long o = 0;
+    for (int r = 0; r < 3; ++r) {
+      for (int t = 0; t < g.T; ++t) {
+        long long start = o;
+        for (auto& d : descs)
+          if (d.region == r && (r == R_FROZEN || d.step == t)) {
+            if (r == R_FROZEN && d.step != t) continue;
+            d.offset = o;
+            o += d.size;
+          }
+        if (r == R_PHI) {
+          long long sz = o - start;
+          if (t == 0) phi_stride = sz;
+        }
+      }
+      if (r == R_THETA) n_live = o;
+    }
+    n_total = o;
+    auto rc = [&](ConvL& c) { c.ow = off(c.w); c.obeta = off(c.beta); };
+    auto rf = [&](FcL& f) { f.ow = off(f.w); f.obeta = off(f.beta); };
+    for (int t = 0; t < g.T; ++t) {
+      for (int l = 0; l < L - 1; ++l) { rc(inf[t].a[l]); rc(inf[t].b[l]); rc(enc[t].a[l]); rc(enc[t].b[l]); rc(gen[t].s2[l]); rc(gen[t].s1[l]); }
+      for (int l = 0; l < L; ++l) {
+        HeadL& h = inf[t].head[l];
+        h.owm = off(h.wm); h.obm = off(h.bm); h.ows = off(h.ws); h.obs = off(h.bs);
+        rf(gen[t].split[l]);
+      }
+      rc(enc[t].c); rf(enc[t].fc); rf(gen[t].top);
+      GenStep& G = gen[t];
+      G.owout = off(G.wout); G.obout = off(G.bout); G.owratio = off(G.wratio); G.obratio = off(G.bratio);
+    }
+  }
+};
+
+const char* g_err_noctx = "";
+thread_local std::string g_tls_err;
+
+}  // namespace
+
+// ============================================================================
+// engine context
+// ============================================================================
+struct View {
+  float* p = nullptr;
+  int ld = 0;
+  long long gs = 0;
+};
+
+struct BNS {  // per-layer BN statistics (mean / invstd), groups x C
+  float* mean = nullptr;
+  float* invstd = nullptr;
+};
+
+struct svae_ctx {
+  Model m;
+  std::string err;
+  int device = 0;
+  float* P = nullptr;   // bound params
+  float* Gr = nullptr;  // bound grads
+  float* adam_m = nullptr;
+  float* adam_v = nullptr;
+  char* arena = nullptr;
+  size_t arena_bytes = 0, arena_used = 0;
+  hipStream_t st = 0;
+  unsigned long long rng_offset = 0;
+  float reg = 1.f;
+
+  // ---------- inference (batched over T, group stride = one step's slab) ----------
+  float *inf_pre_a[8], *inf_act_a[8], *inf_pre_b[8], *inf_act_b[8];
+  long long inf_gs[8];  // elements per step at level lvl
+  BNS inf_bn_a[8], inf_bn_b[8];
+  float *head_part, *mu, *sig, *z, *eps_buf, *kl_img, *kl_coef;
+  int head_nsplit;
+  // ---------- chain (per step) ----------
+  struct StepBufs {
+    float *enc_pre_a[8], *enc_act_a[8], *enc_pre_b[8], *enc_act_b[8];
+    BNS enc_bn_a[8], enc_bn_b[8];
+    float *enc_c_pre, *enc_c_act, *encfc_pre;
+    BNS enc_bn_c, enc_bn_fc;
+    float* split_mean[8];
+    float* split_inv[8];
+    float *top_cat, *top_pre, *top_act;
+    int ktop;
+    BNS top_bn;
+    float *s2_pre[8], *cat[8], *s1_pre[8], *s1_act[8];
+    BNS s2_bn[8], s1_bn[8];
+    float *wpack, *a_out, *xhat, *rec_part, *rec_img, *stats;
+  };
+  std::vector<StepBufs> sb;
+  int out_nblk = 0;
+  // ---------- backward scratch ----------
+  float *dx[2], *da, *dcur, *dnext, *dpre, *dcat, *dtop, *denc_c, *denc_fc;
+  float* denc[8];
+  float *sfc_dpre, *sfc_part, *dz, *dhead;
+  float *idb, *ida, *idpre;  // inference bwd: [T] x max level slab
+  float *part, *ab, *slab;
+  long long part_cap, slab_cap, ab_cap;
+  const float* x_in = nullptr;
+  const float* tgt_in = nullptr;
+  const float* eps_in = nullptr;
+  const float* eps_used = nullptr;
+  float* reg_host = nullptr;  // pinned [T] kl coefficients (read by a memcpy node at replay time)
+  bool counting = false;
+
+  float* alloc(long long n) {
+    size_t bytes = ((size_t)n * sizeof(float) + 255) & ~(size_t)255;
+    if (counting) {
+      arena_used += bytes;
+      return (float*)(uintptr_t)256;
+    }
+    if (arena_used + bytes > arena_bytes) return nullptr;
+    float* p = (float*)(arena + arena_used);
+    arena_used += bytes;
+    return p;
+  }
+};
+
+static int fail(svae_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  else g_tls_err = msg;
+  return code;
+}
+
+#define HIPCHK(ctx, x)                                                                       \
+  do {                                                                                       \
+    hipError_t e_ = (x);                                                                     \
+    if (e_ != hipSuccess) return fail(ctx, SVAE_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// layer helpers
+// ---------------------------------------------------------------------------
+namespace {
+
+FwdArgs fwd_args_conv(const ConvL& L, int B, const float* W, long long w_gs) {
+  FwdArgs a{};
+  a.B = W;
+  a.b_gs = w_gs;
+  a.b_tap = (long long)L.cin * L.cout;
+  a.g.nimg = B;
+  a.g.Hi = a.g.Wi = L.hin;
+  a.g.Ho = a.g.Wo = L.hout;
+  a.g.stride = L.stride;
+  a.g.pad = 1;
+  a.g.ksz = 4;
+  a.N = L.cout;
+  a.Cin = L.cin;
+  if (!L.tr) {  // conv2d: W [tap][ci][co] = KN
+    a.g.mode = GM_CONV;
+    a.b_nk = 0;
+    a.ldb = L.cout;
+    a.rows = B * L.hout * L.hout;
+    a.nclass = 1;
+  } else {  // conv2d_transpose: W [tap][co][ci] = NK
+    a.g.mode = GM_CONVT;
+    a.b_nk = 1;
+    a.ldb = L.cin;
+    if (L.stride == 2) {
+      a.rows = B * (L.hout / 2) * (L.hout / 2);
+      a.nclass = 4;
+    } else {
+      a.rows = B * L.hout * L.hout;
+      a.nclass = 1;
+    }
+  }
+  return a;
+}
+
+int nrb_of(const FwdArgs& a) {
+  int bm = igemm_fwd_bm(a);
+  return a.nclass * ((a.rows + bm - 1) / bm);
+}
+
+}  // namespace
+
+// Forward conv/convT + BN + act.  in: [B,hin,hin,cin] (ld), out view gets act(BN(pre)+res)
+static int conv_bn_act_fwd(svae_ctx* c, const ConvL& L, int groups, long long w_gs, View in, float* pre,
+                           long long pre_gs, BNS bn, long long bn_gs, View res, int act, View out) {
+  const int B = c->m.g.B;
+  FwdArgs a = fwd_args_conv(L, B, c->P + L.ow, w_gs);
+  a.A = in.p;
+  a.a_gs = in.gs;
+  a.lda = in.ld;
+  a.C = pre;
+  a.c_gs = pre_gs;
+  a.ldc = L.cout;
+  const int nrb = nrb_of(a);
+  if ((long long)groups * nrb * 2 * L.cout > c->part_cap) return fail(c, SVAE_EBADARG, "stats scratch too small");
+  a.stats = c->part;
+  a.s_gs = (long long)nrb * 2 * L.cout;
+  igemm_fwd(a, groups, c->st);
+  const long long rows = (long long)B * L.hout * L.hout;
+  bn_finalize(c->part, a.s_gs, nrb, L.cout, rows, 1e-3f, bn.mean, bn.invstd, bn_gs, groups, c->st);
+  bn_apply(pre, L.cout, pre_gs, rows, L.cout, bn.mean, bn.invstd, bn_gs, c->P + L.obeta, w_gs, res.p, res.ld, res.gs,
+           act, out.p, out.ld, out.gs, groups, c->st);
+  return 0;
+}
+
+static void choose_split(long long rows, int taps, int tiles, int groups, long long per_split_elems, long long cap,
+                         int& nsplit, int& chunk) {
+  long long blocks = (long long)taps * tiles * groups;
+  long long want = (2048 + blocks - 1) / blocks;
+  long long maxs = std::max<long long>(1, rows / 256);
+  long long ns = std::min(want, maxs);
+  long long capn = cap / std::max<long long>(1, per_split_elems * groups);
+  ns = std::max<long long>(1, std::min(ns, capn));
+  long long ch = (rows + ns - 1) / ns;
+  ch = (ch + 31) / 32 * 32;
+  nsplit = (int)((rows + ch - 1) / ch);
+  chunk = (int)ch;
+}
+
+// weight gradient of a conv/convT layer: dpre = grad wrt pre-BN output, in = layer input
+static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, View in, const float* dpre,
+                      long long dpre_gs, float* dW) {
+  const int B = c->m.g.B;
+  WgArgs w{};
+  w.g.ksz = 4;
+  w.g.pad = 1;
+  w.g.stride = L.stride;
+  w.g.mode = GM_CONV;
+  w.g.nimg = B;
+  w.ntap = 16;
+  if (!L.tr) {
+    // dW[tap][ci][co] = sum_{p out} x[src(p,tap)][ci] * dpre[p][co]
+    w.G = in.p; w.g_gs = in.gs; w.ldg = in.ld;
+    w.D = dpre; w.d_gs = dpre_gs; w.ldd = L.cout;
+    w.M = L.cin; w.N = L.cout;
+    w.g.Hi = w.g.Wi = L.hin;
+    w.g.Ho = w.g.Wo = L.hout;
+    w.rows = B * L.hout * L.hout;
+  } else {
+    // dW[tap][co][ci] = sum_{p in} dpre[src(p,tap)][co] * x[p][ci]
+    w.G = dpre; w.g_gs = dpre_gs; w.ldg = L.cout;
+    w.D = in.p; w.d_gs = in.gs; w.ldd = in.ld;
+    w.M = L.cout; w.N = L.cin;
+    w.g.Hi = w.g.Wi = L.hout;
+    w.g.Ho = w.g.Wo = L.hin;
+    w.rows = B * L.hin * L.hin;
+  }
+  int tiles = ((w.M + 63) / 64) * ((w.N + 63) / 64);
+  choose_split(w.rows, 16, tiles, groups, 16LL * w.M * w.N, c->slab_cap, w.nsplit, w.chunk);
+  w.part = c->slab;
+  w.p_gs = (long long)w.nsplit * 16 * w.M * w.N;
+  if (w.p_gs * groups > c->slab_cap) return fail(c, SVAE_EBADARG, "wgrad slab too small");
+  wgrad(w, groups, c->st);
+  wgrad_reduce(c->slab, w.p_gs, w.nsplit, 16, w.M, w.N, dW, w_gs, w.M, nullptr, 0, 0, groups, c->st);
+  return 0;
+}
+
+// input gradient of a conv/convT layer: din (+)= dgrad(dpre)
+static int conv_dgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, const float* dpre, long long dpre_gs,
+                      View din, int accumulate) {
+  const int B = c->m.g.B;
+  const float* W = c->P + L.ow;
+  if (L.cin % 4 != 0) {
+    // layer-0 conv (Cin = image channels): small-N gather (CONVT mode from dpre)
+    if (groups != 1) return fail(c, SVAE_EBADARG, "small-N dgrad is not batched");
+    ConvGeom g{GM_CONVT, B, L.hout, L.hout, L.hin, L.hin, L.stride, 1, 4};
+    gconv_smalln(dpre, L.cout, L.cout, W, L.cin, nullptr, 0, (long long)L.cin * L.cout, 0, nullptr, nullptr, g,
+                 (long long)B * L.hin * L.hin, din.p, din.ld, accumulate, c->st);
+    return 0;
+  }
+  FwdArgs a{};
+  a.A = dpre; a.a_gs = dpre_gs; a.lda = L.cout;
+  a.B = W; a.b_gs = w_gs; a.b_tap = (long long)L.cin * L.cout;
+  a.C = din.p; a.c_gs = din.gs; a.ldc = din.ld;
+  a.N = L.cin; a.Cin = L.cout;
+  a.g.nimg = B; a.g.Hi = a.g.Wi = L.hout; a.g.Ho = a.g.Wo = L.hin;
+  a.g.stride = L.stride; a.g.pad = 1; a.g.ksz = 4;
+  a.accumulate = accumulate;
+  if (!L.tr) {  // conv dgrad = CONVT gather, weights read [tap][ci][co] as NK
+    a.g.mode = GM_CONVT;
+    a.b_nk = 1;
+    a.ldb = L.cout;
+    if (L.stride == 2) { a.rows = B * (L.hin / 2) * (L.hin / 2); a.nclass = 4; }
+    else { a.rows = B * L.hin * L.hin; a.nclass = 1; }
+  } else {  // conv-T dgrad = CONV gather, weights [tap][co][ci] as KN
+    a.g.mode = GM_CONV;
+    a.b_nk = 0;
+    a.ldb = L.cin;
+    a.rows = B * L.hin * L.hin;
+    a.nclass = 1;
+  }
+  igemm_fwd(a, groups, c->st);
+  return 0;
+}
+
+// BN(+act) backward: dy (grad wrt post-act out y) -> dpre; dbeta into grads; optional dres
+static int bn_act_bwd(svae_ctx* c, int groups, long long rows, int C, View dy, View y, const float* pre, long long pre_gs,
+                      int ldp, BNS bn, long long bn_gs, long long beta_off, long long w_gs, int act, float* dpre,
+                      long long dpre_gs, View dres, int res_acc) {
+  const int nrb = bn_bwd_rowblocks(rows, C);
+  if ((long long)groups * nrb * 2 * C > c->part_cap) return fail(c, SVAE_EBADARG, "bn bwd scratch too small");
+  if ((long long)groups * 2 * C > c->ab_cap) return fail(c, SVAE_EBADARG, "ab scratch too small");
+  const long long pgs = (long long)nrb * 2 * C;
+  bn_bwd_reduce(dy.p, dy.ld, dy.gs, y.p, y.ld, y.gs, pre, ldp, pre_gs, rows, C, bn.mean, bn.invstd, bn_gs, act, c->part,
+                pgs, groups, c->st);
+  bn_bwd_finalize(c->part, pgs, nrb, C, rows, c->ab, 2LL * C, c->Gr + beta_off, w_gs, groups, c->st);
+  bn_bwd_apply(dy.p, dy.ld, dy.gs, y.p, y.ld, y.gs, pre, ldp, pre_gs, rows, C, bn.mean, bn.invstd, bn_gs, c->ab, 2LL * C,
+               act, dpre, C, dpre_gs, dres.p, dres.ld, dres.gs, res_acc, groups, c->st);
+  return 0;
+}
+
+// dense (FC) forward + BN + lrelu; in [B][nin] (ld), out view
+static int fc_bn_fwd(svae_ctx* c, const FcL& f, View in, float* pre, BNS bn, View out) {
+  const int B = c->m.g.B;
+  FwdArgs a{};
+  a.A = in.p; a.lda = in.ld;
+  a.B = c->P + f.ow; a.b_nk = 0; a.ldb = f.nout; a.b_tap = 0;
+  a.C = pre; a.ldc = f.nout;
+  a.N = f.nout; a.Cin = f.nin;
+  a.g.mode = GM_DENSE; a.g.nimg = B; a.g.ksz = 1; a.g.stride = 1;
+  a.rows = B; a.nclass = 1;
+  const int nrb = nrb_of(a);
+  if ((long long)nrb * 2 * f.nout > c->part_cap) return fail(c, SVAE_EBADARG, "stats scratch too small");
+  a.stats = c->part;
+  igemm_fwd(a, 1, c->st);
+  bn_finalize(c->part, 0, nrb, f.nout, B, 1e-3f, bn.mean, bn.invstd, 0, 1, c->st);
+  bn_apply(pre, f.nout, 0, B, f.nout, bn.mean, bn.invstd, 0, c->P + f.obeta, 0, nullptr, 0, 0, ACT_LRELU, out.p, out.ld,
+           0, 1, c->st);
+  return 0;
+}
+
+// dense backward: dy wrt post-act (view), y, pre -> grads; din (=) if non-null
+static int fc_bn_bwd(svae_ctx* c, const FcL& f, View in, View dy, View y, const float* pre, BNS bn, View din) {
+  const int B = c->m.g.B;
+  int r = bn_act_bwd(c, 1, B, f.nout, dy, y, pre, 0, f.nout, bn, 0, f.obeta, 0, ACT_LRELU, c->dpre, 0, View{}, 0);
+  if (r) return r;
+  WgArgs w{};
+  w.G = in.p; w.ldg = in.ld;
+  w.D = c->dpre; w.ldd = f.nout;
+  w.M = f.nin; w.N = f.nout;
+  w.g.mode = GM_DENSE; w.g.nimg = B; w.g.ksz = 1; w.g.stride = 1;
+  w.ntap = 1;
+  w.rows = B;
+  w.nsplit = 1;
+  w.chunk = (B + 31) / 32 * 32;
+  w.part = c->slab;
+  if ((long long)f.nin * f.nout > c->slab_cap) return fail(c, SVAE_EBADARG, "wgrad slab too small");
+  wgrad(w, 1, c->st);
+  wgrad_reduce(c->slab, 0, 1, 1, f.nin, f.nout, c->Gr + f.ow, 0, f.nin, nullptr, 0, 0, 1, c->st);
+  if (din.p) {
+    FwdArgs a{};
+    a.A = c->dpre; a.lda = f.nout;
+    a.B = c->P + f.ow; a.b_nk = 1; a.ldb = f.nout; a.b_tap = 0;
+    a.C = din.p; a.ldc = din.ld;
+    a.N = f.nin; a.Cin = f.nout;
+    a.g.mode = GM_DENSE; a.g.nimg = B; a.g.ksz = 1; a.g.stride = 1;
+    a.rows = B; a.nclass = 1;
+    igemm_fwd(a, 1, c->st);
+  }
+  return 0;
+}
+
+// ============================================================================
+// forward
+// ============================================================================
+static int engine_forward(svae_ctx* c) {
+  Model& M = c->m;
+  const Geo& g = M.g;
+  const int B = g.B, L = g.L, T = g.T;
+  const int* F = g.F;
+  const int* S = g.S;
+  const long long wg = M.phi_stride;
+  hipStream_t st = c->st;
+  int r;
+
+  // ---------------- recognition ladders, all steps batched (groups = T) ----------------
+  HIPCHK(c, hipMemsetAsync(c->head_part, 0, (size_t)T * c->head_nsplit * B * 2 * g.Dz * sizeof(float), st));
+  for (int lvl = 0; lvl < L - 1; ++lvl) {
+    const InfStep& I0 = M.inf[0];
+    View in = lvl == 0 ? View{(float*)c->x_in, g.C, 0} : View{c->inf_act_b[lvl - 1], F[lvl], c->inf_gs[lvl - 1]};
+    const long long gs = c->inf_gs[lvl];
+    r = conv_bn_act_fwd(c, I0.a[lvl], T, wg, in, c->inf_pre_a[lvl], gs, c->inf_bn_a[lvl], F[lvl + 1], View{}, ACT_LRELU,
+                        View{c->inf_act_a[lvl], F[lvl + 1], gs});
+    if (r) return r;
+    r = conv_bn_act_fwd(c, I0.b[lvl], T, wg, View{c->inf_act_a[lvl], F[lvl + 1], gs}, c->inf_pre_b[lvl], gs,
+                        c->inf_bn_b[lvl], F[lvl + 1], View{}, ACT_LRELU, View{c->inf_act_b[lvl], F[lvl + 1], gs});
+    if (r) return r;
+    for (int hl = 0; hl < L; ++hl) {
+      const HeadL& h = I0.head[hl];
+      if (h.src_level != lvl) continue;
+      heads_fwd(c->inf_act_b[lvl], gs, B, h.nin, c->P + h.owm, c->P + h.ows, wg, h.d, c->head_part,
+                (long long)c->head_nsplit * B * 2 * g.Dz, 2 * g.Dz, h.off, T, st);
+    }
+  }
+  {
+    LatentLvls lv{};
+    lv.L = L;
+    for (int l = 0; l < L; ++l) {
+      const HeadL& h = M.inf[0].head[l];
+      lv.bm[l] = c->P + h.obm;
+      lv.bs[l] = c->P + h.obs;
+      lv.off[l] = h.off;
+      lv.dim[l] = h.d;
+    }
+    const float* eps = c->eps_in;
+    if (!eps) {
+      philox_normal(c->eps_buf, (long long)T * B * g.Dz, 0x5EED5EEDULL, c->rng_offset, st);
+      c->rng_offset += ((long long)T * B * g.Dz + 3) / 4;
+      eps = c->eps_buf;
+    }
+    c->eps_used = eps;
+    const long long ms = (long long)B * g.Dz;
+    latent_fwd(c->head_part, (long long)c->head_nsplit * B * 2 * g.Dz, c->head_nsplit, B, g.Dz, lv, wg, g.clipv, g.prior,
+               eps, ms, c->mu, c->sig, c->z, ms, c->kl_img, B, T, st);
+  }
+
+  // ---------------- the chain ----------------
+  for (int t = 0; t < T; ++t) {
+    svae_ctx::StepBufs& s = c->sb[t];
+    const GenStep& G = M.gen[t];
+    const float* xprev = t >= 1 ? c->sb[t - 1].xhat : nullptr;
+    // g_theta encoder of x_{t-1}  (compute_encodings :1764-1777)
+    if (t >= 1) {
+      const EncStep& E = M.enc[t];
+      View in{(float*)xprev, g.C, 0};
+      for (int lvl = 0; lvl < L - 1; ++lvl) {
+        const int Fl = F[lvl + 1];
+        r = conv_bn_act_fwd(c, E.a[lvl], 1, 0, in, s.enc_pre_a[lvl], 0, s.enc_bn_a[lvl], 0, View{}, ACT_LRELU,
+                            View{s.enc_act_a[lvl], Fl, 0});
+        if (r) return r;
+        r = conv_bn_act_fwd(c, E.b[lvl], 1, 0, View{s.enc_act_a[lvl], Fl, 0}, s.enc_pre_b[lvl], 0, s.enc_bn_b[lvl], 0,
+                            View{}, ACT_LRELU, View{s.enc_act_b[lvl], Fl, 0});
+        if (r) return r;
+        in = View{s.enc_act_b[lvl], Fl, 0};
+      }
+      r = conv_bn_act_fwd(c, E.c, 1, 0, in, s.enc_c_pre, 0, s.enc_bn_c, 0, View{}, ACT_LRELU,
+                          View{s.enc_c_act, F[L - 1], 0});
+      if (r) return r;
+      r = fc_bn_fwd(c, E.fc, View{s.enc_c_act, S[L] * S[L] * F[L - 1], 0}, s.encfc_pre, s.enc_bn_fc,
+                    View{s.top_cat, s.ktop, 0});
+      if (r) return r;
+    }
+    // split_latent (:1796-1806): ladder_i straight into the concat buffers
+    const float* zt = c->z + (long long)t * B * g.Dz;
+    {
+      int zoff = 0;
+      for (int i = 0; i < L; ++i) {
+        const FcL& f = G.split[i];
+        if (i < L - 1) {
+          splitfc_fwd(zt, g.Dz, zoff, B, g.D[i], c->P + f.ow, c->P + f.obeta, f.nout, s.split_mean[i], s.split_inv[i],
+                      s.cat[i] + F[i + 1], (long long)S[i + 1] * S[i + 1] * 2 * F[i + 1], F[i + 1], 2 * F[i + 1], st);
+        } else {
+          const int coff = t >= 1 ? F[L] : 0;
+          splitfc_fwd(zt, g.Dz, zoff, B, g.D[i], c->P + f.ow, c->P + f.obeta, f.nout, s.split_mean[i], s.split_inv[i],
+                      s.top_cat + coff, s.ktop, f.nout, 0, st);
+        }
+        zoff += g.D[i];
+      }
+    }
+    // generator_ladder decoder (:1695-1721)
+    r = fc_bn_fwd(c, G.top, View{s.top_cat, s.ktop, 0}, s.top_pre, s.top_bn, View{s.top_act, S[L] * S[L] * F[L], 0});
+    if (r) return r;
+    View cur{s.top_act, F[L], 0};
+    for (int lvl = L - 2; lvl >= 0; --lvl) {
+      const int Fl = F[lvl + 1];
+      View res = t >= 1 ? View{s.enc_act_b[lvl], Fl, 0} : View{};
+      r = conv_bn_act_fwd(c, G.s2[lvl], 1, 0, cur, s.s2_pre[lvl], 0, s.s2_bn[lvl], 0, res, ACT_RELU,
+                          View{s.cat[lvl], 2 * Fl, 0});
+      if (r) return r;
+      r = conv_bn_act_fwd(c, G.s1[lvl], 1, 0, View{s.cat[lvl], 2 * Fl, 0}, s.s1_pre[lvl], 0, s.s1_bn[lvl], 0, View{},
+                          ACT_RELU, View{s.s1_act[lvl], Fl, 0});
+      if (r) return r;
+      cur = View{s.s1_act[lvl], Fl, 0};
+    }
+    // output + ratio conv-T (:1720, :1727) as one 4-channel small-N gather
+    {
+      const int C1 = g.C + 1;
+      const int F1 = F[1];
+      // pack [tap][C+1][F1] (ratio row zero at t=0) for the fused output conv-T and its dgrad
+      float* bpack = s.wpack + 16 * C1 * F1;
+      HIPCHK(c, hipMemsetAsync(s.wpack, 0, (size_t)(16 * C1 * F1 + 4) * sizeof(float), st));
+      HIPCHK(c, hipMemcpyAsync(bpack, c->P + G.obout, g.C * sizeof(float), hipMemcpyDeviceToDevice, st));
+      if (t >= 1) HIPCHK(c, hipMemcpyAsync(bpack + g.C, c->P + G.obratio, sizeof(float), hipMemcpyDeviceToDevice, st));
+      HIPCHK(c, hipMemcpy2DAsync(s.wpack, (size_t)C1 * F1 * sizeof(float), c->P + G.owout, (size_t)g.C * F1 * sizeof(float),
+                                 (size_t)g.C * F1 * sizeof(float), 16, hipMemcpyDeviceToDevice, st));
+      if (t >= 1)
+        HIPCHK(c, hipMemcpy2DAsync(s.wpack + g.C * F1, (size_t)C1 * F1 * sizeof(float), c->P + G.owratio,
+                                   (size_t)F1 * sizeof(float), (size_t)F1 * sizeof(float), 16, hipMemcpyDeviceToDevice,
+                                   st));
+      ConvGeom og{GM_CONVT, B, S[1], S[1], g.H, g.W, 2, 1, 4};
+      gconv_smalln(cur.p, F1, F1, s.wpack, C1, nullptr, 0, (long long)C1 * F1, 0, bpack, nullptr, og,
+                   (long long)B * g.H * g.W, s.a_out, C1, 0, st);
+      output_fwd(s.a_out, B, g.H * g.W, g.C, xprev, c->tgt_in, g.lo, g.hi, g.minh, g.maxh, s.xhat, s.rec_part,
+                 c->out_nblk, st);
+      loss_reduce(s.rec_part, c->out_nblk, c->kl_img + (long long)t * B, B, g.H * g.W * g.C, s.stats, s.rec_img, st);
+    }
+  }
+  return 0;
+}
+
+// ============================================================================
+// backward  (d self.loss / d theta, phi; sequential_vae.py:1273)
+// ============================================================================
+static int engine_backward(svae_ctx* c) {
+  Model& M = c->m;
+  const Geo& g = M.g;
+  const int B = g.B, L = g.L, T = g.T;
+  const int* F = g.F;
+  const int* S = g.S;
+  const int C1 = g.C + 1;
+  const long long P0 = (long long)B * g.H * g.W;
+  const long long wg = M.phi_stride;
+  hipStream_t st = c->st;
+  int r;
+
+  HIPCHK(c, hipMemsetAsync(c->dz, 0, (size_t)T * B * g.Dz * sizeof(float), st));
+  for (int t = T - 1; t >= 0; --t) {
+    svae_ctx::StepBufs& s = c->sb[t];
+    const GenStep& G = M.gen[t];
+    const float* xprev = t >= 1 ? c->sb[t - 1].xhat : nullptr;
+    const float* dxin = t < T - 1 ? c->dx[t & 1] : nullptr;
+    float* dxout = t >= 1 ? c->dx[(t - 1) & 1] : nullptr;
+    const float cf = t == 0 ? g.c_first : 1.f;
+    const float rec_coef = (g.interm || t == T - 1) ? 16.f * cf / (float)(P0 * g.C) : 0.f;
+    float* dzt = c->dz + (long long)t * B * g.Dz;
+
+    // ---- output + highway (:1720-1729)
+    output_bwd(s.a_out, B, g.H * g.W, g.C, xprev, s.xhat, c->tgt_in, g.lo, g.hi, g.minh, g.maxh, rec_coef, dxin, c->da,
+               dxout, st);
+    {
+      const int M_out = t >= 1 ? C1 : g.C;
+      WgArgs w{};
+      w.G = c->da; w.ldg = C1;
+      w.D = s.s1_act[0]; w.ldd = F[1];
+      w.M = M_out; w.N = F[1];
+      w.g = ConvGeom{GM_CONV, B, g.H, g.W, S[1], S[1], 2, 1, 4};
+      w.ntap = 16;
+      w.rows = B * S[1] * S[1];
+      choose_split(w.rows, 16, (F[1] + 127) / 128, 1, 16LL * M_out * F[1], c->slab_cap, w.nsplit, w.chunk);
+      w.part = c->slab;
+      wgrad(w, 1, st);
+      wgrad_reduce(c->slab, 0, w.nsplit, 16, M_out, F[1], c->Gr + G.owout, 0, g.C,
+                   t >= 1 ? c->Gr + G.owratio : nullptr, 0, 0, 1, st);
+      colsum_small(c->da, C1, P0, M_out, c->part, c->Gr + G.obout, g.C, t >= 1 ? c->Gr + G.obratio : nullptr, st);
+      // d cur = conv-T dgrad (CONV gather over da with the packed [tap][C+1][F1] weights as KN)
+      FwdArgs a{};
+      a.A = c->da; a.lda = C1;
+      a.B = s.wpack; a.b_nk = 0; a.ldb = F[1]; a.b_tap = (long long)C1 * F[1];
+      a.C = c->dcur; a.ldc = F[1];
+      a.N = F[1]; a.Cin = C1;
+      a.g = ConvGeom{GM_CONV, B, g.H, g.W, S[1], S[1], 2, 1, 4};
+      a.rows = B * S[1] * S[1]; a.nclass = 1;
+      igemm_fwd(a, 1, st);
+    }
+    // ---- decoder levels, bottom-up (reverse of :1710-1717)
+    float* dcur = c->dcur;
+    float* dnext = c->dnext;
+    for (int lvl = 0; lvl <= L - 2; ++lvl) {
+      const int Fl = F[lvl + 1];
+      const long long rows = (long long)B * S[lvl + 1] * S[lvl + 1];
+      const ConvL& l1 = G.s1[lvl];
+      const ConvL& l2 = G.s2[lvl];
+      // s1: relu(BN(convT_s1(cat)))
+      r = bn_act_bwd(c, 1, rows, Fl, View{dcur, Fl, 0}, View{s.s1_act[lvl], Fl, 0}, s.s1_pre[lvl], 0, Fl, s.s1_bn[lvl],
+                     0, l1.obeta, 0, ACT_RELU, c->dpre, 0, View{}, 0);
+      if (r) return r;
+      r = conv_wgrad(c, l1, 1, 0, View{s.cat[lvl], 2 * Fl, 0}, c->dpre, 0, c->Gr + l1.ow);
+      if (r) return r;
+      r = conv_dgrad(c, l1, 1, 0, c->dpre, 0, View{c->dcat, 2 * Fl, 0}, 0);
+      if (r) return r;
+      // latent half of the concat -> split_latent level lvl
+      {
+        const FcL& f = G.split[lvl];
+        int zoff = 0;
+        for (int i = 0; i < lvl; ++i) zoff += g.D[i];
+        splitfc_bwd(c->z + (long long)t * B * g.Dz, g.Dz, zoff, B, g.D[lvl], c->P + f.ow, c->P + f.obeta, f.nout,
+                    s.split_mean[lvl], s.split_inv[lvl], c->dcat + Fl, (long long)S[lvl + 1] * S[lvl + 1] * 2 * Fl, Fl,
+                    2 * Fl, c->Gr + f.ow, c->Gr + f.obeta, c->sfc_dpre, st);
+        splitfc_dz_gemm(c->sfc_dpre, B, f.nout, c->P + f.ow, g.D[lvl], c->sfc_part, dzt, g.Dz, zoff, st);
+      }
+      // s2: relu(BN(convT_s2(cur)) + enc_{lvl+1})
+      View dres = t >= 1 ? View{c->denc[lvl], Fl, 0} : View{};
+      r = bn_act_bwd(c, 1, rows, Fl, View{c->dcat, 2 * Fl, 0}, View{s.cat[lvl], 2 * Fl, 0}, s.s2_pre[lvl], 0, Fl,
+                     s.s2_bn[lvl], 0, l2.obeta, 0, ACT_RELU, c->dpre, 0, dres, 0);
+      if (r) return r;
+      View in = lvl == L - 2 ? View{s.top_act, F[L], 0} : View{s.s1_act[lvl + 1], F[lvl + 2], 0};
+      r = conv_wgrad(c, l2, 1, 0, in, c->dpre, 0, c->Gr + l2.ow);
+      if (r) return r;
+      r = conv_dgrad(c, l2, 1, 0, c->dpre, 0, View{dnext, in.ld, 0}, 0);
+      if (r) return r;
+      std::swap(dcur, dnext);
+    }
+    // ---- top fc_bn_lrelu (:1704)
+    const int ntop = S[L] * S[L] * F[L];
+    r = fc_bn_bwd(c, G.top, View{s.top_cat, s.ktop, 0}, View{dcur, ntop, 0}, View{s.top_act, ntop, 0}, s.top_pre,
+                  s.top_bn, View{c->dtop, s.ktop, 0});
+    if (r) return r;
+    {
+      const FcL& f = G.split[L - 1];
+      const int coff = t >= 1 ? F[L] : 0;
+      splitfc_bwd(c->z + (long long)t * B * g.Dz, g.Dz, g.Dz - g.D[L - 1], B, g.D[L - 1], c->P + f.ow, c->P + f.obeta,
+                  f.nout, s.split_mean[L - 1], s.split_inv[L - 1], c->dtop + coff, s.ktop, f.nout, 0, c->Gr + f.ow,
+                  c->Gr + f.obeta, c->sfc_dpre, st);
+      splitfc_dz_gemm(c->sfc_dpre, B, f.nout, c->P + f.ow, g.D[L - 1], c->sfc_part, dzt, g.Dz, g.Dz - g.D[L - 1], st);
+    }
+    // ---- g_theta encoder of x_{t-1} (reverse of :1764-1775)
+    if (t >= 1) {
+      const EncStep& E = M.enc[t];
+      const int nc = S[L] * S[L] * F[L - 1];
+      r = fc_bn_bwd(c, E.fc, View{s.enc_c_act, nc, 0}, View{c->dtop, s.ktop, 0}, View{s.top_cat, s.ktop, 0},
+                    s.encfc_pre, s.enc_bn_fc, View{c->denc_c, nc, 0});
+      if (r) return r;
+      const long long rc = (long long)B * S[L] * S[L];
+      r = bn_act_bwd(c, 1, rc, F[L - 1], View{c->denc_c, F[L - 1], 0}, View{s.enc_c_act, F[L - 1], 0}, s.enc_c_pre, 0,
+                     F[L - 1], s.enc_bn_c, 0, E.c.obeta, 0, ACT_LRELU, c->dpre, 0, View{}, 0);
+      if (r) return r;
+      r = conv_wgrad(c, E.c, 1, 0, View{s.enc_act_b[L - 2], F[L - 1], 0}, c->dpre, 0, c->Gr + E.c.ow);
+      if (r) return r;
+      r = conv_dgrad(c, E.c, 1, 0, c->dpre, 0, View{c->denc[L - 2], F[L - 1], 0}, 1);
+      if (r) return r;
+      for (int lvl = L - 2; lvl >= 0; --lvl) {
+        const int Fl = F[lvl + 1];
+        const long long rows = (long long)B * S[lvl + 1] * S[lvl + 1];
+        r = bn_act_bwd(c, 1, rows, Fl, View{c->denc[lvl], Fl, 0}, View{s.enc_act_b[lvl], Fl, 0}, s.enc_pre_b[lvl], 0,
+                       Fl, s.enc_bn_b[lvl], 0, E.b[lvl].obeta, 0, ACT_LRELU, c->dpre, 0, View{}, 0);
+        if (r) return r;
+        r = conv_wgrad(c, E.b[lvl], 1, 0, View{s.enc_act_a[lvl], Fl, 0}, c->dpre, 0, c->Gr + E.b[lvl].ow);
+        if (r) return r;
+        r = conv_dgrad(c, E.b[lvl], 1, 0, c->dpre, 0, View{c->dcur, Fl, 0}, 0);
+        if (r) return r;
+        r = bn_act_bwd(c, 1, rows, Fl, View{c->dcur, Fl, 0}, View{s.enc_act_a[lvl], Fl, 0}, s.enc_pre_a[lvl], 0, Fl,
+                       s.enc_bn_a[lvl], 0, E.a[lvl].obeta, 0, ACT_LRELU, c->dpre, 0, View{}, 0);
+        if (r) return r;
+        View in = lvl == 0 ? View{(float*)xprev, g.C, 0} : View{s.enc_act_b[lvl - 1], F[lvl], 0};
+        r = conv_wgrad(c, E.a[lvl], 1, 0, in, c->dpre, 0, c->Gr + E.a[lvl].ow);
+        if (r) return r;
+        View din = lvl == 0 ? View{dxout, g.C, 0} : View{c->denc[lvl - 1], F[lvl], 0};
+        r = conv_dgrad(c, E.a[lvl], 1, 0, c->dpre, 0, din, 1);
+        if (r) return r;
+      }
+    }
+  }
+
+  // ---------------- recognition ladders, batched over T ----------------
+  HIPCHK(c, hipMemcpyAsync(c->kl_coef, c->reg_host, T * sizeof(float), hipMemcpyHostToDevice, st));
+  latent_bwd(c->mu, c->sig, c->eps_used, c->dz, (long long)B * g.Dz, (long long)B * g.Dz, B, g.Dz, c->kl_coef, 1,
+             g.prior, g.clipv, c->dhead, (long long)B * 2 * g.Dz, T, st);
+  const InfStep& I0 = M.inf[0];
+  for (int lvl = L - 2; lvl >= 0; --lvl) {
+    const int Fl = F[lvl + 1];
+    const long long gs = c->inf_gs[lvl];
+    const long long rows = (long long)B * S[lvl + 1] * S[lvl + 1];
+    bool first = lvl == L - 2;
+    for (int hl = 0; hl < L; ++hl) {
+      const HeadL& h = I0.head[hl];
+      if (h.src_level != lvl) continue;
+      heads_bwd(c->inf_act_b[lvl], gs, c->idb, gs, B, h.nin, c->P + h.owm, c->P + h.ows, wg, h.d, c->dhead,
+                (long long)B * 2 * g.Dz, 2 * g.Dz, h.off, c->Gr + h.owm, c->Gr + h.ows, c->Gr + h.obm, c->Gr + h.obs,
+                first ? 0 : 1, T, st);
+      first = false;
+    }
+    r = bn_act_bwd(c, T, rows, Fl, View{c->idb, Fl, gs}, View{c->inf_act_b[lvl], Fl, gs}, c->inf_pre_b[lvl], gs, Fl,
+                   c->inf_bn_b[lvl], Fl, I0.b[lvl].obeta, wg, ACT_LRELU, c->idpre, gs, View{}, 0);
+    if (r) return r;
+    r = conv_wgrad(c, I0.b[lvl], T, wg, View{c->inf_act_a[lvl], Fl, gs}, c->idpre, gs, c->Gr + I0.b[lvl].ow);
+    if (r) return r;
+    r = conv_dgrad(c, I0.b[lvl], T, wg, c->idpre, gs, View{c->ida, Fl, gs}, 0);
+    if (r) return r;
+    r = bn_act_bwd(c, T, rows, Fl, View{c->ida, Fl, gs}, View{c->inf_act_a[lvl], Fl, gs}, c->inf_pre_a[lvl], gs, Fl,
+                   c->inf_bn_a[lvl], Fl, I0.a[lvl].obeta, wg, ACT_LRELU, c->idpre, gs, View{}, 0);
+    if (r) return r;
+    View in = lvl == 0 ? View{(float*)c->x_in, g.C, 0} : View{c->inf_act_b[lvl - 1], F[lvl], c->inf_gs[lvl - 1]};
+    r = conv_wgrad(c, I0.a[lvl], T, wg, in, c->idpre, gs, c->Gr + I0.a[lvl].ow);
+    if (r) return r;
+    if (lvl > 0) {
+      r = conv_dgrad(c, I0.a[lvl], T, wg, c->idpre, gs, View{c->idb, F[lvl], c->inf_gs[lvl - 1]}, 0);
+      if (r) return r;
+    }
+  }
+  return 0;
+}
+
+// ============================================================================
+// arena planning (counting pass, then carving pass)
+// ============================================================================
+static bool plan(svae_ctx* c) {
+  const Geo& g = c->m.g;
+  const int B = g.B, L = g.L, T = g.T;
+  const int* F = g.F;
+  const int* S = g.S;
+  const int C1 = g.C + 1;
+  auto A = [&](long long n) { return c->alloc(n); };
+  auto bn = [&](int groups, int C) {
+    BNS b;
+    b.mean = A((long long)groups * C);
+    b.invstd = A((long long)groups * C);
+    return b;
+  };
+  long long max_inf = 0, maxact = 0, maxJ = 0;
+  int maxK = 0;
+  for (int lvl = 0; lvl < L - 1; ++lvl) {
+    long long gs = (long long)B * S[lvl + 1] * S[lvl + 1] * F[lvl + 1];
+    gs = (gs + 63) / 64 * 64;
+    c->inf_gs[lvl] = gs;
+    max_inf = std::max(max_inf, gs);
+    c->inf_pre_a[lvl] = A(T * gs);
+    c->inf_act_a[lvl] = A(T * gs);
+    c->inf_pre_b[lvl] = A(T * gs);
+    c->inf_act_b[lvl] = A(T * gs);
+    c->inf_bn_a[lvl] = bn(T, F[lvl + 1]);
+    c->inf_bn_b[lvl] = bn(T, F[lvl + 1]);
+    maxact = std::max(maxact, 2 * gs);
+  }
+  int maxnin = 0;
+  for (int l = 0; l < L; ++l) maxnin = std::max(maxnin, c->m.inf[0].head[l].nin);
+  c->head_nsplit = heads_splits(maxnin);
+  c->head_part = A((long long)T * c->head_nsplit * B * 2 * g.Dz);
+  c->mu = A((long long)T * B * g.Dz);
+  c->sig = A((long long)T * B * g.Dz);
+  c->z = A((long long)T * B * g.Dz);
+  c->eps_buf = A((long long)T * B * g.Dz);
+  c->kl_img = A((long long)T * B);
+  c->kl_coef = A(64);
+  c->out_nblk = output_blocks_per_img(g.H * g.W);
+  c->sb.assign(T, svae_ctx::StepBufs());
+  for (int t = 0; t < T; ++t) {
+    svae_ctx::StepBufs& s = c->sb[t];
+    memset(&s, 0, sizeof(s));
+    if (t >= 1) {
+      for (int lvl = 0; lvl < L - 1; ++lvl) {
+        long long n = (long long)B * S[lvl + 1] * S[lvl + 1] * F[lvl + 1];
+        s.enc_pre_a[lvl] = A(n); s.enc_act_a[lvl] = A(n); s.enc_pre_b[lvl] = A(n); s.enc_act_b[lvl] = A(n);
+        s.enc_bn_a[lvl] = bn(1, F[lvl + 1]); s.enc_bn_b[lvl] = bn(1, F[lvl + 1]);
+      }
+      long long nc = (long long)B * S[L] * S[L] * F[L - 1];
+      s.enc_c_pre = A(nc); s.enc_c_act = A(nc); s.enc_bn_c = bn(1, F[L - 1]);
+      s.encfc_pre = A((long long)B * F[L]); s.enc_bn_fc = bn(1, F[L]);
+    }
+    for (int i = 0; i < L; ++i) {
+      int J = c->m.gen[t].split[i].nout;
+      maxJ = std::max<long long>(maxJ, J);
+      maxK = std::max(maxK, g.D[i]);
+      s.split_mean[i] = A(J);
+      s.split_inv[i] = A(J);
+    }
+    s.ktop = F[L + 1] + (t >= 1 ? F[L] : 0);
+    s.top_cat = A((long long)B * s.ktop);
+    long long ntop = (long long)B * S[L] * S[L] * F[L];
+    s.top_pre = A(ntop); s.top_act = A(ntop); s.top_bn = bn(1, S[L] * S[L] * F[L]);
+    maxact = std::max(maxact, ntop);
+    for (int lvl = 0; lvl < L - 1; ++lvl) {
+      long long n = (long long)B * S[lvl + 1] * S[lvl + 1] * F[lvl + 1];
+      s.s2_pre[lvl] = A(n); s.cat[lvl] = A(2 * n); s.s1_pre[lvl] = A(n); s.s1_act[lvl] = A(n);
+      s.s2_bn[lvl] = bn(1, F[lvl + 1]); s.s1_bn[lvl] = bn(1, F[lvl + 1]);
+      maxact = std::max(maxact, 2 * n);
+    }
+    s.wpack = A(16LL * C1 * F[1] + 4);
+    s.a_out = A((long long)B * g.H * g.W * C1);
+    s.xhat = A((long long)B * g.H * g.W * g.C);
+    s.rec_part = A((long long)B * c->out_nblk);
+    s.rec_img = A(B);
+    s.stats = A(2);
+  }
+  const long long P0 = (long long)B * g.H * g.W;
+  c->dx[0] = A(P0 * g.C);
+  c->dx[1] = A(P0 * g.C);
+  c->da = A(P0 * C1);
+  c->dcur = A(maxact);
+  c->dnext = A(maxact);
+  c->dpre = A(maxact);
+  c->dcat = A(maxact);
+  c->dtop = A((long long)B * (F[L] + F[L + 1]));
+  c->denc_c = A((long long)B * S[L] * S[L] * F[L - 1]);
+  for (int lvl = 0; lvl < L - 1; ++lvl) c->denc[lvl] = A((long long)B * S[lvl + 1] * S[lvl + 1] * F[lvl + 1]);
+  c->sfc_dpre = A((long long)B * maxJ);
+  c->sfc_part = A((long long)heads_splits((int)maxJ) * B * maxK);
+  c->dz = A((long long)T * B * g.Dz);
+  c->dhead = A((long long)T * B * 2 * g.Dz);
+  c->idb = A((long long)T * max_inf);
+  c->ida = A((long long)T * max_inf);
+  c->idpre = A((long long)T * max_inf);
+  c->part_cap = (long long)T * (maxact / 16 + 65536) + 8LL * 2 * (maxJ + 8192);
+  c->part = A(c->part_cap);
+  c->ab_cap = (long long)T * 2 * 65536;
+  c->ab = A(c->ab_cap);
+  c->slab_cap = 64LL << 20;
+  c->slab = A(c->slab_cap);
+  return true;
+}
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+int svae_param_count(const svae_config* cfg, int64_t* n_total, int64_t* n_live, int32_t* n_tensors) {
+  Model m;
+  std::string err;
+  if (!make_geo(cfg, m.g, err)) return fail(nullptr, SVAE_EBADCONFIG, err);
+  m.build();
+  if (n_total) *n_total = m.n_total;
+  if (n_live) *n_live = m.n_live;
+  if (n_tensors) *n_tensors = (int32_t)m.descs.size();
+  return 0;
+}
+
+int svae_param_layout(const svae_config* cfg, svae_param_desc* out, int32_t cap) {
+  Model m;
+  std::string err;
+  if (!make_geo(cfg, m.g, err)) return fail(nullptr, SVAE_EBADCONFIG, err);
+  m.build();
+  if (!out || cap < (int32_t)m.descs.size()) return fail(nullptr, SVAE_EBADARG, "layout capacity too small");
+  for (size_t i = 0; i < m.descs.size(); ++i) {
+    const PDesc& d = m.descs[i];
+    svae_param_desc& o = out[i];
+    memset(&o, 0, sizeof(o));
+    strncpy(o.name, d.name.c_str(), sizeof(o.name) - 1);
+    o.ndim = (int32_t)d.shape.size();
+    for (size_t k = 0; k < d.shape.size() && k < 4; ++k) o.shape[k] = d.shape[k];
+    o.offset = d.offset;
+    o.init = d.init;
+    o.flags = (d.dead ? 1 : 0) | (d.zero_grad ? 2 : 0);
+  }
+  return 0;
+}
+
+int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
+  if (!out) return fail(nullptr, SVAE_EBADARG, "null out");
+  *out = nullptr;
+  svae_ctx* c = new svae_ctx();
+  std::string err;
+  if (!make_geo(cfg, c->m.g, err)) {
+    delete c;
+    return fail(nullptr, SVAE_EBADCONFIG, err);
+  }
+  c->m.build();
+  c->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(nullptr, SVAE_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+  }
+  c->counting = true;
+  c->arena_used = 0;
+  plan(c);
+  c->arena_bytes = c->arena_used;
+  c->counting = false;
+  c->arena_used = 0;
+  e = hipMalloc((void**)&c->arena, c->arena_bytes);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(nullptr, SVAE_ENOMEM, std::string("hipMalloc arena: ") + hipGetErrorString(e));
+  }
+  plan(c);
+  const long long nl = c->m.n_live;
+  e = hipMalloc((void**)&c->adam_m, (size_t)nl * sizeof(float) * 2);
+  if (e != hipSuccess) {
+    hipFree(c->arena);
+    delete c;
+    return fail(nullptr, SVAE_ENOMEM, std::string("hipMalloc adam: ") + hipGetErrorString(e));
+  }
+  c->adam_v = c->adam_m + nl;
+  hipMemset(c->adam_m, 0, (size_t)nl * sizeof(float) * 2);
+  hipHostMalloc((void**)&c->reg_host, 64 * sizeof(float), hipHostMallocDefault);
+  for (int i = 0; i < 64; ++i) c->reg_host[i] = 0.f;
+  *out = c;
+  return 0;
+}
+
+int svae_destroy(svae_ctx* c) {
+  if (!c) return 0;
+  if (c->arena) hipFree(c->arena);
+  if (c->adam_m) hipFree(c->adam_m);
+  if (c->reg_host) hipHostFree(c->reg_host);
+  delete c;
+  return 0;
+}
+
+const char* svae_last_error(const svae_ctx* c) { return c ? c->err.c_str() : g_tls_err.c_str(); }
+
+int64_t svae_workspace_bytes(const svae_ctx* c) { return c ? (int64_t)c->arena_bytes : 0; }
+
+int svae_bind(svae_ctx* c, float* params, float* grads) {
+  if (!c || !params || !grads) return fail(c, SVAE_EBADARG, "null buffer");
+  c->P = params;
+  c->Gr = grads;
+  HIPCHK(c, hipMemset(grads, 0, (size_t)c->m.n_total * sizeof(float)));
+  return 0;
+}
+
+int svae_forward(svae_ctx* c, const float* x, const float* target, const float* eps, float reg_coeff, void* stream) {
+  if (!c || !x || !target) return fail(c, SVAE_EBADARG, "null input");
+  if (!c->P) return fail(c, SVAE_EBADARG, "parameters not bound (svae_bind)");
+  c->st = (hipStream_t)stream;
+  c->x_in = x;
+  c->tgt_in = target;
+  c->eps_in = eps;
+  c->reg = reg_coeff;
+  const Geo& g = c->m.g;
+  for (int t = 0; t < g.T; ++t) c->reg_host[t] = reg_coeff * (t == 0 ? g.c_first : 1.f) / (float)g.B;
+  int r = engine_forward(c);
+  if (r) return r;
+  HIPCHK(c, hipGetLastError());
+  return 0;
+}
+
+int svae_backward(svae_ctx* c, void* stream) {
+  if (!c || !c->x_in) return fail(c, SVAE_EBADARG, "svae_forward must run first");
+  c->st = (hipStream_t)stream;
+  int r = engine_backward(c);
+  if (r) return r;
+  HIPCHK(c, hipGetLastError());
+  return 0;
+}
+
+int svae_adam(svae_ctx* c, float lr, int64_t step, float clip, void* stream) {
+  if (!c || !c->P || step < 1) return fail(c, SVAE_EBADARG, "bad adam args");
+  const double b1 = 0.9, b2 = 0.999;
+  const double lr_t = lr * std::sqrt(1.0 - std::pow(b2, (double)step)) / (1.0 - std::pow(b1, (double)step));
+  adam_step(c->P, c->Gr, c->adam_m, c->adam_v, c->m.n_live, (float)lr_t, (float)b1, (float)b2, 1e-8f, clip,
+            (hipStream_t)stream);
+  HIPCHK(c, hipGetLastError());
+  return 0;
+}
+
+int svae_copy_out(svae_ctx* c, int which, int step, float* dst, int64_t n, void* stream) {
+  if (!c || !dst) return fail(c, SVAE_EBADARG, "null");
+  const Geo& g = c->m.g;
+  if (step < 0 || step >= g.T) return fail(c, SVAE_EBADARG, "step out of range");
+  const float* src = nullptr;
+  long long cnt = 0;
+  const long long ml = (long long)g.B * g.Dz;
+  switch (which) {
+    case SVAE_BUF_XHAT: src = c->sb[step].xhat; cnt = (long long)g.B * g.H * g.W * g.C; break;
+    case SVAE_BUF_MU: src = c->mu + step * ml; cnt = ml; break;
+    case SVAE_BUF_SIGMA: src = c->sig + step * ml; cnt = ml; break;
+    case SVAE_BUF_Z: src = c->z + step * ml; cnt = ml; break;
+    case SVAE_BUF_STEP_STATS: src = c->sb[step].stats; cnt = 2; break;
+    case SVAE_BUF_REC_IMG: src = c->sb[step].rec_img; cnt = g.B; break;
+    case SVAE_BUF_KL_IMG: src = c->kl_img + (long long)step * g.B; cnt = g.B; break;
+    default: return fail(c, SVAE_EBADARG, "unknown buffer");
+  }
+  if (n < cnt) return fail(c, SVAE_EBADARG, "destination too small");
+  HIPCHK(c, hipMemcpyAsync(dst, src, cnt * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return 0;
+}
+
+}  // extern "C"
+
+// ============================================================================
+// per-op entry points (kernel-level parity tests; same launch paths as the engine)
+// ============================================================================
+extern "C" {
+
+int svae_op_conv(const float* x, int n, int h, int cin, const float* w, int cout, int stride, int transpose, float* y,
+                 void* stream) {
+  if (!x || !w || !y || (stride != 1 && stride != 2) || cout % 4) return fail(nullptr, SVAE_EBADARG, "bad op args");
+  ConvL L;
+  L.cin = cin; L.cout = cout; L.stride = stride; L.hin = h; L.tr = transpose != 0;
+  L.hout = L.tr ? h * stride : h / stride;
+  FwdArgs a = fwd_args_conv(L, n, w, 0);
+  a.A = x; a.lda = cin;
+  a.C = y; a.ldc = cout;
+  igemm_fwd(a, 1, (hipStream_t)stream);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(nullptr, SVAE_EHIP, hipGetErrorString(e));
+}
+
+int svae_op_conv_dgrad(const float* dy, int n, int h, int cin, const float* w, int cout, int stride, int transpose,
+                       float* dx, void* stream) {
+  if (!dy || !w || !dx) return fail(nullptr, SVAE_EBADARG, "bad op args");
+  static svae_ctx dummy;
+  dummy.m.g.B = n;
+  dummy.P = (float*)w;
+  dummy.st = (hipStream_t)stream;
+  ConvL L;
+  L.cin = cin; L.cout = cout; L.stride = stride; L.hin = h; L.tr = transpose != 0;
+  L.hout = L.tr ? h * stride : h / stride;
+  L.ow = 0;
+  int r = conv_dgrad(&dummy, L, 1, 0, dy, 0, View{dx, cin, 0}, 0);
+  if (r) return fail(nullptr, r, dummy.err);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(nullptr, SVAE_EHIP, hipGetErrorString(e));
+}
+
+int svae_op_conv_wgrad(const float* x, int n, int h, int cin, const float* dy, int cout, int stride, int transpose,
+                       float* dw, void* scratch, int64_t scratch_bytes, void* stream) {
+  if (!x || !dy || !dw || !scratch) return fail(nullptr, SVAE_EBADARG, "bad op args");
+  static svae_ctx dummy;
+  dummy.m.g.B = n;
+  dummy.st = (hipStream_t)stream;
+  dummy.slab = (float*)scratch;
+  dummy.slab_cap = scratch_bytes / (int64_t)sizeof(float);
+  ConvL L;
+  L.cin = cin; L.cout = cout; L.stride = stride; L.hin = h; L.tr = transpose != 0;
+  L.hout = L.tr ? h * stride : h / stride;
+  int r = conv_wgrad(&dummy, L, 1, 0, View{(float*)x, cin, 0}, dy, 0, dw);
+  if (r) return fail(nullptr, r, dummy.err);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(nullptr, SVAE_EHIP, hipGetErrorString(e));
+}
+
+int svae_op_bn_act(const float* x, int64_t rows, int c, const float* beta, int act, float* y, float* mean,
+                   float* invstd, void* scratch, int64_t scratch_bytes, void* stream) {
+  if (!x || !beta || !y || !mean || !invstd || !scratch || c % 4) return fail(nullptr, SVAE_EBADARG, "bad op args");
+  hipStream_t s = (hipStream_t)stream;
+  const int nrb = bn_bwd_rowblocks(rows, c);
+  if ((int64_t)nrb * 2 * c * 4 + 2 * c * 4 > scratch_bytes) return fail(nullptr, SVAE_EBADARG, "scratch too small");
+  float* part = (float*)scratch;
+  float* zi = part + (long long)nrb * 2 * c;  // zeros (mean) / ones (invstd) for the raw-moment reduction
+  fill_f32(zi, c, 0.f, s);
+  fill_f32(zi + c, c, 1.f, s);
+  // sum(x), sum(x^2) via the backward reducer with act=none, mean=0, invstd=1
+  bn_bwd_reduce(x, c, 0, x, c, 0, x, c, 0, rows, c, zi, zi + c, 0, ACT_NONE, part, 0, 1, s);
+  bn_finalize(part, 0, nrb, c, rows, 1e-3f, mean, invstd, 0, 1, s);
+  bn_apply(x, c, 0, rows, c, mean, invstd, 0, beta, 0, nullptr, 0, 0, act, y, c, 0, 1, s);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(nullptr, SVAE_EHIP, hipGetErrorString(e));
+}
+
+int svae_op_bn_act_bwd(const float* dy, const float* y, const float* x, int64_t rows, int c, const float* mean,
+                       const float* invstd, int act, float* dx, float* dbeta, void* scratch, int64_t scratch_bytes,
+                       void* stream) {
+  if (!dy || !y || !x || !dx || !dbeta || !scratch || c % 4) return fail(nullptr, SVAE_EBADARG, "bad op args");
+  static svae_ctx dummy;
+  dummy.st = (hipStream_t)stream;
+  const int nrb = bn_bwd_rowblocks(rows, c);
+  dummy.part = (float*)scratch;
+  dummy.part_cap = (long long)nrb * 2 * c;
+  dummy.ab = dummy.part + dummy.part_cap;
+  dummy.ab_cap = 2LL * c;
+  if ((dummy.part_cap + dummy.ab_cap) * 4 > scratch_bytes) return fail(nullptr, SVAE_EBADARG, "scratch too small");
+  dummy.Gr = dbeta;
+  BNS bn{(float*)mean, (float*)invstd};
+  int r = bn_act_bwd(&dummy, 1, rows, c, View{(float*)dy, c, 0}, View{(float*)y, c, 0}, x, 0, c, bn, 0, 0, 0, act, dx,
+                     0, View{}, 0);
+  if (r) return fail(nullptr, r, dummy.err);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(nullptr, SVAE_EHIP, hipGetErrorString(e));
+}
+
+int svae_op_fc(const float* x, int b, int k, const float* w, int nout, float* y, void* stream) {
+  if (!x || !w || !y || nout % 4 || k % 4) return fail(nullptr, SVAE_EBADARG, "bad op args");
+  FwdArgs a{};
+  a.A = x; a.lda = k;
+  a.B = w; a.b_nk = 0; a.ldb = nout; a.b_tap = 0;
+  a.C = y; a.ldc = nout;
+  a.N = nout; a.Cin = k;
+  a.g.mode = GM_DENSE; a.g.nimg = b; a.g.ksz = 1; a.g.stride = 1;
+  a.rows = b; a.nclass = 1;
+  igemm_fwd(a, 1, (hipStream_t)stream);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(nullptr, SVAE_EHIP, hipGetErrorString(e));
+}
+
+}  // extern "C"

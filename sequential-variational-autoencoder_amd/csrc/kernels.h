@@ -1,0 +1,125 @@
+// Host-side launch API of the Sequential-VAE HIP kernels (internal to libsvae_hip.so).
+#pragma once
+#include "common.h"
+
+// gather-GEMM  C[p][n] (+)= act(bias + sum_{tap,k} A[src(p,tap)][k] * B[tap][k|n][n|k])
+struct FwdArgs {
+  const float* A; long long a_gs; int lda;
+  const float* B; long long b_gs; int ldb; long long b_tap; int b_nk;
+  float* C; long long c_gs; int ldc;
+  float* stats; long long s_gs;           // per-column partial (sum,sum^2): [rowblock][2][N]
+  const float* bias; long long bias_gs;
+  int N, Cin;
+  ConvGeom g;
+  int act, accumulate;
+  int rows;     // rows (output pixels) per parity class
+  int nclass;   // 4 for stride-2 conv-transpose, else 1
+  int mtiles;   // filled by the launcher
+};
+
+// weight-GEMM  part[split][tap][m][n] = sum_{p in split} G[src(p,tap)][m] * D[p][n]
+struct WgArgs {
+  const float* G; long long g_gs; int ldg;
+  const float* D; long long d_gs; int ldd;
+  float* part; long long p_gs;
+  int M, N;
+  ConvGeom g;   // mode CONV or DENSE; row space = D's pixels, gathered space = G's pixels
+  int rows, chunk, nsplit, ntap;
+};
+
+int igemm_fwd_bm(const FwdArgs& a);
+void igemm_fwd(FwdArgs a, int groups, hipStream_t s);
+void wgrad(WgArgs a, int groups, hipStream_t s);
+void wgrad_reduce(const float* part, long long p_gs, int nsplit, int ntap, int M, int N, float* out0,
+                  long long o0_gs, int msplit, float* out1, long long o1_gs, int accumulate, int groups,
+                  hipStream_t s);
+
+// ---- BatchNorm (training mode, beta only, eps 1e-3: abstract_network.py:22) ----
+// stats partial [nrb][2][C] -> mean[C], invstd[C]
+void bn_finalize(const float* part, long long part_gs, int nrb, int C, long long count, float eps, float* mean,
+                 float* invstd, long long ms_gs, int groups, hipStream_t s);
+// out = act((pre - mean)*invstd + beta [+ res])
+void bn_apply(const float* pre, int ldp, long long pre_gs, long long rows, int C, const float* mean,
+              const float* invstd, long long ms_gs, const float* beta, long long beta_gs, const float* res,
+              int ldr, long long res_gs, int act, float* out, int ldo, long long out_gs, int groups,
+              hipStream_t s);
+// partial sums of dz and dz*xhat, dz = dy*act'(y)   -> part [nrb][2][C]; returns nrb via out param
+int bn_bwd_rowblocks(long long rows, int C);
+void bn_bwd_reduce(const float* dy, int lddy, long long dy_gs, const float* y, int ldy, long long y_gs,
+                   const float* pre, int ldp, long long pre_gs, long long rows, int C, const float* mean,
+                   const float* invstd, long long ms_gs, int act, float* part, long long part_gs, int groups,
+                   hipStream_t s);
+// per-channel: a = sum(dz)/n, b = sum(dz*xhat)/n, dbeta = sum(dz)
+void bn_bwd_finalize(const float* part, long long part_gs, int nrb, int C, long long count, float* ab,
+                     long long ab_gs, float* dbeta, long long dbeta_gs, int groups, hipStream_t s);
+// dpre = invstd*(dz - a - xhat*b); optional dres (+)= dz
+void bn_bwd_apply(const float* dy, int lddy, long long dy_gs, const float* y, int ldy, long long y_gs,
+                  const float* pre, int ldp, long long pre_gs, long long rows, int C, const float* mean,
+                  const float* invstd, long long ms_gs, const float* ab, long long ab_gs, int act, float* dpre,
+                  int lddp, long long dpre_gs, float* dres, int ldres, long long dres_gs, int res_acc, int groups,
+                  hipStream_t s);
+
+// ---- split_latent FC(K=Dl) + BN over batch + lrelu, fused (sequential_vae.py:1801-1806) ----
+// out[n][j] written at out + n*o_n + (j / F)*ldo + (j % F)
+void splitfc_fwd(const float* z, int ldz, int zoff, int B, int K, const float* W, const float* beta, int J,
+                 float* mean, float* invstd, float* out, long long o_n, int F, int ldo, hipStream_t s);
+// writes dpre [B][J] (scratch), dW [K][J], dbeta [J]
+void splitfc_bwd(const float* z, int ldz, int zoff, int B, int K, const float* W, const float* beta, int J,
+                 const float* mean, const float* invstd, const float* dout, long long o_n, int F, int ldo, float* dW,
+                 float* dbeta, float* dpre, hipStream_t s);
+// dz[n][zoff+d] += sum_j dpre[n][j] W[d][j]   (part: scratch [ceil(J/4096)][B][K])
+void splitfc_dz_gemm(const float* dpre, int B, int J, const float* W, int K, float* part, float* dz, int ldz, int zoff,
+                     hipStream_t s);
+
+// ---- recognition heads: [mean|std] = ladder @ [Wm|Ws] (sequential_vae.py:1592-1594,1607-1609) ----
+int heads_splits(int K);
+// part[split][n][coff+o] (mean) and part[split][n][pcols/2+coff+o] (std)
+void heads_fwd(const float* X, long long x_gs, int B, int K, const float* Wm, const float* Ws, long long w_gs, int D,
+               float* part, long long part_gs, int pcols, int coff, int groups, hipStream_t s);
+struct LatentLvls {
+  const float* bm[8];
+  const float* bs[8];
+  int off[8];
+  int dim[8];
+  int L;
+};
+// mu_raw = sum part + bm, sig = sigmoid(sum part + bs), z = clip(mu) + sig*eps, kl_img per image
+void latent_fwd(const float* part, long long part_gs, int nsplit, int B, int Dz, const LatentLvls& lv,
+                long long bias_gs, float clipv, float prior, const float* eps, long long eps_gs, float* mu, float* sig,
+                float* z, long long ms_gs, float* kl_img, long long kl_gs, int groups, hipStream_t s);
+// dhead[n][0:Dz] = d mu_raw, dhead[n][Dz:2Dz] = d sig_pre; kl_coef (device) = reg*c_first/B
+void latent_bwd(const float* mu, const float* sig, const float* eps, const float* dz, long long gs, long long eps_gs,
+                int B, int Dz, const float* kl_coef, long long kc_gs, float prior, float clipv, float* dhead,
+                long long dh_gs, int groups, hipStream_t s);
+// dX (+)= dhead_l @ [Wm|Ws]^T ; dW = X^T dhead_l ; db = sum_n dhead_l   (w_gs: group stride of W/dW/db)
+void heads_bwd(const float* X, long long x_gs, float* dX, long long dx_gs, int B, int K, const float* Wm,
+               const float* Ws, long long w_gs, int D, const float* dhead, long long dh_gs, int dcols, int coff,
+               float* dWm, float* dWs, float* dbm, float* dbs, int accumulate, int groups, hipStream_t s);
+
+// ---- small-N gather conv (N <= 4: output conv-T 32->3(+1), encoder layer-0 dgrad) ----
+// C[p][o] (+)= bias + sum_tap sum_k A[src(p,tap)][k] * W(tap,o,k); W0 [tap][n0][K], W1 [tap][n1][K]
+void gconv_smalln(const float* A, int lda, int K, const float* W0, int n0, const float* W1, int n1, long long w_tap,
+                  long long w1_tap, const float* bias0, const float* bias1, ConvGeom g, long long rows_total,
+                  float* C, int ldc, int accumulate, hipStream_t s);
+
+// ---- output layer + highway + reconstruction (sequential_vae.py:1720-1729, :1146) ----
+int output_blocks_per_img(int HW);
+void output_fwd(const float* a, int B, int HW, int C, const float* xprev, const float* target, float lo, float hi,
+                float minh, float maxh, float* xhat, float* rec_part, int nblk, hipStream_t s);
+void output_bwd(const float* a, int B, int HW, int C, const float* xprev, const float* xhat, const float* target,
+                float lo, float hi, float minh, float maxh, float rec_coef, const float* dxhat_in, float* da,
+                float* dxprev, hipStream_t s);
+// per-step loss reduction: stats_out[0]=mean recon, [1]=mean kl; rec_img_out[b]
+void loss_reduce(const float* rec_part, int nblk, const float* kl_img, int B, int HWC, float* stats_out,
+                 float* rec_img_out, hipStream_t s);
+
+// ---- optimizer: clip(+-c) + TF Adam (sequential_vae.py:1267-1276) ----
+void adam_step(float* w, const float* g, float* m, float* v, long long n, float lr_t, float b1, float b2, float eps,
+               float clipv, hipStream_t s);
+
+// ---- misc ----
+void fill_f32(float* p, long long n, float v, hipStream_t s);
+void philox_normal(float* out, long long n, unsigned long long seed, unsigned long long offset, hipStream_t s);
+// column sums of X [rows][C<=4] -> out0[0..n0), out1[0..C-n0)   (part: scratch >= 1024 floats)
+void colsum_small(const float* X, int ld, long long rows, int C, float* part, float* out0, int n0, float* out1,
+                  hipStream_t s);

@@ -1,0 +1,638 @@
+// Bandwidth-bound kernels of the hot path: split_latent FC+BN, recognition heads,
+// reparameterised latent + KL, small-N conv (output / layer-0 dgrad), output +
+// highway + reconstruction loss, loss reduction, clip+Adam, Philox normals.
+#include "common.h"
+#include "kernels.h"
+
+#define KMAX 32  // max latent dims per level handled in registers (LSUN: 30)
+
+static int ew_blocks(long long work, int per = 256, int cap = 4096) {
+  long long b = (work + per - 1) / per;
+  return (int)(b < cap ? (b < 1 ? 1 : b) : cap);
+}
+
+// ---------------------------------------------------------------------------
+// split_latent: ladder_i = lrelu(BN_batch(z_i @ W_i + b_i))   (sequential_vae.py:1801-1806)
+// one thread per output feature j, the whole batch column recomputed from z (K <= 32)
+// ---------------------------------------------------------------------------
+__global__ void splitfc_fwd_kernel(const float* z, int ldz, int zoff, int B, int K, const float* W,
+                                   const float* beta, int J, float* mean, float* invstd, float* out, long long o_n,
+                                   int F, int ldo) {
+  extern __shared__ float zs[];  // [B][K]
+  for (int i = threadIdx.x; i < B * K; i += blockDim.x) zs[i] = z[(i / K) * ldz + zoff + (i % K)];
+  __syncthreads();
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= J) return;
+  float w[KMAX];
+#pragma unroll
+  for (int d = 0; d < KMAX; ++d) w[d] = d < K ? W[(long long)d * J + j] : 0.f;
+  auto pre = [&](int n) {
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < KMAX; ++d)
+      if (d < K) s = fmaf(zs[n * K + d], w[d], s);
+    return s;
+  };
+  float s = 0.f;
+  for (int n = 0; n < B; ++n) s += pre(n);
+  const float m = s / B;
+  float q = 0.f;
+  for (int n = 0; n < B; ++n) {
+    float d = pre(n) - m;
+    q += d * d;
+  }
+  const float is = 1.f / sqrtf(q / B + 1e-3f);
+  mean[j] = m;
+  invstd[j] = is;
+  const float b = beta[j];
+  float* dst = out + (long long)(j / F) * ldo + (j % F);
+  for (int n = 0; n < B; ++n) dst[n * o_n] = lrelu_f((pre(n) - m) * is + b);
+}
+
+void splitfc_fwd(const float* z, int ldz, int zoff, int B, int K, const float* W, const float* beta, int J,
+                 float* mean, float* invstd, float* out, long long o_n, int F, int ldo, hipStream_t s) {
+  hipLaunchKernelGGL(splitfc_fwd_kernel, dim3((J + 255) / 256), dim3(256), B * K * sizeof(float), s, z, ldz, zoff,
+                     B, K, W, beta, J, mean, invstd, out, o_n, F, ldo);
+}
+
+int splitfc_blocks(int J) { return (J + 255) / 256; }
+
+// backward: dpre[n][j] -> scratch (dz_part), dW, dbeta.  dz is formed by skinny_gemm afterwards.
+__global__ void splitfc_bwd_kernel(const float* z, int ldz, int zoff, int B, int K, const float* W,
+                                   const float* beta, int J, const float* mean, const float* invstd,
+                                   const float* dout, long long o_n, int F, int ldo, float* dW, float* dbeta,
+                                   float* dpre) {
+  extern __shared__ float zs[];
+  for (int i = threadIdx.x; i < B * K; i += blockDim.x) zs[i] = z[(i / K) * ldz + zoff + (i % K)];
+  __syncthreads();
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= J) return;
+  float w[KMAX];
+#pragma unroll
+  for (int d = 0; d < KMAX; ++d) w[d] = d < K ? W[(long long)d * J + j] : 0.f;
+  const float m = mean[j], is = invstd[j], b = beta[j];
+  const float* src = dout + (long long)(j / F) * ldo + (j % F);
+  auto xhat = [&](int n) {
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < KMAX; ++d)
+      if (d < K) s = fmaf(zs[n * K + d], w[d], s);
+    return (s - m) * is;
+  };
+  float sd = 0.f, sx = 0.f;
+  for (int n = 0; n < B; ++n) {
+    float xh = xhat(n);
+    float dz = src[n * o_n] * ((xh + b) > 0.f ? 1.f : 0.1f);
+    sd += dz;
+    sx += dz * xh;
+  }
+  const float a = sd / B, c = sx / B;
+  float gw[KMAX];
+#pragma unroll
+  for (int d = 0; d < KMAX; ++d) gw[d] = 0.f;
+  for (int n = 0; n < B; ++n) {
+    float xh = xhat(n);
+    float dz = src[n * o_n] * ((xh + b) > 0.f ? 1.f : 0.1f);
+    float dp = is * (dz - a - xh * c);
+    dpre[(long long)n * J + j] = dp;
+#pragma unroll
+    for (int d = 0; d < KMAX; ++d)
+      if (d < K) gw[d] = fmaf(zs[n * K + d], dp, gw[d]);
+  }
+#pragma unroll
+  for (int d = 0; d < KMAX; ++d)
+    if (d < K) dW[(long long)d * J + j] = gw[d];
+  dbeta[j] = sd;
+}
+
+void splitfc_bwd(const float* z, int ldz, int zoff, int B, int K, const float* W, const float* beta, int J,
+                 const float* mean, const float* invstd, const float* dout, long long o_n, int F, int ldo, float* dW,
+                 float* dbeta, float* dpre, hipStream_t s) {
+  hipLaunchKernelGGL(splitfc_bwd_kernel, dim3((J + 255) / 256), dim3(256), B * K * sizeof(float), s, z, ldz, zoff,
+                     B, K, W, beta, J, mean, invstd, dout, o_n, F, ldo, dW, dbeta, dpre);
+}
+
+// ---------------------------------------------------------------------------
+// skinny GEMM over a long reduction: part[split][n][coff+o] = sum_{k in split} X[n][k] * W[k*sk + o*so]
+// (recognition heads K=32768 -> D=3, and dz = dpre @ W^T of split_latent)
+// ---------------------------------------------------------------------------
+#define SK_ROWS 4
+#define SK_CHUNK 4096
+
+template <int DM>
+__global__ __launch_bounds__(256) void skinny_kernel(const float* X, int ldx, long long x_gs, int B, int K,
+                                                     const float* W, long long sk, long long so, long long w_gs,
+                                                     int D, float* part, long long p_gs, int pcols, int coff) {
+  __shared__ float red[4][SK_ROWS][DM];
+  const int group = blockIdx.z;
+  const int split = blockIdx.y;
+  const int r0 = blockIdx.x * SK_ROWS;
+  X += group * x_gs;
+  W += group * w_gs;
+  float acc[SK_ROWS][DM];
+#pragma unroll
+  for (int r = 0; r < SK_ROWS; ++r)
+#pragma unroll
+    for (int o = 0; o < DM; ++o) acc[r][o] = 0.f;
+  const int k0 = split * SK_CHUNK, k1 = min(K, k0 + SK_CHUNK);
+  for (int k = k0 + threadIdx.x; k < k1; k += 256) {
+    float w[DM];
+#pragma unroll
+    for (int o = 0; o < DM; ++o) w[o] = o < D ? W[k * sk + o * so] : 0.f;
+#pragma unroll
+    for (int r = 0; r < SK_ROWS; ++r) {
+      if (r0 + r < B) {
+        const float x = X[(long long)(r0 + r) * ldx + k];
+#pragma unroll
+        for (int o = 0; o < DM; ++o) acc[r][o] = fmaf(x, w[o], acc[r][o]);
+      }
+    }
+  }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int r = 0; r < SK_ROWS; ++r)
+#pragma unroll
+    for (int o = 0; o < DM; ++o) {
+      if (o < D) {
+        float v = wave_sum(acc[r][o]);
+        if (lane == 0) red[wave][r][o] = v;
+      }
+    }
+  __syncthreads();
+  if (threadIdx.x < SK_ROWS * DM) {
+    const int r = threadIdx.x / DM, o = threadIdx.x % DM;
+    if (o < D && r0 + r < B) {
+      float v = red[0][r][o] + red[1][r][o] + red[2][r][o] + red[3][r][o];
+      part[group * p_gs + ((long long)split * B + r0 + r) * pcols + coff + o] = v;
+    }
+  }
+}
+
+static void skinny(const float* X, int ldx, long long x_gs, int B, int K, const float* W, long long sk, long long so,
+                   long long w_gs, int D, float* part, long long p_gs, int pcols, int coff, int groups,
+                   hipStream_t s) {
+  dim3 grid((B + SK_ROWS - 1) / SK_ROWS, (K + SK_CHUNK - 1) / SK_CHUNK, groups);
+  if (D <= 4) hipLaunchKernelGGL(skinny_kernel<4>, grid, dim3(256), 0, s, X, ldx, x_gs, B, K, W, sk, so, w_gs, D,
+                                 part, p_gs, pcols, coff);
+  else if (D <= 8) hipLaunchKernelGGL(skinny_kernel<8>, grid, dim3(256), 0, s, X, ldx, x_gs, B, K, W, sk, so, w_gs, D,
+                                      part, p_gs, pcols, coff);
+  else hipLaunchKernelGGL(skinny_kernel<32>, grid, dim3(256), 0, s, X, ldx, x_gs, B, K, W, sk, so, w_gs, D, part,
+                          p_gs, pcols, coff);
+}
+
+int heads_splits(int K) { return (K + SK_CHUNK - 1) / SK_CHUNK; }
+
+void heads_fwd(const float* X, long long x_gs, int B, int K, const float* Wm, const float* Ws, long long w_gs, int D,
+               float* part, long long part_gs, int pcols, int coff, int groups, hipStream_t s) {
+  skinny(X, K, x_gs, B, K, Wm, D, 1, w_gs, D, part, part_gs, pcols, coff, groups, s);
+  skinny(X, K, x_gs, B, K, Ws, D, 1, w_gs, D, part, part_gs, pcols, pcols / 2 + coff, groups, s);
+}
+
+// dz[n][zoff+d] += sum_split part   where part = skinny(dpre [B][J], W^T)
+__global__ void splitfc_dz_kernel(const float* part, int nsplit, int B, int K, float* dz, int ldz, int zoff) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * K) return;
+  const int n = i / K, d = i % K;
+  float s = 0.f;
+  for (int sp = 0; sp < nsplit; ++sp) s += part[((long long)sp * B + n) * K + d];
+  dz[n * ldz + zoff + d] += s;
+}
+
+void splitfc_dz_gemm(const float* dpre, int B, int J, const float* W, int K, float* part, float* dz, int ldz, int zoff,
+                     hipStream_t s) {
+  skinny(dpre, J, 0, B, J, W, 1, J, 0, K, part, 0, K, 0, 1, s);
+  const int nsplit = (J + SK_CHUNK - 1) / SK_CHUNK;
+  hipLaunchKernelGGL(splitfc_dz_kernel, dim3((B * K + 255) / 256), dim3(256), 0, s, part, nsplit, B, K, dz, ldz, zoff);
+}
+
+// ---------------------------------------------------------------------------
+// latent: mu = clip(sum + bm), sig = sigmoid(sum + bs), z = mu + sig*eps, KL per image
+// (sequential_vae.py:1592-1594, :1023, :1156-1158)
+// ---------------------------------------------------------------------------
+__global__ void latent_fwd_kernel(const float* part, long long part_gs, int nsplit, int B, int Dz, LatentLvls lv,
+                                  long long bias_gs, float clipv, float prior, const float* eps, long long eps_gs,
+                                  float* mu, float* sig, float* z, long long ms_gs, float* kl_img, long long kl_gs) {
+  const int group = blockIdx.y;
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= B) return;
+  const float* P = part + group * part_gs;
+  const float p2 = prior * prior;
+  float kl = 0.f;
+  for (int l = 0; l < lv.L; ++l) {
+    for (int d = 0; d < lv.dim[l]; ++d) {
+      const int c = lv.off[l] + d;
+      float sm = 0.f, ss = 0.f;
+      for (int sp = 0; sp < nsplit; ++sp) {
+        sm += P[((long long)sp * B + n) * 2 * Dz + c];
+        ss += P[((long long)sp * B + n) * 2 * Dz + Dz + c];
+      }
+      float m = sm + lv.bm[l][group * bias_gs + d];
+      float mc = fminf(fmaxf(m, -clipv), clipv);
+      float sg = sigmoid_f(ss + lv.bs[l][group * bias_gs + d]);
+      const long long o = group * ms_gs + (long long)n * Dz + c;
+      mu[o] = m;  // raw (pre-clip) mean; the clip mask is re-derived in latent_bwd
+      sig[o] = sg;
+      z[o] = mc + sg * eps[group * eps_gs + (long long)n * Dz + c];
+      kl += -0.5f - __logf(sg) + 0.5f * sg * sg / p2 + 0.5f * mc * mc / p2;
+    }
+  }
+  kl_img[group * kl_gs + n] = kl / Dz;
+}
+
+void latent_fwd(const float* part, long long part_gs, int nsplit, int B, int Dz, const LatentLvls& lv,
+                long long bias_gs, float clipv, float prior, const float* eps, long long eps_gs, float* mu, float* sig,
+                float* z, long long ms_gs, float* kl_img, long long kl_gs, int groups, hipStream_t s) {
+  hipLaunchKernelGGL(latent_fwd_kernel, dim3((B + 127) / 128, groups), dim3(128), 0, s, part, part_gs, nsplit, B, Dz,
+                     lv, bias_gs, clipv, prior, eps, eps_gs, mu, sig, z, ms_gs, kl_img, kl_gs);
+}
+
+// dhead[n][d] = d(mu_raw), dhead[n][Dz+d] = d(sig pre-sigmoid); kl_coef = reg*c_first/B
+__global__ void latent_bwd_kernel(const float* mu, const float* sig, const float* eps, const float* dz, long long gs,
+                                  long long eps_gs, int B, int Dz, const float* kl_coef, long long kc_gs, float prior,
+                                  float clipv, float* dhead, long long dh_gs) {
+  const int group = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * Dz) return;
+  const int n = i / Dz, c = i % Dz;
+  const long long o = group * gs + i;
+  const float p2 = prior * prior;
+  const float kc = kl_coef[group * kc_gs] / Dz;
+  const float m = mu[o], sg = sig[o], g = dz[o];
+  const bool pass = m >= -clipv && m <= clipv;
+  const float mc = fminf(fmaxf(m, -clipv), clipv);
+  const float dmu = pass ? (g + kc * mc / p2) : 0.f;
+  const float dsig = g * eps[group * eps_gs + i] + kc * (-1.f / sg + sg / p2);
+  dhead[group * dh_gs + (long long)n * 2 * Dz + c] = dmu;
+  dhead[group * dh_gs + (long long)n * 2 * Dz + Dz + c] = dsig * sg * (1.f - sg);
+}
+
+void latent_bwd(const float* mu, const float* sig, const float* eps, const float* dz, long long gs, long long eps_gs,
+                int B, int Dz, const float* kl_coef, long long kc_gs, float prior, float clipv, float* dhead,
+                long long dh_gs, int groups, hipStream_t s) {
+  hipLaunchKernelGGL(latent_bwd_kernel, dim3((B * Dz + 255) / 256, groups), dim3(256), 0, s, mu, sig, eps, dz, gs,
+                     eps_gs, B, Dz, kl_coef, kc_gs, prior, clipv, dhead, dh_gs);
+}
+
+// heads backward for one level: dX (+)= dhead_l @ W^T ; dW = X^T dhead_l ; db = sum_n dhead_l
+template <int DM>
+__global__ __launch_bounds__(256) void heads_bwd_kernel(const float* X, long long x_gs, float* dX, long long dx_gs,
+                                                        int B, int K, const float* Wm, const float* Ws,
+                                                        long long w_gs, int D, const float* dhead, long long dh_gs,
+                                                        int dcols, int coff, float* dWm, float* dWs, float* dbm,
+                                                        float* dbs, int accumulate) {
+  extern __shared__ float dh[];  // [B][2*D]
+  const int group = blockIdx.y;
+  X += group * x_gs;
+  dX += group * dx_gs;
+  Wm += group * w_gs;
+  Ws += group * w_gs;
+  dhead += group * dh_gs;
+  for (int i = threadIdx.x; i < B * 2 * D; i += blockDim.x) {
+    const int n = i / (2 * D), o = i % (2 * D);
+    dh[i] = dhead[(long long)n * dcols + (o < D ? coff + o : dcols / 2 + coff + o - D)];
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x < 2 * D) {
+    float s = 0.f;
+    for (int n = 0; n < B; ++n) s += dh[n * 2 * D + threadIdx.x];
+    if (threadIdx.x < D) dbm[group * w_gs + threadIdx.x] = s;
+    else dbs[group * w_gs + threadIdx.x - D] = s;
+  }
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  float wm[DM], ws[DM], gm[DM], gs[DM];
+#pragma unroll
+  for (int o = 0; o < DM; ++o) {
+    wm[o] = o < D ? Wm[(long long)k * D + o] : 0.f;
+    ws[o] = o < D ? Ws[(long long)k * D + o] : 0.f;
+    gm[o] = gs[o] = 0.f;
+  }
+  for (int n = 0; n < B; ++n) {
+    const float x = X[(long long)n * K + k];
+    float dx = 0.f;
+#pragma unroll
+    for (int o = 0; o < DM; ++o) {
+      if (o < D) {
+        const float a = dh[n * 2 * D + o], b = dh[n * 2 * D + D + o];
+        dx = fmaf(a, wm[o], fmaf(b, ws[o], dx));
+        gm[o] = fmaf(x, a, gm[o]);
+        gs[o] = fmaf(x, b, gs[o]);
+      }
+    }
+    float* d = dX + (long long)n * K + k;
+    *d = accumulate ? *d + dx : dx;
+  }
+#pragma unroll
+  for (int o = 0; o < DM; ++o)
+    if (o < D) {
+      dWm[group * w_gs + (long long)k * D + o] = gm[o];
+      dWs[group * w_gs + (long long)k * D + o] = gs[o];
+    }
+}
+
+void heads_bwd(const float* X, long long x_gs, float* dX, long long dx_gs, int B, int K, const float* Wm,
+               const float* Ws, long long w_gs, int D, const float* dhead, long long dh_gs, int dcols, int coff,
+               float* dWm, float* dWs, float* dbm, float* dbs, int accumulate, int groups, hipStream_t s) {
+  dim3 grid((K + 255) / 256, groups);
+  size_t lds = (size_t)B * 2 * D * sizeof(float);
+  if (D <= 4)
+    hipLaunchKernelGGL(heads_bwd_kernel<4>, grid, dim3(256), lds, s, X, x_gs, dX, dx_gs, B, K, Wm, Ws, w_gs, D, dhead,
+                       dh_gs, dcols, coff, dWm, dWs, dbm, dbs, accumulate);
+  else if (D <= 8)
+    hipLaunchKernelGGL(heads_bwd_kernel<8>, grid, dim3(256), lds, s, X, x_gs, dX, dx_gs, B, K, Wm, Ws, w_gs, D, dhead,
+                       dh_gs, dcols, coff, dWm, dWs, dbm, dbs, accumulate);
+  else
+    hipLaunchKernelGGL(heads_bwd_kernel<32>, grid, dim3(256), lds, s, X, x_gs, dX, dx_gs, B, K, Wm, Ws, w_gs, D,
+                       dhead, dh_gs, dcols, coff, dWm, dWs, dbm, dbs, accumulate);
+}
+
+// ---------------------------------------------------------------------------
+// small-N gather conv (N <= 4): C[p][o] (+)= bias + sum_tap sum_k A[src(p,tap)][k] * W(tap,o,k)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void gconv_smalln_kernel(const float* A, int lda, int K, const float* W0, int n0,
+                                                           const float* W1, int n1, long long w_tap,
+                                                           long long w1_tap, const float* bias0, const float* bias1,
+                                                           ConvGeom g, long long rows, float* C, int ldc,
+                                                           int accumulate) {
+  extern __shared__ float ws[];  // [16 taps][4][K]
+  const int taps = g.ksz * g.ksz;
+  const int N = n0 + n1;
+  for (int i = threadIdx.x; i < taps * 4 * K; i += blockDim.x) {
+    const int t = i / (4 * K), r = i % (4 * K), o = r / K, k = r % K;
+    float v = 0.f;
+    if (o < n0) v = W0[t * w_tap + (long long)o * K + k];
+    else if (o < N) v = W1[t * w1_tap + (long long)(o - n0) * K + k];
+    ws[i] = v;
+  }
+  __syncthreads();
+  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= rows) return;
+  const int HWo = g.Ho * g.Wo;
+  const int n = (int)(p / HWo);
+  const int rem = (int)(p - (long long)n * HWo);
+  const int oy = rem / g.Wo, ox = rem % g.Wo;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int ky = 0; ky < g.ksz; ++ky) {
+    int iy;
+    if (g.mode == GM_CONV) iy = oy * g.stride - g.pad + ky;
+    else {
+      int t = oy + g.pad - ky;
+      if (t < 0 || (t % g.stride) != 0) continue;
+      iy = t / g.stride;
+    }
+    if (iy < 0 || iy >= g.Hi) continue;
+    for (int kx = 0; kx < g.ksz; ++kx) {
+      int ix;
+      if (g.mode == GM_CONV) ix = ox * g.stride - g.pad + kx;
+      else {
+        int t = ox + g.pad - kx;
+        if (t < 0 || (t % g.stride) != 0) continue;
+        ix = t / g.stride;
+      }
+      if (ix < 0 || ix >= g.Wi) continue;
+      const float* a = A + ((long long)(n * g.Hi + iy) * g.Wi + ix) * lda;
+      const float* w = ws + (ky * g.ksz + kx) * 4 * K;
+      if ((K & 3) == 0 && (lda & 3) == 0) {
+        for (int k = 0; k < K; k += 4) {
+          f32x4 av = *(const f32x4*)(a + k);
+#pragma unroll
+          for (int o = 0; o < 4; ++o)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[o] = fmaf(av[e], w[o * K + k + e], acc[o]);
+        }
+      } else {
+        for (int k = 0; k < K; ++k) {
+          const float av = a[k];
+#pragma unroll
+          for (int o = 0; o < 4; ++o) acc[o] = fmaf(av, w[o * K + k], acc[o]);
+        }
+      }
+    }
+  }
+  for (int o = 0; o < N; ++o) {
+    float v = acc[o];
+    if (o < n0 && bias0) v += bias0[o];
+    if (o >= n0 && bias1) v += bias1[o - n0];
+    float* d = C + p * ldc + o;
+    *d = accumulate ? *d + v : v;
+  }
+}
+
+void gconv_smalln(const float* A, int lda, int K, const float* W0, int n0, const float* W1, int n1, long long w_tap,
+                  long long w1_tap, const float* bias0, const float* bias1, ConvGeom g, long long rows_total,
+                  float* C, int ldc, int accumulate, hipStream_t s) {
+  size_t lds = (size_t)g.ksz * g.ksz * 4 * K * sizeof(float);
+  hipLaunchKernelGGL(gconv_smalln_kernel, dim3((unsigned)((rows_total + 255) / 256)), dim3(256), lds, s, A, lda, K, W0,
+                     n0, W1, n1, w_tap, w1_tap, bias0, bias1, g, rows_total, C, ldc, accumulate);
+}
+
+// ---------------------------------------------------------------------------
+// output layer + highway + reconstruction partials (sequential_vae.py:1720-1729, :1146)
+// a[p][0..C) = output deconv pre-act, a[p][C] = ratio deconv pre-act (ld = C+1)
+// ---------------------------------------------------------------------------
+#define OUT_TPB 256
+int output_blocks_per_img(int HW) { return (HW + OUT_TPB - 1) / OUT_TPB; }
+
+__global__ void output_fwd_kernel(const float* a, int HW, int C, const float* xprev, const float* target, float lo,
+                                  float hi, float minh, float maxh, float* xhat, float* rec_part, int nblk) {
+  __shared__ float red[OUT_TPB / 64];
+  const int n = blockIdx.y;
+  const int pix = blockIdx.x * OUT_TPB + threadIdx.x;
+  float s = 0.f;
+  if (pix < HW) {
+    const long long p = (long long)n * HW + pix;
+    const float* ap = a + p * (C + 1);
+    float rr = 1.f;
+    if (xprev) rr = minh + (maxh - minh) * sigmoid_f(ap[C]);
+    for (int c = 0; c < C; ++c) {
+      float out = (hi - lo) * sigmoid_f(ap[c]) + lo;
+      float x = xprev ? rr * out + (1.f - rr) * xprev[p * C + c] : out;
+      xhat[p * C + c] = x;
+      float d = x - target[p * C + c];
+      s += d * d;
+    }
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < OUT_TPB / 64; ++w) t += red[w];
+    rec_part[n * nblk + blockIdx.x] = t;
+  }
+}
+
+void output_fwd(const float* a, int B, int HW, int C, const float* xprev, const float* target, float lo, float hi,
+                float minh, float maxh, float* xhat, float* rec_part, int nblk, hipStream_t s) {
+  hipLaunchKernelGGL(output_fwd_kernel, dim3(nblk, B), dim3(OUT_TPB), 0, s, a, HW, C, xprev, target, lo, hi, minh, maxh,
+                     xhat, rec_part, nblk);
+}
+
+// g = dxhat_in + rec_coef*2*(xhat - target); da (pre-sigmoid), dxprev = (1-r)*g
+__global__ void output_bwd_kernel(const float* a, long long P, int C, const float* xprev, const float* xhat,
+                                  const float* target, float lo, float hi, float minh, float maxh, float rec_coef,
+                                  const float* dxhat_in, float* da, float* dxprev) {
+  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const float* ap = a + p * (C + 1);
+  float* dap = da + p * (C + 1);
+  float rr = 1.f, sr = 0.f;
+  if (xprev) {
+    sr = sigmoid_f(ap[C]);
+    rr = minh + (maxh - minh) * sr;
+  }
+  float drr = 0.f;
+  for (int c = 0; c < C; ++c) {
+    const long long i = p * C + c;
+    float g = rec_coef * 2.f * (xhat[i] - target[i]);
+    if (dxhat_in) g += dxhat_in[i];
+    const float o = sigmoid_f(ap[c]);
+    const float out = (hi - lo) * o + lo;
+    const float dout = xprev ? rr * g : g;
+    dap[c] = dout * (hi - lo) * o * (1.f - o);
+    if (xprev) {
+      drr += g * (out - xprev[i]);
+      dxprev[i] = (1.f - rr) * g;
+    }
+  }
+  dap[C] = xprev ? drr * (maxh - minh) * sr * (1.f - sr) : 0.f;
+}
+
+void output_bwd(const float* a, int B, int HW, int C, const float* xprev, const float* xhat, const float* target,
+                float lo, float hi, float minh, float maxh, float rec_coef, const float* dxhat_in, float* da,
+                float* dxprev, hipStream_t s) {
+  long long P = (long long)B * HW;
+  hipLaunchKernelGGL(output_bwd_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, a, P, C, xprev, xhat,
+                     target, lo, hi, minh, maxh, rec_coef, dxhat_in, da, dxprev);
+}
+
+// step scalars: stats_out[0] = mean_b recon_b, stats_out[1] = mean_b kl_b; rec_img_out[b] = recon_b
+__global__ void loss_reduce_kernel(const float* rec_part, int nblk, const float* kl_img, int B, int HWC,
+                                   float* stats_out, float* rec_img_out) {
+  __shared__ float red[2][4];
+  float sr = 0.f, sk = 0.f;
+  for (int n = threadIdx.x; n < B; n += blockDim.x) {
+    float r = 0.f;
+    for (int b = 0; b < nblk; ++b) r += rec_part[n * nblk + b];
+    r /= HWC;
+    rec_img_out[n] = r;
+    sr += r;
+    sk += kl_img[n];
+  }
+  sr = wave_sum(sr);
+  sk = wave_sum(sk);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = sr;
+    red[1][threadIdx.x >> 6] = sk;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0.f, b = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+      a += red[0][w];
+      b += red[1][w];
+    }
+    stats_out[0] = a / B;
+    stats_out[1] = b / B;
+  }
+}
+
+void loss_reduce(const float* rec_part, int nblk, const float* kl_img, int B, int HWC, float* stats_out,
+                 float* rec_img_out, hipStream_t s) {
+  hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(256), 0, s, rec_part, nblk, kl_img, B, HWC, stats_out,
+                     rec_img_out);
+}
+
+// ---------------------------------------------------------------------------
+// clip_by_value(+-clip) + tf.train.AdamOptimizer (sequential_vae.py:1267,1274-1276)
+// ---------------------------------------------------------------------------
+__global__ void adam_kernel(float* w, const float* g, float* m, float* v, long long n, float lr_t, float b1, float b2,
+                            float eps, float clipv) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    float gg = fminf(fmaxf(g[i], -clipv), clipv);
+    float mm = b1 * m[i] + (1.f - b1) * gg;
+    float vv = b2 * v[i] + (1.f - b2) * gg * gg;
+    m[i] = mm;
+    v[i] = vv;
+    w[i] -= lr_t * mm / (sqrtf(vv) + eps);
+  }
+}
+
+void adam_step(float* w, const float* g, float* m, float* v, long long n, float lr_t, float b1, float b2, float eps,
+               float clipv, hipStream_t s) {
+  hipLaunchKernelGGL(adam_kernel, dim3(ew_blocks(n, 256, 8192)), dim3(256), 0, s, w, g, m, v, n, lr_t, b1, b2, eps,
+                     clipv);
+}
+
+__global__ void fill_kernel(float* p, long long n, float v) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+void fill_f32(float* p, long long n, float v, hipStream_t s) {
+  hipLaunchKernelGGL(fill_kernel, dim3(ew_blocks(n)), dim3(256), 0, s, p, n, v);
+}
+
+// Philox4x32-10 -> Box-Muller normals (throughput-mode eps; parity mode injects eps)
+__device__ __forceinline__ void philox(unsigned& c0, unsigned& c1, unsigned& c2, unsigned& c3, unsigned k0,
+                                       unsigned k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    unsigned long long p0 = (unsigned long long)0xD2511F53u * c0;
+    unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c2;
+    unsigned h0 = (unsigned)(p0 >> 32), l0 = (unsigned)p0;
+    unsigned h1 = (unsigned)(p1 >> 32), l1 = (unsigned)p1;
+    unsigned n0 = h1 ^ c1 ^ k0, n2 = h0 ^ c3 ^ k1;
+    c0 = n0; c1 = l1; c2 = n2; c3 = l0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+__global__ void philox_normal_kernel(float* out, long long n, unsigned long long seed, unsigned long long offset) {
+  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q * 4 >= n) return;
+  unsigned long long ctr = offset + q;
+  unsigned c0 = (unsigned)ctr, c1 = (unsigned)(ctr >> 32), c2 = 0, c3 = 0;
+  philox(c0, c1, c2, c3, (unsigned)seed, (unsigned)(seed >> 32));
+  const float inv = 2.3283064365386963e-10f;
+  float u0 = (c0 + 0.5f) * inv, u1 = (c1 + 0.5f) * inv, u2 = (c2 + 0.5f) * inv, u3 = (c3 + 0.5f) * inv;
+  float r0 = sqrtf(-2.f * __logf(u0)), r1 = sqrtf(-2.f * __logf(u2));
+  float v[4] = {r0 * __cosf(6.2831853f * u1), r0 * __sinf(6.2831853f * u1), r1 * __cosf(6.2831853f * u3),
+                r1 * __sinf(6.2831853f * u3)};
+  for (int e = 0; e < 4; ++e)
+    if (q * 4 + e < n) out[q * 4 + e] = v[e];
+}
+
+void philox_normal(float* out, long long n, unsigned long long seed, unsigned long long offset, hipStream_t s) {
+  long long q = (n + 3) / 4;
+  hipLaunchKernelGGL(philox_normal_kernel, dim3((unsigned)((q + 255) / 256)), dim3(256), 0, s, out, n, seed, offset);
+}
+
+// column sums of a narrow matrix (C <= 4): output conv-T bias gradients (sum over pixels)
+#define CS_BLOCKS 256
+__global__ void colsum_part_kernel(const float* X, int ld, long long rows, int C, float* part) {
+  __shared__ float red[4][4];
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (long long)gridDim.x * blockDim.x)
+    for (int c = 0; c < C; ++c) s[c] += X[r * ld + c];
+  for (int c = 0; c < 4; ++c) {
+    float v = wave_sum(s[c]);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][c] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) part[blockIdx.x * 4 + threadIdx.x] = red[0][threadIdx.x] + red[1][threadIdx.x] +
+                                                            red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+__global__ void colsum_fin_kernel(const float* part, int nblk, int C, float* out0, int n0, float* out1) {
+  const int c = threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += part[b * 4 + c];
+  if (c < n0) out0[c] = s;
+  else if (out1) out1[c - n0] = s;
+}
+void colsum_small(const float* X, int ld, long long rows, int C, float* part, float* out0, int n0, float* out1,
+                  hipStream_t s) {
+  hipLaunchKernelGGL(colsum_part_kernel, dim3(CS_BLOCKS), dim3(256), 0, s, X, ld, rows, C, part);
+  hipLaunchKernelGGL(colsum_fin_kernel, dim3(1), dim3(64), 0, s, part, CS_BLOCKS, C, out0, n0, out1);
+}

@@ -1,0 +1,174 @@
+"""Drop-in mirror of the reference ``SequentialVAE`` training / test interface.
+
+Reference interface (sequential_vae.py:1341-1391, abstract_network.py:155-160):
+
+* ``train(input_batch, batch_target) -> float`` — one optimisation step: advances
+  ``iteration``, decays the learning rate, feeds ``reg_coeff = 1 - exp(-it/5000)``,
+  runs ``[train_op, loss, final_loss]`` and returns ``final_loss / H / W``.
+* ``test(input_batch) -> ndarray[B,H,W,C]`` — the last training-branch MLE
+  ``training_mles[-1]`` (BN in training mode, fresh eps).
+
+Here the step runs on the HIP engine (libsvae_hip.so): the forward + backward of
+the whole unrolled chain, then elementwise clip(+-10) + TF Adam on the flat
+parameter buffer.  Parameters, gradients and inputs are torch device tensors whose
+pointers are handed to the C ABI; no CPU fallback exists.
+"""
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import SVAEConfig, preset
+from .weights import init_flat, param_table, unflatten
+
+
+class SequentialVAE:
+    def __init__(self, config="celeba", batch_size=None, device=None, seed=0, grad_hook=None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("SequentialVAE (HIP engine) needs a GPU; no CPU fallback exists")
+        cfg = preset(config) if isinstance(config, str) else config
+        if batch_size is not None:
+            cfg = preset_copy(cfg, batch=batch_size)
+        self.cfg = cfg
+        self.name = config if isinstance(config, str) else "custom"
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        self.batch_size = cfg.batch
+        self.data_dims = [cfg.height, cfg.width, cfg.channels]
+        self.iteration = 0                                 # abstract_network.py:103
+        self.learning_rate = cfg.learning_rate             # sequential_vae.py:253
+        self.grad_hook = grad_hook                         # e.g. data-parallel all-reduce
+        self.L = _lib.lib()
+        self.table, self.n_total, self.n_live = param_table(cfg)
+        self._by_name = {p["name"]: p for p in self.table}
+        with torch.cuda.device(self.device):
+            self.params = torch.from_numpy(init_flat(cfg, seed)).to(self.device)
+            self.grads = torch.zeros(self.n_total, dtype=torch.float32, device=self.device)
+            h = ctypes.c_void_p()
+            c = cfg.to_c()
+            _lib.check(self.L.svae_create(ctypes.byref(c), self.device.index, ctypes.byref(h)))
+        self.ctx = h
+        _lib.check(self.L.svae_bind(self.ctx, _lib.ptr(self.params), _lib.ptr(self.grads)), self.ctx)
+        self._last_reg = 1.0
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.L.svae_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ low level
+    def _dev(self, a):
+        if isinstance(a, torch.Tensor):
+            t = a.to(self.device, dtype=torch.float32)
+        else:
+            t = torch.as_tensor(np.asarray(a, dtype=np.float32), device=self.device)
+        return t.contiguous()
+
+    def forward(self, x, target, eps=None, reg_coeff=1.0, stream=None):
+        """Forward of the unrolled chain.  eps [T,B,Dz] or None (device Philox)."""
+        x, target = self._dev(x), self._dev(target)
+        exp = (self.cfg.batch, self.cfg.height, self.cfg.width, self.cfg.channels)
+        if tuple(x.shape) != exp or tuple(target.shape) != exp:
+            raise ValueError("input must be %s, got %s / %s" % (exp, tuple(x.shape), tuple(target.shape)))
+        e = None
+        if eps is not None:
+            e = self._dev(eps)
+            if tuple(e.shape) != (self.cfg.mc_steps, self.cfg.batch, self.cfg.latent_dim):
+                raise ValueError("eps must be [T,B,Dz]")
+        self._keep = (x, target, e)  # keep device inputs alive until backward
+        self._last_reg = float(reg_coeff)
+        _lib.check(self.L.svae_forward(self.ctx, _lib.ptr(x), _lib.ptr(target), _lib.ptr(e), float(reg_coeff),
+                                       _lib.stream_ptr(stream)), self.ctx)
+
+    def backward(self, stream=None):
+        _lib.check(self.L.svae_backward(self.ctx, _lib.stream_ptr(stream)), self.ctx)
+        if self.grad_hook is not None:
+            self.grad_hook(self.grads[:self.n_live])
+
+    def apply_gradients(self, lr=None, step=None, stream=None):
+        lr = self.learning_rate if lr is None else lr
+        step = self.iteration if step is None else step
+        _lib.check(self.L.svae_adam(self.ctx, float(lr), int(step), float(self.cfg.clip_grad_value),
+                                    _lib.stream_ptr(stream)), self.ctx)
+
+    def copy_out(self, which, step, n):
+        out = torch.empty(n, dtype=torch.float32, device=self.device)
+        _lib.check(self.L.svae_copy_out(self.ctx, which, step, _lib.ptr(out), n, _lib.stream_ptr()), self.ctx)
+        return out
+
+    def step_stats(self):
+        """[T,2] tensor of (mean recon_t, mean KL_t)  (sequential_vae.py:1163-1164)."""
+        return torch.stack([self.copy_out(_lib.BUF_STEP_STATS, t, 2) for t in range(self.cfg.mc_steps)])
+
+    def loss_value(self, stats=None, reg_coeff=None):
+        """``self.loss`` (sequential_vae.py:1166-1176) = mean over the batch of the per-image ELBO."""
+        st = (self.step_stats() if stats is None else stats).double().cpu().numpy()
+        reg = self._last_reg if reg_coeff is None else reg_coeff
+        T = self.cfg.mc_steps
+        tot = 0.0
+        for t in range(T):
+            c = self.cfg.first_step_loss_coeff if t == 0 else 1.0
+            if self.cfg.intermediate_reconstruction or t == T - 1:
+                tot += 16.0 * c * st[t, 0]
+            tot += reg * c * st[t, 1]
+        return tot
+
+    def elbo_per_image(self):
+        T, B = self.cfg.mc_steps, self.cfg.batch
+        out = torch.zeros(B, dtype=torch.float64, device=self.device)
+        for t in range(T):
+            c = self.cfg.first_step_loss_coeff if t == 0 else 1.0
+            if self.cfg.intermediate_reconstruction or t == T - 1:
+                out += 16.0 * c * self.copy_out(_lib.BUF_REC_IMG, t, B).double()
+            out += self._last_reg * c * self.copy_out(_lib.BUF_KL_IMG, t, B).double()
+        return out
+
+    def xhat(self, t=-1):
+        t = t % self.cfg.mc_steps
+        c = self.cfg
+        return self.copy_out(_lib.BUF_XHAT, t, c.batch * c.height * c.width * c.channels).view(
+            c.batch, c.height, c.width, c.channels)
+
+    def latent(self, which, t):
+        return self.copy_out(which, t, self.cfg.batch * self.cfg.latent_dim).view(self.cfg.batch, self.cfg.latent_dim)
+
+    def param_dict(self):
+        return unflatten(self.params.cpu().numpy(), self.table)
+
+    def grad_dict(self):
+        return unflatten(self.grads.cpu().numpy(), self.table)
+
+    def param(self, name):
+        p = self._by_name[name]
+        return self.params[p["offset"]:p["offset"] + p["size"]].view(p["shape"])
+
+    # ------------------------------------------------------------------ reference API
+    def train(self, input_batch, batch_target):
+        """One training update; returns the final-step reconstruction loss per pixel
+        (sequential_vae.py:1341-1375)."""
+        self.iteration += 1
+        self.learning_rate *= self.cfg.learning_rate_decay
+        reg = 1.0 - math.exp(-self.iteration / self.cfg.reg_coeff_rate)
+        self.forward(input_batch, batch_target, None, reg)
+        self.backward()
+        self.apply_gradients(self.learning_rate, self.iteration)
+        final = float(self.copy_out(_lib.BUF_STEP_STATS, self.cfg.mc_steps - 1, 2)[0])
+        return final / self.data_dims[0] / self.data_dims[1]
+
+    def test(self, input_batch):
+        """training_mles[-1] for the batch (sequential_vae.py:1381-1391; reg_coeff default 1.0)."""
+        self.forward(input_batch, input_batch, None, 1.0)
+        return self.xhat(-1).cpu().numpy()
+
+
+def preset_copy(cfg, **over):
+    from dataclasses import replace
+    return replace(cfg, **over)

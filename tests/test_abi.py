@@ -1,0 +1,70 @@
+"""CPU checks of the drop-in boundary: the C-ABI library builds for gfx950, loads,
+exports every entry point include/svae_hip.h declares, and its (pure-host)
+parameter layout equals the oracle's restatement of the reference variable table."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, pkg_mod
+from oracle import spec, weightgen
+
+
+def _header_symbols():
+    txt = open(os.path.join(ROOT, "include", "svae_hip.h")).read()
+    return sorted(set(re.findall(r"\b(svae_[a-z_]+)\s*\(", txt)))
+
+
+def test_library_exports_header_symbols(built_lib):
+    lib = ctypes.CDLL(built_lib)
+    syms = _header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert sorted(pkg_mod("_lib").EXPORTED) == syms
+
+
+@pytest.mark.parametrize("preset", ["tiny", "celeba", "lsun", "mnist_1step"])
+def test_layout_matches_oracle_table(built_lib, preset):
+    W = pkg_mod("weights")
+    cfg = pkg_mod("config").preset(preset)
+    table, n_total, n_live = W.param_table(cfg)
+    otab, _ = spec.build_params(spec.make_config(preset))
+    key = lambda p: (p["name"], tuple(p["shape"]), p["dead"], p["zero_grad"], p["init"])
+    assert sorted(map(key, table)) == sorted(map(key, otab))
+    # offsets tile [0, n_total) exactly; live tensors first
+    spans = sorted((p["offset"], p["offset"] + p["size"], p["dead"] or p["zero_grad"]) for p in table)
+    pos = 0
+    for a, b, frozen in spans:
+        assert a == pos
+        assert (a >= n_live) == frozen
+        pos = b
+    assert pos == n_total
+    # recognition blocks: identical per-step layout at a constant stride (batched launches)
+    off = {p["name"]: p["offset"] for p in table}
+    t0 = [n for n in off if n.startswith("phi/inference_step_0/") and n in off and off[n] < n_live]
+    if cfg.mc_steps > 1:
+        stride = off[t0[0].replace("step_0", "step_1")] - off[t0[0]]
+        for n in t0:
+            assert off[n.replace("step_0", "step_1")] - off[n] == stride
+
+
+def test_weight_generators_agree(built_lib):
+    W = pkg_mod("weights")
+    cfg = pkg_mod("config").preset("tiny")
+    table, _, _ = W.param_table(cfg)
+    for p in table:
+        a = W.init_value(p["name"], p["shape"], p["init"], 7)
+        b = weightgen.generate(p["name"], p["shape"], p["init"], 7).ravel()
+        np.testing.assert_array_equal(a, b)
+
+
+def test_bad_config_rejected(built_lib):
+    L = pkg_mod("_lib")
+    cfg = pkg_mod("config").preset("tiny", batch=1).to_c()
+    n = ctypes.c_int64()
+    rc = L.lib().svae_param_count(ctypes.byref(cfg), ctypes.byref(n), None, None)
+    assert rc == -1
+    assert b"batch" in L.lib().svae_last_error(None)

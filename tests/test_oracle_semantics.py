@@ -1,0 +1,156 @@
+"""Known-answer tests of the TF-1.x op semantics the oracle restates,
+cross-check of the two independent restatements, and finite-difference gradient checks.
+
+The reference ships no tests or golden vectors and cannot run here (no TensorFlow),
+so these hand-computed cases are what pins the oracle (parity unpinned by the
+reference itself; see oracle/__init__.py)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import model, spec, tape as T, torch_twin
+
+
+def test_same_padding_k4():
+    # stride 2: pad 1/1 ; stride 1: pad 1 before, 2 after (abstract_network.py:18, TF SAME)
+    assert T.same_pads(64, 4, 2) == (32, 1, 1)
+    assert T.same_pads(32, 4, 1) == (32, 1, 2)
+    assert T.same_pads(4, 4, 2) == (2, 1, 1)
+
+
+def test_conv2d_same_known_answer():
+    # 1 channel 4x4 ramp, all-ones 4x4 kernel, stride 1: out[y,x] = sum of x over rows y-1..y+2, cols x-1..x+2
+    tp = T.Tape()
+    x = np.arange(16, dtype=np.float64).reshape(1, 4, 4, 1)
+    w = np.ones((4, 4, 1, 1))
+    y = T.conv2d(tp, tp.leaf(x), tp.leaf(w), 1).v[0, :, :, 0]
+    xp = np.pad(x[0, :, :, 0], ((1, 2), (1, 2)))
+    ref = np.array([[xp[i:i + 4, j:j + 4].sum() for j in range(4)] for i in range(4)])
+    np.testing.assert_allclose(y, ref)
+    assert y[0, 0] == (0 + 1 + 2 + 4 + 5 + 6 + 8 + 9 + 10)  # window rows -1..2, cols -1..2
+
+
+def test_conv2d_transpose_is_adjoint_of_conv():
+    rng = np.random.default_rng(0)
+    for s in (1, 2):
+        tp = T.Tape()
+        xs = rng.standard_normal((2, 8 // s, 8 // s, 3))   # conv output / conv-T input
+        w = rng.standard_normal((4, 4, 5, 3))               # conv [kh,kw,Cin=5,Cout=3] == conv-T [kh,kw,Cout=5,Cin=3]
+        u = rng.standard_normal((2, 8, 8, 5))               # conv input / conv-T output
+        ct = T.conv2d_transpose(tp, tp.leaf(xs), tp.leaf(w), s).v
+        cv = T.conv2d(tp, tp.leaf(u), tp.leaf(w), s).v
+        assert ct.shape == u.shape
+        np.testing.assert_allclose((ct * u).sum(), (cv * xs).sum(), rtol=1e-12)
+
+
+def test_conv2d_transpose_crop_offset():
+    # single impulse at input (0,0): TF SAME conv-T stride 2 places kernel tap (ky,kx) at output (ky-1,kx-1)
+    tp = T.Tape()
+    x = np.zeros((1, 2, 2, 1))
+    x[0, 0, 0, 0] = 1.0
+    w = np.arange(16, dtype=np.float64).reshape(4, 4, 1, 1)
+    y = T.conv2d_transpose(tp, tp.leaf(x), tp.leaf(w), 2).v[0, :, :, 0]
+    assert y.shape == (4, 4)
+    np.testing.assert_allclose(y[0:3, 0:3], w[1:4, 1:4, 0, 0])
+    assert y[3, :].sum() == 0 and y[:, 3].sum() == 0
+
+
+def test_batch_norm_beta_only_biased_var():
+    tp = T.Tape()
+    x = np.array([[1.0], [2.0], [3.0], [6.0]])
+    y = T.batch_norm(tp, tp.leaf(x), tp.leaf(np.array([0.5])), eps=1e-3).v
+    m, v = 3.0, ((x - 3.0) ** 2).mean()  # biased variance = 3.5
+    np.testing.assert_allclose(y[:, 0], (x[:, 0] - m) / np.sqrt(v + 1e-3) + 0.5)
+
+
+def test_lrelu_tie_gradient():
+    tp = T.Tape()
+    x = tp.leaf(np.array([-2.0, 0.0, 3.0]))
+    y = T.lrelu(tp, x)
+    np.testing.assert_allclose(y.v, [-0.2, 0.0, 3.0])
+    tp.backward(y, 1.0)
+    np.testing.assert_allclose(x.g, [0.1, 0.1, 1.0])  # TF Maximum/Minimum tie -> 0.1 at 0
+    tp2 = T.Tape()
+    x2 = tp2.leaf(np.array([0.0, 1.0]))
+    r = T.relu(tp2, x2)
+    tp2.backward(r, 1.0)
+    np.testing.assert_allclose(x2.g, [0.0, 1.0])
+
+
+def test_nhwc_flatten_order():
+    x = np.arange(2 * 2 * 3).reshape(1, 2, 2, 3)
+    flat = x.reshape(1, -1)[0]
+    # index (h*W + w)*C + c
+    assert flat[(1 * 2 + 0) * 3 + 2] == x[0, 1, 0, 2]
+    xt = torch.tensor(x).permute(0, 3, 1, 2)
+    assert torch_twin.nhwc_flatten(xt)[0].tolist() == flat.tolist()
+
+
+def test_last_level_heads_read_level2_ladder():
+    cfg = spec.make_config("celeba")
+    table, struct = spec.build_params(cfg)
+    shapes = {p["name"]: p["shape"] for p in table}
+    st = struct[0]["inference"]
+    # last-level heads consume the level L-2 flatten (8192 = 8*8*128), sequential_vae.py:1607,1609
+    assert shapes[st["last_mean"]["w"]] == (8192, 3)
+    assert shapes[st["levels"][2]["mean"]["w"]] == (8192, 3)
+    dead = [p for p in table if p["dead"] and p["name"].startswith("phi/inference_step_0/")]
+    assert {p["name"].split("/")[2] for p in dead} == {"Conv_6", "BatchNorm_6", "fully_connected_6", "BatchNorm_7"}
+
+
+def test_param_counts_match_survey():
+    for preset, used, dead in (("celeba", 75_371_871, 8_396_800), ("lsun", 108_317_567, 8_396_800),
+                               ("mnist_1step", 3_207_217, 656_000)):
+        table, _ = spec.build_params(spec.make_config(preset))
+        assert sum(np.prod(p["shape"]) for p in table if not p["dead"]) == used
+        assert sum(np.prod(p["shape"]) for p in table if p["dead"]) == dead
+
+
+@pytest.mark.parametrize("preset", ["tiny", "mnist_1step"])
+def test_oracle_matches_torch_twin(preset):
+    cfg = spec.make_config(preset)
+    _, struct, params = spec.init_params(cfg, seed=0)
+    x, tgt, eps = spec.make_inputs(cfg, batch=4)
+    o = model.forward_backward(cfg, struct, params, x, tgt, eps, reg_coeff=0.37)
+    tw = torch_twin.Twin(cfg, struct, params, dtype=torch.float64)
+    p = tw.step(x, tgt, eps, reg_coeff=0.37)
+    assert abs(o["loss"] - p["loss"]) <= 1e-12 * abs(o["loss"])
+    for t in range(cfg["mc_steps"]):
+        np.testing.assert_allclose(o["xhat"][t], p["xhat"][t], rtol=1e-10, atol=1e-12)
+    for k, g in o["grads"].items():
+        np.testing.assert_allclose(g, p["grads"][k], rtol=1e-8, atol=1e-12 * (1 + np.abs(g).max()), err_msg=k)
+
+
+def test_finite_difference_gradients():
+    cfg = spec.make_config("tiny", mc_steps=2)
+    _, struct, params = spec.init_params(cfg, seed=3)
+    x, tgt, eps = spec.make_inputs(cfg, batch=4, seed_x=5, seed_eps=6)
+    o = model.forward_backward(cfg, struct, params, x, tgt, eps, reg_coeff=0.8)
+    rng = np.random.default_rng(0)
+    names = [n for n in params if not n.endswith("biases") or "Conv2d_transpose_6" in n or "fully_connected" in n]
+    checked = 0
+    for name in rng.choice(sorted(names), size=12, replace=False):
+        g = o["grads"][name]
+        if np.abs(g).max() == 0:
+            continue
+        idx = np.unravel_index(np.argmax(np.abs(g)), g.shape)
+        h = 1e-7  # small step: relu/lrelu kinks make the loss only piecewise smooth
+        pp = {k: v.copy() for k, v in params.items()}
+        pp[name][idx] += h
+        lp = model.forward_backward(cfg, struct, pp, x, tgt, eps, 0.8, want_grads=False)["loss"]
+        pp[name][idx] -= 2 * h
+        lm = model.forward_backward(cfg, struct, pp, x, tgt, eps, 0.8, want_grads=False)["loss"]
+        fd = (lp - lm) / (2 * h)
+        assert abs(fd - g[idx]) <= 1e-4 * max(1.0, abs(g[idx])), (name, fd, g[idx])
+        checked += 1
+    assert checked >= 6
+
+
+def test_adam_matches_tf_formula():
+    p = {"w": np.array([1.0, -2.0])}
+    g = {"w": np.array([20.0, -0.5])}
+    m = {"w": np.zeros(2)}
+    v = {"w": np.zeros(2)}
+    p, m, v = model.adam_update(p, g, m, v, step=1, lr=2e-4)
+    # step 1: m = 0.1*clip(g), v = 0.001*g^2, lr_t = lr*sqrt(0.001)/0.1 -> update = lr*sign(g) (up to eps)
+    np.testing.assert_allclose(p["w"], [1.0 - 2e-4, -2.0 + 2e-4], rtol=1e-6)
