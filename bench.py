@@ -1,0 +1,232 @@
+"""Throughput bench of the Sequential-VAE training step on MI355X.
+
+Metric (BASELINE.json): images/sec + ELBO/img, CelebA 64x64 seq-VAE fwd+bwd at N GPUs.
+A step = forward of the unrolled 8-step chain + backward + (N>1: one RCCL all-reduce
+of the flat gradient over xGMI) + clip/Adam, on one synthetic [B,64,64,3] batch per
+GPU (B=128, weak scaling).  Inputs are resident in HBM before the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config celeba]
+N>1 is launched by the driver via torch.distributed.run (one rank per GPU).
+"""
+import argparse
+import importlib
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+PKG = "sequential-variational-autoencoder_amd"
+
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
+
+
+def conv_flops_per_img(cfg):
+    """Algorithmic fwd MACs per image of the executed graph (SURVEY §8a totals), x3 for
+    fwd+dgrad+wgrad, x2 FLOP/MAC."""
+    F, S, L, T = cfg.filter_sizes, cfg.image_sizes, cfg.levels, cfg.mc_steps
+    C = cfg.channels
+
+    def conv(cin, cout, hout):
+        return 16 * cin * cout * hout * hout
+
+    def convt(cin, cout, hin, s):
+        return 16 * cin * cout * hin * hin  # every input pixel scatters to 16 taps (4x4 kernel)
+
+    inf = 0
+    cin = F[0]
+    for lvl in range(L - 1):
+        inf += conv(cin, F[lvl + 1], S[lvl + 1]) + conv(F[lvl + 1], F[lvl + 1], S[lvl + 1])
+        inf += 2 * S[lvl + 1] ** 2 * F[lvl + 1] * cfg.latent_dims[lvl]
+        cin = F[lvl + 1]
+    inf += 2 * S[L - 1] ** 2 * F[L - 1] * cfg.latent_dims[L - 1]
+    enc = 0
+    cin = F[0]
+    for lvl in range(L - 1):
+        enc += conv(cin, F[lvl + 1], S[lvl + 1]) + conv(F[lvl + 1], F[lvl + 1], S[lvl + 1])
+        cin = F[lvl + 1]
+    enc += conv(F[L - 1], F[L - 1], S[L]) + S[L] ** 2 * F[L - 1] * F[L]
+    dec = 0
+    split = sum(cfg.latent_dims[i] * S[i + 1] ** 2 * F[i + 1] for i in range(L - 1)) + cfg.latent_dims[L - 1] * F[L + 1]
+    cin = F[L]
+    for lvl in range(L - 2, -1, -1):
+        dec += convt(cin, F[lvl + 1], S[lvl + 2], 2) + convt(2 * F[lvl + 1], F[lvl + 1], S[lvl + 1], 1)
+        cin = F[lvl + 1]
+    out0 = convt(F[1], C, S[1], 2)
+    ratio = convt(F[1], 1, S[1], 2)
+    top0 = F[L + 1] * S[L] ** 2 * F[L]
+    top = (F[L + 1] + F[L]) * S[L] ** 2 * F[L]
+    macs = T * (inf + dec + split + out0) + (T - 1) * (enc + ratio) + top0 + (T - 1) * top
+    return 3 * 2 * macs
+
+
+def dominant_kernel_shape(cfg):
+    """Decoder level-0 stride-1 conv-T (32x32, 2F1->F1): the largest single launch of
+    the forward (37% of MACs are the three decoder s1 layers)."""
+    F, S = cfg.filter_sizes, cfg.image_sizes
+    return dict(n=cfg.batch, h=S[1], cin=2 * F[1], cout=F[1], stride=1, transpose=1)
+
+
+def time_dominant_kernel(L, shape, iters=50):
+    """Average duration of the dominant kernel launch (HIP events on the launch stream)."""
+    n, h, cin, cout = shape["n"], shape["h"], shape["cin"], shape["cout"]
+    x = torch.randn(n, h, h, cin, device="cuda")
+    w = torch.randn(4, 4, cout, cin, device="cuda") * 0.02
+    y = torch.empty(n, h, h, cout, device="cuda")
+    st = L.stream_ptr()
+    for _ in range(5):
+        L.check(L.lib().svae_op_conv(L.ptr(x), n, h, cin, L.ptr(w), cout, 1, 1, L.ptr(y), st))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        L.check(L.lib().svae_op_conv(L.ptr(x), n, h, cin, L.ptr(w), cout, 1, 1, L.ptr(y), st))
+    e1.record()
+    torch.cuda.synchronize()
+    sec = e0.elapsed_time(e1) / 1000.0 / iters
+    flops = 2.0 * n * h * h * cout * 16 * cin
+    return sec, flops
+
+
+def cpu_baseline(cfg, target_sec=15.0, max_steps=4):
+    """PyTorch-CPU fp32 restatement of the same graph (oracle/torch_twin.py), fwd+bwd,
+    on a bounded sample: B=8 images of the CelebA geometry, whole T=8 chain."""
+    from oracle import spec, torch_twin
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    B = 8
+    cd = spec.make_config("celeba" if cfg.filter_sizes == [3, 32, 64, 128, 384, 512] and
+                          cfg.latent_dims == [3, 3, 3, 3] else "lsun", batch=B)
+    _, struct, params = spec.init_params(cd, seed=0, dtype=np.float32)
+    x, tgt, eps = spec.make_inputs(cd, batch=B)
+    tw = torch_twin.Twin(cd, struct, params, dtype=torch.float32)
+    tw.step(x, tgt, eps, 1.0)  # warm-up
+    t0 = time.time()
+    n = 0
+    while n < max_steps and (time.time() - t0) < target_sec:
+        tw.step(x, tgt, eps, 1.0)
+        n += 1
+    dt = (time.time() - t0) / n
+    return dict(value=B / dt, unit="images/sec", cores=threads, kind="port",
+                sample="%d fwd+bwd steps of B=%d CelebA-geometry images (T=8) with oracle/torch_twin.py fp32, "
+                       "%d threads" % (n, B, threads))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="celeba")
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    cfgmod = importlib.import_module(PKG + ".config")
+    SV = importlib.import_module(PKG + ".sequential_vae").SequentialVAE
+    par = importlib.import_module(PKG + ".parallel")
+    L = importlib.import_module(PKG + "._lib")
+    cfg = cfgmod.preset(args.config, **({"batch": args.batch} if args.batch else {}))
+    B = cfg.batch
+    hook = par.allreduce_hook(dist) if world > 1 else None
+    net = SV(cfg, seed=0, grad_hook=hook)
+
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1234 + rank)
+    lo, hi = cfg.range
+    x = (torch.rand(B, cfg.height, cfg.width, cfg.channels, device="cuda", generator=g) * (hi - lo) + lo).contiguous()
+    tgt = x
+
+    def step(it):
+        reg = 1.0 - math.exp(-it / cfg.reg_coeff_rate)
+        net.forward(x, tgt, None, reg)
+        net.backward()
+        net.apply_gradients(cfg.learning_rate, it)
+
+    it = 0
+    for _ in range(args.warmup):
+        it += 1
+        step(it)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        it += 1
+        step(it)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    elbo = net.loss_value()
+    if dist:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        e = torch.tensor([elbo], device="cuda", dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.SUM)
+        elbo = float(e.item()) / world
+
+    ms = elapsed / args.steps * 1000.0
+    value = world * B * args.steps / elapsed
+    flops_img = conv_flops_per_img(cfg)
+
+    roof = None
+    cpu = None
+    if rank == 0:
+        shape = dominant_kernel_shape(cfg)
+        sec, kflops = time_dominant_kernel(L, shape)
+        ach = kflops / sec / 1e12
+        roof = dict(bound="mfma", achieved=round(ach, 3), peak=FP32_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
+                    frac=round(ach / FP32_MFMA_PEAK_TFLOPS, 4), traffic=None,
+                    kernel="igemm_fwd_kernel<256,32,4,1,NK> decoder level-0 conv-T s1 %s" % (
+                        "x".join(str(shape[k]) for k in ("n", "h", "cin", "cout"))),
+                    kernel_us=round(sec * 1e6, 2),
+                    step_achieved_tflops=round(flops_img * value / world / 1e12, 3))
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(cfg)
+    if rank == 0:
+        line = {
+            "metric": "images/sec (CelebA 64x64 seq-VAE fwd+bwd+Adam step)",
+            "value": round(value, 2),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic U[-1,1] NHWC batch, target=input, eps on-device Philox; deterministic splitmix64 init",
+            "config": {"workload": "CelebA 64x64 default seq-VAE (c_inhomog), T=8 chain, fwd+bwd+clip+Adam",
+                       "model": args.config, "global_batch": B * world, "per_gpu_batch": B,
+                       "image": [cfg.height, cfg.width, cfg.channels], "mc_steps": cfg.mc_steps,
+                       "parallelism": "dp%d" % world},
+            "elbo_per_img": round(elbo, 5),
+            "flops_per_img": flops_img,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

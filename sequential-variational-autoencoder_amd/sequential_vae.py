@@ -110,7 +110,8 @@ class SequentialVAE:
 
     def loss_value(self, stats=None, reg_coeff=None):
         """``self.loss`` (sequential_vae.py:1166-1176) = mean over the batch of the per-image ELBO."""
-        st = (self.step_stats() if stats is None else stats).double().cpu().numpy()
+        st = self.step_stats() if stats is None else stats
+        st = st.double().cpu().numpy() if isinstance(st, torch.Tensor) else np.asarray(st, np.float64)
         reg = self._last_reg if reg_coeff is None else reg_coeff
         T = self.cfg.mc_steps
         tot = 0.0

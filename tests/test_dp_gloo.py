@@ -1,0 +1,80 @@
+"""Data-parallel path on CPU (gloo, world_size 2): per-shard BN semantics + one
+all-reduce of the flat gradient (SURVEY.md §8e parity rule):
+  N-rank loss  = mean over shards of the single-process loss of each shard
+  N-rank grad  = mean over shards of the per-shard gradients
+The per-shard compute is the CPU twin (the GPU engine is covered by test_engine_gpu);
+the exchange is the product's parallel.allreduce_hook."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import pkg_mod
+from oracle import spec, torch_twin
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _shard_grads(rank, world, gx, gt, eps_all):
+    cd = spec.make_config("tiny", batch=gx.shape[0] // world)
+    table, struct, params = spec.init_params(cd, seed=0)
+    par = pkg_mod("parallel")
+    x = par.shard(torch.from_numpy(gx), rank, world).numpy()
+    t = par.shard(torch.from_numpy(gt), rank, world).numpy()
+    eps = eps_all[:, rank * cd["batch"]:(rank + 1) * cd["batch"]]
+    tw = torch_twin.Twin(cd, struct, params, dtype=torch.float64)
+    o = tw.step(x, t, eps, 0.5)
+    names = [p["name"] for p in table]
+    flat = torch.from_numpy(np.concatenate([o["grads"][n].ravel() for n in names]))
+    return o["loss"], flat
+
+
+def _worker(rank, world, port, gx, gt, eps_all, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    par = pkg_mod("parallel")
+    loss, flat = _shard_grads(rank, world, gx, gt, eps_all)
+    hook = par.allreduce_hook(dist)
+    hook(flat)
+    mloss = par.mean_scalar(dist, loss, torch.device("cpu"))
+    np.save(os.path.join(out_dir, "g%d.npy" % rank), flat.numpy())
+    np.save(os.path.join(out_dir, "l%d.npy" % rank), np.array([mloss, loss]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_dp_allreduce_matches_shard_mean(tmp_path, world):
+    B = 4 * world
+    cd = spec.make_config("tiny", batch=B)
+    gx, gt, eps_all = spec.make_inputs(cd, batch=B)
+    mp.spawn(_worker, args=(world, _free_port(), gx, gt, eps_all, str(tmp_path)), nprocs=world, join=True)
+    ref = [_shard_grads(r, world, gx, gt, eps_all) for r in range(world)]
+    mean_g = sum(f for _, f in ref) / world
+    mean_l = sum(l for l, _ in ref) / world
+    for r in range(world):
+        g = np.load(tmp_path / ("g%d.npy" % r))
+        ml, own = np.load(tmp_path / ("l%d.npy" % r))
+        np.testing.assert_allclose(g, mean_g.numpy(), rtol=1e-12, atol=1e-15)
+        assert abs(ml - mean_l) <= 1e-12 * abs(mean_l)
+        assert abs(own - ref[r][0]) <= 1e-12 * abs(own)
+    # replicas identical after the exchange
+    np.testing.assert_array_equal(np.load(tmp_path / "g0.npy"), np.load(tmp_path / "g1.npy"))
+
+
+def test_shard_is_contiguous():
+    par = pkg_mod("parallel")
+    b = torch.arange(1024)
+    parts = [par.shard(b, r, 8) for r in range(8)]
+    assert all(len(p) == 128 for p in parts)
+    assert torch.equal(torch.cat(parts), b)
