@@ -68,7 +68,8 @@ enum svae_buffer {
   SVAE_BUF_Z = 3,        /* latent sample [B,Dz] */
   SVAE_BUF_STEP_STATS = 4, /* [T][2] = (mean_b recon_t, mean_b KL_t)   (:1163-1164) */
   SVAE_BUF_REC_IMG = 5,  /* [B] per-image recon of step t */
-  SVAE_BUF_KL_IMG = 6    /* [B] per-image KL of step t */
+  SVAE_BUF_KL_IMG = 6,   /* [B] per-image KL of step t */
+  SVAE_BUF_DZ = 7        /* [B,Dz] d loss / d z_t (after svae_backward) */
 };
 
 /* Parameter table (pure host; callable without a GPU).  Live (trainable, non-zero-grad)

@@ -101,7 +101,7 @@ def split_latent(tp, P, cfg, st, z):
     return ladder
 
 
-def generator_ladder(tp, P, cfg, st, xprev, z, enc_st):
+def generator_ladder(tp, P, cfg, st, xprev, z, enc_st, rec=None):
     """sequential_vae.py:1679-1739 with combine_noise('concat') (:1833-1834)."""
     L, F, S = cfg["levels"], cfg["filter_sizes"], cfg["image_sizes"]
     encodings = compute_encodings(tp, P, cfg, enc_st, xprev) if xprev is not None else None
@@ -111,6 +111,8 @@ def generator_ladder(tp, P, cfg, st, xprev, z, enc_st):
     else:
         cur = ladder[L - 1]
     cur = _fc_bn_lrelu(tp, P, cur, st["top"])
+    if rec is not None:
+        rec["top_act"] = cur
     cur = T.reshape(tp, cur, (-1, S[L], S[L], F[L]))
     for dl in st["levels"]:
         lvl = dl["level"]
@@ -118,6 +120,9 @@ def generator_ladder(tp, P, cfg, st, xprev, z, enc_st):
         deconv = _conv_bn_act(tp, P, cur, dl["s2"], 2, "relu", transpose=True, residual=res)
         deconv = T.concat_last(tp, [deconv, ladder[lvl]])
         cur = _conv_bn_act(tp, P, deconv, dl["s1"], 1, "relu", transpose=True)
+        if rec is not None:
+            rec["s1_act_%d" % lvl] = cur
+            rec["cat_%d" % lvl] = deconv
     lo, hi = cfg["range"]
     o = T.conv2d_transpose(tp, cur, P[st["out"]["w"]], 2)
     o = T.sigmoid(tp, T.bias_add(tp, o, P[st["out"]["b"]]))
@@ -143,13 +148,16 @@ def forward_backward(cfg, struct, params, x, target, eps, reg_coeff=1.0, want_gr
     Tn = cfg["mc_steps"]
     terms, coeffs = [], []
     out = dict(recon=[], kl=[], recon_img=[], kl_img=[], xhat=[], mu=[], sig=[], z=[])
+    znodes, xnodes, recs = [], [], []
     prev = None
     for t in range(Tn):
         st = struct[t]
         mu, sig = inference_ladder(tp, P, cfg, st["inference"], xin)
         e = tp.leaf(np.asarray(eps[t], np.float64))
         z = T.add(tp, mu, T.mul(tp, sig, e))                       # :1023
-        xhat = generator_ladder(tp, P, cfg, st["generator"], prev, z, st.get("encoder"))
+        recd = {}
+        xhat = generator_ladder(tp, P, cfg, st["generator"], prev, z, st.get("encoder"), recd)
+        recs.append(recd)
         rec = T.mean_sq_err_per_row(tp, xhat, target)              # :1146
         kl = T.kl_per_row(tp, mu, sig, cfg["latent_prior_stddev"])  # :1156-1158
         rec_m, kl_m = T.mean_all(tp, rec), T.mean_all(tp, kl)      # :1163-1164
@@ -167,6 +175,8 @@ def forward_backward(cfg, struct, params, x, target, eps, reg_coeff=1.0, want_gr
         out["mu"].append(mu.v.copy())
         out["sig"].append(sig.v.copy())
         out["z"].append(z.v.copy())
+        znodes.append(z)
+        xnodes.append(xhat)
         prev = xhat
     loss = T.scalar_sum(tp, terms, coeffs)
     out["loss"] = float(loss.v)
@@ -182,6 +192,9 @@ def forward_backward(cfg, struct, params, x, target, eps, reg_coeff=1.0, want_gr
     if want_grads:
         tp.backward(loss)
         out["grads"] = {k: (n.g if n.g is not None else np.zeros_like(n.v)) for k, n in P.items()}
+        out["dz"] = [n.g.copy() for n in znodes]          # d loss / d z_t
+        out["dxhat"] = [n.g.copy() for n in xnodes]       # d loss / d x_hat_t (total)
+        out["dec_grads"] = [{k: (n.g.copy() if n.g is not None else None) for k, n in r.items()} for r in recs]
     return out
 
 

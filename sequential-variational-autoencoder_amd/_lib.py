@@ -33,7 +33,7 @@ class SvaeParamDesc(ctypes.Structure):
                 ("offset", ctypes.c_int64), ("init", ctypes.c_int32), ("flags", ctypes.c_int32)]
 
 
-BUF_XHAT, BUF_MU, BUF_SIGMA, BUF_Z, BUF_STEP_STATS, BUF_REC_IMG, BUF_KL_IMG = range(7)
+BUF_XHAT, BUF_MU, BUF_SIGMA, BUF_Z, BUF_STEP_STATS, BUF_REC_IMG, BUF_KL_IMG, BUF_DZ = range(8)
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 
 _lib = None

@@ -9,29 +9,32 @@
 #include "common.h"
 #include "kernels.h"
 
-__global__ void bn_finalize_kernel(const float* part, long long part_gs, int nrb, int C, double count, float eps,
-                                   float* mean, float* invstd, long long ms_gs, int mode, float* dbeta,
-                                   long long dbeta_gs) {
+#define FIN_COLS 16
+#define FIN_PARTS 16
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* part, long long part_gs, int nrb, int C,
+                                                          double count, float eps, float* mean, float* invstd,
+                                                          long long ms_gs, int mode, float* dbeta,
+                                                          long long dbeta_gs) {
   // mode 0: stats -> mean/invstd ; mode 1: bwd sums -> ab (mean slots), dbeta
-  __shared__ double red[2][4][64];
+  __shared__ double red[2][FIN_PARTS][FIN_COLS];
   const int group = blockIdx.y;
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int part_i = threadIdx.x >> 6;
+  const int ci = threadIdx.x % FIN_COLS, pi = threadIdx.x / FIN_COLS;
+  const int c = blockIdx.x * FIN_COLS + ci;
   const float* P = part + group * part_gs;
   double s = 0.0, q = 0.0;
   if (c < C) {
-    for (int rb = part_i; rb < nrb; rb += 4) {
+    for (int rb = pi; rb < nrb; rb += FIN_PARTS) {
       s += (double)P[(long long)rb * 2 * C + c];
       q += (double)P[(long long)rb * 2 * C + C + c];
     }
   }
-  red[0][part_i][threadIdx.x & 63] = s;
-  red[1][part_i][threadIdx.x & 63] = q;
+  red[0][pi][ci] = s;
+  red[1][pi][ci] = q;
   __syncthreads();
-  if (part_i == 0 && c < C) {
-    for (int i = 1; i < 4; ++i) {
-      s += red[0][i][threadIdx.x];
-      q += red[1][i][threadIdx.x];
+  if (pi == 0 && c < C) {
+    for (int i = 1; i < FIN_PARTS; ++i) {
+      s += red[0][i][ci];
+      q += red[1][i][ci];
     }
     if (mode == 0) {
       double m = s / count;
@@ -49,13 +52,13 @@ __global__ void bn_finalize_kernel(const float* part, long long part_gs, int nrb
 
 void bn_finalize(const float* part, long long part_gs, int nrb, int C, long long count, float eps, float* mean,
                  float* invstd, long long ms_gs, int groups, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64, groups), dim3(256), 0, s, part, part_gs, nrb, C,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + FIN_COLS - 1) / FIN_COLS, groups), dim3(256), 0, s, part, part_gs, nrb, C,
                      (double)count, eps, mean, invstd, ms_gs, 0, (float*)nullptr, 0LL);
 }
 
 void bn_bwd_finalize(const float* part, long long part_gs, int nrb, int C, long long count, float* ab, long long ab_gs,
                      float* dbeta, long long dbeta_gs, int groups, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64, groups), dim3(256), 0, s, part, part_gs, nrb, C,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + FIN_COLS - 1) / FIN_COLS, groups), dim3(256), 0, s, part, part_gs, nrb, C,
                      (double)count, 0.f, ab, (float*)nullptr, ab_gs, 1, dbeta, dbeta_gs);
 }
 

@@ -237,21 +237,22 @@ struct Model {
       sg.convt_plain(F[1], g.C, G.wout, G.bout);
       if (t >= 1) sg.convt_plain(F[1], 1, G.wratio, G.bratio);
     }
-    // offsets: live phi blocks (uniform per-step stride), live theta blocks, frozen tail
+    // offsets: live phi blocks (uniform per-step stride), live theta blocks, frozen tail.
+    // Every tensor starts on a 64-float (256 B) boundary: the GEMM kernels stage weights
+    // with 16-byte vector loads, and rows of NHWC tiles stay line-aligned.
+    auto align = [](long long v) { return (v + 63) / 64 * 64; };
     long long o = 0;
     for (int r = 0; r < 3; ++r) {
       for (int t = 0; t < g.T; ++t) {
         long long start = o;
         for (auto& d : descs)
-          if (d.region == r && (r == R_FROZEN || d.step == t)) {
-            if (r == R_FROZEN && d.step != t) continue;
+          if (d.region == r && d.step == t) {
+            o = align(o);
             d.offset = o;
             o += d.size;
           }
-        if (r == R_PHI) {
-          long long sz = o - start;
-          if (t == 0) phi_stride = sz;
-        }
+        o = align(o);
+        if (r == R_PHI && t == 0) phi_stride = o - start;
       }
       if (r == R_THETA) n_live = o;
     }
@@ -331,7 +332,7 @@ struct svae_ctx {
   // ---------- backward scratch ----------
   float *dx[2], *da, *dcur, *dnext, *dpre, *dcat, *dtop, *denc_c, *denc_fc;
   float* denc[8];
-  float *sfc_dpre, *sfc_part, *dz, *dhead;
+  float *sfc_part, *dz, *dhead;
   float *idb, *ida, *idpre;  // inference bwd: [T] x max level slab
   float *part, *ab, *slab;
   long long part_cap, slab_cap, ab_cap;
@@ -340,6 +341,8 @@ struct svae_ctx {
   const float* eps_in = nullptr;
   const float* eps_used = nullptr;
   float* reg_host = nullptr;  // pinned [T] kl coefficients (read by a memcpy node at replay time)
+  int dbg_stop_step = -1, dbg_stop_lvl = -1, dbg_stop_lvl2 = -1;
+  float* dbg_last = nullptr;
   bool counting = false;
 
   float* alloc(long long n) {
@@ -748,6 +751,7 @@ static int engine_backward(svae_ctx* c) {
 
   HIPCHK(c, hipMemsetAsync(c->dz, 0, (size_t)T * B * g.Dz * sizeof(float), st));
   for (int t = T - 1; t >= 0; --t) {
+    if (t < c->dbg_stop_step) return 0;  // debug: stop after step dbg_stop_step
     svae_ctx::StepBufs& s = c->sb[t];
     const GenStep& G = M.gen[t];
     const float* xprev = t >= 1 ? c->sb[t - 1].xhat : nullptr;
@@ -797,6 +801,7 @@ static int engine_backward(svae_ctx* c) {
       r = bn_act_bwd(c, 1, rows, Fl, View{dcur, Fl, 0}, View{s.s1_act[lvl], Fl, 0}, s.s1_pre[lvl], 0, Fl, s.s1_bn[lvl],
                      0, l1.obeta, 0, ACT_RELU, c->dpre, 0, View{}, 0);
       if (r) return r;
+      if (t == c->dbg_stop_step && lvl == c->dbg_stop_lvl2) { c->dbg_last = dcur; return 0; }
       r = conv_wgrad(c, l1, 1, 0, View{s.cat[lvl], 2 * Fl, 0}, c->dpre, 0, c->Gr + l1.ow);
       if (r) return r;
       r = conv_dgrad(c, l1, 1, 0, c->dpre, 0, View{c->dcat, 2 * Fl, 0}, 0);
@@ -808,8 +813,8 @@ static int engine_backward(svae_ctx* c) {
         for (int i = 0; i < lvl; ++i) zoff += g.D[i];
         splitfc_bwd(c->z + (long long)t * B * g.Dz, g.Dz, zoff, B, g.D[lvl], c->P + f.ow, c->P + f.obeta, f.nout,
                     s.split_mean[lvl], s.split_inv[lvl], c->dcat + Fl, (long long)S[lvl + 1] * S[lvl + 1] * 2 * Fl, Fl,
-                    2 * Fl, c->Gr + f.ow, c->Gr + f.obeta, c->sfc_dpre, st);
-        splitfc_dz_gemm(c->sfc_dpre, B, f.nout, c->P + f.ow, g.D[lvl], c->sfc_part, dzt, g.Dz, zoff, st);
+                    2 * Fl, c->Gr + f.ow, c->Gr + f.obeta, c->sfc_part, st);
+        splitfc_dz_reduce(c->sfc_part, splitfc_blocks(f.nout), B, g.D[lvl], dzt, g.Dz, zoff, st);
       }
       // s2: relu(BN(convT_s2(cur)) + enc_{lvl+1})
       View dres = t >= 1 ? View{c->denc[lvl], Fl, 0} : View{};
@@ -822,6 +827,7 @@ static int engine_backward(svae_ctx* c) {
       r = conv_dgrad(c, l2, 1, 0, c->dpre, 0, View{dnext, in.ld, 0}, 0);
       if (r) return r;
       std::swap(dcur, dnext);
+      if (t == c->dbg_stop_step && lvl == c->dbg_stop_lvl) return 0;
     }
     // ---- top fc_bn_lrelu (:1704)
     const int ntop = S[L] * S[L] * F[L];
@@ -833,8 +839,8 @@ static int engine_backward(svae_ctx* c) {
       const int coff = t >= 1 ? F[L] : 0;
       splitfc_bwd(c->z + (long long)t * B * g.Dz, g.Dz, g.Dz - g.D[L - 1], B, g.D[L - 1], c->P + f.ow, c->P + f.obeta,
                   f.nout, s.split_mean[L - 1], s.split_inv[L - 1], c->dtop + coff, s.ktop, f.nout, 0, c->Gr + f.ow,
-                  c->Gr + f.obeta, c->sfc_dpre, st);
-      splitfc_dz_gemm(c->sfc_dpre, B, f.nout, c->P + f.ow, g.D[L - 1], c->sfc_part, dzt, g.Dz, g.Dz - g.D[L - 1], st);
+                  c->Gr + f.obeta, c->sfc_part, st);
+      splitfc_dz_reduce(c->sfc_part, splitfc_blocks(f.nout), B, g.D[L - 1], dzt, g.Dz, g.Dz - g.D[L - 1], st);
     }
     // ---- g_theta encoder of x_{t-1} (reverse of :1764-1775)
     if (t >= 1) {
@@ -1005,8 +1011,7 @@ static bool plan(svae_ctx* c) {
   c->dtop = A((long long)B * (F[L] + F[L + 1]));
   c->denc_c = A((long long)B * S[L] * S[L] * F[L - 1]);
   for (int lvl = 0; lvl < L - 1; ++lvl) c->denc[lvl] = A((long long)B * S[lvl + 1] * S[lvl + 1] * F[lvl + 1]);
-  c->sfc_dpre = A((long long)B * maxJ);
-  c->sfc_part = A((long long)heads_splits((int)maxJ) * B * maxK);
+  c->sfc_part = A((long long)splitfc_blocks((int)maxJ) * B * maxK);
   c->dz = A((long long)T * B * g.Dz);
   c->dhead = A((long long)T * B * 2 * g.Dz);
   c->idb = A((long long)T * max_inf);
@@ -1159,7 +1164,7 @@ int svae_adam(svae_ctx* c, float lr, int64_t step, float clip, void* stream) {
 int svae_copy_out(svae_ctx* c, int which, int step, float* dst, int64_t n, void* stream) {
   if (!c || !dst) return fail(c, SVAE_EBADARG, "null");
   const Geo& g = c->m.g;
-  if (step < 0 || step >= g.T) return fail(c, SVAE_EBADARG, "step out of range");
+  if (which < 100 && (step < 0 || step >= g.T)) return fail(c, SVAE_EBADARG, "step out of range");
   const float* src = nullptr;
   long long cnt = 0;
   const long long ml = (long long)g.B * g.Dz;
@@ -1171,6 +1176,20 @@ int svae_copy_out(svae_ctx* c, int which, int step, float* dst, int64_t n, void*
     case SVAE_BUF_STEP_STATS: src = c->sb[step].stats; cnt = 2; break;
     case SVAE_BUF_REC_IMG: src = c->sb[step].rec_img; cnt = g.B; break;
     case SVAE_BUF_KL_IMG: src = c->kl_img + (long long)step * g.B; cnt = g.B; break;
+    case SVAE_BUF_DZ: src = c->dz + step * ml; cnt = ml; break;
+    case 100: src = c->dx[step & 1]; cnt = (long long)g.B * g.H * g.W * g.C; break;  // debug: dx carry
+    case 101: c->dbg_stop_step = step; return 0;                                    // debug: stop step
+    case 102: c->dbg_stop_lvl = step; return 0;                                     // debug: stop level
+    case 103: src = c->dcur; cnt = n; break;                                        // debug: raw scratch
+    case 104: src = c->dnext; cnt = n; break;
+    case 105: src = c->sb[c->dbg_stop_step].s1_pre[step]; cnt = n; break;           // debug: saved tensors
+    case 109: src = c->dpre; cnt = n; break;
+    case 110: src = c->dbg_last; cnt = n; break;
+    case 111: c->dbg_stop_lvl2 = step; return 0;
+    case 112: src = c->ab; cnt = n; break;
+    case 106: src = c->sb[c->dbg_stop_step].s1_act[step]; cnt = n; break;
+    case 107: src = c->sb[c->dbg_stop_step].s1_bn[step].mean; cnt = n; break;
+    case 108: src = c->sb[c->dbg_stop_step].s1_bn[step].invstd; cnt = n; break;
     default: return fail(c, SVAE_EBADARG, "unknown buffer");
   }
   if (n < cnt) return fail(c, SVAE_EBADARG, "destination too small");

@@ -63,13 +63,13 @@ void bn_bwd_apply(const float* dy, int lddy, long long dy_gs, const float* y, in
 // out[n][j] written at out + n*o_n + (j / F)*ldo + (j % F)
 void splitfc_fwd(const float* z, int ldz, int zoff, int B, int K, const float* W, const float* beta, int J,
                  float* mean, float* invstd, float* out, long long o_n, int F, int ldo, hipStream_t s);
-// writes dpre [B][J] (scratch), dW [K][J], dbeta [J]
+// writes dW [K][J], dbeta [J] and dz_part [splitfc_blocks(J)][B][K]
 void splitfc_bwd(const float* z, int ldz, int zoff, int B, int K, const float* W, const float* beta, int J,
                  const float* mean, const float* invstd, const float* dout, long long o_n, int F, int ldo, float* dW,
-                 float* dbeta, float* dpre, hipStream_t s);
-// dz[n][zoff+d] += sum_j dpre[n][j] W[d][j]   (part: scratch [ceil(J/4096)][B][K])
-void splitfc_dz_gemm(const float* dpre, int B, int J, const float* W, int K, float* part, float* dz, int ldz, int zoff,
-                     hipStream_t s);
+                 float* dbeta, float* dz_part, hipStream_t s);
+// dz[n][zoff+d] += sum over blocks of dz_part
+void splitfc_dz_reduce(const float* dz_part, int nblk, int B, int K, float* dz, int ldz, int zoff, hipStream_t s);
+int splitfc_blocks(int J);
 
 // ---- recognition heads: [mean|std] = ladder @ [Wm|Ws] (sequential_vae.py:1592-1594,1607-1609) ----
 int heads_splits(int K);

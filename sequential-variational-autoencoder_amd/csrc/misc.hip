@@ -13,19 +13,25 @@ static int ew_blocks(long long work, int per = 256, int cap = 4096) {
 
 // ---------------------------------------------------------------------------
 // split_latent: ladder_i = lrelu(BN_batch(z_i @ W_i + b_i))   (sequential_vae.py:1801-1806)
-// one thread per output feature j, the whole batch column recomputed from z (K <= 32)
+// block = 64 output features x 4 row groups (wave w owns rows n = w mod 4); the batch
+// column of each feature is recomputed from z (K <= 32 FMAs) instead of stored.
 // ---------------------------------------------------------------------------
-__global__ void splitfc_fwd_kernel(const float* z, int ldz, int zoff, int B, int K, const float* W,
-                                   const float* beta, int J, float* mean, float* invstd, float* out, long long o_n,
-                                   int F, int ldo) {
+#define SFC_COLS 64
+#define SFC_RG 4
+
+__global__ __launch_bounds__(256) void splitfc_fwd_kernel(const float* z, int ldz, int zoff, int B, int K,
+                                                          const float* W, const float* beta, int J, float* mean,
+                                                          float* invstd, float* out, long long o_n, int F, int ldo) {
   extern __shared__ float zs[];  // [B][K]
+  __shared__ float red[SFC_RG][SFC_COLS];
   for (int i = threadIdx.x; i < B * K; i += blockDim.x) zs[i] = z[(i / K) * ldz + zoff + (i % K)];
   __syncthreads();
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= J) return;
+  const int c = threadIdx.x & (SFC_COLS - 1), rg = threadIdx.x / SFC_COLS;
+  const int j = blockIdx.x * SFC_COLS + c;
+  const bool ok = j < J;
   float w[KMAX];
 #pragma unroll
-  for (int d = 0; d < KMAX; ++d) w[d] = d < K ? W[(long long)d * J + j] : 0.f;
+  for (int d = 0; d < KMAX; ++d) w[d] = (ok && d < K) ? W[(long long)d * J + j] : 0.f;
   auto pre = [&](int n) {
     float s = 0.f;
 #pragma unroll
@@ -34,43 +40,56 @@ __global__ void splitfc_fwd_kernel(const float* z, int ldz, int zoff, int B, int
     return s;
   };
   float s = 0.f;
-  for (int n = 0; n < B; ++n) s += pre(n);
-  const float m = s / B;
+  for (int n = rg; n < B; n += SFC_RG) s += pre(n);
+  red[rg][c] = s;
+  __syncthreads();
+  const float m = (red[0][c] + red[1][c] + red[2][c] + red[3][c]) / B;
+  __syncthreads();
   float q = 0.f;
-  for (int n = 0; n < B; ++n) {
+  for (int n = rg; n < B; n += SFC_RG) {
     float d = pre(n) - m;
     q += d * d;
   }
-  const float is = 1.f / sqrtf(q / B + 1e-3f);
-  mean[j] = m;
-  invstd[j] = is;
+  red[rg][c] = q;
+  __syncthreads();
+  const float is = 1.f / sqrtf((red[0][c] + red[1][c] + red[2][c] + red[3][c]) / B + 1e-3f);
+  if (!ok) return;
+  if (rg == 0) {
+    mean[j] = m;
+    invstd[j] = is;
+  }
   const float b = beta[j];
   float* dst = out + (long long)(j / F) * ldo + (j % F);
-  for (int n = 0; n < B; ++n) dst[n * o_n] = lrelu_f((pre(n) - m) * is + b);
+  for (int n = rg; n < B; n += SFC_RG) dst[n * o_n] = lrelu_f((pre(n) - m) * is + b);
 }
 
 void splitfc_fwd(const float* z, int ldz, int zoff, int B, int K, const float* W, const float* beta, int J,
                  float* mean, float* invstd, float* out, long long o_n, int F, int ldo, hipStream_t s) {
-  hipLaunchKernelGGL(splitfc_fwd_kernel, dim3((J + 255) / 256), dim3(256), B * K * sizeof(float), s, z, ldz, zoff,
-                     B, K, W, beta, J, mean, invstd, out, o_n, F, ldo);
+  hipLaunchKernelGGL(splitfc_fwd_kernel, dim3((J + SFC_COLS - 1) / SFC_COLS), dim3(256), B * K * sizeof(float), s, z,
+                     ldz, zoff, B, K, W, beta, J, mean, invstd, out, o_n, F, ldo);
 }
 
-int splitfc_blocks(int J) { return (J + 255) / 256; }
+int splitfc_blocks(int J) { return (J + SFC_COLS - 1) / SFC_COLS; }
 
-// backward: dpre[n][j] -> scratch (dz_part), dW, dbeta.  dz is formed by skinny_gemm afterwards.
-__global__ void splitfc_bwd_kernel(const float* z, int ldz, int zoff, int B, int K, const float* W,
-                                   const float* beta, int J, const float* mean, const float* invstd,
-                                   const float* dout, long long o_n, int F, int ldo, float* dW, float* dbeta,
-                                   float* dpre) {
+// backward: dW [K][J], dbeta [J], and per-block partial dz: dz_part[blk][n][d] = sum_{j in blk} dpre[n][j] W[d][j]
+// (each wave owns whole rows and all 64 features of the block in its lanes -> one wave reduction per (n, d))
+__global__ __launch_bounds__(256) void splitfc_bwd_kernel(const float* z, int ldz, int zoff, int B, int K,
+                                                          const float* W, const float* beta, int J,
+                                                          const float* mean, const float* invstd, const float* dout,
+                                                          long long o_n, int F, int ldo, float* dW, float* dbeta,
+                                                          float* dz_part) {
   extern __shared__ float zs[];
+  __shared__ float red[2][SFC_RG][SFC_COLS];
+  __shared__ float gwr[SFC_RG][KMAX][SFC_COLS];
   for (int i = threadIdx.x; i < B * K; i += blockDim.x) zs[i] = z[(i / K) * ldz + zoff + (i % K)];
   __syncthreads();
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= J) return;
+  const int c = threadIdx.x & (SFC_COLS - 1), rg = threadIdx.x / SFC_COLS;
+  const int j = blockIdx.x * SFC_COLS + c;
+  const bool ok = j < J;
   float w[KMAX];
 #pragma unroll
-  for (int d = 0; d < KMAX; ++d) w[d] = d < K ? W[(long long)d * J + j] : 0.f;
-  const float m = mean[j], is = invstd[j], b = beta[j];
+  for (int d = 0; d < KMAX; ++d) w[d] = (ok && d < K) ? W[(long long)d * J + j] : 0.f;
+  const float m = ok ? mean[j] : 0.f, is = ok ? invstd[j] : 0.f, b = ok ? beta[j] : 0.f;
   const float* src = dout + (long long)(j / F) * ldo + (j % F);
   auto xhat = [&](int n) {
     float s = 0.f;
@@ -80,36 +99,56 @@ __global__ void splitfc_bwd_kernel(const float* z, int ldz, int zoff, int B, int
     return (s - m) * is;
   };
   float sd = 0.f, sx = 0.f;
-  for (int n = 0; n < B; ++n) {
-    float xh = xhat(n);
-    float dz = src[n * o_n] * ((xh + b) > 0.f ? 1.f : 0.1f);
-    sd += dz;
-    sx += dz * xh;
-  }
-  const float a = sd / B, c = sx / B;
+  if (ok)
+    for (int n = rg; n < B; n += SFC_RG) {
+      float xh = xhat(n);
+      float dz = src[n * o_n] * ((xh + b) > 0.f ? 1.f : 0.1f);
+      sd += dz;
+      sx += dz * xh;
+    }
+  red[0][rg][c] = sd;
+  red[1][rg][c] = sx;
+  __syncthreads();
+  sd = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+  sx = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+  const float a = sd / B, cc = sx / B;
   float gw[KMAX];
 #pragma unroll
   for (int d = 0; d < KMAX; ++d) gw[d] = 0.f;
-  for (int n = 0; n < B; ++n) {
-    float xh = xhat(n);
-    float dz = src[n * o_n] * ((xh + b) > 0.f ? 1.f : 0.1f);
-    float dp = is * (dz - a - xh * c);
-    dpre[(long long)n * J + j] = dp;
+  float* P = dz_part + (long long)blockIdx.x * B * K;
+  for (int n = rg; n < B; n += SFC_RG) {
+    float dp = 0.f;
+    if (ok) {
+      float xh = xhat(n);
+      float dz = src[n * o_n] * ((xh + b) > 0.f ? 1.f : 0.1f);
+      dp = is * (dz - a - xh * cc);
+    }
 #pragma unroll
-    for (int d = 0; d < KMAX; ++d)
-      if (d < K) gw[d] = fmaf(zs[n * K + d], dp, gw[d]);
+    for (int d = 0; d < KMAX; ++d) {
+      if (d < K) {
+        gw[d] = fmaf(zs[n * K + d], dp, gw[d]);
+        float v = wave_sum(dp * w[d]);
+        if (c == 0) P[n * K + d] = v;
+      }
+    }
   }
 #pragma unroll
   for (int d = 0; d < KMAX; ++d)
-    if (d < K) dW[(long long)d * J + j] = gw[d];
-  dbeta[j] = sd;
+    if (d < K) gwr[rg][d][c] = gw[d];
+  __syncthreads();
+  if (ok && rg == 0) {
+#pragma unroll
+    for (int d = 0; d < KMAX; ++d)
+      if (d < K) dW[(long long)d * J + j] = gwr[0][d][c] + gwr[1][d][c] + gwr[2][d][c] + gwr[3][d][c];
+    dbeta[j] = sd;
+  }
 }
 
 void splitfc_bwd(const float* z, int ldz, int zoff, int B, int K, const float* W, const float* beta, int J,
                  const float* mean, const float* invstd, const float* dout, long long o_n, int F, int ldo, float* dW,
-                 float* dbeta, float* dpre, hipStream_t s) {
-  hipLaunchKernelGGL(splitfc_bwd_kernel, dim3((J + 255) / 256), dim3(256), B * K * sizeof(float), s, z, ldz, zoff,
-                     B, K, W, beta, J, mean, invstd, dout, o_n, F, ldo, dW, dbeta, dpre);
+                 float* dbeta, float* dz_part, hipStream_t s) {
+  hipLaunchKernelGGL(splitfc_bwd_kernel, dim3((J + SFC_COLS - 1) / SFC_COLS), dim3(256), B * K * sizeof(float), s, z,
+                     ldz, zoff, B, K, W, beta, J, mean, invstd, dout, o_n, F, ldo, dW, dbeta, dz_part);
 }
 
 // ---------------------------------------------------------------------------
@@ -198,11 +237,8 @@ __global__ void splitfc_dz_kernel(const float* part, int nsplit, int B, int K, f
   dz[n * ldz + zoff + d] += s;
 }
 
-void splitfc_dz_gemm(const float* dpre, int B, int J, const float* W, int K, float* part, float* dz, int ldz, int zoff,
-                     hipStream_t s) {
-  skinny(dpre, J, 0, B, J, W, 1, J, 0, K, part, 0, K, 0, 1, s);
-  const int nsplit = (J + SK_CHUNK - 1) / SK_CHUNK;
-  hipLaunchKernelGGL(splitfc_dz_kernel, dim3((B * K + 255) / 256), dim3(256), 0, s, part, nsplit, B, K, dz, ldz, zoff);
+void splitfc_dz_reduce(const float* dz_part, int nblk, int B, int K, float* dz, int ldz, int zoff, hipStream_t s) {
+  hipLaunchKernelGGL(splitfc_dz_kernel, dim3((B * K + 255) / 256), dim3(256), 0, s, dz_part, nblk, B, K, dz, ldz, zoff);
 }
 
 // ---------------------------------------------------------------------------

@@ -34,14 +34,14 @@ def test_layout_matches_oracle_table(built_lib, preset):
     otab, _ = spec.build_params(spec.make_config(preset))
     key = lambda p: (p["name"], tuple(p["shape"]), p["dead"], p["zero_grad"], p["init"])
     assert sorted(map(key, table)) == sorted(map(key, otab))
-    # offsets tile [0, n_total) exactly; live tensors first
+    # 64-float aligned, non-overlapping spans inside [0, n_total); live tensors first
     spans = sorted((p["offset"], p["offset"] + p["size"], p["dead"] or p["zero_grad"]) for p in table)
     pos = 0
     for a, b, frozen in spans:
-        assert a == pos
+        assert a % 64 == 0 and a >= pos
         assert (a >= n_live) == frozen
         pos = b
-    assert pos == n_total
+    assert pos <= n_total and n_total - pos < 64 and n_live % 64 == 0
     # recognition blocks: identical per-step layout at a constant stride (batched launches)
     off = {p["name"]: p["offset"] for p in table}
     t0 = [n for n in off if n.startswith("phi/inference_step_0/") and n in off and off[n] < n_live]

@@ -4,12 +4,17 @@ numpy float64), same seeded inputs / injected eps / identical weights.
 Tolerances (BASELINE.json north_star: 1e-4 relative fp32 on ELBO and decoder output):
   loss / per-step recon & KL : |d|/|ref| <= 1e-4                       (all geometries)
   x_hat_t (decoder output)   : ||d||2/||ref||2 <= 1e-4, max-abs <= 1e-3 (tiny / MNIST)
-  gradients                  : per tensor ||d||/||ref|| <= 1e-3         (tiny / MNIST)
-At the CelebA geometry the randomly initialised T=8 chain (~160 BatchNorm layers deep)
-amplifies fp32 rounding ~2.5x per step: the fp32 PyTorch-CPU restatement of the same
-graph itself deviates from float64 by 2e-3 (x_hat_7) and ~1e-2 (gradients, median)
-(DESIGN.md §6).  There x_hat_t and the gradients are checked against that fp32 floor,
-measured in the same test: err(HIP) <= max(floor, 4 * err(fp32 CPU twin)).
+  gradients (flip-robust, see below): all-parameter ||d||/||ref|| <= max(1e-3, 4*fp32 twin),
+     per-tensor median <= 1e-4 and 90th percentile <= max(1e-3, 4*fp32 twin)
+Two fp32 effects have no fp32 cure and are calibrated against the fp32 PyTorch-CPU
+restatement of the same graph, run in the same test:
+ * kink flips: every configuration has ReLU / lrelu pre-activations within 1e-6 of 0;
+   an fp32 evaluation can put one on the other side of the kink than float64, which
+   moves the upstream gradients of that step by a finite amount (the fp32 CPU twin
+   shows the identical 3e-3 shift on tiny B=8 T=3 as the GPU) -> no per-tensor max bound;
+ * chaos at the CelebA geometry: the randomly initialised T=8 chain (~160 BatchNorm
+   layers deep) amplifies rounding ~2.5x per step (fp32 twin vs float64: 2e-3 on
+   x_hat_7, ~1e-2 median on gradients): err(HIP) <= max(floor, 4 * err(fp32 twin)).
 """
 import math
 
@@ -40,6 +45,25 @@ def _rel(a, b):
     return float(np.linalg.norm(np.ravel(a) - np.ravel(b)) / max(np.linalg.norm(np.ravel(b)), 1e-30))
 
 
+def _grad_stats(g, ref):
+    names = [k for k, v in ref.items() if np.linalg.norm(v) > 1e-7]
+    cat = lambda d: np.concatenate([np.ravel(d[k]) for k in names])
+    per = np.array([_rel(g[k], ref[k]) for k in names])
+    return _rel(cat(g), cat(ref)), float(np.median(per)), float(np.percentile(per, 90))
+
+
+def _check_grads(g_hip, ref, g_twin, median_tol=1e-4):
+    gh, mh, ph = _grad_stats(g_hip, ref)
+    gt, mt, pt = _grad_stats(g_twin, ref)
+    msg = "hip(global %.2e median %.2e p90 %.2e) twin32(global %.2e median %.2e p90 %.2e)" % (gh, mh, ph, gt, mt, pt)
+    assert gh <= max(1e-3, 4 * gt), msg
+    assert mh <= max(median_tol, 4 * mt), msg
+    assert ph <= max(1e-3, 4 * pt), msg
+    for k, v in ref.items():  # zero-gradient tensors stay (numerically) zero
+        if np.linalg.norm(v) <= 1e-7:
+            assert np.abs(g_hip[k]).max() <= 1e-5, k
+
+
 @pytest.mark.parametrize("preset,batch,reg", [("tiny", 4, 0.37), ("mnist_1step", 4, 1.0), ("tiny", 7, 1e-3)])
 def test_fwd_bwd_matches_oracle(preset, batch, reg):
     net, cfg = _engine(preset, batch)
@@ -63,16 +87,9 @@ def test_fwd_bwd_matches_oracle(preset, batch, reg):
         np.testing.assert_allclose(net.latent(1, t).cpu().numpy(), o["mu"][t], rtol=1e-3, atol=1e-5)
     elbo = net.elbo_per_image().cpu().numpy()
     np.testing.assert_allclose(elbo, o["elbo_img"], rtol=1e-4)
-    g = net.grad_dict()
-    worst = (0.0, "")
-    for name, ref in o["grads"].items():
-        n = np.linalg.norm(ref)
-        if n <= 1e-7:
-            assert np.abs(g[name]).max() <= 1e-5 + 1e-3 * n, name
-            continue
-        r = _rel(g[name], ref)
-        worst = max(worst, (r, name))
-    assert worst[0] <= 1e-3, worst
+    _, struct = spec.build_params(cd)
+    p32 = torch_twin.Twin(cd, struct, net.param_dict(), dtype=torch.float32).step(x, tgt, eps, reg)
+    _check_grads(net.grad_dict(), o["grads"], p32["grads"])
 
 
 @pytest.mark.parametrize("steps,batch", [(3, 8), (8, 8)])
@@ -97,15 +114,7 @@ def test_celeba_geometry_fwd_bwd(steps, batch):
         e_hip = _rel(net.xhat(t).cpu().numpy(), o["xhat"][t])
         e_32 = _rel(p32["xhat"][t], o["xhat"][t])
         assert e_hip <= max(1e-4, 4 * e_32), (t, e_hip, e_32)
-    g = net.grad_dict()
-    names = [k for k, v in o["grads"].items() if np.linalg.norm(v) > 1e-7]
-    cat = lambda d: np.concatenate([np.ravel(d[k]) for k in names])
-    ref = cat(o["grads"])
-    e_hip, e_32 = _rel(cat(g), ref), _rel(cat(p32["grads"]), ref)
-    assert e_hip <= max(1e-3, 4 * e_32), (e_hip, e_32)
-    per_hip = np.median([_rel(g[k], o["grads"][k]) for k in names])
-    per_32 = np.median([_rel(p32["grads"][k], o["grads"][k]) for k in names])
-    assert per_hip <= max(1e-3, 4 * per_32), (per_hip, per_32)
+    _check_grads(net.grad_dict(), o["grads"], p32["grads"], median_tol=1e-3)
 
 
 def test_train_step_adam_matches_oracle():
@@ -124,12 +133,13 @@ def test_train_step_adam_matches_oracle():
         net.forward(x, tgt, eps[::-1].copy() if it == 2 else eps, reg)
         net.backward()
         torch.cuda.synchronize()
-        grads = {k: g.astype(np.float64) * 1.0 for k, g in net.grad_dict().items()}
-        grads = {k: g * (1e4 if "Conv2d_transpose_6/biases" in k and it == 1 else 1.0) for k, g in grads.items()}
-        if it == 1:  # force the clip path on one tensor
-            name = [k for k in grads if "Conv2d_transpose_6/biases" in k][0]
-            net.grads[net._by_name[name]["offset"]:net._by_name[name]["offset"] + grads[name].size] = \
-                torch.from_numpy(grads[name].astype(np.float32).ravel()).cuda()
+        grads = {k: g.astype(np.float32).astype(np.float64) for k, g in net.grad_dict().items()}
+        if it == 1:  # force the clip(+-10) path on one tensor
+            name = "theta/generative_step_1/Conv2d_transpose_6/biases"
+            big = (grads[name] * 1e4).astype(np.float32)
+            grads[name] = big.astype(np.float64)
+            off = net._by_name[name]["offset"]
+            net.grads[off:off + big.size] = torch.from_numpy(big.ravel()).cuda()
         net.apply_gradients(2e-4, it)
         params, m, v = model.adam_update(params, grads, m, v, it, lr=2e-4, clip=10.0)
         torch.cuda.synchronize()
