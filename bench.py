@@ -123,6 +123,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="celeba")
     ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -139,7 +140,10 @@ def main():
     SV = importlib.import_module(PKG + ".sequential_vae").SequentialVAE
     par = importlib.import_module(PKG + ".parallel")
     L = importlib.import_module(PKG + "._lib")
-    cfg = cfgmod.preset(args.config, **({"batch": args.batch} if args.batch else {}))
+    over = {"dtype": args.dtype}
+    if args.batch:
+        over["batch"] = args.batch
+    cfg = cfgmod.preset(args.config, **over)
     B = cfg.batch
     hook = par.allreduce_hook(dist) if world > 1 else None
     net = SV(cfg, seed=0, grad_hook=hook)
@@ -212,7 +216,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": args.dtype,
             "data": "synthetic U[-1,1] NHWC batch, target=input, eps on-device Philox; deterministic splitmix64 init",
             "config": {"workload": "CelebA 64x64 default seq-VAE (c_inhomog), T=8 chain, fwd+bwd+clip+Adam",
                        "model": args.config, "global_batch": B * world, "per_gpu_batch": B,

@@ -33,6 +33,37 @@ def conv2d_t_same(x, w_tf, s):
     return full[:, :, pb:pb + Ho, pb:pb + Ho]
 
 
+def _bf(t):
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+class _RoundedOp(torch.autograd.Function):
+    """y = op(x, w) whose GEMM operands are rounded to bf16 exactly where the engine's
+    dtype='bf16' path rounds them (fp32 accumulation everywhere):
+      fwd   : round(x), round(w)       (gather-GEMM staging)
+      dgrad : round(dy), round(w)      (gather-GEMM staging)
+      wgrad : round(x), round(dy)      (weight-GEMM staging)
+    each leg individually switchable (output conv-T / layer-0 dgrad run in fp32)."""
+
+    @staticmethod
+    def forward(ctx, x, w, fn, rf, rd, rw):
+        ctx.fn, ctx.rd, ctx.rw = fn, rd, rw
+        ctx.save_for_backward(x, w)
+        return fn(_bf(x) if rf else x, _bf(w) if rf else w)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        with torch.enable_grad():
+            xa = (_bf(x) if ctx.rd else x).detach().requires_grad_(True)
+            wa = (_bf(w) if ctx.rd else w).detach().requires_grad_(True)
+            gx, = torch.autograd.grad(ctx.fn(xa, wa), xa, _bf(gy) if ctx.rd else gy)
+            xw = (_bf(x) if ctx.rw else x).detach().requires_grad_(True)
+            ww = (_bf(w) if ctx.rw else w).detach().requires_grad_(True)
+            gw, = torch.autograd.grad(ctx.fn(xw, ww), ww, _bf(gy) if ctx.rw else gy)
+        return gx, gw, None, None, None, None
+
+
 def bn_train(x, beta, eps=1e-3):
     dims = [0, 2, 3] if x.dim() == 4 else [0]
     m = x.mean(dim=dims, keepdim=True)
@@ -54,14 +85,25 @@ def nhwc_unflatten(x, S, C):
 
 
 class Twin:
-    def __init__(self, cfg, struct, params, dtype=torch.float32, requires_grad=True):
+    def __init__(self, cfg, struct, params, dtype=torch.float32, requires_grad=True, emulate_bf16=False):
         self.cfg, self.struct = cfg, struct
         self.P = {k: torch.tensor(v, dtype=dtype, requires_grad=requires_grad) for k, v in params.items()}
         self.dtype = dtype
+        self.bf16 = emulate_bf16
+
+    def _op(self, fn, x, w, rf=True, rd=True, rw=True):
+        if not self.bf16:
+            return fn(x, w)
+        return _RoundedOp.apply(x, w, fn, rf, rd, rw)
+
+    def _conv(self, x, w, s, transpose):
+        fn = (lambda a, b: conv2d_t_same(a, b, s)) if transpose else (lambda a, b: conv2d_same(a, b, s))
+        # layer-0 input gradient (C <= 3 channels) runs on the fp32 small-N kernel
+        return self._op(fn, x, w, rd=not (not transpose and x.shape[1] <= 3))
 
     def _cba(self, x, lay, s, act, transpose=False, residual=None):
         P = self.P
-        y = (conv2d_t_same if transpose else conv2d_same)(x, P[lay["w"]], s)
+        y = self._conv(x, P[lay["w"]], s, transpose)
         y = y + P[lay["b"]].view(1, -1, 1, 1)
         y = bn_train(y, P[lay["beta"]])
         if residual is not None:
@@ -72,9 +114,10 @@ class Twin:
             y = torch.relu(y)
         return y
 
-    def _fcbn(self, x, lay):
+    def _fcbn(self, x, lay, gemm=True):
         P = self.P
-        return lrelu(bn_train(x @ P[lay["w"]] + P[lay["b"]], P[lay["beta"]]))
+        mm = self._op(lambda a, b: a @ b, x, P[lay["w"]]) if gemm else x @ P[lay["w"]]
+        return lrelu(bn_train(mm + P[lay["b"]], P[lay["beta"]]))
 
     def _fc(self, x, lay):
         return x @ self.P[lay["w"]] + self.P[lay["b"]]
@@ -108,8 +151,9 @@ class Twin:
         L, F, S = cfg["levels"], cfg["filter_sizes"], cfg["image_sizes"]
         encs = self.encodings(enc_st, xprev) if xprev is not None else None
         parts = torch.split(z, cfg["latent_dims"], dim=1)
-        lad = [nhwc_unflatten(self._fcbn(parts[i], st["split"][i]), S[i + 1], F[i + 1]) for i in range(L - 1)]
-        lad.append(self._fcbn(parts[L - 1], st["split"][L - 1]))
+        lad = [nhwc_unflatten(self._fcbn(parts[i], st["split"][i], gemm=False), S[i + 1], F[i + 1])
+               for i in range(L - 1)]
+        lad.append(self._fcbn(parts[L - 1], st["split"][L - 1], gemm=False))
         cur = torch.cat([encs[L], lad[L - 1]], 1) if encs is not None else lad[L - 1]
         cur = nhwc_unflatten(self._fcbn(cur, st["top"]), S[L], F[L])
         for dl in st["levels"]:
@@ -119,10 +163,13 @@ class Twin:
             cur = self._cba(torch.cat([d, lad[lvl]], 1), dl["s1"], 1, "relu", transpose=True)
         lo, hi = cfg["range"]
         P = self.P
-        o = torch.sigmoid(conv2d_t_same(cur, P[st["out"]["w"]], 2) + P[st["out"]["b"]].view(1, -1, 1, 1))
+        oc = lambda a, b: conv2d_t_same(a, b, 2)
+        # output / ratio conv-T: fp32 small-N forward and input gradient, bf16 weight gradient
+        o = torch.sigmoid(self._op(oc, cur, P[st["out"]["w"]], rf=False, rd=False) + P[st["out"]["b"]].view(1, -1, 1, 1))
         out = (hi - lo) * o + lo
         if encs is not None:
-            r = torch.sigmoid(conv2d_t_same(cur, P[st["ratio"]["w"]], 2) + P[st["ratio"]["b"]].view(1, -1, 1, 1))
+            r = torch.sigmoid(self._op(oc, cur, P[st["ratio"]["w"]], rf=False, rd=False) +
+                              P[st["ratio"]["b"]].view(1, -1, 1, 1))
             r = cfg["min_highway"] + (cfg["max_highway"] - cfg["min_highway"]) * r.expand(-1, cfg["C"], -1, -1)
             out = r * out + (1 - r) * encs[0]
         return out

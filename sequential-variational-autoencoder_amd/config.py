@@ -34,7 +34,7 @@ class SVAEConfig:
     learning_rate_decay: float = 1.0                  # :252
     reg_coeff_rate: float = 5000.0                    # :254
     clip_grad_value: float = 10.0                     # :259
-    dtype: str = "fp32"
+    dtype: str = "fp32"                               # "fp32" (parity) | "bf16" (bf16 MFMA, fp32 accumulate)
 
     @property
     def latent_dim(self):
@@ -58,7 +58,7 @@ class SVAEConfig:
         c.latent_mean_clip = self.latent_mean_clip
         c.range_lo, c.range_hi = self.range
         c.min_highway, c.max_highway = self.min_highway, self.max_highway
-        c.dtype = {"fp32": 0}[self.dtype]
+        c.dtype = {"fp32": 0, "bf16": 1}[self.dtype]
         return c
 
     def as_dict(self):

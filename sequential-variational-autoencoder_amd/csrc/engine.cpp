@@ -71,6 +71,7 @@ struct Geo {
   int Dz;
   bool interm;
   float c_first, prior, clipv, lo, hi, minh, maxh;
+  bool bf16;
 };
 
 bool make_geo(const svae_config* c, Geo& g, std::string& err) {
@@ -106,7 +107,8 @@ bool make_geo(const svae_config* c, Geo& g, std::string& err) {
   g.clipv = c->latent_mean_clip;
   g.lo = c->range_lo; g.hi = c->range_hi;
   g.minh = c->min_highway; g.maxh = c->max_highway;
-  if (c->dtype != 0) { err = "only dtype 0 (fp32) is implemented"; return false; }
+  if (c->dtype != 0 && c->dtype != 1) { err = "dtype must be 0 (fp32) or 1 (bf16 MFMA)"; return false; }
+  g.bf16 = c->dtype == 1;
   return true;
 }
 
@@ -335,6 +337,9 @@ struct svae_ctx {
   float *sfc_part, *dz, *dhead;
   float *idb, *ida, *idpre;  // inference bwd: [T] x max level slab
   float *part, *ab, *slab;
+  void *wN = nullptr, *wT = nullptr;   // bf16 weight shadows (dtype=1)
+  void *tiles_d = nullptr, *offs_d = nullptr;
+  int ntiles = 0;
   long long part_cap, slab_cap, ab_cap;
   const float* x_in = nullptr;
   const float* tgt_in = nullptr;
@@ -416,6 +421,19 @@ int nrb_of(const FwdArgs& a) {
 
 }  // namespace
 
+// bf16 shadow views of a weight tensor: N = TF layout, T = per-tap transpose
+static const void* shadowN(svae_ctx* c, long long off) { return (const void*)((const __bf16*)c->wN + off); }
+static const void* shadowT(svae_ctx* c, long long off) { return (const void*)((const __bf16*)c->wT + off); }
+
+static void gemm(svae_ctx* c, FwdArgs a, int groups) {
+  if (c->m.g.bf16 && a.Bh) igemm_bf16(a, groups, c->st);
+  else igemm_fwd(a, groups, c->st);
+}
+static void wgemm(svae_ctx* c, const WgArgs& w, int groups) {
+  if (c->m.g.bf16) wgrad_bf16(w, groups, c->st);
+  else wgrad(w, groups, c->st);
+}
+
 // Forward conv/convT + BN + act.  in: [B,hin,hin,cin] (ld), out view gets act(BN(pre)+res)
 static int conv_bn_act_fwd(svae_ctx* c, const ConvL& L, int groups, long long w_gs, View in, float* pre,
                            long long pre_gs, BNS bn, long long bn_gs, View res, int act, View out) {
@@ -427,11 +445,15 @@ static int conv_bn_act_fwd(svae_ctx* c, const ConvL& L, int groups, long long w_
   a.C = pre;
   a.c_gs = pre_gs;
   a.ldc = L.cout;
+  if (c->m.g.bf16) {  // NK bf16: conv -> T copy [tap][co][ci], conv-T -> N copy [tap][co][ci]
+    a.Bh = L.tr ? shadowN(c, L.ow) : shadowT(c, L.ow);
+    a.ldb = L.cin;
+  }
   const int nrb = nrb_of(a);
   if ((long long)groups * nrb * 2 * L.cout > c->part_cap) return fail(c, SVAE_EBADARG, "stats scratch too small");
   a.stats = c->part;
   a.s_gs = (long long)nrb * 2 * L.cout;
-  igemm_fwd(a, groups, c->st);
+  gemm(c, a, groups);
   const long long rows = (long long)B * L.hout * L.hout;
   bn_finalize(c->part, a.s_gs, nrb, L.cout, rows, 1e-3f, bn.mean, bn.invstd, bn_gs, groups, c->st);
   bn_apply(pre, L.cout, pre_gs, rows, L.cout, bn.mean, bn.invstd, bn_gs, c->P + L.obeta, w_gs, res.p, res.ld, res.gs,
@@ -486,7 +508,7 @@ static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, V
   w.part = c->slab;
   w.p_gs = (long long)w.nsplit * 16 * w.M * w.N;
   if (w.p_gs * groups > c->slab_cap) return fail(c, SVAE_EBADARG, "wgrad slab too small");
-  wgrad(w, groups, c->st);
+  wgemm(c, w, groups);
   wgrad_reduce(c->slab, w.p_gs, w.nsplit, 16, w.M, w.N, dW, w_gs, w.M, nullptr, 0, 0, groups, c->st);
   return 0;
 }
@@ -525,7 +547,11 @@ static int conv_dgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, c
     a.rows = B * L.hin * L.hin;
     a.nclass = 1;
   }
-  igemm_fwd(a, groups, c->st);
+  if (c->m.g.bf16 && c->wN) {  // NK bf16 [tap][ci][co]: conv -> N copy, conv-T -> T copy
+    a.Bh = L.tr ? shadowT(c, L.ow) : shadowN(c, L.ow);
+    a.ldb = L.cout;
+  }
+  gemm(c, a, groups);
   return 0;
 }
 
@@ -555,10 +581,14 @@ static int fc_bn_fwd(svae_ctx* c, const FcL& f, View in, float* pre, BNS bn, Vie
   a.N = f.nout; a.Cin = f.nin;
   a.g.mode = GM_DENSE; a.g.nimg = B; a.g.ksz = 1; a.g.stride = 1;
   a.rows = B; a.nclass = 1;
+  if (c->m.g.bf16) {
+    a.Bh = shadowT(c, f.ow);  // [out][in]
+    a.ldb = f.nin;
+  }
   const int nrb = nrb_of(a);
   if ((long long)nrb * 2 * f.nout > c->part_cap) return fail(c, SVAE_EBADARG, "stats scratch too small");
   a.stats = c->part;
-  igemm_fwd(a, 1, c->st);
+  gemm(c, a, 1);
   bn_finalize(c->part, 0, nrb, f.nout, B, 1e-3f, bn.mean, bn.invstd, 0, 1, c->st);
   bn_apply(pre, f.nout, 0, B, f.nout, bn.mean, bn.invstd, 0, c->P + f.obeta, 0, nullptr, 0, 0, ACT_LRELU, out.p, out.ld,
            0, 1, c->st);
@@ -581,7 +611,7 @@ static int fc_bn_bwd(svae_ctx* c, const FcL& f, View in, View dy, View y, const 
   w.chunk = (B + 31) / 32 * 32;
   w.part = c->slab;
   if ((long long)f.nin * f.nout > c->slab_cap) return fail(c, SVAE_EBADARG, "wgrad slab too small");
-  wgrad(w, 1, c->st);
+  wgemm(c, w, 1);
   wgrad_reduce(c->slab, 0, 1, 1, f.nin, f.nout, c->Gr + f.ow, 0, f.nin, nullptr, 0, 0, 1, c->st);
   if (din.p) {
     FwdArgs a{};
@@ -591,7 +621,8 @@ static int fc_bn_bwd(svae_ctx* c, const FcL& f, View in, View dy, View y, const 
     a.N = f.nin; a.Cin = f.nout;
     a.g.mode = GM_DENSE; a.g.nimg = B; a.g.ksz = 1; a.g.stride = 1;
     a.rows = B; a.nclass = 1;
-    igemm_fwd(a, 1, c->st);
+    if (c->m.g.bf16) a.Bh = shadowN(c, f.ow);  // [in][out] as NK (n = in, k = out)
+    gemm(c, a, 1);
   }
   return 0;
 }
@@ -609,6 +640,7 @@ static int engine_forward(svae_ctx* c) {
   hipStream_t st = c->st;
   int r;
 
+  if (g.bf16) shadow_weights(c->P, c->wN, c->wT, M.n_live, c->tiles_d, c->ntiles, c->offs_d, st);
   // ---------------- recognition ladders, all steps batched (groups = T) ----------------
   HIPCHK(c, hipMemsetAsync(c->head_part, 0, (size_t)T * c->head_nsplit * B * 2 * g.Dz * sizeof(float), st));
   for (int lvl = 0; lvl < L - 1; ++lvl) {
@@ -775,7 +807,7 @@ static int engine_backward(svae_ctx* c) {
       w.rows = B * S[1] * S[1];
       choose_split(w.rows, 16, (F[1] + 127) / 128, 1, 16LL * M_out * F[1], c->slab_cap, w.nsplit, w.chunk);
       w.part = c->slab;
-      wgrad(w, 1, st);
+      wgemm(c, w, 1);
       wgrad_reduce(c->slab, 0, w.nsplit, 16, M_out, F[1], c->Gr + G.owout, 0, g.C,
                    t >= 1 ? c->Gr + G.owratio : nullptr, 0, 0, 1, st);
       colsum_small(c->da, C1, P0, M_out, c->part, c->Gr + G.obout, g.C, t >= 1 ? c->Gr + G.obratio : nullptr, st);
@@ -1099,6 +1131,49 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
   }
   c->adam_v = c->adam_m + nl;
   hipMemset(c->adam_m, 0, (size_t)nl * sizeof(float) * 2);
+  if (c->m.g.bf16) {
+    // bf16 shadows of the live region + the per-tap transpose tile table of every GEMM weight
+    e = hipMalloc(&c->wN, (size_t)nl * 2);
+    if (e == hipSuccess) e = hipMalloc(&c->wT, (size_t)nl * 2);
+    if (e != hipSuccess) {
+      svae_destroy(c);
+      return fail(nullptr, SVAE_ENOMEM, std::string("hipMalloc shadows: ") + hipGetErrorString(e));
+    }
+    hipMemset(c->wT, 0, (size_t)nl * 2);
+    std::vector<long long> offs;
+    std::vector<int> tiles;
+    auto add = [&](long long off, int taps, int R, int Cc) {
+      int id = (int)(offs.size() / 3);
+      offs.push_back(off); offs.push_back(R); offs.push_back(Cc);
+      for (int t = 0; t < taps; ++t)
+        for (int r = 0; r < R; r += 32)
+          for (int q = 0; q < Cc; q += 32) { tiles.push_back(id); tiles.push_back(t); tiles.push_back(r); tiles.push_back(q); }
+    };
+    auto conv = [&](const ConvL& L) {
+      if (L.w < 0) return;
+      if (L.tr) add(L.ow, 16, L.cout, L.cin);   // [tap][co][ci]
+      else add(L.ow, 16, L.cin, L.cout);        // [tap][ci][co]
+    };
+    const Geo& g = c->m.g;
+    for (int t = 0; t < g.T; ++t) {
+      for (int l = 0; l < g.L - 1; ++l) {
+        conv(c->m.inf[t].a[l]); conv(c->m.inf[t].b[l]);
+        conv(c->m.gen[t].s2[l]); conv(c->m.gen[t].s1[l]);
+        if (t >= 1) { conv(c->m.enc[t].a[l]); conv(c->m.enc[t].b[l]); }
+      }
+      if (t >= 1) { conv(c->m.enc[t].c); add(c->m.enc[t].fc.ow, 1, c->m.enc[t].fc.nin, c->m.enc[t].fc.nout); }
+      add(c->m.gen[t].top.ow, 1, c->m.gen[t].top.nin, c->m.gen[t].top.nout);
+    }
+    c->ntiles = (int)(tiles.size() / 4);
+    e = hipMalloc(&c->tiles_d, tiles.size() * sizeof(int));
+    if (e == hipSuccess) e = hipMalloc(&c->offs_d, offs.size() * sizeof(long long));
+    if (e != hipSuccess) {
+      svae_destroy(c);
+      return fail(nullptr, SVAE_ENOMEM, std::string("hipMalloc tiles: ") + hipGetErrorString(e));
+    }
+    hipMemcpy(c->tiles_d, tiles.data(), tiles.size() * sizeof(int), hipMemcpyHostToDevice);
+    hipMemcpy(c->offs_d, offs.data(), offs.size() * sizeof(long long), hipMemcpyHostToDevice);
+  }
   hipHostMalloc((void**)&c->reg_host, 64 * sizeof(float), hipHostMallocDefault);
   for (int i = 0; i < 64; ++i) c->reg_host[i] = 0.f;
   *out = c;
@@ -1110,6 +1185,10 @@ int svae_destroy(svae_ctx* c) {
   if (c->arena) hipFree(c->arena);
   if (c->adam_m) hipFree(c->adam_m);
   if (c->reg_host) hipHostFree(c->reg_host);
+  if (c->wN) hipFree(c->wN);
+  if (c->wT) hipFree(c->wT);
+  if (c->tiles_d) hipFree(c->tiles_d);
+  if (c->offs_d) hipFree(c->offs_d);
   delete c;
   return 0;
 }

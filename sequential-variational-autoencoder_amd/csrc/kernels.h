@@ -6,6 +6,7 @@
 struct FwdArgs {
   const float* A; long long a_gs; int lda;
   const float* B; long long b_gs; int ldb; long long b_tap; int b_nk;
+  const void* Bh;                         // bf16 NK weights (bf16 kernels only)
   float* C; long long c_gs; int ldc;
   float* stats; long long s_gs;           // per-column partial (sum,sum^2): [rowblock][2][N]
   const float* bias; long long bias_gs;
@@ -28,6 +29,12 @@ struct WgArgs {
 };
 
 int igemm_fwd_bm(const FwdArgs& a);
+// bf16-MFMA variants (dtype=1): A fp32 -> bf16 in staging, B = a.Bh bf16 [tap][n][k] (ldb = k pitch)
+void igemm_bf16(FwdArgs a, int groups, hipStream_t s);
+void wgrad_bf16(WgArgs a, int groups, hipStream_t s);
+// bf16 weight shadows: wn = bf16(w) for [0,n); wt = per-tap transposes listed in tiles/offs
+void shadow_weights(const float* w, void* wn, void* wt, long long n, const void* tiles, int ntiles, const void* offs,
+                    hipStream_t s);
 void igemm_fwd(FwdArgs a, int groups, hipStream_t s);
 void wgrad(WgArgs a, int groups, hipStream_t s);
 void wgrad_reduce(const float* part, long long p_gs, int nsplit, int ntap, int M, int N, float* out0,

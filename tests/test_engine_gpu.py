@@ -204,3 +204,35 @@ def test_full_size_properties():
     assert abs(e1 - l1) <= 1e-5 * abs(l1)
     assert torch.isfinite(net.grads).all()
     assert net.grads[net.n_live:].abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize("preset,batch,steps", [("tiny", 8, 3), ("celeba", 8, 3)])
+def test_bf16_mode_close_to_oracle(preset, batch, steps):
+    """dtype='bf16': conv/FC contractions on bf16 MFMA (operands rounded to 8 mantissa
+    bits, fp32 accumulation, fp32 BN/loss).  Reference for the bf16 deviation: the CPU
+    twin with exactly the same operands rounded to bf16 (torch_twin emulate_bf16).
+    Bounds: loss <= 2e-2 rel; x_hat_t and gradient (global, median) errors
+    vs float64 within 2x of the bf16-emulating twin's own error (+ a small floor)."""
+    net, cfg = _engine(preset, batch, mc_steps=steps, dtype="bf16")
+    cd = spec.make_config(preset, batch=batch, mc_steps=steps)
+    x, tgt, eps = spec.make_inputs(cd, batch=batch)
+    net.forward(x, tgt, eps, 1.0)
+    net.backward()
+    torch.cuda.synchronize()
+    o = _oracle_run(net, cd, x, tgt, eps, 1.0)
+    _, struct = spec.build_params(cd)
+    pe = torch_twin.Twin(cd, struct, net.param_dict(), dtype=torch.float32, emulate_bf16=True).step(x, tgt, eps, 1.0)
+    loss = net.loss_value(reg_coeff=1.0)
+    xe = [_rel(net.xhat(t).cpu().numpy(), o["xhat"][t]) for t in range(steps)]
+    xt = [_rel(pe["xhat"][t], o["xhat"][t]) for t in range(steps)]
+    gh, mh, ph = _grad_stats(net.grad_dict(), o["grads"])
+    gt, mt, pt = _grad_stats(pe["grads"], o["grads"])
+    msg = "loss rel %.2e (emul %.2e) xhat %s (emul %s) grads global %.2e/%.2e median %.2e/%.2e" % (
+        abs(loss - o["loss"]) / abs(o["loss"]), abs(pe["loss"] - o["loss"]) / abs(o["loss"]),
+        ["%.1e" % e for e in xe], ["%.1e" % e for e in xt], gh, gt, mh, mt)
+    print(msg)
+    assert abs(loss - o["loss"]) <= 2e-2 * abs(o["loss"]), msg
+    for e, et in zip(xe, xt):
+        assert e <= max(1e-3, 2 * et), msg
+    assert gh <= max(1e-2, 2 * gt), msg
+    assert mh <= max(1e-2, 2 * mt), msg
