@@ -17,12 +17,34 @@ enum SvaeAct { ACT_NONE = 0, ACT_RELU = 1, ACT_LRELU = 2, ACT_SIGMOID = 3 };
 //          stride 2 is split into 4 output-parity classes with 2x2 taps each.
 enum GatherMode { GM_DENSE = 0, GM_CONV = 1, GM_CONVT = 2 };
 
+// Division by a launch-constant d via multiply-shift (exact for 0 <= n < 2^31):
+// q = (n * m) >> s with s = 31 + ceil(log2 d), m = ceil(2^s / d).
+struct FastDiv {
+  unsigned long long m;
+  int s;
+  int d;
+};
+static inline FastDiv make_fastdiv(int d) {
+  FastDiv f;
+  if (d < 1) d = 1;  // dense (FC) launches carry no spatial dims
+  int l = 0;
+  while ((1LL << l) < d) ++l;
+  f.s = 31 + l;
+  f.m = (((unsigned long long)1 << f.s) + (unsigned long long)d - 1) / (unsigned long long)d;
+  f.d = d;
+  return f;
+}
+__device__ __forceinline__ int fdiv(int n, const FastDiv& f) {
+  return (int)(((unsigned long long)(unsigned)n * f.m) >> f.s);
+}
+
 struct ConvGeom {
   int mode;
   int nimg;
   int Hi, Wi;   // spatial dims of the gathered operand
   int Ho, Wo;   // spatial dims of the row space (output pixels)
   int stride, pad, ksz;
+  FastDiv dHW, dW;  // row-space divisors Ho*Wo and Wo (filled by the weight-GEMM launchers)
 };
 
 __device__ __forceinline__ float lrelu_f(float x) { return fmaxf(fminf(0.1f * x, 0.f), x); }

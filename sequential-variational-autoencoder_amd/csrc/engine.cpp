@@ -83,6 +83,7 @@ bool make_geo(const svae_config* c, Geo& g, std::string& err) {
   if (g.H != g.W) { err = "square images only (sequential_vae.py:1701)"; return false; }
   if (g.C < 1 || g.C > 3) { err = "channels must be 1..3"; return false; }
   if (g.B < 2) { err = "batch >= 2 required (training BatchNorm over the batch)"; return false; }
+  if (g.B > 256) { err = "batch <= 256 per context (split-latent backward keeps 64 rows per wave in registers)"; return false; }
   for (int i = 0; i < g.L + 2; ++i) {
     g.F[i] = c->filter_sizes[i];
     if (g.F[i] <= 0) { err = "filter_sizes must be positive"; return false; }
@@ -425,9 +426,24 @@ int nrb_of(const FwdArgs& a) {
 static const void* shadowN(svae_ctx* c, long long off) { return (const void*)((const __bf16*)c->wN + off); }
 static const void* shadowT(svae_ctx* c, long long off) { return (const void*)((const __bf16*)c->wT + off); }
 
-static void gemm(svae_ctx* c, FwdArgs a, int groups) {
-  if (c->m.g.bf16 && a.Bh) igemm_bf16(a, groups, c->st);
-  else igemm_fwd(a, groups, c->st);
+// launches the gather-GEMM; returns the number of BN-stat row blocks it wrote
+static int gemm(svae_ctx* c, FwdArgs a, int groups) {
+  if (c->m.g.bf16 && a.Bh) {
+    a.part = c->slab;
+    a.part_cap = c->slab_cap;
+    return igemm_bf16(a, groups, c->st);
+  }
+  a.ksplit = 1;
+  igemm_fwd(a, groups, c->st);
+  return nrb_of(a);
+}
+static int gemm_nrb(svae_ctx* c, FwdArgs a, int groups) {
+  if (c->m.g.bf16 && a.Bh) {
+    a.part = c->slab;
+    a.part_cap = c->slab_cap;
+    return igemm_bf16_plan(a, groups, nullptr);
+  }
+  return nrb_of(a);
 }
 static void wgemm(svae_ctx* c, const WgArgs& w, int groups) {
   if (c->m.g.bf16) wgrad_bf16(w, groups, c->st);
@@ -449,7 +465,7 @@ static int conv_bn_act_fwd(svae_ctx* c, const ConvL& L, int groups, long long w_
     a.Bh = L.tr ? shadowN(c, L.ow) : shadowT(c, L.ow);
     a.ldb = L.cin;
   }
-  const int nrb = nrb_of(a);
+  const int nrb = gemm_nrb(c, a, groups);
   if ((long long)groups * nrb * 2 * L.cout > c->part_cap) return fail(c, SVAE_EBADARG, "stats scratch too small");
   a.stats = c->part;
   a.s_gs = (long long)nrb * 2 * L.cout;
@@ -462,10 +478,10 @@ static int conv_bn_act_fwd(svae_ctx* c, const ConvL& L, int groups, long long w_
 }
 
 static void choose_split(long long rows, int taps, int tiles, int groups, long long per_split_elems, long long cap,
-                         int& nsplit, int& chunk) {
+                         int& nsplit, int& chunk, int target = 1024, long long min_rows = 512) {
   long long blocks = (long long)taps * tiles * groups;
-  long long want = (2048 + blocks - 1) / blocks;
-  long long maxs = std::max<long long>(1, rows / 256);
+  long long want = (target + blocks - 1) / blocks;
+  long long maxs = std::max<long long>(1, rows / min_rows);
   long long ns = std::min(want, maxs);
   long long capn = cap / std::max<long long>(1, per_split_elems * groups);
   ns = std::max<long long>(1, std::min(ns, capn));
@@ -503,8 +519,18 @@ static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, V
     w.g.Ho = w.g.Wo = L.hin;
     w.rows = B * L.hin * L.hin;
   }
-  int tiles = ((w.M + 63) / 64) * ((w.N + 63) / 64);
-  choose_split(w.rows, 16, tiles, groups, 16LL * w.M * w.N, c->slab_cap, w.nsplit, w.chunk);
+  if (c->m.g.bf16)  // tap-merged tiles; longer splits (less slab traffic)
+    choose_split(w.rows, 1, wgrad_bf16_tiles(w), groups, 16LL * w.M * w.N, c->slab_cap, w.nsplit, w.chunk, 768,
+                 1024);
+  else
+    choose_split(w.rows, 16, ((w.M + 63) / 64) * ((w.N + 63) / 64), groups, 16LL * w.M * w.N, c->slab_cap,
+                 w.nsplit, w.chunk);
+  if (w.nsplit == 1) {  // single split: the [tap][m][n] partial IS the TF weight layout
+    w.part = dW;
+    w.p_gs = w_gs;
+    wgemm(c, w, groups);
+    return 0;
+  }
   w.part = c->slab;
   w.p_gs = (long long)w.nsplit * 16 * w.M * w.N;
   if (w.p_gs * groups > c->slab_cap) return fail(c, SVAE_EBADARG, "wgrad slab too small");
@@ -585,9 +611,10 @@ static int fc_bn_fwd(svae_ctx* c, const FcL& f, View in, float* pre, BNS bn, Vie
     a.Bh = shadowT(c, f.ow);  // [out][in]
     a.ldb = f.nin;
   }
-  const int nrb = nrb_of(a);
+  const int nrb = gemm_nrb(c, a, 1);
   if ((long long)nrb * 2 * f.nout > c->part_cap) return fail(c, SVAE_EBADARG, "stats scratch too small");
   a.stats = c->part;
+  a.s_gs = (long long)nrb * 2 * f.nout;
   gemm(c, a, 1);
   bn_finalize(c->part, 0, nrb, f.nout, B, 1e-3f, bn.mean, bn.invstd, 0, 1, c->st);
   bn_apply(pre, f.nout, 0, B, f.nout, bn.mean, bn.invstd, 0, c->P + f.obeta, 0, nullptr, 0, 0, ACT_LRELU, out.p, out.ld,
@@ -609,10 +636,8 @@ static int fc_bn_bwd(svae_ctx* c, const FcL& f, View in, View dy, View y, const 
   w.rows = B;
   w.nsplit = 1;
   w.chunk = (B + 31) / 32 * 32;
-  w.part = c->slab;
-  if ((long long)f.nin * f.nout > c->slab_cap) return fail(c, SVAE_EBADARG, "wgrad slab too small");
+  w.part = c->Gr + f.ow;  // single split over the batch rows: write dW [nin][nout] directly
   wgemm(c, w, 1);
-  wgrad_reduce(c->slab, 0, 1, 1, f.nin, f.nout, c->Gr + f.ow, 0, f.nin, nullptr, 0, 0, 1, c->st);
   if (din.p) {
     FwdArgs a{};
     a.A = c->dpre; a.lda = f.nout;
@@ -805,7 +830,11 @@ static int engine_backward(svae_ctx* c) {
       w.g = ConvGeom{GM_CONV, B, g.H, g.W, S[1], S[1], 2, 1, 4};
       w.ntap = 16;
       w.rows = B * S[1] * S[1];
-      choose_split(w.rows, 16, (F[1] + 127) / 128, 1, 16LL * M_out * F[1], c->slab_cap, w.nsplit, w.chunk);
+      if (g.bf16)
+        choose_split(w.rows, 1, wgrad_bf16_tiles(w), 1, 16LL * M_out * F[1], c->slab_cap, w.nsplit, w.chunk, 768,
+                     1024);
+      else
+        choose_split(w.rows, 16, (F[1] + 127) / 128, 1, 16LL * M_out * F[1], c->slab_cap, w.nsplit, w.chunk);
       w.part = c->slab;
       wgemm(c, w, 1);
       wgrad_reduce(c->slab, 0, w.nsplit, 16, M_out, F[1], c->Gr + G.owout, 0, g.C,

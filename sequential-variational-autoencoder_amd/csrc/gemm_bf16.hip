@@ -112,13 +112,18 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
   const int lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, h = lane >> 5;
   const int wm0 = (wave / WN) * (TM * 32), wn0 = (wave % WN) * (TN * 32);
-  const int group = blockIdx.z / a.nclass, cls = blockIdx.z - group * a.nclass;
+  const int ks = a.ksplit;
+  const int split = blockIdx.z % ks;
+  const int zc = blockIdx.z / ks;
+  const int group = zc / a.nclass, cls = zc - group * a.nclass;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const float* A = a.A + group * a.a_gs;
   const __bf16* Bw = (const __bf16*)a.Bh + group * a.b_gs;
   const int ntap = ntaps_of_b(g);
   const int Ktot = ntap * a.Cin;
-  const int nk = SMALLC ? (Ktot + BKB - 1) / BKB : ntap * (a.Cin / BKB);
+  const int nk_all = SMALLC ? (Ktot + BKB - 1) / BKB : ntap * (a.Cin / BKB);
+  const int kbeg = (int)((long long)nk_all * split / ks), kend = (int)((long long)nk_all * (split + 1) / ks);
+  const int nk = kend - kbeg;
   const int k8 = (tid & 3) * 8;
 
   RowCoordB rc[RA];
@@ -211,19 +216,21 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  load_tile(0);
-  store_tile(0);
+  if (nk > 0) {
+    load_tile(kbeg);
+    store_tile(0);
+  }
   __syncthreads();
   for (int kc = 0; kc < nk; ++kc) {
     const int cur = kc & 1;
-    if (kc + 1 < nk) load_tile(kc + 1);
+    if (kc + 1 < nk) load_tile(kbeg + kc + 1);
 #pragma unroll
-    for (int ks = 0; ks < BKB / 16; ++ks) {
+    for (int kq = 0; kq < BKB / 16; ++kq) {
       bf16x8 af[TM], bfr[TN];
 #pragma unroll
-      for (int tm = 0; tm < TM; ++tm) af[tm] = *(const bf16x8*)&As[cur][(wm0 + tm * 32 + l32) * ROWP + ks * 16 + 8 * h];
+      for (int tm = 0; tm < TM; ++tm) af[tm] = *(const bf16x8*)&As[cur][(wm0 + tm * 32 + l32) * ROWP + kq * 16 + 8 * h];
 #pragma unroll
-      for (int tn = 0; tn < TN; ++tn) bfr[tn] = *(const bf16x8*)&Bs[cur][(wn0 + tn * 32 + l32) * ROWP + ks * 16 + 8 * h];
+      for (int tn = 0; tn < TN; ++tn) bfr[tn] = *(const bf16x8*)&Bs[cur][(wn0 + tn * 32 + l32) * ROWP + kq * 16 + 8 * h];
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -232,6 +239,24 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
     }
     if (kc + 1 < nk) store_tile(cur ^ 1);
     __syncthreads();
+  }
+
+  if (ks > 1) {  // raw partial tile -> slab[split][out_row][n]; bias/act/stats in splitk_reduce
+    float* P = a.part + (long long)group * ks * a.rows_total * a.N + (long long)split * a.rows_total * a.N;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm0 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m >= a.rows) continue;
+        const long long orow = out_row_b(g, cls, m);
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+          const int n = n0 + wn0 + tn * 32 + l32;
+          if (n < a.N) P[orow * a.N + n] = acc[tm][tn][r];
+        }
+      }
+    return;
   }
 
   // epilogue (identical contract to the fp32 kernel)
@@ -284,7 +309,7 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
         float s = 0.f, q = 0.f;
 #pragma unroll
         for (int w = 0; w < WM; ++w) { s += red[w * BN + tid]; q += red[WM * BN + w * BN + tid]; }
-        const long long rb_idx = (long long)cls * gridDim.x + blockIdx.x;
+        const long long rb_idx = (long long)cls * gridDim.x + blockIdx.x;  // ks == 1 here
         float* st = a.stats + group * a.s_gs + rb_idx * 2 * a.N;
         st[n] = s;
         st[a.N + n] = q;
@@ -294,13 +319,15 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// weight-GEMM, bf16 MFMA: part[split][tap][m][n] = sum_p G[src(p,tap)][m] * D[p][n]
+// weight-GEMM, bf16 MFMA, taps merged into M:  rows r = tap*M + m of
+//   part[split][r][n] = sum_{p in split} G[src(p, tap)][m] * D[p][n]
+// (small-channel layers fill all waves; one dY tile feeds every tap of the row tile)
 // ---------------------------------------------------------------------------
 template <int BM, int BN, int WM, int WN, bool VECG>
 __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
   constexpr int TM = BM / WM / 32;
   constexpr int TN = BN / WN / 32;
-  constexpr int QMc = BM / 4, QNc = BN / 4;   // channel quads
+  constexpr int QMc = BM / 4, QNc = BN / 4;                  // channel quads
   constexpr int UA = QMc * (BKB / 4), UB = QNc * (BKB / 4);  // 4x4 units per tile
   constexpr int RA = (UA + 255) / 256, RB = (UB + 255) / 256;
   __shared__ __attribute__((aligned(16))) __bf16 As[2][BM * ROWP];
@@ -311,40 +338,62 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
   const int lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, h = lane >> 5;
   const int wm0 = (wave / WN) * (TM * 32), wn0 = (wave % WN) * (TN * 32);
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  int z = blockIdx.z;
-  const int split = z % a.nsplit;
-  z /= a.nsplit;
-  const int tap = z % a.ntap;
-  const int group = z / a.ntap;
-  const int ky = tap / g.ksz, kx = tap - (tap / g.ksz) * g.ksz;
+  const int r0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int split = blockIdx.z % a.nsplit;
+  const int group = blockIdx.z / a.nsplit;
+  const int Mtot = a.ntap * a.M;
   const float* G = a.G + group * a.g_gs;
   const float* D = a.D + group * a.d_gs;
   const int p_begin = split * a.chunk;
   const int p_end = min(a.rows, p_begin + a.chunk);
   const int nk = (p_end - p_begin + BKB - 1) / BKB;
 
+  auto pix = [&](int p) {  // row-space pixel -> coordinates, division-free
+    RowCoordB rc;
+    rc.valid = p < a.rows;
+    if (g.mode == GM_DENSE) { rc.img = p; rc.y = rc.x = 0; return rc; }
+    const int n = fdiv(p, g.dHW);
+    const int r = p - n * g.dHW.d;
+    rc.y = fdiv(r, g.dW);
+    rc.x = r - rc.y * g.Wo;
+    rc.img = n * g.Hi * g.Wi;
+    return rc;
+  };
+  // per-unit (tap, channel) of the A rows this thread stages (fixed over the K loop)
+  int utap[RA], um[RA];
+#pragma unroll
+  for (int i = 0; i < RA; ++i) {
+    const int r = r0 + ((tid + 256 * i) % QMc) * 4;
+    utap[i] = r / a.M;
+    um[i] = r - utap[i] * a.M;
+  }
+
   f32x4 va[RA][4], vb[RB][4];
   auto load_tile = [&](int kc) {
 #pragma unroll
     for (int i = 0; i < RA; ++i) {
       const int u = tid + 256 * i;
-      const int mq = u % QMc, pq = u / QMc;
-      const int mc = m0 + mq * 4;
+      const int pq = u / QMc;
+      const int r = r0 + (u % QMc) * 4;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
         const int p = p_begin + kc * BKB + pq * 4 + j;
-        if (u < UA && p < p_end) {
-          RowCoordB rc = row_coord_b(g, 0, p, a.rows);
-          long long sp = src_pixel_b(g, rc, ky, kx);
-          if (sp >= 0) {
-            const float* s = G + sp * a.ldg + mc;
-            if (VECG) {
-              if (mc < a.M) v = *(const f32x4*)s;
-            } else {
+        if (u < UA && p < p_end && r < Mtot) {
+          RowCoordB rc = pix(p);
+          if (VECG) {
+            const int tap = utap[i];
+            long long sp = src_pixel_b(g, rc, tap / g.ksz, tap % g.ksz);
+            if (sp >= 0) v = *(const f32x4*)(G + sp * a.ldg + um[i]);
+          } else {
 #pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = (mc + e < a.M) ? s[e] : 0.f;
+            for (int e = 0; e < 4; ++e) {
+              const int re = r + e;
+              if (re < Mtot) {
+                const int tap = re / a.M, m = re - (re / a.M) * a.M;
+                long long sp = src_pixel_b(g, rc, tap / g.ksz, tap % g.ksz);
+                if (sp >= 0) v[e] = G[sp * a.ldg + m];
+              }
             }
           }
         }
@@ -422,13 +471,13 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
     if (kc + 1 < nk) store_tile(cur ^ 1);
     __syncthreads();
   }
-  float* P = a.part + group * a.p_gs + ((long long)split * a.ntap + tap) * (long long)a.M * a.N;
+  float* P = a.part + group * a.p_gs + (long long)split * Mtot * a.N;
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wm0 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (m >= a.M) continue;
+      const int m = r0 + wm0 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (m >= Mtot) continue;
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) {
         const int n = n0 + wn0 + tn * 32 + l32;
@@ -476,35 +525,125 @@ __global__ __launch_bounds__(256) void shadow_t_kernel(const float* w, __bf16* o
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
+// sum the K-split slabs; bias / act / accumulate into C; per-column (sum, sum^2) of the
+// raw sums per 256-row block -> stats[rb][2][N]  (same contract as the GEMM epilogue)
+#define SKR_ROWS 64
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* part, int ks, int rows_total, int N,
+                                                            float* C, long long c_gs, int ldc, const float* bias,
+                                                            long long bias_gs, int act, int accumulate, float* stats,
+                                                            long long s_gs) {
+  __shared__ f32x4 red[2][256];
+  const int group = blockIdx.z;
+  const int qi = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int n = (blockIdx.x * 16 + qi) * 4;
+  const long long slab = (long long)rows_total * N;
+  const float* P = part + (long long)group * ks * slab;
+  float* Cg = C + group * c_gs;
+  const float* bs = bias ? bias + group * bias_gs : nullptr;
+  f32x4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
+  if (n < N) {
+    const int r0 = blockIdx.y * SKR_ROWS;
+    const int r1 = min(rows_total, r0 + SKR_ROWS);
+    for (int r = r0 + rl; r < r1; r += 16) {
+      f32x4 v = *(const f32x4*)(P + (long long)r * N + n);
+#pragma unroll 4
+      for (int k = 1; k < ks; ++k) v += *(const f32x4*)(P + k * slab + (long long)r * N + n);
+      s1 += v;
+      s2 += v * v;
+      if (bs) v += *(const f32x4*)(bs + n);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = act_f(v[e], act);
+      f32x4* d = (f32x4*)(Cg + (long long)r * ldc + n);
+      *d = accumulate ? *d + v : v;
+    }
+  }
+  if (!stats) return;
+  red[0][threadIdx.x] = s1;
+  red[1][threadIdx.x] = s2;
+  __syncthreads();
+  if (rl == 0 && n < N) {
+    for (int j = 1; j < 16; ++j) {
+      s1 += red[0][j * 16 + qi];
+      s2 += red[1][j * 16 + qi];
+    }
+    float* st = stats + group * s_gs + (long long)blockIdx.y * 2 * N;
+    *(f32x4*)(st + n) = s1;
+    *(f32x4*)(st + N + n) = s2;
+  }
+}
+
 template <int BM, int BN, int WM, int WN>
 static void launch_bf16(const FwdArgs& a, int groups, bool sc, hipStream_t s) {
-  dim3 grid((a.rows + BM - 1) / BM, (a.N + BN - 1) / BN, groups * a.nclass);
+  dim3 grid((a.rows + BM - 1) / BM, (a.N + BN - 1) / BN, groups * a.nclass * a.ksplit);
   if (sc) hipLaunchKernelGGL((igemm_bf16_kernel<BM, BN, WM, WN, true>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((igemm_bf16_kernel<BM, BN, WM, WN, false>), grid, dim3(256), 0, s, a);
 }
 
-void igemm_bf16(FwdArgs a, int groups, hipStream_t s) {
+static int bf16_bm(const FwdArgs& a) {
+  if (a.N <= 32) return 256;
+  if (a.N <= 64) return 128;
+  return igemm_fwd_bm(a) == 128 ? 128 : 64;
+}
+static int bf16_bn(const FwdArgs& a) { return a.N <= 32 ? 32 : (a.N <= 64 ? 64 : 128); }
+
+int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit) {
+  const int bm = bf16_bm(a), bn = bf16_bn(a);
+  const long long blocks = (long long)((a.rows + bm - 1) / bm) * ((a.N + bn - 1) / bn) * a.nclass * groups;
+  const int ntap = a.g.mode == GM_DENSE ? 1 : (a.g.mode == GM_CONVT && a.g.stride == 2 ? 4 : 16);
+  const int Ktot = ntap * a.Cin;
+  const int nk = (a.Cin % BKB) ? (Ktot + BKB - 1) / BKB : ntap * (a.Cin / BKB);
+  int ks = 1;
+  if (blocks < 256 && a.part) {
+    ks = (int)std::min<long long>((384 + blocks - 1) / blocks, 4);
+    ks = std::min(ks, nk / 8);  // keep >= 8 K steps per split
+    const long long rows_total = (long long)a.rows * a.nclass;
+    while (ks > 1 && (long long)ks * rows_total * a.N * groups > a.part_cap) --ks;
+    if (ks < 2) ks = 1;
+  }
+  if (ksplit) *ksplit = ks;
+  if (ks == 1) return a.nclass * ((a.rows + bm - 1) / bm);
+  return (int)(((long long)a.rows * a.nclass + SKR_ROWS - 1) / SKR_ROWS);
+}
+
+int igemm_bf16(FwdArgs a, int groups, hipStream_t s) {
   const bool sc = (a.Cin % BKB) != 0;
-  const int bm = igemm_fwd_bm(a);
+  int ks = 1;
+  const int nrb = igemm_bf16_plan(a, groups, &ks);
+  a.ksplit = ks;
+  a.rows_total = a.rows * a.nclass;
+  const int bm = bf16_bm(a);
   if (a.N <= 32) launch_bf16<256, 32, 4, 1>(a, groups, sc, s);
   else if (a.N <= 64) launch_bf16<128, 64, 2, 2>(a, groups, sc, s);
   else if (bm == 128) launch_bf16<128, 128, 2, 2>(a, groups, sc, s);
   else launch_bf16<64, 128, 1, 4>(a, groups, sc, s);
+  if (ks > 1) {
+    dim3 grid((a.N + 63) / 64, nrb, groups);
+    hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, s, a.part, ks, a.rows_total, a.N, a.C, a.c_gs, a.ldc,
+                       a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs);
+  }
+  return nrb;
 }
 
 template <int BM, int BN, int WM, int WN>
 static void launch_wg_bf16(const WgArgs& a, int groups, bool vec, hipStream_t s) {
-  dim3 grid((a.M + BM - 1) / BM, (a.N + BN - 1) / BN, groups * a.ntap * a.nsplit);
+  dim3 grid((a.ntap * a.M + BM - 1) / BM, (a.N + BN - 1) / BN, groups * a.nsplit);
   if (vec) hipLaunchKernelGGL((wgrad_bf16_kernel<BM, BN, WM, WN, true>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((wgrad_bf16_kernel<BM, BN, WM, WN, false>), grid, dim3(256), 0, s, a);
 }
 
+// tiles of the tap-merged weight-GEMM (for the split heuristic)
+int wgrad_bf16_tiles(const WgArgs& a) {
+  const int bn = a.N <= 32 ? 32 : (a.N <= 64 ? 64 : 128);
+  return ((a.ntap * a.M + 127) / 128) * ((a.N + bn - 1) / bn);
+}
+
 void wgrad_bf16(WgArgs a, int groups, hipStream_t s) {
   const bool vec = (a.M % 4 == 0) && (a.ldg % 4 == 0);
-  if (a.M <= 32) launch_wg_bf16<32, 128, 1, 4>(a, groups, vec, s);
-  else if (a.N <= 32) launch_wg_bf16<128, 32, 4, 1>(a, groups, vec, s);
-  else if (a.M >= 128 && a.N >= 128) launch_wg_bf16<128, 128, 2, 2>(a, groups, vec, s);
-  else launch_wg_bf16<64, 64, 2, 2>(a, groups, vec, s);
+  a.g.dHW = make_fastdiv(a.g.Ho * a.g.Wo);
+  a.g.dW = make_fastdiv(a.g.Wo);
+  if (a.N <= 32) launch_wg_bf16<128, 32, 4, 1>(a, groups, vec, s);
+  else if (a.N <= 64) launch_wg_bf16<128, 64, 2, 2>(a, groups, vec, s);
+  else launch_wg_bf16<128, 128, 2, 2>(a, groups, vec, s);
 }
 
 void shadow_weights(const float* w, void* wn, void* wt, long long n, const void* tiles, int ntiles, const void* offs,

@@ -16,6 +16,8 @@ struct FwdArgs {
   int rows;     // rows (output pixels) per parity class
   int nclass;   // 4 for stride-2 conv-transpose, else 1
   int mtiles;   // filled by the launcher
+  // split-K (bf16 path): fp32 partial slabs [ksplit][rows_total][N] + reduce/stats pass
+  float* part; long long part_cap; int ksplit; int rows_total;
 };
 
 // weight-GEMM  part[split][tap][m][n] = sum_{p in split} G[src(p,tap)][m] * D[p][n]
@@ -30,8 +32,11 @@ struct WgArgs {
 
 int igemm_fwd_bm(const FwdArgs& a);
 // bf16-MFMA variants (dtype=1): A fp32 -> bf16 in staging, B = a.Bh bf16 [tap][n][k] (ldb = k pitch)
-void igemm_bf16(FwdArgs a, int groups, hipStream_t s);
-void wgrad_bf16(WgArgs a, int groups, hipStream_t s);
+// returns the number of stats row-blocks written to a.stats (plan: same value without launching)
+int igemm_bf16(FwdArgs a, int groups, hipStream_t s);
+int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit);
+void wgrad_bf16(WgArgs a, int groups, hipStream_t s);  // taps merged into M (part [split][tap*M+m][n])
+int wgrad_bf16_tiles(const WgArgs& a);
 // bf16 weight shadows: wn = bf16(w) for [0,n); wt = per-tap transposes listed in tiles/offs
 void shadow_weights(const float* w, void* wn, void* wt, long long n, const void* tiles, int ntiles, const void* offs,
                     hipStream_t s);

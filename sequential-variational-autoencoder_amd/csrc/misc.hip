@@ -19,24 +19,27 @@ static int ew_blocks(long long work, int per = 256, int cap = 4096) {
 #define SFC_COLS 64
 #define SFC_RG 4
 
+template <int KM>
 __global__ __launch_bounds__(256) void splitfc_fwd_kernel(const float* z, int ldz, int zoff, int B, int K,
                                                           const float* W, const float* beta, int J, float* mean,
                                                           float* invstd, float* out, long long o_n, int F, int ldo) {
-  extern __shared__ float zs[];  // [B][K]
+  extern __shared__ float zs[];  // [B][KM], zero padded past K
   __shared__ float red[SFC_RG][SFC_COLS];
-  for (int i = threadIdx.x; i < B * K; i += blockDim.x) zs[i] = z[(i / K) * ldz + zoff + (i % K)];
+  for (int i = threadIdx.x; i < B * KM; i += blockDim.x) {
+    const int d = i % KM;
+    zs[i] = d < K ? z[(i / KM) * ldz + zoff + d] : 0.f;
+  }
   __syncthreads();
   const int c = threadIdx.x & (SFC_COLS - 1), rg = threadIdx.x / SFC_COLS;
   const int j = blockIdx.x * SFC_COLS + c;
   const bool ok = j < J;
-  float w[KMAX];
+  float w[KM];
 #pragma unroll
-  for (int d = 0; d < KMAX; ++d) w[d] = (ok && d < K) ? W[(long long)d * J + j] : 0.f;
+  for (int d = 0; d < KM; ++d) w[d] = (ok && d < K) ? W[(long long)d * J + j] : 0.f;
   auto pre = [&](int n) {
     float s = 0.f;
 #pragma unroll
-    for (int d = 0; d < KMAX; ++d)
-      if (d < K) s = fmaf(zs[n * K + d], w[d], s);
+    for (int d = 0; d < KM; ++d) s = fmaf(zs[n * KM + d], w[d], s);
     return s;
   };
   float s = 0.f;
@@ -47,8 +50,8 @@ __global__ __launch_bounds__(256) void splitfc_fwd_kernel(const float* z, int ld
   __syncthreads();
   float q = 0.f;
   for (int n = rg; n < B; n += SFC_RG) {
-    float d = pre(n) - m;
-    q += d * d;
+    const float dd = pre(n) - m;
+    q += dd * dd;
   }
   red[rg][c] = q;
   __syncthreads();
@@ -63,83 +66,109 @@ __global__ __launch_bounds__(256) void splitfc_fwd_kernel(const float* z, int ld
   for (int n = rg; n < B; n += SFC_RG) dst[n * o_n] = lrelu_f((pre(n) - m) * is + b);
 }
 
+static int sfc_km(int K) { return K <= 4 ? 4 : (K <= 8 ? 8 : 32); }
+
 void splitfc_fwd(const float* z, int ldz, int zoff, int B, int K, const float* W, const float* beta, int J,
                  float* mean, float* invstd, float* out, long long o_n, int F, int ldo, hipStream_t s) {
-  hipLaunchKernelGGL(splitfc_fwd_kernel, dim3((J + SFC_COLS - 1) / SFC_COLS), dim3(256), B * K * sizeof(float), s, z,
-                     ldz, zoff, B, K, W, beta, J, mean, invstd, out, o_n, F, ldo);
+  const int km = sfc_km(K);
+  dim3 g((J + SFC_COLS - 1) / SFC_COLS);
+  const size_t lds = (size_t)B * km * sizeof(float);
+  if (km == 4)
+    hipLaunchKernelGGL(splitfc_fwd_kernel<4>, g, dim3(256), lds, s, z, ldz, zoff, B, K, W, beta, J, mean, invstd, out,
+                       o_n, F, ldo);
+  else if (km == 8)
+    hipLaunchKernelGGL(splitfc_fwd_kernel<8>, g, dim3(256), lds, s, z, ldz, zoff, B, K, W, beta, J, mean, invstd, out,
+                       o_n, F, ldo);
+  else
+    hipLaunchKernelGGL(splitfc_fwd_kernel<32>, g, dim3(256), lds, s, z, ldz, zoff, B, K, W, beta, J, mean, invstd,
+                       out, o_n, F, ldo);
 }
 
 int splitfc_blocks(int J) { return (J + SFC_COLS - 1) / SFC_COLS; }
 
-// backward: dW [K][J], dbeta [J], and per-block partial dz: dz_part[blk][n][d] = sum_{j in blk} dpre[n][j] W[d][j]
-// (each wave owns whole rows and all 64 features of the block in its lanes -> one wave reduction per (n, d))
+// backward: dW [K][J], dbeta [J], and per-block partial dz: dz_part[blk][n][d] = sum_{j in blk} dpre[n][j] W[d][j].
+// dpre rows are staged in LDS (pitch 65: conflict-free column reads) and the dz partials are then
+// formed by plain per-thread dot products over the block's 64 features.
+#define SFC_PITCH (SFC_COLS + 1)
+template <int KM>
 __global__ __launch_bounds__(256) void splitfc_bwd_kernel(const float* z, int ldz, int zoff, int B, int K,
                                                           const float* W, const float* beta, int J,
                                                           const float* mean, const float* invstd, const float* dout,
                                                           long long o_n, int F, int ldo, float* dW, float* dbeta,
                                                           float* dz_part) {
-  extern __shared__ float zs[];
+  extern __shared__ float sm[];
+  float* zs = sm;                 // [B][KM]
+  float* dps = sm + B * KM;       // [B][SFC_PITCH]
   __shared__ float red[2][SFC_RG][SFC_COLS];
-  __shared__ float gwr[SFC_RG][KMAX][SFC_COLS];
-  for (int i = threadIdx.x; i < B * K; i += blockDim.x) zs[i] = z[(i / K) * ldz + zoff + (i % K)];
-  __syncthreads();
+  __shared__ float ws[KM][SFC_COLS];
+  for (int i = threadIdx.x; i < B * KM; i += blockDim.x) {
+    const int d = i % KM;
+    zs[i] = d < K ? z[(i / KM) * ldz + zoff + d] : 0.f;
+  }
   const int c = threadIdx.x & (SFC_COLS - 1), rg = threadIdx.x / SFC_COLS;
   const int j = blockIdx.x * SFC_COLS + c;
   const bool ok = j < J;
-  float w[KMAX];
+  float w[KM];
 #pragma unroll
-  for (int d = 0; d < KMAX; ++d) w[d] = (ok && d < K) ? W[(long long)d * J + j] : 0.f;
+  for (int d = 0; d < KM; ++d) w[d] = (ok && d < K) ? W[(long long)d * J + j] : 0.f;
+  if (rg == 0) {
+#pragma unroll
+    for (int d = 0; d < KM; ++d) ws[d][c] = w[d];
+  }
   const float m = ok ? mean[j] : 0.f, is = ok ? invstd[j] : 0.f, b = ok ? beta[j] : 0.f;
   const float* src = dout + (long long)(j / F) * ldo + (j % F);
+  // dout rows are staged into this column of the LDS tile (independent loads, all in flight)
+#pragma unroll 8
+  for (int n = rg; n < B; n += SFC_RG) dps[n * SFC_PITCH + c] = ok ? src[n * o_n] : 0.f;
+  __syncthreads();
   auto xhat = [&](int n) {
     float s = 0.f;
 #pragma unroll
-    for (int d = 0; d < KMAX; ++d)
-      if (d < K) s = fmaf(zs[n * K + d], w[d], s);
+    for (int d = 0; d < KM; ++d) s = fmaf(zs[n * KM + d], w[d], s);
     return (s - m) * is;
   };
   float sd = 0.f, sx = 0.f;
-  if (ok)
-    for (int n = rg; n < B; n += SFC_RG) {
-      float xh = xhat(n);
-      float dz = src[n * o_n] * ((xh + b) > 0.f ? 1.f : 0.1f);
-      sd += dz;
-      sx += dz * xh;
-    }
+  for (int n = rg; n < B; n += SFC_RG) {
+    const float xh = xhat(n);
+    const float dzv = dps[n * SFC_PITCH + c] * ((xh + b) > 0.f ? 1.f : 0.1f);
+    dps[n * SFC_PITCH + c] = dzv;
+    sd += dzv;
+    sx += dzv * xh;
+  }
   red[0][rg][c] = sd;
   red[1][rg][c] = sx;
   __syncthreads();
   sd = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
   sx = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
   const float a = sd / B, cc = sx / B;
-  float gw[KMAX];
+  float gw[KM];
 #pragma unroll
-  for (int d = 0; d < KMAX; ++d) gw[d] = 0.f;
-  float* P = dz_part + (long long)blockIdx.x * B * K;
+  for (int d = 0; d < KM; ++d) gw[d] = 0.f;
   for (int n = rg; n < B; n += SFC_RG) {
-    float dp = 0.f;
-    if (ok) {
-      float xh = xhat(n);
-      float dz = src[n * o_n] * ((xh + b) > 0.f ? 1.f : 0.1f);
-      dp = is * (dz - a - xh * cc);
-    }
+    const float dp = ok ? is * (dps[n * SFC_PITCH + c] - a - xhat(n) * cc) : 0.f;
+    dps[n * SFC_PITCH + c] = dp;
 #pragma unroll
-    for (int d = 0; d < KMAX; ++d) {
-      if (d < K) {
-        gw[d] = fmaf(zs[n * K + d], dp, gw[d]);
-        float v = wave_sum(dp * w[d]);
-        if (c == 0) P[n * K + d] = v;
-      }
-    }
+    for (int d = 0; d < KM; ++d) gw[d] = fmaf(zs[n * KM + d], dp, gw[d]);
   }
+  __syncthreads();
+  float* P = dz_part + (long long)blockIdx.x * B * K;
+  for (int p = threadIdx.x; p < B * K; p += blockDim.x) {
+    const int n = p / K, d = p - n * K;
+    const float* row = dps + n * SFC_PITCH;
+    float s = 0.f;
+#pragma unroll 16
+    for (int q = 0; q < SFC_COLS; ++q) s = fmaf(row[q], ws[d][q], s);
+    P[p] = s;
+  }
+  __syncthreads();  // dps reused below as the dW reduction buffer
+  float* gwr = dps;  // [SFC_RG][KM][SFC_COLS] fits in B*SFC_PITCH floats when B >= 4*KM
 #pragma unroll
-  for (int d = 0; d < KMAX; ++d)
-    if (d < K) gwr[rg][d][c] = gw[d];
+  for (int d = 0; d < KM; ++d) gwr[(rg * KM + d) * SFC_COLS + c] = gw[d];
   __syncthreads();
   if (ok && rg == 0) {
-#pragma unroll
-    for (int d = 0; d < KMAX; ++d)
-      if (d < K) dW[(long long)d * J + j] = gwr[0][d][c] + gwr[1][d][c] + gwr[2][d][c] + gwr[3][d][c];
+    for (int d = 0; d < K; ++d)
+      dW[(long long)d * J + j] = gwr[(0 * KM + d) * SFC_COLS + c] + gwr[(1 * KM + d) * SFC_COLS + c] +
+                                 gwr[(2 * KM + d) * SFC_COLS + c] + gwr[(3 * KM + d) * SFC_COLS + c];
     dbeta[j] = sd;
   }
 }
@@ -147,8 +176,26 @@ __global__ __launch_bounds__(256) void splitfc_bwd_kernel(const float* z, int ld
 void splitfc_bwd(const float* z, int ldz, int zoff, int B, int K, const float* W, const float* beta, int J,
                  const float* mean, const float* invstd, const float* dout, long long o_n, int F, int ldo, float* dW,
                  float* dbeta, float* dz_part, hipStream_t s) {
-  hipLaunchKernelGGL(splitfc_bwd_kernel, dim3((J + SFC_COLS - 1) / SFC_COLS), dim3(256), B * K * sizeof(float), s, z,
-                     ldz, zoff, B, K, W, beta, J, mean, invstd, dout, o_n, F, ldo, dW, dbeta, dz_part);
+  const int km = sfc_km(K);
+  dim3 g((J + SFC_COLS - 1) / SFC_COLS);
+  const int rows = B > 4 * km ? B : 4 * km;  // dps doubles as the [4][KM][64] dW reduction buffer
+  const size_t lds = ((size_t)B * km + (size_t)rows * SFC_PITCH) * sizeof(float);
+  static bool attr = false;
+  if (!attr) {  // B=256, K=30 needs ~100 KB of the 160 KB LDS
+    hipFuncSetAttribute((const void*)splitfc_bwd_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    hipFuncSetAttribute((const void*)splitfc_bwd_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    hipFuncSetAttribute((const void*)splitfc_bwd_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    attr = true;
+  }
+  if (km == 4)
+    hipLaunchKernelGGL(splitfc_bwd_kernel<4>, g, dim3(256), lds, s, z, ldz, zoff, B, K, W, beta, J, mean, invstd,
+                       dout, o_n, F, ldo, dW, dbeta, dz_part);
+  else if (km == 8)
+    hipLaunchKernelGGL(splitfc_bwd_kernel<8>, g, dim3(256), lds, s, z, ldz, zoff, B, K, W, beta, J, mean, invstd,
+                       dout, o_n, F, ldo, dW, dbeta, dz_part);
+  else
+    hipLaunchKernelGGL(splitfc_bwd_kernel<32>, g, dim3(256), lds, s, z, ldz, zoff, B, K, W, beta, J, mean, invstd,
+                       dout, o_n, F, ldo, dW, dbeta, dz_part);
 }
 
 // ---------------------------------------------------------------------------
@@ -228,17 +275,20 @@ void heads_fwd(const float* X, long long x_gs, int B, int K, const float* Wm, co
 }
 
 // dz[n][zoff+d] += sum_split part   where part = skinny(dpre [B][J], W^T)
+// dz[n][zoff+d] += sum over blocks of part[blk][n][d]: one wave per (n, d)
 __global__ void splitfc_dz_kernel(const float* part, int nsplit, int B, int K, float* dz, int ldz, int zoff) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B * K) return;
-  const int n = i / K, d = i % K;
+  const int wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  if (wv >= B * K) return;
+  const int n = wv / K, d = wv % K;
   float s = 0.f;
-  for (int sp = 0; sp < nsplit; ++sp) s += part[((long long)sp * B + n) * K + d];
-  dz[n * ldz + zoff + d] += s;
+  for (int sp = lane; sp < nsplit; sp += 64) s += part[((long long)sp * B + n) * K + d];
+  s = wave_sum(s);
+  if (lane == 0) dz[n * ldz + zoff + d] += s;
 }
 
 void splitfc_dz_reduce(const float* dz_part, int nblk, int B, int K, float* dz, int ldz, int zoff, hipStream_t s) {
-  hipLaunchKernelGGL(splitfc_dz_kernel, dim3((B * K + 255) / 256), dim3(256), 0, s, dz_part, nblk, B, K, dz, ldz, zoff);
+  hipLaunchKernelGGL(splitfc_dz_kernel, dim3((B * K * 64 + 255) / 256), dim3(256), 0, s, dz_part, nblk, B, K, dz, ldz,
+                     zoff);
 }
 
 // ---------------------------------------------------------------------------
