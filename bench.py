@@ -24,6 +24,9 @@ sys.path.insert(0, ROOT)
 PKG = "sequential-variational-autoencoder_amd"
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no 2:1 sparsity)
+# dominant kernel of the bf16 step (profiles/r01_*_bf16_kernel_stats.txt: largest total time)
+DOMINANT_KID = "KID_WGRAD_BF16_128x128"
 
 
 def conv_flops_per_img(cfg):
@@ -90,6 +93,23 @@ def time_dominant_kernel(L, shape, iters=50):
     sec = e0.elapsed_time(e1) / 1000.0 / iters
     flops = 2.0 * n * h * h * cout * 16 * cin
     return sec, flops
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (tools/pmc_traffic.py:
+    separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes, FETCH doubled per the gfx950 note in
+    MI355X_MICROARCH.md), or None when no summary for this kernel is committed."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        k = d.get("kernels", {}).get(kernel)
+        if k and k.get("hbm_bytes_per_launch"):
+            return float(k["hbm_bytes_per_launch"]), os.path.relpath(path, ROOT)
+    return None, None
 
 
 def cpu_baseline(cfg, target_sec=15.0, max_steps=4):
@@ -160,6 +180,7 @@ def main():
         net.backward()
         net.apply_gradients(cfg.learning_rate, it)
 
+    probe_kid = getattr(L, DOMINANT_KID) if args.dtype == "bf16" else None
     it = 0
     for _ in range(args.warmup):
         it += 1
@@ -168,6 +189,8 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    if probe_kid is not None and rank == 0:  # event pairs around every launch of the dominant kernel
+        L.check(L.lib().svae_probe_begin(net.ctx, probe_kid, 400 * args.steps), net.ctx)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         it += 1
@@ -177,6 +200,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    probe = None
+    if probe_kid is not None and rank == 0:
+        import ctypes
+        n, nt = ctypes.c_int64(), ctypes.c_int64()
+        fl, ms_k = ctypes.c_double(), ctypes.c_double()
+        L.check(L.lib().svae_probe_end(net.ctx, ctypes.byref(n), ctypes.byref(nt), ctypes.byref(fl),
+                                       ctypes.byref(ms_k)), net.ctx)
+        probe = dict(kernel=L.lib().svae_kernel_name(probe_kid).decode(), launches=n.value, timed=nt.value,
+                     flops=fl.value, ms=ms_k.value)
     elbo = net.loss_value()
     if dist:
         t = torch.tensor([elapsed], device="cuda")
@@ -192,7 +224,21 @@ def main():
 
     roof = None
     cpu = None
-    if rank == 0:
+    if rank == 0 and probe is not None and probe["timed"] > 0:
+        # dominant kernel, timed live in the timed region: sum of per-launch algorithmic FLOPs
+        # (2*taps*M*N*pixels) / sum of per-launch event durations
+        ach = probe["flops"] / (probe["ms"] / 1e3) / 1e12
+        avg_us = probe["ms"] * 1e3 / probe["timed"]
+        traffic, tsrc = pmc_traffic(probe["kernel"])
+        roof = dict(bound="mfma", achieved=round(ach, 3), peak=BF16_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
+                    frac=round(ach / BF16_MFMA_PEAK_TFLOPS, 5), traffic=traffic,
+                    kernel=probe["kernel"], launches_per_step=probe["launches"] / args.steps,
+                    avg_launch_us=round(avg_us, 2),
+                    flops_per_launch=round(probe["flops"] / probe["timed"]),
+                    traffic_source=tsrc,
+                    step_achieved_tflops=round(flops_img * value / world / 1e12, 3),
+                    step_frac=round(flops_img * value / world / 1e12 / BF16_MFMA_PEAK_TFLOPS, 5))
+    elif rank == 0:
         shape = dominant_kernel_shape(cfg)
         sec, kflops = time_dominant_kernel(L, shape)
         ach = kflops / sec / 1e12
@@ -202,8 +248,8 @@ def main():
                         "x".join(str(shape[k]) for k in ("n", "h", "cin", "cout"))),
                     kernel_us=round(sec * 1e6, 2),
                     step_achieved_tflops=round(flops_img * value / world / 1e12, 3))
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(cfg)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg)
     if rank == 0:
         line = {
             "metric": "images/sec (CelebA 64x64 seq-VAE fwd+bwd+Adam step)",

@@ -96,6 +96,15 @@ int svae_adam(svae_ctx* ctx, float lr, int64_t step, float clip, void* stream);
 /* Copy an internal buffer (device -> caller device pointer). */
 int svae_copy_out(svae_ctx* ctx, int which, int step, float* dst, int64_t n, void* stream);
 
+/* Launch probe (instrumentation, no reference counterpart): between begin and end, every
+ * launch of the bf16 GEMM instance `kernel_id` (see svae_kernel_name) issued by forward /
+ * backward is bracketed by an event pair on the launch stream.  end() synchronises those
+ * events and returns the launch count, the number timed (<= max_launches), their summed
+ * algorithmic FLOPs and summed duration in ms.  Used by bench.py for roofline.achieved. */
+int svae_probe_begin(svae_ctx* ctx, int kernel_id, int max_launches);
+int svae_probe_end(svae_ctx* ctx, int64_t* launches, int64_t* timed, double* flops, double* total_ms);
+const char* svae_kernel_name(int kernel_id);
+
 /* ---- per-op entry points (kernel-level parity tests) ---- */
 /* TF-SAME conv2d (transpose=0, W [4,4,Cin,Cout]) or conv2d_transpose (transpose=1,
  * W [4,4,Cout,Cin]) forward on x [N,H,H,Cin]; stride 1|2. */

@@ -1,10 +1,12 @@
 #!/bin/bash
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests/test_engine_gpu.py -q -x -s > gpurun_out/tests.log 2>&1
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -q -x > gpurun_out/tests.log 2>&1
 rc=$?; echo tests_rc=$rc >> gpurun_out/tests.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bf16 -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --dtype bf16 > gpurun_out/prof.log 2>&1
-echo prof_rc=$? >> gpurun_out/prof.log
-timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --dtype bf16 > gpurun_out/bench.log 2>&1
-echo bench_rc=$? >> gpurun_out/bench.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bf16 -o run -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/prof.log 2>&1 || exit 1
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1 || exit 1
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_fetch.log 2>&1 || exit 1
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_write.log 2>&1 || exit 1

@@ -295,7 +295,18 @@ struct BNS {  // per-layer BN statistics (mean / invstd), groups x C
   float* invstd = nullptr;
 };
 
+// Launch probe: times every launch of one bf16 GEMM instance with an event pair on the
+// launch stream and accumulates its algorithmic FLOPs (bench.py's roofline line).
+struct Probe {
+  int kid = KID_NONE;
+  std::vector<hipEvent_t> ev;  // pairs
+  int used = 0;                // pairs recorded
+  long long launches = 0;
+  double flops = 0;
+};
+
 struct svae_ctx {
+  Probe probe;
   Model m;
   std::string err;
   int device = 0;
@@ -427,10 +438,28 @@ static const void* shadowN(svae_ctx* c, long long off) { return (const void*)((c
 static const void* shadowT(svae_ctx* c, long long off) { return (const void*)((const __bf16*)c->wT + off); }
 
 // launches the gather-GEMM; returns the number of BN-stat row blocks it wrote
+// event pair for the next probed launch (nullptr when the pool is exhausted)
+static hipEvent_t* probe_pair(svae_ctx* c, int kid, double flops) {
+  Probe& p = c->probe;
+  if (p.kid == KID_NONE || kid != p.kid) return nullptr;
+  p.launches++;
+  if (2 * (size_t)p.used + 1 >= p.ev.size()) return nullptr;
+  p.flops += flops;  // FLOPs of timed launches only
+  hipEvent_t* e = &p.ev[2 * p.used++];
+  hipEventRecord(e[0], c->st);
+  return e;
+}
+
 static int gemm(svae_ctx* c, FwdArgs a, int groups) {
   if (c->m.g.bf16 && a.Bh) {
     a.part = c->slab;
     a.part_cap = c->slab_cap;
+    if (c->probe.kid != KID_NONE) {  // algorithmic FLOPs: 2 * rows * N * taps * Cin per class
+      const int ntap = a.g.mode == GM_DENSE ? 1 : (a.g.mode == GM_CONVT && a.g.stride == 2 ? 4 : 16);
+      const double fl = 2.0 * a.rows * a.nclass * a.N * (double)ntap * a.Cin * groups;
+      hipEvent_t* e = probe_pair(c, igemm_bf16_kid(a), fl);
+      if (e) return igemm_bf16(a, groups, c->st, e[1]);
+    }
     return igemm_bf16(a, groups, c->st);
   }
   a.ksplit = 1;
@@ -446,8 +475,19 @@ static int gemm_nrb(svae_ctx* c, FwdArgs a, int groups) {
   return nrb_of(a);
 }
 static void wgemm(svae_ctx* c, const WgArgs& w, int groups) {
-  if (c->m.g.bf16) wgrad_bf16(w, groups, c->st);
-  else wgrad(w, groups, c->st);
+  if (!c->m.g.bf16) {
+    wgrad(w, groups, c->st);
+    return;
+  }
+  if (c->probe.kid != KID_NONE) {  // algorithmic FLOPs: 2 * taps * M * N * row pixels
+    const double fl = 2.0 * w.ntap * (double)w.M * w.N * w.rows * groups;
+    hipEvent_t* e = probe_pair(c, wgrad_bf16_kid(w), fl);
+    if (e) {
+      wgrad_bf16(w, groups, c->st, e[1]);
+      return;
+    }
+  }
+  wgrad_bf16(w, groups, c->st);
 }
 
 // Forward conv/convT + BN + act.  in: [B,hin,hin,cin] (ld), out view gets act(BN(pre)+res)
@@ -1211,6 +1251,7 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
 
 int svae_destroy(svae_ctx* c) {
   if (!c) return 0;
+  for (hipEvent_t ev : c->probe.ev) hipEventDestroy(ev);
   if (c->arena) hipFree(c->arena);
   if (c->adam_m) hipFree(c->adam_m);
   if (c->reg_host) hipHostFree(c->reg_host);
@@ -1221,6 +1262,44 @@ int svae_destroy(svae_ctx* c) {
   delete c;
   return 0;
 }
+
+int svae_probe_begin(svae_ctx* c, int kid, int max_launches) {
+  if (!c || kid < 0 || kid >= KID_COUNT || max_launches < 0) return fail(c, SVAE_EBADARG, "bad probe request");
+  Probe& p = c->probe;
+  const size_t need = 2 * (size_t)max_launches + 2;
+  while (p.ev.size() < need) {
+    hipEvent_t ev;
+    hipError_t er = hipEventCreate(&ev);
+    if (er != hipSuccess) return fail(c, SVAE_EHIP, std::string("hipEventCreate: ") + hipGetErrorString(er));
+    p.ev.push_back(ev);
+  }
+  p.kid = kid;
+  p.used = 0;
+  p.launches = 0;
+  p.flops = 0;
+  return 0;
+}
+
+int svae_probe_end(svae_ctx* c, int64_t* launches, int64_t* timed, double* flops, double* total_ms) {
+  if (!c) return fail(c, SVAE_EBADARG, "null ctx");
+  Probe& p = c->probe;
+  double ms = 0;
+  for (int i = 0; i < p.used; ++i) {
+    hipError_t er = hipEventSynchronize(p.ev[2 * i + 1]);
+    float t = 0.f;
+    if (er == hipSuccess) er = hipEventElapsedTime(&t, p.ev[2 * i], p.ev[2 * i + 1]);
+    if (er != hipSuccess) return fail(c, SVAE_EHIP, std::string("probe events: ") + hipGetErrorString(er));
+    ms += t;
+  }
+  if (launches) *launches = p.launches;
+  if (timed) *timed = p.used;
+  if (flops) *flops = p.flops;
+  if (total_ms) *total_ms = ms;
+  p.kid = KID_NONE;
+  return 0;
+}
+
+const char* svae_kernel_name(int kid) { return kernel_name(kid); }
 
 const char* svae_last_error(const svae_ctx* c) { return c ? c->err.c_str() : g_tls_err.c_str(); }
 

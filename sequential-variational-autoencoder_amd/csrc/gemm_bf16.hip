@@ -605,17 +605,47 @@ int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit) {
   return (int)(((long long)a.rows * a.nclass + SKR_ROWS - 1) / SKR_ROWS);
 }
 
-int igemm_bf16(FwdArgs a, int groups, hipStream_t s) {
+const char* kernel_name(int kid) {
+  static const char* names[KID_COUNT] = {
+      "none", "none",
+      "igemm_bf16_kernel<256, 32, 4, 1, false>", "igemm_bf16_kernel<256, 32, 4, 1, true>",
+      "igemm_bf16_kernel<128, 64, 2, 2, false>", "igemm_bf16_kernel<128, 64, 2, 2, true>",
+      "igemm_bf16_kernel<128, 128, 2, 2, false>", "igemm_bf16_kernel<128, 128, 2, 2, true>",
+      "igemm_bf16_kernel<64, 128, 1, 4, false>", "igemm_bf16_kernel<64, 128, 1, 4, true>",
+      "wgrad_bf16_kernel<128, 32, 4, 1, true>", "wgrad_bf16_kernel<128, 32, 4, 1, false>",
+      "wgrad_bf16_kernel<128, 64, 2, 2, true>", "wgrad_bf16_kernel<128, 64, 2, 2, false>",
+      "wgrad_bf16_kernel<128, 128, 2, 2, true>", "wgrad_bf16_kernel<128, 128, 2, 2, false>"};
+  return (kid >= 0 && kid < KID_COUNT) ? names[kid] : "none";
+}
+
+int igemm_bf16_kid(const FwdArgs& a) {
+  const int sc = (a.Cin % BKB) != 0;
+  if (a.N <= 32) return KID_IGEMM_BF16_256x32 + sc;
+  if (a.N <= 64) return KID_IGEMM_BF16_128x64 + sc;
+  if (bf16_bm(a) == 128) return KID_IGEMM_BF16_128x128 + sc;
+  return KID_IGEMM_BF16_64x128 + sc;
+}
+
+int wgrad_bf16_kid(const WgArgs& a) {
+  const int scalar = !((a.M % 4 == 0) && (a.ldg % 4 == 0));
+  if (a.N <= 32) return KID_WGRAD_BF16_128x32 + scalar;
+  if (a.N <= 64) return KID_WGRAD_BF16_128x64 + scalar;
+  return KID_WGRAD_BF16_128x128 + scalar;
+}
+
+int igemm_bf16(FwdArgs a, int groups, hipStream_t s, hipEvent_t after) {
   const bool sc = (a.Cin % BKB) != 0;
   int ks = 1;
   const int nrb = igemm_bf16_plan(a, groups, &ks);
   a.ksplit = ks;
   a.rows_total = a.rows * a.nclass;
-  const int bm = bf16_bm(a);
-  if (a.N <= 32) launch_bf16<256, 32, 4, 1>(a, groups, sc, s);
-  else if (a.N <= 64) launch_bf16<128, 64, 2, 2>(a, groups, sc, s);
-  else if (bm == 128) launch_bf16<128, 128, 2, 2>(a, groups, sc, s);
-  else launch_bf16<64, 128, 1, 4>(a, groups, sc, s);
+  switch (igemm_bf16_kid(a) & ~1) {
+    case KID_IGEMM_BF16_256x32: launch_bf16<256, 32, 4, 1>(a, groups, sc, s); break;
+    case KID_IGEMM_BF16_128x64: launch_bf16<128, 64, 2, 2>(a, groups, sc, s); break;
+    case KID_IGEMM_BF16_128x128: launch_bf16<128, 128, 2, 2>(a, groups, sc, s); break;
+    default: launch_bf16<64, 128, 1, 4>(a, groups, sc, s); break;
+  }
+  if (after) hipEventRecord(after, s);
   if (ks > 1) {
     dim3 grid((a.N + 63) / 64, nrb, groups);
     hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, s, a.part, ks, a.rows_total, a.N, a.C, a.c_gs, a.ldc,
@@ -637,13 +667,17 @@ int wgrad_bf16_tiles(const WgArgs& a) {
   return ((a.ntap * a.M + 127) / 128) * ((a.N + bn - 1) / bn);
 }
 
-void wgrad_bf16(WgArgs a, int groups, hipStream_t s) {
-  const bool vec = (a.M % 4 == 0) && (a.ldg % 4 == 0);
+void wgrad_bf16(WgArgs a, int groups, hipStream_t s, hipEvent_t after) {
+  const int kid = wgrad_bf16_kid(a);
+  const bool vec = !(kid & 1);
   a.g.dHW = make_fastdiv(a.g.Ho * a.g.Wo);
   a.g.dW = make_fastdiv(a.g.Wo);
-  if (a.N <= 32) launch_wg_bf16<128, 32, 4, 1>(a, groups, vec, s);
-  else if (a.N <= 64) launch_wg_bf16<128, 64, 2, 2>(a, groups, vec, s);
-  else launch_wg_bf16<128, 128, 2, 2>(a, groups, vec, s);
+  switch (kid & ~1) {
+    case KID_WGRAD_BF16_128x32: launch_wg_bf16<128, 32, 4, 1>(a, groups, vec, s); break;
+    case KID_WGRAD_BF16_128x64: launch_wg_bf16<128, 64, 2, 2>(a, groups, vec, s); break;
+    default: launch_wg_bf16<128, 128, 2, 2>(a, groups, vec, s); break;
+  }
+  if (after) hipEventRecord(after, s);
 }
 
 void shadow_weights(const float* w, void* wn, void* wt, long long n, const void* tiles, int ntiles, const void* offs,

@@ -33,9 +33,26 @@ struct WgArgs {
 int igemm_fwd_bm(const FwdArgs& a);
 // bf16-MFMA variants (dtype=1): A fp32 -> bf16 in staging, B = a.Bh bf16 [tap][n][k] (ldb = k pitch)
 // returns the number of stats row-blocks written to a.stats (plan: same value without launching)
-int igemm_bf16(FwdArgs a, int groups, hipStream_t s);
+// Kernel-instance ids of the bf16 GEMMs (one per template instantiation = one rocprof kernel
+// name); used by the launch probe (svae_probe_*) that times every launch of one instance.
+enum KernelId {
+  KID_NONE = 0,
+  KID_IGEMM_BF16_256x32 = 2, KID_IGEMM_BF16_256x32_SC = 3,
+  KID_IGEMM_BF16_128x64 = 4, KID_IGEMM_BF16_128x64_SC = 5,
+  KID_IGEMM_BF16_128x128 = 6, KID_IGEMM_BF16_128x128_SC = 7,
+  KID_IGEMM_BF16_64x128 = 8, KID_IGEMM_BF16_64x128_SC = 9,
+  KID_WGRAD_BF16_128x32 = 10, KID_WGRAD_BF16_128x32_SCALAR = 11,
+  KID_WGRAD_BF16_128x64 = 12, KID_WGRAD_BF16_128x64_SCALAR = 13,
+  KID_WGRAD_BF16_128x128 = 14, KID_WGRAD_BF16_128x128_SCALAR = 15,
+  KID_COUNT = 16
+};
+const char* kernel_name(int kid);
+int igemm_bf16_kid(const FwdArgs& a);
+int wgrad_bf16_kid(const WgArgs& a);
+// `after` (optional) is recorded on s right after the GEMM kernel, before any split-K reduce
+int igemm_bf16(FwdArgs a, int groups, hipStream_t s, hipEvent_t after = nullptr);
 int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit);
-void wgrad_bf16(WgArgs a, int groups, hipStream_t s);  // taps merged into M (part [split][tap*M+m][n])
+void wgrad_bf16(WgArgs a, int groups, hipStream_t s, hipEvent_t after = nullptr);  // taps merged into M (part [split][tap*M+m][n])
 int wgrad_bf16_tiles(const WgArgs& a);
 // bf16 weight shadows: wn = bf16(w) for [0,n); wt = per-tap transposes listed in tiles/offs
 void shadow_weights(const float* w, void* wn, void* wt, long long n, const void* tiles, int ntiles, const void* offs,
