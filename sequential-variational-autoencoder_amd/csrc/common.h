@@ -63,6 +63,26 @@ __device__ __forceinline__ float dact_from_y(float y, int act) {
   return 1.f;
 }
 
+// XCD-aware block order (cdna_hip_programming.md T1, bijective form): workgroups are dealt
+// round-robin over the 8 XCDs, so linear id b runs on XCD-group b % 8.  Remap so that each
+// XCD-group owns a contiguous range of logical tiles (x fastest, then y, then z): neighbouring
+// tiles, which share operand panels, then share one L2.  Speed only, never correctness.
+struct BlockXYZ {
+  int x, y, z;
+};
+__device__ __forceinline__ BlockXYZ xcd_block() {
+  const int X = gridDim.x, Y = gridDim.y;
+  const int nwg = X * Y * gridDim.z;
+  const int orig = blockIdx.x + X * (blockIdx.y + Y * blockIdx.z);
+  const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+  const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  BlockXYZ b;
+  b.x = id % X;
+  b.y = (id / X) % Y;
+  b.z = id / (X * Y);
+  return b;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

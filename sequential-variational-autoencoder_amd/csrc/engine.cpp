@@ -560,8 +560,8 @@ static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, V
     w.rows = B * L.hin * L.hin;
   }
   if (c->m.g.bf16)  // tap-merged tiles; longer splits (less slab traffic)
-    choose_split(w.rows, 1, wgrad_bf16_tiles(w), groups, 16LL * w.M * w.N, c->slab_cap, w.nsplit, w.chunk, 768,
-                 1024);
+    choose_split(w.rows, 1, wgrad_bf16_tiles(w), groups, 16LL * w.M * w.N, c->slab_cap, w.nsplit, w.chunk, 2048,
+                 256);
   else
     choose_split(w.rows, 16, ((w.M + 63) / 64) * ((w.N + 63) / 64), groups, 16LL * w.M * w.N, c->slab_cap,
                  w.nsplit, w.chunk);
@@ -862,7 +862,9 @@ static int engine_backward(svae_ctx* c) {
     output_bwd(s.a_out, B, g.H * g.W, g.C, xprev, s.xhat, c->tgt_in, g.lo, g.hi, g.minh, g.maxh, rec_coef, dxin, c->da,
                dxout, st);
     {
-      const int M_out = t >= 1 ? C1 : g.C;
+      // packed [C | ratio] columns; at t=0 the ratio column of da is zero (output_bwd) and its
+      // gradient row is dropped by the reduce -> always the 4-wide vector gather
+      const int M_out = C1;
       WgArgs w{};
       w.G = c->da; w.ldg = C1;
       w.D = s.s1_act[0]; w.ldd = F[1];
@@ -871,8 +873,8 @@ static int engine_backward(svae_ctx* c) {
       w.ntap = 16;
       w.rows = B * S[1] * S[1];
       if (g.bf16)
-        choose_split(w.rows, 1, wgrad_bf16_tiles(w), 1, 16LL * M_out * F[1], c->slab_cap, w.nsplit, w.chunk, 768,
-                     1024);
+        choose_split(w.rows, 1, wgrad_bf16_tiles(w), 1, 16LL * M_out * F[1], c->slab_cap, w.nsplit, w.chunk, 2048,
+                     256);
       else
         choose_split(w.rows, 16, (F[1] + 127) / 128, 1, 16LL * M_out * F[1], c->slab_cap, w.nsplit, w.chunk);
       w.part = c->slab;

@@ -471,22 +471,48 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs a) {
 }
 
 // sum the split slabs: out[tap][m][n] (rows m < msplit -> out0, else out1)
+__device__ __forceinline__ float* wred_dst(float* out0, long long o0_gs, int msplit, float* out1, long long o1_gs,
+                                           int group, int tap, int M, int m, int N, int n) {
+  if (m < msplit) return out0 + group * o0_gs + ((long long)tap * msplit + m) * N + n;
+  if (!out1) return nullptr;  // rows routed to an absent second output are dropped
+  return out1 + group * o1_gs + ((long long)tap * (M - msplit) + (m - msplit)) * N + n;
+}
+
+// out[tap][m][n] (= or +=) sum_sp part[group][sp][tap][m][n], summed in split order (deterministic).
+// VEC: 4 consecutive n per thread (N % 4 == 0), four independent partial sums over the splits.
+template <bool VEC>
 __global__ void wgrad_reduce_kernel(const float* part, long long p_gs, int nsplit, int ntap, int M, int N,
                                     float* out0, long long o0_gs, int msplit, float* out1, long long o1_gs,
                                     int accumulate) {
   const int group = blockIdx.y;
   const long long per = (long long)ntap * M * N;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < per; i += (long long)gridDim.x * blockDim.x) {
+  const long long nq = VEC ? per / 4 : per;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (long long)gridDim.x * blockDim.x) {
+    const long long i = VEC ? q * 4 : q;
     const float* p = part + group * p_gs + i;
-    float s = 0.f;
-    for (int sp = 0; sp < nsplit; ++sp) s += p[sp * per];
     const int tap = (int)(i / ((long long)M * N));
     const int rem = (int)(i - (long long)tap * M * N);
-    const int m = rem / N, n = rem - (rem / N) * N;
-    float* dst;
-    if (m < msplit) dst = out0 + group * o0_gs + ((long long)tap * msplit + m) * N + n;
-    else dst = out1 + group * o1_gs + ((long long)tap * (M - msplit) + (m - msplit)) * N + n;
-    *dst = accumulate ? *dst + s : s;
+    const int m = rem / N, n = rem - m * N;
+    float* dst = wred_dst(out0, o0_gs, msplit, out1, o1_gs, group, tap, M, m, N, n);
+    if (!dst) continue;
+    if (VEC) {
+      f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0, s3 = s0;
+      int sp = 0;
+      for (; sp + 4 <= nsplit; sp += 4) {
+        s0 += *(const f32x4*)(p + (sp + 0) * per);
+        s1 += *(const f32x4*)(p + (sp + 1) * per);
+        s2 += *(const f32x4*)(p + (sp + 2) * per);
+        s3 += *(const f32x4*)(p + (sp + 3) * per);
+      }
+      for (; sp < nsplit; ++sp) s0 += *(const f32x4*)(p + sp * per);
+      f32x4 s = (s0 + s1) + (s2 + s3);
+      if (accumulate) s += *(const f32x4*)dst;
+      *(f32x4*)dst = s;
+    } else {
+      float s = 0.f;
+      for (int sp = 0; sp < nsplit; ++sp) s += p[sp * per];
+      *dst = accumulate ? *dst + s : s;
+    }
   }
 }
 
@@ -550,7 +576,13 @@ void wgrad(WgArgs a, int groups, hipStream_t s) {
 void wgrad_reduce(const float* part, long long p_gs, int nsplit, int ntap, int M, int N, float* out0, long long o0_gs,
                   int msplit, float* out1, long long o1_gs, int accumulate, int groups, hipStream_t s) {
   long long per = (long long)ntap * M * N;
-  int blocks = (int)std::min<long long>((per + 255) / 256, 4096);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks, groups), dim3(256), 0, s, part, p_gs, nsplit, ntap, M, N, out0,
-                     o0_gs, msplit, out1, o1_gs, accumulate);
+  const bool vec = (N % 4 == 0) && (p_gs % 4 == 0) && (o0_gs % 4 == 0) && (o1_gs % 4 == 0);
+  const long long items = vec ? per / 4 : per;
+  int blocks = (int)std::min<long long>((items + 255) / 256, 8192);
+  if (vec)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<true>, dim3(blocks, groups), dim3(256), 0, s, part, p_gs, nsplit, ntap, M,
+                       N, out0, o0_gs, msplit, out1, o1_gs, accumulate);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel<false>, dim3(blocks, groups), dim3(256), 0, s, part, p_gs, nsplit, ntap, M,
+                       N, out0, o0_gs, msplit, out1, o1_gs, accumulate);
 }

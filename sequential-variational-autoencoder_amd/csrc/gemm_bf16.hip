@@ -113,10 +113,11 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
   const int l32 = lane & 31, h = lane >> 5;
   const int wm0 = (wave / WN) * (TM * 32), wn0 = (wave % WN) * (TN * 32);
   const int ks = a.ksplit;
-  const int split = blockIdx.z % ks;
-  const int zc = blockIdx.z / ks;
+  const BlockXYZ blk = xcd_block();
+  const int split = blk.z % ks;
+  const int zc = blk.z / ks;
   const int group = zc / a.nclass, cls = zc - group * a.nclass;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int m0 = blk.x * BM, n0 = blk.y * BN;
   const float* A = a.A + group * a.a_gs;
   const __bf16* Bw = (const __bf16*)a.Bh + group * a.b_gs;
   const int ntap = ntaps_of_b(g);
@@ -309,7 +310,7 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
         float s = 0.f, q = 0.f;
 #pragma unroll
         for (int w = 0; w < WM; ++w) { s += red[w * BN + tid]; q += red[WM * BN + w * BN + tid]; }
-        const long long rb_idx = (long long)cls * gridDim.x + blockIdx.x;  // ks == 1 here
+        const long long rb_idx = (long long)cls * gridDim.x + blk.x;  // ks == 1 here
         float* st = a.stats + group * a.s_gs + rb_idx * 2 * a.N;
         st[n] = s;
         st[a.N + n] = q;
@@ -338,9 +339,10 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
   const int lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, h = lane >> 5;
   const int wm0 = (wave / WN) * (TM * 32), wn0 = (wave % WN) * (TN * 32);
-  const int r0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  const int split = blockIdx.z % a.nsplit;
-  const int group = blockIdx.z / a.nsplit;
+  const BlockXYZ blk = xcd_block();
+  const int r0 = blk.x * BM, n0 = blk.y * BN;
+  const int split = blk.z % a.nsplit;
+  const int group = blk.z / a.nsplit;
   const int Mtot = a.ntap * a.M;
   const float* G = a.G + group * a.g_gs;
   const float* D = a.D + group * a.d_gs;
@@ -593,9 +595,9 @@ int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit) {
   const int Ktot = ntap * a.Cin;
   const int nk = (a.Cin % BKB) ? (Ktot + BKB - 1) / BKB : ntap * (a.Cin / BKB);
   int ks = 1;
-  if (blocks < 256 && a.part) {
-    ks = (int)std::min<long long>((384 + blocks - 1) / blocks, 4);
-    ks = std::min(ks, nk / 8);  // keep >= 8 K steps per split
+  if (blocks < 512 && a.part) {
+    ks = (int)std::min<long long>((768 + blocks - 1) / blocks, 8);
+    ks = std::min(ks, nk / 4);  // keep >= 4 K steps per split
     const long long rows_total = (long long)a.rows * a.nclass;
     while (ks > 1 && (long long)ks * rows_total * a.N * groups > a.part_cap) --ks;
     if (ks < 2) ks = 1;
