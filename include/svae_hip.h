@@ -111,6 +111,13 @@ const char* svae_kernel_name(int kernel_id);
 int svae_op_conv(const float* x, int n, int h, int cin, const float* w, int cout, int stride, int transpose,
                  float* y, void* stream);
 /* input gradient and weight gradient of the same op */
+/* bf16 gather-GEMM (throughput mode kernels): y = conv2d (transpose=0) or conv2d_transpose
+ * (transpose=1) of fp32 NHWC x with bf16 weights already in the engine's NK shadow layout
+ * w_nk[tap][cout][cin] (tap = ky*4+kx); x is rounded to bf16 while staged, fp32 accumulate.
+ * path: 0 per-tap gather kernel, 1 halo-tile kernel (SVAE_EBADARG if the shape does not
+ * qualify), 2 automatic.  scratch (optional) enables split-K. */
+int svae_op_gather_bf16(const float* x, int n, int h, int cin, const void* w_nk, int cout, int stride, int transpose,
+                        int path, float* y, void* scratch, int64_t scratch_bytes, void* stream);
 int svae_op_conv_dgrad(const float* dy, int n, int h, int cin, const float* w, int cout, int stride, int transpose,
                        float* dx, void* stream);
 int svae_op_conv_wgrad(const float* x, int n, int h, int cin, const float* dy, int cout, int stride, int transpose,

@@ -1376,6 +1376,10 @@ int svae_copy_out(svae_ctx* c, int which, int step, float* dst, int64_t n, void*
     case 110: src = c->dbg_last; cnt = n; break;
     case 111: c->dbg_stop_lvl2 = step; return 0;
     case 112: src = c->ab; cnt = n; break;
+    case 113: src = c->inf_pre_a[step]; cnt = n; break;   // debug: inference level `step`, all T groups
+    case 114: src = c->inf_act_a[step]; cnt = n; break;
+    case 115: src = c->inf_pre_b[step]; cnt = n; break;
+    case 116: src = c->inf_act_b[step]; cnt = n; break;
     case 106: src = c->sb[c->dbg_stop_step].s1_act[step]; cnt = n; break;
     case 107: src = c->sb[c->dbg_stop_step].s1_bn[step].mean; cnt = n; break;
     case 108: src = c->sb[c->dbg_stop_step].s1_bn[step].invstd; cnt = n; break;
@@ -1403,6 +1407,25 @@ int svae_op_conv(const float* x, int n, int h, int cin, const float* w, int cout
   a.A = x; a.lda = cin;
   a.C = y; a.ldc = cout;
   igemm_fwd(a, 1, (hipStream_t)stream);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(nullptr, SVAE_EHIP, hipGetErrorString(e));
+}
+
+int svae_op_gather_bf16(const float* x, int n, int h, int cin, const void* w_nk, int cout, int stride, int transpose,
+                        int path, float* y, void* scratch, int64_t scratch_bytes, void* stream) {
+  if (!x || !w_nk || !y || (stride != 1 && stride != 2) || path < 0 || path > 2)
+    return fail(nullptr, SVAE_EBADARG, "bad op args");
+  ConvL L;
+  L.cin = cin; L.cout = cout; L.stride = stride; L.hin = h; L.tr = transpose != 0;
+  L.hout = L.tr ? h * stride : h / stride;
+  FwdArgs a = fwd_args_conv(L, n, nullptr, 0);
+  a.A = x; a.lda = cin;
+  a.Bh = w_nk; a.ldb = cin; a.b_tap = (long long)cin * cout;
+  a.C = y; a.ldc = cout;
+  a.part = (float*)scratch;
+  a.part_cap = scratch ? scratch_bytes / (int64_t)sizeof(float) : 0;
+  if (igemm_bf16_path(a, 1, path, (hipStream_t)stream) < 0)
+    return fail(nullptr, SVAE_EBADARG, "shape does not qualify for the halo-tile kernel");
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(nullptr, SVAE_EHIP, hipGetErrorString(e));
 }

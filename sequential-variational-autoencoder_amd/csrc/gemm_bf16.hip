@@ -8,6 +8,8 @@
 // LDS tiles are [row][k] bf16 with an 80-byte row pitch (conflict-free ds_read_b128 of
 // the 8-element k fragments).  Weight-GEMM operands are pixel-major in HBM and are
 // transposed in registers (4 pixels x 4 channels -> 4 x ds_write_b64).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -320,6 +322,278 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Halo-tile gather-GEMM (conv / conv-T forward and input gradient, bf16 MFMA).
+// A block owns BM row-space pixels that form whole image rows (or whole images).  For each
+// 32-channel chunk of the gathered operand the block stages the input window those pixels
+// touch -- PR x PC pixels per image, zero-padded at the borders -- in LDS once, as bf16 with an
+// 80-byte pixel pitch, and every tap of the chunk reads its A fragments from that window at a
+// fixed (dy, dx) shift.  The per-tap gather of the plain kernel re-reads every input element
+// through L2 once per tap (16x); here each element is read once per block (plus the halo).
+// Weights keep the per-(chunk, tap) double-buffered B tiles of the plain kernel.
+//   CONV          iy = ry*s - pad + ky         window rows (R-1)*s + 4, dy = ky
+//   CONVT s=1     iy = ry + pad - ky           window rows R + 3,       dy = 3 - ky
+//   CONVT s=2     class (cy,cx), ky = k0+2*ty  window rows R + 1,       dy = 1 - ty
+// ---------------------------------------------------------------------------
+#define HALO_CK 32   // channels per window stage
+#define HALO_PI 8    // window items (8 channels each) per thread and stage: npix*4 <= 256*HALO_PI
+
+struct HaloArgs {
+  FwdArgs f;
+  int Hr, Wr;        // row-space image dims (per parity class for CONVT s2)
+  int R, nimg;       // image rows per block (per image) and images per block
+  int PR, PC;        // window dims per image
+  int sy;            // row-space -> input stride (CONV stride, else 1)
+  int npix;          // nimg * PR * PC
+};
+
+template <int BM, int BN, int WM, int WN, bool S2T>
+__global__ __launch_bounds__(256, 2) void igemm_halo_kernel(HaloArgs h) {
+  constexpr int TM = BM / WM / 32;
+  constexpr int TN = BN / WN / 32;
+  constexpr int NTAP = S2T ? 4 : 16;
+  constexpr int P = 4;  // B-fragment prefetch distance in taps (NTAP % P == 0)
+  extern __shared__ __attribute__((aligned(16))) __bf16 hsm[];
+  const FwdArgs& a = h.f;
+  const ConvGeom& g = a.g;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int wm0 = (wave / WN) * (TM * 32), wn0 = (wave % WN) * (TN * 32);
+  const int ks = a.ksplit;
+  const BlockXYZ blk = xcd_block();
+  const int split = blk.z % ks;
+  const int zc = blk.z / ks;
+  const int group = zc / a.nclass, cls = zc - group * a.nclass;
+  const int m0 = blk.x * BM, n0 = blk.y * BN;
+  const float* A = a.A + group * a.a_gs;
+  const __bf16* Bw = (const __bf16*)a.Bh + group * a.b_gs;
+  const int nchunk = a.Cin / HALO_CK;
+  const int cbeg = (int)((long long)nchunk * split / ks), cend = (int)((long long)nchunk * (split + 1) / ks);
+
+  // ---- block window origin and per-tap geometry (uniform) ----
+  const int per_img = h.Hr * h.Wr;
+  const int img0 = m0 / per_img;
+  const int ry0 = (m0 - img0 * per_img) / h.Wr;
+  int oy_min, ox_min, tap0, toff0, tsgn;
+  if (S2T) {
+    const int cy = cls >> 1, cx = cls & 1;
+    const int ky0 = (cy + g.pad) & 1, kx0 = (cx + g.pad) & 1;
+    oy_min = (cy + g.pad - ky0) / 2 - 1;
+    ox_min = (cx + g.pad - kx0) / 2 - 1;
+    tap0 = ky0 * 4 + kx0;  // B tap of t: tap0 + 8*(t>>1) + 2*(t&1)
+    toff0 = h.PC + 1;      // window shift of t: (1-(t>>1))*PC + (1-(t&1))
+    tsgn = -1;
+  } else if (g.mode == GM_CONV) {
+    oy_min = ox_min = -g.pad;
+    tap0 = 0;
+    toff0 = 0;  // shift of tap t: (t>>2)*PC + (t&3)
+    tsgn = 1;
+  } else {
+    oy_min = ox_min = g.pad - 3;
+    tap0 = 0;
+    toff0 = 3 * h.PC + 3;  // shift: (3-(t>>2))*PC + (3-(t&3))
+    tsgn = -1;
+  }
+  const int iy_base = ry0 * h.sy + oy_min;
+
+  // ---- window staging: per-thread item offsets, identical for every chunk ----
+  int woff[HALO_PI];
+#pragma unroll
+  for (int i = 0; i < HALO_PI; ++i) {
+    const int it = tid + 256 * i;
+    woff[i] = -2;  // -2: no item, -1: zero (outside the image)
+    if (it < h.npix * 4) {
+      const int pix = it >> 2, part = it & 3;
+      const int il = pix / (h.PR * h.PC);
+      const int r2 = pix - il * h.PR * h.PC;
+      const int pr = r2 / h.PC, pc = r2 - pr * h.PC;
+      const int iy = iy_base + pr, ix = ox_min + pc;
+      woff[i] = (iy >= 0 && iy < g.Hi && ix >= 0 && ix < g.Wi)
+                    ? (((img0 + il) * g.Hi + iy) * g.Wi + ix) * a.lda + part * 8
+                    : -1;
+    }
+  }
+  // staged in two halves (items [0, PI/2) and [PI/2, PI)) to halve the registers in flight
+  constexpr int HP = HALO_PI / 2;
+  f32x4 wv[HP][2];
+  auto load_window = [&](int chunk, int half) {
+    const float* Ac = A + chunk * HALO_CK;
+#pragma unroll
+    for (int j = 0; j < HP; ++j) {
+      const int i = half * HP + j;
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      wv[j][0] = z;
+      wv[j][1] = z;
+      if (woff[i] >= 0) {
+        wv[j][0] = *(const f32x4*)(Ac + woff[i]);
+        wv[j][1] = *(const f32x4*)(Ac + woff[i] + 4);
+      }
+    }
+  };
+  auto store_window = [&](int buf, int half) {
+    __bf16* W = hsm + buf * h.npix * ROWP;
+#pragma unroll
+    for (int j = 0; j < HP; ++j) {
+      const int i = half * HP + j;
+      const int it = tid + 256 * i;
+      if (woff[i] >= -1) *(bf16x8*)&W[(it >> 2) * ROWP + (it & 3) * 8] = cvt8(wv[j][0], wv[j][1]);
+    }
+  };
+
+  // ---- A fragment bases (window pixel of tap shift 0) ----
+  int abase[TM];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const int ml = wm0 + tm * 32 + l32;
+    const int rows_img = h.R * h.Wr;
+    const int il = ml / rows_img;
+    const int rem = ml - il * rows_img;
+    const int ryl = rem / h.Wr, rx = rem - ryl * h.Wr;
+    abase[tm] = ((il * h.PR + ryl * h.sy) * h.PC + rx * h.sy) * ROWP + 8 * hh;
+  }
+
+  // ---- B fragments straight from the bf16 shadow (L2-resident), P taps ahead ----
+  bool nok[TN];
+  const __bf16* bptr[TN];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    const int n = n0 + wn0 + tn * 32 + l32;
+    nok[tn] = (n0 + wn0 + tn * 32) < a.N;  // uniform per 32-column group (N % 32 == 0)
+    bptr[tn] = Bw + (long long)(nok[tn] ? n : 0) * a.ldb + 8 * hh;
+  }
+  bf16x8 bq[P][TN][2];
+  auto load_b = [&](int slot, int chunk, int t) {
+    const int tap = S2T ? tap0 + 8 * (t >> 1) + 2 * (t & 1) : t;
+    const long long off = (long long)tap * a.b_tap + chunk * HALO_CK;
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+      for (int kq = 0; kq < 2; ++kq) bq[slot][tn][kq] = *(const bf16x8*)(bptr[tn] + off + kq * 16);
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (cbeg < cend) {
+    load_window(cbeg, 0);
+    store_window(0, 0);
+    load_window(cbeg, 1);
+#pragma unroll
+    for (int t = 0; t < P; ++t) load_b(t, cbeg, t);
+    store_window(0, 1);
+  }
+  __syncthreads();
+  for (int c = cbeg; c < cend; ++c) {
+    const int buf = (c - cbeg) & 1;
+    const bool has_next = c + 1 < cend;
+    const __bf16* W = hsm + buf * h.npix * ROWP;
+#pragma unroll
+    for (int t = 0; t < NTAP; ++t) {
+      // next chunk's window: half 0 issued at tap 0 and stored at NTAP/2-1, half 1 at NTAP/2 .. NTAP-1
+      if (has_next && (t == 0 || t == NTAP / 2)) load_window(c + 1, t == 0 ? 0 : 1);
+      const int shift = S2T ? toff0 + tsgn * ((t >> 1) * h.PC + (t & 1)) : toff0 + tsgn * ((t >> 2) * h.PC + (t & 3));
+      const int sh = shift * ROWP;
+#pragma unroll
+      for (int kq = 0; kq < 2; ++kq) {
+        bf16x8 af[TM];
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) af[tm] = *(const bf16x8*)&W[abase[tm] + sh + kq * 16];
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < TN; ++tn)
+            if (nok[tn])
+              acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm], bq[t % P][tn][kq], acc[tm][tn], 0, 0, 0);
+      }
+      // refill this slot with the fragments P taps ahead
+      if (t + P < NTAP) load_b(t % P, c, t + P);
+      else if (has_next) load_b(t % P, c + 1, t + P - NTAP);
+      if (has_next && (t == NTAP / 2 - 1 || t == NTAP - 1)) store_window(buf ^ 1, t == NTAP - 1 ? 1 : 0);
+    }
+    __syncthreads();
+  }
+
+  if (ks > 1) {  // raw partial tile -> slab[split][out_row][n]; bias/act/stats in splitk_reduce
+    float* Pp = a.part + (long long)group * ks * a.rows_total * a.N + (long long)split * a.rows_total * a.N;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm0 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const long long orow = out_row_b(g, cls, m);
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+          const int n = n0 + wn0 + tn * 32 + l32;
+          if (nok[tn]) Pp[orow * a.N + n] = acc[tm][tn][r];
+        }
+      }
+    return;
+  }
+
+  float* Cp = a.C + group * a.c_gs;
+  const float* bias = a.bias ? a.bias + group * a.bias_gs : nullptr;
+  float csum[TN], csq[TN];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) { csum[tn] = 0.f; csq[tn] = 0.f; }
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wm0 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      const long long orow = out_row_b(g, cls, m);
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int n = n0 + wn0 + tn * 32 + l32;
+        if (!nok[tn]) continue;
+        float v = acc[tm][tn][r];
+        csum[tn] += v;
+        csq[tn] += v * v;
+        if (bias) v += bias[n];
+        v = act_f(v, a.act);
+        float* dst = Cp + orow * a.ldc + n;
+        if (a.accumulate) v += *dst;
+        *dst = v;
+      }
+    }
+  }
+  if (a.stats) {
+    float* red = (float*)hsm;
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      csum[tn] += __shfl_xor(csum[tn], 32, 64);
+      csq[tn] += __shfl_xor(csq[tn], 32, 64);
+    }
+    __syncthreads();
+    if (hh == 0) {
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        red[(wave / WN) * BN + wn0 + tn * 32 + l32] = csum[tn];
+        red[WM * BN + (wave / WN) * BN + wn0 + tn * 32 + l32] = csq[tn];
+      }
+    }
+    __syncthreads();
+    if (tid < BN) {
+      const int n = n0 + tid;
+      if (n < a.N) {
+        float s = 0.f, q = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) { s += red[w * BN + tid]; q += red[WM * BN + w * BN + tid]; }
+        const long long rb_idx = (long long)cls * gridDim.x + blk.x;  // ks == 1 here
+        float* st = a.stats + group * a.s_gs + rb_idx * 2 * a.N;
+        st[n] = s;
+        st[a.N + n] = q;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // weight-GEMM, bf16 MFMA, taps merged into M:  rows r = tap*M + m of
 //   part[split][r][n] = sum_{p in split} G[src(p, tap)][m] * D[p][n]
 // (small-channel layers fill all waves; one dY tile feeds every tap of the row tile)
@@ -588,7 +862,114 @@ static int bf16_bm(const FwdArgs& a) {
 }
 static int bf16_bn(const FwdArgs& a) { return a.N <= 32 ? 32 : (a.N <= 64 ? 64 : 128); }
 
+// ---- halo-tile planner: which (BM, BN) instance, window geometry, split-K ----
+struct HaloPlan {
+  bool ok = false;
+  int bm = 0, bn = 0, kid = KID_NONE, ks = 1, nrb = 0;
+  HaloArgs h;
+  size_t lds = 0;
+};
+#define HALO_LDS_MAX (80 * 1024)  // two blocks per CU
+
+static HaloPlan halo_plan(const FwdArgs& a, int groups) {
+  HaloPlan p;
+  const ConvGeom& g = a.g;
+  if (g.mode == GM_DENSE || g.ksz != 4 || a.Cin % HALO_CK != 0 || !a.Bh || a.N % 32 != 0) return p;
+  const bool s2t = g.mode == GM_CONVT && g.stride == 2;
+  const int Hr = s2t ? g.Ho / 2 : g.Ho, Wr = s2t ? g.Wo / 2 : g.Wo;
+  const int sy = g.mode == GM_CONV ? g.stride : 1;
+  const int span = s2t ? 2 : 4;
+  if (g.mode == GM_CONVT && g.stride > 2) return p;
+  // measured (tools/bench_gather.py): the window pays off on wide rows; deep 8x8 / 4x4 layers
+  // with long K stay on the per-tap kernel
+  if (!(Wr >= 16 || (s2t && Wr >= 8))) return p;
+  const int bn = a.N <= 32 ? 32 : (a.N <= 64 ? 64 : 128);
+  const int cands[2] = {bn == 32 ? 256 : 128, bn == 32 ? 128 : 64};
+  const int per_img = Hr * Wr;
+  for (int ci = 0; ci < 2; ++ci) {
+    const int bm = cands[ci];
+    if (bm % Wr != 0 || a.rows % bm != 0) continue;
+    if (!(per_img % bm == 0 || bm % per_img == 0)) continue;
+    HaloArgs h;
+    h.Hr = Hr;
+    h.Wr = Wr;
+    h.R = bm >= per_img ? Hr : bm / Wr;
+    h.nimg = bm >= per_img ? bm / per_img : 1;
+    h.sy = sy;
+    h.PR = (h.R - 1) * sy + span;
+    h.PC = (Wr - 1) * sy + span;
+    h.npix = h.nimg * h.PR * h.PC;
+    if (h.npix * 4 > 256 * HALO_PI) continue;
+    const size_t lds = (size_t)(2 * h.npix) * ROWP * sizeof(__bf16);
+    if (lds > HALO_LDS_MAX) continue;
+    const long long blocks = (long long)(a.rows / bm) * ((a.N + bn - 1) / bn) * a.nclass * groups;
+    if (ci == 0 && blocks < 256) {  // prefer the smaller tile when the large one underfills
+      const int bm2 = cands[1];
+      if (bm2 % Wr == 0 && a.rows % bm2 == 0 && (per_img % bm2 == 0 || bm2 % per_img == 0)) {
+        const int R2 = bm2 >= per_img ? Hr : bm2 / Wr, n2 = bm2 >= per_img ? bm2 / per_img : 1;
+        const int np2 = n2 * ((R2 - 1) * sy + span) * ((Wr - 1) * sy + span);
+        if (np2 * 4 <= 256 * HALO_PI && (size_t)(2 * np2) * ROWP * sizeof(__bf16) <= HALO_LDS_MAX) continue;
+      }
+    }
+    p.ok = true;
+    p.bm = bm;
+    p.bn = bn;
+    p.h = h;
+    p.lds = lds;
+    const int nchunk = a.Cin / HALO_CK;
+    int ks = 1;
+    if (blocks < 512 && a.part) {
+      ks = (int)std::min<long long>((768 + blocks - 1) / blocks, 8);
+      ks = std::min(ks, nchunk);
+      const long long rows_total = (long long)a.rows * a.nclass;
+      while (ks > 1 && (long long)ks * rows_total * a.N * groups > a.part_cap) --ks;
+      if (ks < 2) ks = 1;
+    }
+    p.ks = ks;
+    p.nrb = ks == 1 ? a.nclass * (a.rows / bm) : (int)(((long long)a.rows * a.nclass + SKR_ROWS - 1) / SKR_ROWS);
+    if (bn == 32) p.kid = bm == 256 ? KID_HALO_256x32 : KID_HALO_128x32;
+    else if (bn == 64) p.kid = bm == 128 ? KID_HALO_128x64 : KID_HALO_64x64;
+    else p.kid = bm == 128 ? KID_HALO_128x128 : KID_HALO_64x128;
+    return p;
+  }
+  return p;
+}
+
+template <int BM, int BN, int WM, int WN>
+static void launch_halo(const HaloArgs& h, int groups, size_t lds, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)igemm_halo_kernel<BM, BN, WM, WN, false>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, HALO_LDS_MAX);
+    hipFuncSetAttribute((const void*)igemm_halo_kernel<BM, BN, WM, WN, true>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, HALO_LDS_MAX);
+    attr = true;
+  }
+  const FwdArgs& a = h.f;
+  dim3 grid(a.rows / BM, (a.N + BN - 1) / BN, groups * a.nclass * a.ksplit);
+  if (a.g.mode == GM_CONVT && a.g.stride == 2)
+    hipLaunchKernelGGL((igemm_halo_kernel<BM, BN, WM, WN, true>), grid, dim3(256), lds, s, h);
+  else
+    hipLaunchKernelGGL((igemm_halo_kernel<BM, BN, WM, WN, false>), grid, dim3(256), lds, s, h);
+}
+
+static int halo_disabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SVAE_NO_HALO");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v;
+}
+
 int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit) {
+  if (!halo_disabled()) {
+    const HaloPlan hp = halo_plan(a, groups);
+    if (hp.ok) {
+      if (ksplit) *ksplit = hp.ks;
+      return hp.nrb;
+    }
+  }
   const int bm = bf16_bm(a), bn = bf16_bn(a);
   const long long blocks = (long long)((a.rows + bm - 1) / bm) * ((a.N + bn - 1) / bn) * a.nclass * groups;
   const int ntap = a.g.mode == GM_DENSE ? 1 : (a.g.mode == GM_CONVT && a.g.stride == 2 ? 4 : 16);
@@ -616,11 +997,18 @@ const char* kernel_name(int kid) {
       "igemm_bf16_kernel<64, 128, 1, 4, false>", "igemm_bf16_kernel<64, 128, 1, 4, true>",
       "wgrad_bf16_kernel<128, 32, 4, 1, true>", "wgrad_bf16_kernel<128, 32, 4, 1, false>",
       "wgrad_bf16_kernel<128, 64, 2, 2, true>", "wgrad_bf16_kernel<128, 64, 2, 2, false>",
-      "wgrad_bf16_kernel<128, 128, 2, 2, true>", "wgrad_bf16_kernel<128, 128, 2, 2, false>"};
+      "wgrad_bf16_kernel<128, 128, 2, 2, true>", "wgrad_bf16_kernel<128, 128, 2, 2, false>",
+      "igemm_halo_kernel<256, 32, 4, 1>", "igemm_halo_kernel<128, 32, 4, 1>",
+      "igemm_halo_kernel<128, 64, 2, 2>", "igemm_halo_kernel<64, 64, 2, 2>",
+      "igemm_halo_kernel<128, 128, 2, 2>", "igemm_halo_kernel<64, 128, 1, 4>"};
   return (kid >= 0 && kid < KID_COUNT) ? names[kid] : "none";
 }
 
 int igemm_bf16_kid(const FwdArgs& a) {
+  if (!halo_disabled()) {
+    const HaloPlan hp = halo_plan(a, 1);
+    if (hp.ok) return hp.kid;
+  }
   const int sc = (a.Cin % BKB) != 0;
   if (a.N <= 32) return KID_IGEMM_BF16_256x32 + sc;
   if (a.N <= 64) return KID_IGEMM_BF16_128x64 + sc;
@@ -636,6 +1024,34 @@ int wgrad_bf16_kid(const WgArgs& a) {
 }
 
 int igemm_bf16(FwdArgs a, int groups, hipStream_t s, hipEvent_t after) {
+  return igemm_bf16_path(a, groups, 2, s, after);
+}
+
+int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t after) {
+  if (path == 1 || (path == 2 && !halo_disabled())) {
+    HaloPlan hp = halo_plan(a, groups);
+    if (!hp.ok && path == 1) return -1;
+    if (hp.ok) {
+      a.ksplit = hp.ks;
+      a.rows_total = a.rows * a.nclass;
+      hp.h.f = a;
+      switch (hp.kid) {
+        case KID_HALO_256x32: launch_halo<256, 32, 4, 1>(hp.h, groups, hp.lds, s); break;
+        case KID_HALO_128x32: launch_halo<128, 32, 4, 1>(hp.h, groups, hp.lds, s); break;
+        case KID_HALO_128x64: launch_halo<128, 64, 2, 2>(hp.h, groups, hp.lds, s); break;
+        case KID_HALO_64x64: launch_halo<64, 64, 2, 2>(hp.h, groups, hp.lds, s); break;
+        case KID_HALO_128x128: launch_halo<128, 128, 2, 2>(hp.h, groups, hp.lds, s); break;
+        default: launch_halo<64, 128, 1, 4>(hp.h, groups, hp.lds, s); break;
+      }
+      if (after) hipEventRecord(after, s);
+      if (hp.ks > 1) {
+        dim3 grid((a.N + 63) / 64, hp.nrb, groups);
+        hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, s, a.part, hp.ks, a.rows_total, a.N, a.C, a.c_gs,
+                           a.ldc, a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs);
+      }
+      return hp.nrb;
+    }
+  }
   const bool sc = (a.Cin % BKB) != 0;
   int ks = 1;
   const int nrb = igemm_bf16_plan(a, groups, &ks);

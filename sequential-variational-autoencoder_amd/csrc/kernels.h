@@ -44,13 +44,18 @@ enum KernelId {
   KID_WGRAD_BF16_128x32 = 10, KID_WGRAD_BF16_128x32_SCALAR = 11,
   KID_WGRAD_BF16_128x64 = 12, KID_WGRAD_BF16_128x64_SCALAR = 13,
   KID_WGRAD_BF16_128x128 = 14, KID_WGRAD_BF16_128x128_SCALAR = 15,
-  KID_COUNT = 16
+  KID_HALO_256x32 = 16, KID_HALO_128x32 = 17, KID_HALO_128x64 = 18, KID_HALO_64x64 = 19,
+  KID_HALO_128x128 = 20, KID_HALO_64x128 = 21,
+  KID_COUNT = 22
 };
 const char* kernel_name(int kid);
 int igemm_bf16_kid(const FwdArgs& a);
 int wgrad_bf16_kid(const WgArgs& a);
 // `after` (optional) is recorded on s right after the GEMM kernel, before any split-K reduce
 int igemm_bf16(FwdArgs a, int groups, hipStream_t s, hipEvent_t after = nullptr);
+// path: 0 = per-tap gather kernel, 1 = halo-tile kernel (returns -1 if the shape does not
+// qualify), 2 = automatic (halo when it qualifies, unless SVAE_NO_HALO=1)
+int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t after = nullptr);
 int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit);
 void wgrad_bf16(WgArgs a, int groups, hipStream_t s, hipEvent_t after = nullptr);  // taps merged into M (part [split][tap*M+m][n])
 int wgrad_bf16_tiles(const WgArgs& a);

@@ -1,0 +1,54 @@
+"""Time single bf16 gather-GEMM launches (svae_op_gather_bf16) on CelebA B=128 layer shapes.
+    python tools/bench_gather.py [path ...]       # path 0 = per-tap gather, 1 = halo window"""
+import importlib
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+L = importlib.import_module("sequential-variational-autoencoder_amd._lib")
+
+SHAPES = [  # (n, h_in, cin, cout, stride, transpose) -- CelebA B=128 forward layers
+    (128, 32, 64, 32, 1, 1), (128, 32, 32, 32, 1, 0), (128, 16, 64, 32, 2, 1), (128, 32, 32, 64, 2, 0),
+    (128, 16, 128, 64, 1, 1), (128, 16, 64, 64, 1, 0), (128, 8, 128, 64, 2, 1), (128, 16, 64, 128, 2, 0),
+    (128, 8, 256, 128, 1, 1), (128, 8, 128, 128, 1, 0), (128, 4, 384, 128, 2, 1),
+]
+
+
+def run(path, iters=20):
+    torch.manual_seed(0)
+    scratch = torch.empty(64 << 20, device="cuda")
+    tot_f, tot_t = 0.0, 0.0
+    for (n, h, cin, cout, s, tr) in SHAPES:
+        x = torch.randn(n, h, h, cin, device="cuda")
+        w = (torch.randn(16, cout, cin, device="cuda") * 0.05).to(torch.bfloat16)
+        ho = h * s if tr else h // s
+        y = torch.empty(n, ho, ho, cout, device="cuda")
+        args = (L.ptr(x), n, h, cin, L.ptr(w), cout, s, tr, path, L.ptr(y), L.ptr(scratch), scratch.numel() * 4,
+                L.stream_ptr())
+        rc = L.lib().svae_op_gather_bf16(*args)
+        if rc != 0:
+            print("%-28s path %d: not eligible" % (str((n, h, cin, cout, s, tr)), path))
+            continue
+        for _ in range(3):
+            L.lib().svae_op_gather_bf16(*args)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            L.lib().svae_op_gather_bf16(*args)
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / iters
+        fl = 2.0 * n * ho * ho * cout * cin * 16 / (s * s if tr else 1) * (s * s if tr else 1)
+        fl = 2.0 * n * ho * ho * cout * cin * (16 if not (tr and s == 2) else 4)
+        tot_f += fl
+        tot_t += us
+        print("%-28s path %d: %8.2f us  %7.1f TF/s" % (str((n, h, cin, cout, s, tr)), path, us, fl / us / 1e6))
+    print("path %d total %.1f us, %.1f TF/s" % (path, tot_t, tot_f / tot_t / 1e6))
+
+
+if __name__ == "__main__":
+    for p in (sys.argv[1:] or ["0", "1"]):
+        run(int(p))
