@@ -636,12 +636,14 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
     return rc;
   };
   // per-unit (tap, channel) of the A rows this thread stages (fixed over the K loop)
-  int utap[RA], um[RA];
+  int utap[RA], um[RA], uky[RA], ukx[RA];
 #pragma unroll
   for (int i = 0; i < RA; ++i) {
     const int r = r0 + ((tid + 256 * i) % QMc) * 4;
     utap[i] = r / a.M;
     um[i] = r - utap[i] * a.M;
+    uky[i] = utap[i] / g.ksz;
+    ukx[i] = utap[i] - uky[i] * g.ksz;
   }
 
   f32x4 va[RA][4], vb[RB][4];
@@ -651,6 +653,35 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
       const int u = tid + 256 * i;
       const int pq = u / QMc;
       const int r = r0 + (u % QMc) * 4;
+      if (VECG) {
+        // a quad of 4 row-space pixels never crosses an image row (chunks are 32-aligned and
+        // every row-space width is a multiple of 4): decode it once, step x by the stride
+        const int p0 = p_begin + kc * BKB + pq * 4;
+        const bool uok = u < UA && r < Mtot && p0 < p_end;
+        const RowCoordB rc = pix(uok ? p0 : 0);
+        int iy = 0, ix0 = 0;
+        if (g.mode == GM_DENSE) {
+          iy = 0;
+          ix0 = 0;
+        } else {
+          iy = rc.y * g.stride - g.pad + uky[i];
+          ix0 = rc.x * g.stride - g.pad + ukx[i];
+        }
+        const bool rowok = uok && (g.mode == GM_DENSE || (iy >= 0 && iy < g.Hi));
+        const float* gp = G + (g.mode == GM_DENSE ? (long long)p0 * a.ldg
+                                                  : ((long long)rc.img + (long long)iy * g.Wi + ix0) * a.ldg) +
+                          um[i];
+        const int step = g.mode == GM_DENSE ? a.ldg : g.stride * a.ldg;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f32x4 v = {0.f, 0.f, 0.f, 0.f};
+          const int ix = ix0 + j * g.stride;
+          const bool ok = rowok && (p0 + j < p_end) && (g.mode == GM_DENSE || (ix >= 0 && ix < g.Wi));
+          if (ok) v = *(const f32x4*)(gp + j * step);
+          va[i][j] = v;
+        }
+        continue;
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
@@ -658,9 +689,6 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
         if (u < UA && p < p_end && r < Mtot) {
           RowCoordB rc = pix(p);
           if (VECG) {
-            const int tap = utap[i];
-            long long sp = src_pixel_b(g, rc, tap / g.ksz, tap % g.ksz);
-            if (sp >= 0) v = *(const f32x4*)(G + sp * a.ldg + um[i]);
           } else {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {

@@ -1,6 +1,8 @@
 // Bandwidth-bound kernels of the hot path: split_latent FC+BN, recognition heads,
 // reparameterised latent + KL, small-N conv (output / layer-0 dgrad), output +
 // highway + reconstruction loss, loss reduction, clip+Adam, Philox normals.
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -504,10 +506,185 @@ __global__ __launch_bounds__(256) void gconv_smalln_kernel(const float* A, int l
   }
 }
 
+// Lane-parallel variant for K % 4 == 0, K/4 a power of two <= 64 (the CelebA output layer and
+// layer-0 input gradient: K = 32): LP = K/4 lanes share one output pixel, each owning a channel
+// quad, so a pixel's gather is one coalesced 16*LP-byte read; the 4 partial outputs are
+// summed across the LP lanes with xor shuffles.  stride is 1 or 2 (shift / mask, no division).
+template <int LP>
+__global__ __launch_bounds__(256) void gconv_smalln_lp_kernel(const float* A, int lda, int K, const float* W0, int n0,
+                                                              const float* W1, int n1, long long w_tap,
+                                                              long long w1_tap, const float* bias0, const float* bias1,
+                                                              ConvGeom g, long long rows, float* C, int ldc,
+                                                              int accumulate) {
+  extern __shared__ float ws[];  // [16 taps][K][4] (output fastest: one f32x4 per channel)
+  const int taps = g.ksz * g.ksz;
+  const int N = n0 + n1;
+  for (int i = threadIdx.x; i < taps * 4 * K; i += blockDim.x) {
+    const int t = i / (4 * K), r = i - t * 4 * K, k = r >> 2, o = r & 3;
+    float v = 0.f;
+    if (o < n0) v = W0[t * w_tap + (long long)o * K + k];
+    else if (o < N) v = W1[t * w1_tap + (long long)(o - n0) * K + k];
+    ws[i] = v;
+  }
+  __syncthreads();
+  const int HWo = g.Ho * g.Wo;
+  const int sm = g.stride - 1, sh = g.stride == 2 ? 1 : 0;
+  const int cq = threadIdx.x % LP;
+  // grid-stride over pixels: the weight table above is staged once per block
+  for (long long p0 = (long long)blockIdx.x * (blockDim.x / LP); p0 < rows; p0 += (long long)gridDim.x * (blockDim.x / LP)) {
+    const long long p = p0 + threadIdx.x / LP;
+    const bool live = p < rows;
+    const long long pp = live ? p : 0;
+    const int n = (int)(pp / HWo);
+    const int rem = (int)(pp - (long long)n * HWo);
+    const int oy = rem / g.Wo, ox = rem - (rem / g.Wo) * g.Wo;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int ky = 0; ky < g.ksz; ++ky) {
+      int iy;
+      if (g.mode == GM_CONV) iy = oy * g.stride - g.pad + ky;
+      else {
+        const int t = oy + g.pad - ky;
+        if (t < 0 || (t & sm)) continue;
+        iy = t >> sh;
+      }
+      if (iy < 0 || iy >= g.Hi) continue;
+      for (int kx = 0; kx < g.ksz; ++kx) {
+        int ix;
+        if (g.mode == GM_CONV) ix = ox * g.stride - g.pad + kx;
+        else {
+          const int t = ox + g.pad - kx;
+          if (t < 0 || (t & sm)) continue;
+          ix = t >> sh;
+        }
+        if (ix < 0 || ix >= g.Wi) continue;
+        const f32x4* w = (const f32x4*)(ws + (ky * g.ksz + kx) * 4 * K) + cq * 4;
+        for (int kk = cq * 4; kk < K; kk += 4 * LP) {
+          const f32x4 av = *(const f32x4*)(A + ((long long)(n * g.Hi + iy) * g.Wi + ix) * lda + kk);
+          const f32x4* wk = w + (kk - cq * 4);
+          acc += av[0] * wk[0] + av[1] * wk[1] + av[2] * wk[2] + av[3] * wk[3];
+        }
+      }
+    }
+#pragma unroll
+    for (int o = LP / 2; o > 0; o >>= 1) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] += __shfl_xor(acc[e], o, 64);
+    }
+    if (live && cq < N) {
+      float v = acc[cq];
+      if (cq < n0 && bias0) v += bias0[cq];
+      if (cq >= n0 && bias1) v += bias1[cq - n0];
+      float* d = C + p * ldc + cq;
+      *d = accumulate ? *d + v : v;
+    }
+  }
+}
+
+// Stride-2 conv-T gather with <= 4 outputs and K = 4*LP channels (output / ratio conv-T and the
+// layer-0 input gradient): grid.y = output parity class (cy, cx), whose 2x2 taps are fixed, so
+// each lane keeps its 4 channels x 4 taps x 4 outputs of weights in registers; LP lanes share a
+// pixel (one coalesced 16*LP-byte read per tap) and are summed with xor shuffles.
+template <int LP>
+__global__ __launch_bounds__(256) void gconv_s2t_kernel(const float* A, int lda, int K, const float* W0, int n0,
+                                                        const float* W1, int n1, long long w_tap, long long w1_tap,
+                                                        const float* bias0, const float* bias1, ConvGeom g,
+                                                        float* C, int ldc, int accumulate) {
+  const int cls = blockIdx.y, cy = cls >> 1, cx = cls & 1;
+  const int ky0 = (cy + g.pad) & 1, kx0 = (cx + g.pad) & 1;
+  const int N = n0 + n1;
+  const int cq = threadIdx.x % LP;
+  f32x4 w[4][4];  // [tap][channel e] -> 4 outputs
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int tap = (ky0 + 2 * (t >> 1)) * g.ksz + kx0 + 2 * (t & 1);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = cq * 4 + e;
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        float v = 0.f;
+        if (o < n0) v = W0[tap * w_tap + (long long)o * K + k];
+        else if (o < N) v = W1[tap * w1_tap + (long long)(o - n0) * K + k];
+        w[t][e][o] = v;
+      }
+    }
+  }
+  const int qh = g.Ho >> 1, qw = g.Wo >> 1;
+  const long long rows = (long long)g.nimg * qh * qw;
+  for (long long q0 = (long long)blockIdx.x * (blockDim.x / LP); q0 < rows; q0 += (long long)gridDim.x * (blockDim.x / LP)) {
+    const long long q = q0 + threadIdx.x / LP;
+    const bool live = q < rows;
+    const long long qq = live ? q : 0;
+    const int n = (int)(qq / (qh * qw));
+    const int r = (int)(qq - (long long)n * qh * qw);
+    const int qy = r / qw, qx = r - (r / qw) * qw;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int iy = qy + (cy + g.pad - ky0) / 2 - (t >> 1);
+      const int ix = qx + (cx + g.pad - kx0) / 2 - (t & 1);
+      if (iy >= 0 && iy < g.Hi && ix >= 0 && ix < g.Wi) {
+        const f32x4 av = *(const f32x4*)(A + ((long long)(n * g.Hi + iy) * g.Wi + ix) * lda + cq * 4);
+        acc += av[0] * w[t][0] + av[1] * w[t][1] + av[2] * w[t][2] + av[3] * w[t][3];
+      }
+    }
+#pragma unroll
+    for (int o = LP / 2; o > 0; o >>= 1) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] += __shfl_xor(acc[e], o, 64);
+    }
+    if (live && cq < N) {
+      float v = acc[cq];
+      if (cq < n0 && bias0) v += bias0[cq];
+      if (cq >= n0 && bias1) v += bias1[cq - n0];
+      const long long orow = ((long long)n * g.Ho + 2 * qy + cy) * g.Wo + 2 * qx + cx;
+      float* d = C + orow * ldc + cq;
+      *d = accumulate ? *d + v : v;
+    }
+  }
+}
+
 void gconv_smalln(const float* A, int lda, int K, const float* W0, int n0, const float* W1, int n1, long long w_tap,
                   long long w1_tap, const float* bias0, const float* bias1, ConvGeom g, long long rows_total,
                   float* C, int ldc, int accumulate, hipStream_t s) {
   size_t lds = (size_t)g.ksz * g.ksz * 4 * K * sizeof(float);
+  if (g.mode == GM_CONVT && g.stride == 2 && g.ksz == 4 && (lda & 3) == 0 && n0 + n1 <= 4 &&
+      (K == 16 || K == 32 || K == 64) && g.Ho % 2 == 0 && g.Wo % 2 == 0) {
+    const long long pix = (long long)g.nimg * (g.Ho / 2) * (g.Wo / 2);
+    const int lp = K / 4;
+    dim3 grid((unsigned)std::min<long long>((pix * lp + 255) / 256, 1024), 4);
+    if (lp == 4)
+      hipLaunchKernelGGL(gconv_s2t_kernel<4>, grid, dim3(256), 0, s, A, lda, K, W0, n0, W1, n1, w_tap, w1_tap, bias0,
+                         bias1, g, C, ldc, accumulate);
+    else if (lp == 8)
+      hipLaunchKernelGGL(gconv_s2t_kernel<8>, grid, dim3(256), 0, s, A, lda, K, W0, n0, W1, n1, w_tap, w1_tap, bias0,
+                         bias1, g, C, ldc, accumulate);
+    else
+      hipLaunchKernelGGL(gconv_s2t_kernel<16>, grid, dim3(256), 0, s, A, lda, K, W0, n0, W1, n1, w_tap, w1_tap, bias0,
+                         bias1, g, C, ldc, accumulate);
+    return;
+  }
+  if ((K & 3) == 0 && (lda & 3) == 0 && K >= 16 && K <= 256 && (K & (K - 1)) == 0 && g.ksz <= 4 && n0 + n1 <= 4) {
+    const int lp = K / 4 > 64 ? 64 : K / 4;  // lanes per pixel (power of two)
+    const long long threads = rows_total * lp;
+    dim3 grid((unsigned)std::min<long long>((threads + 255) / 256, 2048));
+    if (lp == 4)
+      hipLaunchKernelGGL(gconv_smalln_lp_kernel<4>, grid, dim3(256), lds, s, A, lda, K, W0, n0, W1, n1, w_tap, w1_tap,
+                         bias0, bias1, g, rows_total, C, ldc, accumulate);
+    else if (lp == 8)
+      hipLaunchKernelGGL(gconv_smalln_lp_kernel<8>, grid, dim3(256), lds, s, A, lda, K, W0, n0, W1, n1, w_tap, w1_tap,
+                         bias0, bias1, g, rows_total, C, ldc, accumulate);
+    else if (lp == 16)
+      hipLaunchKernelGGL(gconv_smalln_lp_kernel<16>, grid, dim3(256), lds, s, A, lda, K, W0, n0, W1, n1, w_tap, w1_tap,
+                         bias0, bias1, g, rows_total, C, ldc, accumulate);
+    else if (lp == 32)
+      hipLaunchKernelGGL(gconv_smalln_lp_kernel<32>, grid, dim3(256), lds, s, A, lda, K, W0, n0, W1, n1, w_tap, w1_tap,
+                         bias0, bias1, g, rows_total, C, ldc, accumulate);
+    else
+      hipLaunchKernelGGL(gconv_smalln_lp_kernel<64>, grid, dim3(256), lds, s, A, lda, K, W0, n0, W1, n1, w_tap, w1_tap,
+                         bias0, bias1, g, rows_total, C, ldc, accumulate);
+    return;
+  }
   hipLaunchKernelGGL(gconv_smalln_kernel, dim3((unsigned)((rows_total + 255) / 256)), dim3(256), lds, s, A, lda, K, W0,
                      n0, W1, n1, w_tap, w1_tap, bias0, bias1, g, rows_total, C, ldc, accumulate);
 }
