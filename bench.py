@@ -29,6 +29,17 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no 2:1 s
 DOMINANT_KID = "KID_WGRAD_BF16_128x128"
 
 
+# metric / workload per preset (BASELINE.json configs[1] is the headline: CelebA B=128)
+METRIC = {
+    "celeba": ("images/sec (CelebA 64x64 seq-VAE fwd+bwd+Adam step)",
+               "CelebA 64x64 default seq-VAE (c_inhomog), T=8 chain, fwd+bwd+clip+Adam"),
+    "lsun": ("images/sec (LSUN-bedroom 64x64 seq-VAE fwd+bwd+Adam step)",
+             "LSUN-bedroom 64x64 seq-VAE (sequential_vae_lsun, latent 110), T=8 chain, fwd+bwd+clip+Adam"),
+    "mnist_1step": ("images/sec (MNIST 32x32 1-step seq-VAE fwd+bwd+Adam step)",
+                    "MNIST 1-step seq-VAE (m_* geometry, latent 24), fwd+bwd+clip+Adam"),
+}
+
+
 def conv_flops_per_img(cfg):
     """Algorithmic fwd MACs per image of the executed graph (SURVEY §8a totals), x3 for
     fwd+dgrad+wgrad, x2 FLOP/MAC."""
@@ -112,15 +123,14 @@ def pmc_traffic(kernel):
     return None, None
 
 
-def cpu_baseline(cfg, target_sec=15.0, max_steps=4):
+def cpu_baseline(cfg, cfgname, target_sec=15.0, max_steps=4):
     """PyTorch-CPU fp32 restatement of the same graph (oracle/torch_twin.py), fwd+bwd,
     on a bounded sample: B=8 images of the CelebA geometry, whole T=8 chain."""
     from oracle import spec, torch_twin
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     B = 8
-    cd = spec.make_config("celeba" if cfg.filter_sizes == [3, 32, 64, 128, 384, 512] and
-                          cfg.latent_dims == [3, 3, 3, 3] else "lsun", batch=B)
+    cd = spec.make_config(cfgname, batch=B)
     _, struct, params = spec.init_params(cd, seed=0, dtype=np.float32)
     x, tgt, eps = spec.make_inputs(cd, batch=B)
     tw = torch_twin.Twin(cd, struct, params, dtype=torch.float32)
@@ -132,8 +142,8 @@ def cpu_baseline(cfg, target_sec=15.0, max_steps=4):
         n += 1
     dt = (time.time() - t0) / n
     return dict(value=B / dt, unit="images/sec", cores=threads, kind="port",
-                sample="%d fwd+bwd steps of B=%d CelebA-geometry images (T=8) with oracle/torch_twin.py fp32, "
-                       "%d threads" % (n, B, threads))
+                sample="%d fwd+bwd steps of B=%d %s-geometry images (T=%d) with oracle/torch_twin.py fp32, "
+                       "%d threads" % (n, B, cfgname, cd["mc_steps"], threads))
 
 
 def main():
@@ -164,6 +174,7 @@ def main():
     if args.batch:
         over["batch"] = args.batch
     cfg = cfgmod.preset(args.config, **over)
+    cfgname = cfgmod.NETNAMES.get(args.config, args.config)
     B = cfg.batch
     hook = par.allreduce_hook(dist) if world > 1 else None
     net = SV(cfg, seed=0, grad_hook=hook)
@@ -249,10 +260,10 @@ def main():
                     kernel_us=round(sec * 1e6, 2),
                     step_achieved_tflops=round(flops_img * value / world / 1e12, 3))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(cfg)
+        cpu = cpu_baseline(cfg, cfgname)
     if rank == 0:
         line = {
-            "metric": "images/sec (CelebA 64x64 seq-VAE fwd+bwd+Adam step)",
+            "metric": METRIC[cfgname][0],
             "value": round(value, 2),
             "unit": "images/sec",
             "n_gpus": world,
@@ -264,7 +275,7 @@ def main():
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic U[-1,1] NHWC batch, target=input, eps on-device Philox; deterministic splitmix64 init",
-            "config": {"workload": "CelebA 64x64 default seq-VAE (c_inhomog), T=8 chain, fwd+bwd+clip+Adam",
+            "config": {"workload": METRIC[cfgname][1],
                        "model": args.config, "global_batch": B * world, "per_gpu_batch": B,
                        "image": [cfg.height, cfg.width, cfg.channels], "mc_steps": cfg.mc_steps,
                        "parallelism": "dp%d" % world},

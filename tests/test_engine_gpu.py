@@ -186,11 +186,13 @@ def test_celeba_b128_forward_matches_twin():
         assert e_hip <= max(1e-4, 4 * e_32), (t, e_hip, e_32)
 
 
-def test_full_size_properties():
-    """Size-independent properties at the bench geometry: determinism, ELBO mean ==
-    loss, zero gradient on the frozen (dead / pre-BN bias) region."""
-    net, cfg = _engine("celeba", 128)
-    cd = spec.make_config("celeba")
+@pytest.mark.parametrize("preset,batch,dtype", [("celeba", 128, "fp32"), ("celeba", 128, "bf16"),
+                                                ("lsun", 256, "bf16"), ("lsun", 256, "fp32")])
+def test_full_size_properties(preset, batch, dtype):
+    """Size-independent properties at the BASELINE geometries (CelebA B=128, LSUN B=256):
+    determinism, ELBO mean == loss, zero gradient on the frozen (dead / pre-BN bias) region."""
+    net, cfg = _engine(preset, batch, dtype=dtype)
+    cd = spec.make_config(preset)
     x, tgt, eps = spec.make_inputs(cd)
     net.forward(x, tgt, eps, 1.0)
     net.backward()

@@ -23,7 +23,7 @@ def _rel(a, b):
 
 def test_fixtures_present():
     names = {os.path.basename(f)[:-4] for f in FILES}
-    assert {"tiny_b4", "tiny_b4_reg2e-4", "mnist_1step_b4", "celeba_b4"} <= names
+    assert {"tiny_b4", "tiny_b4_reg2e-4", "mnist_1step_b4", "celeba_b4", "lsun_b4"} <= names
 
 
 @pytest.mark.parametrize("path", FILES, ids=lambda p: os.path.basename(p)[:-4])

@@ -33,6 +33,7 @@ CASES = {
     "tiny_b4_reg2e-4": ("tiny", dict(batch=4), 2e-4),
     "mnist_1step_b4": ("mnist_1step", dict(batch=4), 1.0),
     "celeba_b4": ("celeba", dict(batch=4), 1.0),
+    "lsun_b4": ("lsun", dict(batch=4), 1.0),
 }
 SAMPLES = 512
 SMALL = 1024
