@@ -69,6 +69,7 @@ def lib():
         "svae_op_bn_act_bwd": ([vp, vp, vp, i64, i32, vp, vp, i32, vp, vp, vp, i64, vp], i32),
         "svae_op_fc": ([vp, i32, i32, vp, i32, vp, vp], i32),
         "svae_op_gather_bf16": ([vp, i32, i32, i32, vp, i32, i32, i32, i32, vp, vp, i64, vp], i32),
+        "svae_op_wgrad_bf16": ([vp, i32, i32, i32, vp, i32, i32, i32, i32, vp, vp, i64, vp], i32),
         "svae_probe_begin": ([vp, i32, i32], i32),
         "svae_probe_end": ([vp, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double),
                             ctypes.POINTER(ctypes.c_double)], i32),
@@ -86,7 +87,7 @@ EXPORTED = ["svae_param_count", "svae_param_layout", "svae_create", "svae_destro
             "svae_bind", "svae_workspace_bytes", "svae_forward", "svae_backward", "svae_adam", "svae_copy_out",
             "svae_op_conv", "svae_op_conv_dgrad", "svae_op_conv_wgrad", "svae_op_bn_act",
             "svae_op_bn_act_bwd", "svae_op_fc", "svae_probe_begin", "svae_probe_end", "svae_kernel_name",
-            "svae_op_gather_bf16"]
+            "svae_op_gather_bf16", "svae_op_wgrad_bf16"]
 
 # bf16 GEMM instance ids (csrc/kernels.h KernelId) for svae_probe_begin
 KID_IGEMM_BF16_256x32 = 2

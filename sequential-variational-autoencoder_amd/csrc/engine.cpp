@@ -307,6 +307,7 @@ struct Probe {
 
 struct svae_ctx {
   Probe probe;
+  int wg_path = 2;  // bf16 weight-GEMM: 0 tap-merged kernel only, 2 halo kernel where it qualifies
   Model m;
   std::string err;
   int device = 0;
@@ -558,6 +559,33 @@ static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, V
     w.g.Hi = w.g.Wi = L.hout;
     w.g.Ho = w.g.Wo = L.hin;
     w.rows = B * L.hin * L.hin;
+  }
+  if (c->m.g.bf16 && c->wg_path != 0 && wgrad_halo_enabled()) {
+    WHaloPlanOut pl;
+    if (wgrad_halo_plan(w, groups, &pl)) {
+      // pixel chunks split over blocks: ~1024 blocks in flight, slab within capacity
+      const long long per = 16LL * w.M * w.N;
+      // ~512 blocks, but >= 4 chunks per block: every split writes a full 16*M*N partial
+      long long ns = (512 + (long long)pl.tiles * groups - 1) / ((long long)pl.tiles * groups);
+      ns = std::min<long long>(ns, std::max<long long>(1, pl.h.nchunk / 4));
+      ns = std::min<long long>(ns, std::max<long long>(1, c->slab_cap / (per * groups)));
+      w.nsplit = (int)std::max<long long>(1, ns);
+      if (w.nsplit == 1) {
+        w.part = dW;
+        w.p_gs = w_gs;
+      } else {
+        w.part = c->slab;
+        w.p_gs = (long long)w.nsplit * per;
+      }
+      hipEvent_t* ev = nullptr;
+      if (c->probe.kid != KID_NONE)
+        ev = probe_pair(c, w.g.stride == 1 ? KID_WHALO_32_S1 : KID_WHALO_32_S2,
+                        2.0 * 16 * (double)w.M * w.N * w.rows * groups);
+      wgrad_halo(pl, w, groups, c->st, ev ? ev[1] : nullptr);
+      if (w.nsplit > 1)
+        wgrad_reduce(c->slab, w.p_gs, w.nsplit, 16, w.M, w.N, dW, w_gs, w.M, nullptr, 0, 0, groups, c->st);
+      return 0;
+    }
   }
   if (c->m.g.bf16)  // tap-merged tiles; longer splits (less slab traffic)
     choose_split(w.rows, 1, wgrad_bf16_tiles(w), groups, 16LL * w.M * w.N, c->slab_cap, w.nsplit, w.chunk, 2048,
@@ -1426,6 +1454,26 @@ int svae_op_gather_bf16(const float* x, int n, int h, int cin, const void* w_nk,
   a.part_cap = scratch ? scratch_bytes / (int64_t)sizeof(float) : 0;
   if (igemm_bf16_path(a, 1, path, (hipStream_t)stream) < 0)
     return fail(nullptr, SVAE_EBADARG, "shape does not qualify for the halo-tile kernel");
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(nullptr, SVAE_EHIP, hipGetErrorString(e));
+}
+
+int svae_op_wgrad_bf16(const float* x, int n, int h, int cin, const float* dy, int cout, int stride, int transpose,
+                       int path, float* dw, void* scratch, int64_t scratch_bytes, void* stream) {
+  if (!x || !dy || !dw || !scratch || (path != 0 && path != 2)) return fail(nullptr, SVAE_EBADARG, "bad op args");
+  static svae_ctx dummy;
+  dummy.m.g.B = n;
+  dummy.m.g.bf16 = 1;
+  dummy.wg_path = path;
+  dummy.st = (hipStream_t)stream;
+  dummy.slab = (float*)scratch;
+  dummy.slab_cap = scratch_bytes / (int64_t)sizeof(float);
+  ConvL L;
+  L.cin = cin; L.cout = cout; L.stride = stride; L.hin = h; L.tr = transpose != 0;
+  L.hout = L.tr ? h * stride : h / stride;
+  const int r = conv_wgrad(&dummy, L, 1, 0, View{(float*)x, cin, 0}, dy, 0, dw);
+  dummy.m.g.bf16 = 0;
+  if (r) return fail(nullptr, r, dummy.err);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(nullptr, SVAE_EHIP, hipGetErrorString(e));
 }

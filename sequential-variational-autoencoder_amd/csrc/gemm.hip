@@ -480,39 +480,59 @@ __device__ __forceinline__ float* wred_dst(float* out0, long long o0_gs, int msp
 
 // out[tap][m][n] (= or +=) sum_sp part[group][sp][tap][m][n], summed in split order (deterministic).
 // VEC: 4 consecutive n per thread (N % 4 == 0), four independent partial sums over the splits.
-template <bool VEC>
-__global__ void wgrad_reduce_kernel(const float* part, long long p_gs, int nsplit, int ntap, int M, int N,
-                                    float* out0, long long o0_gs, int msplit, float* out1, long long o1_gs,
-                                    int accumulate) {
+// out[tap][m][n] (= or +=) sum_sp part[group][sp][tap][m][n].  A block is QB float4 columns x
+// SL split lanes (QB*SL = 256): split lane l sums splits l, l+SL, ... with two partial sums,
+// then the SL partials are combined in LDS in lane order -- a fixed order, so deterministic.
+template <int SL>
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* part, long long p_gs, int nsplit, int ntap,
+                                                           int M, int N, float* out0, long long o0_gs, int msplit,
+                                                           float* out1, long long o1_gs, int accumulate) {
+  constexpr int QB = 256 / SL;
+  __shared__ f32x4 red[SL][QB];
   const int group = blockIdx.y;
   const long long per = (long long)ntap * M * N;
-  const long long nq = VEC ? per / 4 : per;
-  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (long long)gridDim.x * blockDim.x) {
-    const long long i = VEC ? q * 4 : q;
+  const int ql = threadIdx.x % QB, sl = threadIdx.x / QB;
+  const long long q = (long long)blockIdx.x * QB + ql;
+  const bool ok = q * 4 < per;
+  const float* p = part + group * p_gs + (ok ? q * 4 : 0);
+  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
+  int sp = sl;
+  for (; sp + SL < nsplit; sp += 2 * SL) {
+    s0 += *(const f32x4*)(p + sp * per);
+    s1 += *(const f32x4*)(p + (sp + SL) * per);
+  }
+  if (sp < nsplit) s0 += *(const f32x4*)(p + sp * per);
+  red[sl][ql] = s0 + s1;
+  __syncthreads();
+  if (sl != 0 || !ok) return;
+  f32x4 s = red[0][ql];
+#pragma unroll
+  for (int l = 1; l < SL; ++l) s += red[l][ql];
+  const long long i = q * 4;
+  const int tap = (int)(i / ((long long)M * N));
+  const int rem = (int)(i - (long long)tap * M * N);
+  const int m = rem / N, n = rem - m * N;
+  float* dst = wred_dst(out0, o0_gs, msplit, out1, o1_gs, group, tap, M, m, N, n);
+  if (!dst) return;
+  if (accumulate) s += *(const f32x4*)dst;
+  *(f32x4*)dst = s;
+}
+
+__global__ void wgrad_reduce_scalar_kernel(const float* part, long long p_gs, int nsplit, int ntap, int M, int N,
+                                           float* out0, long long o0_gs, int msplit, float* out1, long long o1_gs,
+                                           int accumulate) {
+  const int group = blockIdx.y;
+  const long long per = (long long)ntap * M * N;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < per; i += (long long)gridDim.x * blockDim.x) {
     const float* p = part + group * p_gs + i;
+    float s = 0.f;
+    for (int sp = 0; sp < nsplit; ++sp) s += p[sp * per];
     const int tap = (int)(i / ((long long)M * N));
     const int rem = (int)(i - (long long)tap * M * N);
     const int m = rem / N, n = rem - m * N;
     float* dst = wred_dst(out0, o0_gs, msplit, out1, o1_gs, group, tap, M, m, N, n);
     if (!dst) continue;
-    if (VEC) {
-      f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0, s3 = s0;
-      int sp = 0;
-      for (; sp + 4 <= nsplit; sp += 4) {
-        s0 += *(const f32x4*)(p + (sp + 0) * per);
-        s1 += *(const f32x4*)(p + (sp + 1) * per);
-        s2 += *(const f32x4*)(p + (sp + 2) * per);
-        s3 += *(const f32x4*)(p + (sp + 3) * per);
-      }
-      for (; sp < nsplit; ++sp) s0 += *(const f32x4*)(p + sp * per);
-      f32x4 s = (s0 + s1) + (s2 + s3);
-      if (accumulate) s += *(const f32x4*)dst;
-      *(f32x4*)dst = s;
-    } else {
-      float s = 0.f;
-      for (int sp = 0; sp < nsplit; ++sp) s += p[sp * per];
-      *dst = accumulate ? *dst + s : s;
-    }
+    *dst = accumulate ? *dst + s : s;
   }
 }
 
@@ -577,12 +597,24 @@ void wgrad_reduce(const float* part, long long p_gs, int nsplit, int ntap, int M
                   int msplit, float* out1, long long o1_gs, int accumulate, int groups, hipStream_t s) {
   long long per = (long long)ntap * M * N;
   const bool vec = (N % 4 == 0) && (p_gs % 4 == 0) && (o0_gs % 4 == 0) && (o1_gs % 4 == 0);
-  const long long items = vec ? per / 4 : per;
-  int blocks = (int)std::min<long long>((items + 255) / 256, 8192);
-  if (vec)
-    hipLaunchKernelGGL(wgrad_reduce_kernel<true>, dim3(blocks, groups), dim3(256), 0, s, part, p_gs, nsplit, ntap, M,
+  if (!vec) {
+    int blocks = (int)std::min<long long>((per + 255) / 256, 8192);
+    hipLaunchKernelGGL(wgrad_reduce_scalar_kernel, dim3(blocks, groups), dim3(256), 0, s, part, p_gs, nsplit, ntap, M,
                        N, out0, o0_gs, msplit, out1, o1_gs, accumulate);
-  else
-    hipLaunchKernelGGL(wgrad_reduce_kernel<false>, dim3(blocks, groups), dim3(256), 0, s, part, p_gs, nsplit, ntap, M,
-                       N, out0, o0_gs, msplit, out1, o1_gs, accumulate);
+    return;
+  }
+  const long long nq = per / 4;
+  // split lanes: enough blocks to stream the slab at full bandwidth even for small outputs
+  int sl = 1;
+  while (sl < 64 && sl < nsplit && (nq * sl) / 256 * groups < 1024) sl *= 4;
+  const int qb = 256 / sl;
+  dim3 grid((unsigned)((nq + qb - 1) / qb), groups);
+#define WRED(SLV)                                                                                                    \
+  hipLaunchKernelGGL(wgrad_reduce_kernel<SLV>, grid, dim3(256), 0, s, part, p_gs, nsplit, ntap, M, N, out0, o0_gs, \
+                     msplit, out1, o1_gs, accumulate)
+  if (sl == 1) WRED(1);
+  else if (sl == 4) WRED(4);
+  else if (sl == 16) WRED(16);
+  else WRED(64);
+#undef WRED
 }

@@ -594,6 +594,166 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kernel(HaloArgs h) {
 }
 
 // ---------------------------------------------------------------------------
+// Halo weight-GEMM (conv / conv-T weight gradient, bf16 MFMA, gfx950 transposed LDS reads).
+//   dW[tap][m][n] = sum_p G[src(p, tap)][m] * D[p][n],  src = (y*s - pad + ky, x*s - pad + kx)
+// A block owns 32 G-channels x BN D-channels and all 16 taps (wave w: kernel row ky = w, kx 0..3)
+// and walks chunks of CP row-space pixels (whole image rows, or whole images).  Per chunk it
+// stages, once, the G input window those pixels touch (halo included) and the D rows, both
+// pixel-major bf16 exactly as they lie in HBM (no register transpose).  MFMA fragments need
+// K = pixels contiguous per channel: ds_read_b64_tr_b16 delivers 4 consecutive pixels of one
+// channel per lane, so every tap's A fragment is the window read at a pixel shift.
+//   G window pitch: 64 B (s = 1) / 96 B (s = 2) -> conflict-free transposed reads;
+//   D rows (BN = 64): 8-byte slot XOR 8 on pixel bit 1 -> conflict-free.
+// ---------------------------------------------------------------------------
+#define WH_WPI 12  // window items (4 channels each, 8 per pixel) per thread: npix*8 <= 256*WH_WPI
+#define WH_DPI 8   // D items per thread: CP*BN/4 <= 256*WH_DPI
+
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4i16 lds_tr16(const __bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(p));
+}
+__device__ __forceinline__ bf16x8 join_tr(v4i16 lo, v4i16 hi) {
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  v8i16 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int BN, int S>
+__global__ __launch_bounds__(256) void wgrad_halo_kernel(WHaloArgs h) {
+  constexpr int NS = BN / 32;              // 32-column MFMA subtiles
+  constexpr int GP = S == 1 ? 32 : 48;     // window pixel pitch (bf16)
+  extern __shared__ __attribute__((aligned(16))) __bf16 wsm[];
+  const WgArgs& a = h.w;
+  const ConvGeom& g = a.g;
+  __bf16* Gw = wsm;
+  __bf16* Dt = wsm + h.npix * GP;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int grp = lane >> 4, i16 = lane & 15, q = i16 >> 2, p4 = i16 & 3;
+  const BlockXYZ blk = xcd_block();
+  const int m0 = blk.x * 32, n0 = blk.y * BN;
+  const int split = blk.z % a.nsplit, group = blk.z / a.nsplit;
+  const float* G = a.G + group * a.g_gs;
+  const float* D = a.D + group * a.d_gs;
+  const int cbeg = (int)((long long)h.nchunk * split / a.nsplit);
+  const int cend = (int)((long long)h.nchunk * (split + 1) / a.nsplit);
+  const int per_img = g.Ho * g.Wo;
+
+  // window items: chunk-invariant relative offset (from the chunk's window origin) + row index
+  int wrel[WH_WPI], wpr[WH_WPI];
+#pragma unroll
+  for (int i = 0; i < WH_WPI; ++i) {
+    const int it = tid + 256 * i;
+    wrel[i] = 0;
+    wpr[i] = -1;  // -1: no item
+    if (it < h.npix * 8) {
+      const int pix = it >> 3, part = it & 7;
+      const int il = pix / (h.PR * h.PC);
+      const int r2 = pix - il * h.PR * h.PC;
+      const int pr = r2 / h.PC, pc = r2 - pr * h.PC;
+      const int ix = pc - g.pad;
+      wrel[i] = ((il * g.Hi + pr) * g.Wi + ix) * a.ldg + m0 + part * 4;
+      wpr[i] = (ix >= 0 && ix < g.Wi) ? pr : -2;  // -2: column outside the image (zero)
+    }
+  }
+
+  // per-lane fragment geometry: the 4 pixels of this lane's transposed read, per K step
+  f32x16 acc[4][NS];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NS; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int lgR = h.lgImgPix - h.lgWo;
+  for (int c = cbeg; c < cend; ++c) {
+    const int row0 = c * h.CP;
+    const int img0 = row0 / per_img;
+    const int ry0 = (row0 - img0 * per_img) >> h.lgWo;
+    const int iy0 = ry0 * S - g.pad;  // input row of window row 0
+    // ---- stage the G window (fp32 -> bf16, pixel-major) ----
+    const float* Gc = G + ((long long)img0 * g.Hi + iy0) * g.Wi * a.ldg;
+#pragma unroll
+    for (int i = 0; i < WH_WPI; ++i) {
+      if (wpr[i] == -1) continue;
+      const int it = tid + 256 * i;
+      const int iy = iy0 + wpr[i];
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (wpr[i] >= 0 && iy >= 0 && iy < g.Hi) v = *(const f32x4*)(Gc + wrel[i]);
+      *(bf16x4*)&Gw[(it >> 3) * GP + (it & 7) * 4] = __builtin_convertvector(v, bf16x4);
+    }
+    // ---- stage the D rows of the chunk ----
+    const float* Dc = D + (long long)row0 * a.ldd + n0;
+#pragma unroll
+    for (int i = 0; i < WH_DPI; ++i) {
+      const int it = tid + 256 * i;
+      if (it < h.CP * (BN / 4)) {
+        const int k = it / (BN / 4), slot = it - k * (BN / 4);
+        const f32x4 v = *(const f32x4*)(Dc + (long long)k * a.ldd + slot * 4);
+        const int sw = BN == 64 ? (slot ^ (((k >> 1) & 1) << 3)) : slot;
+        *(bf16x4*)&Dt[k * BN + sw * 4] = __builtin_convertvector(v, bf16x4);
+      }
+    }
+    __syncthreads();
+    // ---- K steps of 16 pixels ----
+    for (int kk = 0; kk < h.CP / 16; ++kk) {
+      int wp[2], kr[2];
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int k = kk * 16 + 8 * (grp >> 1) + 4 * r + q;
+        kr[r] = k;
+        const int il = k >> h.lgImgPix;
+        const int ry = (k >> h.lgWo) & ((1 << lgR) - 1);
+        const int rx = k & ((1 << h.lgWo) - 1);
+        wp[r] = (il * h.PR + ry * S) * h.PC + rx * S;
+      }
+      bf16x8 bfr[NS];
+#pragma unroll
+      for (int ns = 0; ns < NS; ++ns) {
+        v4i16 t[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          const int slot = ns * 8 + 4 * (grp & 1) + p4;
+          const int sw = BN == 64 ? (slot ^ (((kr[r] >> 1) & 1) << 3)) : slot;
+          t[r] = lds_tr16(&Dt[kr[r] * BN + sw * 4]);
+        }
+        bfr[ns] = join_tr(t[0], t[1]);
+      }
+      const int ch = 16 * (grp & 1) + 4 * p4;
+#pragma unroll
+      for (int kx = 0; kx < 4; ++kx) {
+        const int shift = wave * h.PC + kx;  // tap (ky = wave, kx)
+        const bf16x8 af = join_tr(lds_tr16(&Gw[(wp[0] + shift) * GP + ch]), lds_tr16(&Gw[(wp[1] + shift) * GP + ch]));
+#pragma unroll
+        for (int ns = 0; ns < NS; ++ns)
+          acc[kx][ns] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[ns], acc[kx][ns], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- partial dW[tap][m][n] of this split (or the gradient itself when nsplit == 1) ----
+  float* out = a.part + group * a.p_gs + (long long)split * 16 * a.M * a.N;
+#pragma unroll
+  for (int kx = 0; kx < 4; ++kx) {
+    const int tap = wave * 4 + kx;
+#pragma unroll
+    for (int ns = 0; ns < NS; ++ns) {
+      const int n = n0 + ns * 32 + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        out[((long long)tap * a.M + m) * a.N + n] = acc[kx][ns][r];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // weight-GEMM, bf16 MFMA, taps merged into M:  rows r = tap*M + m of
 //   part[split][r][n] = sum_{p in split} G[src(p, tap)][m] * D[p][n]
 // (small-channel layers fill all waves; one dY tile feeds every tap of the row tile)
@@ -1028,7 +1188,8 @@ const char* kernel_name(int kid) {
       "wgrad_bf16_kernel<128, 128, 2, 2, true>", "wgrad_bf16_kernel<128, 128, 2, 2, false>",
       "igemm_halo_kernel<256, 32, 4, 1>", "igemm_halo_kernel<128, 32, 4, 1>",
       "igemm_halo_kernel<128, 64, 2, 2>", "igemm_halo_kernel<64, 64, 2, 2>",
-      "igemm_halo_kernel<128, 128, 2, 2>", "igemm_halo_kernel<64, 128, 1, 4>"};
+      "igemm_halo_kernel<128, 128, 2, 2>", "igemm_halo_kernel<64, 128, 1, 4>",
+      "wgrad_halo_kernel<32, 1>", "wgrad_halo_kernel<32, 2>", "wgrad_halo_kernel<64, 1>", "wgrad_halo_kernel<64, 2>"};
   return (kid >= 0 && kid < KID_COUNT) ? names[kid] : "none";
 }
 
@@ -1122,6 +1283,78 @@ void wgrad_bf16(WgArgs a, int groups, hipStream_t s, hipEvent_t after) {
     case KID_WGRAD_BF16_128x32: launch_wg_bf16<128, 32, 4, 1>(a, groups, vec, s); break;
     case KID_WGRAD_BF16_128x64: launch_wg_bf16<128, 64, 2, 2>(a, groups, vec, s); break;
     default: launch_wg_bf16<128, 128, 2, 2>(a, groups, vec, s); break;
+  }
+  if (after) hipEventRecord(after, s);
+}
+
+// ---- halo weight-GEMM planner ----
+static int ilog2(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return (1 << l) == v ? l : -1;
+}
+
+int wgrad_halo_plan(const WgArgs& a, int groups, WHaloPlanOut* out) {
+  const ConvGeom& g = a.g;
+  if (g.mode != GM_CONV || g.ksz != 4 || a.ntap != 16 || (g.stride != 1 && g.stride != 2)) return 0;
+  if (a.M % 32 != 0 || a.N % 32 != 0 || a.ldg % 4 != 0 || a.ldd % 4 != 0) return 0;
+  const int lgWo = ilog2(g.Wo), per_img = g.Ho * g.Wo;
+  if (lgWo < 2 || ilog2(per_img) < 0 || g.Ho != g.Wo) return 0;
+  const int bn = 32;  // BN = 64 needs 128 accumulators per lane (1 wave/SIMD): not used
+  const int S = g.stride;
+  const int GP = S == 1 ? 32 : 48;
+  for (int CP = 128; CP >= 32; CP >>= 1) {
+    if (a.rows % CP != 0 || CP < g.Wo) continue;
+    WHaloArgs h;
+    h.CP = CP;
+    h.lgWo = lgWo;
+    if (CP <= per_img) {
+      h.R = CP / g.Wo;
+      h.img_per_ch = 1;
+      h.ch_per_img = per_img / CP;
+      h.lgImgPix = ilog2(CP);  // a chunk never spans images: image index term stays 0
+    } else {
+      h.R = g.Ho;
+      h.img_per_ch = CP / per_img;
+      h.ch_per_img = 0;
+      h.lgImgPix = ilog2(per_img);
+    }
+    h.PR = (h.R - 1) * S + 4;
+    h.PC = (g.Wo - 1) * S + 4;
+    h.npix = h.img_per_ch * h.PR * h.PC;
+    if (h.npix * 8 > 256 * WH_WPI || CP * bn / 4 > 256 * WH_DPI) continue;
+    const size_t lds = ((size_t)h.npix * GP + (size_t)CP * bn) * sizeof(__bf16);
+    if (lds > 64 * 1024) continue;
+    h.nchunk = a.rows / CP;
+    out->h = h;
+    out->bn = bn;
+    out->lds = lds;
+    out->tiles = (a.M / 32) * (a.N / bn);
+    return 1;
+  }
+  return 0;
+}
+
+static int wgrad_halo_disabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SVAE_NO_HALO");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v;
+}
+int wgrad_halo_enabled() { return !wgrad_halo_disabled(); }
+
+void wgrad_halo(const WHaloPlanOut& pl, const WgArgs& a, int groups, hipStream_t s, hipEvent_t after) {
+  WHaloArgs h = pl.h;
+  h.w = a;
+  dim3 grid(a.M / 32, a.N / pl.bn, groups * a.nsplit);
+  if (pl.bn == 32) {
+    if (a.g.stride == 1) hipLaunchKernelGGL((wgrad_halo_kernel<32, 1>), grid, dim3(256), pl.lds, s, h);
+    else hipLaunchKernelGGL((wgrad_halo_kernel<32, 2>), grid, dim3(256), pl.lds, s, h);
+  } else {
+    if (a.g.stride == 1) hipLaunchKernelGGL((wgrad_halo_kernel<64, 1>), grid, dim3(256), pl.lds, s, h);
+    else hipLaunchKernelGGL((wgrad_halo_kernel<64, 2>), grid, dim3(256), pl.lds, s, h);
   }
   if (after) hipEventRecord(after, s);
 }

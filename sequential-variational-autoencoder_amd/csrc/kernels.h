@@ -46,7 +46,8 @@ enum KernelId {
   KID_WGRAD_BF16_128x128 = 14, KID_WGRAD_BF16_128x128_SCALAR = 15,
   KID_HALO_256x32 = 16, KID_HALO_128x32 = 17, KID_HALO_128x64 = 18, KID_HALO_64x64 = 19,
   KID_HALO_128x128 = 20, KID_HALO_64x128 = 21,
-  KID_COUNT = 22
+  KID_WHALO_32_S1 = 22, KID_WHALO_32_S2 = 23, KID_WHALO_64_S1 = 24, KID_WHALO_64_S2 = 25,
+  KID_COUNT = 26
 };
 const char* kernel_name(int kid);
 int igemm_bf16_kid(const FwdArgs& a);
@@ -59,6 +60,25 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
 int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit);
 void wgrad_bf16(WgArgs a, int groups, hipStream_t s, hipEvent_t after = nullptr);  // taps merged into M (part [split][tap*M+m][n])
 int wgrad_bf16_tiles(const WgArgs& a);
+// halo weight-GEMM (csrc/gemm_bf16.hip): plan (0 = shape does not qualify) and launch.  The caller
+// chooses a.nsplit over pl.h.nchunk chunks and points a.part / a.p_gs at the slab or at dW.
+struct WHaloArgs {
+  WgArgs w;
+  int CP, lgWo, lgImgPix;  // chunk pixels, log2(Wo), log2(pixels per image within a chunk)
+  int R, PR, PC, npix;      // image rows per chunk (per image), window rows/cols per image, window pixels
+  int nchunk;               // chunks per group
+  int ch_per_img;           // chunks per image (0 when a chunk spans several images)
+  int img_per_ch;           // images per chunk (1 when chunks split an image)
+};
+struct WHaloPlanOut {
+  WHaloArgs h;
+  int bn;
+  size_t lds;
+  int tiles;
+};
+int wgrad_halo_plan(const WgArgs& a, int groups, WHaloPlanOut* out);
+int wgrad_halo_enabled();
+void wgrad_halo(const WHaloPlanOut& pl, const WgArgs& a, int groups, hipStream_t s, hipEvent_t after = nullptr);
 // bf16 weight shadows: wn = bf16(w) for [0,n); wt = per-tap transposes listed in tiles/offs
 void shadow_weights(const float* w, void* wn, void* wt, long long n, const void* tiles, int ntiles, const void* offs,
                     hipStream_t s);
