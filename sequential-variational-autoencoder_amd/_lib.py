@@ -97,6 +97,12 @@ KID_IGEMM_BF16_64x128 = 8
 KID_WGRAD_BF16_128x32 = 10
 KID_WGRAD_BF16_128x64 = 12
 KID_WGRAD_BF16_128x128 = 14
+KID_HALO_256x32 = 16
+KID_HALO_128x64 = 18
+KID_HALO_128x128 = 20
+KID_HALO_64x128 = 21
+KID_WHALO_32_S1 = 22
+KID_WHALO_32_S2 = 23
 
 
 def check(rc, ctx=None):

@@ -9,6 +9,10 @@
 #include "common.h"
 #include "kernels.h"
 
+// BN output before the activation; forward apply and the backward's act' test share this one
+// expression so the recomputed sign is bitwise the forward's (kinks: TF tie rules)
+__device__ __forceinline__ f32x4 bn_y(f32x4 x, f32x4 m, f32x4 is, f32x4 b) { return (x - m) * is + b; }
+
 #define FIN_COLS 16
 #define FIN_PARTS 16
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* part, long long part_gs, int nrb, int C,
@@ -80,7 +84,7 @@ __global__ void bn_apply_kernel(const float* pre, int ldp, long long pre_gs, lon
     const int c = (int)(i - r * Q) * 4;
     f32x4 x = *(const f32x4*)(pre + r * ldp + c);
     f32x4 m = *(const f32x4*)(mean + c), is = *(const f32x4*)(invstd + c), b = *(const f32x4*)(beta + c);
-    f32x4 y = (x - m) * is + b;
+    f32x4 y = bn_y(x, m, is, b);
     if (res) y += *(const f32x4*)(res + r * ldr + c);
 #pragma unroll
     for (int e = 0; e < 4; ++e) y[e] = act_f(y[e], act);
@@ -107,10 +111,11 @@ int bn_bwd_rowblocks(long long rows, int C) {
   return (int)((rows + BWD_RPB - 1) / BWD_RPB);
 }
 
+// y == nullptr: act' from the recomputed pre-activation bn_y(pre) (layers without a shortcut add)
 __global__ void bn_bwd_reduce_kernel(const float* dy, int lddy, long long dy_gs, const float* y, int ldy,
                                      long long y_gs, const float* pre, int ldp, long long pre_gs, long long rows,
-                                     int C, const float* mean, const float* invstd, long long ms_gs, int act,
-                                     float* part, long long part_gs) {
+                                     int C, const float* mean, const float* invstd, long long ms_gs, const float* beta,
+                                     long long beta_gs, int act, float* part, long long part_gs) {
   __shared__ f32x4 red[2][256];
   const int group = blockIdx.z;
   const int Q = C >> 2;
@@ -121,7 +126,7 @@ __global__ void bn_bwd_reduce_kernel(const float* dy, int lddy, long long dy_gs,
   const int q = blockIdx.x * QB + qi;
   const bool active = rl < RL && q < Q;
   dy += group * dy_gs;
-  y += group * y_gs;
+  if (y) y += group * y_gs;
   pre += group * pre_gs;
   mean += group * ms_gs;
   invstd += group * ms_gs;
@@ -129,12 +134,14 @@ __global__ void bn_bwd_reduce_kernel(const float* dy, int lddy, long long dy_gs,
   if (active) {
     const int c = q * 4;
     const f32x4 m = *(const f32x4*)(mean + c), is = *(const f32x4*)(invstd + c);
+    const f32x4 bb = y ? f32x4{0.f, 0.f, 0.f, 0.f} : *(const f32x4*)(beta + group * beta_gs + c);
     const long long r0 = (long long)blockIdx.y * BWD_RPB;
     const long long r1 = r0 + BWD_RPB < rows ? r0 + BWD_RPB : rows;
     for (long long r = r0 + rl; r < r1; r += RL) {
       f32x4 g = *(const f32x4*)(dy + r * lddy + c);
-      f32x4 yy = *(const f32x4*)(y + r * ldy + c);
-      f32x4 xh = (*(const f32x4*)(pre + r * ldp + c) - m) * is;
+      const f32x4 xp = *(const f32x4*)(pre + r * ldp + c);
+      f32x4 yy = y ? *(const f32x4*)(y + r * ldy + c) : bn_y(xp, m, is, bb);
+      f32x4 xh = (xp - m) * is;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float dz = g[e] * dact_from_y(yy[e], act);
@@ -159,25 +166,26 @@ __global__ void bn_bwd_reduce_kernel(const float* dy, int lddy, long long dy_gs,
 
 void bn_bwd_reduce(const float* dy, int lddy, long long dy_gs, const float* y, int ldy, long long y_gs,
                    const float* pre, int ldp, long long pre_gs, long long rows, int C, const float* mean,
-                   const float* invstd, long long ms_gs, int act, float* part, long long part_gs, int groups,
-                   hipStream_t s) {
+                   const float* invstd, long long ms_gs, const float* beta, long long beta_gs, int act, float* part,
+                   long long part_gs, int groups, hipStream_t s) {
   const int Q = C / 4;
   const int QB = Q < 16 ? Q : 16;
   dim3 grid((Q + QB - 1) / QB, bn_bwd_rowblocks(rows, C), groups);
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, grid, dim3(256), 0, s, dy, lddy, dy_gs, y, ldy, y_gs, pre, ldp, pre_gs,
-                     rows, C, mean, invstd, ms_gs, act, part, part_gs);
+                     rows, C, mean, invstd, ms_gs, beta, beta_gs, act, part, part_gs);
 }
 
 __global__ void bn_bwd_apply_kernel(const float* dy, int lddy, long long dy_gs, const float* y, int ldy,
                                     long long y_gs, const float* pre, int ldp, long long pre_gs, long long rows,
-                                    int C, const float* mean, const float* invstd, long long ms_gs, const float* ab,
-                                    long long ab_gs, int act, float* dpre, int lddp, long long dpre_gs, float* dres,
-                                    int ldres, long long dres_gs, int res_acc) {
+                                    int C, const float* mean, const float* invstd, long long ms_gs, const float* beta,
+                                    long long beta_gs, const float* ab, long long ab_gs, int act, float* dpre, int lddp,
+                                    long long dpre_gs, float* dres, int ldres, long long dres_gs, int res_acc) {
   const int group = blockIdx.y;
   const int Q = C >> 2;
   const long long total = rows * Q;
   dy += group * dy_gs;
-  y += group * y_gs;
+  if (y) y += group * y_gs;
+  else beta += group * beta_gs;
   pre += group * pre_gs;
   mean += group * ms_gs;
   invstd += group * ms_gs;
@@ -188,9 +196,11 @@ __global__ void bn_bwd_apply_kernel(const float* dy, int lddy, long long dy_gs, 
     const long long r = i / Q;
     const int c = (int)(i - r * Q) * 4;
     f32x4 g = *(const f32x4*)(dy + r * lddy + c);
-    f32x4 yy = *(const f32x4*)(y + r * ldy + c);
     f32x4 is = *(const f32x4*)(invstd + c);
-    f32x4 xh = (*(const f32x4*)(pre + r * ldp + c) - *(const f32x4*)(mean + c)) * is;
+    const f32x4 m = *(const f32x4*)(mean + c);
+    const f32x4 xp = *(const f32x4*)(pre + r * ldp + c);
+    f32x4 yy = y ? *(const f32x4*)(y + r * ldy + c) : bn_y(xp, m, is, *(const f32x4*)(beta + c));
+    f32x4 xh = (xp - m) * is;
     f32x4 a = *(const f32x4*)(ab + c), b = *(const f32x4*)(ab + C + c);
     f32x4 dz;
 #pragma unroll
@@ -205,10 +215,10 @@ __global__ void bn_bwd_apply_kernel(const float* dy, int lddy, long long dy_gs, 
 
 void bn_bwd_apply(const float* dy, int lddy, long long dy_gs, const float* y, int ldy, long long y_gs,
                   const float* pre, int ldp, long long pre_gs, long long rows, int C, const float* mean,
-                  const float* invstd, long long ms_gs, const float* ab, long long ab_gs, int act, float* dpre,
-                  int lddp, long long dpre_gs, float* dres, int ldres, long long dres_gs, int res_acc, int groups,
-                  hipStream_t s) {
+                  const float* invstd, long long ms_gs, const float* beta, long long beta_gs, const float* ab,
+                  long long ab_gs, int act, float* dpre, int lddp, long long dpre_gs, float* dres, int ldres,
+                  long long dres_gs, int res_acc, int groups, hipStream_t s) {
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_blocks(rows * (C / 4)), groups), dim3(256), 0, s, dy, lddy, dy_gs,
-                     y, ldy, y_gs, pre, ldp, pre_gs, rows, C, mean, invstd, ms_gs, ab, ab_gs, act, dpre, lddp,
-                     dpre_gs, dres, ldres, dres_gs, res_acc);
+                     y, ldy, y_gs, pre, ldp, pre_gs, rows, C, mean, invstd, ms_gs, beta, beta_gs, ab, ab_gs, act, dpre,
+                     lddp, dpre_gs, dres, ldres, dres_gs, res_acc);
 }

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -307,6 +308,16 @@ struct Probe {
 
 struct svae_ctx {
   Probe probe;
+  // ---- backward: weight gradients on a side stream (overlap the BN / dgrad chain) ----
+  static constexpr int NR = 3;  // dpre ring slots (generator / encoder layers)
+  bool side = false;
+  hipStream_t st2 = nullptr;
+  float* slab2 = nullptr;
+  float* dpre_ring[NR] = {};
+  float* idpre_ring[2] = {};
+  hipEvent_t ev_ready[NR] = {}, ev_free[NR] = {}, ev_iready[2] = {}, ev_ifree[2] = {};
+  hipEvent_t ev_da_ready = nullptr, ev_da_free = nullptr, ev_start = nullptr, ev_join = nullptr;
+  int ring_pos = 0, iring_pos = 0;
   int wg_path = 2;  // bf16 weight-GEMM: 0 tap-merged kernel only, 2 halo kernel where it qualifies
   Model m;
   std::string err;
@@ -449,6 +460,45 @@ static hipEvent_t* probe_pair(svae_ctx* c, int kid, double flops) {
   hipEvent_t* e = &p.ev[2 * p.used++];
   hipEventRecord(e[0], c->st);
   return e;
+}
+
+// ---- side-stream weight gradients ----
+// Next BN-backward output slot: the main stream first waits until the side stream has finished
+// the weight gradient that read the slot's previous contents.
+struct Slot {
+  float* p;
+  hipEvent_t ready, freed;
+};
+static Slot dpre_next(svae_ctx* c) {
+  if (!c->side) return Slot{c->dpre, nullptr, nullptr};
+  const int i = c->ring_pos;
+  c->ring_pos = (i + 1) % svae_ctx::NR;
+  hipStreamWaitEvent(c->st, c->ev_free[i], 0);
+  return Slot{c->dpre_ring[i], c->ev_ready[i], c->ev_free[i]};
+}
+static Slot idpre_next(svae_ctx* c) {
+  if (!c->side) return Slot{c->idpre, nullptr, nullptr};
+  const int i = c->iring_pos;
+  c->iring_pos = (i + 1) & 1;
+  hipStreamWaitEvent(c->st, c->ev_ifree[i], 0);
+  return Slot{c->idpre_ring[i], c->ev_iready[i], c->ev_ifree[i]};
+}
+// run fn (weight-gradient launches) on the side stream after everything enqueued so far on the
+// main stream; the side stream uses its own split slab
+template <class Fn>
+static int on_side(svae_ctx* c, hipEvent_t ready, hipEvent_t freed, Fn&& fn) {
+  if (!c->side || !ready) return fn();
+  hipEventRecord(ready, c->st);
+  hipStreamWaitEvent(c->st2, ready, 0);
+  hipStream_t s0 = c->st;
+  float* sl0 = c->slab;
+  c->st = c->st2;
+  c->slab = c->slab2;
+  const int r = fn();
+  c->st = s0;
+  c->slab = sl0;
+  hipEventRecord(freed, c->st2);
+  return r;
 }
 
 static int gemm(svae_ctx* c, FwdArgs a, int groups) {
@@ -657,11 +707,14 @@ static int bn_act_bwd(svae_ctx* c, int groups, long long rows, int C, View dy, V
   if ((long long)groups * nrb * 2 * C > c->part_cap) return fail(c, SVAE_EBADARG, "bn bwd scratch too small");
   if ((long long)groups * 2 * C > c->ab_cap) return fail(c, SVAE_EBADARG, "ab scratch too small");
   const long long pgs = (long long)nrb * 2 * C;
-  bn_bwd_reduce(dy.p, dy.ld, dy.gs, y.p, y.ld, y.gs, pre, ldp, pre_gs, rows, C, bn.mean, bn.invstd, bn_gs, act, c->part,
-                pgs, groups, c->st);
+  // without a shortcut add, act'(y) follows from the recomputed BN output: y is not read
+  const float* yp = (dres.p || !c->P) ? y.p : nullptr;  // (per-op entry: no beta, reads y)
+  const float* beta = c->P + beta_off;
+  bn_bwd_reduce(dy.p, dy.ld, dy.gs, yp, y.ld, y.gs, pre, ldp, pre_gs, rows, C, bn.mean, bn.invstd, bn_gs, beta, w_gs,
+                act, c->part, pgs, groups, c->st);
   bn_bwd_finalize(c->part, pgs, nrb, C, rows, c->ab, 2LL * C, c->Gr + beta_off, w_gs, groups, c->st);
-  bn_bwd_apply(dy.p, dy.ld, dy.gs, y.p, y.ld, y.gs, pre, ldp, pre_gs, rows, C, bn.mean, bn.invstd, bn_gs, c->ab, 2LL * C,
-               act, dpre, C, dpre_gs, dres.p, dres.ld, dres.gs, res_acc, groups, c->st);
+  bn_bwd_apply(dy.p, dy.ld, dy.gs, yp, y.ld, y.gs, pre, ldp, pre_gs, rows, C, bn.mean, bn.invstd, bn_gs, beta, w_gs,
+               c->ab, 2LL * C, act, dpre, C, dpre_gs, dres.p, dres.ld, dres.gs, res_acc, groups, c->st);
   return 0;
 }
 
@@ -693,11 +746,12 @@ static int fc_bn_fwd(svae_ctx* c, const FcL& f, View in, float* pre, BNS bn, Vie
 // dense backward: dy wrt post-act (view), y, pre -> grads; din (=) if non-null
 static int fc_bn_bwd(svae_ctx* c, const FcL& f, View in, View dy, View y, const float* pre, BNS bn, View din) {
   const int B = c->m.g.B;
-  int r = bn_act_bwd(c, 1, B, f.nout, dy, y, pre, 0, f.nout, bn, 0, f.obeta, 0, ACT_LRELU, c->dpre, 0, View{}, 0);
+  const Slot sl = dpre_next(c);
+  int r = bn_act_bwd(c, 1, B, f.nout, dy, y, pre, 0, f.nout, bn, 0, f.obeta, 0, ACT_LRELU, sl.p, 0, View{}, 0);
   if (r) return r;
   WgArgs w{};
   w.G = in.p; w.ldg = in.ld;
-  w.D = c->dpre; w.ldd = f.nout;
+  w.D = sl.p; w.ldd = f.nout;
   w.M = f.nin; w.N = f.nout;
   w.g.mode = GM_DENSE; w.g.nimg = B; w.g.ksz = 1; w.g.stride = 1;
   w.ntap = 1;
@@ -705,10 +759,13 @@ static int fc_bn_bwd(svae_ctx* c, const FcL& f, View in, View dy, View y, const 
   w.nsplit = 1;
   w.chunk = (B + 31) / 32 * 32;
   w.part = c->Gr + f.ow;  // single split over the batch rows: write dW [nin][nout] directly
-  wgemm(c, w, 1);
+  on_side(c, sl.ready, sl.freed, [&] {
+    wgemm(c, w, 1);
+    return 0;
+  });
   if (din.p) {
     FwdArgs a{};
-    a.A = c->dpre; a.lda = f.nout;
+    a.A = sl.p; a.lda = f.nout;
     a.B = c->P + f.ow; a.b_nk = 1; a.ldb = f.nout; a.b_tap = 0;
     a.C = din.p; a.ldc = din.ld;
     a.N = f.nin; a.Cin = f.nout;
@@ -875,6 +932,10 @@ static int engine_backward(svae_ctx* c) {
   int r;
 
   HIPCHK(c, hipMemsetAsync(c->dz, 0, (size_t)T * B * g.Dz * sizeof(float), st));
+  if (c->side) {  // the side stream starts after the forward (and anything before it)
+    hipEventRecord(c->ev_start, st);
+    hipStreamWaitEvent(c->st2, c->ev_start, 0);
+  }
   for (int t = T - 1; t >= 0; --t) {
     if (t < c->dbg_stop_step) return 0;  // debug: stop after step dbg_stop_step
     svae_ctx::StepBufs& s = c->sb[t];
@@ -887,6 +948,7 @@ static int engine_backward(svae_ctx* c) {
     float* dzt = c->dz + (long long)t * B * g.Dz;
 
     // ---- output + highway (:1720-1729)
+    if (c->side) hipStreamWaitEvent(st, c->ev_da_free, 0);  // previous step's output wgrad read da
     output_bwd(s.a_out, B, g.H * g.W, g.C, xprev, s.xhat, c->tgt_in, g.lo, g.hi, g.minh, g.maxh, rec_coef, dxin, c->da,
                dxout, st);
     {
@@ -905,10 +967,13 @@ static int engine_backward(svae_ctx* c) {
                      256);
       else
         choose_split(w.rows, 16, (F[1] + 127) / 128, 1, 16LL * M_out * F[1], c->slab_cap, w.nsplit, w.chunk);
-      w.part = c->slab;
-      wgemm(c, w, 1);
-      wgrad_reduce(c->slab, 0, w.nsplit, 16, M_out, F[1], c->Gr + G.owout, 0, g.C,
-                   t >= 1 ? c->Gr + G.owratio : nullptr, 0, 0, 1, st);
+      on_side(c, c->ev_da_ready, c->ev_da_free, [&] {
+        w.part = c->slab;
+        wgemm(c, w, 1);
+        wgrad_reduce(c->slab, 0, w.nsplit, 16, M_out, F[1], c->Gr + G.owout, 0, g.C,
+                     t >= 1 ? c->Gr + G.owratio : nullptr, 0, 0, 1, c->st);
+        return 0;
+      });
       colsum_small(c->da, C1, P0, M_out, c->part, c->Gr + G.obout, g.C, t >= 1 ? c->Gr + G.obratio : nullptr, st);
       // d cur = conv-T dgrad (CONV gather over da with the packed [tap][C+1][F1] weights as KN)
       FwdArgs a{};
@@ -929,13 +994,15 @@ static int engine_backward(svae_ctx* c) {
       const ConvL& l1 = G.s1[lvl];
       const ConvL& l2 = G.s2[lvl];
       // s1: relu(BN(convT_s1(cat)))
+      Slot sl = dpre_next(c);
       r = bn_act_bwd(c, 1, rows, Fl, View{dcur, Fl, 0}, View{s.s1_act[lvl], Fl, 0}, s.s1_pre[lvl], 0, Fl, s.s1_bn[lvl],
-                     0, l1.obeta, 0, ACT_RELU, c->dpre, 0, View{}, 0);
+                     0, l1.obeta, 0, ACT_RELU, sl.p, 0, View{}, 0);
       if (r) return r;
       if (t == c->dbg_stop_step && lvl == c->dbg_stop_lvl2) { c->dbg_last = dcur; return 0; }
-      r = conv_wgrad(c, l1, 1, 0, View{s.cat[lvl], 2 * Fl, 0}, c->dpre, 0, c->Gr + l1.ow);
+      r = on_side(c, sl.ready, sl.freed,
+                  [&] { return conv_wgrad(c, l1, 1, 0, View{s.cat[lvl], 2 * Fl, 0}, sl.p, 0, c->Gr + l1.ow); });
       if (r) return r;
-      r = conv_dgrad(c, l1, 1, 0, c->dpre, 0, View{c->dcat, 2 * Fl, 0}, 0);
+      r = conv_dgrad(c, l1, 1, 0, sl.p, 0, View{c->dcat, 2 * Fl, 0}, 0);
       if (r) return r;
       // latent half of the concat -> split_latent level lvl
       {
@@ -949,13 +1016,14 @@ static int engine_backward(svae_ctx* c) {
       }
       // s2: relu(BN(convT_s2(cur)) + enc_{lvl+1})
       View dres = t >= 1 ? View{c->denc[lvl], Fl, 0} : View{};
+      sl = dpre_next(c);
       r = bn_act_bwd(c, 1, rows, Fl, View{c->dcat, 2 * Fl, 0}, View{s.cat[lvl], 2 * Fl, 0}, s.s2_pre[lvl], 0, Fl,
-                     s.s2_bn[lvl], 0, l2.obeta, 0, ACT_RELU, c->dpre, 0, dres, 0);
+                     s.s2_bn[lvl], 0, l2.obeta, 0, ACT_RELU, sl.p, 0, dres, 0);
       if (r) return r;
       View in = lvl == L - 2 ? View{s.top_act, F[L], 0} : View{s.s1_act[lvl + 1], F[lvl + 2], 0};
-      r = conv_wgrad(c, l2, 1, 0, in, c->dpre, 0, c->Gr + l2.ow);
+      r = on_side(c, sl.ready, sl.freed, [&] { return conv_wgrad(c, l2, 1, 0, in, sl.p, 0, c->Gr + l2.ow); });
       if (r) return r;
-      r = conv_dgrad(c, l2, 1, 0, c->dpre, 0, View{dnext, in.ld, 0}, 0);
+      r = conv_dgrad(c, l2, 1, 0, sl.p, 0, View{dnext, in.ld, 0}, 0);
       if (r) return r;
       std::swap(dcur, dnext);
       if (t == c->dbg_stop_step && lvl == c->dbg_stop_lvl) return 0;
@@ -981,31 +1049,38 @@ static int engine_backward(svae_ctx* c) {
                     s.encfc_pre, s.enc_bn_fc, View{c->denc_c, nc, 0});
       if (r) return r;
       const long long rc = (long long)B * S[L] * S[L];
+      Slot sl = dpre_next(c);
       r = bn_act_bwd(c, 1, rc, F[L - 1], View{c->denc_c, F[L - 1], 0}, View{s.enc_c_act, F[L - 1], 0}, s.enc_c_pre, 0,
-                     F[L - 1], s.enc_bn_c, 0, E.c.obeta, 0, ACT_LRELU, c->dpre, 0, View{}, 0);
+                     F[L - 1], s.enc_bn_c, 0, E.c.obeta, 0, ACT_LRELU, sl.p, 0, View{}, 0);
       if (r) return r;
-      r = conv_wgrad(c, E.c, 1, 0, View{s.enc_act_b[L - 2], F[L - 1], 0}, c->dpre, 0, c->Gr + E.c.ow);
+      r = on_side(c, sl.ready, sl.freed, [&] {
+        return conv_wgrad(c, E.c, 1, 0, View{s.enc_act_b[L - 2], F[L - 1], 0}, sl.p, 0, c->Gr + E.c.ow);
+      });
       if (r) return r;
-      r = conv_dgrad(c, E.c, 1, 0, c->dpre, 0, View{c->denc[L - 2], F[L - 1], 0}, 1);
+      r = conv_dgrad(c, E.c, 1, 0, sl.p, 0, View{c->denc[L - 2], F[L - 1], 0}, 1);
       if (r) return r;
       for (int lvl = L - 2; lvl >= 0; --lvl) {
         const int Fl = F[lvl + 1];
         const long long rows = (long long)B * S[lvl + 1] * S[lvl + 1];
+        Slot sb = dpre_next(c);
         r = bn_act_bwd(c, 1, rows, Fl, View{c->denc[lvl], Fl, 0}, View{s.enc_act_b[lvl], Fl, 0}, s.enc_pre_b[lvl], 0,
-                       Fl, s.enc_bn_b[lvl], 0, E.b[lvl].obeta, 0, ACT_LRELU, c->dpre, 0, View{}, 0);
+                       Fl, s.enc_bn_b[lvl], 0, E.b[lvl].obeta, 0, ACT_LRELU, sb.p, 0, View{}, 0);
         if (r) return r;
-        r = conv_wgrad(c, E.b[lvl], 1, 0, View{s.enc_act_a[lvl], Fl, 0}, c->dpre, 0, c->Gr + E.b[lvl].ow);
+        r = on_side(c, sb.ready, sb.freed, [&] {
+          return conv_wgrad(c, E.b[lvl], 1, 0, View{s.enc_act_a[lvl], Fl, 0}, sb.p, 0, c->Gr + E.b[lvl].ow);
+        });
         if (r) return r;
-        r = conv_dgrad(c, E.b[lvl], 1, 0, c->dpre, 0, View{c->dcur, Fl, 0}, 0);
+        r = conv_dgrad(c, E.b[lvl], 1, 0, sb.p, 0, View{c->dcur, Fl, 0}, 0);
         if (r) return r;
+        Slot sa = dpre_next(c);
         r = bn_act_bwd(c, 1, rows, Fl, View{c->dcur, Fl, 0}, View{s.enc_act_a[lvl], Fl, 0}, s.enc_pre_a[lvl], 0, Fl,
-                       s.enc_bn_a[lvl], 0, E.a[lvl].obeta, 0, ACT_LRELU, c->dpre, 0, View{}, 0);
+                       s.enc_bn_a[lvl], 0, E.a[lvl].obeta, 0, ACT_LRELU, sa.p, 0, View{}, 0);
         if (r) return r;
         View in = lvl == 0 ? View{(float*)xprev, g.C, 0} : View{s.enc_act_b[lvl - 1], F[lvl], 0};
-        r = conv_wgrad(c, E.a[lvl], 1, 0, in, c->dpre, 0, c->Gr + E.a[lvl].ow);
+        r = on_side(c, sa.ready, sa.freed, [&] { return conv_wgrad(c, E.a[lvl], 1, 0, in, sa.p, 0, c->Gr + E.a[lvl].ow); });
         if (r) return r;
         View din = lvl == 0 ? View{dxout, g.C, 0} : View{c->denc[lvl - 1], F[lvl], 0};
-        r = conv_dgrad(c, E.a[lvl], 1, 0, c->dpre, 0, din, 1);
+        r = conv_dgrad(c, E.a[lvl], 1, 0, sa.p, 0, din, 1);
         if (r) return r;
       }
     }
@@ -1029,21 +1104,25 @@ static int engine_backward(svae_ctx* c) {
                 first ? 0 : 1, T, st);
       first = false;
     }
+    Slot sb = idpre_next(c);
     r = bn_act_bwd(c, T, rows, Fl, View{c->idb, Fl, gs}, View{c->inf_act_b[lvl], Fl, gs}, c->inf_pre_b[lvl], gs, Fl,
-                   c->inf_bn_b[lvl], Fl, I0.b[lvl].obeta, wg, ACT_LRELU, c->idpre, gs, View{}, 0);
+                   c->inf_bn_b[lvl], Fl, I0.b[lvl].obeta, wg, ACT_LRELU, sb.p, gs, View{}, 0);
     if (r) return r;
-    r = conv_wgrad(c, I0.b[lvl], T, wg, View{c->inf_act_a[lvl], Fl, gs}, c->idpre, gs, c->Gr + I0.b[lvl].ow);
+    r = on_side(c, sb.ready, sb.freed, [&] {
+      return conv_wgrad(c, I0.b[lvl], T, wg, View{c->inf_act_a[lvl], Fl, gs}, sb.p, gs, c->Gr + I0.b[lvl].ow);
+    });
     if (r) return r;
-    r = conv_dgrad(c, I0.b[lvl], T, wg, c->idpre, gs, View{c->ida, Fl, gs}, 0);
+    r = conv_dgrad(c, I0.b[lvl], T, wg, sb.p, gs, View{c->ida, Fl, gs}, 0);
     if (r) return r;
+    Slot sa = idpre_next(c);
     r = bn_act_bwd(c, T, rows, Fl, View{c->ida, Fl, gs}, View{c->inf_act_a[lvl], Fl, gs}, c->inf_pre_a[lvl], gs, Fl,
-                   c->inf_bn_a[lvl], Fl, I0.a[lvl].obeta, wg, ACT_LRELU, c->idpre, gs, View{}, 0);
+                   c->inf_bn_a[lvl], Fl, I0.a[lvl].obeta, wg, ACT_LRELU, sa.p, gs, View{}, 0);
     if (r) return r;
     View in = lvl == 0 ? View{(float*)c->x_in, g.C, 0} : View{c->inf_act_b[lvl - 1], F[lvl], c->inf_gs[lvl - 1]};
-    r = conv_wgrad(c, I0.a[lvl], T, wg, in, c->idpre, gs, c->Gr + I0.a[lvl].ow);
+    r = on_side(c, sa.ready, sa.freed, [&] { return conv_wgrad(c, I0.a[lvl], T, wg, in, sa.p, gs, c->Gr + I0.a[lvl].ow); });
     if (r) return r;
     if (lvl > 0) {
-      r = conv_dgrad(c, I0.a[lvl], T, wg, c->idpre, gs, View{c->idb, F[lvl], c->inf_gs[lvl - 1]}, 0);
+      r = conv_dgrad(c, I0.a[lvl], T, wg, sa.p, gs, View{c->idb, F[lvl], c->inf_gs[lvl - 1]}, 0);
       if (r) return r;
     }
   }
@@ -1138,6 +1217,7 @@ static bool plan(svae_ctx* c) {
   c->dcur = A(maxact);
   c->dnext = A(maxact);
   c->dpre = A(maxact);
+  for (int i = 0; i < svae_ctx::NR; ++i) c->dpre_ring[i] = A(maxact);
   c->dcat = A(maxact);
   c->dtop = A((long long)B * (F[L] + F[L + 1]));
   c->denc_c = A((long long)B * S[L] * S[L] * F[L - 1]);
@@ -1148,12 +1228,14 @@ static bool plan(svae_ctx* c) {
   c->idb = A((long long)T * max_inf);
   c->ida = A((long long)T * max_inf);
   c->idpre = A((long long)T * max_inf);
+  for (int i = 0; i < 2; ++i) c->idpre_ring[i] = A((long long)T * max_inf);
   c->part_cap = (long long)T * (maxact / 16 + 65536) + 8LL * 2 * (maxJ + 8192);
   c->part = A(c->part_cap);
   c->ab_cap = (long long)T * 2 * 65536;
   c->ab = A(c->ab_cap);
   c->slab_cap = 64LL << 20;
   c->slab = A(c->slab_cap);
+  c->slab2 = A(c->slab_cap);
   return true;
 }
 
@@ -1274,6 +1356,17 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
     hipMemcpy(c->offs_d, offs.data(), offs.size() * sizeof(long long), hipMemcpyHostToDevice);
   }
   hipHostMalloc((void**)&c->reg_host, 64 * sizeof(float), hipHostMallocDefault);
+  {
+    const char* ns = getenv("SVAE_NO_SIDE");
+    if (!(ns && ns[0] == '1')) {
+      bool ok = hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking) == hipSuccess;
+      auto mk = [&](hipEvent_t* ev) { ok = ok && hipEventCreateWithFlags(ev, hipEventDisableTiming) == hipSuccess; };
+      for (int i = 0; i < svae_ctx::NR; ++i) { mk(&c->ev_ready[i]); mk(&c->ev_free[i]); }
+      for (int i = 0; i < 2; ++i) { mk(&c->ev_iready[i]); mk(&c->ev_ifree[i]); }
+      mk(&c->ev_da_ready); mk(&c->ev_da_free); mk(&c->ev_start); mk(&c->ev_join);
+      c->side = ok;
+    }
+  }
   for (int i = 0; i < 64; ++i) c->reg_host[i] = 0.f;
   *out = c;
   return 0;
@@ -1281,6 +1374,20 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
 
 int svae_destroy(svae_ctx* c) {
   if (!c) return 0;
+  if (c->st2) {
+    hipStreamSynchronize(c->st2);
+    hipStreamDestroy(c->st2);
+  }
+  for (hipEvent_t ev : {c->ev_da_ready, c->ev_da_free, c->ev_start, c->ev_join})
+    if (ev) hipEventDestroy(ev);
+  for (int i = 0; i < svae_ctx::NR; ++i) {
+    if (c->ev_ready[i]) hipEventDestroy(c->ev_ready[i]);
+    if (c->ev_free[i]) hipEventDestroy(c->ev_free[i]);
+  }
+  for (int i = 0; i < 2; ++i) {
+    if (c->ev_iready[i]) hipEventDestroy(c->ev_iready[i]);
+    if (c->ev_ifree[i]) hipEventDestroy(c->ev_ifree[i]);
+  }
   for (hipEvent_t ev : c->probe.ev) hipEventDestroy(ev);
   if (c->arena) hipFree(c->arena);
   if (c->adam_m) hipFree(c->adam_m);
@@ -1363,6 +1470,10 @@ int svae_backward(svae_ctx* c, void* stream) {
   if (!c || !c->x_in) return fail(c, SVAE_EBADARG, "svae_forward must run first");
   c->st = (hipStream_t)stream;
   int r = engine_backward(c);
+  if (c->side) {  // join: the side stream's weight gradients are ordered before later caller work
+    hipEventRecord(c->ev_join, c->st2);
+    hipStreamWaitEvent(c->st, c->ev_join, 0);
+  }
   if (r) return r;
   HIPCHK(c, hipGetLastError());
   return 0;
@@ -1523,7 +1634,7 @@ int svae_op_bn_act(const float* x, int64_t rows, int c, const float* beta, int a
   fill_f32(zi, c, 0.f, s);
   fill_f32(zi + c, c, 1.f, s);
   // sum(x), sum(x^2) via the backward reducer with act=none, mean=0, invstd=1
-  bn_bwd_reduce(x, c, 0, x, c, 0, x, c, 0, rows, c, zi, zi + c, 0, ACT_NONE, part, 0, 1, s);
+  bn_bwd_reduce(x, c, 0, x, c, 0, x, c, 0, rows, c, zi, zi + c, 0, nullptr, 0, ACT_NONE, part, 0, 1, s);
   bn_finalize(part, 0, nrb, c, rows, 1e-3f, mean, invstd, 0, 1, s);
   bn_apply(x, c, 0, rows, c, mean, invstd, 0, beta, 0, nullptr, 0, 0, act, y, c, 0, 1, s);
   hipError_t e = hipGetLastError();

@@ -101,17 +101,17 @@ void bn_apply(const float* pre, int ldp, long long pre_gs, long long rows, int C
 int bn_bwd_rowblocks(long long rows, int C);
 void bn_bwd_reduce(const float* dy, int lddy, long long dy_gs, const float* y, int ldy, long long y_gs,
                    const float* pre, int ldp, long long pre_gs, long long rows, int C, const float* mean,
-                   const float* invstd, long long ms_gs, int act, float* part, long long part_gs, int groups,
-                   hipStream_t s);
+                   const float* invstd, long long ms_gs, const float* beta, long long beta_gs, int act, float* part,
+                   long long part_gs, int groups, hipStream_t s);
 // per-channel: a = sum(dz)/n, b = sum(dz*xhat)/n, dbeta = sum(dz)
 void bn_bwd_finalize(const float* part, long long part_gs, int nrb, int C, long long count, float* ab,
                      long long ab_gs, float* dbeta, long long dbeta_gs, int groups, hipStream_t s);
 // dpre = invstd*(dz - a - xhat*b); optional dres (+)= dz
 void bn_bwd_apply(const float* dy, int lddy, long long dy_gs, const float* y, int ldy, long long y_gs,
                   const float* pre, int ldp, long long pre_gs, long long rows, int C, const float* mean,
-                  const float* invstd, long long ms_gs, const float* ab, long long ab_gs, int act, float* dpre,
-                  int lddp, long long dpre_gs, float* dres, int ldres, long long dres_gs, int res_acc, int groups,
-                  hipStream_t s);
+                  const float* invstd, long long ms_gs, const float* beta, long long beta_gs, const float* ab,
+                  long long ab_gs, int act, float* dpre, int lddp, long long dpre_gs, float* dres, int ldres,
+                  long long dres_gs, int res_acc, int groups, hipStream_t s);
 
 // ---- split_latent FC(K=Dl) + BN over batch + lrelu, fused (sequential_vae.py:1801-1806) ----
 // out[n][j] written at out + n*o_n + (j / F)*ldo + (j % F)

@@ -14,7 +14,7 @@ from oracle import spec, weightgen
 
 def _header_symbols():
     txt = open(os.path.join(ROOT, "include", "svae_hip.h")).read()
-    return sorted(set(re.findall(r"\b(svae_[a-z_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(svae_[a-z0-9_]+)\s*\(", txt)))
 
 
 def test_library_exports_header_symbols(built_lib):
