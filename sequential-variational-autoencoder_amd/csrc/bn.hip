@@ -13,57 +13,79 @@
 // expression so the recomputed sign is bitwise the forward's (kinks: TF tie rules)
 __device__ __forceinline__ f32x4 bn_y(f32x4 x, f32x4 m, f32x4 is, f32x4 b) { return (x - m) * is + b; }
 
-#define FIN_COLS 16
-#define FIN_PARTS 16
+// partial rows are reduced by FIN_L lanes per channel quad (4 quads = 16 channels per block),
+// each lane summing its share in fp64, then a fixed-order LDS tree: deterministic, and short
+// serial chains (the kernel is latency-bound at these sizes)
+#define FIN_Q 4
+#define FIN_L 64
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* part, long long part_gs, int nrb, int C,
                                                           double count, float eps, float* mean, float* invstd,
                                                           long long ms_gs, int mode, float* dbeta,
                                                           long long dbeta_gs) {
   // mode 0: stats -> mean/invstd ; mode 1: bwd sums -> ab (mean slots), dbeta
-  __shared__ double red[2][FIN_PARTS][FIN_COLS];
+  __shared__ double red[2][FIN_L][FIN_Q * 4];
   const int group = blockIdx.y;
-  const int ci = threadIdx.x % FIN_COLS, pi = threadIdx.x / FIN_COLS;
-  const int c = blockIdx.x * FIN_COLS + ci;
+  const int qi = threadIdx.x % FIN_Q, li = threadIdx.x / FIN_Q;
+  const int c0 = (blockIdx.x * FIN_Q + qi) * 4;
   const float* P = part + group * part_gs;
-  double s = 0.0, q = 0.0;
-  if (c < C) {
-    for (int rb = pi; rb < nrb; rb += FIN_PARTS) {
-      s += (double)P[(long long)rb * 2 * C + c];
-      q += (double)P[(long long)rb * 2 * C + C + c];
+  double s[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
+  if (c0 < C) {
+    for (int rb = li; rb < nrb; rb += FIN_L) {
+      const f32x4 a = *(const f32x4*)(P + (long long)rb * 2 * C + c0);
+      const f32x4 b2 = *(const f32x4*)(P + (long long)rb * 2 * C + C + c0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s[e] += (double)a[e];
+        q[e] += (double)b2[e];
+      }
     }
   }
-  red[0][pi][ci] = s;
-  red[1][pi][ci] = q;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    red[0][li][qi * 4 + e] = s[e];
+    red[1][li][qi * 4 + e] = q[e];
+  }
   __syncthreads();
-  if (pi == 0 && c < C) {
-    for (int i = 1; i < FIN_PARTS; ++i) {
-      s += red[0][i][ci];
-      q += red[1][i][ci];
+  for (int w = FIN_L / 2; w > 0; w >>= 1) {
+    if (li < w) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        red[0][li][qi * 4 + e] += red[0][li + w][qi * 4 + e];
+        red[1][li][qi * 4 + e] += red[1][li + w][qi * 4 + e];
+      }
     }
-    if (mode == 0) {
-      double m = s / count;
-      double var = q / count - m * m;
-      if (var < 0.0) var = 0.0;
-      mean[group * ms_gs + c] = (float)m;
-      invstd[group * ms_gs + c] = (float)(1.0 / sqrt(var + (double)eps));
-    } else {
-      mean[group * ms_gs + c] = (float)(s / count);        // a = mean(dz)
-      mean[group * ms_gs + C + c] = (float)(q / count);    // b = mean(dz*xhat)
-      if (dbeta) dbeta[group * dbeta_gs + c] = (float)s;
+    __syncthreads();
+  }
+  if (li == 0 && c0 < C) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int cc = c0 + e;
+      const double ss = red[0][0][qi * 4 + e], qq = red[1][0][qi * 4 + e];
+      if (mode == 0) {
+        const double m = ss / count;
+        double var = qq / count - m * m;
+        if (var < 0.0) var = 0.0;
+        mean[group * ms_gs + cc] = (float)m;
+        invstd[group * ms_gs + cc] = (float)(1.0 / sqrt(var + (double)eps));
+      } else {
+        mean[group * ms_gs + cc] = (float)(ss / count);        // a = mean(dz)
+        mean[group * ms_gs + C + cc] = (float)(qq / count);    // b = mean(dz*xhat)
+        if (dbeta) dbeta[group * dbeta_gs + cc] = (float)ss;
+      }
     }
   }
 }
 
 void bn_finalize(const float* part, long long part_gs, int nrb, int C, long long count, float eps, float* mean,
                  float* invstd, long long ms_gs, int groups, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + FIN_COLS - 1) / FIN_COLS, groups), dim3(256), 0, s, part, part_gs, nrb, C,
-                     (double)count, eps, mean, invstd, ms_gs, 0, (float*)nullptr, 0LL);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 4 * FIN_Q - 1) / (4 * FIN_Q), groups), dim3(256), 0, s, part,
+                     part_gs, nrb, C, (double)count, eps, mean, invstd, ms_gs, 0, (float*)nullptr, 0LL);
 }
 
 void bn_bwd_finalize(const float* part, long long part_gs, int nrb, int C, long long count, float* ab, long long ab_gs,
                      float* dbeta, long long dbeta_gs, int groups, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + FIN_COLS - 1) / FIN_COLS, groups), dim3(256), 0, s, part, part_gs, nrb, C,
-                     (double)count, 0.f, ab, (float*)nullptr, ab_gs, 1, dbeta, dbeta_gs);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 4 * FIN_Q - 1) / (4 * FIN_Q), groups), dim3(256), 0, s, part,
+                     part_gs, nrb, C, (double)count, 0.f, ab, (float*)nullptr, ab_gs, 1, dbeta, dbeta_gs);
 }
 
 __global__ void bn_apply_kernel(const float* pre, int ldp, long long pre_gs, long long rows, int C,
@@ -137,6 +159,7 @@ __global__ void bn_bwd_reduce_kernel(const float* dy, int lddy, long long dy_gs,
     const f32x4 bb = y ? f32x4{0.f, 0.f, 0.f, 0.f} : *(const f32x4*)(beta + group * beta_gs + c);
     const long long r0 = (long long)blockIdx.y * BWD_RPB;
     const long long r1 = r0 + BWD_RPB < rows ? r0 + BWD_RPB : rows;
+#pragma unroll 4
     for (long long r = r0 + rl; r < r1; r += RL) {
       f32x4 g = *(const f32x4*)(dy + r * lddy + c);
       const f32x4 xp = *(const f32x4*)(pre + r * ldp + c);
