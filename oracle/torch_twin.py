@@ -98,8 +98,9 @@ class Twin:
 
     def _conv(self, x, w, s, transpose):
         fn = (lambda a, b: conv2d_t_same(a, b, s)) if transpose else (lambda a, b: conv2d_same(a, b, s))
-        # layer-0 input gradient (C <= 3 channels) runs on the fp32 small-N kernel
-        return self._op(fn, x, w, rd=not (not transpose and x.shape[1] <= 3))
+        # every conv / conv-T leg is a bf16 gather- or weight-GEMM (the layer-0 input gradient,
+        # N = image channels, included: bf16 halo gather)
+        return self._op(fn, x, w)
 
     def _cba(self, x, lay, s, act, transpose=False, residual=None):
         P = self.P
@@ -164,11 +165,12 @@ class Twin:
         lo, hi = cfg["range"]
         P = self.P
         oc = lambda a, b: conv2d_t_same(a, b, 2)
-        # output / ratio conv-T: fp32 small-N forward and input gradient, bf16 weight gradient
-        o = torch.sigmoid(self._op(oc, cur, P[st["out"]["w"]], rf=False, rd=False) + P[st["out"]["b"]].view(1, -1, 1, 1))
+        # output / ratio conv-T: bf16 forward (halo gather, N = C+1), fp32 input gradient (small-C
+        # gather over the 4-channel packed gradient), bf16 weight gradient
+        o = torch.sigmoid(self._op(oc, cur, P[st["out"]["w"]], rd=False) + P[st["out"]["b"]].view(1, -1, 1, 1))
         out = (hi - lo) * o + lo
         if encs is not None:
-            r = torch.sigmoid(self._op(oc, cur, P[st["ratio"]["w"]], rf=False, rd=False) +
+            r = torch.sigmoid(self._op(oc, cur, P[st["ratio"]["w"]], rd=False) +
                               P[st["ratio"]["b"]].view(1, -1, 1, 1))
             r = cfg["min_highway"] + (cfg["max_highway"] - cfg["min_highway"]) * r.expand(-1, cfg["C"], -1, -1)
             out = r * out + (1 - r) * encs[0]

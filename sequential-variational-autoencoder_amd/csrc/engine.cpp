@@ -318,6 +318,7 @@ struct svae_ctx {
   hipEvent_t ev_ready[NR] = {}, ev_free[NR] = {}, ev_iready[2] = {}, ev_ifree[2] = {};
   hipEvent_t ev_da_ready = nullptr, ev_da_free = nullptr, ev_start = nullptr, ev_join = nullptr;
   int ring_pos = 0, iring_pos = 0;
+  float* cs_part = nullptr;  // output-bias column-sum partials (side stream)
   int wg_path = 2;  // bf16 weight-GEMM: 0 tap-merged kernel only, 2 halo kernel where it qualifies
   Model m;
   std::string err;
@@ -352,6 +353,7 @@ struct svae_ctx {
     float *s2_pre[8], *cat[8], *s1_pre[8], *s1_act[8];
     BNS s2_bn[8], s1_bn[8];
     float *wpack, *a_out, *xhat, *rec_part, *rec_img, *stats;
+    void* wpack_h;  // bf16 copy of wpack (NK [tap][C+1][F1]) for the bf16 output conv-T
   };
   std::vector<StepBufs> sb;
   int out_nblk = 0;
@@ -662,6 +664,20 @@ static int conv_dgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, c
                       View din, int accumulate) {
   const int B = c->m.g.B;
   const float* W = c->P + L.ow;
+  if (L.cin % 4 != 0 && c->m.g.bf16 && L.cout % 32 == 0 && !L.tr) {
+    // layer-0 conv input gradient (N = image channels): bf16 halo gather (CONVT mode from dpre)
+    FwdArgs a{};
+    a.A = dpre; a.a_gs = dpre_gs; a.lda = L.cout;
+    a.Bh = shadowN(c, L.ow); a.b_nk = 1; a.ldb = L.cout; a.b_tap = (long long)L.cin * L.cout; a.b_gs = w_gs;
+    a.C = din.p; a.c_gs = din.gs; a.ldc = din.ld;
+    a.N = L.cin; a.Cin = L.cout;
+    a.g = ConvGeom{GM_CONVT, B, L.hout, L.hout, L.hin, L.hin, L.stride, 1, 4};
+    a.rows = L.stride == 2 ? B * (L.hin / 2) * (L.hin / 2) : B * L.hin * L.hin;
+    a.nclass = L.stride == 2 ? 4 : 1;
+    a.accumulate = accumulate;
+    gemm(c, a, groups);
+    return 0;
+  }
   if (L.cin % 4 != 0) {
     // layer-0 conv (Cin = image channels): small-N gather (CONVT mode from dpre)
     if (groups != 1) return fail(c, SVAE_EBADARG, "small-N dgrad is not batched");
@@ -906,8 +922,21 @@ static int engine_forward(svae_ctx* c) {
                                    (size_t)F1 * sizeof(float), (size_t)F1 * sizeof(float), 16, hipMemcpyDeviceToDevice,
                                    st));
       ConvGeom og{GM_CONVT, B, S[1], S[1], g.H, g.W, 2, 1, 4};
-      gconv_smalln(cur.p, F1, F1, s.wpack, C1, nullptr, 0, (long long)C1 * F1, 0, bpack, nullptr, og,
-                   (long long)B * g.H * g.W, s.a_out, C1, 0, st);
+      if (g.bf16) {  // bf16 halo gather-GEMM, N = C+1 of one 32-column tile, bias in the epilogue
+        shadow_weights(s.wpack, s.wpack_h, nullptr, 16LL * C1 * F1, nullptr, 0, nullptr, st);
+        FwdArgs a{};
+        a.A = cur.p; a.lda = F1;
+        a.Bh = s.wpack_h; a.b_nk = 1; a.ldb = F1; a.b_tap = (long long)C1 * F1;
+        a.C = s.a_out; a.ldc = C1;
+        a.N = C1; a.Cin = F1;
+        a.g = og;
+        a.rows = B * (g.H / 2) * (g.W / 2); a.nclass = 4;
+        a.bias = bpack;
+        gemm(c, a, 1);
+      } else {
+        gconv_smalln(cur.p, F1, F1, s.wpack, C1, nullptr, 0, (long long)C1 * F1, 0, bpack, nullptr, og,
+                     (long long)B * g.H * g.W, s.a_out, C1, 0, st);
+      }
       output_fwd(s.a_out, B, g.H * g.W, g.C, xprev, c->tgt_in, g.lo, g.hi, g.minh, g.maxh, s.xhat, s.rec_part,
                  c->out_nblk, st);
       loss_reduce(s.rec_part, c->out_nblk, c->kl_img + (long long)t * B, B, g.H * g.W * g.C, s.stats, s.rec_img, st);
@@ -972,9 +1001,11 @@ static int engine_backward(svae_ctx* c) {
         wgemm(c, w, 1);
         wgrad_reduce(c->slab, 0, w.nsplit, 16, M_out, F[1], c->Gr + G.owout, 0, g.C,
                      t >= 1 ? c->Gr + G.owratio : nullptr, 0, 0, 1, c->st);
+        // output / ratio bias gradients (own scratch: c->part belongs to the main stream's BN)
+        colsum_small(c->da, C1, P0, M_out, c->cs_part, c->Gr + G.obout, g.C, t >= 1 ? c->Gr + G.obratio : nullptr,
+                     c->st);
         return 0;
       });
-      colsum_small(c->da, C1, P0, M_out, c->part, c->Gr + G.obout, g.C, t >= 1 ? c->Gr + G.obratio : nullptr, st);
       // d cur = conv-T dgrad (CONV gather over da with the packed [tap][C+1][F1] weights as KN)
       FwdArgs a{};
       a.A = c->da; a.lda = C1;
@@ -1204,6 +1235,7 @@ static bool plan(svae_ctx* c) {
       maxact = std::max(maxact, 2 * n);
     }
     s.wpack = A(16LL * C1 * F[1] + 4);
+    s.wpack_h = A(8LL * C1 * F[1] + 4);
     s.a_out = A((long long)B * g.H * g.W * C1);
     s.xhat = A((long long)B * g.H * g.W * g.C);
     s.rec_part = A((long long)B * c->out_nblk);
@@ -1236,6 +1268,7 @@ static bool plan(svae_ctx* c) {
   c->slab_cap = 64LL << 20;
   c->slab = A(c->slab_cap);
   c->slab2 = A(c->slab_cap);
+  c->cs_part = A(64 * 1024);
   return true;
 }
 

@@ -459,8 +459,8 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kernel(HaloArgs h) {
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) {
     const int n = n0 + wn0 + tn * 32 + l32;
-    nok[tn] = (n0 + wn0 + tn * 32) < a.N;  // uniform per 32-column group (N % 32 == 0)
-    bptr[tn] = Bw + (long long)(nok[tn] ? n : 0) * a.ldb + 8 * hh;
+    nok[tn] = (n0 + wn0 + tn * 32) < a.N;  // uniform per 32-column group
+    bptr[tn] = Bw + (long long)((nok[tn] && n < a.N) ? n : 0) * a.ldb + 8 * hh;  // N < 32: clamp, discard
   }
   bf16x8 bq[P][TN][2];
   auto load_b = [&](int slot, int chunk, int t) {
@@ -530,7 +530,7 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kernel(HaloArgs h) {
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn) {
           const int n = n0 + wn0 + tn * 32 + l32;
-          if (nok[tn]) Pp[orow * a.N + n] = acc[tm][tn][r];
+          if (nok[tn] && n < a.N) Pp[orow * a.N + n] = acc[tm][tn][r];
         }
       }
     return;
@@ -550,7 +550,7 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kernel(HaloArgs h) {
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) {
         const int n = n0 + wn0 + tn * 32 + l32;
-        if (!nok[tn]) continue;
+        if (!nok[tn] || n >= a.N) continue;
         float v = acc[tm][tn][r];
         csum[tn] += v;
         csq[tn] += v * v;
@@ -1062,7 +1062,8 @@ struct HaloPlan {
 static HaloPlan halo_plan(const FwdArgs& a, int groups) {
   HaloPlan p;
   const ConvGeom& g = a.g;
-  if (g.mode == GM_DENSE || g.ksz != 4 || a.Cin % HALO_CK != 0 || !a.Bh || a.N % 32 != 0) return p;
+  // N: multiples of 32, or a single partial 32-column tile (the 3/4-channel image-space layers)
+  if (g.mode == GM_DENSE || g.ksz != 4 || a.Cin % HALO_CK != 0 || !a.Bh || (a.N % 32 != 0 && a.N > 32)) return p;
   const bool s2t = g.mode == GM_CONVT && g.stride == 2;
   const int Hr = s2t ? g.Ho / 2 : g.Ho, Wr = s2t ? g.Wo / 2 : g.Wo;
   const int sy = g.mode == GM_CONV ? g.stride : 1;
@@ -1106,7 +1107,7 @@ static HaloPlan halo_plan(const FwdArgs& a, int groups) {
     p.lds = lds;
     const int nchunk = a.Cin / HALO_CK;
     int ks = 1;
-    if (blocks < 512 && a.part) {
+    if (blocks < 512 && a.part && a.N % 4 == 0) {  // the split-K reduce works on column quads
       ks = (int)std::min<long long>((768 + blocks - 1) / blocks, 8);
       ks = std::min(ks, nchunk);
       const long long rows_total = (long long)a.rows * a.nclass;

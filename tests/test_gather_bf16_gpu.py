@@ -21,6 +21,8 @@ SHAPES = [
     (4, 16, 64, 32, 2, 1), (4, 32, 64, 32, 1, 1),
     # input-gradient launches: conv dgrad = conv-T gather, conv-T dgrad = conv gather
     (4, 16, 64, 32, 2, 1), (4, 8, 128, 256, 1, 0), (4, 32, 32, 64, 1, 0),
+    # image-space layers: output conv-T (N = C+1 = 4) and layer-0 input gradient (N = 3)
+    (4, 32, 32, 4, 2, 1), (4, 32, 32, 3, 2, 1),
 ]
 
 
