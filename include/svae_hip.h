@@ -90,6 +90,13 @@ int64_t svae_workspace_bytes(const svae_ctx* ctx);
 int svae_forward(svae_ctx* ctx, const float* x, const float* target, const float* eps, float reg_coeff,
                  void* stream);
 /* d self.loss / d every variable (sequential_vae.py:1273) into the bound gradient buffer. */
+/* Generative mode (sequential_vae.py:947-952 / :1025 / generate_mc_samples :1393-1428): run the
+ * unrolled generator chain on latents z [T,B,Dz] fp32 (device; NULL = N(0,1) drawn on device),
+ * without the recognition networks: x_0 = generator_first_step(z_0), x_t = generator(x_{t-1}, z_t),
+ * BatchNorm on the generated batch's statistics (training mode, as the reference's shared
+ * variables).  Outputs via svae_copy_out(SVAE_BUF_XHAT, t).  Invalidates the training forward
+ * state (svae_backward needs a new svae_forward). */
+int svae_generate(svae_ctx* ctx, const float* z, void* stream);
 int svae_backward(svae_ctx* ctx, void* stream);
 /* clip(+-clip) + TF Adam on the live region (sequential_vae.py:1274-1276); step >= 1. */
 int svae_adam(svae_ctx* ctx, float lr, int64_t step, float clip, void* stream);

@@ -198,6 +198,23 @@ def forward_backward(cfg, struct, params, x, target, eps, reg_coeff=1.0, want_gr
     return out
 
 
+def generate(cfg, struct, params, z):
+    """Generative mode (sequential_vae.py:947-952, :1025, :1070-1073): the generator chain on
+    given latents z [T,B,Dz] (N(0,1) at generation time, generate_mc_samples :1393-1428), no
+    recognition network, x_0 = generator_first_step(z_0), x_t = generator(x_{t-1}, z_t), the same
+    (reused) variables, BatchNorm in training mode on the generated batch.  Returns [x_hat_t]."""
+    tp = T.Tape()
+    P = {k: tp.leaf(v) for k, v in params.items()}
+    out, prev = [], None
+    for t in range(cfg["mc_steps"]):
+        st = struct[t]
+        zt = tp.leaf(np.asarray(z[t], np.float64))
+        xhat = generator_ladder(tp, P, cfg, st["generator"], prev, zt, st.get("encoder"))
+        out.append(xhat.v.copy())
+        prev = xhat
+    return out
+
+
 def adam_update(params, grads, m, v, step, lr=2e-4, clip=10.0, b1=0.9, b2=0.999, eps=1e-8):
     """clip_by_value(±10) (sequential_vae.py:1274-1275) + tf.train.AdamOptimizer
     (:1267,1276): lr_t = lr*sqrt(1-b2^t)/(1-b1^t); w -= lr_t*m/(sqrt(v)+eps)."""

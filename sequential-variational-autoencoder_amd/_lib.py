@@ -60,6 +60,7 @@ def lib():
         "svae_workspace_bytes": ([vp], i64),
         "svae_forward": ([vp, vp, vp, vp, f32, vp], i32),
         "svae_backward": ([vp, vp], i32),
+        "svae_generate": ([vp, vp, vp], i32),
         "svae_adam": ([vp, f32, i64, f32, vp], i32),
         "svae_copy_out": ([vp, i32, i32, vp, i64, vp], i32),
         "svae_op_conv": ([vp, i32, i32, i32, vp, i32, i32, i32, vp, vp], i32),
@@ -87,7 +88,7 @@ EXPORTED = ["svae_param_count", "svae_param_layout", "svae_create", "svae_destro
             "svae_bind", "svae_workspace_bytes", "svae_forward", "svae_backward", "svae_adam", "svae_copy_out",
             "svae_op_conv", "svae_op_conv_dgrad", "svae_op_conv_wgrad", "svae_op_bn_act",
             "svae_op_bn_act_bwd", "svae_op_fc", "svae_probe_begin", "svae_probe_end", "svae_kernel_name",
-            "svae_op_gather_bf16", "svae_op_wgrad_bf16"]
+            "svae_op_gather_bf16", "svae_op_wgrad_bf16", "svae_generate"]
 
 # bf16 GEMM instance ids (csrc/kernels.h KernelId) for svae_probe_begin
 KID_IGEMM_BF16_256x32 = 2

@@ -319,6 +319,8 @@ struct svae_ctx {
   hipEvent_t ev_da_ready = nullptr, ev_da_free = nullptr, ev_start = nullptr, ev_join = nullptr;
   int ring_pos = 0, iring_pos = 0;
   float* cs_part = nullptr;  // output-bias column-sum partials (side stream)
+  bool generative = false;   // svae_generate: chain on caller / prior latents, no recognition
+  float* zero_img = nullptr; // [B,H,W,C] zeros: reconstruction target of the generative chain
   int wg_path = 2;  // bf16 weight-GEMM: 0 tap-merged kernel only, 2 halo kernel where it qualifies
   Model m;
   std::string err;
@@ -807,6 +809,18 @@ static int engine_forward(svae_ctx* c) {
   int r;
 
   if (g.bf16) shadow_weights(c->P, c->wN, c->wT, M.n_live, c->tiles_d, c->ntiles, c->offs_d, st);
+  if (c->generative) {
+    // generative mode (sequential_vae.py:947-952, :1025 latent_generative = self.latents[t]):
+    // z_t comes from the caller (or N(0,1)), the recognition networks do not run
+    const long long n = (long long)T * B * g.Dz;
+    if (c->eps_in) {
+      HIPCHK(c, hipMemcpyAsync(c->z, c->eps_in, n * sizeof(float), hipMemcpyDeviceToDevice, st));
+    } else {
+      philox_normal(c->z, n, 0x6E6E6E6EULL, c->rng_offset, st);
+      c->rng_offset += (n + 3) / 4;
+    }
+    HIPCHK(c, hipMemsetAsync(c->kl_img, 0, (size_t)T * B * sizeof(float), st));
+  } else {
   // ---------------- recognition ladders, all steps batched (groups = T) ----------------
   HIPCHK(c, hipMemsetAsync(c->head_part, 0, (size_t)T * c->head_nsplit * B * 2 * g.Dz * sizeof(float), st));
   for (int lvl = 0; lvl < L - 1; ++lvl) {
@@ -847,6 +861,7 @@ static int engine_forward(svae_ctx* c) {
     latent_fwd(c->head_part, (long long)c->head_nsplit * B * 2 * g.Dz, c->head_nsplit, B, g.Dz, lv, wg, g.clipv, g.prior,
                eps, ms, c->mu, c->sig, c->z, ms, c->kl_img, B, T, st);
   }
+  }  // !generative
 
   // ---------------- the chain ----------------
   for (int t = 0; t < T; ++t) {
@@ -1269,6 +1284,7 @@ static bool plan(svae_ctx* c) {
   c->slab = A(c->slab_cap);
   c->slab2 = A(c->slab_cap);
   c->cs_part = A(64 * 1024);
+  c->zero_img = A((long long)B * g.H * g.W * g.C);
   return true;
 }
 
@@ -1494,6 +1510,22 @@ int svae_forward(svae_ctx* c, const float* x, const float* target, const float* 
   const Geo& g = c->m.g;
   for (int t = 0; t < g.T; ++t) c->reg_host[t] = reg_coeff * (t == 0 ? g.c_first : 1.f) / (float)g.B;
   int r = engine_forward(c);
+  if (r) return r;
+  HIPCHK(c, hipGetLastError());
+  return 0;
+}
+
+int svae_generate(svae_ctx* c, const float* z, void* stream) {
+  if (!c || !c->P) return fail(c, SVAE_EBADARG, "svae_bind must run first");
+  const Geo& g = c->m.g;
+  c->st = (hipStream_t)stream;
+  HIPCHK(c, hipMemsetAsync(c->zero_img, 0, (size_t)g.B * g.H * g.W * g.C * sizeof(float), c->st));
+  c->generative = true;
+  c->x_in = nullptr;  // no training forward state: svae_backward is refused until svae_forward
+  c->tgt_in = c->zero_img;
+  c->eps_in = z;
+  const int r = engine_forward(c);
+  c->generative = false;
   if (r) return r;
   HIPCHK(c, hipGetLastError());
   return 0;

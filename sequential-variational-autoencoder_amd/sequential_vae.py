@@ -164,6 +164,28 @@ class SequentialVAE:
         final = float(self.copy_out(_lib.BUF_STEP_STATS, self.cfg.mc_steps - 1, 2)[0])
         return final / self.data_dims[0] / self.data_dims[1]
 
+    def generate(self, z=None, stream=None):
+        """Generator chain on latents z [T,B,Dz] (None: N(0,1) on device), no recognition network
+        (sequential_vae.py:947-952, :1025).  Returns [x_hat_t] device tensors [B,H,W,C]."""
+        e = None
+        if z is not None:
+            e = self._dev(z)
+            if tuple(e.shape) != (self.cfg.mc_steps, self.cfg.batch, self.cfg.latent_dim):
+                raise ValueError("z must be [T,B,Dz]")
+        self._keep = (e,)
+        _lib.check(self.L.svae_generate(self.ctx, _lib.ptr(e), _lib.stream_ptr(stream)), self.ctx)
+        return [self.xhat(t) for t in range(self.cfg.mc_steps)]
+
+    def generate_mc_samples(self, input_batch=None, batch_size=None):
+        """Reference generate_mc_samples (sequential_vae.py:1393-1428, add_noise_to_chain=False):
+        [x_0 ~ U[0,1) (the chain's unused initial sample, :947-949), x_hat_0, ..., x_hat_{T-1}]
+        as numpy arrays; latents N(0,1).  Only the batch size the context was built for is valid."""
+        bs = self.cfg.batch if batch_size is None else batch_size
+        if bs != self.cfg.batch:
+            raise ValueError("batch_size must equal the context batch (%d)" % self.cfg.batch)
+        x0 = torch.rand(bs, self.cfg.height, self.cfg.width, self.cfg.channels, device=self.device)
+        return [x0.cpu().numpy()] + [x.cpu().numpy() for x in self.generate()]
+
     def test(self, input_batch):
         """training_mles[-1] for the batch (sequential_vae.py:1381-1391; reg_coeff default 1.0)."""
         self.forward(input_batch, input_batch, None, 1.0)

@@ -35,6 +35,11 @@ CASES = {
     "celeba_b4": ("celeba", dict(batch=4), 1.0),
     "lsun_b4": ("lsun", dict(batch=4), 1.0),
 }
+# generative-mode fixtures (oracle.model.generate): z ~ N(0,1) PCG64 seed 2, [T,B,Dz]
+GEN_CASES = {
+    "gen_tiny_b4": ("tiny", dict(batch=4)),
+    "gen_mnist_1step_b4": ("mnist_1step", dict(batch=4)),
+}
 SAMPLES = 512
 SMALL = 1024
 
@@ -74,7 +79,19 @@ def make(name):
     print("%-18s loss=%.10f  %.1fs  %d KB" % (name, o["loss"], dt, os.path.getsize(path) // 1024))
 
 
+def make_gen(name):
+    preset, over = GEN_CASES[name]
+    cfg = spec.make_config(preset, **over)
+    table, struct, params = spec.init_params(cfg, seed=0, dtype=np.float32)
+    params = {k: v.astype(np.float64) for k, v in params.items()}
+    z = np.random.default_rng(2).standard_normal((cfg["mc_steps"], cfg["batch"], cfg["latent_dim"])).astype(np.float32)
+    xs = model.generate(cfg, struct, params, z)
+    path = os.path.join(OUT, name + ".npz")
+    np.savez_compressed(path, preset=np.array(preset), batch=np.int64(cfg["batch"]), z=z, xhat=np.stack(xs))
+    print("%-18s |x_T|=%.6f  %d KB" % (name, np.linalg.norm(xs[-1]), os.path.getsize(path) // 1024))
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
-    for n in (sys.argv[1:] or CASES):
-        make(n)
+    for n in (sys.argv[1:] or list(CASES) + list(GEN_CASES)):
+        (make_gen if n in GEN_CASES else make)(n)
