@@ -9,9 +9,14 @@
 #include "common.h"
 #include "kernels.h"
 
-// BN output before the activation; forward apply and the backward's act' test share this one
-// expression so the recomputed sign is bitwise the forward's (kinks: TF tie rules)
-__device__ __forceinline__ f32x4 bn_y(f32x4 x, f32x4 m, f32x4 is, f32x4 b) { return (x - m) * is + b; }
+// BN output before the activation, per element through common.h bn_y1 (one expression shared
+// by every kernel that needs it, so the backward's act' sign is bitwise the forward's)
+__device__ __forceinline__ f32x4 bn_y(f32x4 x, f32x4 m, f32x4 is, f32x4 b) {
+  f32x4 r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) r[e] = bn_y1(x[e], m[e], is[e], b[e]);
+  return r;
+}
 
 // partial rows are reduced by FIN_L lanes per channel quad (4 quads = 16 channels per block),
 // each lane summing its share in fp64, then a fixed-order LDS tree: deterministic, and short

@@ -83,6 +83,20 @@ __device__ __forceinline__ BlockXYZ xcd_block() {
   return b;
 }
 
+// BN output before the activation, (x - mean) * invstd + beta as one explicit fma: the forward
+// apply, the backward kernels and the fused GEMM epilogues all evaluate exactly this, so the
+// act'(y) sign recomputed in the backward is bitwise the forward's (TF tie rules at kinks)
+__device__ __forceinline__ float bn_y1(float x, float m, float is, float b) { return fmaf(x - m, is, b); }
+
+// the fused backward-BN epilogue term for one element of the final dy (see BwStat)
+__device__ __forceinline__ void bw_term(float v, float pre, float m, float is, float b, const float* y, int act,
+                                        float& sd, float& sx) {
+  const float yv = y ? *y : bn_y1(pre, m, is, b);
+  const float dz = v * dact_from_y(yv, act);
+  sd += dz;
+  sx += dz * ((pre - m) * is);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

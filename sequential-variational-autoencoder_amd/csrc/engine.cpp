@@ -662,8 +662,28 @@ static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, V
 }
 
 // input gradient of a conv/convT layer: din (+)= dgrad(dpre)
+// Fused backward-BN reduction: the input-gradient GEMM that is the LAST writer of a layer's dy
+// also emits that layer's (sum dz, sum dz*xhat) partials (BwStat epilogue, bf16 kernels), and
+// bn_act_bwd then skips bn_bwd_reduce (one full read of dy and pre less per layer).
+struct BwFuse {
+  BwStat bw{};
+  int nrb = 0;
+  bool used = false;
+};
+static BwFuse bw_fuse(svae_ctx* c, const float* pre, int ldp, long long pre_gs, const float* y, int ldy, long long y_gs,
+                      BNS bn, long long bn_gs, long long beta_off, long long w_gs, int act, int C) {
+  BwFuse f;
+  f.bw.pre = pre; f.bw.ldp = ldp; f.bw.pre_gs = pre_gs;
+  f.bw.y = y; f.bw.ldy = ldy; f.bw.y_gs = y_gs;
+  f.bw.mean = bn.mean; f.bw.invstd = bn.invstd; f.bw.ms_gs = bn_gs;
+  f.bw.beta = c->P + beta_off; f.bw.beta_gs = w_gs;
+  f.bw.act = act; f.bw.C = C;
+  return f;
+}
+
 static int conv_dgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, const float* dpre, long long dpre_gs,
-                      View din, int accumulate) {
+                      View din, int accumulate, BwFuse* fu = nullptr) {
+  if (fu) fu->used = false;
   const int B = c->m.g.B;
   const float* W = c->P + L.ow;
   if (L.cin % 4 != 0 && c->m.g.bf16 && L.cout % 32 == 0 && !L.tr) {
@@ -712,6 +732,22 @@ static int conv_dgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, c
   if (c->m.g.bf16 && c->wN) {  // NK bf16 [tap][ci][co]: conv -> N copy, conv-T -> T copy
     a.Bh = L.tr ? shadowT(c, L.ow) : shadowN(c, L.ow);
     a.ldb = L.cout;
+    static const int nofuse = [] {
+      const char* v = getenv("SVAE_NO_BWFUSE");
+      return (v && v[0] == '1') ? 1 : 0;
+    }();
+    if (fu && fu->bw.pre && fu->bw.C % 4 == 0 && !nofuse) {
+      a.bw = fu->bw;
+      const int nrb = gemm_nrb(c, a, groups);
+      if ((long long)groups * nrb * 2 * fu->bw.C <= c->part_cap) {
+        a.stats = c->part;
+        a.s_gs = (long long)nrb * 2 * fu->bw.C;
+        fu->nrb = nrb;
+        fu->used = true;
+      } else {
+        a.bw = BwStat{};
+      }
+    }
   }
   gemm(c, a, groups);
   return 0;
@@ -720,16 +756,18 @@ static int conv_dgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, c
 // BN(+act) backward: dy (grad wrt post-act out y) -> dpre; dbeta into grads; optional dres
 static int bn_act_bwd(svae_ctx* c, int groups, long long rows, int C, View dy, View y, const float* pre, long long pre_gs,
                       int ldp, BNS bn, long long bn_gs, long long beta_off, long long w_gs, int act, float* dpre,
-                      long long dpre_gs, View dres, int res_acc) {
-  const int nrb = bn_bwd_rowblocks(rows, C);
+                      long long dpre_gs, View dres, int res_acc, const BwFuse* fu = nullptr) {
+  const bool pre_reduced = fu && fu->used;  // partials already in c->part (fused dgrad epilogue)
+  const int nrb = pre_reduced ? fu->nrb : bn_bwd_rowblocks(rows, C);
   if ((long long)groups * nrb * 2 * C > c->part_cap) return fail(c, SVAE_EBADARG, "bn bwd scratch too small");
   if ((long long)groups * 2 * C > c->ab_cap) return fail(c, SVAE_EBADARG, "ab scratch too small");
   const long long pgs = (long long)nrb * 2 * C;
   // without a shortcut add, act'(y) follows from the recomputed BN output: y is not read
   const float* yp = (dres.p || !c->P) ? y.p : nullptr;  // (per-op entry: no beta, reads y)
   const float* beta = c->P + beta_off;
-  bn_bwd_reduce(dy.p, dy.ld, dy.gs, yp, y.ld, y.gs, pre, ldp, pre_gs, rows, C, bn.mean, bn.invstd, bn_gs, beta, w_gs,
-                act, c->part, pgs, groups, c->st);
+  if (!pre_reduced)
+    bn_bwd_reduce(dy.p, dy.ld, dy.gs, yp, y.ld, y.gs, pre, ldp, pre_gs, rows, C, bn.mean, bn.invstd, bn_gs, beta, w_gs,
+                  act, c->part, pgs, groups, c->st);
   bn_bwd_finalize(c->part, pgs, nrb, C, rows, c->ab, 2LL * C, c->Gr + beta_off, w_gs, groups, c->st);
   bn_bwd_apply(dy.p, dy.ld, dy.gs, yp, y.ld, y.gs, pre, ldp, pre_gs, rows, C, bn.mean, bn.invstd, bn_gs, beta, w_gs,
                c->ab, 2LL * C, act, dpre, C, dpre_gs, dres.p, dres.ld, dres.gs, res_acc, groups, c->st);
@@ -1034,6 +1072,7 @@ static int engine_backward(svae_ctx* c) {
     // ---- decoder levels, bottom-up (reverse of :1710-1717)
     float* dcur = c->dcur;
     float* dnext = c->dnext;
+    BwFuse fu_s1;  // s1[lvl]'s BN partials from the s2[lvl-1] input-gradient epilogue
     for (int lvl = 0; lvl <= L - 2; ++lvl) {
       const int Fl = F[lvl + 1];
       const long long rows = (long long)B * S[lvl + 1] * S[lvl + 1];
@@ -1042,13 +1081,16 @@ static int engine_backward(svae_ctx* c) {
       // s1: relu(BN(convT_s1(cat)))
       Slot sl = dpre_next(c);
       r = bn_act_bwd(c, 1, rows, Fl, View{dcur, Fl, 0}, View{s.s1_act[lvl], Fl, 0}, s.s1_pre[lvl], 0, Fl, s.s1_bn[lvl],
-                     0, l1.obeta, 0, ACT_RELU, sl.p, 0, View{}, 0);
+                     0, l1.obeta, 0, ACT_RELU, sl.p, 0, View{}, 0, &fu_s1);
       if (r) return r;
       if (t == c->dbg_stop_step && lvl == c->dbg_stop_lvl2) { c->dbg_last = dcur; return 0; }
       r = on_side(c, sl.ready, sl.freed,
                   [&] { return conv_wgrad(c, l1, 1, 0, View{s.cat[lvl], 2 * Fl, 0}, sl.p, 0, c->Gr + l1.ow); });
       if (r) return r;
-      r = conv_dgrad(c, l1, 1, 0, sl.p, 0, View{c->dcat, 2 * Fl, 0}, 0);
+      // s2[lvl]'s BN partials over the d-half of dcat (shortcut at t >= 1: act' from the stored y)
+      BwFuse fu_s2 = bw_fuse(c, s.s2_pre[lvl], Fl, 0, t >= 1 ? s.cat[lvl] : nullptr, 2 * Fl, 0, s.s2_bn[lvl], 0,
+                             l2.obeta, 0, ACT_RELU, Fl);
+      r = conv_dgrad(c, l1, 1, 0, sl.p, 0, View{c->dcat, 2 * Fl, 0}, 0, &fu_s2);
       if (r) return r;
       // latent half of the concat -> split_latent level lvl
       {
@@ -1064,12 +1106,18 @@ static int engine_backward(svae_ctx* c) {
       View dres = t >= 1 ? View{c->denc[lvl], Fl, 0} : View{};
       sl = dpre_next(c);
       r = bn_act_bwd(c, 1, rows, Fl, View{c->dcat, 2 * Fl, 0}, View{s.cat[lvl], 2 * Fl, 0}, s.s2_pre[lvl], 0, Fl,
-                     s.s2_bn[lvl], 0, l2.obeta, 0, ACT_RELU, sl.p, 0, dres, 0);
+                     s.s2_bn[lvl], 0, l2.obeta, 0, ACT_RELU, sl.p, 0, dres, 0, &fu_s2);
       if (r) return r;
       View in = lvl == L - 2 ? View{s.top_act, F[L], 0} : View{s.s1_act[lvl + 1], F[lvl + 2], 0};
       r = on_side(c, sl.ready, sl.freed, [&] { return conv_wgrad(c, l2, 1, 0, in, sl.p, 0, c->Gr + l2.ow); });
       if (r) return r;
-      r = conv_dgrad(c, l2, 1, 0, sl.p, 0, View{dnext, in.ld, 0}, 0);
+      if (lvl < L - 2) {  // next: s1[lvl+1] (no shortcut)
+        fu_s1 = bw_fuse(c, s.s1_pre[lvl + 1], F[lvl + 2], 0, nullptr, 0, 0, s.s1_bn[lvl + 1], 0, G.s1[lvl + 1].obeta, 0,
+                        ACT_RELU, F[lvl + 2]);
+        r = conv_dgrad(c, l2, 1, 0, sl.p, 0, View{dnext, in.ld, 0}, 0, &fu_s1);
+      } else {
+        r = conv_dgrad(c, l2, 1, 0, sl.p, 0, View{dnext, in.ld, 0}, 0);
+      }
       if (r) return r;
       std::swap(dcur, dnext);
       if (t == c->dbg_stop_step && lvl == c->dbg_stop_lvl) return 0;
@@ -1103,30 +1151,41 @@ static int engine_backward(svae_ctx* c) {
         return conv_wgrad(c, E.c, 1, 0, View{s.enc_act_b[L - 2], F[L - 1], 0}, sl.p, 0, c->Gr + E.c.ow);
       });
       if (r) return r;
-      r = conv_dgrad(c, E.c, 1, 0, sl.p, 0, View{c->denc[L - 2], F[L - 1], 0}, 1);
+      // E.c's input gradient accumulates last into denc[L-2] (after the decoder shortcut term)
+      BwFuse fu_eb = bw_fuse(c, s.enc_pre_b[L - 2], F[L - 1], 0, nullptr, 0, 0, s.enc_bn_b[L - 2], 0, E.b[L - 2].obeta,
+                             0, ACT_LRELU, F[L - 1]);
+      r = conv_dgrad(c, E.c, 1, 0, sl.p, 0, View{c->denc[L - 2], F[L - 1], 0}, 1, &fu_eb);
       if (r) return r;
       for (int lvl = L - 2; lvl >= 0; --lvl) {
         const int Fl = F[lvl + 1];
         const long long rows = (long long)B * S[lvl + 1] * S[lvl + 1];
         Slot sb = dpre_next(c);
         r = bn_act_bwd(c, 1, rows, Fl, View{c->denc[lvl], Fl, 0}, View{s.enc_act_b[lvl], Fl, 0}, s.enc_pre_b[lvl], 0,
-                       Fl, s.enc_bn_b[lvl], 0, E.b[lvl].obeta, 0, ACT_LRELU, sb.p, 0, View{}, 0);
+                       Fl, s.enc_bn_b[lvl], 0, E.b[lvl].obeta, 0, ACT_LRELU, sb.p, 0, View{}, 0, &fu_eb);
         if (r) return r;
         r = on_side(c, sb.ready, sb.freed, [&] {
           return conv_wgrad(c, E.b[lvl], 1, 0, View{s.enc_act_a[lvl], Fl, 0}, sb.p, 0, c->Gr + E.b[lvl].ow);
         });
         if (r) return r;
-        r = conv_dgrad(c, E.b[lvl], 1, 0, sb.p, 0, View{c->dcur, Fl, 0}, 0);
+        BwFuse fu_ea = bw_fuse(c, s.enc_pre_a[lvl], Fl, 0, nullptr, 0, 0, s.enc_bn_a[lvl], 0, E.a[lvl].obeta, 0,
+                               ACT_LRELU, Fl);
+        r = conv_dgrad(c, E.b[lvl], 1, 0, sb.p, 0, View{c->dcur, Fl, 0}, 0, &fu_ea);
         if (r) return r;
         Slot sa = dpre_next(c);
         r = bn_act_bwd(c, 1, rows, Fl, View{c->dcur, Fl, 0}, View{s.enc_act_a[lvl], Fl, 0}, s.enc_pre_a[lvl], 0, Fl,
-                       s.enc_bn_a[lvl], 0, E.a[lvl].obeta, 0, ACT_LRELU, sa.p, 0, View{}, 0);
+                       s.enc_bn_a[lvl], 0, E.a[lvl].obeta, 0, ACT_LRELU, sa.p, 0, View{}, 0, &fu_ea);
         if (r) return r;
         View in = lvl == 0 ? View{(float*)xprev, g.C, 0} : View{s.enc_act_b[lvl - 1], F[lvl], 0};
         r = on_side(c, sa.ready, sa.freed, [&] { return conv_wgrad(c, E.a[lvl], 1, 0, in, sa.p, 0, c->Gr + E.a[lvl].ow); });
         if (r) return r;
         View din = lvl == 0 ? View{dxout, g.C, 0} : View{c->denc[lvl - 1], F[lvl], 0};
-        r = conv_dgrad(c, E.a[lvl], 1, 0, sa.p, 0, din, 1);
+        if (lvl > 0) {  // accumulates last into denc[lvl-1]: E.b[lvl-1]'s BN partials
+          fu_eb = bw_fuse(c, s.enc_pre_b[lvl - 1], F[lvl], 0, nullptr, 0, 0, s.enc_bn_b[lvl - 1], 0, E.b[lvl - 1].obeta,
+                          0, ACT_LRELU, F[lvl]);
+          r = conv_dgrad(c, E.a[lvl], 1, 0, sa.p, 0, din, 1, &fu_eb);
+        } else {
+          r = conv_dgrad(c, E.a[lvl], 1, 0, sa.p, 0, din, 1);
+        }
         if (r) return r;
       }
     }
@@ -1137,38 +1196,50 @@ static int engine_backward(svae_ctx* c) {
   latent_bwd(c->mu, c->sig, c->eps_used, c->dz, (long long)B * g.Dz, (long long)B * g.Dz, B, g.Dz, c->kl_coef, 1,
              g.prior, g.clipv, c->dhead, (long long)B * 2 * g.Dz, T, st);
   const InfStep& I0 = M.inf[0];
-  for (int lvl = L - 2; lvl >= 0; --lvl) {
-    const int Fl = F[lvl + 1];
-    const long long gs = c->inf_gs[lvl];
-    const long long rows = (long long)B * S[lvl + 1] * S[lvl + 1];
-    bool first = lvl == L - 2;
+  // heads of ladder level l -> idb (first write), l's own conv-a input gradient (level l+1) after them
+  auto heads_of = [&](int l) {
+    bool first = true;
     for (int hl = 0; hl < L; ++hl) {
       const HeadL& h = I0.head[hl];
-      if (h.src_level != lvl) continue;
-      heads_bwd(c->inf_act_b[lvl], gs, c->idb, gs, B, h.nin, c->P + h.owm, c->P + h.ows, wg, h.d, c->dhead,
+      if (h.src_level != l) continue;
+      const long long gl = c->inf_gs[l];
+      heads_bwd(c->inf_act_b[l], gl, c->idb, gl, B, h.nin, c->P + h.owm, c->P + h.ows, wg, h.d, c->dhead,
                 (long long)B * 2 * g.Dz, 2 * g.Dz, h.off, c->Gr + h.owm, c->Gr + h.ows, c->Gr + h.obm, c->Gr + h.obs,
                 first ? 0 : 1, T, st);
       first = false;
     }
+    return !first;  // wrote idb
+  };
+  BwFuse fu_ib;  // level lvl's conv-b BN partials from level lvl+1's conv-a input-gradient epilogue
+  for (int lvl = L - 2; lvl >= 0; --lvl) {
+    const int Fl = F[lvl + 1];
+    const long long gs = c->inf_gs[lvl];
+    const long long rows = (long long)B * S[lvl + 1] * S[lvl + 1];
+    if (lvl == L - 2) heads_of(lvl);
     Slot sb = idpre_next(c);
     r = bn_act_bwd(c, T, rows, Fl, View{c->idb, Fl, gs}, View{c->inf_act_b[lvl], Fl, gs}, c->inf_pre_b[lvl], gs, Fl,
-                   c->inf_bn_b[lvl], Fl, I0.b[lvl].obeta, wg, ACT_LRELU, sb.p, gs, View{}, 0);
+                   c->inf_bn_b[lvl], Fl, I0.b[lvl].obeta, wg, ACT_LRELU, sb.p, gs, View{}, 0, &fu_ib);
     if (r) return r;
     r = on_side(c, sb.ready, sb.freed, [&] {
       return conv_wgrad(c, I0.b[lvl], T, wg, View{c->inf_act_a[lvl], Fl, gs}, sb.p, gs, c->Gr + I0.b[lvl].ow);
     });
     if (r) return r;
-    r = conv_dgrad(c, I0.b[lvl], T, wg, sb.p, gs, View{c->ida, Fl, gs}, 0);
+    BwFuse fu_ia = bw_fuse(c, c->inf_pre_a[lvl], Fl, gs, nullptr, 0, 0, c->inf_bn_a[lvl], Fl, I0.a[lvl].obeta, wg,
+                           ACT_LRELU, Fl);
+    r = conv_dgrad(c, I0.b[lvl], T, wg, sb.p, gs, View{c->ida, Fl, gs}, 0, &fu_ia);
     if (r) return r;
     Slot sa = idpre_next(c);
     r = bn_act_bwd(c, T, rows, Fl, View{c->ida, Fl, gs}, View{c->inf_act_a[lvl], Fl, gs}, c->inf_pre_a[lvl], gs, Fl,
-                   c->inf_bn_a[lvl], Fl, I0.a[lvl].obeta, wg, ACT_LRELU, sa.p, gs, View{}, 0);
+                   c->inf_bn_a[lvl], Fl, I0.a[lvl].obeta, wg, ACT_LRELU, sa.p, gs, View{}, 0, &fu_ia);
     if (r) return r;
     View in = lvl == 0 ? View{(float*)c->x_in, g.C, 0} : View{c->inf_act_b[lvl - 1], F[lvl], c->inf_gs[lvl - 1]};
     r = on_side(c, sa.ready, sa.freed, [&] { return conv_wgrad(c, I0.a[lvl], T, wg, in, sa.p, gs, c->Gr + I0.a[lvl].ow); });
     if (r) return r;
     if (lvl > 0) {
-      r = conv_dgrad(c, I0.a[lvl], T, wg, sa.p, gs, View{c->idb, F[lvl], c->inf_gs[lvl - 1]}, 0);
+      const bool wrote = heads_of(lvl - 1);
+      fu_ib = bw_fuse(c, c->inf_pre_b[lvl - 1], F[lvl], c->inf_gs[lvl - 1], nullptr, 0, 0, c->inf_bn_b[lvl - 1], F[lvl],
+                      I0.b[lvl - 1].obeta, wg, ACT_LRELU, F[lvl]);
+      r = conv_dgrad(c, I0.a[lvl], T, wg, sa.p, gs, View{c->idb, F[lvl], c->inf_gs[lvl - 1]}, wrote ? 1 : 0, &fu_ib);
       if (r) return r;
     }
   }

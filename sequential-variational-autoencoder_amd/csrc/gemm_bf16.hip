@@ -268,6 +268,19 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
   float csum[TN], csq[TN];
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) { csum[tn] = 0.f; csq[tn] = 0.f; }
+  // fused backward-BN reductions (BwStat): per-column mean / invstd / beta of dy's BN layer
+  const bool bwm = a.bw.pre != nullptr;
+  float bwmean[TN], bwis[TN], bwb[TN];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    const int n = n0 + wn0 + tn * 32 + l32;
+    bwmean[tn] = bwis[tn] = bwb[tn] = 0.f;
+    if (bwm && n < a.bw.C) {
+      bwmean[tn] = a.bw.mean[group * a.bw.ms_gs + n];
+      bwis[tn] = a.bw.invstd[group * a.bw.ms_gs + n];
+      bwb[tn] = a.bw.y ? 0.f : a.bw.beta[group * a.bw.beta_gs + n];
+    }
+  }
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
 #pragma unroll
@@ -280,13 +293,18 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
         const int n = n0 + wn0 + tn * 32 + l32;
         if (n >= a.N) continue;
         float v = acc[tm][tn][r];
-        csum[tn] += v;
-        csq[tn] += v * v;
+        if (!bwm) {
+          csum[tn] += v;
+          csq[tn] += v * v;
+        }
         if (bias) v += bias[n];
         v = act_f(v, a.act);
         float* dst = Cp + orow * a.ldc + n;
         if (a.accumulate) v += *dst;
         *dst = v;
+        if (bwm && n < a.bw.C)
+          bw_term(v, a.bw.pre[group * a.bw.pre_gs + orow * a.bw.ldp + n], bwmean[tn], bwis[tn], bwb[tn],
+                  a.bw.y ? a.bw.y + group * a.bw.y_gs + orow * a.bw.ldy + n : nullptr, a.bw.act, csum[tn], csq[tn]);
       }
     }
   }
@@ -308,14 +326,15 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
     __syncthreads();
     if (tid < BN) {
       const int n = n0 + tid;
-      if (n < a.N) {
+      const int SC = bwm ? a.bw.C : a.N;  // stats columns (row-block stride 2*SC)
+      if (n < SC) {
         float s = 0.f, q = 0.f;
 #pragma unroll
         for (int w = 0; w < WM; ++w) { s += red[w * BN + tid]; q += red[WM * BN + w * BN + tid]; }
         const long long rb_idx = (long long)cls * gridDim.x + blk.x;  // ks == 1 here
-        float* st = a.stats + group * a.s_gs + rb_idx * 2 * a.N;
+        float* st = a.stats + group * a.s_gs + rb_idx * 2 * SC;
         st[n] = s;
-        st[a.N + n] = q;
+        st[SC + n] = q;
       }
     }
   }
@@ -541,6 +560,19 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kernel(HaloArgs h) {
   float csum[TN], csq[TN];
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) { csum[tn] = 0.f; csq[tn] = 0.f; }
+  // fused backward-BN reductions (BwStat): per-column mean / invstd / beta of dy's BN layer
+  const bool bwm = a.bw.pre != nullptr;
+  float bwmean[TN], bwis[TN], bwb[TN];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    const int n = n0 + wn0 + tn * 32 + l32;
+    bwmean[tn] = bwis[tn] = bwb[tn] = 0.f;
+    if (bwm && n < a.bw.C) {
+      bwmean[tn] = a.bw.mean[group * a.bw.ms_gs + n];
+      bwis[tn] = a.bw.invstd[group * a.bw.ms_gs + n];
+      bwb[tn] = a.bw.y ? 0.f : a.bw.beta[group * a.bw.beta_gs + n];
+    }
+  }
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
 #pragma unroll
@@ -552,13 +584,18 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kernel(HaloArgs h) {
         const int n = n0 + wn0 + tn * 32 + l32;
         if (!nok[tn] || n >= a.N) continue;
         float v = acc[tm][tn][r];
-        csum[tn] += v;
-        csq[tn] += v * v;
+        if (!bwm) {
+          csum[tn] += v;
+          csq[tn] += v * v;
+        }
         if (bias) v += bias[n];
         v = act_f(v, a.act);
         float* dst = Cp + orow * a.ldc + n;
         if (a.accumulate) v += *dst;
         *dst = v;
+        if (bwm && n < a.bw.C)
+          bw_term(v, a.bw.pre[group * a.bw.pre_gs + orow * a.bw.ldp + n], bwmean[tn], bwis[tn], bwb[tn],
+                  a.bw.y ? a.bw.y + group * a.bw.y_gs + orow * a.bw.ldy + n : nullptr, a.bw.act, csum[tn], csq[tn]);
       }
     }
   }
@@ -580,14 +617,15 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kernel(HaloArgs h) {
     __syncthreads();
     if (tid < BN) {
       const int n = n0 + tid;
-      if (n < a.N) {
+      const int SC = bwm ? a.bw.C : a.N;  // stats columns (row-block stride 2*SC)
+      if (n < SC) {
         float s = 0.f, q = 0.f;
 #pragma unroll
         for (int w = 0; w < WM; ++w) { s += red[w * BN + tid]; q += red[WM * BN + w * BN + tid]; }
         const long long rb_idx = (long long)cls * gridDim.x + blk.x;  // ks == 1 here
-        float* st = a.stats + group * a.s_gs + rb_idx * 2 * a.N;
+        float* st = a.stats + group * a.s_gs + rb_idx * 2 * SC;
         st[n] = s;
-        st[a.N + n] = q;
+        st[SC + n] = q;
       }
     }
   }
@@ -995,7 +1033,7 @@ __global__ __launch_bounds__(256) void shadow_t_kernel(const float* w, __bf16* o
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* part, int ks, int rows_total, int N,
                                                             float* C, long long c_gs, int ldc, const float* bias,
                                                             long long bias_gs, int act, int accumulate, float* stats,
-                                                            long long s_gs) {
+                                                            long long s_gs, BwStat bw) {
   __shared__ f32x4 red[2][256];
   const int group = blockIdx.z;
   const int qi = threadIdx.x & 15, rl = threadIdx.x >> 4;
@@ -1005,6 +1043,13 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* part, i
   float* Cg = C + group * c_gs;
   const float* bs = bias ? bias + group * bias_gs : nullptr;
   f32x4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
+  const bool bwq = bw.pre && n < bw.C;  // fused backward-BN terms on this column quad
+  f32x4 bm = {0.f, 0.f, 0.f, 0.f}, bi = bm, bb = bm;
+  if (bwq) {
+    bm = *(const f32x4*)(bw.mean + group * bw.ms_gs + n);
+    bi = *(const f32x4*)(bw.invstd + group * bw.ms_gs + n);
+    if (!bw.y) bb = *(const f32x4*)(bw.beta + group * bw.beta_gs + n);
+  }
   if (n < N) {
     const int r0 = blockIdx.y * SKR_ROWS;
     const int r1 = min(rows_total, r0 + SKR_ROWS);
@@ -1012,27 +1057,42 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* part, i
       f32x4 v = *(const f32x4*)(P + (long long)r * N + n);
 #pragma unroll 4
       for (int k = 1; k < ks; ++k) v += *(const f32x4*)(P + k * slab + (long long)r * N + n);
-      s1 += v;
-      s2 += v * v;
+      if (!bw.pre) {
+        s1 += v;
+        s2 += v * v;
+      }
       if (bs) v += *(const f32x4*)(bs + n);
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = act_f(v[e], act);
       f32x4* d = (f32x4*)(Cg + (long long)r * ldc + n);
-      *d = accumulate ? *d + v : v;
+      if (accumulate) v += *d;
+      *d = v;
+      if (bwq) {
+        const f32x4 pr = *(const f32x4*)(bw.pre + group * bw.pre_gs + (long long)r * bw.ldp + n);
+        const float* yr = bw.y ? bw.y + group * bw.y_gs + (long long)r * bw.ldy + n : nullptr;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float sd = s1[e], sx = s2[e];
+          bw_term(v[e], pr[e], bm[e], bi[e], bb[e], yr ? yr + e : nullptr, bw.act, sd, sx);
+          s1[e] = sd;
+          s2[e] = sx;
+        }
+      }
     }
   }
   if (!stats) return;
   red[0][threadIdx.x] = s1;
   red[1][threadIdx.x] = s2;
   __syncthreads();
-  if (rl == 0 && n < N) {
+  const int SC = bw.pre ? bw.C : N;  // stats columns (row-block stride 2*SC)
+  if (rl == 0 && n < SC) {
     for (int j = 1; j < 16; ++j) {
       s1 += red[0][j * 16 + qi];
       s2 += red[1][j * 16 + qi];
     }
-    float* st = stats + group * s_gs + (long long)blockIdx.y * 2 * N;
+    float* st = stats + group * s_gs + (long long)blockIdx.y * 2 * SC;
     *(f32x4*)(st + n) = s1;
-    *(f32x4*)(st + N + n) = s2;
+    *(f32x4*)(st + SC + n) = s2;
   }
 }
 
@@ -1237,7 +1297,7 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
       if (hp.ks > 1) {
         dim3 grid((a.N + 63) / 64, hp.nrb, groups);
         hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, s, a.part, hp.ks, a.rows_total, a.N, a.C, a.c_gs,
-                           a.ldc, a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs);
+                           a.ldc, a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs, a.bw);
       }
       return hp.nrb;
     }
@@ -1257,7 +1317,7 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
   if (ks > 1) {
     dim3 grid((a.N + 63) / 64, nrb, groups);
     hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, s, a.part, ks, a.rows_total, a.N, a.C, a.c_gs, a.ldc,
-                       a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs);
+                       a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs, a.bw);
   }
   return nrb;
 }

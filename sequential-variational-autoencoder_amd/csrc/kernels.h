@@ -2,6 +2,18 @@
 #pragma once
 #include "common.h"
 
+// Backward-BN reductions fused into the epilogue of the GEMM that produces dy (bf16 kernels):
+// with dz = dy * act'(y), the epilogue emits per-row-block partials [rb][2C] = (sum dz,
+// sum dz*xhat) over columns [0, C) of its final output (after accumulate) into FwdArgs::stats,
+// exactly what bn_bwd_reduce would write.  pre == nullptr: off.
+struct BwStat {
+  const float* pre; int ldp; long long pre_gs;
+  const float* y; int ldy; long long y_gs;      // shortcut layers: act' from the stored output
+  const float* mean; const float* invstd; long long ms_gs;
+  const float* beta; long long beta_gs;
+  int act, C;
+};
+
 // gather-GEMM  C[p][n] (+)= act(bias + sum_{tap,k} A[src(p,tap)][k] * B[tap][k|n][n|k])
 struct FwdArgs {
   const float* A; long long a_gs; int lda;
@@ -18,6 +30,7 @@ struct FwdArgs {
   int mtiles;   // filled by the launcher
   // split-K (bf16 path): fp32 partial slabs [ksplit][rows_total][N] + reduce/stats pass
   float* part; long long part_cap; int ksplit; int rows_total;
+  BwStat bw;    // bf16 kernels: backward-BN partials instead of forward stats (bw.pre != nullptr)
 };
 
 // weight-GEMM  part[split][tap][m][n] = sum_{p in split} G[src(p,tap)][m] * D[p][n]
