@@ -1129,9 +1129,9 @@ static HaloPlan halo_plan(const FwdArgs& a, int groups) {
   const int sy = g.mode == GM_CONV ? g.stride : 1;
   const int span = s2t ? 2 : 4;
   if (g.mode == GM_CONVT && g.stride > 2) return p;
-  // measured (tools/bench_gather.py): the window pays off on wide rows; deep 8x8 / 4x4 layers
-  // with long K stay on the per-tap kernel
-  if (!(Wr >= 16 || (s2t && Wr >= 8))) return p;
+  // measured (tools/bench_gather.py, profiles/r01_v10_gather_microbench.txt): the v2 kernel is
+  // faster than the per-tap kernel on every CelebA layer shape, 4x4 .. 32x32; only the LDS
+  // window capacity below excludes shapes
   const int bn = a.N <= 32 ? 32 : (a.N <= 64 ? 64 : 128);
   const int cands[2] = {bn == 32 ? 256 : 128, bn == 32 ? 128 : 64};
   const int per_img = Hr * Wr;

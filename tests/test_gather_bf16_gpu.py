@@ -28,12 +28,12 @@ SHAPES = [
 
 
 
+# shapes whose input window exceeds the halo kernel's LDS budget (csrc/gemm_bf16.hip halo_plan)
+NOT_HALO = set()
+
+
 def halo_eligible(shape):
-    """The planner's rule (csrc/gemm_bf16.hip halo_plan): row-space width >= 16, or >= 8 for
-    stride-2 conv-T parity classes; everything else stays on the per-tap kernel."""
-    n, h, cin, cout, s, tr = shape
-    wr = h if tr else h // s  # conv-T s2 class row space = input size
-    return wr >= 16 or (tr and s == 2 and wr >= 8)
+    return shape not in NOT_HALO
 
 
 def _bf(t):
