@@ -560,6 +560,7 @@ static void dispatch_fwd_nk(const FwdArgs& a, int groups, bool nk, bool sc, hipS
 
 int igemm_fwd_bm(const FwdArgs& a) {
   // must mirror the tile choice in igemm_fwd (stats partial row-block count)
+  if (smallc_ok(a, false)) return smallc_bm();  // smallc.hip pixel blocks
   int N = a.N;
   long long rows = (long long)a.rows * a.nclass;
   if (N <= 32) return 256;
@@ -569,6 +570,10 @@ int igemm_fwd_bm(const FwdArgs& a) {
 }
 
 void igemm_fwd(FwdArgs a, int groups, hipStream_t s) {
+  if (smallc_ok(a, false)) {
+    conv_smallc(a, groups, false, s);
+    return;
+  }
   const bool nk = a.b_nk != 0;
   const bool sc = (a.Cin % BK) != 0;
   const int bm = igemm_fwd_bm(a);

@@ -1211,14 +1211,8 @@ static int halo_disabled() {
   return v;
 }
 
-int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit) {
-  if (!halo_disabled()) {
-    const HaloPlan hp = halo_plan(a, groups);
-    if (hp.ok) {
-      if (ksplit) *ksplit = hp.ks;
-      return hp.nrb;
-    }
-  }
+// per-tap kernel (igemm_bf16_kernel) split-K and stats row-blocks
+static int pertap_plan(const FwdArgs& a, int groups, int* ksplit) {
   const int bm = bf16_bm(a), bn = bf16_bn(a);
   const long long blocks = (long long)((a.rows + bm - 1) / bm) * ((a.N + bn - 1) / bn) * a.nclass * groups;
   const int ntap = a.g.mode == GM_DENSE ? 1 : (a.g.mode == GM_CONVT && a.g.stride == 2 ? 4 : 16);
@@ -1235,6 +1229,21 @@ int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit) {
   if (ksplit) *ksplit = ks;
   if (ks == 1) return a.nclass * ((a.rows + bm - 1) / bm);
   return (int)(((long long)a.rows * a.nclass + SKR_ROWS - 1) / SKR_ROWS);
+}
+
+int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit) {
+  if (smallc_ok(a, true)) {
+    if (ksplit) *ksplit = 1;
+    return smallc_nrb(a);
+  }
+  if (!halo_disabled()) {
+    const HaloPlan hp = halo_plan(a, groups);
+    if (hp.ok) {
+      if (ksplit) *ksplit = hp.ks;
+      return hp.nrb;
+    }
+  }
+  return pertap_plan(a, groups, ksplit);
 }
 
 const char* kernel_name(int kid) {
@@ -1278,6 +1287,11 @@ int igemm_bf16(FwdArgs a, int groups, hipStream_t s, hipEvent_t after) {
 }
 
 int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t after) {
+  if (path == 2 && smallc_ok(a, true)) {
+    conv_smallc(a, groups, true, s);
+    if (after) hipEventRecord(after, s);
+    return smallc_nrb(a);
+  }
   if (path == 1 || (path == 2 && !halo_disabled())) {
     HaloPlan hp = halo_plan(a, groups);
     if (!hp.ok && path == 1) return -1;
@@ -1304,7 +1318,7 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
   }
   const bool sc = (a.Cin % BKB) != 0;
   int ks = 1;
-  const int nrb = igemm_bf16_plan(a, groups, &ks);
+  const int nrb = pertap_plan(a, groups, &ks);
   a.ksplit = ks;
   a.rows_total = a.rows * a.nclass;
   switch (igemm_bf16_kid(a) & ~1) {

@@ -44,6 +44,13 @@ struct WgArgs {
 };
 
 int igemm_fwd_bm(const FwdArgs& a);
+// image-space stride-2 4x4 convs with Cin <= 4 (smallc.hip): eligibility, stats row-blocks
+// (smallc_bm() output pixels each) and launch; bf = the bf16 model (B = a.Bh, operands rounded)
+bool smallc_ok(const FwdArgs& a, bool bf);
+int smallc_nrb(const FwdArgs& a);
+int smallc_bm();
+bool smallc_disabled();  // SVAE_NO_SMALLC=1
+void conv_smallc(const FwdArgs& a, int groups, bool bf, hipStream_t s);
 // bf16-MFMA variants (dtype=1): A fp32 -> bf16 in staging, B = a.Bh bf16 [tap][n][k] (ldb = k pitch)
 // returns the number of stats row-blocks written to a.stats (plan: same value without launching)
 // Kernel-instance ids of the bf16 GEMMs (one per template instantiation = one rocprof kernel

@@ -1,0 +1,254 @@
+// Image-space stride-2 4x4 convolutions with few input channels (Cin <= 4): one MFMA
+// gather-GEMM per block over an LDS window of whole input rows.
+//
+//   * conv 0 of the recognition ladder and of every g_theta encoder step: conv2d of the image,
+//     Cin = C = 3 (abstract_network.py:18 conv2d_bn_lrelu; sequential_vae.py:1738,1766);
+//   * the output conv-T's input gradient: CONV gather over d[x_hat | ratio], Cin = C+1 = 4
+//     (the adjoint of abstract_network.py:37 conv2d_t, sequential_vae.py:1723-1729).
+//
+// The generic gather-GEMMs reach Cin % 32 != 0 through an element-wise gather with a tap decode
+// per element (igemm_fwd_kernel / igemm_bf16_kernel SMALLC): 60-80 us per launch for a 16.8 MB
+// output.  Here a block owns 256 consecutive output pixels = R = 256/Wo whole output rows of one
+// image, stages the (2R+2) x (Wi+2) input window once, channel-padded to 4 with zeros (TF SAME
+// padding and the missing channel), and runs K = 16 taps x 4 channels from it:
+//   BF   (bf16 model): 4 x v_mfma_f32_32x32x16_bf16 per 32x32 tile; lane h's 8 k values are
+//        taps (ky, 2h) and (ky, 2h+1) x 4 channels = ONE 16-byte LDS read.  Operands are
+//        RNE-rounded to bf16 exactly as the staging of the other bf16 gathers; B = the bf16
+//        shadow weights a.Bh [tap][n][k];
+//   fp32 (fp32 model, and the output conv-T input gradient in both): 32 x
+//        v_mfma_f32_32x32x2_f32 per tile (exact fp32 fma chains); in step (tap, s) lane h holds
+//        channel 2h+s, so one 8-byte LDS read feeds two MFMAs.
+// The epilogue is the generic one: optional bias, activation, accumulate, and the per-column
+// (sum, sum^2) BatchNorm partials of the block's 256 rows -> stats[rowblock = blockIdx.x].
+// 128-pixel blocks (twice the blocks in flight) measured the same step time (19.12 vs 19.17 ms,
+// 3 alternating bench pairs on one box), so the larger block with half the stats partials stays.
+#include <type_traits>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int SC_TM = 2;               // 32-pixel tiles per wave
+constexpr int SC_BM = 4 * 32 * SC_TM;  // output pixels per block (4 waves)
+
+template <int TN, int TM, bool BF>
+__global__ __launch_bounds__(256) void conv_smallc_kernel(FwdArgs a) {
+  constexpr int BM = 128 * TM;
+  // window: BF 8 B per pixel (4 x bf16), fp32 16 B per pixel; sized by the host (dynamic LDS)
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ float red[2][4][TN * 32];
+
+  const ConvGeom& g = a.g;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int group = blockIdx.z;
+  const int HWo = g.Ho * g.Wo;
+  const int p0 = blockIdx.x * BM;  // first output pixel (row space)
+  const int img = p0 / HWo;
+  const int oy0 = (p0 - img * HWo) / g.Wo;
+  const int R = BM / g.Wo;
+  const int WR = 2 * R + 2, WC = g.Wi + 2;
+  const int iy0 = 2 * oy0 - g.pad;
+
+  const float* A = a.A + group * a.a_gs + (long long)img * g.Hi * g.Wi * a.lda;
+
+  // ---- stage the window (rows iy0 .. iy0+WR-1, cols -1 .. Wi), 4 channels, zeros outside
+  for (int q = tid; q < WR * WC; q += 256) {
+    const int r = q / WC, col = q - r * WC;
+    const int iy = iy0 + r, ix = col - 1;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (iy >= 0 && iy < g.Hi && ix >= 0 && ix < g.Wi) {
+      const float* src = A + ((long long)iy * g.Wi + ix) * a.lda;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (c < a.Cin) v[c] = src[c];
+    }
+    if (BF) ((bf16x4*)smem)[q] = __builtin_convertvector(v, bf16x4);
+    else ((f32x4*)smem)[q] = v;
+  }
+
+  // ---- B fragments (registers, once per block)
+  const int N = a.N;
+  typedef typename std::conditional<BF, bf16x8, float>::type BFrag;
+  constexpr int KSTEPS = BF ? 4 : 32;
+  BFrag bfr[TN][KSTEPS];
+  if constexpr (BF) {
+    const __bf16* Bw = (const __bf16*)a.Bh + group * a.b_gs;
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int n = tn * 32 + l32;
+#pragma unroll
+      for (int j = 0; j < KSTEPS; ++j) {
+        bf16x8 w = {};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int tap = 4 * j + 2 * h + (e >> 2), c = e & 3;
+          if (c < a.Cin) w[e] = Bw[tap * a.b_tap + (long long)n * a.ldb + c];
+        }
+        bfr[tn][j] = w;
+      }
+    }
+  } else {
+    const float* Bw = a.B + group * a.b_gs;
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int n = tn * 32 + l32;
+#pragma unroll
+      for (int j = 0; j < KSTEPS; ++j) {
+        const int tap = j >> 1, c = 2 * h + (j & 1);
+        float w = 0.f;
+        if (c < a.Cin)
+          w = a.b_nk ? Bw[tap * a.b_tap + (long long)n * a.ldb + c] : Bw[tap * a.b_tap + (long long)c * a.ldb + n];
+        bfr[tn][j] = w;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- per-lane window base of its pixel in each tile: output (oy, ox) reads window row
+  //      2(oy-oy0)+ky, col 2ox+kx
+  int base[TM];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const int pi = p0 - img * HWo + 32 * (wave * TM + tm) + l32;
+    const int oy = pi / g.Wo, ox = pi - (pi / g.Wo) * g.Wo;
+    base[tm] = 2 * (oy - oy0) * WC + 2 * ox;
+  }
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[tm][tn][r] = 0.f;
+
+  if constexpr (BF) {
+    const bf16x4* Wb = (const bf16x4*)smem;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // ky = j; lane h: kx = 2h, 2h+1
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const bf16x8 av = *(const bf16x8*)&Wb[base[tm] + j * WC + 2 * h];
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bfr[tn][j], acc[tm][tn], 0, 0, 0);
+      }
+    }
+  } else {
+    const float* Wf = (const float*)smem;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int off = (t >> 2) * WC + (t & 3);
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const f32x2 av = *(const f32x2*)&Wf[(base[tm] + off) * 4 + 2 * h];
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[0], bfr[tn][2 * t], acc[tm][tn], 0, 0, 0);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[1], bfr[tn][2 * t + 1], acc[tm][tn], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // ---- epilogue
+  float* Cp = a.C + group * a.c_gs;
+  const float* bias = a.bias ? a.bias + group * a.bias_gs : nullptr;
+  float csum[TN], csq[TN];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) { csum[tn] = 0.f; csq[tn] = 0.f; }
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const long long m = p0 + 32 * (wave * TM + tm) + (r & 3) + 8 * (r >> 2) + 4 * h;
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int n = tn * 32 + l32;
+        float v = acc[tm][tn][r];
+        csum[tn] += v;
+        csq[tn] += v * v;
+        if (bias) v += bias[n];
+        v = act_f(v, a.act);
+        float* dst = Cp + m * a.ldc + n;
+        if (a.accumulate) v += *dst;
+        *dst = v;
+      }
+    }
+  }
+  if (a.stats) {
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      csum[tn] += __shfl_xor(csum[tn], 32, 64);
+      csq[tn] += __shfl_xor(csq[tn], 32, 64);
+      if (h == 0) {
+        red[0][wave][tn * 32 + l32] = csum[tn];
+        red[1][wave][tn * 32 + l32] = csq[tn];
+      }
+    }
+    __syncthreads();
+    if (tid < N) {
+      const float s = ((red[0][0][tid] + red[0][1][tid]) + red[0][2][tid]) + red[0][3][tid];
+      const float q = ((red[1][0][tid] + red[1][1][tid]) + red[1][2][tid]) + red[1][3][tid];
+      float* st = a.stats + group * a.s_gs + (long long)blockIdx.x * 2 * N;
+      st[tid] = s;
+      st[N + tid] = q;
+    }
+  }
+}
+
+int smallc_lds(const FwdArgs& a, bool bf) {
+  const int R = SC_BM / a.g.Wo;
+  return (2 * R + 2) * (a.g.Wi + 2) * (bf ? 8 : 16);
+}
+
+template <int TN, bool BF>
+void launch_smallc(const FwdArgs& a, int groups, hipStream_t s) {
+  dim3 grid(a.rows / SC_BM, 1, groups);
+  hipLaunchKernelGGL((conv_smallc_kernel<TN, SC_TM, BF>), grid, dim3(256), smallc_lds(a, BF), s, a);
+}
+
+}  // namespace
+
+bool smallc_ok(const FwdArgs& a, bool bf) {
+  const ConvGeom& g = a.g;
+  if (smallc_disabled()) return false;
+  if (g.mode != GM_CONV || g.ksz != 4 || g.stride != 2 || g.pad != 1 || a.nclass != 1) return false;
+  if (a.Cin < 1 || a.Cin > 4 || a.bw.pre) return false;
+  if (!(a.N == 32 || a.N == 64 || a.N == 128)) return false;
+  if (g.Hi != 2 * g.Ho || g.Wi != 2 * g.Wo || g.Wo > SC_BM || SC_BM % g.Wo) return false;
+  if ((g.Ho * g.Wo) % SC_BM || a.rows % SC_BM) return false;
+  if (bf ? !a.Bh : !a.B) return false;
+  return smallc_lds(a, bf) <= 64 * 1024;
+}
+
+int smallc_nrb(const FwdArgs& a) { return a.rows / SC_BM; }
+
+bool smallc_disabled() {
+  static const int off = [] {
+    const char* e = getenv("SVAE_NO_SMALLC");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return off != 0;
+}
+
+void conv_smallc(const FwdArgs& a, int groups, bool bf, hipStream_t s) {
+  if (bf) {
+    if (a.N == 32) launch_smallc<1, true>(a, groups, s);
+    else if (a.N == 64) launch_smallc<2, true>(a, groups, s);
+    else launch_smallc<4, true>(a, groups, s);
+  } else {
+    if (a.N == 32) launch_smallc<1, false>(a, groups, s);
+    else if (a.N == 64) launch_smallc<2, false>(a, groups, s);
+    else launch_smallc<4, false>(a, groups, s);
+  }
+}
+
+int smallc_bm() { return SC_BM; }

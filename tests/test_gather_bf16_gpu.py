@@ -3,7 +3,8 @@ conv / conv-T layer shape of the CelebA geometry (forward shapes; the input-grad
 launches are the same two gather modes).  Reference: float64 torch conv of the SAME
 bf16-rounded operands (oracle/torch_twin.py TF-SAME helpers), so the only difference left
 is fp32 accumulation order: bound 2e-5 relative (L2) and 1e-4 of max|ref| pointwise.
-Both kernels are checked: path 0 (per-tap gather) and path 1 (halo-tile window)."""
+Every kernel is checked: path 0 (per-tap gather), path 1 (halo-tile window) and path 2 (the
+default dispatch, which adds the small-channel window kernel of csrc/smallc.hip for Cin <= 4)."""
 import numpy as np
 import pytest
 import torch
@@ -23,6 +24,9 @@ SHAPES = [
     (4, 16, 64, 32, 2, 1), (4, 8, 128, 256, 1, 0), (4, 32, 32, 64, 1, 0),
     # image-space layers: output conv-T (N = C+1 = 4) and layer-0 input gradient (N = 3)
     (4, 32, 32, 4, 2, 1), (4, 32, 32, 3, 2, 1),
+    # small-channel convs (csrc/smallc.hip on path 2): layer-0 conv of the image (Cin = 3) at the
+    # CelebA / tiny geometries, 4 channels, N = 64 and 128 column tiles
+    (4, 64, 3, 32, 2, 0), (2, 32, 3, 32, 2, 0), (2, 64, 4, 64, 2, 0), (2, 32, 1, 128, 2, 0),
 ]
 
 
@@ -33,7 +37,7 @@ NOT_HALO = set()
 
 
 def halo_eligible(shape):
-    return shape not in NOT_HALO
+    return shape[2] % 32 == 0 and shape not in NOT_HALO
 
 
 def _bf(t):
@@ -42,7 +46,7 @@ def _bf(t):
 
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "n%d_h%d_%dto%d_s%d_%s" % (s[0], s[1], s[2], s[3], s[4],
                                                                                  "T" if s[5] else "C"))
-@pytest.mark.parametrize("path", [0, 1])
+@pytest.mark.parametrize("path", [0, 1, 2])
 def test_gather_bf16(shape, path):
     L = pkg_mod("_lib")
     n, h, cin, cout, s, tr = shape

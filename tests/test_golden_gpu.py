@@ -2,12 +2,14 @@
 (tests/golden/*.npz, fp64 oracle outputs; see tests/test_golden.py for how they are pinned).
 
 Bounds (BASELINE.json north_star: 1e-4 rel fp32 on ELBO and decoder output):
-  loss, per-step recon/KL, per-image ELBO   : 1e-4 rel              (every fixture)
+  loss, per-image ELBO                     : 1e-4 rel              (every fixture)
+  per-step recon / KL                      : 1e-4 rel              (tiny, MNIST)
   mu, sigma, x_hat samples / final x_hat   : 1e-4 rel  (tiny, MNIST)
   gradient norms (per tensor)              : median 1e-4, all-tensor vector 1e-3 (tiny, MNIST)
   full small gradients (<=1024 elems)      : vector 1e-3 (tiny, MNIST)
 CelebA / LSUN geometry (T=8, B=4): the random-init chain amplifies fp32 rounding ~2.5x per step
-(DESIGN.md §6), so every non-loss quantity is bounded by max(floor, 4 x the error of the
+(DESIGN.md §6), so every quantity but the loss and the per-image ELBO (per-step recon/KL
+included: the last steps carry the amplified error) is bounded by max(floor, 4 x the error of the
 fp32 PyTorch-CPU twin of the same graph on the same inputs) -- the floors are the bounds above.
 The gradient bounds are vector-wise, not per-tensor max: fp32 can flip ReLU/lrelu kinks
 that float64 resolves the other way.
@@ -45,11 +47,21 @@ def test_engine_matches_golden(path):
     stats = net.step_stats().cpu().numpy()
     loss = net.loss_value(stats, reg)
     assert abs(loss - g["loss"]) <= 1e-4 * abs(g["loss"]), (loss, float(g["loss"]))
-    T = len(g["recon"])
-    for t in range(T):
-        assert abs(stats[t, 0] - g["recon"][t]) <= 1e-4 * abs(g["recon"][t]), t
-        assert abs(stats[t, 1] - g["kl"][t]) <= 1e-4 * abs(g["kl"][t]), t
     np.testing.assert_allclose(net.elbo_per_image().cpu().numpy(), g["elbo_img"], rtol=1e-4)
+    T = len(g["recon"])
+    tw = o = None
+    if chaotic:  # fp32 twin of the same graph on the same inputs (bounds below)
+        cd = spec.make_config(preset, batch=int(g["batch"]))
+        _, struct = spec.build_params(cd)
+        tw = torch_twin.Twin(cd, struct, net.param_dict(), dtype=torch.float32)
+        o = tw.step(g["x"], g["target"], g["eps"], reg)
+    for t in range(T):
+        for j, key in ((0, "recon"), (1, "kl")):
+            ref_t = float(g[key][t])
+            tol = 1e-4
+            if chaotic:
+                tol = max(tol, 4 * abs(o[key][t] - ref_t) / abs(ref_t))
+            assert abs(stats[t, j] - ref_t) <= tol * abs(ref_t), (key, t, float(stats[t, j]), ref_t, tol)
     s = int(g["xhat_sample_stride"])
     names = list(g["grad_names"])
     ref = g["grad_norm"]
@@ -74,10 +86,6 @@ def test_engine_matches_golden(path):
     floor = dict(gmed=1e-4, gvec=1e-3, small=1e-3)
     bound = {k: floor.get(k, 1e-4) for k in hip}
     if chaotic:
-        cd = spec.make_config(preset, batch=int(g["batch"]))
-        _, struct = spec.build_params(cd)
-        tw = torch_twin.Twin(cd, struct, net.param_dict(), dtype=torch.float32)
-        o = tw.step(g["x"], g["target"], g["eps"], reg)
         with torch.no_grad():  # latents of the twin: rerun the recognition ladders
             x = torch.as_tensor(g["x"]).permute(0, 3, 1, 2)
             lat = [tw.inference(struct[t]["inference"], x) for t in range(T)]

@@ -5,7 +5,7 @@ per layer, grid.z = step), the stored pre-BatchNorm output is recomputed in floa
 stored bf16-rounded input activation and weights.  The kernels round exactly those operands
 and accumulate in fp32, so the bound is accumulation-order only: 1e-6 relative (L2) and
 1e-5 of max|ref| pointwise.  At the CelebA geometry these launches run on the halo-tile
-kernel (igemm_halo_kernel) except level-0 conv a (Cin = 3, per-tap small-channel kernel).
+kernel (igemm_halo_kernel) except level-0 conv a (Cin = 3: conv_smallc_kernel, csrc/smallc.hip).
 
 Why not compare halo against the per-tap kernel through the whole step: in bf16 mode a
 1e-7 summation-order difference flips the bf16 rounding of a few downstream operands

@@ -13,6 +13,9 @@ pytestmark = pytest.mark.gpu
 CONV_CASES = [
     # n, h, cin, cout, stride, transpose
     (2, 16, 3, 32, 2, 0),     # layer-0 conv (small-C gather path)
+    (2, 64, 3, 32, 2, 0),     # layer-0 conv at 64x64 (csrc/smallc.hip window kernel)
+    (2, 32, 4, 64, 2, 0),     # 4 input channels, N = 64
+    (2, 32, 32, 4, 2, 1),     # packed output conv-T [C | ratio]: its input gradient is the small-C gather
     (2, 8, 32, 32, 1, 0),     # stride-1 conv, N<=32 tile
     (2, 8, 64, 64, 1, 0),
     (2, 8, 128, 128, 2, 0),
