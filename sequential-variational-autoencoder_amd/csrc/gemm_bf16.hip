@@ -1236,6 +1236,8 @@ int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit) {
     if (ksplit) *ksplit = 1;
     return smallc_nrb(a);
   }
+  // (no shortcut for convt_smalln: it only takes launches without stats, and the plan is asked
+  //  before a.stats is set -- a BN layer must plan as the kernel that will carry its stats)
   if (!halo_disabled()) {
     const HaloPlan hp = halo_plan(a, groups);
     if (hp.ok) {
@@ -1291,6 +1293,11 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
     conv_smallc(a, groups, true, s);
     if (after) hipEventRecord(after, s);
     return smallc_nrb(a);
+  }
+  if (path == 2 && smalln_ok(a)) {
+    convt_smalln(a, groups, s);
+    if (after) hipEventRecord(after, s);
+    return 0;  // no stats (smalln_ok requires none)
   }
   if (path == 1 || (path == 2 && !halo_disabled())) {
     HaloPlan hp = halo_plan(a, groups);

@@ -51,6 +51,9 @@ int smallc_nrb(const FwdArgs& a);
 int smallc_bm();
 bool smallc_disabled();  // SVAE_NO_SMALLC=1
 void conv_smallc(const FwdArgs& a, int groups, bool bf, hipStream_t s);
+// stride-2 4x4 conv-T gathers with N <= 16 output channels (smallc.hip, bf16 operands)
+bool smalln_ok(const FwdArgs& a);
+void convt_smalln(const FwdArgs& a, int groups, hipStream_t s);
 // bf16-MFMA variants (dtype=1): A fp32 -> bf16 in staging, B = a.Bh bf16 [tap][n][k] (ldb = k pitch)
 // returns the number of stats row-blocks written to a.stats (plan: same value without launching)
 // Kernel-instance ids of the bf16 GEMMs (one per template instantiation = one rocprof kernel

@@ -215,6 +215,108 @@ void launch_smallc(const FwdArgs& a, int groups, hipStream_t s) {
   hipLaunchKernelGGL((conv_smallc_kernel<TN, SC_TM, BF>), grid, dim3(256), smallc_lds(a, BF), s, a);
 }
 
+// ---------------------------------------------------------------------------
+// Stride-2 4x4 conv-T gathers with few output channels (N <= 16): the output conv-T of the
+// decoder (F1 -> [x_hat | ratio], N = C+1 = 4; sequential_vae.py:1720,1727 via
+// abstract_network.py:37) and the input gradient of layer-0 conv (CONVT gather over its dpre,
+// N = C = 3).  On the 32-column tiles of the general gathers these cost what an N = 32 launch
+// does (61 us at CelebA B=128) for a tenth of the output.
+//
+// A block owns R = 8 full-width output rows of one image; wave w owns output parity class
+// (cy, cx) = (w >> 1, w & 1), whose pixels all use the same 4 taps (ky = ky0 + 2ty,
+// kx = kx0 + 2tx) and read input pixel (qy + cy - ty, qx + cx - tx) for class pixel (qy, qx).
+// The R/2 + 2 input rows (+1 column of zeros each side) of a 32-channel chunk are staged once
+// as bf16 (80-byte pixel pitch), and every 16-pixel class-row segment is one
+// v_mfma_f32_16x16x32_bf16 per tap: K = the chunk's 32 channels, N padded to 16.
+// ---------------------------------------------------------------------------
+constexpr int SN_R = 8;      // output rows per block
+constexpr int SN_PITCH = 40; // LDS pixel pitch in bf16 (32 channels + 8 pad)
+constexpr int SN_MAXT = 16;  // class-row tiles per wave: (R/2) x (Wi/16) <= 16  -> Wi <= 64
+
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+
+__global__ __launch_bounds__(256) void convt_smalln_kernel(FwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) __bf16 wsm[];
+  const ConvGeom& g = a.g;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cy = wave >> 1, cx = wave & 1;
+  const int r16 = lane & 15, kg = lane >> 4;
+  const int bpi = g.Ho / SN_R;
+  const int img = blockIdx.x / bpi;
+  const int Y0 = (blockIdx.x - img * bpi) * SN_R;
+  const int group = blockIdx.z;
+  const int PR = SN_R / 2 + 2, PC = g.Wi + 2;
+  const int iy0 = Y0 / 2 - 1;
+  const int WT = g.Wi / 16;             // 16-pixel segments per class row
+  const int ntile = (SN_R / 2) * WT;
+  const float* A = a.A + group * a.a_gs + (long long)img * g.Hi * g.Wi * a.lda;
+  const __bf16* Bw = (const __bf16*)a.Bh + group * a.b_gs;
+  const int ky0 = (cy + g.pad) & 1, kx0 = (cx + g.pad) & 1;
+  const bool nvalid = r16 < a.N;
+
+  f32x4 acc[SN_MAXT];
+#pragma unroll
+  for (int i = 0; i < SN_MAXT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int ch = 0; ch < a.Cin; ch += 32) {
+    if (ch) __syncthreads();  // previous chunk's window fully read
+    for (int it = tid; it < PR * PC * 4; it += 256) {
+      const int pix = it >> 2, part = it & 3;
+      const int pr = pix / PC, pc = pix - pr * PC;
+      const int iy = iy0 + pr, ix = pc - 1;
+      f32x8 v = {};
+      if (iy >= 0 && iy < g.Hi && ix >= 0 && ix < g.Wi) {
+        const float* src = A + ((long long)iy * g.Wi + ix) * a.lda + ch + part * 8;
+        const f32x4 lo = *(const f32x4*)src, hi = *(const f32x4*)(src + 4);
+        v = f32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      *(bf16x8*)&wsm[pix * SN_PITCH + part * 8] = __builtin_convertvector(v, bf16x8);
+    }
+    // this class's 4 tap fragments of the chunk (columns >= N are zero)
+    bf16x8 bq[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int tap = (ky0 + 2 * (t >> 1)) * 4 + kx0 + 2 * (t & 1);
+      bq[t] = nvalid ? *(const bf16x8*)(Bw + tap * a.b_tap + (long long)r16 * a.ldb + ch + 8 * kg) : bf16x8{};
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < SN_MAXT; ++i) {
+      if (i < ntile) {
+        const int j = i / WT, hseg = i - j * WT;
+        // class pixel (qy, qx) = (Y0/2 + j, 16*hseg + r16): window row qy + cy - ty - iy0
+        const int wr = j + 1 + cy, wc = 16 * hseg + r16 + cx + 1;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int ty = t >> 1, tx = t & 1;
+          const bf16x8 af = *(const bf16x8*)&wsm[((wr - ty) * PC + wc - tx) * SN_PITCH + 8 * kg];
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bq[t], acc[i], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  if (!nvalid) return;
+  float* Cp = a.C + group * a.c_gs;
+  const float bv = a.bias ? a.bias[group * a.bias_gs + r16] : 0.f;
+#pragma unroll
+  for (int i = 0; i < SN_MAXT; ++i) {
+    if (i < ntile) {
+      const int j = i / WT, hseg = i - j * WT;
+      const int Y = Y0 + 2 * j + cy;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int X = 2 * (16 * hseg + 4 * kg + e) + cx;
+        float v = acc[i][e] + bv;
+        v = act_f(v, a.act);
+        float* dst = Cp + (((long long)img * g.Ho + Y) * g.Wo + X) * a.ldc + r16;
+        if (a.accumulate) v += *dst;
+        *dst = v;
+      }
+    }
+  }
+}
+
 }  // namespace
 
 bool smallc_ok(const FwdArgs& a, bool bf) {
@@ -252,3 +354,20 @@ void conv_smallc(const FwdArgs& a, int groups, bool bf, hipStream_t s) {
 }
 
 int smallc_bm() { return SC_BM; }
+
+bool smalln_ok(const FwdArgs& a) {
+  const ConvGeom& g = a.g;
+  if (smallc_disabled()) return false;
+  if (g.mode != GM_CONVT || g.ksz != 4 || g.stride != 2 || g.pad != 1 || a.nclass != 4) return false;
+  if (a.N < 1 || a.N > 16 || a.Cin % 32 || !a.Bh || a.stats || a.bw.pre) return false;
+  if (g.Ho != 2 * g.Hi || g.Wo != 2 * g.Wi || g.Ho % SN_R || g.Wi % 16) return false;
+  if ((SN_R / 2) * (g.Wi / 16) > SN_MAXT) return false;
+  if (a.ldb % 8 || a.b_tap % 8 || a.lda % 4) return false;  // 16-byte fragment / staging loads
+  return (SN_R / 2 + 2) * (g.Wi + 2) * SN_PITCH * 2 <= 64 * 1024;
+}
+
+void convt_smalln(const FwdArgs& a, int groups, hipStream_t s) {
+  const int lds = (SN_R / 2 + 2) * (a.g.Wi + 2) * SN_PITCH * 2;
+  dim3 grid(a.g.nimg * (a.g.Ho / SN_R), 1, groups);
+  hipLaunchKernelGGL(convt_smalln_kernel, grid, dim3(256), lds, s, a);
+}

@@ -4,7 +4,8 @@ launches are the same two gather modes).  Reference: float64 torch conv of the S
 bf16-rounded operands (oracle/torch_twin.py TF-SAME helpers), so the only difference left
 is fp32 accumulation order: bound 2e-5 relative (L2) and 1e-4 of max|ref| pointwise.
 Every kernel is checked: path 0 (per-tap gather), path 1 (halo-tile window) and path 2 (the
-default dispatch, which adds the small-channel window kernel of csrc/smallc.hip for Cin <= 4)."""
+default dispatch, which adds the small-channel window kernels of csrc/smallc.hip: Cin <= 4 convs and
+N <= 16 stride-2 conv-T gathers)."""
 import numpy as np
 import pytest
 import torch
@@ -27,6 +28,8 @@ SHAPES = [
     # small-channel convs (csrc/smallc.hip on path 2): layer-0 conv of the image (Cin = 3) at the
     # CelebA / tiny geometries, 4 channels, N = 64 and 128 column tiles
     (4, 64, 3, 32, 2, 0), (2, 32, 3, 32, 2, 0), (2, 64, 4, 64, 2, 0), (2, 32, 1, 128, 2, 0),
+    # small-N conv-T gathers (convt_smalln_kernel on path 2): 2 channel chunks, N = 16 / 1, Wi = 16 / 64
+    (2, 16, 64, 16, 2, 1), (2, 32, 32, 1, 2, 1), (1, 64, 32, 4, 2, 1),
 ]
 
 

@@ -1,5 +1,6 @@
 """Time single bf16 gather-GEMM launches (svae_op_gather_bf16) on CelebA B=128 layer shapes.
-    python tools/bench_gather.py [path ...]       # path 0 = per-tap gather, 1 = halo window"""
+    python tools/bench_gather.py [image] [path ...]   # path 0 per-tap, 1 halo window, 2 default dispatch
+    image: the image-space shapes (N <= 4 outputs, Cin = 3 input) instead of the CelebA layer shapes"""
 import importlib
 import os
 import sys
@@ -15,13 +16,16 @@ SHAPES = [  # (n, h_in, cin, cout, stride, transpose) -- CelebA B=128 forward la
     (128, 16, 128, 64, 1, 1), (128, 16, 64, 64, 1, 0), (128, 8, 128, 64, 2, 1), (128, 16, 64, 128, 2, 0),
     (128, 8, 256, 128, 1, 1), (128, 8, 128, 128, 1, 0), (128, 4, 384, 128, 2, 1),
 ]
+IMAGE = [  # image-space launches: output conv-T (N = C+1 = 4), layer-0 input gradient (N = 3), layer-0 conv
+    (128, 32, 32, 4, 2, 1), (128, 32, 32, 3, 2, 1), (128, 64, 3, 32, 2, 0),
+]
 
 
-def run(path, iters=20):
+def run(path, iters=20, shapes=SHAPES):
     torch.manual_seed(0)
     scratch = torch.empty(64 << 20, device="cuda")
     tot_f, tot_t = 0.0, 0.0
-    for (n, h, cin, cout, s, tr) in SHAPES:
+    for (n, h, cin, cout, s, tr) in shapes:
         x = torch.randn(n, h, h, cin, device="cuda")
         w = (torch.randn(16, cout, cin, device="cuda") * 0.05).to(torch.bfloat16)
         ho = h * s if tr else h // s
@@ -50,5 +54,9 @@ def run(path, iters=20):
 
 
 if __name__ == "__main__":
-    for p in (sys.argv[1:] or ["0", "1"]):
-        run(int(p))
+    args = sys.argv[1:]
+    shapes = SHAPES
+    if args and args[0] == "image":
+        shapes, args = IMAGE, args[1:]
+    for p in (args or ["0", "1"]):
+        run(int(p), shapes=shapes)
