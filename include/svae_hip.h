@@ -135,7 +135,8 @@ int svae_op_conv_dgrad(const float* dy, int n, int h, int cin, const float* w, i
                        float* dx, void* stream);
 int svae_op_conv_wgrad(const float* x, int n, int h, int cin, const float* dy, int cout, int stride, int transpose,
                        float* dw, void* scratch, int64_t scratch_bytes, void* stream);
-/* training BN (+act 0 none,1 relu,2 lrelu) over rows of x [rows,C] */
+/* training BN (+act 0 none,1 relu,2 lrelu) over rows of x [rows,C].
+ * scratch: >= 1032*c bytes (sharded fixed-point column accumulators + constants); bwd: >= 1024*c bytes */
 int svae_op_bn_act(const float* x, int64_t rows, int c, const float* beta, int act, float* y, float* mean,
                    float* invstd, void* scratch, int64_t scratch_bytes, void* stream);
 int svae_op_bn_act_bwd(const float* dy, const float* y, const float* x, int64_t rows, int c, const float* mean,

@@ -1,7 +1,7 @@
 // Training-mode BatchNorm (center=True, scale=False, eps=1e-3; abstract_network.py:22) + activation.
 //
-// Forward statistics come from the producing GEMM's epilogue (per-row-block
-// partial sum / sum^2); bn_finalize reduces them in fp64.  The normalise +
+// Forward statistics come from the producing GEMM's epilogue, added into fixed-point
+// per-column accumulators (common.h stat_put); the apply pass finalises them in fp64.  The normalise +
 // beta + shortcut + activation pass writes straight into the consumer's view
 // (e.g. the channel half of a concat buffer, combine_noise sequential_vae.py:1833).
 // Backward: dz = dy*act'(y) (act' from the stored output, TF tie rules),
@@ -18,100 +18,128 @@ __device__ __forceinline__ f32x4 bn_y(f32x4 x, f32x4 m, f32x4 is, f32x4 b) {
   return r;
 }
 
-// partial rows are reduced by FIN_L lanes per channel quad (4 quads = 16 channels per block),
-// each lane summing its share in fp64, then a fixed-order LDS tree: deterministic, and short
-// serial chains (the kernel is latency-bound at these sizes)
-#define FIN_Q 4
-#define FIN_L 64
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* part, long long part_gs, int nrb, int C,
-                                                          double count, float eps, float* mean, float* invstd,
-                                                          long long ms_gs, int mode, float* dbeta,
-                                                          long long dbeta_gs) {
-  // mode 0: stats -> mean/invstd ; mode 1: bwd sums -> ab (mean slots), dbeta
-  __shared__ double red[2][FIN_L][FIN_Q * 4];
-  const int group = blockIdx.y;
-  const int qi = threadIdx.x % FIN_Q, li = threadIdx.x / FIN_Q;
-  const int c0 = (blockIdx.x * FIN_Q + qi) * 4;
-  const float* P = part + group * part_gs;
-  double s[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
-  if (c0 < C) {
-    for (int rb = li; rb < nrb; rb += FIN_L) {
-      const f32x4 a = *(const f32x4*)(P + (long long)rb * 2 * C + c0);
-      const f32x4 b2 = *(const f32x4*)(P + (long long)rb * 2 * C + C + c0);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        s[e] += (double)a[e];
-        q[e] += (double)b2[e];
-      }
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    red[0][li][qi * 4 + e] = s[e];
-    red[1][li][qi * 4 + e] = q[e];
-  }
-  __syncthreads();
-  for (int w = FIN_L / 2; w > 0; w >>= 1) {
-    if (li < w) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        red[0][li][qi * 4 + e] += red[0][li + w][qi * 4 + e];
-        red[1][li][qi * 4 + e] += red[1][li + w][qi * 4 + e];
-      }
+// Elementwise BN passes: a block owns up to AP_QB channel quads (contiguous 16-B column
+// segments of a row) and a range of rows.  It first finalises its channels' statistics from
+// the fixed-point accumulators (fp64, the same expression for every block, so all blocks agree
+// bitwise) into LDS; the blocks of row range 0 also store them for the backward.  This replaces
+// a separate finalize launch per BN layer.
+#define AP_QB 64
+
+// shards so that at most ~16 row-blocks add into one accumulator line
+int bn_acc_shards(long long rowblocks) {
+  int n = 1;
+  while (n < 16 && (long long)n * 16 < rowblocks) n *= 2;
+  return n;
+}
+
+// integer sum over the nsh shards of the accumulators of channels [c0, c0 + nch) into LDS
+// tot[4 * nch] (exact and order-free), block-cooperative; ends with a barrier.  Each thread sums
+// its word over a stride of shards in registers (independent loads, one L2 round trip), then
+// the k threads that share a word combine by LDS integer atomics.
+__device__ __forceinline__ void acc_gather(const u64* acc, long long sh, int nsh, int c0, int nch, u64* tot) {
+  const int nw = 4 * nch;
+  const int tid = threadIdx.x;
+  const u64* base = acc + 4LL * c0;
+  if (nw >= 256) {
+    for (int w = tid; w < nw; w += 256) {
+      u64 v = 0;
+#pragma unroll 8
+      for (int k = 0; k < nsh; ++k) v += base[k * sh + w];
+      tot[w] = v;
     }
     __syncthreads();
+    return;
   }
-  if (li == 0 && c0 < C) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int cc = c0 + e;
-      const double ss = red[0][0][qi * 4 + e], qq = red[1][0][qi * 4 + e];
-      if (mode == 0) {
-        const double m = ss / count;
-        double var = qq / count - m * m;
-        if (var < 0.0) var = 0.0;
-        mean[group * ms_gs + cc] = (float)m;
-        invstd[group * ms_gs + cc] = (float)(1.0 / sqrt(var + (double)eps));
-      } else {
-        mean[group * ms_gs + cc] = (float)(ss / count);        // a = mean(dz)
-        mean[group * ms_gs + C + cc] = (float)(qq / count);    // b = mean(dz*xhat)
-        if (dbeta) dbeta[group * dbeta_gs + cc] = (float)ss;
-      }
-    }
+  int k = 256 / nw;  // threads per word
+  if (k > nsh) k = nsh;
+  for (int i = tid; i < nw; i += 256) tot[i] = 0;
+  __syncthreads();
+  if (tid < k * nw) {
+    const int w = tid % nw, part = tid / nw;
+    u64 v = 0;
+#pragma unroll 4
+    for (int j = part; j < nsh; j += k) v += base[j * sh + w];
+    if (k == 1) tot[w] = v;
+    else atomicAdd(&tot[w], v);
   }
+  __syncthreads();
 }
 
-void bn_finalize(const float* part, long long part_gs, int nrb, int C, long long count, float eps, float* mean,
-                 float* invstd, long long ms_gs, int groups, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 4 * FIN_Q - 1) / (4 * FIN_Q), groups), dim3(256), 0, s, part,
-                     part_gs, nrb, C, (double)count, eps, mean, invstd, ms_gs, 0, (float*)nullptr, 0LL);
+struct ApGrid {
+  dim3 grid;
+  int rpb;
+};
+static ApGrid ap_grid(long long rows, int C, int groups) {
+  const int Q = C / 4;
+  const int QB = Q < AP_QB ? Q : AP_QB;
+  const int RL = 256 / QB;
+  const int gx = (Q + QB - 1) / QB;
+  long long want = (rows + 4LL * RL - 1) / (4LL * RL);  // >= 4 rows per thread
+  long long cap = 2048 / ((long long)gx * groups);
+  if (cap < 1) cap = 1;
+  long long ry = want < cap ? want : cap;
+  if (ry < 1) ry = 1;
+  ApGrid g;
+  g.rpb = (int)((rows + ry - 1) / ry);
+  g.grid = dim3(gx, (unsigned)((rows + g.rpb - 1) / g.rpb), groups);
+  return g;
 }
 
-void bn_bwd_finalize(const float* part, long long part_gs, int nrb, int C, long long count, float* ab, long long ab_gs,
-                     float* dbeta, long long dbeta_gs, int groups, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 4 * FIN_Q - 1) / (4 * FIN_Q), groups), dim3(256), 0, s, part,
-                     part_gs, nrb, C, (double)count, 0.f, ab, (float*)nullptr, ab_gs, 1, dbeta, dbeta_gs);
-}
-
-__global__ void bn_apply_kernel(const float* pre, int ldp, long long pre_gs, long long rows, int C,
-                                const float* mean, const float* invstd, long long ms_gs, const float* beta,
-                                long long beta_gs, const float* res, int ldr, long long res_gs, int act, float* out,
-                                int ldo, long long out_gs) {
-  const int group = blockIdx.y;
+__global__ __launch_bounds__(256) void bn_apply_kernel(const float* pre, int ldp, long long pre_gs, long long rows,
+                                                       int C, const u64* acc, long long acc_gs, long long sh,
+                                                       int nsh, float eps,
+                                                       float* mean, float* invstd, long long ms_gs, const float* beta,
+                                                       long long beta_gs, const float* res, int ldr, long long res_gs,
+                                                       int act, float* out, int ldo, long long out_gs, int rpb) {
+  __shared__ __attribute__((aligned(16))) float sm[2][AP_QB * 4];
+  __shared__ u64 tot[4 * AP_QB * 4];
+  const int group = blockIdx.z;
   const int Q = C >> 2;
-  const long long total = rows * Q;
-  pre += group * pre_gs;
-  out += group * out_gs;
+  const int QB = Q < AP_QB ? Q : AP_QB;
+  const int RL = 256 / QB;
+  const int tid = threadIdx.x, qi = tid % QB, rl = tid / QB;
+  const int q0 = blockIdx.x * QB;
+  const int nch = min(QB * 4, C - q0 * 4);
   mean += group * ms_gs;
   invstd += group * ms_gs;
-  beta += group * beta_gs;
+  if (acc) acc_gather(acc + group * acc_gs, sh, nsh, q0 * 4, nch, tot);
+  if (tid < nch) {
+    const int c = q0 * 4 + tid;
+    {
+      float m, is;
+      if (acc) {
+        const double cnt = (double)rows;
+        const double md = fx_get(tot + 4 * tid) / cnt;
+        double var = fx_get(tot + 4 * tid + 2) / cnt - md * md;
+        if (var < 0.0) var = 0.0;
+        m = (float)md;
+        is = (float)(1.0 / sqrt(var + (double)eps));
+        if (blockIdx.y == 0) {
+          mean[c] = m;
+          invstd[c] = is;
+        }
+      } else {
+        m = mean[c];
+        is = invstd[c];
+      }
+      sm[0][tid] = m;
+      sm[1][tid] = is;
+    }
+  }
+  __syncthreads();
+  const int q = q0 + qi;
+  if (rl >= RL || q >= Q) return;
+  const int c = q * 4;
+  pre += group * pre_gs;
+  out += group * out_gs;
   if (res) res += group * res_gs;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const long long r = i / Q;
-    const int c = (int)(i - r * Q) * 4;
-    f32x4 x = *(const f32x4*)(pre + r * ldp + c);
-    f32x4 m = *(const f32x4*)(mean + c), is = *(const f32x4*)(invstd + c), b = *(const f32x4*)(beta + c);
-    f32x4 y = bn_y(x, m, is, b);
+  const f32x4 m = *(const f32x4*)&sm[0][qi * 4], is = *(const f32x4*)&sm[1][qi * 4];
+  const f32x4 b = *(const f32x4*)(beta + group * beta_gs + c);
+  const long long r0 = (long long)blockIdx.y * rpb;
+  const long long r1 = r0 + rpb < rows ? r0 + rpb : rows;
+#pragma unroll 4
+  for (long long r = r0 + rl; r < r1; r += RL) {
+    f32x4 y = bn_y(*(const f32x4*)(pre + r * ldp + c), m, is, b);
     if (res) y += *(const f32x4*)(res + r * ldr + c);
 #pragma unroll
     for (int e = 0; e < 4; ++e) y[e] = act_f(y[e], act);
@@ -119,30 +147,24 @@ __global__ void bn_apply_kernel(const float* pre, int ldp, long long pre_gs, lon
   }
 }
 
-static int ew_blocks(long long work) {
-  long long b = (work + 255) / 256;
-  return (int)(b < 2048 ? (b < 1 ? 1 : b) : 2048);
-}
-
-void bn_apply(const float* pre, int ldp, long long pre_gs, long long rows, int C, const float* mean,
-              const float* invstd, long long ms_gs, const float* beta, long long beta_gs, const float* res, int ldr,
-              long long res_gs, int act, float* out, int ldo, long long out_gs, int groups, hipStream_t s) {
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_blocks(rows * (C / 4)), groups), dim3(256), 0, s, pre, ldp, pre_gs,
-                     rows, C, mean, invstd, ms_gs, beta, beta_gs, res, ldr, res_gs, act, out, ldo, out_gs);
+void bn_apply(const float* pre, int ldp, long long pre_gs, long long rows, int C, const u64* acc, long long acc_gs,
+              long long sh, int nsh, float eps, float* mean, float* invstd, long long ms_gs, const float* beta, long long beta_gs,
+              const float* res, int ldr, long long res_gs, int act, float* out, int ldo, long long out_gs, int groups,
+              hipStream_t s) {
+  const ApGrid g = ap_grid(rows, C, groups);
+  hipLaunchKernelGGL(bn_apply_kernel, g.grid, dim3(256), 0, s, pre, ldp, pre_gs, rows, C, acc, acc_gs, sh, nsh, eps, mean,
+                     invstd, ms_gs, beta, beta_gs, res, ldr, res_gs, act, out, ldo, out_gs, g.rpb);
 }
 
 #define BWD_RPB 256  // rows per row-block of the backward reduction
-
-int bn_bwd_rowblocks(long long rows, int C) {
-  (void)C;
-  return (int)((rows + BWD_RPB - 1) / BWD_RPB);
-}
+int bn_bwd_rowblocks(long long rows) { return (int)((rows + BWD_RPB - 1) / BWD_RPB); }
 
 // y == nullptr: act' from the recomputed pre-activation bn_y(pre) (layers without a shortcut add)
 __global__ void bn_bwd_reduce_kernel(const float* dy, int lddy, long long dy_gs, const float* y, int ldy,
                                      long long y_gs, const float* pre, int ldp, long long pre_gs, long long rows,
                                      int C, const float* mean, const float* invstd, long long ms_gs, const float* beta,
-                                     long long beta_gs, int act, float* part, long long part_gs) {
+                                     long long beta_gs, int act, u64* acc, long long acc_gs, long long sh,
+                                     int nsh) {
   __shared__ f32x4 red[2][256];
   const int group = blockIdx.z;
   const int Q = C >> 2;
@@ -181,55 +203,74 @@ __global__ void bn_bwd_reduce_kernel(const float* dy, int lddy, long long dy_gs,
   red[0][tid] = sd;
   red[1][tid] = sx;
   __syncthreads();
-  if (active && rl == 0) {
-    for (int j = 1; j < RL; ++j) {
-      sd += red[0][j * QB + qi];
-      sx += red[1][j * QB + qi];
+  // one (channel, sum|sum*xhat) per thread, row lanes combined in a fixed order
+  if (tid < 8 * QB) {
+    const int cc = tid % (4 * QB), kind = tid / (4 * QB), qq = cc >> 2, e = cc & 3;
+    const int q2 = blockIdx.x * QB + qq;
+    if (q2 < Q) {
+      float v = 0.f;
+      for (int j = 0; j < RL; ++j) v += red[kind][j * QB + qq][e];
+      fx_add(acc + (blockIdx.y & (nsh - 1)) * sh + group * acc_gs + 4LL * (q2 * 4 + e) + 2 * kind, v);
     }
-    float* P = part + group * part_gs + (long long)blockIdx.y * 2 * C;
-    *(f32x4*)(P + q * 4) = sd;
-    *(f32x4*)(P + C + q * 4) = sx;
   }
 }
 
 void bn_bwd_reduce(const float* dy, int lddy, long long dy_gs, const float* y, int ldy, long long y_gs,
                    const float* pre, int ldp, long long pre_gs, long long rows, int C, const float* mean,
-                   const float* invstd, long long ms_gs, const float* beta, long long beta_gs, int act, float* part,
-                   long long part_gs, int groups, hipStream_t s) {
+                   const float* invstd, long long ms_gs, const float* beta, long long beta_gs, int act, u64* acc,
+                   long long acc_gs, long long sh, int nsh, int groups, hipStream_t s) {
   const int Q = C / 4;
   const int QB = Q < 16 ? Q : 16;
-  dim3 grid((Q + QB - 1) / QB, bn_bwd_rowblocks(rows, C), groups);
+  dim3 grid((Q + QB - 1) / QB, (unsigned)bn_bwd_rowblocks(rows), groups);
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, grid, dim3(256), 0, s, dy, lddy, dy_gs, y, ldy, y_gs, pre, ldp, pre_gs,
-                     rows, C, mean, invstd, ms_gs, beta, beta_gs, act, part, part_gs);
+                     rows, C, mean, invstd, ms_gs, beta, beta_gs, act, acc, acc_gs, sh, nsh);
 }
 
-__global__ void bn_bwd_apply_kernel(const float* dy, int lddy, long long dy_gs, const float* y, int ldy,
-                                    long long y_gs, const float* pre, int ldp, long long pre_gs, long long rows,
-                                    int C, const float* mean, const float* invstd, long long ms_gs, const float* beta,
-                                    long long beta_gs, const float* ab, long long ab_gs, int act, float* dpre, int lddp,
-                                    long long dpre_gs, float* dres, int ldres, long long dres_gs, int res_acc) {
-  const int group = blockIdx.y;
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
+    const float* dy, int lddy, long long dy_gs, const float* y, int ldy, long long y_gs, const float* pre, int ldp,
+    long long pre_gs, long long rows, int C, const float* mean, const float* invstd, long long ms_gs,
+    const float* beta, long long beta_gs, const u64* acc, long long acc_gs, long long sh, int nsh, float* dbeta,
+    long long dbeta_gs, int act,
+    float* dpre, int lddp, long long dpre_gs, float* dres, int ldres, long long dres_gs, int res_acc, int rpb) {
+  __shared__ __attribute__((aligned(16))) float sm[2][AP_QB * 4];
+  __shared__ u64 tot[4 * AP_QB * 4];
+  const int group = blockIdx.z;
   const int Q = C >> 2;
-  const long long total = rows * Q;
+  const int QB = Q < AP_QB ? Q : AP_QB;
+  const int RL = 256 / QB;
+  const int tid = threadIdx.x, qi = tid % QB, rl = tid / QB;
+  const int q0 = blockIdx.x * QB;
+  const int nch = min(QB * 4, C - q0 * 4);
+  acc_gather(acc + group * acc_gs, sh, nsh, q0 * 4, nch, tot);
+  if (tid < nch) {
+    const int c = q0 * 4 + tid;
+    {
+      const double sd = fx_get(tot + 4 * tid), sx = fx_get(tot + 4 * tid + 2);
+      sm[0][tid] = (float)(sd / (double)rows);  // a = mean(dz)
+      sm[1][tid] = (float)(sx / (double)rows);  // b = mean(dz*xhat)
+      if (blockIdx.y == 0 && dbeta) dbeta[group * dbeta_gs + c] = (float)sd;
+    }
+  }
+  __syncthreads();
+  const int q = q0 + qi;
+  if (rl >= RL || q >= Q) return;
+  const int c = q * 4;
   dy += group * dy_gs;
   if (y) y += group * y_gs;
-  else beta += group * beta_gs;
   pre += group * pre_gs;
-  mean += group * ms_gs;
-  invstd += group * ms_gs;
-  ab += group * ab_gs;
   dpre += group * dpre_gs;
   if (dres) dres += group * dres_gs;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const long long r = i / Q;
-    const int c = (int)(i - r * Q) * 4;
-    f32x4 g = *(const f32x4*)(dy + r * lddy + c);
-    f32x4 is = *(const f32x4*)(invstd + c);
-    const f32x4 m = *(const f32x4*)(mean + c);
+  const f32x4 m = *(const f32x4*)(mean + group * ms_gs + c), is = *(const f32x4*)(invstd + group * ms_gs + c);
+  const f32x4 bb = y ? f32x4{0.f, 0.f, 0.f, 0.f} : *(const f32x4*)(beta + group * beta_gs + c);
+  const f32x4 a = *(const f32x4*)&sm[0][qi * 4], b = *(const f32x4*)&sm[1][qi * 4];
+  const long long r0 = (long long)blockIdx.y * rpb;
+  const long long r1 = r0 + rpb < rows ? r0 + rpb : rows;
+#pragma unroll 2
+  for (long long r = r0 + rl; r < r1; r += RL) {
+    const f32x4 g = *(const f32x4*)(dy + r * lddy + c);
     const f32x4 xp = *(const f32x4*)(pre + r * ldp + c);
-    f32x4 yy = y ? *(const f32x4*)(y + r * ldy + c) : bn_y(xp, m, is, *(const f32x4*)(beta + c));
-    f32x4 xh = (xp - m) * is;
-    f32x4 a = *(const f32x4*)(ab + c), b = *(const f32x4*)(ab + C + c);
+    const f32x4 yy = y ? *(const f32x4*)(y + r * ldy + c) : bn_y(xp, m, is, bb);
+    const f32x4 xh = (xp - m) * is;
     f32x4 dz;
 #pragma unroll
     for (int e = 0; e < 4; ++e) dz[e] = g[e] * dact_from_y(yy[e], act);
@@ -243,10 +284,12 @@ __global__ void bn_bwd_apply_kernel(const float* dy, int lddy, long long dy_gs, 
 
 void bn_bwd_apply(const float* dy, int lddy, long long dy_gs, const float* y, int ldy, long long y_gs,
                   const float* pre, int ldp, long long pre_gs, long long rows, int C, const float* mean,
-                  const float* invstd, long long ms_gs, const float* beta, long long beta_gs, const float* ab,
-                  long long ab_gs, int act, float* dpre, int lddp, long long dpre_gs, float* dres, int ldres,
-                  long long dres_gs, int res_acc, int groups, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_blocks(rows * (C / 4)), groups), dim3(256), 0, s, dy, lddy, dy_gs,
-                     y, ldy, y_gs, pre, ldp, pre_gs, rows, C, mean, invstd, ms_gs, beta, beta_gs, ab, ab_gs, act, dpre,
-                     lddp, dpre_gs, dres, ldres, dres_gs, res_acc);
+                  const float* invstd, long long ms_gs, const float* beta, long long beta_gs, const u64* acc,
+                  long long acc_gs, long long sh, int nsh, float* dbeta, long long dbeta_gs, int act, float* dpre, int lddp,
+                  long long dpre_gs, float* dres, int ldres, long long dres_gs, int res_acc, int groups,
+                  hipStream_t s) {
+  const ApGrid g = ap_grid(rows, C, groups);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, g.grid, dim3(256), 0, s, dy, lddy, dy_gs, y, ldy, y_gs, pre, ldp, pre_gs,
+                     rows, C, mean, invstd, ms_gs, beta, beta_gs, acc, acc_gs, sh, nsh, dbeta, dbeta_gs, act, dpre, lddp,
+                     dpre_gs, dres, ldres, dres_gs, res_acc, g.rpb);
 }

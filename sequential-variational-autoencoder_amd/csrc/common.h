@@ -97,6 +97,30 @@ __device__ __forceinline__ void bw_term(float v, float pre, float m, float is, f
   sx += dz * ((pre - m) * is);
 }
 
+// ---- deterministic BN statistics ----
+// Every producer block adds its fp32 partial (sum, sum^2) of a column into a per-column
+// fixed-point accumulator with integer atomics.  Integer adds commute, so the total does not
+// depend on block order (bit-deterministic), and no finalize pass over per-block partials is
+// needed: the consumer reads the C totals directly.  Value v is held as v * 2^48 split into two
+// int64 words, hi = floor(v * 2^16) and lo = frac(v * 2^16) * 2^32 (resolution 2^-48 ~ 3.6e-15
+// absolute; |v| < 2^47 / blocks).  Layout per group: acc[4c + {0,1}] = sum, acc[4c + {2,3}] = sum^2.
+// Same-line atomics serialise, so producers spread over nsh (power of 2) shards by row-block
+// (shard = rb & (nsh-1), shard stride sh words); the consumer adds the shards as integers.
+typedef unsigned long long u64;
+__device__ __forceinline__ void fx_add(u64* p, float v) {
+  const double d = (double)v * 65536.0;  // exact
+  const double fl = floor(d);
+  atomicAdd(p, (u64)(long long)fl);
+  atomicAdd(p + 1, (u64)((d - fl) * 4294967296.0));
+}
+__device__ __forceinline__ double fx_get(const u64* p) {
+  return (double)(long long)p[0] * (1.0 / 65536.0) + (double)p[1] * (1.0 / 281474976710656.0);
+}
+__device__ __forceinline__ void stat_put(u64* acc, int c, float s, float q) {
+  fx_add(acc + 4 * c, s);
+  fx_add(acc + 4 * c + 2, q);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

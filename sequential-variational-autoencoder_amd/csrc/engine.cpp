@@ -364,11 +364,15 @@ struct svae_ctx {
   float* denc[8];
   float *sfc_part, *dz, *dhead;
   float *idb, *ida, *idpre;  // inference bwd: [T] x max level slab
-  float *part, *ab, *slab;
+  float* slab;
+  // BN statistics: fixed-point column accumulators (common.h stat_put), one region per BN
+  // instance of a pass, handed out in launch order and zeroed once per pass (acc_reset)
+  u64* bnacc = nullptr;
+  long long bnacc_cap = 0, bnacc_used = 0, bnacc_hw = -1;
   void *wN = nullptr, *wT = nullptr;   // bf16 weight shadows (dtype=1)
   void *tiles_d = nullptr, *offs_d = nullptr;
   int ntiles = 0;
-  long long part_cap, slab_cap, ab_cap;
+  long long slab_cap;
   const float* x_in = nullptr;
   const float* tgt_in = nullptr;
   const float* eps_in = nullptr;
@@ -402,6 +406,44 @@ static int fail(svae_ctx* c, int code, const std::string& msg) {
     hipError_t e_ = (x);                                                                     \
     if (e_ != hipSuccess) return fail(ctx, SVAE_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
   } while (0)
+
+// BN accumulator regions: acc_reset zeroes what the previous passes used (all of it the
+// first time) with one memset; acc_take hands out the next region of n words
+static int acc_reset(svae_ctx* c) {
+  const long long n = c->bnacc_hw < 0 ? c->bnacc_cap : c->bnacc_hw;
+  if (n > 0) HIPCHK(c, hipMemsetAsync(c->bnacc, 0, (size_t)n * sizeof(u64), c->st));
+  c->bnacc_used = 0;
+  c->bnacc_hw = 0;
+  return 0;
+}
+static u64* acc_take(svae_ctx* c, long long n) {
+  if (c->bnacc_used + n > c->bnacc_cap) return nullptr;
+  u64* p = c->bnacc + c->bnacc_used;
+  c->bnacc_used += (n + 31) / 32 * 32;
+  if (c->bnacc_used > c->bnacc_hw) c->bnacc_hw = c->bnacc_used;
+  return p;
+}
+
+// the accumulators of one BN instance: groups x 4C words per shard, shards by row-block count
+struct AccR {
+  u64* p = nullptr;
+  long long gs = 0, sh = 0;
+  int nsh = 1;
+};
+static AccR acc_bn(svae_ctx* c, int groups, int C, long long rowblocks) {
+  AccR r;
+  r.nsh = bn_acc_shards(rowblocks);
+  r.gs = 4LL * C;
+  r.sh = ((long long)groups * r.gs + 31) / 32 * 32;
+  r.p = acc_take(c, r.sh * r.nsh);
+  return r;
+}
+static void set_stats(FwdArgs& a, const AccR& r) {
+  a.stats = r.p;
+  a.s_gs = r.gs;
+  a.s_sh = r.sh;
+  a.s_nsh = r.nsh;
+}
 
 // ---------------------------------------------------------------------------
 // layer helpers
@@ -519,8 +561,9 @@ static int gemm(svae_ctx* c, FwdArgs a, int groups) {
   }
   a.ksplit = 1;
   igemm_fwd(a, groups, c->st);
-  return nrb_of(a);
+  return 0;
 }
+// stats row-blocks the GEMM will use (accumulator sharding)
 static int gemm_nrb(svae_ctx* c, FwdArgs a, int groups) {
   if (c->m.g.bf16 && a.Bh) {
     a.part = c->slab;
@@ -560,15 +603,13 @@ static int conv_bn_act_fwd(svae_ctx* c, const ConvL& L, int groups, long long w_
     a.Bh = L.tr ? shadowN(c, L.ow) : shadowT(c, L.ow);
     a.ldb = L.cin;
   }
-  const int nrb = gemm_nrb(c, a, groups);
-  if ((long long)groups * nrb * 2 * L.cout > c->part_cap) return fail(c, SVAE_EBADARG, "stats scratch too small");
-  a.stats = c->part;
-  a.s_gs = (long long)nrb * 2 * L.cout;
+  const AccR acc = acc_bn(c, groups, L.cout, gemm_nrb(c, a, groups));
+  if (!acc.p) return fail(c, SVAE_EBADARG, "BN accumulator arena too small");
+  set_stats(a, acc);
   gemm(c, a, groups);
   const long long rows = (long long)B * L.hout * L.hout;
-  bn_finalize(c->part, a.s_gs, nrb, L.cout, rows, 1e-3f, bn.mean, bn.invstd, bn_gs, groups, c->st);
-  bn_apply(pre, L.cout, pre_gs, rows, L.cout, bn.mean, bn.invstd, bn_gs, c->P + L.obeta, w_gs, res.p, res.ld, res.gs,
-           act, out.p, out.ld, out.gs, groups, c->st);
+  bn_apply(pre, L.cout, pre_gs, rows, L.cout, acc.p, acc.gs, acc.sh, acc.nsh, 1e-3f, bn.mean, bn.invstd, bn_gs, c->P + L.obeta, w_gs,
+           res.p, res.ld, res.gs, act, out.p, out.ld, out.gs, groups, c->st);
   return 0;
 }
 
@@ -667,7 +708,7 @@ static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, V
 // bn_act_bwd then skips bn_bwd_reduce (one full read of dy and pre less per layer).
 struct BwFuse {
   BwStat bw{};
-  int nrb = 0;
+  AccR acc;  // accumulators the fused epilogue adds into
   bool used = false;
 };
 static BwFuse bw_fuse(svae_ctx* c, const float* pre, int ldp, long long pre_gs, const float* y, int ldy, long long y_gs,
@@ -738,15 +779,11 @@ static int conv_dgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, c
     }();
     if (fu && fu->bw.pre && fu->bw.C % 4 == 0 && !nofuse) {
       a.bw = fu->bw;
-      const int nrb = gemm_nrb(c, a, groups);
-      if ((long long)groups * nrb * 2 * fu->bw.C <= c->part_cap) {
-        a.stats = c->part;
-        a.s_gs = (long long)nrb * 2 * fu->bw.C;
-        fu->nrb = nrb;
-        fu->used = true;
-      } else {
-        a.bw = BwStat{};
-      }
+      const AccR acc = acc_bn(c, groups, fu->bw.C, gemm_nrb(c, a, groups));
+      if (!acc.p) return fail(c, SVAE_EBADARG, "BN accumulator arena too small");
+      set_stats(a, acc);
+      fu->acc = acc;
+      fu->used = true;
     }
   }
   gemm(c, a, groups);
@@ -757,20 +794,18 @@ static int conv_dgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, c
 static int bn_act_bwd(svae_ctx* c, int groups, long long rows, int C, View dy, View y, const float* pre, long long pre_gs,
                       int ldp, BNS bn, long long bn_gs, long long beta_off, long long w_gs, int act, float* dpre,
                       long long dpre_gs, View dres, int res_acc, const BwFuse* fu = nullptr) {
-  const bool pre_reduced = fu && fu->used;  // partials already in c->part (fused dgrad epilogue)
-  const int nrb = pre_reduced ? fu->nrb : bn_bwd_rowblocks(rows, C);
-  if ((long long)groups * nrb * 2 * C > c->part_cap) return fail(c, SVAE_EBADARG, "bn bwd scratch too small");
-  if ((long long)groups * 2 * C > c->ab_cap) return fail(c, SVAE_EBADARG, "ab scratch too small");
-  const long long pgs = (long long)nrb * 2 * C;
+  const bool pre_reduced = fu && fu->used;  // sums already added by the fused dgrad epilogue
+  const AccR acc = pre_reduced ? fu->acc : acc_bn(c, groups, C, bn_bwd_rowblocks(rows));
+  if (!acc.p) return fail(c, SVAE_EBADARG, "BN accumulator arena too small");
   // without a shortcut add, act'(y) follows from the recomputed BN output: y is not read
   const float* yp = (dres.p || !c->P) ? y.p : nullptr;  // (per-op entry: no beta, reads y)
   const float* beta = c->P + beta_off;
   if (!pre_reduced)
     bn_bwd_reduce(dy.p, dy.ld, dy.gs, yp, y.ld, y.gs, pre, ldp, pre_gs, rows, C, bn.mean, bn.invstd, bn_gs, beta, w_gs,
-                  act, c->part, pgs, groups, c->st);
-  bn_bwd_finalize(c->part, pgs, nrb, C, rows, c->ab, 2LL * C, c->Gr + beta_off, w_gs, groups, c->st);
+                  act, acc.p, acc.gs, acc.sh, acc.nsh, groups, c->st);
   bn_bwd_apply(dy.p, dy.ld, dy.gs, yp, y.ld, y.gs, pre, ldp, pre_gs, rows, C, bn.mean, bn.invstd, bn_gs, beta, w_gs,
-               c->ab, 2LL * C, act, dpre, C, dpre_gs, dres.p, dres.ld, dres.gs, res_acc, groups, c->st);
+               acc.p, acc.gs, acc.sh, acc.nsh, c->Gr + beta_off, w_gs, act, dpre, C, dpre_gs, dres.p, dres.ld, dres.gs, res_acc, groups,
+               c->st);
   return 0;
 }
 
@@ -788,14 +823,12 @@ static int fc_bn_fwd(svae_ctx* c, const FcL& f, View in, float* pre, BNS bn, Vie
     a.Bh = shadowT(c, f.ow);  // [out][in]
     a.ldb = f.nin;
   }
-  const int nrb = gemm_nrb(c, a, 1);
-  if ((long long)nrb * 2 * f.nout > c->part_cap) return fail(c, SVAE_EBADARG, "stats scratch too small");
-  a.stats = c->part;
-  a.s_gs = (long long)nrb * 2 * f.nout;
+  const AccR acc = acc_bn(c, 1, f.nout, gemm_nrb(c, a, 1));
+  if (!acc.p) return fail(c, SVAE_EBADARG, "BN accumulator arena too small");
+  set_stats(a, acc);
   gemm(c, a, 1);
-  bn_finalize(c->part, 0, nrb, f.nout, B, 1e-3f, bn.mean, bn.invstd, 0, 1, c->st);
-  bn_apply(pre, f.nout, 0, B, f.nout, bn.mean, bn.invstd, 0, c->P + f.obeta, 0, nullptr, 0, 0, ACT_LRELU, out.p, out.ld,
-           0, 1, c->st);
+  bn_apply(pre, f.nout, 0, B, f.nout, acc.p, acc.gs, acc.sh, acc.nsh, 1e-3f, bn.mean, bn.invstd, 0, c->P + f.obeta, 0, nullptr, 0, 0,
+           ACT_LRELU, out.p, out.ld, 0, 1, c->st);
   return 0;
 }
 
@@ -846,6 +879,7 @@ static int engine_forward(svae_ctx* c) {
   hipStream_t st = c->st;
   int r;
 
+  if ((r = acc_reset(c))) return r;
   if (g.bf16) shadow_weights(c->P, c->wN, c->wT, M.n_live, c->tiles_d, c->ntiles, c->offs_d, st);
   if (c->generative) {
     // generative mode (sequential_vae.py:947-952, :1025 latent_generative = self.latents[t]):
@@ -1013,6 +1047,7 @@ static int engine_backward(svae_ctx* c) {
   hipStream_t st = c->st;
   int r;
 
+  if ((r = acc_reset(c))) return r;
   HIPCHK(c, hipMemsetAsync(c->dz, 0, (size_t)T * B * g.Dz * sizeof(float), st));
   if (c->side) {  // the side stream starts after the forward (and anything before it)
     hipEventRecord(c->ev_start, st);
@@ -1054,7 +1089,7 @@ static int engine_backward(svae_ctx* c) {
         wgemm(c, w, 1);
         wgrad_reduce(c->slab, 0, w.nsplit, 16, M_out, F[1], c->Gr + G.owout, 0, g.C,
                      t >= 1 ? c->Gr + G.owratio : nullptr, 0, 0, 1, c->st);
-        // output / ratio bias gradients (own scratch: c->part belongs to the main stream's BN)
+        // output / ratio bias gradients (own scratch)
         colsum_small(c->da, C1, P0, M_out, c->cs_part, c->Gr + G.obout, g.C, t >= 1 ? c->Gr + G.obratio : nullptr,
                      c->st);
         return 0;
@@ -1347,10 +1382,8 @@ static bool plan(svae_ctx* c) {
   c->ida = A((long long)T * max_inf);
   c->idpre = A((long long)T * max_inf);
   for (int i = 0; i < 2; ++i) c->idpre_ring[i] = A((long long)T * max_inf);
-  c->part_cap = (long long)T * (maxact / 16 + 65536) + 8LL * 2 * (maxJ + 8192);
-  c->part = A(c->part_cap);
-  c->ab_cap = (long long)T * 2 * 65536;
-  c->ab = A(c->ab_cap);
+  c->bnacc_cap = 8LL << 20;  // words (64 MB); a CelebA pass takes a few M
+  c->bnacc = (u64*)A(2 * c->bnacc_cap);
   c->slab_cap = 64LL << 20;
   c->slab = A(c->slab_cap);
   c->slab2 = A(c->slab_cap);
@@ -1650,7 +1683,6 @@ int svae_copy_out(svae_ctx* c, int which, int step, float* dst, int64_t n, void*
     case 109: src = c->dpre; cnt = n; break;
     case 110: src = c->dbg_last; cnt = n; break;
     case 111: c->dbg_stop_lvl2 = step; return 0;
-    case 112: src = c->ab; cnt = n; break;
     case 113: src = c->inf_pre_a[step]; cnt = n; break;   // debug: inference level `step`, all T groups
     case 114: src = c->inf_act_a[step]; cnt = n; break;
     case 115: src = c->inf_pre_b[step]; cnt = n; break;
@@ -1763,16 +1795,17 @@ int svae_op_bn_act(const float* x, int64_t rows, int c, const float* beta, int a
                    float* invstd, void* scratch, int64_t scratch_bytes, void* stream) {
   if (!x || !beta || !y || !mean || !invstd || !scratch || c % 4) return fail(nullptr, SVAE_EBADARG, "bad op args");
   hipStream_t s = (hipStream_t)stream;
-  const int nrb = bn_bwd_rowblocks(rows, c);
-  if ((int64_t)nrb * 2 * c * 4 + 2 * c * 4 > scratch_bytes) return fail(nullptr, SVAE_EBADARG, "scratch too small");
-  float* part = (float*)scratch;
-  float* zi = part + (long long)nrb * 2 * c;  // zeros (mean) / ones (invstd) for the raw-moment reduction
+  const int nsh = bn_acc_shards(bn_bwd_rowblocks(rows));
+  if ((int64_t)nsh * 4 * c * 8 + 2 * c * 4 > scratch_bytes) return fail(nullptr, SVAE_EBADARG, "scratch too small");
+  u64* acc = (u64*)scratch;
+  float* zi = (float*)(acc + (long long)nsh * 4 * c);  // zeros (mean) / ones (invstd): raw-moment reduction
+  if (hipMemsetAsync(acc, 0, (size_t)nsh * 4 * c * sizeof(u64), s) != hipSuccess)
+    return fail(nullptr, SVAE_EHIP, "hipMemsetAsync");
   fill_f32(zi, c, 0.f, s);
   fill_f32(zi + c, c, 1.f, s);
   // sum(x), sum(x^2) via the backward reducer with act=none, mean=0, invstd=1
-  bn_bwd_reduce(x, c, 0, x, c, 0, x, c, 0, rows, c, zi, zi + c, 0, nullptr, 0, ACT_NONE, part, 0, 1, s);
-  bn_finalize(part, 0, nrb, c, rows, 1e-3f, mean, invstd, 0, 1, s);
-  bn_apply(x, c, 0, rows, c, mean, invstd, 0, beta, 0, nullptr, 0, 0, act, y, c, 0, 1, s);
+  bn_bwd_reduce(x, c, 0, x, c, 0, x, c, 0, rows, c, zi, zi + c, 0, nullptr, 0, ACT_NONE, acc, 0, 4LL * c, nsh, 1, s);
+  bn_apply(x, c, 0, rows, c, acc, 0, 4LL * c, nsh, 1e-3f, mean, invstd, 0, beta, 0, nullptr, 0, 0, act, y, c, 0, 1, s);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(nullptr, SVAE_EHIP, hipGetErrorString(e));
 }
@@ -1783,12 +1816,11 @@ int svae_op_bn_act_bwd(const float* dy, const float* y, const float* x, int64_t 
   if (!dy || !y || !x || !dx || !dbeta || !scratch || c % 4) return fail(nullptr, SVAE_EBADARG, "bad op args");
   static svae_ctx dummy;
   dummy.st = (hipStream_t)stream;
-  const int nrb = bn_bwd_rowblocks(rows, c);
-  dummy.part = (float*)scratch;
-  dummy.part_cap = (long long)nrb * 2 * c;
-  dummy.ab = dummy.part + dummy.part_cap;
-  dummy.ab_cap = 2LL * c;
-  if ((dummy.part_cap + dummy.ab_cap) * 4 > scratch_bytes) return fail(nullptr, SVAE_EBADARG, "scratch too small");
+  dummy.bnacc = (u64*)scratch;
+  dummy.bnacc_cap = scratch_bytes / (int64_t)sizeof(u64);
+  dummy.bnacc_hw = 4LL * c * bn_acc_shards(bn_bwd_rowblocks(rows));  // zero just the region this op takes
+  if (dummy.bnacc_hw > dummy.bnacc_cap) return fail(nullptr, SVAE_EBADARG, "scratch too small");
+  if (acc_reset(&dummy)) return fail(nullptr, SVAE_EHIP, dummy.err);
   dummy.Gr = dbeta;
   BNS bn{(float*)mean, (float*)invstd};
   int r = bn_act_bwd(&dummy, 1, rows, c, View{(float*)dy, c, 0}, View{(float*)y, c, 0}, x, 0, c, bn, 0, 0, 0, act, dx,

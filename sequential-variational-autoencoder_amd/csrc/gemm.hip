@@ -311,7 +311,7 @@ __global__ __launch_bounds__(256) void igemm_fwd_kernel(FwdArgs a) {
     }
   }
   if (a.stats) {
-    // per-column partial (sum, sum^2) of this block's valid rows -> stats[rowblock][2][N]
+    // per-column partial (sum, sum^2) of this block's valid rows -> fixed-point accumulators
     float* red = &As[0][0];  // reuse: [WM][BN] sums then [WM][BN] squares
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
@@ -333,10 +333,8 @@ __global__ __launch_bounds__(256) void igemm_fwd_kernel(FwdArgs a) {
         float s = 0.f, q = 0.f;
 #pragma unroll
         for (int w = 0; w < WM; ++w) { s += red[w * BN + tid]; q += red[WM * BN + w * BN + tid]; }
-        const long long rb_idx = (long long)cls * gridDim.x + blockIdx.x;
-        float* st = a.stats + group * a.s_gs + rb_idx * 2 * a.N;
-        st[n] = s;
-        st[a.N + n] = q;
+        const int rb = cls * gridDim.x + blockIdx.x;
+        stat_put(a.stats + (rb & (a.s_nsh - 1)) * a.s_sh + group * a.s_gs, n, s, q);
       }
     }
   }

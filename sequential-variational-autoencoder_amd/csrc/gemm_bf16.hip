@@ -331,10 +331,8 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
         float s = 0.f, q = 0.f;
 #pragma unroll
         for (int w = 0; w < WM; ++w) { s += red[w * BN + tid]; q += red[WM * BN + w * BN + tid]; }
-        const long long rb_idx = (long long)cls * gridDim.x + blk.x;  // ks == 1 here
-        float* st = a.stats + group * a.s_gs + rb_idx * 2 * SC;
-        st[n] = s;
-        st[SC + n] = q;
+        const int rb = cls * gridDim.x + blk.x;
+        stat_put(a.stats + (rb & (a.s_nsh - 1)) * a.s_sh + group * a.s_gs, n, s, q);
       }
     }
   }
@@ -622,10 +620,8 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kernel(HaloArgs h) {
         float s = 0.f, q = 0.f;
 #pragma unroll
         for (int w = 0; w < WM; ++w) { s += red[w * BN + tid]; q += red[WM * BN + w * BN + tid]; }
-        const long long rb_idx = (long long)cls * gridDim.x + blk.x;  // ks == 1 here
-        float* st = a.stats + group * a.s_gs + rb_idx * 2 * SC;
-        st[n] = s;
-        st[SC + n] = q;
+        const int rb = cls * gridDim.x + blk.x;
+        stat_put(a.stats + (rb & (a.s_nsh - 1)) * a.s_sh + group * a.s_gs, n, s, q);
       }
     }
   }
@@ -1028,12 +1024,12 @@ __global__ __launch_bounds__(256) void shadow_t_kernel(const float* w, __bf16* o
 // launchers
 // ---------------------------------------------------------------------------
 // sum the K-split slabs; bias / act / accumulate into C; per-column (sum, sum^2) of the
-// raw sums per 256-row block -> stats[rb][2][N]  (same contract as the GEMM epilogue)
+// raw sums per 64-row block -> fixed-point column accumulators (same contract as the GEMM epilogue)
 #define SKR_ROWS 64
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* part, int ks, int rows_total, int N,
                                                             float* C, long long c_gs, int ldc, const float* bias,
-                                                            long long bias_gs, int act, int accumulate, float* stats,
-                                                            long long s_gs, BwStat bw) {
+                                                            long long bias_gs, int act, int accumulate, u64* stats,
+                                                            long long s_gs, long long s_sh, int s_nsh, BwStat bw) {
   __shared__ f32x4 red[2][256];
   const int group = blockIdx.z;
   const int qi = threadIdx.x & 15, rl = threadIdx.x >> 4;
@@ -1085,14 +1081,17 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* part, i
   red[1][threadIdx.x] = s2;
   __syncthreads();
   const int SC = bw.pre ? bw.C : N;  // stats columns (row-block stride 2*SC)
-  if (rl == 0 && n < SC) {
-    for (int j = 1; j < 16; ++j) {
-      s1 += red[0][j * 16 + qi];
-      s2 += red[1][j * 16 + qi];
+  // one (column, sum|sum^2) per thread: the row lanes are combined in a fixed order and the
+  // atomics issue in parallel
+  if (threadIdx.x < 128) {
+    const int cc = threadIdx.x & 63, kind = threadIdx.x >> 6, qq = cc >> 2, e = cc & 3;
+    const int n2 = blockIdx.x * 64 + cc;
+    if (n2 < SC) {
+      float v = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v += red[kind][j * 16 + qq][e];
+      fx_add(stats + (blockIdx.y & (s_nsh - 1)) * s_sh + group * s_gs + 4LL * n2 + 2 * kind, v);
     }
-    float* st = stats + group * s_gs + (long long)blockIdx.y * 2 * SC;
-    *(f32x4*)(st + n) = s1;
-    *(f32x4*)(st + SC + n) = s2;
   }
 }
 
@@ -1318,7 +1317,7 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
       if (hp.ks > 1) {
         dim3 grid((a.N + 63) / 64, hp.nrb, groups);
         hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, s, a.part, hp.ks, a.rows_total, a.N, a.C, a.c_gs,
-                           a.ldc, a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs, a.bw);
+                           a.ldc, a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs, a.s_sh, a.s_nsh, a.bw);
       }
       return hp.nrb;
     }
@@ -1338,7 +1337,7 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
   if (ks > 1) {
     dim3 grid((a.N + 63) / 64, nrb, groups);
     hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, s, a.part, ks, a.rows_total, a.N, a.C, a.c_gs, a.ldc,
-                       a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs, a.bw);
+                       a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs, a.s_sh, a.s_nsh, a.bw);
   }
   return nrb;
 }

@@ -5,7 +5,7 @@
 // Backward-BN reductions fused into the epilogue of the GEMM that produces dy (bf16 kernels):
 // with dz = dy * act'(y), the epilogue emits per-row-block partials [rb][2C] = (sum dz,
 // sum dz*xhat) over columns [0, C) of its final output (after accumulate) into FwdArgs::stats,
-// exactly what bn_bwd_reduce would write.  pre == nullptr: off.
+// exactly what bn_bwd_reduce would add (fixed-point accumulators, common.h stat_put).  pre == nullptr: off.
 struct BwStat {
   const float* pre; int ldp; long long pre_gs;
   const float* y; int ldy; long long y_gs;      // shortcut layers: act' from the stored output
@@ -20,7 +20,8 @@ struct FwdArgs {
   const float* B; long long b_gs; int ldb; long long b_tap; int b_nk;
   const void* Bh;                         // bf16 NK weights (bf16 kernels only)
   float* C; long long c_gs; int ldc;
-  float* stats; long long s_gs;           // per-column partial (sum,sum^2): [rowblock][2][N]
+  u64* stats; long long s_gs;             // per-column fixed-point (sum,sum^2) accumulators [4*N] (common.h stat_put)
+  long long s_sh; int s_nsh;              // accumulator shards: row-block rb adds into shard rb & (s_nsh-1)
   const float* bias; long long bias_gs;
   int N, Cin;
   ConvGeom g;
@@ -112,29 +113,30 @@ void wgrad_reduce(const float* part, long long p_gs, int nsplit, int ntap, int M
                   hipStream_t s);
 
 // ---- BatchNorm (training mode, beta only, eps 1e-3: abstract_network.py:22) ----
-// stats partial [nrb][2][C] -> mean[C], invstd[C]
-void bn_finalize(const float* part, long long part_gs, int nrb, int C, long long count, float eps, float* mean,
-                 float* invstd, long long ms_gs, int groups, hipStream_t s);
-// out = act((pre - mean)*invstd + beta [+ res])
-void bn_apply(const float* pre, int ldp, long long pre_gs, long long rows, int C, const float* mean,
-              const float* invstd, long long ms_gs, const float* beta, long long beta_gs, const float* res,
-              int ldr, long long res_gs, int act, float* out, int ldo, long long out_gs, int groups,
+// Statistics arrive as fixed-point column accumulators acc[group][4*C] (common.h stat_put),
+// added by the producing GEMM epilogue (or bn_bwd_reduce); the apply kernels finalise them.
+// out = act((pre - mean)*invstd + beta [+ res]).  acc != nullptr: mean/invstd are computed from
+// acc (count rows, eps) and written to mean/invstd for the backward; acc == nullptr: read them.
+// Accumulators: acc[shard][group][4*C], shard stride sh words, nsh shards.
+int bn_acc_shards(long long rowblocks);
+void bn_apply(const float* pre, int ldp, long long pre_gs, long long rows, int C, const u64* acc, long long acc_gs,
+              long long sh, int nsh, float eps, float* mean, float* invstd, long long ms_gs, const float* beta, long long beta_gs,
+              const float* res, int ldr, long long res_gs, int act, float* out, int ldo, long long out_gs, int groups,
               hipStream_t s);
-// partial sums of dz and dz*xhat, dz = dy*act'(y)   -> part [nrb][2][C]; returns nrb via out param
-int bn_bwd_rowblocks(long long rows, int C);
+// sums of dz and dz*xhat, dz = dy*act'(y)   -> added into acc[group][4*C]
 void bn_bwd_reduce(const float* dy, int lddy, long long dy_gs, const float* y, int ldy, long long y_gs,
                    const float* pre, int ldp, long long pre_gs, long long rows, int C, const float* mean,
-                   const float* invstd, long long ms_gs, const float* beta, long long beta_gs, int act, float* part,
-                   long long part_gs, int groups, hipStream_t s);
-// per-channel: a = sum(dz)/n, b = sum(dz*xhat)/n, dbeta = sum(dz)
-void bn_bwd_finalize(const float* part, long long part_gs, int nrb, int C, long long count, float* ab,
-                     long long ab_gs, float* dbeta, long long dbeta_gs, int groups, hipStream_t s);
-// dpre = invstd*(dz - a - xhat*b); optional dres (+)= dz
+                   const float* invstd, long long ms_gs, const float* beta, long long beta_gs, int act, u64* acc,
+                   long long acc_gs, long long sh, int nsh, int groups, hipStream_t s);
+int bn_bwd_rowblocks(long long rows);
+// dpre = invstd*(dz - a - xhat*b), a = sum(dz)/n, b = sum(dz*xhat)/n from acc; dbeta = sum(dz);
+// optional dres (+)= dz
 void bn_bwd_apply(const float* dy, int lddy, long long dy_gs, const float* y, int ldy, long long y_gs,
                   const float* pre, int ldp, long long pre_gs, long long rows, int C, const float* mean,
-                  const float* invstd, long long ms_gs, const float* beta, long long beta_gs, const float* ab,
-                  long long ab_gs, int act, float* dpre, int lddp, long long dpre_gs, float* dres, int ldres,
-                  long long dres_gs, int res_acc, int groups, hipStream_t s);
+                  const float* invstd, long long ms_gs, const float* beta, long long beta_gs, const u64* acc,
+                  long long acc_gs, long long sh, int nsh, float* dbeta, long long dbeta_gs, int act, float* dpre, int lddp,
+                  long long dpre_gs, float* dres, int ldres, long long dres_gs, int res_acc, int groups,
+                  hipStream_t s);
 
 // ---- split_latent FC(K=Dl) + BN over batch + lrelu, fused (sequential_vae.py:1801-1806) ----
 // out[n][j] written at out + n*o_n + (j / F)*ldo + (j % F)

@@ -197,9 +197,7 @@ __global__ __launch_bounds__(256) void conv_smallc_kernel(FwdArgs a) {
     if (tid < N) {
       const float s = ((red[0][0][tid] + red[0][1][tid]) + red[0][2][tid]) + red[0][3][tid];
       const float q = ((red[1][0][tid] + red[1][1][tid]) + red[1][2][tid]) + red[1][3][tid];
-      float* st = a.stats + group * a.s_gs + (long long)blockIdx.x * 2 * N;
-      st[tid] = s;
-      st[N + tid] = q;
+      stat_put(a.stats + (blockIdx.x & (a.s_nsh - 1)) * a.s_sh + group * a.s_gs, tid, s, q);
     }
   }
 }
