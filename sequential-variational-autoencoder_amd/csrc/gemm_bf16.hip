@@ -654,7 +654,7 @@ __device__ __forceinline__ bf16x8 join_tr(v4i16 lo, v4i16 hi) {
 }
 
 template <int BN, int S>
-__global__ __launch_bounds__(256) void wgrad_halo_kernel(WHaloArgs h) {
+__global__ __launch_bounds__(256, BN == 32 ? 2 : 1) void wgrad_halo_kernel(WHaloArgs h) {
   constexpr int NS = BN / 32;              // 32-column MFMA subtiles
   constexpr int GP = S == 1 ? 32 : 48;     // window pixel pitch (bf16)
   extern __shared__ __attribute__((aligned(16))) __bf16 wsm[];
@@ -704,35 +704,54 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(WHaloArgs h) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int lgR = h.lgImgPix - h.lgWo;
-  for (int c = cbeg; c < cend; ++c) {
+  // Chunk c+1's G window and D rows are loaded into registers while chunk c computes (one
+  // chunk of MFMA work hides the HBM latency); they are converted and stored to LDS after the
+  // chunk's closing barrier.
+  f32x4 gv[WH_WPI], dv[WH_DPI];
+  auto load_chunk = [&](int c) {
     const int row0 = c * h.CP;
     const int img0 = row0 / per_img;
     const int ry0 = (row0 - img0 * per_img) >> h.lgWo;
     const int iy0 = ry0 * S - g.pad;  // input row of window row 0
-    // ---- stage the G window (fp32 -> bf16, pixel-major) ----
     const float* Gc = G + ((long long)img0 * g.Hi + iy0) * g.Wi * a.ldg;
 #pragma unroll
     for (int i = 0; i < WH_WPI; ++i) {
-      if (wpr[i] == -1) continue;
-      const int it = tid + 256 * i;
+      gv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       const int iy = iy0 + wpr[i];
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (wpr[i] >= 0 && iy >= 0 && iy < g.Hi) v = *(const f32x4*)(Gc + wrel[i]);
-      *(bf16x4*)&Gw[(it >> 3) * GP + (it & 7) * 4] = __builtin_convertvector(v, bf16x4);
+      if (wpr[i] >= 0 && iy >= 0 && iy < g.Hi) gv[i] = *(const f32x4*)(Gc + wrel[i]);
     }
-    // ---- stage the D rows of the chunk ----
     const float* Dc = D + (long long)row0 * a.ldd + n0;
 #pragma unroll
     for (int i = 0; i < WH_DPI; ++i) {
       const int it = tid + 256 * i;
       if (it < h.CP * (BN / 4)) {
         const int k = it / (BN / 4), slot = it - k * (BN / 4);
-        const f32x4 v = *(const f32x4*)(Dc + (long long)k * a.ldd + slot * 4);
-        const int sw = BN == 64 ? (slot ^ (((k >> 1) & 1) << 3)) : slot;
-        *(bf16x4*)&Dt[k * BN + sw * 4] = __builtin_convertvector(v, bf16x4);
+        dv[i] = *(const f32x4*)(Dc + (long long)k * a.ldd + slot * 4);
       }
     }
+  };
+  auto store_chunk = [&]() {
+#pragma unroll
+    for (int i = 0; i < WH_WPI; ++i) {
+      if (wpr[i] == -1) continue;
+      const int it = tid + 256 * i;
+      *(bf16x4*)&Gw[(it >> 3) * GP + (it & 7) * 4] = __builtin_convertvector(gv[i], bf16x4);
+    }
+#pragma unroll
+    for (int i = 0; i < WH_DPI; ++i) {
+      const int it = tid + 256 * i;
+      if (it < h.CP * (BN / 4)) {
+        const int k = it / (BN / 4), slot = it - k * (BN / 4);
+        const int sw = BN == 64 ? (slot ^ (((k >> 1) & 1) << 3)) : slot;
+        *(bf16x4*)&Dt[k * BN + sw * 4] = __builtin_convertvector(dv[i], bf16x4);
+      }
+    }
+  };
+  if (cbeg < cend) load_chunk(cbeg);
+  for (int c = cbeg; c < cend; ++c) {
+    store_chunk();
     __syncthreads();
+    if (c + 1 < cend) load_chunk(c + 1);
     // ---- K steps of 16 pixels ----
     for (int kk = 0; kk < h.CP / 16; ++kk) {
       int wp[2], kr[2];
@@ -1118,6 +1137,16 @@ struct HaloPlan {
 };
 #define HALO_LDS_MAX (80 * 1024)  // two blocks per CU
 
+// the large tile is kept only when it fills this many blocks; below it the smaller tile (no or
+// less split-K) wins (tools/bench_gather.py: 16x16 / 8x8 conv-T layers).  SVAE_HALO_FILL overrides.
+static int halo_fill() {
+  static const int v = [] {
+    const char* e = getenv("SVAE_HALO_FILL");
+    return e ? atoi(e) : 512;
+  }();
+  return v;
+}
+
 static HaloPlan halo_plan(const FwdArgs& a, int groups) {
   HaloPlan p;
   const ConvGeom& g = a.g;
@@ -1134,7 +1163,11 @@ static HaloPlan halo_plan(const FwdArgs& a, int groups) {
   const int bn = a.N <= 32 ? 32 : (a.N <= 64 ? 64 : 128);
   const int cands[2] = {bn == 32 ? 256 : 128, bn == 32 ? 128 : 64};
   const int per_img = Hr * Wr;
-  for (int ci = 0; ci < 2; ++ci) {
+  static const bool small_only = [] {
+    const char* v = getenv("SVAE_HALO_SMALL");
+    return v && v[0] == '1';
+  }();
+  for (int ci = small_only ? 1 : 0; ci < 2; ++ci) {
     const int bm = cands[ci];
     if (bm % Wr != 0 || a.rows % bm != 0) continue;
     if (!(per_img % bm == 0 || bm % per_img == 0)) continue;
@@ -1151,7 +1184,7 @@ static HaloPlan halo_plan(const FwdArgs& a, int groups) {
     const size_t lds = (size_t)(2 * h.npix) * ROWP * sizeof(__bf16);
     if (lds > HALO_LDS_MAX) continue;
     const long long blocks = (long long)(a.rows / bm) * ((a.N + bn - 1) / bn) * a.nclass * groups;
-    if (ci == 0 && blocks < 256) {  // prefer the smaller tile when the large one underfills
+    if (ci == 0 && blocks < halo_fill()) {  // prefer the smaller tile when the large one underfills
       const int bm2 = cands[1];
       if (bm2 % Wr == 0 && a.rows % bm2 == 0 && (per_img % bm2 == 0 || bm2 % per_img == 0)) {
         const int R2 = bm2 >= per_img ? Hr : bm2 / Wr, n2 = bm2 >= per_img ? bm2 / per_img : 1;
