@@ -156,6 +156,8 @@ def main():
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="N>1: one all-reduce after the backward instead of per-step buckets during it")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -177,8 +179,11 @@ def main():
     cfg = cfgmod.preset(args.config, **over)
     cfgname = cfgmod.NETNAMES.get(args.config, args.config)
     B = cfg.batch
-    hook = par.allreduce_hook(dist) if world > 1 else None
+    overlap = world > 1 and not args.no_overlap
+    hook = par.allreduce_hook(dist) if world > 1 and not overlap else None
     net = SV(cfg, seed=0, grad_hook=hook)
+    if overlap:  # per-step gradient buckets all-reduced (RCCL) while the earlier steps' backward runs
+        net.enable_overlapped_allreduce(dist)
 
     g = torch.Generator(device="cuda")
     g.manual_seed(1234 + rank)
@@ -279,7 +284,8 @@ def main():
             "config": {"workload": METRIC[cfgname][1],
                        "model": args.config, "global_batch": B * world, "per_gpu_batch": B,
                        "image": [cfg.height, cfg.width, cfg.channels], "mc_steps": cfg.mc_steps,
-                       "parallelism": "dp%d" % world},
+                       "parallelism": "dp%d" % world,
+                       "grad_allreduce": ("per-step buckets overlapped with the backward" if overlap else "one call after the backward") if world > 1 else None},
             "elbo_per_img": round(elbo, 5),
             "flops_per_img": flops_img,
             "roofline": roof,

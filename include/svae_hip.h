@@ -98,6 +98,15 @@ int svae_forward(svae_ctx* ctx, const float* x, const float* target, const float
  * state (svae_backward needs a new svae_forward). */
 int svae_generate(svae_ctx* ctx, const float* z, void* stream);
 int svae_backward(svae_ctx* ctx, void* stream);
+/* Data-parallel hook (no reference counterpart; the reference has no collective).  During
+ * svae_backward, hook(user, t) is called on the host after the backward of chain step t is
+ * enqueued (t = T-1 .. 0): at that point svae_hook_stream(ctx) is ordered after every kernel of
+ * that step, so a collective enqueued on it reduces the step's complete generator/encoder
+ * gradients while the earlier steps' backward still runs.  hook(user, -1) follows the whole
+ * backward (recognition gradients complete, on the caller's stream).  NULL hook: off. */
+typedef void (*svae_step_hook)(void* user, int t);
+int svae_set_backward_hook(svae_ctx* ctx, svae_step_hook hook, void* user);
+void* svae_hook_stream(svae_ctx* ctx);
 /* clip(+-clip) + TF Adam on the live region (sequential_vae.py:1274-1276); step >= 1. */
 int svae_adam(svae_ctx* ctx, float lr, int64_t step, float clip, void* stream);
 /* Copy an internal buffer (device -> caller device pointer). */

@@ -39,6 +39,10 @@ ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 _lib = None
 
 
+# void (*svae_step_hook)(void* user, int t)   (include/svae_hip.h)
+STEP_HOOK = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int)
+
+
 def lib():
     """Load (once) and return the library; raises if it is absent."""
     global _lib
@@ -75,6 +79,8 @@ def lib():
         "svae_probe_end": ([vp, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double),
                             ctypes.POINTER(ctypes.c_double)], i32),
         "svae_kernel_name": ([i32], ctypes.c_char_p),
+        "svae_set_backward_hook": ([vp, STEP_HOOK, vp], i32),
+        "svae_hook_stream": ([vp], vp),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -88,7 +94,8 @@ EXPORTED = ["svae_param_count", "svae_param_layout", "svae_create", "svae_destro
             "svae_bind", "svae_workspace_bytes", "svae_forward", "svae_backward", "svae_adam", "svae_copy_out",
             "svae_op_conv", "svae_op_conv_dgrad", "svae_op_conv_wgrad", "svae_op_bn_act",
             "svae_op_bn_act_bwd", "svae_op_fc", "svae_probe_begin", "svae_probe_end", "svae_kernel_name",
-            "svae_op_gather_bf16", "svae_op_wgrad_bf16", "svae_generate"]
+            "svae_op_gather_bf16", "svae_op_wgrad_bf16", "svae_generate", "svae_set_backward_hook",
+            "svae_hook_stream"]
 
 # bf16 GEMM instance ids (csrc/kernels.h KernelId) for svae_probe_begin
 KID_IGEMM_BF16_256x32 = 2

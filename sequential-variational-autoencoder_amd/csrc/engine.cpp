@@ -318,6 +318,12 @@ struct svae_ctx {
   hipEvent_t ev_ready[NR] = {}, ev_free[NR] = {}, ev_iready[2] = {}, ev_ifree[2] = {};
   hipEvent_t ev_da_ready = nullptr, ev_da_free = nullptr, ev_start = nullptr, ev_join = nullptr;
   int ring_pos = 0, iring_pos = 0;
+  // backward step hook (data-parallel bucketed all-reduce): called on the host after the
+  // backward of chain step t is enqueued, with the side stream ordered after all of that step's
+  // work on both streams; t = -1 after the whole backward (streams joined)
+  svae_step_hook hook = nullptr;
+  void* hook_user = nullptr;
+  hipEvent_t ev_hook = nullptr;
   float* cs_part = nullptr;  // output-bias column-sum partials (side stream)
   bool generative = false;   // svae_generate: chain on caller / prior latents, no recognition
   float* zero_img = nullptr; // [B,H,W,C] zeros: reconstruction target of the generative chain
@@ -866,6 +872,17 @@ static int fc_bn_bwd(svae_ctx* c, const FcL& f, View in, View dy, View y, const 
   return 0;
 }
 
+// host hook after chain step t's backward: the side stream is ordered after all of the step's
+// work on both streams, so a collective issued on it sees that step's complete gradients
+static void step_hook(svae_ctx* c, int t) {
+  if (!c->hook) return;
+  if (c->side) {
+    hipEventRecord(c->ev_hook, c->st);
+    hipStreamWaitEvent(c->st2, c->ev_hook, 0);
+  }
+  c->hook(c->hook_user, t);
+}
+
 // ============================================================================
 // forward
 // ============================================================================
@@ -1054,6 +1071,7 @@ static int engine_backward(svae_ctx* c) {
     hipStreamWaitEvent(c->st2, c->ev_start, 0);
   }
   for (int t = T - 1; t >= 0; --t) {
+    if (t < T - 1) step_hook(c, t + 1);  // step t+1's gradients are complete
     if (t < c->dbg_stop_step) return 0;  // debug: stop after step dbg_stop_step
     svae_ctx::StepBufs& s = c->sb[t];
     const GenStep& G = M.gen[t];
@@ -1225,6 +1243,8 @@ static int engine_backward(svae_ctx* c) {
       }
     }
   }
+
+  step_hook(c, 0);
 
   // ---------------- recognition ladders, batched over T ----------------
   HIPCHK(c, hipMemcpyAsync(c->kl_coef, c->reg_host, T * sizeof(float), hipMemcpyHostToDevice, st));
@@ -1516,7 +1536,7 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
       auto mk = [&](hipEvent_t* ev) { ok = ok && hipEventCreateWithFlags(ev, hipEventDisableTiming) == hipSuccess; };
       for (int i = 0; i < svae_ctx::NR; ++i) { mk(&c->ev_ready[i]); mk(&c->ev_free[i]); }
       for (int i = 0; i < 2; ++i) { mk(&c->ev_iready[i]); mk(&c->ev_ifree[i]); }
-      mk(&c->ev_da_ready); mk(&c->ev_da_free); mk(&c->ev_start); mk(&c->ev_join);
+      mk(&c->ev_da_ready); mk(&c->ev_da_free); mk(&c->ev_start); mk(&c->ev_join); mk(&c->ev_hook);
       c->side = ok;
     }
   }
@@ -1531,7 +1551,7 @@ int svae_destroy(svae_ctx* c) {
     hipStreamSynchronize(c->st2);
     hipStreamDestroy(c->st2);
   }
-  for (hipEvent_t ev : {c->ev_da_ready, c->ev_da_free, c->ev_start, c->ev_join})
+  for (hipEvent_t ev : {c->ev_da_ready, c->ev_da_free, c->ev_start, c->ev_join, c->ev_hook})
     if (ev) hipEventDestroy(ev);
   for (int i = 0; i < svae_ctx::NR; ++i) {
     if (c->ev_ready[i]) hipEventDestroy(c->ev_ready[i]);
@@ -1643,10 +1663,20 @@ int svae_backward(svae_ctx* c, void* stream) {
     hipEventRecord(c->ev_join, c->st2);
     hipStreamWaitEvent(c->st, c->ev_join, 0);
   }
+  if (!r && c->hook) c->hook(c->hook_user, -1);
   if (r) return r;
   HIPCHK(c, hipGetLastError());
   return 0;
 }
+
+int svae_set_backward_hook(svae_ctx* c, svae_step_hook hook, void* user) {
+  if (!c) return fail(c, SVAE_EBADARG, "null ctx");
+  c->hook = hook;
+  c->hook_user = user;
+  return 0;
+}
+
+void* svae_hook_stream(svae_ctx* c) { return c ? (void*)(c->side ? c->st2 : c->st) : nullptr; }
 
 int svae_adam(svae_ctx* c, float lr, int64_t step, float clip, void* stream) {
   if (!c || !c->P || step < 1) return fail(c, SVAE_EBADARG, "bad adam args");

@@ -39,6 +39,7 @@ class SequentialVAE:
         self.iteration = 0                                 # abstract_network.py:103
         self.learning_rate = cfg.learning_rate             # sequential_vae.py:253
         self.grad_hook = grad_hook                         # e.g. data-parallel all-reduce
+        self.overlap = None                                # bucketed all-reduce during backward
         self.L = _lib.lib()
         self.table, self.n_total, self.n_live = param_table(cfg)
         self._by_name = {p["name"]: p for p in self.table}
@@ -89,9 +90,20 @@ class SequentialVAE:
                                        _lib.stream_ptr(stream)), self.ctx)
 
     def backward(self, stream=None):
-        _lib.check(self.L.svae_backward(self.ctx, _lib.stream_ptr(stream)), self.ctx)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(s):  # overlapped DP hooks enqueue on the caller's stream
+            _lib.check(self.L.svae_backward(self.ctx, _lib.stream_ptr(s)), self.ctx)
+        if self.overlap is not None:
+            self.overlap.check()
         if self.grad_hook is not None:
             self.grad_hook(self.grads[:self.n_live])
+
+    def enable_overlapped_allreduce(self, dist, group=None, force=False):
+        """Data parallel: all-reduce the gradient in per-step buckets during the backward
+        (parallel.OverlappedAllReduce) instead of one call after it."""
+        from .parallel import OverlappedAllReduce
+        self.overlap = OverlappedAllReduce(self, dist, group, force=force)
+        return self.overlap
 
     def apply_gradients(self, lr=None, step=None, stream=None):
         lr = self.learning_rate if lr is None else lr

@@ -78,3 +78,54 @@ def test_shard_is_contiguous():
     parts = [par.shard(b, r, 8) for r in range(8)]
     assert all(len(p) == 128 for p in parts)
     assert torch.equal(torch.cat(parts), b)
+
+
+@pytest.mark.parametrize("preset", ["tiny", "celeba", "lsun"])
+def test_step_buckets_tile_the_live_gradient(preset):
+    """The overlapped all-reduce's buckets: theta_t in backward order T-1..0, then phi; together
+    they cover [0, n_live) exactly once."""
+    par, w, cfgmod = pkg_mod("parallel"), pkg_mod("weights"), pkg_mod("config")
+    cfg = cfgmod.preset(preset)
+    table, _, n_live = w.param_table(cfg)
+    steps, phi = par.step_buckets(table, n_live)
+    assert [t for t, _, _ in steps] == list(range(cfg.mc_steps - 1, -1, -1))
+    spans = sorted([(lo, hi) for _, lo, hi in steps] + [phi])
+    assert spans[0][0] == 0 and spans[-1][1] == n_live
+    assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+
+
+class _FakeNet:  # the hook's view of SequentialVAE without the GPU engine
+    def __init__(self, grads, table, n_live):
+        self.grads, self.table, self.n_live, self.ctx = grads, table, n_live, None
+
+
+def _overlap_worker(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    par, w, cfgmod = pkg_mod("parallel"), pkg_mod("weights"), pkg_mod("config")
+    cfg = cfgmod.preset("tiny")
+    table, n_total, n_live = w.param_table(cfg)
+    g = torch.from_numpy(np.random.default_rng(rank).standard_normal(n_total).astype(np.float32))
+    net = _FakeNet(g, table, n_live)
+    ov = par.OverlappedAllReduce(net, dist)
+    for t in range(cfg.mc_steps - 1, -1, -1):  # the engine's call order
+        ov._on_step(None, t)
+    ov._on_step(None, -1)
+    ov.check()
+    np.save(os.path.join(out_dir, "o%d.npy" % rank), g.numpy())
+    dist.destroy_process_group()
+
+
+def test_overlapped_allreduce_equals_mean(tmp_path):
+    world = 2
+    mp.spawn(_overlap_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    w, cfgmod = pkg_mod("weights"), pkg_mod("config")
+    _, n_total, n_live = w.param_table(cfgmod.preset("tiny"))
+    src = [np.random.default_rng(r).standard_normal(n_total).astype(np.float32) for r in range(world)]
+    mean = (src[0][:n_live] + src[1][:n_live]) * np.float32(0.5)
+    for r in range(world):
+        o = np.load(tmp_path / ("o%d.npy" % r))
+        np.testing.assert_allclose(o[:n_live], mean, rtol=1e-6, atol=1e-7)
+        np.testing.assert_array_equal(o[n_live:], src[r][n_live:])  # dead tail untouched
+    np.testing.assert_array_equal(np.load(tmp_path / "o0.npy")[:n_live], np.load(tmp_path / "o1.npy")[:n_live])
