@@ -47,6 +47,12 @@ typedef struct svae_config {
   float range_lo, range_hi; /* dataset.range */
   float min_highway, max_highway;
   int32_t dtype;            /* 0 = fp32 (parity) */
+  /* homogeneous chain (sequential_vae.py:107-113, scopes :1573-1577, :1683-1687, :1757-1761):
+   * share_phi: one "phi/inference_network" for every step; share_theta: one
+   * "theta/generative_encoder_network" and one "theta/generative_network" for steps >= 1
+   * ("theta/generative_step_0" stays its own).  The parameter table then lists each shared
+   * tensor once and its gradient is the sum over the steps that use it. */
+  int32_t share_theta, share_phi;
 } svae_config;
 
 typedef struct svae_param_desc {

@@ -171,3 +171,49 @@ def make_inputs(cfg, batch=None, seed_x=0, seed_eps=1):
     re = np.random.default_rng(seed_eps)
     eps = re.standard_normal(size=(cfg["mc_steps"], B, cfg["latent_dim"])).astype(np.float32)
     return x, x.copy(), eps
+
+
+# ---- homogeneous chains: TF variable sharing (sequential_vae.py:107-113) ----
+def shared_name(name, share_theta, share_phi):
+    """Scope a per-step variable takes under weight sharing:
+    share_phi   -> "phi/inference_network" for every step (:1573-1577, predict_latent_code off);
+    share_theta -> "theta/generative_encoder_network" (:1757-1761) and, for steps >= 1 only,
+                   "theta/generative_network" (:1683-1687; step 0 keeps generative_step_0)."""
+    head, _, rest = name.partition("/")
+    scope, _, tail = rest.partition("/")
+    if share_phi and head == "phi" and scope.startswith("inference_step_"):
+        return "phi/inference_network/" + tail
+    if share_theta and head == "theta" and scope.startswith("generative_encoder_step_"):
+        return "theta/generative_encoder_network/" + tail
+    if share_theta and head == "theta" and scope.startswith("generative_step_") and int(scope.split("_")[-1]) >= 1:
+        return "theta/generative_network/" + tail
+    return name
+
+
+def shared_table(cfg, share_theta=True, share_phi=True):
+    """Variables of the homogeneous model in TF creation order (first use creates, AUTO_REUSE
+    reuses): one entry per shared name."""
+    table, _ = build_params(cfg)
+    seen, out = set(), []
+    for p in table:
+        n = shared_name(p["name"], share_theta, share_phi)
+        if n not in seen:
+            seen.add(n)
+            out.append(dict(p, name=n))
+    return out
+
+
+def expand_shared(params_pub, cfg, share_theta=True, share_phi=True):
+    """Per-step (inhomogeneous-layout) parameter dict whose copies alias the shared tensors."""
+    table, _ = build_params(cfg)
+    return {p["name"]: params_pub[shared_name(p["name"], share_theta, share_phi)] for p in table}
+
+
+def sum_shared_grads(grads, share_theta=True, share_phi=True):
+    """Gradient of each shared variable = sum over the steps that use it (TF's gradient of a
+    variable read in several places)."""
+    out = {}
+    for n, g in grads.items():
+        k = shared_name(n, share_theta, share_phi)
+        out[k] = out[k] + g if k in out else np.array(g, copy=True)
+    return out

@@ -25,6 +25,7 @@ class SvaeConfig(ctypes.Structure):
         ("first_step_loss_coeff", ctypes.c_float), ("latent_prior_stddev", ctypes.c_float),
         ("latent_mean_clip", ctypes.c_float), ("range_lo", ctypes.c_float), ("range_hi", ctypes.c_float),
         ("min_highway", ctypes.c_float), ("max_highway", ctypes.c_float), ("dtype", ctypes.c_int32),
+        ("share_theta", ctypes.c_int32), ("share_phi", ctypes.c_int32),
     ]
 
 

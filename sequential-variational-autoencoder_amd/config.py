@@ -35,6 +35,8 @@ class SVAEConfig:
     reg_coeff_rate: float = 5000.0                    # :254
     clip_grad_value: float = 10.0                     # :259
     dtype: str = "fp32"                               # "fp32" (parity) | "bf16" (bf16 MFMA, fp32 accumulate)
+    share_theta_weights: bool = False                 # :213 (homogeneous generator / encoder)
+    share_phi_weights: bool = False                   # :214 (homogeneous recognition)
 
     @property
     def latent_dim(self):
@@ -59,6 +61,7 @@ class SVAEConfig:
         c.range_lo, c.range_hi = self.range
         c.min_highway, c.max_highway = self.min_highway, self.max_highway
         c.dtype = {"fp32": 0, "bf16": 1}[self.dtype]
+        c.share_theta, c.share_phi = int(self.share_theta_weights), int(self.share_phi_weights)
         return c
 
     def as_dict(self):
@@ -70,7 +73,8 @@ class SVAEConfig:
                     first_step_loss_coeff=self.first_step_loss_coeff,
                     latent_prior_stddev=self.latent_prior_stddev, latent_mean_clip=self.latent_mean_clip,
                     min_highway=self.min_highway, max_highway=self.max_highway,
-                    image_sizes=self.image_sizes, latent_dim=self.latent_dim)
+                    image_sizes=self.image_sizes, latent_dim=self.latent_dim,
+                    share_theta=self.share_theta_weights, share_phi=self.share_phi_weights)
 
 
 PRESETS = {
@@ -81,6 +85,14 @@ PRESETS = {
                               range=(0.0, 1.0)),
     "tiny": SVAEConfig(batch=4, height=32, width=32, channels=3, levels=4, filter_sizes=[3, 8, 8, 16, 24, 16],
                        latent_dims=[2, 2, 3, 2], mc_steps=3),
+    # homogeneous chains (shared phi / theta across steps)
+    "c_homog_v1": SVAEConfig(latent_dims=[12, 12, 12, 12], filter_sizes=[3, 16, 32, 64, 128, 384],
+                             share_theta_weights=True, share_phi_weights=True),         # :316-321
+    "c_homog_one_step": SVAEConfig(latent_dims=[12, 12, 12, 12], filter_sizes=[3, 16, 32, 64, 128, 384],
+                                   share_theta_weights=True, share_phi_weights=True, mc_steps=1),  # :281-288
+    "tiny_homog": SVAEConfig(batch=4, height=32, width=32, channels=3, levels=4, filter_sizes=[3, 8, 8, 16, 24, 16],
+                             latent_dims=[2, 2, 3, 2], mc_steps=3, share_theta_weights=True,
+                             share_phi_weights=True),
 }
 # reference netnames that map onto the presets (sequential_vae.py:671, :712, :727)
 NETNAMES = {"c_inhomog": "celeba", "sequential_vae_celebA_inhomog": "celeba", "sequential_vae_lsun": "lsun"}

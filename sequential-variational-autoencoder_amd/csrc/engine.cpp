@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -73,6 +74,7 @@ struct Geo {
   bool interm;
   float c_first, prior, clipv, lo, hi, minh, maxh;
   bool bf16;
+  bool share_theta, share_phi;
 };
 
 bool make_geo(const svae_config* c, Geo& g, std::string& err) {
@@ -111,6 +113,8 @@ bool make_geo(const svae_config* c, Geo& g, std::string& err) {
   g.minh = c->min_highway; g.maxh = c->max_highway;
   if (c->dtype != 0 && c->dtype != 1) { err = "dtype must be 0 (fp32) or 1 (bf16 MFMA)"; return false; }
   g.bf16 = c->dtype == 1;
+  g.share_theta = c->share_theta != 0;
+  g.share_phi = c->share_phi != 0;
   return true;
 }
 
@@ -176,7 +180,72 @@ struct Model {
   std::vector<GenStep> gen;
   long long n_total = 0, n_live = 0, phi_stride = 0;
 
+  // Public table (what svae_param_layout reports and the caller's buffers hold).  Without
+  // weight sharing it is descs itself.  With sharing the engine still runs on a private
+  // "virtual" copy in the inhomogeneous layout above (descs, offsets): every step's scope gets
+  // its own copy of the shared tensor (broadcast from the public buffer before the forward),
+  // and each public gradient is the fixed-order sum of its copies' gradients after the
+  // backward -- exactly TF's gradient of a variable used by several steps.
+  std::vector<PDesc> pub;
+  std::vector<int> vpub;  // descs index -> pub index
+  long long p_total = 0, p_live = 0;
+  bool shared = false;
+
   long long off(int idx) const { return idx < 0 ? -1 : descs[idx].offset; }
+
+  // TF scope of a virtual tensor under variable sharing (sequential_vae.py:1573-1577,1683-1687,1757-1761)
+  std::string public_name(const std::string& n) const {
+    auto swap = [&](const char* pre, const char* to, int min_step, std::string& out) {
+      const size_t lp = strlen(pre);
+      if (n.compare(0, lp, pre) != 0) return false;
+      const size_t sl = n.find('/', lp);
+      if (sl == std::string::npos || atoi(n.c_str() + lp) < min_step) return false;
+      out = std::string(to) + n.substr(sl);
+      return true;
+    };
+    std::string o;
+    if (g.share_phi && swap("phi/inference_step_", "phi/inference_network", 0, o)) return o;
+    if (g.share_theta && swap("theta/generative_encoder_step_", "theta/generative_encoder_network", 0, o)) return o;
+    if (g.share_theta && swap("theta/generative_step_", "theta/generative_network", 1, o)) return o;
+    return n;
+  }
+
+  void build_public() {
+    shared = g.share_theta || g.share_phi;
+    std::vector<int> order(descs.size());
+    for (size_t i = 0; i < descs.size(); ++i) order[i] = (int)i;
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return descs[a].offset < descs[b].offset; });
+    std::map<std::string, int> by_name;
+    vpub.assign(descs.size(), -1);
+    pub.clear();
+    for (int i : order) {
+      const std::string pn = public_name(descs[i].name);
+      auto it = by_name.find(pn);
+      if (it == by_name.end()) {
+        PDesc d = descs[i];
+        d.name = pn;
+        by_name[pn] = (int)pub.size();
+        vpub[i] = (int)pub.size();
+        pub.push_back(d);
+      } else {
+        vpub[i] = it->second;
+      }
+    }
+    // first-appearance order keeps the live tensors ahead of the frozen tail
+    long long o = 0;
+    bool frozen_seen = false;
+    p_live = -1;
+    for (auto& d : pub) {
+      const bool fz = d.region == R_FROZEN;
+      if (fz && !frozen_seen) { frozen_seen = true; p_live = o; }
+      o = (o + 63) / 64 * 64;
+      d.offset = o;
+      o += d.size;
+      o = (o + 63) / 64 * 64;
+    }
+    p_total = o;
+    if (p_live < 0) p_live = o;
+  }
 
   void build() {
     const int L = g.L;
@@ -261,6 +330,7 @@ struct Model {
       if (r == R_THETA) n_live = o;
     }
     n_total = o;
+    build_public();
     auto rc = [&](ConvL& c) { c.ow = off(c.w); c.obeta = off(c.beta); };
     auto rf = [&](FcL& f) { f.ow = off(f.w); f.obeta = off(f.beta); };
     for (int t = 0; t < g.T; ++t) {
@@ -331,8 +401,17 @@ struct svae_ctx {
   Model m;
   std::string err;
   int device = 0;
-  float* P = nullptr;   // bound params
-  float* Gr = nullptr;  // bound grads
+  float* P = nullptr;   // params the engine reads (the caller's, or the virtual copy under sharing)
+  float* Gr = nullptr;  // grads the engine writes (likewise)
+  // weight sharing (Model::shared): the caller's public buffers and the virtual copies
+  float* Ppub = nullptr;
+  float* Gpub = nullptr;
+  float* Pv = nullptr;
+  float* Gv = nullptr;
+  long long* share_seg = nullptr;   // [nseg][3] virtual offset, public offset, size (broadcast)
+  long long* share_tab = nullptr;   // [ntab][4] public offset, size, first copy, copies (gather-sum)
+  long long* share_cp = nullptr;    // virtual offsets of the copies
+  int share_nseg = 0, share_ntab = 0;
   float* adam_m = nullptr;
   float* adam_v = nullptr;
   char* arena = nullptr;
@@ -875,7 +954,7 @@ static int fc_bn_bwd(svae_ctx* c, const FcL& f, View in, View dy, View y, const 
 // host hook after chain step t's backward: the side stream is ordered after all of the step's
 // work on both streams, so a collective issued on it sees that step's complete gradients
 static void step_hook(svae_ctx* c, int t) {
-  if (!c->hook) return;
+  if (!c->hook || c->m.shared) return;  // shared tensors are complete only after every step
   if (c->side) {
     hipEventRecord(c->ev_hook, c->st);
     hipStreamWaitEvent(c->st2, c->ev_hook, 0);
@@ -897,6 +976,7 @@ static int engine_forward(svae_ctx* c) {
   int r;
 
   if ((r = acc_reset(c))) return r;
+  if (M.shared) share_broadcast(c->Ppub, c->Pv, c->share_seg, c->share_nseg, st);
   if (g.bf16) shadow_weights(c->P, c->wN, c->wT, M.n_live, c->tiles_d, c->ntiles, c->offs_d, st);
   if (c->generative) {
     // generative mode (sequential_vae.py:947-952, :1025 latent_generative = self.latents[t]):
@@ -1298,6 +1378,13 @@ static int engine_backward(svae_ctx* c) {
       if (r) return r;
     }
   }
+  if (M.shared) {  // public gradient = fixed-order sum of the step copies (side stream joined first)
+    if (c->side) {
+      hipEventRecord(c->ev_join, c->st2);
+      hipStreamWaitEvent(st, c->ev_join, 0);
+    }
+    share_gather(c->Gv, c->Gpub, c->share_tab, c->share_cp, c->share_ntab, st);
+  }
   return 0;
 }
 
@@ -1422,9 +1509,9 @@ int svae_param_count(const svae_config* cfg, int64_t* n_total, int64_t* n_live, 
   std::string err;
   if (!make_geo(cfg, m.g, err)) return fail(nullptr, SVAE_EBADCONFIG, err);
   m.build();
-  if (n_total) *n_total = m.n_total;
-  if (n_live) *n_live = m.n_live;
-  if (n_tensors) *n_tensors = (int32_t)m.descs.size();
+  if (n_total) *n_total = m.p_total;
+  if (n_live) *n_live = m.p_live;
+  if (n_tensors) *n_tensors = (int32_t)m.pub.size();
   return 0;
 }
 
@@ -1433,9 +1520,9 @@ int svae_param_layout(const svae_config* cfg, svae_param_desc* out, int32_t cap)
   std::string err;
   if (!make_geo(cfg, m.g, err)) return fail(nullptr, SVAE_EBADCONFIG, err);
   m.build();
-  if (!out || cap < (int32_t)m.descs.size()) return fail(nullptr, SVAE_EBADARG, "layout capacity too small");
-  for (size_t i = 0; i < m.descs.size(); ++i) {
-    const PDesc& d = m.descs[i];
+  if (!out || cap < (int32_t)m.pub.size()) return fail(nullptr, SVAE_EBADARG, "layout capacity too small");
+  for (size_t i = 0; i < m.pub.size(); ++i) {
+    const PDesc& d = m.pub[i];
     svae_param_desc& o = out[i];
     memset(&o, 0, sizeof(o));
     strncpy(o.name, d.name.c_str(), sizeof(o.name) - 1);
@@ -1485,6 +1572,41 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
   }
   c->adam_v = c->adam_m + nl;
   hipMemset(c->adam_m, 0, (size_t)nl * sizeof(float) * 2);
+  if (c->m.shared) {
+    const Model& M = c->m;
+    std::vector<long long> seg, tab, cp;
+    std::vector<std::vector<long long>> copies(M.pub.size());
+    std::vector<int> order(M.descs.size());
+    for (size_t i = 0; i < M.descs.size(); ++i) order[i] = (int)i;
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return M.descs[a].offset < M.descs[b].offset; });
+    for (int i : order) {  // step order within a public tensor = virtual layout order (fixed)
+      const PDesc& d = M.descs[i];
+      const PDesc& p = M.pub[M.vpub[i]];
+      seg.insert(seg.end(), {d.offset, p.offset, d.size});
+      if (!d.zero_grad) copies[M.vpub[i]].push_back(d.offset);
+    }
+    for (size_t j = 0; j < M.pub.size(); ++j) {
+      if (copies[j].empty()) continue;
+      tab.insert(tab.end(), {M.pub[j].offset, M.pub[j].size, (long long)cp.size(), (long long)copies[j].size()});
+      cp.insert(cp.end(), copies[j].begin(), copies[j].end());
+    }
+    c->share_nseg = (int)(seg.size() / 3);
+    c->share_ntab = (int)(tab.size() / 4);
+    size_t bytes = (seg.size() + tab.size() + cp.size()) * sizeof(long long);
+    e = hipMalloc((void**)&c->Pv, (size_t)M.n_total * sizeof(float) * 2);
+    if (e == hipSuccess) e = hipMalloc((void**)&c->share_seg, bytes);
+    if (e != hipSuccess) {
+      svae_destroy(c);
+      return fail(nullptr, SVAE_ENOMEM, std::string("hipMalloc shared copies: ") + hipGetErrorString(e));
+    }
+    c->Gv = c->Pv + M.n_total;
+    c->share_tab = c->share_seg + seg.size();
+    c->share_cp = c->share_tab + tab.size();
+    hipMemset(c->Pv, 0, (size_t)M.n_total * sizeof(float) * 2);
+    hipMemcpy(c->share_seg, seg.data(), seg.size() * sizeof(long long), hipMemcpyHostToDevice);
+    hipMemcpy(c->share_tab, tab.data(), tab.size() * sizeof(long long), hipMemcpyHostToDevice);
+    hipMemcpy(c->share_cp, cp.data(), cp.size() * sizeof(long long), hipMemcpyHostToDevice);
+  }
   if (c->m.g.bf16) {
     // bf16 shadows of the live region + the per-tap transpose tile table of every GEMM weight
     e = hipMalloc(&c->wN, (size_t)nl * 2);
@@ -1569,6 +1691,8 @@ int svae_destroy(svae_ctx* c) {
   if (c->wT) hipFree(c->wT);
   if (c->tiles_d) hipFree(c->tiles_d);
   if (c->offs_d) hipFree(c->offs_d);
+  if (c->Pv) hipFree(c->Pv);
+  if (c->share_seg) hipFree(c->share_seg);
   delete c;
   return 0;
 }
@@ -1617,9 +1741,17 @@ int64_t svae_workspace_bytes(const svae_ctx* c) { return c ? (int64_t)c->arena_b
 
 int svae_bind(svae_ctx* c, float* params, float* grads) {
   if (!c || !params || !grads) return fail(c, SVAE_EBADARG, "null buffer");
-  c->P = params;
-  c->Gr = grads;
-  HIPCHK(c, hipMemset(grads, 0, (size_t)c->m.n_total * sizeof(float)));
+  c->Ppub = params;
+  c->Gpub = grads;
+  HIPCHK(c, hipMemset(grads, 0, (size_t)c->m.p_total * sizeof(float)));
+  if (c->m.shared) {
+    c->P = c->Pv;
+    c->Gr = c->Gv;
+    HIPCHK(c, hipMemset(c->Gv, 0, (size_t)c->m.n_total * sizeof(float)));
+  } else {
+    c->P = params;
+    c->Gr = grads;
+  }
   return 0;
 }
 
@@ -1682,7 +1814,7 @@ int svae_adam(svae_ctx* c, float lr, int64_t step, float clip, void* stream) {
   if (!c || !c->P || step < 1) return fail(c, SVAE_EBADARG, "bad adam args");
   const double b1 = 0.9, b2 = 0.999;
   const double lr_t = lr * std::sqrt(1.0 - std::pow(b2, (double)step)) / (1.0 - std::pow(b1, (double)step));
-  adam_step(c->P, c->Gr, c->adam_m, c->adam_v, c->m.n_live, (float)lr_t, (float)b1, (float)b2, 1e-8f, clip,
+  adam_step(c->Ppub, c->Gpub, c->adam_m, c->adam_v, c->m.p_live, (float)lr_t, (float)b1, (float)b2, 1e-8f, clip,
             (hipStream_t)stream);
   HIPCHK(c, hipGetLastError());
   return 0;

@@ -196,6 +196,12 @@ void loss_reduce(const float* rec_part, int nblk, const float* kl_img, int B, in
 void adam_step(float* w, const float* g, float* m, float* v, long long n, float lr_t, float b1, float b2, float eps,
                float clipv, hipStream_t s);
 
+// ---- weight sharing (homogeneous chain): virtual per-step copies <-> public tensors ----
+// Pv[v + i] = P[p + i] for every segment {v, p, size} of seg[nseg][3]
+void share_broadcast(const float* P, float* Pv, const long long* seg, int nseg, hipStream_t s);
+// G[p + i] = sum_{k < n} Gv[cp[first + k] + i]  (fixed order) for every {p, size, first, n} of tab[ntab][4]
+void share_gather(const float* Gv, float* G, const long long* tab, const long long* cp, int ntab, hipStream_t s);
+
 // ---- misc ----
 void fill_f32(float* p, long long n, float v, hipStream_t s);
 void philox_normal(float* out, long long n, unsigned long long seed, unsigned long long offset, hipStream_t s);

@@ -899,3 +899,31 @@ void colsum_small(const float* X, int ld, long long rows, int C, float* part, fl
   hipLaunchKernelGGL(colsum_part_kernel, dim3(CS_BLOCKS), dim3(256), 0, s, X, ld, rows, C, part);
   hipLaunchKernelGGL(colsum_fin_kernel, dim3(1), dim3(64), 0, s, part, CS_BLOCKS, C, out0, n0, out1);
 }
+
+// ---- weight sharing: broadcast the public tensors into the per-step copies, and sum the
+// copies' gradients into the public gradient (sequential_vae.py:1573-1577,1683-1687,1757-1761:
+// a TF variable used by several steps receives the sum of their gradients) ----
+__global__ void share_bcast_kernel(const float* P, float* Pv, const long long* seg) {
+  const long long* sg = seg + 3LL * blockIdx.y;
+  const long long v = sg[0], p = sg[1], n = sg[2];
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    Pv[v + i] = P[p + i];
+}
+
+__global__ void share_gather_kernel(const float* Gv, float* G, const long long* tab, const long long* cp) {
+  const long long* t = tab + 4LL * blockIdx.y;
+  const long long p = t[0], n = t[1], first = t[2], nc = t[3];
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    float acc = 0.f;
+    for (long long k = 0; k < nc; ++k) acc += Gv[cp[first + k] + i];
+    G[p + i] = acc;
+  }
+}
+
+void share_broadcast(const float* P, float* Pv, const long long* seg, int nseg, hipStream_t s) {
+  if (nseg > 0) hipLaunchKernelGGL(share_bcast_kernel, dim3(64, nseg), dim3(256), 0, s, P, Pv, seg);
+}
+
+void share_gather(const float* Gv, float* G, const long long* tab, const long long* cp, int ntab, hipStream_t s) {
+  if (ntab > 0) hipLaunchKernelGGL(share_gather_kernel, dim3(64, ntab), dim3(256), 0, s, Gv, G, tab, cp);
+}

@@ -68,3 +68,18 @@ def test_bad_config_rejected(built_lib):
     rc = L.lib().svae_param_count(ctypes.byref(cfg), ctypes.byref(n), None, None)
     assert rc == -1
     assert b"batch" in L.lib().svae_last_error(None)
+
+
+def test_homog_layout_matches_oracle_sharing(built_lib):
+    """Public parameter table of the homogeneous presets = the oracle's restatement of TF's
+    variable sharing (names and shapes); the live region precedes the frozen tail."""
+    from oracle import spec
+    w, cfgmod = pkg_mod("weights"), pkg_mod("config")
+    for theta, phi in [(True, True), (True, False), (False, True)]:
+        cfg = cfgmod.preset("tiny", share_theta_weights=theta, share_phi_weights=phi)
+        table, n_total, n_live = w.param_table(cfg)
+        ref = {p["name"]: tuple(p["shape"]) for p in spec.shared_table(spec.make_config("tiny"), theta, phi)}
+        assert {p["name"]: tuple(p["shape"]) for p in table} == ref
+        for p in table:
+            assert (p["offset"] < n_live) == (not p["zero_grad"]), p["name"]
+            assert p["offset"] + p["size"] <= n_total
