@@ -53,6 +53,14 @@ typedef struct svae_config {
    * ("theta/generative_step_0" stays its own).  The parameter table then lists each shared
    * tensor once and its gradient is the sum over the steps that use it. */
   int32_t share_theta, share_phi;
+  /* Latent InfoMax (predict_latent_code :129-131, create_recognition_network :1013-1020):
+   * q(z_t | x_{t-1}) for t >= 1 (gradient flows into x_{t-1}); the KL term only at step 0
+   * unless predict_latent_code_with_regularization (:1170-1172).  Under share_phi step 0 keeps
+   * its own "phi/inference_step_0" (:1573).  The improvement-maximisation loss and its separate
+   * optimiser (:1182-1201, :1302-1316) are not part of this path. */
+  int32_t predict_latent_code, predict_latent_code_with_regularization;
+  /* regularized_steps (:220, :1154): bit t set = step t carries NO KL term (0 = every step) */
+  uint32_t unregularized_steps_mask[2];
 } svae_config;
 
 typedef struct svae_param_desc {

@@ -9,6 +9,7 @@ injected ([T,B,Dz]) instead of drawn by ``tf.random_normal`` (:1023).
 import numpy as np
 
 from . import tape as T
+from . import spec as S
 
 
 def _conv_bn_act(tp, P, x, layer, stride, act, transpose=False, residual=None):
@@ -152,7 +153,9 @@ def forward_backward(cfg, struct, params, x, target, eps, reg_coeff=1.0, want_gr
     prev = None
     for t in range(Tn):
         st = struct[t]
-        mu, sig = inference_ladder(tp, P, cfg, st["inference"], xin)
+        # recognition input: x, or x_{t-1} in Latent InfoMax mode (sequential_vae.py:1013-1016)
+        rin = prev if (cfg.get("predict_latent_code", False) and t >= 1) else xin
+        mu, sig = inference_ladder(tp, P, cfg, st["inference"], rin)
         e = tp.leaf(np.asarray(eps[t], np.float64))
         z = T.add(tp, mu, T.mul(tp, sig, e))                       # :1023
         recd = {}
@@ -165,8 +168,8 @@ def forward_backward(cfg, struct, params, x, target, eps, reg_coeff=1.0, want_gr
         if cfg["intermediate_reconstruction"] or t == Tn - 1:       # :1167-1168
             terms.append(rec_m)
             coeffs.append(16.0 * c_first)
-        terms.append(kl_m)                                          # :1171-1172
-        coeffs.append(reg_coeff * c_first)
+        terms.append(kl_m)                                          # :1154, :1170-1172
+        coeffs.append(reg_coeff * c_first * S.kl_on(cfg, t))
         out["recon"].append(float(rec_m.v))
         out["kl"].append(float(kl_m.v))
         out["recon_img"].append(rec.v.copy())
@@ -187,7 +190,7 @@ def forward_backward(cfg, struct, params, x, target, eps, reg_coeff=1.0, want_gr
         c_first = cfg["first_step_loss_coeff"] if t == 0 else 1.0
         if cfg["intermediate_reconstruction"] or t == Tn - 1:
             elbo_img += 16.0 * c_first * out["recon_img"][t]
-        elbo_img += reg_coeff * c_first * out["kl_img"][t]
+        elbo_img += reg_coeff * c_first * S.kl_on(cfg, t) * out["kl_img"][t]
     out["elbo_img"] = elbo_img
     if want_grads:
         tp.backward(loss)

@@ -34,7 +34,19 @@ PRESETS = {
 
 DEFAULTS = dict(intermediate_reconstruction=True, first_step_loss_coeff=1.0,
                 latent_prior_stddev=1.0, latent_mean_clip=float("inf"),
-                min_highway=0.0, max_highway=1.0)
+                min_highway=0.0, max_highway=1.0, predict_latent_code=False,
+                predict_latent_code_with_regularization=False, regularized_steps=None)
+
+
+def kl_on(cfg, t):
+    """Does step t's KL term enter self.loss?  sequential_vae.py:1154 (``step in
+    self.regularized_steps``) and :1170-1172 (Latent InfoMax: step 0 only, unless
+    predict_latent_code_with_regularization)."""
+    rs = cfg.get("regularized_steps")
+    if rs is not None and t not in rs:
+        return 0.0
+    plc = cfg.get("predict_latent_code", False)
+    return 1.0 if (not plc or cfg.get("predict_latent_code_with_regularization", False) or t == 0) else 0.0
 
 
 def make_config(preset="celeba", **over):
@@ -174,14 +186,14 @@ def make_inputs(cfg, batch=None, seed_x=0, seed_eps=1):
 
 
 # ---- homogeneous chains: TF variable sharing (sequential_vae.py:107-113) ----
-def shared_name(name, share_theta, share_phi):
+def shared_name(name, share_theta, share_phi, plc=False):
     """Scope a per-step variable takes under weight sharing:
     share_phi   -> "phi/inference_network" for every step (:1573-1577, predict_latent_code off);
     share_theta -> "theta/generative_encoder_network" (:1757-1761) and, for steps >= 1 only,
                    "theta/generative_network" (:1683-1687; step 0 keeps generative_step_0)."""
     head, _, rest = name.partition("/")
     scope, _, tail = rest.partition("/")
-    if share_phi and head == "phi" and scope.startswith("inference_step_"):
+    if share_phi and head == "phi" and scope.startswith("inference_step_") and not (plc and scope == "inference_step_0"):
         return "phi/inference_network/" + tail
     if share_theta and head == "theta" and scope.startswith("generative_encoder_step_"):
         return "theta/generative_encoder_network/" + tail
@@ -191,12 +203,13 @@ def shared_name(name, share_theta, share_phi):
 
 
 def shared_table(cfg, share_theta=True, share_phi=True):
+    plc = cfg.get("predict_latent_code", False)
     """Variables of the homogeneous model in TF creation order (first use creates, AUTO_REUSE
     reuses): one entry per shared name."""
     table, _ = build_params(cfg)
     seen, out = set(), []
     for p in table:
-        n = shared_name(p["name"], share_theta, share_phi)
+        n = shared_name(p["name"], share_theta, share_phi, plc)
         if n not in seen:
             seen.add(n)
             out.append(dict(p, name=n))
@@ -206,14 +219,15 @@ def shared_table(cfg, share_theta=True, share_phi=True):
 def expand_shared(params_pub, cfg, share_theta=True, share_phi=True):
     """Per-step (inhomogeneous-layout) parameter dict whose copies alias the shared tensors."""
     table, _ = build_params(cfg)
-    return {p["name"]: params_pub[shared_name(p["name"], share_theta, share_phi)] for p in table}
+    plc = cfg.get("predict_latent_code", False)
+    return {p["name"]: params_pub[shared_name(p["name"], share_theta, share_phi, plc)] for p in table}
 
 
-def sum_shared_grads(grads, share_theta=True, share_phi=True):
+def sum_shared_grads(grads, share_theta=True, share_phi=True, plc=False):
     """Gradient of each shared variable = sum over the steps that use it (TF's gradient of a
     variable read in several places)."""
     out = {}
     for n, g in grads.items():
-        k = shared_name(n, share_theta, share_phi)
+        k = shared_name(n, share_theta, share_phi, plc)
         out[k] = out[k] + g if k in out else np.array(g, copy=True)
     return out

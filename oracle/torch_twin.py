@@ -8,6 +8,7 @@ the reference's own TF-CPU path cannot run here (no TensorFlow).
 """
 import torch
 import torch.nn.functional as Fn
+from . import spec as _spec
 
 
 def _same(n_in, k, s):
@@ -185,7 +186,8 @@ class Twin:
         loss, prev, recs, kls, xhats = 0.0, None, [], [], []
         for t in range(Tn):
             st = self.struct[t]
-            mu, sig = self.inference(st["inference"], x)
+            rin = prev if (cfg.get("predict_latent_code", False) and t >= 1) else x  # :1013-1016
+            mu, sig = self.inference(st["inference"], rin)
             z = mu + sig * eps[t]
             xh = self.generator(st["generator"], prev, z, st.get("encoder"))
             rec = ((xh - tgt) ** 2).mean()
@@ -193,7 +195,7 @@ class Twin:
             c = cfg["first_step_loss_coeff"] if t == 0 else 1.0
             if cfg["intermediate_reconstruction"] or t == Tn - 1:
                 loss = loss + 16.0 * c * rec
-            loss = loss + reg_coeff * c * kl
+            loss = loss + reg_coeff * c * _spec.kl_on(cfg, t) * kl  # :1154, :1170-1172
             recs.append(rec.detach())
             kls.append(kl.detach())
             xhats.append(xh.detach().permute(0, 2, 3, 1))

@@ -26,6 +26,8 @@ class SvaeConfig(ctypes.Structure):
         ("latent_mean_clip", ctypes.c_float), ("range_lo", ctypes.c_float), ("range_hi", ctypes.c_float),
         ("min_highway", ctypes.c_float), ("max_highway", ctypes.c_float), ("dtype", ctypes.c_int32),
         ("share_theta", ctypes.c_int32), ("share_phi", ctypes.c_int32),
+        ("predict_latent_code", ctypes.c_int32), ("predict_latent_code_with_regularization", ctypes.c_int32),
+        ("unregularized_steps_mask", ctypes.c_uint32 * 2),
     ]
 
 

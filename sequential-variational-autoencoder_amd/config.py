@@ -37,6 +37,9 @@ class SVAEConfig:
     dtype: str = "fp32"                               # "fp32" (parity) | "bf16" (bf16 MFMA, fp32 accumulate)
     share_theta_weights: bool = False                 # :213 (homogeneous generator / encoder)
     share_phi_weights: bool = False                   # :214 (homogeneous recognition)
+    predict_latent_code: bool = False                 # :225 (Latent InfoMax: q(z_t | x_{t-1}))
+    predict_latent_code_with_regularization: bool = False  # :230
+    regularized_steps: Tuple[int, ...] = None         # :220 (None = every step)
 
     @property
     def latent_dim(self):
@@ -62,6 +65,14 @@ class SVAEConfig:
         c.min_highway, c.max_highway = self.min_highway, self.max_highway
         c.dtype = {"fp32": 0, "bf16": 1}[self.dtype]
         c.share_theta, c.share_phi = int(self.share_theta_weights), int(self.share_phi_weights)
+        c.predict_latent_code = int(self.predict_latent_code)
+        c.predict_latent_code_with_regularization = int(self.predict_latent_code_with_regularization)
+        unreg = 0
+        if self.regularized_steps is not None:
+            for t in range(self.mc_steps):
+                if t not in self.regularized_steps:
+                    unreg |= 1 << t
+        c.unregularized_steps_mask[0], c.unregularized_steps_mask[1] = unreg & 0xFFFFFFFF, unreg >> 32
         return c
 
     def as_dict(self):
@@ -74,7 +85,16 @@ class SVAEConfig:
                     latent_prior_stddev=self.latent_prior_stddev, latent_mean_clip=self.latent_mean_clip,
                     min_highway=self.min_highway, max_highway=self.max_highway,
                     image_sizes=self.image_sizes, latent_dim=self.latent_dim,
-                    share_theta=self.share_theta_weights, share_phi=self.share_phi_weights)
+                    share_theta=self.share_theta_weights, share_phi=self.share_phi_weights,
+                    predict_latent_code=self.predict_latent_code,
+                    predict_latent_code_with_regularization=self.predict_latent_code_with_regularization,
+                    regularized_steps=self.regularized_steps)
+
+    def kl_on(self, t):
+        """1 if step t's KL term enters self.loss (sequential_vae.py:1154, :1170-1172), else 0."""
+        if self.regularized_steps is not None and t not in self.regularized_steps:
+            return 0.0
+        return 1.0 if (not self.predict_latent_code or self.predict_latent_code_with_regularization or t == 0) else 0.0
 
 
 PRESETS = {
@@ -90,6 +110,16 @@ PRESETS = {
                              share_theta_weights=True, share_phi_weights=True),         # :316-321
     "c_homog_one_step": SVAEConfig(latent_dims=[12, 12, 12, 12], filter_sizes=[3, 16, 32, 64, 128, 384],
                                    share_theta_weights=True, share_phi_weights=True, mc_steps=1),  # :281-288
+    # Latent InfoMax chains (:369-405)
+    "c_homog_reg_pred_latent": SVAEConfig(latent_dims=[12, 12, 12, 12], filter_sizes=[3, 16, 32, 64, 128, 384],
+                                          share_theta_weights=True, share_phi_weights=True, predict_latent_code=True,
+                                          latent_mean_clip=32.0, predict_latent_code_with_regularization=True),
+    "c_homog_no_reg_pred_latent": SVAEConfig(latent_dims=[12, 12, 12, 12], filter_sizes=[3, 16, 32, 64, 128, 384],
+                                             share_theta_weights=True, share_phi_weights=True,
+                                             predict_latent_code=True, regularized_steps=(0,), latent_mean_clip=32.0),
+    "c_v2_coeff_change_abl": SVAEConfig(latent_dims=[12, 12, 12, 12], filter_sizes=[3, 16, 32, 64, 128, 384],
+                                        share_theta_weights=True, share_phi_weights=True, predict_latent_code=True,
+                                        regularized_steps=(0,), latent_mean_clip=32.0, first_step_loss_coeff=2.0),
     "tiny_homog": SVAEConfig(batch=4, height=32, width=32, channels=3, levels=4, filter_sizes=[3, 8, 8, 16, 24, 16],
                              latent_dims=[2, 2, 3, 2], mc_steps=3, share_theta_weights=True,
                              share_phi_weights=True),

@@ -75,6 +75,13 @@ struct Geo {
   float c_first, prior, clipv, lo, hi, minh, maxh;
   bool bf16;
   bool share_theta, share_phi;
+  bool plc, plc_reg;          // predict_latent_code (+ _with_regularization)
+  unsigned long long unreg;   // steps without a KL term
+  // weight of step t's KL term relative to reg * c_first (compute_and_accumulate_loss :1154-1172)
+  float kl_on(int t) const {
+    if ((unreg >> t) & 1ULL) return 0.f;
+    return (!plc || plc_reg || t == 0) ? 1.f : 0.f;
+  }
 };
 
 bool make_geo(const svae_config* c, Geo& g, std::string& err) {
@@ -115,6 +122,9 @@ bool make_geo(const svae_config* c, Geo& g, std::string& err) {
   g.bf16 = c->dtype == 1;
   g.share_theta = c->share_theta != 0;
   g.share_phi = c->share_phi != 0;
+  g.plc = c->predict_latent_code != 0;
+  g.plc_reg = c->predict_latent_code_with_regularization != 0;
+  g.unreg = (unsigned long long)c->unregularized_steps_mask[0] | ((unsigned long long)c->unregularized_steps_mask[1] << 32);
   return true;
 }
 
@@ -204,7 +214,7 @@ struct Model {
       return true;
     };
     std::string o;
-    if (g.share_phi && swap("phi/inference_step_", "phi/inference_network", 0, o)) return o;
+    if (g.share_phi && swap("phi/inference_step_", "phi/inference_network", g.plc ? 1 : 0, o)) return o;
     if (g.share_theta && swap("theta/generative_encoder_step_", "theta/generative_encoder_network", 0, o)) return o;
     if (g.share_theta && swap("theta/generative_step_", "theta/generative_network", 1, o)) return o;
     return n;
@@ -462,7 +472,7 @@ struct svae_ctx {
   const float* tgt_in = nullptr;
   const float* eps_in = nullptr;
   const float* eps_used = nullptr;
-  float* reg_host = nullptr;  // pinned [T] kl coefficients (read by a memcpy node at replay time)
+  float* reg_host = nullptr;  // [T] kl coefficients staged on the host (set_small copies them by value)
   int dbg_stop_step = -1, dbg_stop_lvl = -1, dbg_stop_lvl2 = -1;
   float* dbg_last = nullptr;
   bool counting = false;
@@ -962,6 +972,52 @@ static void step_hook(svae_ctx* c, int t) {
   c->hook(c->hook_user, t);
 }
 
+// Recognition ladders of steps [t0, t0+n) (inference_ladder :1579-1630, heads :1592-1609) on
+// input `in` (group stride in.gs), then mu / sigma / z / KL (:1022-1024, :1156-1158).
+static int inference_fwd(svae_ctx* c, int t0, int n, View in0) {
+  Model& M = c->m;
+  const Geo& g = M.g;
+  const int B = g.B, L = g.L;
+  const int* F = g.F;
+  const long long wg = M.phi_stride;
+  hipStream_t st = c->st;
+  const InfStep& I = M.inf[t0];
+  const long long hps = (long long)c->head_nsplit * B * 2 * g.Dz;
+  int r;
+  HIPCHK(c, hipMemsetAsync(c->head_part + t0 * hps, 0, (size_t)n * hps * sizeof(float), st));
+  auto bns = [&](const BNS& b, int C) { return BNS{b.mean + (long long)t0 * C, b.invstd + (long long)t0 * C}; };
+  for (int lvl = 0; lvl < L - 1; ++lvl) {
+    const long long gs = c->inf_gs[lvl];
+    const int Fl = F[lvl + 1];
+    View in = lvl == 0 ? in0 : View{c->inf_act_b[lvl - 1] + t0 * c->inf_gs[lvl - 1], F[lvl], c->inf_gs[lvl - 1]};
+    r = conv_bn_act_fwd(c, I.a[lvl], n, wg, in, c->inf_pre_a[lvl] + t0 * gs, gs, bns(c->inf_bn_a[lvl], Fl), Fl, View{},
+                        ACT_LRELU, View{c->inf_act_a[lvl] + t0 * gs, Fl, gs});
+    if (r) return r;
+    r = conv_bn_act_fwd(c, I.b[lvl], n, wg, View{c->inf_act_a[lvl] + t0 * gs, Fl, gs}, c->inf_pre_b[lvl] + t0 * gs, gs,
+                        bns(c->inf_bn_b[lvl], Fl), Fl, View{}, ACT_LRELU, View{c->inf_act_b[lvl] + t0 * gs, Fl, gs});
+    if (r) return r;
+    for (int hl = 0; hl < L; ++hl) {
+      const HeadL& h = I.head[hl];
+      if (h.src_level != lvl) continue;
+      heads_fwd(c->inf_act_b[lvl] + t0 * gs, gs, B, h.nin, c->P + h.owm, c->P + h.ows, wg, h.d, c->head_part + t0 * hps,
+                hps, 2 * g.Dz, h.off, n, st);
+    }
+  }
+  LatentLvls lv{};
+  lv.L = L;
+  for (int l = 0; l < L; ++l) {
+    const HeadL& h = I.head[l];
+    lv.bm[l] = c->P + h.obm;
+    lv.bs[l] = c->P + h.obs;
+    lv.off[l] = h.off;
+    lv.dim[l] = h.d;
+  }
+  const long long ms = (long long)B * g.Dz;
+  latent_fwd(c->head_part + t0 * hps, hps, c->head_nsplit, B, g.Dz, lv, wg, g.clipv, g.prior, c->eps_used + t0 * ms, ms,
+             c->mu + t0 * ms, c->sig + t0 * ms, c->z + t0 * ms, ms, c->kl_img + (long long)t0 * B, B, n, st);
+  return 0;
+}
+
 // ============================================================================
 // forward
 // ============================================================================
@@ -990,46 +1046,17 @@ static int engine_forward(svae_ctx* c) {
     }
     HIPCHK(c, hipMemsetAsync(c->kl_img, 0, (size_t)T * B * sizeof(float), st));
   } else {
-  // ---------------- recognition ladders, all steps batched (groups = T) ----------------
-  HIPCHK(c, hipMemsetAsync(c->head_part, 0, (size_t)T * c->head_nsplit * B * 2 * g.Dz * sizeof(float), st));
-  for (int lvl = 0; lvl < L - 1; ++lvl) {
-    const InfStep& I0 = M.inf[0];
-    View in = lvl == 0 ? View{(float*)c->x_in, g.C, 0} : View{c->inf_act_b[lvl - 1], F[lvl], c->inf_gs[lvl - 1]};
-    const long long gs = c->inf_gs[lvl];
-    r = conv_bn_act_fwd(c, I0.a[lvl], T, wg, in, c->inf_pre_a[lvl], gs, c->inf_bn_a[lvl], F[lvl + 1], View{}, ACT_LRELU,
-                        View{c->inf_act_a[lvl], F[lvl + 1], gs});
-    if (r) return r;
-    r = conv_bn_act_fwd(c, I0.b[lvl], T, wg, View{c->inf_act_a[lvl], F[lvl + 1], gs}, c->inf_pre_b[lvl], gs,
-                        c->inf_bn_b[lvl], F[lvl + 1], View{}, ACT_LRELU, View{c->inf_act_b[lvl], F[lvl + 1], gs});
-    if (r) return r;
-    for (int hl = 0; hl < L; ++hl) {
-      const HeadL& h = I0.head[hl];
-      if (h.src_level != lvl) continue;
-      heads_fwd(c->inf_act_b[lvl], gs, B, h.nin, c->P + h.owm, c->P + h.ows, wg, h.d, c->head_part,
-                (long long)c->head_nsplit * B * 2 * g.Dz, 2 * g.Dz, h.off, T, st);
-    }
+  // eps for every step up front (device Philox unless injected)
+  const float* eps = c->eps_in;
+  if (!eps) {
+    philox_normal(c->eps_buf, (long long)T * B * g.Dz, 0x5EED5EEDULL, c->rng_offset, st);
+    c->rng_offset += ((long long)T * B * g.Dz + 3) / 4;
+    eps = c->eps_buf;
   }
-  {
-    LatentLvls lv{};
-    lv.L = L;
-    for (int l = 0; l < L; ++l) {
-      const HeadL& h = M.inf[0].head[l];
-      lv.bm[l] = c->P + h.obm;
-      lv.bs[l] = c->P + h.obs;
-      lv.off[l] = h.off;
-      lv.dim[l] = h.d;
-    }
-    const float* eps = c->eps_in;
-    if (!eps) {
-      philox_normal(c->eps_buf, (long long)T * B * g.Dz, 0x5EED5EEDULL, c->rng_offset, st);
-      c->rng_offset += ((long long)T * B * g.Dz + 3) / 4;
-      eps = c->eps_buf;
-    }
-    c->eps_used = eps;
-    const long long ms = (long long)B * g.Dz;
-    latent_fwd(c->head_part, (long long)c->head_nsplit * B * 2 * g.Dz, c->head_nsplit, B, g.Dz, lv, wg, g.clipv, g.prior,
-               eps, ms, c->mu, c->sig, c->z, ms, c->kl_img, B, T, st);
-  }
+  c->eps_used = eps;
+  // recognition: q(z_t | x) for every step at once (groups = T), or, in Latent InfoMax mode,
+  // q(z_0 | x) here and q(z_t | x_{t-1}) inside the chain (create_recognition_network :1013-1027)
+  if ((r = inference_fwd(c, 0, g.plc ? 1 : T, View{(float*)c->x_in, g.C, 0}))) return r;
   }  // !generative
 
   // ---------------- the chain ----------------
@@ -1037,6 +1064,8 @@ static int engine_forward(svae_ctx* c) {
     svae_ctx::StepBufs& s = c->sb[t];
     const GenStep& G = M.gen[t];
     const float* xprev = t >= 1 ? c->sb[t - 1].xhat : nullptr;
+    if (g.plc && t >= 1 && !c->generative)  // Latent InfoMax: z_t from the previous sample (:1014-1015)
+      if ((r = inference_fwd(c, t, 1, View{(float*)xprev, g.C, 0}))) return r;
     // g_theta encoder of x_{t-1}  (compute_encodings :1764-1777)
     if (t >= 1) {
       const EncStep& E = M.enc[t];
@@ -1132,6 +1161,79 @@ static int engine_forward(svae_ctx* c) {
 // ============================================================================
 // backward  (d self.loss / d theta, phi; sequential_vae.py:1273)
 // ============================================================================
+// Backward of the recognition ladders of steps [t0, t0+n) (reverse of inference_fwd): dz_t ->
+// latent / heads / ladder weight gradients; dx0 != nullptr adds d loss / d in0 (one step).
+static int inference_bwd(svae_ctx* c, int t0, int n, View in0, float* dx0) {
+  Model& M = c->m;
+  const Geo& g = M.g;
+  const int B = g.B, L = g.L;
+  const int* F = g.F;
+  const int* S = g.S;
+  const long long wg = M.phi_stride;
+  hipStream_t st = c->st;
+  int r;
+  const long long ms = (long long)B * g.Dz;
+  latent_bwd(c->mu + t0 * ms, c->sig + t0 * ms, c->eps_used + t0 * ms, c->dz + t0 * ms, ms, ms, B, g.Dz,
+             c->kl_coef + t0, 1, g.prior, g.clipv, c->dhead, (long long)B * 2 * g.Dz, n, st);
+  const InfStep& I0 = M.inf[t0];
+  auto bns = [&](const BNS& b, int C) { return BNS{b.mean + (long long)t0 * C, b.invstd + (long long)t0 * C}; };
+  auto act_a = [&](int l) { return c->inf_act_a[l] + t0 * c->inf_gs[l]; };
+  auto act_b = [&](int l) { return c->inf_act_b[l] + t0 * c->inf_gs[l]; };
+  auto pre_a = [&](int l) { return c->inf_pre_a[l] + t0 * c->inf_gs[l]; };
+  auto pre_b = [&](int l) { return c->inf_pre_b[l] + t0 * c->inf_gs[l]; };
+  // heads of ladder level l -> idb (first write), l's own conv-a input gradient (level l+1) after them
+  auto heads_of = [&](int l) {
+    bool first = true;
+    for (int hl = 0; hl < L; ++hl) {
+      const HeadL& h = I0.head[hl];
+      if (h.src_level != l) continue;
+      const long long gl = c->inf_gs[l];
+      heads_bwd(act_b(l), gl, c->idb, gl, B, h.nin, c->P + h.owm, c->P + h.ows, wg, h.d, c->dhead,
+                (long long)B * 2 * g.Dz, 2 * g.Dz, h.off, c->Gr + h.owm, c->Gr + h.ows, c->Gr + h.obm, c->Gr + h.obs,
+                first ? 0 : 1, n, st);
+      first = false;
+    }
+    return !first;  // wrote idb
+  };
+  BwFuse fu_ib;  // level lvl's conv-b BN partials from level lvl+1's conv-a input-gradient epilogue
+  for (int lvl = L - 2; lvl >= 0; --lvl) {
+    const int Fl = F[lvl + 1];
+    const long long gs = c->inf_gs[lvl];
+    const long long rows = (long long)B * S[lvl + 1] * S[lvl + 1];
+    if (lvl == L - 2) heads_of(lvl);
+    Slot sb = idpre_next(c);
+    r = bn_act_bwd(c, n, rows, Fl, View{c->idb, Fl, gs}, View{act_b(lvl), Fl, gs}, pre_b(lvl), gs, Fl,
+                   bns(c->inf_bn_b[lvl], Fl), Fl, I0.b[lvl].obeta, wg, ACT_LRELU, sb.p, gs, View{}, 0, &fu_ib);
+    if (r) return r;
+    r = on_side(c, sb.ready, sb.freed, [&] {
+      return conv_wgrad(c, I0.b[lvl], n, wg, View{act_a(lvl), Fl, gs}, sb.p, gs, c->Gr + I0.b[lvl].ow);
+    });
+    if (r) return r;
+    BwFuse fu_ia = bw_fuse(c, pre_a(lvl), Fl, gs, nullptr, 0, 0, bns(c->inf_bn_a[lvl], Fl), Fl, I0.a[lvl].obeta, wg,
+                           ACT_LRELU, Fl);
+    r = conv_dgrad(c, I0.b[lvl], n, wg, sb.p, gs, View{c->ida, Fl, gs}, 0, &fu_ia);
+    if (r) return r;
+    Slot sa = idpre_next(c);
+    r = bn_act_bwd(c, n, rows, Fl, View{c->ida, Fl, gs}, View{act_a(lvl), Fl, gs}, pre_a(lvl), gs, Fl,
+                   bns(c->inf_bn_a[lvl], Fl), Fl, I0.a[lvl].obeta, wg, ACT_LRELU, sa.p, gs, View{}, 0, &fu_ia);
+    if (r) return r;
+    View in = lvl == 0 ? in0 : View{act_b(lvl - 1), F[lvl], c->inf_gs[lvl - 1]};
+    r = on_side(c, sa.ready, sa.freed, [&] { return conv_wgrad(c, I0.a[lvl], n, wg, in, sa.p, gs, c->Gr + I0.a[lvl].ow); });
+    if (r) return r;
+    if (lvl > 0) {
+      const bool wrote = heads_of(lvl - 1);
+      fu_ib = bw_fuse(c, pre_b(lvl - 1), F[lvl], c->inf_gs[lvl - 1], nullptr, 0, 0, bns(c->inf_bn_b[lvl - 1], F[lvl]), F[lvl],
+                      I0.b[lvl - 1].obeta, wg, ACT_LRELU, F[lvl]);
+      r = conv_dgrad(c, I0.a[lvl], n, wg, sa.p, gs, View{c->idb, F[lvl], c->inf_gs[lvl - 1]}, wrote ? 1 : 0, &fu_ib);
+      if (r) return r;
+    } else if (dx0) {  // Latent InfoMax: d loss / d x_{t-1} through q(z_t | x_{t-1})
+      r = conv_dgrad(c, I0.a[0], n, wg, sa.p, gs, View{dx0, g.C, 0}, 1);
+      if (r) return r;
+    }
+  }
+  return 0;
+}
+
 static int engine_backward(svae_ctx* c) {
   Model& M = c->m;
   const Geo& g = M.g;
@@ -1151,7 +1253,13 @@ static int engine_backward(svae_ctx* c) {
     hipStreamWaitEvent(c->st2, c->ev_start, 0);
   }
   for (int t = T - 1; t >= 0; --t) {
-    if (t < T - 1) step_hook(c, t + 1);  // step t+1's gradients are complete
+    if (t < T - 1) {
+      if (g.plc) {  // q(z_{t+1} | x_t): its weights' gradients and its share of d loss / d x_t
+        r = inference_bwd(c, t + 1, 1, View{c->sb[t].xhat, g.C, 0}, c->dx[t & 1]);
+        if (r) return r;
+      }
+      step_hook(c, t + 1);  // step t+1's gradients are complete
+    }
     if (t < c->dbg_stop_step) return 0;  // debug: stop after step dbg_stop_step
     svae_ctx::StepBufs& s = c->sb[t];
     const GenStep& G = M.gen[t];
@@ -1326,58 +1434,8 @@ static int engine_backward(svae_ctx* c) {
 
   step_hook(c, 0);
 
-  // ---------------- recognition ladders, batched over T ----------------
-  HIPCHK(c, hipMemcpyAsync(c->kl_coef, c->reg_host, T * sizeof(float), hipMemcpyHostToDevice, st));
-  latent_bwd(c->mu, c->sig, c->eps_used, c->dz, (long long)B * g.Dz, (long long)B * g.Dz, B, g.Dz, c->kl_coef, 1,
-             g.prior, g.clipv, c->dhead, (long long)B * 2 * g.Dz, T, st);
-  const InfStep& I0 = M.inf[0];
-  // heads of ladder level l -> idb (first write), l's own conv-a input gradient (level l+1) after them
-  auto heads_of = [&](int l) {
-    bool first = true;
-    for (int hl = 0; hl < L; ++hl) {
-      const HeadL& h = I0.head[hl];
-      if (h.src_level != l) continue;
-      const long long gl = c->inf_gs[l];
-      heads_bwd(c->inf_act_b[l], gl, c->idb, gl, B, h.nin, c->P + h.owm, c->P + h.ows, wg, h.d, c->dhead,
-                (long long)B * 2 * g.Dz, 2 * g.Dz, h.off, c->Gr + h.owm, c->Gr + h.ows, c->Gr + h.obm, c->Gr + h.obs,
-                first ? 0 : 1, T, st);
-      first = false;
-    }
-    return !first;  // wrote idb
-  };
-  BwFuse fu_ib;  // level lvl's conv-b BN partials from level lvl+1's conv-a input-gradient epilogue
-  for (int lvl = L - 2; lvl >= 0; --lvl) {
-    const int Fl = F[lvl + 1];
-    const long long gs = c->inf_gs[lvl];
-    const long long rows = (long long)B * S[lvl + 1] * S[lvl + 1];
-    if (lvl == L - 2) heads_of(lvl);
-    Slot sb = idpre_next(c);
-    r = bn_act_bwd(c, T, rows, Fl, View{c->idb, Fl, gs}, View{c->inf_act_b[lvl], Fl, gs}, c->inf_pre_b[lvl], gs, Fl,
-                   c->inf_bn_b[lvl], Fl, I0.b[lvl].obeta, wg, ACT_LRELU, sb.p, gs, View{}, 0, &fu_ib);
-    if (r) return r;
-    r = on_side(c, sb.ready, sb.freed, [&] {
-      return conv_wgrad(c, I0.b[lvl], T, wg, View{c->inf_act_a[lvl], Fl, gs}, sb.p, gs, c->Gr + I0.b[lvl].ow);
-    });
-    if (r) return r;
-    BwFuse fu_ia = bw_fuse(c, c->inf_pre_a[lvl], Fl, gs, nullptr, 0, 0, c->inf_bn_a[lvl], Fl, I0.a[lvl].obeta, wg,
-                           ACT_LRELU, Fl);
-    r = conv_dgrad(c, I0.b[lvl], T, wg, sb.p, gs, View{c->ida, Fl, gs}, 0, &fu_ia);
-    if (r) return r;
-    Slot sa = idpre_next(c);
-    r = bn_act_bwd(c, T, rows, Fl, View{c->ida, Fl, gs}, View{c->inf_act_a[lvl], Fl, gs}, c->inf_pre_a[lvl], gs, Fl,
-                   c->inf_bn_a[lvl], Fl, I0.a[lvl].obeta, wg, ACT_LRELU, sa.p, gs, View{}, 0, &fu_ia);
-    if (r) return r;
-    View in = lvl == 0 ? View{(float*)c->x_in, g.C, 0} : View{c->inf_act_b[lvl - 1], F[lvl], c->inf_gs[lvl - 1]};
-    r = on_side(c, sa.ready, sa.freed, [&] { return conv_wgrad(c, I0.a[lvl], T, wg, in, sa.p, gs, c->Gr + I0.a[lvl].ow); });
-    if (r) return r;
-    if (lvl > 0) {
-      const bool wrote = heads_of(lvl - 1);
-      fu_ib = bw_fuse(c, c->inf_pre_b[lvl - 1], F[lvl], c->inf_gs[lvl - 1], nullptr, 0, 0, c->inf_bn_b[lvl - 1], F[lvl],
-                      I0.b[lvl - 1].obeta, wg, ACT_LRELU, F[lvl]);
-      r = conv_dgrad(c, I0.a[lvl], T, wg, sa.p, gs, View{c->idb, F[lvl], c->inf_gs[lvl - 1]}, wrote ? 1 : 0, &fu_ib);
-      if (r) return r;
-    }
-  }
+  // ---------------- recognition ladders: all steps batched, or step 0 (Latent InfoMax) ----------------
+  if ((r = inference_bwd(c, 0, g.plc ? 1 : T, View{(float*)c->x_in, g.C, 0}, nullptr))) return r;
   if (M.shared) {  // public gradient = fixed-order sum of the step copies (side stream joined first)
     if (c->side) {
       hipEventRecord(c->ev_join, c->st2);
@@ -1764,7 +1822,10 @@ int svae_forward(svae_ctx* c, const float* x, const float* target, const float* 
   c->eps_in = eps;
   c->reg = reg_coeff;
   const Geo& g = c->m.g;
-  for (int t = 0; t < g.T; ++t) c->reg_host[t] = reg_coeff * (t == 0 ? g.c_first : 1.f) / (float)g.B;
+  // per-step KL coefficients, passed by value to a one-block kernel: captured at enqueue time,
+  // so a host running steps ahead of the GPU cannot change an earlier step's values
+  for (int t = 0; t < g.T; ++t) c->reg_host[t] = reg_coeff * (t == 0 ? g.c_first : 1.f) * g.kl_on(t) / (float)g.B;
+  set_small(c->kl_coef, c->reg_host, g.T, c->st);
   int r = engine_forward(c);
   if (r) return r;
   HIPCHK(c, hipGetLastError());

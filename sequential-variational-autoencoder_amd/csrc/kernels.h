@@ -203,6 +203,8 @@ void share_broadcast(const float* P, float* Pv, const long long* seg, int nseg, 
 void share_gather(const float* Gv, float* G, const long long* tab, const long long* cp, int ntab, hipStream_t s);
 
 // ---- misc ----
+// dst[0..n) = vals[0..n) (n <= 64), values passed by value in the kernel arguments
+void set_small(float* dst, const float* vals, int n, hipStream_t s);
 void fill_f32(float* p, long long n, float v, hipStream_t s);
 void philox_normal(float* out, long long n, unsigned long long seed, unsigned long long offset, hipStream_t s);
 // column sums of X [rows][C<=4] -> out0[0..n0), out1[0..C-n0)   (part: scratch >= 1024 floats)

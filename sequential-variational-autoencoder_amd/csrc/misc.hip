@@ -927,3 +927,15 @@ void share_broadcast(const float* P, float* Pv, const long long* seg, int nseg, 
 void share_gather(const float* Gv, float* G, const long long* tab, const long long* cp, int ntab, hipStream_t s) {
   if (ntab > 0) hipLaunchKernelGGL(share_gather_kernel, dim3(64, ntab), dim3(256), 0, s, Gv, G, tab, cp);
 }
+
+struct Small64 {
+  float v[64];
+};
+__global__ void set_small_kernel(float* dst, Small64 a, int n) {
+  if ((int)threadIdx.x < n) dst[threadIdx.x] = a.v[threadIdx.x];
+}
+void set_small(float* dst, const float* vals, int n, hipStream_t s) {
+  Small64 a{};
+  for (int i = 0; i < n && i < 64; ++i) a.v[i] = vals[i];
+  hipLaunchKernelGGL(set_small_kernel, dim3(1), dim3(64), 0, s, dst, a, n);
+}

@@ -131,7 +131,7 @@ class SequentialVAE:
             c = self.cfg.first_step_loss_coeff if t == 0 else 1.0
             if self.cfg.intermediate_reconstruction or t == T - 1:
                 tot += 16.0 * c * st[t, 0]
-            tot += reg * c * st[t, 1]
+            tot += reg * c * self.cfg.kl_on(t) * st[t, 1]
         return tot
 
     def elbo_per_image(self):
@@ -141,7 +141,7 @@ class SequentialVAE:
             c = self.cfg.first_step_loss_coeff if t == 0 else 1.0
             if self.cfg.intermediate_reconstruction or t == T - 1:
                 out += 16.0 * c * self.copy_out(_lib.BUF_REC_IMG, t, B).double()
-            out += self._last_reg * c * self.copy_out(_lib.BUF_KL_IMG, t, B).double()
+            out += self._last_reg * c * self.cfg.kl_on(t) * self.copy_out(_lib.BUF_KL_IMG, t, B).double()
         return out
 
     def xhat(self, t=-1):

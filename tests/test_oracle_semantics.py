@@ -106,9 +106,13 @@ def test_param_counts_match_survey():
         assert sum(np.prod(p["shape"]) for p in table if p["dead"]) == dead
 
 
-@pytest.mark.parametrize("preset", ["tiny", "mnist_1step"])
-def test_oracle_matches_torch_twin(preset):
-    cfg = spec.make_config(preset)
+@pytest.mark.parametrize("preset,over", [("tiny", {}), ("mnist_1step", {}),
+                                         ("tiny", dict(predict_latent_code=True)),
+                                         ("tiny", dict(predict_latent_code=True, predict_latent_code_with_regularization=True)),
+                                         ("tiny", dict(regularized_steps=(0, 2)))])
+def test_oracle_matches_torch_twin(preset, over):
+    """The two independent restatements agree (incl. Latent InfoMax and regularized_steps)."""
+    cfg = spec.make_config(preset, **over)
     _, struct, params = spec.init_params(cfg, seed=0)
     x, tgt, eps = spec.make_inputs(cfg, batch=4)
     o = model.forward_backward(cfg, struct, params, x, tgt, eps, reg_coeff=0.37)
@@ -121,9 +125,11 @@ def test_oracle_matches_torch_twin(preset):
         np.testing.assert_allclose(g, p["grads"][k], rtol=1e-8, atol=1e-12 * (1 + np.abs(g).max()), err_msg=k)
 
 
-def test_finite_difference_gradients():
-    cfg = spec.make_config("tiny", mc_steps=2)
-    _, struct, params = spec.init_params(cfg, seed=3)
+@pytest.mark.parametrize("over", [{}, dict(predict_latent_code=True)])
+def test_finite_difference_gradients(over):
+    cfg = spec.make_config("tiny", mc_steps=2, **over)
+    # seed 5 for Latent InfoMax: with seed 3 a ReLU pre-activation sits within h of its kink
+    _, struct, params = spec.init_params(cfg, seed=5 if over else 3)
     x, tgt, eps = spec.make_inputs(cfg, batch=4, seed_x=5, seed_eps=6)
     o = model.forward_backward(cfg, struct, params, x, tgt, eps, reg_coeff=0.8)
     rng = np.random.default_rng(0)
@@ -154,3 +160,21 @@ def test_adam_matches_tf_formula():
     p, m, v = model.adam_update(p, g, m, v, step=1, lr=2e-4)
     # step 1: m = 0.1*clip(g), v = 0.001*g^2, lr_t = lr*sqrt(0.001)/0.1 -> update = lr*sign(g) (up to eps)
     np.testing.assert_allclose(p["w"], [1.0 - 2e-4, -2.0 + 2e-4], rtol=1e-6)
+
+
+def test_kl_terms_follow_regularized_steps_and_infomax():
+    """sequential_vae.py:1154 and :1170-1172: which steps' KL enters self.loss."""
+    c = spec.make_config("tiny")
+    assert [spec.kl_on(c, t) for t in range(3)] == [1, 1, 1]
+    c = spec.make_config("tiny", predict_latent_code=True)
+    assert [spec.kl_on(c, t) for t in range(3)] == [1, 0, 0]
+    c = spec.make_config("tiny", predict_latent_code=True, predict_latent_code_with_regularization=True)
+    assert [spec.kl_on(c, t) for t in range(3)] == [1, 1, 1]
+    c = spec.make_config("tiny", regularized_steps=(0,))
+    assert [spec.kl_on(c, t) for t in range(3)] == [1, 0, 0]
+    # the loss difference is exactly the dropped KL terms
+    _, struct, params = spec.init_params(c, seed=0)
+    x, tgt, eps = spec.make_inputs(c, batch=4)
+    a = model.forward_backward(spec.make_config("tiny"), struct, params, x, tgt, eps, 0.5, want_grads=False)
+    b = model.forward_backward(c, struct, params, x, tgt, eps, 0.5, want_grads=False)
+    assert abs((a["loss"] - b["loss"]) - 0.5 * (a["kl"][1] + a["kl"][2])) <= 1e-12 * abs(a["loss"])
