@@ -26,7 +26,7 @@ PKG = "sequential-variational-autoencoder_amd"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no 2:1 sparsity)
 # dominant kernel of the bf16 step (profiles/r01_*_bf16_kernel_stats.txt: largest total time):
-# the halo weight-GEMM, stride 1 (runs on the engine's side stream, overlapped with the BN chain)
+# the halo weight-GEMM, stride-1 instance (side stream, overlapped with the BN chain; profiles/r01_v13)
 DOMINANT_KID = "KID_WHALO_32_S1"
 
 

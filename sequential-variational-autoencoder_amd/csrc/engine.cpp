@@ -755,9 +755,12 @@ static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, V
     if (wgrad_halo_plan(w, groups, &pl)) {
       // pixel chunks split over blocks: ~1024 blocks in flight, slab within capacity
       const long long per = 16LL * w.M * w.N;
-      // ~512 blocks, but >= 4 chunks per block: every split writes a full 16*M*N partial
-      long long ns = (512 + (long long)pl.tiles * groups - 1) / ((long long)pl.tiles * groups);
-      ns = std::min<long long>(ns, std::max<long long>(1, pl.h.nchunk / 4));
+      // ~wh_target blocks, but >= wh_minch chunks per block: every split writes (and the reduce
+      // reads) a full 16*M*N partial, so short splits cost more partial traffic than they save
+      static const int wh_target = getenv("SVAE_WH_TARGET") ? atoi(getenv("SVAE_WH_TARGET")) : 256;
+      static const int wh_minch = getenv("SVAE_WH_MINCH") ? atoi(getenv("SVAE_WH_MINCH")) : 8;
+      long long ns = (wh_target + (long long)pl.tiles * groups - 1) / ((long long)pl.tiles * groups);
+      ns = std::min<long long>(ns, std::max<long long>(1, pl.h.nchunk / wh_minch));
       ns = std::min<long long>(ns, std::max<long long>(1, c->slab_cap / (per * groups)));
       w.nsplit = (int)std::max<long long>(1, ns);
       if (w.nsplit == 1) {

@@ -654,7 +654,7 @@ __device__ __forceinline__ bf16x8 join_tr(v4i16 lo, v4i16 hi) {
 }
 
 template <int BN, int S>
-__global__ __launch_bounds__(256, BN == 32 ? 2 : 1) void wgrad_halo_kernel(WHaloArgs h) {
+__global__ __launch_bounds__(256, (BN == 32 && S == 1) ? 2 : 1) void wgrad_halo_kernel(WHaloArgs h) {
   constexpr int NS = BN / 32;              // 32-column MFMA subtiles
   constexpr int GP = S == 1 ? 32 : 48;     // window pixel pitch (bf16)
   extern __shared__ __attribute__((aligned(16))) __bf16 wsm[];
