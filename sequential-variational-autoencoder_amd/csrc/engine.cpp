@@ -392,6 +392,8 @@ struct svae_ctx {
   static constexpr int NR = 3;  // dpre ring slots (generator / encoder layers)
   bool side = false;
   hipStream_t st2 = nullptr;
+  hipStream_t st3 = nullptr;  // split-latent FCs (fwd up front, bwd per level): no weight-GEMM queue ahead
+  hipEvent_t ev_dz = nullptr, ev_j3 = nullptr;
   float* slab2 = nullptr;
   float* dpre_ring[NR] = {};
   float* idpre_ring[2] = {};
@@ -401,6 +403,13 @@ struct svae_ctx {
   // backward step hook (data-parallel bucketed all-reduce): called on the host after the
   // backward of chain step t is enqueued, with the side stream ordered after all of that step's
   // work on both streams; t = -1 after the whole backward (streams joined)
+  // split-latent FCs on the side stream: forward for all steps up front (they depend only on z),
+  // backward per level off the critical path, reading ring copies of dcat / dtop
+  float* dcat_ring[2] = {};
+  float* dtop_ring[2] = {};
+  int dcat_pos = 0, dtop_pos = 0;
+  hipEvent_t ev_dcat_free[2] = {}, ev_dtop_free[2] = {}, ev_aux = nullptr, ev_aux2 = nullptr;
+  hipEvent_t ev_sfc[64] = {};
   svae_step_hook hook = nullptr;
   void* hook_user = nullptr;
   hipEvent_t ev_hook = nullptr;
@@ -971,6 +980,8 @@ static void step_hook(svae_ctx* c, int t) {
   if (c->side) {
     hipEventRecord(c->ev_hook, c->st);
     hipStreamWaitEvent(c->st2, c->ev_hook, 0);
+    hipEventRecord(c->ev_j3, c->st3);  // the step's split-latent gradients
+    hipStreamWaitEvent(c->st2, c->ev_j3, 0);
   }
   c->hook(c->hook_user, t);
 }
@@ -1021,6 +1032,31 @@ static int inference_fwd(svae_ctx* c, int t0, int n, View in0) {
   return 0;
 }
 
+// split_latent of step t (:1796-1806): ladder_i straight into the step's concat buffers
+static void split_latent_fwd(svae_ctx* c, int t, hipStream_t stream) {
+  const Model& M = c->m;
+  const Geo& g = M.g;
+  const int B = g.B, L = g.L;
+  const int* F = g.F;
+  const int* S = g.S;
+  svae_ctx::StepBufs& s = c->sb[t];
+  const GenStep& G = M.gen[t];
+  const float* zt = c->z + (long long)t * B * g.Dz;
+  int zoff = 0;
+  for (int i = 0; i < L; ++i) {
+    const FcL& f = G.split[i];
+    if (i < L - 1) {
+      splitfc_fwd(zt, g.Dz, zoff, B, g.D[i], c->P + f.ow, c->P + f.obeta, f.nout, s.split_mean[i], s.split_inv[i],
+                  s.cat[i] + F[i + 1], (long long)S[i + 1] * S[i + 1] * 2 * F[i + 1], F[i + 1], 2 * F[i + 1], stream);
+    } else {
+      const int coff = t >= 1 ? F[L] : 0;
+      splitfc_fwd(zt, g.Dz, zoff, B, g.D[i], c->P + f.ow, c->P + f.obeta, f.nout, s.split_mean[i], s.split_inv[i],
+                  s.top_cat + coff, s.ktop, f.nout, 0, stream);
+    }
+    zoff += g.D[i];
+  }
+}
+
 // ============================================================================
 // forward
 // ============================================================================
@@ -1061,6 +1097,17 @@ static int engine_forward(svae_ctx* c) {
   // q(z_0 | x) here and q(z_t | x_{t-1}) inside the chain (create_recognition_network :1013-1027)
   if ((r = inference_fwd(c, 0, g.plc ? 1 : T, View{(float*)c->x_in, g.C, 0}))) return r;
   }  // !generative
+  // split_latent of every step on the side stream (z is known for all steps unless Latent
+  // InfoMax draws z_t inside the chain); step t's decoder waits on ev_sfc[t]
+  const bool sfc_side = c->side && !g.plc && T <= 64;
+  if (sfc_side) {
+    hipEventRecord(c->ev_aux, st);
+    hipStreamWaitEvent(c->st3, c->ev_aux, 0);
+    for (int t = 0; t < T; ++t) {
+      split_latent_fwd(c, t, c->st3);
+      hipEventRecord(c->ev_sfc[t], c->st3);
+    }
+  }
 
   // ---------------- the chain ----------------
   for (int t = 0; t < T; ++t) {
@@ -1091,22 +1138,8 @@ static int engine_forward(svae_ctx* c) {
       if (r) return r;
     }
     // split_latent (:1796-1806): ladder_i straight into the concat buffers
-    const float* zt = c->z + (long long)t * B * g.Dz;
-    {
-      int zoff = 0;
-      for (int i = 0; i < L; ++i) {
-        const FcL& f = G.split[i];
-        if (i < L - 1) {
-          splitfc_fwd(zt, g.Dz, zoff, B, g.D[i], c->P + f.ow, c->P + f.obeta, f.nout, s.split_mean[i], s.split_inv[i],
-                      s.cat[i] + F[i + 1], (long long)S[i + 1] * S[i + 1] * 2 * F[i + 1], F[i + 1], 2 * F[i + 1], st);
-        } else {
-          const int coff = t >= 1 ? F[L] : 0;
-          splitfc_fwd(zt, g.Dz, zoff, B, g.D[i], c->P + f.ow, c->P + f.obeta, f.nout, s.split_mean[i], s.split_inv[i],
-                      s.top_cat + coff, s.ktop, f.nout, 0, st);
-        }
-        zoff += g.D[i];
-      }
-    }
+    if (sfc_side) hipStreamWaitEvent(st, c->ev_sfc[t], 0);
+    else split_latent_fwd(c, t, st);
     // generator_ladder decoder (:1695-1721)
     r = fc_bn_fwd(c, G.top, View{s.top_cat, s.ktop, 0}, s.top_pre, s.top_bn, View{s.top_act, S[L] * S[L] * F[L], 0});
     if (r) return r;
@@ -1176,6 +1209,7 @@ static int inference_bwd(svae_ctx* c, int t0, int n, View in0, float* dx0) {
   hipStream_t st = c->st;
   int r;
   const long long ms = (long long)B * g.Dz;
+  if (c->side) hipStreamWaitEvent(st, c->ev_dz, 0);  // dz_t: split-latent backward (st3)
   latent_bwd(c->mu + t0 * ms, c->sig + t0 * ms, c->eps_used + t0 * ms, c->dz + t0 * ms, ms, ms, B, g.Dz,
              c->kl_coef + t0, 1, g.prior, g.clipv, c->dhead, (long long)B * 2 * g.Dz, n, st);
   const InfStep& I0 = M.inf[t0];
@@ -1334,22 +1368,38 @@ static int engine_backward(svae_ctx* c) {
       // s2[lvl]'s BN partials over the d-half of dcat (shortcut at t >= 1: act' from the stored y)
       BwFuse fu_s2 = bw_fuse(c, s.s2_pre[lvl], Fl, 0, t >= 1 ? s.cat[lvl] : nullptr, 2 * Fl, 0, s.s2_bn[lvl], 0,
                              l2.obeta, 0, ACT_RELU, Fl);
-      r = conv_dgrad(c, l1, 1, 0, sl.p, 0, View{c->dcat, 2 * Fl, 0}, 0, &fu_s2);
+      // dcat: ring of two when the split-latent backward reads it on the side stream
+      float* dcat = c->dcat;
+      int kc = 0;
+      if (c->side) {
+        kc = c->dcat_pos;
+        c->dcat_pos ^= 1;
+        dcat = c->dcat_ring[kc];
+        hipStreamWaitEvent(st, c->ev_dcat_free[kc], 0);
+      }
+      r = conv_dgrad(c, l1, 1, 0, sl.p, 0, View{dcat, 2 * Fl, 0}, 0, &fu_s2);
       if (r) return r;
-      // latent half of the concat -> split_latent level lvl
+      // latent half of the concat -> split_latent level lvl (side stream: off the critical path)
       {
         const FcL& f = G.split[lvl];
         int zoff = 0;
         for (int i = 0; i < lvl; ++i) zoff += g.D[i];
+        hipStream_t ss = st;
+        if (c->side) {
+          hipEventRecord(c->ev_aux, st);
+          hipStreamWaitEvent(c->st3, c->ev_aux, 0);
+          ss = c->st3;
+        }
         splitfc_bwd(c->z + (long long)t * B * g.Dz, g.Dz, zoff, B, g.D[lvl], c->P + f.ow, c->P + f.obeta, f.nout,
-                    s.split_mean[lvl], s.split_inv[lvl], c->dcat + Fl, (long long)S[lvl + 1] * S[lvl + 1] * 2 * Fl, Fl,
-                    2 * Fl, c->Gr + f.ow, c->Gr + f.obeta, c->sfc_part, st);
-        splitfc_dz_reduce(c->sfc_part, splitfc_blocks(f.nout), B, g.D[lvl], dzt, g.Dz, zoff, st);
+                    s.split_mean[lvl], s.split_inv[lvl], dcat + Fl, (long long)S[lvl + 1] * S[lvl + 1] * 2 * Fl, Fl,
+                    2 * Fl, c->Gr + f.ow, c->Gr + f.obeta, c->sfc_part, ss);
+        splitfc_dz_reduce(c->sfc_part, splitfc_blocks(f.nout), B, g.D[lvl], dzt, g.Dz, zoff, ss);
+        if (c->side) hipEventRecord(c->ev_dcat_free[kc], c->st3);
       }
       // s2: relu(BN(convT_s2(cur)) + enc_{lvl+1})
       View dres = t >= 1 ? View{c->denc[lvl], Fl, 0} : View{};
       sl = dpre_next(c);
-      r = bn_act_bwd(c, 1, rows, Fl, View{c->dcat, 2 * Fl, 0}, View{s.cat[lvl], 2 * Fl, 0}, s.s2_pre[lvl], 0, Fl,
+      r = bn_act_bwd(c, 1, rows, Fl, View{dcat, 2 * Fl, 0}, View{s.cat[lvl], 2 * Fl, 0}, s.s2_pre[lvl], 0, Fl,
                      s.s2_bn[lvl], 0, l2.obeta, 0, ACT_RELU, sl.p, 0, dres, 0, &fu_s2);
       if (r) return r;
       View in = lvl == L - 2 ? View{s.top_act, F[L], 0} : View{s.s1_act[lvl + 1], F[lvl + 2], 0};
@@ -1368,22 +1418,40 @@ static int engine_backward(svae_ctx* c) {
     }
     // ---- top fc_bn_lrelu (:1704)
     const int ntop = S[L] * S[L] * F[L];
+    float* dtop = c->dtop;
+    int kt = 0;
+    if (c->side) {  // ring of two: the side stream's split-latent backward reads it
+      kt = c->dtop_pos;
+      c->dtop_pos ^= 1;
+      dtop = c->dtop_ring[kt];
+      hipStreamWaitEvent(st, c->ev_dtop_free[kt], 0);
+    }
     r = fc_bn_bwd(c, G.top, View{s.top_cat, s.ktop, 0}, View{dcur, ntop, 0}, View{s.top_act, ntop, 0}, s.top_pre,
-                  s.top_bn, View{c->dtop, s.ktop, 0});
+                  s.top_bn, View{dtop, s.ktop, 0});
     if (r) return r;
     {
       const FcL& f = G.split[L - 1];
       const int coff = t >= 1 ? F[L] : 0;
+      hipStream_t ss = st;
+      if (c->side) {
+        hipEventRecord(c->ev_aux, st);
+        hipStreamWaitEvent(c->st3, c->ev_aux, 0);
+        ss = c->st3;
+      }
       splitfc_bwd(c->z + (long long)t * B * g.Dz, g.Dz, g.Dz - g.D[L - 1], B, g.D[L - 1], c->P + f.ow, c->P + f.obeta,
-                  f.nout, s.split_mean[L - 1], s.split_inv[L - 1], c->dtop + coff, s.ktop, f.nout, 0, c->Gr + f.ow,
-                  c->Gr + f.obeta, c->sfc_part, st);
-      splitfc_dz_reduce(c->sfc_part, splitfc_blocks(f.nout), B, g.D[L - 1], dzt, g.Dz, g.Dz - g.D[L - 1], st);
+                  f.nout, s.split_mean[L - 1], s.split_inv[L - 1], dtop + coff, s.ktop, f.nout, 0, c->Gr + f.ow,
+                  c->Gr + f.obeta, c->sfc_part, ss);
+      splitfc_dz_reduce(c->sfc_part, splitfc_blocks(f.nout), B, g.D[L - 1], dzt, g.Dz, g.Dz - g.D[L - 1], ss);
+      if (c->side) {
+        hipEventRecord(c->ev_dtop_free[kt], c->st3);
+        hipEventRecord(c->ev_dz, c->st3);  // dz_t complete (the top level is the step's last split FC)
+      }
     }
     // ---- g_theta encoder of x_{t-1} (reverse of :1764-1775)
     if (t >= 1) {
       const EncStep& E = M.enc[t];
       const int nc = S[L] * S[L] * F[L - 1];
-      r = fc_bn_bwd(c, E.fc, View{s.enc_c_act, nc, 0}, View{c->dtop, s.ktop, 0}, View{s.top_cat, s.ktop, 0},
+      r = fc_bn_bwd(c, E.fc, View{s.enc_c_act, nc, 0}, View{dtop, s.ktop, 0}, View{s.top_cat, s.ktop, 0},
                     s.encfc_pre, s.enc_bn_fc, View{c->denc_c, nc, 0});
       if (r) return r;
       const long long rc = (long long)B * S[L] * S[L];
@@ -1443,6 +1511,8 @@ static int engine_backward(svae_ctx* c) {
     if (c->side) {
       hipEventRecord(c->ev_join, c->st2);
       hipStreamWaitEvent(st, c->ev_join, 0);
+      hipEventRecord(c->ev_j3, c->st3);
+      hipStreamWaitEvent(st, c->ev_j3, 0);
     }
     share_gather(c->Gv, c->Gpub, c->share_tab, c->share_cp, c->share_ntab, st);
   }
@@ -1541,6 +1611,10 @@ static bool plan(svae_ctx* c) {
   for (int i = 0; i < svae_ctx::NR; ++i) c->dpre_ring[i] = A(maxact);
   c->dcat = A(maxact);
   c->dtop = A((long long)B * (F[L] + F[L + 1]));
+  c->dcat_ring[0] = c->dcat;
+  c->dcat_ring[1] = A(maxact);
+  c->dtop_ring[0] = c->dtop;
+  c->dtop_ring[1] = A((long long)B * (F[L] + F[L + 1]));
   c->denc_c = A((long long)B * S[L] * S[L] * F[L - 1]);
   for (int lvl = 0; lvl < L - 1; ++lvl) c->denc[lvl] = A((long long)B * S[lvl + 1] * S[lvl + 1] * F[lvl + 1]);
   c->sfc_part = A((long long)splitfc_blocks((int)maxJ) * B * maxK);
@@ -1716,10 +1790,14 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
     const char* ns = getenv("SVAE_NO_SIDE");
     if (!(ns && ns[0] == '1')) {
       bool ok = hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking) == hipSuccess;
+      ok = ok && hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking) == hipSuccess;
       auto mk = [&](hipEvent_t* ev) { ok = ok && hipEventCreateWithFlags(ev, hipEventDisableTiming) == hipSuccess; };
       for (int i = 0; i < svae_ctx::NR; ++i) { mk(&c->ev_ready[i]); mk(&c->ev_free[i]); }
       for (int i = 0; i < 2; ++i) { mk(&c->ev_iready[i]); mk(&c->ev_ifree[i]); }
       mk(&c->ev_da_ready); mk(&c->ev_da_free); mk(&c->ev_start); mk(&c->ev_join); mk(&c->ev_hook);
+      mk(&c->ev_aux); mk(&c->ev_aux2); mk(&c->ev_dz); mk(&c->ev_j3);
+      for (int i = 0; i < 2; ++i) { mk(&c->ev_dcat_free[i]); mk(&c->ev_dtop_free[i]); }
+      for (int i = 0; i < 64; ++i) mk(&c->ev_sfc[i]);
       c->side = ok;
     }
   }
@@ -1730,11 +1808,15 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
 
 int svae_destroy(svae_ctx* c) {
   if (!c) return 0;
-  if (c->st2) {
-    hipStreamSynchronize(c->st2);
-    hipStreamDestroy(c->st2);
-  }
-  for (hipEvent_t ev : {c->ev_da_ready, c->ev_da_free, c->ev_start, c->ev_join, c->ev_hook})
+  for (hipStream_t sx : {c->st2, c->st3})
+    if (sx) {
+      hipStreamSynchronize(sx);
+      hipStreamDestroy(sx);
+    }
+  for (hipEvent_t ev : {c->ev_da_ready, c->ev_da_free, c->ev_start, c->ev_join, c->ev_hook, c->ev_aux, c->ev_aux2, c->ev_dz, c->ev_j3,
+                        c->ev_dcat_free[0], c->ev_dcat_free[1], c->ev_dtop_free[0], c->ev_dtop_free[1]})
+    if (ev) hipEventDestroy(ev);
+  for (hipEvent_t ev : c->ev_sfc)
     if (ev) hipEventDestroy(ev);
   for (int i = 0; i < svae_ctx::NR; ++i) {
     if (c->ev_ready[i]) hipEventDestroy(c->ev_ready[i]);
@@ -1858,6 +1940,8 @@ int svae_backward(svae_ctx* c, void* stream) {
   if (c->side) {  // join: the side stream's weight gradients are ordered before later caller work
     hipEventRecord(c->ev_join, c->st2);
     hipStreamWaitEvent(c->st, c->ev_join, 0);
+    hipEventRecord(c->ev_j3, c->st3);
+    hipStreamWaitEvent(c->st, c->ev_j3, 0);
   }
   if (!r && c->hook) c->hook(c->hook_user, -1);
   if (r) return r;
