@@ -389,7 +389,7 @@ struct Probe {
 struct svae_ctx {
   Probe probe;
   // ---- backward: weight gradients on a side stream (overlap the BN / dgrad chain) ----
-  static constexpr int NR = 3;  // dpre ring slots (generator / encoder layers)
+  static constexpr int NR = 6;  // dpre ring slots (generator / encoder layers)
   bool side = false;
   hipStream_t st2 = nullptr;
   hipStream_t st3 = nullptr;  // split-latent FCs (fwd up front, bwd per level): no weight-GEMM queue ahead
