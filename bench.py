@@ -194,8 +194,7 @@ def main():
     def step(it):
         reg = 1.0 - math.exp(-it / cfg.reg_coeff_rate)
         net.forward(x, tgt, None, reg)
-        net.backward()
-        net.apply_gradients(cfg.learning_rate, it)
+        net.backward_apply(cfg.learning_rate, it)  # backward + clip/Adam per chain-step bucket
 
     probe_kid = getattr(L, DOMINANT_KID) if args.dtype == "bf16" else None
     it = 0

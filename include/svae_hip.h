@@ -121,8 +121,23 @@ int svae_backward(svae_ctx* ctx, void* stream);
 typedef void (*svae_step_hook)(void* user, int t);
 int svae_set_backward_hook(svae_ctx* ctx, svae_step_hook hook, void* user);
 void* svae_hook_stream(svae_ctx* ctx);
-/* clip(+-clip) + TF Adam on the live region (sequential_vae.py:1274-1276); step >= 1. */
+/* clip(+-clip) + TF Adam on the live region (sequential_vae.py:1274-1276); step >= 1.  In bf16
+ * mode (no weight sharing) the update also refreshes the engine's bf16 weight copies, and the next
+ * svae_forward reuses them when the updates since the last forward covered the whole live region.
+ * Parameters the caller writes itself must be announced with svae_bind before the next forward. */
 int svae_adam(svae_ctx* ctx, float lr, int64_t step, float clip, void* stream);
+/* The same update on the live sub-range [lo, hi) (lo a multiple of 4; tensor-aligned ranges). */
+int svae_adam_range(svae_ctx* ctx, int64_t lo, int64_t hi, float lr, int64_t step, float clip, void* stream);
+/* svae_backward then svae_adam as one call (sess.run(train_op), sequential_vae.py:1365), bit for bit
+ * the same parameters: each chain step's generator/encoder bucket is updated on the engine's side
+ * stream as soon as its gradient is final, right after hook(user, t) -- a hook that exchanges
+ * gradients must have made svae_hook_stream(ctx) wait for the exchange of that bucket before it
+ * returns -- and the recognition bucket after hook(user, -1).  Shared weights: the two calls in
+ * sequence. */
+int svae_backward_adam(svae_ctx* ctx, float lr, int64_t step, float clip, void* stream);
+/* Adam moments of the live region [0, n_live) (tf.train.Saver's "<var>/Adam", "<var>/Adam_1" slots,
+ * abstract_network.py:124-152): dir 0 copies them out to m, v; dir 1 in.  Device pointers. */
+int svae_adam_state(svae_ctx* ctx, int dir, float* m, float* v, int64_t n, void* stream);
 /* Copy an internal buffer (device -> caller device pointer). */
 int svae_copy_out(svae_ctx* ctx, int which, int step, float* dst, int64_t n, void* stream);
 

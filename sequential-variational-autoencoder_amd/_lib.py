@@ -69,6 +69,9 @@ def lib():
         "svae_backward": ([vp, vp], i32),
         "svae_generate": ([vp, vp, vp], i32),
         "svae_adam": ([vp, f32, i64, f32, vp], i32),
+        "svae_adam_range": ([vp, i64, i64, f32, i64, f32, vp], i32),
+        "svae_backward_adam": ([vp, f32, i64, f32, vp], i32),
+        "svae_adam_state": ([vp, i32, vp, vp, i64, vp], i32),
         "svae_copy_out": ([vp, i32, i32, vp, i64, vp], i32),
         "svae_op_conv": ([vp, i32, i32, i32, vp, i32, i32, i32, vp, vp], i32),
         "svae_op_conv_dgrad": ([vp, i32, i32, i32, vp, i32, i32, i32, vp, vp], i32),
@@ -98,7 +101,7 @@ EXPORTED = ["svae_param_count", "svae_param_layout", "svae_create", "svae_destro
             "svae_op_conv", "svae_op_conv_dgrad", "svae_op_conv_wgrad", "svae_op_bn_act",
             "svae_op_bn_act_bwd", "svae_op_fc", "svae_probe_begin", "svae_probe_end", "svae_kernel_name",
             "svae_op_gather_bf16", "svae_op_wgrad_bf16", "svae_generate", "svae_set_backward_hook",
-            "svae_hook_stream"]
+            "svae_hook_stream", "svae_adam_range", "svae_backward_adam", "svae_adam_state"]
 
 # bf16 GEMM instance ids (csrc/kernels.h KernelId) for svae_probe_begin
 KID_IGEMM_BF16_256x32 = 2

@@ -189,6 +189,10 @@ struct Model {
   std::vector<EncStep> enc;
   std::vector<GenStep> gen;
   long long n_total = 0, n_live = 0, phi_stride = 0;
+  // gradient buckets in backward completion order: theta of step t = [step_lo[t], step_hi[t]),
+  // all recognition weights = [0, phi_hi) (parallel.step_buckets restates these)
+  std::vector<long long> step_lo, step_hi;
+  long long phi_hi = 0;
 
   // Public table (what svae_param_layout reports and the caller's buffers hold).  Without
   // weight sharing it is descs itself.  With sharing the engine still runs on a private
@@ -325,6 +329,8 @@ struct Model {
     // with 16-byte vector loads, and rows of NHWC tiles stay line-aligned.
     auto align = [](long long v) { return (v + 63) / 64 * 64; };
     long long o = 0;
+    step_lo.assign(g.T, 0);
+    step_hi.assign(g.T, 0);
     for (int r = 0; r < 3; ++r) {
       for (int t = 0; t < g.T; ++t) {
         long long start = o;
@@ -336,7 +342,9 @@ struct Model {
           }
         o = align(o);
         if (r == R_PHI && t == 0) phi_stride = o - start;
+        if (r == R_THETA) { step_lo[t] = start; step_hi[t] = o; }
       }
+      if (r == R_PHI) phi_hi = o;
       if (r == R_THETA) n_live = o;
     }
     n_total = o;
@@ -476,6 +484,12 @@ struct svae_ctx {
   void *wN = nullptr, *wT = nullptr;   // bf16 weight shadows (dtype=1)
   void *tiles_d = nullptr, *offs_d = nullptr;
   int ntiles = 0;
+  std::vector<long long> tile_off;  // tiles sorted by tensor offset: each tile's tensor offset
+  long long fresh = 0;  // live elements whose bf16 shadows an Adam update refreshed since the last forward
+  // svae_backward_adam: clip + Adam of each step's bucket inside the backward (side stream)
+  bool fa_on = false;
+  float fa_lr = 0.f, fa_clip = 0.f;
+  long long fa_step = 0;
   long long slab_cap;
   const float* x_in = nullptr;
   const float* tgt_in = nullptr;
@@ -975,15 +989,20 @@ static int fc_bn_bwd(svae_ctx* c, const FcL& f, View in, View dy, View y, const 
 
 // host hook after chain step t's backward: the side stream is ordered after all of the step's
 // work on both streams, so a collective issued on it sees that step's complete gradients
+static void adam_range(svae_ctx* c, long long lo, long long hi, float lr, long long step, float clip, hipStream_t s);
+
 static void step_hook(svae_ctx* c, int t) {
-  if (!c->hook || c->m.shared) return;  // shared tensors are complete only after every step
+  if ((!c->hook && !c->fa_on) || c->m.shared) return;  // shared tensors are complete only after every step
   if (c->side) {
     hipEventRecord(c->ev_hook, c->st);
     hipStreamWaitEvent(c->st2, c->ev_hook, 0);
     hipEventRecord(c->ev_j3, c->st3);  // the step's split-latent gradients
     hipStreamWaitEvent(c->st2, c->ev_j3, 0);
   }
-  c->hook(c->hook_user, t);
+  if (c->hook) c->hook(c->hook_user, t);
+  // the bucket's update follows whatever exchange the hook ordered on the side stream; the
+  // backward of steps < t reads neither theta_t nor its shadows
+  if (c->fa_on) adam_range(c, c->m.step_lo[t], c->m.step_hi[t], c->fa_lr, c->fa_step, c->fa_clip, c->st2);
 }
 
 // Recognition ladders of steps [t0, t0+n) (inference_ladder :1579-1630, heads :1592-1609) on
@@ -1072,7 +1091,10 @@ static int engine_forward(svae_ctx* c) {
 
   if ((r = acc_reset(c))) return r;
   if (M.shared) share_broadcast(c->Ppub, c->Pv, c->share_seg, c->share_nseg, st);
-  if (g.bf16) shadow_weights(c->P, c->wN, c->wT, M.n_live, c->tiles_d, c->ntiles, c->offs_d, st);
+  // the shadows are current when the last Adam updates covered the whole live region
+  if (g.bf16 && !(c->fresh == M.n_live && !M.shared))
+    shadow_weights(c->P, c->wN, c->wT, M.n_live, c->tiles_d, c->ntiles, c->offs_d, st);
+  c->fresh = 0;
   if (c->generative) {
     // generative mode (sequential_vae.py:947-952, :1025 latent_generative = self.latents[t]):
     // z_t comes from the caller (or N(0,1)), the recognition networks do not run
@@ -1753,13 +1775,9 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
     hipMemset(c->wT, 0, (size_t)nl * 2);
     std::vector<long long> offs;
     std::vector<int> tiles;
-    auto add = [&](long long off, int taps, int R, int Cc) {
-      int id = (int)(offs.size() / 3);
-      offs.push_back(off); offs.push_back(R); offs.push_back(Cc);
-      for (int t = 0; t < taps; ++t)
-        for (int r = 0; r < R; r += 32)
-          for (int q = 0; q < Cc; q += 32) { tiles.push_back(id); tiles.push_back(t); tiles.push_back(r); tiles.push_back(q); }
-    };
+    struct TT { long long off; int taps, R, Cc; };
+    std::vector<TT> tt;
+    auto add = [&](long long off, int taps, int R, int Cc) { tt.push_back(TT{off, taps, R, Cc}); };
     auto conv = [&](const ConvL& L) {
       if (L.w < 0) return;
       if (L.tr) add(L.ow, 16, L.cout, L.cin);   // [tap][co][ci]
@@ -1774,6 +1792,18 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
       }
       if (t >= 1) { conv(c->m.enc[t].c); add(c->m.enc[t].fc.ow, 1, c->m.enc[t].fc.nin, c->m.enc[t].fc.nout); }
       add(c->m.gen[t].top.ow, 1, c->m.gen[t].top.nin, c->m.gen[t].top.nout);
+    }
+    // tiles in tensor-offset order, so the tiles of a parameter range are contiguous (adam_range)
+    std::sort(tt.begin(), tt.end(), [](const TT& a, const TT& b) { return a.off < b.off; });
+    for (const TT& x : tt) {
+      int id = (int)(offs.size() / 3);
+      offs.push_back(x.off); offs.push_back(x.R); offs.push_back(x.Cc);
+      for (int t = 0; t < x.taps; ++t)
+        for (int r = 0; r < x.R; r += 32)
+          for (int q = 0; q < x.Cc; q += 32) {
+            tiles.push_back(id); tiles.push_back(t); tiles.push_back(r); tiles.push_back(q);
+            c->tile_off.push_back(x.off);
+          }
     }
     c->ntiles = (int)(tiles.size() / 4);
     e = hipMalloc(&c->tiles_d, tiles.size() * sizeof(int));
@@ -1886,6 +1916,7 @@ int svae_bind(svae_ctx* c, float* params, float* grads) {
   if (!c || !params || !grads) return fail(c, SVAE_EBADARG, "null buffer");
   c->Ppub = params;
   c->Gpub = grads;
+  c->fresh = 0;  // caller-written parameters: the next forward rebuilds the bf16 shadows
   HIPCHK(c, hipMemset(grads, 0, (size_t)c->m.p_total * sizeof(float)));
   if (c->m.shared) {
     c->P = c->Pv;
@@ -1958,13 +1989,65 @@ int svae_set_backward_hook(svae_ctx* c, svae_step_hook hook, void* user) {
 
 void* svae_hook_stream(svae_ctx* c) { return c ? (void*)(c->side ? c->st2 : c->st) : nullptr; }
 
-int svae_adam(svae_ctx* c, float lr, int64_t step, float clip, void* stream) {
-  if (!c || !c->P || step < 1) return fail(c, SVAE_EBADARG, "bad adam args");
+// clip + TF Adam (sequential_vae.py:1267,1274-1276) on the public live sub-range [lo, hi); in bf16
+// mode without sharing also the bf16 shadows of the tensors that start in it (N layout fused into
+// the update, per-tap transposes of its tiles), counted in c->fresh for the next forward
+static void adam_range(svae_ctx* c, long long lo, long long hi, float lr, long long step, float clip, hipStream_t s) {
   const double b1 = 0.9, b2 = 0.999;
   const double lr_t = lr * std::sqrt(1.0 - std::pow(b2, (double)step)) / (1.0 - std::pow(b1, (double)step));
-  adam_step(c->Ppub, c->Gpub, c->adam_m, c->adam_v, c->m.p_live, (float)lr_t, (float)b1, (float)b2, 1e-8f, clip,
-            (hipStream_t)stream);
+  const bool sh = c->m.g.bf16 && !c->m.shared && c->wN;
+  adam_step(c->Ppub + lo, c->Gpub + lo, c->adam_m + lo, c->adam_v + lo, sh ? (void*)((__bf16*)c->wN + lo) : nullptr,
+            hi - lo, (float)lr_t, (float)b1, (float)b2, 1e-8f, clip, s);
+  if (sh) {
+    const long long tb = std::lower_bound(c->tile_off.begin(), c->tile_off.end(), lo) - c->tile_off.begin();
+    const long long te = std::lower_bound(c->tile_off.begin(), c->tile_off.end(), hi) - c->tile_off.begin();
+    shadow_t_tiles(c->Ppub, c->wT, (const int*)c->tiles_d + 4 * tb, (int)(te - tb), c->offs_d, s);
+    c->fresh += hi - lo;
+  }
+}
+
+int svae_adam(svae_ctx* c, float lr, int64_t step, float clip, void* stream) {
+  if (!c || !c->P || step < 1) return fail(c, SVAE_EBADARG, "bad adam args");
+  adam_range(c, 0, c->m.p_live, lr, step, clip, (hipStream_t)stream);
   HIPCHK(c, hipGetLastError());
+  return 0;
+}
+
+int svae_adam_range(svae_ctx* c, int64_t lo, int64_t hi, float lr, int64_t step, float clip, void* stream) {
+  if (!c || !c->P || step < 1 || lo < 0 || hi > c->m.p_live || lo >= hi || (lo & 3))
+    return fail(c, SVAE_EBADARG, "bad adam range");
+  adam_range(c, lo, hi, lr, step, clip, (hipStream_t)stream);
+  HIPCHK(c, hipGetLastError());
+  return 0;
+}
+
+int svae_backward_adam(svae_ctx* c, float lr, int64_t step, float clip, void* stream) {
+  if (!c || !c->P || step < 1) return fail(c, SVAE_EBADARG, "bad adam args");
+  const bool fuse = c->side && !c->m.shared;
+  c->fa_on = fuse;
+  c->fa_lr = lr;
+  c->fa_step = step;
+  c->fa_clip = clip;
+  const int r = svae_backward(c, stream);
+  c->fa_on = false;
+  if (r) return r;
+  if (!fuse) return svae_adam(c, lr, step, clip, stream);
+  adam_range(c, 0, c->m.phi_hi, lr, step, clip, (hipStream_t)stream);  // recognition bucket, after hook(-1)
+  HIPCHK(c, hipGetLastError());
+  return 0;
+}
+
+int svae_adam_state(svae_ctx* c, int dir, float* m, float* v, int64_t n, void* stream) {
+  if (!c || !m || !v || n != c->m.p_live || (dir != 0 && dir != 1)) return fail(c, SVAE_EBADARG, "bad adam_state args");
+  const size_t b = (size_t)n * sizeof(float);
+  hipStream_t s = (hipStream_t)stream;
+  if (dir == 0) {
+    HIPCHK(c, hipMemcpyAsync(m, c->adam_m, b, hipMemcpyDeviceToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(v, c->adam_v, b, hipMemcpyDeviceToDevice, s));
+  } else {
+    HIPCHK(c, hipMemcpyAsync(c->adam_m, m, b, hipMemcpyDeviceToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->adam_v, v, b, hipMemcpyDeviceToDevice, s));
+  }
   return 0;
 }
 

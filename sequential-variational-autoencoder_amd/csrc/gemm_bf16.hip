@@ -1482,3 +1482,9 @@ void shadow_weights(const float* w, void* wn, void* wt, long long n, const void*
     hipLaunchKernelGGL(shadow_t_kernel, dim3(ntiles), dim3(256), 0, s, w, (__bf16*)wt, (const int4*)tiles,
                        (const long long*)offs);
 }
+
+void shadow_t_tiles(const float* w, void* wt, const void* tiles, int ntiles, const void* offs, hipStream_t s) {
+  if (ntiles > 0)
+    hipLaunchKernelGGL(shadow_t_kernel, dim3(ntiles), dim3(256), 0, s, w, (__bf16*)wt, (const int4*)tiles,
+                       (const long long*)offs);
+}

@@ -106,6 +106,8 @@ void wgrad_halo(const WHaloPlanOut& pl, const WgArgs& a, int groups, hipStream_t
 // bf16 weight shadows: wn = bf16(w) for [0,n); wt = per-tap transposes listed in tiles/offs
 void shadow_weights(const float* w, void* wn, void* wt, long long n, const void* tiles, int ntiles, const void* offs,
                     hipStream_t s);
+// per-tap transposed bf16 shadow of the ntiles tiles starting at `tiles` only
+void shadow_t_tiles(const float* w, void* wt, const void* tiles, int ntiles, const void* offs, hipStream_t s);
 void igemm_fwd(FwdArgs a, int groups, hipStream_t s);
 void wgrad(WgArgs a, int groups, hipStream_t s);
 void wgrad_reduce(const float* part, long long p_gs, int nsplit, int ntap, int M, int N, float* out0,
@@ -193,8 +195,9 @@ void loss_reduce(const float* rec_part, int nblk, const float* kl_img, int B, in
                  float* rec_img_out, hipStream_t s);
 
 // ---- optimizer: clip(+-c) + TF Adam (sequential_vae.py:1267-1276) ----
-void adam_step(float* w, const float* g, float* m, float* v, long long n, float lr_t, float b1, float b2, float eps,
-               float clipv, hipStream_t s);
+// clip + TF Adam on n elements; wn != nullptr: also the bf16 copy of the updated weights
+void adam_step(float* w, const float* g, float* m, float* v, void* wn, long long n, float lr_t, float b1, float b2,
+               float eps, float clipv, hipStream_t s);
 
 // ---- weight sharing (homogeneous chain): virtual per-step copies <-> public tensors ----
 // Pv[v + i] = P[p + i] for every segment {v, p, size} of seg[nseg][3]

@@ -809,22 +809,50 @@ void loss_reduce(const float* rec_part, int nblk, const float* kl_img, int B, in
 // ---------------------------------------------------------------------------
 // clip_by_value(+-clip) + tf.train.AdamOptimizer (sequential_vae.py:1267,1274-1276)
 // ---------------------------------------------------------------------------
-__global__ void adam_kernel(float* w, const float* g, float* m, float* v, long long n, float lr_t, float b1, float b2,
-                            float eps, float clipv) {
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    float gg = fminf(fmaxf(g[i], -clipv), clipv);
-    float mm = b1 * m[i] + (1.f - b1) * gg;
-    float vv = b2 * v[i] + (1.f - b2) * gg * gg;
-    m[i] = mm;
-    v[i] = vv;
-    w[i] -= lr_t * mm / (sqrtf(vv) + eps);
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void adam1(float& w, float g, float& m, float& v, float lr_t, float b1, float b2, float eps,
+                                      float clipv) {
+  const float gg = fminf(fmaxf(g, -clipv), clipv);
+  m = b1 * m + (1.f - b1) * gg;
+  v = b2 * v + (1.f - b2) * gg * gg;
+  w -= lr_t * m / (sqrtf(v) + eps);
+}
+
+// 16-B vectors (w/g/m/v 16-B aligned: ranges start on a multiple of 4 elements); wn != nullptr
+// also writes the bf16 copy of the updated weights (the GEMMs' N-layout shadow, shadow_n_kernel's
+// rounding), which saves the next forward's separate conversion pass over the live region
+__global__ void adam_kernel(float* w, const float* g, float* m, float* v, __bf16* wn, long long n, float lr_t, float b1,
+                            float b2, float eps, float clipv) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long nq = n >> 2;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += stride) {
+    const f32x4 gg = ((const f32x4*)g)[q];
+    f32x4 mm = ((f32x4*)m)[q], vv = ((f32x4*)v)[q], ww = ((f32x4*)w)[q];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float w1 = ww[e], m1 = mm[e], v1 = vv[e];
+      adam1(w1, gg[e], m1, v1, lr_t, b1, b2, eps, clipv);
+      ww[e] = w1;
+      mm[e] = m1;
+      vv[e] = v1;
+    }
+    ((f32x4*)m)[q] = mm;
+    ((f32x4*)v)[q] = vv;
+    ((f32x4*)w)[q] = ww;
+    if (wn) *(bf16x4_t*)(wn + 4 * q) = __builtin_convertvector(ww, bf16x4_t);
+  }
+  for (long long i = 4 * nq + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    adam1(w[i], g[i], m[i], v[i], lr_t, b1, b2, eps, clipv);
+    if (wn) wn[i] = (__bf16)w[i];
   }
 }
 
-void adam_step(float* w, const float* g, float* m, float* v, long long n, float lr_t, float b1, float b2, float eps,
-               float clipv, hipStream_t s) {
-  hipLaunchKernelGGL(adam_kernel, dim3(ew_blocks(n, 256, 8192)), dim3(256), 0, s, w, g, m, v, n, lr_t, b1, b2, eps,
-                     clipv);
+void adam_step(float* w, const float* g, float* m, float* v, void* wn, long long n, float lr_t, float b1, float b2,
+               float eps, float clipv, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(adam_kernel, dim3(ew_blocks((n + 3) / 4, 256, 8192)), dim3(256), 0, s, w, g, m, v, (__bf16*)wn,
+                     n, lr_t, b1, b2, eps, clipv);
 }
 
 __global__ void fill_kernel(float* p, long long n, float v) {

@@ -10,6 +10,7 @@ rank applies the identical clip+Adam update, so replicas stay bitwise equal.
 The reference has no collective at all; this is the added DP path.
 """
 import re
+from contextlib import nullcontext as _nullctx
 
 import torch
 
@@ -86,6 +87,8 @@ class OverlappedAllReduce:
         self.avg = dist.get_backend(group) == "nccl"  # ReduceOp.AVG (RCCL); gloo: SUM then scale
         self.pending = []
         self.error = None
+        self.eager = False  # svae_backward_adam: each bucket's update follows its exchange on the hook stream
+        self.done = []
         self.side = None
         self.by_t = {t: (lo, hi) for t, lo, hi in self.buckets}
         self._cb = _lib.STEP_HOOK(self._on_step)  # keep the ctypes thunk alive
@@ -101,18 +104,25 @@ class OverlappedAllReduce:
         try:
             if t >= 0:
                 lo, hi = self.by_t[t]
-                if self.side is not None:
-                    with torch.cuda.stream(self.side):
-                        self._reduce(lo, hi)
-                else:
+                with torch.cuda.stream(self.side) if self.side is not None else _nullctx():
                     self._reduce(lo, hi)
+                    if self.eager:  # the engine enqueues this bucket's Adam on the hook stream next
+                        self.pending.pop().wait()
+                        if not self.avg:
+                            self.grads[lo:hi].mul_(1.0 / self.world)
+                        self.done.append((lo, hi))
             else:
                 self._reduce(*self.phi)
                 for w in self.pending:
                     w.wait()
                 self.pending = []
                 if not self.avg:
-                    self.grads[:self.n_live].mul_(1.0 / self.world)
+                    if self.done:
+                        for lo, hi in [self.phi] + [(lo, hi) for _, lo, hi in self.buckets if (lo, hi) not in self.done]:
+                            self.grads[lo:hi].mul_(1.0 / self.world)
+                    else:
+                        self.grads[:self.n_live].mul_(1.0 / self.world)
+                self.done = []
         except BaseException as e:  # a ctypes callback cannot raise into C: re-raised by check()
             self.error = e
 

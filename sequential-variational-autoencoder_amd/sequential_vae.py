@@ -105,6 +105,30 @@ class SequentialVAE:
         self.overlap = OverlappedAllReduce(self, dist, group, force=force)
         return self.overlap
 
+    def backward_apply(self, lr=None, step=None, stream=None):
+        """backward() then apply_gradients() as one engine call (svae_backward_adam): every chain
+        step's generator/encoder bucket gets its clip + Adam update on the engine's side stream as
+        soon as the backward has finished it (after that bucket's overlapped all-reduce), the
+        recognition bucket last.  Bit for bit the parameters of the two separate calls."""
+        lr = self.learning_rate if lr is None else lr
+        step = self.iteration if step is None else step
+        if self.grad_hook is not None:  # the exchange follows the whole backward: Adam after it
+            self.backward(stream)
+            self.apply_gradients(lr, step, stream)
+            return
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        if self.overlap is not None:
+            self.overlap.eager = True
+        try:
+            with torch.cuda.stream(s):
+                _lib.check(self.L.svae_backward_adam(self.ctx, float(lr), int(step), float(self.cfg.clip_grad_value),
+                                                     _lib.stream_ptr(s)), self.ctx)
+        finally:
+            if self.overlap is not None:
+                self.overlap.eager = False
+        if self.overlap is not None:
+            self.overlap.check()
+
     def apply_gradients(self, lr=None, step=None, stream=None):
         lr = self.learning_rate if lr is None else lr
         step = self.iteration if step is None else step
@@ -171,10 +195,69 @@ class SequentialVAE:
         self.learning_rate *= self.cfg.learning_rate_decay
         reg = 1.0 - math.exp(-self.iteration / self.cfg.reg_coeff_rate)
         self.forward(input_batch, batch_target, None, reg)
-        self.backward()
-        self.apply_gradients(self.learning_rate, self.iteration)
+        self.backward_apply(self.learning_rate, self.iteration)
         final = float(self.copy_out(_lib.BUF_STEP_STATS, self.cfg.mc_steps - 1, 2)[0])
         return final / self.data_dims[0] / self.data_dims[1]
+
+    # ------------------------------------------------------------------ checkpoint / resume
+    def _adam_state(self, m=None, v=None):
+        load = m is not None
+        if not load:
+            m = torch.empty(self.n_live, dtype=torch.float32, device=self.device)
+            v = torch.empty_like(m)
+        _lib.check(self.L.svae_adam_state(self.ctx, 1 if load else 0, _lib.ptr(m), _lib.ptr(v), self.n_live,
+                                          _lib.stream_ptr(torch.cuda.current_stream(self.device))), self.ctx)
+        return m, v
+
+    def save_checkpoint(self, path):
+        """Training state under the reference's names (tf.train.Saver, abstract_network.py:124-135):
+        every variable, the Adam slots "<name>/Adam" and "<name>/Adam_1" of the tensors on the
+        executed path, "beta1_power" / "beta2_power", and iteration / learning_rate as metadata
+        (which the reference does not restore).  safetensors file."""
+        from safetensors.torch import save_file
+        m, v = self._adam_state()
+        torch.cuda.synchronize(self.device)
+        P, M, V = self.params.cpu(), m.cpu(), v.cpu()
+        out = {}
+        for p in self.table:
+            a, b = p["offset"], p["offset"] + p["size"]
+            out[p["name"]] = P[a:b].reshape(p["shape"]).clone()
+            if b <= self.n_live:
+                out[p["name"] + "/Adam"] = M[a:b].reshape(p["shape"]).clone()
+                out[p["name"] + "/Adam_1"] = V[a:b].reshape(p["shape"]).clone()
+        out["beta1_power"] = torch.tensor(0.9 ** self.iteration, dtype=torch.float32)
+        out["beta2_power"] = torch.tensor(0.999 ** self.iteration, dtype=torch.float32)
+        save_file(out, path, metadata={"iteration": str(self.iteration), "learning_rate": repr(self.learning_rate),
+                                       "config": self.name})
+
+    def load_checkpoint(self, path):
+        """Restore save_checkpoint's state (init_network's restore, abstract_network.py:139-152);
+        every variable must be present with its shape."""
+        from safetensors import safe_open
+        P = self.params.cpu()
+        M = torch.zeros(self.n_live, dtype=torch.float32)
+        V = torch.zeros(self.n_live, dtype=torch.float32)
+        with safe_open(path, framework="pt") as f:
+            meta = f.metadata() or {}
+            keys = set(f.keys())
+            for p in self.table:
+                a, b = p["offset"], p["offset"] + p["size"]
+                if p["name"] not in keys:
+                    raise KeyError("checkpoint lacks %s" % p["name"])
+                t = f.get_tensor(p["name"])
+                if tuple(t.shape) != tuple(p["shape"]):
+                    raise ValueError("%s: shape %s, expected %s" % (p["name"], tuple(t.shape), tuple(p["shape"])))
+                P[a:b] = t.reshape(-1)
+                if b <= self.n_live and p["name"] + "/Adam" in keys:
+                    M[a:b] = f.get_tensor(p["name"] + "/Adam").reshape(-1)
+                    V[a:b] = f.get_tensor(p["name"] + "/Adam_1").reshape(-1)
+        self.params.copy_(P.to(self.device))
+        self._adam_state(M.to(self.device), V.to(self.device))
+        # caller-written parameters: re-bind so the next forward rebuilds the engine's bf16 copies
+        _lib.check(self.L.svae_bind(self.ctx, _lib.ptr(self.params), _lib.ptr(self.grads)), self.ctx)
+        torch.cuda.synchronize(self.device)
+        self.iteration = int(meta.get("iteration", 0))
+        self.learning_rate = float(meta.get("learning_rate", self.learning_rate))
 
     def generate(self, z=None, stream=None):
         """Generator chain on latents z [T,B,Dz] (None: N(0,1) on device), no recognition network

@@ -1,0 +1,54 @@
+"""Checkpoint / resume (SequentialVAE.save_checkpoint / load_checkpoint).
+
+The reference saves and restores with tf.train.Saver (abstract_network.py:124-152): every
+variable under its TF name plus the Adam slots "<name>/Adam" and "<name>/Adam_1".  The same
+names go into a safetensors file here; a restored network must continue training exactly as the
+one that was saved."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import pkg_mod
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("preset,dtype", [("tiny", "bf16"), ("tiny_homog", "fp32")])
+def test_save_load_resume(tmp_path, preset, dtype):
+    cfgmod, SV = pkg_mod("config"), pkg_mod("sequential_vae").SequentialVAE
+    cfg = cfgmod.preset(preset, batch=4, dtype=dtype)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(21)
+    x = torch.rand(cfg.batch, cfg.height, cfg.width, cfg.channels, device="cuda", generator=g) * 2 - 1
+    a = SV(cfg, seed=3)
+    for _ in range(2):
+        a.train(x, x)
+    path = str(tmp_path / "ckpt.safetensors")
+    a.save_checkpoint(path)
+
+    b = SV(cfg, seed=7)
+    assert not torch.equal(a.params, b.params)
+    b.load_checkpoint(path)
+    assert b.iteration == a.iteration == 2
+    assert b.learning_rate == a.learning_rate
+    assert torch.equal(a.params, b.params)
+
+    eps = torch.randn(cfg.mc_steps, cfg.batch, cfg.latent_dim, device="cuda", generator=g)
+    for net in (a, b):
+        net.iteration += 1
+        net.forward(x, x, eps, 0.3)
+        net.backward_apply(net.learning_rate, net.iteration)
+    torch.cuda.synchronize()
+    assert torch.equal(a.params, b.params)
+    assert a.loss_value() == b.loss_value()
+
+    from safetensors.numpy import load_file
+    t = load_file(path)
+    for p in a.table:
+        assert t[p["name"]].shape == tuple(p["shape"])
+        live = p["offset"] + p["size"] <= a.n_live
+        assert (p["name"] + "/Adam" in t) == live and (p["name"] + "/Adam_1" in t) == live
+    assert float(t["beta1_power"]) == pytest.approx(0.9 ** 2)
+    assert np.isfinite(t[a.table[0]["name"]]).all()
+    a.close()
+    b.close()

@@ -65,6 +65,47 @@ def test_overlapped_allreduce_matches_single_exchange(tmp_path, preset, dtype):
     np.testing.assert_array_equal(np.load(tmp_path / "ov0.npy"), np.load(tmp_path / "ov1.npy"))
 
 
+def _fused_worker(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfgmod, SV = pkg_mod("config"), pkg_mod("sequential_vae").SequentialVAE
+    cfg = cfgmod.preset("tiny", batch=4, dtype="bf16")
+    ref, net = SV(cfg, seed=0), SV(cfg, seed=0)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(200 + rank)
+    x = torch.rand(cfg.batch, cfg.height, cfg.width, cfg.channels, device="cuda", generator=g) * 2 - 1
+    eps = torch.randn(cfg.mc_steps, cfg.batch, cfg.latent_dim, device="cuda", generator=g)
+    for it in (1, 2):  # one exchange after the backward, then Adam
+        ref.forward(x, x, eps, 0.7)
+        ref.backward()
+        gr = ref.grads[:ref.n_live]
+        dist.all_reduce(gr, op=dist.ReduceOp.SUM)
+        gr.mul_(1.0 / world)
+        ref.apply_gradients(1e-3, it)
+    net.enable_overlapped_allreduce(dist)
+    for it in (1, 2):  # per-bucket exchange + Adam inside the backward
+        net.forward(x, x, eps, 0.7)
+        net.backward_apply(1e-3, it)
+    torch.cuda.synchronize()
+    np.save(os.path.join(out_dir, "fref%d.npy" % rank), ref.params.cpu().numpy())
+    np.save(os.path.join(out_dir, "fov%d.npy" % rank), net.params.cpu().numpy())
+    ref.close()
+    net.close()
+    dist.destroy_process_group()
+
+
+def test_overlapped_allreduce_with_fused_adam(tmp_path):
+    """backward_apply under the overlapped exchange: every bucket's Adam runs after that bucket's
+    all-reduce on the hook stream; parameters equal exchange-then-Adam bit for bit on both ranks."""
+    world = 2
+    mp.spawn(_fused_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / ("fov%d.npy" % r)), np.load(tmp_path / ("fref%d.npy" % r)))
+    np.testing.assert_array_equal(np.load(tmp_path / "fov0.npy"), np.load(tmp_path / "fov1.npy"))
+
+
 def _nccl_worker(rank, port, out_dir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)

@@ -1,0 +1,79 @@
+"""Backward with the optimizer step folded in (svae_backward_adam / SequentialVAE.backward_apply).
+
+Each chain step's generator/encoder bucket gets its clip + Adam update (and, in bf16 mode, its
+bf16 weight copies) on the engine's side stream as soon as the backward has finished it; the
+recognition bucket follows the whole backward.  Adam is elementwise, so after several steps the
+parameters must equal, bit for bit, those of svae_backward + svae_adam.  In bf16 mode the next
+forward reuses the refreshed weight copies instead of rebuilding them, so equal losses on later
+steps also check that every copy was refreshed."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import pkg_mod
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(preset, dtype, fused, over, steps=3):
+    cfgmod, SV = pkg_mod("config"), pkg_mod("sequential_vae").SequentialVAE
+    cfg = cfgmod.preset(preset, batch=4, dtype=dtype, **over)
+    net = SV(cfg, seed=0)
+    p0 = net.params.clone()
+    g = torch.Generator(device="cuda")
+    g.manual_seed(11)
+    x = torch.rand(cfg.batch, cfg.height, cfg.width, cfg.channels, device="cuda", generator=g) * 2 - 1
+    losses = []
+    for it in range(1, steps + 1):
+        eps = torch.randn(cfg.mc_steps, cfg.batch, cfg.latent_dim, device="cuda", generator=g)
+        net.forward(x, x, eps, 0.5)
+        if fused:
+            net.backward_apply(1e-3, it)
+        else:
+            net.backward()
+            net.apply_gradients(1e-3, it)
+        losses.append(net.loss_value())
+    torch.cuda.synchronize()
+    changed = float((net.params - p0).abs().max())
+    p = net.params.cpu().numpy().copy()
+    net.close()
+    return p, losses, changed
+
+
+@pytest.mark.parametrize("preset,dtype,over", [
+    ("tiny", "fp32", {}),
+    ("tiny", "bf16", {}),
+    ("tiny", "bf16", {"predict_latent_code": True}),
+    ("tiny_homog", "bf16", {}),
+    ("celeba", "bf16", {}),
+])
+def test_backward_apply_equals_backward_then_adam(preset, dtype, over):
+    p0, l0, _ = _run(preset, dtype, False, over)
+    p1, l1, changed = _run(preset, dtype, True, over)
+    assert changed > 0
+    assert np.isfinite(p1).all()
+    assert l0 == l1, (l0, l1)
+    np.testing.assert_array_equal(p0, p1)
+
+
+def test_rebind_after_external_write_rebuilds_weight_copies():
+    """Parameters written by the caller after an update are announced with svae_bind; the next
+    forward then rebuilds the bf16 copies (same loss as a fresh network on those parameters)."""
+    cfgmod, SV = pkg_mod("config"), pkg_mod("sequential_vae").SequentialVAE
+    L = pkg_mod("_lib")
+    cfg = cfgmod.preset("tiny", batch=4, dtype="bf16")
+    a, b = SV(cfg, seed=0), SV(cfg, seed=5)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    x = torch.rand(cfg.batch, cfg.height, cfg.width, cfg.channels, device="cuda", generator=g) * 2 - 1
+    eps = torch.randn(cfg.mc_steps, cfg.batch, cfg.latent_dim, device="cuda", generator=g)
+    a.forward(x, x, eps, 1.0)
+    a.backward_apply(1e-3, 1)
+    a.params.copy_(b.params)
+    L.check(a.L.svae_bind(a.ctx, L.ptr(a.params), L.ptr(a.grads)), a.ctx)
+    a.forward(x, x, eps, 1.0)
+    b.forward(x, x, eps, 1.0)
+    torch.cuda.synchronize()
+    assert a.loss_value() == b.loss_value()
+    a.close()
+    b.close()
