@@ -9,7 +9,7 @@ import sys
 db = sqlite3.connect(sys.argv[1])
 top = int(sys.argv[2]) if len(sys.argv) > 2 else 28
 rows = db.execute("select name,start,end,stream_id from kernels order by start").fetchall()
-ends = [i for i, r in enumerate(rows) if r[0].startswith('adam_kernel')]
+ends = [i for i, r in enumerate(rows) if r[0].startswith('philox_normal_kernel')]  # one per step (forward start)
 step = rows[ends[-2] + 1:ends[-1] + 1]
 print("step span %.1f us, %d launches" % ((step[-1][2] - step[0][1]) / 1e3, len(step)))
 for sid in sorted({r[3] for r in step}):
