@@ -124,27 +124,81 @@ def pmc_traffic(kernel):
     return None, None
 
 
-def cpu_baseline(cfg, cfgname, target_sec=15.0, max_steps=4):
-    """PyTorch-CPU fp32 restatement of the same graph (oracle/torch_twin.py), fwd+bwd,
-    on a bounded sample: B=8 images of the CelebA geometry, whole T=8 chain."""
+def _cpu_threads():
+    """Host threads for the CPU baseline: the physical cores this process may use, capped by the
+    box's CPU share (OMP_NUM_THREADS, set to 16 on the GPU boxes)."""
+    try:
+        import psutil
+        phys = psutil.cpu_count(logical=False) or os.cpu_count() or 1
+    except ImportError:
+        phys = os.cpu_count() or 1
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else phys
+    n = min(phys, avail)
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return max(1, n), phys, avail
+
+
+def cpu_baseline(cfg, cfgname, target_sec=20.0, max_steps=3):
+    """PyTorch-CPU fp32 restatement of the same graph (oracle/torch_twin.py) at the workload's
+    own batch (B=128 for CelebA, T=8), fwd+bwd, on a bounded sample of steps."""
     from oracle import spec, torch_twin
-    threads = min(16, os.cpu_count() or 1)
+    threads, phys, avail = _cpu_threads()
     torch.set_num_threads(threads)
-    B = 8
+    B = cfg.batch
     cd = spec.make_config(cfgname, batch=B)
     _, struct, params = spec.init_params(cd, seed=0, dtype=np.float32)
     x, tgt, eps = spec.make_inputs(cd, batch=B)
     tw = torch_twin.Twin(cd, struct, params, dtype=torch.float32)
-    tw.step(x, tgt, eps, 1.0)  # warm-up
+    # warm-up (oneDNN primitive creation) on a small slice of the same batch
+    cw = spec.make_config(cfgname, batch=8)
+    torch_twin.Twin(cw, struct, params, dtype=torch.float32).step(x[:8], tgt[:8], eps[:, :8], 1.0)
     t0 = time.time()
     n = 0
-    while n < max_steps and (time.time() - t0) < target_sec:
+    while n < max_steps and (n == 0 or (time.time() - t0) < target_sec):
         tw.step(x, tgt, eps, 1.0)
         n += 1
     dt = (time.time() - t0) / n
     return dict(value=B / dt, unit="images/sec", cores=threads, kind="port",
-                sample="%d fwd+bwd steps of B=%d %s-geometry images (T=%d) with oracle/torch_twin.py fp32, "
-                       "%d threads" % (n, B, cfgname, cd["mc_steps"], threads))
+                sample="%d fwd+bwd step(s) of the full B=%d %s batch (T=%d) with oracle/torch_twin.py fp32 on "
+                       "%d threads (host: %d physical cores, %d in this process's affinity; the box's CPU share "
+                       "OMP_NUM_THREADS=%s)" % (n, B, cfgname, cd["mc_steps"], threads, phys, avail,
+                                                os.environ.get("OMP_NUM_THREADS", "unset")))
+
+
+def fp32_throughput(cfg, SV, steps=10, warmup=3):
+    """images/sec of the same training step in the fp32 parity mode (1e-4 ELBO parity)."""
+    from dataclasses import replace
+    c32 = replace(cfg, dtype="fp32")
+    net = SV(c32, seed=0)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(99)
+    lo, hi = c32.range
+    x = (torch.rand(c32.batch, c32.height, c32.width, c32.channels, device="cuda", generator=g) * (hi - lo) + lo)
+    for it in range(1, warmup + steps + 1):
+        if it == warmup + 1:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+        net.forward(x, x, None, 1.0 - math.exp(-it / c32.reg_coeff_rate))
+        net.backward_apply(c32.learning_rate, it)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    net.close()
+    return c32.batch * steps / dt, dt / steps * 1e3
+
+
+def _spawn_ranks(n):
+    """--gpus N without a torch.distributed launcher: start N ranks as child processes (nothing
+    here has touched the GPU yet) and exit with their status."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def main():
@@ -158,9 +212,14 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N>1: one all-reduce after the backward instead of per-step buckets during it")
+    ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 parity-mode throughput (fp32_value)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d (launch one rank per GPU)" % (args.gpus, world))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -264,6 +323,10 @@ def main():
                         "x".join(str(shape[k]) for k in ("n", "h", "cin", "cout"))),
                     kernel_us=round(sec * 1e6, 2),
                     step_achieved_tflops=round(flops_img * value / world / 1e12, 3))
+    fp32_value = fp32_ms = None
+    if world == 1 and args.dtype == "bf16" and not args.no_fp32:
+        net.close()
+        fp32_value, fp32_ms = fp32_throughput(cfg, SV)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, cfgname)
     if rank == 0:
@@ -286,6 +349,8 @@ def main():
                        "parallelism": "dp%d" % world,
                        "grad_allreduce": ("per-step buckets overlapped with the backward" if overlap else "one call after the backward") if world > 1 else None},
             "elbo_per_img": round(elbo, 5),
+            "fp32_value": None if fp32_value is None else round(fp32_value, 2),
+            "fp32_ms_per_step": None if fp32_ms is None else round(fp32_ms, 3),
             "flops_per_img": flops_img,
             "roofline": roof,
             "cpu_baseline": cpu,

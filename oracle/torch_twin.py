@@ -200,7 +200,7 @@ class Twin:
             kls.append(kl.detach())
             xhats.append(xh.detach().permute(0, 2, 3, 1))
             prev = xh
-        out = dict(loss=float(loss), final_loss=float(recs[-1]), recon=[float(r) for r in recs],
+        out = dict(loss=float(loss.detach()), final_loss=float(recs[-1]), recon=[float(r) for r in recs],
                    kl=[float(k) for k in kls], xhat=[h.numpy() for h in xhats])
         if backward:
             for p in self.P.values():

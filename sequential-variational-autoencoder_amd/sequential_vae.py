@@ -184,17 +184,32 @@ class SequentialVAE:
         return unflatten(self.grads.cpu().numpy(), self.table)
 
     def param(self, name):
+        """Read-only copy of one variable (write through set_param, or write ``params`` and call
+        params_updated(): in bf16 mode the engine keeps bf16 copies of the weights that an
+        unannounced write would leave stale)."""
         p = self._by_name[name]
-        return self.params[p["offset"]:p["offset"] + p["size"]].view(p["shape"])
+        return self.params[p["offset"]:p["offset"] + p["size"]].view(p["shape"]).clone()
+
+    def set_param(self, name, value):
+        p = self._by_name[name]
+        self.params[p["offset"]:p["offset"] + p["size"]] = self._dev(value).reshape(-1)
+        self.params_updated()
+
+    def params_updated(self):
+        """Announce a direct write to ``params`` (copy_, dist.broadcast, a checkpoint load): the
+        next forward rebuilds the engine's bf16 weight copies from the fp32 master.  Gradients
+        are zeroed as by svae_bind."""
+        _lib.check(self.L.svae_bind(self.ctx, _lib.ptr(self.params), _lib.ptr(self.grads)), self.ctx)
 
     # ------------------------------------------------------------------ reference API
-    def train(self, input_batch, batch_target):
+    def train(self, input_batch, batch_target, eps=None):
         """One training update; returns the final-step reconstruction loss per pixel
-        (sequential_vae.py:1341-1375)."""
+        (sequential_vae.py:1341-1375).  ``eps`` [T,B,Dz] (an extension for parity tests) replaces
+        the on-device N(0,1) draw of tf.random_normal (:1022)."""
         self.iteration += 1
         self.learning_rate *= self.cfg.learning_rate_decay
         reg = 1.0 - math.exp(-self.iteration / self.cfg.reg_coeff_rate)
-        self.forward(input_batch, batch_target, None, reg)
+        self.forward(input_batch, batch_target, eps, reg)
         self.backward_apply(self.learning_rate, self.iteration)
         final = float(self.copy_out(_lib.BUF_STEP_STATS, self.cfg.mc_steps - 1, 2)[0])
         return final / self.data_dims[0] / self.data_dims[1]
@@ -225,8 +240,10 @@ class SequentialVAE:
             if b <= self.n_live:
                 out[p["name"] + "/Adam"] = M[a:b].reshape(p["shape"]).clone()
                 out[p["name"] + "/Adam_1"] = V[a:b].reshape(p["shape"]).clone()
-        out["beta1_power"] = torch.tensor(0.9 ** self.iteration, dtype=torch.float32)
-        out["beta2_power"] = torch.tensor(0.999 ** self.iteration, dtype=torch.float32)
+        # TF's AdamOptimizer starts beta{1,2}_power at beta{1,2} and multiplies after every update,
+        # so after N updates it holds beta^(N+1) (tf.train.AdamOptimizer._create_slots / _finish)
+        out["beta1_power"] = torch.tensor(0.9 ** (self.iteration + 1), dtype=torch.float32)
+        out["beta2_power"] = torch.tensor(0.999 ** (self.iteration + 1), dtype=torch.float32)
         save_file(out, path, metadata={"iteration": str(self.iteration), "learning_rate": repr(self.learning_rate),
                                        "config": self.name})
 
@@ -253,10 +270,16 @@ class SequentialVAE:
                     V[a:b] = f.get_tensor(p["name"] + "/Adam_1").reshape(-1)
         self.params.copy_(P.to(self.device))
         self._adam_state(M.to(self.device), V.to(self.device))
-        # caller-written parameters: re-bind so the next forward rebuilds the engine's bf16 copies
-        _lib.check(self.L.svae_bind(self.ctx, _lib.ptr(self.params), _lib.ptr(self.grads)), self.ctx)
+        self.params_updated()  # caller-written parameters: rebuild the engine's bf16 copies
         torch.cuda.synchronize(self.device)
-        self.iteration = int(meta.get("iteration", 0))
+        if "iteration" in meta:
+            self.iteration = int(meta["iteration"])
+        elif "beta1_power" in keys:  # a TF-converted checkpoint: recover the Adam step from beta1^(N+1)
+            with safe_open(path, framework="pt") as f:
+                b1p = float(f.get_tensor("beta1_power"))
+            self.iteration = max(0, int(round(math.log(b1p) / math.log(0.9))) - 1)
+        else:
+            self.iteration = 0
         self.learning_rate = float(meta.get("learning_rate", self.learning_rate))
 
     def generate(self, z=None, stream=None):

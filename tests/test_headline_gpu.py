@@ -1,0 +1,85 @@
+"""Parity at the headline configuration itself (BASELINE.json configs[1]: CelebA 64x64, B=128,
+T=8), in both precision modes, on the same inputs and the same injected eps.
+
+* fp32 engine: loss within 1e-4 of the float64 restatement (north_star), and the first two
+  decoder outputs x_hat_0, x_hat_1 within 1e-4 (relative L2) before the chain's amplification
+  sets in (tests/test_chaos.py: ~3-4x per step at this geometry).
+* bf16 engine (the mode bench.py measures): loss within the documented bf16 bound of the fp32
+  engine (2e-2) and within 3x (+ floor) of the error of the bf16-emulating CPU
+  restatement (oracle/torch_twin.py emulate_bf16, the same operands rounded); gradients against
+  the fp32 engine's.
+Every measured error is printed (pytest -s / the GPU log)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import pkg_mod
+from oracle import spec, torch_twin
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return float(np.linalg.norm(np.ravel(a) - np.ravel(b)) / max(np.linalg.norm(np.ravel(b)), 1e-30))
+
+
+def _engine(dtype):
+    cfg = pkg_mod("config").preset("celeba", dtype=dtype)
+    return pkg_mod("sequential_vae").SequentialVAE(cfg, seed=0), cfg
+
+
+def test_headline_config_both_precisions():
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    cd = spec.make_config("celeba")            # B=128, T=8
+    x, tgt, eps = spec.make_inputs(cd)
+    res = {}
+    for dt in ("fp32", "bf16"):
+        net, cfg = _engine(dt)
+        net.forward(x, tgt, eps, 1.0)
+        net.backward()
+        torch.cuda.synchronize()
+        res[dt] = dict(loss=net.loss_value(reg_coeff=1.0), elbo=net.elbo_per_image().cpu().numpy(),
+                       xhat=[net.xhat(t).cpu().numpy() for t in range(cfg.mc_steps)],
+                       grads=net.grads[:net.n_live].cpu().numpy().astype(np.float64), params=net.param_dict())
+        net.close()
+    params = res["fp32"]["params"]
+    _, struct = spec.build_params(cd)
+    with torch.no_grad():
+        o64 = torch_twin.Twin(cd, struct, params, dtype=torch.float64, requires_grad=False).step(
+            x, tgt, eps, 1.0, backward=False)
+        emul = torch_twin.Twin(cd, struct, params, dtype=torch.float32, requires_grad=False,
+                               emulate_bf16=True).step(x, tgt, eps, 1.0, backward=False)
+    L64 = o64["loss"]
+    e32 = abs(res["fp32"]["loss"] - L64) / abs(L64)
+    e16 = abs(res["bf16"]["loss"] - L64) / abs(L64)
+    eem = abs(emul["loss"] - L64) / abs(L64)
+    e16_32 = abs(res["bf16"]["loss"] - res["fp32"]["loss"]) / abs(res["fp32"]["loss"])
+    x32 = [_rel(res["fp32"]["xhat"][t], o64["xhat"][t]) for t in range(8)]
+    x16 = [_rel(res["bf16"]["xhat"][t], o64["xhat"][t]) for t in range(8)]
+    xem = [_rel(emul["xhat"][t], o64["xhat"][t]) for t in range(8)]
+    g32, g16 = res["fp32"]["grads"], res["bf16"]["grads"]
+    gvec = _rel(g16, g32)
+    table = pkg_mod("weights").param_table(pkg_mod("config").preset("celeba"))[0]
+    per = [_rel(g16[p["offset"]:p["offset"] + p["size"]], g32[p["offset"]:p["offset"] + p["size"]])
+           for p in table if p["offset"] + p["size"] <= len(g32)
+           and np.linalg.norm(g32[p["offset"]:p["offset"] + p["size"]]) > 1e-7]
+    print("\nheadline CelebA B=128 T=8: loss float64 %.6f  fp32 %.6f (rel %.2e)  bf16 %.6f (rel %.2e vs f64, "
+          "%.2e vs fp32)  bf16-emulating twin %.6f (rel %.2e)" % (
+              L64, res["fp32"]["loss"], e32, res["bf16"]["loss"], e16, e16_32, emul["loss"], eem))
+    print("x_hat_t rel L2 vs float64: fp32 %s" % ["%.1e" % e for e in x32])
+    print("                           bf16 %s" % ["%.1e" % e for e in x16])
+    print("                 bf16-emul twin %s" % ["%.1e" % e for e in xem])
+    print("gradients bf16 vs fp32 engine: vector %.3e, per-tensor median %.3e, p90 %.3e" % (
+        gvec, float(np.median(per)), float(np.percentile(per, 90))))
+    print("per-image ELBO bf16 vs fp32: max rel %.2e" % float(
+        np.max(np.abs(res["bf16"]["elbo"] - res["fp32"]["elbo"]) / np.abs(res["fp32"]["elbo"]))))
+    # fp32: north_star 1e-4 on the ELBO and on the decoder output before amplification
+    assert e32 <= 1e-4
+    assert x32[0] <= 1e-4 and x32[1] <= 1e-4
+    assert np.abs(res["fp32"]["xhat"][0] - o64["xhat"][0]).max() <= 1e-3
+    # bf16: the documented bound, and consistent with the emulated rounding
+    assert e16_32 <= 2e-2
+    assert e16 <= max(2e-3, 3 * eem)
+    for t in range(8):
+        assert x16[t] <= max(2e-3, 3 * xem[t]), (t, x16[t], xem[t])
+    assert gvec <= 0.25

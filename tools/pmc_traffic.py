@@ -5,8 +5,10 @@
     python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json> [label]
 
 FETCH_SIZE / WRITE_SIZE are KiB per dispatch.  MI355X_MICROARCH.md (HBM section): on
-gfx950 FETCH_SIZE reports 1/2 of the bytes of wide coalesced streaming reads, so it is
-doubled here; WRITE_SIZE is taken as is.  The two counters cannot share a pass (TCC slots),
+gfx950 FETCH_SIZE reports 1/2 of the bytes of WIDE (16 B/lane) coalesced streaming reads, so it
+is doubled only for kernels whose HBM operand loads are 16 B/lane (WIDE16 below, from the
+kernel sources); other access widths are uncalibrated and are reported as counted ("x1,
+uncalibrated").  WRITE_SIZE is taken as is.  Each kernel's entry records the rule applied.  The two counters cannot share a pass (TCC slots),
 hence two runs of the same command; per-kernel averages are matched by kernel name.
 """
 import csv
@@ -30,6 +32,20 @@ def _short(name):
         elif ch == "(" and depth == 0:
             return name[:i]
     return name
+
+
+# kernels whose operand loads from HBM are 16 B per lane (f32x4 / bf16x8 / int4 vectors)
+WIDE16 = ("wgrad_halo_kernel", "igemm_halo_kernel", "igemm_bf16_kernel", "wgrad_bf16_kernel", "igemm_fwd_kernel",
+          "wgrad_kernel", "wgrad_reduce_kernel<", "splitk_reduce_kernel", "bn_apply_kernel", "bn_bwd_reduce_kernel",
+          "bn_bwd_apply_kernel", "adam_kernel", "shadow_n_kernel", "shadow_t_kernel", "loss_reduce_kernel")
+
+
+def fetch_rule(kernel):
+    k = kernel.split("(")[0]
+    for w in WIDE16:
+        if k.startswith(w) or (w.endswith("<") and k.startswith(w[:-1])):
+            return 2.0, "FETCH_SIZE x2 (16 B/lane loads: gfx950 half-count)"
+    return 1.0, "FETCH_SIZE x1 (loads narrower than 16 B/lane: uncalibrated, as counted)"
 
 
 def _load(d, counter):
@@ -56,13 +72,15 @@ def main():
     for k in sorted(set(fe) & set(wr)):
         nf, kf = fe[k]
         nw, kw = wr[k]
-        fetch = 2.0 * kf * 1024.0 / nf   # gfx950: FETCH_SIZE counts half the streamed bytes
+        mult, rule = fetch_rule(k)
+        fetch = mult * kf * 1024.0 / nf
         write = kw * 1024.0 / nw
-        kernels[k] = dict(dispatches_fetch_pass=nf, dispatches_write_pass=nw,
+        kernels[k] = dict(dispatches_fetch_pass=nf, dispatches_write_pass=nw, fetch_rule=rule,
                           fetch_bytes_per_launch=round(fetch), write_bytes_per_launch=round(write),
                           hbm_bytes_per_launch=round(fetch + write))
     doc = dict(label=label, source="rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), csv",
-               correction="FETCH_SIZE x2 (gfx950 half-count of wide coalesced reads), KiB->bytes x1024",
+               correction="per kernel (fetch_rule): FETCH_SIZE x2 only for 16 B/lane loads (gfx950 half-count), "
+                          "x1 otherwise (uncalibrated); KiB->bytes x1024",
                kernels=kernels)
     with open(out, "w") as fh:
         json.dump(doc, fh, indent=1, sort_keys=True)
