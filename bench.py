@@ -25,9 +25,10 @@ PKG = "sequential-variational-autoencoder_amd"
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no 2:1 sparsity)
-# dominant kernel of the bf16 step (profiles/r01_*_bf16_kernel_stats.txt: largest total time):
-# the halo weight-GEMM, stride-1 instance (side stream, overlapped with the BN chain; profiles/r01_v13)
-DOMINANT_KID = "KID_WHALO_32_S1"
+# dominant kernel of the bf16 step (profiles/r0*_bf16_kernel_stats.txt: largest total time): the
+# stride-1 halo weight-GEMM (side stream, overlapped with the BN chain), since round 2 the
+# compile-time-geometry wgrad_halo2_kernel (its instances together; csrc/wgrad_halo2.hip)
+DOMINANT_KID = "KID_WHALO2_S1"
 
 
 # metric / workload per preset (BASELINE.json configs[1] is the headline: CelebA B=128)
@@ -108,19 +109,25 @@ def time_dominant_kernel(L, shape, iters=50):
 
 
 def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC summary (tools/pmc_traffic.py:
-    separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes, FETCH doubled per the gfx950 note in
-    MI355X_MICROARCH.md), or None when no summary for this kernel is committed."""
+    """HBM bytes per launch of `kernel` (a family: every template instance whose name starts with
+    the kernel's base name, weighted by dispatch count) from the newest committed PMC summary
+    (tools/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of the bench command,
+    the gfx950 FETCH correction per kernel as recorded there), or (None, None)."""
     import glob
+    base = kernel.split("<")[0].split(" ")[0]
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        k = d.get("kernels", {}).get(kernel)
-        if k and k.get("hbm_bytes_per_launch"):
-            return float(k["hbm_bytes_per_launch"]), os.path.relpath(path, ROOT)
+        tot = n = 0
+        for k, v in d.get("kernels", {}).items():
+            if k.split("<")[0] == base and v.get("hbm_bytes_per_launch"):
+                tot += v["hbm_bytes_per_launch"] * v["dispatches_fetch_pass"]
+                n += v["dispatches_fetch_pass"]
+        if n:
+            return float(tot) / n, os.path.relpath(path, ROOT)
     return None, None
 
 

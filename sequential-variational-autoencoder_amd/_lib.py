@@ -117,6 +117,7 @@ KID_HALO_128x128 = 20
 KID_HALO_64x128 = 21
 KID_WHALO_32_S1 = 22
 KID_WHALO_32_S2 = 23
+KID_WHALO2_S1 = 26   # wgrad_halo2_kernel<...>: every instance of the stride-1 halo weight-GEMM
 
 
 def check(rc, ctx=None):

