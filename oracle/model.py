@@ -2,9 +2,12 @@
 
 Mirrors, function for function, the reference graph built by
 ``SequentialVAE.construct_network`` (sequential_vae.py:877-984) for the
-configurations in BASELINE.json (inhomogeneous chain, concat noise, no chain
-noise, no predicted generator noise, intermediate reconstruction).  ε is
-injected ([T,B,Dz]) instead of drawn by ``tf.random_normal`` (:1023).
+configurations in BASELINE.json (inhomogeneous chain, concat noise, intermediate
+reconstruction) and the chain variants of SURVEY §8(f3): Latent InfoMax, chain noise
+with fixed or predicted stddevs (:1088-1091, :1147-1150, :1848-1875), the uniform
+prior (:1159-1160) and the improvement-maximisation loss (:1182-1201).  ε is
+injected ([T,B,Dz]) instead of drawn by ``tf.random_normal`` (:1023), and so is
+the chain noise ([T,B,H,W,C], ``tf.random_normal(image_batch_shape)`` :1090).
 """
 import numpy as np
 
@@ -127,6 +130,8 @@ def generator_ladder(tp, P, cfg, st, xprev, z, enc_st, rec=None):
     lo, hi = cfg["range"]
     o = T.conv2d_transpose(tp, cur, P[st["out"]["w"]], 2)
     o = T.sigmoid(tp, T.bias_add(tp, o, P[st["out"]["b"]]))
+    if rec is not None:
+        rec["conv_output"] = o  # input of stddevs_prediction (:1734)
     output = T.affine(tp, o, hi - lo, lo)
     if encodings is not None:
         r = T.conv2d_transpose(tp, cur, P[st["ratio"]["w"]], 2)
@@ -138,10 +143,23 @@ def generator_ladder(tp, P, cfg, st, xprev, z, enc_st, rec=None):
     return output
 
 
-def forward_backward(cfg, struct, params, x, target, eps, reg_coeff=1.0, want_grads=True):
+def stddevs_prediction(tp, P, cfg, sst, o):
+    """sequential_vae.py:1866-1875: conv2d_bn_lrelu (4x4, stride 1) per filter size, a 1x1
+    conv2d with sigmoid, times predict_generator_stddev_max -> [B,H,W,1]."""
+    cur = o
+    for lay in sst["convs"]:
+        cur = _conv_bn_act(tp, P, cur, lay, 1, "lrelu")
+    s = T.conv2d(tp, cur, P[sst["out"]["w"]], 1)
+    s = T.sigmoid(tp, T.bias_add(tp, s, P[sst["out"]["b"]]))
+    return T.affine(tp, s, cfg["predict_generator_stddev_max"], 0.0)
+
+
+def forward_backward(cfg, struct, params, x, target, eps, reg_coeff=1.0, want_grads=True, noise=None):
     """One training iteration's fwd (+bwd) — the value of ``self.loss``,
     ``self.final_loss`` and d loss / d every trainable variable
-    (sequential_vae.py:1273 ``compute_gradients``, before clipping)."""
+    (sequential_vae.py:1273 ``compute_gradients``, before clipping).  With the chain noise on,
+    ``noise`` [T,B,H,W,C] is the N(0,1) draw of :1090 per step.  With the improvement-maximisation
+    loss on, ``imp_loss`` and ``imp_grads`` (its gradient, :1302-1303) are returned as well."""
     tp = T.Tape()
     P = {k: tp.leaf(v) for k, v in params.items()}
     xin = tp.leaf(np.asarray(x, np.float64))
@@ -150,7 +168,11 @@ def forward_backward(cfg, struct, params, x, target, eps, reg_coeff=1.0, want_gr
     terms, coeffs = [], []
     out = dict(recon=[], kl=[], recon_img=[], kl_img=[], xhat=[], mu=[], sig=[], z=[])
     znodes, xnodes, recs = [], [], []
-    prev = None
+    out.update(sample=[], sd=[])
+    noisy = cfg.get("add_noise_to_chain", False)
+    pgn = cfg.get("predict_generator_noise", False)
+    imp_terms = []
+    prev, prev_mle = None, None   # training_samples[t-1], training_mles[t-1]
     for t in range(Tn):
         st = struct[t]
         # recognition input: x, or x_{t-1} in Latent InfoMax mode (sequential_vae.py:1013-1016)
@@ -161,8 +183,26 @@ def forward_backward(cfg, struct, params, x, target, eps, reg_coeff=1.0, want_gr
         recd = {}
         xhat = generator_ladder(tp, P, cfg, st["generator"], prev, z, st.get("encoder"), recd)
         recs.append(recd)
-        rec = T.mean_sq_err_per_row(tp, xhat, target)              # :1146
-        kl = T.kl_per_row(tp, mu, sig, cfg["latent_prior_stddev"])  # :1156-1158
+        sd = None
+        sample = xhat
+        if noisy:  # training_sample = mle + reg * stddevs * N(0,1)  (:1088-1090)
+            nt = np.asarray(noise[t], np.float64)
+            if pgn:
+                sd = stddevs_prediction(tp, P, cfg, st["generator"]["stddev"], recd["conv_output"])
+                sample = T.add_scaled_noise(tp, xhat, sd, nt, reg_coeff)
+            else:
+                sample = T.add_scaled_noise(tp, xhat, cfg["noise_stddevs"][t], nt, reg_coeff)
+        if pgn:
+            rec = T.nll_per_row(tp, xhat, target, sd)              # :1149-1150
+        else:
+            rec = T.mean_sq_err_per_row(tp, xhat, target)          # :1146
+        if cfg.get("use_uniform_prior", False):
+            kl = T.kl_uniform_per_row(tp, sig)                     # :1159-1160
+        else:
+            kl = T.kl_per_row(tp, mu, sig, cfg["latent_prior_stddev"])  # :1156-1158
+        if cfg.get("add_improvement_maximization_loss", False) and prev_mle is not None:
+            # reg * latent_pred_loss_coeff * -reduce_mean(||x_t - x_{t-1}||^2)  (:1189-1199)
+            imp_terms.append(T.mean_all(tp, T.sq_norm_diff_per_row(tp, xhat, prev_mle)))
         rec_m, kl_m = T.mean_all(tp, rec), T.mean_all(tp, kl)      # :1163-1164
         c_first = cfg["first_step_loss_coeff"] if t == 0 else 1.0  # :1175-1176 (applies to step-0 terms)
         if cfg["intermediate_reconstruction"] or t == Tn - 1:       # :1167-1168
@@ -178,9 +218,11 @@ def forward_backward(cfg, struct, params, x, target, eps, reg_coeff=1.0, want_gr
         out["mu"].append(mu.v.copy())
         out["sig"].append(sig.v.copy())
         out["z"].append(z.v.copy())
+        out["sample"].append(sample.v.copy())
+        out["sd"].append(None if sd is None else sd.v.copy())
         znodes.append(z)
         xnodes.append(xhat)
-        prev = xhat
+        prev, prev_mle = sample, xhat
     loss = T.scalar_sum(tp, terms, coeffs)
     out["loss"] = float(loss.v)
     out["final_loss"] = out["recon"][-1]                            # :1204
@@ -198,6 +240,14 @@ def forward_backward(cfg, struct, params, x, target, eps, reg_coeff=1.0, want_gr
         out["dz"] = [n.g.copy() for n in znodes]          # d loss / d z_t
         out["dxhat"] = [n.g.copy() for n in xnodes]       # d loss / d x_hat_t (total)
         out["dec_grads"] = [{k: (n.g.copy() if n.g is not None else None) for k, n in r.items()} for r in recs]
+    if imp_terms:
+        c = -reg_coeff * cfg["latent_pred_loss_coeff"]
+        imp = T.scalar_sum(tp, imp_terms, [c] * len(imp_terms))
+        out["imp_loss"] = float(imp.v)
+        if want_grads:
+            T.zero_grads(tp)
+            tp.backward(imp)
+            out["imp_grads"] = {k: (n.g if n.g is not None else np.zeros_like(n.v)) for k, n in P.items()}
     return out
 
 

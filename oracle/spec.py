@@ -35,7 +35,17 @@ PRESETS = {
 DEFAULTS = dict(intermediate_reconstruction=True, first_step_loss_coeff=1.0,
                 latent_prior_stddev=1.0, latent_mean_clip=float("inf"),
                 min_highway=0.0, max_highway=1.0, predict_latent_code=False,
-                predict_latent_code_with_regularization=False, regularized_steps=None)
+                predict_latent_code_with_regularization=False, regularized_steps=None,
+                # chain-noise variants (sequential_vae.py:232-240): noise added to the sample fed to
+                # the next step, fixed per-step stddevs or predicted by a per-step conv network
+                use_uniform_prior=False, add_noise_to_chain=False, noise_stddevs=None,
+                predict_generator_noise=False, predict_generator_stddev_max=1.0,
+                stddev_filter_sizes=(5, 5, 5, 5, 5),
+                # improvement maximisation (:227, :253, :1182-1201, own optimiser :1299-1316)
+                add_improvement_maximization_loss=False, latent_pred_loss_coeff=0.001)
+
+# sequential_vae.py:239 (exactly mc_steps long; the last entry 0 so the chain ends on its MLE)
+DEFAULT_NOISE_STDDEVS = [0.5 ** 1, 0.5 ** 2, 0.5 ** 3, 0.5 ** 4, 0.5 ** 5, 0.5 ** 6, 0.5 ** 7, 0.0]
 
 
 def kl_on(cfg, t):
@@ -56,6 +66,13 @@ def make_config(preset="celeba", **over):
     L = cfg["levels"]
     cfg["image_sizes"] = [cfg["H"] // (2 ** i) for i in range(L + 1)]
     cfg["latent_dim"] = int(sum(cfg["latent_dims"]))
+    if cfg["add_noise_to_chain"] and not cfg["predict_generator_noise"] and cfg["noise_stddevs"] is None:
+        nd = DEFAULT_NOISE_STDDEVS
+        assert cfg["mc_steps"] <= len(nd), "noise_stddevs must be given for mc_steps > 8"
+        cfg["noise_stddevs"] = list(nd[:cfg["mc_steps"]])  # the reference indexes noise_stddevs[step]
+    if cfg["predict_generator_noise"]:
+        # stddevs = 0 without the chain noise (:1664-1671), and the NLL then takes log(0)
+        assert cfg["add_noise_to_chain"], "predict_generator_noise needs add_noise_to_chain"
     assert len(cfg["filter_sizes"]) == L + 2 and len(cfg["latent_dims"]) == L
     return cfg
 
@@ -162,6 +179,16 @@ def build_params(cfg):
         out = sc.convt_plain((4, 4, C, F[1]))
         ratio = sc.convt_plain((4, 4, 1, F[1])) if t >= 1 else None
         st["generator"] = dict(split=split, top=top, levels=dec, out=out, ratio=ratio)
+        if cfg.get("add_noise_to_chain") and cfg.get("predict_generator_noise"):
+            # stddevs_prediction (:1866-1875), created after the output / ratio conv-T: conv2d_bn_lrelu
+            # 4x4 s1 per entry of predict_generator_stddev_filter_sizes, then a 1x1 conv2d (default
+            # xavier init, bias) with sigmoid
+            convs, cin = [], C
+            for f in cfg["stddev_filter_sizes"]:
+                convs.append(sc.conv_bn((4, 4, cin, f)))
+                cin = f
+            w, b = sc.add("Conv", [("weights", (1, 1, cin, 1), "glorot", False), ("biases", (1,), "zeros", False)])
+            st["generator"]["stddev"] = dict(convs=convs, out=dict(w=w, b=b))
         struct.append(st)
     return table, struct
 
@@ -183,6 +210,14 @@ def make_inputs(cfg, batch=None, seed_x=0, seed_eps=1):
     re = np.random.default_rng(seed_eps)
     eps = re.standard_normal(size=(cfg["mc_steps"], B, cfg["latent_dim"])).astype(np.float32)
     return x, x.copy(), eps
+
+
+def make_chain_noise(cfg, batch=None, seed=2):
+    """N(0,1) chain noise [T,B,H,W,C] of training_sample = mle + reg*stddevs*noise
+    (sequential_vae.py:1090), PCG64 seed 2 (injected like eps)."""
+    B = batch or cfg["batch"]
+    r = np.random.default_rng(seed)
+    return r.standard_normal(size=(cfg["mc_steps"], B, cfg["H"], cfg["W"], cfg["C"])).astype(np.float32)
 
 
 # ---- homogeneous chains: TF variable sharing (sequential_vae.py:107-113) ----

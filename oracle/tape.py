@@ -252,3 +252,58 @@ def kl_per_row(tp, mu, sig, prior=1.0):
 def mean_all(tp, x):
     n = x.v.size
     return tp.op(np.asarray(x.v.mean()), (x,), lambda g: (np.full(x.v.shape, g / n),))
+
+
+# ---- chain-noise / predicted-noise / uniform-prior / improvement-maximisation variants ----
+def zero_grads(tp):
+    """Reset every node's gradient (a second backward on the same tape: the improvement-
+    maximisation loss has its own compute_gradients, sequential_vae.py:1302-1303)."""
+    for n in tp.nodes:
+        n.g = None
+
+
+def add_scaled_noise(tp, mle, sd, noise, scale):
+    """training_sample = mle + reg * stddevs * N(0,1) (sequential_vae.py:1090): ``sd`` a node
+    [B,H,W,1] broadcast over channels (predicted noise) or a python float (fixed noise_stddevs)."""
+    if isinstance(sd, Node):
+        y = mle.v + scale * sd.v * noise
+        return tp.op(y, (mle, sd), lambda g: (g, scale * (g * noise).sum(axis=-1, keepdims=True)))
+    return tp.op(mle.v + scale * float(sd) * noise, (mle,), lambda g: (g,))
+
+
+def nll_per_row(tp, a, target, sd):
+    """Per-image mean over H,W,C of log sd + 0.5 log 2pi + 0.5 ((a - target)/sd)^2
+    (sequential_vae.py:1149-1150; its batch mean is the reference's reduce_mean over all axes).
+    sd [B,H,W,1] broadcasts over the channels."""
+    d = a.v - target
+    s = sd.v
+    m = d[0].size
+    e = np.log(s) + 0.5 * np.log(2.0 * np.pi) + 0.5 * (d / s) ** 2
+    y = e.reshape(e.shape[0], -1).mean(axis=1)
+
+    def bw(g):
+        gb = g.reshape((-1,) + (1,) * (d.ndim - 1)) / m
+        da = gb * d / s ** 2
+        ds = (gb * (1.0 / s - d ** 2 / s ** 3)).sum(axis=-1, keepdims=True)
+        return da, ds
+
+    return tp.op(y, (a, sd), bw)
+
+
+def kl_uniform_per_row(tp, sig):
+    """use_uniform_prior: reduce_mean(-log sigma, 1) (sequential_vae.py:1159-1160)."""
+    D = sig.v.shape[1]
+    y = (-np.log(sig.v)).mean(axis=1)
+    return tp.op(y, (sig,), lambda g: (g[:, None] * (-1.0 / sig.v) / D,))
+
+
+def sq_norm_diff_per_row(tp, a, b):
+    """reduce_sum((a - b)^2, [1,2,3]) (sequential_vae.py:1190-1191)."""
+    d = a.v - b.v
+    y = (d ** 2).reshape(d.shape[0], -1).sum(axis=1)
+
+    def bw(g):
+        gd = 2.0 * d * g.reshape((-1,) + (1,) * (d.ndim - 1))
+        return gd, -gd
+
+    return tp.op(y, (a, b), bw)

@@ -6,6 +6,8 @@ flatten order for every FC input.  Used (a) to cross-check oracle/model.py and
 (b) as the CPU throughput baseline in bench.py (``cpu_baseline.kind = "port"``):
 the reference's own TF-CPU path cannot run here (no TensorFlow).
 """
+import math
+
 import torch
 import torch.nn.functional as Fn
 from . import spec as _spec
@@ -169,6 +171,7 @@ class Twin:
         # output / ratio conv-T: bf16 forward (halo gather, N = C+1), fp32 input gradient (small-C
         # gather over the 4-channel packed gradient), bf16 weight gradient
         o = torch.sigmoid(self._op(oc, cur, P[st["out"]["w"]], rd=False) + P[st["out"]["b"]].view(1, -1, 1, 1))
+        self._conv_output = o  # stddevs_prediction input (sequential_vae.py:1734)
         out = (hi - lo) * o + lo
         if encs is not None:
             r = torch.sigmoid(self._op(oc, cur, P[st["ratio"]["w"]], rd=False) +
@@ -177,21 +180,47 @@ class Twin:
             out = r * out + (1 - r) * encs[0]
         return out
 
-    def step(self, x_nhwc, target_nhwc, eps, reg_coeff=1.0, backward=True):
+    def stddevs(self, sst, o):
+        """stddevs_prediction (sequential_vae.py:1866-1875): fp32 (no bf16 legs in the engine)."""
+        cur = o
+        for lay in sst["convs"]:
+            P = self.P
+            y = conv2d_same(cur, P[lay["w"]], 1) + P[lay["b"]].view(1, -1, 1, 1)
+            cur = lrelu(bn_train(y, P[lay["beta"]]))
+        s = torch.sigmoid(conv2d_same(cur, self.P[sst["out"]["w"]], 1) + self.P[sst["out"]["b"]].view(1, -1, 1, 1))
+        return self.cfg["predict_generator_stddev_max"] * s
+
+    def step(self, x_nhwc, target_nhwc, eps, reg_coeff=1.0, backward=True, noise=None):
         cfg = self.cfg
         x = torch.as_tensor(x_nhwc, dtype=self.dtype).permute(0, 3, 1, 2)
         tgt = torch.as_tensor(target_nhwc, dtype=self.dtype).permute(0, 3, 1, 2)
         eps = torch.as_tensor(eps, dtype=self.dtype)
         Tn, p2 = cfg["mc_steps"], cfg["latent_prior_stddev"] ** 2
         loss, prev, recs, kls, xhats = 0.0, None, [], [], []
+        noisy, pgn = cfg.get("add_noise_to_chain", False), cfg.get("predict_generator_noise", False)
+        imp, prev_mle = 0.0, None
         for t in range(Tn):
             st = self.struct[t]
             rin = prev if (cfg.get("predict_latent_code", False) and t >= 1) else x  # :1013-1016
             mu, sig = self.inference(st["inference"], rin)
             z = mu + sig * eps[t]
             xh = self.generator(st["generator"], prev, z, st.get("encoder"))
-            rec = ((xh - tgt) ** 2).mean()
-            kl = (-0.5 - torch.log(sig) + 0.5 * sig ** 2 / p2 + 0.5 * mu ** 2 / p2).mean(1).mean()
+            sample = xh
+            if noisy:  # :1088-1090
+                nt = torch.as_tensor(noise[t], dtype=self.dtype).permute(0, 3, 1, 2)
+                sd = self.stddevs(st["generator"]["stddev"], self._conv_output) if pgn else cfg["noise_stddevs"][t]
+                sample = xh + reg_coeff * sd * nt
+            if pgn:  # :1149-1150
+                rec = (torch.log(sd) + 0.5 * math.log(2 * math.pi) + 0.5 * ((xh - tgt) / sd) ** 2).mean()
+            else:
+                rec = ((xh - tgt) ** 2).mean()
+            if cfg.get("use_uniform_prior", False):  # :1159-1160
+                kl = (-torch.log(sig)).mean(1).mean()
+            else:
+                kl = (-0.5 - torch.log(sig) + 0.5 * sig ** 2 / p2 + 0.5 * mu ** 2 / p2).mean(1).mean()
+            if cfg.get("add_improvement_maximization_loss", False) and prev_mle is not None:  # :1189-1199
+                imp = imp - reg_coeff * cfg["latent_pred_loss_coeff"] * ((xh - prev_mle) ** 2).sum(dim=(1, 2, 3)).mean()
+            prev_mle = xh
             c = cfg["first_step_loss_coeff"] if t == 0 else 1.0
             if cfg["intermediate_reconstruction"] or t == Tn - 1:
                 loss = loss + 16.0 * c * rec
@@ -199,13 +228,21 @@ class Twin:
             recs.append(rec.detach())
             kls.append(kl.detach())
             xhats.append(xh.detach().permute(0, 2, 3, 1))
-            prev = xh
+            prev = sample
         out = dict(loss=float(loss.detach()), final_loss=float(recs[-1]), recon=[float(r) for r in recs],
                    kl=[float(k) for k in kls], xhat=[h.numpy() for h in xhats])
         if backward:
             for p in self.P.values():
                 p.grad = None
-            loss.backward()
+            loss.backward(retain_graph=torch.is_tensor(imp))
             out["grads"] = {k: (p.grad.numpy() if p.grad is not None else torch.zeros_like(p).numpy())
                             for k, p in self.P.items()}
+            if torch.is_tensor(imp):
+                for p in self.P.values():
+                    p.grad = None
+                imp.backward()
+                out["imp_grads"] = {k: (p.grad.numpy() if p.grad is not None else torch.zeros_like(p).numpy())
+                                    for k, p in self.P.items()}
+        if torch.is_tensor(imp):
+            out["imp_loss"] = float(imp.detach())
         return out

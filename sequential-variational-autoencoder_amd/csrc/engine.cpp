@@ -1316,6 +1316,16 @@ static int engine_backward(svae_ctx* c) {
   if (c->side) {  // the side stream starts after the forward (and anything before it)
     hipEventRecord(c->ev_start, st);
     hipStreamWaitEvent(c->st2, c->ev_start, 0);
+    // re-arm the slot-free events on the main stream: the previous backward's side-stream work
+    // was joined into it, so "free" holds now, and every later wait depends only on work of this
+    // pass (required when the step is captured into a graph)
+    for (int i = 0; i < svae_ctx::NR; ++i) hipEventRecord(c->ev_free[i], st);
+    for (int i = 0; i < 2; ++i) {
+      hipEventRecord(c->ev_ifree[i], st);
+      hipEventRecord(c->ev_dcat_free[i], st);
+      hipEventRecord(c->ev_dtop_free[i], st);
+    }
+    hipEventRecord(c->ev_da_free, st);
   }
   for (int t = T - 1; t >= 0; --t) {
     if (t < T - 1) {
