@@ -56,11 +56,29 @@ typedef struct svae_config {
   /* Latent InfoMax (predict_latent_code :129-131, create_recognition_network :1013-1020):
    * q(z_t | x_{t-1}) for t >= 1 (gradient flows into x_{t-1}); the KL term only at step 0
    * unless predict_latent_code_with_regularization (:1170-1172).  Under share_phi step 0 keeps
-   * its own "phi/inference_step_0" (:1573).  The improvement-maximisation loss and its separate
-   * optimiser (:1182-1201, :1302-1316) are not part of this path. */
+   * its own "phi/inference_step_0" (:1573). */
   int32_t predict_latent_code, predict_latent_code_with_regularization;
   /* regularized_steps (:220, :1154): bit t set = step t carries NO KL term (0 = every step) */
   uint32_t unregularized_steps_mask[2];
+  /* ---- chain variants ---- */
+  int32_t use_uniform_prior;          /* KL_b = mean_d(-log sigma) (:1159-1160) */
+  /* add_noise_to_chain (:1088-1090): the sample fed to step t+1 is mle_t + reg * sd_t * N(0,1);
+   * sd_t = noise_stddevs[t] (:1665-1666), or predicted (below).  The loss keeps the MLE. */
+  int32_t add_noise_to_chain;
+  float noise_stddevs[64];            /* mc_steps entries (:239) */
+  /* predict_generator_noise (:1667, stddevs_prediction :1866-1875): sd_t = max * sigmoid(1x1 conv of
+   * stddev_layers x conv2d_bn_lrelu(4x4, s1) of the output conv-T's sigmoid); the reconstruction
+   * term becomes the Gaussian NLL mean(log sd + 0.5 log 2pi + 0.5 ((mle - target)/sd)^2) (:1149-1150).
+   * Requires add_noise_to_chain.  Filter sizes <= 8 (reference default 5 x 5). */
+  int32_t predict_generator_noise;
+  float predict_generator_stddev_max;
+  int32_t stddev_layers;
+  int32_t stddev_filter_sizes[8];
+  /* add_improvement_maximization_loss (:1182-1201): imp = reg * latent_pred_loss_coeff *
+   * -mean_b sum_{t>=1} ||mle_t - mle_{t-1}||^2, minimised over the recognition variables only by its
+   * own clip + Adam update (:1299-1316): svae_backward_imp / svae_adam_imp. */
+  int32_t add_improvement_maximization_loss;
+  float latent_pred_loss_coeff;
 } svae_config;
 
 typedef struct svae_param_desc {
@@ -83,7 +101,10 @@ enum svae_buffer {
   SVAE_BUF_STEP_STATS = 4, /* [T][2] = (mean_b recon_t, mean_b KL_t)   (:1163-1164) */
   SVAE_BUF_REC_IMG = 5,  /* [B] per-image recon of step t */
   SVAE_BUF_KL_IMG = 6,   /* [B] per-image KL of step t */
-  SVAE_BUF_DZ = 7        /* [B,Dz] d loss / d z_t (after svae_backward) */
+  SVAE_BUF_DZ = 7,       /* [B,Dz] d loss / d z_t (after svae_backward) */
+  SVAE_BUF_SAMPLE = 8,   /* training_samples[t] [B,H,W,C] (= the MLE without chain noise, :963) */
+  SVAE_BUF_STDDEV = 9,   /* predicted stddevs [B,H,W,1] of step t (predict_generator_noise) */
+  SVAE_BUF_IMP_IMG = 10  /* [B] ||mle_t - mle_{t-1}||^2 per image (improvement loss, t >= 1) */
 };
 
 /* Parameter table (pure host; callable without a GPU).  Live (trainable, non-zero-grad)
@@ -112,6 +133,18 @@ int svae_forward(svae_ctx* ctx, const float* x, const float* target, const float
  * state (svae_backward needs a new svae_forward). */
 int svae_generate(svae_ctx* ctx, const float* z, void* stream);
 int svae_backward(svae_ctx* ctx, void* stream);
+/* Chain noise N(0,1) [T,B,H,W,C] used by every later svae_forward / svae_generate (device pointer,
+ * kept by reference; NULL = drawn on device per forward, as tf.random_normal :1090). */
+int svae_set_chain_noise(svae_ctx* ctx, const float* noise);
+/* Improvement-maximisation loss (add_improvement_maximization_loss): bind a caller-owned gradient
+ * buffer (n_total elements, public layout), then after svae_forward, svae_backward_imp writes
+ * d imp / d every variable into it (the optimiser uses only the recognition part, :1302).
+ * svae_adam_imp applies clip + Adam to the recognition variables [0, phi_end) with that gradient and
+ * the same Adam moments (one AdamOptimizer, :1267); *phi_end from svae_imp_range. */
+int svae_bind_imp(svae_ctx* ctx, float* grads_imp);
+int svae_backward_imp(svae_ctx* ctx, void* stream);
+int svae_adam_imp(svae_ctx* ctx, float lr, int64_t step, float clip, void* stream);
+int svae_imp_range(svae_ctx* ctx, int64_t* phi_end);
 /* Data-parallel hook (no reference counterpart; the reference has no collective).  During
  * svae_backward, hook(user, t) is called on the host after the backward of chain step t is
  * enqueued (t = T-1 .. 0): at that point svae_hook_stream(ctx) is ordered after every kernel of

@@ -28,6 +28,11 @@ class SvaeConfig(ctypes.Structure):
         ("share_theta", ctypes.c_int32), ("share_phi", ctypes.c_int32),
         ("predict_latent_code", ctypes.c_int32), ("predict_latent_code_with_regularization", ctypes.c_int32),
         ("unregularized_steps_mask", ctypes.c_uint32 * 2),
+        ("use_uniform_prior", ctypes.c_int32), ("add_noise_to_chain", ctypes.c_int32),
+        ("noise_stddevs", ctypes.c_float * 64), ("predict_generator_noise", ctypes.c_int32),
+        ("predict_generator_stddev_max", ctypes.c_float), ("stddev_layers", ctypes.c_int32),
+        ("stddev_filter_sizes", ctypes.c_int32 * 8), ("add_improvement_maximization_loss", ctypes.c_int32),
+        ("latent_pred_loss_coeff", ctypes.c_float),
     ]
 
 
@@ -37,6 +42,7 @@ class SvaeParamDesc(ctypes.Structure):
 
 
 BUF_XHAT, BUF_MU, BUF_SIGMA, BUF_Z, BUF_STEP_STATS, BUF_REC_IMG, BUF_KL_IMG, BUF_DZ = range(8)
+BUF_SAMPLE, BUF_STDDEV, BUF_IMP_IMG = 8, 9, 10
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 
 _lib = None
@@ -87,6 +93,11 @@ def lib():
         "svae_kernel_name": ([i32], ctypes.c_char_p),
         "svae_set_backward_hook": ([vp, STEP_HOOK, vp], i32),
         "svae_hook_stream": ([vp], vp),
+        "svae_set_chain_noise": ([vp, vp], i32),
+        "svae_bind_imp": ([vp, vp], i32),
+        "svae_backward_imp": ([vp, vp], i32),
+        "svae_adam_imp": ([vp, f32, i64, f32, vp], i32),
+        "svae_imp_range": ([vp, ctypes.POINTER(i64)], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -101,7 +112,8 @@ EXPORTED = ["svae_param_count", "svae_param_layout", "svae_create", "svae_destro
             "svae_op_conv", "svae_op_conv_dgrad", "svae_op_conv_wgrad", "svae_op_bn_act",
             "svae_op_bn_act_bwd", "svae_op_fc", "svae_probe_begin", "svae_probe_end", "svae_kernel_name",
             "svae_op_gather_bf16", "svae_op_wgrad_bf16", "svae_generate", "svae_set_backward_hook",
-            "svae_hook_stream", "svae_adam_range", "svae_backward_adam", "svae_adam_state"]
+            "svae_hook_stream", "svae_adam_range", "svae_backward_adam", "svae_adam_state",
+            "svae_set_chain_noise", "svae_bind_imp", "svae_backward_imp", "svae_adam_imp", "svae_imp_range"]
 
 # bf16 GEMM instance ids (csrc/kernels.h KernelId) for svae_probe_begin
 KID_IGEMM_BF16_256x32 = 2

@@ -40,6 +40,26 @@ class SVAEConfig:
     predict_latent_code: bool = False                 # :225 (Latent InfoMax: q(z_t | x_{t-1}))
     predict_latent_code_with_regularization: bool = False  # :230
     regularized_steps: Tuple[int, ...] = None         # :220 (None = every step)
+    # chain variants
+    use_uniform_prior: bool = False                   # :232, KL = mean(-log sigma) (:1159-1160)
+    add_noise_to_chain: bool = False                  # :233, sample = mle + reg*sd*N(0,1) (:1090)
+    noise_stddevs: Tuple[float, ...] = None           # :239 (None = the reference's list)
+    predict_generator_noise: bool = False             # :234, stddevs_prediction + NLL (:1147-1150)
+    predict_generator_stddev_max: float = 1.0         # :236
+    predict_generator_stddev_filter_sizes: Tuple[int, ...] = (5, 5, 5, 5, 5)  # :237-238
+    add_improvement_maximization_loss: bool = False   # :227, own optimiser over phi (:1299-1316)
+    latent_pred_loss_coeff: float = 0.001             # :253
+
+    def noise_list(self):
+        """noise_stddevs[t] per step (sequential_vae.py:239; the reference indexes noise_stddevs[step])."""
+        if not self.add_noise_to_chain or self.predict_generator_noise:
+            return [0.0] * self.mc_steps
+        nd = self.noise_stddevs
+        if nd is None:
+            nd = [0.5 ** 1, 0.5 ** 2, 0.5 ** 3, 0.5 ** 4, 0.5 ** 5, 0.5 ** 6, 0.5 ** 7, 0.0]
+        if len(nd) < self.mc_steps:
+            raise ValueError("noise_stddevs needs mc_steps = %d entries" % self.mc_steps)
+        return [float(v) for v in nd[:self.mc_steps]]
 
     @property
     def latent_dim(self):
@@ -73,6 +93,18 @@ class SVAEConfig:
                 if t not in self.regularized_steps:
                     unreg |= 1 << t
         c.unregularized_steps_mask[0], c.unregularized_steps_mask[1] = unreg & 0xFFFFFFFF, unreg >> 32
+        c.use_uniform_prior = int(self.use_uniform_prior)
+        c.add_noise_to_chain = int(self.add_noise_to_chain)
+        for t, v in enumerate(self.noise_list()):
+            c.noise_stddevs[t] = v
+        c.predict_generator_noise = int(self.predict_generator_noise)
+        c.predict_generator_stddev_max = self.predict_generator_stddev_max
+        fs = list(self.predict_generator_stddev_filter_sizes)
+        c.stddev_layers = len(fs)
+        for i, f in enumerate(fs[:8]):
+            c.stddev_filter_sizes[i] = f
+        c.add_improvement_maximization_loss = int(self.add_improvement_maximization_loss)
+        c.latent_pred_loss_coeff = self.latent_pred_loss_coeff
         return c
 
     def as_dict(self):
@@ -88,7 +120,15 @@ class SVAEConfig:
                     share_theta=self.share_theta_weights, share_phi=self.share_phi_weights,
                     predict_latent_code=self.predict_latent_code,
                     predict_latent_code_with_regularization=self.predict_latent_code_with_regularization,
-                    regularized_steps=self.regularized_steps)
+                    regularized_steps=self.regularized_steps,
+                    use_uniform_prior=self.use_uniform_prior, add_noise_to_chain=self.add_noise_to_chain,
+                    noise_stddevs=(self.noise_list() if self.add_noise_to_chain and not self.predict_generator_noise
+                                   else None),
+                    predict_generator_noise=self.predict_generator_noise,
+                    predict_generator_stddev_max=self.predict_generator_stddev_max,
+                    stddev_filter_sizes=tuple(self.predict_generator_stddev_filter_sizes),
+                    add_improvement_maximization_loss=self.add_improvement_maximization_loss,
+                    latent_pred_loss_coeff=self.latent_pred_loss_coeff)
 
     def kl_on(self, t):
         """1 if step t's KL term enters self.loss (sequential_vae.py:1154, :1170-1172), else 0."""
@@ -120,6 +160,22 @@ PRESETS = {
     "c_v2_coeff_change_abl": SVAEConfig(latent_dims=[12, 12, 12, 12], filter_sizes=[3, 16, 32, 64, 128, 384],
                                         share_theta_weights=True, share_phi_weights=True, predict_latent_code=True,
                                         regularized_steps=(0,), latent_mean_clip=32.0, first_step_loss_coeff=2.0),
+    # chain variants
+    "sequential_vae_celebA_inhomog_inf_max_uniform": SVAEConfig(predict_latent_code=True,
+                                                                use_uniform_prior=True),          # :700-702
+    "c_homog_no_reg_imp_max": SVAEConfig(latent_dims=[12, 12, 12, 12], filter_sizes=[3, 16, 32, 64, 128, 384],
+                                         share_theta_weights=True, share_phi_weights=True, predict_latent_code=True,
+                                         regularized_steps=(0,), add_improvement_maximization_loss=True,
+                                         latent_mean_clip=32.0),                                    # :408-418
+    "c_v2_diag_noise_abl": SVAEConfig(latent_dims=[12, 12, 12, 12], filter_sizes=[3, 16, 32, 64, 128, 384],
+                                      share_theta_weights=True, share_phi_weights=True, predict_latent_code=True,
+                                      regularized_steps=(0,), latent_mean_clip=32.0, add_noise_to_chain=True,
+                                      predict_generator_noise=True),                                # :469-482
+    "c_homog_imp_max_var_pred": SVAEConfig(latent_dims=[12, 12, 12, 12], filter_sizes=[3, 16, 32, 64, 128, 384],
+                                           share_theta_weights=True, share_phi_weights=True,
+                                           predict_latent_code=True, add_improvement_maximization_loss=True,
+                                           latent_mean_clip=32.0, predict_latent_code_with_regularization=True,
+                                           add_noise_to_chain=True, predict_generator_noise=True),  # :568-582
     "tiny_homog": SVAEConfig(batch=4, height=32, width=32, channels=3, levels=4, filter_sizes=[3, 8, 8, 16, 24, 16],
                              latent_dims=[2, 2, 3, 2], mc_steps=3, share_theta_weights=True,
                              share_phi_weights=True),

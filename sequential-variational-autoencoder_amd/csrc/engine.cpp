@@ -65,6 +65,10 @@ struct GenStep {
   ConvL s2[8], s1[8];  // indexed by level
   int wout = -1, bout = -1, wratio = -1, bratio = -1;
   long long owout = 0, obout = 0, owratio = 0, obratio = 0;
+  // stddevs_prediction (:1866-1875): conv2d_bn_lrelu layers + 1x1 conv
+  ConvL sd[8];
+  int wsd = -1, bsd = -1;
+  long long owsd = 0, obsd = 0;
 };
 
 struct Geo {
@@ -77,6 +81,12 @@ struct Geo {
   bool share_theta, share_phi;
   bool plc, plc_reg;          // predict_latent_code (+ _with_regularization)
   unsigned long long unreg;   // steps without a KL term
+  // chain variants
+  bool uniform;               // use_uniform_prior
+  bool noisy, pgn, imp;       // add_noise_to_chain, predict_generator_noise, improvement loss
+  float nstd[64];             // noise_stddevs
+  float sd_max, lp_coef;      // predict_generator_stddev_max, latent_pred_loss_coeff
+  int sd_nl, sd_F[9];         // stddev network: layers and channels (sd_F[0] = C)
   // weight of step t's KL term relative to reg * c_first (compute_and_accumulate_loss :1154-1172)
   float kl_on(int t) const {
     if ((unreg >> t) & 1ULL) return 0.f;
@@ -125,6 +135,27 @@ bool make_geo(const svae_config* c, Geo& g, std::string& err) {
   g.plc = c->predict_latent_code != 0;
   g.plc_reg = c->predict_latent_code_with_regularization != 0;
   g.unreg = (unsigned long long)c->unregularized_steps_mask[0] | ((unsigned long long)c->unregularized_steps_mask[1] << 32);
+  g.uniform = c->use_uniform_prior != 0;
+  g.noisy = c->add_noise_to_chain != 0;
+  g.pgn = c->predict_generator_noise != 0;
+  g.imp = c->add_improvement_maximization_loss != 0;
+  g.sd_max = c->predict_generator_stddev_max;
+  g.lp_coef = c->latent_pred_loss_coeff;
+  for (int t = 0; t < 64; ++t) g.nstd[t] = g.noisy ? c->noise_stddevs[t] : 0.f;
+  g.sd_nl = 0;
+  g.sd_F[0] = g.C;
+  if (g.pgn) {
+    // stddevs = 0 without chain noise (:1664-1671) and the NLL would take log(0)
+    if (!g.noisy) { err = "predict_generator_noise needs add_noise_to_chain"; return false; }
+    g.sd_nl = c->stddev_layers;
+    if (g.sd_nl < 1 || g.sd_nl > 8) { err = "stddev_layers must be in [1,8]"; return false; }
+    for (int i = 0; i < g.sd_nl; ++i) {
+      g.sd_F[i + 1] = c->stddev_filter_sizes[i];
+      if (g.sd_F[i + 1] < 1 || g.sd_F[i + 1] > 8) { err = "stddev_filter_sizes must be in [1,8]"; return false; }
+    }
+    if (!(g.sd_max > 0.f)) { err = "predict_generator_stddev_max must be > 0"; return false; }
+    if (g.H % 4) { err = "predict_generator_noise needs an image size divisible by 4"; return false; }
+  }
   return true;
 }
 
@@ -175,6 +206,11 @@ struct Scope {
     w = add(ln, "weights", {nin, nout}, INIT_GLOROT, false, false);
     b = add(ln, "biases", {nout}, INIT_ZERO, false, false);
   }
+  void conv_plain(int k, int cin, int cout, int& w, int& b) {  // conv2d without BN (default xavier init)
+    std::string ln = nm("Conv", n_conv++);
+    w = add(ln, "weights", {k, k, cin, cout}, INIT_GLOROT, false, false);
+    b = add(ln, "biases", {cout}, INIT_ZERO, false, false);
+  }
   void convt_plain(int cin, int cout, int& w, int& b) {
     std::string ln = nm("Conv2d_transpose", n_convt++);
     w = add(ln, "weights", {4, 4, cout, cin}, INIT_GLOROT, false, false);
@@ -203,6 +239,7 @@ struct Model {
   std::vector<PDesc> pub;
   std::vector<int> vpub;  // descs index -> pub index
   long long p_total = 0, p_live = 0;
+  long long p_phi_end = 0;  // public recognition variables occupy [0, p_phi_end)
   bool shared = false;
 
   long long off(int idx) const { return idx < 0 ? -1 : descs[idx].offset; }
@@ -259,6 +296,10 @@ struct Model {
     }
     p_total = o;
     if (p_live < 0) p_live = o;
+    p_phi_end = 0;
+    for (auto& d : pub)
+      if (d.region == R_PHI) p_phi_end = std::max(p_phi_end, d.offset + d.size);
+    p_phi_end = (p_phi_end + 63) / 64 * 64;
   }
 
   void build() {
@@ -323,6 +364,9 @@ struct Model {
       }
       sg.convt_plain(F[1], g.C, G.wout, G.bout);
       if (t >= 1) sg.convt_plain(F[1], 1, G.wratio, G.bratio);
+      // stddevs_prediction, created after the output / ratio conv-T (:1734-1735, :1866-1870)
+      for (int l = 0; l < g.sd_nl; ++l) G.sd[l] = sg.conv_bn(g.sd_F[l], g.sd_F[l + 1], 1, g.H, false);
+      if (g.sd_nl) sg.conv_plain(1, g.sd_F[g.sd_nl], 1, G.wsd, G.bsd);
     }
     // offsets: live phi blocks (uniform per-step stride), live theta blocks, frozen tail.
     // Every tensor starts on a 64-float (256 B) boundary: the GEMM kernels stage weights
@@ -361,6 +405,8 @@ struct Model {
       rc(enc[t].c); rf(enc[t].fc); rf(gen[t].top);
       GenStep& G = gen[t];
       G.owout = off(G.wout); G.obout = off(G.bout); G.owratio = off(G.wratio); G.obratio = off(G.bratio);
+      for (int l = 0; l < g.sd_nl; ++l) rc(G.sd[l]);
+      G.owsd = off(G.wsd); G.obsd = off(G.bsd);
     }
   }
 };
@@ -468,6 +514,11 @@ struct svae_ctx {
     BNS s2_bn[8], s1_bn[8];
     float *wpack, *a_out, *xhat, *rec_part, *rec_img, *stats;
     void* wpack_h;  // bf16 copy of wpack (NK [tap][C+1][F1]) for the bf16 output conv-T
+    // chain variants: training_samples[t] (when noise perturbs it), predicted stddevs and the
+    // stddev network's saved tensors
+    bool has_sample;
+    float *sample, *sd;
+    float *sd_pre[8], *sd_act[8], *sd_mean[8], *sd_inv[8];
   };
   std::vector<StepBufs> sb;
   int out_nblk = 0;
@@ -477,6 +528,16 @@ struct svae_ctx {
   float *sfc_part, *dz, *dhead;
   float *idb, *ida, *idpre;  // inference bwd: [T] x max level slab
   float* slab;
+  // chain variants: chain noise, stddev-network backward scratch, improvement loss
+  const float* noise_in = nullptr;   // caller's N(0,1) [T,B,H,W,C] (svae_set_chain_noise)
+  const float* noise_used = nullptr;
+  float* noise_buf = nullptr;
+  float *sd_d[2] = {}, *sd_dpre = nullptr, *sd_wpart = nullptr, *sd_sums = nullptr, *dmle = nullptr;
+  double* sd_part = nullptr;
+  float *dseed = nullptr, *imp_img = nullptr, *kl_zero = nullptr;
+  bool imp_pass = false;             // svae_backward_imp: seeds from the improvement loss only
+  float* Gimp_pub = nullptr;         // caller's improvement-loss gradient (svae_bind_imp)
+  float* Gimp_v = nullptr;           // its virtual copy under weight sharing
   // BN statistics: fixed-point column accumulators (common.h stat_put), one region per BN
   // instance of a pass, handed out in launch order and zeroed once per pass (acc_reset)
   u64* bnacc = nullptr;
@@ -1052,7 +1113,7 @@ static int inference_fwd(svae_ctx* c, int t0, int n, View in0) {
     lv.dim[l] = h.d;
   }
   const long long ms = (long long)B * g.Dz;
-  latent_fwd(c->head_part + t0 * hps, hps, c->head_nsplit, B, g.Dz, lv, wg, g.clipv, g.prior, c->eps_used + t0 * ms, ms,
+  latent_fwd(c->head_part + t0 * hps, hps, c->head_nsplit, B, g.Dz, lv, wg, g.clipv, g.prior, g.uniform, c->eps_used + t0 * ms, ms,
              c->mu + t0 * ms, c->sig + t0 * ms, c->z + t0 * ms, ms, c->kl_img + (long long)t0 * B, B, n, st);
   return 0;
 }
@@ -1082,6 +1143,77 @@ static void split_latent_fwd(svae_ctx* c, int t, hipStream_t stream) {
   }
 }
 
+// training_samples[t] (:963, :1090): what step t+1 (encoder, highway, Latent InfoMax recognition)
+// consumes -- the MLE unless chain noise perturbs it
+static const float* chain_x(const svae_ctx* c, int t) {
+  const svae_ctx::StepBufs& s = c->sb[t];
+  return s.has_sample ? s.sample : s.xhat;
+}
+
+// stddevs_prediction of step t (:1866-1875) on conv_output = sigmoid(output conv-T pre-activation),
+// then sample = mle + reg * sd * noise and the NLL per-image partials (:1090, :1149-1150)
+static void sd_forward(svae_ctx* c, int t) {
+  const Geo& g = c->m.g;
+  const GenStep& G = c->m.gen[t];
+  svae_ctx::StepBufs& s = c->sb[t];
+  hipStream_t st = c->st;
+  const long long P = (long long)g.B * g.H * g.W;
+  const int nblk = sd_pixel_blocks(P);
+  const float* in = s.a_out;
+  int ldi = g.C + 1, sig = 1;
+  for (int l = 0; l < g.sd_nl; ++l) {
+    const int Ci = g.sd_F[l], Co = g.sd_F[l + 1];
+    sd_conv_fwd(in, ldi, sig, Ci, c->P + G.sd[l].ow, Co, g.H, g.W, P, s.sd_pre[l], c->sd_part, st);
+    sd_stat_fin(c->sd_part, nblk, Co, P, 1e-3f, 0, s.sd_mean[l], s.sd_inv[l], nullptr, nullptr, st);
+    sd_bn_apply(s.sd_pre[l], Co, P, s.sd_mean[l], s.sd_inv[l], c->P + G.sd[l].obeta, s.sd_act[l], st);
+    in = s.sd_act[l];
+    ldi = Co;
+    sig = 0;
+  }
+  sd_head_fwd(in, g.sd_F[g.sd_nl], c->P + G.owsd, c->P + G.obsd, g.sd_max, s.xhat, c->tgt_in,
+              c->noise_used + (long long)t * P * g.C, c->reg, g.B, g.C, g.H * g.W, s.sd, s.sample, s.rec_part,
+              c->out_nblk, st);
+}
+
+// backward of sd_forward's head: dmle (-> c->dmle) = dsample + NLL term; the stddev network's
+// gradients; its input gradient accumulates into da (the output conv-T pre-activation)
+static void sd_backward(svae_ctx* c, int t, const float* dsample, float nll_coef) {
+  const Geo& g = c->m.g;
+  const GenStep& G = c->m.gen[t];
+  svae_ctx::StepBufs& s = c->sb[t];
+  hipStream_t st = c->st;
+  const long long P = (long long)g.B * g.H * g.W;
+  const int nblk = sd_pixel_blocks(P);
+  const int nl = g.sd_nl;
+  sd_head_bwd(s.sd_act[nl - 1], g.sd_F[nl], c->P + G.owsd, c->P + G.obsd, g.sd_max, s.xhat, c->tgt_in,
+              c->noise_used + (long long)t * P * g.C, c->reg, nll_coef, dsample, g.C, P, c->dmle, c->sd_d[0],
+              c->sd_wpart, c->Gr + G.owsd, c->Gr + G.obsd, st);
+  int cur = 0;
+  for (int l = nl - 1; l >= 0; --l) {
+    const int Ci = g.sd_F[l], Co = g.sd_F[l + 1];
+    const ConvL& L = G.sd[l];
+    const float* dact = c->sd_d[cur];
+    sd_bn_bwd_reduce(dact, s.sd_pre[l], Co, P, s.sd_mean[l], s.sd_inv[l], c->P + L.obeta, c->sd_part, st);
+    sd_stat_fin(c->sd_part, nblk, Co, P, 0.f, 1, nullptr, nullptr, c->sd_sums, c->Gr + L.obeta, st);
+    sd_bn_bwd_apply(dact, s.sd_pre[l], Co, P, s.sd_mean[l], s.sd_inv[l], c->P + L.obeta, c->sd_sums, c->sd_dpre, st);
+    if (l > 0) {
+      sd_conv_wgrad(s.sd_act[l - 1], Ci, 0, Ci, c->sd_dpre, Co, g.B, g.H, g.W, c->sd_wpart, c->Gr + L.ow, st);
+      sd_conv_dgrad(c->sd_dpre, Co, c->P + L.ow, Ci, g.H, g.W, P, c->sd_d[cur ^ 1], Ci, nullptr, 0, 0, st);
+      cur ^= 1;
+    } else {  // layer 0's input gradient waits in sd_dpre for sd_backward_input
+      sd_conv_wgrad(s.a_out, g.C + 1, 1, Ci, c->sd_dpre, Co, g.B, g.H, g.W, c->sd_wpart, c->Gr + L.ow, st);
+    }
+  }
+}
+
+// d conv_output of the stddev network, times sigmoid', added into da after output_bwd wrote it
+static void sd_backward_input(svae_ctx* c, int t) {
+  const Geo& g = c->m.g;
+  const long long P = (long long)g.B * g.H * g.W;
+  sd_conv_dgrad(c->sd_dpre, g.sd_F[1], c->P + c->m.gen[t].sd[0].ow, g.C, g.H, g.W, P, c->da, g.C + 1, c->sb[t].a_out,
+                g.C + 1, 1, c->st);
+}
+
 // ============================================================================
 // forward
 // ============================================================================
@@ -1101,6 +1233,16 @@ static int engine_forward(svae_ctx* c) {
   if (g.bf16 && !(c->fresh == M.n_live && !M.shared))
     shadow_weights(c->P, c->wN, c->wT, M.n_live, c->tiles_d, c->ntiles, c->offs_d, st);
   c->fresh = 0;
+  if (g.noisy) {  // chain noise N(0,1) [T,B,H,W,C] (tf.random_normal(image_batch_shape), :1090)
+    const long long n = (long long)T * B * g.H * g.W * g.C;
+    if (c->noise_in) {
+      c->noise_used = c->noise_in;
+    } else {
+      philox_normal(c->noise_buf, n, 0xC4A1C4A1ULL, c->rng_offset, st);
+      c->rng_offset += (n + 3) / 4;
+      c->noise_used = c->noise_buf;
+    }
+  }
   if (c->generative) {
     // generative mode (sequential_vae.py:947-952, :1025 latent_generative = self.latents[t]):
     // z_t comes from the caller (or N(0,1)), the recognition networks do not run
@@ -1141,7 +1283,7 @@ static int engine_forward(svae_ctx* c) {
   for (int t = 0; t < T; ++t) {
     svae_ctx::StepBufs& s = c->sb[t];
     const GenStep& G = M.gen[t];
-    const float* xprev = t >= 1 ? c->sb[t - 1].xhat : nullptr;
+    const float* xprev = t >= 1 ? chain_x(c, t - 1) : nullptr;
     if (g.plc && t >= 1 && !c->generative)  // Latent InfoMax: z_t from the previous sample (:1014-1015)
       if ((r = inference_fwd(c, t, 1, View{(float*)xprev, g.C, 0}))) return r;
     // g_theta encoder of x_{t-1}  (compute_encodings :1764-1777)
@@ -1216,7 +1358,14 @@ static int engine_forward(svae_ctx* c) {
       }
       output_fwd(s.a_out, B, g.H * g.W, g.C, xprev, c->tgt_in, g.lo, g.hi, g.minh, g.maxh, s.xhat, s.rec_part,
                  c->out_nblk, st);
+      const long long nimg = (long long)B * g.H * g.W * g.C;
+      if (g.pgn)  // predicted stddevs: noisy sample and the NLL partials (replace the MSE partials)
+        sd_forward(c, t);
+      else if (s.has_sample)  // fixed noise_stddevs[t]
+        chain_noise(s.xhat, c->noise_used + t * nimg, c->reg * g.nstd[t], nimg, s.sample, st);
       loss_reduce(s.rec_part, c->out_nblk, c->kl_img + (long long)t * B, B, g.H * g.W * g.C, s.stats, s.rec_img, st);
+      if (g.imp && t >= 1)  // ||mle_t - mle_{t-1}||^2 per image (:1190-1191)
+        sqdiff_img(s.xhat, c->sb[t - 1].xhat, B, (long long)g.H * g.W * g.C, c->imp_img + (long long)t * B, st);
     }
   }
   return 0;
@@ -1238,8 +1387,10 @@ static int inference_bwd(svae_ctx* c, int t0, int n, View in0, float* dx0) {
   int r;
   const long long ms = (long long)B * g.Dz;
   if (c->side) hipStreamWaitEvent(st, c->ev_dz, 0);  // dz_t: split-latent backward (st3)
+  // the improvement-loss pass carries no KL term
   latent_bwd(c->mu + t0 * ms, c->sig + t0 * ms, c->eps_used + t0 * ms, c->dz + t0 * ms, ms, ms, B, g.Dz,
-             c->kl_coef + t0, 1, g.prior, g.clipv, c->dhead, (long long)B * 2 * g.Dz, n, st);
+             (c->imp_pass ? c->kl_zero : c->kl_coef) + t0, 1, g.prior, g.uniform, g.clipv, c->dhead,
+             (long long)B * 2 * g.Dz, n, st);
   const InfStep& I0 = M.inf[t0];
   auto bns = [&](const BNS& b, int C) { return BNS{b.mean + (long long)t0 * C, b.invstd + (long long)t0 * C}; };
   auto act_a = [&](int l) { return c->inf_act_a[l] + t0 * c->inf_gs[l]; };
@@ -1330,7 +1481,7 @@ static int engine_backward(svae_ctx* c) {
   for (int t = T - 1; t >= 0; --t) {
     if (t < T - 1) {
       if (g.plc) {  // q(z_{t+1} | x_t): its weights' gradients and its share of d loss / d x_t
-        r = inference_bwd(c, t + 1, 1, View{c->sb[t].xhat, g.C, 0}, c->dx[t & 1]);
+        r = inference_bwd(c, t + 1, 1, View{(float*)chain_x(c, t), g.C, 0}, c->dx[t & 1]);
         if (r) return r;
       }
       step_hook(c, t + 1);  // step t+1's gradients are complete
@@ -1338,17 +1489,37 @@ static int engine_backward(svae_ctx* c) {
     if (t < c->dbg_stop_step) return 0;  // debug: stop after step dbg_stop_step
     svae_ctx::StepBufs& s = c->sb[t];
     const GenStep& G = M.gen[t];
-    const float* xprev = t >= 1 ? c->sb[t - 1].xhat : nullptr;
-    const float* dxin = t < T - 1 ? c->dx[t & 1] : nullptr;
+    const float* xprev = t >= 1 ? chain_x(c, t - 1) : nullptr;
+    const float* dxin = t < T - 1 ? c->dx[t & 1] : nullptr;  // d loss / d training_samples[t]
     float* dxout = t >= 1 ? c->dx[(t - 1) & 1] : nullptr;
     const float cf = t == 0 ? g.c_first : 1.f;
-    const float rec_coef = (g.interm || t == T - 1) ? 16.f * cf / (float)(P0 * g.C) : 0.f;
+    float rec_coef = (g.interm || t == T - 1) ? 16.f * cf / (float)(P0 * g.C) : 0.f;
+    const float imp_coef = -c->reg * g.lp_coef / (float)B;
+    if (c->imp_pass) {  // improvement loss: its d / d mle_t seeds the chain instead of the ELBO's
+      rec_coef = 0.f;
+      if (!g.pgn) {  // d sample / d mle = 1: the seed joins the chain gradient
+        imp_seed(dxin, t >= 1 ? c->sb[t - 1].xhat : nullptr, s.xhat, t < T - 1 ? c->sb[t + 1].xhat : nullptr,
+                 imp_coef, P0 * g.C, c->dseed, st);
+        dxin = c->dseed;
+      }
+    }
     float* dzt = c->dz + (long long)t * B * g.Dz;
 
     // ---- output + highway (:1720-1729)
     if (c->side) hipStreamWaitEvent(st, c->ev_da_free, 0);  // previous step's output wgrad read da
-    output_bwd(s.a_out, B, g.H * g.W, g.C, xprev, s.xhat, c->tgt_in, g.lo, g.hi, g.minh, g.maxh, rec_coef, dxin, c->da,
-               dxout, st);
+    if (g.pgn) {  // NLL + sample = mle + reg*sd*noise: d mle and the stddev network, then the output layer
+      sd_backward(c, t, dxin, rec_coef);  // rec_coef = 16 cf / (B H W C), the NLL's element weight
+      if (c->imp_pass)  // the improvement seed is on the MLE, not on the noisy sample: no stddev term
+        imp_seed(c->dmle, t >= 1 ? c->sb[t - 1].xhat : nullptr, s.xhat, t < T - 1 ? c->sb[t + 1].xhat : nullptr,
+                 imp_coef, P0 * g.C, c->dmle, st);
+      output_bwd(s.a_out, B, g.H * g.W, g.C, xprev, s.xhat, c->tgt_in, g.lo, g.hi, g.minh, g.maxh, 0.f, c->dmle, c->da,
+                 dxout, st);
+      // the stddev network's input gradient (d conv_output) joins da after output_bwd wrote it
+      sd_backward_input(c, t);
+    } else {
+      output_bwd(s.a_out, B, g.H * g.W, g.C, xprev, s.xhat, c->tgt_in, g.lo, g.hi, g.minh, g.maxh, rec_coef, dxin,
+                 c->da, dxout, st);
+    }
     {
       // packed [C | ratio] columns; at t=0 the ratio column of da is zero (output_bwd) and its
       // gradient row is dropped by the reduce -> always the 4-wide vector gather
@@ -1638,6 +1809,37 @@ static bool plan(svae_ctx* c) {
     s.rec_part = A((long long)B * c->out_nblk);
     s.rec_img = A(B);
     s.stats = A(2);
+    const long long npx = (long long)B * g.H * g.W;
+    // training_samples[t] differs from the MLE under predicted noise, or a fixed stddev != 0
+    s.has_sample = g.pgn || (g.noisy && g.nstd[t] != 0.f);
+    if (s.has_sample) s.sample = A(npx * g.C);
+    if (g.pgn) {
+      s.sd = A(npx);
+      for (int l = 0; l < g.sd_nl; ++l) {
+        const int Co = g.sd_F[l + 1];
+        s.sd_pre[l] = A(npx * Co);
+        s.sd_act[l] = A(npx * Co);
+        s.sd_mean[l] = A(Co);
+        s.sd_inv[l] = A(Co);
+      }
+    }
+  }
+  {
+    const long long npx = (long long)B * g.H * g.W;
+    if (g.noisy) c->noise_buf = A((long long)T * npx * g.C);
+    if (g.pgn) {
+      for (int i = 0; i < 2; ++i) c->sd_d[i] = A(npx * 8);
+      c->sd_dpre = A(npx * 8);
+      c->sd_part = (double*)A(2LL * sd_pixel_blocks(npx) * 2 * 8);
+      c->sd_wpart = A(std::max<long long>((long long)sd_wgrad_blocks(B, g.H) * 16 * 64, 9LL * sd_pixel_blocks(npx)));
+      c->sd_sums = A(16);
+      c->dmle = A(npx * g.C);
+    }
+    if (g.imp) {
+      c->dseed = A(npx * g.C);
+      c->imp_img = A((long long)T * B);
+    }
+    c->kl_zero = A(64);
   }
   const long long P0 = (long long)B * g.H * g.W;
   c->dx[0] = A(P0 * g.C);
@@ -1881,6 +2083,7 @@ int svae_destroy(svae_ctx* c) {
   if (c->tiles_d) hipFree(c->tiles_d);
   if (c->offs_d) hipFree(c->offs_d);
   if (c->Pv) hipFree(c->Pv);
+  if (c->Gimp_v) hipFree(c->Gimp_v);
   if (c->share_seg) hipFree(c->share_seg);
   delete c;
   return 0;
@@ -1973,6 +2176,7 @@ int svae_generate(svae_ctx* c, const float* z, void* stream) {
   c->x_in = nullptr;  // no training forward state: svae_backward is refused until svae_forward
   c->tgt_in = c->zero_img;
   c->eps_in = z;
+  c->reg = 1.f;  // the generative chain's noise uses reg_coeff's default (placeholder_with_default 1.0, :917)
   const int r = engine_forward(c);
   c->generative = false;
   if (r) return r;
@@ -1991,6 +2195,67 @@ int svae_backward(svae_ctx* c, void* stream) {
     hipStreamWaitEvent(c->st, c->ev_j3, 0);
   }
   if (!r && c->hook) c->hook(c->hook_user, -1);
+  if (r) return r;
+  HIPCHK(c, hipGetLastError());
+  return 0;
+}
+
+int svae_set_chain_noise(svae_ctx* c, const float* noise) {
+  if (!c) return fail(c, SVAE_EBADARG, "null ctx");
+  if (noise && !c->m.g.noisy) return fail(c, SVAE_EBADARG, "add_noise_to_chain is off");
+  c->noise_in = noise;
+  return 0;
+}
+
+int svae_imp_range(svae_ctx* c, int64_t* phi_end) {
+  if (!c || !phi_end) return fail(c, SVAE_EBADARG, "null");
+  *phi_end = c->m.p_phi_end;
+  return 0;
+}
+
+int svae_bind_imp(svae_ctx* c, float* grads_imp) {
+  if (!c || !grads_imp) return fail(c, SVAE_EBADARG, "null buffer");
+  if (!c->m.g.imp) return fail(c, SVAE_EBADARG, "add_improvement_maximization_loss is off");
+  HIPCHK(c, hipMemset(grads_imp, 0, (size_t)c->m.p_total * sizeof(float)));
+  if (c->m.shared && !c->Gimp_v) {
+    hipError_t e = hipMalloc((void**)&c->Gimp_v, (size_t)c->m.n_total * sizeof(float));
+    if (e != hipSuccess) return fail(c, SVAE_ENOMEM, std::string("hipMalloc imp copies: ") + hipGetErrorString(e));
+  }
+  if (c->Gimp_v) HIPCHK(c, hipMemset(c->Gimp_v, 0, (size_t)c->m.n_total * sizeof(float)));
+  c->Gimp_pub = grads_imp;
+  return 0;
+}
+
+// d improvement_maximization_loss / d every variable (:1302-1303): the chain backward again, seeded
+// by the improvement loss alone, into the svae_bind_imp buffer (no hook, no fused update)
+int svae_backward_imp(svae_ctx* c, void* stream) {
+  if (!c || !c->x_in) return fail(c, SVAE_EBADARG, "svae_forward must run first");
+  if (!c->m.g.imp || !c->Gimp_pub) return fail(c, SVAE_EBADARG, "svae_bind_imp must run first");
+  if (c->m.g.T < 2) return fail(c, SVAE_EBADARG, "the improvement loss needs mc_steps >= 2");
+  c->st = (hipStream_t)stream;
+  HIPCHK(c, hipMemsetAsync(c->kl_zero, 0, 64 * sizeof(float), c->st));
+  float *gr = c->Gr, *gv = c->Gv, *gp = c->Gpub;
+  svae_step_hook hk = c->hook;
+  const bool fa = c->fa_on;
+  c->hook = nullptr;
+  c->fa_on = false;
+  c->imp_pass = true;
+  c->Gpub = c->Gimp_pub;
+  c->Gv = c->Gimp_v;
+  c->Gr = c->m.shared ? c->Gimp_v : c->Gimp_pub;
+  int r = engine_backward(c);
+  if (c->side) {
+    hipEventRecord(c->ev_join, c->st2);
+    hipStreamWaitEvent(c->st, c->ev_join, 0);
+    hipEventRecord(c->ev_j3, c->st3);
+    hipStreamWaitEvent(c->st, c->ev_j3, 0);
+  }
+  c->imp_pass = false;
+  c->Gr = gr;
+  c->Gv = gv;
+  c->Gpub = gp;
+  c->hook = hk;
+  c->fa_on = fa;
   if (r) return r;
   HIPCHK(c, hipGetLastError());
   return 0;
@@ -2053,6 +2318,20 @@ int svae_backward_adam(svae_ctx* c, float lr, int64_t step, float clip, void* st
   return 0;
 }
 
+// the improvement loss's own apply_gradients over the recognition variables (:1304-1306), with the
+// ELBO update's Adam moments (one AdamOptimizer)
+int svae_adam_imp(svae_ctx* c, float lr, int64_t step, float clip, void* stream) {
+  if (!c || !c->P || step < 1 || !c->Gimp_pub) return fail(c, SVAE_EBADARG, "bad adam_imp args");
+  float* gp = c->Gpub;
+  const long long f0 = c->fresh;  // re-refreshes shadows the ELBO update already counted
+  c->Gpub = c->Gimp_pub;
+  adam_range(c, 0, c->m.p_phi_end, lr, step, clip, (hipStream_t)stream);
+  c->Gpub = gp;
+  c->fresh = f0;
+  HIPCHK(c, hipGetLastError());
+  return 0;
+}
+
 int svae_adam_state(svae_ctx* c, int dir, float* m, float* v, int64_t n, void* stream) {
   if (!c || !m || !v || n != c->m.p_live || (dir != 0 && dir != 1)) return fail(c, SVAE_EBADARG, "bad adam_state args");
   const size_t b = (size_t)n * sizeof(float);
@@ -2083,6 +2362,15 @@ int svae_copy_out(svae_ctx* c, int which, int step, float* dst, int64_t n, void*
     case SVAE_BUF_REC_IMG: src = c->sb[step].rec_img; cnt = g.B; break;
     case SVAE_BUF_KL_IMG: src = c->kl_img + (long long)step * g.B; cnt = g.B; break;
     case SVAE_BUF_DZ: src = c->dz + step * ml; cnt = ml; break;
+    case SVAE_BUF_SAMPLE: src = chain_x(c, step); cnt = (long long)g.B * g.H * g.W * g.C; break;
+    case SVAE_BUF_STDDEV:
+      if (!g.pgn) return fail(c, SVAE_EBADARG, "predict_generator_noise is off");
+      src = c->sb[step].sd; cnt = (long long)g.B * g.H * g.W;
+      break;
+    case SVAE_BUF_IMP_IMG:
+      if (!g.imp || step < 1) return fail(c, SVAE_EBADARG, "improvement loss off, or step 0");
+      src = c->imp_img + (long long)step * g.B; cnt = g.B;
+      break;
     case 100: src = c->dx[step & 1]; cnt = (long long)g.B * g.H * g.W * g.C; break;  // debug: dx carry
     case 101: c->dbg_stop_step = step; return 0;                                    // debug: stop step
     case 102: c->dbg_stop_lvl = step; return 0;                                     // debug: stop level

@@ -173,11 +173,11 @@ struct LatentLvls {
 };
 // mu_raw = sum part + bm, sig = sigmoid(sum part + bs), z = clip(mu) + sig*eps, kl_img per image
 void latent_fwd(const float* part, long long part_gs, int nsplit, int B, int Dz, const LatentLvls& lv,
-                long long bias_gs, float clipv, float prior, const float* eps, long long eps_gs, float* mu, float* sig,
-                float* z, long long ms_gs, float* kl_img, long long kl_gs, int groups, hipStream_t s);
+                long long bias_gs, float clipv, float prior, int uniform, const float* eps, long long eps_gs, float* mu,
+                float* sig, float* z, long long ms_gs, float* kl_img, long long kl_gs, int groups, hipStream_t s);
 // dhead[n][0:Dz] = d mu_raw, dhead[n][Dz:2Dz] = d sig_pre; kl_coef (device) = reg*c_first/B
 void latent_bwd(const float* mu, const float* sig, const float* eps, const float* dz, long long gs, long long eps_gs,
-                int B, int Dz, const float* kl_coef, long long kc_gs, float prior, float clipv, float* dhead,
+                int B, int Dz, const float* kl_coef, long long kc_gs, float prior, int uniform, float clipv, float* dhead,
                 long long dh_gs, int groups, hipStream_t s);
 // dX (+)= dhead_l @ [Wm|Ws]^T ; dW = X^T dhead_l ; db = sum_n dhead_l   (w_gs: group stride of W/dW/db)
 void heads_bwd(const float* X, long long x_gs, float* dX, long long dx_gs, int B, int K, const float* Wm,
@@ -220,3 +220,39 @@ void philox_normal(float* out, long long n, unsigned long long seed, unsigned lo
 // column sums of X [rows][C<=4] -> out0[0..n0), out1[0..C-n0)   (part: scratch >= 1024 floats)
 void colsum_small(const float* X, int ld, long long rows, int C, float* part, float* out0, int n0, float* out1,
                   hipStream_t s);
+
+// ---- chain variants (chain.hip): chain noise, predicted-stddev network + NLL, improvement loss ----
+// stddev network layers: 4x4 stride-1 TF-SAME conv, <= 8 channels, fp32 direct convolution.
+// in_sig: the input is sigmoid(in) (layer 0 reads the output conv-T pre-activation, ld = C+1).
+int sd_pixel_blocks(long long P);
+int sd_wgrad_blocks(int B, int H);
+void sd_conv_fwd(const float* in, int ldi, int in_sig, int Ci, const float* W, int Co, int H, int Wd, long long P,
+                 float* pre, double* part, hipStream_t s);
+// mode 0: mean / invstd of the (sum, sum^2) partials; mode 1: sums[2c..2c+1] (and dbeta[c] = sum)
+void sd_stat_fin(const double* part, int nblk, int Co, long long n, float eps, int mode, float* mean, float* invstd,
+                 float* sums, float* dbeta, hipStream_t s);
+void sd_bn_apply(const float* pre, int Co, long long P, const float* mean, const float* invstd, const float* beta,
+                 float* act, hipStream_t s);
+void sd_bn_bwd_reduce(const float* dact, const float* pre, int Co, long long P, const float* mean, const float* invstd,
+                      const float* beta, double* part, hipStream_t s);
+void sd_bn_bwd_apply(const float* dact, const float* pre, int Co, long long P, const float* mean, const float* invstd,
+                     const float* beta, const float* sums, float* dpre, hipStream_t s);
+// mode 0: din = dgrad; mode 1: da[q*ldd+ci] += dgrad * s(1-s), s = sigmoid(src[q*lds+ci])
+void sd_conv_dgrad(const float* dpre, int Co, const float* W, int Ci, int H, int Wd, long long P, float* din, int ldd,
+                   const float* src, int lds, int mode, hipStream_t s);
+// dW [4,4,Ci,Co] (part: scratch of sd_wgrad_blocks(B,H) * 16*Ci*Co floats)
+void sd_conv_wgrad(const float* in, int ldi, int in_sig, int Ci, const float* dpre, int Co, int B, int H, int Wd,
+                   float* part, float* dW, hipStream_t s);
+void sd_head_fwd(const float* act, int Ci, const float* W5, const float* b5, float smax, const float* mle,
+                 const float* target, const float* noise, float reg, int B, int C, int HW, float* sd, float* sample,
+                 float* rec_part, int nblk, hipStream_t s);
+void sd_head_bwd(const float* act, int Ci, const float* W5, const float* b5, float smax, const float* mle,
+                 const float* target, const float* noise, float reg, float nll_coef, const float* dsample, int C,
+                 long long P, float* dmle, float* dact, float* part, float* dW5, float* db5, hipStream_t s);
+// sample = mle + scale * noise
+void chain_noise(const float* mle, const float* noise, float scale, long long n, float* sample, hipStream_t s);
+// improvement-loss seed: out = dxin + 2 coef ((x - xp) - (xn - x)) (null xp / xn / dxin: term absent)
+void imp_seed(const float* dxin, const float* xp, const float* x, const float* xn, float coef, long long n, float* out,
+              hipStream_t s);
+// out[b] = ||a_b - b_b||^2 per image
+void sqdiff_img(const float* a, const float* b, int B, long long per_img, float* out, hipStream_t s);

@@ -298,8 +298,9 @@ void splitfc_dz_reduce(const float* dz_part, int nblk, int B, int K, float* dz, 
 // (sequential_vae.py:1592-1594, :1023, :1156-1158)
 // ---------------------------------------------------------------------------
 __global__ void latent_fwd_kernel(const float* part, long long part_gs, int nsplit, int B, int Dz, LatentLvls lv,
-                                  long long bias_gs, float clipv, float prior, const float* eps, long long eps_gs,
-                                  float* mu, float* sig, float* z, long long ms_gs, float* kl_img, long long kl_gs) {
+                                  long long bias_gs, float clipv, float prior, int uniform, const float* eps,
+                                  long long eps_gs, float* mu, float* sig, float* z, long long ms_gs, float* kl_img,
+                                  long long kl_gs) {
   const int group = blockIdx.y;
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= B) return;
@@ -321,23 +322,24 @@ __global__ void latent_fwd_kernel(const float* part, long long part_gs, int nspl
       mu[o] = m;  // raw (pre-clip) mean; the clip mask is re-derived in latent_bwd
       sig[o] = sg;
       z[o] = mc + sg * eps[group * eps_gs + (long long)n * Dz + c];
-      kl += -0.5f - __logf(sg) + 0.5f * sg * sg / p2 + 0.5f * mc * mc / p2;
+      // use_uniform_prior: reduce_mean(-log sigma) (sequential_vae.py:1159-1160)
+      kl += uniform ? -__logf(sg) : -0.5f - __logf(sg) + 0.5f * sg * sg / p2 + 0.5f * mc * mc / p2;
     }
   }
   kl_img[group * kl_gs + n] = kl / Dz;
 }
 
 void latent_fwd(const float* part, long long part_gs, int nsplit, int B, int Dz, const LatentLvls& lv,
-                long long bias_gs, float clipv, float prior, const float* eps, long long eps_gs, float* mu, float* sig,
-                float* z, long long ms_gs, float* kl_img, long long kl_gs, int groups, hipStream_t s) {
+                long long bias_gs, float clipv, float prior, int uniform, const float* eps, long long eps_gs, float* mu,
+                float* sig, float* z, long long ms_gs, float* kl_img, long long kl_gs, int groups, hipStream_t s) {
   hipLaunchKernelGGL(latent_fwd_kernel, dim3((B + 127) / 128, groups), dim3(128), 0, s, part, part_gs, nsplit, B, Dz,
-                     lv, bias_gs, clipv, prior, eps, eps_gs, mu, sig, z, ms_gs, kl_img, kl_gs);
+                     lv, bias_gs, clipv, prior, uniform, eps, eps_gs, mu, sig, z, ms_gs, kl_img, kl_gs);
 }
 
 // dhead[n][d] = d(mu_raw), dhead[n][Dz+d] = d(sig pre-sigmoid); kl_coef = reg*c_first/B
 __global__ void latent_bwd_kernel(const float* mu, const float* sig, const float* eps, const float* dz, long long gs,
                                   long long eps_gs, int B, int Dz, const float* kl_coef, long long kc_gs, float prior,
-                                  float clipv, float* dhead, long long dh_gs) {
+                                  int uniform, float clipv, float* dhead, long long dh_gs) {
   const int group = blockIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B * Dz) return;
@@ -348,17 +350,17 @@ __global__ void latent_bwd_kernel(const float* mu, const float* sig, const float
   const float m = mu[o], sg = sig[o], g = dz[o];
   const bool pass = m >= -clipv && m <= clipv;
   const float mc = fminf(fmaxf(m, -clipv), clipv);
-  const float dmu = pass ? (g + kc * mc / p2) : 0.f;
-  const float dsig = g * eps[group * eps_gs + i] + kc * (-1.f / sg + sg / p2);
+  const float dmu = pass ? (uniform ? g : g + kc * mc / p2) : 0.f;
+  const float dsig = g * eps[group * eps_gs + i] + kc * (uniform ? -1.f / sg : -1.f / sg + sg / p2);
   dhead[group * dh_gs + (long long)n * 2 * Dz + c] = dmu;
   dhead[group * dh_gs + (long long)n * 2 * Dz + Dz + c] = dsig * sg * (1.f - sg);
 }
 
 void latent_bwd(const float* mu, const float* sig, const float* eps, const float* dz, long long gs, long long eps_gs,
-                int B, int Dz, const float* kl_coef, long long kc_gs, float prior, float clipv, float* dhead,
+                int B, int Dz, const float* kl_coef, long long kc_gs, float prior, int uniform, float clipv, float* dhead,
                 long long dh_gs, int groups, hipStream_t s) {
   hipLaunchKernelGGL(latent_bwd_kernel, dim3((B * Dz + 255) / 256, groups), dim3(256), 0, s, mu, sig, eps, dz, gs,
-                     eps_gs, B, Dz, kl_coef, kc_gs, prior, clipv, dhead, dh_gs);
+                     eps_gs, B, Dz, kl_coef, kc_gs, prior, uniform, clipv, dhead, dh_gs);
 }
 
 // heads backward for one level: dX (+)= dhead_l @ W^T ; dW = X^T dhead_l ; db = sum_n dhead_l

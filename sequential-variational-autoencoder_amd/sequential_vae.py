@@ -52,6 +52,17 @@ class SequentialVAE:
         self.ctx = h
         _lib.check(self.L.svae_bind(self.ctx, _lib.ptr(self.params), _lib.ptr(self.grads)), self.ctx)
         self._last_reg = 1.0
+        # Adam updates applied so far (the AdamOptimizer's step count behind beta1_power); with the
+        # improvement-maximisation loss two apply_gradients run per iteration (:1267, :1306)
+        self.adam_updates = 0
+        self.grads_imp = None
+        if cfg.add_improvement_maximization_loss:
+            with torch.cuda.device(self.device):
+                self.grads_imp = torch.zeros(self.n_total, dtype=torch.float32, device=self.device)
+            _lib.check(self.L.svae_bind_imp(self.ctx, _lib.ptr(self.grads_imp)), self.ctx)
+            pe = ctypes.c_int64()
+            _lib.check(self.L.svae_imp_range(self.ctx, ctypes.byref(pe)), self.ctx)
+            self.phi_end = int(pe.value)
 
     # ------------------------------------------------------------------ lifecycle
     def close(self):
@@ -73,9 +84,21 @@ class SequentialVAE:
             t = torch.as_tensor(np.asarray(a, dtype=np.float32), device=self.device)
         return t.contiguous()
 
-    def forward(self, x, target, eps=None, reg_coeff=1.0, stream=None):
-        """Forward of the unrolled chain.  eps [T,B,Dz] or None (device Philox)."""
+    def forward(self, x, target, eps=None, reg_coeff=1.0, stream=None, noise=None):
+        """Forward of the unrolled chain.  eps [T,B,Dz] or None (device Philox).  With
+        add_noise_to_chain, noise [T,B,H,W,C] is the N(0,1) of training_sample = mle + reg*sd*noise
+        (sequential_vae.py:1090), or None (device Philox)."""
         x, target = self._dev(x), self._dev(target)
+        nz = None
+        if self.cfg.add_noise_to_chain:
+            if noise is not None:
+                nz = self._dev(noise)
+                c = self.cfg
+                if tuple(nz.shape) != (c.mc_steps, c.batch, c.height, c.width, c.channels):
+                    raise ValueError("noise must be [T,B,H,W,C]")
+            _lib.check(self.L.svae_set_chain_noise(self.ctx, _lib.ptr(nz)), self.ctx)
+        elif noise is not None:
+            raise ValueError("noise given but add_noise_to_chain is off")
         exp = (self.cfg.batch, self.cfg.height, self.cfg.width, self.cfg.channels)
         if tuple(x.shape) != exp or tuple(target.shape) != exp:
             raise ValueError("input must be %s, got %s / %s" % (exp, tuple(x.shape), tuple(target.shape)))
@@ -84,7 +107,7 @@ class SequentialVAE:
             e = self._dev(eps)
             if tuple(e.shape) != (self.cfg.mc_steps, self.cfg.batch, self.cfg.latent_dim):
                 raise ValueError("eps must be [T,B,Dz]")
-        self._keep = (x, target, e)  # keep device inputs alive until backward
+        self._keep = (x, target, e, nz)  # keep device inputs alive until backward
         self._last_reg = float(reg_coeff)
         _lib.check(self.L.svae_forward(self.ctx, _lib.ptr(x), _lib.ptr(target), _lib.ptr(e), float(reg_coeff),
                                        _lib.stream_ptr(stream)), self.ctx)
@@ -129,6 +152,32 @@ class SequentialVAE:
         if self.overlap is not None:
             self.overlap.check()
 
+    def backward_imp(self, stream=None):
+        """d improvement_maximization_loss / d every variable into ``grads_imp``
+        (sequential_vae.py:1302-1303; the optimiser reads only the recognition part)."""
+        if self.grads_imp is None:
+            raise RuntimeError("add_improvement_maximization_loss is off")
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _lib.check(self.L.svae_backward_imp(self.ctx, _lib.stream_ptr(s)), self.ctx)
+        if self.grad_hook is not None:
+            self.grad_hook(self.grads_imp[:self.phi_end])
+
+    def apply_imp_gradients(self, lr=None, step=None, stream=None):
+        """clip + Adam of the recognition variables with ``grads_imp`` (:1304-1306)."""
+        lr = self.learning_rate if lr is None else lr
+        step = self.adam_updates if step is None else step
+        _lib.check(self.L.svae_adam_imp(self.ctx, float(lr), int(step), float(self.cfg.clip_grad_value),
+                                        _lib.stream_ptr(stream)), self.ctx)
+
+    def imp_loss_value(self, reg_coeff=None):
+        """``self.improvement_maximization_loss`` (:1189-1199) = sum_{t>=1} reg * coeff * -mean_b
+        ||mle_t - mle_{t-1}||^2."""
+        reg = self._last_reg if reg_coeff is None else reg_coeff
+        tot = 0.0
+        for t in range(1, self.cfg.mc_steps):
+            tot += float(self.copy_out(_lib.BUF_IMP_IMG, t, self.cfg.batch).double().mean())
+        return -reg * self.cfg.latent_pred_loss_coeff * tot
+
     def apply_gradients(self, lr=None, step=None, stream=None):
         lr = self.learning_rate if lr is None else lr
         step = self.iteration if step is None else step
@@ -168,6 +217,19 @@ class SequentialVAE:
             out += self._last_reg * c * self.cfg.kl_on(t) * self.copy_out(_lib.BUF_KL_IMG, t, B).double()
         return out
 
+    def sample(self, t=-1):
+        """training_samples[t] (:963): the MLE plus reg * stddevs * noise under add_noise_to_chain."""
+        t = t % self.cfg.mc_steps
+        c = self.cfg
+        return self.copy_out(_lib.BUF_SAMPLE, t, c.batch * c.height * c.width * c.channels).view(
+            c.batch, c.height, c.width, c.channels)
+
+    def stddevs(self, t=-1):
+        """Predicted stddevs [B,H,W,1] of step t (stddevs_prediction, :1866-1875)."""
+        t = t % self.cfg.mc_steps
+        c = self.cfg
+        return self.copy_out(_lib.BUF_STDDEV, t, c.batch * c.height * c.width).view(c.batch, c.height, c.width, 1)
+
     def xhat(self, t=-1):
         t = t % self.cfg.mc_steps
         c = self.cfg
@@ -202,15 +264,30 @@ class SequentialVAE:
         _lib.check(self.L.svae_bind(self.ctx, _lib.ptr(self.params), _lib.ptr(self.grads)), self.ctx)
 
     # ------------------------------------------------------------------ reference API
-    def train(self, input_batch, batch_target, eps=None):
+    def train(self, input_batch, batch_target, eps=None, noise=None):
         """One training update; returns the final-step reconstruction loss per pixel
-        (sequential_vae.py:1341-1375).  ``eps`` [T,B,Dz] (an extension for parity tests) replaces
-        the on-device N(0,1) draw of tf.random_normal (:1022)."""
+        (sequential_vae.py:1341-1375).  ``eps`` [T,B,Dz] and ``noise`` [T,B,H,W,C] (extensions for
+        parity tests) replace the on-device N(0,1) draws of tf.random_normal (:1022, :1090).
+
+        With the improvement-maximisation loss, train_op = tf.group(elbo_train_op,
+        pred_latent_train_op) (:1316): two apply_gradients of one AdamOptimizer, both on gradients of
+        the same forward.  TF leaves their order open; here the ELBO update (all variables, Adam step
+        2k-1) runs first and the improvement update (recognition variables, step 2k) second, sharing
+        the Adam moments, so beta1_power advances twice per iteration as in TF."""
         self.iteration += 1
         self.learning_rate *= self.cfg.learning_rate_decay
         reg = 1.0 - math.exp(-self.iteration / self.cfg.reg_coeff_rate)
-        self.forward(input_batch, batch_target, eps, reg)
-        self.backward_apply(self.learning_rate, self.iteration)
+        self.forward(input_batch, batch_target, eps, reg, noise=noise)
+        if self.grads_imp is None:
+            self.adam_updates += 1
+            self.backward_apply(self.learning_rate, self.adam_updates)
+        else:
+            self.backward()
+            self.backward_imp()
+            self.adam_updates += 1
+            self.apply_gradients(self.learning_rate, self.adam_updates)
+            self.adam_updates += 1
+            self.apply_imp_gradients(self.learning_rate, self.adam_updates)
         final = float(self.copy_out(_lib.BUF_STEP_STATS, self.cfg.mc_steps - 1, 2)[0])
         return final / self.data_dims[0] / self.data_dims[1]
 
@@ -242,10 +319,10 @@ class SequentialVAE:
                 out[p["name"] + "/Adam_1"] = V[a:b].reshape(p["shape"]).clone()
         # TF's AdamOptimizer starts beta{1,2}_power at beta{1,2} and multiplies after every update,
         # so after N updates it holds beta^(N+1) (tf.train.AdamOptimizer._create_slots / _finish)
-        out["beta1_power"] = torch.tensor(0.9 ** (self.iteration + 1), dtype=torch.float32)
-        out["beta2_power"] = torch.tensor(0.999 ** (self.iteration + 1), dtype=torch.float32)
+        out["beta1_power"] = torch.tensor(0.9 ** (self.adam_updates + 1), dtype=torch.float32)
+        out["beta2_power"] = torch.tensor(0.999 ** (self.adam_updates + 1), dtype=torch.float32)
         save_file(out, path, metadata={"iteration": str(self.iteration), "learning_rate": repr(self.learning_rate),
-                                       "config": self.name})
+                                       "adam_updates": str(self.adam_updates), "config": self.name})
 
     def load_checkpoint(self, path):
         """Restore save_checkpoint's state (init_network's restore, abstract_network.py:139-152);
@@ -272,14 +349,18 @@ class SequentialVAE:
         self._adam_state(M.to(self.device), V.to(self.device))
         self.params_updated()  # caller-written parameters: rebuild the engine's bf16 copies
         torch.cuda.synchronize(self.device)
+        per_it = 2 if self.grads_imp is not None else 1  # Adam updates per iteration
         if "iteration" in meta:
             self.iteration = int(meta["iteration"])
+            self.adam_updates = int(meta.get("adam_updates", per_it * self.iteration))
         elif "beta1_power" in keys:  # a TF-converted checkpoint: recover the Adam step from beta1^(N+1)
             with safe_open(path, framework="pt") as f:
                 b1p = float(f.get_tensor("beta1_power"))
-            self.iteration = max(0, int(round(math.log(b1p) / math.log(0.9))) - 1)
+            self.adam_updates = max(0, int(round(math.log(b1p) / math.log(0.9))) - 1)
+            self.iteration = self.adam_updates // per_it
         else:
             self.iteration = 0
+            self.adam_updates = 0
         self.learning_rate = float(meta.get("learning_rate", self.learning_rate))
 
     def generate(self, z=None, stream=None):

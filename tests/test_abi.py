@@ -83,3 +83,39 @@ def test_homog_layout_matches_oracle_sharing(built_lib):
         for p in table:
             assert (p["offset"] < n_live) == (not p["zero_grad"]), p["name"]
             assert p["offset"] + p["size"] <= n_total
+
+
+@pytest.mark.parametrize("preset", ["tiny", "celeba"])
+def test_stddev_network_layout_matches_oracle(built_lib, preset):
+    """predict_generator_noise adds stddevs_prediction's variables to every generator scope
+    (sequential_vae.py:1866-1875): the engine's table equals the oracle's, names and TF order."""
+    W, cfgmod = pkg_mod("weights"), pkg_mod("config")
+    cfg = cfgmod.preset(preset, add_noise_to_chain=True, predict_generator_noise=True)
+    table, n_total, n_live = W.param_table(cfg)
+    otab, _ = spec.build_params(spec.make_config(preset, add_noise_to_chain=True, predict_generator_noise=True))
+    key = lambda p: (p["name"], tuple(p["shape"]), p["dead"], p["zero_grad"], p["init"])
+    assert sorted(map(key, table)) == sorted(map(key, otab))
+    names = [p["name"] for p in table]
+    assert "theta/generative_step_0/Conv_5/weights" in names and "theta/generative_step_0/Conv_5/biases" in names
+    # homogeneous chain: the stddev network is shared like the rest of the generator (:1683-1687)
+    cfg = cfgmod.preset(preset, add_noise_to_chain=True, predict_generator_noise=True, share_theta_weights=True,
+                        share_phi_weights=True)
+    table, _, _ = W.param_table(cfg)
+    cd = spec.make_config(preset, add_noise_to_chain=True, predict_generator_noise=True)
+    ref = {p["name"]: tuple(p["shape"]) for p in spec.shared_table(cd, True, True)}
+    assert {p["name"]: tuple(p["shape"]) for p in table} == ref
+
+
+def test_chain_variant_configs_rejected(built_lib):
+    L = pkg_mod("_lib")
+    cfgmod = pkg_mod("config")
+    for over, msg in [(dict(predict_generator_noise=True), b"add_noise_to_chain"),
+                      (dict(add_noise_to_chain=True, predict_generator_noise=True,
+                            predict_generator_stddev_filter_sizes=(5, 9)), b"stddev_filter_sizes")]:
+        c = cfgmod.preset("tiny", **over).to_c()
+        n = ctypes.c_int64()
+        assert L.lib().svae_param_count(ctypes.byref(c), ctypes.byref(n), None, None) == -1
+        assert msg in L.lib().svae_last_error(None)
+    # noise_stddevs follow the reference list (sequential_vae.py:239), indexed by step
+    c = cfgmod.preset("tiny", add_noise_to_chain=True).to_c()
+    assert [c.noise_stddevs[t] for t in range(4)] == [0.5, 0.25, 0.125, 0.0]
