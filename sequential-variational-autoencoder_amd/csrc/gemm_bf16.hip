@@ -1207,6 +1207,13 @@ static HaloPlan halo_plan(const FwdArgs& a, int groups) {
       if (ks < 2) ks = 1;
     }
     p.ks = ks;
+    // a split of one chunk never prefetches a second window: one LDS buffer, so that three blocks
+    // (the register limit) instead of two fit a CU and hide each other's window-load latency
+    static const bool two_buf = [] {
+      const char* v = getenv("SVAE_HALO_1BUF");
+      return v && v[0] == '0';
+    }();
+    if (!two_buf && (nchunk + ks - 1) / ks <= 1) p.lds = (size_t)h.npix * ROWP * sizeof(__bf16);
     p.nrb = ks == 1 ? a.nclass * (a.rows / bm) : (int)(((long long)a.rows * a.nclass + SKR_ROWS - 1) / SKR_ROWS);
     if (bn == 32) p.kid = bm == 256 ? KID_HALO_256x32 : KID_HALO_128x32;
     else if (bn == 64) p.kid = bm == 128 ? KID_HALO_128x64 : KID_HALO_64x64;
@@ -1273,6 +1280,13 @@ int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit) {
   if (!halo_disabled()) {
     const HaloPlan hp = halo_plan(a, groups);
     if (hp.ok) {
+      if (hp.ks > 1) {  // grid split-K -> K split over the waves of one block where it fits
+        const int nrb = halo_kw_plan(a, groups);
+        if (nrb) {
+          if (ksplit) *ksplit = 1;
+          return nrb;
+        }
+      }
       if (ksplit) *ksplit = hp.ks;
       return hp.nrb;
     }
@@ -1294,14 +1308,15 @@ const char* kernel_name(int kid) {
       "igemm_halo_kernel<128, 64, 2, 2>", "igemm_halo_kernel<64, 64, 2, 2>",
       "igemm_halo_kernel<128, 128, 2, 2>", "igemm_halo_kernel<64, 128, 1, 4>",
       "wgrad_halo_kernel<32, 1>", "wgrad_halo_kernel<32, 2>", "wgrad_halo_kernel<64, 1>", "wgrad_halo_kernel<64, 2>",
-      "wgrad_halo2_kernel (stride-1 halo weight-GEMM, all instances)"};
+      "wgrad_halo2_kernel (stride-1 halo weight-GEMM, all instances)",
+      "igemm_halo_kw_kernel (small-image gather-GEMM, K split over waves, all instances)"};
   return (kid >= 0 && kid < KID_COUNT) ? names[kid] : "none";
 }
 
 int igemm_bf16_kid(const FwdArgs& a) {
   if (!halo_disabled()) {
     const HaloPlan hp = halo_plan(a, 1);
-    if (hp.ok) return hp.kid;
+    if (hp.ok) return (hp.ks > 1 && halo_kw_plan(a, 1)) ? KID_HALO_KW : hp.kid;
   }
   const int sc = (a.Cin % BKB) != 0;
   if (a.N <= 32) return KID_IGEMM_BF16_256x32 + sc;
@@ -1335,6 +1350,13 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
   if (path == 1 || (path == 2 && !halo_disabled())) {
     HaloPlan hp = halo_plan(a, groups);
     if (!hp.ok && path == 1) return -1;
+    if (hp.ok && hp.ks > 1 && path == 2) {  // K over the block's waves instead of the grid
+      const int nrb = halo_kw(a, groups, s);
+      if (nrb > 0) {
+        if (after) hipEventRecord(after, s);
+        return nrb;
+      }
+    }
     if (hp.ok) {
       a.ksplit = hp.ks;
       a.rows_total = a.rows * a.nclass;

@@ -1,0 +1,329 @@
+// Small-image halo gather-GEMM with the K dimension split over the block's waves (bf16 MFMA).
+//
+// The 8x8 and 4x4 layers of the ladders (CelebA: every level-2 conv / conv-T, the encoder's last
+// conv, and their input gradients) have only 8K or 2K output pixels per chain step.  Tiled like
+// the larger layers they give 128-256 blocks, so igemm_halo_kernel splits K over the grid and a
+// separate splitk_reduce pass sums fp32 partial slabs (up to 6 x 4 MB written, read back, one more
+// launch).  Here a block owns BM x 32 outputs and all of K: each of its four waves runs a quarter
+// of the taps of every 32-channel chunk (kernel row ky = wave; for stride-2 conv-T classes one tap
+// each) over the SAME staged input window, and the four partial tiles are summed in LDS in a fixed
+// wave order before one epilogue (bias / act / accumulate, forward BN statistics or the fused
+// backward-BN partials, exactly the splitk_reduce contract).  32-column tiles give >= 512 blocks.
+//
+// Window geometry, staging and A-fragment addressing follow igemm_halo_kernel (gemm_bf16.hip):
+//   CONV          iy = ry*s - pad + ky         window rows (R-1)*s + 4, dy = ky
+//   CONVT s=1     iy = ry + pad - ky           window rows R + 3,       dy = 3 - ky
+//   CONVT s=2     class (cy,cx), ky = k0+2*ty  window rows R + 1,       dy = 1 - ty
+#include <cstdlib>
+
+#include "common.h"
+#include "kernels.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+
+#define KW_CK 32   // channels per window stage
+#define KW_ROWP 40 // LDS pixel pitch in bf16 (80 B: conflict-free 16-B fragment reads)
+#define KW_PI 4    // window items (8 channels) per thread: npix * 4 <= 256 * KW_PI
+
+struct KwArgs {
+  FwdArgs f;
+  int Hr, Wr;   // row-space image dims (per parity class for conv-T stride 2)
+  int R, nimg;  // image rows per block (per image), images per block
+  int PR, PC;   // window dims per image
+  int sy;       // row-space -> input stride (conv stride, else 1)
+  int npix;     // nimg * PR * PC
+};
+
+namespace {
+
+__device__ __forceinline__ bf16x8 kw_cvt8(f32x4 a, f32x4 b) {
+  f32x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_convertvector(v, bf16x8);
+}
+
+__device__ __forceinline__ long long kw_out_row(const ConvGeom& g, int cls, int m) {
+  if (g.mode == GM_CONVT && g.stride == 2) {
+    const int qh = g.Ho >> 1, qw = g.Wo >> 1;
+    const int n = m / (qh * qw);
+    const int r = m - n * qh * qw;
+    const int qy = r / qw, qx = r - qy * qw;
+    return ((long long)n * g.Ho + 2 * qy + (cls >> 1)) * g.Wo + 2 * qx + (cls & 1);
+  }
+  return m;
+}
+
+template <int BM, bool S2T>
+__global__ __launch_bounds__(256, 2) void igemm_halo_kw_kernel(KwArgs h) {
+  constexpr int BN = 32;
+  constexpr int TM = BM / 32;
+  constexpr int NTAP = S2T ? 4 : 16;
+  constexpr int NTW = NTAP / 4;  // taps per wave (and B prefetch distance: one chunk ahead)
+  extern __shared__ __attribute__((aligned(16))) __bf16 ksm[];
+  const FwdArgs& a = h.f;
+  const ConvGeom& g = a.g;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const BlockXYZ blk = xcd_block();
+  const int group = blk.z / a.nclass, cls = blk.z - group * a.nclass;
+  const int m0 = blk.x * BM, n0 = blk.y * BN;
+  const float* A = a.A + group * a.a_gs;
+  const __bf16* Bw = (const __bf16*)a.Bh + group * a.b_gs;
+  const int nchunk = a.Cin / KW_CK;
+
+  // ---- window origin and tap geometry (uniform; igemm_halo_kernel's) ----
+  const int per_img = h.Hr * h.Wr;
+  const int img0 = m0 / per_img;
+  const int ry0 = (m0 - img0 * per_img) / h.Wr;
+  int oy_min, ox_min, tap0, toff0, tsgn;
+  if (S2T) {
+    const int cy = cls >> 1, cx = cls & 1;
+    const int ky0 = (cy + g.pad) & 1, kx0 = (cx + g.pad) & 1;
+    oy_min = (cy + g.pad - ky0) / 2 - 1;
+    ox_min = (cx + g.pad - kx0) / 2 - 1;
+    tap0 = ky0 * 4 + kx0;
+    toff0 = h.PC + 1;
+    tsgn = -1;
+  } else if (g.mode == GM_CONV) {
+    oy_min = ox_min = -g.pad;
+    tap0 = 0;
+    toff0 = 0;
+    tsgn = 1;
+  } else {
+    oy_min = ox_min = g.pad - 3;
+    tap0 = 0;
+    toff0 = 3 * h.PC + 3;
+    tsgn = -1;
+  }
+  const int iy_base = ry0 * h.sy + oy_min;
+
+  int woff[KW_PI];
+#pragma unroll
+  for (int i = 0; i < KW_PI; ++i) {
+    const int it = tid + 256 * i;
+    woff[i] = -2;  // -2: no item, -1: zero (outside the image)
+    if (it < h.npix * 4) {
+      const int pix = it >> 2, part = it & 3;
+      const int il = pix / (h.PR * h.PC);
+      const int r2 = pix - il * h.PR * h.PC;
+      const int pr = r2 / h.PC, pc = r2 - pr * h.PC;
+      const int iy = iy_base + pr, ix = ox_min + pc;
+      woff[i] = (iy >= 0 && iy < g.Hi && ix >= 0 && ix < g.Wi)
+                    ? (((img0 + il) * g.Hi + iy) * g.Wi + ix) * a.lda + part * 8
+                    : -1;
+    }
+  }
+  f32x4 wv[KW_PI][2];
+  auto load_window = [&](int chunk) {
+    const float* Ac = A + chunk * KW_CK;
+#pragma unroll
+    for (int i = 0; i < KW_PI; ++i) {
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      wv[i][0] = z;
+      wv[i][1] = z;
+      if (woff[i] >= 0) {
+        wv[i][0] = *(const f32x4*)(Ac + woff[i]);
+        wv[i][1] = *(const f32x4*)(Ac + woff[i] + 4);
+      }
+    }
+  };
+  auto store_window = [&](int buf) {
+    __bf16* W = ksm + buf * h.npix * KW_ROWP;
+#pragma unroll
+    for (int i = 0; i < KW_PI; ++i) {
+      const int it = tid + 256 * i;
+      if (woff[i] >= -1) *(bf16x8*)&W[(it >> 2) * KW_ROWP + (it & 3) * 8] = kw_cvt8(wv[i][0], wv[i][1]);
+    }
+  };
+
+  // ---- A fragment bases: the whole BM-row tile, every wave ----
+  int abase[TM];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const int ml = tm * 32 + l32;
+    const int rows_img = h.R * h.Wr;
+    const int il = ml / rows_img;
+    const int rem = ml - il * rows_img;
+    const int ryl = rem / h.Wr, rx = rem - ryl * h.Wr;
+    abase[tm] = ((il * h.PR + ryl * h.sy) * h.PC + rx * h.sy) * KW_ROWP + 8 * hh;
+  }
+
+  // ---- this wave's taps: t = wave * NTW + u; B fragments one chunk ahead ----
+  const __bf16* bptr = Bw + (long long)(n0 + l32) * a.ldb + 8 * hh;
+  bf16x8 bq[NTW][2];
+  auto load_b = [&](int u, int chunk) {
+    const int t = wave * NTW + u;
+    const int tap = S2T ? tap0 + 8 * (t >> 1) + 2 * (t & 1) : t;
+    const long long off = (long long)tap * a.b_tap + chunk * KW_CK;
+#pragma unroll
+    for (int kq = 0; kq < 2; ++kq) bq[u][kq] = *(const bf16x8*)(bptr + off + kq * 16);
+  };
+
+  f32x16 acc[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+
+  load_window(0);
+#pragma unroll
+  for (int u = 0; u < NTW; ++u) load_b(u, 0);
+  store_window(0);
+  __syncthreads();
+  for (int c = 0; c < nchunk; ++c) {
+    const int buf = c & 1;
+    const bool has_next = c + 1 < nchunk;
+    if (has_next) load_window(c + 1);
+    const __bf16* W = ksm + buf * h.npix * KW_ROWP;
+#pragma unroll
+    for (int u = 0; u < NTW; ++u) {
+      const int t = wave * NTW + u;
+      const int shift = S2T ? toff0 + tsgn * ((t >> 1) * h.PC + (t & 1)) : toff0 + tsgn * ((t >> 2) * h.PC + (t & 3));
+      const int sh = shift * KW_ROWP;
+#pragma unroll
+      for (int kq = 0; kq < 2; ++kq) {
+        bf16x8 af[TM];
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) af[tm] = *(const bf16x8*)&W[abase[tm] + sh + kq * 16];
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+          acc[tm] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm], bq[u][kq], acc[tm], 0, 0, 0);
+      }
+      if (has_next) load_b(u, c + 1);
+    }
+    if (has_next) store_window(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- sum the four waves' partial tiles in LDS (fixed order), then one epilogue ----
+  float* red = (float*)ksm;  // [4][BM][BN]
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      red[(wave * BM + m) * BN + l32] = acc[tm][r];
+    }
+  __syncthreads();
+  const int col = tid & 31, rg = tid >> 5;  // 8 row groups
+  const int n = n0 + col;
+  float* Cp = a.C + group * a.c_gs;
+  const float* bias = a.bias ? a.bias + group * a.bias_gs : nullptr;
+  const bool bwm = a.bw.pre != nullptr;
+  const bool bwc = bwm && n < a.bw.C;
+  float bm = 0.f, bi = 0.f, bb = 0.f;
+  if (bwc) {
+    bm = a.bw.mean[group * a.bw.ms_gs + n];
+    bi = a.bw.invstd[group * a.bw.ms_gs + n];
+    bb = a.bw.y ? 0.f : a.bw.beta[group * a.bw.beta_gs + n];
+  }
+  float s1 = 0.f, s2 = 0.f;
+  for (int m = rg; m < BM; m += 8) {
+    float v = red[(0 * BM + m) * BN + col];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) v += red[(w * BM + m) * BN + col];
+    if (!bwm) {
+      s1 += v;
+      s2 += v * v;
+    }
+    if (bias) v += bias[n];
+    v = act_f(v, a.act);
+    const long long orow = kw_out_row(g, cls, m0 + m);
+    float* dst = Cp + orow * a.ldc + n;
+    if (a.accumulate) v += *dst;
+    *dst = v;
+    if (bwc)
+      bw_term(v, a.bw.pre[group * a.bw.pre_gs + orow * a.bw.ldp + n], bm, bi, bb,
+              a.bw.y ? a.bw.y + group * a.bw.y_gs + orow * a.bw.ldy + n : nullptr, a.bw.act, s1, s2);
+  }
+  if (!a.stats) return;
+  __syncthreads();  // every wave is done reading red
+  red[tid] = s1;
+  red[256 + tid] = s2;
+  __syncthreads();
+  if (tid < BN) {
+    const int SC = bwm ? a.bw.C : a.N;  // stats columns (row-block stride 2*SC)
+    if (n0 + tid < SC) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s += red[j * 32 + tid];
+        q += red[256 + j * 32 + tid];
+      }
+      const int rb = cls * gridDim.x + blk.x;
+      stat_put(a.stats + (rb & (a.s_nsh - 1)) * a.s_sh + group * a.s_gs, n0 + tid, s, q);
+    }
+  }
+}
+
+}  // namespace
+
+// ---- planner: eligible shapes, BM, window geometry, LDS, stats row-blocks ----
+static bool kw_plan(const FwdArgs& a, int groups, KwArgs* out, int* bm_out, size_t* lds_out) {
+  const ConvGeom& g = a.g;
+  if (g.mode == GM_DENSE || g.ksz != 4 || g.pad != 1 || !a.Bh || a.Cin % KW_CK != 0 || a.N % 32 != 0) return false;
+  const bool s2t = g.mode == GM_CONVT && g.stride == 2;
+  if (g.mode == GM_CONVT && g.stride > 2) return false;
+  const int Hr = s2t ? g.Ho / 2 : g.Ho, Wr = s2t ? g.Wo / 2 : g.Wo;
+  const int sy = g.mode == GM_CONV ? g.stride : 1;
+  const int span = s2t ? 2 : 4;
+  const int per_img = Hr * Wr;
+  for (int bm : {64, 32}) {
+    if (bm % Wr != 0 || a.rows % bm != 0) continue;
+    if (!(per_img % bm == 0 || bm % per_img == 0)) continue;
+    KwArgs h;
+    h.Hr = Hr;
+    h.Wr = Wr;
+    h.R = bm >= per_img ? Hr : bm / Wr;
+    h.nimg = bm >= per_img ? bm / per_img : 1;
+    h.sy = sy;
+    h.PR = (h.R - 1) * sy + span;
+    h.PC = (Wr - 1) * sy + span;
+    h.npix = h.nimg * h.PR * h.PC;
+    if (h.npix * 4 > 256 * KW_PI) continue;
+    const long long blocks = (long long)(a.rows / bm) * (a.N / 32) * a.nclass * groups;
+    if (blocks < 256 && bm == 64) continue;  // the 32-row tile doubles the blocks
+    *out = h;
+    *bm_out = bm;
+    *lds_out = std::max((size_t)(2 * h.npix) * KW_ROWP * sizeof(__bf16), (size_t)4 * bm * 32 * sizeof(float));
+    return true;
+  }
+  return false;
+}
+
+static bool kw_disabled() {
+  static const bool v = [] {
+    const char* e = getenv("SVAE_NO_KW");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
+int halo_kw_plan(const FwdArgs& a, int groups) {
+  if (kw_disabled()) return 0;
+  KwArgs h;
+  int bm;
+  size_t lds;
+  if (!kw_plan(a, groups, &h, &bm, &lds)) return 0;
+  return a.nclass * (a.rows / bm);
+}
+
+int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
+  KwArgs h;
+  int bm;
+  size_t lds;
+  if (kw_disabled() || !kw_plan(a, groups, &h, &bm, &lds)) return -1;
+  h.f = a;
+  const bool s2t = a.g.mode == GM_CONVT && a.g.stride == 2;
+  dim3 grid(a.rows / bm, a.N / 32, groups * a.nclass);
+  if (bm == 64) {
+    if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<64, true>), grid, dim3(256), lds, s, h);
+    else hipLaunchKernelGGL((igemm_halo_kw_kernel<64, false>), grid, dim3(256), lds, s, h);
+  } else {
+    if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<32, true>), grid, dim3(256), lds, s, h);
+    else hipLaunchKernelGGL((igemm_halo_kw_kernel<32, false>), grid, dim3(256), lds, s, h);
+  }
+  return a.nclass * (a.rows / bm);
+}

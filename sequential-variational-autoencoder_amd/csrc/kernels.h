@@ -72,7 +72,8 @@ enum KernelId {
   KID_HALO_128x128 = 20, KID_HALO_64x128 = 21,
   KID_WHALO_32_S1 = 22, KID_WHALO_32_S2 = 23, KID_WHALO_64_S1 = 24, KID_WHALO_64_S2 = 25,
   KID_WHALO2_S1 = 26,  // wgrad_halo2_kernel<...> (all instances: stride-1 halo weight-GEMM, wgrad_halo2.hip)
-  KID_COUNT = 27
+  KID_HALO_KW = 27,    // igemm_halo_kw_kernel<...> (all instances: small-image gather, K over waves, halo_kw.hip)
+  KID_COUNT = 28
 };
 const char* kernel_name(int kid);
 int igemm_bf16_kid(const FwdArgs& a);
@@ -83,6 +84,10 @@ int igemm_bf16(FwdArgs a, int groups, hipStream_t s, hipEvent_t after = nullptr)
 // qualify), 2 = automatic (halo when it qualifies, unless SVAE_NO_HALO=1)
 int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t after = nullptr);
 int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit);
+// small-image halo gather-GEMM with K split over the block's waves (halo_kw.hip), used where the
+// tiled halo kernel would split K over the grid: stats row-blocks (0 = shape not eligible) / launch
+int halo_kw_plan(const FwdArgs& a, int groups);
+int halo_kw(const FwdArgs& a, int groups, hipStream_t s);
 void wgrad_bf16(WgArgs a, int groups, hipStream_t s, hipEvent_t after = nullptr);  // taps merged into M (part [split][tap*M+m][n])
 int wgrad_bf16_tiles(const WgArgs& a);
 // halo weight-GEMM (csrc/gemm_bf16.hip): plan (0 = shape does not qualify) and launch.  The caller

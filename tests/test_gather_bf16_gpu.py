@@ -30,6 +30,9 @@ SHAPES = [
     (4, 64, 3, 32, 2, 0), (2, 32, 3, 32, 2, 0), (2, 64, 4, 64, 2, 0), (2, 32, 1, 128, 2, 0),
     # small-N conv-T gathers (convt_smalln_kernel on path 2): 2 channel chunks, N = 16 / 1, Wi = 16 / 64
     (2, 16, 64, 16, 2, 1), (2, 32, 32, 1, 2, 1), (1, 64, 32, 4, 2, 1),
+    # CelebA B=128 small-image layers: path 2 runs them on the wave-split kernel (csrc/halo_kw.hip)
+    # with 64-row tiles instead of grid split-K
+    (128, 8, 256, 128, 1, 1), (128, 4, 384, 128, 2, 1), (128, 8, 128, 128, 1, 0), (128, 8, 128, 64, 2, 1),
 ]
 
 
