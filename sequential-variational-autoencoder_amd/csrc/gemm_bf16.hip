@@ -1241,6 +1241,20 @@ static void launch_halo(const HaloArgs& h, int groups, size_t lds, hipStream_t s
     hipLaunchKernelGGL((igemm_halo_kernel<BM, BN, WM, WN, false>), grid, dim3(256), lds, s, h);
 }
 
+// the wave-split kernel (halo_kw.hip) is tried first where the tiled halo kernel would split K over
+// the grid, and on every layer with >= 2 channel chunks: 32-column tiles, four waves over the taps
+// (tools/bench_gather.py: 16x16 layers 39->27 / 24->18 us, 8x8 s2 conv-T 20->15; the one-chunk
+// 32x32 layers stay on the tiled kernel, where the wave split was 3-7 % slower)
+static bool kw_first(const FwdArgs& a, const HaloPlan& hp) {
+  static const int mode = [] {  // SVAE_KW: 0 = only instead of split-K, 2 = wherever it fits
+    const char* v = getenv("SVAE_KW");
+    return v ? atoi(v) : 1;
+  }();
+  if (hp.ks > 1) return true;
+  if (mode == 2) return true;
+  return mode == 1 && a.Cin >= 2 * HALO_CK;
+}
+
 static int halo_disabled() {
   static int v = -1;
   if (v < 0) {
@@ -1280,7 +1294,7 @@ int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit) {
   if (!halo_disabled()) {
     const HaloPlan hp = halo_plan(a, groups);
     if (hp.ok) {
-      if (hp.ks > 1) {  // grid split-K -> K split over the waves of one block where it fits
+      if (kw_first(a, hp)) {  // K split over the waves of one block where it fits
         const int nrb = halo_kw_plan(a, groups);
         if (nrb) {
           if (ksplit) *ksplit = 1;
@@ -1316,7 +1330,7 @@ const char* kernel_name(int kid) {
 int igemm_bf16_kid(const FwdArgs& a) {
   if (!halo_disabled()) {
     const HaloPlan hp = halo_plan(a, 1);
-    if (hp.ok) return (hp.ks > 1 && halo_kw_plan(a, 1)) ? KID_HALO_KW : hp.kid;
+    if (hp.ok) return (kw_first(a, hp) && halo_kw_plan(a, 1)) ? KID_HALO_KW : hp.kid;
   }
   const int sc = (a.Cin % BKB) != 0;
   if (a.N <= 32) return KID_IGEMM_BF16_256x32 + sc;
@@ -1350,7 +1364,7 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
   if (path == 1 || (path == 2 && !halo_disabled())) {
     HaloPlan hp = halo_plan(a, groups);
     if (!hp.ok && path == 1) return -1;
-    if (hp.ok && hp.ks > 1 && path == 2) {  // K over the block's waves instead of the grid
+    if (hp.ok && path == 2 && kw_first(a, hp)) {  // K over the block's waves
       const int nrb = halo_kw(a, groups, s);
       if (nrb > 0) {
         if (after) hipEventRecord(after, s);
