@@ -9,6 +9,8 @@
 #include "common.h"
 #include "kernels.h"
 
+typedef __bf16 bf16x4_bn __attribute__((ext_vector_type(4)));
+
 // BN output before the activation, per element through common.h bn_y1 (one expression shared
 // by every kernel that needs it, so the backward's act' sign is bitwise the forward's)
 __device__ __forceinline__ f32x4 bn_y(f32x4 x, f32x4 m, f32x4 is, f32x4 b) {
@@ -231,7 +233,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     long long pre_gs, long long rows, int C, const float* mean, const float* invstd, long long ms_gs,
     const float* beta, long long beta_gs, const u64* acc, long long acc_gs, long long sh, int nsh, float* dbeta,
     long long dbeta_gs, int act,
-    float* dpre, int lddp, long long dpre_gs, float* dres, int ldres, long long dres_gs, int res_acc, int rpb) {
+    float* dpre, int lddp, long long dpre_gs, float* dres, int ldres, long long dres_gs, int res_acc, int rpb,
+    int dpre_bf16) {
   __shared__ __attribute__((aligned(16))) float sm[2][AP_QB * 4];
   __shared__ u64 tot[4 * AP_QB * 4];
   const int group = blockIdx.z;
@@ -258,7 +261,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   dy += group * dy_gs;
   if (y) y += group * y_gs;
   pre += group * pre_gs;
-  dpre += group * dpre_gs;
   if (dres) dres += group * dres_gs;
   const f32x4 m = *(const f32x4*)(mean + group * ms_gs + c), is = *(const f32x4*)(invstd + group * ms_gs + c);
   const f32x4 bb = y ? f32x4{0.f, 0.f, 0.f, 0.f} : *(const f32x4*)(beta + group * beta_gs + c);
@@ -274,7 +276,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     f32x4 dz;
 #pragma unroll
     for (int e = 0; e < 4; ++e) dz[e] = g[e] * dact_from_y(yy[e], act);
-    *(f32x4*)(dpre + r * lddp + c) = is * (dz - a - xh * b);
+    const f32x4 dp = is * (dz - a - xh * b);
+    const long long o = group * dpre_gs + r * lddp + c;
+    if (dpre_bf16)  // consumed only by bf16 GEMMs, which round it the same way while staging
+      *(bf16x4_bn*)((__bf16*)dpre + o) = __builtin_convertvector(dp, bf16x4_bn);
+    else
+      *(f32x4*)(dpre + o) = dp;
     if (dres) {
       f32x4* d = (f32x4*)(dres + r * ldres + c);
       *d = res_acc ? *d + dz : dz;
@@ -287,9 +294,9 @@ void bn_bwd_apply(const float* dy, int lddy, long long dy_gs, const float* y, in
                   const float* invstd, long long ms_gs, const float* beta, long long beta_gs, const u64* acc,
                   long long acc_gs, long long sh, int nsh, float* dbeta, long long dbeta_gs, int act, float* dpre, int lddp,
                   long long dpre_gs, float* dres, int ldres, long long dres_gs, int res_acc, int groups,
-                  hipStream_t s) {
+                  hipStream_t s, int dpre_bf16) {
   const ApGrid g = ap_grid(rows, C, groups);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, g.grid, dim3(256), 0, s, dy, lddy, dy_gs, y, ldy, y_gs, pre, ldp, pre_gs,
                      rows, C, mean, invstd, ms_gs, beta, beta_gs, acc, acc_gs, sh, nsh, dbeta, dbeta_gs, act, dpre, lddp,
-                     dpre_gs, dres, ldres, dres_gs, res_acc, g.rpb);
+                     dpre_gs, dres, ldres, dres_gs, res_acc, g.rpb, dpre_bf16);
 }

@@ -448,6 +448,12 @@ struct svae_ctx {
   hipStream_t st2 = nullptr;
   hipStream_t st3 = nullptr;  // split-latent FCs (fwd up front, bwd per level): no weight-GEMM queue ahead
   hipEvent_t ev_dz = nullptr, ev_j3 = nullptr;
+  // recognition backward overlapped with the chain backward: groups of rec_group steps on st4 as soon
+  // as their dz_t are final (0 = one batched launch per layer after the chain)
+  hipStream_t st4 = nullptr;
+  hipEvent_t ev_j4 = nullptr;
+  float* slab4 = nullptr;
+  int rec_group = 0;
   float* slab2 = nullptr;
   float* dpre_ring[NR] = {};
   float* idpre_ring[2] = {};
@@ -536,6 +542,9 @@ struct svae_ctx {
   double* sd_part = nullptr;
   float *dseed = nullptr, *imp_img = nullptr, *kl_zero = nullptr;
   bool imp_pass = false;             // svae_backward_imp: seeds from the improvement loss only
+  // bf16 mode: BN-backward outputs (dpre) stored as bf16 -- their only consumers, the dgrad and
+  // wgrad GEMMs, round them identically while staging (opload.h)
+  int dbf = 0;
   float* Gimp_pub = nullptr;         // caller's improvement-loss gradient (svae_bind_imp)
   float* Gimp_v = nullptr;           // its virtual copy under weight sharing
   // BN statistics: fixed-point column accumulators (common.h stat_put), one region per BN
@@ -806,6 +815,13 @@ static void choose_split(long long rows, int taps, int tiles, int groups, long l
   chunk = (int)ch;
 }
 
+// dpre of layer L is stored as bf16 (bf16 mode) unless its input gradient takes the fp32 small-N
+// gather (image-channel conv whose Cout is not a multiple of 32: tiny test geometries)
+static int dpre_bf(const svae_ctx* c, const ConvL& L) {
+  if (!c->dbf) return 0;
+  return (L.cin % 4 != 0 && !(L.cout % 32 == 0 && !L.tr)) ? 0 : 1;
+}
+
 // weight gradient of a conv/convT layer: dpre = grad wrt pre-BN output, in = layer input
 static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, View in, const float* dpre,
                       long long dpre_gs, float* dW) {
@@ -821,6 +837,7 @@ static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, V
     // dW[tap][ci][co] = sum_{p out} x[src(p,tap)][ci] * dpre[p][co]
     w.G = in.p; w.g_gs = in.gs; w.ldg = in.ld;
     w.D = dpre; w.d_gs = dpre_gs; w.ldd = L.cout;
+    w.d_bf16 = dpre_bf(c, L);
     w.M = L.cin; w.N = L.cout;
     w.g.Hi = w.g.Wi = L.hin;
     w.g.Ho = w.g.Wo = L.hout;
@@ -828,6 +845,7 @@ static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, V
   } else {
     // dW[tap][co][ci] = sum_{p in} dpre[src(p,tap)][co] * x[p][ci]
     w.G = dpre; w.g_gs = dpre_gs; w.ldg = L.cout;
+    w.g_bf16 = dpre_bf(c, L);
     w.D = in.p; w.d_gs = in.gs; w.ldd = in.ld;
     w.M = L.cout; w.N = L.cin;
     w.g.Hi = w.g.Wi = L.hout;
@@ -918,7 +936,7 @@ static int conv_dgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, c
   if (L.cin % 4 != 0 && c->m.g.bf16 && L.cout % 32 == 0 && !L.tr) {
     // layer-0 conv input gradient (N = image channels): bf16 halo gather (CONVT mode from dpre)
     FwdArgs a{};
-    a.A = dpre; a.a_gs = dpre_gs; a.lda = L.cout;
+    a.A = dpre; a.a_gs = dpre_gs; a.lda = L.cout; a.a_bf16 = dpre_bf(c, L);
     a.Bh = shadowN(c, L.ow); a.b_nk = 1; a.ldb = L.cout; a.b_tap = (long long)L.cin * L.cout; a.b_gs = w_gs;
     a.C = din.p; a.c_gs = din.gs; a.ldc = din.ld;
     a.N = L.cin; a.Cin = L.cout;
@@ -938,7 +956,7 @@ static int conv_dgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, c
     return 0;
   }
   FwdArgs a{};
-  a.A = dpre; a.a_gs = dpre_gs; a.lda = L.cout;
+  a.A = dpre; a.a_gs = dpre_gs; a.lda = L.cout; a.a_bf16 = dpre_bf(c, L);
   a.B = W; a.b_gs = w_gs; a.b_tap = (long long)L.cin * L.cout;
   a.C = din.p; a.c_gs = din.gs; a.ldc = din.ld;
   a.N = L.cin; a.Cin = L.cout;
@@ -981,7 +999,7 @@ static int conv_dgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, c
 // BN(+act) backward: dy (grad wrt post-act out y) -> dpre; dbeta into grads; optional dres
 static int bn_act_bwd(svae_ctx* c, int groups, long long rows, int C, View dy, View y, const float* pre, long long pre_gs,
                       int ldp, BNS bn, long long bn_gs, long long beta_off, long long w_gs, int act, float* dpre,
-                      long long dpre_gs, View dres, int res_acc, const BwFuse* fu = nullptr) {
+                      long long dpre_gs, View dres, int res_acc, const BwFuse* fu = nullptr, int dpre_bf16 = 0) {
   const bool pre_reduced = fu && fu->used;  // sums already added by the fused dgrad epilogue
   const AccR acc = pre_reduced ? fu->acc : acc_bn(c, groups, C, bn_bwd_rowblocks(rows));
   if (!acc.p) return fail(c, SVAE_EBADARG, "BN accumulator arena too small");
@@ -993,7 +1011,7 @@ static int bn_act_bwd(svae_ctx* c, int groups, long long rows, int C, View dy, V
                   act, acc.p, acc.gs, acc.sh, acc.nsh, groups, c->st);
   bn_bwd_apply(dy.p, dy.ld, dy.gs, yp, y.ld, y.gs, pre, ldp, pre_gs, rows, C, bn.mean, bn.invstd, bn_gs, beta, w_gs,
                acc.p, acc.gs, acc.sh, acc.nsh, c->Gr + beta_off, w_gs, act, dpre, C, dpre_gs, dres.p, dres.ld, dres.gs, res_acc, groups,
-               c->st);
+               c->st, dpre_bf16);
   return 0;
 }
 
@@ -1024,11 +1042,12 @@ static int fc_bn_fwd(svae_ctx* c, const FcL& f, View in, float* pre, BNS bn, Vie
 static int fc_bn_bwd(svae_ctx* c, const FcL& f, View in, View dy, View y, const float* pre, BNS bn, View din) {
   const int B = c->m.g.B;
   const Slot sl = dpre_next(c);
-  int r = bn_act_bwd(c, 1, B, f.nout, dy, y, pre, 0, f.nout, bn, 0, f.obeta, 0, ACT_LRELU, sl.p, 0, View{}, 0);
+  int r = bn_act_bwd(c, 1, B, f.nout, dy, y, pre, 0, f.nout, bn, 0, f.obeta, 0, ACT_LRELU, sl.p, 0, View{}, 0, nullptr,
+                     c->dbf);
   if (r) return r;
   WgArgs w{};
   w.G = in.p; w.ldg = in.ld;
-  w.D = sl.p; w.ldd = f.nout;
+  w.D = sl.p; w.ldd = f.nout; w.d_bf16 = c->dbf;
   w.M = f.nin; w.N = f.nout;
   w.g.mode = GM_DENSE; w.g.nimg = B; w.g.ksz = 1; w.g.stride = 1;
   w.ntap = 1;
@@ -1042,7 +1061,7 @@ static int fc_bn_bwd(svae_ctx* c, const FcL& f, View in, View dy, View y, const 
   });
   if (din.p) {
     FwdArgs a{};
-    a.A = sl.p; a.lda = f.nout;
+    a.A = sl.p; a.lda = f.nout; a.a_bf16 = c->dbf;
     a.B = c->P + f.ow; a.b_nk = 1; a.ldb = f.nout; a.b_tap = 0;
     a.C = din.p; a.ldc = din.ld;
     a.N = f.nin; a.Cin = f.nout;
@@ -1419,7 +1438,8 @@ static int inference_bwd(svae_ctx* c, int t0, int n, View in0, float* dx0) {
     if (lvl == L - 2) heads_of(lvl);
     Slot sb = idpre_next(c);
     r = bn_act_bwd(c, n, rows, Fl, View{c->idb, Fl, gs}, View{act_b(lvl), Fl, gs}, pre_b(lvl), gs, Fl,
-                   bns(c->inf_bn_b[lvl], Fl), Fl, I0.b[lvl].obeta, wg, ACT_LRELU, sb.p, gs, View{}, 0, &fu_ib);
+                   bns(c->inf_bn_b[lvl], Fl), Fl, I0.b[lvl].obeta, wg, ACT_LRELU, sb.p, gs, View{}, 0, &fu_ib,
+                   dpre_bf(c, I0.b[lvl]));
     if (r) return r;
     r = on_side(c, sb.ready, sb.freed, [&] {
       return conv_wgrad(c, I0.b[lvl], n, wg, View{act_a(lvl), Fl, gs}, sb.p, gs, c->Gr + I0.b[lvl].ow);
@@ -1431,7 +1451,8 @@ static int inference_bwd(svae_ctx* c, int t0, int n, View in0, float* dx0) {
     if (r) return r;
     Slot sa = idpre_next(c);
     r = bn_act_bwd(c, n, rows, Fl, View{c->ida, Fl, gs}, View{act_a(lvl), Fl, gs}, pre_a(lvl), gs, Fl,
-                   bns(c->inf_bn_a[lvl], Fl), Fl, I0.a[lvl].obeta, wg, ACT_LRELU, sa.p, gs, View{}, 0, &fu_ia);
+                   bns(c->inf_bn_a[lvl], Fl), Fl, I0.a[lvl].obeta, wg, ACT_LRELU, sa.p, gs, View{}, 0, &fu_ia,
+                   dpre_bf(c, I0.a[lvl]));
     if (r) return r;
     View in = lvl == 0 ? in0 : View{act_b(lvl - 1), F[lvl], c->inf_gs[lvl - 1]};
     r = on_side(c, sa.ready, sa.freed, [&] { return conv_wgrad(c, I0.a[lvl], n, wg, in, sa.p, gs, c->Gr + I0.a[lvl].ow); });
@@ -1464,6 +1485,11 @@ static int engine_backward(svae_ctx* c) {
 
   if ((r = acc_reset(c))) return r;
   HIPCHK(c, hipMemsetAsync(c->dz, 0, (size_t)T * B * g.Dz * sizeof(float), st));
+  const bool rec_ov = c->side && c->st4 && c->rec_group > 0 && !g.plc;
+  if (rec_ov) {  // st4 starts after the forward and the accumulator / dz zeroing
+    hipEventRecord(c->ev_start, st);
+    hipStreamWaitEvent(c->st4, c->ev_start, 0);
+  }
   if (c->side) {  // the side stream starts after the forward (and anything before it)
     hipEventRecord(c->ev_start, st);
     hipStreamWaitEvent(c->st2, c->ev_start, 0);
@@ -1568,7 +1594,7 @@ static int engine_backward(svae_ctx* c) {
       // s1: relu(BN(convT_s1(cat)))
       Slot sl = dpre_next(c);
       r = bn_act_bwd(c, 1, rows, Fl, View{dcur, Fl, 0}, View{s.s1_act[lvl], Fl, 0}, s.s1_pre[lvl], 0, Fl, s.s1_bn[lvl],
-                     0, l1.obeta, 0, ACT_RELU, sl.p, 0, View{}, 0, &fu_s1);
+                     0, l1.obeta, 0, ACT_RELU, sl.p, 0, View{}, 0, &fu_s1, dpre_bf(c, l1));
       if (r) return r;
       if (t == c->dbg_stop_step && lvl == c->dbg_stop_lvl2) { c->dbg_last = dcur; return 0; }
       r = on_side(c, sl.ready, sl.freed,
@@ -1609,7 +1635,7 @@ static int engine_backward(svae_ctx* c) {
       View dres = t >= 1 ? View{c->denc[lvl], Fl, 0} : View{};
       sl = dpre_next(c);
       r = bn_act_bwd(c, 1, rows, Fl, View{dcat, 2 * Fl, 0}, View{s.cat[lvl], 2 * Fl, 0}, s.s2_pre[lvl], 0, Fl,
-                     s.s2_bn[lvl], 0, l2.obeta, 0, ACT_RELU, sl.p, 0, dres, 0, &fu_s2);
+                     s.s2_bn[lvl], 0, l2.obeta, 0, ACT_RELU, sl.p, 0, dres, 0, &fu_s2, dpre_bf(c, l2));
       if (r) return r;
       View in = lvl == L - 2 ? View{s.top_act, F[L], 0} : View{s.s1_act[lvl + 1], F[lvl + 2], 0};
       r = on_side(c, sl.ready, sl.freed, [&] { return conv_wgrad(c, l2, 1, 0, in, sl.p, 0, c->Gr + l2.ow); });
@@ -1666,7 +1692,8 @@ static int engine_backward(svae_ctx* c) {
       const long long rc = (long long)B * S[L] * S[L];
       Slot sl = dpre_next(c);
       r = bn_act_bwd(c, 1, rc, F[L - 1], View{c->denc_c, F[L - 1], 0}, View{s.enc_c_act, F[L - 1], 0}, s.enc_c_pre, 0,
-                     F[L - 1], s.enc_bn_c, 0, E.c.obeta, 0, ACT_LRELU, sl.p, 0, View{}, 0);
+                     F[L - 1], s.enc_bn_c, 0, E.c.obeta, 0, ACT_LRELU, sl.p, 0, View{}, 0, nullptr,
+                     dpre_bf(c, E.c));
       if (r) return r;
       r = on_side(c, sl.ready, sl.freed, [&] {
         return conv_wgrad(c, E.c, 1, 0, View{s.enc_act_b[L - 2], F[L - 1], 0}, sl.p, 0, c->Gr + E.c.ow);
@@ -1682,7 +1709,8 @@ static int engine_backward(svae_ctx* c) {
         const long long rows = (long long)B * S[lvl + 1] * S[lvl + 1];
         Slot sb = dpre_next(c);
         r = bn_act_bwd(c, 1, rows, Fl, View{c->denc[lvl], Fl, 0}, View{s.enc_act_b[lvl], Fl, 0}, s.enc_pre_b[lvl], 0,
-                       Fl, s.enc_bn_b[lvl], 0, E.b[lvl].obeta, 0, ACT_LRELU, sb.p, 0, View{}, 0, &fu_eb);
+                       Fl, s.enc_bn_b[lvl], 0, E.b[lvl].obeta, 0, ACT_LRELU, sb.p, 0, View{}, 0, &fu_eb,
+                       dpre_bf(c, E.b[lvl]));
         if (r) return r;
         r = on_side(c, sb.ready, sb.freed, [&] {
           return conv_wgrad(c, E.b[lvl], 1, 0, View{s.enc_act_a[lvl], Fl, 0}, sb.p, 0, c->Gr + E.b[lvl].ow);
@@ -1694,7 +1722,8 @@ static int engine_backward(svae_ctx* c) {
         if (r) return r;
         Slot sa = dpre_next(c);
         r = bn_act_bwd(c, 1, rows, Fl, View{c->dcur, Fl, 0}, View{s.enc_act_a[lvl], Fl, 0}, s.enc_pre_a[lvl], 0, Fl,
-                       s.enc_bn_a[lvl], 0, E.a[lvl].obeta, 0, ACT_LRELU, sa.p, 0, View{}, 0, &fu_ea);
+                       s.enc_bn_a[lvl], 0, E.a[lvl].obeta, 0, ACT_LRELU, sa.p, 0, View{}, 0, &fu_ea,
+                       dpre_bf(c, E.a[lvl]));
         if (r) return r;
         View in = lvl == 0 ? View{(float*)xprev, g.C, 0} : View{s.enc_act_b[lvl - 1], F[lvl], 0};
         r = on_side(c, sa.ready, sa.freed, [&] { return conv_wgrad(c, E.a[lvl], 1, 0, in, sa.p, 0, c->Gr + E.a[lvl].ow); });
@@ -1710,12 +1739,30 @@ static int engine_backward(svae_ctx* c) {
         if (r) return r;
       }
     }
+    // recognition backward of steps [t, t + rec_group) on st4, overlapping the chain backward of the
+    // earlier steps: q(z_t | x) needs only dz_t (inference_bwd waits on ev_dz), its weight gradients
+    // go to the side stream like every other; own split slab
+    if (rec_ov && t % c->rec_group == 0) {
+      hipStream_t s0 = c->st;
+      float* sl0 = c->slab;
+      c->st = c->st4;
+      c->slab = c->slab4;
+      r = inference_bwd(c, t, std::min(c->rec_group, T - t), View{(float*)c->x_in, g.C, 0}, nullptr);
+      c->st = s0;
+      c->slab = sl0;
+      if (r) return r;
+    }
   }
 
   step_hook(c, 0);
 
   // ---------------- recognition ladders: all steps batched, or step 0 (Latent InfoMax) ----------------
-  if ((r = inference_bwd(c, 0, g.plc ? 1 : T, View{(float*)c->x_in, g.C, 0}, nullptr))) return r;
+  if (rec_ov) {  // joined: every recognition group was enqueued on st4 during the chain backward
+    hipEventRecord(c->ev_j4, c->st4);
+    hipStreamWaitEvent(st, c->ev_j4, 0);
+  } else if ((r = inference_bwd(c, 0, g.plc ? 1 : T, View{(float*)c->x_in, g.C, 0}, nullptr))) {
+    return r;
+  }
   if (M.shared) {  // public gradient = fixed-order sum of the step copies (side stream joined first)
     if (c->side) {
       hipEventRecord(c->ev_join, c->st2);
@@ -1869,6 +1916,7 @@ static bool plan(svae_ctx* c) {
   c->slab_cap = 64LL << 20;
   c->slab = A(c->slab_cap);
   c->slab2 = A(c->slab_cap);
+  if (c->rec_group > 0) c->slab4 = A(c->slab_cap);
   c->cs_part = A(64 * 1024);
   c->zero_img = A((long long)B * g.H * g.W * g.C);
   return true;
@@ -1925,6 +1973,15 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
   if (e != hipSuccess) {
     delete c;
     return fail(nullptr, SVAE_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+  }
+  {
+    const char* rg = getenv("SVAE_REC_GROUP");  // recognition-backward group size (0 = batched after the chain)
+    c->rec_group = rg ? atoi(rg) : 0;
+    if (c->rec_group < 0 || c->m.g.plc) c->rec_group = 0;
+  }
+  {
+    const char* v = getenv("SVAE_DPRE_F32");  // A/B: keep the BN-backward outputs in fp32
+    c->dbf = (c->m.g.bf16 && !(v && v[0] == '1')) ? 1 : 0;
   }
   c->counting = true;
   c->arena_used = 0;
@@ -2039,11 +2096,12 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
     if (!(ns && ns[0] == '1')) {
       bool ok = hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking) == hipSuccess;
       ok = ok && hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking) == hipSuccess;
+      if (c->rec_group > 0) ok = ok && hipStreamCreateWithFlags(&c->st4, hipStreamNonBlocking) == hipSuccess;
       auto mk = [&](hipEvent_t* ev) { ok = ok && hipEventCreateWithFlags(ev, hipEventDisableTiming) == hipSuccess; };
       for (int i = 0; i < svae_ctx::NR; ++i) { mk(&c->ev_ready[i]); mk(&c->ev_free[i]); }
       for (int i = 0; i < 2; ++i) { mk(&c->ev_iready[i]); mk(&c->ev_ifree[i]); }
       mk(&c->ev_da_ready); mk(&c->ev_da_free); mk(&c->ev_start); mk(&c->ev_join); mk(&c->ev_hook);
-      mk(&c->ev_aux); mk(&c->ev_aux2); mk(&c->ev_dz); mk(&c->ev_j3);
+      mk(&c->ev_aux); mk(&c->ev_aux2); mk(&c->ev_dz); mk(&c->ev_j3); mk(&c->ev_j4);
       for (int i = 0; i < 2; ++i) { mk(&c->ev_dcat_free[i]); mk(&c->ev_dtop_free[i]); }
       for (int i = 0; i < 64; ++i) mk(&c->ev_sfc[i]);
       c->side = ok;
@@ -2056,12 +2114,12 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
 
 int svae_destroy(svae_ctx* c) {
   if (!c) return 0;
-  for (hipStream_t sx : {c->st2, c->st3})
+  for (hipStream_t sx : {c->st2, c->st3, c->st4})
     if (sx) {
       hipStreamSynchronize(sx);
       hipStreamDestroy(sx);
     }
-  for (hipEvent_t ev : {c->ev_da_ready, c->ev_da_free, c->ev_start, c->ev_join, c->ev_hook, c->ev_aux, c->ev_aux2, c->ev_dz, c->ev_j3,
+  for (hipEvent_t ev : {c->ev_da_ready, c->ev_da_free, c->ev_start, c->ev_join, c->ev_hook, c->ev_aux, c->ev_aux2, c->ev_dz, c->ev_j3, c->ev_j4,
                         c->ev_dcat_free[0], c->ev_dcat_free[1], c->ev_dtop_free[0], c->ev_dtop_free[1]})
     if (ev) hipEventDestroy(ev);
   for (hipEvent_t ev : c->ev_sfc)

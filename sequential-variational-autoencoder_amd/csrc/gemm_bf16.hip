@@ -12,6 +12,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "opload.h"
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -98,7 +99,7 @@ __device__ __forceinline__ bf16x8 cvt8(f32x4 a, f32x4 b) {
 // ---------------------------------------------------------------------------
 // gather-GEMM forward, bf16 MFMA.  A fp32 (gathered, converted), B bf16 NK [tap][n][k].
 // ---------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, bool SMALLC>
+template <int BM, int BN, int WM, int WN, bool SMALLC, bool ABF>
 __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
   constexpr int TM = BM / WM / 32;
   constexpr int TN = BN / WN / 32;
@@ -120,7 +121,8 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
   const int zc = blk.z / ks;
   const int group = zc / a.nclass, cls = zc - group * a.nclass;
   const int m0 = blk.x * BM, n0 = blk.y * BN;
-  const float* A = a.A + group * a.a_gs;
+  const long long a0 = group * a.a_gs;  // element offset of this group's A (fp32 or bf16)
+  constexpr bool abf = ABF;
   const __bf16* Bw = (const __bf16*)a.Bh + group * a.b_gs;
   const int ntap = ntaps_of_b(g);
   const int Ktot = ntap * a.Cin;
@@ -149,8 +151,9 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
         if (tid + 256 * i < CA) {
           long long sp = src_pixel_b(g, rc[i], ky, kx);
           if (sp >= 0) {
-            const float* p = A + sp * a.lda + ci0 + k8;
-            ra[i] = cvt8(*(const f32x4*)p, *(const f32x4*)(p + 4));
+            const long long off = a0 + sp * a.lda + ci0 + k8;
+            ra[i] = abf ? *(const bf16x8*)((const __bf16*)a.A + off)
+                        : cvt8(*(const f32x4*)(a.A + off), *(const f32x4*)(a.A + off + 4));
           }
         }
       }
@@ -175,7 +178,7 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
               int ky, kx;
               tap_of_b(g, cls, t, ky, kx);
               long long sp = src_pixel_b(g, rc[i], ky, kx);
-              if (sp >= 0) v[e] = A[sp * a.lda + ci];
+              if (sp >= 0) v[e] = ld1(a.A, a0 + sp * a.lda + ci, abf);
             }
           }
         }
@@ -363,7 +366,7 @@ struct HaloArgs {
   int npix;          // nimg * PR * PC
 };
 
-template <int BM, int BN, int WM, int WN, bool S2T>
+template <int BM, int BN, int WM, int WN, bool S2T, bool ABF>
 __global__ __launch_bounds__(256, 2) void igemm_halo_kernel(HaloArgs h) {
   constexpr int TM = BM / WM / 32;
   constexpr int TN = BN / WN / 32;
@@ -383,7 +386,8 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kernel(HaloArgs h) {
   const int zc = blk.z / ks;
   const int group = zc / a.nclass, cls = zc - group * a.nclass;
   const int m0 = blk.x * BM, n0 = blk.y * BN;
-  const float* A = a.A + group * a.a_gs;
+  const long long a0 = group * a.a_gs;  // element offset of this group's A (fp32 or bf16)
+  constexpr bool abf = ABF;
   const __bf16* Bw = (const __bf16*)a.Bh + group * a.b_gs;
   const int nchunk = a.Cin / HALO_CK;
   const int cbeg = (int)((long long)nchunk * split / ks), cend = (int)((long long)nchunk * (split + 1) / ks);
@@ -435,17 +439,14 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kernel(HaloArgs h) {
   constexpr int HP = HALO_PI / 2;
   f32x4 wv[HP][2];
   auto load_window = [&](int chunk, int half) {
-    const float* Ac = A + chunk * HALO_CK;
+    const long long ac = a0 + chunk * HALO_CK;
 #pragma unroll
     for (int j = 0; j < HP; ++j) {
       const int i = half * HP + j;
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
       wv[j][0] = z;
       wv[j][1] = z;
-      if (woff[i] >= 0) {
-        wv[j][0] = *(const f32x4*)(Ac + woff[i]);
-        wv[j][1] = *(const f32x4*)(Ac + woff[i] + 4);
-      }
+      if (woff[i] >= 0) ld8_raw(a.A, ac + woff[i], abf, wv[j][0], wv[j][1]);
     }
   };
   auto store_window = [&](int buf, int half) {
@@ -454,7 +455,7 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kernel(HaloArgs h) {
     for (int j = 0; j < HP; ++j) {
       const int i = half * HP + j;
       const int it = tid + 256 * i;
-      if (woff[i] >= -1) *(bf16x8*)&W[(it >> 2) * ROWP + (it & 3) * 8] = cvt8(wv[j][0], wv[j][1]);
+      if (woff[i] >= -1) *(bf16x8*)&W[(it >> 2) * ROWP + (it & 3) * 8] = raw8_bf(wv[j][0], wv[j][1], abf);
     }
   };
 
@@ -653,7 +654,7 @@ __device__ __forceinline__ bf16x8 join_tr(v4i16 lo, v4i16 hi) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int BN, int S>
+template <int BN, int S, int OPB>
 __global__ __launch_bounds__(256, (BN == 32 && S == 1) ? 2 : 1) void wgrad_halo_kernel(WHaloArgs h) {
   constexpr int NS = BN / 32;              // 32-column MFMA subtiles
   constexpr int GP = S == 1 ? 32 : 48;     // window pixel pitch (bf16)
@@ -670,8 +671,8 @@ __global__ __launch_bounds__(256, (BN == 32 && S == 1) ? 2 : 1) void wgrad_halo_
   const BlockXYZ blk = xcd_block();
   const int m0 = blk.x * 32, n0 = blk.y * BN;
   const int split = blk.z % a.nsplit, group = blk.z / a.nsplit;
-  const float* G = a.G + group * a.g_gs;
-  const float* D = a.D + group * a.d_gs;
+  const long long gg0 = group * a.g_gs, dd0 = group * a.d_gs;  // element offsets (fp32 or bf16)
+  constexpr bool gbf = (OPB & 1) != 0, dbf = (OPB & 2) != 0;  // G / D stored as bf16
   const int cbeg = (int)((long long)h.nchunk * split / a.nsplit);
   const int cend = (int)((long long)h.nchunk * (split + 1) / a.nsplit);
   const int per_img = g.Ho * g.Wo;
@@ -713,20 +714,20 @@ __global__ __launch_bounds__(256, (BN == 32 && S == 1) ? 2 : 1) void wgrad_halo_
     const int img0 = row0 / per_img;
     const int ry0 = (row0 - img0 * per_img) >> h.lgWo;
     const int iy0 = ry0 * S - g.pad;  // input row of window row 0
-    const float* Gc = G + ((long long)img0 * g.Hi + iy0) * g.Wi * a.ldg;
+    const long long gc = gg0 + ((long long)img0 * g.Hi + iy0) * g.Wi * a.ldg;
 #pragma unroll
     for (int i = 0; i < WH_WPI; ++i) {
       gv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       const int iy = iy0 + wpr[i];
-      if (wpr[i] >= 0 && iy >= 0 && iy < g.Hi) gv[i] = *(const f32x4*)(Gc + wrel[i]);
+      if (wpr[i] >= 0 && iy >= 0 && iy < g.Hi) gv[i] = ld4_raw(a.G, gc + wrel[i], gbf);
     }
-    const float* Dc = D + (long long)row0 * a.ldd + n0;
+    const long long dc = dd0 + (long long)row0 * a.ldd + n0;
 #pragma unroll
     for (int i = 0; i < WH_DPI; ++i) {
       const int it = tid + 256 * i;
       if (it < h.CP * (BN / 4)) {
         const int k = it / (BN / 4), slot = it - k * (BN / 4);
-        dv[i] = *(const f32x4*)(Dc + (long long)k * a.ldd + slot * 4);
+        dv[i] = ld4_raw(a.D, dc + (long long)k * a.ldd + slot * 4, dbf);
       }
     }
   };
@@ -735,7 +736,7 @@ __global__ __launch_bounds__(256, (BN == 32 && S == 1) ? 2 : 1) void wgrad_halo_
     for (int i = 0; i < WH_WPI; ++i) {
       if (wpr[i] == -1) continue;
       const int it = tid + 256 * i;
-      *(bf16x4*)&Gw[(it >> 3) * GP + (it & 7) * 4] = __builtin_convertvector(gv[i], bf16x4);
+      *(bf16x4*)&Gw[(it >> 3) * GP + (it & 7) * 4] = raw4_bf(gv[i], gbf);
     }
 #pragma unroll
     for (int i = 0; i < WH_DPI; ++i) {
@@ -743,7 +744,7 @@ __global__ __launch_bounds__(256, (BN == 32 && S == 1) ? 2 : 1) void wgrad_halo_
       if (it < h.CP * (BN / 4)) {
         const int k = it / (BN / 4), slot = it - k * (BN / 4);
         const int sw = BN == 64 ? (slot ^ (((k >> 1) & 1) << 3)) : slot;
-        *(bf16x4*)&Dt[k * BN + sw * 4] = __builtin_convertvector(dv[i], bf16x4);
+        *(bf16x4*)&Dt[k * BN + sw * 4] = raw4_bf(dv[i], dbf);
       }
     }
   };
@@ -831,8 +832,8 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
   const int split = blk.z % a.nsplit;
   const int group = blk.z / a.nsplit;
   const int Mtot = a.ntap * a.M;
-  const float* G = a.G + group * a.g_gs;
-  const float* D = a.D + group * a.d_gs;
+  const long long gg0 = group * a.g_gs, dd0 = group * a.d_gs;  // element offsets (fp32 or bf16)
+  const bool gbf = a.g_bf16 != 0, dbf = a.d_bf16 != 0;
   const int p_begin = split * a.chunk;
   const int p_end = min(a.rows, p_begin + a.chunk);
   const int nk = (p_end - p_begin + BKB - 1) / BKB;
@@ -881,16 +882,16 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
           ix0 = rc.x * g.stride - g.pad + ukx[i];
         }
         const bool rowok = uok && (g.mode == GM_DENSE || (iy >= 0 && iy < g.Hi));
-        const float* gp = G + (g.mode == GM_DENSE ? (long long)p0 * a.ldg
-                                                  : ((long long)rc.img + (long long)iy * g.Wi + ix0) * a.ldg) +
-                          um[i];
+        const long long gp = gg0 + (g.mode == GM_DENSE ? (long long)p0 * a.ldg
+                                                       : ((long long)rc.img + (long long)iy * g.Wi + ix0) * a.ldg) +
+                             um[i];
         const int step = g.mode == GM_DENSE ? a.ldg : g.stride * a.ldg;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           f32x4 v = {0.f, 0.f, 0.f, 0.f};
           const int ix = ix0 + j * g.stride;
           const bool ok = rowok && (p0 + j < p_end) && (g.mode == GM_DENSE || (ix >= 0 && ix < g.Wi));
-          if (ok) v = *(const f32x4*)(gp + j * step);
+          if (ok) v = ld4_raw(a.G, gp + (long long)j * step, gbf);
           va[i][j] = v;
         }
         continue;
@@ -909,7 +910,7 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
               if (re < Mtot) {
                 const int tap = re / a.M, m = re - (re / a.M) * a.M;
                 long long sp = src_pixel_b(g, rc, tap / g.ksz, tap % g.ksz);
-                if (sp >= 0) v[e] = G[sp * a.ldg + m];
+                if (sp >= 0) v[e] = ld1(a.G, gg0 + sp * a.ldg + m, gbf);
               }
             }
           }
@@ -926,7 +927,7 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
       for (int j = 0; j < 4; ++j) {
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
         const int p = p_begin + kc * BKB + pq * 4 + j;
-        if (u < UB && p < p_end && nc < a.N) v = *(const f32x4*)(D + (long long)p * a.ldd + nc);
+        if (u < UB && p < p_end && nc < a.N) v = ld4_raw(a.D, dd0 + (long long)p * a.ldd + nc, dbf);
         vb[i][j] = v;
       }
     }
@@ -939,7 +940,9 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
       const int mq = u % QMc, pq = u / QMc;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        f32x4 col = {va[i][0][c], va[i][1][c], va[i][2][c], va[i][3][c]};
+        const bool rg = VECG && gbf;  // raw bf16 bits (the scalar gather path holds fp32 values)
+        f32x4 col = {raw4_elem(va[i][0], c, rg), raw4_elem(va[i][1], c, rg), raw4_elem(va[i][2], c, rg),
+                     raw4_elem(va[i][3], c, rg)};
         *(bf16x4*)&As[buf][(mq * 4 + c) * ROWP + pq * 4] = __builtin_convertvector(col, bf16x4);
       }
     }
@@ -950,7 +953,8 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
       const int nq = u % QNc, pq = u / QNc;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        f32x4 col = {vb[i][0][c], vb[i][1][c], vb[i][2][c], vb[i][3][c]};
+        f32x4 col = {raw4_elem(vb[i][0], c, dbf), raw4_elem(vb[i][1], c, dbf), raw4_elem(vb[i][2], c, dbf),
+                     raw4_elem(vb[i][3], c, dbf)};
         *(bf16x4*)&Bs[buf][(nq * 4 + c) * ROWP + pq * 4] = __builtin_convertvector(col, bf16x4);
       }
     }
@@ -1117,8 +1121,13 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* part, i
 template <int BM, int BN, int WM, int WN>
 static void launch_bf16(const FwdArgs& a, int groups, bool sc, hipStream_t s) {
   dim3 grid((a.rows + BM - 1) / BM, (a.N + BN - 1) / BN, groups * a.nclass * a.ksplit);
-  if (sc) hipLaunchKernelGGL((igemm_bf16_kernel<BM, BN, WM, WN, true>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((igemm_bf16_kernel<BM, BN, WM, WN, false>), grid, dim3(256), 0, s, a);
+  if (a.a_bf16) {
+    if (sc) hipLaunchKernelGGL((igemm_bf16_kernel<BM, BN, WM, WN, true, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((igemm_bf16_kernel<BM, BN, WM, WN, false, true>), grid, dim3(256), 0, s, a);
+  } else {
+    if (sc) hipLaunchKernelGGL((igemm_bf16_kernel<BM, BN, WM, WN, true, false>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((igemm_bf16_kernel<BM, BN, WM, WN, false, false>), grid, dim3(256), 0, s, a);
+  }
 }
 
 static int bf16_bm(const FwdArgs& a) {
@@ -1227,18 +1236,26 @@ template <int BM, int BN, int WM, int WN>
 static void launch_halo(const HaloArgs& h, int groups, size_t lds, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)igemm_halo_kernel<BM, BN, WM, WN, false>,
+    hipFuncSetAttribute((const void*)igemm_halo_kernel<BM, BN, WM, WN, false, false>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, HALO_LDS_MAX);
-    hipFuncSetAttribute((const void*)igemm_halo_kernel<BM, BN, WM, WN, true>,
+    hipFuncSetAttribute((const void*)igemm_halo_kernel<BM, BN, WM, WN, true, false>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, HALO_LDS_MAX);
+    hipFuncSetAttribute((const void*)igemm_halo_kernel<BM, BN, WM, WN, false, true>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, HALO_LDS_MAX);
+    hipFuncSetAttribute((const void*)igemm_halo_kernel<BM, BN, WM, WN, true, true>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, HALO_LDS_MAX);
     attr = true;
   }
   const FwdArgs& a = h.f;
   dim3 grid(a.rows / BM, (a.N + BN - 1) / BN, groups * a.nclass * a.ksplit);
-  if (a.g.mode == GM_CONVT && a.g.stride == 2)
-    hipLaunchKernelGGL((igemm_halo_kernel<BM, BN, WM, WN, true>), grid, dim3(256), lds, s, h);
-  else
-    hipLaunchKernelGGL((igemm_halo_kernel<BM, BN, WM, WN, false>), grid, dim3(256), lds, s, h);
+  const bool s2t = a.g.mode == GM_CONVT && a.g.stride == 2;
+  if (a.a_bf16) {
+    if (s2t) hipLaunchKernelGGL((igemm_halo_kernel<BM, BN, WM, WN, true, true>), grid, dim3(256), lds, s, h);
+    else hipLaunchKernelGGL((igemm_halo_kernel<BM, BN, WM, WN, false, true>), grid, dim3(256), lds, s, h);
+  } else {
+    if (s2t) hipLaunchKernelGGL((igemm_halo_kernel<BM, BN, WM, WN, true, false>), grid, dim3(256), lds, s, h);
+    else hipLaunchKernelGGL((igemm_halo_kernel<BM, BN, WM, WN, false, false>), grid, dim3(256), lds, s, h);
+  }
 }
 
 // the wave-split kernel (halo_kw.hip) is tried first where the tiled halo kernel would split K over
@@ -1500,13 +1517,20 @@ void wgrad_halo(const WHaloPlanOut& pl, const WgArgs& a, int groups, hipStream_t
   WHaloArgs h = pl.h;
   h.w = a;
   dim3 grid(a.M / 32, a.N / pl.bn, groups * a.nsplit);
-  if (pl.bn == 32) {
-    if (a.g.stride == 1) hipLaunchKernelGGL((wgrad_halo_kernel<32, 1>), grid, dim3(256), pl.lds, s, h);
-    else hipLaunchKernelGGL((wgrad_halo_kernel<32, 2>), grid, dim3(256), pl.lds, s, h);
-  } else {
-    if (a.g.stride == 1) hipLaunchKernelGGL((wgrad_halo_kernel<64, 1>), grid, dim3(256), pl.lds, s, h);
-    else hipLaunchKernelGGL((wgrad_halo_kernel<64, 2>), grid, dim3(256), pl.lds, s, h);
+  const int op = (a.g_bf16 ? 1 : 0) | (a.d_bf16 ? 2 : 0);  // operand storage: compile-time in the kernel
+#define WHL(BN_, S_)                                                                                   \
+  switch (op) {                                                                                        \
+    case 0: hipLaunchKernelGGL((wgrad_halo_kernel<BN_, S_, 0>), grid, dim3(256), pl.lds, s, h); break; \
+    case 1: hipLaunchKernelGGL((wgrad_halo_kernel<BN_, S_, 1>), grid, dim3(256), pl.lds, s, h); break; \
+    case 2: hipLaunchKernelGGL((wgrad_halo_kernel<BN_, S_, 2>), grid, dim3(256), pl.lds, s, h); break; \
+    default: hipLaunchKernelGGL((wgrad_halo_kernel<BN_, S_, 3>), grid, dim3(256), pl.lds, s, h); break; \
   }
+  if (pl.bn == 32) {
+    if (a.g.stride == 1) { WHL(32, 1) } else { WHL(32, 2) }
+  } else {
+    if (a.g.stride == 1) { WHL(64, 1) } else { WHL(64, 2) }
+  }
+#undef WHL
   if (after) hipEventRecord(after, s);
 }
 

@@ -18,6 +18,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "opload.h"
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x8 __attribute__((ext_vector_type(8)));
@@ -37,11 +38,6 @@ struct KwArgs {
 
 namespace {
 
-__device__ __forceinline__ bf16x8 kw_cvt8(f32x4 a, f32x4 b) {
-  f32x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-  return __builtin_convertvector(v, bf16x8);
-}
-
 __device__ __forceinline__ long long kw_out_row(const ConvGeom& g, int cls, int m) {
   if (g.mode == GM_CONVT && g.stride == 2) {
     const int qh = g.Ho >> 1, qw = g.Wo >> 1;
@@ -53,10 +49,10 @@ __device__ __forceinline__ long long kw_out_row(const ConvGeom& g, int cls, int 
   return m;
 }
 
-template <int BM, bool S2T>
+template <int BM, int BN, bool S2T, bool ABF>
 __global__ __launch_bounds__(256, 2) void igemm_halo_kw_kernel(KwArgs h) {
-  constexpr int BN = 32;
   constexpr int TM = BM / 32;
+  constexpr int TN = BN / 32;
   constexpr int NTAP = S2T ? 4 : 16;
   constexpr int NTW = NTAP / 4;  // taps per wave (and B prefetch distance: one chunk ahead)
   extern __shared__ __attribute__((aligned(16))) __bf16 ksm[];
@@ -69,7 +65,8 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kw_kernel(KwArgs h) {
   const BlockXYZ blk = xcd_block();
   const int group = blk.z / a.nclass, cls = blk.z - group * a.nclass;
   const int m0 = blk.x * BM, n0 = blk.y * BN;
-  const float* A = a.A + group * a.a_gs;
+  const long long a0 = group * a.a_gs;  // element offset of this group's A (fp32 or bf16)
+  constexpr bool abf = ABF;
   const __bf16* Bw = (const __bf16*)a.Bh + group * a.b_gs;
   const int nchunk = a.Cin / KW_CK;
 
@@ -117,16 +114,13 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kw_kernel(KwArgs h) {
   }
   f32x4 wv[KW_PI][2];
   auto load_window = [&](int chunk) {
-    const float* Ac = A + chunk * KW_CK;
+    const long long ac = a0 + chunk * KW_CK;
 #pragma unroll
     for (int i = 0; i < KW_PI; ++i) {
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
       wv[i][0] = z;
       wv[i][1] = z;
-      if (woff[i] >= 0) {
-        wv[i][0] = *(const f32x4*)(Ac + woff[i]);
-        wv[i][1] = *(const f32x4*)(Ac + woff[i] + 4);
-      }
+      if (woff[i] >= 0) ld8_raw(a.A, ac + woff[i], abf, wv[i][0], wv[i][1]);
     }
   };
   auto store_window = [&](int buf) {
@@ -134,7 +128,7 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kw_kernel(KwArgs h) {
 #pragma unroll
     for (int i = 0; i < KW_PI; ++i) {
       const int it = tid + 256 * i;
-      if (woff[i] >= -1) *(bf16x8*)&W[(it >> 2) * KW_ROWP + (it & 3) * 8] = kw_cvt8(wv[i][0], wv[i][1]);
+      if (woff[i] >= -1) *(bf16x8*)&W[(it >> 2) * KW_ROWP + (it & 3) * 8] = raw8_bf(wv[i][0], wv[i][1], abf);
     }
   };
 
@@ -152,20 +146,24 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kw_kernel(KwArgs h) {
 
   // ---- this wave's taps: t = wave * NTW + u; B fragments one chunk ahead ----
   const __bf16* bptr = Bw + (long long)(n0 + l32) * a.ldb + 8 * hh;
-  bf16x8 bq[NTW][2];
+  bf16x8 bq[NTW][TN][2];
   auto load_b = [&](int u, int chunk) {
     const int t = wave * NTW + u;
     const int tap = S2T ? tap0 + 8 * (t >> 1) + 2 * (t & 1) : t;
     const long long off = (long long)tap * a.b_tap + chunk * KW_CK;
 #pragma unroll
-    for (int kq = 0; kq < 2; ++kq) bq[u][kq] = *(const bf16x8*)(bptr + off + kq * 16);
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+      for (int kq = 0; kq < 2; ++kq) bq[u][tn][kq] = *(const bf16x8*)(bptr + (long long)tn * 32 * a.ldb + off + kq * 16);
   };
 
-  f32x16 acc[TM];
+  f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   load_window(0);
 #pragma unroll
@@ -189,7 +187,9 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kw_kernel(KwArgs h) {
         for (int tm = 0; tm < TM; ++tm) af[tm] = *(const bf16x8*)&W[abase[tm] + sh + kq * 16];
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm)
-          acc[tm] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm], bq[u][kq], acc[tm], 0, 0, 0);
+#pragma unroll
+          for (int tn = 0; tn < TN; ++tn)
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm], bq[u][tn][kq], acc[tm][tn], 0, 0, 0);
       }
       if (has_next) load_b(u, c + 1);
     }
@@ -202,12 +202,15 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kw_kernel(KwArgs h) {
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-      red[(wave * BM + m) * BN + l32] = acc[tm][r];
-    }
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        red[(wave * BM + m) * BN + tn * 32 + l32] = acc[tm][tn][r];
+      }
   __syncthreads();
-  const int col = tid & 31, rg = tid >> 5;  // 8 row groups
+  constexpr int NRG = 256 / BN;  // row groups
+  const int col = tid % BN, rg = tid / BN;
   const int n = n0 + col;
   float* Cp = a.C + group * a.c_gs;
   const float* bias = a.bias ? a.bias + group * a.bias_gs : nullptr;
@@ -220,7 +223,7 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kw_kernel(KwArgs h) {
     bb = a.bw.y ? 0.f : a.bw.beta[group * a.bw.beta_gs + n];
   }
   float s1 = 0.f, s2 = 0.f;
-  for (int m = rg; m < BM; m += 8) {
+  for (int m = rg; m < BM; m += NRG) {
     float v = red[(0 * BM + m) * BN + col];
 #pragma unroll
     for (int w = 1; w < 4; ++w) v += red[(w * BM + m) * BN + col];
@@ -248,9 +251,9 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kw_kernel(KwArgs h) {
     if (n0 + tid < SC) {
       float s = 0.f, q = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        s += red[j * 32 + tid];
-        q += red[256 + j * 32 + tid];
+      for (int j = 0; j < NRG; ++j) {
+        s += red[j * BN + tid];
+        q += red[256 + j * BN + tid];
       }
       const int rb = cls * gridDim.x + blk.x;
       stat_put(a.stats + (rb & (a.s_nsh - 1)) * a.s_sh + group * a.s_gs, n0 + tid, s, q);
@@ -261,7 +264,15 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kw_kernel(KwArgs h) {
 }  // namespace
 
 // ---- planner: eligible shapes, BM, window geometry, LDS, stats row-blocks ----
-static bool kw_plan(const FwdArgs& a, int groups, KwArgs* out, int* bm_out, size_t* lds_out) {
+static int kw_bn_mode() {  // SVAE_KW_BN: 32 (default) or 64 column tiles
+  static const int v = [] {
+    const char* e = getenv("SVAE_KW_BN");
+    return e ? atoi(e) : 32;
+  }();
+  return v;
+}
+
+static bool kw_plan(const FwdArgs& a, int groups, KwArgs* out, int* bm_out, int* bn_out, size_t* lds_out) {
   const ConvGeom& g = a.g;
   if (g.mode == GM_DENSE || g.ksz != 4 || g.pad != 1 || !a.Bh || a.Cin % KW_CK != 0 || a.N % 32 != 0) return false;
   const bool s2t = g.mode == GM_CONVT && g.stride == 2;
@@ -283,11 +294,14 @@ static bool kw_plan(const FwdArgs& a, int groups, KwArgs* out, int* bm_out, size
     h.PC = (Wr - 1) * sy + span;
     h.npix = h.nimg * h.PR * h.PC;
     if (h.npix * 4 > 256 * KW_PI) continue;
-    const long long blocks = (long long)(a.rows / bm) * (a.N / 32) * a.nclass * groups;
+    int bn = 32;
+    if (kw_bn_mode() == 64 && a.N % 64 == 0 && (long long)(a.rows / bm) * (a.N / 64) * a.nclass * groups >= 512) bn = 64;
+    const long long blocks = (long long)(a.rows / bm) * (a.N / bn) * a.nclass * groups;
     if (blocks < 256 && bm == 64) continue;  // the 32-row tile doubles the blocks
     *out = h;
     *bm_out = bm;
-    *lds_out = std::max((size_t)(2 * h.npix) * KW_ROWP * sizeof(__bf16), (size_t)4 * bm * 32 * sizeof(float));
+    *bn_out = bn;
+    *lds_out = std::max((size_t)(2 * h.npix) * KW_ROWP * sizeof(__bf16), (size_t)4 * bm * bn * sizeof(float));
     return true;
   }
   return false;
@@ -304,26 +318,46 @@ static bool kw_disabled() {
 int halo_kw_plan(const FwdArgs& a, int groups) {
   if (kw_disabled()) return 0;
   KwArgs h;
-  int bm;
+  int bm, bn;
   size_t lds;
-  if (!kw_plan(a, groups, &h, &bm, &lds)) return 0;
+  if (!kw_plan(a, groups, &h, &bm, &bn, &lds)) return 0;
   return a.nclass * (a.rows / bm);
 }
 
 int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
   KwArgs h;
-  int bm;
+  int bm, bn;
   size_t lds;
-  if (kw_disabled() || !kw_plan(a, groups, &h, &bm, &lds)) return -1;
+  if (kw_disabled() || !kw_plan(a, groups, &h, &bm, &bn, &lds)) return -1;
   h.f = a;
   const bool s2t = a.g.mode == GM_CONVT && a.g.stride == 2;
-  dim3 grid(a.rows / bm, a.N / 32, groups * a.nclass);
-  if (bm == 64) {
-    if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<64, true>), grid, dim3(256), lds, s, h);
-    else hipLaunchKernelGGL((igemm_halo_kw_kernel<64, false>), grid, dim3(256), lds, s, h);
-  } else {
-    if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<32, true>), grid, dim3(256), lds, s, h);
-    else hipLaunchKernelGGL((igemm_halo_kw_kernel<32, false>), grid, dim3(256), lds, s, h);
+  dim3 grid(a.rows / bm, a.N / bn, groups * a.nclass);
+#define KW_LAUNCH(BM_, BN_)                                                                                  \
+  if (a.a_bf16) {                                                                                            \
+    if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<BM_, BN_, true, true>), grid, dim3(256), lds, s, h);    \
+    else hipLaunchKernelGGL((igemm_halo_kw_kernel<BM_, BN_, false, true>), grid, dim3(256), lds, s, h);       \
+  } else {                                                                                                   \
+    if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<BM_, BN_, true, false>), grid, dim3(256), lds, s, h);   \
+    else hipLaunchKernelGGL((igemm_halo_kw_kernel<BM_, BN_, false, false>), grid, dim3(256), lds, s, h);      \
   }
+  if (bm == 64 && bn == 64) {
+    static bool attr = false;
+    if (!attr) {  // 4 x 64 x 64 fp32 partial tiles: 64 KB
+      for (const void* f : {(const void*)igemm_halo_kw_kernel<64, 64, true, false>,
+                            (const void*)igemm_halo_kw_kernel<64, 64, false, false>,
+                            (const void*)igemm_halo_kw_kernel<64, 64, true, true>,
+                            (const void*)igemm_halo_kw_kernel<64, 64, false, true>})
+        hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+      attr = true;
+    }
+    KW_LAUNCH(64, 64)
+  } else if (bm == 64) {
+    KW_LAUNCH(64, 32)
+  } else if (bn == 64) {
+    KW_LAUNCH(32, 64)
+  } else {
+    KW_LAUNCH(32, 32)
+  }
+#undef KW_LAUNCH
   return a.nclass * (a.rows / bm);
 }

@@ -32,6 +32,7 @@ struct FwdArgs {
   // split-K (bf16 path): fp32 partial slabs [ksplit][rows_total][N] + reduce/stats pass
   float* part; long long part_cap; int ksplit; int rows_total;
   BwStat bw;    // bf16 kernels: backward-BN partials instead of forward stats (bw.pre != nullptr)
+  int a_bf16;   // bf16 kernels: A is stored as bf16 (element offsets / strides unchanged; opload.h)
 };
 
 // weight-GEMM  part[split][tap][m][n] = sum_{p in split} G[src(p,tap)][m] * D[p][n]
@@ -42,6 +43,7 @@ struct WgArgs {
   int M, N;
   ConvGeom g;   // mode CONV or DENSE; row space = D's pixels, gathered space = G's pixels
   int rows, chunk, nsplit, ntap;
+  int g_bf16, d_bf16;  // bf16 kernels: G / D stored as bf16 (opload.h)
 };
 
 int igemm_fwd_bm(const FwdArgs& a);
@@ -150,7 +152,7 @@ void bn_bwd_apply(const float* dy, int lddy, long long dy_gs, const float* y, in
                   const float* invstd, long long ms_gs, const float* beta, long long beta_gs, const u64* acc,
                   long long acc_gs, long long sh, int nsh, float* dbeta, long long dbeta_gs, int act, float* dpre, int lddp,
                   long long dpre_gs, float* dres, int ldres, long long dres_gs, int res_acc, int groups,
-                  hipStream_t s);
+                  hipStream_t s, int dpre_bf16 = 0);  // dpre_bf16: write dpre as bf16 (RNE)
 
 // ---- split_latent FC(K=Dl) + BN over batch + lrelu, fused (sequential_vae.py:1801-1806) ----
 // out[n][j] written at out + n*o_n + (j / F)*ldo + (j % F)

@@ -1,0 +1,57 @@
+// Operand loads of the bf16-MFMA GEMM kernels from fp32 OR bf16 tensors.
+//
+// In bf16 mode the BN-backward outputs (the gradients at the BN inputs, "dpre") are stored as
+// bf16: their only consumers are the input-gradient and weight-gradient GEMMs, which round their
+// operands to bf16 while staging them into LDS anyway, so storing them rounded (RNE, the same
+// conversion) changes no result bit and halves the bytes written and re-read.
+//
+// The kernels keep their fp32 register staging and defer the conversion to the LDS store (so the
+// load latency stays hidden behind the MFMAs); for a bf16 source the same registers carry the
+// raw bf16 bits and the store passes them through.  `bf` is uniform per launch.
+#pragma once
+#include "common.h"
+
+typedef __bf16 ol_bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 ol_bf16x4 __attribute__((ext_vector_type(4)));
+typedef float ol_f32x8 __attribute__((ext_vector_type(8)));
+typedef float ol_f32x2 __attribute__((ext_vector_type(2)));
+
+// 8 consecutive elements at element offset `off`: fp32 -> (lo, hi); bf16 -> lo holds the 16 bytes
+__device__ __forceinline__ void ld8_raw(const void* base, long long off, bool bf, f32x4& lo, f32x4& hi) {
+  if (bf) {
+    lo = *(const f32x4*)((const __bf16*)base + off);
+  } else {
+    const float* p = (const float*)base + off;
+    lo = *(const f32x4*)p;
+    hi = *(const f32x4*)(p + 4);
+  }
+}
+__device__ __forceinline__ ol_bf16x8 raw8_bf(f32x4 lo, f32x4 hi, bool bf) {
+  if (bf) return __builtin_bit_cast(ol_bf16x8, lo);
+  const ol_f32x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_convertvector(v, ol_bf16x8);
+}
+// 4 consecutive elements: fp32 -> v; bf16 -> the 8 bytes in v[0], v[1]
+__device__ __forceinline__ f32x4 ld4_raw(const void* base, long long off, bool bf) {
+  if (bf) {
+    const ol_f32x2 t = *(const ol_f32x2*)((const __bf16*)base + off);
+    return f32x4{t[0], t[1], 0.f, 0.f};
+  }
+  return *(const f32x4*)((const float*)base + off);
+}
+__device__ __forceinline__ ol_bf16x4 raw4_bf(f32x4 v, bool bf) {
+  if (bf) {
+    const ol_f32x2 t = {v[0], v[1]};
+    return __builtin_bit_cast(ol_bf16x4, t);
+  }
+  return __builtin_convertvector(v, ol_bf16x4);
+}
+// element e of a raw 4-vector as fp32 (exact for a bf16 source)
+__device__ __forceinline__ float raw4_elem(f32x4 v, int e, bool bf) {
+  if (!bf) return v[e];
+  const unsigned u = __float_as_uint(v[e >> 1]);
+  return __uint_as_float((e & 1) ? (u & 0xFFFF0000u) : (u << 16));
+}
+__device__ __forceinline__ float ld1(const void* base, long long off, bool bf) {
+  return bf ? (float)((const __bf16*)base)[off] : ((const float*)base)[off];
+}

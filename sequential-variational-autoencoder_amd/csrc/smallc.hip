@@ -26,6 +26,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "opload.h"
 
 namespace {
 
@@ -247,7 +248,8 @@ __global__ __launch_bounds__(256) void convt_smalln_kernel(FwdArgs a) {
   const int iy0 = Y0 / 2 - 1;
   const int WT = g.Wi / 16;             // 16-pixel segments per class row
   const int ntile = (SN_R / 2) * WT;
-  const float* A = a.A + group * a.a_gs + (long long)img * g.Hi * g.Wi * a.lda;
+  const long long a0 = group * a.a_gs + (long long)img * g.Hi * g.Wi * a.lda;  // element offset (fp32 or bf16 A)
+  const bool abf = a.a_bf16 != 0;
   const __bf16* Bw = (const __bf16*)a.Bh + group * a.b_gs;
   const int ky0 = (cy + g.pad) & 1, kx0 = (cx + g.pad) & 1;
   const bool nvalid = r16 < a.N;
@@ -262,13 +264,10 @@ __global__ __launch_bounds__(256) void convt_smalln_kernel(FwdArgs a) {
       const int pix = it >> 2, part = it & 3;
       const int pr = pix / PC, pc = pix - pr * PC;
       const int iy = iy0 + pr, ix = pc - 1;
-      f32x8 v = {};
-      if (iy >= 0 && iy < g.Hi && ix >= 0 && ix < g.Wi) {
-        const float* src = A + ((long long)iy * g.Wi + ix) * a.lda + ch + part * 8;
-        const f32x4 lo = *(const f32x4*)src, hi = *(const f32x4*)(src + 4);
-        v = f32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-      *(bf16x8*)&wsm[pix * SN_PITCH + part * 8] = __builtin_convertvector(v, bf16x8);
+      f32x4 lo = {0.f, 0.f, 0.f, 0.f}, hi = lo;
+      if (iy >= 0 && iy < g.Hi && ix >= 0 && ix < g.Wi)
+        ld8_raw(a.A, a0 + ((long long)iy * g.Wi + ix) * a.lda + ch + part * 8, abf, lo, hi);
+      *(bf16x8*)&wsm[pix * SN_PITCH + part * 8] = raw8_bf(lo, hi, abf);
     }
     // this class's 4 tap fragments of the chunk (columns >= N are zero)
     bf16x8 bq[4];

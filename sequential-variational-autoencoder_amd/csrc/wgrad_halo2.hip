@@ -23,6 +23,7 @@
 // ds_read_b64_tr_b16 reads conflict-free (same layouts as gemm_bf16.hip's halo weight-GEMM).
 #include "common.h"
 #include "kernels.h"
+#include "opload.h"
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -60,9 +61,10 @@ struct WH2Args {
   const float* D; long long d_gs; int ldd;
   float* part; long long p_gs;   // [split][16][M][N] partials (or dW itself when nsplit == 1)
   int M, N, nsplit, nchunk;      // nchunk: chunks per group
+  int g_bf16, d_bf16;            // G / D stored as bf16 (opload.h)
 };
 
-template <int WO, int CP, int KYR, int WN, int WK, bool DB>
+template <int WO, int CP, int KYR, int WN, int WK, bool DB, int OPB>
 __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args a) {
   using GE = Geo2<WO, CP>;
   constexpr int NT = 64 * KYR * WN * WK;
@@ -89,8 +91,8 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
   const int zs = blk.z / NTG;
   const int split = zs % a.nsplit, group = zs / a.nsplit;
   const int ky = tg * KYR + kyw;
-  const float* G = a.G + group * a.g_gs;
-  const float* D = a.D + group * a.d_gs;
+  const long long gg0 = group * a.g_gs, dd0 = group * a.d_gs;  // element offsets (fp32 or bf16)
+  constexpr bool gbf = (OPB & 1) != 0, dbf = (OPB & 2) != 0;  // G / D stored as bf16
   const int cbeg = (int)((long long)a.nchunk * split / a.nsplit);
   const int cend = (int)((long long)a.nchunk * (split + 1) / a.nsplit);
 
@@ -137,15 +139,15 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
     for (int i = 0; i < GI; ++i) {
       gv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       const int iy = ry0 - 1 + wpr[i];
-      if (wpr[i] >= 0 && iy >= 0 && iy < WO) gv[i] = *(const f32x4*)(G + gbase + wrel[i]);
+      if (wpr[i] >= 0 && iy >= 0 && iy < WO) gv[i] = ld4_raw(a.G, gg0 + gbase + wrel[i], gbf);
     }
-    const float* Dc = D + (long long)row0 * a.ldd + n0;
+    const long long dc = dd0 + (long long)row0 * a.ldd + n0;
 #pragma unroll
     for (int i = 0; i < DI; ++i) {
       const int it = tid + NT * i;
       if (it < CP * DN / 4) {
         const int k = it / (DN / 4), sl = it - k * (DN / 4);
-        dv[i] = *(const f32x4*)(Dc + (long long)k * a.ldd + sl * 4);
+        dv[i] = ld4_raw(a.D, dc + (long long)k * a.ldd + sl * 4, dbf);
       }
     }
   };
@@ -154,7 +156,7 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
     for (int i = 0; i < GI; ++i) {
       if (wpr[i] == -1) continue;
       const int it = tid + NT * i;
-      *(bf16x4*)&st[(it >> 3) * 32 + (it & 7) * 4] = __builtin_convertvector(gv[i], bf16x4);
+      *(bf16x4*)&st[(it >> 3) * 32 + (it & 7) * 4] = raw4_bf(gv[i], gbf);
     }
 #pragma unroll
     for (int i = 0; i < DI; ++i) {
@@ -162,7 +164,7 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
       if (it < CP * DN / 4) {
         const int k = it / (DN / 4), sl = it - k * (DN / 4);
         const int s2 = DN == 64 ? (sl ^ (((k >> 1) & 1) << 3)) : sl;
-        *(bf16x4*)&st[GWB + k * DN + s2 * 4] = __builtin_convertvector(dv[i], bf16x4);
+        *(bf16x4*)&st[GWB + k * DN + s2 * 4] = raw4_bf(dv[i], dbf);
       }
     }
   };
@@ -241,17 +243,27 @@ size_t wh2_lds() {
   return std::max((DB ? 2 : 1) * stage, red);
 }
 
-template <int WO, int CP, int KYR, int WN, int WK, bool DB>
-void wh2_launch(const WH2Args& a, int groups, hipStream_t s) {
+template <int WO, int CP, int KYR, int WN, int WK, bool DB, int OPB>
+void wh2_launch_op(const WH2Args& a, int groups, hipStream_t s) {
   const size_t lds = wh2_lds<WO, CP, KYR, WN, WK, DB>();
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)wgrad_halo2_kernel<WO, CP, KYR, WN, WK, DB>,
+    hipFuncSetAttribute((const void*)wgrad_halo2_kernel<WO, CP, KYR, WN, WK, DB, OPB>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   dim3 grid(a.M / 32, a.N / (32 * WN), (4 / KYR) * a.nsplit * groups);
-  hipLaunchKernelGGL((wgrad_halo2_kernel<WO, CP, KYR, WN, WK, DB>), grid, dim3(64 * KYR * WN * WK), lds, s, a);
+  hipLaunchKernelGGL((wgrad_halo2_kernel<WO, CP, KYR, WN, WK, DB, OPB>), grid, dim3(64 * KYR * WN * WK), lds, s, a);
+}
+// operand storage (G fp32/bf16 x D fp32/bf16) as a compile-time parameter: no branches in the loads
+template <int WO, int CP, int KYR, int WN, int WK, bool DB>
+void wh2_launch(const WH2Args& a, int groups, hipStream_t s) {
+  switch ((a.g_bf16 ? 1 : 0) | (a.d_bf16 ? 2 : 0)) {
+    case 0: wh2_launch_op<WO, CP, KYR, WN, WK, DB, 0>(a, groups, s); break;
+    case 1: wh2_launch_op<WO, CP, KYR, WN, WK, DB, 1>(a, groups, s); break;
+    case 2: wh2_launch_op<WO, CP, KYR, WN, WK, DB, 2>(a, groups, s); break;
+    default: wh2_launch_op<WO, CP, KYR, WN, WK, DB, 3>(a, groups, s); break;
+  }
 }
 
 int env_int(const char* name, int dflt) {
@@ -268,8 +280,8 @@ int wgrad_halo2_enabled() {
 }
 
 // Config per layer: WN = 2 where N >= 64 (one staged G window feeds 64 D columns), else the
-// 32-column tile with two K-interleaved wave sets; KYR = 4 (all 16 taps per block) unless
-// SVAE_WH2_KYR = 2 (8 taps per block: half the partial slab per block, twice the staging).
+// 32-column tile with two K-interleaved wave sets; KYR = 4 (all 16 taps per block; the 8-tap
+// variant and the double-buffered stage were measured slower in round 2 and are not built).
 // Split count: ~target blocks over the machine (SVAE_WH2_TARGET, default 128: in the step the
 // kernel shares the GPU with the main stream, and half the splits halve the slab traffic), >= minch chunks
 // per split (SVAE_WH2_MINCH, default 4), slab within capacity.
@@ -293,13 +305,12 @@ int wgrad_halo2(const WgArgs& w, int groups, float* slab, long long slab_cap, fl
   const int cp = wh2_cp(WO);
   static const int target = env_int("SVAE_WH2_TARGET", 128);
   static const int minch = env_int("SVAE_WH2_MINCH", 4);
-  static const int kyr_env = env_int("SVAE_WH2_KYR", 4);
-  static const int db = env_int("SVAE_WH2_DB", 0);
   const int wn = (w.N % 64 == 0) ? 2 : 1;
-  const int kyr = kyr_env == 2 ? 2 : 4;
+  const int kyr = 4;
   WH2Args a;
   a.G = w.G; a.g_gs = w.g_gs; a.ldg = w.ldg;
   a.D = w.D; a.d_gs = w.d_gs; a.ldd = w.ldd;
+  a.g_bf16 = w.g_bf16; a.d_bf16 = w.d_bf16;
   a.M = w.M; a.N = w.N;
   a.nchunk = w.rows / cp;
   const long long tiles = (long long)(w.M / 32) * (w.N / (32 * wn)) * (4 / kyr) * groups;
@@ -315,17 +326,10 @@ int wgrad_halo2(const WgArgs& w, int groups, float* slab, long long slab_cap, fl
     a.part = slab;
     a.p_gs = (long long)a.nsplit * per;
   }
-#define WH2(WOV, CPV, KY, WNV, WKV)                        \
-  if (db) wh2_launch<WOV, CPV, KY, WNV, WKV, true>(a, groups, s); \
-  else wh2_launch<WOV, CPV, KY, WNV, WKV, false>(a, groups, s)
+#define WH2(WOV, CPV, KY, WNV, WKV) wh2_launch<WOV, CPV, KY, WNV, WKV, false>(a, groups, s)
 #define WH2_WO(WOV, CPV)                                   \
-  if (kyr == 4) {                                          \
-    if (wn == 2) { WH2(WOV, CPV, 4, 2, 1); }               \
-    else { WH2(WOV, CPV, 4, 1, 2); }                       \
-  } else {                                                 \
-    if (wn == 2) { WH2(WOV, CPV, 2, 2, 2); }               \
-    else { WH2(WOV, CPV, 2, 1, 4); }                       \
-  }
+  if (wn == 2) { WH2(WOV, CPV, 4, 2, 1); }                 \
+  else { WH2(WOV, CPV, 4, 1, 2); }
   if (WO == 32) { WH2_WO(32, 128) }
   else if (WO == 16) { WH2_WO(16, 256) }
   else { WH2_WO(8, 256) }
