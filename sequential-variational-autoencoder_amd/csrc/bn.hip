@@ -92,7 +92,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* pre, int ldp
                                                        int nsh, float eps,
                                                        float* mean, float* invstd, long long ms_gs, const float* beta,
                                                        long long beta_gs, const float* res, int ldr, long long res_gs,
-                                                       int act, float* out, int ldo, long long out_gs, int rpb) {
+                                                       int act, float* out, int ldo, long long out_gs, int rpb,
+                                                       int out_bf16) {
   __shared__ __attribute__((aligned(16))) float sm[2][AP_QB * 4];
   __shared__ u64 tot[4 * AP_QB * 4];
   const int group = blockIdx.z;
@@ -133,7 +134,6 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* pre, int ldp
   if (rl >= RL || q >= Q) return;
   const int c = q * 4;
   pre += group * pre_gs;
-  out += group * out_gs;
   if (res) res += group * res_gs;
   const f32x4 m = *(const f32x4*)&sm[0][qi * 4], is = *(const f32x4*)&sm[1][qi * 4];
   const f32x4 b = *(const f32x4*)(beta + group * beta_gs + c);
@@ -145,17 +145,21 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* pre, int ldp
     if (res) y += *(const f32x4*)(res + r * ldr + c);
 #pragma unroll
     for (int e = 0; e < 4; ++e) y[e] = act_f(y[e], act);
-    *(f32x4*)(out + r * ldo + c) = y;
+    const long long o = group * out_gs + r * ldo + c;
+    if (out_bf16)  // read only by bf16 GEMMs, which round it the same way while staging
+      *(bf16x4_bn*)((__bf16*)out + o) = __builtin_convertvector(y, bf16x4_bn);
+    else
+      *(f32x4*)(out + o) = y;
   }
 }
 
 void bn_apply(const float* pre, int ldp, long long pre_gs, long long rows, int C, const u64* acc, long long acc_gs,
               long long sh, int nsh, float eps, float* mean, float* invstd, long long ms_gs, const float* beta, long long beta_gs,
               const float* res, int ldr, long long res_gs, int act, float* out, int ldo, long long out_gs, int groups,
-              hipStream_t s) {
+              hipStream_t s, int out_bf16) {
   const ApGrid g = ap_grid(rows, C, groups);
   hipLaunchKernelGGL(bn_apply_kernel, g.grid, dim3(256), 0, s, pre, ldp, pre_gs, rows, C, acc, acc_gs, sh, nsh, eps, mean,
-                     invstd, ms_gs, beta, beta_gs, res, ldr, res_gs, act, out, ldo, out_gs, g.rpb);
+                     invstd, ms_gs, beta, beta_gs, res, ldr, res_gs, act, out, ldo, out_gs, g.rpb, out_bf16);
 }
 
 #define BWD_RPB 256  // rows per row-block of the backward reduction

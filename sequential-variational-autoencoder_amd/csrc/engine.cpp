@@ -423,6 +423,7 @@ struct View {
   float* p = nullptr;
   int ld = 0;
   long long gs = 0;
+  int bf = 0;  // stored as bf16 (element ld / gs unchanged): only bf16 GEMMs read it (opload.h)
 };
 
 struct BNS {  // per-layer BN statistics (mean / invstd), groups x C
@@ -545,6 +546,7 @@ struct svae_ctx {
   // bf16 mode: BN-backward outputs (dpre) stored as bf16 -- their only consumers, the dgrad and
   // wgrad GEMMs, round them identically while staging (opload.h)
   int dbf = 0;
+  int abf = 0;  // bf16 mode: the post-activation tensors read only by bf16 GEMMs are stored as bf16
   float* Gimp_pub = nullptr;         // caller's improvement-loss gradient (svae_bind_imp)
   float* Gimp_v = nullptr;           // its virtual copy under weight sharing
   // BN statistics: fixed-point column accumulators (common.h stat_put), one region per BN
@@ -784,6 +786,7 @@ static int conv_bn_act_fwd(svae_ctx* c, const ConvL& L, int groups, long long w_
   a.A = in.p;
   a.a_gs = in.gs;
   a.lda = in.ld;
+  a.a_bf16 = in.bf;
   a.C = pre;
   a.c_gs = pre_gs;
   a.ldc = L.cout;
@@ -797,7 +800,7 @@ static int conv_bn_act_fwd(svae_ctx* c, const ConvL& L, int groups, long long w_
   gemm(c, a, groups);
   const long long rows = (long long)B * L.hout * L.hout;
   bn_apply(pre, L.cout, pre_gs, rows, L.cout, acc.p, acc.gs, acc.sh, acc.nsh, 1e-3f, bn.mean, bn.invstd, bn_gs, c->P + L.obeta, w_gs,
-           res.p, res.ld, res.gs, act, out.p, out.ld, out.gs, groups, c->st);
+           res.p, res.ld, res.gs, act, out.p, out.ld, out.gs, groups, c->st, out.bf);
   return 0;
 }
 
@@ -835,7 +838,7 @@ static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, V
   w.ntap = 16;
   if (!L.tr) {
     // dW[tap][ci][co] = sum_{p out} x[src(p,tap)][ci] * dpre[p][co]
-    w.G = in.p; w.g_gs = in.gs; w.ldg = in.ld;
+    w.G = in.p; w.g_gs = in.gs; w.ldg = in.ld; w.g_bf16 = in.bf;
     w.D = dpre; w.d_gs = dpre_gs; w.ldd = L.cout;
     w.d_bf16 = dpre_bf(c, L);
     w.M = L.cin; w.N = L.cout;
@@ -846,7 +849,7 @@ static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, V
     // dW[tap][co][ci] = sum_{p in} dpre[src(p,tap)][co] * x[p][ci]
     w.G = dpre; w.g_gs = dpre_gs; w.ldg = L.cout;
     w.g_bf16 = dpre_bf(c, L);
-    w.D = in.p; w.d_gs = in.gs; w.ldd = in.ld;
+    w.D = in.p; w.d_gs = in.gs; w.ldd = in.ld; w.d_bf16 = in.bf;
     w.M = L.cout; w.N = L.cin;
     w.g.Hi = w.g.Wi = L.hout;
     w.g.Ho = w.g.Wo = L.hin;
@@ -1019,7 +1022,7 @@ static int bn_act_bwd(svae_ctx* c, int groups, long long rows, int C, View dy, V
 static int fc_bn_fwd(svae_ctx* c, const FcL& f, View in, float* pre, BNS bn, View out) {
   const int B = c->m.g.B;
   FwdArgs a{};
-  a.A = in.p; a.lda = in.ld;
+  a.A = in.p; a.lda = in.ld; a.a_bf16 = in.bf;
   a.B = c->P + f.ow; a.b_nk = 0; a.ldb = f.nout; a.b_tap = 0;
   a.C = pre; a.ldc = f.nout;
   a.N = f.nout; a.Cin = f.nin;
@@ -1034,7 +1037,7 @@ static int fc_bn_fwd(svae_ctx* c, const FcL& f, View in, float* pre, BNS bn, Vie
   set_stats(a, acc);
   gemm(c, a, 1);
   bn_apply(pre, f.nout, 0, B, f.nout, acc.p, acc.gs, acc.sh, acc.nsh, 1e-3f, bn.mean, bn.invstd, 0, c->P + f.obeta, 0, nullptr, 0, 0,
-           ACT_LRELU, out.p, out.ld, 0, 1, c->st);
+           ACT_LRELU, out.p, out.ld, 0, 1, c->st, out.bf);
   return 0;
 }
 
@@ -1046,7 +1049,7 @@ static int fc_bn_bwd(svae_ctx* c, const FcL& f, View in, View dy, View y, const 
                      c->dbf);
   if (r) return r;
   WgArgs w{};
-  w.G = in.p; w.ldg = in.ld;
+  w.G = in.p; w.ldg = in.ld; w.g_bf16 = in.bf;
   w.D = sl.p; w.ldd = f.nout; w.d_bf16 = c->dbf;
   w.M = f.nin; w.N = f.nout;
   w.g.mode = GM_DENSE; w.g.nimg = B; w.g.ksz = 1; w.g.stride = 1;
@@ -1110,9 +1113,9 @@ static int inference_fwd(svae_ctx* c, int t0, int n, View in0) {
     const int Fl = F[lvl + 1];
     View in = lvl == 0 ? in0 : View{c->inf_act_b[lvl - 1] + t0 * c->inf_gs[lvl - 1], F[lvl], c->inf_gs[lvl - 1]};
     r = conv_bn_act_fwd(c, I.a[lvl], n, wg, in, c->inf_pre_a[lvl] + t0 * gs, gs, bns(c->inf_bn_a[lvl], Fl), Fl, View{},
-                        ACT_LRELU, View{c->inf_act_a[lvl] + t0 * gs, Fl, gs});
+                        ACT_LRELU, View{c->inf_act_a[lvl] + t0 * gs, Fl, gs, c->abf});
     if (r) return r;
-    r = conv_bn_act_fwd(c, I.b[lvl], n, wg, View{c->inf_act_a[lvl] + t0 * gs, Fl, gs}, c->inf_pre_b[lvl] + t0 * gs, gs,
+    r = conv_bn_act_fwd(c, I.b[lvl], n, wg, View{c->inf_act_a[lvl] + t0 * gs, Fl, gs, c->abf}, c->inf_pre_b[lvl] + t0 * gs, gs,
                         bns(c->inf_bn_b[lvl], Fl), Fl, View{}, ACT_LRELU, View{c->inf_act_b[lvl] + t0 * gs, Fl, gs});
     if (r) return r;
     for (int hl = 0; hl < L; ++hl) {
@@ -1312,17 +1315,17 @@ static int engine_forward(svae_ctx* c) {
       for (int lvl = 0; lvl < L - 1; ++lvl) {
         const int Fl = F[lvl + 1];
         r = conv_bn_act_fwd(c, E.a[lvl], 1, 0, in, s.enc_pre_a[lvl], 0, s.enc_bn_a[lvl], 0, View{}, ACT_LRELU,
-                            View{s.enc_act_a[lvl], Fl, 0});
+                            View{s.enc_act_a[lvl], Fl, 0, c->abf});
         if (r) return r;
-        r = conv_bn_act_fwd(c, E.b[lvl], 1, 0, View{s.enc_act_a[lvl], Fl, 0}, s.enc_pre_b[lvl], 0, s.enc_bn_b[lvl], 0,
+        r = conv_bn_act_fwd(c, E.b[lvl], 1, 0, View{s.enc_act_a[lvl], Fl, 0, c->abf}, s.enc_pre_b[lvl], 0, s.enc_bn_b[lvl], 0,
                             View{}, ACT_LRELU, View{s.enc_act_b[lvl], Fl, 0});
         if (r) return r;
         in = View{s.enc_act_b[lvl], Fl, 0};
       }
       r = conv_bn_act_fwd(c, E.c, 1, 0, in, s.enc_c_pre, 0, s.enc_bn_c, 0, View{}, ACT_LRELU,
-                          View{s.enc_c_act, F[L - 1], 0});
+                          View{s.enc_c_act, F[L - 1], 0, c->abf});
       if (r) return r;
-      r = fc_bn_fwd(c, E.fc, View{s.enc_c_act, S[L] * S[L] * F[L - 1], 0}, s.encfc_pre, s.enc_bn_fc,
+      r = fc_bn_fwd(c, E.fc, View{s.enc_c_act, S[L] * S[L] * F[L - 1], 0, c->abf}, s.encfc_pre, s.enc_bn_fc,
                     View{s.top_cat, s.ktop, 0});
       if (r) return r;
     }
@@ -1330,9 +1333,9 @@ static int engine_forward(svae_ctx* c) {
     if (sfc_side) hipStreamWaitEvent(st, c->ev_sfc[t], 0);
     else split_latent_fwd(c, t, st);
     // generator_ladder decoder (:1695-1721)
-    r = fc_bn_fwd(c, G.top, View{s.top_cat, s.ktop, 0}, s.top_pre, s.top_bn, View{s.top_act, S[L] * S[L] * F[L], 0});
+    r = fc_bn_fwd(c, G.top, View{s.top_cat, s.ktop, 0}, s.top_pre, s.top_bn, View{s.top_act, S[L] * S[L] * F[L], 0, c->abf});
     if (r) return r;
-    View cur{s.top_act, F[L], 0};
+    View cur{s.top_act, F[L], 0, c->abf};
     for (int lvl = L - 2; lvl >= 0; --lvl) {
       const int Fl = F[lvl + 1];
       View res = t >= 1 ? View{s.enc_act_b[lvl], Fl, 0} : View{};
@@ -1340,9 +1343,9 @@ static int engine_forward(svae_ctx* c) {
                           View{s.cat[lvl], 2 * Fl, 0});
       if (r) return r;
       r = conv_bn_act_fwd(c, G.s1[lvl], 1, 0, View{s.cat[lvl], 2 * Fl, 0}, s.s1_pre[lvl], 0, s.s1_bn[lvl], 0, View{},
-                          ACT_RELU, View{s.s1_act[lvl], Fl, 0});
+                          ACT_RELU, View{s.s1_act[lvl], Fl, 0, c->abf});
       if (r) return r;
-      cur = View{s.s1_act[lvl], Fl, 0};
+      cur = View{s.s1_act[lvl], Fl, 0, c->abf};
     }
     // output + ratio conv-T (:1720, :1727) as one 4-channel small-N gather
     {
@@ -1363,7 +1366,7 @@ static int engine_forward(svae_ctx* c) {
       if (g.bf16) {  // bf16 halo gather-GEMM, N = C+1 of one 32-column tile, bias in the epilogue
         shadow_weights(s.wpack, s.wpack_h, nullptr, 16LL * C1 * F1, nullptr, 0, nullptr, st);
         FwdArgs a{};
-        a.A = cur.p; a.lda = F1;
+        a.A = cur.p; a.lda = F1; a.a_bf16 = cur.bf;
         a.Bh = s.wpack_h; a.b_nk = 1; a.ldb = F1; a.b_tap = (long long)C1 * F1;
         a.C = s.a_out; a.ldc = C1;
         a.N = C1; a.Cin = F1;
@@ -1442,7 +1445,7 @@ static int inference_bwd(svae_ctx* c, int t0, int n, View in0, float* dx0) {
                    dpre_bf(c, I0.b[lvl]));
     if (r) return r;
     r = on_side(c, sb.ready, sb.freed, [&] {
-      return conv_wgrad(c, I0.b[lvl], n, wg, View{act_a(lvl), Fl, gs}, sb.p, gs, c->Gr + I0.b[lvl].ow);
+      return conv_wgrad(c, I0.b[lvl], n, wg, View{act_a(lvl), Fl, gs, c->abf}, sb.p, gs, c->Gr + I0.b[lvl].ow);
     });
     if (r) return r;
     BwFuse fu_ia = bw_fuse(c, pre_a(lvl), Fl, gs, nullptr, 0, 0, bns(c->inf_bn_a[lvl], Fl), Fl, I0.a[lvl].obeta, wg,
@@ -1552,7 +1555,7 @@ static int engine_backward(svae_ctx* c) {
       const int M_out = C1;
       WgArgs w{};
       w.G = c->da; w.ldg = C1;
-      w.D = s.s1_act[0]; w.ldd = F[1];
+      w.D = s.s1_act[0]; w.ldd = F[1]; w.d_bf16 = c->abf;
       w.M = M_out; w.N = F[1];
       w.g = ConvGeom{GM_CONV, B, g.H, g.W, S[1], S[1], 2, 1, 4};
       w.ntap = 16;
@@ -1637,7 +1640,7 @@ static int engine_backward(svae_ctx* c) {
       r = bn_act_bwd(c, 1, rows, Fl, View{dcat, 2 * Fl, 0}, View{s.cat[lvl], 2 * Fl, 0}, s.s2_pre[lvl], 0, Fl,
                      s.s2_bn[lvl], 0, l2.obeta, 0, ACT_RELU, sl.p, 0, dres, 0, &fu_s2, dpre_bf(c, l2));
       if (r) return r;
-      View in = lvl == L - 2 ? View{s.top_act, F[L], 0} : View{s.s1_act[lvl + 1], F[lvl + 2], 0};
+      View in = lvl == L - 2 ? View{s.top_act, F[L], 0, c->abf} : View{s.s1_act[lvl + 1], F[lvl + 2], 0, c->abf};
       r = on_side(c, sl.ready, sl.freed, [&] { return conv_wgrad(c, l2, 1, 0, in, sl.p, 0, c->Gr + l2.ow); });
       if (r) return r;
       if (lvl < L - 2) {  // next: s1[lvl+1] (no shortcut)
@@ -1686,7 +1689,7 @@ static int engine_backward(svae_ctx* c) {
     if (t >= 1) {
       const EncStep& E = M.enc[t];
       const int nc = S[L] * S[L] * F[L - 1];
-      r = fc_bn_bwd(c, E.fc, View{s.enc_c_act, nc, 0}, View{dtop, s.ktop, 0}, View{s.top_cat, s.ktop, 0},
+      r = fc_bn_bwd(c, E.fc, View{s.enc_c_act, nc, 0, c->abf}, View{dtop, s.ktop, 0}, View{s.top_cat, s.ktop, 0},
                     s.encfc_pre, s.enc_bn_fc, View{c->denc_c, nc, 0});
       if (r) return r;
       const long long rc = (long long)B * S[L] * S[L];
@@ -1713,7 +1716,7 @@ static int engine_backward(svae_ctx* c) {
                        dpre_bf(c, E.b[lvl]));
         if (r) return r;
         r = on_side(c, sb.ready, sb.freed, [&] {
-          return conv_wgrad(c, E.b[lvl], 1, 0, View{s.enc_act_a[lvl], Fl, 0}, sb.p, 0, c->Gr + E.b[lvl].ow);
+          return conv_wgrad(c, E.b[lvl], 1, 0, View{s.enc_act_a[lvl], Fl, 0, c->abf}, sb.p, 0, c->Gr + E.b[lvl].ow);
         });
         if (r) return r;
         BwFuse fu_ea = bw_fuse(c, s.enc_pre_a[lvl], Fl, 0, nullptr, 0, 0, s.enc_bn_a[lvl], 0, E.a[lvl].obeta, 0,
@@ -1982,6 +1985,8 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
   {
     const char* v = getenv("SVAE_DPRE_F32");  // A/B: keep the BN-backward outputs in fp32
     c->dbf = (c->m.g.bf16 && !(v && v[0] == '1')) ? 1 : 0;
+    const char* va = getenv("SVAE_ACT_F32");  // A/B: keep every activation in fp32
+    c->abf = (c->m.g.bf16 && !(va && va[0] == '1')) ? 1 : 0;
   }
   c->counting = true;
   c->arena_used = 0;
@@ -2439,10 +2444,14 @@ int svae_copy_out(svae_ctx* c, int which, int step, float* dst, int64_t n, void*
     case 110: src = c->dbg_last; cnt = n; break;
     case 111: c->dbg_stop_lvl2 = step; return 0;
     case 113: src = c->inf_pre_a[step]; cnt = n; break;   // debug: inference level `step`, all T groups
-    case 114: src = c->inf_act_a[step]; cnt = n; break;
+    case 114:  // (bf16-stored under abf: not a float buffer)
+      if (c->abf) return fail(c, SVAE_EBADARG, "activation stored as bf16 (SVAE_ACT_F32=1 keeps it fp32)");
+      src = c->inf_act_a[step]; cnt = n; break;
     case 115: src = c->inf_pre_b[step]; cnt = n; break;
     case 116: src = c->inf_act_b[step]; cnt = n; break;
-    case 106: src = c->sb[c->dbg_stop_step].s1_act[step]; cnt = n; break;
+    case 106:
+      if (c->abf) return fail(c, SVAE_EBADARG, "activation stored as bf16 (SVAE_ACT_F32=1 keeps it fp32)");
+      src = c->sb[c->dbg_stop_step].s1_act[step]; cnt = n; break;
     case 107: src = c->sb[c->dbg_stop_step].s1_bn[step].mean; cnt = n; break;
     case 108: src = c->sb[c->dbg_stop_step].s1_bn[step].invstd; cnt = n; break;
     default: return fail(c, SVAE_EBADARG, "unknown buffer");

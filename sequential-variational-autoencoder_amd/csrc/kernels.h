@@ -138,7 +138,7 @@ int bn_acc_shards(long long rowblocks);
 void bn_apply(const float* pre, int ldp, long long pre_gs, long long rows, int C, const u64* acc, long long acc_gs,
               long long sh, int nsh, float eps, float* mean, float* invstd, long long ms_gs, const float* beta, long long beta_gs,
               const float* res, int ldr, long long res_gs, int act, float* out, int ldo, long long out_gs, int groups,
-              hipStream_t s);
+              hipStream_t s, int out_bf16 = 0);  // out_bf16: write the activation as bf16 (RNE)
 // sums of dz and dz*xhat, dz = dy*act'(y)   -> added into acc[group][4*C]
 void bn_bwd_reduce(const float* dy, int lddy, long long dy_gs, const float* y, int ldy, long long y_gs,
                    const float* pre, int ldp, long long pre_gs, long long rows, int C, const float* mean,
