@@ -444,7 +444,7 @@ struct Probe {
 struct svae_ctx {
   Probe probe;
   // ---- backward: weight gradients on a side stream (overlap the BN / dgrad chain) ----
-  static constexpr int NR = 6;  // dpre ring slots (generator / encoder layers)
+  static constexpr int NR = 6;  // "ready" events (re-recorded in turn: each is waited on right after its record)
   bool side = false;
   hipStream_t st2 = nullptr;
   hipStream_t st3 = nullptr;  // split-latent FCs (fwd up front, bwd per level): no weight-GEMM queue ahead
@@ -456,9 +456,16 @@ struct svae_ctx {
   float* slab4 = nullptr;
   int rec_group = 0;
   float* slab2 = nullptr;
-  float* dpre_ring[NR] = {};
-  float* idpre_ring[2] = {};
-  hipEvent_t ev_ready[NR] = {}, ev_free[NR] = {}, ev_iready[2] = {}, ev_ifree[2] = {};
+  // BN-backward outputs read by the side stream's weight GEMMs: every one of a backward pass gets
+  // its own region of these arenas (bump-allocated, reset per pass), so the main stream never
+  // waits for the side stream to release a buffer -- the previous pass's side-stream work is
+  // joined into the caller's stream at its end (svae_backward).  A cross-stream wait costs the
+  // main stream a 5-7 us dispatch gap even when already satisfied (profiles/r02_v4_streams.txt).
+  float* dpre_arena = nullptr;
+  float* idpre_arena = nullptr;
+  long long dpre_cap = 0, dpre_off = 0, idpre_cap = 0, idpre_off = 0;
+  hipEvent_t ev_ready[NR] = {}, ev_iready[NR] = {};
+  hipEvent_t ev_drain = nullptr;  // arena overflow: the side stream drained before reuse
   hipEvent_t ev_da_ready = nullptr, ev_da_free = nullptr, ev_start = nullptr, ev_join = nullptr;
   int ring_pos = 0, iring_pos = 0;
   // backward step hook (data-parallel bucketed all-reduce): called on the host after the
@@ -705,19 +712,30 @@ struct Slot {
   float* p;
   hipEvent_t ready, freed;
 };
-static Slot dpre_next(svae_ctx* c) {
+// next region of `n` elements of a per-pass arena; on overflow (a geometry the plan did not
+// size) the main stream waits for the side stream to drain and the arena starts over
+static float* arena_next(svae_ctx* c, float* base, long long cap, long long& off, long long n) {
+  n = (n + 63) / 64 * 64;
+  if (off + n > cap) {
+    hipEventRecord(c->ev_drain, c->st2);
+    hipStreamWaitEvent(c->st, c->ev_drain, 0);
+    off = 0;
+  }
+  float* p = base + off;
+  off += n;
+  return p;
+}
+static Slot dpre_next(svae_ctx* c, long long n) {
   if (!c->side) return Slot{c->dpre, nullptr, nullptr};
   const int i = c->ring_pos;
   c->ring_pos = (i + 1) % svae_ctx::NR;
-  hipStreamWaitEvent(c->st, c->ev_free[i], 0);
-  return Slot{c->dpre_ring[i], c->ev_ready[i], c->ev_free[i]};
+  return Slot{arena_next(c, c->dpre_arena, c->dpre_cap, c->dpre_off, n), c->ev_ready[i], nullptr};
 }
-static Slot idpre_next(svae_ctx* c) {
+static Slot idpre_next(svae_ctx* c, long long n) {
   if (!c->side) return Slot{c->idpre, nullptr, nullptr};
   const int i = c->iring_pos;
-  c->iring_pos = (i + 1) & 1;
-  hipStreamWaitEvent(c->st, c->ev_ifree[i], 0);
-  return Slot{c->idpre_ring[i], c->ev_iready[i], c->ev_ifree[i]};
+  c->iring_pos = (i + 1) % svae_ctx::NR;
+  return Slot{arena_next(c, c->idpre_arena, c->idpre_cap, c->idpre_off, n), c->ev_iready[i], nullptr};
 }
 // run fn (weight-gradient launches) on the side stream after everything enqueued so far on the
 // main stream; the side stream uses its own split slab
@@ -733,7 +751,7 @@ static int on_side(svae_ctx* c, hipEvent_t ready, hipEvent_t freed, Fn&& fn) {
   const int r = fn();
   c->st = s0;
   c->slab = sl0;
-  hipEventRecord(freed, c->st2);
+  if (freed) hipEventRecord(freed, c->st2);
   return r;
 }
 
@@ -1044,7 +1062,7 @@ static int fc_bn_fwd(svae_ctx* c, const FcL& f, View in, float* pre, BNS bn, Vie
 // dense backward: dy wrt post-act (view), y, pre -> grads; din (=) if non-null
 static int fc_bn_bwd(svae_ctx* c, const FcL& f, View in, View dy, View y, const float* pre, BNS bn, View din) {
   const int B = c->m.g.B;
-  const Slot sl = dpre_next(c);
+  const Slot sl = dpre_next(c, (long long)B * f.nout);
   int r = bn_act_bwd(c, 1, B, f.nout, dy, y, pre, 0, f.nout, bn, 0, f.obeta, 0, ACT_LRELU, sl.p, 0, View{}, 0, nullptr,
                      c->dbf);
   if (r) return r;
@@ -1439,7 +1457,7 @@ static int inference_bwd(svae_ctx* c, int t0, int n, View in0, float* dx0) {
     const long long gs = c->inf_gs[lvl];
     const long long rows = (long long)B * S[lvl + 1] * S[lvl + 1];
     if (lvl == L - 2) heads_of(lvl);
-    Slot sb = idpre_next(c);
+    Slot sb = idpre_next(c, n * gs);
     r = bn_act_bwd(c, n, rows, Fl, View{c->idb, Fl, gs}, View{act_b(lvl), Fl, gs}, pre_b(lvl), gs, Fl,
                    bns(c->inf_bn_b[lvl], Fl), Fl, I0.b[lvl].obeta, wg, ACT_LRELU, sb.p, gs, View{}, 0, &fu_ib,
                    dpre_bf(c, I0.b[lvl]));
@@ -1452,7 +1470,7 @@ static int inference_bwd(svae_ctx* c, int t0, int n, View in0, float* dx0) {
                            ACT_LRELU, Fl);
     r = conv_dgrad(c, I0.b[lvl], n, wg, sb.p, gs, View{c->ida, Fl, gs}, 0, &fu_ia);
     if (r) return r;
-    Slot sa = idpre_next(c);
+    Slot sa = idpre_next(c, n * gs);
     r = bn_act_bwd(c, n, rows, Fl, View{c->ida, Fl, gs}, View{act_a(lvl), Fl, gs}, pre_a(lvl), gs, Fl,
                    bns(c->inf_bn_a[lvl], Fl), Fl, I0.a[lvl].obeta, wg, ACT_LRELU, sa.p, gs, View{}, 0, &fu_ia,
                    dpre_bf(c, I0.a[lvl]));
@@ -1499,9 +1517,8 @@ static int engine_backward(svae_ctx* c) {
     // re-arm the slot-free events on the main stream: the previous backward's side-stream work
     // was joined into it, so "free" holds now, and every later wait depends only on work of this
     // pass (required when the step is captured into a graph)
-    for (int i = 0; i < svae_ctx::NR; ++i) hipEventRecord(c->ev_free[i], st);
+    c->dpre_off = c->idpre_off = 0;  // the previous pass's readers were joined into this stream
     for (int i = 0; i < 2; ++i) {
-      hipEventRecord(c->ev_ifree[i], st);
       hipEventRecord(c->ev_dcat_free[i], st);
       hipEventRecord(c->ev_dtop_free[i], st);
     }
@@ -1595,7 +1612,7 @@ static int engine_backward(svae_ctx* c) {
       const ConvL& l1 = G.s1[lvl];
       const ConvL& l2 = G.s2[lvl];
       // s1: relu(BN(convT_s1(cat)))
-      Slot sl = dpre_next(c);
+      Slot sl = dpre_next(c, rows * Fl);
       r = bn_act_bwd(c, 1, rows, Fl, View{dcur, Fl, 0}, View{s.s1_act[lvl], Fl, 0}, s.s1_pre[lvl], 0, Fl, s.s1_bn[lvl],
                      0, l1.obeta, 0, ACT_RELU, sl.p, 0, View{}, 0, &fu_s1, dpre_bf(c, l1));
       if (r) return r;
@@ -1636,7 +1653,7 @@ static int engine_backward(svae_ctx* c) {
       }
       // s2: relu(BN(convT_s2(cur)) + enc_{lvl+1})
       View dres = t >= 1 ? View{c->denc[lvl], Fl, 0} : View{};
-      sl = dpre_next(c);
+      sl = dpre_next(c, rows * Fl);
       r = bn_act_bwd(c, 1, rows, Fl, View{dcat, 2 * Fl, 0}, View{s.cat[lvl], 2 * Fl, 0}, s.s2_pre[lvl], 0, Fl,
                      s.s2_bn[lvl], 0, l2.obeta, 0, ACT_RELU, sl.p, 0, dres, 0, &fu_s2, dpre_bf(c, l2));
       if (r) return r;
@@ -1693,7 +1710,7 @@ static int engine_backward(svae_ctx* c) {
                     s.encfc_pre, s.enc_bn_fc, View{c->denc_c, nc, 0});
       if (r) return r;
       const long long rc = (long long)B * S[L] * S[L];
-      Slot sl = dpre_next(c);
+      Slot sl = dpre_next(c, rc * F[L - 1]);
       r = bn_act_bwd(c, 1, rc, F[L - 1], View{c->denc_c, F[L - 1], 0}, View{s.enc_c_act, F[L - 1], 0}, s.enc_c_pre, 0,
                      F[L - 1], s.enc_bn_c, 0, E.c.obeta, 0, ACT_LRELU, sl.p, 0, View{}, 0, nullptr,
                      dpre_bf(c, E.c));
@@ -1710,7 +1727,7 @@ static int engine_backward(svae_ctx* c) {
       for (int lvl = L - 2; lvl >= 0; --lvl) {
         const int Fl = F[lvl + 1];
         const long long rows = (long long)B * S[lvl + 1] * S[lvl + 1];
-        Slot sb = dpre_next(c);
+        Slot sb = dpre_next(c, rows * Fl);
         r = bn_act_bwd(c, 1, rows, Fl, View{c->denc[lvl], Fl, 0}, View{s.enc_act_b[lvl], Fl, 0}, s.enc_pre_b[lvl], 0,
                        Fl, s.enc_bn_b[lvl], 0, E.b[lvl].obeta, 0, ACT_LRELU, sb.p, 0, View{}, 0, &fu_eb,
                        dpre_bf(c, E.b[lvl]));
@@ -1723,7 +1740,7 @@ static int engine_backward(svae_ctx* c) {
                                ACT_LRELU, Fl);
         r = conv_dgrad(c, E.b[lvl], 1, 0, sb.p, 0, View{c->dcur, Fl, 0}, 0, &fu_ea);
         if (r) return r;
-        Slot sa = dpre_next(c);
+        Slot sa = dpre_next(c, rows * Fl);
         r = bn_act_bwd(c, 1, rows, Fl, View{c->dcur, Fl, 0}, View{s.enc_act_a[lvl], Fl, 0}, s.enc_pre_a[lvl], 0, Fl,
                        s.enc_bn_a[lvl], 0, E.a[lvl].obeta, 0, ACT_LRELU, sa.p, 0, View{}, 0, &fu_ea,
                        dpre_bf(c, E.a[lvl]));
@@ -1898,7 +1915,28 @@ static bool plan(svae_ctx* c) {
   c->dcur = A(maxact);
   c->dnext = A(maxact);
   c->dpre = A(maxact);
-  for (int i = 0; i < svae_ctx::NR; ++i) c->dpre_ring[i] = A(maxact);
+  {  // one region per BN-backward output of a pass (dpre_next / idpre_next sizes, 64-element aligned)
+    const Model& M = c->m;
+    auto cl = [&](const ConvL& l) { return ((long long)B * l.hout * l.hout * l.cout + 63) / 64 * 64; };
+    auto fl = [&](const FcL& f) { return ((long long)B * f.nout + 63) / 64 * 64; };
+    long long n = 0;
+    for (int t = 0; t < T; ++t) {
+      const GenStep& G = M.gen[t];
+      for (int lvl = 0; lvl < L - 1; ++lvl) n += cl(G.s1[lvl]) + cl(G.s2[lvl]);
+      n += fl(G.top);
+      if (t >= 1) {
+        const EncStep& E = M.enc[t];
+        n += fl(E.fc) + cl(E.c);
+        for (int lvl = 0; lvl < L - 1; ++lvl) n += cl(E.a[lvl]) + cl(E.b[lvl]);
+      }
+    }
+    c->dpre_cap = n;
+    c->dpre_arena = A(n);
+    long long ni = 0;
+    for (int lvl = 0; lvl < L - 1; ++lvl) ni += 2 * (((long long)T * c->inf_gs[lvl] + 63) / 64 * 64 + 64 * T);
+    c->idpre_cap = ni;
+    c->idpre_arena = A(ni);
+  }
   c->dcat = A(maxact);
   c->dtop = A((long long)B * (F[L] + F[L + 1]));
   c->dcat_ring[0] = c->dcat;
@@ -1913,7 +1951,7 @@ static bool plan(svae_ctx* c) {
   c->idb = A((long long)T * max_inf);
   c->ida = A((long long)T * max_inf);
   c->idpre = A((long long)T * max_inf);
-  for (int i = 0; i < 2; ++i) c->idpre_ring[i] = A((long long)T * max_inf);
+
   c->bnacc_cap = 8LL << 20;  // words (64 MB); a CelebA pass takes a few M
   c->bnacc = (u64*)A(2 * c->bnacc_cap);
   c->slab_cap = 64LL << 20;
@@ -2103,8 +2141,8 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
       ok = ok && hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking) == hipSuccess;
       if (c->rec_group > 0) ok = ok && hipStreamCreateWithFlags(&c->st4, hipStreamNonBlocking) == hipSuccess;
       auto mk = [&](hipEvent_t* ev) { ok = ok && hipEventCreateWithFlags(ev, hipEventDisableTiming) == hipSuccess; };
-      for (int i = 0; i < svae_ctx::NR; ++i) { mk(&c->ev_ready[i]); mk(&c->ev_free[i]); }
-      for (int i = 0; i < 2; ++i) { mk(&c->ev_iready[i]); mk(&c->ev_ifree[i]); }
+      for (int i = 0; i < svae_ctx::NR; ++i) { mk(&c->ev_ready[i]); mk(&c->ev_iready[i]); }
+      mk(&c->ev_drain);
       mk(&c->ev_da_ready); mk(&c->ev_da_free); mk(&c->ev_start); mk(&c->ev_join); mk(&c->ev_hook);
       mk(&c->ev_aux); mk(&c->ev_aux2); mk(&c->ev_dz); mk(&c->ev_j3); mk(&c->ev_j4);
       for (int i = 0; i < 2; ++i) { mk(&c->ev_dcat_free[i]); mk(&c->ev_dtop_free[i]); }
@@ -2131,12 +2169,9 @@ int svae_destroy(svae_ctx* c) {
     if (ev) hipEventDestroy(ev);
   for (int i = 0; i < svae_ctx::NR; ++i) {
     if (c->ev_ready[i]) hipEventDestroy(c->ev_ready[i]);
-    if (c->ev_free[i]) hipEventDestroy(c->ev_free[i]);
-  }
-  for (int i = 0; i < 2; ++i) {
     if (c->ev_iready[i]) hipEventDestroy(c->ev_iready[i]);
-    if (c->ev_ifree[i]) hipEventDestroy(c->ev_ifree[i]);
   }
+  if (c->ev_drain) hipEventDestroy(c->ev_drain);
   for (hipEvent_t ev : c->probe.ev) hipEventDestroy(ev);
   if (c->arena) hipFree(c->arena);
   if (c->adam_m) hipFree(c->adam_m);

@@ -24,3 +24,17 @@ for sid in sorted({r[3] for r in step}):
     print("stream", sid, "launches", sum(c.values()), "busy %.1f us" % sum(tot.values()))
     for k, v in sorted(tot.items(), key=lambda kv: -kv[1])[:top]:
         print("  %-50s %4d %8.1f  avg %6.1f" % (k, c[k], v, v / c[k]))
+
+# main-stream idle gaps: launch boundaries (~1.5-2 us) vs waits on the side streams' events
+main = max({r[3] for r in step}, key=lambda sid: sum(1 for r in step if r[3] == sid))
+ms = [r for r in step if r[3] == main]
+gaps = [(ms[i + 1][1] - ms[i][2]) / 1e3 for i in range(len(ms) - 1)]
+bins = [(0, 2), (2, 4), (4, 10), (10, 50), (50, 1e9)]
+print("main stream %d idle gaps, total %.1f us" % (len(gaps), sum(gaps)))
+for lo, hi in bins:
+    sel = [g for g in gaps if lo <= g < hi]
+    print("  gap [%g, %g) us: %4d gaps, %8.1f us" % (lo, hi, len(sel), sum(sel)))
+name = lambda n: n.replace('void ', '').replace('(anonymous namespace)::', '').split('(')[0][:40]
+order = sorted(range(len(gaps)), key=lambda i: -gaps[i])[:int(sys.argv[3]) if len(sys.argv) > 3 else 20]
+for i in sorted(order):
+    print("  %7.1f us after %-40s before %-40s" % (gaps[i], name(ms[i][0]), name(ms[i + 1][0])))
