@@ -1,0 +1,116 @@
+/* PixelCNN++ decoder head: C ABI of the MI355X kernels.
+ *
+ * Replaces the TF graph that pixel_cnn/pixelvae.py:68-158 builds over
+ * pixel_cnn/pixel_cnn_pp/model.py:11-117 and nn.py:46-320 (every op below cites the reference
+ * function it computes).  Plain pointers (device memory), sizes and a hipStream_t passed as
+ * void*; every tensor is NHWC fp32 with an explicit pixel stride (ld, in elements).
+ *
+ * Convolution geometry (one gather rule for every conv / deconv and their input gradients):
+ *   mode 0 (conv):       out(oy, ox) += in(oy*s - pt + ky, ox*s - pl + kx) . W[ky][kx]
+ *   mode 1 (transposed): out(oy, ox) += in(iy, ix) . W[ky][kx]  where  iy*s + ky = oy + pt,
+ *                                                                      ix*s + kx = ox + pl
+ * Out-of-image sources read zero.  nn.down_shifted_conv2d = mode 0, pt = kh-1, pl = (kw-1)/2;
+ * nn.down_right_shifted_conv2d: pt = kh-1, pl = kw-1; nn.down_shifted_deconv2d (stride 2, VALID,
+ * cropped): mode 1, pt = 0, pl = (kw-1)/2.  The input gradient of a mode-m op is the mode-(1-m)
+ * op with the same s, pt, pl over the output gradient and the transposed weight copy.
+ *
+ * Weights: canonical V [kh][kw][Cin][Cout] fp32 (nn.py's weight norm W = g V / ||V||, the norm
+ * over all axes but Cout).  svae_pcnn_wnorm writes the two bf16 copies the bf16-MFMA kernels read:
+ *   wk_f [tap][Cout][kf]  (forward: K = Cin contiguous, zero-padded to kf = roundup(Cin, 16))
+ *   wk_d [tap][Cin][kd]   (input gradient: K = Cout contiguous, kd = roundup(Cout, 16))
+ * Returns 0 on success, a negative SVAE_E* code on bad arguments (message: svae_last_error of a NULL context).
+ */
+#ifndef SVAE_PCNN_H
+#define SVAE_PCNN_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* nn.conv2d / deconv2d / dense weight norm (nn.py:173, :201, :236): norm[co] = ||V[..,co]||,
+ * W = g / norm * V into both bf16 copies (either may be NULL). */
+int svae_pcnn_wnorm(const float* V, const float* g, int taps, int cin, int cout, float* norm, void* wk_f, int kf,
+                    void* wk_d, int kd, void* stream);
+/* weight-norm backward: dW [tap][Cin][Cout] -> dg[co] = sum dW . V / norm,
+ * dV = g / norm (dW - dg V / norm)  (written, not accumulated). */
+int svae_pcnn_wnorm_bwd(const float* V, const float* g, const float* norm, const float* dW, int taps, int cin,
+                        int cout, float* dV, float* dg, void* stream);
+
+/* gather conv (bf16 MFMA, fp32 accumulate): y[rows][ldy] (rows = n*ho*wo) = gather(x) . wk
+ * (+ bias); wk [tap][cout][kpad]; accumulate: y += result; zero_edge 1 / 2: output row oy == 0 /
+ * column ox == 0 written as 0 (nn.down_shift / right_shift folded in: pass pt + 1 / pl + 1). */
+int svae_pcnn_conv(const float* x, int n, int hi, int wi, int cin, int ldx, const void* wk, int kpad,
+                   const float* bias, float* y, int ho, int wo, int cout, int ldy, int kh, int kw, int s, int pt,
+                   int pl, int mode, int accumulate, int zero_edge, void* stream);
+/* weight gradient of that conv: dW[tap][cin][cout] = sum_rows gather(x)[row][ci] . dy[row][co]
+ * (split over rows into `scratch` slabs, then a fixed-order reduce: deterministic). */
+int svae_pcnn_conv_wgrad(const float* x, int n, int hi, int wi, int cin, int ldx, const float* dy, int ldd, int ho,
+                         int wo, int cout, int kh, int kw, int s, int pt, int pl, int mode, float* dW, float* scratch,
+                         int64_t scratch_elems, void* stream);
+/* column sums over rows (bias gradients): out[c] (+)= sum_r x[r][c]; mask_edge 1 / 2 skips
+ * rows with oy == 0 / ox == 0 of a [n][ho][wo] row space (the zeroed shifted outputs). */
+int svae_pcnn_colsum(const float* x, int64_t rows, int c, int ldx, int ho, int wo, int mask_edge, float* out,
+                     int accumulate, float* scratch, void* stream);
+/* zero the rows / columns a zero_edge conv wrote as 0 (its output gradient there is dead). */
+int svae_pcnn_mask_edge(float* x, int n, int ho, int wo, int c, int ldx, int mask_edge, void* stream);
+
+/* resnet nonlinearity (model.py:24-31): kind 0 relu, 1 elu, 2 concat_elu (y has 2c channels
+ * [elu(x), elu(-x)], nn.py:12-15). */
+int svae_pcnn_nonlin(const float* x, int64_t rows, int c, int ldx, int kind, float* y, int ldy, void* stream);
+/* its backward: dx (+)= dy . f'(x) */
+int svae_pcnn_nonlin_bwd(const float* x, int64_t rows, int c, int ldx, int kind, const float* dy, int ldy, float* dx,
+                         int lddx, int accumulate, void* stream);
+
+/* gated_resnet tail (nn.py:283-288): with c2 = [a | b] (2f channels) + hp[img] (h . hw):
+ * out = x + a . sigmoid(b). */
+int svae_pcnn_gate(const float* x, int ldx, const float* c2, const float* hp, int64_t rows, int pix_per_img, int f,
+                   float* out, int ldo, void* stream);
+/* its backward from the saved c2 and hp: dc2 [rows][2f] = [dout . sig(b), dout . a . sig'(b)]
+ * (the residual's gradient dx is dout itself). */
+int svae_pcnn_gate_bwd(const float* c2, const float* hp, const float* dout, int lddo, int64_t rows, int pix_per_img,
+                       int f, float* dc2, void* stream);
+
+/* small fp32 GEMM (conditioning projections, highway FC): C[m][n] = beta C + sum_k A(m,k) B(k,n),
+ * A(m,k) = ta ? A[k*lda + m] : A[m*lda + k], B(k,n) = tb ? B[n*ldb + k] : B[k*ldb + n]. */
+int svae_pcnn_gemm_small(const float* A, int lda, int ta, const float* B, int ldb, int tb, float* C, int ldc, int m,
+                         int n, int k, float beta, void* stream);
+/* per-image channel sums: out[img][c] = sum_{p < pix_per_img} x[img*pix + p][c]. */
+int svae_pcnn_imgsum(const float* x, int ldx, int nimg, int pix_per_img, int c, float* out, void* stream);
+
+/* strided channel copy: y[r][0..c) = x[r][0..c) (concat / split of channel slices). */
+int svae_pcnn_copy(const float* x, int ldx, int64_t rows, int c, float* y, int ldy, int accumulate, void* stream);
+/* x_pad (model.py:37): y[r] = [x[r][0..c), 1, 0 ...] with ldy channels. */
+int svae_pcnn_pad_ones(const float* x, int64_t rows, int c, float* y, int ldy, void* stream);
+
+/* discretized_mix_logistic_loss (nn.py:46-87) per pixel and its gradient: logp[p] = log p(x_p)
+ * (the negated loss summand), dl[p][10m] = coef * d(-logp_p)/dl (skipped if dl == NULL).
+ * x [pixels][3] in [-1, 1], l [pixels][10 m]. */
+int svae_pcnn_mixlogistic(const float* x, const float* l, int64_t pixels, int m, float* logp, float* dl, float coef,
+                          void* stream);
+/* fixed-order sum of n floats into out[0] (fp64 accumulation, written as fp32 and fp64). */
+int svae_pcnn_sum(const float* x, int64_t n, float* out, double* out64, void* stream);
+/* sample_from_discretized_mix_logistic (nn.py:89-109) with its uniforms given:
+ * u_mix [pixels][m], u_log [pixels][3] (pixels = nimg * per_img); only the positions q in [q0, q1)
+ * of every image are written (x [pixels][pix_stride]): one autoregressive step writes one q. */
+int svae_pcnn_sample(const float* l, const float* u_mix, const float* u_log, int nimg, int per_img, int m, float* x,
+                     int q0, int q1, int pix_stride, void* stream);
+/* highway mix (pixelvae.py:135-137): out = r . s + (1 - r) . prev,
+ * r = lo + (hi - lo) sigmoid(z[img] + zb[0]) (z = latents . W of the 1-unit FC; zb its bias or NULL). */
+int svae_pcnn_highway(const float* s, const float* prev, const float* z, const float* zb, int nimg, int64_t per_img,
+                      float lo, float hi, float* out, float* ratio, void* stream);
+
+/* data-dependent init (nn.py:176-180, :206-210): column moments of y [rows][c] (fp64), then
+ * g *= scale / sqrt(v + 1e-10), b -= m * scale / sqrt(v + 1e-10). */
+int svae_pcnn_wn_init(const float* y, int64_t rows, int c, int ldy, float init_scale, float* g, float* b,
+                      double* scratch, void* stream);
+/* TF Adam (tf.train.AdamOptimizer semantics as sequential_vae.py's optimiser, with the gradient
+ * clipped to +-clip) on a flat buffer; and the Polyak EMA (pixelvae.py:113-114). */
+int svae_pcnn_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, int64_t step, float clip,
+                   void* stream);
+int svae_pcnn_ema(float* avg, const float* p, int64_t n, float decay, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -98,6 +98,30 @@ def lib():
         "svae_backward_imp": ([vp, vp], i32),
         "svae_adam_imp": ([vp, f32, i64, f32, vp], i32),
         "svae_imp_range": ([vp, ctypes.POINTER(i64)], i32),
+        # PixelCNN++ head (include/svae_pcnn.h)
+        "svae_pcnn_wnorm": ([vp, vp, i32, i32, i32, vp, vp, i32, vp, i32, vp], i32),
+        "svae_pcnn_wnorm_bwd": ([vp, vp, vp, vp, i32, i32, i32, vp, vp, vp], i32),
+        "svae_pcnn_conv": ([vp, i32, i32, i32, i32, i32, vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32,
+                            i32, i32, i32, i32, vp], i32),
+        "svae_pcnn_conv_wgrad": ([vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32,
+                                  vp, vp, i64, vp], i32),
+        "svae_pcnn_colsum": ([vp, i64, i32, i32, i32, i32, i32, vp, i32, vp, vp], i32),
+        "svae_pcnn_mask_edge": ([vp, i32, i32, i32, i32, i32, i32, vp], i32),
+        "svae_pcnn_nonlin": ([vp, i64, i32, i32, i32, vp, i32, vp], i32),
+        "svae_pcnn_nonlin_bwd": ([vp, i64, i32, i32, i32, vp, i32, vp, i32, i32, vp], i32),
+        "svae_pcnn_gate": ([vp, i32, vp, vp, i64, i32, i32, vp, i32, vp], i32),
+        "svae_pcnn_gate_bwd": ([vp, vp, vp, i32, i64, i32, i32, vp, vp], i32),
+        "svae_pcnn_gemm_small": ([vp, i32, i32, vp, i32, i32, vp, i32, i32, i32, i32, f32, vp], i32),
+        "svae_pcnn_imgsum": ([vp, i32, i32, i32, i32, vp, vp], i32),
+        "svae_pcnn_copy": ([vp, i32, i64, i32, vp, i32, i32, vp], i32),
+        "svae_pcnn_pad_ones": ([vp, i64, i32, vp, i32, vp], i32),
+        "svae_pcnn_mixlogistic": ([vp, vp, i64, i32, vp, vp, f32, vp], i32),
+        "svae_pcnn_sum": ([vp, i64, vp, vp, vp], i32),
+        "svae_pcnn_sample": ([vp, vp, vp, i32, i32, i32, vp, i32, i32, i32, vp], i32),
+        "svae_pcnn_highway": ([vp, vp, vp, vp, i32, i64, f32, f32, vp, vp, vp], i32),
+        "svae_pcnn_wn_init": ([vp, i64, i32, i32, f32, vp, vp, vp, vp], i32),
+        "svae_pcnn_adam": ([vp, vp, vp, vp, i64, f32, i64, f32, vp], i32),
+        "svae_pcnn_ema": ([vp, vp, i64, f32, vp], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -114,6 +138,12 @@ EXPORTED = ["svae_param_count", "svae_param_layout", "svae_create", "svae_destro
             "svae_op_gather_bf16", "svae_op_wgrad_bf16", "svae_generate", "svae_set_backward_hook",
             "svae_hook_stream", "svae_adam_range", "svae_backward_adam", "svae_adam_state",
             "svae_set_chain_noise", "svae_bind_imp", "svae_backward_imp", "svae_adam_imp", "svae_imp_range"]
+# include/svae_pcnn.h (the PixelCNN++ head)
+PCNN_EXPORTED = ["svae_pcnn_wnorm", "svae_pcnn_wnorm_bwd", "svae_pcnn_conv", "svae_pcnn_conv_wgrad", "svae_pcnn_colsum",
+                 "svae_pcnn_mask_edge", "svae_pcnn_nonlin", "svae_pcnn_nonlin_bwd", "svae_pcnn_gate",
+                 "svae_pcnn_gate_bwd", "svae_pcnn_gemm_small", "svae_pcnn_imgsum", "svae_pcnn_copy",
+                 "svae_pcnn_pad_ones", "svae_pcnn_mixlogistic", "svae_pcnn_sum", "svae_pcnn_sample",
+                 "svae_pcnn_highway", "svae_pcnn_wn_init", "svae_pcnn_adam", "svae_pcnn_ema"]
 
 # bf16 GEMM instance ids (csrc/kernels.h KernelId) for svae_probe_begin
 KID_IGEMM_BF16_256x32 = 2

@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 OUT = os.path.join(HERE, "libsvae_hip.so")
-SOURCES = ["gemm.hip", "gemm_bf16.hip", "wgrad_halo2.hip", "smallc.hip", "bn.hip", "misc.hip", "chain.hip", "halo_kw.hip", "engine.cpp"]
+SOURCES = ["gemm.hip", "gemm_bf16.hip", "wgrad_halo2.hip", "smallc.hip", "bn.hip", "misc.hip", "chain.hip", "halo_kw.hip", "pcnn.hip", "engine.cpp"]
 HEADERS = ["common.h", "kernels.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-mcode-object-version=5",
@@ -29,7 +29,7 @@ def build(force=False, verbose=False):
     bdir = os.path.join(CSRC, "build")
     os.makedirs(bdir, exist_ok=True)
     hdr_t = max(_mtime(os.path.join(CSRC, h)) for h in HEADERS)
-    hdr_t = max(hdr_t, _mtime(os.path.join(INCLUDE, "svae_hip.h")))
+    hdr_t = max(hdr_t, _mtime(os.path.join(INCLUDE, "svae_hip.h")), _mtime(os.path.join(INCLUDE, "svae_pcnn.h")))
     jobs = []
     objs = []
     for src in SOURCES:

@@ -416,6 +416,9 @@ thread_local std::string g_tls_err;
 
 }  // namespace
 
+// the context-free ops of other translation units (pcnn.hip) report through svae_last_error(NULL)
+void svae_tls_error(const std::string& msg) { g_tls_err = msg; }
+
 // ============================================================================
 // engine context
 // ============================================================================

@@ -1,0 +1,908 @@
+// PixelCNN++ decoder head on gfx950: weight-normed shifted convolutions as
+// bf16-MFMA gather GEMMs, their weight gradients, the gated-resnet / nonlinearity elementwise
+// ops, the discretized logistic mixture loss (forward + analytic gradient in one pass) and its
+// sampler.  C ABI: include/svae_pcnn.h.  Reference: pixel_cnn/pixel_cnn_pp/{model,nn}.py,
+// pixel_cnn/pixelvae.py (cited per function).
+#include <math.h>
+#include <string>
+
+#include "common.h"
+#include "kernels.h"
+#include "svae_hip.h"
+#include "svae_pcnn.h"
+
+void svae_tls_error(const std::string& msg);  // engine.cpp: svae_last_error(NULL)
+
+namespace {
+
+typedef __bf16 pc_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float pc_f32x8 __attribute__((ext_vector_type(8)));
+
+int bad(const char* msg) {
+  svae_tls_error(msg);
+  return SVAE_EBADARG;
+}
+int hipchk() {
+  const hipError_t e = hipGetLastError();
+  if (e == hipSuccess) return 0;
+  svae_tls_error(std::string("HIP: ") + hipGetErrorString(e));
+  return SVAE_EHIP;
+}
+int blocks_for(long long n, int per = 256, int cap = 16384) {
+  long long b = (n + per - 1) / per;
+  if (b < 1) b = 1;
+  return (int)(b < cap ? b : cap);
+}
+
+// ---------------------------------------------------------------------------------------------
+// gather geometry (svae_pcnn.h): source pixel of output pixel (oy, ox) for tap (ky, kx)
+// ---------------------------------------------------------------------------------------------
+struct PcGeom {
+  int n, hi, wi, cin, ldx;  // gathered operand
+  int ho, wo, cout;         // row space (output pixels) and output channels
+  int kh, kw, s, pt, pl, mode;
+};
+
+__device__ __forceinline__ bool pc_src(const PcGeom& g, int oy, int ox, int ky, int kx, int& iy, int& ix) {
+  if (g.mode == 0) {
+    iy = oy * g.s - g.pt + ky;
+    ix = ox * g.s - g.pl + kx;
+  } else {
+    const int ty = oy + g.pt - ky, tx = ox + g.pl - kx;
+    if (ty < 0 || tx < 0) return false;
+    if (g.s == 2) {
+      if ((ty | tx) & 1) return false;
+      iy = ty >> 1;
+      ix = tx >> 1;
+    } else {
+      iy = ty;
+      ix = tx;
+    }
+  }
+  return iy >= 0 && iy < g.hi && ix >= 0 && ix < g.wi;
+}
+
+// ---------------------------------------------------------------------------------------------
+// weight norm (nn.py:173, :201, :236)
+// ---------------------------------------------------------------------------------------------
+// norm[co] = sqrt(sum_{tap, ci} V^2): one block per 64 output channels, fixed-order sums
+__global__ __launch_bounds__(256) void wn_norm_kernel(const float* __restrict__ V, int K, int cout,
+                                                      float* __restrict__ norm) {
+  __shared__ double red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6;
+  double s = 0.0;
+  if (c < cout)
+    for (int k = q; k < K; k += 4) {
+      const double v = V[(long long)k * cout + c];
+      s += v * v;
+    }
+  red[q][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (q == 0 && c < cout) norm[c] = (float)sqrt(red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                                                red[3][threadIdx.x]);
+}
+
+// W = g / norm * V -> wk_f [tap][co][kf] (K = ci) and wk_d [tap][ci][kd] (K = co), zero padded
+__global__ void wn_apply_kernel(const float* __restrict__ V, const float* __restrict__ g,
+                                const float* __restrict__ norm, int taps, int cin, int cout, __bf16* wk_f, int kf,
+                                __bf16* wk_d, int kd) {
+  const long long nf = wk_f ? (long long)taps * cout * kf : 0, nd = wk_d ? (long long)taps * cin * kd : 0;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nf + nd; i += stride) {
+    if (i < nf) {
+      const int ci = (int)(i % kf);
+      const long long r = i / kf;
+      const int co = (int)(r % cout), tap = (int)(r / cout);
+      float w = 0.f;
+      if (ci < cin) w = V[((long long)tap * cin + ci) * cout + co] * (g[co] / norm[co]);
+      wk_f[i] = (__bf16)w;
+    } else {
+      const long long j = i - nf;
+      const int co = (int)(j % kd);
+      const long long r = j / kd;
+      const int ci = (int)(r % cin), tap = (int)(r / cin);
+      float w = 0.f;
+      if (co < cout) w = V[((long long)tap * cin + ci) * cout + co] * (g[co] / norm[co]);
+      wk_d[j] = (__bf16)w;
+    }
+  }
+}
+
+// dg[co] = sum_k dW V / norm  (fixed order, fp64)
+__global__ __launch_bounds__(256) void wn_dg_kernel(const float* __restrict__ V, const float* __restrict__ dW,
+                                                    const float* __restrict__ norm, int K, int cout,
+                                                    float* __restrict__ dg) {
+  __shared__ double red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6;
+  double s = 0.0;
+  if (c < cout)
+    for (int k = q; k < K; k += 4) s += (double)dW[(long long)k * cout + c] * V[(long long)k * cout + c];
+  red[q][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (q == 0 && c < cout)
+    dg[c] = (float)((red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]) / norm[c]);
+}
+
+__global__ void wn_dv_kernel(const float* __restrict__ V, const float* __restrict__ g, const float* __restrict__ norm,
+                             const float* __restrict__ dW, const float* __restrict__ dg, long long n, int cout,
+                             float* __restrict__ dV) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int c = (int)(i % cout);
+    const float in = 1.f / norm[c];
+    dV[i] = g[c] * in * (dW[i] - dg[c] * in * V[i]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// gather conv: one wave = 32 output pixels x 32*NT output channels, fragments straight from
+// HBM/L2 (no LDS: each lane's A row is its own gathered pixel, 8 consecutive channels = two 16-B
+// loads; B rows are 16-B bf16 runs of the K-contiguous weight copy).  4 waves per block stacked
+// along the pixels, so the block's B fragments are shared through L1.
+// ---------------------------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(256) void pc_conv_kernel(PcGeom g, const float* __restrict__ X,
+                                                      const __bf16* __restrict__ Wk, int kpad,
+                                                      const float* __restrict__ bias, float* __restrict__ Y, int ldy,
+                                                      int accumulate, int zero_edge) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l32 = lane & 31, h = lane >> 5;
+  const int per_img = g.ho * g.wo;
+  const long long rows = (long long)g.n * per_img;
+  const long long m0 = ((long long)blockIdx.x * 4 + wave) * 32;
+  if (m0 >= rows) return;
+  const int n0 = blockIdx.y * 32 * NT;
+  const long long m = m0 + l32;
+  const bool mv = m < rows;
+  int img = 0, oy = 0, ox = 0;
+  if (mv) {
+    img = (int)(m / per_img);
+    const int r = (int)(m - (long long)img * per_img);
+    oy = r / g.wo;
+    ox = r - oy * g.wo;
+  }
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  const int ntap = g.kh * g.kw;
+  for (int tap = 0; tap < ntap; ++tap) {
+    const int ky = tap / g.kw, kx = tap - ky * g.kw;
+    int iy = 0, ix = 0;
+    const bool v = mv && pc_src(g, oy, ox, ky, kx, iy, ix);
+    const float* xp = X + ((long long)(img * g.hi + iy) * g.wi + ix) * g.ldx;
+    const __bf16* wp = Wk + (long long)tap * g.cout * kpad;
+#pragma unroll 2
+    for (int k0 = 0; k0 < kpad; k0 += 16) {
+      const int ci = k0 + 8 * h;
+      f32x4 lo = {0.f, 0.f, 0.f, 0.f}, hi = {0.f, 0.f, 0.f, 0.f};
+      if (v) {
+        if (ci < g.cin) lo = *(const f32x4*)(xp + ci);
+        if (ci + 4 < g.cin) hi = *(const f32x4*)(xp + ci + 4);
+      }
+      const pc_f32x8 a8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const pc_bf16x8 af = __builtin_convertvector(a8, pc_bf16x8);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n = n0 + t * 32 + l32;
+        pc_bf16x8 bf = {};
+        if (n < g.cout) bf = *(const pc_bf16x8*)(wp + (long long)n * kpad + ci);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc[t], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const long long mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (mm >= rows) continue;
+    bool zero = false;
+    if (zero_edge) {
+      const int rr = (int)(mm % per_img);
+      zero = zero_edge == 1 ? (rr / g.wo == 0) : (rr % g.wo == 0);
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int n = n0 + t * 32 + l32;
+      if (n >= g.cout) continue;
+      float val = zero ? 0.f : acc[t][r] + (bias ? bias[n] : 0.f);
+      float* p = Y + mm * ldy + n;
+      if (accumulate) val += *p;
+      *p = val;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// weight gradient: block = one tap x 64 ci x 64 co (2 x 2 waves of 32 x 32), K = a split of the
+// output rows in chunks of 32, staged through LDS transposed (row-contiguous per channel, so
+// each MFMA fragment is one 16-B LDS read).  Partial slabs [split][tap][ci][co].
+// ---------------------------------------------------------------------------------------------
+#define PW_RP 40  // LDS row pitch (bf16): 32 rows + 8 pad
+__global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const float* __restrict__ X,
+                                                       const float* __restrict__ D, int ldd, long long rows,
+                                                       long long rows_per_split, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) __bf16 Xs[64 * PW_RP];
+  __shared__ __attribute__((aligned(16))) __bf16 Ds[64 * PW_RP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int nci = (g.cin + 63) / 64;
+  const int ci0 = (blockIdx.x % nci) * 64, co0 = (blockIdx.x / nci) * 64;
+  const int tap = blockIdx.y, split = blockIdx.z;
+  const int ky = tap / g.kw, kx = tap - ky * g.kw;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int per_img = g.ho * g.wo;
+  const long long r0 = (long long)split * rows_per_split;
+  long long r1 = r0 + rows_per_split;
+  if (r1 > rows) r1 = rows;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  // staging role: row lr = tid >> 3 (0..31), channel quads q = tid & 7 and q + 8
+  const int lr = tid >> 3, q0 = tid & 7;
+  for (long long rc = r0; rc < r1; rc += 32) {
+    const long long row = rc + lr;
+    const float* xp = nullptr;
+    const float* dp = nullptr;
+    if (row < r1) {
+      const int img = (int)(row / per_img);
+      const int rr = (int)(row - (long long)img * per_img);
+      const int oy = rr / g.wo, ox = rr - (rr / g.wo) * g.wo;
+      int iy, ix;
+      if (pc_src(g, oy, ox, ky, kx, iy, ix)) xp = X + ((long long)(img * g.hi + iy) * g.wi + ix) * g.ldx;
+      dp = D + row * ldd;
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = (q0 + 8 * j) * 4;
+      f32x4 xv = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
+      if (xp && ci0 + c < g.cin) xv = *(const f32x4*)(xp + ci0 + c);
+      if (dp && co0 + c < g.cout) dv = *(const f32x4*)(dp + co0 + c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        Xs[(c + e) * PW_RP + lr] = (__bf16)xv[e];
+        Ds[(c + e) * PW_RP + lr] = (__bf16)dv[e];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kq = 0; kq < 2; ++kq) {
+      const pc_bf16x8 af = *(const pc_bf16x8*)&Xs[(wm * 32 + l32) * PW_RP + kq * 16 + 8 * h];
+      const pc_bf16x8 bf = *(const pc_bf16x8*)&Ds[(wn * 32 + l32) * PW_RP + kq * 16 + 8 * h];
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  float* out = part + ((long long)split * g.kh * g.kw + tap) * g.cin * g.cout;
+  const int co = co0 + wn * 32 + l32;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int ci = ci0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (ci < g.cin && co < g.cout) out[(long long)ci * g.cout + co] = acc[r];
+  }
+}
+
+__global__ void split_reduce_kernel(const float* __restrict__ part, int nsplit, long long n, float* __restrict__ out) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float s = 0.f;
+    for (int k = 0; k < nsplit; ++k) s += part[(long long)k * n + i];
+    out[i] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// column sums (bias gradients) and edge masks
+// ---------------------------------------------------------------------------------------------
+// stage 1: blockIdx.x = 64-column group, blockIdx.y = row split -> scratch[split][c]
+__global__ __launch_bounds__(256) void colsum_part_kernel_pc(const float* __restrict__ x, long long rows, int c,
+                                                             int ldx, int per_img, int wo, int mask_edge,
+                                                             long long rows_per_split, float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6;
+  const long long r0 = (long long)blockIdx.y * rows_per_split;
+  long long r1 = r0 + rows_per_split;
+  if (r1 > rows) r1 = rows;
+  float s = 0.f;
+  if (col < c)
+    for (long long r = r0 + q; r < r1; r += 4) {
+      if (mask_edge) {
+        const int rr = (int)(r % per_img);
+        if (mask_edge == 1 ? (rr / wo == 0) : (rr % wo == 0)) continue;
+      }
+      s += x[r * ldx + col];
+    }
+  red[q][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (q == 0 && col < c)
+    part[(long long)blockIdx.y * c + col] =
+        red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+__global__ void colsum_fin_kernel_pc(const float* __restrict__ part, int nsplit, int c, float* __restrict__ out,
+                                     int accumulate) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= c) return;
+  float s = 0.f;
+  for (int k = 0; k < nsplit; ++k) s += part[(long long)k * c + col];
+  out[col] = accumulate ? out[col] + s : s;
+}
+
+__global__ void mask_edge_kernel(float* x, long long n_rows, int per_img, int wo, int c, int ldx, int mask_edge) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long total = n_rows * c;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const long long r = i / c;
+    const int rr = (int)(r % per_img);
+    if (mask_edge == 1 ? (rr / wo == 0) : (rr % wo == 0)) x[r * ldx + (int)(i % c)] = 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// elementwise ops
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float elu_f(float x) { return x > 0.f ? x : expm1f(x); }
+__device__ __forceinline__ float delu_f(float x) { return x > 0.f ? 1.f : expf(x); }
+
+__global__ void nonlin_kernel(const float* __restrict__ x, long long rows, int c, int ldx, int kind,
+                              float* __restrict__ y, int ldy) {
+  const long long stride = (long long)gridDim.x * blockDim.x, total = rows * c;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const long long r = i / c;
+    const int j = (int)(i - r * c);
+    const float v = x[r * ldx + j];
+    if (kind == 0) {
+      y[r * ldy + j] = fmaxf(v, 0.f);
+    } else if (kind == 1) {
+      y[r * ldy + j] = elu_f(v);
+    } else {
+      y[r * ldy + j] = elu_f(v);
+      y[r * ldy + c + j] = elu_f(-v);
+    }
+  }
+}
+
+__global__ void nonlin_bwd_kernel(const float* __restrict__ x, long long rows, int c, int ldx, int kind,
+                                  const float* __restrict__ dy, int ldy, float* __restrict__ dx, int lddx,
+                                  int accumulate) {
+  const long long stride = (long long)gridDim.x * blockDim.x, total = rows * c;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const long long r = i / c;
+    const int j = (int)(i - r * c);
+    const float v = x[r * ldx + j];
+    float d;
+    if (kind == 0) d = v > 0.f ? dy[r * ldy + j] : 0.f;  // tf.nn.relu: relu'(0) = 0
+    else if (kind == 1) d = dy[r * ldy + j] * delu_f(v);
+    else d = dy[r * ldy + j] * delu_f(v) - dy[r * ldy + c + j] * delu_f(-v);
+    float* p = dx + r * lddx + j;
+    *p = accumulate ? *p + d : d;
+  }
+}
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+
+__global__ void gate_kernel(const float* __restrict__ x, int ldx, const float* __restrict__ c2,
+                            const float* __restrict__ hp, long long rows, int per_img, int f, float* __restrict__ out,
+                            int ldo) {
+  const long long stride = (long long)gridDim.x * blockDim.x, total = rows * f;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const long long r = i / f;
+    const int j = (int)(i - r * f);
+    const long long img = r / per_img;
+    float a = c2[r * 2 * f + j], b = c2[r * 2 * f + f + j];
+    if (hp) {
+      a += hp[img * 2 * f + j];
+      b += hp[img * 2 * f + f + j];
+    }
+    out[r * ldo + j] = x[r * ldx + j] + a * sigm(b);
+  }
+}
+
+__global__ void gate_bwd_kernel(const float* __restrict__ c2, const float* __restrict__ hp,
+                                const float* __restrict__ dout, int lddo, long long rows, int per_img, int f,
+                                float* __restrict__ dc2) {
+  const long long stride = (long long)gridDim.x * blockDim.x, total = rows * f;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const long long r = i / f;
+    const int j = (int)(i - r * f);
+    const long long img = r / per_img;
+    float a = c2[r * 2 * f + j], b = c2[r * 2 * f + f + j];
+    if (hp) {
+      a += hp[img * 2 * f + j];
+      b += hp[img * 2 * f + f + j];
+    }
+    const float d = dout[r * lddo + j], sb = sigm(b);
+    dc2[r * 2 * f + j] = d * sb;
+    dc2[r * 2 * f + f + j] = d * a * sb * (1.f - sb);
+  }
+}
+
+__global__ void gemm_small_kernel(const float* __restrict__ A, int lda, int ta, const float* __restrict__ B, int ldb,
+                                  int tb, float* __restrict__ C, int ldc, int m, int n, int k, float beta) {
+  const long long stride = (long long)gridDim.x * blockDim.x, total = (long long)m * n;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int mi = (int)(i / n), ni = (int)(i - (long long)mi * n);
+    float s = 0.f;
+    for (int kk = 0; kk < k; ++kk) {
+      const float a = ta ? A[(long long)kk * lda + mi] : A[(long long)mi * lda + kk];
+      const float b = tb ? B[(long long)ni * ldb + kk] : B[(long long)kk * ldb + ni];
+      s = fmaf(a, b, s);
+    }
+    float* p = C + (long long)mi * ldc + ni;
+    *p = beta != 0.f ? beta * *p + s : s;
+  }
+}
+
+// per-image channel sums: block (64-column group, image), fixed order
+__global__ __launch_bounds__(256) void imgsum_kernel(const float* __restrict__ x, int ldx, int per_img, int c,
+                                                     float* __restrict__ out) {
+  __shared__ float red[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6, img = blockIdx.y;
+  float s = 0.f;
+  if (col < c)
+    for (int p = q; p < per_img; p += 4) s += x[((long long)img * per_img + p) * ldx + col];
+  red[q][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (q == 0 && col < c)
+    out[(long long)img * c + col] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+
+__global__ void copy_kernel(const float* __restrict__ x, int ldx, long long rows, int c, float* __restrict__ y,
+                            int ldy, int accumulate) {
+  const long long stride = (long long)gridDim.x * blockDim.x, total = rows * c;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const long long r = i / c;
+    const int j = (int)(i - r * c);
+    float v = x[r * ldx + j];
+    if (accumulate) v += y[r * ldy + j];
+    y[r * ldy + j] = v;
+  }
+}
+
+__global__ void pad_ones_kernel(const float* __restrict__ x, long long rows, int c, float* __restrict__ y, int ldy) {
+  const long long stride = (long long)gridDim.x * blockDim.x, total = rows * ldy;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const long long r = i / ldy;
+    const int j = (int)(i - r * ldy);
+    y[i] = j < c ? x[r * c + j] : (j == c ? 1.f : 0.f);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// discretized logistic mixture (nn.py:46-87): log p(x) per pixel and d(-log p)/dl in one pass
+// ---------------------------------------------------------------------------------------------
+#define PC_MAXMIX 16
+__device__ __forceinline__ float softplus_f(float x) { return x > 0.f ? x + log1pf(expf(-x)) : log1pf(expf(x)); }
+
+__global__ void mixlogistic_kernel(const float* __restrict__ x, const float* __restrict__ l, long long pixels, int M,
+                                   float* __restrict__ logp, float* __restrict__ dl, float coef) {
+  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= pixels) return;
+  const float* lp = l + p * 10 * M;
+  const float x0 = x[p * 3], x1 = x[p * 3 + 1], x2 = x[p * 3 + 2];
+  const float xs[3] = {x0, x1, x2};
+  float lpj[PC_MAXMIX];
+  // log_softmax of the logits
+  float lmax = -INFINITY;
+  for (int j = 0; j < M; ++j) lmax = fmaxf(lmax, lp[j]);
+  float lsum = 0.f;
+  for (int j = 0; j < M; ++j) lsum += expf(lp[j] - lmax);
+  const float llse = lmax + logf(lsum);
+  for (int j = 0; j < M; ++j) {
+    float acc = lp[j] - llse;
+    for (int c = 0; c < 3; ++c) {
+      const float* pc = lp + M + c * 3 * M;
+      float mean = pc[j];
+      if (c == 1) mean += tanhf(lp[M + 0 * 3 * M + 2 * M + j]) * x0;
+      if (c == 2) mean += tanhf(lp[M + 1 * 3 * M + 2 * M + j]) * x0 + tanhf(lp[M + 2 * 3 * M + 2 * M + j]) * x1;
+      const float ls = fmaxf(pc[M + j], -7.f);
+      const float cx = xs[c] - mean, inv = expf(-ls);
+      const float plus_in = inv * (cx + 1.f / 255.f), min_in = inv * (cx - 1.f / 255.f);
+      float v;
+      if (xs[c] < -0.999f) {
+        v = plus_in - softplus_f(plus_in);
+      } else if (xs[c] > 0.999f) {
+        v = -softplus_f(min_in);
+      } else {
+        const float cd = sigm(plus_in) - sigm(min_in);
+        if (cd > 1e-5f) {
+          v = logf(fmaxf(cd, 1e-12f));
+        } else {
+          const float mid = inv * cx;
+          v = mid - ls - 2.f * softplus_f(mid) - logf(127.5f);
+        }
+      }
+      acc += v;
+    }
+    lpj[j] = acc;
+  }
+  float mx = -INFINITY;
+  for (int j = 0; j < M; ++j) mx = fmaxf(mx, lpj[j]);
+  float se = 0.f;
+  for (int j = 0; j < M; ++j) se += expf(lpj[j] - mx);
+  const float out = mx + logf(se);
+  logp[p] = out;
+  if (!dl) return;
+  // d(-out)/d lp_j = -w_j (w = softmax(lpj)); d/d logit_k = -(w_k - softmax(logit)_k)
+  float* dp = dl + p * 10 * M;
+  for (int j = 0; j < M; ++j) {
+    const float w = expf(lpj[j] - out);
+    dp[j] = -coef * (w - expf(lp[j] - llse));
+    const float gw = -coef * w;  // d loss / d lp_cj for every c
+    float dmean[3], dls[3];
+    const float tc0 = tanhf(lp[M + 0 * 3 * M + 2 * M + j]), tc1 = tanhf(lp[M + 1 * 3 * M + 2 * M + j]),
+                tc2 = tanhf(lp[M + 2 * 3 * M + 2 * M + j]);
+    for (int c = 0; c < 3; ++c) {
+      const float* pc = lp + M + c * 3 * M;
+      float mean = pc[j];
+      if (c == 1) mean += tc0 * x0;
+      if (c == 2) mean += tc1 * x0 + tc2 * x1;
+      const float lsr = pc[M + j];
+      const float ls = fmaxf(lsr, -7.f);
+      const float cx = xs[c] - mean, inv = expf(-ls);
+      const float plus_in = inv * (cx + 1.f / 255.f), min_in = inv * (cx - 1.f / 255.f);
+      float d_plus = 0.f, d_min = 0.f, d_mid = 0.f, d_ls_direct = 0.f;
+      if (xs[c] < -0.999f) {
+        d_plus = 1.f - sigm(plus_in);
+      } else if (xs[c] > 0.999f) {
+        d_min = -sigm(min_in);
+      } else {
+        const float sp = sigm(plus_in), sm = sigm(min_in), cd = sp - sm;
+        if (cd > 1e-5f) {
+          d_plus = sp * (1.f - sp) / cd;
+          d_min = -sm * (1.f - sm) / cd;
+        } else {
+          d_mid = 1.f - 2.f * sigm(inv * cx);
+          d_ls_direct = -1.f;
+        }
+      }
+      // plus_in = inv (cx + 1/255): d/dcx = inv, d/dls = -plus_in (likewise min_in, mid)
+      const float mid = inv * cx;
+      const float dcx = (d_plus + d_min + d_mid) * inv;
+      const float dlsv = -(d_plus * plus_in + d_min * min_in + d_mid * mid) + d_ls_direct;
+      dmean[c] = -dcx * gw;
+      dls[c] = (lsr >= -7.f) ? dlsv * gw : 0.f;  // tf.maximum routes the gradient to x when x >= y
+    }
+    for (int c = 0; c < 3; ++c) {
+      dp[M + c * 3 * M + j] = dmean[c];
+      dp[M + c * 3 * M + M + j] = dls[c];
+    }
+    // coeffs: m1 += tc0 x0, m2 += tc1 x0 + tc2 x1; d tanh = 1 - t^2
+    dp[M + 0 * 3 * M + 2 * M + j] = dmean[1] * x0 * (1.f - tc0 * tc0);
+    dp[M + 1 * 3 * M + 2 * M + j] = dmean[2] * x0 * (1.f - tc1 * tc1);
+    dp[M + 2 * 3 * M + 2 * M + j] = dmean[2] * x1 * (1.f - tc2 * tc2);
+  }
+}
+
+__global__ __launch_bounds__(256) void sum_kernel(const float* __restrict__ x, long long n, float* out, double* out64) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (long long i = threadIdx.x; i < n; i += 256) s += x[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (out) out[0] = (float)red[0];
+    if (out64) out64[0] = red[0];
+  }
+}
+
+__global__ void sample_kernel(const float* __restrict__ l, const float* __restrict__ u_mix,
+                              const float* __restrict__ u_log, int nimg, int per_img, int M, float* __restrict__ x,
+                              int q0, int q1, int pix_stride) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nq = q1 - q0;
+  if (i >= (long long)nimg * nq) return;
+  const long long p = (i / nq) * per_img + q0 + (int)(i % nq);
+  const float* lp = l + p * 10 * M;
+  int sel = 0;
+  float best = -INFINITY;
+  for (int j = 0; j < M; ++j) {
+    const float v = lp[j] - logf(-logf(u_mix[p * M + j]));
+    if (v > best) {  // tf.argmax: first maximum
+      best = v;
+      sel = j;
+    }
+  }
+  float xs[3], co[3];
+  for (int c = 0; c < 3; ++c) {
+    const float* pc = lp + M + c * 3 * M;
+    const float u = u_log[p * 3 + c];
+    xs[c] = pc[sel] + expf(fmaxf(pc[M + sel], -7.f)) * (logf(u) - logf(1.f - u));
+    co[c] = tanhf(pc[2 * M + sel]);
+  }
+  const float x0 = fminf(fmaxf(xs[0], -1.f), 1.f);
+  const float x1 = fminf(fmaxf(xs[1] + co[0] * x0, -1.f), 1.f);
+  const float x2 = fminf(fmaxf(xs[2] + co[1] * x0 + co[2] * x1, -1.f), 1.f);
+  float* o = x + p * pix_stride;
+  o[0] = x0;
+  o[1] = x1;
+  o[2] = x2;
+}
+
+__global__ void highway_kernel(const float* __restrict__ s, const float* __restrict__ prev,
+                               const float* __restrict__ z, const float* __restrict__ zb, long long per_img,
+                               long long total, float lo, float hi, float* __restrict__ out) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const float b = zb ? zb[0] : 0.f;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const float r = lo + (hi - lo) * sigm(z[i / per_img] + b);
+    out[i] = r * s[i] + (1.f - r) * prev[i];
+  }
+}
+__global__ void ratio_kernel(const float* __restrict__ z, const float* __restrict__ zb, int nimg, float lo, float hi,
+                             float* __restrict__ ratio) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nimg) ratio[i] = lo + (hi - lo) * sigm(z[i] + (zb ? zb[0] : 0.f));
+}
+
+// column moments in fp64 (two-pass per column group): scratch [2][c]
+__global__ __launch_bounds__(256) void wn_init_kernel(const float* __restrict__ y, long long rows, int c, int ldy,
+                                                      float init_scale, float* g, float* b) {
+  __shared__ double red[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6, t = threadIdx.x & 63;
+  double s = 0.0;
+  if (col < c)
+    for (long long r = q; r < rows; r += 4) s += y[r * ldy + col];
+  red[q][t] = s;
+  __syncthreads();
+  const double mean = (red[0][t] + red[1][t] + red[2][t] + red[3][t]) / (double)rows;
+  __syncthreads();
+  double v = 0.0;
+  if (col < c)
+    for (long long r = q; r < rows; r += 4) {
+      const double d = y[r * ldy + col] - mean;
+      v += d * d;
+    }
+  red[q][t] = v;
+  __syncthreads();
+  if (q == 0 && col < c) {
+    const double var = (red[0][t] + red[1][t] + red[2][t] + red[3][t]) / (double)rows;
+    const double si = init_scale / sqrt(var + 1e-10);
+    g[col] = (float)(g[col] * si);
+    b[col] = (float)(b[col] - mean * si);
+  }
+}
+
+__global__ void ema_kernel(float* avg, const float* p, long long n, float decay) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    avg[i] = decay * avg[i] + (1.f - decay) * p[i];  // tf.train.ExponentialMovingAverage
+}
+
+PcGeom make_geom(int n, int hi, int wi, int cin, int ldx, int ho, int wo, int cout, int kh, int kw, int s, int pt,
+                 int pl, int mode) {
+  PcGeom g;
+  g.n = n; g.hi = hi; g.wi = wi; g.cin = cin; g.ldx = ldx;
+  g.ho = ho; g.wo = wo; g.cout = cout;
+  g.kh = kh; g.kw = kw; g.s = s; g.pt = pt; g.pl = pl; g.mode = mode;
+  return g;
+}
+bool geom_ok(const PcGeom& g) {
+  return g.n > 0 && g.hi > 0 && g.wi > 0 && g.cin > 0 && g.ho > 0 && g.wo > 0 && g.cout > 0 && g.kh > 0 &&
+         g.kw > 0 && (g.s == 1 || g.s == 2) && (g.mode == 0 || g.mode == 1) && g.ldx >= g.cin && g.ldx % 4 == 0 &&
+         g.cin % 4 == 0;
+}
+
+}  // namespace
+
+// =============================================================================================
+// C ABI
+// =============================================================================================
+extern "C" {
+
+int svae_pcnn_wnorm(const float* V, const float* g, int taps, int cin, int cout, float* norm, void* wk_f, int kf,
+                    void* wk_d, int kd, void* stream) {
+  if (!V || !g || !norm || taps < 1 || cin < 1 || cout < 1) return bad("pcnn_wnorm: bad arguments");
+  if ((wk_f && (kf < cin || kf % 16)) || (wk_d && (kd < cout || kd % 16))) return bad("pcnn_wnorm: bad padding");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(wn_norm_kernel, dim3((cout + 63) / 64), dim3(256), 0, s, V, taps * cin, cout, norm);
+  const long long n = (wk_f ? (long long)taps * cout * kf : 0) + (wk_d ? (long long)taps * cin * kd : 0);
+  if (n) hipLaunchKernelGGL(wn_apply_kernel, dim3(blocks_for(n)), dim3(256), 0, s, V, g, norm, taps, cin, cout,
+                            (__bf16*)wk_f, kf, (__bf16*)wk_d, kd);
+  return hipchk();
+}
+
+int svae_pcnn_wnorm_bwd(const float* V, const float* g, const float* norm, const float* dW, int taps, int cin,
+                        int cout, float* dV, float* dg, void* stream) {
+  if (!V || !g || !norm || !dW || !dV || !dg || taps < 1 || cin < 1 || cout < 1) return bad("pcnn_wnorm_bwd: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(wn_dg_kernel, dim3((cout + 63) / 64), dim3(256), 0, s, V, dW, norm, taps * cin, cout, dg);
+  const long long n = (long long)taps * cin * cout;
+  hipLaunchKernelGGL(wn_dv_kernel, dim3(blocks_for(n)), dim3(256), 0, s, V, g, norm, dW, dg, n, cout, dV);
+  return hipchk();
+}
+
+int svae_pcnn_conv(const float* x, int n, int hi, int wi, int cin, int ldx, const void* wk, int kpad,
+                   const float* bias, float* y, int ho, int wo, int cout, int ldy, int kh, int kw, int s, int pt,
+                   int pl, int mode, int accumulate, int zero_edge, void* stream) {
+  const PcGeom g = make_geom(n, hi, wi, cin, ldx, ho, wo, cout, kh, kw, s, pt, pl, mode);
+  if (!x || !wk || !y || !geom_ok(g) || ldy < cout || kpad < cin || kpad % 16 || zero_edge < 0 || zero_edge > 2)
+    return bad("pcnn_conv: bad arguments");
+  const long long rows = (long long)n * ho * wo;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)((rows + 127) / 128), 1);
+  if (cout > 32) {
+    const dim3 g2(grid.x, (cout + 63) / 64);
+    hipLaunchKernelGGL(pc_conv_kernel<2>, g2, dim3(256), 0, st, g, x, (const __bf16*)wk, kpad, bias, y, ldy,
+                       accumulate, zero_edge);
+  } else {
+    hipLaunchKernelGGL(pc_conv_kernel<1>, grid, dim3(256), 0, st, g, x, (const __bf16*)wk, kpad, bias, y, ldy,
+                       accumulate, zero_edge);
+  }
+  return hipchk();
+}
+
+int svae_pcnn_conv_wgrad(const float* x, int n, int hi, int wi, int cin, int ldx, const float* dy, int ldd, int ho,
+                         int wo, int cout, int kh, int kw, int s, int pt, int pl, int mode, float* dW, float* scratch,
+                         int64_t scratch_elems, void* stream) {
+  const PcGeom g = make_geom(n, hi, wi, cin, ldx, ho, wo, cout, kh, kw, s, pt, pl, mode);
+  if (!x || !dy || !dW || !scratch || !geom_ok(g) || ldd < cout || ldd % 4 || cout % 4)
+    return bad("pcnn_wgrad: bad arguments");
+  const long long rows = (long long)n * ho * wo;
+  const int taps = kh * kw;
+  const long long wsz = (long long)taps * cin * cout;
+  const int tiles = ((cin + 63) / 64) * ((cout + 63) / 64);
+  // splits: ~2048 blocks, >= 256 rows (8 chunks) per split, bounded by the scratch slabs
+  long long ns = (2048 + (long long)tiles * taps - 1) / ((long long)tiles * taps);
+  const long long max_rows = (rows + 255) / 256;
+  if (ns > max_rows) ns = max_rows;
+  if (ns > scratch_elems / wsz) ns = scratch_elems / wsz;
+  if (ns < 1) return bad("pcnn_wgrad: scratch too small");
+  long long rps = (rows + ns - 1) / ns;
+  rps = (rps + 31) / 32 * 32;
+  ns = (rows + rps - 1) / rps;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(pc_wgrad_kernel, dim3(tiles, taps, (unsigned)ns), dim3(256), 0, st, g, x, dy, ldd, rows, rps,
+                     scratch);
+  hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(wsz)), dim3(256), 0, st, scratch, (int)ns, wsz, dW);
+  return hipchk();
+}
+
+int svae_pcnn_colsum(const float* x, int64_t rows, int c, int ldx, int ho, int wo, int mask_edge, float* out,
+                     int accumulate, float* scratch, void* stream) {
+  if (!x || !out || !scratch || rows < 1 || c < 1 || ldx < c || (mask_edge && (ho < 1 || wo < 1)))
+    return bad("pcnn_colsum: bad arguments");
+  long long ns = (rows + 2047) / 2048;
+  if (ns > 256) ns = 256;
+  const long long rps = (rows + ns - 1) / ns;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(colsum_part_kernel_pc, dim3((c + 63) / 64, (unsigned)ns), dim3(256), 0, st, x, (long long)rows, c,
+                     ldx, ho * wo, wo, mask_edge, rps, scratch);
+  hipLaunchKernelGGL(colsum_fin_kernel_pc, dim3((c + 255) / 256), dim3(256), 0, st, scratch, (int)ns, c, out,
+                     accumulate);
+  return hipchk();
+}
+
+int svae_pcnn_mask_edge(float* x, int n, int ho, int wo, int c, int ldx, int mask_edge, void* stream) {
+  if (!x || n < 1 || ho < 1 || wo < 1 || c < 1 || ldx < c || mask_edge < 1 || mask_edge > 2)
+    return bad("pcnn_mask_edge: bad arguments");
+  const long long rows = (long long)n * ho * wo;
+  hipLaunchKernelGGL(mask_edge_kernel, dim3(blocks_for(rows * c)), dim3(256), 0, (hipStream_t)stream, x, rows, ho * wo,
+                     wo, c, ldx, mask_edge);
+  return hipchk();
+}
+
+int svae_pcnn_nonlin(const float* x, int64_t rows, int c, int ldx, int kind, float* y, int ldy, void* stream) {
+  if (!x || !y || rows < 1 || c < 1 || kind < 0 || kind > 2 || ldx < c || ldy < (kind == 2 ? 2 * c : c))
+    return bad("pcnn_nonlin: bad arguments");
+  hipLaunchKernelGGL(nonlin_kernel, dim3(blocks_for(rows * c)), dim3(256), 0, (hipStream_t)stream, x, (long long)rows,
+                     c, ldx, kind, y, ldy);
+  return hipchk();
+}
+
+int svae_pcnn_nonlin_bwd(const float* x, int64_t rows, int c, int ldx, int kind, const float* dy, int ldy, float* dx,
+                         int lddx, int accumulate, void* stream) {
+  if (!x || !dy || !dx || rows < 1 || c < 1 || kind < 0 || kind > 2) return bad("pcnn_nonlin_bwd: bad arguments");
+  hipLaunchKernelGGL(nonlin_bwd_kernel, dim3(blocks_for(rows * c)), dim3(256), 0, (hipStream_t)stream, x,
+                     (long long)rows, c, ldx, kind, dy, ldy, dx, lddx, accumulate);
+  return hipchk();
+}
+
+int svae_pcnn_gate(const float* x, int ldx, const float* c2, const float* hp, int64_t rows, int pix_per_img, int f,
+                   float* out, int ldo, void* stream) {
+  if (!x || !c2 || !out || rows < 1 || f < 1 || pix_per_img < 1 || rows % pix_per_img) return bad("pcnn_gate: bad arguments");
+  hipLaunchKernelGGL(gate_kernel, dim3(blocks_for(rows * f)), dim3(256), 0, (hipStream_t)stream, x, ldx, c2, hp,
+                     (long long)rows, pix_per_img, f, out, ldo);
+  return hipchk();
+}
+
+int svae_pcnn_gate_bwd(const float* c2, const float* hp, const float* dout, int lddo, int64_t rows, int pix_per_img,
+                       int f, float* dc2, void* stream) {
+  if (!c2 || !dout || !dc2 || rows < 1 || f < 1 || pix_per_img < 1 || rows % pix_per_img)
+    return bad("pcnn_gate_bwd: bad arguments");
+  hipLaunchKernelGGL(gate_bwd_kernel, dim3(blocks_for(rows * f)), dim3(256), 0, (hipStream_t)stream, c2, hp, dout,
+                     lddo, (long long)rows, pix_per_img, f, dc2);
+  return hipchk();
+}
+
+int svae_pcnn_gemm_small(const float* A, int lda, int ta, const float* B, int ldb, int tb, float* C, int ldc, int m,
+                         int n, int k, float beta, void* stream) {
+  if (!A || !B || !C || m < 1 || n < 1 || k < 1) return bad("pcnn_gemm_small: bad arguments");
+  hipLaunchKernelGGL(gemm_small_kernel, dim3(blocks_for((long long)m * n)), dim3(256), 0, (hipStream_t)stream, A, lda,
+                     ta, B, ldb, tb, C, ldc, m, n, k, beta);
+  return hipchk();
+}
+
+int svae_pcnn_imgsum(const float* x, int ldx, int nimg, int pix_per_img, int c, float* out, void* stream) {
+  if (!x || !out || nimg < 1 || pix_per_img < 1 || c < 1 || ldx < c) return bad("pcnn_imgsum: bad arguments");
+  hipLaunchKernelGGL(imgsum_kernel, dim3((c + 63) / 64, nimg), dim3(256), 0, (hipStream_t)stream, x, ldx, pix_per_img,
+                     c, out);
+  return hipchk();
+}
+
+int svae_pcnn_copy(const float* x, int ldx, int64_t rows, int c, float* y, int ldy, int accumulate, void* stream) {
+  if (!x || !y || rows < 1 || c < 1 || ldx < c || ldy < c) return bad("pcnn_copy: bad arguments");
+  hipLaunchKernelGGL(copy_kernel, dim3(blocks_for(rows * c)), dim3(256), 0, (hipStream_t)stream, x, ldx,
+                     (long long)rows, c, y, ldy, accumulate);
+  return hipchk();
+}
+
+int svae_pcnn_pad_ones(const float* x, int64_t rows, int c, float* y, int ldy, void* stream) {
+  if (!x || !y || rows < 1 || c < 1 || ldy < c + 1) return bad("pcnn_pad_ones: bad arguments");
+  hipLaunchKernelGGL(pad_ones_kernel, dim3(blocks_for(rows * ldy)), dim3(256), 0, (hipStream_t)stream, x,
+                     (long long)rows, c, y, ldy);
+  return hipchk();
+}
+
+int svae_pcnn_mixlogistic(const float* x, const float* l, int64_t pixels, int m, float* logp, float* dl, float coef,
+                          void* stream) {
+  if (!x || !l || !logp || pixels < 1 || m < 1 || m > PC_MAXMIX) return bad("pcnn_mixlogistic: bad arguments");
+  hipLaunchKernelGGL(mixlogistic_kernel, dim3((unsigned)((pixels + 127) / 128)), dim3(128), 0, (hipStream_t)stream, x,
+                     l, (long long)pixels, m, logp, dl, coef);
+  return hipchk();
+}
+
+int svae_pcnn_sum(const float* x, int64_t n, float* out, double* out64, void* stream) {
+  if (!x || n < 1 || (!out && !out64)) return bad("pcnn_sum: bad arguments");
+  hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, x, (long long)n, out, out64);
+  return hipchk();
+}
+
+int svae_pcnn_sample(const float* l, const float* u_mix, const float* u_log, int nimg, int per_img, int m, float* x,
+                     int q0, int q1, int pix_stride, void* stream) {
+  if (!l || !u_mix || !u_log || !x || nimg < 1 || per_img < 1 || m < 1 || m > PC_MAXMIX || q0 < 0 || q1 <= q0 ||
+      q1 > per_img || pix_stride < 3)
+    return bad("pcnn_sample: bad arguments");
+  const long long n = (long long)nimg * (q1 - q0);
+  hipLaunchKernelGGL(sample_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, l, u_mix,
+                     u_log, nimg, per_img, m, x, q0, q1, pix_stride);
+  return hipchk();
+}
+
+int svae_pcnn_highway(const float* s, const float* prev, const float* z, const float* zb, int nimg, int64_t per_img,
+                      float lo, float hi, float* out, float* ratio, void* stream) {
+  if (!s || !prev || !z || !out || nimg < 1 || per_img < 1) return bad("pcnn_highway: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)nimg * per_img;
+  hipLaunchKernelGGL(highway_kernel, dim3(blocks_for(total)), dim3(256), 0, st, s, prev, z, zb, (long long)per_img,
+                     total, lo, hi, out);
+  if (ratio) hipLaunchKernelGGL(ratio_kernel, dim3((nimg + 255) / 256), dim3(256), 0, st, z, zb, nimg, lo, hi, ratio);
+  return hipchk();
+}
+
+int svae_pcnn_wn_init(const float* y, int64_t rows, int c, int ldy, float init_scale, float* g, float* b,
+                      double* scratch, void* stream) {
+  (void)scratch;
+  if (!y || !g || !b || rows < 1 || c < 1 || ldy < c) return bad("pcnn_wn_init: bad arguments");
+  hipLaunchKernelGGL(wn_init_kernel, dim3((c + 63) / 64), dim3(256), 0, (hipStream_t)stream, y, (long long)rows, c,
+                     ldy, init_scale, g, b);
+  return hipchk();
+}
+
+int svae_pcnn_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, int64_t step, float clip,
+                   void* stream) {
+  if (!p || !g || !m || !v || n < 1 || step < 1) return bad("pcnn_adam: bad arguments");
+  const double b1 = 0.9, b2 = 0.999;
+  const double lr_t = lr * sqrt(1.0 - pow(b2, (double)step)) / (1.0 - pow(b1, (double)step));
+  adam_step(p, g, m, v, nullptr, n, (float)lr_t, (float)b1, (float)b2, 1e-8f, clip, (hipStream_t)stream);
+  return hipchk();
+}
+
+int svae_pcnn_ema(float* avg, const float* p, int64_t n, float decay, void* stream) {
+  if (!avg || !p || n < 1) return bad("pcnn_ema: bad arguments");
+  hipLaunchKernelGGL(ema_kernel, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, avg, p, (long long)n, decay);
+  return hipchk();
+}
+
+}  // extern "C"

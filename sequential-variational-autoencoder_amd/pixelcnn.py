@@ -1,0 +1,562 @@
+"""PixelCNN++ decoder head over the HIP kernels of include/svae_pcnn.h.
+
+Mirrors the reference's interface for this head:
+  * ``PixelCNNpp.model(x, h)``      pixel_cnn_pp/model.py:11-117 (model_spec, conditional on h)
+  * ``PixelCNNpp.loss(x, h)``       + nn.discretized_mix_logistic_loss (nn.py:46-87), sum_all
+  * ``PixelCNNpp.data_init(x, h)``  the init pass (pixelvae.py:103-105; nn.py:176-180, :206-210)
+  * ``PixelCNNpp.sample(h, ...)``   sample_from_model's autoregressive loop (pixelvae.py:170-194)
+                                    with nn.sample_from_discretized_mix_logistic (nn.py:89-109)
+  * ``make_pixel_cnn(...)``         pixelvae.py:68-158, repaired: returns
+                                    (highway_train_out, 0, cache) like the reference.
+
+Every tensor op runs in libsvae_hip.so (bf16-MFMA gather convolutions and weight gradients, fused
+elementwise kernels, the mixture loss with its analytic gradient); torch only allocates device
+memory.  The backward is an explicit tape of the forward's primitive ops in reverse.
+
+Parameters live in one flat fp32 buffer (canonical layouts: conv / deconv V [kh, kw, Cin, Cout],
+dense V [in, out], hw [K, 2F]); names follow the reference's layer counters (nn.py:151-157).
+"""
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+
+NL_KIND = {"relu": 0, "elu": 1, "concat_elu": 2}
+
+
+def _p(t, off=0):
+    """Device pointer of fp32 tensor ``t`` at element offset ``off`` (None-safe)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr() + 4 * off)
+
+
+def _ck(rc):
+    _lib.check(rc)
+
+
+def _r16(c):
+    return (c + 15) // 16 * 16
+
+
+class Act:
+    """An NHWC activation: ``buf`` [n*h*w][ld] fp32, channels [off, off + c)."""
+    __slots__ = ("buf", "off", "c", "ld", "n", "h", "w")
+
+    def __init__(self, buf, c, n, h, w, off=0, ld=None):
+        self.buf, self.c, self.n, self.h, self.w, self.off = buf, c, n, h, w, off
+        self.ld = c if ld is None else ld
+
+    @property
+    def rows(self):
+        return self.n * self.h * self.w
+
+    def ptr(self):
+        return _p(self.buf, self.off)
+
+
+def param_shapes(spec):
+    """Ordered {name: shape} of every variable model_spec creates (model.py:35-112 in TF
+    construction order; counters nn.py:151-157), plus the highway FC (pixelvae.py:136)."""
+    shapes = {}
+    cnt = {}
+
+    def nm(kind):
+        i = cnt.get(kind, 0)
+        cnt[kind] = i + 1
+        return "%s_%d" % (kind, i)
+
+    F, R, K, M = spec["F"], spec["R"], spec["K"], spec["M"]
+    nlc = (lambda c: 2 * c) if spec["nl"] == "concat_elu" else (lambda c: c)
+
+    def conv(cin, cout, kh, kw, kind="conv2d"):
+        n = nm(kind)
+        shapes[n + "/V"] = (kh, kw, cin, cout)
+        shapes[n + "/g"] = (cout,)
+        shapes[n + "/b"] = (cout,)
+
+    def dense(cin, cout):
+        n = nm("dense")
+        shapes[n + "/V"] = (cin, cout)
+        shapes[n + "/g"] = (cout,)
+        shapes[n + "/b"] = (cout,)
+
+    def resnet(kh, kw, a_ch=None):
+        conv(nlc(F), F, kh, kw)
+        if a_ch is not None:
+            dense(nlc(a_ch), F)
+        conv(nlc(F), 2 * F, kh, kw)
+        shapes[nm("conditional_weights") + "/hw"] = (K, 2 * F)
+
+    conv(spec["C"] + 1, F, 2, 3)
+    conv(spec["C"] + 1, F, 1, 3)
+    conv(spec["C"] + 1, F, 2, 1)
+    for stage in range(3):
+        for _ in range(R):
+            resnet(2, 3)
+            resnet(2, 2, F)
+        if stage < 2:
+            conv(F, F, 2, 3)
+            conv(F, F, 2, 2)
+    for stage in range(3):
+        for _ in range(R if stage == 0 else R + 1):
+            resnet(2, 3, F)
+            resnet(2, 2, 2 * F)
+        if stage < 2:
+            conv(F, F, 2, 3, "deconv2d")
+            conv(F, F, 2, 2, "deconv2d")
+    dense(F, 10 * M)
+    shapes["highway/W"] = (K, 1)
+    shapes["highway/b"] = (1,)
+    return shapes
+
+
+def make_spec(H=64, W=64, C=3, K=48, nr_resnet=3, nr_filters=160, nr_mix=10, nonlinearity="relu"):
+    """pixelvae.py Args (:54-63): nr_resnet 3, nr_filters 160, nr_logistic_mix 10, 'relu'."""
+    if H % 4 or W % 4:
+        raise ValueError("H and W must be multiples of 4 (two stride-2 stages)")
+    if C != 3:
+        raise ValueError("the discretized logistic mixture models RGB (nn.py:57-59)")
+    if nonlinearity not in NL_KIND:
+        raise ValueError("resnet nonlinearity %r is not supported (model.py:24-31)" % nonlinearity)
+    if nr_filters % 4 or nr_mix > 16:
+        raise ValueError("nr_filters must be a multiple of 4 and nr_logistic_mix <= 16")
+    return dict(H=H, W=W, C=C, K=K, R=nr_resnet, F=nr_filters, M=nr_mix, nl=nonlinearity)
+
+
+class PixelCNNpp:
+    """Conditional PixelCNN++ on libsvae_hip.so.  One instance owns its parameters, gradients,
+    Adam moments and Polyak averages (flat fp32 device buffers)."""
+
+    def __init__(self, spec, params=None, seed=0, device="cuda", scratch_elems=1 << 26):
+        if not torch.cuda.is_available():
+            raise RuntimeError("PixelCNNpp needs a GPU (HIP kernels in libsvae_hip.so); there is no CPU fallback")
+        self.s = spec
+        self.L = _lib.lib()
+        self.dev = torch.device(device)
+        shapes = param_shapes(spec)
+        self.table = {}
+        off = 0
+        for k, shp in shapes.items():
+            n = int(np.prod(shp))
+            self.table[k] = (off, shp, n)
+            off += (n + 63) // 64 * 64
+        self.n_params = off
+        self.P = torch.zeros(off, dtype=torch.float32, device=self.dev)
+        self.G = torch.zeros_like(self.P)
+        self.m = torch.zeros_like(self.P)
+        self.v = torch.zeros_like(self.P)
+        self.ema = None
+        if params is None:
+            params = self.init_values(seed)
+        self.set_params(params)
+        self.scratch = torch.empty(scratch_elems, dtype=torch.float32, device=self.dev)
+        self.iteration = 0
+        self._dh = None
+        self._tape, self._g, self._keep, self._same, self._cnt = [], {}, [], {}, {}
+        self._record = self._init = False
+
+    # ---------------- parameters ----------------
+    def init_values(self, seed=0):
+        """nn.py initialisers: V, hw ~ N(0, 0.05); g = 1; b = 0; highway FC Xavier-uniform."""
+        rng = np.random.default_rng(seed)
+        out = {}
+        for k, (_, shp, _) in self.table.items():
+            leaf = k.split("/")[-1]
+            if leaf in ("V", "hw"):
+                out[k] = rng.normal(0.0, 0.05, size=shp)
+            elif leaf == "g":
+                out[k] = np.ones(shp)
+            elif k == "highway/W":
+                lim = math.sqrt(6.0 / (shp[0] + shp[1]))
+                out[k] = rng.uniform(-lim, lim, size=shp)
+            else:
+                out[k] = np.zeros(shp)
+        return out
+
+    def set_params(self, params):
+        host = np.zeros(self.n_params, np.float32)
+        for k, (off, shp, n) in self.table.items():
+            host[off:off + n] = np.asarray(params[k], np.float32).reshape(-1)
+        self.P.copy_(torch.from_numpy(host))
+
+    def get(self, buf, name):
+        off, shp, n = self.table[name]
+        return buf[off:off + n].view(*shp)
+
+    def params(self):
+        host = self.P.cpu().numpy()
+        return {k: host[off:off + n].reshape(shp).copy() for k, (off, shp, n) in self.table.items()}
+
+    def grads(self):
+        host = self.G.cpu().numpy()
+        return {k: host[off:off + n].reshape(shp).copy() for k, (off, shp, n) in self.table.items()}
+
+    # ---------------- tape primitives ----------------
+    def _new(self, rows, c):
+        return torch.empty(rows, c, dtype=torch.float32, device=self.dev)
+
+    def _grad(self, a):
+        """Gradient buffer of activation ``a`` ([rows][c], zero on first use); a reshaped view
+        (``_view``) shares its source's buffer."""
+        while id(a) in self._same:
+            a = self._same[id(a)]
+        g = self._g.get(id(a))
+        if g is None:
+            g = torch.zeros(a.rows, a.c, dtype=torch.float32, device=self.dev)
+            self._g[id(a)] = g
+            self._keep.append(a)
+        return g
+
+    def _has_grad(self, a):
+        while id(a) in self._same:
+            a = self._same[id(a)]
+        return id(a) in self._g
+
+    def _view(self, a, n, h, w):
+        """``a`` reshaped to another row space (same buffer and gradient)."""
+        v = Act(a.buf, a.c, n, h, w, a.off, a.ld)
+        self._same[id(v)] = a
+        self._keep.append(v)
+        return v
+
+    def _st(self):
+        return _lib.stream_ptr()
+
+    def _wconv(self, x, name, cout, kh, kw, s, pt, pl, mode=0, ho=None, wo=None, zero_edge=0, out=None,
+               init_scale=1.0):
+        """Weight-normed conv / deconv / dense (nn.py:160-252) as a gather GEMM; returns the output Act
+        (or accumulates into ``out``, whose existing values it adds to)."""
+        L = self.L
+        st = self._st()
+        taps, cin = kh * kw, x.c
+        off_v, _, _ = self.table[name + "/V"]
+        off_g, _, _ = self.table[name + "/g"]
+        off_b, _, _ = self.table[name + "/b"]
+        kf, kd = _r16(cin), _r16(cout)
+        norm = torch.empty(cout, dtype=torch.float32, device=self.dev)
+        wkf = torch.empty(taps * cout * kf, dtype=torch.bfloat16, device=self.dev)
+        wkd = torch.empty(taps * cin * kd, dtype=torch.bfloat16, device=self.dev)
+        _ck(L.svae_pcnn_wnorm(_p(self.P, off_v), _p(self.P, off_g), taps, cin, cout, _p(norm), _p(wkf), kf,
+                              ctypes.c_void_p(wkd.data_ptr()), kd, st))
+        if ho is None:
+            ho, wo = (x.h - 1) // s + 1, (x.w - 1) // s + 1
+        acc = out is not None
+        if out is None:
+            out = Act(self._new(x.n * ho * wo, cout), cout, x.n, ho, wo)
+        _ck(L.svae_pcnn_conv(x.ptr(), x.n, x.h, x.w, cin, x.ld, ctypes.c_void_p(wkf.data_ptr()), kf,
+                             _p(self.P, off_b), out.ptr(), ho, wo, cout, out.ld, kh, kw, s, pt, pl, mode,
+                             1 if acc else 0, zero_edge, st))
+        if self._init:  # data-dependent init: this layer's g, b from the moments of its own output
+            # (before any shift or sum), which is passed on un-normalised (tf.identity of the old x)
+            src = out
+            if acc or zero_edge:
+                src = Act(self._new(x.n * ho * wo, cout), cout, x.n, ho, wo)
+                _ck(L.svae_pcnn_conv(x.ptr(), x.n, x.h, x.w, cin, x.ld, ctypes.c_void_p(wkf.data_ptr()), kf,
+                                     _p(self.P, off_b), src.ptr(), ho, wo, cout, cout, kh, kw, s,
+                                     pt - (zero_edge == 1), pl - (zero_edge == 2), mode, 0, 0, st))
+            _ck(L.svae_pcnn_wn_init(src.ptr(), src.rows, cout, src.ld, float(init_scale), _p(self.P, off_g),
+                                    _p(self.P, off_b), None, st))
+        if self._record:
+            geo = (kh, kw, s, pt, pl, mode, zero_edge, kf, kd, off_v, off_g, off_b)
+            self._tape.append(lambda: self._wconv_bwd(x, out, norm, wkd, geo))
+        return out
+
+    def _wconv_bwd(self, x, y, norm, wkd, geo):
+        L = self.L
+        st = self._st()
+        kh, kw, s, pt, pl, mode, zero_edge, kf, kd, off_v, off_g, off_b = geo
+        taps, cin, cout = kh * kw, x.c, y.c
+        dy = self._grad(y)
+        if zero_edge:  # the zeroed shifted outputs pass no gradient
+            dy = dy.clone()
+            _ck(L.svae_pcnn_mask_edge(_p(dy), y.n, y.h, y.w, cout, cout, zero_edge, st))
+        _ck(L.svae_pcnn_colsum(_p(dy), y.rows, cout, cout, y.h, y.w, 0, _p(self.G, off_b), 0, _p(self.scratch), st))
+        dW = torch.empty(taps * cin * cout, dtype=torch.float32, device=self.dev)
+        sc = self.scratch
+        _ck(L.svae_pcnn_conv_wgrad(x.ptr(), x.n, x.h, x.w, cin, x.ld, _p(dy), cout, y.h, y.w, cout, kh, kw, s, pt, pl,
+                                   mode, _p(dW), _p(sc), sc.numel(), st))
+        _ck(L.svae_pcnn_wnorm_bwd(_p(self.P, off_v), _p(self.P, off_g), _p(norm), _p(dW), taps, cin, cout,
+                                  _p(self.G, off_v), _p(self.G, off_g), st))
+        if id(x) in self._nograd:
+            return
+        dx = self._grad(x)
+        # the input gradient: the transposed gather over dy with the [tap][Cin][Cout] copy
+        _ck(L.svae_pcnn_conv(_p(dy), y.n, y.h, y.w, cout, cout, ctypes.c_void_p(wkd.data_ptr()), kd, None, _p(dx),
+                             x.h, x.w, cin, cin, kh, kw, s, pt, pl, 1 - mode, 1, 0, st))
+
+    def _dense(self, x, name, cout, init_scale=1.0):
+        """nn.nin / dense over the channel axis (nn.py:255-260): a 1x1 gather GEMM over every pixel."""
+        y = self._wconv(self._view(x, x.rows, 1, 1), name, cout, 1, 1, 1, 0, 0, init_scale=init_scale)
+        return self._view(y, x.n, x.h, x.w)
+
+    def _nonlin(self, x, kind):
+        k = NL_KIND[kind]
+        c = 2 * x.c if k == 2 else x.c
+        y = Act(self._new(x.rows, c), c, x.n, x.h, x.w)
+        _ck(self.L.svae_pcnn_nonlin(x.ptr(), x.rows, x.c, x.ld, k, y.ptr(), y.ld, self._st()))
+        if self._record:
+            def bwd():
+                if not self._has_grad(y):
+                    return
+                _ck(self.L.svae_pcnn_nonlin_bwd(x.ptr(), x.rows, x.c, x.ld, k, _p(self._grad(y)), c,
+                                                _p(self._grad(x)), x.c, 1, self._st()))
+            self._tape.append(bwd)
+        return y
+
+    def _cat(self, a, b):
+        c = a.c + b.c
+        y = Act(self._new(a.rows, c), c, a.n, a.h, a.w)
+        st = self._st()
+        _ck(self.L.svae_pcnn_copy(a.ptr(), a.ld, a.rows, a.c, y.ptr(), c, 0, st))
+        _ck(self.L.svae_pcnn_copy(b.ptr(), b.ld, b.rows, b.c, _p(y.buf, a.c), c, 0, st))
+        if self._record:
+            def bwd():
+                if not self._has_grad(y):
+                    return
+                dy = self._grad(y)
+                _ck(self.L.svae_pcnn_copy(_p(dy), c, a.rows, a.c, _p(self._grad(a)), a.c, 1, self._st()))
+                _ck(self.L.svae_pcnn_copy(_p(dy, a.c), c, b.rows, b.c, _p(self._grad(b)), b.c, 1, self._st()))
+            self._tape.append(bwd)
+        return y
+
+    def _gate(self, x, c2, h, hw_name):
+        """out = x + a * sigmoid(b), [a | b] = c2 + h . hw (nn.py:277-288)."""
+        F = x.c
+        st = self._st()
+        off_hw, _, _ = self.table[hw_name]
+        K = self.s["K"]
+        hp = torch.empty(x.n, 2 * F, dtype=torch.float32, device=self.dev)
+        _ck(self.L.svae_pcnn_gemm_small(_p(h), K, 0, _p(self.P, off_hw), 2 * F, 0, _p(hp), 2 * F, x.n, 2 * F, K, 0.0,
+                                        st))
+        y = Act(self._new(x.rows, F), F, x.n, x.h, x.w)
+        _ck(self.L.svae_pcnn_gate(x.ptr(), x.ld, c2.ptr(), _p(hp), x.rows, x.h * x.w, F, y.ptr(), F, st))
+        if self._record:
+            def bwd():
+                if not self._has_grad(y):
+                    return
+                st2 = self._st()
+                dy = self._grad(y)
+                _ck(self.L.svae_pcnn_copy(_p(dy), F, x.rows, F, _p(self._grad(x)), F, 1, st2))
+                dc2 = self._grad(c2)
+                _ck(self.L.svae_pcnn_gate_bwd(c2.ptr(), _p(hp), _p(dy), F, x.rows, x.h * x.w, F, _p(dc2), st2))
+                dhp = torch.empty(x.n, 2 * F, dtype=torch.float32, device=self.dev)
+                _ck(self.L.svae_pcnn_imgsum(_p(dc2), 2 * F, x.n, x.h * x.w, 2 * F, _p(dhp), st2))
+                # d hw [K][2F] = h^T . dhp
+                _ck(self.L.svae_pcnn_gemm_small(_p(h), K, 1, _p(dhp), 2 * F, 0, _p(self.G, off_hw), 2 * F, K, 2 * F,
+                                                x.n, 0.0, st2))
+                if self._dh is not None:  # d h += dhp . hw^T
+                    _ck(self.L.svae_pcnn_gemm_small(_p(dhp), 2 * F, 0, _p(self.P, off_hw), 2 * F, 1, _p(self._dh), K,
+                                                    x.n, K, 2 * F, 1.0, st2))
+            self._tape.append(bwd)
+        return y
+
+    # ---------------- the network ----------------
+    def _gated_resnet(self, x, h, kh, kw, a=None):
+        nl = self.s["nl"]
+        pt, pl = kh - 1, (kw - 1) // 2 if kw == 3 else kw - 1
+        c1 = self._wconv(self._nonlin(x, nl), self._nm("conv2d"), x.c, kh, kw, 1, pt, pl)
+        if a is not None:
+            self._dense_into(self._nonlin(a, nl), self._nm("dense"), c1)
+        t2 = self._nonlin(c1, nl)
+        c2 = self._wconv(t2, self._nm("conv2d"), 2 * x.c, kh, kw, 1, pt, pl, init_scale=0.1)
+        return self._gate(x, c2, h, self._nm("conditional_weights") + "/hw")
+
+    def _dense_into(self, x, name, out):
+        self._wconv(self._view(x, x.rows, 1, 1), name, out.c, 1, 1, 1, 0, 0, out=self._view(out, out.rows, 1, 1))
+
+    def _nm(self, kind):
+        i = self._cnt.get(kind, 0)
+        self._cnt[kind] = i + 1
+        return "%s_%d" % (kind, i)
+
+    def _run(self, x, h, record, init=False):
+        """model_spec(x, h) (model.py:11-117) -> l Act [rows][10 M]."""
+        s = self.s
+        self._record, self._init = record, init
+        self._tape, self._g, self._keep, self._same, self._cnt = [], {}, [], {}, {}
+        self._nograd = set()
+        B, H, W = x.shape[0], s["H"], s["W"]
+        F, R = s["F"], s["R"]
+        rows = B * H * W
+        xp = Act(self._new(rows, 4), 4, B, H, W)
+        _ck(self.L.svae_pcnn_pad_ones(_p(x), rows, 3, xp.ptr(), 4, self._st()))
+        self._nograd.add(id(xp))
+        self._keep.append(xp)
+        # u: down_shift(down_shifted_conv2d(x_pad, [2, 3])): pt + 1 and the first row zeroed
+        u = [self._wconv(xp, self._nm("conv2d"), F, 2, 3, 1, 2, 1, zero_edge=1)]
+        # ul: down_shift(ds_conv [1, 3]) + right_shift(drs_conv [2, 1])
+        ul0 = self._wconv(xp, self._nm("conv2d"), F, 1, 3, 1, 1, 1, zero_edge=1)
+        self._wconv(xp, self._nm("conv2d"), F, 2, 1, 1, 1, 1, zero_edge=2, out=ul0)
+        ul = [ul0]
+        for stage in range(3):
+            for _ in range(R):
+                u.append(self._gated_resnet(u[-1], h, 2, 3))
+                ul.append(self._gated_resnet(ul[-1], h, 2, 2, a=u[-1]))
+            if stage < 2:
+                u.append(self._wconv(u[-1], self._nm("conv2d"), F, 2, 3, 2, 1, 1))
+                ul.append(self._wconv(ul[-1], self._nm("conv2d"), F, 2, 2, 2, 1, 1))
+        uu, uul = u.pop(), ul.pop()
+        for stage in range(3):
+            for _ in range(R if stage == 0 else R + 1):
+                uu = self._gated_resnet(uu, h, 2, 3, a=u.pop())
+                uul = self._gated_resnet(uul, h, 2, 2, a=self._cat(uu, ul.pop()))
+            if stage < 2:  # down_shifted_deconv2d / down_right_shifted_deconv2d (stride 2, VALID, cropped)
+                uu = self._wconv(uu, self._nm("deconv2d"), F, 2, 3, 2, 0, 1, mode=1, ho=2 * uu.h, wo=2 * uu.w)
+                uul = self._wconv(uul, self._nm("deconv2d"), F, 2, 2, 2, 0, 0, mode=1, ho=2 * uul.h, wo=2 * uul.w)
+        assert not u and not ul
+        e = self._nonlin(uul, "elu")
+        return self._dense(e, self._nm("dense"), 10 * s["M"])
+
+    def _inputs(self, x, h):
+        s = self.s
+        x = torch.as_tensor(x, dtype=torch.float32, device=self.dev).contiguous()
+        h = torch.as_tensor(h, dtype=torch.float32, device=self.dev).contiguous()
+        if tuple(x.shape[1:]) != (s["H"], s["W"], 3) or h.shape != (x.shape[0], s["K"]):
+            raise ValueError("x must be [B, %d, %d, 3] and h [B, %d]" % (s["H"], s["W"], s["K"]))
+        return x, h
+
+    def model(self, x, h):
+        """l = model_spec(x, h): [B, H, W, 10 M] (no tape)."""
+        x, h = self._inputs(x, h)
+        l = self._run(x, h, record=False)
+        self._drop()
+        return l.buf.view(x.shape[0], self.s["H"], self.s["W"], 10 * self.s["M"])
+
+    def _drop(self):
+        self._tape, self._g, self._keep, self._same = [], {}, [], {}
+
+    def loss(self, x, h, backward=True, grad_h=False, coef=1.0):
+        """NLL = discretized_mix_logistic_loss(x, model(x, h)) summed (nn.py:84-85).  With
+        ``backward``, d(coef * NLL)/d every parameter lands in ``self.G`` (written) and, with
+        ``grad_h``, d/dh is returned too."""
+        x, h = self._inputs(x, h)
+        st = self._st()
+        l = self._run(x, h, record=backward)
+        pix = l.rows
+        logp = torch.empty(pix, dtype=torch.float32, device=self.dev)
+        dl = self._grad(l) if backward else None
+        _ck(self.L.svae_pcnn_mixlogistic(_p(x), l.ptr(), pix, self.s["M"], _p(logp), _p(dl), float(coef), st))
+        tot = torch.empty(1, dtype=torch.float64, device=self.dev)
+        _ck(self.L.svae_pcnn_sum(_p(logp), pix, None, ctypes.c_void_p(tot.data_ptr()), st))
+        dh = None
+        if backward:
+            self.G.zero_()
+            self._dh = torch.zeros(x.shape[0], self.s["K"], dtype=torch.float32, device=self.dev) if grad_h else None
+            for fn in reversed(self._tape):
+                fn()
+            dh = self._dh
+            self._dh = None
+        self._drop()
+        nll = -float(tot.item())
+        return (nll, dh) if grad_h else nll
+
+    def data_init(self, x, h):
+        """The data-dependent init pass (pixelvae.py:103-105): every weight-normed layer's g, b from
+        its own output moments, in construction order (nn.py:176-180, :206-210)."""
+        x, h = self._inputs(x, h)
+        self._run(x, h, record=False, init=True)
+        self._init = False
+        self._drop()
+
+    def adam(self, lr, step=None, clip=float("inf")):
+        """One Adam update of every parameter from ``self.G`` (TF AdamOptimizer, the optimiser
+        sequential_vae.py:1246-1276 applies to every trainable variable)."""
+        self.iteration = self.iteration + 1 if step is None else step
+        _ck(self.L.svae_pcnn_adam(_p(self.P), _p(self.G), _p(self.m), _p(self.v), self.n_params, float(lr),
+                                  int(self.iteration), float(clip), self._st()))
+
+    def ema_update(self, decay=0.9995):
+        """Polyak averages (pixelvae.py:113-114, ExponentialMovingAverage(polyak_decay))."""
+        if self.ema is None:
+            self.ema = self.P.clone()
+            return
+        _ck(self.L.svae_pcnn_ema(_p(self.ema), _p(self.P), self.n_params, float(decay), self._st()))
+
+    def train_step(self, x, h, lr=1e-3, clip=float("inf")):
+        nll = self.loss(x, h, backward=True)
+        self.adam(lr, clip=clip)
+        return nll
+
+    def sample(self, h, u_mix=None, u_log=None, seed=0, use_ema=False):
+        """sample_from_model (pixelvae.py:170-194): x = 0, then for every position in raster order
+        one network evaluation and one draw from the mixture at that position
+        (sample_from_discretized_mix_logistic, nn.py:89-109).  u_mix [B,H,W,M] / u_log [B,H,W,3]
+        may be injected (parity); otherwise drawn on the device per position."""
+        s = self.s
+        h = torch.as_tensor(h, dtype=torch.float32, device=self.dev).contiguous()
+        B, H, W, M = h.shape[0], s["H"], s["W"], s["M"]
+        gen = torch.Generator(device=self.dev)
+        gen.manual_seed(seed)
+        if u_mix is None:
+            u_mix = torch.rand(B, H, W, M, device=self.dev, generator=gen) * (1 - 2e-5) + 1e-5
+        if u_log is None:
+            u_log = torch.rand(B, H, W, 3, device=self.dev, generator=gen) * (1 - 2e-5) + 1e-5
+        u_mix = torch.as_tensor(u_mix, dtype=torch.float32, device=self.dev).contiguous()
+        u_log = torch.as_tensor(u_log, dtype=torch.float32, device=self.dev).contiguous()
+        saved = None
+        if use_ema and self.ema is not None:
+            saved = self.P.clone()
+            self.P.copy_(self.ema)
+        x = torch.zeros(B, H, W, 3, dtype=torch.float32, device=self.dev)
+        try:
+            for q in range(H * W):
+                l = self._run(x, h, record=False)
+                _ck(self.L.svae_pcnn_sample(l.ptr(), _p(u_mix), _p(u_log), B, H * W, M, _p(x), q, q + 1, 3,
+                                            self._st()))
+                self._drop()
+        finally:
+            if saved is not None:
+                self.P.copy_(saved)
+        return x
+
+    def highway(self, sample, prev, latents, lo, hi):
+        """pixelvae.py:135-137: per-image ratio r = lo + (hi - lo) sigmoid(latents . W + b),
+        out = r sample + (1 - r) prev."""
+        latents = torch.as_tensor(latents, dtype=torch.float32, device=self.dev).contiguous()
+        B = latents.shape[0]
+        z = torch.empty(B, dtype=torch.float32, device=self.dev)
+        ow, _, _ = self.table["highway/W"]
+        ob, _, _ = self.table["highway/b"]
+        st = self._st()
+        _ck(self.L.svae_pcnn_gemm_small(_p(latents), self.s["K"], 0, _p(self.P, ow), 1, 0, _p(z), 1, B, 1,
+                                        self.s["K"], 0.0, st))
+        sample = sample.contiguous()
+        prev = prev.contiguous()
+        out = torch.empty_like(sample)
+        ratio = torch.empty(B, dtype=torch.float32, device=self.dev)
+        _ck(self.L.svae_pcnn_highway(_p(sample), _p(prev), _p(z), _p(self.P, ob), B, sample[0].numel(), float(lo),
+                                     float(hi), _p(out), _p(ratio), st))
+        return out, ratio
+
+
+def make_pixel_cnn(ground_images, prev_samples, latents, min_highway_connection, max_highway_connection,
+                   net=None, u_mix=None, u_log=None):
+    """pixelvae.make_pixel_cnn (pixelvae.py:68-158), repaired: the head conditioned on the latents,
+    its training output the mixture sample of model(ground_images, latents) (:123-125) mixed per
+    image with the previous chain sample (:135-137).  Returns (highway_train_out, 0, cache) like
+    the reference; cache['net'] is the PixelCNNpp (its NLL via net.loss)."""
+    B, H, W, C = ground_images.shape
+    if net is None:
+        net = PixelCNNpp(make_spec(H=H, W=W, K=latents.shape[1]))
+    l = net.model(ground_images, latents)
+    M = net.s["M"]
+    dev = net.dev
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(0)
+    if u_mix is None:
+        u_mix = torch.rand(B, H, W, M, device=dev, generator=gen) * (1 - 2e-5) + 1e-5
+    if u_log is None:
+        u_log = torch.rand(B, H, W, 3, device=dev, generator=gen) * (1 - 2e-5) + 1e-5
+    x = torch.empty(B, H, W, 3, dtype=torch.float32, device=dev)
+    # (device copies held in locals: a temporary's memory could be reused before the kernel runs)
+    um = torch.as_tensor(u_mix, dtype=torch.float32, device=dev).contiguous()
+    ul = torch.as_tensor(u_log, dtype=torch.float32, device=dev).contiguous()
+    _ck(net.L.svae_pcnn_sample(_p(l), _p(um), _p(ul), B, H * W, M, _p(x), 0, H * W, 3, _lib.stream_ptr()))
+    prev = torch.as_tensor(prev_samples, dtype=torch.float32, device=dev)
+    out, ratio = net.highway(x, prev, latents, min_highway_connection, max_highway_connection)
+    cache = {"net": net, "sample_op": x, "highway_test_ratio": ratio, "prev_samples": prev}
+    return out, 0, cache

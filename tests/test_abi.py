@@ -12,8 +12,8 @@ from conftest import ROOT, pkg_mod
 from oracle import spec, weightgen
 
 
-def _header_symbols():
-    txt = open(os.path.join(ROOT, "include", "svae_hip.h")).read()
+def _header_symbols(name="svae_hip.h"):
+    txt = open(os.path.join(ROOT, "include", name)).read()
     return sorted(set(re.findall(r"\b(svae_[a-z0-9_]+)\s*\(", txt)))
 
 
@@ -24,6 +24,17 @@ def test_library_exports_header_symbols(built_lib):
     for s in syms:
         assert hasattr(lib, s), s
     assert sorted(pkg_mod("_lib").EXPORTED) == syms
+
+
+def test_library_exports_pcnn_symbols(built_lib):
+    """include/svae_pcnn.h (the PixelCNN++ head): every entry point is exported and
+    has a ctypes signature."""
+    lib = ctypes.CDLL(built_lib)
+    syms = _header_symbols("svae_pcnn.h")
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert sorted(pkg_mod("_lib").PCNN_EXPORTED) == syms
 
 
 @pytest.mark.parametrize("preset", ["tiny", "celeba", "lsun", "mnist_1step"])
