@@ -75,8 +75,10 @@ int svae_pcnn_gate_bwd(const float* c2, const float* hp, const float* dout, int 
  * A(m,k) = ta ? A[k*lda + m] : A[m*lda + k], B(k,n) = tb ? B[n*ldb + k] : B[k*ldb + n]. */
 int svae_pcnn_gemm_small(const float* A, int lda, int ta, const float* B, int ldb, int tb, float* C, int ldc, int m,
                          int n, int k, float beta, void* stream);
-/* per-image channel sums: out[img][c] = sum_{p < pix_per_img} x[img*pix + p][c]. */
-int svae_pcnn_imgsum(const float* x, int ldx, int nimg, int pix_per_img, int c, float* out, void* stream);
+/* per-image channel sums: out[img][c] = sum_{p < pix_per_img} x[img*pix + p][c] (fixed order over
+ * 256-pixel partials in `scratch`, nimg * c * ceil(pix_per_img / 256) floats). */
+int svae_pcnn_imgsum(const float* x, int ldx, int nimg, int pix_per_img, int c, float* out, float* scratch,
+                     void* stream);
 
 /* strided channel copy: y[r][0..c) = x[r][0..c) (concat / split of channel slices). */
 int svae_pcnn_copy(const float* x, int ldx, int64_t rows, int c, float* y, int ldy, int accumulate, void* stream);

@@ -112,7 +112,7 @@ def lib():
         "svae_pcnn_gate": ([vp, i32, vp, vp, i64, i32, i32, vp, i32, vp], i32),
         "svae_pcnn_gate_bwd": ([vp, vp, vp, i32, i64, i32, i32, vp, vp], i32),
         "svae_pcnn_gemm_small": ([vp, i32, i32, vp, i32, i32, vp, i32, i32, i32, i32, f32, vp], i32),
-        "svae_pcnn_imgsum": ([vp, i32, i32, i32, i32, vp, vp], i32),
+        "svae_pcnn_imgsum": ([vp, i32, i32, i32, i32, vp, vp, vp], i32),
         "svae_pcnn_copy": ([vp, i32, i64, i32, vp, i32, i32, vp], i32),
         "svae_pcnn_pad_ones": ([vp, i64, i32, vp, i32, vp], i32),
         "svae_pcnn_mixlogistic": ([vp, vp, i64, i32, vp, vp, f32, vp], i32),

@@ -65,21 +65,29 @@ __device__ __forceinline__ bool pc_src(const PcGeom& g, int oy, int ox, int ky, 
 // ---------------------------------------------------------------------------------------------
 // weight norm (nn.py:173, :201, :236)
 // ---------------------------------------------------------------------------------------------
-// norm[co] = sqrt(sum_{tap, ci} V^2): one block per 64 output channels, fixed-order sums
+// fixed-order block sum (256 threads, fp64)
+__device__ __forceinline__ double block_sum256(double v, double* red) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  return red[0];
+}
+
+// norm[co] = sqrt(sum_{tap, ci} V^2): one block per output channel, fixed-order sums
 __global__ __launch_bounds__(256) void wn_norm_kernel(const float* __restrict__ V, int K, int cout,
                                                       float* __restrict__ norm) {
-  __shared__ double red[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6;
+  __shared__ double red[256];
+  const int c = blockIdx.x;
   double s = 0.0;
-  if (c < cout)
-    for (int k = q; k < K; k += 4) {
-      const double v = V[(long long)k * cout + c];
-      s += v * v;
-    }
-  red[q][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (q == 0 && c < cout) norm[c] = (float)sqrt(red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
-                                                red[3][threadIdx.x]);
+  for (int k = threadIdx.x; k < K; k += 256) {
+    const double v = V[(long long)k * cout + c];
+    s += v * v;
+  }
+  s = block_sum256(s, red);
+  if (threadIdx.x == 0) norm[c] = (float)sqrt(s);
 }
 
 // W = g / norm * V -> wk_f [tap][co][kf] (K = ci) and wk_d [tap][ci][kd] (K = co), zero padded
@@ -108,19 +116,16 @@ __global__ void wn_apply_kernel(const float* __restrict__ V, const float* __rest
   }
 }
 
-// dg[co] = sum_k dW V / norm  (fixed order, fp64)
+// dg[co] = sum_k dW V / norm  (one block per output channel, fixed order, fp64)
 __global__ __launch_bounds__(256) void wn_dg_kernel(const float* __restrict__ V, const float* __restrict__ dW,
                                                     const float* __restrict__ norm, int K, int cout,
                                                     float* __restrict__ dg) {
-  __shared__ double red[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6;
+  __shared__ double red[256];
+  const int c = blockIdx.x;
   double s = 0.0;
-  if (c < cout)
-    for (int k = q; k < K; k += 4) s += (double)dW[(long long)k * cout + c] * V[(long long)k * cout + c];
-  red[q][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (q == 0 && c < cout)
-    dg[c] = (float)((red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]) / norm[c]);
+  for (int k = threadIdx.x; k < K; k += 256) s += (double)dW[(long long)k * cout + c] * V[(long long)k * cout + c];
+  s = block_sum256(s, red);
+  if (threadIdx.x == 0) dg[c] = (float)(s / norm[c]);
 }
 
 __global__ void wn_dv_kernel(const float* __restrict__ V, const float* __restrict__ g, const float* __restrict__ norm,
@@ -430,18 +435,23 @@ __global__ void gemm_small_kernel(const float* __restrict__ A, int lda, int ta, 
   }
 }
 
-// per-image channel sums: block (64-column group, image), fixed order
+// per-image channel sums: block (64-column group, image, pixel split) -> part[split][img][c],
+// then a fixed-order sum over the splits
+#define IMGSUM_PIX 256
 __global__ __launch_bounds__(256) void imgsum_kernel(const float* __restrict__ x, int ldx, int per_img, int c,
-                                                     float* __restrict__ out) {
+                                                     float* __restrict__ part) {
   __shared__ float red[4][64];
   const int col = blockIdx.x * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6, img = blockIdx.y;
+  const int p0 = blockIdx.z * IMGSUM_PIX;
+  const int p1 = p0 + IMGSUM_PIX < per_img ? p0 + IMGSUM_PIX : per_img;
   float s = 0.f;
   if (col < c)
-    for (int p = q; p < per_img; p += 4) s += x[((long long)img * per_img + p) * ldx + col];
+    for (int p = p0 + q; p < p1; p += 4) s += x[((long long)img * per_img + p) * ldx + col];
   red[q][threadIdx.x & 63] = s;
   __syncthreads();
   if (q == 0 && col < c)
-    out[(long long)img * c + col] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    part[((long long)blockIdx.z * gridDim.y + img) * c + col] =
+        red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
 }
 
 __global__ void copy_kernel(const float* __restrict__ x, int ldx, long long rows, int c, float* __restrict__ y,
@@ -696,7 +706,7 @@ int svae_pcnn_wnorm(const float* V, const float* g, int taps, int cin, int cout,
   if (!V || !g || !norm || taps < 1 || cin < 1 || cout < 1) return bad("pcnn_wnorm: bad arguments");
   if ((wk_f && (kf < cin || kf % 16)) || (wk_d && (kd < cout || kd % 16))) return bad("pcnn_wnorm: bad padding");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(wn_norm_kernel, dim3((cout + 63) / 64), dim3(256), 0, s, V, taps * cin, cout, norm);
+  hipLaunchKernelGGL(wn_norm_kernel, dim3(cout), dim3(256), 0, s, V, taps * cin, cout, norm);
   const long long n = (wk_f ? (long long)taps * cout * kf : 0) + (wk_d ? (long long)taps * cin * kd : 0);
   if (n) hipLaunchKernelGGL(wn_apply_kernel, dim3(blocks_for(n)), dim3(256), 0, s, V, g, norm, taps, cin, cout,
                             (__bf16*)wk_f, kf, (__bf16*)wk_d, kd);
@@ -707,7 +717,7 @@ int svae_pcnn_wnorm_bwd(const float* V, const float* g, const float* norm, const
                         int cout, float* dV, float* dg, void* stream) {
   if (!V || !g || !norm || !dW || !dV || !dg || taps < 1 || cin < 1 || cout < 1) return bad("pcnn_wnorm_bwd: bad arguments");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(wn_dg_kernel, dim3((cout + 63) / 64), dim3(256), 0, s, V, dW, norm, taps * cin, cout, dg);
+  hipLaunchKernelGGL(wn_dg_kernel, dim3(cout), dim3(256), 0, s, V, dW, norm, taps * cin, cout, dg);
   const long long n = (long long)taps * cin * cout;
   hipLaunchKernelGGL(wn_dv_kernel, dim3(blocks_for(n)), dim3(256), 0, s, V, g, norm, dW, dg, n, cout, dV);
   return hipchk();
@@ -763,8 +773,9 @@ int svae_pcnn_colsum(const float* x, int64_t rows, int c, int ldx, int ho, int w
                      int accumulate, float* scratch, void* stream) {
   if (!x || !out || !scratch || rows < 1 || c < 1 || ldx < c || (mask_edge && (ho < 1 || wo < 1)))
     return bad("pcnn_colsum: bad arguments");
-  long long ns = (rows + 2047) / 2048;
-  if (ns > 256) ns = 256;
+  long long ns = (rows + 255) / 256;  // ~256 rows per block: hundreds of blocks for the 64x64 layers
+  if (ns > 1024) ns = 1024;
+  if (ns * c > (1LL << 24)) ns = ((1LL << 24) / c > 0) ? (1LL << 24) / c : 1;
   const long long rps = (rows + ns - 1) / ns;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(colsum_part_kernel_pc, dim3((c + 63) / 64, (unsigned)ns), dim3(256), 0, st, x, (long long)rows, c,
@@ -824,10 +835,14 @@ int svae_pcnn_gemm_small(const float* A, int lda, int ta, const float* B, int ld
   return hipchk();
 }
 
-int svae_pcnn_imgsum(const float* x, int ldx, int nimg, int pix_per_img, int c, float* out, void* stream) {
-  if (!x || !out || nimg < 1 || pix_per_img < 1 || c < 1 || ldx < c) return bad("pcnn_imgsum: bad arguments");
-  hipLaunchKernelGGL(imgsum_kernel, dim3((c + 63) / 64, nimg), dim3(256), 0, (hipStream_t)stream, x, ldx, pix_per_img,
-                     c, out);
+int svae_pcnn_imgsum(const float* x, int ldx, int nimg, int pix_per_img, int c, float* out, float* scratch,
+                     void* stream) {
+  if (!x || !out || !scratch || nimg < 1 || pix_per_img < 1 || c < 1 || ldx < c) return bad("pcnn_imgsum: bad arguments");
+  const int ps = (pix_per_img + IMGSUM_PIX - 1) / IMGSUM_PIX;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(imgsum_kernel, dim3((c + 63) / 64, nimg, ps), dim3(256), 0, st, x, ldx, pix_per_img, c, scratch);
+  const long long n = (long long)nimg * c;
+  hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(n)), dim3(256), 0, st, scratch, ps, n, out);
   return hipchk();
 }
 

@@ -158,6 +158,7 @@ class PixelCNNpp:
         self._dh = None
         self._tape, self._g, self._keep, self._same, self._cnt = [], {}, [], {}, {}
         self._record = self._init = False
+        self.conv_flops = 0.0  # running total of forward conv FLOPs (tools/bench_pcnn.py)
 
     # ---------------- parameters ----------------
     def init_values(self, seed=0):
@@ -244,6 +245,8 @@ class PixelCNNpp:
                               ctypes.c_void_p(wkd.data_ptr()), kd, st))
         if ho is None:
             ho, wo = (x.h - 1) // s + 1, (x.w - 1) // s + 1
+        # algorithmic FLOPs of the forward gather GEMM (valid taps only for the stride-2 deconvs)
+        self.conv_flops += 2.0 * x.n * ho * wo * cout * cin * taps / (s * s if mode == 1 else 1)
         acc = out is not None
         if out is None:
             out = Act(self._new(x.n * ho * wo, cout), cout, x.n, ho, wo)
@@ -344,7 +347,7 @@ class PixelCNNpp:
                 dc2 = self._grad(c2)
                 _ck(self.L.svae_pcnn_gate_bwd(c2.ptr(), _p(hp), _p(dy), F, x.rows, x.h * x.w, F, _p(dc2), st2))
                 dhp = torch.empty(x.n, 2 * F, dtype=torch.float32, device=self.dev)
-                _ck(self.L.svae_pcnn_imgsum(_p(dc2), 2 * F, x.n, x.h * x.w, 2 * F, _p(dhp), st2))
+                _ck(self.L.svae_pcnn_imgsum(_p(dc2), 2 * F, x.n, x.h * x.w, 2 * F, _p(dhp), _p(self.scratch), st2))
                 # d hw [K][2F] = h^T . dhp
                 _ck(self.L.svae_pcnn_gemm_small(_p(h), K, 1, _p(dhp), 2 * F, 0, _p(self.G, off_hw), 2 * F, K, 2 * F,
                                                 x.n, 0.0, st2))
