@@ -476,10 +476,13 @@ struct svae_ctx {
   // work on both streams; t = -1 after the whole backward (streams joined)
   // split-latent FCs on the side stream: forward for all steps up front (they depend only on z),
   // backward per level off the critical path, reading ring copies of dcat / dtop
-  float* dcat_ring[2] = {};
-  float* dtop_ring[2] = {};
-  int dcat_pos = 0, dtop_pos = 0;
-  hipEvent_t ev_dcat_free[2] = {}, ev_dtop_free[2] = {}, ev_aux = nullptr, ev_aux2 = nullptr;
+  // their inputs (dcat, dtop) and the output layer's da: per-pass regions as for dpre
+  float* dcat_arena = nullptr;
+  float* dtop_arena = nullptr;
+  float* da_base = nullptr;  // [T][B*H*W][C+1]: step t's da (the output weight gradient reads it on st2)
+  long long dcat_cap = 0, dcat_off = 0, dtop_cap = 0, dtop_off = 0;
+  hipEvent_t ev_drain3 = nullptr;
+  hipEvent_t ev_aux = nullptr, ev_aux2 = nullptr;
   hipEvent_t ev_sfc[64] = {};
   svae_step_hook hook = nullptr;
   void* hook_user = nullptr;
@@ -717,11 +720,13 @@ struct Slot {
 };
 // next region of `n` elements of a per-pass arena; on overflow (a geometry the plan did not
 // size) the main stream waits for the side stream to drain and the arena starts over
-static float* arena_next(svae_ctx* c, float* base, long long cap, long long& off, long long n) {
+static float* arena_next(svae_ctx* c, float* base, long long cap, long long& off, long long n,
+                         bool st3_reads = false) {
   n = (n + 63) / 64 * 64;
   if (off + n > cap) {
-    hipEventRecord(c->ev_drain, c->st2);
-    hipStreamWaitEvent(c->st, c->ev_drain, 0);
+    hipEvent_t ev = st3_reads ? c->ev_drain3 : c->ev_drain;
+    hipEventRecord(ev, st3_reads ? c->st3 : c->st2);
+    hipStreamWaitEvent(c->st, ev, 0);
     off = 0;
   }
   float* p = base + off;
@@ -1520,12 +1525,8 @@ static int engine_backward(svae_ctx* c) {
     // re-arm the slot-free events on the main stream: the previous backward's side-stream work
     // was joined into it, so "free" holds now, and every later wait depends only on work of this
     // pass (required when the step is captured into a graph)
-    c->dpre_off = c->idpre_off = 0;  // the previous pass's readers were joined into this stream
-    for (int i = 0; i < 2; ++i) {
-      hipEventRecord(c->ev_dcat_free[i], st);
-      hipEventRecord(c->ev_dtop_free[i], st);
-    }
-    hipEventRecord(c->ev_da_free, st);
+    // the previous pass's readers were joined into this stream: every per-pass region is free
+    c->dpre_off = c->idpre_off = c->dcat_off = c->dtop_off = 0;
   }
   for (int t = T - 1; t >= 0; --t) {
     if (t < T - 1) {
@@ -1555,7 +1556,7 @@ static int engine_backward(svae_ctx* c) {
     float* dzt = c->dz + (long long)t * B * g.Dz;
 
     // ---- output + highway (:1720-1729)
-    if (c->side) hipStreamWaitEvent(st, c->ev_da_free, 0);  // previous step's output wgrad read da
+    c->da = c->da_base + (long long)t * P0 * C1;  // own region per step: no wait for the previous reader
     if (g.pgn) {  // NLL + sample = mle + reg*sd*noise: d mle and the stddev network, then the output layer
       sd_backward(c, t, dxin, rec_coef);  // rec_coef = 16 cf / (B H W C), the NLL's element weight
       if (c->imp_pass)  // the improvement seed is on the MLE, not on the noisy sample: no stddev term
@@ -1585,7 +1586,7 @@ static int engine_backward(svae_ctx* c) {
                      256);
       else
         choose_split(w.rows, 16, (F[1] + 127) / 128, 1, 16LL * M_out * F[1], c->slab_cap, w.nsplit, w.chunk);
-      on_side(c, c->ev_da_ready, c->ev_da_free, [&] {
+      on_side(c, c->ev_da_ready, nullptr, [&] {
         w.part = c->slab;
         wgemm(c, w, 1);
         wgrad_reduce(c->slab, 0, w.nsplit, 16, M_out, F[1], c->Gr + G.owout, 0, g.C,
@@ -1626,15 +1627,8 @@ static int engine_backward(svae_ctx* c) {
       // s2[lvl]'s BN partials over the d-half of dcat (shortcut at t >= 1: act' from the stored y)
       BwFuse fu_s2 = bw_fuse(c, s.s2_pre[lvl], Fl, 0, t >= 1 ? s.cat[lvl] : nullptr, 2 * Fl, 0, s.s2_bn[lvl], 0,
                              l2.obeta, 0, ACT_RELU, Fl);
-      // dcat: ring of two when the split-latent backward reads it on the side stream
-      float* dcat = c->dcat;
-      int kc = 0;
-      if (c->side) {
-        kc = c->dcat_pos;
-        c->dcat_pos ^= 1;
-        dcat = c->dcat_ring[kc];
-        hipStreamWaitEvent(st, c->ev_dcat_free[kc], 0);
-      }
+      // dcat: its own region per pass when the split-latent backward reads it on the side stream
+      float* dcat = c->side ? arena_next(c, c->dcat_arena, c->dcat_cap, c->dcat_off, rows * 2 * Fl, true) : c->dcat;
       r = conv_dgrad(c, l1, 1, 0, sl.p, 0, View{dcat, 2 * Fl, 0}, 0, &fu_s2);
       if (r) return r;
       // latent half of the concat -> split_latent level lvl (side stream: off the critical path)
@@ -1652,7 +1646,6 @@ static int engine_backward(svae_ctx* c) {
                     s.split_mean[lvl], s.split_inv[lvl], dcat + Fl, (long long)S[lvl + 1] * S[lvl + 1] * 2 * Fl, Fl,
                     2 * Fl, c->Gr + f.ow, c->Gr + f.obeta, c->sfc_part, ss);
         splitfc_dz_reduce(c->sfc_part, splitfc_blocks(f.nout), B, g.D[lvl], dzt, g.Dz, zoff, ss);
-        if (c->side) hipEventRecord(c->ev_dcat_free[kc], c->st3);
       }
       // s2: relu(BN(convT_s2(cur)) + enc_{lvl+1})
       View dres = t >= 1 ? View{c->denc[lvl], Fl, 0} : View{};
@@ -1676,14 +1669,9 @@ static int engine_backward(svae_ctx* c) {
     }
     // ---- top fc_bn_lrelu (:1704)
     const int ntop = S[L] * S[L] * F[L];
-    float* dtop = c->dtop;
-    int kt = 0;
-    if (c->side) {  // ring of two: the side stream's split-latent backward reads it
-      kt = c->dtop_pos;
-      c->dtop_pos ^= 1;
-      dtop = c->dtop_ring[kt];
-      hipStreamWaitEvent(st, c->ev_dtop_free[kt], 0);
-    }
+    // own region per pass when the side stream's split-latent backward reads it
+    float* dtop = c->side ? arena_next(c, c->dtop_arena, c->dtop_cap, c->dtop_off, (long long)B * s.ktop, true)
+                          : c->dtop;
     r = fc_bn_bwd(c, G.top, View{s.top_cat, s.ktop, 0}, View{dcur, ntop, 0}, View{s.top_act, ntop, 0}, s.top_pre,
                   s.top_bn, View{dtop, s.ktop, 0});
     if (r) return r;
@@ -1700,10 +1688,7 @@ static int engine_backward(svae_ctx* c) {
                   f.nout, s.split_mean[L - 1], s.split_inv[L - 1], dtop + coff, s.ktop, f.nout, 0, c->Gr + f.ow,
                   c->Gr + f.obeta, c->sfc_part, ss);
       splitfc_dz_reduce(c->sfc_part, splitfc_blocks(f.nout), B, g.D[L - 1], dzt, g.Dz, g.Dz - g.D[L - 1], ss);
-      if (c->side) {
-        hipEventRecord(c->ev_dtop_free[kt], c->st3);
-        hipEventRecord(c->ev_dz, c->st3);  // dz_t complete (the top level is the step's last split FC)
-      }
+      if (c->side) hipEventRecord(c->ev_dz, c->st3);  // dz_t complete (the top level is the step's last split FC)
     }
     // ---- g_theta encoder of x_{t-1} (reverse of :1764-1775)
     if (t >= 1) {
@@ -1914,7 +1899,8 @@ static bool plan(svae_ctx* c) {
   const long long P0 = (long long)B * g.H * g.W;
   c->dx[0] = A(P0 * g.C);
   c->dx[1] = A(P0 * g.C);
-  c->da = A(P0 * C1);
+  c->da_base = A((long long)T * P0 * C1);
+  c->da = c->da_base;
   c->dcur = A(maxact);
   c->dnext = A(maxact);
   c->dpre = A(maxact);
@@ -1942,10 +1928,14 @@ static bool plan(svae_ctx* c) {
   }
   c->dcat = A(maxact);
   c->dtop = A((long long)B * (F[L] + F[L + 1]));
-  c->dcat_ring[0] = c->dcat;
-  c->dcat_ring[1] = A(maxact);
-  c->dtop_ring[0] = c->dtop;
-  c->dtop_ring[1] = A((long long)B * (F[L] + F[L + 1]));
+  {  // per-pass regions of dcat (every decoder level of every step) and dtop (every step)
+    long long n = 0;
+    for (int lvl = 0; lvl < L - 1; ++lvl) n += ((long long)B * S[lvl + 1] * S[lvl + 1] * 2 * F[lvl + 1] + 63) / 64 * 64;
+    c->dcat_cap = T * n;
+    c->dcat_arena = A(c->dcat_cap);
+    c->dtop_cap = T * (((long long)B * (F[L] + F[L + 1]) + 63) / 64 * 64);
+    c->dtop_arena = A(c->dtop_cap);
+  }
   c->denc_c = A((long long)B * S[L] * S[L] * F[L - 1]);
   for (int lvl = 0; lvl < L - 1; ++lvl) c->denc[lvl] = A((long long)B * S[lvl + 1] * S[lvl + 1] * F[lvl + 1]);
   c->sfc_part = A((long long)splitfc_blocks((int)maxJ) * B * maxK);
@@ -2148,7 +2138,7 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
       mk(&c->ev_drain);
       mk(&c->ev_da_ready); mk(&c->ev_da_free); mk(&c->ev_start); mk(&c->ev_join); mk(&c->ev_hook);
       mk(&c->ev_aux); mk(&c->ev_aux2); mk(&c->ev_dz); mk(&c->ev_j3); mk(&c->ev_j4);
-      for (int i = 0; i < 2; ++i) { mk(&c->ev_dcat_free[i]); mk(&c->ev_dtop_free[i]); }
+      mk(&c->ev_drain3);
       for (int i = 0; i < 64; ++i) mk(&c->ev_sfc[i]);
       c->side = ok;
     }
@@ -2166,7 +2156,7 @@ int svae_destroy(svae_ctx* c) {
       hipStreamDestroy(sx);
     }
   for (hipEvent_t ev : {c->ev_da_ready, c->ev_da_free, c->ev_start, c->ev_join, c->ev_hook, c->ev_aux, c->ev_aux2, c->ev_dz, c->ev_j3, c->ev_j4,
-                        c->ev_dcat_free[0], c->ev_dcat_free[1], c->ev_dtop_free[0], c->ev_dtop_free[1]})
+                        c->ev_drain3})
     if (ev) hipEventDestroy(ev);
   for (hipEvent_t ev : c->ev_sfc)
     if (ev) hipEventDestroy(ev);

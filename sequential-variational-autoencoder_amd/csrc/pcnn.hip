@@ -731,15 +731,16 @@ int svae_pcnn_conv(const float* x, int n, int hi, int wi, int cin, int ldx, cons
     return bad("pcnn_conv: bad arguments");
   const long long rows = (long long)n * ho * wo;
   hipStream_t st = (hipStream_t)stream;
-  const dim3 grid((unsigned)((rows + 127) / 128), 1);
-  if (cout > 32) {
-    const dim3 g2(grid.x, (cout + 63) / 64);
-    hipLaunchKernelGGL(pc_conv_kernel<2>, g2, dim3(256), 0, st, g, x, (const __bf16*)wk, kpad, bias, y, ldy,
+  // two 32-column subtiles per wave: wider tiles (up to 5, every A fragment feeding 5 MFMAs)
+  // measured slower -- a third of the waves, and this kernel hides its load latency by occupancy
+  const __bf16* w = (const __bf16*)wk;
+  const unsigned gx = (unsigned)((rows + 127) / 128);
+  if (cout > 32)
+    hipLaunchKernelGGL(pc_conv_kernel<2>, dim3(gx, (cout + 63) / 64), dim3(256), 0, st, g, x, w, kpad, bias, y, ldy,
                        accumulate, zero_edge);
-  } else {
-    hipLaunchKernelGGL(pc_conv_kernel<1>, grid, dim3(256), 0, st, g, x, (const __bf16*)wk, kpad, bias, y, ldy,
-                       accumulate, zero_edge);
-  }
+  else
+    hipLaunchKernelGGL(pc_conv_kernel<1>, dim3(gx, 1), dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate,
+                       zero_edge);
   return hipchk();
 }
 
@@ -773,7 +774,7 @@ int svae_pcnn_colsum(const float* x, int64_t rows, int c, int ldx, int ho, int w
                      int accumulate, float* scratch, void* stream) {
   if (!x || !out || !scratch || rows < 1 || c < 1 || ldx < c || (mask_edge && (ho < 1 || wo < 1)))
     return bad("pcnn_colsum: bad arguments");
-  long long ns = (rows + 255) / 256;  // ~256 rows per block: hundreds of blocks for the 64x64 layers
+  long long ns = (rows + 255) / 256;  // ~256 rows per block (1024-row blocks measured slower)
   if (ns > 1024) ns = 1024;
   if (ns * c > (1LL << 24)) ns = ((1LL << 24) / c > 0) ? (1LL << 24) / c : 1;
   const long long rps = (rows + ns - 1) / ns;
