@@ -9,6 +9,7 @@ GPU (B=128, weak scaling).  Inputs are resident in HBM before the timed region.
 N>1 is launched by the driver via torch.distributed.run (one rank per GPU).
 """
 import argparse
+import ctypes
 import importlib
 import json
 import math
@@ -106,6 +107,50 @@ def time_dominant_kernel(L, shape, iters=50):
     sec = e0.elapsed_time(e1) / 1000.0 / iters
     flops = 2.0 * n * h * h * cout * 16 * cin
     return sec, flops
+
+
+def isolated_wgrad(L, cfg, iters=20):
+    """The dominant kernel's launches of one step, each timed alone on an idle GPU (HIP events,
+    svae_op_wgrad_bf16 with the step's operand storage): the stride-1 halo weight-GEMMs of the
+    decoder s1 conv-Ts (dY bf16, input = the fp32 concat), the encoder b convs (both bf16) and the
+    T-batched recognition b convs (both bf16; one launch of T*B images).  In the step these run on
+    the side stream concurrently with the main stream's kernels, which is why the live average is
+    higher: this separates the kernel's own speed from that sharing."""
+    F, S, T, B = cfg.filter_sizes, cfg.image_sizes, cfg.mc_steps, cfg.batch
+    shapes = []  # (n, h, cin, cout, transpose, x_bf16, dy_bf16, launches per step)
+    for lvl in range(cfg.levels - 1):
+        Fl, h = F[lvl + 1], S[lvl + 1]
+        shapes.append((B, h, 2 * Fl, Fl, 1, 0, 1, T))
+        shapes.append((B, h, Fl, Fl, 0, 1, 1, T - 1))
+        shapes.append((T * B, h, Fl, Fl, 0, 1, 1, 1))
+    scratch = torch.empty(64 << 20, device="cuda")
+    tot_t = tot_f = 0.0
+    n_launch = 0
+    for (n, h, cin, cout, tr, xb, db, cnt) in shapes:
+        if cnt < 1:
+            continue
+        x = torch.randn(n, h, h, cin, device="cuda").to(torch.bfloat16 if xb else torch.float32)
+        dy = (torch.randn(n, h, h, cout, device="cuda") * 0.1).to(torch.bfloat16 if db else torch.float32)
+        dw = torch.empty(16 * cin * cout, device="cuda")
+        path = 2 | (16 if xb else 0) | (32 if db else 0)
+        args = (ctypes.c_void_p(x.data_ptr()), n, h, cin, ctypes.c_void_p(dy.data_ptr()), cout, 1, tr, path,
+                L.ptr(dw), L.ptr(scratch), scratch.numel() * 4, L.stream_ptr())
+        L.check(L.lib().svae_op_wgrad_bf16(*args))
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            L.lib().svae_op_wgrad_bf16(*args)
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / iters  # kernel + its split reduce, as launched by the engine
+        tot_t += us * cnt
+        tot_f += 2.0 * 16 * cin * cout * n * h * h * cnt
+        n_launch += cnt
+    ach = tot_f / (tot_t * 1e-6) / 1e12
+    return dict(achieved=round(ach, 3), frac=round(ach / BF16_MFMA_PEAK_TFLOPS, 5),
+                avg_launch_us=round(tot_t / n_launch, 2), launches=n_launch,
+                method="each of the step's launches alone on the idle GPU (svae_op_wgrad_bf16, split reduce "
+                       "included), same shapes and operand storage; the live figure above is the in-step one")
 
 
 def pmc_traffic(kernel):
@@ -284,7 +329,6 @@ def main():
     elapsed = time.perf_counter() - t0
     probe = None
     if probe_kid is not None and rank == 0:
-        import ctypes
         n, nt = ctypes.c_int64(), ctypes.c_int64()
         fl, ms_k = ctypes.c_double(), ctypes.c_double()
         L.check(L.lib().svae_probe_end(net.ctx, ctypes.byref(n), ctypes.byref(nt), ctypes.byref(fl),
@@ -330,6 +374,8 @@ def main():
                         "x".join(str(shape[k]) for k in ("n", "h", "cin", "cout"))),
                     kernel_us=round(sec * 1e6, 2),
                     step_achieved_tflops=round(flops_img * value / world / 1e12, 3))
+    if rank == 0 and roof is not None and probe is not None and probe["timed"] > 0:
+        roof["isolated"] = isolated_wgrad(L, cfg)
     fp32_value = fp32_ms = None
     if world == 1 and args.dtype == "bf16" and not args.no_fp32:
         net.close()

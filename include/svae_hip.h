@@ -198,8 +198,9 @@ int svae_op_gather_bf16(const float* x, int n, int h, int cin, const void* w_nk,
                         int path, float* y, void* scratch, int64_t scratch_bytes, void* stream);
 /* bf16 weight gradient of a conv (transpose=0) / conv-T (transpose=1) layer: dw in TF layout
  * ([4,4,cin,cout] / [4,4,cout,cin]) from fp32 NHWC x and dy, operands rounded to bf16, fp32
- * accumulation.  path: 0 tap-merged weight-GEMM kernel, 2 halo weight-GEMM where it qualifies.
- * scratch: split slab (required). */
+ * accumulation.  path: 0 tap-merged weight-GEMM kernel, 2 halo weight-GEMM where it qualifies;
+ * + 16: x is a bf16 tensor, + 32: dy is a bf16 tensor (the engine's bf16 activation / BN-backward
+ * storage, opload.h).  scratch: split slab (required). */
 int svae_op_wgrad_bf16(const float* x, int n, int h, int cin, const float* dy, int cout, int stride, int transpose,
                        int path, float* dw, void* scratch, int64_t scratch_bytes, void* stream);
 int svae_op_conv_dgrad(const float* dy, int n, int h, int cin, const float* w, int cout, int stride, int transpose,

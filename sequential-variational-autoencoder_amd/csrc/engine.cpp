@@ -1317,7 +1317,11 @@ static int engine_forward(svae_ctx* c) {
   }  // !generative
   // split_latent of every step on the side stream (z is known for all steps unless Latent
   // InfoMax draws z_t inside the chain); step t's decoder waits on ev_sfc[t]
-  const bool sfc_side = c->side && !g.plc && T <= 64;
+  static const int sfc_mode = [] {  // SVAE_SFC: 0 = split-latent forward on the main stream per step
+    const char* v = getenv("SVAE_SFC");
+    return v ? atoi(v) : 1;
+  }();
+  const bool sfc_side = sfc_mode != 0 && c->side && !g.plc && T <= 64;
   if (sfc_side) {
     hipEventRecord(c->ev_aux, st);
     hipStreamWaitEvent(c->st3, c->ev_aux, 0);
@@ -2531,11 +2535,14 @@ int svae_op_gather_bf16(const float* x, int n, int h, int cin, const void* w_nk,
 
 int svae_op_wgrad_bf16(const float* x, int n, int h, int cin, const float* dy, int cout, int stride, int transpose,
                        int path, float* dw, void* scratch, int64_t scratch_bytes, void* stream) {
+  const int xbf = (path >> 4) & 1, dybf = (path >> 5) & 1;  // operand storage bits (bf16 tensors)
+  path &= 15;
   if (!x || !dy || !dw || !scratch || (path != 0 && path != 2 && path != 3))
     return fail(nullptr, SVAE_EBADARG, "bad op args");
   static svae_ctx dummy;
   dummy.m.g.B = n;
   dummy.m.g.bf16 = 1;
+  dummy.dbf = dybf;
   dummy.wg_path = path;
   dummy.st = (hipStream_t)stream;
   dummy.slab = (float*)scratch;
@@ -2543,8 +2550,9 @@ int svae_op_wgrad_bf16(const float* x, int n, int h, int cin, const float* dy, i
   ConvL L;
   L.cin = cin; L.cout = cout; L.stride = stride; L.hin = h; L.tr = transpose != 0;
   L.hout = L.tr ? h * stride : h / stride;
-  const int r = conv_wgrad(&dummy, L, 1, 0, View{(float*)x, cin, 0}, dy, 0, dw);
+  const int r = conv_wgrad(&dummy, L, 1, 0, View{(float*)x, cin, 0, xbf}, dy, 0, dw);
   dummy.m.g.bf16 = 0;
+  dummy.dbf = 0;
   if (r) return fail(nullptr, r, dummy.err);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(nullptr, SVAE_EHIP, hipGetErrorString(e));
