@@ -4,6 +4,7 @@
 // sampler.  C ABI: include/svae_pcnn.h.  Reference: pixel_cnn/pixel_cnn_pp/{model,nn}.py,
 // pixel_cnn/pixelvae.py (cited per function).
 #include <math.h>
+#include <cstdlib>
 #include <string>
 
 #include "common.h"
@@ -199,6 +200,120 @@ __global__ __launch_bounds__(256) void pc_conv_kernel(PcGeom g, const float* __r
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const long long mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (mm >= rows) continue;
+    bool zero = false;
+    if (zero_edge) {
+      const int rr = (int)(mm % per_img);
+      zero = zero_edge == 1 ? (rr / g.wo == 0) : (rr % g.wo == 0);
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int n = n0 + t * 32 + l32;
+      if (n >= g.cout) continue;
+      float val = zero ? 0.f : acc[t][r] + (bias ? bias[n] : 0.f);
+      float* p = Y + mm * ldy + n;
+      if (accumulate) val += *p;
+      *p = val;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// LDS-staged gather conv: block = 128 output pixels x 32*NT output channels, K in chunks of one tap
+// x 32 channels.  Per chunk the block stages the 128 gathered pixel rows (fp32 -> bf16, 16-B
+// stores) and the 32*NT weight rows once in LDS (80-B pitch: conflict-free 16-B fragment reads);
+// each wave then runs 2*NT MFMAs on its 32 rows.  The next chunk's rows are loaded into registers
+// while the current chunk's MFMAs run (double-buffered LDS, one barrier per chunk).  Needs kpad
+// % 32 == 0.
+// ---------------------------------------------------------------------------------------------
+#define PC2_P 40  // LDS row pitch (bf16)
+template <int NT>
+__global__ __launch_bounds__(256) void pc_conv2_kernel(PcGeom g, const float* __restrict__ X,
+                                                       const __bf16* __restrict__ Wk, int kpad,
+                                                       const float* __restrict__ bias, float* __restrict__ Y,
+                                                       int ldy, int accumulate, int zero_edge) {
+  constexpr int BR = 32 * NT;  // weight rows (output channels) per block
+  __shared__ __attribute__((aligned(16))) __bf16 As[2][128 * PC2_P];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[2][BR * PC2_P];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int per_img = g.ho * g.wo;
+  const long long rows = (long long)g.n * per_img;
+  const long long m0 = (long long)blockIdx.x * 128;
+  const int n0 = blockIdx.y * BR;
+  // staging roles: A row ar = tid >> 1, channel half ah (16 channels); B items tid + 256 i
+  const int ar = tid >> 1, ah = tid & 1;
+  const long long am = m0 + ar;
+  int aimg = 0, aoy = 0, aox = 0;
+  const bool amv = am < rows;
+  if (amv) {
+    aimg = (int)(am / per_img);
+    const int r = (int)(am - (long long)aimg * per_img);
+    aoy = r / g.wo;
+    aox = r - aoy * g.wo;
+  }
+  constexpr int BI = (BR * 4 + 255) / 256;  // 16-B weight items per thread (4 per row of 32 k)
+  const int nk = kpad / 32, ntap = g.kh * g.kw, nchunk = ntap * nk;
+  f32x4 ra[4];
+  pc_bf16x8 rb[BI];
+  auto load = [&](int c) {
+    const int tap = c / nk, k0 = (c - tap * nk) * 32;
+    const int ky = tap / g.kw, kx = tap - ky * g.kw;
+    int iy = 0, ix = 0;
+    const bool v = amv && pc_src(g, aoy, aox, ky, kx, iy, ix);
+    const float* xp = X + ((long long)(aimg * g.hi + iy) * g.wi + ix) * g.ldx + k0 + 16 * ah;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ci = k0 + 16 * ah + 4 * j;
+      ra[j] = (v && ci < g.cin) ? *(const f32x4*)(xp + 4 * j) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const __bf16* wp = Wk + (long long)tap * g.cout * kpad + k0;
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int it = tid + 256 * i, row = it >> 2, q = it & 3;
+      pc_bf16x8 z = {};
+      rb[i] = (row < BR && n0 + row < g.cout) ? *(const pc_bf16x8*)(wp + (long long)(n0 + row) * kpad + q * 8) : z;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const pc_f32x8 v8 = {ra[2 * j][0], ra[2 * j][1], ra[2 * j][2], ra[2 * j][3],
+                           ra[2 * j + 1][0], ra[2 * j + 1][1], ra[2 * j + 1][2], ra[2 * j + 1][3]};
+      *(pc_bf16x8*)&As[buf][ar * PC2_P + 16 * ah + 8 * j] = __builtin_convertvector(v8, pc_bf16x8);
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int it = tid + 256 * i, row = it >> 2, q = it & 3;
+      if (row < BR) *(pc_bf16x8*)&Bs[buf][row * PC2_P + q * 8] = rb[i];
+    }
+  };
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int c = 0; c < nchunk; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < nchunk) load(c + 1);
+#pragma unroll
+    for (int kq = 0; kq < 2; ++kq) {
+      const pc_bf16x8 af = *(const pc_bf16x8*)&As[buf][(wave * 32 + l32) * PC2_P + kq * 16 + 8 * h];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const pc_bf16x8 bf = *(const pc_bf16x8*)&Bs[buf][(t * 32 + l32) * PC2_P + kq * 16 + 8 * h];
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc[t], 0, 0, 0);
+      }
+    }
+    if (c + 1 < nchunk) store(buf ^ 1);
+    __syncthreads();
+  }
+  const long long mw = m0 + wave * 32;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const long long mm = mw + (r & 3) + 8 * (r >> 2) + 4 * h;
     if (mm >= rows) continue;
     bool zero = false;
     if (zero_edge) {
@@ -731,10 +846,27 @@ int svae_pcnn_conv(const float* x, int n, int hi, int wi, int cin, int ldx, cons
     return bad("pcnn_conv: bad arguments");
   const long long rows = (long long)n * ho * wo;
   hipStream_t st = (hipStream_t)stream;
-  // two 32-column subtiles per wave: wider tiles (up to 5, every A fragment feeding 5 MFMAs)
-  // measured slower -- a third of the waves, and this kernel hides its load latency by occupancy
   const __bf16* w = (const __bf16*)wk;
   const unsigned gx = (unsigned)((rows + 127) / 128);
+  static const bool old = [] {
+    const char* v = getenv("SVAE_PC_CONV1");
+    return v && v[0] == '1';
+  }();
+  if (kpad % 32 == 0 && !old) {  // LDS-staged kernel, up to 160 output channels per block
+    const int n32 = (cout + 31) / 32;
+    const int tiles = (n32 + 4) / 5;
+    const int NT = (n32 + tiles - 1) / tiles;
+    const dim3 grid(gx, tiles);
+    switch (NT) {
+      case 1: hipLaunchKernelGGL(pc_conv2_kernel<1>, grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge); break;
+      case 2: hipLaunchKernelGGL(pc_conv2_kernel<2>, grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge); break;
+      case 3: hipLaunchKernelGGL(pc_conv2_kernel<3>, grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge); break;
+      case 4: hipLaunchKernelGGL(pc_conv2_kernel<4>, grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge); break;
+      default: hipLaunchKernelGGL(pc_conv2_kernel<5>, grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge); break;
+    }
+    return hipchk();
+  }
+  // register-direct kernel: two 32-column subtiles per wave (wider tiles measured slower here)
   if (cout > 32)
     hipLaunchKernelGGL(pc_conv_kernel<2>, dim3(gx, (cout + 63) / 64), dim3(256), 0, st, g, x, w, kpad, bias, y, ldy,
                        accumulate, zero_edge);

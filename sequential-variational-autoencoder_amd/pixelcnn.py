@@ -39,7 +39,8 @@ def _ck(rc):
 
 
 def _r16(c):
-    return (c + 15) // 16 * 16
+    """K padding of the bf16 weight copies: 32 (the LDS-staged conv's K chunk)."""
+    return (c + 31) // 32 * 32
 
 
 class Act:
