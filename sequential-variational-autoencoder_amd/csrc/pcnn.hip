@@ -337,12 +337,12 @@ __global__ __launch_bounds__(256) void pc_conv2_kernel(PcGeom g, const float* __
 // output rows in chunks of 32, staged through LDS transposed (row-contiguous per channel, so
 // each MFMA fragment is one 16-B LDS read).  Partial slabs [split][tap][ci][co].
 // ---------------------------------------------------------------------------------------------
-#define PW_RP 40  // LDS row pitch (bf16): 32 rows + 8 pad
+#define PW_RP 72  // LDS row pitch (bf16): 64 rows + 8 pad
 __global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const float* __restrict__ X,
                                                        const float* __restrict__ D, int ldd, long long rows,
                                                        long long rows_per_split, float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) __bf16 Xs[64 * PW_RP];
-  __shared__ __attribute__((aligned(16))) __bf16 Ds[64 * PW_RP];
+  __shared__ __attribute__((aligned(16))) __bf16 Xs[2][64 * PW_RP];
+  __shared__ __attribute__((aligned(16))) __bf16 Ds[2][64 * PW_RP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int nci = (g.cin + 63) / 64;
   const int ci0 = (blockIdx.x % nci) * 64, co0 = (blockIdx.x / nci) * 64;
@@ -356,40 +356,64 @@ __global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const float* __
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  // staging role: row lr = tid >> 3 (0..31), channel quads q = tid & 7 and q + 8
+  // staging role: rows lr and lr + 32 (lr = tid >> 3), channel quads q0 and q0 + 8; chunks of 64
+  // rows, the next chunk loaded into registers while the current one's MFMAs run
   const int lr = tid >> 3, q0 = tid & 7;
-  for (long long rc = r0; rc < r1; rc += 32) {
-    const long long row = rc + lr;
-    const float* xp = nullptr;
-    const float* dp = nullptr;
-    if (row < r1) {
-      const int img = (int)(row / per_img);
-      const int rr = (int)(row - (long long)img * per_img);
-      const int oy = rr / g.wo, ox = rr - (rr / g.wo) * g.wo;
-      int iy, ix;
-      if (pc_src(g, oy, ox, ky, kx, iy, ix)) xp = X + ((long long)(img * g.hi + iy) * g.wi + ix) * g.ldx;
-      dp = D + row * ldd;
-    }
+  f32x4 xv[2][2], dv[2][2];
+  auto load = [&](long long rc) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int c = (q0 + 8 * j) * 4;
-      f32x4 xv = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
-      if (xp && ci0 + c < g.cin) xv = *(const f32x4*)(xp + ci0 + c);
-      if (dp && co0 + c < g.cout) dv = *(const f32x4*)(dp + co0 + c);
+    for (int u = 0; u < 2; ++u) {
+      const long long row = rc + lr + 32 * u;
+      const float* xp = nullptr;
+      const float* dp = nullptr;
+      if (row < r1) {
+        const int img = (int)(row / per_img);
+        const int rr = (int)(row - (long long)img * per_img);
+        const int oy = rr / g.wo, ox = rr - (rr / g.wo) * g.wo;
+        int iy, ix;
+        if (pc_src(g, oy, ox, ky, kx, iy, ix)) xp = X + ((long long)(img * g.hi + iy) * g.wi + ix) * g.ldx;
+        dp = D + row * ldd;
+      }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        Xs[(c + e) * PW_RP + lr] = (__bf16)xv[e];
-        Ds[(c + e) * PW_RP + lr] = (__bf16)dv[e];
+      for (int j = 0; j < 2; ++j) {
+        const int c = (q0 + 8 * j) * 4;
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        xv[u][j] = (xp && ci0 + c < g.cin) ? *(const f32x4*)(xp + ci0 + c) : z;
+        dv[u][j] = (dp && co0 + c < g.cout) ? *(const f32x4*)(dp + co0 + c) : z;
       }
     }
-    __syncthreads();
+  };
+  auto store = [&](int buf) {
 #pragma unroll
-    for (int kq = 0; kq < 2; ++kq) {
-      const pc_bf16x8 af = *(const pc_bf16x8*)&Xs[(wm * 32 + l32) * PW_RP + kq * 16 + 8 * h];
-      const pc_bf16x8 bf = *(const pc_bf16x8*)&Ds[(wn * 32 + l32) * PW_RP + kq * 16 + 8 * h];
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = (q0 + 8 * j) * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          Xs[buf][(c + e) * PW_RP + lr + 32 * u] = (__bf16)xv[u][j][e];
+          Ds[buf][(c + e) * PW_RP + lr + 32 * u] = (__bf16)dv[u][j][e];
+        }
+      }
+  };
+  if (r0 < r1) {
+    load(r0);
+    store(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (long long rc = r0; rc < r1; rc += 64) {
+    const bool more = rc + 64 < r1;
+    if (more) load(rc + 64);
+#pragma unroll
+    for (int kq = 0; kq < 4; ++kq) {
+      const pc_bf16x8 af = *(const pc_bf16x8*)&Xs[buf][(wm * 32 + l32) * PW_RP + kq * 16 + 8 * h];
+      const pc_bf16x8 bf = *(const pc_bf16x8*)&Ds[buf][(wn * 32 + l32) * PW_RP + kq * 16 + 8 * h];
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc, 0, 0, 0);
     }
+    if (more) store(buf ^ 1);
     __syncthreads();
+    buf ^= 1;
   }
   float* out = part + ((long long)split * g.kh * g.kw + tap) * g.cin * g.cout;
   const int co = co0 + wn * 32 + l32;
@@ -436,13 +460,20 @@ __global__ __launch_bounds__(256) void colsum_part_kernel_pc(const float* __rest
     part[(long long)blockIdx.y * c + col] =
         red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
 }
-__global__ void colsum_fin_kernel_pc(const float* __restrict__ part, int nsplit, int c, float* __restrict__ out,
-                                     int accumulate) {
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= c) return;
+// stage 2: 64 columns per block, 4 split-lanes, fixed-order combine
+__global__ __launch_bounds__(256) void colsum_fin_kernel_pc(const float* __restrict__ part, int nsplit, int c,
+                                                            float* __restrict__ out, int accumulate) {
+  __shared__ float red[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6;
   float s = 0.f;
-  for (int k = 0; k < nsplit; ++k) s += part[(long long)k * c + col];
-  out[col] = accumulate ? out[col] + s : s;
+  if (col < c)
+    for (int k = q; k < nsplit; k += 4) s += part[(long long)k * c + col];
+  red[q][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (q == 0 && col < c) {
+    const float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    out[col] = accumulate ? out[col] + v : v;
+  }
 }
 
 __global__ void mask_edge_kernel(float* x, long long n_rows, int per_img, int wo, int c, int ldx, int mask_edge) {
@@ -893,7 +924,7 @@ int svae_pcnn_conv_wgrad(const float* x, int n, int hi, int wi, int cin, int ldx
   if (ns > scratch_elems / wsz) ns = scratch_elems / wsz;
   if (ns < 1) return bad("pcnn_wgrad: scratch too small");
   long long rps = (rows + ns - 1) / ns;
-  rps = (rps + 31) / 32 * 32;
+  rps = (rps + 63) / 64 * 64;
   ns = (rows + rps - 1) / rps;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(pc_wgrad_kernel, dim3(tiles, taps, (unsigned)ns), dim3(256), 0, st, g, x, dy, ldd, rows, rps,
@@ -913,7 +944,7 @@ int svae_pcnn_colsum(const float* x, int64_t rows, int c, int ldx, int ho, int w
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(colsum_part_kernel_pc, dim3((c + 63) / 64, (unsigned)ns), dim3(256), 0, st, x, (long long)rows, c,
                      ldx, ho * wo, wo, mask_edge, rps, scratch);
-  hipLaunchKernelGGL(colsum_fin_kernel_pc, dim3((c + 255) / 256), dim3(256), 0, st, scratch, (int)ns, c, out,
+  hipLaunchKernelGGL(colsum_fin_kernel_pc, dim3((c + 63) / 64), dim3(256), 0, st, scratch, (int)ns, c, out,
                      accumulate);
   return hipchk();
 }
