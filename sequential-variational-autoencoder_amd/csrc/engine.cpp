@@ -2447,6 +2447,7 @@ int svae_copy_out(svae_ctx* c, int which, int step, float* dst, int64_t n, void*
   if (which < 100 && (step < 0 || step >= g.T)) return fail(c, SVAE_EBADARG, "step out of range");
   const float* src = nullptr;
   long long cnt = 0;
+  bool src_bf16 = false;  // bf16-stored activation (abf): widened to fp32 on the way out
   const long long ml = (long long)g.B * g.Dz;
   switch (which) {
     case SVAE_BUF_XHAT: src = c->sb[step].xhat; cnt = (long long)g.B * g.H * g.W * g.C; break;
@@ -2476,19 +2477,20 @@ int svae_copy_out(svae_ctx* c, int which, int step, float* dst, int64_t n, void*
     case 110: src = c->dbg_last; cnt = n; break;
     case 111: c->dbg_stop_lvl2 = step; return 0;
     case 113: src = c->inf_pre_a[step]; cnt = n; break;   // debug: inference level `step`, all T groups
-    case 114:  // (bf16-stored under abf: not a float buffer)
-      if (c->abf) return fail(c, SVAE_EBADARG, "activation stored as bf16 (SVAE_ACT_F32=1 keeps it fp32)");
-      src = c->inf_act_a[step]; cnt = n; break;
+    case 114: src = c->inf_act_a[step]; cnt = n; src_bf16 = c->abf; break;
     case 115: src = c->inf_pre_b[step]; cnt = n; break;
     case 116: src = c->inf_act_b[step]; cnt = n; break;
-    case 106:
-      if (c->abf) return fail(c, SVAE_EBADARG, "activation stored as bf16 (SVAE_ACT_F32=1 keeps it fp32)");
-      src = c->sb[c->dbg_stop_step].s1_act[step]; cnt = n; break;
+    case 106: src = c->sb[c->dbg_stop_step].s1_act[step]; cnt = n; src_bf16 = c->abf; break;
     case 107: src = c->sb[c->dbg_stop_step].s1_bn[step].mean; cnt = n; break;
     case 108: src = c->sb[c->dbg_stop_step].s1_bn[step].invstd; cnt = n; break;
     default: return fail(c, SVAE_EBADARG, "unknown buffer");
   }
   if (n < cnt) return fail(c, SVAE_EBADARG, "destination too small");
+  if (src_bf16) {
+    bf16_to_f32(src, dst, cnt, (hipStream_t)stream);
+    HIPCHK(c, hipGetLastError());
+    return 0;
+  }
   HIPCHK(c, hipMemcpyAsync(dst, src, cnt * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return 0;
 }

@@ -222,6 +222,7 @@ void share_gather(const float* Gv, float* G, const long long* tab, const long lo
 // ---- misc ----
 // dst[0..n) = vals[0..n) (n <= 64), values passed by value in the kernel arguments
 void set_small(float* dst, const float* vals, int n, hipStream_t s);
+void bf16_to_f32(const void* src, float* dst, long long n, hipStream_t s);  // debug copies of bf16 activations
 void fill_f32(float* p, long long n, float v, hipStream_t s);
 void philox_normal(float* out, long long n, unsigned long long seed, unsigned long long offset, hipStream_t s);
 // column sums of X [rows][C<=4] -> out0[0..n0), out1[0..C-n0)   (part: scratch >= 1024 floats)

@@ -857,6 +857,14 @@ void adam_step(float* w, const float* g, float* m, float* v, void* wn, long long
                      n, lr_t, b1, b2, eps, clipv);
 }
 
+__global__ void bf16_to_f32_kernel(const __bf16* src, float* dst, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    dst[i] = (float)src[i];
+}
+void bf16_to_f32(const void* src, float* dst, long long n, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(bf16_to_f32_kernel, dim3(ew_blocks(n)), dim3(256), 0, s, (const __bf16*)src, dst, n);
+}
+
 __global__ void fill_kernel(float* p, long long n, float v) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
     p[i] = v;
