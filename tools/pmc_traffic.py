@@ -40,8 +40,24 @@ WIDE16 = ("wgrad_halo_kernel", "igemm_halo_kernel", "igemm_bf16_kernel", "wgrad_
           "bn_bwd_apply_kernel", "adam_kernel", "shadow_n_kernel", "shadow_t_kernel", "loss_reduce_kernel")
 
 
+# kernels whose operand width follows their storage template parameter (opload.h): OPB (last
+# template argument) 0 = both operands fp32 (16 B/lane loads), else a bf16 operand loads 8 B/lane
+OPB_LAST = ("wgrad_halo2_kernel", "wgrad_halo_kernel")
+# 16 B/lane whatever the storage (8 fp32 = two 16-B loads, 8 bf16 = one)
+WIDE16_ANY = ("igemm_halo_kw_kernel", "(anonymous namespace)::igemm_halo_kw_kernel")
+
+
 def fetch_rule(kernel):
-    k = kernel.split("(")[0]
+    k = kernel.split("(")[0] if not kernel.startswith("(anonymous") else kernel
+    for w in WIDE16_ANY:
+        if k.startswith(w):
+            return 2.0, "FETCH_SIZE x2 (16 B/lane loads: gfx950 half-count)"
+    for w in OPB_LAST:
+        if k.startswith(w + "<"):
+            opb = k.rstrip(">").split(",")[-1].strip()
+            if opb == "0":
+                return 2.0, "FETCH_SIZE x2 (fp32 operands, 16 B/lane loads: gfx950 half-count)"
+            return 1.0, "FETCH_SIZE x1 (a bf16 operand loads 8 B/lane: uncalibrated, as counted)"
     for w in WIDE16:
         if k.startswith(w) or (w.endswith("<") and k.startswith(w[:-1])):
             return 2.0, "FETCH_SIZE x2 (16 B/lane loads: gfx950 half-count)"
