@@ -64,11 +64,11 @@ struct WH2Args {
   int g_bf16, d_bf16;            // G / D stored as bf16 (opload.h)
 };
 
-template <int WO, int CP, int KYR, int WN, int WK, bool DB, int OPB>
+template <int WO, int CP, int KYR, int WN, int WK, bool DB, int OPB, int NSW>
 __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args a) {
   using GE = Geo2<WO, CP>;
   constexpr int NT = 64 * KYR * WN * WK;
-  constexpr int DN = 32 * WN;                     // D columns per block
+  constexpr int DN = 32 * WN * NSW;               // D columns per block (NSW 32-column subtiles per wave)
   constexpr int GI = (GE::NPIX * 8 + NT - 1) / NT;  // window items (4 channels) per thread
   constexpr int DI = (CP * DN / 4 + NT - 1) / NT;   // D items per thread
   constexpr int GWB = GE::NPIX * 32;                // bf16 elements of one window buffer
@@ -119,15 +119,21 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
   const int ch = 16 * (grp & 1) + 4 * p4;                  // this lane's G channel quad
   const int wlane = (lk / WO) * GE::PC + (lk % WO);        // its window offset (additive, no carry)
   const int ga = ((wlane + ky * GE::PC) * 32 + ch) * 2;    // + (wpos(k0) + kx) * 64
-  const int slot = wn * 8 + 4 * (grp & 1) + p4;
-  const int sw = DN == 64 ? (slot ^ (((lk >> 1) & 1) << 3)) : slot;
-  const int da = (GWB + lk * DN + sw * 4) * 2;             // + k0 * DN * 2
+  int da[NSW];                                              // + k0 * DN * 2
+#pragma unroll
+  for (int sn = 0; sn < NSW; ++sn) {
+    const int slot = (wn * NSW + sn) * 8 + 4 * (grp & 1) + p4;
+    const int sw = DN == 64 ? (slot ^ (((lk >> 1) & 1) << 3)) : slot;
+    da[sn] = (GWB + lk * DN + sw * 4) * 2;
+  }
 
-  f32x16 acc[4];
+  f32x16 acc[4][NSW];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+    for (int sn = 0; sn < NSW; ++sn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][sn][r] = 0.f;
 
   f32x4 gv[GI], dv[DI];
   auto load_chunk = [&](int c) {
@@ -178,18 +184,25 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
     const char* sb = (const char*)st;
     // K steps kk = j*WK + wk: the wave set's offset wpos(16*wk) lives in gw / dw (additive for
     // every instantiated geometry), the rest is a compile-time constant of the unrolled j
-    const int gw = ga + GE::wpos(16 * wk) * 64, dw = da + 16 * wk * DN * 2;
+    const int gw = ga + GE::wpos(16 * wk) * 64;
 #pragma unroll
     for (int j = 0; j < GE::KSTEPS / WK; ++j) {
       const int k0 = j * WK * 16;
-      const bf16x8 bfr = join(tr16((const __bf16*)(sb + dw + (k0 * DN) * 2)),
-                              tr16((const __bf16*)(sb + dw + ((k0 + 4) * DN) * 2)));
+      bf16x8 bfr[NSW];
+#pragma unroll
+      for (int sn = 0; sn < NSW; ++sn) {
+        const int dw = da[sn] + 16 * wk * DN * 2;
+        bfr[sn] = join(tr16((const __bf16*)(sb + dw + (k0 * DN) * 2)),
+                       tr16((const __bf16*)(sb + dw + ((k0 + 4) * DN) * 2)));
+      }
       const int w0 = GE::wpos(k0), w1 = GE::wpos(k0 + 4);
 #pragma unroll
       for (int kx = 0; kx < 4; ++kx) {
         const bf16x8 af = join(tr16((const __bf16*)(sb + gw + (w0 + kx) * 64)),
                                tr16((const __bf16*)(sb + gw + (w1 + kx) * 64)));
-        acc[kx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[kx], 0, 0, 0);
+#pragma unroll
+        for (int sn = 0; sn < NSW; ++sn)  // every transposed A fragment feeds NSW MFMAs
+          acc[kx][sn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[sn], acc[kx][sn], 0, 0, 0);
       }
     }
     if constexpr (!DB) __syncthreads();  // single stage: the next store waits for every reader
@@ -204,7 +217,7 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
 #pragma unroll
       for (int kx = 0; kx < 4; ++kx)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) red[((((wk - 1) * KYR * WN + wl) * 4 + kx) * 16 + r) * 64 + lane] = acc[kx][r];
+        for (int r = 0; r < 16; ++r) red[((((wk - 1) * KYR * WN + wl) * 4 + kx) * 16 + r) * 64 + lane] = acc[kx][0][r];
     }
     __syncthreads();
     if (wk > 0) return;
@@ -213,19 +226,22 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
 #pragma unroll
       for (int kx = 0; kx < 4; ++kx)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[kx][r] += red[((((j - 1) * KYR * WN + wl) * 4 + kx) * 16 + r) * 64 + lane];
+        for (int r = 0; r < 16; ++r) acc[kx][0][r] += red[((((j - 1) * KYR * WN + wl) * 4 + kx) * 16 + r) * 64 + lane];
   }
 
   // ---- partial dW[tap][m][n] of this split (the gradient itself when nsplit == 1) ----
   float* out = a.part + group * a.p_gs + (long long)split * 16 * a.M * a.N;
-  const int n = n0 + wn * 32 + l32;
 #pragma unroll
-  for (int kx = 0; kx < 4; ++kx) {
-    const int tap = ky * 4 + kx;
+  for (int sn = 0; sn < NSW; ++sn) {
+    const int n = n0 + (wn * NSW + sn) * 32 + l32;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-      out[((long long)tap * a.M + m) * a.N + n] = acc[kx][r];
+    for (int kx = 0; kx < 4; ++kx) {
+      const int tap = ky * 4 + kx;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        out[((long long)tap * a.M + m) * a.N + n] = acc[kx][sn][r];
+      }
     }
   }
 }
@@ -235,34 +251,35 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
 // ---------------------------------------------------------------------------
 namespace {
 
-template <int WO, int CP, int KYR, int WN, int WK, bool DB>
+template <int WO, int CP, int KYR, int WN, int WK, bool DB, int NSW>
 size_t wh2_lds() {
   using GE = Geo2<WO, CP>;
-  const size_t stage = ((size_t)GE::NPIX * 32 + (size_t)CP * 32 * WN) * 2;
+  const size_t stage = ((size_t)GE::NPIX * 32 + (size_t)CP * 32 * WN * NSW) * 2;
   const size_t red = WK > 1 ? (size_t)(WK - 1) * KYR * WN * 4 * 16 * 64 * 4 : 0;
   return std::max((DB ? 2 : 1) * stage, red);
 }
 
-template <int WO, int CP, int KYR, int WN, int WK, bool DB, int OPB>
+template <int WO, int CP, int KYR, int WN, int WK, bool DB, int OPB, int NSW>
 void wh2_launch_op(const WH2Args& a, int groups, hipStream_t s) {
-  const size_t lds = wh2_lds<WO, CP, KYR, WN, WK, DB>();
+  const size_t lds = wh2_lds<WO, CP, KYR, WN, WK, DB, NSW>();
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)wgrad_halo2_kernel<WO, CP, KYR, WN, WK, DB, OPB>,
+    hipFuncSetAttribute((const void*)wgrad_halo2_kernel<WO, CP, KYR, WN, WK, DB, OPB, NSW>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  dim3 grid(a.M / 32, a.N / (32 * WN), (4 / KYR) * a.nsplit * groups);
-  hipLaunchKernelGGL((wgrad_halo2_kernel<WO, CP, KYR, WN, WK, DB, OPB>), grid, dim3(64 * KYR * WN * WK), lds, s, a);
+  dim3 grid(a.M / 32, a.N / (32 * WN * NSW), (4 / KYR) * a.nsplit * groups);
+  hipLaunchKernelGGL((wgrad_halo2_kernel<WO, CP, KYR, WN, WK, DB, OPB, NSW>), grid, dim3(64 * KYR * WN * WK), lds, s,
+                     a);
 }
 // operand storage (G fp32/bf16 x D fp32/bf16) as a compile-time parameter: no branches in the loads
-template <int WO, int CP, int KYR, int WN, int WK, bool DB>
+template <int WO, int CP, int KYR, int WN, int WK, bool DB, int NSW = 1>
 void wh2_launch(const WH2Args& a, int groups, hipStream_t s) {
   switch ((a.g_bf16 ? 1 : 0) | (a.d_bf16 ? 2 : 0)) {
-    case 0: wh2_launch_op<WO, CP, KYR, WN, WK, DB, 0>(a, groups, s); break;
-    case 1: wh2_launch_op<WO, CP, KYR, WN, WK, DB, 1>(a, groups, s); break;
-    case 2: wh2_launch_op<WO, CP, KYR, WN, WK, DB, 2>(a, groups, s); break;
-    default: wh2_launch_op<WO, CP, KYR, WN, WK, DB, 3>(a, groups, s); break;
+    case 0: wh2_launch_op<WO, CP, KYR, WN, WK, DB, 0, NSW>(a, groups, s); break;
+    case 1: wh2_launch_op<WO, CP, KYR, WN, WK, DB, 1, NSW>(a, groups, s); break;
+    case 2: wh2_launch_op<WO, CP, KYR, WN, WK, DB, 2, NSW>(a, groups, s); break;
+    default: wh2_launch_op<WO, CP, KYR, WN, WK, DB, 3, NSW>(a, groups, s); break;
   }
 }
 
@@ -305,6 +322,9 @@ int wgrad_halo2(const WgArgs& w, int groups, float* slab, long long slab_cap, fl
   const int cp = wh2_cp(WO);
   static const int target = env_int("SVAE_WH2_TARGET", 128);
   static const int minch = env_int("SVAE_WH2_MINCH", 4);
+  // SVAE_WH2_NSW=2: a 64-column block as 4 waves of two 32-column subtiles (each transposed A
+  // fragment feeds two MFMAs) instead of 8 waves of one
+  static const int nsw = env_int("SVAE_WH2_NSW", 1);
   const int wn = (w.N % 64 == 0) ? 2 : 1;
   const int kyr = 4;
   WH2Args a;
@@ -327,8 +347,9 @@ int wgrad_halo2(const WgArgs& w, int groups, float* slab, long long slab_cap, fl
     a.p_gs = (long long)a.nsplit * per;
   }
 #define WH2(WOV, CPV, KY, WNV, WKV) wh2_launch<WOV, CPV, KY, WNV, WKV, false>(a, groups, s)
-#define WH2_WO(WOV, CPV)                                   \
-  if (wn == 2) { WH2(WOV, CPV, 4, 2, 1); }                 \
+#define WH2_WO(WOV, CPV)                                                            \
+  if (wn == 2 && nsw == 2) { wh2_launch<WOV, CPV, 4, 1, 1, false, 2>(a, groups, s); } \
+  else if (wn == 2) { WH2(WOV, CPV, 4, 2, 1); }                                     \
   else { WH2(WOV, CPV, 4, 1, 2); }
   if (WO == 32) { WH2_WO(32, 128) }
   else if (WO == 16) { WH2_WO(16, 256) }

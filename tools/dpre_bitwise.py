@@ -26,8 +26,9 @@ np.save(%r, np.concatenate([net.grads.cpu().numpy().ravel(), st]))
 
 def run(preset, batch, f32, out, var="SVAE_DPRE_F32"):
     env = dict(os.environ)
-    if f32:
-        env[var] = "1"
+    if f32:  # "NAME" -> NAME=1, or an explicit "NAME=VALUE"
+        k, _, v = var.partition("=")
+        env[k] = v or "1"
     subprocess.run([sys.executable, "-c", CHILD % (ROOT, preset, batch, out)], env=env, check=True)
     return np.load(out)
 
