@@ -208,9 +208,10 @@ void splitfc_bwd(const float* z, int ldz, int zoff, int B, int K, const float* W
 #define SK_CHUNK 4096
 
 template <int DM>
-__global__ __launch_bounds__(256) void skinny_kernel(const float* X, int ldx, long long x_gs, int B, int K,
-                                                     const float* W, long long sk, long long so, long long w_gs,
-                                                     int D, float* part, long long p_gs, int pcols, int coff) {
+__global__ __launch_bounds__(256) void skinny_kernel(const float* __restrict__ X, int ldx, long long x_gs, int B,
+                                                     int K, const float* __restrict__ W, long long sk, long long so,
+                                                     long long w_gs, int D, float* __restrict__ part, long long p_gs,
+                                                     int pcols, int coff) {
   __shared__ float red[4][SK_ROWS][DM];
   const int group = blockIdx.z;
   const int split = blockIdx.y;
@@ -365,11 +366,13 @@ void latent_bwd(const float* mu, const float* sig, const float* eps, const float
 
 // heads backward for one level: dX (+)= dhead_l @ W^T ; dW = X^T dhead_l ; db = sum_n dhead_l
 template <int DM>
-__global__ __launch_bounds__(256) void heads_bwd_kernel(const float* X, long long x_gs, float* dX, long long dx_gs,
-                                                        int B, int K, const float* Wm, const float* Ws,
-                                                        long long w_gs, int D, const float* dhead, long long dh_gs,
-                                                        int dcols, int coff, float* dWm, float* dWs, float* dbm,
-                                                        float* dbs, int accumulate) {
+__global__ __launch_bounds__(256) void heads_bwd_kernel(const float* __restrict__ X, long long x_gs,
+                                                        float* __restrict__ dX, long long dx_gs, int B, int K,
+                                                        const float* __restrict__ Wm, const float* __restrict__ Ws,
+                                                        long long w_gs, int D, const float* __restrict__ dhead,
+                                                        long long dh_gs, int dcols, int coff, float* __restrict__ dWm,
+                                                        float* __restrict__ dWs, float* __restrict__ dbm,
+                                                        float* __restrict__ dbs, int accumulate) {
   extern __shared__ float dh[];  // [B][2*D]
   const int group = blockIdx.y;
   X += group * x_gs;
@@ -397,20 +400,33 @@ __global__ __launch_bounds__(256) void heads_bwd_kernel(const float* X, long lon
     ws[o] = o < D ? Ws[(long long)k * D + o] : 0.f;
     gm[o] = gs[o] = 0.f;
   }
-  for (int n = 0; n < B; ++n) {
-    const float x = X[(long long)n * K + k];
-    float dx = 0.f;
+  // rows in groups of 8: the 8 independent loads (and accumulate reads) issue together
+  // (same per-thread operation order as one row at a time: bitwise the same result)
+  constexpr int RB = 8;
+  for (int n0 = 0; n0 < B; n0 += RB) {
+    float xs[RB], old[RB];
 #pragma unroll
-    for (int o = 0; o < DM; ++o) {
-      if (o < D) {
-        const float a = dh[n * 2 * D + o], b = dh[n * 2 * D + D + o];
-        dx = fmaf(a, wm[o], fmaf(b, ws[o], dx));
-        gm[o] = fmaf(x, a, gm[o]);
-        gs[o] = fmaf(x, b, gs[o]);
-      }
+    for (int j = 0; j < RB; ++j) {
+      const int n = n0 + j;
+      xs[j] = n < B ? X[(long long)n * K + k] : 0.f;
+      old[j] = (accumulate && n < B) ? dX[(long long)n * K + k] : 0.f;
     }
-    float* d = dX + (long long)n * K + k;
-    *d = accumulate ? *d + dx : dx;
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+      const int n = n0 + j;
+      if (n >= B) break;
+      float dx = 0.f;
+#pragma unroll
+      for (int o = 0; o < DM; ++o) {
+        if (o < D) {
+          const float a = dh[n * 2 * D + o], b = dh[n * 2 * D + D + o];
+          dx = fmaf(a, wm[o], fmaf(b, ws[o], dx));
+          gm[o] = fmaf(xs[j], a, gm[o]);
+          gs[o] = fmaf(xs[j], b, gs[o]);
+        }
+      }
+      dX[(long long)n * K + k] = accumulate ? old[j] + dx : dx;
+    }
   }
 #pragma unroll
   for (int o = 0; o < DM; ++o)
@@ -698,8 +714,9 @@ void gconv_smalln(const float* A, int lda, int K, const float* W0, int n0, const
 #define OUT_TPB 256
 int output_blocks_per_img(int HW) { return (HW + OUT_TPB - 1) / OUT_TPB; }
 
-__global__ void output_fwd_kernel(const float* a, int HW, int C, const float* xprev, const float* target, float lo,
-                                  float hi, float minh, float maxh, float* xhat, float* rec_part, int nblk) {
+__global__ void output_fwd_kernel(const float* __restrict__ a, int HW, int C, const float* __restrict__ xprev,
+                                  const float* __restrict__ target, float lo, float hi, float minh, float maxh,
+                                  float* __restrict__ xhat, float* __restrict__ rec_part, int nblk) {
   __shared__ float red[OUT_TPB / 64];
   const int n = blockIdx.y;
   const int pix = blockIdx.x * OUT_TPB + threadIdx.x;
@@ -734,9 +751,10 @@ void output_fwd(const float* a, int B, int HW, int C, const float* xprev, const 
 }
 
 // g = dxhat_in + rec_coef*2*(xhat - target); da (pre-sigmoid), dxprev = (1-r)*g
-__global__ void output_bwd_kernel(const float* a, long long P, int C, const float* xprev, const float* xhat,
-                                  const float* target, float lo, float hi, float minh, float maxh, float rec_coef,
-                                  const float* dxhat_in, float* da, float* dxprev) {
+__global__ void output_bwd_kernel(const float* __restrict__ a, long long P, int C, const float* __restrict__ xprev,
+                                  const float* __restrict__ xhat, const float* __restrict__ target, float lo, float hi,
+                                  float minh, float maxh, float rec_coef, const float* __restrict__ dxhat_in,
+                                  float* __restrict__ da, float* __restrict__ dxprev) {
   const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
   const float* ap = a + p * (C + 1);
