@@ -208,16 +208,20 @@ void splitfc_bwd(const float* z, int ldz, int zoff, int B, int K, const float* W
 #define SK_CHUNK 4096
 
 template <int DM>
+// D outputs from W, and (W2 != nullptr) D more from W2 into columns coff2.. of part: the mean and
+// stddev heads read the shared input X once (per-output arithmetic unchanged)
 __global__ __launch_bounds__(256) void skinny_kernel(const float* __restrict__ X, int ldx, long long x_gs, int B,
                                                      int K, const float* __restrict__ W, long long sk, long long so,
                                                      long long w_gs, int D, float* __restrict__ part, long long p_gs,
-                                                     int pcols, int coff) {
+                                                     int pcols, int coff, const float* __restrict__ W2, int coff2) {
   __shared__ float red[4][SK_ROWS][DM];
   const int group = blockIdx.z;
   const int split = blockIdx.y;
   const int r0 = blockIdx.x * SK_ROWS;
   X += group * x_gs;
   W += group * w_gs;
+  if (W2) W2 += group * w_gs;
+  const int DT = W2 ? 2 * D : D;  // outputs of this launch
   float acc[SK_ROWS][DM];
 #pragma unroll
   for (int r = 0; r < SK_ROWS; ++r)
@@ -227,7 +231,7 @@ __global__ __launch_bounds__(256) void skinny_kernel(const float* __restrict__ X
   for (int k = k0 + threadIdx.x; k < k1; k += 256) {
     float w[DM];
 #pragma unroll
-    for (int o = 0; o < DM; ++o) w[o] = o < D ? W[k * sk + o * so] : 0.f;
+    for (int o = 0; o < DM; ++o) w[o] = o < D ? W[k * sk + o * so] : (o < DT ? W2[k * sk + (o - D) * so] : 0.f);
 #pragma unroll
     for (int r = 0; r < SK_ROWS; ++r) {
       if (r0 + r < B) {
@@ -242,7 +246,7 @@ __global__ __launch_bounds__(256) void skinny_kernel(const float* __restrict__ X
   for (int r = 0; r < SK_ROWS; ++r)
 #pragma unroll
     for (int o = 0; o < DM; ++o) {
-      if (o < D) {
+      if (o < DT) {
         float v = wave_sum(acc[r][o]);
         if (lane == 0) red[wave][r][o] = v;
       }
@@ -250,31 +254,36 @@ __global__ __launch_bounds__(256) void skinny_kernel(const float* __restrict__ X
   __syncthreads();
   if (threadIdx.x < SK_ROWS * DM) {
     const int r = threadIdx.x / DM, o = threadIdx.x % DM;
-    if (o < D && r0 + r < B) {
+    if (o < DT && r0 + r < B) {
       float v = red[0][r][o] + red[1][r][o] + red[2][r][o] + red[3][r][o];
-      part[group * p_gs + ((long long)split * B + r0 + r) * pcols + coff + o] = v;
+      part[group * p_gs + ((long long)split * B + r0 + r) * pcols + (o < D ? coff + o : coff2 + o - D)] = v;
     }
   }
 }
 
 static void skinny(const float* X, int ldx, long long x_gs, int B, int K, const float* W, long long sk, long long so,
                    long long w_gs, int D, float* part, long long p_gs, int pcols, int coff, int groups,
-                   hipStream_t s) {
+                   hipStream_t s, const float* W2 = nullptr, int coff2 = 0) {
   dim3 grid((B + SK_ROWS - 1) / SK_ROWS, (K + SK_CHUNK - 1) / SK_CHUNK, groups);
-  if (D <= 4) hipLaunchKernelGGL(skinny_kernel<4>, grid, dim3(256), 0, s, X, ldx, x_gs, B, K, W, sk, so, w_gs, D,
-                                 part, p_gs, pcols, coff);
-  else if (D <= 8) hipLaunchKernelGGL(skinny_kernel<8>, grid, dim3(256), 0, s, X, ldx, x_gs, B, K, W, sk, so, w_gs, D,
-                                      part, p_gs, pcols, coff);
-  else hipLaunchKernelGGL(skinny_kernel<32>, grid, dim3(256), 0, s, X, ldx, x_gs, B, K, W, sk, so, w_gs, D, part,
-                          p_gs, pcols, coff);
+  const int DT = W2 ? 2 * D : D;
+  if (DT <= 4) hipLaunchKernelGGL(skinny_kernel<4>, grid, dim3(256), 0, s, X, ldx, x_gs, B, K, W, sk, so, w_gs, D,
+                                  part, p_gs, pcols, coff, W2, coff2);
+  else if (DT <= 8) hipLaunchKernelGGL(skinny_kernel<8>, grid, dim3(256), 0, s, X, ldx, x_gs, B, K, W, sk, so, w_gs,
+                                       D, part, p_gs, pcols, coff, W2, coff2);
+  else if (DT <= 32) hipLaunchKernelGGL(skinny_kernel<32>, grid, dim3(256), 0, s, X, ldx, x_gs, B, K, W, sk, so, w_gs,
+                                        D, part, p_gs, pcols, coff, W2, coff2);
+  else {  // wide heads: the two passes
+    skinny(X, ldx, x_gs, B, K, W, sk, so, w_gs, D, part, p_gs, pcols, coff, groups, s);
+    skinny(X, ldx, x_gs, B, K, W2, sk, so, w_gs, D, part, p_gs, pcols, coff2, groups, s);
+  }
 }
 
 int heads_splits(int K) { return (K + SK_CHUNK - 1) / SK_CHUNK; }
 
 void heads_fwd(const float* X, long long x_gs, int B, int K, const float* Wm, const float* Ws, long long w_gs, int D,
                float* part, long long part_gs, int pcols, int coff, int groups, hipStream_t s) {
-  skinny(X, K, x_gs, B, K, Wm, D, 1, w_gs, D, part, part_gs, pcols, coff, groups, s);
-  skinny(X, K, x_gs, B, K, Ws, D, 1, w_gs, D, part, part_gs, pcols, pcols / 2 + coff, groups, s);
+  // mean and stddev heads in one pass over X (the shared recognition features)
+  skinny(X, K, x_gs, B, K, Wm, D, 1, w_gs, D, part, part_gs, pcols, coff, groups, s, Ws, pcols / 2 + coff);
 }
 
 // dz[n][zoff+d] += sum_split part   where part = skinny(dpre [B][J], W^T)
