@@ -364,7 +364,27 @@ struct HaloArgs {
   int PR, PC;        // window dims per image
   int sy;            // row-space -> input stride (CONV stride, else 1)
   int npix;          // nimg * PR * PC
+  // launch-constant divisors (multiply-shift): no integer divisions in the index decode
+  FastDiv d_win, d_pc, d_img, d_wr, d_rimg, d_q, d_qw;  // PR*PC, PC, Hr*Wr, Wr, R*Wr, (Ho/2)*(Wo/2), Wo/2
 };
+__device__ __forceinline__ long long out_row_h(const HaloArgs& h, const ConvGeom& g, int cls, int m) {
+  if (g.mode == GM_CONVT && g.stride == 2) {
+    const int n = fdiv(m, h.d_q);
+    const int r = m - n * h.d_q.d;
+    const int qy = fdiv(r, h.d_qw), qx = r - qy * h.d_qw.d;
+    return ((long long)n * g.Ho + 2 * qy + (cls >> 1)) * g.Wo + 2 * qx + (cls & 1);
+  }
+  return m;
+}
+static void halo_divisors(HaloArgs& h, const ConvGeom& g) {
+  h.d_win = make_fastdiv(h.PR * h.PC);
+  h.d_pc = make_fastdiv(h.PC);
+  h.d_img = make_fastdiv(h.Hr * h.Wr);
+  h.d_wr = make_fastdiv(h.Wr);
+  h.d_rimg = make_fastdiv(h.R * h.Wr);
+  h.d_q = make_fastdiv((g.Ho >> 1) * (g.Wo >> 1));
+  h.d_qw = make_fastdiv(g.Wo >> 1);
+}
 
 template <int BM, int BN, int WM, int WN, bool S2T, bool ABF>
 __global__ __launch_bounds__(256, 2) void igemm_halo_kernel(HaloArgs h) {
@@ -394,8 +414,8 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kernel(HaloArgs h) {
 
   // ---- block window origin and per-tap geometry (uniform) ----
   const int per_img = h.Hr * h.Wr;
-  const int img0 = m0 / per_img;
-  const int ry0 = (m0 - img0 * per_img) / h.Wr;
+  const int img0 = fdiv(m0, h.d_img);
+  const int ry0 = fdiv(m0 - img0 * per_img, h.d_wr);
   int oy_min, ox_min, tap0, toff0, tsgn;
   if (S2T) {
     const int cy = cls >> 1, cx = cls & 1;
@@ -426,9 +446,9 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kernel(HaloArgs h) {
     woff[i] = -2;  // -2: no item, -1: zero (outside the image)
     if (it < h.npix * 4) {
       const int pix = it >> 2, part = it & 3;
-      const int il = pix / (h.PR * h.PC);
+      const int il = fdiv(pix, h.d_win);
       const int r2 = pix - il * h.PR * h.PC;
-      const int pr = r2 / h.PC, pc = r2 - pr * h.PC;
+      const int pr = fdiv(r2, h.d_pc), pc = r2 - pr * h.PC;
       const int iy = iy_base + pr, ix = ox_min + pc;
       woff[i] = (iy >= 0 && iy < g.Hi && ix >= 0 && ix < g.Wi)
                     ? (((img0 + il) * g.Hi + iy) * g.Wi + ix) * a.lda + part * 8
@@ -465,9 +485,9 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kernel(HaloArgs h) {
   for (int tm = 0; tm < TM; ++tm) {
     const int ml = wm0 + tm * 32 + l32;
     const int rows_img = h.R * h.Wr;
-    const int il = ml / rows_img;
+    const int il = fdiv(ml, h.d_rimg);
     const int rem = ml - il * rows_img;
-    const int ryl = rem / h.Wr, rx = rem - ryl * h.Wr;
+    const int ryl = fdiv(rem, h.d_wr), rx = rem - ryl * h.Wr;
     abase[tm] = ((il * h.PR + ryl * h.sy) * h.PC + rx * h.sy) * ROWP + 8 * hh;
   }
 
@@ -544,7 +564,7 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kernel(HaloArgs h) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm0 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        const long long orow = out_row_b(g, cls, m);
+        const long long orow = out_row_h(h, g, cls, m);
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn) {
           const int n = n0 + wn0 + tn * 32 + l32;
@@ -577,7 +597,7 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kernel(HaloArgs h) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int m = m0 + wm0 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-      const long long orow = out_row_b(g, cls, m);
+      const long long orow = out_row_h(h, g, cls, m);
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) {
         const int n = n0 + wn0 + tn * 32 + l32;
@@ -1204,6 +1224,7 @@ static HaloPlan halo_plan(const FwdArgs& a, int groups) {
     p.ok = true;
     p.bm = bm;
     p.bn = bn;
+    halo_divisors(h, g);
     p.h = h;
     p.lds = lds;
     const int nchunk = a.Cin / HALO_CK;

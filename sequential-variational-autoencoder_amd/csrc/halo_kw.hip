@@ -34,16 +34,17 @@ struct KwArgs {
   int PR, PC;   // window dims per image
   int sy;       // row-space -> input stride (conv stride, else 1)
   int npix;     // nimg * PR * PC
+  // launch-constant divisors (multiply-shift): the kernel's index decode has no integer divisions
+  FastDiv d_win, d_pc, d_img, d_wr, d_rimg, d_q, d_qw;  // PR*PC, PC, Hr*Wr, Wr, R*Wr, (Ho/2)*(Wo/2), Wo/2
 };
 
 namespace {
 
-__device__ __forceinline__ long long kw_out_row(const ConvGeom& g, int cls, int m) {
+__device__ __forceinline__ long long kw_out_row(const KwArgs& h, const ConvGeom& g, int cls, int m) {
   if (g.mode == GM_CONVT && g.stride == 2) {
-    const int qh = g.Ho >> 1, qw = g.Wo >> 1;
-    const int n = m / (qh * qw);
-    const int r = m - n * qh * qw;
-    const int qy = r / qw, qx = r - qy * qw;
+    const int n = fdiv(m, h.d_q);
+    const int r = m - n * h.d_q.d;
+    const int qy = fdiv(r, h.d_qw), qx = r - qy * h.d_qw.d;
     return ((long long)n * g.Ho + 2 * qy + (cls >> 1)) * g.Wo + 2 * qx + (cls & 1);
   }
   return m;
@@ -72,8 +73,8 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kw_kernel(KwArgs h) {
 
   // ---- window origin and tap geometry (uniform; igemm_halo_kernel's) ----
   const int per_img = h.Hr * h.Wr;
-  const int img0 = m0 / per_img;
-  const int ry0 = (m0 - img0 * per_img) / h.Wr;
+  const int img0 = fdiv(m0, h.d_img);
+  const int ry0 = fdiv(m0 - img0 * per_img, h.d_wr);
   int oy_min, ox_min, tap0, toff0, tsgn;
   if (S2T) {
     const int cy = cls >> 1, cx = cls & 1;
@@ -103,9 +104,9 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kw_kernel(KwArgs h) {
     woff[i] = -2;  // -2: no item, -1: zero (outside the image)
     if (it < h.npix * 4) {
       const int pix = it >> 2, part = it & 3;
-      const int il = pix / (h.PR * h.PC);
+      const int il = fdiv(pix, h.d_win);
       const int r2 = pix - il * h.PR * h.PC;
-      const int pr = r2 / h.PC, pc = r2 - pr * h.PC;
+      const int pr = fdiv(r2, h.d_pc), pc = r2 - pr * h.PC;
       const int iy = iy_base + pr, ix = ox_min + pc;
       woff[i] = (iy >= 0 && iy < g.Hi && ix >= 0 && ix < g.Wi)
                     ? (((img0 + il) * g.Hi + iy) * g.Wi + ix) * a.lda + part * 8
@@ -138,9 +139,9 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kw_kernel(KwArgs h) {
   for (int tm = 0; tm < TM; ++tm) {
     const int ml = tm * 32 + l32;
     const int rows_img = h.R * h.Wr;
-    const int il = ml / rows_img;
+    const int il = fdiv(ml, h.d_rimg);
     const int rem = ml - il * rows_img;
-    const int ryl = rem / h.Wr, rx = rem - ryl * h.Wr;
+    const int ryl = fdiv(rem, h.d_wr), rx = rem - ryl * h.Wr;
     abase[tm] = ((il * h.PR + ryl * h.sy) * h.PC + rx * h.sy) * KW_ROWP + 8 * hh;
   }
 
@@ -233,7 +234,7 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kw_kernel(KwArgs h) {
     }
     if (bias) v += bias[n];
     v = act_f(v, a.act);
-    const long long orow = kw_out_row(g, cls, m0 + m);
+    const long long orow = kw_out_row(h, g, cls, m0 + m);
     float* dst = Cp + orow * a.ldc + n;
     if (a.accumulate) v += *dst;
     *dst = v;
@@ -294,6 +295,13 @@ static bool kw_plan(const FwdArgs& a, int groups, KwArgs* out, int* bm_out, int*
     h.PC = (Wr - 1) * sy + span;
     h.npix = h.nimg * h.PR * h.PC;
     if (h.npix * 4 > 256 * KW_PI) continue;
+    h.d_win = make_fastdiv(h.PR * h.PC);
+    h.d_pc = make_fastdiv(h.PC);
+    h.d_img = make_fastdiv(Hr * Wr);
+    h.d_wr = make_fastdiv(Wr);
+    h.d_rimg = make_fastdiv(h.R * Wr);
+    h.d_q = make_fastdiv((g.Ho >> 1) * (g.Wo >> 1));
+    h.d_qw = make_fastdiv(g.Wo >> 1);
     int bn = 32;
     if (kw_bn_mode() == 64 && a.N % 64 == 0 && (long long)(a.rows / bm) * (a.N / 64) * a.nclass * groups >= 512) bn = 64;
     const long long blocks = (long long)(a.rows / bm) * (a.N / bn) * a.nclass * groups;
