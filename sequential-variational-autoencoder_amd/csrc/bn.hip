@@ -6,6 +6,8 @@
 // (e.g. the channel half of a concat buffer, combine_noise sequential_vae.py:1833).
 // Backward: dz = dy*act'(y) (act' from the stored output, TF tie rules),
 // dpre = invstd*(dz - mean(dz) - xhat*mean(dz*xhat)), dbeta = sum(dz).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -76,8 +78,20 @@ static ApGrid ap_grid(long long rows, int C, int groups) {
   const int QB = Q < AP_QB ? Q : AP_QB;
   const int RL = 256 / QB;
   const int gx = (Q + QB - 1) / QB;
-  long long want = (rows + 4LL * RL - 1) / (4LL * RL);  // >= 4 rows per thread
-  long long cap = 2048 / ((long long)gx * groups);
+  // >= rpt rows per thread (SVAE_AP_RPT, default 2) within a budget of SVAE_AP_CAP blocks (default
+  // 4096): these latency-bound passes want blocks even though every block re-finalises its channels'
+  // statistics (tools/gpu/r02_rpt.sh: 2 / 4096 is 1 % faster per step than round 1's 4 / 2048; 8, 16,
+  // 32 rows per thread 3, 10, 25 % slower)
+  static const int rpt = [] {
+    const char* v = getenv("SVAE_AP_RPT");
+    return v ? atoi(v) : 2;
+  }();
+  long long want = (rows + (long long)rpt * RL - 1) / ((long long)rpt * RL);
+  static const int capb = [] {  // SVAE_AP_CAP: block budget of one pass
+    const char* v = getenv("SVAE_AP_CAP");
+    return v ? atoi(v) : 4096;
+  }();
+  long long cap = capb / ((long long)gx * groups);
   if (cap < 1) cap = 1;
   long long ry = want < cap ? want : cap;
   if (ry < 1) ry = 1;
