@@ -293,9 +293,42 @@ __global__ __launch_bounds__(256) void convt_smalln_kernel(FwdArgs a) {
     }
   }
 
-  if (!nvalid) return;
   float* Cp = a.C + group * a.c_gs;
-  const float bv = a.bias ? a.bias[group * a.bias_gs + r16] : 0.f;
+  const float bv = nvalid && a.bias ? a.bias[group * a.bias_gs + r16] : 0.f;
+  if (a.ldc == a.N) {
+    // the block's SN_R output rows are one contiguous run of SN_R * Wo * N floats: assemble them in
+    // LDS (the four classes interleave), then store the run with 16-byte vectors
+    __syncthreads();  // every wave is done reading the window
+    float* ot = (float*)wsm;  // [SN_R][Wo][N]
+    if (nvalid) {
+#pragma unroll
+      for (int i = 0; i < SN_MAXT; ++i) {
+        if (i < ntile) {
+          const int j = i / WT, hseg = i - j * WT;
+          const int y = 2 * j + cy;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int X = 2 * (16 * hseg + 4 * kg + e) + cx;
+            ot[(y * g.Wo + X) * a.N + r16] = act_f(acc[i][e] + bv, a.act);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    const int n = SN_R * g.Wo * a.N;
+    float* dst = Cp + ((long long)img * g.Ho + Y0) * g.Wo * a.N;
+    if ((n & 3) == 0 && (((long long)img * g.Ho + Y0) * g.Wo * a.N & 3) == 0) {
+      for (int q = tid; q < n / 4; q += 256) {
+        f32x4 v = *(const f32x4*)&ot[4 * q];
+        if (a.accumulate) v += *(const f32x4*)(dst + 4 * q);
+        *(f32x4*)(dst + 4 * q) = v;
+      }
+    } else {
+      for (int q = tid; q < n; q += 256) dst[q] = a.accumulate ? dst[q] + ot[q] : ot[q];
+    }
+    return;
+  }
+  if (!nvalid) return;
 #pragma unroll
   for (int i = 0; i < SN_MAXT; ++i) {
     if (i < ntile) {
@@ -360,11 +393,13 @@ bool smalln_ok(const FwdArgs& a) {
   if (g.Ho != 2 * g.Hi || g.Wo != 2 * g.Wi || g.Ho % SN_R || g.Wi % 16) return false;
   if ((SN_R / 2) * (g.Wi / 16) > SN_MAXT) return false;
   if (a.ldb % 8 || a.b_tap % 8 || a.lda % 4) return false;  // 16-byte fragment / staging loads
-  return (SN_R / 2 + 2) * (g.Wi + 2) * SN_PITCH * 2 <= 64 * 1024;
+  return (SN_R / 2 + 2) * (g.Wi + 2) * SN_PITCH * 2 <= 64 * 1024 && SN_R * g.Wo * a.N * 4 <= 64 * 1024;
 }
 
 void convt_smalln(const FwdArgs& a, int groups, hipStream_t s) {
-  const int lds = (SN_R / 2 + 2) * (a.g.Wi + 2) * SN_PITCH * 2;
+  const int win = (SN_R / 2 + 2) * (a.g.Wi + 2) * SN_PITCH * 2;
+  const int tile = a.ldc == a.N ? SN_R * a.g.Wo * a.N * 4 : 0;  // the assembled output rows
+  const int lds = win > tile ? win : tile;
   dim3 grid(a.g.nimg * (a.g.Ho / SN_R), 1, groups);
   hipLaunchKernelGGL(convt_smalln_kernel, grid, dim3(256), lds, s, a);
 }
