@@ -733,10 +733,12 @@ __global__ void output_fwd_kernel(const float* __restrict__ a, int HW, int C, co
   if (pix < HW) {
     const long long p = (long long)n * HW + pix;
     const float* ap = a + p * (C + 1);
+    f32x4 av = {0.f, 0.f, 0.f, 0.f};
+    if (C == 3) av = *(const f32x4*)ap;  // RGB: the packed [C | ratio] row as one 16-byte load
     float rr = 1.f;
-    if (xprev) rr = minh + (maxh - minh) * sigmoid_f(ap[C]);
+    if (xprev) rr = minh + (maxh - minh) * sigmoid_f(C == 3 ? av[3] : ap[C]);
     for (int c = 0; c < C; ++c) {
-      float out = (hi - lo) * sigmoid_f(ap[c]) + lo;
+      float out = (hi - lo) * sigmoid_f(C == 3 ? av[c] : ap[c]) + lo;
       float x = xprev ? rr * out + (1.f - rr) * xprev[p * C + c] : out;
       xhat[p * C + c] = x;
       float d = x - target[p * C + c];
@@ -766,6 +768,33 @@ __global__ void output_bwd_kernel(const float* __restrict__ a, long long P, int 
                                   float* __restrict__ da, float* __restrict__ dxprev) {
   const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
+  if (C == 3) {  // RGB: the packed [C | ratio] row is one 16-byte vector in and out (same arithmetic)
+    const f32x4 av = *(const f32x4*)(a + p * 4);
+    float rr = 1.f, sr = 0.f;
+    if (xprev) {
+      sr = sigmoid_f(av[3]);
+      rr = minh + (maxh - minh) * sr;
+    }
+    float drr = 0.f;
+    f32x4 dv;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const long long i = p * 3 + c;
+      float g = rec_coef * 2.f * (xhat[i] - target[i]);
+      if (dxhat_in) g += dxhat_in[i];
+      const float o = sigmoid_f(av[c]);
+      const float out = (hi - lo) * o + lo;
+      const float dout = xprev ? rr * g : g;
+      dv[c] = dout * (hi - lo) * o * (1.f - o);
+      if (xprev) {
+        drr += g * (out - xprev[i]);
+        dxprev[i] = (1.f - rr) * g;
+      }
+    }
+    dv[3] = xprev ? drr * (maxh - minh) * sr * (1.f - sr) : 0.f;
+    *(f32x4*)(da + p * 4) = dv;
+    return;
+  }
   const float* ap = a + p * (C + 1);
   float* dap = da + p * (C + 1);
   float rr = 1.f, sr = 0.f;
