@@ -1327,6 +1327,10 @@ int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit) {
     if (ksplit) *ksplit = 1;
     return smallc_nrb(a);
   }
+  if (dense_kw_ok(a, groups)) {  // FC layers: K over the waves of a block (dense_kw.hip)
+    if (ksplit) *ksplit = 1;
+    return dense_kw_nrb(a);
+  }
   // (no shortcut for convt_smalln: it only takes launches without stats, and the plan is asked
   //  before a.stats is set -- a BN layer must plan as the kernel that will carry its stats)
   if (!halo_disabled()) {
@@ -1398,6 +1402,11 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
     convt_smalln(a, groups, s);
     if (after) hipEventRecord(after, s);
     return 0;  // no stats (smalln_ok requires none)
+  }
+  if (path == 2 && dense_kw_ok(a, groups)) {
+    const int nrb = dense_kw(a, s);
+    if (after) hipEventRecord(after, s);
+    return nrb;
   }
   if (path == 1 || (path == 2 && !halo_disabled())) {
     HaloPlan hp = halo_plan(a, groups);

@@ -222,6 +222,10 @@ void share_gather(const float* Gv, float* G, const long long* tab, const long lo
 // ---- misc ----
 // dst[0..n) = vals[0..n) (n <= 64), values passed by value in the kernel arguments
 void set_small(float* dst, const float* vals, int n, hipStream_t s);
+// dense (FC) bf16 GEMM with K over the block's waves (dense_kw.hip)
+bool dense_kw_ok(const FwdArgs& a, int groups);
+int dense_kw_nrb(const FwdArgs& a);
+int dense_kw(const FwdArgs& a, hipStream_t s);
 void bf16_to_f32(const void* src, float* dst, long long n, hipStream_t s);  // debug copies of bf16 activations
 void fill_f32(float* p, long long n, float v, hipStream_t s);
 void philox_normal(float* out, long long n, unsigned long long seed, unsigned long long offset, hipStream_t s);
