@@ -7,7 +7,9 @@
 // waves take interleaved 16-wide K steps (step j on wave j % 4), fragments straight from HBM/L2
 // (each lane's A row is one batch row, 8 consecutive k; B from the [n][k] bf16 weight copy), and
 // the four partial tiles are summed in LDS in a fixed wave order before one epilogue (bias, act,
-// accumulate, forward BN column statistics -- the splitk_reduce contract).
+// accumulate, forward BN column statistics -- the splitk_reduce contract).  Where that grid is
+// short of 512 blocks (the encoder FC, N = 384, and the input gradients) K is also split over the
+// grid (blockIdx.z), each split writing a raw fp32 slab that splitk_reduce sums in a fixed order.
 #include <cstdlib>
 
 #include "common.h"
@@ -24,7 +26,8 @@ __global__ __launch_bounds__(256) void dense_kw_kernel(FwdArgs a) {
   __shared__ float red[4][32][BN + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int m0 = blockIdx.x * 32, n0 = blockIdx.y * BN;
-  const int K = a.Cin, nks = K / 16;
+  const int nks = a.Cin / 16, ks = gridDim.z, z = blockIdx.z;
+  const int j0 = (int)((long long)nks * z / ks), j1 = (int)((long long)nks * (z + 1) / ks);
   const int m = m0 + l32;
   const bool mv = m < a.rows;
   const __bf16* Bw = (const __bf16*)a.Bh;
@@ -35,7 +38,7 @@ __global__ __launch_bounds__(256) void dense_kw_kernel(FwdArgs a) {
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
   const long long arow = (long long)m * a.lda;
 #pragma unroll 2
-  for (int j = wave; j < nks; j += 4) {
+  for (int j = j0 + wave; j < j1; j += 4) {
     const int k = 16 * j + 8 * h;
     f32x4 lo = {0.f, 0.f, 0.f, 0.f}, hi = lo;
     if (mv) ld8_raw(a.A, arow + k, ABF, lo, hi);
@@ -57,6 +60,20 @@ __global__ __launch_bounds__(256) void dense_kw_kernel(FwdArgs a) {
   constexpr int NRG = 256 / BN;  // row groups
   const int col = tid % BN, rg = tid / BN;
   const int n = n0 + col;
+  if (ks > 1) {  // raw partial -> slab[split][row][n]; bias / act / stats in splitk_reduce
+    if (n < a.N) {
+      float* P = a.part + (long long)z * a.rows * a.N;
+      for (int r = rg; r < 32; r += NRG) {
+        const int mm = m0 + r;
+        if (mm >= a.rows) break;
+        float v = red[0][r][col];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) v += red[w][r][col];
+        P[(long long)mm * a.N + n] = v;
+      }
+    }
+    return;
+  }
   float s1 = 0.f, s2 = 0.f;
   if (n < a.N) {
     const float bias = a.bias ? a.bias[n] : 0.f;
@@ -101,19 +118,35 @@ bool dkw_disabled() {
 
 }  // namespace
 
-bool dense_kw_ok(const FwdArgs& a, int groups) {
-  if (dkw_disabled() || a.g.mode != GM_DENSE || groups != 1 || a.nclass != 1 || !a.Bh || a.bw.pre) return false;
-  if (a.Cin % 16 || a.N % 32 || a.lda % 8 || a.ldb % 8 || a.rows < 1) return false;
-  // only where the grid still fills the chip without splitting K, and the per-wave K chain is short
-  const long long blocks = (long long)((a.rows + 31) / 32) * (a.N / (a.N % 64 == 0 ? 64 : 32));
-  return blocks >= 256 && a.Cin <= 2048;
+static long long dkw_blocks(const FwdArgs& a) {
+  return (long long)((a.rows + 31) / 32) * (a.N / (a.N % 64 == 0 ? 64 : 32));
 }
 
-int dense_kw_nrb(const FwdArgs& a) { return (a.rows + 31) / 32; }
+// K splits over the grid: double while the grid is short of 512 blocks, each split keeps >= 2
+// K steps per wave and the slabs fit the scratch
+int dense_kw_ks(const FwdArgs& a) {
+  const long long blocks = dkw_blocks(a);
+  const int nks = a.Cin / 16;
+  int ks = 1;
+  if (!a.part || a.ldc % 4) return 1;
+  while (blocks * ks < 512 && nks / (2 * ks) >= 8 && (long long)(2 * ks) * a.rows * a.N <= a.part_cap) ks *= 2;
+  return ks;
+}
 
-int dense_kw(const FwdArgs& a, hipStream_t s) {
+bool dense_kw_ok(const FwdArgs& a, int groups) {
+  if (dkw_disabled() || a.g.mode != GM_DENSE || groups != 1 || a.nclass != 1 || !a.Bh) return false;
+  if (a.Cin % 16 || a.N % 32 || a.lda % 8 || a.ldb % 8 || a.rows < 1) return false;
+  if (dense_kw_ks(a) > 1) return true;
+  // unsplit: only where the grid fills the chip and the per-wave K chain is short; the fused
+  // backward-BN terms live in splitk_reduce only
+  return !a.bw.pre && dkw_blocks(a) >= 256 && a.Cin <= 2048;
+}
+
+int dense_kw_nrb(const FwdArgs& a) { return dense_kw_ks(a) > 1 ? (a.rows + 63) / 64 : (a.rows + 31) / 32; }
+
+int dense_kw(const FwdArgs& a, int ks, hipStream_t s) {
   const int tn = a.N % 64 == 0 ? 2 : 1;
-  const dim3 grid((a.rows + 31) / 32, a.N / (32 * tn));
+  const dim3 grid((a.rows + 31) / 32, a.N / (32 * tn), ks);
   if (tn == 2) {
     if (a.a_bf16) hipLaunchKernelGGL((dense_kw_kernel<2, true>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((dense_kw_kernel<2, false>), grid, dim3(256), 0, s, a);
@@ -121,5 +154,5 @@ int dense_kw(const FwdArgs& a, hipStream_t s) {
     if (a.a_bf16) hipLaunchKernelGGL((dense_kw_kernel<1, true>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((dense_kw_kernel<1, false>), grid, dim3(256), 0, s, a);
   }
-  return dense_kw_nrb(a);
+  return ks;
 }

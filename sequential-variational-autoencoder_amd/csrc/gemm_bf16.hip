@@ -1404,9 +1404,14 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
     return 0;  // no stats (smalln_ok requires none)
   }
   if (path == 2 && dense_kw_ok(a, groups)) {
-    const int nrb = dense_kw(a, s);
+    const int ks = dense_kw(a, dense_kw_ks(a), s);
     if (after) hipEventRecord(after, s);
-    return nrb;
+    if (ks > 1) {
+      dim3 grid((a.N + 63) / 64, (a.rows + SKR_ROWS - 1) / SKR_ROWS, 1);
+      hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, s, a.part, ks, a.rows, a.N, a.C, a.c_gs, a.ldc,
+                         a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs, a.s_sh, a.s_nsh, a.bw);
+    }
+    return dense_kw_nrb(a);
   }
   if (path == 1 || (path == 2 && !halo_disabled())) {
     HaloPlan hp = halo_plan(a, groups);
