@@ -20,15 +20,26 @@ namespace {
 
 typedef __bf16 dk_bf16x8 __attribute__((ext_vector_type(8)));
 
-template <int TN, bool ABF>
+#ifndef DKW_U
+#define DKW_U 4
+#endif
+
+// WK waves interleave the K steps of a 32-row tile; 4 / WK such tiles per block (BMR rows).
+// WK = 4: 32-row blocks, K over the waves.  WK = 1: 128-row blocks (the whole batch), every wave
+// its own 32 rows over the split's full K range, so each weight column is read by one block.
+template <int TN, bool ABF, int WK>
 __global__ __launch_bounds__(256) void dense_kw_kernel(FwdArgs a) {
-  constexpr int BN = 32 * TN;
-  __shared__ float red[4][32][BN + 1];
+  constexpr int BN = 32 * TN, BMR = 32 * (4 / WK);
+  __shared__ float red[WK][BMR][BN + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
-  const int m0 = blockIdx.x * 32, n0 = blockIdx.y * BN;
-  const int nks = a.Cin / 16, ks = gridDim.z, z = blockIdx.z;
+  const int wk = wave % WK, wr = wave / WK;
+  // XCD-aware order: the row blocks of one column tile (which read the same weight columns) run
+  // on one XCD and share its L2
+  const BlockXYZ blk = xcd_block();
+  const int m0 = blk.x * BMR, n0 = blk.y * BN;
+  const int nks = a.Cin / 16, ks = gridDim.z, z = blk.z;
   const int j0 = (int)((long long)nks * z / ks), j1 = (int)((long long)nks * (z + 1) / ks);
-  const int m = m0 + l32;
+  const int m = m0 + wr * 32 + l32;
   const bool mv = m < a.rows;
   const __bf16* Bw = (const __bf16*)a.Bh;
   f32x16 acc[TN];
@@ -37,25 +48,35 @@ __global__ __launch_bounds__(256) void dense_kw_kernel(FwdArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
   const long long arow = (long long)m * a.lda;
-#pragma unroll 2
-  for (int j = j0 + wave; j < j1; j += 4) {
-    const int k = 16 * j + 8 * h;
-    f32x4 lo = {0.f, 0.f, 0.f, 0.f}, hi = lo;
-    if (mv) ld8_raw(a.A, arow + k, ABF, lo, hi);
-    const dk_bf16x8 af = raw8_bf(lo, hi, ABF);
+  // DKW_U K steps per batch, all loads of a batch issued before its MFMAs (the per-wave chain is
+  // latency-bound: a handful of K steps per wave, few waves per CU); steps past the split's end
+  // load zero fragments
+  for (int jb = j0 + wk; jb < j1; jb += WK * DKW_U) {
+    dk_bf16x8 af[DKW_U], bf[DKW_U][TN];
 #pragma unroll
-    for (int t = 0; t < TN; ++t) {
-      const int n = n0 + t * 32 + l32;
-      dk_bf16x8 bf = {};
-      if (n < a.N) bf = *(const dk_bf16x8*)(Bw + (long long)n * a.ldb + k);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc[t], 0, 0, 0);
+    for (int u = 0; u < DKW_U; ++u) {
+      const int j = jb + WK * u;
+      const int k = 16 * j + 8 * h;
+      f32x4 lo = {0.f, 0.f, 0.f, 0.f}, hi = lo;
+      if (mv && j < j1) ld8_raw(a.A, arow + k, ABF, lo, hi);
+      af[u] = raw8_bf(lo, hi, ABF);
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        const int n = n0 + t * 32 + l32;
+        bf[u][t] = dk_bf16x8{};
+        if (n < a.N && j < j1) bf[u][t] = *(const dk_bf16x8*)(Bw + (long long)n * a.ldb + k);
+      }
     }
+#pragma unroll
+    for (int u = 0; u < DKW_U; ++u)
+#pragma unroll
+      for (int t = 0; t < TN; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[u], bf[u][t], acc[t], 0, 0, 0);
   }
-  // ---- the four waves' partial tiles, summed in a fixed order ----
+  // ---- the WK waves' partial tiles, summed in a fixed order ----
 #pragma unroll
   for (int t = 0; t < TN; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) red[wave][(r & 3) + 8 * (r >> 2) + 4 * h][t * 32 + l32] = acc[t][r];
+    for (int r = 0; r < 16; ++r) red[wk][wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * h][t * 32 + l32] = acc[t][r];
   __syncthreads();
   constexpr int NRG = 256 / BN;  // row groups
   const int col = tid % BN, rg = tid / BN;
@@ -63,12 +84,12 @@ __global__ __launch_bounds__(256) void dense_kw_kernel(FwdArgs a) {
   if (ks > 1) {  // raw partial -> slab[split][row][n]; bias / act / stats in splitk_reduce
     if (n < a.N) {
       float* P = a.part + (long long)z * a.rows * a.N;
-      for (int r = rg; r < 32; r += NRG) {
+      for (int r = rg; r < BMR; r += NRG) {
         const int mm = m0 + r;
         if (mm >= a.rows) break;
         float v = red[0][r][col];
 #pragma unroll
-        for (int w = 1; w < 4; ++w) v += red[w][r][col];
+        for (int w = 1; w < WK; ++w) v += red[w][r][col];
         P[(long long)mm * a.N + n] = v;
       }
     }
@@ -77,12 +98,12 @@ __global__ __launch_bounds__(256) void dense_kw_kernel(FwdArgs a) {
   float s1 = 0.f, s2 = 0.f;
   if (n < a.N) {
     const float bias = a.bias ? a.bias[n] : 0.f;
-    for (int r = rg; r < 32; r += NRG) {
+    for (int r = rg; r < BMR; r += NRG) {
       const int mm = m0 + r;
       if (mm >= a.rows) break;
       float v = red[0][r][col];
 #pragma unroll
-      for (int w = 1; w < 4; ++w) v += red[w][r][col];
+      for (int w = 1; w < WK; ++w) v += red[w][r][col];
       s1 += v;
       s2 += v * v;
       v = act_f(v + bias, a.act);
@@ -104,7 +125,7 @@ __global__ __launch_bounds__(256) void dense_kw_kernel(FwdArgs a) {
       s += sr[g * BN + tid];
       q += sr[256 + g * BN + tid];
     }
-    stat_put(a.stats + (blockIdx.x & (a.s_nsh - 1)) * a.s_sh, n0 + tid, s, q);
+    stat_put(a.stats + (blk.x & (a.s_nsh - 1)) * a.s_sh, n0 + tid, s, q);
   }
 }
 
@@ -118,18 +139,30 @@ bool dkw_disabled() {
 
 }  // namespace
 
+static int dkw_wk() {  // SVAE_DKW_WK: 4 (32-row blocks), 2 or 1 (128-row blocks)
+  static const int v = [] {
+    const char* e = getenv("SVAE_DKW_WK");
+    const int w = e ? atoi(e) : 4;
+    return (w == 1 || w == 2) ? w : 4;
+  }();
+  return v;
+}
+static int dkw_bmr() { return 32 * (4 / dkw_wk()); }
+
 static long long dkw_blocks(const FwdArgs& a) {
-  return (long long)((a.rows + 31) / 32) * (a.N / (a.N % 64 == 0 ? 64 : 32));
+  return (long long)((a.rows + dkw_bmr() - 1) / dkw_bmr()) * (a.N / (a.N % 64 == 0 ? 64 : 32));
 }
 
-// K splits over the grid: double while the grid is short of 512 blocks, each split keeps >= 2
-// K steps per wave and the slabs fit the scratch
+// K splits over the grid: double while the grid is short of the target, each split keeps >= mink
+// K steps and the slabs fit the scratch
 int dense_kw_ks(const FwdArgs& a) {
   const long long blocks = dkw_blocks(a);
   const int nks = a.Cin / 16;
+  static const int tgt = [] { const char* e = getenv("SVAE_DKW_TGT"); return e ? atoi(e) : 512; }();
+  static const int mink = [] { const char* e = getenv("SVAE_DKW_MINK"); return e ? atoi(e) : 8; }();
   int ks = 1;
   if (!a.part || a.ldc % 4) return 1;
-  while (blocks * ks < 512 && nks / (2 * ks) >= 8 && (long long)(2 * ks) * a.rows * a.N <= a.part_cap) ks *= 2;
+  while (blocks * ks < tgt && nks / (2 * ks) >= mink && (long long)(2 * ks) * a.rows * a.N <= a.part_cap) ks *= 2;
   return ks;
 }
 
@@ -142,17 +175,26 @@ bool dense_kw_ok(const FwdArgs& a, int groups) {
   return !a.bw.pre && dkw_blocks(a) >= 256 && a.Cin <= 2048;
 }
 
-int dense_kw_nrb(const FwdArgs& a) { return dense_kw_ks(a) > 1 ? (a.rows + 63) / 64 : (a.rows + 31) / 32; }
+// rows per splitk_reduce block: 16-row groups where 64-row blocks would leave the reduce with
+// fewer than 128 blocks (latency-bound), else 64 (fewer statistics atomics)
+int dense_kw_rpb(const FwdArgs& a) { return (long long)((a.N + 63) / 64) * ((a.rows + 63) / 64) < 128 ? 16 : 64; }
+
+int dense_kw_nrb(const FwdArgs& a) {
+  if (dense_kw_ks(a) > 1) return (a.rows + dense_kw_rpb(a) - 1) / dense_kw_rpb(a);
+  return (a.rows + dkw_bmr() - 1) / dkw_bmr();
+}
 
 int dense_kw(const FwdArgs& a, int ks, hipStream_t s) {
-  const int tn = a.N % 64 == 0 ? 2 : 1;
-  const dim3 grid((a.rows + 31) / 32, a.N / (32 * tn), ks);
+  const int tn = a.N % 64 == 0 ? 2 : 1, wk = dkw_wk();
+  const dim3 grid((a.rows + dkw_bmr() - 1) / dkw_bmr(), a.N / (32 * tn), ks);
+#define DKW_L(TN_, WK_)                                                                         \
+  if (a.a_bf16) hipLaunchKernelGGL((dense_kw_kernel<TN_, true, WK_>), grid, dim3(256), 0, s, a); \
+  else hipLaunchKernelGGL((dense_kw_kernel<TN_, false, WK_>), grid, dim3(256), 0, s, a);
   if (tn == 2) {
-    if (a.a_bf16) hipLaunchKernelGGL((dense_kw_kernel<2, true>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((dense_kw_kernel<2, false>), grid, dim3(256), 0, s, a);
+    if (wk == 4) { DKW_L(2, 4) } else if (wk == 2) { DKW_L(2, 2) } else { DKW_L(2, 1) }
   } else {
-    if (a.a_bf16) hipLaunchKernelGGL((dense_kw_kernel<1, true>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((dense_kw_kernel<1, false>), grid, dim3(256), 0, s, a);
+    if (wk == 4) { DKW_L(1, 4) } else if (wk == 2) { DKW_L(1, 2) } else { DKW_L(1, 1) }
   }
+#undef DKW_L
   return ks;
 }

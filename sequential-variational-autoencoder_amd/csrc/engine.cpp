@@ -763,7 +763,38 @@ static int on_side(svae_ctx* c, hipEvent_t ready, hipEvent_t freed, Fn&& fn) {
   return r;
 }
 
+// SVAE_TRACE_GEMM=1: every main-stream gather-GEMM timed alone (the stream is drained around
+// it) and printed with its shape -- a per-layer breakdown for tuning, not for measurement runs
+static bool trace_gemm() {
+  static const bool v = [] {
+    const char* e = getenv("SVAE_TRACE_GEMM");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
 static int gemm(svae_ctx* c, FwdArgs a, int groups) {
+  if (c->m.g.bf16 && a.Bh && trace_gemm()) {
+    a.part = c->slab;
+    a.part_cap = c->slab_cap;
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipDeviceSynchronize();
+    hipEventRecord(e0, c->st);
+    const int r = igemm_bf16(a, groups, c->st);
+    hipEventRecord(e1, c->st);
+    hipEventSynchronize(e1);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    const int ntap = a.g.mode == GM_DENSE ? 1 : (a.g.mode == GM_CONVT && a.g.stride == 2 ? 4 : 16);
+    const double fl = 2.0 * a.rows * a.nclass * a.N * (double)ntap * a.Cin * groups;
+    fprintf(stderr, "GEMM mode %d s %d hi %d ho %d cin %d n %d rows %d cls %d grp %d abf %d bw %d st %d  %8.2f us %7.1f TF/s\n",
+            a.g.mode, a.g.stride, a.g.Hi, a.g.Ho, a.Cin, a.N, a.rows, a.nclass, groups, a.a_bf16, a.bw.pre != nullptr,
+            a.stats != nullptr, ms * 1e3, fl / (ms * 1e9));
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    return r;
+  }
   if (c->m.g.bf16 && a.Bh) {
     a.part = c->slab;
     a.part_cap = c->slab_cap;

@@ -1072,7 +1072,8 @@ __global__ __launch_bounds__(256) void shadow_t_kernel(const float* w, __bf16* o
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* part, int ks, int rows_total, int N,
                                                             float* C, long long c_gs, int ldc, const float* bias,
                                                             long long bias_gs, int act, int accumulate, u64* stats,
-                                                            long long s_gs, long long s_sh, int s_nsh, BwStat bw) {
+                                                            long long s_gs, long long s_sh, int s_nsh, BwStat bw,
+                                                            int rpb) {
   __shared__ f32x4 red[2][256];
   const int group = blockIdx.z;
   const int qi = threadIdx.x & 15, rl = threadIdx.x >> 4;
@@ -1090,11 +1091,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* part, i
     if (!bw.y) bb = *(const f32x4*)(bw.beta + group * bw.beta_gs + n);
   }
   if (n < N) {
-    const int r0 = blockIdx.y * SKR_ROWS;
-    const int r1 = min(rows_total, r0 + SKR_ROWS);
+    const int r0 = blockIdx.y * rpb;  // rows per block: SKR_ROWS, or 16 for the few-row FC layers
+    const int r1 = min(rows_total, r0 + rpb);
     for (int r = r0 + rl; r < r1; r += 16) {
       f32x4 v = *(const f32x4*)(P + (long long)r * N + n);
-#pragma unroll 4
+#pragma unroll 8
       for (int k = 1; k < ks; ++k) v += *(const f32x4*)(P + k * slab + (long long)r * N + n);
       if (!bw.pre) {
         s1 += v;
@@ -1407,9 +1408,10 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
     const int ks = dense_kw(a, dense_kw_ks(a), s);
     if (after) hipEventRecord(after, s);
     if (ks > 1) {
-      dim3 grid((a.N + 63) / 64, (a.rows + SKR_ROWS - 1) / SKR_ROWS, 1);
+      const int rpb = dense_kw_rpb(a);
+      dim3 grid((a.N + 63) / 64, (a.rows + rpb - 1) / rpb, 1);
       hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, s, a.part, ks, a.rows, a.N, a.C, a.c_gs, a.ldc,
-                         a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs, a.s_sh, a.s_nsh, a.bw);
+                         a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs, a.s_sh, a.s_nsh, a.bw, rpb);
     }
     return dense_kw_nrb(a);
   }
@@ -1439,7 +1441,7 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
       if (hp.ks > 1) {
         dim3 grid((a.N + 63) / 64, hp.nrb, groups);
         hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, s, a.part, hp.ks, a.rows_total, a.N, a.C, a.c_gs,
-                           a.ldc, a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs, a.s_sh, a.s_nsh, a.bw);
+                           a.ldc, a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs, a.s_sh, a.s_nsh, a.bw, SKR_ROWS);
       }
       return hp.nrb;
     }
@@ -1459,7 +1461,7 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
   if (ks > 1) {
     dim3 grid((a.N + 63) / 64, nrb, groups);
     hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, s, a.part, ks, a.rows_total, a.N, a.C, a.c_gs, a.ldc,
-                       a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs, a.s_sh, a.s_nsh, a.bw);
+                       a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs, a.s_sh, a.s_nsh, a.bw, SKR_ROWS);
   }
   return nrb;
 }

@@ -225,7 +225,8 @@ void set_small(float* dst, const float* vals, int n, hipStream_t s);
 // dense (FC) bf16 GEMM with K over the block's waves (dense_kw.hip)
 bool dense_kw_ok(const FwdArgs& a, int groups);
 int dense_kw_nrb(const FwdArgs& a);
-int dense_kw_ks(const FwdArgs& a);                     // grid K splits (> 1: raw slabs for splitk_reduce)
+int dense_kw_ks(const FwdArgs& a);
+int dense_kw_rpb(const FwdArgs& a);                    // rows per splitk_reduce block                     // grid K splits (> 1: raw slabs for splitk_reduce)
 int dense_kw(const FwdArgs& a, int ks, hipStream_t s);  // returns ks
 void bf16_to_f32(const void* src, float* dst, long long n, hipStream_t s);  // debug copies of bf16 activations
 void fill_f32(float* p, long long n, float v, hipStream_t s);

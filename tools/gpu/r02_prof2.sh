@@ -1,0 +1,14 @@
+#!/bin/bash
+# parity subset + bench x2 + kernel-trace profile (tag $1)
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TAG=${1:-r02_p}
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_headline_gpu.py tests/test_engine_gpu.py tests/test_pcnn_gpu.py > gpurun_out/p2_t.log 2>&1 || { tail -30 gpurun_out/p2_t.log; exit 1; }
+tail -1 gpurun_out/p2_t.log
+for i in 1 2; do
+  timeout -k 10 200 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-fp32 > gpurun_out/p2_b.log 2>&1 || exit 1
+  echo "bench $(tail -1 gpurun_out/p2_b.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["elbo_per_img"])')"
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp32 > gpurun_out/${TAG}_prof.log 2>&1 || exit 1
+python3 tools/prof_summary.py gpurun_out/${TAG}_prof/run_results.db > gpurun_out/${TAG}_kernel_stats.txt 2>&1 || true
