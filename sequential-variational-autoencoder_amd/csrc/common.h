@@ -97,6 +97,15 @@ __device__ __forceinline__ void bw_term(float v, float pre, float m, float is, f
   sx += dz * ((pre - m) * is);
 }
 
+// the same with y already loaded (has_y) or recomputed from pre
+__device__ __forceinline__ void bw_term_v(float v, float pre, float m, float is, float b, bool has_y, float y, int act,
+                                          float& sd, float& sx) {
+  const float yv = has_y ? y : bn_y1(pre, m, is, b);
+  const float dz = v * dact_from_y(yv, act);
+  sd += dz;
+  sx += dz * ((pre - m) * is);
+}
+
 // ---- deterministic BN statistics ----
 // Every producer block adds its fp32 partial (sum, sum^2) of a column into a per-column
 // fixed-point accumulator with integer atomics.  Integer adds commute, so the total does not

@@ -284,30 +284,58 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
       bwb[tn] = a.bw.y ? 0.f : a.bw.beta[group * a.bw.beta_gs + n];
     }
   }
+  // batches of 8 rows, all loads of a batch before its stores (see igemm_halo_kernel)
+  float biasv[TN];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    const int n = n0 + wn0 + tn * 32 + l32;
+    biasv[tn] = (bias && n < a.N) ? bias[n] : 0.f;
+  }
+  const float* bwpre = bwm ? a.bw.pre + group * a.bw.pre_gs : nullptr;
+  const float* bwy = (bwm && a.bw.y) ? a.bw.y + group * a.bw.y_gs : nullptr;
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wm0 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (m >= a.rows) continue;
-      const long long orow = out_row_b(g, cls, m);
+    for (int rb = 0; rb < 16; rb += 8) {
+      long long orow[8];
+      bool mok[8];
+      float cv[8][TN], pv[8][TN], yv[8][TN];
 #pragma unroll
-      for (int tn = 0; tn < TN; ++tn) {
-        const int n = n0 + wn0 + tn * 32 + l32;
-        if (n >= a.N) continue;
-        float v = acc[tm][tn][r];
-        if (!bwm) {
-          csum[tn] += v;
-          csq[tn] += v * v;
+      for (int i = 0; i < 8; ++i) {
+        const int r = rb + i;
+        const int m = m0 + wm0 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        mok[i] = m < a.rows;
+        orow[i] = mok[i] ? out_row_b(g, cls, m) : 0;
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+          const int n = n0 + wn0 + tn * 32 + l32;
+          const bool ok = mok[i] && n < a.N;
+          const bool bwc = ok && bwm && n < a.bw.C;
+          cv[i][tn] = (ok && a.accumulate) ? Cp[orow[i] * a.ldc + n] : 0.f;
+          pv[i][tn] = bwc ? bwpre[orow[i] * a.bw.ldp + n] : 0.f;
+          yv[i][tn] = (bwc && bwy) ? bwy[orow[i] * a.bw.ldy + n] : 0.f;
         }
-        if (bias) v += bias[n];
-        v = act_f(v, a.act);
-        float* dst = Cp + orow * a.ldc + n;
-        if (a.accumulate) v += *dst;
-        *dst = v;
-        if (bwm && n < a.bw.C)
-          bw_term(v, a.bw.pre[group * a.bw.pre_gs + orow * a.bw.ldp + n], bwmean[tn], bwis[tn], bwb[tn],
-                  a.bw.y ? a.bw.y + group * a.bw.y_gs + orow * a.bw.ldy + n : nullptr, a.bw.act, csum[tn], csq[tn]);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (!mok[i]) continue;
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+          const int n = n0 + wn0 + tn * 32 + l32;
+          if (n >= a.N) continue;
+          float v = acc[tm][tn][rb + i];
+          if (!bwm) {
+            csum[tn] += v;
+            csq[tn] += v * v;
+          }
+          if (bias) v += biasv[tn];
+          v = act_f(v, a.act);
+          if (a.accumulate) v += cv[i][tn];
+          Cp[orow[i] * a.ldc + n] = v;
+          if (bwm && n < a.bw.C)
+            bw_term_v(v, pv[i][tn], bwmean[tn], bwis[tn], bwb[tn], bwy != nullptr, yv[i][tn], a.bw.act, csum[tn],
+                      csq[tn]);
+        }
       }
     }
   }
@@ -592,29 +620,57 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kernel(HaloArgs h) {
       bwb[tn] = a.bw.y ? 0.f : a.bw.beta[group * a.bw.beta_gs + n];
     }
   }
+  // batches of 8 rows: every global load of a batch (accumulate target, BN-backward pre / y) is
+  // issued before the first store, so the batch pays one memory round trip, not one per element
+  // (C may alias nothing it reads here, but the compiler cannot know that across the stores)
+  float biasv[TN];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    const int n = n0 + wn0 + tn * 32 + l32;
+    biasv[tn] = (bias && nok[tn] && n < a.N) ? bias[n] : 0.f;
+  }
+  const float* bwpre = bwm ? a.bw.pre + group * a.bw.pre_gs : nullptr;
+  const float* bwy = (bwm && a.bw.y) ? a.bw.y + group * a.bw.y_gs : nullptr;
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wm0 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-      const long long orow = out_row_h(h, g, cls, m);
+    for (int rb = 0; rb < 16; rb += 8) {
+      long long orow[8];
+      float cv[8][TN], pv[8][TN], yv[8][TN];
 #pragma unroll
-      for (int tn = 0; tn < TN; ++tn) {
-        const int n = n0 + wn0 + tn * 32 + l32;
-        if (!nok[tn] || n >= a.N) continue;
-        float v = acc[tm][tn][r];
-        if (!bwm) {
-          csum[tn] += v;
-          csq[tn] += v * v;
+      for (int i = 0; i < 8; ++i) {
+        const int r = rb + i;
+        const int m = m0 + wm0 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        orow[i] = out_row_h(h, g, cls, m);
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+          const int n = n0 + wn0 + tn * 32 + l32;
+          const bool ok = nok[tn] && n < a.N;
+          const bool bwc = ok && bwm && n < a.bw.C;
+          cv[i][tn] = (ok && a.accumulate) ? Cp[orow[i] * a.ldc + n] : 0.f;
+          pv[i][tn] = bwc ? bwpre[orow[i] * a.bw.ldp + n] : 0.f;
+          yv[i][tn] = (bwc && bwy) ? bwy[orow[i] * a.bw.ldy + n] : 0.f;
         }
-        if (bias) v += bias[n];
-        v = act_f(v, a.act);
-        float* dst = Cp + orow * a.ldc + n;
-        if (a.accumulate) v += *dst;
-        *dst = v;
-        if (bwm && n < a.bw.C)
-          bw_term(v, a.bw.pre[group * a.bw.pre_gs + orow * a.bw.ldp + n], bwmean[tn], bwis[tn], bwb[tn],
-                  a.bw.y ? a.bw.y + group * a.bw.y_gs + orow * a.bw.ldy + n : nullptr, a.bw.act, csum[tn], csq[tn]);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+          const int n = n0 + wn0 + tn * 32 + l32;
+          if (!nok[tn] || n >= a.N) continue;
+          float v = acc[tm][tn][rb + i];
+          if (!bwm) {
+            csum[tn] += v;
+            csq[tn] += v * v;
+          }
+          if (bias) v += biasv[tn];
+          v = act_f(v, a.act);
+          if (a.accumulate) v += cv[i][tn];
+          Cp[orow[i] * a.ldc + n] = v;
+          if (bwm && n < a.bw.C)
+            bw_term_v(v, pv[i][tn], bwmean[tn], bwis[tn], bwb[tn], bwy != nullptr, yv[i][tn], a.bw.act, csum[tn],
+                      csq[tn]);
+        }
       }
     }
   }

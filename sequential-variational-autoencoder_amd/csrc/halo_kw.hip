@@ -224,7 +224,24 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kw_kernel(KwArgs h) {
     bb = a.bw.y ? 0.f : a.bw.beta[group * a.bw.beta_gs + n];
   }
   float s1 = 0.f, s2 = 0.f;
-  for (int m = rg; m < BM; m += NRG) {
+  // every global load (accumulate target, BN-backward pre / y) before the first store: one
+  // memory round trip for the thread's BM / NRG rows, not one per row
+  constexpr int NR = BM / NRG;
+  long long orow[NR];
+  float cv[NR], pv[NR], yv[NR];
+  const float* bwpre = bwc ? a.bw.pre + group * a.bw.pre_gs : nullptr;
+  const float* bwy = (bwc && a.bw.y) ? a.bw.y + group * a.bw.y_gs : nullptr;
+  const float biasv = bias ? bias[n] : 0.f;
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    orow[i] = kw_out_row(h, g, cls, m0 + rg + i * NRG);
+    cv[i] = a.accumulate ? Cp[orow[i] * a.ldc + n] : 0.f;
+    pv[i] = bwpre ? bwpre[orow[i] * a.bw.ldp + n] : 0.f;
+    yv[i] = bwy ? bwy[orow[i] * a.bw.ldy + n] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int m = rg + i * NRG;
     float v = red[(0 * BM + m) * BN + col];
 #pragma unroll
     for (int w = 1; w < 4; ++w) v += red[(w * BM + m) * BN + col];
@@ -232,15 +249,11 @@ __global__ __launch_bounds__(256, 2) void igemm_halo_kw_kernel(KwArgs h) {
       s1 += v;
       s2 += v * v;
     }
-    if (bias) v += bias[n];
+    if (bias) v += biasv;
     v = act_f(v, a.act);
-    const long long orow = kw_out_row(h, g, cls, m0 + m);
-    float* dst = Cp + orow * a.ldc + n;
-    if (a.accumulate) v += *dst;
-    *dst = v;
-    if (bwc)
-      bw_term(v, a.bw.pre[group * a.bw.pre_gs + orow * a.bw.ldp + n], bm, bi, bb,
-              a.bw.y ? a.bw.y + group * a.bw.y_gs + orow * a.bw.ldy + n : nullptr, a.bw.act, s1, s2);
+    if (a.accumulate) v += cv[i];
+    Cp[orow[i] * a.ldc + n] = v;
+    if (bwc) bw_term_v(v, pv[i], bm, bi, bb, bwy != nullptr, yv[i], a.bw.act, s1, s2);
   }
   if (!a.stats) return;
   __syncthreads();  // every wave is done reading red
