@@ -1149,27 +1149,50 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* part, i
   if (n < N) {
     const int r0 = blockIdx.y * rpb;  // rows per block: SKR_ROWS, or 16 for the few-row FC layers
     const int r1 = min(rows_total, r0 + rpb);
-    for (int r = r0 + rl; r < r1; r += 16) {
-      f32x4 v = *(const f32x4*)(P + (long long)r * N + n);
-#pragma unroll 8
-      for (int k = 1; k < ks; ++k) v += *(const f32x4*)(P + k * slab + (long long)r * N + n);
-      if (!bw.pre) {
-        s1 += v;
-        s2 += v * v;
-      }
-      if (bs) v += *(const f32x4*)(bs + n);
+    // up to SKR_ROWS / 16 rows per thread: every load of all of them (slabs, accumulate target,
+    // BN-backward pre / y) before the first store
+    constexpr int NRT = SKR_ROWS / 16;
+    f32x4 v[NRT], pr[NRT], yr[NRT];
+    const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+    const f32x4 bsv = bs ? *(const f32x4*)(bs + n) : z4;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = act_f(v[e], act);
-      f32x4* d = (f32x4*)(Cg + (long long)r * ldc + n);
-      if (accumulate) v += *d;
-      *d = v;
+    for (int i = 0; i < NRT; ++i) {
+      const int r = r0 + rl + 16 * i;
+      v[i] = pr[i] = yr[i] = z4;
+      if (r >= r1) continue;
+      v[i] = *(const f32x4*)(P + (long long)r * N + n);
+#pragma unroll 8
+      for (int k = 1; k < ks; ++k) v[i] += *(const f32x4*)(P + k * slab + (long long)r * N + n);
       if (bwq) {
-        const f32x4 pr = *(const f32x4*)(bw.pre + group * bw.pre_gs + (long long)r * bw.ldp + n);
-        const float* yr = bw.y ? bw.y + group * bw.y_gs + (long long)r * bw.ldy + n : nullptr;
+        pr[i] = *(const f32x4*)(bw.pre + group * bw.pre_gs + (long long)r * bw.ldp + n);
+        if (bw.y) yr[i] = *(const f32x4*)(bw.y + group * bw.y_gs + (long long)r * bw.ldy + n);
+      }
+    }
+    f32x4 cv[NRT];
+#pragma unroll
+    for (int i = 0; i < NRT; ++i) {
+      const int r = r0 + rl + 16 * i;
+      cv[i] = (accumulate && r < r1) ? *(const f32x4*)(Cg + (long long)r * ldc + n) : z4;
+    }
+#pragma unroll
+    for (int i = 0; i < NRT; ++i) {
+      const int r = r0 + rl + 16 * i;
+      if (r >= r1) continue;
+      f32x4 w = v[i];
+      if (!bw.pre) {
+        s1 += w;
+        s2 += w * w;
+      }
+      if (bs) w += bsv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[e] = act_f(w[e], act);
+      if (accumulate) w += cv[i];
+      *(f32x4*)(Cg + (long long)r * ldc + n) = w;
+      if (bwq) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float sd = s1[e], sx = s2[e];
-          bw_term(v[e], pr[e], bm[e], bi[e], bb[e], yr ? yr + e : nullptr, bw.act, sd, sx);
+          bw_term_v(w[e], pr[i][e], bm[e], bi[e], bb[e], bw.y != nullptr, yr[i][e], bw.act, sd, sx);
           s1[e] = sd;
           s2[e] = sx;
         }
