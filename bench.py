@@ -268,6 +268,10 @@ def main():
     ap.add_argument("--no-overlap", action="store_true",
                     help="N>1: one all-reduce after the backward instead of per-step buckets during it")
     ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 parity-mode throughput (fp32_value)")
+    ap.add_argument("--probe-launches", type=int, default=96,
+                    help="dominant-kernel launches timed with HIP event pairs inside the timed region (the first N; "
+                         "0 = every launch). Each pair is two event records on the kernel's stream, so timing all "
+                         "~1000 launches of a 20-step run costs the step itself ~2 %%")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -320,7 +324,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     if probe_kid is not None and rank == 0:  # event pairs around every launch of the dominant kernel
-        L.check(L.lib().svae_probe_begin(net.ctx, probe_kid, 400 * args.steps), net.ctx)
+        cap = args.probe_launches if args.probe_launches > 0 else 400 * args.steps
+        L.check(L.lib().svae_probe_begin(net.ctx, probe_kid, cap), net.ctx)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         it += 1
@@ -362,7 +367,7 @@ def main():
         roof = dict(bound="mfma", achieved=round(ach, 3), peak=BF16_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
                     frac=round(ach / BF16_MFMA_PEAK_TFLOPS, 5), traffic=traffic,
                     kernel=probe["kernel"], launches_per_step=probe["launches"] / args.steps,
-                    avg_launch_us=round(avg_us, 2),
+                    avg_launch_us=round(avg_us, 2), timed_launches=probe["timed"],
                     flops_per_launch=round(probe["flops"] / probe["timed"]),
                     traffic_source=tsrc,
                     step_achieved_tflops=round(flops_img * value / world / 1e12, 3),

@@ -16,6 +16,10 @@ SHAPES = [  # (n, h_in, cin, cout, stride, transpose) -- CelebA B=128 forward la
     (128, 16, 128, 64, 1, 1), (128, 16, 64, 64, 1, 0), (128, 8, 128, 64, 2, 1), (128, 16, 64, 128, 2, 0),
     (128, 8, 256, 128, 1, 1), (128, 8, 128, 128, 1, 0), (128, 4, 384, 128, 2, 1),
 ]
+MAIN = [  # the heaviest main-stream launches of the step (SVAE_TRACE_GEMM), without their fused epilogues
+    (128, 32, 32, 64, 1, 0), (128, 16, 64, 128, 1, 0), (128, 8, 128, 256, 1, 0), (128, 32, 64, 32, 1, 1),
+    (128, 32, 32, 32, 1, 1), (128, 32, 32, 32, 1, 0),
+]
 IMAGE = [  # image-space launches: output conv-T (N = C+1 = 4), layer-0 input gradient (N = 3), layer-0 conv
     (128, 32, 32, 4, 2, 1), (128, 32, 32, 3, 2, 1), (128, 64, 3, 32, 2, 0),
 ]
@@ -58,5 +62,7 @@ if __name__ == "__main__":
     shapes = SHAPES
     if args and args[0] == "image":
         shapes, args = IMAGE, args[1:]
+    elif args and args[0] == "main":
+        shapes, args = MAIN, args[1:]
     for p in (args or ["0", "1"]):
         run(int(p), shapes=shapes)
