@@ -64,7 +64,7 @@ struct WH2Args {
   int g_bf16, d_bf16;            // G / D stored as bf16 (opload.h)
 };
 
-template <int WO, int CP, int KYR, int WN, int WK, bool DB, int OPB, int NSW>
+template <int WO, int CP, int KYR, int WN, int WK, bool DB, int OPB, int NSW, int PF>
 __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args a) {
   using GE = Geo2<WO, CP>;
   constexpr int NT = 64 * KYR * WN * WK;
@@ -135,8 +135,10 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][sn][r] = 0.f;
 
-  f32x4 gv[GI], dv[DI];
-  auto load_chunk = [&](int c) {
+  // PF register sets: chunk c + PF is loaded while chunk c computes (PF = 2: two chunks of
+  // compute to cover a load's latency instead of one)
+  f32x4 gvs[PF][GI], dvs[PF][DI];
+  auto load_chunk = [&](int c, f32x4 (&gv)[GI], f32x4 (&dv)[DI]) {
     const int row0 = c * CP;
     const int img0 = row0 / GE::PER_IMG;
     const int ry0 = (row0 - img0 * GE::PER_IMG) / WO;
@@ -157,7 +159,7 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
       }
     }
   };
-  auto store_chunk = [&](__bf16* st) {
+  auto store_chunk = [&](__bf16* st, const f32x4 (&gv)[GI], const f32x4 (&dv)[DI]) {
 #pragma unroll
     for (int i = 0; i < GI; ++i) {
       if (wpr[i] == -1) continue;
@@ -175,12 +177,11 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
     }
   };
 
-  if (cbeg < cend) load_chunk(cbeg);
-  for (int c = cbeg; c < cend; ++c) {
+  auto chunk_body = [&](int c, f32x4 (&gv)[GI], f32x4 (&dv)[DI]) {
     __bf16* st = DB ? wsm + ((c - cbeg) & 1) * BUF : wsm;  // DB: one barrier per chunk
-    store_chunk(st);
+    store_chunk(st, gv, dv);
     __syncthreads();
-    if (c + 1 < cend) load_chunk(c + 1);
+    if (c + PF < cend) load_chunk(c + PF, gv, dv);
     const char* sb = (const char*)st;
     // K steps kk = j*WK + wk: the wave set's offset wpos(16*wk) lives in gw / dw (additive for
     // every instantiated geometry), the rest is a compile-time constant of the unrolled j
@@ -206,6 +207,14 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
       }
     }
     if constexpr (!DB) __syncthreads();  // single stage: the next store waits for every reader
+  };
+#pragma unroll
+  for (int i = 0; i < PF; ++i)
+    if (cbeg + i < cend) load_chunk(cbeg + i, gvs[i], dvs[i]);
+  for (int c = cbeg; c < cend; c += PF) {
+#pragma unroll
+    for (int i = 0; i < PF; ++i)
+      if (c + i < cend) chunk_body(c + i, gvs[i], dvs[i]);
   }
 
   // ---- K-interleaved wave sets: sum through LDS (fixed order: deterministic) ----
@@ -259,27 +268,34 @@ size_t wh2_lds() {
   return std::max((DB ? 2 : 1) * stage, red);
 }
 
-template <int WO, int CP, int KYR, int WN, int WK, bool DB, int OPB, int NSW>
+template <int WO, int CP, int KYR, int WN, int WK, bool DB, int OPB, int NSW, int PF>
 void wh2_launch_op(const WH2Args& a, int groups, hipStream_t s) {
   const size_t lds = wh2_lds<WO, CP, KYR, WN, WK, DB, NSW>();
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)wgrad_halo2_kernel<WO, CP, KYR, WN, WK, DB, OPB, NSW>,
+    hipFuncSetAttribute((const void*)wgrad_halo2_kernel<WO, CP, KYR, WN, WK, DB, OPB, NSW, PF>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   dim3 grid(a.M / 32, a.N / (32 * WN * NSW), (4 / KYR) * a.nsplit * groups);
-  hipLaunchKernelGGL((wgrad_halo2_kernel<WO, CP, KYR, WN, WK, DB, OPB, NSW>), grid, dim3(64 * KYR * WN * WK), lds, s,
+  hipLaunchKernelGGL((wgrad_halo2_kernel<WO, CP, KYR, WN, WK, DB, OPB, NSW, PF>), grid, dim3(64 * KYR * WN * WK), lds, s,
                      a);
 }
 // operand storage (G fp32/bf16 x D fp32/bf16) as a compile-time parameter: no branches in the loads
+int env_int(const char* name, int dflt);
+template <int WO, int CP, int KYR, int WN, int WK, bool DB, int OPB, int NSW>
+void wh2_launch_pf(const WH2Args& a, int groups, hipStream_t s) {
+  static const int pf = env_int("SVAE_WH2_PF", 2);  // register prefetch depth in chunks (1 or 2)
+  if (pf == 1) wh2_launch_op<WO, CP, KYR, WN, WK, DB, OPB, NSW, 1>(a, groups, s);
+  else wh2_launch_op<WO, CP, KYR, WN, WK, DB, OPB, NSW, 2>(a, groups, s);
+}
 template <int WO, int CP, int KYR, int WN, int WK, bool DB, int NSW = 1>
 void wh2_launch(const WH2Args& a, int groups, hipStream_t s) {
   switch ((a.g_bf16 ? 1 : 0) | (a.d_bf16 ? 2 : 0)) {
-    case 0: wh2_launch_op<WO, CP, KYR, WN, WK, DB, 0, NSW>(a, groups, s); break;
-    case 1: wh2_launch_op<WO, CP, KYR, WN, WK, DB, 1, NSW>(a, groups, s); break;
-    case 2: wh2_launch_op<WO, CP, KYR, WN, WK, DB, 2, NSW>(a, groups, s); break;
-    default: wh2_launch_op<WO, CP, KYR, WN, WK, DB, 3, NSW>(a, groups, s); break;
+    case 0: wh2_launch_pf<WO, CP, KYR, WN, WK, DB, 0, NSW>(a, groups, s); break;
+    case 1: wh2_launch_pf<WO, CP, KYR, WN, WK, DB, 1, NSW>(a, groups, s); break;
+    case 2: wh2_launch_pf<WO, CP, KYR, WN, WK, DB, 2, NSW>(a, groups, s); break;
+    default: wh2_launch_pf<WO, CP, KYR, WN, WK, DB, 3, NSW>(a, groups, s); break;
   }
 }
 
