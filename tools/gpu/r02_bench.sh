@@ -12,5 +12,6 @@ head -25 gpurun_out/${TAG}_kernel_stats.txt
 if [ "$2" = "pmc" ]; then
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${TAG}_pmc_fetch -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-fp32 > gpurun_out/${TAG}_pmc_fetch.log 2>&1 || exit 1
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${TAG}_pmc_write -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-fp32 > gpurun_out/${TAG}_pmc_write.log 2>&1 || exit 1
-python3 tools/pmc_traffic.py gpurun_out/${TAG}_pmc_fetch gpurun_out/${TAG}_pmc_write gpurun_out/${TAG}_pmc_traffic.json $TAG | head -20
+python3 tools/pmc_traffic.py gpurun_out/${TAG}_pmc_fetch gpurun_out/${TAG}_pmc_write gpurun_out/${TAG}_pmc_traffic.json $TAG > gpurun_out/${TAG}_pmc.txt; head -20 gpurun_out/${TAG}_pmc.txt; rm -rf gpurun_out/${TAG}_pmc_fetch gpurun_out/${TAG}_pmc_write
 fi
+python3 tools/stream_breakdown.py gpurun_out/${TAG}_prof/run_results.db > gpurun_out/${TAG}_streams.txt 2>&1 || true

@@ -23,6 +23,7 @@ def _short(name):
     name = name.strip()
     if name.startswith("void "):
         name = name[5:]
+    name = name.replace("(anonymous namespace)::", "")
     depth = 0
     for i, ch in enumerate(name):  # cut the argument list, keep template arguments
         if ch == "<":
@@ -41,20 +42,21 @@ WIDE16 = ("wgrad_halo_kernel", "igemm_halo_kernel", "igemm_bf16_kernel", "wgrad_
 
 
 # kernels whose operand width follows their storage template parameter (opload.h): OPB (last
-# template argument) 0 = both operands fp32 (16 B/lane loads), else a bf16 operand loads 8 B/lane
-OPB_LAST = ("wgrad_halo2_kernel", "wgrad_halo_kernel")
+# template argument at OPB_POS) 0 = both operands fp32 (16 B/lane loads), else a bf16 operand loads 8 B/lane
+OPB_POS = {"wgrad_halo2_kernel": 6, "wgrad_halo_kernel": 2}
 # 16 B/lane whatever the storage (8 fp32 = two 16-B loads, 8 bf16 = one)
-WIDE16_ANY = ("igemm_halo_kw_kernel", "(anonymous namespace)::igemm_halo_kw_kernel")
+WIDE16_ANY = ("igemm_halo_kw_kernel",)
 
 
 def fetch_rule(kernel):
-    k = kernel.split("(")[0] if not kernel.startswith("(anonymous") else kernel
+    k = kernel.replace("(anonymous namespace)::", "").split("(")[0]
     for w in WIDE16_ANY:
         if k.startswith(w):
             return 2.0, "FETCH_SIZE x2 (16 B/lane loads: gfx950 half-count)"
-    for w in OPB_LAST:
+    for w, pos in OPB_POS.items():
         if k.startswith(w + "<"):
-            opb = k.rstrip(">").split(",")[-1].strip()
+            targs = k[len(w) + 1:].rstrip(">").split(",")
+            opb = targs[pos].strip() if pos < len(targs) else targs[-1].strip()
             if opb == "0":
                 return 2.0, "FETCH_SIZE x2 (fp32 operands, 16 B/lane loads: gfx950 half-count)"
             return 1.0, "FETCH_SIZE x1 (a bf16 operand loads 8 B/lane: uncalibrated, as counted)"
