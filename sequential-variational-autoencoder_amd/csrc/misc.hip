@@ -120,7 +120,7 @@ __global__ __launch_bounds__(256) void splitfc_bwd_kernel(const float* z, int ld
   const float m = ok ? mean[j] : 0.f, is = ok ? invstd[j] : 0.f, b = ok ? beta[j] : 0.f;
   const float* src = dout + (long long)(j / F) * ldo + (j % F);
   // dout rows are staged into this column of the LDS tile (independent loads, all in flight)
-#pragma unroll 8
+#pragma unroll 32
   for (int n = rg; n < B; n += SFC_RG) dps[n * SFC_PITCH + c] = ok ? src[n * o_n] : 0.f;
   __syncthreads();
   auto xhat = [&](int n) {
@@ -307,10 +307,11 @@ void splitfc_dz_reduce(const float* dz_part, int nblk, int B, int K, float* dz, 
 // latent: mu = clip(sum + bm), sig = sigmoid(sum + bs), z = mu + sig*eps, KL per image
 // (sequential_vae.py:1592-1594, :1023, :1156-1158)
 // ---------------------------------------------------------------------------
-__global__ void latent_fwd_kernel(const float* part, long long part_gs, int nsplit, int B, int Dz, LatentLvls lv,
-                                  long long bias_gs, float clipv, float prior, int uniform, const float* eps,
-                                  long long eps_gs, float* mu, float* sig, float* z, long long ms_gs, float* kl_img,
-                                  long long kl_gs) {
+__global__ void latent_fwd_kernel(const float* __restrict__ part, long long part_gs, int nsplit, int B, int Dz,
+                                  LatentLvls lv, long long bias_gs, float clipv, float prior, int uniform,
+                                  const float* __restrict__ eps, long long eps_gs, float* __restrict__ mu,
+                                  float* __restrict__ sig, float* __restrict__ z, long long ms_gs,
+                                  float* __restrict__ kl_img, long long kl_gs) {
   const int group = blockIdx.y;
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= B) return;
@@ -321,7 +322,8 @@ __global__ void latent_fwd_kernel(const float* part, long long part_gs, int nspl
     for (int d = 0; d < lv.dim[l]; ++d) {
       const int c = lv.off[l] + d;
       float sm = 0.f, ss = 0.f;
-      for (int sp = 0; sp < nsplit; ++sp) {
+#pragma unroll 8
+      for (int sp = 0; sp < nsplit; ++sp) {  // loads batched, adds in the same order
         sm += P[((long long)sp * B + n) * 2 * Dz + c];
         ss += P[((long long)sp * B + n) * 2 * Dz + Dz + c];
       }
@@ -967,9 +969,10 @@ void philox_normal(float* out, long long n, unsigned long long seed, unsigned lo
 
 // column sums of a narrow matrix (C <= 4): output conv-T bias gradients (sum over pixels)
 #define CS_BLOCKS 256
-__global__ void colsum_part_kernel(const float* X, int ld, long long rows, int C, float* part) {
+__global__ void colsum_part_kernel(const float* __restrict__ X, int ld, long long rows, int C, float* __restrict__ part) {
   __shared__ float red[4][4];
   float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
   for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (long long)gridDim.x * blockDim.x)
     for (int c = 0; c < C; ++c) s[c] += X[r * ld + c];
   for (int c = 0; c < 4; ++c) {
@@ -984,7 +987,8 @@ __global__ void colsum_fin_kernel(const float* part, int nblk, int C, float* out
   const int c = threadIdx.x;
   if (c >= C) return;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[b * 4 + c];
+#pragma unroll 16
+  for (int b = 0; b < nblk; ++b) s += part[b * 4 + c];  // loads batched, adds in the same order
   if (c < n0) out0[c] = s;
   else if (out1) out1[c - n0] = s;
 }

@@ -10,4 +10,4 @@ for i in 1 2; do
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/misc_prof -o run -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp32 > gpurun_out/misc_prof.log 2>&1 || exit 1
 python3 tools/prof_summary.py gpurun_out/misc_prof/run_results.db > gpurun_out/misc_kernel_stats.txt 2>&1 || true
-grep -E "convt_smalln|conv_smallc|output_bwd" gpurun_out/misc_kernel_stats.txt | cut -c1-60,110-175
+grep -E "colsum|latent_fwd|splitfc_bwd|splitfc_dz" gpurun_out/misc_kernel_stats.txt | cut -c1-60,110-175
