@@ -2168,10 +2168,20 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
       bool ok = hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking) == hipSuccess;
       ok = ok && hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking) == hipSuccess;
       if (c->rec_group > 0) ok = ok && hipStreamCreateWithFlags(&c->st4, hipStreamNonBlocking) == hipSuccess;
-      auto mk = [&](hipEvent_t* ev) { ok = ok && hipEventCreateWithFlags(ev, hipEventDisableTiming) == hipSuccess; };
+      // cross-stream ordering on this device only: no system-scope fence (a system-scope release
+      // writes the L2s back for host / peer visibility, a GPU-side bubble at every record); the
+      // gradient-hook event, which orders a collective's peer traffic, keeps it
+      // (SVAE_EV_SYSFENCE=1: every event with the system fence)
+      static const bool sysf = [] {
+        const char* e = getenv("SVAE_EV_SYSFENCE");
+        return e && e[0] == '1';
+      }();
+      const unsigned evf = hipEventDisableTiming | (sysf ? 0u : (unsigned)hipEventDisableSystemFence);
+      auto mk = [&](hipEvent_t* ev) { ok = ok && hipEventCreateWithFlags(ev, evf) == hipSuccess; };
       for (int i = 0; i < svae_ctx::NR; ++i) { mk(&c->ev_ready[i]); mk(&c->ev_iready[i]); }
       mk(&c->ev_drain);
-      mk(&c->ev_da_ready); mk(&c->ev_da_free); mk(&c->ev_start); mk(&c->ev_join); mk(&c->ev_hook);
+      mk(&c->ev_da_ready); mk(&c->ev_da_free); mk(&c->ev_start); mk(&c->ev_join);
+      ok = ok && hipEventCreateWithFlags(&c->ev_hook, hipEventDisableTiming) == hipSuccess;
       mk(&c->ev_aux); mk(&c->ev_aux2); mk(&c->ev_dz); mk(&c->ev_j3); mk(&c->ev_j4);
       mk(&c->ev_drain3);
       for (int i = 0; i < 64; ++i) mk(&c->ev_sfc[i]);
