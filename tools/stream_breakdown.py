@@ -38,3 +38,14 @@ name = lambda n: n.replace('void ', '').replace('(anonymous namespace)::', '').s
 order = sorted(range(len(gaps)), key=lambda i: -gaps[i])[:int(sys.argv[3]) if len(sys.argv) > 3 else 20]
 for i in sorted(order):
     print("  %7.1f us after %-40s before %-40s" % (gaps[i], name(ms[i][0]), name(ms[i + 1][0])))
+
+# what the other streams ran during the largest main-stream gaps (cross-stream waits vs CU contention)
+if len(sys.argv) > 4:
+    for i in sorted(order)[:int(sys.argv[4])]:
+        g0, g1 = ms[i][2], ms[i + 1][1]
+        if g1 - g0 < 15e3:
+            continue
+        print("gap %.1f us after %s:" % ((g1 - g0) / 1e3, name(ms[i][0])))
+        for n, s, e, sid in step:
+            if sid != main and s < g1 and e > g0:
+                print("    stream %d %-40s %8.1f .. %8.1f us" % (sid, name(n), (s - g0) / 1e3, (e - g0) / 1e3))
