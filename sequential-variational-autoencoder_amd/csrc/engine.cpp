@@ -1198,6 +1198,40 @@ static int inference_fwd(svae_ctx* c, int t0, int n, View in0) {
 }
 
 // split_latent of step t (:1796-1806): ladder_i straight into the step's concat buffers
+// The output / ratio conv-T operands of every step, PACK_MAXT steps per launch (misc.hip
+// pack_out_kernel): [tap][C+1][F1] weights (ratio row zero at t = 0), 4 bias floats, bf16 copy.
+static bool pack_step_mode() {
+  static const bool v = [] {
+    const char* e = getenv("SVAE_PACK_STEP");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
+static void pack_out_all(svae_ctx* c, hipStream_t st) {
+  if (pack_step_mode()) return;
+  const Model& M = c->m;
+  const Geo& g = M.g;
+  for (int t0 = 0; t0 < g.T; t0 += PACK_MAXT) {
+    const int nt = std::min(PACK_MAXT, g.T - t0);
+    PackOutArgs a{};
+    a.P = c->P;
+    a.C = g.C;
+    a.F1 = g.F[1];
+    for (int i = 0; i < nt; ++i) {
+      const int t = t0 + i;
+      const GenStep& G = M.gen[t];
+      a.owout[i] = G.owout;
+      a.obout[i] = G.obout;
+      a.owratio[i] = t >= 1 ? G.owratio : -1;
+      a.obratio[i] = t >= 1 ? G.obratio : -1;
+      a.wpack[i] = c->sb[t].wpack;
+      a.wpack_h[i] = g.bf16 ? (__bf16*)c->sb[t].wpack_h : nullptr;
+    }
+    pack_out(a, nt, st);
+  }
+}
+
 static void split_latent_fwd(svae_ctx* c, int t, hipStream_t stream) {
   const Model& M = c->m;
   const Geo& g = M.g;
@@ -1362,6 +1396,8 @@ static int engine_forward(svae_ctx* c) {
     }
   }
 
+  pack_out_all(c, st);
+
   // ---------------- the chain ----------------
   for (int t = 0; t < T; ++t) {
     svae_ctx::StepBufs& s = c->sb[t];
@@ -1413,19 +1449,24 @@ static int engine_forward(svae_ctx* c) {
       const int C1 = g.C + 1;
       const int F1 = F[1];
       // pack [tap][C+1][F1] (ratio row zero at t=0) for the fused output conv-T and its dgrad
+      // (wpack / wpack_h / bias packed for every step by pack_out_all at the start of the forward;
+      // SVAE_PACK_STEP=1: the former per-step copies, kept for bitwise A/B checks)
       float* bpack = s.wpack + 16 * C1 * F1;
-      HIPCHK(c, hipMemsetAsync(s.wpack, 0, (size_t)(16 * C1 * F1 + 4) * sizeof(float), st));
-      HIPCHK(c, hipMemcpyAsync(bpack, c->P + G.obout, g.C * sizeof(float), hipMemcpyDeviceToDevice, st));
-      if (t >= 1) HIPCHK(c, hipMemcpyAsync(bpack + g.C, c->P + G.obratio, sizeof(float), hipMemcpyDeviceToDevice, st));
-      HIPCHK(c, hipMemcpy2DAsync(s.wpack, (size_t)C1 * F1 * sizeof(float), c->P + G.owout, (size_t)g.C * F1 * sizeof(float),
-                                 (size_t)g.C * F1 * sizeof(float), 16, hipMemcpyDeviceToDevice, st));
-      if (t >= 1)
-        HIPCHK(c, hipMemcpy2DAsync(s.wpack + g.C * F1, (size_t)C1 * F1 * sizeof(float), c->P + G.owratio,
-                                   (size_t)F1 * sizeof(float), (size_t)F1 * sizeof(float), 16, hipMemcpyDeviceToDevice,
-                                   st));
+      if (pack_step_mode()) {
+        HIPCHK(c, hipMemsetAsync(s.wpack, 0, (size_t)(16 * C1 * F1 + 4) * sizeof(float), st));
+        HIPCHK(c, hipMemcpyAsync(bpack, c->P + G.obout, g.C * sizeof(float), hipMemcpyDeviceToDevice, st));
+        if (t >= 1) HIPCHK(c, hipMemcpyAsync(bpack + g.C, c->P + G.obratio, sizeof(float), hipMemcpyDeviceToDevice, st));
+        HIPCHK(c, hipMemcpy2DAsync(s.wpack, (size_t)C1 * F1 * sizeof(float), c->P + G.owout,
+                                   (size_t)g.C * F1 * sizeof(float), (size_t)g.C * F1 * sizeof(float), 16,
+                                   hipMemcpyDeviceToDevice, st));
+        if (t >= 1)
+          HIPCHK(c, hipMemcpy2DAsync(s.wpack + g.C * F1, (size_t)C1 * F1 * sizeof(float), c->P + G.owratio,
+                                     (size_t)F1 * sizeof(float), (size_t)F1 * sizeof(float), 16,
+                                     hipMemcpyDeviceToDevice, st));
+        if (g.bf16) shadow_weights(s.wpack, s.wpack_h, nullptr, 16LL * C1 * F1, nullptr, 0, nullptr, st);
+      }
       ConvGeom og{GM_CONVT, B, S[1], S[1], g.H, g.W, 2, 1, 4};
       if (g.bf16) {  // bf16 halo gather-GEMM, N = C+1 of one 32-column tile, bias in the epilogue
-        shadow_weights(s.wpack, s.wpack_h, nullptr, 16LL * C1 * F1, nullptr, 0, nullptr, st);
         FwdArgs a{};
         a.A = cur.p; a.lda = F1; a.a_bf16 = cur.bf;
         a.Bh = s.wpack_h; a.b_nk = 1; a.ldb = F1; a.b_tap = (long long)C1 * F1;

@@ -199,6 +199,17 @@ void gconv_smalln(const float* A, int lda, int K, const float* W0, int n0, const
 
 // ---- output layer + highway + reconstruction (sequential_vae.py:1720-1729, :1146) ----
 int output_blocks_per_img(int HW);
+// packed output / ratio conv-T weights and bias of up to PACK_MAXT chain steps (misc.hip)
+#define PACK_MAXT 16
+struct PackOutArgs {
+  const float* P;                       // flat fp32 parameters
+  long long owout[PACK_MAXT], obout[PACK_MAXT];
+  long long owratio[PACK_MAXT], obratio[PACK_MAXT];  // -1: no ratio layer (step 0)
+  float* wpack[PACK_MAXT];
+  __bf16* wpack_h[PACK_MAXT];           // nullptr in fp32 mode
+  int C, F1;
+};
+void pack_out(const PackOutArgs& a, int nt, hipStream_t s);
 void output_fwd(const float* a, int B, int HW, int C, const float* xprev, const float* target, float lo, float hi,
                 float minh, float maxh, float* xhat, float* rec_part, int nblk, hipStream_t s);
 void output_bwd(const float* a, int B, int HW, int C, const float* xprev, const float* xhat, const float* target,

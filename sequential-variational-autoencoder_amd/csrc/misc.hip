@@ -1037,3 +1037,37 @@ void set_small(float* dst, const float* vals, int n, hipStream_t s) {
   for (int i = 0; i < n && i < 64; ++i) a.v[i] = vals[i];
   hipLaunchKernelGGL(set_small_kernel, dim3(1), dim3(64), 0, s, dst, a, n);
 }
+
+// ---------------------------------------------------------------------------
+// packed output / ratio conv-T operands of up to PACK_MAXT chain steps in one launch
+// (sequential_vae.py:1720 `conv2d_t` out, :1727 ratio): wpack[t] = [tap][C+1][F1] with the
+// ratio row zero at t = 0, then 4 bias floats [b_out | b_ratio | 0...]; wpack_h[t] its bf16
+// copy (shadow_n_kernel's rounding).  Replaces per step a memset, two copies, two 2-D copies and
+// a conversion pass on the main stream (6 dependent launches -> one per forward).
+// ---------------------------------------------------------------------------
+__global__ void pack_out_kernel(PackOutArgs a) {
+  const int t = blockIdx.y;
+  const int C = a.C, C1 = C + 1, F1 = a.F1;
+  const int nw = 16 * C1 * F1;
+  const float* wout = a.P + a.owout[t];
+  const float* wratio = a.owratio[t] >= 0 ? a.P + a.owratio[t] : nullptr;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nw + 4; i += gridDim.x * blockDim.x) {
+    float v;
+    if (i < nw) {
+      const int tap = i / (C1 * F1);
+      const int rem = i - tap * C1 * F1;
+      const int co = rem / F1, ci = rem - co * F1;
+      v = co < C ? wout[((long long)tap * C + co) * F1 + ci] : (wratio ? wratio[tap * F1 + ci] : 0.f);
+      if (a.wpack_h[t]) a.wpack_h[t][i] = (__bf16)v;
+    } else {
+      const int j = i - nw;
+      v = j < C ? a.P[a.obout[t] + j] : ((j == C && a.obratio[t] >= 0) ? a.P[a.obratio[t]] : 0.f);
+    }
+    a.wpack[t][i] = v;
+  }
+}
+
+void pack_out(const PackOutArgs& a, int nt, hipStream_t s) {
+  const int n = 16 * (a.C + 1) * a.F1 + 4;
+  hipLaunchKernelGGL(pack_out_kernel, dim3((n + 255) / 256, nt), dim3(256), 0, s, a);
+}
