@@ -948,6 +948,8 @@ static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, V
       return 0;
     }
   }
+  // image-space stride-2 conv with Cin <= 3: im2col in LDS, MFMA over pixel chunks
+  if (c->m.g.bf16 && wgrad_smallc(w, groups, c->slab, c->slab_cap, dW, w_gs, c->st)) return 0;
   if (c->m.g.bf16)  // tap-merged tiles; longer splits (less slab traffic)
     choose_split(w.rows, 1, wgrad_bf16_tiles(w), groups, 16LL * w.M * w.N, c->slab_cap, w.nsplit, w.chunk, 2048,
                  256);
