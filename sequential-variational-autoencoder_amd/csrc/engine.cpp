@@ -1666,7 +1666,9 @@ static int engine_backward(svae_ctx* c) {
         choose_split(w.rows, 16, (F[1] + 127) / 128, 1, 16LL * M_out * F[1], c->slab_cap, w.nsplit, w.chunk);
       on_side(c, c->ev_da_ready, nullptr, [&] {
         w.part = c->slab;
-        wgemm(c, w, 1);
+        const int ns = g.bf16 ? wgrad_smallc_part(w, 1, c->slab, c->slab_cap, c->st) : 0;
+        if (ns) w.nsplit = ns;  // LDS im2col kernel (wgrad_smallc.hip)
+        else wgemm(c, w, 1);
         wgrad_reduce(c->slab, 0, w.nsplit, 16, M_out, F[1], c->Gr + G.owout, 0, g.C,
                      t >= 1 ? c->Gr + G.owratio : nullptr, 0, 0, 1, c->st);
         // output / ratio bias gradients (own scratch)

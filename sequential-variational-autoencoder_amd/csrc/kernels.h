@@ -46,10 +46,11 @@ struct WgArgs {
   int g_bf16, d_bf16;  // bf16 kernels: G / D stored as bf16 (opload.h)
 };
 
-// weight gradient of the 64x64 -> 32x32 stride-2 4x4 conv with Cin <= 3 (wgrad_smallc.hip):
+// weight gradient of the 64x64 -> 32x32 stride-2 4x4 layers with <= 4 image channels (wgrad_smallc.hip):
 // eligibility, and the launch (splits through slab, reduced into dW); returns 0 if not eligible
 int wgrad_smallc_ok(const WgArgs& w);
 int wgrad_smallc(const WgArgs& w, int groups, float* slab, long long slab_cap, float* dW, long long w_gs, hipStream_t s);
+int wgrad_smallc_part(const WgArgs& w, int groups, float* part, long long cap, hipStream_t s);
 int igemm_fwd_bm(const FwdArgs& a);
 // image-space stride-2 4x4 convs with Cin <= 4 (smallc.hip): eligibility, stats row-blocks
 // (smallc_bm() output pixels each) and launch; bf = the bf16 model (B = a.Bh, operands rounded)

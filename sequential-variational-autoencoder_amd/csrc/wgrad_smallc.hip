@@ -1,4 +1,4 @@
-// Weight gradient of the image-space stride-2 4x4 conv with Cin <= 3 (bf16 MFMA).
+// Weight gradient of the image-space stride-2 4x4 layers with <= 4 image channels (bf16 MFMA).
 //
 //   dW[tap][ci][co] = sum_p x[src(p, tap)][ci] * dpre[p][co],   src = (2*oy - 1 + ky, 2*ox - 1 + kx)
 //
@@ -66,9 +66,11 @@ __global__ __launch_bounds__(256) void wgrad_smallc_kernel(SCArgs a) {
   constexpr int DI = SC_CP * 4 / 256;     // 16-byte dpre items per thread (4 per pixel)
   static_assert(XROW % 4 == 0, "input rows are float4 multiples");
   // LDS: x window (fp32) | im2col planes (bf16) | dpre rows (bf16); reused for the wave reduction
-  __shared__ __attribute__((aligned(16))) float xw[SC_WR * SC_WC * CI];
-  __shared__ __attribute__((aligned(16))) __bf16 ap[NPL * SC_CP * 32];
-  __shared__ __attribute__((aligned(16))) __bf16 dr[SC_CP * 32];
+  extern __shared__ __attribute__((aligned(16))) char wsc_lds[];
+  float* xw = (float*)wsc_lds;                                          // [SC_WR][SC_WC][CI]
+  __bf16* ap = (__bf16*)(wsc_lds + SC_WR * SC_WC * CI * 4);              // [NPL][SC_CP][32]
+  __bf16* dr = (__bf16*)(wsc_lds + SC_WR * SC_WC * CI * 4 + NPL * SC_CP * 64);  // [SC_CP][32]
+  static_assert((SC_WR * SC_WC * CI * 4) % 16 == 0, "16-byte aligned planes");
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
@@ -213,21 +215,38 @@ int wgrad_smallc_disabled() {
   return v;
 }
 
-// eligible: conv (not conv-T) 4x4 stride 2 pad 1 from 64x64 to 32x32, Cin <= 3 contiguous fp32
-// input, bf16 dpre with N a multiple of 32
+// eligible: 4x4 stride 2 pad 1 gather from 64x64 to 32x32 row space, <= 4 contiguous fp32 gathered
+// channels (conv input / the output conv-T's packed gradient), bf16 row operand with N % 32 == 0
 int wgrad_smallc_ok(const WgArgs& w) {
   const ConvGeom& g = w.g;
   if (wgrad_smallc_disabled()) return 0;
   if (g.mode != GM_CONV || g.ksz != 4 || g.stride != 2 || g.pad != 1 || w.ntap != 16) return 0;
   if (g.Ho != SC_WO || g.Wo != SC_WO || g.Hi != 2 * SC_WO || g.Wi != 2 * SC_WO) return 0;
-  if (w.M < 1 || w.M > 3 || w.ldg != w.M || w.g_bf16 || !w.d_bf16) return 0;
+  if (w.M < 1 || w.M > 4 || w.ldg != w.M || w.g_bf16 || !w.d_bf16) return 0;
   if (w.N % 32 || w.ldd % 8) return 0;
   return w.rows % SC_CP == 0 && w.rows % (SC_WO * SC_WO) == 0;
 }
 
-// dW (TF layout [16][M][N], group stride w_gs) of an eligible layer; the splits go through slab
-int wgrad_smallc(const WgArgs& w, int groups, float* slab, long long slab_cap, float* dW, long long w_gs,
-                 hipStream_t s) {
+template <int CI>
+size_t wsc_lds_bytes() {
+  constexpr int NPL = (16 * CI + 31) / 32;
+  return (size_t)SC_WR * SC_WC * CI * 4 + (size_t)NPL * SC_CP * 64 + (size_t)SC_CP * 64;
+}
+template <int CI>
+void wsc_launch(const SCArgs& a, dim3 grid, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)wgrad_smallc_kernel<CI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)wsc_lds_bytes<CI>());
+    attr = true;
+  }
+  hipLaunchKernelGGL(wgrad_smallc_kernel<CI>, grid, dim3(256), wsc_lds_bytes<CI>(), s, a);
+}
+
+// partials [split][16][M][N] of an eligible layer into part (group stride nsplit*16*M*N), ~512
+// blocks with >= 2 chunks per split and the slab within cap; returns the split count (0: not
+// eligible).  The caller reduces them (wgrad_reduce), e.g. routing rows to several tensors.
+int wgrad_smallc_part(const WgArgs& w, int groups, float* part, long long cap, hipStream_t s) {
   if (!wgrad_smallc_ok(w)) return 0;
   SCArgs a;
   a.X = w.G; a.x_gs = w.g_gs;
@@ -237,25 +256,27 @@ int wgrad_smallc(const WgArgs& w, int groups, float* slab, long long slab_cap, f
   a.nchunk = w.rows / SC_CP;
   const long long per = 16LL * w.M * w.N;
   const long long tiles = (long long)(w.N / 32) * groups;
-  // ~512 blocks, >= 2 chunks per split, slab within capacity
   long long ns = (512 + tiles - 1) / tiles;
   ns = std::min<long long>(ns, std::max(1, a.nchunk / 2));
-  ns = std::min<long long>(ns, std::max<long long>(1, slab_cap / (per * groups)));
+  ns = std::min<long long>(ns, std::max<long long>(1, cap / (per * groups)));
   a.nsplit = (int)std::max<long long>(1, ns);
-  if (a.nsplit == 1) {
-    a.part = dW;
-    a.p_gs = w_gs;
-  } else {
-    a.part = slab;
-    a.p_gs = (long long)a.nsplit * per;
-  }
+  a.part = part;
+  a.p_gs = (long long)a.nsplit * per;
   dim3 grid(a.nsplit, w.N / 32, groups);
   switch (w.M) {
-    case 1: hipLaunchKernelGGL(wgrad_smallc_kernel<1>, grid, dim3(256), 0, s, a); break;
-    case 2: hipLaunchKernelGGL(wgrad_smallc_kernel<2>, grid, dim3(256), 0, s, a); break;
-    case 3: hipLaunchKernelGGL(wgrad_smallc_kernel<3>, grid, dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL(wgrad_smallc_kernel<3>, grid, dim3(256), 0, s, a); break;
+    case 1: wsc_launch<1>(a, grid, s); break;
+    case 2: wsc_launch<2>(a, grid, s); break;
+    case 3: wsc_launch<3>(a, grid, s); break;
+    default: wsc_launch<4>(a, grid, s); break;
   }
-  if (a.nsplit > 1) wgrad_reduce(slab, a.p_gs, a.nsplit, 16, w.M, w.N, dW, w_gs, w.M, nullptr, 0, 0, groups, s);
+  return a.nsplit;
+}
+
+// dW (TF layout [16][M][N], group stride w_gs) of an eligible layer through the slab
+int wgrad_smallc(const WgArgs& w, int groups, float* slab, long long slab_cap, float* dW, long long w_gs,
+                 hipStream_t s) {
+  const int ns = wgrad_smallc_part(w, groups, slab, slab_cap, s);
+  if (!ns) return 0;
+  wgrad_reduce(slab, (long long)ns * 16 * w.M * w.N, ns, 16, w.M, w.N, dW, w_gs, w.M, nullptr, 0, 0, groups, s);
   return 1;
 }
