@@ -1,3 +1,4 @@
+#include <cstdlib>
 // Implicit-GEMM convolution / FC kernels on CDNA4 MFMA (fp32 parity path).
 //
 // Every conv-like op of the hot path is one of two GEMM shapes:
@@ -608,8 +609,11 @@ void wgrad_reduce(const float* part, long long p_gs, int nsplit, int ntap, int M
   }
   const long long nq = per / 4;
   // split lanes: enough blocks to stream the slab at full bandwidth even for small outputs
+  // SVAE_WRED_SLMAX / SVAE_WRED_BLOCKS: split-lane cap and block target (A/B knobs)
+  static const int sl_max = getenv("SVAE_WRED_SLMAX") ? atoi(getenv("SVAE_WRED_SLMAX")) : 16;
+  static const int blk_target = getenv("SVAE_WRED_BLOCKS") ? atoi(getenv("SVAE_WRED_BLOCKS")) : 1024;
   int sl = 1;
-  while (sl < 64 && sl < nsplit && (nq * sl) / 256 * groups < 1024) sl *= 4;
+  while (sl < sl_max && sl < nsplit && (nq * sl) / 256 * groups < blk_target) sl *= 4;
   const int qb = 256 / sl;
   dim3 grid((unsigned)((nq + qb - 1) / qb), groups);
 #define WRED(SLV)                                                                                                    \
