@@ -912,9 +912,10 @@ static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, V
     w.g.Ho = w.g.Wo = L.hin;
     w.rows = B * L.hin * L.hin;
   }
-  if (c->m.g.bf16 && c->wg_path == 2 && wgrad_halo2_ok(w)) {  // stride 1: compile-time-geometry kernel
+  if (c->m.g.bf16 && c->wg_path == 2 && wgrad_halo2_ok(w)) {  // stride 1 / 2: compile-time-geometry kernel
     hipEvent_t* ev = nullptr;
-    if (c->probe.kid != KID_NONE) ev = probe_pair(c, KID_WHALO2_S1, 2.0 * 16 * (double)w.M * w.N * w.rows * groups);
+    if (c->probe.kid != KID_NONE)
+      ev = probe_pair(c, w.g.stride == 1 ? KID_WHALO2_S1 : KID_WHALO_32_S2, 2.0 * 16 * (double)w.M * w.N * w.rows * groups);
     wgrad_halo2(w, groups, c->slab, c->slab_cap, dW, w_gs, c->st, ev ? ev[1] : nullptr);
     return 0;
   }

@@ -40,17 +40,22 @@ __device__ __forceinline__ bf16x8 join(v4i16 lo, v4i16 hi) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int WO, int CP>
+// S: the gather stride (1: stride-1 conv / conv-T; 2: stride-2 conv, and stride-2 conv-T with dY
+// as the gathered operand), input width HI = S * WO; GP: window pitch in bf16 (64 B at stride 1,
+// 96 B at stride 2, where consecutive pixels of a K step sit two window pixels apart)
+template <int WO, int CP, int S = 1>
 struct Geo2 {
+  static constexpr int HI = S * WO;
+  static constexpr int GP = S == 1 ? 32 : 48;
   static constexpr int PER_IMG = WO * WO;
   static constexpr int IMG = CP <= PER_IMG ? 1 : CP / PER_IMG;   // images per chunk
   static constexpr int R = CP <= PER_IMG ? CP / WO : WO;         // image rows per chunk (per image)
-  static constexpr int PR = R + 3, PC = WO + 3;                  // window rows / cols per image
+  static constexpr int PR = S * (R - 1) + 4, PC = S * (WO - 1) + 4;  // window rows / cols per image
   static constexpr int NPIX = IMG * PR * PC;
   static constexpr int KSTEPS = CP / 16;
   // window position of chunk pixel k (k = il*PER_IMG' + ry*WO + rx within the chunk)
   static constexpr int wpos(int k) {
-    return ((k / (R * WO)) * PR + (k % (R * WO)) / WO) * PC + k % WO;
+    return ((k / (R * WO)) * PR + S * ((k % (R * WO)) / WO)) * PC + S * (k % WO);
   }
 };
 
@@ -64,14 +69,15 @@ struct WH2Args {
   int g_bf16, d_bf16;            // G / D stored as bf16 (opload.h)
 };
 
-template <int WO, int CP, int KYR, int WN, int WK, bool DB, int OPB, int NSW, int PF>
+template <int WO, int CP, int KYR, int WN, int WK, bool DB, int OPB, int NSW, int PF, int S = 1>
 __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args a) {
-  using GE = Geo2<WO, CP>;
+  using GE = Geo2<WO, CP, S>;
+  constexpr int GP = GE::GP, HI = GE::HI;
   constexpr int NT = 64 * KYR * WN * WK;
   constexpr int DN = 32 * WN * NSW;               // D columns per block (NSW 32-column subtiles per wave)
   constexpr int GI = (GE::NPIX * 8 + NT - 1) / NT;  // window items (4 channels) per thread
   constexpr int DI = (CP * DN / 4 + NT - 1) / NT;   // D items per thread
-  constexpr int GWB = GE::NPIX * 32;                // bf16 elements of one window buffer
+  constexpr int GWB = GE::NPIX * GP;                // bf16 elements of one window buffer
   constexpr int BUF = GWB + CP * DN;                // one stage (window + D rows)
   static_assert((CP % WO) == 0 || (CP % GE::PER_IMG) == 0, "chunks are whole rows or whole images");
   static_assert(GE::KSTEPS % WK == 0, "K steps split evenly over the wave sets");
@@ -109,16 +115,16 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
       const int r2 = pix - il * GE::PR * GE::PC;
       const int pr = r2 / GE::PC, pc = r2 - pr * GE::PC;
       const int ix = pc - 1;
-      wrel[i] = ((il * WO + pr) * WO + ix) * a.ldg + m0 + part * 4;
-      wpr[i] = (ix >= 0 && ix < WO) ? pr : -2;  // -2: column outside the image (zero)
+      wrel[i] = ((il * HI + pr) * HI + ix) * a.ldg + m0 + part * 4;
+      wpr[i] = (ix >= 0 && ix < HI) ? pr : -2;  // -2: column outside the image (zero)
     }
   }
 
   // ---- lane-dependent LDS read bases (byte offsets within a stage) ----
   const int lk = 8 * (grp >> 1) + q;                       // this lane's pixel within a K step
   const int ch = 16 * (grp & 1) + 4 * p4;                  // this lane's G channel quad
-  const int wlane = (lk / WO) * GE::PC + (lk % WO);        // its window offset (additive, no carry)
-  const int ga = ((wlane + ky * GE::PC) * 32 + ch) * 2;    // + (wpos(k0) + kx) * 64
+  const int wlane = S * ((lk / WO) * GE::PC + (lk % WO));  // its window offset (additive, no carry)
+  const int ga = ((wlane + ky * GE::PC) * GP + ch) * 2;    // + (wpos(k0) + kx) * GP * 2
   int da[NSW];                                              // + k0 * DN * 2
 #pragma unroll
   for (int sn = 0; sn < NSW; ++sn) {
@@ -142,12 +148,12 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
     const int row0 = c * CP;
     const int img0 = row0 / GE::PER_IMG;
     const int ry0 = (row0 - img0 * GE::PER_IMG) / WO;
-    const long long gbase = ((long long)img0 * WO + ry0 - 1) * WO * a.ldg;
+    const long long gbase = ((long long)img0 * HI + S * ry0 - 1) * HI * a.ldg;
 #pragma unroll
     for (int i = 0; i < GI; ++i) {
       gv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int iy = ry0 - 1 + wpr[i];
-      if (wpr[i] >= 0 && iy >= 0 && iy < WO) gv[i] = ld4_raw(a.G, gg0 + gbase + wrel[i], gbf);
+      const int iy = S * ry0 - 1 + wpr[i];
+      if (wpr[i] >= 0 && iy >= 0 && iy < HI) gv[i] = ld4_raw(a.G, gg0 + gbase + wrel[i], gbf);
     }
     const long long dc = dd0 + (long long)row0 * a.ldd + n0;
 #pragma unroll
@@ -164,7 +170,7 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
     for (int i = 0; i < GI; ++i) {
       if (wpr[i] == -1) continue;
       const int it = tid + NT * i;
-      *(bf16x4*)&st[(it >> 3) * 32 + (it & 7) * 4] = raw4_bf(gv[i], gbf);
+      *(bf16x4*)&st[(it >> 3) * GP + (it & 7) * 4] = raw4_bf(gv[i], gbf);
     }
 #pragma unroll
     for (int i = 0; i < DI; ++i) {
@@ -185,7 +191,7 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
     const char* sb = (const char*)st;
     // K steps kk = j*WK + wk: the wave set's offset wpos(16*wk) lives in gw / dw (additive for
     // every instantiated geometry), the rest is a compile-time constant of the unrolled j
-    const int gw = ga + GE::wpos(16 * wk) * 64;
+    const int gw = ga + GE::wpos(16 * wk) * GP * 2;
 #pragma unroll
     for (int j = 0; j < GE::KSTEPS / WK; ++j) {
       const int k0 = j * WK * 16;
@@ -199,8 +205,8 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
       const int w0 = GE::wpos(k0), w1 = GE::wpos(k0 + 4);
 #pragma unroll
       for (int kx = 0; kx < 4; ++kx) {
-        const bf16x8 af = join(tr16((const __bf16*)(sb + gw + (w0 + kx) * 64)),
-                               tr16((const __bf16*)(sb + gw + (w1 + kx) * 64)));
+        const bf16x8 af = join(tr16((const __bf16*)(sb + gw + (w0 + kx) * GP * 2)),
+                               tr16((const __bf16*)(sb + gw + (w1 + kx) * GP * 2)));
 #pragma unroll
         for (int sn = 0; sn < NSW; ++sn)  // every transposed A fragment feeds NSW MFMAs
           acc[kx][sn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[sn], acc[kx][sn], 0, 0, 0);
@@ -260,42 +266,42 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
 // ---------------------------------------------------------------------------
 namespace {
 
-template <int WO, int CP, int KYR, int WN, int WK, bool DB, int NSW>
+template <int WO, int CP, int KYR, int WN, int WK, bool DB, int NSW, int S>
 size_t wh2_lds() {
-  using GE = Geo2<WO, CP>;
-  const size_t stage = ((size_t)GE::NPIX * 32 + (size_t)CP * 32 * WN * NSW) * 2;
+  using GE = Geo2<WO, CP, S>;
+  const size_t stage = ((size_t)GE::NPIX * GE::GP + (size_t)CP * 32 * WN * NSW) * 2;
   const size_t red = WK > 1 ? (size_t)(WK - 1) * KYR * WN * 4 * 16 * 64 * 4 : 0;
   return std::max((DB ? 2 : 1) * stage, red);
 }
 
-template <int WO, int CP, int KYR, int WN, int WK, bool DB, int OPB, int NSW, int PF>
+template <int WO, int CP, int KYR, int WN, int WK, bool DB, int OPB, int NSW, int PF, int S>
 void wh2_launch_op(const WH2Args& a, int groups, hipStream_t s) {
-  const size_t lds = wh2_lds<WO, CP, KYR, WN, WK, DB, NSW>();
+  const size_t lds = wh2_lds<WO, CP, KYR, WN, WK, DB, NSW, S>();
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)wgrad_halo2_kernel<WO, CP, KYR, WN, WK, DB, OPB, NSW, PF>,
+    hipFuncSetAttribute((const void*)wgrad_halo2_kernel<WO, CP, KYR, WN, WK, DB, OPB, NSW, PF, S>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   dim3 grid(a.M / 32, a.N / (32 * WN * NSW), (4 / KYR) * a.nsplit * groups);
-  hipLaunchKernelGGL((wgrad_halo2_kernel<WO, CP, KYR, WN, WK, DB, OPB, NSW, PF>), grid, dim3(64 * KYR * WN * WK), lds, s,
-                     a);
+  hipLaunchKernelGGL((wgrad_halo2_kernel<WO, CP, KYR, WN, WK, DB, OPB, NSW, PF, S>), grid, dim3(64 * KYR * WN * WK), lds,
+                     s, a);
 }
 // operand storage (G fp32/bf16 x D fp32/bf16) as a compile-time parameter: no branches in the loads
 int env_int(const char* name, int dflt);
-template <int WO, int CP, int KYR, int WN, int WK, bool DB, int OPB, int NSW>
+template <int WO, int CP, int KYR, int WN, int WK, bool DB, int OPB, int NSW, int S>
 void wh2_launch_pf(const WH2Args& a, int groups, hipStream_t s) {
   static const int pf = env_int("SVAE_WH2_PF", 2);  // register prefetch depth in chunks (1 or 2)
-  if (pf == 1) wh2_launch_op<WO, CP, KYR, WN, WK, DB, OPB, NSW, 1>(a, groups, s);
-  else wh2_launch_op<WO, CP, KYR, WN, WK, DB, OPB, NSW, 2>(a, groups, s);
+  if (pf == 1) wh2_launch_op<WO, CP, KYR, WN, WK, DB, OPB, NSW, 1, S>(a, groups, s);
+  else wh2_launch_op<WO, CP, KYR, WN, WK, DB, OPB, NSW, 2, S>(a, groups, s);
 }
-template <int WO, int CP, int KYR, int WN, int WK, bool DB, int NSW = 1>
+template <int WO, int CP, int KYR, int WN, int WK, bool DB, int NSW = 1, int S = 1>
 void wh2_launch(const WH2Args& a, int groups, hipStream_t s) {
   switch ((a.g_bf16 ? 1 : 0) | (a.d_bf16 ? 2 : 0)) {
-    case 0: wh2_launch_pf<WO, CP, KYR, WN, WK, DB, 0, NSW>(a, groups, s); break;
-    case 1: wh2_launch_pf<WO, CP, KYR, WN, WK, DB, 1, NSW>(a, groups, s); break;
-    case 2: wh2_launch_pf<WO, CP, KYR, WN, WK, DB, 2, NSW>(a, groups, s); break;
-    default: wh2_launch_pf<WO, CP, KYR, WN, WK, DB, 3, NSW>(a, groups, s); break;
+    case 0: wh2_launch_pf<WO, CP, KYR, WN, WK, DB, 0, NSW, S>(a, groups, s); break;
+    case 1: wh2_launch_pf<WO, CP, KYR, WN, WK, DB, 1, NSW, S>(a, groups, s); break;
+    case 2: wh2_launch_pf<WO, CP, KYR, WN, WK, DB, 2, NSW, S>(a, groups, s); break;
+    default: wh2_launch_pf<WO, CP, KYR, WN, WK, DB, 3, NSW, S>(a, groups, s); break;
   }
 }
 
@@ -318,24 +324,32 @@ int wgrad_halo2_enabled() {
 // Split count: ~target blocks over the machine (SVAE_WH2_TARGET, default 128: in the step the
 // kernel shares the GPU with the main stream, and half the splits halve the slab traffic), >= minch chunks
 // per split (SVAE_WH2_MINCH, default 4), slab within capacity.
-static int wh2_cp(int WO) { return WO == 32 ? 128 : 256; }
+// stride 2 (SVAE_WH2_S2=0 keeps those layers on gemm_bf16.hip's generic halo weight-GEMM): 64-pixel
+// chunks (the window is ~4x the chunk's pixels), row-space widths 8 and 16
+static int wh2_cp(int WO, int S) { return S == 2 ? 64 : (WO == 32 ? 128 : 256); }
+static int wh2_s2_enabled() {
+  static const int v = env_int("SVAE_WH2_S2", 1);
+  return v;
+}
 
 int wgrad_halo2_ok(const WgArgs& w) {
   const ConvGeom& g = w.g;
   if (!wgrad_halo2_enabled()) return 0;
-  if (g.mode != GM_CONV || g.ksz != 4 || w.ntap != 16 || g.stride != 1 || g.pad != 1) return 0;
-  if (g.Ho != g.Wo || g.Hi != g.Ho || g.Wi != g.Wo) return 0;
+  if (g.mode != GM_CONV || g.ksz != 4 || w.ntap != 16 || g.pad != 1) return 0;
+  if (g.stride != 1 && !(g.stride == 2 && wh2_s2_enabled())) return 0;
+  if (g.Ho != g.Wo || g.Hi != g.stride * g.Ho || g.Wi != g.stride * g.Wo) return 0;
   const int WO = g.Wo;
-  if (WO != 8 && WO != 16 && WO != 32) return 0;
+  if (g.stride == 1 ? (WO != 8 && WO != 16 && WO != 32) : (WO != 8 && WO != 16)) return 0;
   if (w.M % 32 || w.N % 32 || w.ldg % 4 || w.ldd % 4) return 0;
-  return w.rows % wh2_cp(WO) == 0;
+  return w.rows % wh2_cp(WO, g.stride) == 0;
 }
 
 int wgrad_halo2(const WgArgs& w, int groups, float* slab, long long slab_cap, float* dW, long long w_gs,
                 hipStream_t s, hipEvent_t after) {
   if (!wgrad_halo2_ok(w)) return 0;
   const int WO = w.g.Wo;
-  const int cp = wh2_cp(WO);
+  const int S = w.g.stride;
+  const int cp = wh2_cp(WO, S);
   static const int target = env_int("SVAE_WH2_TARGET", 128);
   static const int minch = env_int("SVAE_WH2_MINCH", 4);
   // SVAE_WH2_NSW=2: a 64-column block as 4 waves of two 32-column subtiles (each transposed A
@@ -367,7 +381,16 @@ int wgrad_halo2(const WgArgs& w, int groups, float* slab, long long slab_cap, fl
   if (wn == 2 && nsw == 2) { wh2_launch<WOV, CPV, 4, 1, 1, false, 2>(a, groups, s); } \
   else if (wn == 2) { WH2(WOV, CPV, 4, 2, 1); }                                     \
   else { WH2(WOV, CPV, 4, 1, 2); }
-  if (WO == 32) { WH2_WO(32, 128) }
+  if (S == 2) {  // 64-pixel chunks: WN = 2 where N >= 64, else two K-interleaved wave sets
+    if (WO == 16) {
+      if (wn == 2) wh2_launch<16, 64, 4, 2, 1, false, 1, 2>(a, groups, s);
+      else wh2_launch<16, 64, 4, 1, 2, false, 1, 2>(a, groups, s);
+    } else {
+      if (wn == 2) wh2_launch<8, 64, 4, 2, 1, false, 1, 2>(a, groups, s);
+      else wh2_launch<8, 64, 4, 1, 2, false, 1, 2>(a, groups, s);
+    }
+  }
+  else if (WO == 32) { WH2_WO(32, 128) }
   else if (WO == 16) { WH2_WO(16, 256) }
   else { WH2_WO(8, 256) }
 #undef WH2_WO
