@@ -11,7 +11,8 @@ import os
 import torch  # noqa: F401  (must be imported before the HIP library is mapped)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsvae_hip.so")
+# SVAE_LIB: another build of the library (A/B runs of compile-time variants)
+LIB_PATH = os.environ.get("SVAE_LIB") or os.path.join(_HERE, "libsvae_hip.so")
 
 _c_float_p = ctypes.POINTER(ctypes.c_float)
 

@@ -414,8 +414,10 @@ static void halo_divisors(HaloArgs& h, const ConvGeom& g) {
   h.d_qw = make_fastdiv(g.Wo >> 1);
 }
 
+// bf16-A instances up to 128x64 at 4 waves per SIMD (128 VGPRs, 8-32 bytes of spill): +0.8 % of the step
+// in a same-box A/B; the fp32-A instances spill 70-90 bytes there and were 1 % slower
 template <int BM, int BN, int WM, int WN, bool S2T, bool ABF>
-__global__ __launch_bounds__(256, 2) void igemm_halo_kernel(HaloArgs h) {
+__global__ __launch_bounds__(256, (ABF && BN * BM <= 8192) ? 4 : 2) void igemm_halo_kernel(HaloArgs h) {
   constexpr int TM = BM / WM / 32;
   constexpr int TN = BN / WN / 32;
   constexpr int NTAP = S2T ? 4 : 16;

@@ -50,8 +50,10 @@ __device__ __forceinline__ long long kw_out_row(const KwArgs& h, const ConvGeom&
   return m;
 }
 
+// bf16-A 32-column instances at 4 waves per SIMD (<= 128 VGPRs, no spills; was 132 -> 3 waves): +0.3 %
+// of the step in a same-box A/B (tools/gpu/r02_libab.sh); the fp32-A ones would spill
 template <int BM, int BN, bool S2T, bool ABF>
-__global__ __launch_bounds__(256, 2) void igemm_halo_kw_kernel(KwArgs h) {
+__global__ __launch_bounds__(256, (ABF && BN == 32) ? 4 : 2) void igemm_halo_kw_kernel(KwArgs h) {
   constexpr int TM = BM / 32;
   constexpr int TN = BN / 32;
   constexpr int NTAP = S2T ? 4 : 16;
