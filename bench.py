@@ -30,7 +30,7 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no 2:1 s
 # stride-1 halo weight-GEMM (side stream, overlapped with the BN chain), since round 2 the
 # compile-time-geometry wgrad_halo2_kernel (its instances together; csrc/wgrad_halo2.hip)
 DOMINANT_KID = "KID_WHALO2_S1"
-PMC_FILE = "profiles/r02_v6_pmc_traffic.json"  # tools/gpu/r02_bench.sh <tag> pmc (bench command, two passes)
+PMC_FILE = "profiles/r02_v41_pmc_traffic.json"  # tools/gpu/r02_bench.sh <tag> pmc (bench command, two passes)
 
 
 # metric / workload per preset (BASELINE.json configs[1] is the headline: CelebA B=128)
@@ -171,6 +171,10 @@ def pmc_traffic(kernel):
             continue
         tot = n = 0
         for k, v in d.get("kernels", {}).items():
+            if base == "wgrad_halo2_kernel" and "<" in k:  # the stride-1 instances (last template argument S)
+                targs = k[k.index("<") + 1:k.rindex(">")].split(",")
+                if len(targs) >= 10 and targs[9].strip() != "1":
+                    continue
             if k.split("<")[0] == base and v.get("hbm_bytes_per_launch"):
                 tot += v["hbm_bytes_per_launch"] * v["dispatches_fetch_pass"]
                 n += v["dispatches_fetch_pass"]
