@@ -1,5 +1,5 @@
 """bf16 weight-gradient kernels (csrc/gemm_bf16.hip) through svae_op_wgrad_bf16 on the conv /
-conv-T layer shapes of the CelebA geometry.  Reference: float64 torch autograd of the TF-SAME
+conv-T layer shapes of the CelebA geometry (and wgrad_smallc.hip for the Cin <= 3 image convs).  Reference: float64 torch autograd of the TF-SAME
 conv on the SAME bf16-rounded x and dy (oracle/torch_twin.py), so only fp32 accumulation order
 differs: bound 2e-5 relative (L2), 1e-4 of max|ref| pointwise.  path 0 = tap-merged weight-GEMM,
 path 2 = halo weight-GEMMs (transposed LDS reads; stride 1 on the compile-time-geometry kernel of
@@ -52,4 +52,34 @@ def test_wgrad_bf16(shape, path):
     assert torch.isfinite(out).all()
     rel = float((out - ref).norm() / ref.norm())
     mx = float((out - ref).abs().max() / ref.abs().max())
+    assert rel <= 2e-5 and mx <= 1e-4, (rel, mx)
+
+
+# image-space stride-2 convs with Cin <= 3 (the first conv of every recognition ladder / encoder):
+# wgrad_smallc.hip, taken when dY is stored as bf16 (path bit 5), as the engine stores dpre
+@pytest.mark.parametrize("shape", [(4, 64, 3, 32, 2, 0), (2, 64, 1, 32, 2, 0), (2, 64, 2, 64, 2, 0)],
+                         ids=lambda s: "n%d_h%d_%dto%d" % (s[0], s[1], s[2], s[3]))
+def test_wgrad_smallc(shape):
+    L = pkg_mod("_lib")
+    n, h, cin, cout, s, tr = shape
+    g = torch.Generator().manual_seed(11 + cin)
+    ho = h // s
+    x = torch.randn(n, h, h, cin, generator=g)
+    dy = torch.randn(n, ho, ho, cout, generator=g)
+    dw = torch.full((4, 4, cin, cout), float("nan"), device="cuda")
+    scratch = torch.empty(32 << 20, device="cuda")
+    xd, dyd = x.cuda(), dy.to(torch.bfloat16).cuda()
+    rc = L.lib().svae_op_wgrad_bf16(L.ptr(xd), n, h, cin, L.ptr(dyd), cout, s, tr, 2 | 32, L.ptr(dw),
+                                    L.ptr(scratch), scratch.numel() * 4, L.stream_ptr())
+    L.check(rc)
+    torch.cuda.synchronize()
+    xr = _bf(x).double().permute(0, 3, 1, 2)
+    dyr = _bf(dy).double().permute(0, 3, 1, 2)
+    w = torch.zeros((4, 4, cin, cout), dtype=torch.float64, requires_grad=True)
+    ref, = torch.autograd.grad(torch_twin.conv2d_same(xr, w, s), w, dyr)
+    out = dw.cpu().double()
+    assert torch.isfinite(out).all()
+    rel = float((out - ref).norm() / ref.norm())
+    mx = float((out - ref).abs().max() / ref.abs().max())
+    print("wgrad_smallc %s: rel L2 %.2e, max %.2e" % (shape, rel, mx))
     assert rel <= 2e-5 and mx <= 1e-4, (rel, mx)
