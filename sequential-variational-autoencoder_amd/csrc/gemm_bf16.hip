@@ -1364,14 +1364,15 @@ static void launch_halo(const HaloArgs& h, int groups, size_t lds, hipStream_t s
   }
 }
 
-// the wave-split kernel (halo_kw.hip) is tried first where the tiled halo kernel would split K over
-// the grid, and on every layer with >= 2 channel chunks: 32-column tiles, four waves over the taps
-// (tools/bench_gather.py: 16x16 layers 39->27 / 24->18 us, 8x8 s2 conv-T 20->15; the one-chunk
-// 32x32 layers stay on the tiled kernel, where the wave split was 3-7 % slower)
+// the wave-split kernel (halo_kw.hip) is tried first wherever it fits: 32-column tiles, four waves
+// over the taps (tools/bench_gather.py: 16x16 layers 39->27 / 24->18 us, 8x8 s2 conv-T 20->15).
+// Until v42 the one-chunk 32x32 layers stayed on the tiled kernel (the wave split was 3-7 % slower
+// per launch there); at 4 waves per SIMD (v41) the wave split on every layer is 2.3 % faster per
+// step (v43, same-box A/B).  SVAE_KW: 0 = only instead of split-K, 1 = layers with >= 2 chunks
 static bool kw_first(const FwdArgs& a, const HaloPlan& hp) {
-  static const int mode = [] {  // SVAE_KW: 0 = only instead of split-K, 2 = wherever it fits
+  static const int mode = [] {  // SVAE_KW: 0 = only instead of split-K, 2 = wherever it fits (default)
     const char* v = getenv("SVAE_KW");
-    return v ? atoi(v) : 1;
+    return v ? atoi(v) : 2;
   }();
   if (hp.ks > 1) return true;
   if (mode == 2) return true;
