@@ -30,7 +30,7 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no 2:1 s
 # stride-1 halo weight-GEMM (side stream, overlapped with the BN chain), since round 2 the
 # compile-time-geometry wgrad_halo2_kernel (its instances together; csrc/wgrad_halo2.hip)
 DOMINANT_KID = "KID_WHALO2_S1"
-PMC_FILE = "profiles/r02_v41_pmc_traffic.json"  # tools/gpu/r02_bench.sh <tag> pmc (bench command, two passes)
+PMC_FILE = "profiles/r02_v43_pmc_traffic.json"  # tools/gpu/r02_bench.sh <tag> pmc (bench command, two passes)
 
 
 # metric / workload per preset (BASELINE.json configs[1] is the headline: CelebA B=128)

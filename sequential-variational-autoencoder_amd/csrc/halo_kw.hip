@@ -53,7 +53,7 @@ __device__ __forceinline__ long long kw_out_row(const KwArgs& h, const ConvGeom&
 // bf16-A 32-column instances at 4 waves per SIMD (<= 128 VGPRs, no spills; was 132 -> 3 waves): +0.3 %
 // of the step in a same-box A/B (tools/gpu/r02_libab.sh); the fp32-A ones would spill
 template <int BM, int BN, bool S2T, bool ABF>
-__global__ __launch_bounds__(256, (ABF && BN == 32) ? 4 : 2) void igemm_halo_kw_kernel(KwArgs h) {
+__global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64) ? 4 : 2) void igemm_halo_kw_kernel(KwArgs h) {
   constexpr int TM = BM / 32;
   constexpr int TN = BN / 32;
   constexpr int NTAP = S2T ? 4 : 16;
@@ -297,7 +297,12 @@ static bool kw_plan(const FwdArgs& a, int groups, KwArgs* out, int* bm_out, int*
   const int sy = g.mode == GM_CONV ? g.stride : 1;
   const int span = s2t ? 2 : 4;
   const int per_img = Hr * Wr;
-  for (int bm : {64, 32}) {
+  static const int bm_max = [] {  // SVAE_KW_BM: largest row tile (32, 64 = default, 128)
+    const char* e = getenv("SVAE_KW_BM");
+    return e ? atoi(e) : 64;
+  }();
+  for (int bm : {128, 64, 32}) {
+    if (bm > bm_max) continue;
     if (bm % Wr != 0 || a.rows % bm != 0) continue;
     if (!(per_img % bm == 0 || bm % per_img == 0)) continue;
     KwArgs h;
@@ -320,7 +325,7 @@ static bool kw_plan(const FwdArgs& a, int groups, KwArgs* out, int* bm_out, int*
     int bn = 32;
     if (kw_bn_mode() == 64 && a.N % 64 == 0 && (long long)(a.rows / bm) * (a.N / 64) * a.nclass * groups >= 512) bn = 64;
     const long long blocks = (long long)(a.rows / bm) * (a.N / bn) * a.nclass * groups;
-    if (blocks < 256 && bm == 64) continue;  // the 32-row tile doubles the blocks
+    if (blocks < 256 && bm > 32) continue;  // the smaller tile doubles the blocks
     *out = h;
     *bm_out = bm;
     *bn_out = bn;
@@ -363,7 +368,18 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
     if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<BM_, BN_, true, false>), grid, dim3(256), lds, s, h);   \
     else hipLaunchKernelGGL((igemm_halo_kw_kernel<BM_, BN_, false, false>), grid, dim3(256), lds, s, h);      \
   }
-  if (bm == 64 && bn == 64) {
+  if (bm == 128) {
+    static bool attr = false;
+    if (!attr) {  // 4 x 128 x 32 fp32 partial tiles: 64 KB
+      for (const void* f : {(const void*)igemm_halo_kw_kernel<128, 32, true, false>,
+                            (const void*)igemm_halo_kw_kernel<128, 32, false, false>,
+                            (const void*)igemm_halo_kw_kernel<128, 32, true, true>,
+                            (const void*)igemm_halo_kw_kernel<128, 32, false, true>})
+        hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+      attr = true;
+    }
+    KW_LAUNCH(128, 32)
+  } else if (bm == 64 && bn == 64) {
     static bool attr = false;
     if (!attr) {  // 4 x 64 x 64 fp32 partial tiles: 64 KB
       for (const void* f : {(const void*)igemm_halo_kw_kernel<64, 64, true, false>,
