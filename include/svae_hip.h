@@ -46,7 +46,10 @@ typedef struct svae_config {
   float latent_mean_clip;   /* +inf = no clip */
   float range_lo, range_hi; /* dataset.range */
   float min_highway, max_highway;
-  int32_t dtype;            /* 0 = fp32 (parity) */
+  int32_t dtype;            /* 0 = fp32 (parity, fp32 MFMA); 1 = bf16 MFMA, fp32 accumulate (throughput);
+                             * 2 = bf16x6: fp32-accurate on bf16 MFMA (operands split into bf16 planes,
+                             * 6 plane products in the forward / input-gradient GEMMs, 3 in the
+                             * weight-gradient GEMMs; fp32 storage) */
   /* homogeneous chain (sequential_vae.py:107-113, scopes :1573-1577, :1683-1687, :1757-1761):
    * share_phi: one "phi/inference_network" for every step; share_theta: one
    * "theta/generative_encoder_network" and one "theta/generative_network" for steps >= 1
@@ -79,6 +82,11 @@ typedef struct svae_config {
    * own clip + Adam update (:1299-1316): svae_backward_imp / svae_adam_imp. */
   int32_t add_improvement_maximization_loss;
   float latent_pred_loss_coeff;
+  /* External generator (c_pixelvae, :529-543; generator_pixelcnn :1943-1971): steps t >= this run
+   * the caller's generator (the PixelCNN++ head of svae_pcnn.h); the engine runs only their
+   * recognition (z_t, KL_t) and creates no encoder / generator variables for them.  The caller hands
+   * d loss / d x_hat_{e-1} and d loss / d z_t back with svae_set_external_grads.  0 = off. */
+  int32_t external_generator_from;
 } svae_config;
 
 typedef struct svae_param_desc {
@@ -133,8 +141,16 @@ int svae_forward(svae_ctx* ctx, const float* x, const float* target, const float
  * state (svae_backward needs a new svae_forward). */
 int svae_generate(svae_ctx* ctx, const float* z, void* stream);
 int svae_backward(svae_ctx* ctx, void* stream);
-/* Chain noise N(0,1) [T,B,H,W,C] used by every later svae_forward / svae_generate (device pointer,
- * kept by reference; NULL = drawn on device per forward, as tf.random_normal :1090). */
+/* external_generator_from = e: gradients from the caller's generator steps for the NEXT backward
+ * (device pointers, one-shot): dxhat [B,H,W,C] = d loss / d x_hat_{e-1} (the chain sample the
+ * external step reads, e.g. the PixelVAE highway's previous sample, pixelvae.py:136), dz [T,B,Dz]
+ * whose rows t >= e are d loss / d z_t (the head's conditioning and highway ratio, :123-136); the
+ * KL terms' gradients are the engine's own.  NULL = zero. */
+int svae_set_external_grads(svae_ctx* ctx, const float* dxhat, const float* dz);
+/* Chain noise N(0,1) [T,B,H,W,C] for the NEXT svae_forward or svae_generate only (device pointer,
+ * kept by reference until that call's backward; NULL or not set = drawn on device, as
+ * tf.random_normal :1090-1091).  One-shot: every forward / generate call clears it, so a generative
+ * chain never reuses the noise injected for an earlier training forward. */
 int svae_set_chain_noise(svae_ctx* ctx, const float* noise);
 /* Improvement-maximisation loss (add_improvement_maximization_loss): bind a caller-owned gradient
  * buffer (n_total elements, public layout), then after svae_forward, svae_backward_imp writes

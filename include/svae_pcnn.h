@@ -102,6 +102,22 @@ int svae_pcnn_sample(const float* l, const float* u_mix, const float* u_log, int
 int svae_pcnn_highway(const float* s, const float* prev, const float* z, const float* zb, int nimg, int64_t per_img,
                       float lo, float hi, float* out, float* ratio, void* stream);
 
+/* backward of svae_pcnn_sample over every position: dl [pixels][10 m] = d x / d l . dx (dx [pixels]
+ * [dx_stride], first 3 used): the selected component's mean, log-scale (not where clamped at -7)
+ * and tanh coefficients, through the [-1, 1] clips (inclusive) and the channel coupling; zero
+ * elsewhere (the mixture indicator carries no gradient). */
+int svae_pcnn_sample_bwd(const float* l, const float* u_mix, const float* u_log, int nimg, int per_img, int m,
+                         const float* dx, int dx_stride, float* dl, void* stream);
+/* backward of svae_pcnn_highway: ds = r dout (NULL: skipped), dprev (+)= (1 - r) dout (prev_acc),
+ * dz[img] = d loss / d z[img] (the 1-unit FC's output, before the sigmoid). */
+int svae_pcnn_highway_bwd(const float* s, const float* prev, const float* z, const float* zb, int nimg, int64_t per_img,
+                          float lo, float hi, const float* dout, float* ds, float* dprev, int prev_acc, float* dz,
+                          void* stream);
+/* dropout with a given mask (nn.py:273-274, tf.nn.dropout): y = x * mask elementwise, mask
+ * [rows][c] holding 1 / keep_prob (kept) or 0; in place allowed; the backward is the same call on
+ * the gradient. */
+int svae_pcnn_dropout(const float* x, int64_t rows, int c, int ldx, const float* mask, float* y, int ldy, void* stream);
+
 /* data-dependent init (nn.py:176-180, :206-210): column moments of y [rows][c] (fp64), then
  * g *= scale / sqrt(v + 1e-10), b -= m * scale / sqrt(v + 1e-10). */
 int svae_pcnn_wn_init(const float* y, int64_t rows, int c, int ldy, float init_scale, float* g, float* b,

@@ -40,6 +40,20 @@ def _bf(t):
     return t.to(torch.bfloat16).to(t.dtype)
 
 
+def _split(t):
+    """bf16 hi/lo split of an operand (the engine's dtype='bf16x3' staging): t ~ hi + lo."""
+    hi = _bf(t)
+    return hi, _bf(t - hi)
+
+
+def _x3(f, a, b):
+    """f bilinear in (a, b), evaluated as the engine's split-bf16 MFMA mode does:
+    a_hi*b_hi + a_hi*b_lo + a_lo*b_hi (the a_lo*b_lo term dropped), summed in the working dtype."""
+    ah, al = _split(a)
+    bh, bl = _split(b)
+    return f(ah, bh) + f(ah, bl) + f(al, bh)
+
+
 class _RoundedOp(torch.autograd.Function):
     """y = op(x, w) whose GEMM operands are rounded to bf16 exactly where the engine's
     dtype='bf16' path rounds them (fp32 accumulation everywhere):
@@ -49,14 +63,29 @@ class _RoundedOp(torch.autograd.Function):
     each leg individually switchable (output conv-T / layer-0 dgrad run in fp32)."""
 
     @staticmethod
-    def forward(ctx, x, w, fn, rf, rd, rw):
-        ctx.fn, ctx.rd, ctx.rw = fn, rd, rw
+    def forward(ctx, x, w, fn, rf, rd, rw, split=False):
+        ctx.fn, ctx.rd, ctx.rw, ctx.split = fn, rd, rw, split
         ctx.save_for_backward(x, w)
+        if split:
+            return _x3(fn, x, w) if rf else fn(x, w)
         return fn(_bf(x) if rf else x, _bf(w) if rf else w)
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
+        if ctx.split:  # vjp_x(w, gy) and vjp_w(x, gy) are bilinear: split both operands of each
+            def vx(ww, g):
+                with torch.enable_grad():
+                    xa = x.detach().requires_grad_(True)
+                    return torch.autograd.grad(ctx.fn(xa, ww), xa, g)[0]
+
+            def vw(xx, g):
+                with torch.enable_grad():
+                    wa = w.detach().requires_grad_(True)
+                    return torch.autograd.grad(ctx.fn(xx, wa), wa, g)[0]
+            gx = _x3(vx, w, gy) if ctx.rd else vx(w, gy)
+            gw = _x3(vw, x, gy) if ctx.rw else vw(x, gy)
+            return gx, gw, None, None, None, None, None
         with torch.enable_grad():
             xa = (_bf(x) if ctx.rd else x).detach().requires_grad_(True)
             wa = (_bf(w) if ctx.rd else w).detach().requires_grad_(True)
@@ -64,7 +93,7 @@ class _RoundedOp(torch.autograd.Function):
             xw = (_bf(x) if ctx.rw else x).detach().requires_grad_(True)
             ww = (_bf(w) if ctx.rw else w).detach().requires_grad_(True)
             gw, = torch.autograd.grad(ctx.fn(xw, ww), ww, _bf(gy) if ctx.rw else gy)
-        return gx, gw, None, None, None, None
+        return gx, gw, None, None, None, None, None
 
 
 def bn_train(x, beta, eps=1e-3):
@@ -88,16 +117,18 @@ def nhwc_unflatten(x, S, C):
 
 
 class Twin:
-    def __init__(self, cfg, struct, params, dtype=torch.float32, requires_grad=True, emulate_bf16=False):
+    def __init__(self, cfg, struct, params, dtype=torch.float32, requires_grad=True, emulate_bf16=False,
+                 emulate_split=False):
         self.cfg, self.struct = cfg, struct
         self.P = {k: torch.tensor(v, dtype=dtype, requires_grad=requires_grad) for k, v in params.items()}
         self.dtype = dtype
-        self.bf16 = emulate_bf16
+        self.bf16 = emulate_bf16 or emulate_split
+        self.split = emulate_split  # dtype='bf16x3': every rounded leg as hi/lo split products
 
     def _op(self, fn, x, w, rf=True, rd=True, rw=True):
         if not self.bf16:
             return fn(x, w)
-        return _RoundedOp.apply(x, w, fn, rf, rd, rw)
+        return _RoundedOp.apply(x, w, fn, rf, rd, rw, self.split)
 
     def _conv(self, x, w, s, transpose):
         fn = (lambda a, b: conv2d_t_same(a, b, s)) if transpose else (lambda a, b: conv2d_same(a, b, s))

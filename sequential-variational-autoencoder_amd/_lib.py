@@ -33,7 +33,7 @@ class SvaeConfig(ctypes.Structure):
         ("noise_stddevs", ctypes.c_float * 64), ("predict_generator_noise", ctypes.c_int32),
         ("predict_generator_stddev_max", ctypes.c_float), ("stddev_layers", ctypes.c_int32),
         ("stddev_filter_sizes", ctypes.c_int32 * 8), ("add_improvement_maximization_loss", ctypes.c_int32),
-        ("latent_pred_loss_coeff", ctypes.c_float),
+        ("latent_pred_loss_coeff", ctypes.c_float), ("external_generator_from", ctypes.c_int32),
     ]
 
 
@@ -95,6 +95,7 @@ def lib():
         "svae_set_backward_hook": ([vp, STEP_HOOK, vp], i32),
         "svae_hook_stream": ([vp], vp),
         "svae_set_chain_noise": ([vp, vp], i32),
+        "svae_set_external_grads": ([vp, vp, vp], i32),
         "svae_bind_imp": ([vp, vp], i32),
         "svae_backward_imp": ([vp, vp], i32),
         "svae_adam_imp": ([vp, f32, i64, f32, vp], i32),
@@ -123,6 +124,9 @@ def lib():
         "svae_pcnn_wn_init": ([vp, i64, i32, i32, f32, vp, vp, vp, vp], i32),
         "svae_pcnn_adam": ([vp, vp, vp, vp, i64, f32, i64, f32, vp], i32),
         "svae_pcnn_ema": ([vp, vp, i64, f32, vp], i32),
+        "svae_pcnn_sample_bwd": ([vp, vp, vp, i32, i32, i32, vp, i32, vp, vp], i32),
+        "svae_pcnn_highway_bwd": ([vp, vp, vp, vp, i32, i64, f32, f32, vp, vp, vp, i32, vp, vp], i32),
+        "svae_pcnn_dropout": ([vp, i64, i32, i32, vp, vp, i32, vp], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -138,13 +142,15 @@ EXPORTED = ["svae_param_count", "svae_param_layout", "svae_create", "svae_destro
             "svae_op_bn_act_bwd", "svae_op_fc", "svae_probe_begin", "svae_probe_end", "svae_kernel_name",
             "svae_op_gather_bf16", "svae_op_wgrad_bf16", "svae_generate", "svae_set_backward_hook",
             "svae_hook_stream", "svae_adam_range", "svae_backward_adam", "svae_adam_state",
-            "svae_set_chain_noise", "svae_bind_imp", "svae_backward_imp", "svae_adam_imp", "svae_imp_range"]
+            "svae_set_chain_noise", "svae_bind_imp", "svae_backward_imp", "svae_adam_imp", "svae_imp_range",
+            "svae_set_external_grads"]
 # include/svae_pcnn.h (the PixelCNN++ head)
 PCNN_EXPORTED = ["svae_pcnn_wnorm", "svae_pcnn_wnorm_bwd", "svae_pcnn_conv", "svae_pcnn_conv_wgrad", "svae_pcnn_colsum",
                  "svae_pcnn_mask_edge", "svae_pcnn_nonlin", "svae_pcnn_nonlin_bwd", "svae_pcnn_gate",
                  "svae_pcnn_gate_bwd", "svae_pcnn_gemm_small", "svae_pcnn_imgsum", "svae_pcnn_copy",
                  "svae_pcnn_pad_ones", "svae_pcnn_mixlogistic", "svae_pcnn_sum", "svae_pcnn_sample",
-                 "svae_pcnn_highway", "svae_pcnn_wn_init", "svae_pcnn_adam", "svae_pcnn_ema"]
+                 "svae_pcnn_highway", "svae_pcnn_wn_init", "svae_pcnn_adam", "svae_pcnn_ema", "svae_pcnn_sample_bwd",
+                 "svae_pcnn_highway_bwd", "svae_pcnn_dropout"]
 
 # bf16 GEMM instance ids (csrc/kernels.h KernelId) for svae_probe_begin
 KID_IGEMM_BF16_256x32 = 2
@@ -161,6 +167,8 @@ KID_HALO_64x128 = 21
 KID_WHALO_32_S1 = 22
 KID_WHALO_32_S2 = 23
 KID_WHALO2_S1 = 26   # wgrad_halo2_kernel<...>: every instance of the stride-1 halo weight-GEMM
+KID_HALO_KW = 27     # igemm_halo_kw_kernel<...>: the wave-split gather-GEMM (main stream)
+KID_WHALO2_S2 = 28   # wgrad_halo2_kernel<..., S = 2>: the stride-2 instances
 
 
 def check(rc, ctx=None):

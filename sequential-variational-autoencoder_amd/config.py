@@ -34,7 +34,9 @@ class SVAEConfig:
     learning_rate_decay: float = 1.0                  # :252
     reg_coeff_rate: float = 5000.0                    # :254
     clip_grad_value: float = 10.0                     # :259
-    dtype: str = "fp32"                               # "fp32" (parity) | "bf16" (bf16 MFMA, fp32 accumulate)
+    # "fp32" (parity, fp32 MFMA) | "bf16" (bf16 MFMA, fp32 accumulate) | "bf16x6" (fp32-accurate on bf16
+    # MFMA: operands split into bf16 planes, 6 plane products per gather-GEMM, 3 per weight-GEMM)
+    dtype: str = "fp32"
     share_theta_weights: bool = False                 # :213 (homogeneous generator / encoder)
     share_phi_weights: bool = False                   # :214 (homogeneous recognition)
     predict_latent_code: bool = False                 # :225 (Latent InfoMax: q(z_t | x_{t-1}))
@@ -49,6 +51,9 @@ class SVAEConfig:
     predict_generator_stddev_filter_sizes: Tuple[int, ...] = (5, 5, 5, 5, 5)  # :237-238
     add_improvement_maximization_loss: bool = False   # :227, own optimiser over phi (:1299-1316)
     latent_pred_loss_coeff: float = 0.001             # :253
+    # c_pixelvae (generator = generator_pixelcnn, :535): steps t >= this run the PixelCNN++ head
+    # (pixelvae.PixelVAE); the engine runs their recognition only.  0 = off
+    external_generator_from: int = 0
 
     def noise_list(self):
         """noise_stddevs[t] per step (sequential_vae.py:239; the reference indexes noise_stddevs[step])."""
@@ -83,7 +88,7 @@ class SVAEConfig:
         c.latent_mean_clip = self.latent_mean_clip
         c.range_lo, c.range_hi = self.range
         c.min_highway, c.max_highway = self.min_highway, self.max_highway
-        c.dtype = {"fp32": 0, "bf16": 1}[self.dtype]
+        c.dtype = {"fp32": 0, "bf16": 1, "bf16x6": 2}[self.dtype]
         c.share_theta, c.share_phi = int(self.share_theta_weights), int(self.share_phi_weights)
         c.predict_latent_code = int(self.predict_latent_code)
         c.predict_latent_code_with_regularization = int(self.predict_latent_code_with_regularization)
@@ -105,6 +110,7 @@ class SVAEConfig:
             c.stddev_filter_sizes[i] = f
         c.add_improvement_maximization_loss = int(self.add_improvement_maximization_loss)
         c.latent_pred_loss_coeff = self.latent_pred_loss_coeff
+        c.external_generator_from = int(self.external_generator_from)
         return c
 
     def as_dict(self):
@@ -128,7 +134,8 @@ class SVAEConfig:
                     predict_generator_stddev_max=self.predict_generator_stddev_max,
                     stddev_filter_sizes=tuple(self.predict_generator_stddev_filter_sizes),
                     add_improvement_maximization_loss=self.add_improvement_maximization_loss,
-                    latent_pred_loss_coeff=self.latent_pred_loss_coeff)
+                    latent_pred_loss_coeff=self.latent_pred_loss_coeff,
+                    external_generator_from=self.external_generator_from)
 
     def kl_on(self, t):
         """1 if step t's KL term enters self.loss (sequential_vae.py:1154, :1170-1172), else 0."""
@@ -176,6 +183,14 @@ PRESETS = {
                                            predict_latent_code=True, add_improvement_maximization_loss=True,
                                            latent_mean_clip=32.0, predict_latent_code_with_regularization=True,
                                            add_noise_to_chain=True, predict_generator_noise=True),  # :568-582
+    # c_pixelvae (:529-543): shared theta / phi, T=2, step 1's generator is the PixelCNN++ head
+    # (generator_pixelcnn :1943-1971 via pixelvae.make_pixel_cnn): the engine runs the recognition of
+    # both steps and step 0's ladder generator (generator_first_step is still generator_ladder, :216)
+    "c_pixelvae": SVAEConfig(latent_mean_clip=4.0, max_highway=0.8, min_highway=0.2, mc_steps=2,
+                             learning_rate_decay=0.99999, latent_dims=[12, 12, 12, 12],
+                             filter_sizes=[3, 16, 32, 64, 128, 384], share_theta_weights=True,
+                             share_phi_weights=True, regularized_steps=(0,), first_step_loss_coeff=2.0,
+                             external_generator_from=1),
     "tiny_homog": SVAEConfig(batch=4, height=32, width=32, channels=3, levels=4, filter_sizes=[3, 8, 8, 16, 24, 16],
                              latent_dims=[2, 2, 3, 2], mc_steps=3, share_theta_weights=True,
                              share_phi_weights=True),

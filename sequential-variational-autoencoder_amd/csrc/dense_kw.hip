@@ -27,7 +27,9 @@ typedef __bf16 dk_bf16x8 __attribute__((ext_vector_type(8)));
 // WK waves interleave the K steps of a 32-row tile; 4 / WK such tiles per block (BMR rows).
 // WK = 4: 32-row blocks, K over the waves.  WK = 1: 128-row blocks (the whole batch), every wave
 // its own 32 rows over the split's full K range, so each weight column is read by one block.
-template <int TN, bool ABF, int WK>
+// NS = 3: split-bf16 planes (dtype bf16x6, opload.h): A split in registers, B from the three
+// shadow planes, six MFMAs per fragment pair
+template <int TN, bool ABF, int WK, int NS = 1>
 __global__ __launch_bounds__(256) void dense_kw_kernel(FwdArgs a) {
   constexpr int BN = 32 * TN, BMR = 32 * (4 / WK);
   __shared__ float red[WK][BMR][BN + 1];
@@ -52,25 +54,29 @@ __global__ __launch_bounds__(256) void dense_kw_kernel(FwdArgs a) {
   // latency-bound: a handful of K steps per wave, few waves per CU); steps past the split's end
   // load zero fragments
   for (int jb = j0 + wk; jb < j1; jb += WK * DKW_U) {
-    dk_bf16x8 af[DKW_U], bf[DKW_U][TN];
+    dk_bf16x8 af[DKW_U][NS], bf[DKW_U][TN][NS];
 #pragma unroll
     for (int u = 0; u < DKW_U; ++u) {
       const int j = jb + WK * u;
       const int k = 16 * j + 8 * h;
       f32x4 lo = {0.f, 0.f, 0.f, 0.f}, hi = lo;
       if (mv && j < j1) ld8_raw(a.A, arow + k, ABF, lo, hi);
-      af[u] = raw8_bf(lo, hi, ABF);
+      if constexpr (NS == 1) af[u][0] = raw8_bf(lo, hi, ABF);
+      else split8<NS>(lo, hi, af[u]);
 #pragma unroll
       for (int t = 0; t < TN; ++t) {
         const int n = n0 + t * 32 + l32;
-        bf[u][t] = dk_bf16x8{};
-        if (n < a.N && j < j1) bf[u][t] = *(const dk_bf16x8*)(Bw + (long long)n * a.ldb + k);
+#pragma unroll
+        for (int p = 0; p < NS; ++p) {
+          bf[u][t][p] = dk_bf16x8{};
+          if (n < a.N && j < j1) bf[u][t][p] = *(const dk_bf16x8*)(Bw + p * a.b_plane + (long long)n * a.ldb + k);
+        }
       }
     }
 #pragma unroll
     for (int u = 0; u < DKW_U; ++u)
 #pragma unroll
-      for (int t = 0; t < TN; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[u], bf[u][t], acc[t], 0, 0, 0);
+      for (int t = 0; t < TN; ++t) acc[t] = mfma_split<NS>(af[u], bf[u][t], acc[t]);
   }
   // ---- the WK waves' partial tiles, summed in a fixed order ----
 #pragma unroll
@@ -148,9 +154,10 @@ static int dkw_wk() {  // SVAE_DKW_WK: 4 (32-row blocks), 2 or 1 (128-row blocks
   return v;
 }
 static int dkw_bmr() { return 32 * (4 / dkw_wk()); }
+static int dkw_bmr(const FwdArgs& a) { return a.nsp > 1 ? 32 : dkw_bmr(); }
 
 static long long dkw_blocks(const FwdArgs& a) {
-  return (long long)((a.rows + dkw_bmr() - 1) / dkw_bmr()) * (a.N / (a.N % 64 == 0 ? 64 : 32));
+  return (long long)((a.rows + dkw_bmr(a) - 1) / dkw_bmr(a)) * (a.N / (a.N % 64 == 0 ? 64 : 32));
 }
 
 // K splits over the grid: double while the grid is short of the target, each split keeps >= mink
@@ -169,6 +176,7 @@ int dense_kw_ks(const FwdArgs& a) {
 bool dense_kw_ok(const FwdArgs& a, int groups) {
   if (dkw_disabled() || a.g.mode != GM_DENSE || groups != 1 || a.nclass != 1 || !a.Bh) return false;
   if (a.Cin % 16 || a.N % 32 || a.lda % 8 || a.ldb % 8 || a.rows < 1) return false;
+  if (a.nsp > 1) return !a.a_bf16 && (dense_kw_ks(a) > 1 || !a.bw.pre);  // the split kernel: every FC shape
   if (dense_kw_ks(a) > 1) return true;
   // unsplit: only where the grid fills the chip and the per-wave K chain is short; the fused
   // backward-BN terms live in splitk_reduce only
@@ -181,16 +189,19 @@ int dense_kw_rpb(const FwdArgs& a) { return (long long)((a.N + 63) / 64) * ((a.r
 
 int dense_kw_nrb(const FwdArgs& a) {
   if (dense_kw_ks(a) > 1) return (a.rows + dense_kw_rpb(a) - 1) / dense_kw_rpb(a);
-  return (a.rows + dkw_bmr() - 1) / dkw_bmr();
+  return (a.rows + dkw_bmr(a) - 1) / dkw_bmr(a);
 }
 
 int dense_kw(const FwdArgs& a, int ks, hipStream_t s) {
   const int tn = a.N % 64 == 0 ? 2 : 1, wk = dkw_wk();
-  const dim3 grid((a.rows + dkw_bmr() - 1) / dkw_bmr(), a.N / (32 * tn), ks);
+  const dim3 grid((a.rows + dkw_bmr(a) - 1) / dkw_bmr(a), a.N / (32 * tn), ks);
 #define DKW_L(TN_, WK_)                                                                         \
   if (a.a_bf16) hipLaunchKernelGGL((dense_kw_kernel<TN_, true, WK_>), grid, dim3(256), 0, s, a); \
   else hipLaunchKernelGGL((dense_kw_kernel<TN_, false, WK_>), grid, dim3(256), 0, s, a);
-  if (tn == 2) {
+  if (a.nsp > 1) {  // split-bf16 planes: fp32 A, 32-row blocks with K over the waves
+    if (tn == 2) hipLaunchKernelGGL((dense_kw_kernel<2, false, 4, 3>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((dense_kw_kernel<1, false, 4, 3>), grid, dim3(256), 0, s, a);
+  } else if (tn == 2) {
     if (wk == 4) { DKW_L(2, 4) } else if (wk == 2) { DKW_L(2, 2) } else { DKW_L(2, 1) }
   } else {
     if (wk == 4) { DKW_L(1, 4) } else if (wk == 2) { DKW_L(1, 2) } else { DKW_L(1, 1) }

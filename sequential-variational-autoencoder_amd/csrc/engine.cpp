@@ -78,6 +78,15 @@ struct Geo {
   bool interm;
   float c_first, prior, clipv, lo, hi, minh, maxh;
   bool bf16;
+  // dtype = 2 (bf16x6): the fp32-accurate mode on bf16 MFMA.  bf16 is set too (shadows, the bf16
+  // kernel families); split = operands as bf16 planes (opload.h split8): 3 planes / 6 products in the
+  // gather-GEMMs (forward, input gradients), 2 planes / 3 products in the weight-GEMMs; fp32 storage
+  // everywhere; shapes without a split kernel run the fp32 kernels
+  bool split;
+  // external generator (c_pixelvae, generator_pixelcnn sequential_vae.py:535, :1943-1971): steps
+  // t >= Te run the caller's generator (the PixelCNN++ head); the engine runs their recognition
+  // (z_t, KL_t) only and takes d loss / d x_hat_{Te-1} and d loss / d z_t back (svae_set_external_grads)
+  int Te;
   bool share_theta, share_phi;
   bool plc, plc_reg;          // predict_latent_code (+ _with_regularization)
   unsigned long long unreg;   // steps without a KL term
@@ -128,10 +137,23 @@ bool make_geo(const svae_config* c, Geo& g, std::string& err) {
   g.clipv = c->latent_mean_clip;
   g.lo = c->range_lo; g.hi = c->range_hi;
   g.minh = c->min_highway; g.maxh = c->max_highway;
-  if (c->dtype != 0 && c->dtype != 1) { err = "dtype must be 0 (fp32) or 1 (bf16 MFMA)"; return false; }
-  g.bf16 = c->dtype == 1;
+  if (c->dtype < 0 || c->dtype > 2) { err = "dtype must be 0 (fp32), 1 (bf16 MFMA) or 2 (bf16x6 split)"; return false; }
+  g.bf16 = c->dtype == 1 || c->dtype == 2;
+  g.split = c->dtype == 2;
   g.share_theta = c->share_theta != 0;
   g.share_phi = c->share_phi != 0;
+  g.Te = g.T;
+  if (c->external_generator_from != 0) {
+    if (c->external_generator_from < 1 || c->external_generator_from >= g.T) {
+      err = "external_generator_from must be in [1, mc_steps)";
+      return false;
+    }
+    if (c->predict_latent_code || c->add_noise_to_chain || c->add_improvement_maximization_loss) {
+      err = "external_generator_from: no Latent InfoMax / chain noise / improvement loss";
+      return false;
+    }
+    g.Te = c->external_generator_from;
+  }
   g.plc = c->predict_latent_code != 0;
   g.plc_reg = c->predict_latent_code_with_regularization != 0;
   g.unreg = (unsigned long long)c->unregularized_steps_mask[0] | ((unsigned long long)c->unregularized_steps_mask[1] << 32);
@@ -337,7 +359,8 @@ struct Model {
       h.src_level = L - 2;
       sc.fc(h.nin, h.d, h.wm, h.bm);
       sc.fc(h.nin, h.d, h.ws, h.bs);
-      // theta/generative_encoder_step_t  (:1764-1775)
+      // theta/generative_encoder_step_t  (:1764-1775); steps t >= Te have no encoder / generator here
+      if (t >= g.Te) continue;
       if (t >= 1) {
         Scope se{"theta/generative_encoder_step_" + std::to_string(t), &descs, R_THETA, t};
         EncStep& E = enc[t];
@@ -556,6 +579,10 @@ struct svae_ctx {
   double* sd_part = nullptr;
   float *dseed = nullptr, *imp_img = nullptr, *kl_zero = nullptr;
   bool imp_pass = false;             // svae_backward_imp: seeds from the improvement loss only
+  // external generator steps (Geo::Te < T): the caller's d loss / d x_hat_{Te-1} [B,H,W,C] and
+  // d loss / d z [T,B,Dz] (rows t >= Te) for the next backward (svae_set_external_grads, one-shot)
+  const float* ext_dx = nullptr;
+  const float* ext_dz = nullptr;
   // bf16 mode: BN-backward outputs (dpre) stored as bf16 -- their only consumers, the dgrad and
   // wgrad GEMMs, round them identically while staging (opload.h)
   int dbf = 0;
@@ -566,7 +593,9 @@ struct svae_ctx {
   // instance of a pass, handed out in launch order and zeroed once per pass (acc_reset)
   u64* bnacc = nullptr;
   long long bnacc_cap = 0, bnacc_used = 0, bnacc_hw = -1;
-  void *wN = nullptr, *wT = nullptr;   // bf16 weight shadows (dtype=1)
+  void *wN = nullptr, *wT = nullptr;   // bf16 weight shadows (dtype=1; dtype=2: nsp planes of wplane elements each)
+  int nsp = 1;                         // shadow planes (3 in the split mode)
+  long long wplane = 0;
   void *tiles_d = nullptr, *offs_d = nullptr;
   int ntiles = 0;
   std::vector<long long> tile_off;  // tiles sorted by tensor offset: each tile's tensor offset
@@ -773,6 +802,21 @@ static bool trace_gemm() {
   return v;
 }
 static int gemm(svae_ctx* c, FwdArgs a, int groups) {
+  if (c->m.g.split && a.Bh) {
+    a.nsp = 3;
+    a.b_plane = c->wplane;
+    a.part = c->slab;
+    a.part_cap = c->slab_cap;
+    if (!igemm_split_ok(a, groups)) {  // no split kernel for this shape: the fp32 kernels
+      a.Bh = nullptr;
+      a.nsp = 0;
+      a.ldb = a.b_nk ? a.Cin : a.N;  // the fp32 weight's own layout (TF [tap][k][n] or [tap][n][k])
+      a.bw = BwStat{};                // (conv_dgrad fused the BN partials only where a split kernel runs)
+      a.ksplit = 1;
+      igemm_fwd(a, groups, c->st);
+      return 0;
+    }
+  }
   if (c->m.g.bf16 && a.Bh && trace_gemm()) {
     a.part = c->slab;
     a.part_cap = c->slab_cap;
@@ -812,6 +856,15 @@ static int gemm(svae_ctx* c, FwdArgs a, int groups) {
 }
 // stats row-blocks the GEMM will use (accumulator sharding)
 static int gemm_nrb(svae_ctx* c, FwdArgs a, int groups) {
+  if (c->m.g.split && a.Bh) {
+    a.nsp = 3;
+    a.part = c->slab;
+    a.part_cap = c->slab_cap;
+    if (!igemm_split_ok(a, groups)) {
+      a.Bh = nullptr;
+      return nrb_of(a);
+    }
+  }
   if (c->m.g.bf16 && a.Bh) {
     a.part = c->slab;
     a.part_cap = c->slab_cap;
@@ -820,7 +873,7 @@ static int gemm_nrb(svae_ctx* c, FwdArgs a, int groups) {
   return nrb_of(a);
 }
 static void wgemm(svae_ctx* c, const WgArgs& w, int groups) {
-  if (!c->m.g.bf16) {
+  if (!c->m.g.bf16 || c->m.g.split) {  // (split mode: the tap-merged bf16 kernel has no split form)
     wgrad(w, groups, c->st);
     return;
   }
@@ -912,14 +965,15 @@ static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, V
     w.g.Ho = w.g.Wo = L.hin;
     w.rows = B * L.hin * L.hin;
   }
+  w.nsp = c->m.g.split ? 2 : 1;
   if (c->m.g.bf16 && c->wg_path == 2 && wgrad_halo2_ok(w)) {  // stride 1 / 2: compile-time-geometry kernel
     hipEvent_t* ev = nullptr;
     if (c->probe.kid != KID_NONE)
-      ev = probe_pair(c, w.g.stride == 1 ? KID_WHALO2_S1 : KID_WHALO_32_S2, 2.0 * 16 * (double)w.M * w.N * w.rows * groups);
-    wgrad_halo2(w, groups, c->slab, c->slab_cap, dW, w_gs, c->st, ev ? ev[1] : nullptr);
-    return 0;
+      ev = probe_pair(c, w.g.stride == 1 ? KID_WHALO2_S1 : KID_WHALO2_S2, 2.0 * 16 * (double)w.M * w.N * w.rows * groups);
+    if (wgrad_halo2(w, groups, c->slab, c->slab_cap, dW, w_gs, c->st, ev ? ev[1] : nullptr)) return 0;
   }
-  if (c->m.g.bf16 && c->wg_path != 0 && wgrad_halo_enabled()) {
+  const bool bfk = c->m.g.bf16 && !c->m.g.split;  // plain-bf16 weight-GEMM kernels
+  if (bfk && c->wg_path != 0 && wgrad_halo_enabled()) {
     WHaloPlanOut pl;
     if (wgrad_halo_plan(w, groups, &pl)) {
       // pixel chunks split over blocks: ~1024 blocks in flight, slab within capacity
@@ -950,8 +1004,8 @@ static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, V
     }
   }
   // image-space stride-2 conv with Cin <= 3: im2col in LDS, MFMA over pixel chunks
-  if (c->m.g.bf16 && wgrad_smallc(w, groups, c->slab, c->slab_cap, dW, w_gs, c->st)) return 0;
-  if (c->m.g.bf16)  // tap-merged tiles; longer splits (less slab traffic)
+  if (bfk && wgrad_smallc(w, groups, c->slab, c->slab_cap, dW, w_gs, c->st)) return 0;
+  if (bfk)  // tap-merged tiles; longer splits (less slab traffic)
     choose_split(w.rows, 1, wgrad_bf16_tiles(w), groups, 16LL * w.M * w.N, c->slab_cap, w.nsplit, w.chunk, 2048,
                  256);
   else
@@ -996,7 +1050,7 @@ static int conv_dgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, c
   if (fu) fu->used = false;
   const int B = c->m.g.B;
   const float* W = c->P + L.ow;
-  if (L.cin % 4 != 0 && c->m.g.bf16 && L.cout % 32 == 0 && !L.tr) {
+  if (L.cin % 4 != 0 && c->m.g.bf16 && !c->m.g.split && L.cout % 32 == 0 && !L.tr) {
     // layer-0 conv input gradient (N = image channels): bf16 halo gather (CONVT mode from dpre)
     FwdArgs a{};
     a.A = dpre; a.a_gs = dpre_gs; a.lda = L.cout; a.a_bf16 = dpre_bf(c, L);
@@ -1046,7 +1100,10 @@ static int conv_dgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, c
       const char* v = getenv("SVAE_NO_BWFUSE");
       return (v && v[0] == '1') ? 1 : 0;
     }();
-    if (fu && fu->bw.pre && fu->bw.C % 4 == 0 && !nofuse) {
+    FwdArgs sa = a;  // split mode: the fused partials need the split kernel (the fp32 one has none)
+    sa.nsp = 3;
+    const bool fuse_ok = !c->m.g.split || igemm_split_ok(sa, groups);
+    if (fu && fu->bw.pre && fu->bw.C % 4 == 0 && !nofuse && fuse_ok) {
       a.bw = fu->bw;
       const AccR acc = acc_bn(c, groups, fu->bw.C, gemm_nrb(c, a, groups));
       if (!acc.p) return fail(c, SVAE_EBADARG, "BN accumulator arena too small");
@@ -1215,8 +1272,8 @@ static void pack_out_all(svae_ctx* c, hipStream_t st) {
   if (pack_step_mode()) return;
   const Model& M = c->m;
   const Geo& g = M.g;
-  for (int t0 = 0; t0 < g.T; t0 += PACK_MAXT) {
-    const int nt = std::min(PACK_MAXT, g.T - t0);
+  for (int t0 = 0; t0 < g.Te; t0 += PACK_MAXT) {
+    const int nt = std::min(PACK_MAXT, g.Te - t0);
     PackOutArgs a{};
     a.P = c->P;
     a.C = g.C;
@@ -1229,7 +1286,7 @@ static void pack_out_all(svae_ctx* c, hipStream_t st) {
       a.owratio[i] = t >= 1 ? G.owratio : -1;
       a.obratio[i] = t >= 1 ? G.obratio : -1;
       a.wpack[i] = c->sb[t].wpack;
-      a.wpack_h[i] = g.bf16 ? (__bf16*)c->sb[t].wpack_h : nullptr;
+      a.wpack_h[i] = (g.bf16 && !g.split) ? (__bf16*)c->sb[t].wpack_h : nullptr;
     }
     pack_out(a, nt, st);
   }
@@ -1347,7 +1404,7 @@ static int engine_forward(svae_ctx* c) {
   if (M.shared) share_broadcast(c->Ppub, c->Pv, c->share_seg, c->share_nseg, st);
   // the shadows are current when the last Adam updates covered the whole live region
   if (g.bf16 && !(c->fresh == M.n_live && !M.shared))
-    shadow_weights(c->P, c->wN, c->wT, M.n_live, c->tiles_d, c->ntiles, c->offs_d, st);
+    shadow_weights(c->P, c->wN, c->wT, M.n_live, c->tiles_d, c->ntiles, c->offs_d, c->nsp, c->wplane, st);
   c->fresh = 0;
   if (g.noisy) {  // chain noise N(0,1) [T,B,H,W,C] (tf.random_normal(image_batch_shape), :1090)
     const long long n = (long long)T * B * g.H * g.W * g.C;
@@ -1393,7 +1450,7 @@ static int engine_forward(svae_ctx* c) {
   if (sfc_side) {
     hipEventRecord(c->ev_aux, st);
     hipStreamWaitEvent(c->st3, c->ev_aux, 0);
-    for (int t = 0; t < T; ++t) {
+    for (int t = 0; t < g.Te; ++t) {
       split_latent_fwd(c, t, c->st3);
       hipEventRecord(c->ev_sfc[t], c->st3);
     }
@@ -1404,6 +1461,11 @@ static int engine_forward(svae_ctx* c) {
   // ---------------- the chain ----------------
   for (int t = 0; t < T; ++t) {
     svae_ctx::StepBufs& s = c->sb[t];
+    if (t >= g.Te) {  // external generator step: only its KL statistics here (recon 0: the caller's)
+      HIPCHK(c, hipMemsetAsync(s.rec_part, 0, (size_t)B * c->out_nblk * sizeof(float), st));
+      loss_reduce(s.rec_part, c->out_nblk, c->kl_img + (long long)t * B, B, g.H * g.W * g.C, s.stats, s.rec_img, st);
+      continue;
+    }
     const GenStep& G = M.gen[t];
     const float* xprev = t >= 1 ? chain_x(c, t - 1) : nullptr;
     if (g.plc && t >= 1 && !c->generative)  // Latent InfoMax: z_t from the previous sample (:1014-1015)
@@ -1466,10 +1528,10 @@ static int engine_forward(svae_ctx* c) {
           HIPCHK(c, hipMemcpy2DAsync(s.wpack + g.C * F1, (size_t)C1 * F1 * sizeof(float), c->P + G.owratio,
                                      (size_t)F1 * sizeof(float), (size_t)F1 * sizeof(float), 16,
                                      hipMemcpyDeviceToDevice, st));
-        if (g.bf16) shadow_weights(s.wpack, s.wpack_h, nullptr, 16LL * C1 * F1, nullptr, 0, nullptr, st);
+        if (g.bf16 && !g.split) shadow_weights(s.wpack, s.wpack_h, nullptr, 16LL * C1 * F1, nullptr, 0, nullptr, 1, 0, st);
       }
       ConvGeom og{GM_CONVT, B, S[1], S[1], g.H, g.W, 2, 1, 4};
-      if (g.bf16) {  // bf16 halo gather-GEMM, N = C+1 of one 32-column tile, bias in the epilogue
+      if (g.bf16 && !g.split) {  // bf16 halo gather-GEMM, N = C+1 of one 32-column tile, bias in the epilogue
         FwdArgs a{};
         a.A = cur.p; a.lda = F1; a.a_bf16 = cur.bf;
         a.Bh = s.wpack_h; a.b_nk = 1; a.ldb = F1; a.b_tap = (long long)C1 * F1;
@@ -1593,7 +1655,12 @@ static int engine_backward(svae_ctx* c) {
 
   if ((r = acc_reset(c))) return r;
   HIPCHK(c, hipMemsetAsync(c->dz, 0, (size_t)T * B * g.Dz * sizeof(float), st));
-  const bool rec_ov = c->side && c->st4 && c->rec_group > 0 && !g.plc;
+  if (g.Te < T && c->ext_dz) {  // d loss / d z_t of the external generator's steps (t >= Te)
+    const long long off = (long long)g.Te * B * g.Dz;
+    HIPCHK(c, hipMemcpyAsync(c->dz + off, c->ext_dz + off, (size_t)((long long)T * B * g.Dz - off) * sizeof(float),
+                             hipMemcpyDeviceToDevice, st));
+  }
+  const bool rec_ov = c->side && c->st4 && c->rec_group > 0 && !g.plc && g.Te == T;
   if (rec_ov) {  // st4 starts after the forward and the accumulator / dz zeroing
     hipEventRecord(c->ev_start, st);
     hipStreamWaitEvent(c->st4, c->ev_start, 0);
@@ -1607,8 +1674,8 @@ static int engine_backward(svae_ctx* c) {
     // the previous pass's readers were joined into this stream: every per-pass region is free
     c->dpre_off = c->idpre_off = c->dcat_off = c->dtop_off = 0;
   }
-  for (int t = T - 1; t >= 0; --t) {
-    if (t < T - 1) {
+  for (int t = g.Te - 1; t >= 0; --t) {
+    if (t < g.Te - 1) {
       if (g.plc) {  // q(z_{t+1} | x_t): its weights' gradients and its share of d loss / d x_t
         r = inference_bwd(c, t + 1, 1, View{(float*)chain_x(c, t), g.C, 0}, c->dx[t & 1]);
         if (r) return r;
@@ -1619,7 +1686,9 @@ static int engine_backward(svae_ctx* c) {
     svae_ctx::StepBufs& s = c->sb[t];
     const GenStep& G = M.gen[t];
     const float* xprev = t >= 1 ? chain_x(c, t - 1) : nullptr;
-    const float* dxin = t < T - 1 ? c->dx[t & 1] : nullptr;  // d loss / d training_samples[t]
+    // d loss / d training_samples[t]: from step t+1's backward, or for the last internal step from
+    // the external generator (svae_set_external_grads)
+    const float* dxin = t < g.Te - 1 ? c->dx[t & 1] : (g.Te < T ? c->ext_dx : nullptr);
     float* dxout = t >= 1 ? c->dx[(t - 1) & 1] : nullptr;
     const float cf = t == 0 ? g.c_first : 1.f;
     float rec_coef = (g.interm || t == T - 1) ? 16.f * cf / (float)(P0 * g.C) : 0.f;
@@ -1660,14 +1729,15 @@ static int engine_backward(svae_ctx* c) {
       w.g = ConvGeom{GM_CONV, B, g.H, g.W, S[1], S[1], 2, 1, 4};
       w.ntap = 16;
       w.rows = B * S[1] * S[1];
-      if (g.bf16)
+      const bool bfk = g.bf16 && !g.split;  // (split mode: the fp32 weight-GEMM)
+      if (bfk)
         choose_split(w.rows, 1, wgrad_bf16_tiles(w), 1, 16LL * M_out * F[1], c->slab_cap, w.nsplit, w.chunk, 2048,
                      256);
       else
         choose_split(w.rows, 16, (F[1] + 127) / 128, 1, 16LL * M_out * F[1], c->slab_cap, w.nsplit, w.chunk);
       on_side(c, c->ev_da_ready, nullptr, [&] {
         w.part = c->slab;
-        const int ns = g.bf16 ? wgrad_smallc_part(w, 1, c->slab, c->slab_cap, c->st) : 0;
+        const int ns = bfk ? wgrad_smallc_part(w, 1, c->slab, c->slab_cap, c->st) : 0;
         if (ns) w.nsplit = ns;  // LDS im2col kernel (wgrad_smallc.hip)
         else wgemm(c, w, 1);
         wgrad_reduce(c->slab, 0, w.nsplit, 16, M_out, F[1], c->Gr + G.owout, 0, g.C,
@@ -2096,9 +2166,9 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
   }
   {
     const char* v = getenv("SVAE_DPRE_F32");  // A/B: keep the BN-backward outputs in fp32
-    c->dbf = (c->m.g.bf16 && !(v && v[0] == '1')) ? 1 : 0;
+    c->dbf = (c->m.g.bf16 && !c->m.g.split && !(v && v[0] == '1')) ? 1 : 0;
     const char* va = getenv("SVAE_ACT_F32");  // A/B: keep every activation in fp32
-    c->abf = (c->m.g.bf16 && !(va && va[0] == '1')) ? 1 : 0;
+    c->abf = (c->m.g.bf16 && !c->m.g.split && !(va && va[0] == '1')) ? 1 : 0;
   }
   c->counting = true;
   c->arena_used = 0;
@@ -2158,13 +2228,17 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
   }
   if (c->m.g.bf16) {
     // bf16 shadows of the live region + the per-tap transpose tile table of every GEMM weight
-    e = hipMalloc(&c->wN, (size_t)nl * 2);
-    if (e == hipSuccess) e = hipMalloc(&c->wT, (size_t)nl * 2);
+    // split mode: three planes (hi / mid / lo, opload.h split8) of wplane elements each
+    c->nsp = c->m.g.split ? 3 : 1;
+    c->wplane = ((long long)nl + 127) / 128 * 128;
+    const size_t sbytes = (size_t)c->nsp * c->wplane * 2;
+    e = hipMalloc(&c->wN, sbytes);
+    if (e == hipSuccess) e = hipMalloc(&c->wT, sbytes);
     if (e != hipSuccess) {
       svae_destroy(c);
       return fail(nullptr, SVAE_ENOMEM, std::string("hipMalloc shadows: ") + hipGetErrorString(e));
     }
-    hipMemset(c->wT, 0, (size_t)nl * 2);
+    hipMemset(c->wT, 0, sbytes);
     std::vector<long long> offs;
     std::vector<int> tiles;
     struct TT { long long off; int taps, R, Cc; };
@@ -2179,9 +2253,11 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
     for (int t = 0; t < g.T; ++t) {
       for (int l = 0; l < g.L - 1; ++l) {
         conv(c->m.inf[t].a[l]); conv(c->m.inf[t].b[l]);
+        if (t >= g.Te) continue;
         conv(c->m.gen[t].s2[l]); conv(c->m.gen[t].s1[l]);
         if (t >= 1) { conv(c->m.enc[t].a[l]); conv(c->m.enc[t].b[l]); }
       }
+      if (t >= g.Te) continue;
       if (t >= 1) { conv(c->m.enc[t].c); add(c->m.enc[t].fc.ow, 1, c->m.enc[t].fc.nin, c->m.enc[t].fc.nout); }
       add(c->m.gen[t].top.ow, 1, c->m.gen[t].top.nin, c->m.gen[t].top.nout);
     }
@@ -2344,6 +2420,7 @@ int svae_forward(svae_ctx* c, const float* x, const float* target, const float* 
   for (int t = 0; t < g.T; ++t) c->reg_host[t] = reg_coeff * (t == 0 ? g.c_first : 1.f) * g.kl_on(t) / (float)g.B;
   set_small(c->kl_coef, c->reg_host, g.T, c->st);
   int r = engine_forward(c);
+  c->noise_in = nullptr;  // one-shot (svae_set_chain_noise); the backward reads noise_used
   if (r) return r;
   HIPCHK(c, hipGetLastError());
   return 0;
@@ -2361,8 +2438,18 @@ int svae_generate(svae_ctx* c, const float* z, void* stream) {
   c->reg = 1.f;  // the generative chain's noise uses reg_coeff's default (placeholder_with_default 1.0, :917)
   const int r = engine_forward(c);
   c->generative = false;
+  // injected chain noise is one-shot: the next call draws its own (tf.random_normal, :1090-1091)
+  c->noise_in = nullptr;
   if (r) return r;
   HIPCHK(c, hipGetLastError());
+  return 0;
+}
+
+int svae_set_external_grads(svae_ctx* c, const float* dxhat, const float* dz) {
+  if (!c) return fail(c, SVAE_EBADARG, "null ctx");
+  if (c->m.g.Te == c->m.g.T && (dxhat || dz)) return fail(c, SVAE_EBADARG, "external_generator_from is off");
+  c->ext_dx = dxhat;
+  c->ext_dz = dz;
   return 0;
 }
 
@@ -2370,6 +2457,7 @@ int svae_backward(svae_ctx* c, void* stream) {
   if (!c || !c->x_in) return fail(c, SVAE_EBADARG, "svae_forward must run first");
   c->st = (hipStream_t)stream;
   int r = engine_backward(c);
+  c->ext_dx = c->ext_dz = nullptr;  // one-shot
   if (c->side) {  // join: the side stream's weight gradients are ordered before later caller work
     hipEventRecord(c->ev_join, c->st2);
     hipStreamWaitEvent(c->st, c->ev_join, 0);
@@ -2460,11 +2548,11 @@ static void adam_range(svae_ctx* c, long long lo, long long hi, float lr, long l
   const double lr_t = lr * std::sqrt(1.0 - std::pow(b2, (double)step)) / (1.0 - std::pow(b1, (double)step));
   const bool sh = c->m.g.bf16 && !c->m.shared && c->wN;
   adam_step(c->Ppub + lo, c->Gpub + lo, c->adam_m + lo, c->adam_v + lo, sh ? (void*)((__bf16*)c->wN + lo) : nullptr,
-            hi - lo, (float)lr_t, (float)b1, (float)b2, 1e-8f, clip, s);
+            hi - lo, (float)lr_t, (float)b1, (float)b2, 1e-8f, clip, c->nsp, c->wplane, s);
   if (sh) {
     const long long tb = std::lower_bound(c->tile_off.begin(), c->tile_off.end(), lo) - c->tile_off.begin();
     const long long te = std::lower_bound(c->tile_off.begin(), c->tile_off.end(), hi) - c->tile_off.begin();
-    shadow_t_tiles(c->Ppub, c->wT, (const int*)c->tiles_d + 4 * tb, (int)(te - tb), c->offs_d, s);
+    shadow_t_tiles(c->Ppub, c->wT, (const int*)c->tiles_d + 4 * tb, (int)(te - tb), c->offs_d, c->nsp, c->wplane, s);
     c->fresh += hi - lo;
   }
 }

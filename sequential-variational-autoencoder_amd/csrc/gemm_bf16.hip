@@ -1088,21 +1088,33 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
 // ---------------------------------------------------------------------------
 // bf16 weight shadows: N = plain conversion; T = per-tap transpose of [rows][cols]
 // ---------------------------------------------------------------------------
-__global__ void shadow_n_kernel(const float* w, __bf16* out, long long n) {
+// split mode (nsp planes): plane p holds bf16(w - sum of the earlier planes) (opload.h split4)
+__global__ void shadow_n_kernel(const float* w, __bf16* out, long long n, int nsp, long long plane) {
   for (long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n;
        i += (long long)gridDim.x * blockDim.x * 4) {
     if (i + 3 < n) {
       f32x4 v = *(const f32x4*)(w + i);
-      *(bf16x4*)(out + i) = __builtin_convertvector(v, bf16x4);
+      for (int p = 0; p < nsp; ++p) {
+        const bf16x4 h = __builtin_convertvector(v, bf16x4);
+        *(bf16x4*)(out + p * plane + i) = h;
+        v = v - __builtin_convertvector(h, f32x4);
+      }
     } else {
-      for (long long j = i; j < n; ++j) out[j] = (__bf16)w[j];
+      for (long long j = i; j < n; ++j) {
+        float v = w[j];
+        for (int p = 0; p < nsp; ++p) {
+          const __bf16 h = (__bf16)v;
+          out[p * plane + j] = h;
+          v -= (float)h;
+        }
+      }
     }
   }
 }
 
 // one 32x32 tile per block; tiles enumerated by the host table (tensor, tap, r0, c0)
 __global__ __launch_bounds__(256) void shadow_t_kernel(const float* w, __bf16* out, const int4* tiles,
-                                                       const long long* offs) {
+                                                       const long long* offs, int nsp, long long plane) {
   __shared__ float t[32][33];
   const int4 d = tiles[blockIdx.x];  // x: tensor index, y: tap, z: r0, w: c0
   const long long off = offs[3 * d.x];
@@ -1117,7 +1129,14 @@ __global__ __launch_bounds__(256) void shadow_t_kernel(const float* w, __bf16* o
   __syncthreads();
   for (int i = ty; i < 32; i += 8) {
     int c = d.w + i, r = d.z + tx;
-    if (r < R && c < Cc) dst[(long long)c * R + r] = (__bf16)t[tx][i];
+    if (r < R && c < Cc) {
+      float v = t[tx][i];
+      for (int p = 0; p < nsp; ++p) {
+        const __bf16 h = (__bf16)v;
+        dst[p * plane + (long long)c * R + r] = h;
+        v -= (float)h;
+      }
+    }
   }
 }
 
@@ -1408,7 +1427,15 @@ static int pertap_plan(const FwdArgs& a, int groups, int* ksplit) {
   return (int)(((long long)a.rows * a.nclass + SKR_ROWS - 1) / SKR_ROWS);
 }
 
+bool igemm_split_ok(const FwdArgs& a, int groups) {
+  return a.Bh && !a.a_bf16 && (dense_kw_ok(a, groups) || halo_kw_plan(a, groups) > 0);
+}
+
 int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit) {
+  if (a.nsp > 1) {  // split-bf16 planes: dense_kw or halo_kw only (igemm_split_ok)
+    if (ksplit) *ksplit = 1;
+    return dense_kw_ok(a, groups) ? dense_kw_nrb(a) : halo_kw_plan(a, groups);
+  }
   if (smallc_ok(a, true)) {
     if (ksplit) *ksplit = 1;
     return smallc_nrb(a);
@@ -1450,12 +1477,14 @@ const char* kernel_name(int kid) {
       "igemm_halo_kernel<128, 64, 2, 2>", "igemm_halo_kernel<64, 64, 2, 2>",
       "igemm_halo_kernel<128, 128, 2, 2>", "igemm_halo_kernel<64, 128, 1, 4>",
       "wgrad_halo_kernel<32, 1>", "wgrad_halo_kernel<32, 2>", "wgrad_halo_kernel<64, 1>", "wgrad_halo_kernel<64, 2>",
-      "wgrad_halo2_kernel (stride-1 halo weight-GEMM, all instances)",
-      "igemm_halo_kw_kernel (small-image gather-GEMM, K split over waves, all instances)"};
+      "wgrad_halo2_kernel (stride-1 halo weight-GEMM, all S = 1 instances)",
+      "igemm_halo_kw_kernel (small-image gather-GEMM, K split over waves, all instances)",
+      "wgrad_halo2_kernel (stride-2 halo weight-GEMM, all instances)"};
   return (kid >= 0 && kid < KID_COUNT) ? names[kid] : "none";
 }
 
 int igemm_bf16_kid(const FwdArgs& a) {
+  if (a.nsp > 1) return (!dense_kw_ok(a, 1) && halo_kw_plan(a, 1) > 0) ? KID_HALO_KW : KID_NONE;
   if (!halo_disabled()) {
     const HaloPlan hp = halo_plan(a, 1);
     if (hp.ok) return (kw_first(a, hp) && halo_kw_plan(a, 1)) ? KID_HALO_KW : hp.kid;
@@ -1479,12 +1508,13 @@ int igemm_bf16(FwdArgs a, int groups, hipStream_t s, hipEvent_t after) {
 }
 
 int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t after) {
-  if (path == 2 && smallc_ok(a, true)) {
+  if (a.nsp > 1 && !igemm_split_ok(a, groups)) return -2;  // no split kernel for this shape
+  if (path == 2 && a.nsp <= 1 && smallc_ok(a, true)) {
     conv_smallc(a, groups, true, s);
     if (after) hipEventRecord(after, s);
     return smallc_nrb(a);
   }
-  if (path == 2 && smalln_ok(a)) {
+  if (path == 2 && a.nsp <= 1 && smalln_ok(a)) {
     convt_smalln(a, groups, s);
     if (after) hipEventRecord(after, s);
     return 0;  // no stats (smalln_ok requires none)
@@ -1499,6 +1529,11 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
                          a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs, a.s_sh, a.s_nsh, a.bw, rpb);
     }
     return dense_kw_nrb(a);
+  }
+  if (a.nsp > 1) {  // igemm_split_ok: the wave-split halo gather takes every other split shape
+    const int nrb = halo_kw(a, groups, s);
+    if (after) hipEventRecord(after, s);
+    return nrb;
   }
   if (path == 1 || (path == 2 && !halo_disabled())) {
     HaloPlan hp = halo_plan(a, groups);
@@ -1657,17 +1692,18 @@ void wgrad_halo(const WHaloPlanOut& pl, const WgArgs& a, int groups, hipStream_t
 }
 
 void shadow_weights(const float* w, void* wn, void* wt, long long n, const void* tiles, int ntiles, const void* offs,
-                    hipStream_t s) {
+                    int nsp, long long plane, hipStream_t s) {
   long long q = (n + 3) / 4;
   int blocks = (int)std::min<long long>((q + 255) / 256, 8192);
-  hipLaunchKernelGGL(shadow_n_kernel, dim3(blocks), dim3(256), 0, s, w, (__bf16*)wn, n);
+  hipLaunchKernelGGL(shadow_n_kernel, dim3(blocks), dim3(256), 0, s, w, (__bf16*)wn, n, nsp, plane);
   if (ntiles > 0)
     hipLaunchKernelGGL(shadow_t_kernel, dim3(ntiles), dim3(256), 0, s, w, (__bf16*)wt, (const int4*)tiles,
-                       (const long long*)offs);
+                       (const long long*)offs, nsp, plane);
 }
 
-void shadow_t_tiles(const float* w, void* wt, const void* tiles, int ntiles, const void* offs, hipStream_t s) {
+void shadow_t_tiles(const float* w, void* wt, const void* tiles, int ntiles, const void* offs, int nsp, long long plane,
+                    hipStream_t s) {
   if (ntiles > 0)
     hipLaunchKernelGGL(shadow_t_kernel, dim3(ntiles), dim3(256), 0, s, w, (__bf16*)wt, (const int4*)tiles,
-                       (const long long*)offs);
+                       (const long long*)offs, nsp, plane);
 }

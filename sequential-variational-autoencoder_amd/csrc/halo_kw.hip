@@ -52,8 +52,12 @@ __device__ __forceinline__ long long kw_out_row(const KwArgs& h, const ConvGeom&
 
 // bf16-A 32-column instances at 4 waves per SIMD (<= 128 VGPRs, no spills; was 132 -> 3 waves): +0.3 %
 // of the step in a same-box A/B (tools/gpu/r02_libab.sh); the fp32-A ones would spill
-template <int BM, int BN, bool S2T, bool ABF>
+// NS = 3: the split-bf16 mode (dtype bf16x6, opload.h split8 / mfma_split): the fp32 window is
+// staged as three bf16 planes (one LDS buffer, restaged under a second barrier per chunk) and every
+// A x B fragment pair runs the six plane products; B comes from the three shadow planes
+template <int BM, int BN, bool S2T, bool ABF, int NS = 1>
 __global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64) ? 4 : 2) void igemm_halo_kw_kernel(KwArgs h) {
+  static_assert(NS == 1 || (NS == 3 && !ABF), "split planes from fp32 activations only");
   constexpr int TM = BM / 32;
   constexpr int TN = BN / 32;
   constexpr int NTAP = S2T ? 4 : 16;
@@ -126,12 +130,22 @@ __global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64) ? 4 : 2) void ig
       if (woff[i] >= 0) ld8_raw(a.A, ac + woff[i], abf, wv[i][0], wv[i][1]);
     }
   };
+  // NS == 1: buffer `buf` of two; NS == 3: plane p of the one buffer at p * npix * KW_ROWP
   auto store_window = [&](int buf) {
     __bf16* W = ksm + buf * h.npix * KW_ROWP;
 #pragma unroll
     for (int i = 0; i < KW_PI; ++i) {
       const int it = tid + 256 * i;
-      if (woff[i] >= -1) *(bf16x8*)&W[(it >> 2) * KW_ROWP + (it & 3) * 8] = raw8_bf(wv[i][0], wv[i][1], abf);
+      if (woff[i] < -1) continue;
+      const int o = (it >> 2) * KW_ROWP + (it & 3) * 8;
+      if constexpr (NS == 1) {
+        *(bf16x8*)&W[o] = raw8_bf(wv[i][0], wv[i][1], abf);
+      } else {
+        bf16x8 pl[NS];
+        split8<NS>(wv[i][0], wv[i][1], pl);
+#pragma unroll
+        for (int p = 0; p < NS; ++p) *(bf16x8*)&ksm[p * h.npix * KW_ROWP + o] = pl[p];
+      }
     }
   };
 
@@ -149,7 +163,7 @@ __global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64) ? 4 : 2) void ig
 
   // ---- this wave's taps: t = wave * NTW + u; B fragments one chunk ahead ----
   const __bf16* bptr = Bw + (long long)(n0 + l32) * a.ldb + 8 * hh;
-  bf16x8 bq[NTW][TN][2];
+  bf16x8 bq[NTW][TN][2][NS];
   auto load_b = [&](int u, int chunk) {
     const int t = wave * NTW + u;
     const int tap = S2T ? tap0 + 8 * (t >> 1) + 2 * (t & 1) : t;
@@ -157,7 +171,10 @@ __global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64) ? 4 : 2) void ig
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
-      for (int kq = 0; kq < 2; ++kq) bq[u][tn][kq] = *(const bf16x8*)(bptr + (long long)tn * 32 * a.ldb + off + kq * 16);
+      for (int kq = 0; kq < 2; ++kq)
+#pragma unroll
+        for (int p = 0; p < NS; ++p)
+          bq[u][tn][kq][p] = *(const bf16x8*)(bptr + p * a.b_plane + (long long)tn * 32 * a.ldb + off + kq * 16);
   };
 
   f32x16 acc[TM][TN];
@@ -171,11 +188,17 @@ __global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64) ? 4 : 2) void ig
   load_window(0);
 #pragma unroll
   for (int u = 0; u < NTW; ++u) load_b(u, 0);
-  store_window(0);
-  __syncthreads();
+  if constexpr (NS == 1) {
+    store_window(0);
+    __syncthreads();
+  }
   for (int c = 0; c < nchunk; ++c) {
-    const int buf = c & 1;
+    const int buf = NS == 1 ? (c & 1) : 0;
     const bool has_next = c + 1 < nchunk;
+    if constexpr (NS > 1) {  // one buffer of NS planes: stage chunk c, then prefetch c + 1
+      store_window(0);
+      __syncthreads();
+    }
     if (has_next) load_window(c + 1);
     const __bf16* W = ksm + buf * h.npix * KW_ROWP;
 #pragma unroll
@@ -185,18 +208,21 @@ __global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64) ? 4 : 2) void ig
       const int sh = shift * KW_ROWP;
 #pragma unroll
       for (int kq = 0; kq < 2; ++kq) {
-        bf16x8 af[TM];
-#pragma unroll
-        for (int tm = 0; tm < TM; ++tm) af[tm] = *(const bf16x8*)&W[abase[tm] + sh + kq * 16];
+        bf16x8 af[TM][NS];
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-          for (int tn = 0; tn < TN; ++tn)
-            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm], bq[u][tn][kq], acc[tm][tn], 0, 0, 0);
+          for (int p = 0; p < NS; ++p) af[tm][p] = *(const bf16x8*)&W[p * h.npix * KW_ROWP + abase[tm] + sh + kq * 16];
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_split<NS>(af[tm], bq[u][tn][kq], acc[tm][tn]);
       }
       if (has_next) load_b(u, c + 1);
     }
-    if (has_next) store_window(buf ^ 1);
+    if constexpr (NS == 1) {
+      if (has_next) store_window(buf ^ 1);
+    }
     __syncthreads();
   }
 
@@ -323,13 +349,18 @@ static bool kw_plan(const FwdArgs& a, int groups, KwArgs* out, int* bm_out, int*
     h.d_q = make_fastdiv((g.Ho >> 1) * (g.Wo >> 1));
     h.d_qw = make_fastdiv(g.Wo >> 1);
     int bn = 32;
-    if (kw_bn_mode() == 64 && a.N % 64 == 0 && (long long)(a.rows / bm) * (a.N / 64) * a.nclass * groups >= 512) bn = 64;
+    if (kw_bn_mode() == 64 && a.nsp <= 1 && a.N % 64 == 0 &&
+        (long long)(a.rows / bm) * (a.N / 64) * a.nclass * groups >= 512)
+      bn = 64;
     const long long blocks = (long long)(a.rows / bm) * (a.N / bn) * a.nclass * groups;
     if (blocks < 256 && bm > 32) continue;  // the smaller tile doubles the blocks
     *out = h;
     *bm_out = bm;
     *bn_out = bn;
-    *lds_out = std::max((size_t)(2 * h.npix) * KW_ROWP * sizeof(__bf16), (size_t)4 * bm * bn * sizeof(float));
+    // NS = 1: two window buffers; NS = 3 (split planes): one buffer of three planes
+    const int wbufs = a.nsp > 1 ? 3 : 2;
+    if (a.nsp > 1 && (a.a_bf16 || bm > 64)) continue;  // split instances: fp32 A, 32 / 64-row tiles
+    *lds_out = std::max((size_t)(wbufs * h.npix) * KW_ROWP * sizeof(__bf16), (size_t)4 * bm * bn * sizeof(float));
     return true;
   }
   return false;
@@ -360,6 +391,25 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
   h.f = a;
   const bool s2t = a.g.mode == GM_CONVT && a.g.stride == 2;
   dim3 grid(a.rows / bm, a.N / bn, groups * a.nclass);
+  if (a.nsp > 1) {  // split-bf16 planes (fp32 A): 64 / 32-row tiles, 32 columns
+    static bool attr = false;
+    if (!attr) {
+      for (const void* f : {(const void*)igemm_halo_kw_kernel<64, 32, true, false, 3>,
+                            (const void*)igemm_halo_kw_kernel<64, 32, false, false, 3>,
+                            (const void*)igemm_halo_kw_kernel<32, 32, true, false, 3>,
+                            (const void*)igemm_halo_kw_kernel<32, 32, false, false, 3>})
+        hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+      attr = true;
+    }
+    if (bm == 64) {
+      if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, true, false, 3>), grid, dim3(256), lds, s, h);
+      else hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, false, false, 3>), grid, dim3(256), lds, s, h);
+    } else {
+      if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<32, 32, true, false, 3>), grid, dim3(256), lds, s, h);
+      else hipLaunchKernelGGL((igemm_halo_kw_kernel<32, 32, false, false, 3>), grid, dim3(256), lds, s, h);
+    }
+    return a.nclass * (a.rows / bm);
+  }
 #define KW_LAUNCH(BM_, BN_)                                                                                  \
   if (a.a_bf16) {                                                                                            \
     if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<BM_, BN_, true, true>), grid, dim3(256), lds, s, h);    \

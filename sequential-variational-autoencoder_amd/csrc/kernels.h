@@ -33,6 +33,9 @@ struct FwdArgs {
   float* part; long long part_cap; int ksplit; int rows_total;
   BwStat bw;    // bf16 kernels: backward-BN partials instead of forward stats (bw.pre != nullptr)
   int a_bf16;   // bf16 kernels: A is stored as bf16 (element offsets / strides unchanged; opload.h)
+  // split-bf16 mode (dtype = bf16x6, opload.h split8): A and B as nsp bf16 planes each (1 = plain
+  // bf16); B plane p at Bh + p * b_plane elements.  Only kernels that implement it accept nsp > 1
+  int nsp; long long b_plane;
 };
 
 // weight-GEMM  part[split][tap][m][n] = sum_{p in split} G[src(p,tap)][m] * D[p][n]
@@ -44,6 +47,7 @@ struct WgArgs {
   ConvGeom g;   // mode CONV or DENSE; row space = D's pixels, gathered space = G's pixels
   int rows, chunk, nsplit, ntap;
   int g_bf16, d_bf16;  // bf16 kernels: G / D stored as bf16 (opload.h)
+  int nsp;             // split-bf16 planes per operand (1 = plain bf16; 2 = the 3-product fp32-class mode)
 };
 
 // weight gradient of the 64x64 -> 32x32 stride-2 4x4 layers with <= 4 image channels (wgrad_smallc.hip):
@@ -80,7 +84,8 @@ enum KernelId {
   KID_WHALO_32_S1 = 22, KID_WHALO_32_S2 = 23, KID_WHALO_64_S1 = 24, KID_WHALO_64_S2 = 25,
   KID_WHALO2_S1 = 26,  // wgrad_halo2_kernel<...> (all instances: stride-1 halo weight-GEMM, wgrad_halo2.hip)
   KID_HALO_KW = 27,    // igemm_halo_kw_kernel<...> (all instances: small-image gather, K over waves, halo_kw.hip)
-  KID_COUNT = 28
+  KID_WHALO2_S2 = 28, // wgrad_halo2_kernel<..., S = 2> (stride-2 instances, separate from KID_WHALO_32_S2)
+  KID_COUNT = 29
 };
 const char* kernel_name(int kid);
 int igemm_bf16_kid(const FwdArgs& a);
@@ -94,6 +99,9 @@ int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit);
 // small-image halo gather-GEMM with K split over the block's waves (halo_kw.hip), used where the
 // tiled halo kernel would split K over the grid: stats row-blocks (0 = shape not eligible) / launch
 int halo_kw_plan(const FwdArgs& a, int groups);
+// the split-bf16 (nsp = 3) gather-GEMMs: does a launch of this shape have a split kernel (halo_kw,
+// dense_kw)?  Shapes without one run the fp32 kernels (igemm_fwd) in that mode.
+bool igemm_split_ok(const FwdArgs& a, int groups);
 int halo_kw(const FwdArgs& a, int groups, hipStream_t s);
 void wgrad_bf16(WgArgs a, int groups, hipStream_t s, hipEvent_t after = nullptr);  // taps merged into M (part [split][tap*M+m][n])
 int wgrad_bf16_tiles(const WgArgs& a);
@@ -122,11 +130,13 @@ int wgrad_halo2_ok(const WgArgs& w);
 int wgrad_halo2(const WgArgs& w, int groups, float* slab, long long slab_cap, float* dW, long long w_gs,
                 hipStream_t s, hipEvent_t after = nullptr);
 void wgrad_halo(const WHaloPlanOut& pl, const WgArgs& a, int groups, hipStream_t s, hipEvent_t after = nullptr);
-// bf16 weight shadows: wn = bf16(w) for [0,n); wt = per-tap transposes listed in tiles/offs
+// bf16 weight shadows: wn = bf16(w) for [0,n); wt = per-tap transposes listed in tiles/offs.
+// nsp > 1 (split mode): plane p (at p * plane elements) holds the p-th bf16 term of opload.h split8
 void shadow_weights(const float* w, void* wn, void* wt, long long n, const void* tiles, int ntiles, const void* offs,
-                    hipStream_t s);
+                    int nsp, long long plane, hipStream_t s);
 // per-tap transposed bf16 shadow of the ntiles tiles starting at `tiles` only
-void shadow_t_tiles(const float* w, void* wt, const void* tiles, int ntiles, const void* offs, hipStream_t s);
+void shadow_t_tiles(const float* w, void* wt, const void* tiles, int ntiles, const void* offs, int nsp, long long plane,
+                    hipStream_t s);
 void igemm_fwd(FwdArgs a, int groups, hipStream_t s);
 void wgrad(WgArgs a, int groups, hipStream_t s);
 void wgrad_reduce(const float* part, long long p_gs, int nsplit, int ntap, int M, int N, float* out0,
@@ -225,9 +235,10 @@ void loss_reduce(const float* rec_part, int nblk, const float* kl_img, int B, in
                  float* rec_img_out, hipStream_t s);
 
 // ---- optimizer: clip(+-c) + TF Adam (sequential_vae.py:1267-1276) ----
-// clip + TF Adam on n elements; wn != nullptr: also the bf16 copy of the updated weights
+// clip + TF Adam on n elements; wn != nullptr: also the bf16 copy of the updated weights (nsp planes
+// of the split mode at wn + p * plane)
 void adam_step(float* w, const float* g, float* m, float* v, void* wn, long long n, float lr_t, float b1, float b2,
-               float eps, float clipv, hipStream_t s);
+               float eps, float clipv, int nsp, long long plane, hipStream_t s);
 
 // ---- weight sharing (homogeneous chain): virtual per-step copies <-> public tensors ----
 // Pv[v + i] = P[p + i] for every segment {v, p, size} of seg[nseg][3]

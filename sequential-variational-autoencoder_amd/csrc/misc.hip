@@ -883,7 +883,7 @@ __device__ __forceinline__ void adam1(float& w, float g, float& m, float& v, flo
 // also writes the bf16 copy of the updated weights (the GEMMs' N-layout shadow, shadow_n_kernel's
 // rounding), which saves the next forward's separate conversion pass over the live region
 __global__ void adam_kernel(float* w, const float* g, float* m, float* v, __bf16* wn, long long n, float lr_t, float b1,
-                            float b2, float eps, float clipv) {
+                            float b2, float eps, float clipv, int nsp, long long plane) {
   const long long stride = (long long)gridDim.x * blockDim.x;
   const long long nq = n >> 2;
   for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += stride) {
@@ -900,19 +900,32 @@ __global__ void adam_kernel(float* w, const float* g, float* m, float* v, __bf16
     ((f32x4*)m)[q] = mm;
     ((f32x4*)v)[q] = vv;
     ((f32x4*)w)[q] = ww;
-    if (wn) *(bf16x4_t*)(wn + 4 * q) = __builtin_convertvector(ww, bf16x4_t);
+    if (wn) {  // the bf16 N-layout copy (split mode: nsp planes, opload.h split4)
+      for (int p = 0; p < nsp; ++p) {
+        const bf16x4_t h = __builtin_convertvector(ww, bf16x4_t);
+        *(bf16x4_t*)(wn + p * plane + 4 * q) = h;
+        ww = ww - __builtin_convertvector(h, f32x4);
+      }
+    }
   }
   for (long long i = 4 * nq + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     adam1(w[i], g[i], m[i], v[i], lr_t, b1, b2, eps, clipv);
-    if (wn) wn[i] = (__bf16)w[i];
+    if (wn) {
+      float x = w[i];
+      for (int p = 0; p < nsp; ++p) {
+        const __bf16 h = (__bf16)x;
+        wn[p * plane + i] = h;
+        x -= (float)h;
+      }
+    }
   }
 }
 
 void adam_step(float* w, const float* g, float* m, float* v, void* wn, long long n, float lr_t, float b1, float b2,
-               float eps, float clipv, hipStream_t s) {
+               float eps, float clipv, int nsp, long long plane, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(adam_kernel, dim3(ew_blocks((n + 3) / 4, 256, 8192)), dim3(256), 0, s, w, g, m, v, (__bf16*)wn,
-                     n, lr_t, b1, b2, eps, clipv);
+                     n, lr_t, b1, b2, eps, clipv, nsp, plane);
 }
 
 __global__ void bf16_to_f32_kernel(const __bf16* src, float* dst, long long n) {

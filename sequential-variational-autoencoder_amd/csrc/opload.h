@@ -55,3 +55,42 @@ __device__ __forceinline__ float raw4_elem(f32x4 v, int e, bool bf) {
 __device__ __forceinline__ float ld1(const void* base, long long off, bool bf) {
   return bf ? (float)((const __bf16*)base)[off] : ((const float*)base)[off];
 }
+
+// ---- split-bf16 operands (dtype = bf16x6: the fp32-accurate mode on bf16 MFMA) ----
+// x = p0 + p1 + p2 + r with p0 = bf16(x), p1 = bf16(x - p0), p2 = bf16(x - p0 - p1) (RNE each; every
+// residual is exact in fp32), |r| <= 2^-27 |x| roughly.  A product a*b is then summed from the
+// plane products down to order 2^-18 |ab|:
+//   NS = 2:  a0 b0 + a0 b1 + a1 b0                         (3 MFMAs, ~2^-17 relative per product)
+//   NS = 3:  a0 b0 + a0 b1 + a1 b0 + a0 b2 + a2 b0 + a1 b1  (6 MFMAs, below fp32 rounding)
+// with fp32 accumulation, so a split GEMM is an fp32 GEMM to within fp32 summation error.
+template <int NS>
+__device__ __forceinline__ void split8(f32x4 lo, f32x4 hi, ol_bf16x8 (&p)[NS]) {
+  ol_f32x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    p[s] = __builtin_convertvector(v, ol_bf16x8);
+    if (s + 1 < NS) v = v - __builtin_convertvector(p[s], ol_f32x8);
+  }
+}
+template <int NS>
+__device__ __forceinline__ void split4(f32x4 x, ol_bf16x4 (&p)[NS]) {
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    p[s] = __builtin_convertvector(x, ol_bf16x4);
+    if (s + 1 < NS) x = x - __builtin_convertvector(p[s], f32x4);
+  }
+}
+template <int NS>
+__device__ __forceinline__ f32x16 mfma_split(const ol_bf16x8 (&a)[NS], const ol_bf16x8 (&b)[NS], f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+  if constexpr (NS >= 2) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
+  }
+  if constexpr (NS >= 3) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
+  }
+  return acc;
+}

@@ -776,6 +776,102 @@ __global__ void sample_kernel(const float* __restrict__ l, const float* __restri
   o[2] = x2;
 }
 
+// d sample / d l (the reparameterised logistic draw of sample_kernel, nn.py:89-109): the selected
+// component's mean, log-scale (unless clamped at -7: tf.maximum routes the gradient to the
+// argument where it is >= -7) and tanh coefficients; the clip to [-1, 1] passes the gradient where
+// its argument lies inside (tf.minimum / tf.maximum tie rules, both bounds inclusive).  The mixture
+// indicator is piecewise constant: no gradient to the logits.  dl [pixels][10 M] is overwritten.
+__global__ void sample_bwd_kernel(const float* __restrict__ l, const float* __restrict__ u_mix,
+                                  const float* __restrict__ u_log, long long npix, int M,
+                                  const float* __restrict__ dx, int dx_stride, float* __restrict__ dl) {
+  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npix) return;
+  const float* lp = l + p * 10 * M;
+  float* dp = dl + p * 10 * M;
+  for (int j = 0; j < 10 * M; ++j) dp[j] = 0.f;
+  int sel = 0;
+  float best = -INFINITY;
+  for (int j = 0; j < M; ++j) {
+    const float v = lp[j] - logf(-logf(u_mix[p * M + j]));
+    if (v > best) {
+      best = v;
+      sel = j;
+    }
+  }
+  float xs[3], co[3], es[3], lg[3], lsr[3];
+  for (int c = 0; c < 3; ++c) {
+    const float* pc = lp + M + c * 3 * M;
+    const float u = u_log[p * 3 + c];
+    lsr[c] = pc[M + sel];
+    es[c] = expf(fmaxf(lsr[c], -7.f));
+    lg[c] = logf(u) - logf(1.f - u);
+    xs[c] = pc[sel] + es[c] * lg[c];
+    co[c] = tanhf(pc[2 * M + sel]);
+  }
+  const float v0 = xs[0];
+  const float x0 = fminf(fmaxf(v0, -1.f), 1.f);
+  const float v1 = xs[1] + co[0] * x0;
+  const float x1 = fminf(fmaxf(v1, -1.f), 1.f);
+  const float v2 = xs[2] + co[1] * x0 + co[2] * x1;
+  const float* g = dx + p * dx_stride;
+  auto in = [](float v) { return (v >= -1.f && v <= 1.f) ? 1.f : 0.f; };
+  const float g2 = g[2] * in(v2);
+  float gx1 = g[1] + g2 * co[2];
+  const float g1 = gx1 * in(v1);
+  float gx0 = g[0] + g2 * co[1] + g1 * co[0];
+  const float g0 = gx0 * in(v0);
+  const float gv[3] = {g0, g1, g2};
+  const float dco[3] = {g1 * x0, g2 * x0, g2 * x1};
+  for (int c = 0; c < 3; ++c) {
+    float* dc = dp + M + c * 3 * M;
+    dc[sel] = gv[c];                                                   // d mean
+    dc[M + sel] = lsr[c] >= -7.f ? gv[c] * es[c] * lg[c] : 0.f;         // d log_scale
+    dc[2 * M + sel] = dco[c] * (1.f - co[c] * co[c]);                   // d coeff (tanh')
+  }
+}
+
+// highway backward (pixelvae.py:135-137): ds = r dout; dprev (+)= (1 - r) dout;
+// dz[img] = sum_i dout (s - prev) * (hi - lo) sigmoid'(z + zb).  One block per image (fixed order).
+__global__ __launch_bounds__(256) void highway_bwd_kernel(const float* __restrict__ s, const float* __restrict__ prev,
+                                                          const float* __restrict__ z, const float* __restrict__ zb,
+                                                          long long per_img, float lo, float hi,
+                                                          const float* __restrict__ dout, float* __restrict__ ds,
+                                                          float* __restrict__ dprev, int prev_acc,
+                                                          float* __restrict__ dz) {
+  __shared__ float red[256];
+  const int b = blockIdx.x;
+  const float zz = z[b] + (zb ? zb[0] : 0.f);
+  const float sg = sigm(zz);
+  const float r = lo + (hi - lo) * sg;
+  const long long o = (long long)b * per_img;
+  float acc = 0.f;
+  for (long long i = threadIdx.x; i < per_img; i += 256) {
+    const float d = dout[o + i];
+    if (ds) ds[o + i] = r * d;
+    if (dprev) dprev[o + i] = (prev_acc ? dprev[o + i] : 0.f) + (1.f - r) * d;
+    acc += d * (s[o + i] - prev[o + i]);
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dz[b] = red[0] * (hi - lo) * sg * (1.f - sg);
+}
+
+// dropout with a given mask (nn.py:273-274, tf.nn.dropout): y = x * mask, mask = keep / keep_prob or 0;
+// the backward is the same product on the gradient
+__global__ void dropout_kernel(const float* __restrict__ x, long long rows, int c, int ldx, const float* __restrict__ mask,
+                               float* __restrict__ y, int ldy) {
+  const long long n = rows * c;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / c;
+    const int k = (int)(i - r * c);
+    y[r * ldy + k] = x[r * ldx + k] * mask[i];
+  }
+}
+
 __global__ void highway_kernel(const float* __restrict__ s, const float* __restrict__ prev,
                                const float* __restrict__ z, const float* __restrict__ zb, long long per_img,
                                long long total, float lo, float hi, float* __restrict__ out) {
@@ -1049,6 +1145,32 @@ int svae_pcnn_sample(const float* l, const float* u_mix, const float* u_log, int
   return hipchk();
 }
 
+int svae_pcnn_sample_bwd(const float* l, const float* u_mix, const float* u_log, int nimg, int per_img, int m,
+                         const float* dx, int dx_stride, float* dl, void* stream) {
+  if (!l || !u_mix || !u_log || !dx || !dl || nimg < 1 || per_img < 1 || m < 1 || m > PC_MAXMIX || dx_stride < 3)
+    return bad("pcnn_sample_bwd: bad arguments");
+  const long long n = (long long)nimg * per_img;
+  hipLaunchKernelGGL(sample_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, l, u_mix,
+                     u_log, n, m, dx, dx_stride, dl);
+  return hipchk();
+}
+
+int svae_pcnn_highway_bwd(const float* s, const float* prev, const float* z, const float* zb, int nimg, int64_t per_img,
+                          float lo, float hi, const float* dout, float* ds, float* dprev, int prev_acc, float* dz,
+                          void* stream) {
+  if (!s || !prev || !z || !dout || !dz || nimg < 1 || per_img < 1) return bad("pcnn_highway_bwd: bad arguments");
+  hipLaunchKernelGGL(highway_bwd_kernel, dim3(nimg), dim3(256), 0, (hipStream_t)stream, s, prev, z, zb,
+                     (long long)per_img, lo, hi, dout, ds, dprev, prev_acc, dz);
+  return hipchk();
+}
+
+int svae_pcnn_dropout(const float* x, int64_t rows, int c, int ldx, const float* mask, float* y, int ldy, void* stream) {
+  if (!x || !mask || !y || rows < 1 || c < 1 || ldx < c || ldy < c) return bad("pcnn_dropout: bad arguments");
+  hipLaunchKernelGGL(dropout_kernel, dim3(blocks_for((long long)rows * c)), dim3(256), 0, (hipStream_t)stream, x,
+                     (long long)rows, c, ldx, mask, y, ldy);
+  return hipchk();
+}
+
 int svae_pcnn_highway(const float* s, const float* prev, const float* z, const float* zb, int nimg, int64_t per_img,
                       float lo, float hi, float* out, float* ratio, void* stream) {
   if (!s || !prev || !z || !out || nimg < 1 || per_img < 1) return bad("pcnn_highway: bad arguments");
@@ -1074,7 +1196,7 @@ int svae_pcnn_adam(float* p, const float* g, float* m, float* v, int64_t n, floa
   if (!p || !g || !m || !v || n < 1 || step < 1) return bad("pcnn_adam: bad arguments");
   const double b1 = 0.9, b2 = 0.999;
   const double lr_t = lr * sqrt(1.0 - pow(b2, (double)step)) / (1.0 - pow(b1, (double)step));
-  adam_step(p, g, m, v, nullptr, n, (float)lr_t, (float)b1, (float)b2, 1e-8f, clip, (hipStream_t)stream);
+  adam_step(p, g, m, v, nullptr, n, (float)lr_t, (float)b1, (float)b2, 1e-8f, clip, 1, 0, (hipStream_t)stream);
   return hipchk();
 }
 

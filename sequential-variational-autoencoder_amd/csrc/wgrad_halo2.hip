@@ -67,10 +67,15 @@ struct WH2Args {
   float* part; long long p_gs;   // [split][16][M][N] partials (or dW itself when nsplit == 1)
   int M, N, nsplit, nchunk;      // nchunk: chunks per group
   int g_bf16, d_bf16;            // G / D stored as bf16 (opload.h)
+  int nsp;                       // 2: split-bf16 planes (fp32 G / D)
 };
 
-template <int WO, int CP, int KYR, int WN, int WK, bool DB, int OPB, int NSW, int PF, int S = 1>
+// NSP = 2: split-bf16 operands (dtype bf16x6's weight gradients, opload.h): the fp32 G window and D
+// rows are staged as hi / lo bf16 planes (plane p of the stage at p * BUF) and every fragment pair
+// runs the three plane products hi*hi + hi*lo + lo*hi
+template <int WO, int CP, int KYR, int WN, int WK, bool DB, int OPB, int NSW, int PF, int S = 1, int NSP = 1>
 __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args a) {
+  static_assert(NSP == 1 || (OPB == 0 && !DB), "split planes: fp32 operands, one stage");
   using GE = Geo2<WO, CP, S>;
   constexpr int GP = GE::GP, HI = GE::HI;
   constexpr int NT = 64 * KYR * WN * WK;
@@ -165,12 +170,23 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
       }
     }
   };
+  // one bf16 plane (NSP = 1), or the hi / lo planes of the fp32 values (NSP = 2)
+  auto put4 = [&](__bf16* st, int o, f32x4 v, bool bfs) {
+    if constexpr (NSP == 1) {
+      *(bf16x4*)&st[o] = raw4_bf(v, bfs);
+    } else {
+      ol_bf16x4 pl[NSP];
+      split4<NSP>(v, pl);
+#pragma unroll
+      for (int p = 0; p < NSP; ++p) *(bf16x4*)&st[p * BUF + o] = pl[p];
+    }
+  };
   auto store_chunk = [&](__bf16* st, const f32x4 (&gv)[GI], const f32x4 (&dv)[DI]) {
 #pragma unroll
     for (int i = 0; i < GI; ++i) {
       if (wpr[i] == -1) continue;
       const int it = tid + NT * i;
-      *(bf16x4*)&st[(it >> 3) * GP + (it & 7) * 4] = raw4_bf(gv[i], gbf);
+      put4(st, (it >> 3) * GP + (it & 7) * 4, gv[i], gbf);
     }
 #pragma unroll
     for (int i = 0; i < DI; ++i) {
@@ -178,7 +194,7 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
       if (it < CP * DN / 4) {
         const int k = it / (DN / 4), sl = it - k * (DN / 4);
         const int s2 = DN == 64 ? (sl ^ (((k >> 1) & 1) << 3)) : sl;
-        *(bf16x4*)&st[GWB + k * DN + s2 * 4] = raw4_bf(dv[i], dbf);
+        put4(st, GWB + k * DN + s2 * 4, dv[i], dbf);
       }
     }
   };
@@ -195,21 +211,26 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
 #pragma unroll
     for (int j = 0; j < GE::KSTEPS / WK; ++j) {
       const int k0 = j * WK * 16;
-      bf16x8 bfr[NSW];
+      bf16x8 bfr[NSW][NSP];
 #pragma unroll
       for (int sn = 0; sn < NSW; ++sn) {
         const int dw = da[sn] + 16 * wk * DN * 2;
-        bfr[sn] = join(tr16((const __bf16*)(sb + dw + (k0 * DN) * 2)),
-                       tr16((const __bf16*)(sb + dw + ((k0 + 4) * DN) * 2)));
+#pragma unroll
+        for (int p = 0; p < NSP; ++p)
+          bfr[sn][p] = join(tr16((const __bf16*)(sb + p * BUF * 2 + dw + (k0 * DN) * 2)),
+                            tr16((const __bf16*)(sb + p * BUF * 2 + dw + ((k0 + 4) * DN) * 2)));
       }
       const int w0 = GE::wpos(k0), w1 = GE::wpos(k0 + 4);
 #pragma unroll
       for (int kx = 0; kx < 4; ++kx) {
-        const bf16x8 af = join(tr16((const __bf16*)(sb + gw + (w0 + kx) * GP * 2)),
-                               tr16((const __bf16*)(sb + gw + (w1 + kx) * GP * 2)));
+        bf16x8 af[NSP];
+#pragma unroll
+        for (int p = 0; p < NSP; ++p)
+          af[p] = join(tr16((const __bf16*)(sb + p * BUF * 2 + gw + (w0 + kx) * GP * 2)),
+                       tr16((const __bf16*)(sb + p * BUF * 2 + gw + (w1 + kx) * GP * 2)));
 #pragma unroll
         for (int sn = 0; sn < NSW; ++sn)  // every transposed A fragment feeds NSW MFMAs
-          acc[kx][sn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[sn], acc[kx][sn], 0, 0, 0);
+          acc[kx][sn] = mfma_split<NSP>(af, bfr[sn], acc[kx][sn]);
       }
     }
     if constexpr (!DB) __syncthreads();  // single stage: the next store waits for every reader
@@ -266,26 +287,26 @@ __global__ __launch_bounds__(64 * KYR * WN * WK) void wgrad_halo2_kernel(WH2Args
 // ---------------------------------------------------------------------------
 namespace {
 
-template <int WO, int CP, int KYR, int WN, int WK, bool DB, int NSW, int S>
+template <int WO, int CP, int KYR, int WN, int WK, bool DB, int NSW, int S, int NSP = 1>
 size_t wh2_lds() {
   using GE = Geo2<WO, CP, S>;
-  const size_t stage = ((size_t)GE::NPIX * GE::GP + (size_t)CP * 32 * WN * NSW) * 2;
+  const size_t stage = NSP * ((size_t)GE::NPIX * GE::GP + (size_t)CP * 32 * WN * NSW) * 2;
   const size_t red = WK > 1 ? (size_t)(WK - 1) * KYR * WN * 4 * 16 * 64 * 4 : 0;
   return std::max((DB ? 2 : 1) * stage, red);
 }
 
-template <int WO, int CP, int KYR, int WN, int WK, bool DB, int OPB, int NSW, int PF, int S>
+template <int WO, int CP, int KYR, int WN, int WK, bool DB, int OPB, int NSW, int PF, int S, int NSP = 1>
 void wh2_launch_op(const WH2Args& a, int groups, hipStream_t s) {
-  const size_t lds = wh2_lds<WO, CP, KYR, WN, WK, DB, NSW, S>();
+  const size_t lds = wh2_lds<WO, CP, KYR, WN, WK, DB, NSW, S, NSP>();
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)wgrad_halo2_kernel<WO, CP, KYR, WN, WK, DB, OPB, NSW, PF, S>,
+    hipFuncSetAttribute((const void*)wgrad_halo2_kernel<WO, CP, KYR, WN, WK, DB, OPB, NSW, PF, S, NSP>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   dim3 grid(a.M / 32, a.N / (32 * WN * NSW), (4 / KYR) * a.nsplit * groups);
-  hipLaunchKernelGGL((wgrad_halo2_kernel<WO, CP, KYR, WN, WK, DB, OPB, NSW, PF, S>), grid, dim3(64 * KYR * WN * WK), lds,
-                     s, a);
+  hipLaunchKernelGGL((wgrad_halo2_kernel<WO, CP, KYR, WN, WK, DB, OPB, NSW, PF, S, NSP>), grid,
+                     dim3(64 * KYR * WN * WK), lds, s, a);
 }
 // operand storage (G fp32/bf16 x D fp32/bf16) as a compile-time parameter: no branches in the loads
 int env_int(const char* name, int dflt);
@@ -297,6 +318,10 @@ void wh2_launch_pf(const WH2Args& a, int groups, hipStream_t s) {
 }
 template <int WO, int CP, int KYR, int WN, int WK, bool DB, int NSW = 1, int S = 1>
 void wh2_launch(const WH2Args& a, int groups, hipStream_t s) {
+  if (a.nsp > 1) {  // split-bf16 planes (fp32 operands): one chunk of register prefetch
+    wh2_launch_op<WO, CP, KYR, WN, WK, false, 0, NSW, 1, S, 2>(a, groups, s);
+    return;
+  }
   switch ((a.g_bf16 ? 1 : 0) | (a.d_bf16 ? 2 : 0)) {
     case 0: wh2_launch_pf<WO, CP, KYR, WN, WK, DB, 0, NSW, S>(a, groups, s); break;
     case 1: wh2_launch_pf<WO, CP, KYR, WN, WK, DB, 1, NSW, S>(a, groups, s); break;
@@ -361,6 +386,8 @@ int wgrad_halo2(const WgArgs& w, int groups, float* slab, long long slab_cap, fl
   a.G = w.G; a.g_gs = w.g_gs; a.ldg = w.ldg;
   a.D = w.D; a.d_gs = w.d_gs; a.ldd = w.ldd;
   a.g_bf16 = w.g_bf16; a.d_bf16 = w.d_bf16;
+  a.nsp = w.nsp > 1 ? 2 : 1;
+  if (a.nsp > 1 && (a.g_bf16 || a.d_bf16)) return 0;  // split planes come from fp32 operands
   a.M = w.M; a.N = w.N;
   a.nchunk = w.rows / cp;
   const long long tiles = (long long)(w.M / 32) * (w.N / (32 * wn)) * (4 / kyr) * groups;

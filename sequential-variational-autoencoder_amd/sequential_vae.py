@@ -134,7 +134,7 @@ class SequentialVAE:
         soon as the backward has finished it (after that bucket's overlapped all-reduce), the
         recognition bucket last.  Bit for bit the parameters of the two separate calls."""
         lr = self.learning_rate if lr is None else lr
-        step = self.iteration if step is None else step
+        step = self._adam_step(step)
         if self.grad_hook is not None:  # the exchange follows the whole backward: Adam after it
             self.backward(stream)
             self.apply_gradients(lr, step, stream)
@@ -165,7 +165,7 @@ class SequentialVAE:
     def apply_imp_gradients(self, lr=None, step=None, stream=None):
         """clip + Adam of the recognition variables with ``grads_imp`` (:1304-1306)."""
         lr = self.learning_rate if lr is None else lr
-        step = self.adam_updates if step is None else step
+        step = self._adam_step(step)
         _lib.check(self.L.svae_adam_imp(self.ctx, float(lr), int(step), float(self.cfg.clip_grad_value),
                                         _lib.stream_ptr(stream)), self.ctx)
 
@@ -178,9 +178,17 @@ class SequentialVAE:
             tot += float(self.copy_out(_lib.BUF_IMP_IMG, t, self.cfg.batch).double().mean())
         return -reg * self.cfg.latent_pred_loss_coeff * tot
 
+    def _adam_step(self, step):
+        """The Adam step an update runs as (TF's beta1_power = 0.9^step): the next one by default.
+        Every update path records it, so save_checkpoint's beta powers match the updates taken
+        whichever API (train, backward_apply, apply_gradients, apply_imp_gradients) drove them."""
+        step = self.adam_updates + 1 if step is None else int(step)
+        self.adam_updates = step
+        return step
+
     def apply_gradients(self, lr=None, step=None, stream=None):
         lr = self.learning_rate if lr is None else lr
-        step = self.iteration if step is None else step
+        step = self._adam_step(step)
         _lib.check(self.L.svae_adam(self.ctx, float(lr), int(step), float(self.cfg.clip_grad_value),
                                     _lib.stream_ptr(stream)), self.ctx)
 
@@ -279,15 +287,12 @@ class SequentialVAE:
         reg = 1.0 - math.exp(-self.iteration / self.cfg.reg_coeff_rate)
         self.forward(input_batch, batch_target, eps, reg, noise=noise)
         if self.grads_imp is None:
-            self.adam_updates += 1
-            self.backward_apply(self.learning_rate, self.adam_updates)
+            self.backward_apply(self.learning_rate)
         else:
             self.backward()
             self.backward_imp()
-            self.adam_updates += 1
-            self.apply_gradients(self.learning_rate, self.adam_updates)
-            self.adam_updates += 1
-            self.apply_imp_gradients(self.learning_rate, self.adam_updates)
+            self.apply_gradients(self.learning_rate)
+            self.apply_imp_gradients(self.learning_rate)
         final = float(self.copy_out(_lib.BUF_STEP_STATS, self.cfg.mc_steps - 1, 2)[0])
         return final / self.data_dims[0] / self.data_dims[1]
 
@@ -363,15 +368,23 @@ class SequentialVAE:
             self.adam_updates = 0
         self.learning_rate = float(meta.get("learning_rate", self.learning_rate))
 
-    def generate(self, z=None, stream=None):
+    def generate(self, z=None, stream=None, noise=None):
         """Generator chain on latents z [T,B,Dz] (None: N(0,1) on device), no recognition network
-        (sequential_vae.py:947-952, :1025).  Returns [x_hat_t] device tensors [B,H,W,C]."""
+        (sequential_vae.py:947-952, :1025).  With add_noise_to_chain, ``noise`` [T,B,H,W,C] injects
+        the chain noise (None: drawn on device, never the last forward's).  Returns [x_hat_t]
+        device tensors [B,H,W,C]."""
         e = None
         if z is not None:
             e = self._dev(z)
             if tuple(e.shape) != (self.cfg.mc_steps, self.cfg.batch, self.cfg.latent_dim):
                 raise ValueError("z must be [T,B,Dz]")
-        self._keep = (e,)
+        nz = None
+        if noise is not None:
+            if not self.cfg.add_noise_to_chain:
+                raise ValueError("noise given but add_noise_to_chain is off")
+            nz = self._dev(noise)
+            _lib.check(self.L.svae_set_chain_noise(self.ctx, _lib.ptr(nz)), self.ctx)
+        self._keep = (e, nz)
         _lib.check(self.L.svae_generate(self.ctx, _lib.ptr(e), _lib.stream_ptr(stream)), self.ctx)
         return [self.xhat(t) for t in range(self.cfg.mc_steps)]
 

@@ -122,8 +122,10 @@ def test_chain_variant_matches_oracle(name):
     if cd["predict_generator_noise"]:
         sens = _oracle_sensitivity(net, cd, shared, x, tgt, eps, noise, reg, o, summ)
         for key, (svec, smed) in sens.items():
-            bounds[key] = (max(1e-3, 10 * svec), max(1e-4, 10 * smed))
-            msg.append("oracle's own %s under a 1e-6 input move: vector %.2e median %.2e" % (key, svec, smed))
+            # capped: the conditioning widens the fixed bounds by at most 10x
+            bounds[key] = (min(1e-2, max(1e-3, 10 * svec)), min(1e-3, max(1e-4, 10 * smed)))
+            msg.append("oracle's own %s under a 1e-6 input move: vector %.2e median %.2e -> bounds %.1e / %.1e" % (
+                key, svec, smed, bounds[key][0], bounds[key][1]))
     bvec, bmed = bounds["grads"]
     msg.append("grads vector %.2e median %.2e (bounds %.1e / %.1e)" % (gvec, gmed, bvec, bmed))
     assert gvec <= bvec and gmed <= bmed, (gvec, gmed, bvec, bmed)

@@ -74,3 +74,36 @@ def test_checkpoint_without_metadata_recovers_adam_step(tmp_path):
     assert b.iteration == 3
     a.close()
     b.close()
+
+
+def test_checkpoint_after_low_level_updates(tmp_path):
+    """Adam steps taken through forward + backward_apply / apply_gradients (bench.py's and the DP
+    loop's API, not train()) are counted too: beta1_power in the file matches the updates taken, and
+    a resumed train() continues the bias correction from there."""
+    from safetensors.numpy import load_file
+    cfg = pkg_mod("config").preset("tiny", batch=4)
+    SV = pkg_mod("sequential_vae").SequentialVAE
+    a = SV(cfg, seed=0)
+    x = torch.rand(cfg.batch, cfg.height, cfg.width, cfg.channels, device="cuda") * 2 - 1
+    a.forward(x, x, None, 1.0)
+    a.backward_apply()           # Adam step 1
+    a.forward(x, x, None, 1.0)
+    a.backward()
+    a.apply_gradients()          # Adam step 2
+    assert a.adam_updates == 2
+    path = str(tmp_path / "low.safetensors")
+    a.save_checkpoint(path)
+    t = load_file(path)
+    assert float(t["beta1_power"]) == pytest.approx(0.9 ** 3)
+    assert float(t["beta2_power"]) == pytest.approx(0.999 ** 3)
+    b = SV(cfg, seed=5)
+    b.load_checkpoint(path)
+    assert b.adam_updates == 2
+    eps = torch.randn(cfg.mc_steps, cfg.batch, cfg.latent_dim, device="cuda")
+    a.train(x, x, eps=eps)
+    b.train(x, x, eps=eps)
+    assert a.adam_updates == b.adam_updates == 3
+    torch.cuda.synchronize()
+    assert torch.equal(a.params, b.params)
+    a.close()
+    b.close()

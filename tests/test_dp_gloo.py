@@ -1,4 +1,4 @@
-"""Data-parallel path on CPU (gloo, world_size 2): per-shard BN semantics + one
+"""Data-parallel path on CPU (gloo, world_size 2 and 8): per-shard BN semantics + one
 all-reduce of the flat gradient (SURVEY.md §8e parity rule):
   N-rank loss  = mean over shards of the single-process loss of each shard
   N-rank grad  = mean over shards of the per-shard gradients
@@ -129,3 +129,67 @@ def test_overlapped_allreduce_equals_mean(tmp_path):
         np.testing.assert_allclose(o[:n_live], mean, rtol=1e-6, atol=1e-7)
         np.testing.assert_array_equal(o[n_live:], src[r][n_live:])  # dead tail untouched
     np.testing.assert_array_equal(np.load(tmp_path / "o0.npy")[:n_live], np.load(tmp_path / "o1.npy")[:n_live])
+
+
+def _twin_flat(rank, world, gx, gt, eps_all, table, n_total):
+    """Rank `rank`'s shard of the global batch through the fp64 twin; its gradient laid out in the
+    engine's flat buffer (weights.param_table offsets), so the product's buckets apply to it."""
+    cd = spec.make_config("tiny", batch=gx.shape[0] // world)
+    _, struct, params = spec.init_params(cd, seed=0)
+    par = pkg_mod("parallel")
+    x = par.shard(torch.from_numpy(gx), rank, world).numpy()
+    t = par.shard(torch.from_numpy(gt), rank, world).numpy()
+    eps = eps_all[:, rank * cd["batch"]:(rank + 1) * cd["batch"]]
+    o = torch_twin.Twin(cd, struct, params, dtype=torch.float64).step(x, t, eps, 0.5)
+    flat = torch.zeros(n_total, dtype=torch.float64)
+    for p in table:
+        flat[p["offset"]:p["offset"] + p["size"]] = torch.from_numpy(np.ravel(o["grads"][p["name"]]))
+    return o["loss"], flat
+
+
+def _overlap_twin_worker(rank, world, port, gx, gt, eps_all, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    par, w, cfgmod = pkg_mod("parallel"), pkg_mod("weights"), pkg_mod("config")
+    table, n_total, n_live = w.param_table(cfgmod.preset("tiny"))
+    loss, flat = _twin_flat(rank, world, gx, gt, eps_all, table, n_total)
+    ov = par.OverlappedAllReduce(_FakeNet(flat, table, n_live), dist)
+    T = cfgmod.preset("tiny").mc_steps
+    for t in range(T - 1, -1, -1):  # the engine's call order: theta_t buckets, then phi
+        ov._on_step(None, t)
+    ov._on_step(None, -1)
+    ov.check()
+    np.save(os.path.join(out_dir, "tg%d.npy" % rank), flat.numpy())
+    np.save(os.path.join(out_dir, "tl%d.npy" % rank), np.array([par.mean_scalar(dist, loss, torch.device("cpu")), loss]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_overlapped_buckets_on_twin_gradients(tmp_path, world):
+    """The DP8 configuration's exchange on real gradients: a global batch of 128*world images
+    (1024 -> 8 x 128 at world 8) in contiguous shards, each rank's fp64 twin gradient in the flat
+    engine layout, the per-step buckets of parallel.OverlappedAllReduce in the engine's call order.
+    Every replica ends with the mean of the per-shard gradients (the dead tail untouched) and the
+    mean of the per-shard losses (SURVEY §8e parity rule)."""
+    B = 128 * world
+    cd = spec.make_config("tiny", batch=B)
+    gx, gt, eps_all = spec.make_inputs(cd, batch=B)
+    mp.spawn(_overlap_twin_worker, args=(world, _free_port(), gx, gt, eps_all, str(tmp_path)), nprocs=world, join=True)
+    w, cfgmod = pkg_mod("weights"), pkg_mod("config")
+    table, n_total, n_live = w.param_table(cfgmod.preset("tiny"))
+    torch.set_num_threads(max(1, min(8, torch.get_num_threads())))
+    ref = [_twin_flat(r, world, gx, gt, eps_all, table, n_total) for r in range(world)]
+    mean_g = (sum(f for _, f in ref) / world).numpy()
+    mean_l = sum(l for l, _ in ref) / world
+    g0 = np.load(tmp_path / "tg0.npy")
+    for r in range(world):
+        g = np.load(tmp_path / ("tg%d.npy" % r))
+        np.testing.assert_allclose(g[:n_live], mean_g[:n_live], rtol=1e-12, atol=1e-15)
+        # the dead / zero-gradient tail is not exchanged: each rank keeps its own (round-off) values
+        np.testing.assert_allclose(g[n_live:], ref[r][1].numpy()[n_live:], rtol=0, atol=1e-12)
+        np.testing.assert_array_equal(g[:n_live], g0[:n_live])  # replicas bitwise equal
+        ml, own = np.load(tmp_path / ("tl%d.npy" % r))
+        assert abs(ml - mean_l) <= 1e-12 * abs(mean_l)
+        assert abs(own - ref[r][0]) <= 1e-12 * abs(own)

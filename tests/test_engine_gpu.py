@@ -64,9 +64,11 @@ def _check_grads(g_hip, ref, g_twin, median_tol=1e-4):
             assert np.abs(g_hip[k]).max() <= 1e-5, k
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "bf16x6"])
 @pytest.mark.parametrize("preset,batch,reg", [("tiny", 4, 0.37), ("mnist_1step", 4, 1.0), ("tiny", 7, 1e-3)])
-def test_fwd_bwd_matches_oracle(preset, batch, reg):
-    net, cfg = _engine(preset, batch)
+def test_fwd_bwd_matches_oracle(preset, batch, reg, dtype):
+    """dtype bf16x6 (split-bf16 MFMA) is held to exactly the fp32 bounds."""
+    net, cfg = _engine(preset, batch, dtype=dtype)
     cd = spec.make_config(preset, batch=batch)
     x, tgt, eps = spec.make_inputs(cd, batch=batch)
     if preset == "tiny" and batch == 7:
@@ -92,10 +94,12 @@ def test_fwd_bwd_matches_oracle(preset, batch, reg):
     _check_grads(net.grad_dict(), o["grads"], p32["grads"])
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "bf16x6"])
 @pytest.mark.parametrize("steps,batch", [(3, 8), (8, 8)])
-def test_celeba_geometry_fwd_bwd(steps, batch):
-    """CelebA geometry (64x64, filters [3,32,64,128,384,512], latent [3,3,3,3])."""
-    net, cfg = _engine("celeba", batch, mc_steps=steps)
+def test_celeba_geometry_fwd_bwd(steps, batch, dtype):
+    """CelebA geometry (64x64, filters [3,32,64,128,384,512], latent [3,3,3,3]); bf16x6 at the
+    fp32 bounds (every split kernel runs here: 32-channel layers, FCs, weight gradients)."""
+    net, cfg = _engine("celeba", batch, mc_steps=steps, dtype=dtype)
     cd = spec.make_config("celeba", batch=batch, mc_steps=steps)
     x, tgt, eps = spec.make_inputs(cd, batch=batch)
     net.forward(x, tgt, eps, 1.0)
@@ -186,7 +190,7 @@ def test_celeba_b128_forward_matches_twin():
         assert e_hip <= max(1e-4, 4 * e_32), (t, e_hip, e_32)
 
 
-@pytest.mark.parametrize("preset,batch,dtype", [("celeba", 128, "fp32"), ("celeba", 128, "bf16"),
+@pytest.mark.parametrize("preset,batch,dtype", [("celeba", 128, "fp32"), ("celeba", 128, "bf16"), ("celeba", 128, "bf16x6"),
                                                 ("lsun", 256, "bf16"), ("lsun", 256, "fp32")])
 def test_full_size_properties(preset, batch, dtype):
     """Size-independent properties at the BASELINE geometries (CelebA B=128, LSUN B=256):

@@ -33,12 +33,14 @@ def _rel(a, b):
     return float(np.linalg.norm(np.ravel(a) - np.ravel(b)) / max(np.linalg.norm(np.ravel(b)), 1e-30))
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "bf16x6"])
 @pytest.mark.parametrize("path", FILES, ids=lambda p: os.path.basename(p)[:-4])
-def test_engine_matches_golden(path):
+def test_engine_matches_golden(path, dtype):
+    """dtype bf16x6 (split-bf16 MFMA, the fp32-accurate mode) is held to the fp32 bounds."""
     g = np.load(path)
     preset = str(g["preset"])
     chaotic = preset in ("celeba", "lsun")  # full-depth T=8 chains
-    cfg = pkg_mod("config").preset(preset, batch=int(g["batch"]))
+    cfg = pkg_mod("config").preset(preset, batch=int(g["batch"]), dtype=dtype)
     net = pkg_mod("sequential_vae").SequentialVAE(cfg, seed=0)
     reg = float(g["reg"])
     net.forward(g["x"], g["target"], g["eps"], reg)

@@ -4,11 +4,10 @@
     rocprofv3 --pmc WRITE_SIZE --output-format csv -d <write_dir> -o run -- python3 bench.py ...
     python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json> [label]
 
-FETCH_SIZE / WRITE_SIZE are KiB per dispatch.  MI355X_MICROARCH.md (HBM section): on
-gfx950 FETCH_SIZE reports 1/2 of the bytes of WIDE (16 B/lane) coalesced streaming reads, so it
-is doubled only for kernels whose HBM operand loads are 16 B/lane (WIDE16 below, from the
-kernel sources); other access widths are uncalibrated and are reported as counted ("x1,
-uncalibrated").  WRITE_SIZE is taken as is.  Each kernel's entry records the rule applied.  The two counters cannot share a pass (TCC slots),
+FETCH_SIZE / WRITE_SIZE are KiB per dispatch.  FETCH_SIZE is corrected per kernel by the
+calibrated rule of fetch_rule() below (tools/calib/fetch_calib.hip, profiles/r03_fetch_calib.txt:
+whole-128-B-line reads count half, 64-B-segment reads count exactly); WRITE_SIZE is taken as is.
+Each kernel's entry records the rule applied.  The two counters cannot share a pass (TCC slots),
 hence two runs of the same command; per-kernel averages are matched by kernel name.
 """
 import csv
@@ -35,35 +34,54 @@ def _short(name):
     return name
 
 
-# kernels whose operand loads from HBM are 16 B per lane (f32x4 / bf16x8 / int4 vectors)
+# Calibration (tools/calib/fetch_calib.hip, profiles/r03_fetch_calib.txt, 768 MiB streamed past the
+# Infinity Cache): FETCH_SIZE counts HALF the bytes of fully coalesced reads of whole 128-B lines,
+# at 16, 8 and 4 B per lane alike, and EXACTLY the bytes of reads that take 64-B halves of lines.
+# So the factor follows each operand's contiguous span per row, not the lane width:
+#   >= 128 B per row segment -> x2;  64 B segments -> x1.
+# kernels whose HBM operand rows are >= 128 B (fp32 rows of >= 32 channels, 16 B/lane streams)
 WIDE16 = ("wgrad_halo_kernel", "igemm_halo_kernel", "igemm_bf16_kernel", "wgrad_bf16_kernel", "igemm_fwd_kernel",
           "wgrad_kernel", "wgrad_reduce_kernel<", "splitk_reduce_kernel", "bn_apply_kernel", "bn_bwd_reduce_kernel",
-          "bn_bwd_apply_kernel", "adam_kernel", "shadow_n_kernel", "shadow_t_kernel", "loss_reduce_kernel")
+          "bn_bwd_apply_kernel", "adam_kernel", "shadow_n_kernel", "shadow_t_kernel", "loss_reduce_kernel",
+          "dense_kw_kernel")
 
 
-# kernels whose operand width follows their storage template parameter (opload.h): OPB (last
-# template argument at OPB_POS) 0 = both operands fp32 (16 B/lane loads), else a bf16 operand loads 8 B/lane
-OPB_POS = {"wgrad_halo2_kernel": 6, "wgrad_halo_kernel": 2}
-# 16 B/lane whatever the storage (8 fp32 = two 16-B loads, 8 bf16 = one)
-WIDE16_ANY = ("igemm_halo_kw_kernel",)
+def _targs(k, name):
+    return [t.strip() for t in k[len(name) + 1:k.rindex(">")].split(",")]
+
+
+def _wh2_factor(targs):
+    """wgrad_halo2_kernel<WO, CP, KYR, WN, WK, DB, OPB, NSW, PF, S[, NSP]>: the G window rows are 32
+    channels (64 B bf16 -> x1, 128 B fp32 -> x2), the D rows 32*WN*NSW channels; the factor is the
+    byte-weighted harmonic mix of the two operands' factors (algorithmic bytes per chunk)."""
+    WO, CP, WN, OPB, NSW = int(targs[0]), int(targs[1]), int(targs[3]), int(targs[6]), int(targs[7])
+    S = int(targs[9]) if len(targs) > 9 else 1
+    per = WO * WO
+    img = 1 if CP <= per else CP // per
+    R = CP // WO if CP <= per else WO
+    npix = img * (S * (R - 1) + 4) * (S * (WO - 1) + 4)
+    gb, db = (2 if OPB & 1 else 4), (2 if OPB & 2 else 4)
+    DN = 32 * WN * NSW
+    g_bytes, d_bytes = npix * 32 * gb, CP * DN * db
+    fg = 2.0 if 32 * gb >= 128 else 1.0
+    fd = 2.0 if DN * db >= 128 else 1.0
+    return (g_bytes + d_bytes) / (g_bytes / fg + d_bytes / fd)
 
 
 def fetch_rule(kernel):
     k = kernel.replace("(anonymous namespace)::", "").split("(")[0]
-    for w in WIDE16_ANY:
-        if k.startswith(w):
-            return 2.0, "FETCH_SIZE x2 (16 B/lane loads: gfx950 half-count)"
-    for w, pos in OPB_POS.items():
-        if k.startswith(w + "<"):
-            targs = k[len(w) + 1:].rstrip(">").split(",")
-            opb = targs[pos].strip() if pos < len(targs) else targs[-1].strip()
-            if opb == "0":
-                return 2.0, "FETCH_SIZE x2 (fp32 operands, 16 B/lane loads: gfx950 half-count)"
-            return 1.0, "FETCH_SIZE x1 (a bf16 operand loads 8 B/lane: uncalibrated, as counted)"
+    if k.startswith("igemm_halo_kw_kernel<"):
+        abf = _targs(k, "igemm_halo_kw_kernel")[3] == "true"
+        if abf:
+            return 1.0, "FETCH_SIZE x1 (bf16 window rows of 32 channels = 64-B line halves: calibrated exact)"
+        return 2.0, "FETCH_SIZE x2 (fp32 window rows of 32 channels = whole 128-B lines: calibrated half-count)"
+    if k.startswith("wgrad_halo2_kernel<"):
+        f = _wh2_factor(_targs(k, "wgrad_halo2_kernel"))
+        return f, "FETCH_SIZE x%.3f (G window / D row mix of 64-B (x1) and >= 128-B (x2) segments, calibrated)" % f
     for w in WIDE16:
         if k.startswith(w) or (w.endswith("<") and k.startswith(w[:-1])):
-            return 2.0, "FETCH_SIZE x2 (16 B/lane loads: gfx950 half-count)"
-    return 1.0, "FETCH_SIZE x1 (loads narrower than 16 B/lane: uncalibrated, as counted)"
+            return 2.0, "FETCH_SIZE x2 (rows of >= 128 B: calibrated half-count)"
+    return 1.0, "FETCH_SIZE x1 (row segments below 128 B or unknown: as counted)"
 
 
 def _load(d, counter):
