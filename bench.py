@@ -43,6 +43,9 @@ METRIC = {
              "LSUN-bedroom 64x64 seq-VAE (sequential_vae_lsun, latent 110), T=8 chain, fwd+bwd+clip+Adam"),
     "mnist_1step": ("images/sec (MNIST 32x32 1-step seq-VAE fwd+bwd+Adam step)",
                     "MNIST 1-step seq-VAE (m_* geometry, latent 24), fwd+bwd+clip+Adam"),
+    "c_pixelvae": ("images/sec (CelebA 64x64 seq-VAE + PixelCNN++ decoder, c_pixelvae, fwd+bwd+Adam step)",
+                   "c_pixelvae (sequential_vae.py:529-543): T=2 shared theta/phi, step 0 ladder, step 1 PixelCNN++ "
+                   "head (nr_resnet 3, 160 filters, 10 mixtures, dropout 0.3), fwd+bwd+clip+Adam+EMA"),
 }
 
 
@@ -251,6 +254,80 @@ def mode_throughput(cfg, SV, dtype, steps=10, warmup=3):
     return c32.batch * steps / dt, dt / steps * 1e3
 
 
+def run_pixelvae(args, cfgmod):
+    """BASELINE configs[4] (CelebA + pixel_cnn decoder, 1 GPU): the c_pixelvae training step
+    (pixelvae.PixelVAE.train: engine forward, head training pass with dropout, sampler + highway,
+    both backwards, Adam + Polyak EMA) on a synthetic batch resident in HBM.  The roofline entry is
+    the head's conv kernel (pc_conv2_kernel: every forward convolution of the head, timed live by
+    event pairs around its first --probe-launches launches inside the timed region)."""
+    PV = importlib.import_module(PKG + ".pixelvae").PixelVAE
+    B = args.batch or 128
+    dtype = args.dtype
+    pv = PV("c_pixelvae", batch_size=B, dtype=dtype)
+    c = pv.cfg
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1234)
+    x = (torch.rand(B, c.height, c.width, c.channels, device="cuda", generator=g) * 2 - 1).contiguous()
+    for _ in range(args.warmup):
+        pv.train(x, x)
+    torch.cuda.synchronize()
+    pv.head.probe, pv.head.probe_cap = [], args.probe_launches or 96
+    pv.head.conv_flops = 0.0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pv.train(x, x)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    probe, pv.head.probe = pv.head.probe, None
+    pflops = sum(f for f, _, _ in probe)
+    pms = sum(e0.elapsed_time(e1) for _, e0, e1 in probe)
+    ach = pflops / (pms / 1e3) / 1e12 if pms > 0 else None
+    head_flops = 3.0 * pv.head.conv_flops / args.steps  # forward + input gradient + weight gradient
+    vae_flops = conv_flops_per_img(c) * B  # the engine's part (both steps' recognition + step 0 ladder)
+    ms = dt / args.steps * 1e3
+    line = {
+        "metric": METRIC["c_pixelvae"][0], "value": round(B * args.steps / dt, 2), "unit": "images/sec", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": dtype + " engine, bf16-MFMA head",
+        "data": "synthetic U[-1,1] NHWC batch, target=input, eps / sampler uniforms / dropout masks on device",
+        "config": {"workload": METRIC["c_pixelvae"][1], "model": "c_pixelvae", "global_batch": B, "per_gpu_batch": B,
+                   "image": [c.height, c.width, c.channels], "mc_steps": c.mc_steps, "parallelism": "dp1"},
+        "elbo_per_img": round(pv.loss_value(), 5),
+        "head_conv_tflop_per_step": round(head_flops / 1e12, 3),
+        "roofline": None if ach is None else {
+            "bound": "mfma", "achieved": round(ach, 3), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 5), "traffic": None,
+            "kernel": "pc_conv2_kernel (PixelCNN++ head forward convolutions, all instances)",
+            "timed_launches": len(probe), "avg_launch_us": round(pms * 1e3 / max(1, len(probe)), 2),
+            "step_achieved_tflops": round((head_flops + vae_flops) / (ms / 1e3) / 1e12, 3)},
+        "cpu_baseline": None,
+    }
+    if not args.no_cpu_baseline:  # the fp64 CPU restatement of the same chain on a 2-image sample
+        from oracle import pcnn as opc, pixelvae as opv, spec as ospec_mod
+        threads, phys, avail = _cpu_threads()
+        torch.set_num_threads(threads)
+        cd = ospec_mod.make_config("celeba", batch=2, mc_steps=2, latent_dims=list(c.latent_dims),
+                                   filter_sizes=list(c.filter_sizes), latent_mean_clip=c.latent_mean_clip,
+                                   min_highway=c.min_highway, max_highway=c.max_highway, regularized_steps=(0,),
+                                   first_step_loss_coeff=c.first_step_loss_coeff)
+        cd["share_theta"] = cd["share_phi"] = True
+        hs = opc.make_spec(H=64, W=64, K=c.latent_dim)
+        xs = x[:2].cpu().numpy()
+        eps = np.random.default_rng(1).standard_normal((2, 2, c.latent_dim))
+        um = np.random.default_rng(2).uniform(1e-5, 1 - 1e-5, (2, 64, 64, 10))
+        ul = np.random.default_rng(3).uniform(1e-5, 1 - 1e-5, (2, 64, 64, 3))
+        pub, hp = pv.vae.param_dict(), pv.head.params()
+        t0 = time.perf_counter()
+        opv.forward_backward(cd, pub, hs, hp, xs, xs, eps, 1.0, um, ul, None, bf16_head=False)
+        cdt = time.perf_counter() - t0
+        line["cpu_baseline"] = dict(value=round(2 / cdt, 4), unit="images/sec", cores=threads, kind="port",
+                                    sample="1 fwd+bwd of 2 images of the c_pixelvae chain with oracle/pixelvae.py "
+                                           "(fp64 torch CPU, dropout off) on %d threads (host: %d physical cores)"
+                                           % (threads, phys))
+    print(json.dumps(line), flush=True)
+    pv.close()
+
+
 def _spawn_ranks(n):
     """--gpus N without a torch.distributed launcher: start N ranks as child processes (nothing
     here has touched the GPU yet) and exit with their status."""
@@ -297,6 +374,11 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     cfgmod = importlib.import_module(PKG + ".config")
+    if args.config == "c_pixelvae":
+        if world != 1:
+            sys.exit("bench.py: --config c_pixelvae is the 1-GPU configuration (BASELINE configs[4])")
+        run_pixelvae(args, cfgmod)
+        return
     SV = importlib.import_module(PKG + ".sequential_vae").SequentialVAE
     par = importlib.import_module(PKG + ".parallel")
     L = importlib.import_module(PKG + "._lib")

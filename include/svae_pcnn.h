@@ -118,6 +118,11 @@ int svae_pcnn_highway_bwd(const float* s, const float* prev, const float* z, con
  * the gradient. */
 int svae_pcnn_dropout(const float* x, int64_t rows, int c, int ldx, const float* mask, float* y, int ldy, void* stream);
 
+/* per-image mean squared error (compute_and_accumulate_loss :1146 on the head's chain output):
+ * rec[img] = mean (a - t)^2 over per_img elements; da = coef * 2 (a - t) / per_img (either may be NULL). */
+int svae_pcnn_sqerr(const float* a, const float* t, int nimg, int64_t per_img, float coef, float* rec, float* da,
+                    void* stream);
+
 /* data-dependent init (nn.py:176-180, :206-210): column moments of y [rows][c] (fp64), then
  * g *= scale / sqrt(v + 1e-10), b -= m * scale / sqrt(v + 1e-10). */
 int svae_pcnn_wn_init(const float* y, int64_t rows, int c, int ldy, float init_scale, float* g, float* b,

@@ -229,25 +229,32 @@ class Net:
         F = x.shape[-1]
         return x + c2[..., :F] * torch.sigmoid(c2[..., F:])
 
-    def model(self, x, h):
-        """model_spec(x, h) (model.py:11-117) -> l [B, H, W, 10 M]."""
+    def model(self, x, h, masks=None):
+        """model_spec(x, h) (model.py:11-117) -> l [B, H, W, 10 M].  masks: the training pass's
+        dropout keep-masks (1 / keep_prob or 0), one per gated resnet in construction order."""
         R = self.s["R"]
+        mk = iter(masks) if masks is not None else None
+        grn = self.gated_resnet
+
+        def gr(x_, h_, kh, kw, a=None):
+            m = None if mk is None else torch.as_tensor(next(mk), dtype=x_.dtype).reshape(x_.shape)
+            return grn(x_, h_, kh, kw, a=a, dmask=m)
         ones = torch.ones(x.shape[:-1] + (1,), dtype=x.dtype)
         xp = torch.cat([x, ones], dim=-1)
         u = [down_shift(self.ds_conv(xp, 2, 3))]
         ul = [down_shift(self.ds_conv(xp, 1, 3)) + right_shift(self.drs_conv(xp, 2, 1))]
         for stage in range(3):
             for _ in range(R):
-                u.append(self.gated_resnet(u[-1], h, 2, 3))
-                ul.append(self.gated_resnet(ul[-1], h, 2, 2, a=u[-1]))
+                u.append(gr(u[-1], h, 2, 3))
+                ul.append(gr(ul[-1], h, 2, 2, a=u[-1]))
             if stage < 2:
                 u.append(self.ds_conv(u[-1], 2, 3, stride=2))
                 ul.append(self.drs_conv(ul[-1], 2, 2, stride=2))
         uu, uul = u.pop(), ul.pop()
         for stage in range(3):
             for _ in range(R if stage == 0 else R + 1):
-                uu = self.gated_resnet(uu, h, 2, 3, a=u.pop())
-                uul = self.gated_resnet(uul, h, 2, 2, a=torch.cat([uu, ul.pop()], dim=-1))
+                uu = gr(uu, h, 2, 3, a=u.pop())
+                uul = gr(uul, h, 2, 2, a=torch.cat([uu, ul.pop()], dim=-1))
             if stage < 2:
                 uu = self.deconv(uu, 2, 3, 1)
                 uul = self.deconv(uul, 2, 2, 0)

@@ -127,6 +127,7 @@ def lib():
         "svae_pcnn_sample_bwd": ([vp, vp, vp, i32, i32, i32, vp, i32, vp, vp], i32),
         "svae_pcnn_highway_bwd": ([vp, vp, vp, vp, i32, i64, f32, f32, vp, vp, vp, i32, vp, vp], i32),
         "svae_pcnn_dropout": ([vp, i64, i32, i32, vp, vp, i32, vp], i32),
+        "svae_pcnn_sqerr": ([vp, vp, i32, i64, f32, vp, vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -150,7 +151,7 @@ PCNN_EXPORTED = ["svae_pcnn_wnorm", "svae_pcnn_wnorm_bwd", "svae_pcnn_conv", "sv
                  "svae_pcnn_gate_bwd", "svae_pcnn_gemm_small", "svae_pcnn_imgsum", "svae_pcnn_copy",
                  "svae_pcnn_pad_ones", "svae_pcnn_mixlogistic", "svae_pcnn_sum", "svae_pcnn_sample",
                  "svae_pcnn_highway", "svae_pcnn_wn_init", "svae_pcnn_adam", "svae_pcnn_ema", "svae_pcnn_sample_bwd",
-                 "svae_pcnn_highway_bwd", "svae_pcnn_dropout"]
+                 "svae_pcnn_highway_bwd", "svae_pcnn_dropout", "svae_pcnn_sqerr"]
 
 # bf16 GEMM instance ids (csrc/kernels.h KernelId) for svae_probe_begin
 KID_IGEMM_BF16_256x32 = 2

@@ -1004,7 +1004,7 @@ static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, V
     }
   }
   // image-space stride-2 conv with Cin <= 3: im2col in LDS, MFMA over pixel chunks
-  if (bfk && wgrad_smallc(w, groups, c->slab, c->slab_cap, dW, w_gs, c->st)) return 0;
+  if ((bfk || c->m.g.split) && wgrad_smallc(w, groups, c->slab, c->slab_cap, dW, w_gs, c->st)) return 0;
   if (bfk)  // tap-merged tiles; longer splits (less slab traffic)
     choose_split(w.rows, 1, wgrad_bf16_tiles(w), groups, 16LL * w.M * w.N, c->slab_cap, w.nsplit, w.chunk, 2048,
                  256);
@@ -1735,9 +1735,10 @@ static int engine_backward(svae_ctx* c) {
                      256);
       else
         choose_split(w.rows, 16, (F[1] + 127) / 128, 1, 16LL * M_out * F[1], c->slab_cap, w.nsplit, w.chunk);
+      w.nsp = g.split ? 2 : 1;
       on_side(c, c->ev_da_ready, nullptr, [&] {
         w.part = c->slab;
-        const int ns = bfk ? wgrad_smallc_part(w, 1, c->slab, c->slab_cap, c->st) : 0;
+        const int ns = (bfk || g.split) ? wgrad_smallc_part(w, 1, c->slab, c->slab_cap, c->st) : 0;
         if (ns) w.nsplit = ns;  // LDS im2col kernel (wgrad_smallc.hip)
         else wgemm(c, w, 1);
         wgrad_reduce(c->slab, 0, w.nsplit, 16, M_out, F[1], c->Gr + G.owout, 0, g.C,

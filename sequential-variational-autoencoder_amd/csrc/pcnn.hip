@@ -872,6 +872,28 @@ __global__ void dropout_kernel(const float* __restrict__ x, long long rows, int 
   }
 }
 
+// per-image mean squared error and its gradient (the chain's reconstruction term on the head's
+// output, compute_and_accumulate_loss :1146): rec[b] = mean_i (a - t)^2, da = coef * 2 (a - t) / per_img
+__global__ __launch_bounds__(256) void sqerr_kernel(const float* __restrict__ a, const float* __restrict__ t,
+                                                    long long per_img, float coef, float* __restrict__ rec,
+                                                    float* __restrict__ da) {
+  __shared__ float red[256];
+  const long long o = (long long)blockIdx.x * per_img;
+  float acc = 0.f;
+  for (long long i = threadIdx.x; i < per_img; i += 256) {
+    const float d = a[o + i] - t[o + i];
+    acc += d * d;
+    if (da) da[o + i] = coef * 2.f * d / (float)per_img;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && rec) rec[blockIdx.x] = red[0] / (float)per_img;
+}
+
 __global__ void highway_kernel(const float* __restrict__ s, const float* __restrict__ prev,
                                const float* __restrict__ z, const float* __restrict__ zb, long long per_img,
                                long long total, float lo, float hi, float* __restrict__ out) {
@@ -1161,6 +1183,13 @@ int svae_pcnn_highway_bwd(const float* s, const float* prev, const float* z, con
   if (!s || !prev || !z || !dout || !dz || nimg < 1 || per_img < 1) return bad("pcnn_highway_bwd: bad arguments");
   hipLaunchKernelGGL(highway_bwd_kernel, dim3(nimg), dim3(256), 0, (hipStream_t)stream, s, prev, z, zb,
                      (long long)per_img, lo, hi, dout, ds, dprev, prev_acc, dz);
+  return hipchk();
+}
+
+int svae_pcnn_sqerr(const float* a, const float* t, int nimg, int64_t per_img, float coef, float* rec, float* da,
+                    void* stream) {
+  if (!a || !t || nimg < 1 || per_img < 1 || (!rec && !da)) return bad("pcnn_sqerr: bad arguments");
+  hipLaunchKernelGGL(sqerr_kernel, dim3(nimg), dim3(256), 0, (hipStream_t)stream, a, t, (long long)per_img, coef, rec, da);
   return hipchk();
 }
 

@@ -26,6 +26,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "opload.h"
 
 typedef __bf16 sc_bf16x8 __attribute__((ext_vector_type(8)));
 typedef float sc_f32x8 __attribute__((ext_vector_type(8)));
@@ -51,25 +52,29 @@ __device__ __forceinline__ sc_bf16x8 sc_join(sc_v4i16 lo, sc_v4i16 hi) {
 
 struct SCArgs {
   const float* X; long long x_gs;        // input image, fp32 NHWC [B][64][64][CI] (row-contiguous)
-  const __bf16* D; long long d_gs; int ldd;  // dpre, bf16 [B*32*32][ldd]
+  const void* D; long long d_gs; int ldd;  // dpre [B*32*32][ldd]: bf16 (NSP = 1) or fp32 (NSP = 2)
   float* part; long long p_gs;           // [split][16][CI][N] partials (or dW when nsplit == 1)
   int N, nsplit, nchunk, Hi;             // Hi = 64 (input rows per image)
 };
 
-template <int CI>
+// NSP = 2: the split-bf16 mode (dtype bf16x6's weight gradients, opload.h): fp32 dpre, the im2col
+// vectors and the dpre rows staged as hi / lo bf16 planes, three MFMAs per fragment pair
+template <int CI, int NSP = 1>
 __global__ __launch_bounds__(256) void wgrad_smallc_kernel(SCArgs a) {
   constexpr int MP = 16 * CI;             // im2col length
   constexpr int NPL = (MP + 31) / 32;     // 32-column planes
   constexpr int XROW = SC_WI * CI;        // floats of one input row
   constexpr int XQ = SC_WR * XROW / 4;    // float4 items of the chunk's input rows
   constexpr int XI = (XQ + 255) / 256;    // per thread
-  constexpr int DI = SC_CP * 4 / 256;     // 16-byte dpre items per thread (4 per pixel)
+  constexpr int DI = SC_CP * 4 / 256;     // dpre items per thread (4 per pixel, 8 elements each)
   static_assert(XROW % 4 == 0, "input rows are float4 multiples");
-  // LDS: x window (fp32) | im2col planes (bf16) | dpre rows (bf16); reused for the wave reduction
+  // LDS: x window (fp32) | im2col planes (bf16) x NSP | dpre rows (bf16) x NSP; reused for the wave reduction
   extern __shared__ __attribute__((aligned(16))) char wsc_lds[];
   float* xw = (float*)wsc_lds;                                          // [SC_WR][SC_WC][CI]
-  __bf16* ap = (__bf16*)(wsc_lds + SC_WR * SC_WC * CI * 4);              // [NPL][SC_CP][32]
-  __bf16* dr = (__bf16*)(wsc_lds + SC_WR * SC_WC * CI * 4 + NPL * SC_CP * 64);  // [SC_CP][32]
+  __bf16* ap = (__bf16*)(wsc_lds + SC_WR * SC_WC * CI * 4);              // [NSP][NPL][SC_CP][32]
+  __bf16* dr = (__bf16*)(wsc_lds + SC_WR * SC_WC * CI * 4 + NSP * NPL * SC_CP * 64);  // [NSP][SC_CP][32]
+  constexpr int APL = NPL * SC_CP * 32;   // bf16 elements of one split plane of ap
+  constexpr int DPL = SC_CP * 32;         // ... of dr
   static_assert((SC_WR * SC_WC * CI * 4) % 16 == 0, "16-byte aligned planes");
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -79,7 +84,8 @@ __global__ __launch_bounds__(256) void wgrad_smallc_kernel(SCArgs a) {
   const int cbeg = (int)((long long)a.nchunk * split / a.nsplit);
   const int cend = (int)((long long)a.nchunk * (split + 1) / a.nsplit);
   const float* X = a.X + group * a.x_gs;
-  const __bf16* D = a.D + group * a.d_gs;
+  const __bf16* D = (const __bf16*)a.D + group * a.d_gs;
+  const float* Df = (const float*)a.D + group * a.d_gs;
   constexpr int PER_IMG = SC_WO * SC_WO;
 
   // zero columns of the window and the im2col columns past MP: written once
@@ -90,10 +96,13 @@ __global__ __launch_bounds__(256) void wgrad_smallc_kernel(SCArgs a) {
   }
   if (MP % 32) {
 #pragma unroll
-    for (int m = MP; m < NPL * 32; m += 8) *(sc_bf16x8*)&ap[((m >> 5) * SC_CP + tid) * 32 + (m & 31)] = sc_bf16x8{};
+    for (int p = 0; p < NSP; ++p)
+#pragma unroll
+      for (int m = MP; m < NPL * 32; m += 8)
+        *(sc_bf16x8*)&ap[p * APL + ((m >> 5) * SC_CP + tid) * 32 + (m & 31)] = sc_bf16x8{};
   }
 
-  f32x4 xv[XI], dv[DI];
+  f32x4 xv[XI], dv[DI][NSP];
   auto load_chunk = [&](int c) {
     const int r0 = c * SC_CP;
     const int img = r0 / PER_IMG, oy0 = (r0 - img * PER_IMG) / SC_WO;
@@ -112,7 +121,13 @@ __global__ __launch_bounds__(256) void wgrad_smallc_kernel(SCArgs a) {
     for (int i = 0; i < DI; ++i) {
       const int it = tid + 256 * i;
       const int k = it >> 2, sl = it & 3;
-      dv[i] = *(const f32x4*)(D + (long long)(r0 + k) * a.ldd + n0 + sl * 8);
+      const long long o = (long long)(r0 + k) * a.ldd + n0 + sl * 8;
+      if constexpr (NSP == 1) {
+        dv[i][0] = *(const f32x4*)(D + o);
+      } else {  // 8 fp32 in the two registers, split at the LDS store
+        dv[i][0] = *(const f32x4*)(Df + o);
+        dv[i][1] = *(const f32x4*)(Df + o + 4);
+      }
     }
   };
 
@@ -144,7 +159,15 @@ __global__ __launch_bounds__(256) void wgrad_smallc_kernel(SCArgs a) {
 #pragma unroll
     for (int i = 0; i < DI; ++i) {
       const int it = tid + 256 * i;
-      *(f32x4*)&dr[(it >> 2) * 32 + (it & 3) * 8] = dv[i];
+      const int o = (it >> 2) * 32 + (it & 3) * 8;
+      if constexpr (NSP == 1) {
+        *(f32x4*)&dr[o] = dv[i][0];
+      } else {
+        ol_bf16x8 pl[NSP];
+        split8<NSP>(dv[i][0], dv[i][1], pl);
+#pragma unroll
+        for (int p = 0; p < NSP; ++p) *(ol_bf16x8*)&dr[p * DPL + o] = pl[p];
+      }
     }
     __syncthreads();
     // im2col of pixel tid: m = (ky*4 + kx)*CI + ci
@@ -159,8 +182,16 @@ __global__ __launch_bounds__(256) void wgrad_smallc_kernel(SCArgs a) {
           for (int ci = 0; ci < CI; ++ci) v[(ky * 4 + kx) * CI + ci] = xw[((2 * oyl + ky) * SC_WC + 2 * ox + kx) * CI + ci];
 #pragma unroll
       for (int m = 0; m < MP; m += 8) {
-        const sc_f32x8 w8 = {v[m], v[m + 1], v[m + 2], v[m + 3], v[m + 4], v[m + 5], v[m + 6], v[m + 7]};
-        *(sc_bf16x8*)&ap[((m >> 5) * SC_CP + tid) * 32 + (m & 31)] = __builtin_convertvector(w8, sc_bf16x8);
+        const int o = ((m >> 5) * SC_CP + tid) * 32 + (m & 31);
+        if constexpr (NSP == 1) {
+          const sc_f32x8 w8 = {v[m], v[m + 1], v[m + 2], v[m + 3], v[m + 4], v[m + 5], v[m + 6], v[m + 7]};
+          *(sc_bf16x8*)&ap[o] = __builtin_convertvector(w8, sc_bf16x8);
+        } else {
+          ol_bf16x8 pl[NSP];
+          split8<NSP>(f32x4{v[m], v[m + 1], v[m + 2], v[m + 3]}, f32x4{v[m + 4], v[m + 5], v[m + 6], v[m + 7]}, pl);
+#pragma unroll
+          for (int p = 0; p < NSP; ++p) *(ol_bf16x8*)&ap[p * APL + o] = pl[p];
+        }
       }
     }
     __syncthreads();
@@ -170,12 +201,19 @@ __global__ __launch_bounds__(256) void wgrad_smallc_kernel(SCArgs a) {
 #pragma unroll
     for (int j = 0; j < SC_CP / 16 / 4; ++j) {
       const int k0 = (j * 4 + wave) * 16;
-      const sc_bf16x8 bf = sc_join(sc_tr16(Db + dbyte + k0 * 64), sc_tr16(Db + dbyte + (k0 + 4) * 64));
+      ol_bf16x8 bf[NSP];
+#pragma unroll
+      for (int p = 0; p < NSP; ++p)
+        bf[p] = sc_join(sc_tr16(Db + p * DPL * 2 + dbyte + k0 * 64), sc_tr16(Db + p * DPL * 2 + dbyte + (k0 + 4) * 64));
 #pragma unroll
       for (int pl = 0; pl < NPL; ++pl) {
-        const char* Ap = A + pl * SC_CP * 64;
-        const sc_bf16x8 af = sc_join(sc_tr16(Ap + abyte + k0 * 64), sc_tr16(Ap + abyte + (k0 + 4) * 64));
-        acc[pl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc[pl], 0, 0, 0);
+        ol_bf16x8 af[NSP];
+#pragma unroll
+        for (int p = 0; p < NSP; ++p) {
+          const char* Ap = A + p * APL * 2 + pl * SC_CP * 64;
+          af[p] = sc_join(sc_tr16(Ap + abyte + k0 * 64), sc_tr16(Ap + abyte + (k0 + 4) * 64));
+        }
+        acc[pl] = mfma_split<NSP>(af, bf, acc[pl]);
       }
     }
   }
@@ -222,25 +260,32 @@ int wgrad_smallc_ok(const WgArgs& w) {
   if (wgrad_smallc_disabled()) return 0;
   if (g.mode != GM_CONV || g.ksz != 4 || g.stride != 2 || g.pad != 1 || w.ntap != 16) return 0;
   if (g.Ho != SC_WO || g.Wo != SC_WO || g.Hi != 2 * SC_WO || g.Wi != 2 * SC_WO) return 0;
-  if (w.M < 1 || w.M > 4 || w.ldg != w.M || w.g_bf16 || !w.d_bf16) return 0;
+  if (w.M < 1 || w.M > 4 || w.ldg != w.M || w.g_bf16) return 0;
+  if (w.nsp > 1 ? w.d_bf16 != 0 : !w.d_bf16) return 0;  // bf16 dpre, or fp32 dpre for the split planes
   if (w.N % 32 || w.ldd % 8) return 0;
   return w.rows % SC_CP == 0 && w.rows % (SC_WO * SC_WO) == 0;
 }
 
-template <int CI>
+template <int CI, int NSP>
 size_t wsc_lds_bytes() {
   constexpr int NPL = (16 * CI + 31) / 32;
-  return (size_t)SC_WR * SC_WC * CI * 4 + (size_t)NPL * SC_CP * 64 + (size_t)SC_CP * 64;
+  return (size_t)SC_WR * SC_WC * CI * 4 + NSP * ((size_t)NPL * SC_CP * 64 + (size_t)SC_CP * 64);
 }
-template <int CI>
-void wsc_launch(const SCArgs& a, dim3 grid, hipStream_t s) {
+template <int CI, int NSP>
+void wsc_launch1(const SCArgs& a, dim3 grid, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)wgrad_smallc_kernel<CI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)wsc_lds_bytes<CI>());
+    hipFuncSetAttribute((const void*)wgrad_smallc_kernel<CI, NSP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)wsc_lds_bytes<CI, NSP>());
     attr = true;
   }
-  hipLaunchKernelGGL(wgrad_smallc_kernel<CI>, grid, dim3(256), wsc_lds_bytes<CI>(), s, a);
+  const size_t lds = wsc_lds_bytes<CI, NSP>();
+  hipLaunchKernelGGL((wgrad_smallc_kernel<CI, NSP>), grid, dim3(256), lds, s, a);
+}
+template <int CI>
+void wsc_launch(const SCArgs& a, int nsp, dim3 grid, hipStream_t s) {
+  if (nsp > 1) wsc_launch1<CI, 2>(a, grid, s);
+  else wsc_launch1<CI, 1>(a, grid, s);
 }
 
 // partials [split][16][M][N] of an eligible layer into part (group stride nsplit*16*M*N), ~512
@@ -250,7 +295,7 @@ int wgrad_smallc_part(const WgArgs& w, int groups, float* part, long long cap, h
   if (!wgrad_smallc_ok(w)) return 0;
   SCArgs a;
   a.X = w.G; a.x_gs = w.g_gs;
-  a.D = (const __bf16*)w.D; a.d_gs = w.d_gs; a.ldd = w.ldd;
+  a.D = w.D; a.d_gs = w.d_gs; a.ldd = w.ldd;
   a.N = w.N;
   a.Hi = 2 * SC_WO;
   a.nchunk = w.rows / SC_CP;
@@ -264,10 +309,10 @@ int wgrad_smallc_part(const WgArgs& w, int groups, float* part, long long cap, h
   a.p_gs = (long long)a.nsplit * per;
   dim3 grid(a.nsplit, w.N / 32, groups);
   switch (w.M) {
-    case 1: wsc_launch<1>(a, grid, s); break;
-    case 2: wsc_launch<2>(a, grid, s); break;
-    case 3: wsc_launch<3>(a, grid, s); break;
-    default: wsc_launch<4>(a, grid, s); break;
+    case 1: wsc_launch<1>(a, w.nsp, grid, s); break;
+    case 2: wsc_launch<2>(a, w.nsp, grid, s); break;
+    case 3: wsc_launch<3>(a, w.nsp, grid, s); break;
+    default: wsc_launch<4>(a, w.nsp, grid, s); break;
   }
   return a.nsplit;
 }

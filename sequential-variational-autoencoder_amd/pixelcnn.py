@@ -159,6 +159,8 @@ class PixelCNNpp:
         self._dh = None
         self._tape, self._g, self._keep, self._same, self._cnt = [], {}, [], {}, {}
         self._record = self._init = False
+        self._dropout_p, self._masks, self.last_masks = 0.0, None, []
+        self.probe, self.probe_cap = None, 0  # [(flops, event, event)] of timed forward conv launches
         self.conv_flops = 0.0  # running total of forward conv FLOPs (tools/bench_pcnn.py)
 
     # ---------------- parameters ----------------
@@ -251,9 +253,16 @@ class PixelCNNpp:
         acc = out is not None
         if out is None:
             out = Act(self._new(x.n * ho * wo, cout), cout, x.n, ho, wo)
+        pr = self.probe is not None and len(self.probe) < self.probe_cap
+        if pr:  # bench.py's live roofline probe: an event pair around this forward conv launch
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         _ck(L.svae_pcnn_conv(x.ptr(), x.n, x.h, x.w, cin, x.ld, ctypes.c_void_p(wkf.data_ptr()), kf,
                              _p(self.P, off_b), out.ptr(), ho, wo, cout, out.ld, kh, kw, s, pt, pl, mode,
                              1 if acc else 0, zero_edge, st))
+        if pr:
+            e1.record()
+            self.probe.append((2.0 * x.n * ho * wo * cout * cin * taps / (s * s if mode == 1 else 1), e0, e1))
         if self._init:  # data-dependent init: this layer's g, b from the moments of its own output
             # (before any shift or sum), which is passed on un-normalised (tf.identity of the old x)
             src = out
@@ -366,8 +375,38 @@ class PixelCNNpp:
         if a is not None:
             self._dense_into(self._nonlin(a, nl), self._nm("dense"), c1)
         t2 = self._nonlin(c1, nl)
+        mask = self._next_mask(t2.rows, t2.c)
+        if mask is not None:  # training-pass dropout (nn.py:273-274)
+            t2 = self._dropout(t2, mask)
         c2 = self._wconv(t2, self._nm("conv2d"), 2 * x.c, kh, kw, 1, pt, pl, init_scale=0.1)
         return self._gate(x, c2, h, self._nm("conditional_weights") + "/hw")
+
+    def _next_mask(self, rows, c):
+        """The next gated resnet's dropout mask (1 / keep_prob where kept, else 0; tf.nn.dropout,
+        nn.py:273-274): from the injected list (parity), else drawn on the device when dropout_p > 0.
+        Every mask used is appended to ``self.last_masks``."""
+        if self._masks is not None:
+            m = next(self._masks)
+            m = torch.as_tensor(m, dtype=torch.float32, device=self.dev).reshape(rows, c).contiguous()
+        elif self._dropout_p > 0.0:
+            keep = 1.0 - self._dropout_p
+            m = (torch.rand(rows, c, device=self.dev) < keep).to(torch.float32) * (1.0 / keep)
+        else:
+            return None
+        self.last_masks.append(m)
+        return m
+
+    def _dropout(self, x, mask):
+        y = Act(self._new(x.rows, x.c), x.c, x.n, x.h, x.w)
+        _ck(self.L.svae_pcnn_dropout(x.ptr(), x.rows, x.c, x.ld, _p(mask), y.ptr(), y.ld, self._st()))
+        if self._record:
+            def bwd():  # x (a fresh nonlinearity output) has no other consumer: its gradient is written
+                if not self._has_grad(y):
+                    return
+                _ck(self.L.svae_pcnn_dropout(_p(self._grad(y)), x.rows, x.c, x.c, _p(mask), _p(self._grad(x)), x.c,
+                                             self._st()))
+            self._tape.append(bwd)
+        return y
 
     def _dense_into(self, x, name, out):
         self._wconv(self._view(x, x.rows, 1, 1), name, out.c, 1, 1, 1, 0, 0, out=self._view(out, out.rows, 1, 1))
@@ -377,10 +416,15 @@ class PixelCNNpp:
         self._cnt[kind] = i + 1
         return "%s_%d" % (kind, i)
 
-    def _run(self, x, h, record, init=False):
-        """model_spec(x, h) (model.py:11-117) -> l Act [rows][10 M]."""
+    def _run(self, x, h, record, init=False, dropout_p=0.0, masks=None):
+        """model_spec(x, h) (model.py:11-117) -> l Act [rows][10 M].  dropout_p > 0: the training
+        pass's dropout in every gated resnet, masks injected (``masks``, in gated-resnet order) or
+        drawn on the device."""
         s = self.s
         self._record, self._init = record, init
+        self._dropout_p = float(dropout_p)
+        self._masks = iter(masks) if masks is not None else None
+        self.last_masks = []
         self._tape, self._g, self._keep, self._same, self._cnt = [], {}, [], {}, {}
         self._nograd = set()
         B, H, W = x.shape[0], s["H"], s["W"]
@@ -458,11 +502,34 @@ class PixelCNNpp:
         nll = -float(tot.item())
         return (nll, dh) if grad_h else nll
 
-    def data_init(self, x, h):
+    def forward_train(self, x, h, dropout_p=0.0, masks=None):
+        """l = model_spec(x, h) of the training pass (dropout in the gated resnets), with the tape
+        kept for backward_from.  Returns l [B, H, W, 10 M] (the tape's own buffer)."""
+        x, h = self._inputs(x, h)
+        self._fw_in = (x, h)
+        l = self._run(x, h, record=True, dropout_p=dropout_p, masks=masks)
+        self._fw_l = l
+        return l.buf.view(x.shape[0], self.s["H"], self.s["W"], 10 * self.s["M"])
+
+    def backward_from(self, dl, grad_h=True):
+        """Backward of the last forward_train from dl = d loss / d l ([rows][10 M] device tensor): every
+        parameter's gradient is WRITTEN into ``self.G`` (zeroed first); returns d loss / d h [B, K]."""
+        x, _ = self._fw_in
+        self.G.zero_()
+        self._grad(self._fw_l).copy_(dl.reshape(self._fw_l.rows, self._fw_l.c))
+        self._dh = torch.zeros(x.shape[0], self.s["K"], dtype=torch.float32, device=self.dev) if grad_h else None
+        for fn in reversed(self._tape):
+            fn()
+        dh, self._dh = self._dh, None
+        self._drop()
+        self._fw_in = self._fw_l = None
+        return dh
+
+    def data_init(self, x, h, dropout_p=0.0, masks=None):
         """The data-dependent init pass (pixelvae.py:103-105): every weight-normed layer's g, b from
         its own output moments, in construction order (nn.py:176-180, :206-210)."""
         x, h = self._inputs(x, h)
-        self._run(x, h, record=False, init=True)
+        self._run(x, h, record=False, init=True, dropout_p=dropout_p, masks=masks)
         self._init = False
         self._drop()
 

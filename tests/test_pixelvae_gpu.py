@@ -1,0 +1,130 @@
+"""The c_pixelvae chain (BASELINE.json configs[4]; sequential_vae.py:529-543, generator_pixelcnn
+:1943-1971, pixel_cnn/pixelvae.py:68-158 repaired) on the GPU against oracle/pixelvae.py (fp64 torch,
+PARITY UNPINNED: the reference glue cannot run, see that module's header).
+
+Small geometry (16x16, a 4-level ladder, a 1-resnet 8-filter head with 2 mixtures), B = 4, T = 2,
+shared theta / phi, injected eps, sampler uniforms and dropout keep-masks (p = 0.3).  The engine
+runs fp32 (parity mode); the head is bf16 MFMA (its only mode), compared against the oracle with
+the same bf16 operand rounding.  Bounds:
+  loss, step-0 recon / KL, x_hat_0          : 1e-4 rel (the engine's fp32 bounds)
+  x_hat_1 (the head's highway output)         : 1e-3 rel L2
+  engine gradients (via d/dz_1, d/dx_hat_0)   : vector 2e-2, per-tensor median 1e-2 (the head's
+                                                backward is bf16, the oracle's is not)
+  head gradients                              : vector 3e-2, per-tensor median 1e-2
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import pkg_mod
+from oracle import pcnn as opc
+from oracle import pixelvae as opv
+from oracle import spec
+
+pytestmark = pytest.mark.gpu
+
+GEO = dict(height=16, width=16, filter_sizes=[3, 8, 8, 16, 16, 32], latent_dims=[2, 2, 2, 2], batch=4)
+HEAD = dict(nr_resnet=1, nr_filters=8, nr_mix=2)
+
+
+def _rel(a, b):
+    return float(np.linalg.norm(np.ravel(a) - np.ravel(b)) / max(np.linalg.norm(np.ravel(b)), 1e-30))
+
+
+def _setup(dtype="fp32", seed=0):
+    PV = pkg_mod("pixelvae").PixelVAE
+    pv = PV("c_pixelvae", head=HEAD, seed=seed, dtype=dtype, **GEO)
+    c = pv.cfg
+    cd = spec.make_config("tiny", H=16, W=16, C=3, levels=4, filter_sizes=GEO["filter_sizes"],
+                          latent_dims=GEO["latent_dims"], mc_steps=2, batch=4, latent_mean_clip=4.0,
+                          min_highway=0.2, max_highway=0.8, regularized_steps=(0,), first_step_loss_coeff=2.0)
+    cd["share_theta"] = cd["share_phi"] = True
+    ospec = opc.make_spec(H=16, W=16, K=c.latent_dim, **HEAD)
+    hp = opc.init_params(ospec, seed + 11)
+    pv.head.set_params(hp)
+    x, tgt, eps = spec.make_inputs(cd, batch=4)
+    rng = np.random.default_rng(seed + 5)
+    u_mix = rng.uniform(1e-5, 1 - 1e-5, (4, 16, 16, HEAD["nr_mix"]))
+    u_log = rng.uniform(1e-5, 1 - 1e-5, (4, 16, 16, 3))
+    return pv, cd, ospec, hp, x, tgt, eps, u_mix, u_log, rng
+
+
+def _masks(rng, pv, p=0.3):
+    """keep-masks (1 / keep or 0) in the head's gated-resnet order: their shapes come from a dry
+    training pass of the head (recorded in head.last_masks)."""
+    return [np.where(rng.uniform(size=tuple(m.shape)) < 1 - p, 1.0 / (1 - p), 0.0) for m in pv.head.last_masks]
+
+
+def test_pixelvae_step_matches_oracle():
+    pv, cd, ospec, hp, x, tgt, eps, u_mix, u_log, rng = _setup()
+    pv.forward(x, tgt, eps, 0.6, u_mix, u_log)      # dry pass: mask shapes
+    masks = _masks(rng, pv)
+    pv.forward(x, tgt, eps, 0.6, u_mix, u_log, masks=masks)
+    pv.backward()
+    torch.cuda.synchronize()
+    loss = pv.loss_value()
+    x0, x1 = pv.xhat(0).cpu().numpy(), pv.xhat(1).cpu().numpy()
+    g_eng = pv.vae.grad_dict()
+    g_head = pv.head.grads()
+    o = opv.forward_backward(cd, pv.vae.param_dict(), ospec, hp, x, tgt, eps, 0.6, u_mix, u_log, masks)
+    el = abs(loss - o["loss"]) / abs(o["loss"])
+    e0, e1 = _rel(x0, o["xhat"][0]), _rel(x1, o["xhat"][1])
+    live = [k for k, v in o["grads"].items() if np.linalg.norm(v) > 1e-7]
+    cat = lambda d, ks: np.concatenate([np.ravel(d[k]) for k in ks])
+    gv = _rel(cat(g_eng, live), cat(o["grads"], live))
+    gm = float(np.median([_rel(g_eng[k], o["grads"][k]) for k in live]))
+    hlive = [k for k, v in o["head_grads"].items() if np.linalg.norm(v) > 1e-9]
+    hv = _rel(cat(g_head, hlive), cat(o["head_grads"], hlive))
+    hm = float(np.median([_rel(g_head[k], o["head_grads"][k]) for k in hlive]))
+    print("\nc_pixelvae small: loss %.6f oracle %.6f (rel %.2e); x_hat_0 %.2e x_hat_1 %.2e; engine grads vector %.2e "
+          "median %.2e; head grads vector %.2e median %.2e" % (loss, o["loss"], el, e0, e1, gv, gm, hv, hm))
+    assert el <= 1e-4
+    assert abs(pv.recon(0) - o["rec"][0]) <= 1e-4 * abs(o["rec"][0])
+    assert e0 <= 1e-4 and e1 <= 1e-3
+    assert gv <= 2e-2 and gm <= 1e-2
+    assert hv <= 3e-2 and hm <= 1e-2
+    # variables: the engine creates no encoder / generator for the head's step, the head owns its own
+    names = [p["name"] for p in pv.vae.table]
+    assert not any("encoder" in n or "generative_network" in n for n in names)
+    assert any(n.startswith("phi/inference_network/") for n in names)
+    pv.close()
+
+
+def test_pixelvae_train_and_generate():
+    pv, cd, ospec, hp, x, tgt, eps, u_mix, u_log, rng = _setup()
+    p0 = pv.head.P.clone()
+    losses = [pv.train(x, tgt) for _ in range(3)]
+    torch.cuda.synchronize()
+    assert all(np.isfinite(losses)) and pv.vae.adam_updates == 3 and pv.head.iteration == 3
+    assert pv.head.ema is not None and not torch.equal(pv.head.P, p0)
+    assert torch.isfinite(pv.vae.grads).all() and torch.isfinite(pv.head.G).all()
+    out = pv.generate_mc_samples()
+    assert len(out) == 2 and all(o.shape == (4, 16, 16, 3) for o in out)
+    assert all(np.isfinite(o).all() for o in out) and np.abs(out[1]).max() <= 1.0 + 1e-6
+    pv.close()
+
+
+def test_pixelvae_full_size_properties():
+    """c_pixelvae at 64x64 with the reference head (nr_resnet 3, 160 filters, 10 mixtures), B = 8:
+    finite gradients, and the step is deterministic given its randomness (eps, uniforms, masks)."""
+    PV = pkg_mod("pixelvae").PixelVAE
+    pv = PV("c_pixelvae", batch_size=8, dtype="bf16")
+    c = pv.cfg
+    rng = np.random.default_rng(0)
+    x = rng.uniform(-1, 1, (8, 64, 64, 3)).astype(np.float32)
+    eps = rng.standard_normal((2, 8, c.latent_dim)).astype(np.float32)
+    um = rng.uniform(1e-5, 1 - 1e-5, (8, 64, 64, 10))
+    ul = rng.uniform(1e-5, 1 - 1e-5, (8, 64, 64, 3))
+    pv.forward(x, x, eps, 1.0, um, ul)
+    masks = [m.clone() for m in pv.head.last_masks]
+    res = []
+    for _ in range(2):
+        pv.forward(x, x, eps, 1.0, um, ul, masks=masks)
+        pv.backward()
+        torch.cuda.synchronize()
+        res.append((pv.loss_value(), pv.vae.grads.clone(), pv.head.G.clone()))
+    assert np.isfinite(res[0][0])
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
+    assert torch.isfinite(res[0][1]).all() and torch.isfinite(res[0][2]).all()
+    pv.close()
