@@ -36,6 +36,8 @@ struct KwArgs {
   int npix;     // nimg * PR * PC
   // launch-constant divisors (multiply-shift): the kernel's index decode has no integer divisions
   FastDiv d_win, d_pc, d_img, d_wr, d_rimg, d_q, d_qw;  // PR*PC, PC, Hr*Wr, Wr, R*Wr, (Ho/2)*(Wo/2), Wo/2
+  int ntx, nty, ntz;  // tiles along rows / columns / (groups x classes)
+  int tpb;            // tiles per block: 1 = one tile per block (3-D grid); > 1 = persistent (1-D grid)
 };
 
 namespace {
@@ -55,8 +57,9 @@ __device__ __forceinline__ long long kw_out_row(const KwArgs& h, const ConvGeom&
 // NS = 3: the split-bf16 mode (dtype bf16x6, opload.h split8 / mfma_split): the fp32 window is
 // staged as three bf16 planes (one LDS buffer, restaged under a second barrier per chunk) and every
 // A x B fragment pair runs the six plane products; B comes from the three shadow planes
-template <int BM, int BN, bool S2T, bool ABF, int NS = 1>
-__global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64) ? 4 : 2) void igemm_halo_kw_kernel(KwArgs h) {
+// PST: the persistent form (h.tpb > 1 tiles per block, 1-D grid); without it the tile loop runs once
+template <int BM, int BN, bool S2T, bool ABF, int NS = 1, bool PST = false>
+__global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64 && !PST) ? 4 : 2) void igemm_halo_kw_kernel(KwArgs h) {
   static_assert(NS == 1 || (NS == 3 && !ABF), "split planes from fp32 activations only");
   constexpr int TM = BM / 32;
   constexpr int TN = BN / 32;
@@ -69,59 +72,91 @@ __global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64) ? 4 : 2) void ig
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
-  const BlockXYZ blk = xcd_block();
-  const int group = blk.z / a.nclass, cls = blk.z - group * a.nclass;
-  const int m0 = blk.x * BM, n0 = blk.y * BN;
-  const long long a0 = group * a.a_gs;  // element offset of this group's A (fp32 or bf16)
   constexpr bool abf = ABF;
-  const __bf16* Bw = (const __bf16*)a.Bh + group * a.b_gs;
   const int nchunk = a.Cin / KW_CK;
-
-  // ---- window origin and tap geometry (uniform; igemm_halo_kernel's) ----
   const int per_img = h.Hr * h.Wr;
-  const int img0 = fdiv(m0, h.d_img);
-  const int ry0 = fdiv(m0 - img0 * per_img, h.d_wr);
-  int oy_min, ox_min, tap0, toff0, tsgn;
+
+  // ---- tiles of this block: one (3-D XCD-ordered grid), or a contiguous run of tpb tiles of the
+  // linear order (x fastest, then y, then z) in the persistent form (1-D grid): tile i + 1's
+  // window and B fragments are loaded while tile i's last chunk computes and its epilogue runs ----
+  long long t_cur, t_end;
+  int bx, by, bz;
+  if constexpr (!PST) {
+    const BlockXYZ blk = xcd_block();
+    bx = blk.x; by = blk.y; bz = blk.z;
+    t_cur = 0; t_end = 1;
+  } else {
+    const long long ntiles = (long long)h.ntx * h.nty * h.ntz;
+    t_cur = (long long)blockIdx.x * h.tpb;
+    t_end = t_cur + h.tpb < ntiles ? t_cur + h.tpb : ntiles;
+    bx = (int)(t_cur % h.ntx); by = (int)((t_cur / h.ntx) % h.nty); bz = (int)(t_cur / ((long long)h.ntx * h.nty));
+  }
+
+  // per-tile geometry (uniform): the current tile's, and the next one's while its loads are issued
+  struct TileG {
+    int m0, n0, group, cls, tap0;
+  };
+  auto tile_geo = [&](int x, int y, int z) {
+    TileG q;
+    q.group = z / a.nclass;
+    q.cls = z - q.group * a.nclass;
+    q.m0 = x * BM;
+    q.n0 = y * BN;
+    q.tap0 = 0;
+    if (S2T) {
+      const int cy = q.cls >> 1, cx = q.cls & 1;
+      q.tap0 = ((cy + g.pad) & 1) * 4 + ((cx + g.pad) & 1);
+    }
+    return q;
+  };
+  // tap shift constants (the same for every tile of a launch)
+  int toff0, tsgn;
   if (S2T) {
-    const int cy = cls >> 1, cx = cls & 1;
-    const int ky0 = (cy + g.pad) & 1, kx0 = (cx + g.pad) & 1;
-    oy_min = (cy + g.pad - ky0) / 2 - 1;
-    ox_min = (cx + g.pad - kx0) / 2 - 1;
-    tap0 = ky0 * 4 + kx0;
     toff0 = h.PC + 1;
     tsgn = -1;
   } else if (g.mode == GM_CONV) {
-    oy_min = ox_min = -g.pad;
-    tap0 = 0;
     toff0 = 0;
     tsgn = 1;
   } else {
-    oy_min = ox_min = g.pad - 3;
-    tap0 = 0;
     toff0 = 3 * h.PC + 3;
     tsgn = -1;
   }
-  const int iy_base = ry0 * h.sy + oy_min;
 
   int woff[KW_PI];
-#pragma unroll
-  for (int i = 0; i < KW_PI; ++i) {
-    const int it = tid + 256 * i;
-    woff[i] = -2;  // -2: no item, -1: zero (outside the image)
-    if (it < h.npix * 4) {
-      const int pix = it >> 2, part = it & 3;
-      const int il = fdiv(pix, h.d_win);
-      const int r2 = pix - il * h.PR * h.PC;
-      const int pr = fdiv(r2, h.d_pc), pc = r2 - pr * h.PC;
-      const int iy = iy_base + pr, ix = ox_min + pc;
-      woff[i] = (iy >= 0 && iy < g.Hi && ix >= 0 && ix < g.Wi)
-                    ? (((img0 + il) * g.Hi + iy) * g.Wi + ix) * a.lda + part * 8
-                    : -1;
+  auto set_window = [&](const TileG& q) {  // window item offsets of tile q (igemm_halo_kernel's origin)
+    int oy_min, ox_min;
+    if (S2T) {
+      const int cy = q.cls >> 1, cx = q.cls & 1;
+      const int ky0 = (cy + g.pad) & 1, kx0 = (cx + g.pad) & 1;
+      oy_min = (cy + g.pad - ky0) / 2 - 1;
+      ox_min = (cx + g.pad - kx0) / 2 - 1;
+    } else if (g.mode == GM_CONV) {
+      oy_min = ox_min = -g.pad;
+    } else {
+      oy_min = ox_min = g.pad - 3;
     }
-  }
+    const int img0 = fdiv(q.m0, h.d_img);
+    const int ry0 = fdiv(q.m0 - img0 * per_img, h.d_wr);
+    const int iy_base = ry0 * h.sy + oy_min;
+#pragma unroll
+    for (int i = 0; i < KW_PI; ++i) {
+      const int it = tid + 256 * i;
+      woff[i] = -2;  // -2: no item, -1: zero (outside the image)
+      if (it < h.npix * 4) {
+        const int pix = it >> 2, part = it & 3;
+        const int il = fdiv(pix, h.d_win);
+        const int r2 = pix - il * h.PR * h.PC;
+        const int pr = fdiv(r2, h.d_pc), pc = r2 - pr * h.PC;
+        const int iy = iy_base + pr, ix = ox_min + pc;
+        woff[i] = (iy >= 0 && iy < g.Hi && ix >= 0 && ix < g.Wi)
+                      ? (((img0 + il) * g.Hi + iy) * g.Wi + ix) * a.lda + part * 8
+                      : -1;
+      }
+    }
+  };
   f32x4 wv[KW_PI][2];
-  auto load_window = [&](int chunk) {
-    const long long ac = a0 + chunk * KW_CK;
+  auto load_window = [&](const TileG& q, int chunk) {
+    const long long ac = q.group * a.a_gs + chunk * KW_CK;
 #pragma unroll
     for (int i = 0; i < KW_PI; ++i) {
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
@@ -149,7 +184,7 @@ __global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64) ? 4 : 2) void ig
     }
   };
 
-  // ---- A fragment bases: the whole BM-row tile, every wave ----
+  // ---- A fragment bases: the whole BM-row tile, every wave (the same for every tile) ----
   int abase[TM];
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
@@ -162,11 +197,11 @@ __global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64) ? 4 : 2) void ig
   }
 
   // ---- this wave's taps: t = wave * NTW + u; B fragments one chunk ahead ----
-  const __bf16* bptr = Bw + (long long)(n0 + l32) * a.ldb + 8 * hh;
   bf16x8 bq[NTW][TN][2][NS];
-  auto load_b = [&](int u, int chunk) {
+  auto load_b = [&](const TileG& q, int u, int chunk) {
+    const __bf16* bptr = (const __bf16*)a.Bh + q.group * a.b_gs + (long long)(q.n0 + l32) * a.ldb + 8 * hh;
     const int t = wave * NTW + u;
-    const int tap = S2T ? tap0 + 8 * (t >> 1) + 2 * (t & 1) : t;
+    const int tap = S2T ? q.tap0 + 8 * (t >> 1) + 2 * (t & 1) : t;
     const long long off = (long long)tap * a.b_tap + chunk * KW_CK;
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn)
@@ -177,128 +212,156 @@ __global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64) ? 4 : 2) void ig
           bq[u][tn][kq][p] = *(const bf16x8*)(bptr + p * a.b_plane + (long long)tn * 32 * a.ldb + off + kq * 16);
   };
 
-  f32x16 acc[TM][TN];
+  TileG cur = tile_geo(bx, by, bz);
+  set_window(cur);
+  load_window(cur, 0);
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  load_window(0);
-#pragma unroll
-  for (int u = 0; u < NTW; ++u) load_b(u, 0);
+  for (int u = 0; u < NTW; ++u) load_b(cur, u, 0);
   if constexpr (NS == 1) {
     store_window(0);
     __syncthreads();
   }
-  for (int c = 0; c < nchunk; ++c) {
-    const int buf = NS == 1 ? (c & 1) : 0;
-    const bool has_next = c + 1 < nchunk;
-    if constexpr (NS > 1) {  // one buffer of NS planes: stage chunk c, then prefetch c + 1
-      store_window(0);
+  for (;;) {
+    // the next tile of this block (persistent form)
+    const bool has_tile = PST && t_cur + 1 < t_end;
+    TileG nxt = cur;
+    if (has_tile) {
+      const long long tn_ = t_cur + 1;
+      nxt = tile_geo((int)(tn_ % h.ntx), (int)((tn_ / h.ntx) % h.nty), (int)(tn_ / ((long long)h.ntx * h.nty)));
+    }
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    for (int c = 0; c < nchunk; ++c) {
+      const int buf = NS == 1 ? (c & 1) : 0;
+      const bool has_next = c + 1 < nchunk;
+      if constexpr (NS > 1) {  // one buffer of NS planes: stage chunk c, then prefetch c + 1
+        store_window(0);
+        __syncthreads();
+      }
+      if (has_next) {
+        load_window(cur, c + 1);
+      } else if (has_tile) {  // the next tile's first window, under this chunk's MFMAs and the epilogue
+        set_window(nxt);
+        load_window(nxt, 0);
+      }
+      const __bf16* W = ksm + buf * h.npix * KW_ROWP;
+#pragma unroll
+      for (int u = 0; u < NTW; ++u) {
+        const int t = wave * NTW + u;
+        const int shift = S2T ? toff0 + tsgn * ((t >> 1) * h.PC + (t & 1)) : toff0 + tsgn * ((t >> 2) * h.PC + (t & 3));
+        const int sh = shift * KW_ROWP;
+#pragma unroll
+        for (int kq = 0; kq < 2; ++kq) {
+          bf16x8 af[TM][NS];
+#pragma unroll
+          for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+            for (int p = 0; p < NS; ++p) af[tm][p] = *(const bf16x8*)&W[p * h.npix * KW_ROWP + abase[tm] + sh + kq * 16];
+#pragma unroll
+          for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_split<NS>(af[tm], bq[u][tn][kq], acc[tm][tn]);
+        }
+        if (has_next) load_b(cur, u, c + 1);
+        else if (has_tile) load_b(nxt, u, 0);
+      }
+      if constexpr (NS == 1) {
+        if (has_next) store_window(buf ^ 1);
+      }
       __syncthreads();
     }
-    if (has_next) load_window(c + 1);
-    const __bf16* W = ksm + buf * h.npix * KW_ROWP;
-#pragma unroll
-    for (int u = 0; u < NTW; ++u) {
-      const int t = wave * NTW + u;
-      const int shift = S2T ? toff0 + tsgn * ((t >> 1) * h.PC + (t & 1)) : toff0 + tsgn * ((t >> 2) * h.PC + (t & 3));
-      const int sh = shift * KW_ROWP;
-#pragma unroll
-      for (int kq = 0; kq < 2; ++kq) {
-        bf16x8 af[TM][NS];
-#pragma unroll
-        for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-          for (int p = 0; p < NS; ++p) af[tm][p] = *(const bf16x8*)&W[p * h.npix * KW_ROWP + abase[tm] + sh + kq * 16];
-#pragma unroll
-        for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-          for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_split<NS>(af[tm], bq[u][tn][kq], acc[tm][tn]);
-      }
-      if (has_next) load_b(u, c + 1);
-    }
-    if constexpr (NS == 1) {
-      if (has_next) store_window(buf ^ 1);
-    }
-    __syncthreads();
-  }
 
-  // ---- sum the four waves' partial tiles in LDS (fixed order), then one epilogue ----
-  float* red = (float*)ksm;  // [4][BM][BN]
+    // ---- sum the four waves' partial tiles in LDS (fixed order), then one epilogue ----
+    const int m0 = cur.m0, n0 = cur.n0, group = cur.group, cls = cur.cls;
+    float* red = (float*)ksm;  // [4][BM][BN]
 #pragma unroll
-  for (int tm = 0; tm < TM; ++tm)
+    for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-    for (int tn = 0; tn < TN; ++tn)
+      for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        red[(wave * BM + m) * BN + tn * 32 + l32] = acc[tm][tn][r];
-      }
-  __syncthreads();
-  constexpr int NRG = 256 / BN;  // row groups
-  const int col = tid % BN, rg = tid / BN;
-  const int n = n0 + col;
-  float* Cp = a.C + group * a.c_gs;
-  const float* bias = a.bias ? a.bias + group * a.bias_gs : nullptr;
-  const bool bwm = a.bw.pre != nullptr;
-  const bool bwc = bwm && n < a.bw.C;
-  float bm = 0.f, bi = 0.f, bb = 0.f;
-  if (bwc) {
-    bm = a.bw.mean[group * a.bw.ms_gs + n];
-    bi = a.bw.invstd[group * a.bw.ms_gs + n];
-    bb = a.bw.y ? 0.f : a.bw.beta[group * a.bw.beta_gs + n];
-  }
-  float s1 = 0.f, s2 = 0.f;
-  // every global load (accumulate target, BN-backward pre / y) before the first store: one
-  // memory round trip for the thread's BM / NRG rows, not one per row
-  constexpr int NR = BM / NRG;
-  long long orow[NR];
-  float cv[NR], pv[NR], yv[NR];
-  const float* bwpre = bwc ? a.bw.pre + group * a.bw.pre_gs : nullptr;
-  const float* bwy = (bwc && a.bw.y) ? a.bw.y + group * a.bw.y_gs : nullptr;
-  const float biasv = bias ? bias[n] : 0.f;
-#pragma unroll
-  for (int i = 0; i < NR; ++i) {
-    orow[i] = kw_out_row(h, g, cls, m0 + rg + i * NRG);
-    cv[i] = a.accumulate ? Cp[orow[i] * a.ldc + n] : 0.f;
-    pv[i] = bwpre ? bwpre[orow[i] * a.bw.ldp + n] : 0.f;
-    yv[i] = bwy ? bwy[orow[i] * a.bw.ldy + n] : 0.f;
-  }
-#pragma unroll
-  for (int i = 0; i < NR; ++i) {
-    const int m = rg + i * NRG;
-    float v = red[(0 * BM + m) * BN + col];
-#pragma unroll
-    for (int w = 1; w < 4; ++w) v += red[(w * BM + m) * BN + col];
-    if (!bwm) {
-      s1 += v;
-      s2 += v * v;
+        for (int r = 0; r < 16; ++r) {
+          const int m = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          red[(wave * BM + m) * BN + tn * 32 + l32] = acc[tm][tn][r];
+        }
+    __syncthreads();
+    constexpr int NRG = 256 / BN;  // row groups
+    const int col = tid % BN, rg = tid / BN;
+    const int n = n0 + col;
+    float* Cp = a.C + group * a.c_gs;
+    const float* bias = a.bias ? a.bias + group * a.bias_gs : nullptr;
+    const bool bwm = a.bw.pre != nullptr;
+    const bool bwc = bwm && n < a.bw.C;
+    float bm = 0.f, bi = 0.f, bb = 0.f;
+    if (bwc) {
+      bm = a.bw.mean[group * a.bw.ms_gs + n];
+      bi = a.bw.invstd[group * a.bw.ms_gs + n];
+      bb = a.bw.y ? 0.f : a.bw.beta[group * a.bw.beta_gs + n];
     }
-    if (bias) v += biasv;
-    v = act_f(v, a.act);
-    if (a.accumulate) v += cv[i];
-    Cp[orow[i] * a.ldc + n] = v;
-    if (bwc) bw_term_v(v, pv[i], bm, bi, bb, bwy != nullptr, yv[i], a.bw.act, s1, s2);
-  }
-  if (!a.stats) return;
-  __syncthreads();  // every wave is done reading red
-  red[tid] = s1;
-  red[256 + tid] = s2;
-  __syncthreads();
-  if (tid < BN) {
-    const int SC = bwm ? a.bw.C : a.N;  // stats columns (row-block stride 2*SC)
-    if (n0 + tid < SC) {
-      float s = 0.f, q = 0.f;
+    float s1 = 0.f, s2 = 0.f;
+    // every global load (accumulate target, BN-backward pre / y) before the first store: one
+    // memory round trip for the thread's BM / NRG rows, not one per row
+    constexpr int NR = BM / NRG;
+    long long orow[NR];
+    float cv[NR], pv[NR], yv[NR];
+    const float* bwpre = bwc ? a.bw.pre + group * a.bw.pre_gs : nullptr;
+    const float* bwy = (bwc && a.bw.y) ? a.bw.y + group * a.bw.y_gs : nullptr;
+    const float biasv = bias ? bias[n] : 0.f;
 #pragma unroll
-      for (int j = 0; j < NRG; ++j) {
-        s += red[j * BN + tid];
-        q += red[256 + j * BN + tid];
+    for (int i = 0; i < NR; ++i) {
+      orow[i] = kw_out_row(h, g, cls, m0 + rg + i * NRG);
+      cv[i] = a.accumulate ? Cp[orow[i] * a.ldc + n] : 0.f;
+      pv[i] = bwpre ? bwpre[orow[i] * a.bw.ldp + n] : 0.f;
+      yv[i] = bwy ? bwy[orow[i] * a.bw.ldy + n] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int m = rg + i * NRG;
+      float v = red[(0 * BM + m) * BN + col];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) v += red[(w * BM + m) * BN + col];
+      if (!bwm) {
+        s1 += v;
+        s2 += v * v;
       }
-      const int rb = cls * gridDim.x + blk.x;
-      stat_put(a.stats + (rb & (a.s_nsh - 1)) * a.s_sh + group * a.s_gs, n0 + tid, s, q);
+      if (bias) v += biasv;
+      v = act_f(v, a.act);
+      if (a.accumulate) v += cv[i];
+      Cp[orow[i] * a.ldc + n] = v;
+      if (bwc) bw_term_v(v, pv[i], bm, bi, bb, bwy != nullptr, yv[i], a.bw.act, s1, s2);
+    }
+    if (a.stats) {
+      __syncthreads();  // every wave is done reading red
+      red[tid] = s1;
+      red[256 + tid] = s2;
+      __syncthreads();
+      if (tid < BN) {
+        const int SC = bwm ? a.bw.C : a.N;  // stats columns (row-block stride 2*SC)
+        if (n0 + tid < SC) {
+          float s = 0.f, q = 0.f;
+#pragma unroll
+          for (int j = 0; j < NRG; ++j) {
+            s += red[j * BN + tid];
+            q += red[256 + j * BN + tid];
+          }
+          const int rb = cls * h.ntx + m0 / BM;
+          stat_put(a.stats + (rb & (a.s_nsh - 1)) * a.s_sh + group * a.s_gs, n0 + tid, s, q);
+        }
+      }
+    }
+    if (!has_tile) break;
+    // ---- the next tile: its window (prefetched above) into LDS once every wave is done with red ----
+    __syncthreads();
+    cur = nxt;
+    ++t_cur;
+    if constexpr (NS == 1) {
+      store_window(0);
+      __syncthreads();
     }
   }
 }
@@ -391,6 +454,27 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
   h.f = a;
   const bool s2t = a.g.mode == GM_CONVT && a.g.stride == 2;
   dim3 grid(a.rows / bm, a.N / bn, groups * a.nclass);
+  h.ntx = (int)grid.x;
+  h.nty = (int)grid.y;
+  h.ntz = (int)grid.z;
+  h.tpb = 1;
+  // persistent form (SVAE_KW_PERSIST=1): where the tiles exceed the resident blocks, each block runs
+  // a contiguous run of tiles with the next tile's window / B loads under the current tile's last
+  // chunk and epilogue
+  static const int persist = [] {
+    const char* e = getenv("SVAE_KW_PERSIST");
+    return e ? atoi(e) : 0;
+  }();
+  if (persist && a.nsp <= 1 && a.a_bf16 && bn == 32 && bm == 64) {  // the persistent instances
+    const int occ_w = 2;
+    const int occ_l = (int)std::max<size_t>(1, (size_t)163840 / std::max<size_t>(lds, 1));
+    const long long slots = 256LL * std::min(occ_w, occ_l) * (persist > 1 ? persist : 1);
+    const long long ntiles = (long long)h.ntx * h.nty * h.ntz;
+    if (ntiles > slots) {
+      h.tpb = (int)((ntiles + slots - 1) / slots);
+      grid = dim3((unsigned)((ntiles + h.tpb - 1) / h.tpb), 1, 1);
+    }
+  }
   if (a.nsp > 1) {  // split-bf16 planes (fp32 A): 64 / 32-row tiles, 32 columns
     static bool attr = false;
     if (!attr) {
@@ -411,7 +495,10 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
     return a.nclass * (a.rows / bm);
   }
 #define KW_LAUNCH(BM_, BN_)                                                                                  \
-  if (a.a_bf16) {                                                                                            \
+  if (h.tpb > 1 && a.a_bf16 && BN_ == 32 && BM_ == 64) {  /* persistent: the bf16-A 64x32 instances */     \
+    if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, true, true, 1, true>), grid, dim3(256), lds, s, h); \
+    else hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, false, true, 1, true>), grid, dim3(256), lds, s, h);    \
+  } else if (a.a_bf16) {                                                                                     \
     if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<BM_, BN_, true, true>), grid, dim3(256), lds, s, h);    \
     else hipLaunchKernelGGL((igemm_halo_kw_kernel<BM_, BN_, false, true>), grid, dim3(256), lds, s, h);       \
   } else {                                                                                                   \
