@@ -39,13 +39,17 @@ int svae_pcnn_wnorm_bwd(const float* V, const float* g, const float* norm, const
 
 /* gather conv (bf16 MFMA, fp32 accumulate): y[rows][ldy] (rows = n*ho*wo) = gather(x) . wk
  * (+ bias); wk [tap][cout][kpad]; accumulate: y += result; zero_edge 1 / 2: output row oy == 0 /
- * column ox == 0 written as 0 (nn.down_shift / right_shift folded in: pass pt + 1 / pl + 1). */
-int svae_pcnn_conv(const float* x, int n, int hi, int wi, int cin, int ldx, const void* wk, int kpad,
+ * column ox == 0 written as 0 (nn.down_shift / right_shift folded in: pass pt + 1 / pl + 1).
+ * x is fp32, or bf16 with x_bf16 = 1 (cin, ldx multiples of 8): the MFMA operand precision, so a
+ * bf16 x gives bitwise the result of its fp32 source.  Stride-1 launches whose rows fill 256-row
+ * blocks of whole image rows (or whole images) run the halo-window kernel, the rest pc_conv2. */
+int svae_pcnn_conv(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, const void* wk, int kpad,
                    const float* bias, float* y, int ho, int wo, int cout, int ldy, int kh, int kw, int s, int pt,
                    int pl, int mode, int accumulate, int zero_edge, void* stream);
 /* weight gradient of that conv: dW[tap][cin][cout] = sum_rows gather(x)[row][ci] . dy[row][co]
- * (split over rows into `scratch` slabs, then a fixed-order reduce: deterministic). */
-int svae_pcnn_conv_wgrad(const float* x, int n, int hi, int wi, int cin, int ldx, const float* dy, int ldd, int ho,
+ * (split over rows into `scratch` slabs, then a fixed-order reduce: deterministic); x fp32 or bf16
+ * (x_bf16 = 1). */
+int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, const float* dy, int ldd, int ho,
                          int wo, int cout, int kh, int kw, int s, int pt, int pl, int mode, float* dW, float* scratch,
                          int64_t scratch_elems, void* stream);
 /* column sums over rows (bias gradients): out[c] (+)= sum_r x[r][c]; mask_edge 1 / 2 skips
@@ -56,11 +60,15 @@ int svae_pcnn_colsum(const float* x, int64_t rows, int c, int ldx, int ho, int w
 int svae_pcnn_mask_edge(float* x, int n, int ho, int wo, int c, int ldx, int mask_edge, void* stream);
 
 /* resnet nonlinearity (model.py:24-31): kind 0 relu, 1 elu, 2 concat_elu (y has 2c channels
- * [elu(x), elu(-x)], nn.py:12-15). */
-int svae_pcnn_nonlin(const float* x, int64_t rows, int c, int ldx, int kind, float* y, int ldy, void* stream);
-/* its backward: dx (+)= dy . f'(x) */
-int svae_pcnn_nonlin_bwd(const float* x, int64_t rows, int c, int ldx, int kind, const float* dy, int ldy, float* dx,
-                         int lddx, int accumulate, void* stream);
+ * [elu(x), elu(-x)], nn.py:12-15), times the training pass's dropout keep-mask (nn.py:273-274;
+ * mask [rows][cy] holding 1 / keep_prob or 0, cy = y's channels; NULL: none); y fp32 or bf16
+ * (y_bf16 = 1: for a consumer that reads it as a bf16 MFMA operand).  A mask or a bf16 y needs
+ * c, ldx, ldy multiples of 4 and 16-B aligned rows. */
+int svae_pcnn_nonlin(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, void* y, int ldy,
+                     int y_bf16, void* stream);
+/* its backward: dx (+)= f'(x) . (dy . mask) */
+int svae_pcnn_nonlin_bwd(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, const float* dy,
+                         int ldy, float* dx, int lddx, int accumulate, void* stream);
 
 /* gated_resnet tail (nn.py:283-288): with c2 = [a | b] (2f channels) + hp[img] (h . hw):
  * out = x + a . sigmoid(b). */
@@ -123,8 +131,9 @@ int svae_pcnn_dropout(const float* x, int64_t rows, int c, int ldx, const float*
 int svae_pcnn_sqerr(const float* a, const float* t, int nimg, int64_t per_img, float coef, float* rec, float* da,
                     void* stream);
 
-/* data-dependent init (nn.py:176-180, :206-210): column moments of y [rows][c] (fp64), then
- * g *= scale / sqrt(v + 1e-10), b -= m * scale / sqrt(v + 1e-10). */
+/* data-dependent init (nn.py:176-180, :206-210): column moments of y [rows][c] (fp64, two passes over
+ * row blocks, fixed order), then g *= scale / sqrt(v + 1e-10), b -= m * scale / sqrt(v + 1e-10).
+ * scratch: 1024 * c doubles. */
 int svae_pcnn_wn_init(const float* y, int64_t rows, int c, int ldy, float init_scale, float* g, float* b,
                       double* scratch, void* stream);
 /* TF Adam (tf.train.AdamOptimizer semantics as sequential_vae.py's optimiser, with the gradient

@@ -103,14 +103,14 @@ def lib():
         # PixelCNN++ head (include/svae_pcnn.h)
         "svae_pcnn_wnorm": ([vp, vp, i32, i32, i32, vp, vp, i32, vp, i32, vp], i32),
         "svae_pcnn_wnorm_bwd": ([vp, vp, vp, vp, i32, i32, i32, vp, vp, vp], i32),
-        "svae_pcnn_conv": ([vp, i32, i32, i32, i32, i32, vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32,
-                            i32, i32, i32, i32, vp], i32),
-        "svae_pcnn_conv_wgrad": ([vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32,
-                                  vp, vp, i64, vp], i32),
+        "svae_pcnn_conv": ([vp, i32, i32, i32, i32, i32, i32, vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, i32,
+                            i32, i32, i32, i32, i32, vp], i32),
+        "svae_pcnn_conv_wgrad": ([vp, i32, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32,
+                                  i32, vp, vp, i64, vp], i32),
         "svae_pcnn_colsum": ([vp, i64, i32, i32, i32, i32, i32, vp, i32, vp, vp], i32),
         "svae_pcnn_mask_edge": ([vp, i32, i32, i32, i32, i32, i32, vp], i32),
-        "svae_pcnn_nonlin": ([vp, i64, i32, i32, i32, vp, i32, vp], i32),
-        "svae_pcnn_nonlin_bwd": ([vp, i64, i32, i32, i32, vp, i32, vp, i32, i32, vp], i32),
+        "svae_pcnn_nonlin": ([vp, i64, i32, i32, i32, vp, vp, i32, i32, vp], i32),
+        "svae_pcnn_nonlin_bwd": ([vp, i64, i32, i32, i32, vp, vp, i32, vp, i32, i32, vp], i32),
         "svae_pcnn_gate": ([vp, i32, vp, vp, i64, i32, i32, vp, i32, vp], i32),
         "svae_pcnn_gate_bwd": ([vp, vp, vp, i32, i64, i32, i32, vp, vp], i32),
         "svae_pcnn_gemm_small": ([vp, i32, i32, vp, i32, i32, vp, i32, i32, i32, i32, f32, vp], i32),

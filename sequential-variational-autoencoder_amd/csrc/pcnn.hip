@@ -4,6 +4,7 @@
 // sampler.  C ABI: include/svae_pcnn.h.  Reference: pixel_cnn/pixel_cnn_pp/{model,nn}.py,
 // pixel_cnn/pixelvae.py (cited per function).
 #include <math.h>
+#include <cstdint>
 #include <cstdlib>
 #include <string>
 
@@ -227,8 +228,8 @@ __global__ __launch_bounds__(256) void pc_conv_kernel(PcGeom g, const float* __r
 // % 32 == 0.
 // ---------------------------------------------------------------------------------------------
 #define PC2_P 40  // LDS row pitch (bf16)
-template <int NT>
-__global__ __launch_bounds__(256) void pc_conv2_kernel(PcGeom g, const float* __restrict__ X,
+template <int NT, bool XB>
+__global__ __launch_bounds__(256) void pc_conv2_kernel(PcGeom g, const void* __restrict__ Xv,
                                                        const __bf16* __restrict__ Wk, int kpad,
                                                        const float* __restrict__ bias, float* __restrict__ Y,
                                                        int ldy, int accumulate, int zero_edge) {
@@ -254,17 +255,29 @@ __global__ __launch_bounds__(256) void pc_conv2_kernel(PcGeom g, const float* __
   constexpr int BI = (BR * 4 + 255) / 256;  // 16-B weight items per thread (4 per row of 32 k)
   const int nk = kpad / 32, ntap = g.kh * g.kw, nchunk = ntap * nk;
   f32x4 ra[4];
+  pc_bf16x8 rh[2];
   pc_bf16x8 rb[BI];
   auto load = [&](int c) {
     const int tap = c / nk, k0 = (c - tap * nk) * 32;
     const int ky = tap / g.kw, kx = tap - ky * g.kw;
     int iy = 0, ix = 0;
     const bool v = amv && pc_src(g, aoy, aox, ky, kx, iy, ix);
-    const float* xp = X + ((long long)(aimg * g.hi + iy) * g.wi + ix) * g.ldx + k0 + 16 * ah;
+    const long long xo = ((long long)(aimg * g.hi + iy) * g.wi + ix) * g.ldx + k0 + 16 * ah;
+    if constexpr (XB) {  // bf16 X: 8 channels per 16-B load (cin % 8 == 0)
+      const __bf16* xp = (const __bf16*)Xv + xo;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int ci = k0 + 16 * ah + 4 * j;
-      ra[j] = (v && ci < g.cin) ? *(const f32x4*)(xp + 4 * j) : f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 2; ++j) {
+        const int ci = k0 + 16 * ah + 8 * j;
+        pc_bf16x8 z = {};
+        rh[j] = (v && ci < g.cin) ? *(const pc_bf16x8*)(xp + 8 * j) : z;
+      }
+    } else {
+      const float* xp = (const float*)Xv + xo;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ci = k0 + 16 * ah + 4 * j;
+        ra[j] = (v && ci < g.cin) ? *(const f32x4*)(xp + 4 * j) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
     const __bf16* wp = Wk + (long long)tap * g.cout * kpad + k0;
 #pragma unroll
@@ -277,9 +290,13 @@ __global__ __launch_bounds__(256) void pc_conv2_kernel(PcGeom g, const float* __
   auto store = [&](int buf) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const pc_f32x8 v8 = {ra[2 * j][0], ra[2 * j][1], ra[2 * j][2], ra[2 * j][3],
-                           ra[2 * j + 1][0], ra[2 * j + 1][1], ra[2 * j + 1][2], ra[2 * j + 1][3]};
-      *(pc_bf16x8*)&As[buf][ar * PC2_P + 16 * ah + 8 * j] = __builtin_convertvector(v8, pc_bf16x8);
+      if constexpr (XB) {
+        *(pc_bf16x8*)&As[buf][ar * PC2_P + 16 * ah + 8 * j] = rh[j];
+      } else {
+        const pc_f32x8 v8 = {ra[2 * j][0], ra[2 * j][1], ra[2 * j][2], ra[2 * j][3],
+                             ra[2 * j + 1][0], ra[2 * j + 1][1], ra[2 * j + 1][2], ra[2 * j + 1][3]};
+        *(pc_bf16x8*)&As[buf][ar * PC2_P + 16 * ah + 8 * j] = __builtin_convertvector(v8, pc_bf16x8);
+      }
     }
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
@@ -333,12 +350,245 @@ __global__ __launch_bounds__(256) void pc_conv2_kernel(PcGeom g, const float* __
 }
 
 // ---------------------------------------------------------------------------------------------
+// Halo-window gather conv (stride 1, both modes; every shifted conv of the resnets and its input
+// gradient, and the 1x1 nin / dense layers): block = BM = 256 * TM output pixels (whole image rows,
+// or whole images) x 32*NT output channels, eight waves of 32 * TM rows x all NT column tiles.  K
+// runs in chunks of 32 input channels; per chunk the block stages ONE input window -- its rows plus
+// the kernel's halo, nimg x (R + kh - 1) x (wo + kw - 1) pixels, ~1.3x the block's pixels instead of
+// taps x as pc_conv2 gathers them -- and the chunk's weight rows of every tap, then each wave runs
+// taps x 2 x NT x TM MFMAs (60 - 120 for the [2, 3] convs) between two barriers.  The next chunk's
+// window and weights are loaded into registers under the current chunk's MFMAs.
+//   mode 0: iy = oy - pt + ky -> window row ry + ky          (origin oy0 - pt, column origin -pl)
+//   mode 1: iy = oy + pt - ky -> window row ry + kh - 1 - ky (origin oy0 + pt - kh + 1, pl - kw + 1)
+// ---------------------------------------------------------------------------------------------
+struct Pc3 {
+  int R, nimg, PR, PC, npix;  // image rows per block (per image), images per block, window dims
+  int oy_off, ox_off;         // window origin relative to the block's first output row / column 0
+};
+#define PC3_MAXPIX 640
+#define PC3_MAXTAPS 6
+// XB: X stored as bf16 (a nonlinearity output the head writes in the conv's operand precision)
+template <int NT, int TM, bool XB>
+__global__ __launch_bounds__(512) void pc_conv3_kernel(PcGeom g, Pc3 h, const void* __restrict__ Xv,
+                                                       const __bf16* __restrict__ Wk, int kpad,
+                                                       const float* __restrict__ bias, float* __restrict__ Y,
+                                                       int ldy, int accumulate, int zero_edge) {
+  constexpr int BM = 256 * TM;
+  constexpr int BR = 32 * NT;                                  // weight rows (output channels) per tap
+  constexpr int AI = (PC3_MAXPIX * 4 + 511) / 512;             // window items (8 channels) per thread
+  constexpr int BI = (PC3_MAXTAPS * BR * 4 + 511) / 512;       // 16-B weight items per thread
+  extern __shared__ __attribute__((aligned(16))) __bf16 pc3s[];
+  __bf16* As = pc3s;                    // [npix][PC2_P]
+  __bf16* Bs = pc3s + h.npix * PC2_P;   // [tap][BR][PC2_P]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hh = lane >> 5;
+  const int taps = g.kh * g.kw;
+  const int per_img = g.ho * g.wo;
+  const long long m0 = (long long)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BR;
+  const int img0 = (int)(m0 / per_img);
+  const int oy0 = (int)(m0 - (long long)img0 * per_img) / g.wo;
+  const int iy0 = oy0 + h.oy_off, ix0 = h.ox_off;
+
+  // window items: pixel it >> 2, channels (it & 3) * 8 .. + 8 of the chunk; -1 zero, -2 no item
+  long long aoff[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int it = tid + 512 * i;
+    aoff[i] = -2;
+    if (it < h.npix * 4) {
+      const int pix = it >> 2, part = it & 3;
+      const int il = pix / (h.PR * h.PC);
+      const int r2 = pix - il * h.PR * h.PC;
+      const int pr = r2 / h.PC, pc = r2 - pr * h.PC;
+      const int iy = iy0 + pr, ix = ix0 + pc;
+      aoff[i] = (iy >= 0 && iy < g.hi && ix >= 0 && ix < g.wi)
+                    ? ((long long)((img0 + il) * g.hi + iy) * g.wi + ix) * g.ldx + part * 8
+                    : -1;
+    }
+  }
+  const float* X = (const float*)Xv;
+  const __bf16* Xh = (const __bf16*)Xv;
+  f32x4 ra[XB ? 1 : AI][2];
+  pc_bf16x8 rh[XB ? AI : 1];
+  pc_bf16x8 rb[BI];
+  const int nb = taps * BR;  // staged weight rows
+  auto load = [&](int c) {
+    const int k0 = c * 32;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int ci = k0 + ((tid + 512 * i) & 3) * 8;
+      if constexpr (XB) {  // 8 channels = one 16-B load (cin % 8 == 0)
+        pc_bf16x8 z = {};
+        rh[i] = (aoff[i] >= 0 && ci < g.cin) ? *(const pc_bf16x8*)(Xh + aoff[i] + k0) : z;
+      } else {
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        ra[i][0] = z;
+        ra[i][1] = z;
+        if (aoff[i] >= 0) {
+          const float* xp = X + aoff[i] + k0;
+          if (ci < g.cin) ra[i][0] = *(const f32x4*)xp;
+          if (ci + 4 < g.cin) ra[i][1] = *(const f32x4*)(xp + 4);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int it = tid + 512 * i, row = it >> 2, q = it & 3;
+      const int t = row / BR, n = row - t * BR;
+      pc_bf16x8 z = {};
+      rb[i] = (row < nb && n0 + n < g.cout) ? *(const pc_bf16x8*)(Wk + ((long long)t * g.cout + n0 + n) * kpad + k0 + q * 8)
+                                            : z;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      if (aoff[i] < -1) continue;
+      const int it = tid + 512 * i;
+      if constexpr (XB) {
+        *(pc_bf16x8*)&As[(it >> 2) * PC2_P + (it & 3) * 8] = rh[i];
+      } else {
+        const pc_f32x8 v8 = {ra[i][0][0], ra[i][0][1], ra[i][0][2], ra[i][0][3],
+                             ra[i][1][0], ra[i][1][1], ra[i][1][2], ra[i][1][3]};
+        *(pc_bf16x8*)&As[(it >> 2) * PC2_P + (it & 3) * 8] = __builtin_convertvector(v8, pc_bf16x8);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int it = tid + 512 * i, row = it >> 2, q = it & 3;
+      if (row < nb) *(pc_bf16x8*)&Bs[row * PC2_P + q * 8] = rb[i];
+    }
+  };
+
+  // this lane's A rows: block row ml -> window pixel (il * PR + ry) * PC + rx
+  int abase[TM];
+  const int rows_img = h.R * g.wo;
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const int ml = wave * 32 * TM + tm * 32 + l32;
+    const int il = ml / rows_img;
+    const int rem = ml - il * rows_img;
+    const int ry = rem / g.wo, rx = rem - ry * g.wo;
+    abase[tm] = ((il * h.PR + ry) * h.PC + rx) * PC2_P + 8 * hh;
+  }
+  f32x16 acc[TM][NT];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[tm][t][r] = 0.f;
+
+  const int nchunk = kpad / 32;
+  load(0);
+  store();
+  __syncthreads();
+  for (int c = 0; c < nchunk; ++c) {
+    if (c + 1 < nchunk) load(c + 1);
+    for (int t = 0; t < taps; ++t) {
+      const int ky = t / g.kw, kx = t - ky * g.kw;
+      const int toff = (g.mode == 0 ? ky * h.PC + kx : (g.kh - 1 - ky) * h.PC + (g.kw - 1 - kx)) * PC2_P;
+      const __bf16* bt = Bs + (t * BR + l32) * PC2_P + 8 * hh;
+#pragma unroll
+      for (int kq = 0; kq < 2; ++kq) {
+        pc_bf16x8 af[TM];
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) af[tm] = *(const pc_bf16x8*)&As[abase[tm] + toff + kq * 16];
+#pragma unroll
+        for (int tn = 0; tn < NT; ++tn) {
+          const pc_bf16x8 bf = *(const pc_bf16x8*)(bt + tn * 32 * PC2_P + kq * 16);
+#pragma unroll
+          for (int tm = 0; tm < TM; ++tm) acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm], bf, acc[tm][tn], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();  // every wave is done with this chunk's window and weights
+    if (c + 1 < nchunk) {
+      store();
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const long long mw = m0 + wave * 32 * TM + tm * 32;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const long long mm = mw + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      bool zero = false;
+      if (zero_edge) {
+        const int rr = (int)(mm % per_img);
+        zero = zero_edge == 1 ? (rr / g.wo == 0) : (rr % g.wo == 0);
+      }
+#pragma unroll
+      for (int tn = 0; tn < NT; ++tn) {
+        const int n = n0 + tn * 32 + l32;
+        if (n >= g.cout) continue;
+        float val = zero ? 0.f : acc[tm][tn][r] + (bias ? bias[n] : 0.f);
+        float* p = Y + mm * ldy + n;
+        if (accumulate) val += *p;
+        *p = val;
+      }
+    }
+  }
+}
+
+// plan of the halo kernel for a launch (false: not eligible -> pc_conv2)
+bool pc3_plan(const PcGeom& g, int kpad, int TM, Pc3* out, size_t* lds) {
+  const int BM = 256 * TM;
+  const int taps = g.kh * g.kw;
+  if (g.s != 1 || kpad % 32 || taps > PC3_MAXTAPS) return false;
+  const long long rows = (long long)g.n * g.ho * g.wo;
+  const int per_img = g.ho * g.wo;
+  if (rows % BM) return false;
+  Pc3 h;
+  if (per_img % BM == 0 && BM % g.wo == 0) {
+    h.R = BM / g.wo;
+    h.nimg = 1;
+  } else if (BM % per_img == 0) {
+    h.R = g.ho;
+    h.nimg = BM / per_img;
+  } else {
+    return false;
+  }
+  h.PR = h.R + g.kh - 1;
+  h.PC = g.wo + g.kw - 1;
+  h.npix = h.nimg * h.PR * h.PC;
+  if (h.npix > PC3_MAXPIX) return false;
+  if (g.mode == 0) {
+    h.oy_off = -g.pt;
+    h.ox_off = -g.pl;
+  } else {
+    h.oy_off = g.pt - (g.kh - 1);
+    h.ox_off = g.pl - (g.kw - 1);
+  }
+  *out = h;
+  return true;
+}
+
+template <int NT, int TM, bool XB>
+void pc3_launch(const PcGeom& g, const Pc3& h, const void* x, const __bf16* w, int kpad, const float* bias, float* y,
+                int ldy, int accumulate, int zero_edge, hipStream_t st) {
+  const size_t lds = (size_t)(h.npix + g.kh * g.kw * 32 * NT) * PC2_P * 2;
+  static bool attr = false;
+  if (!attr) {  // the largest window + weight stage: 640 pixels + 6 taps x 160 rows (128 KB)
+    hipFuncSetAttribute((const void*)pc_conv3_kernel<NT, TM, XB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (PC3_MAXPIX + PC3_MAXTAPS * 32 * NT) * PC2_P * 2);
+    attr = true;
+  }
+  const long long rows = (long long)g.n * g.ho * g.wo;
+  const dim3 grid((unsigned)(rows / (256 * TM)), (unsigned)((g.cout + 32 * NT - 1) / (32 * NT)));
+  hipLaunchKernelGGL((pc_conv3_kernel<NT, TM, XB>), grid, dim3(512), lds, st, g, h, x, w, kpad, bias, y, ldy, accumulate,
+                     zero_edge);
+}
+
+// ---------------------------------------------------------------------------------------------
 // weight gradient: block = one tap x 64 ci x 64 co (2 x 2 waves of 32 x 32), K = a split of the
 // output rows in chunks of 32, staged through LDS transposed (row-contiguous per channel, so
 // each MFMA fragment is one 16-B LDS read).  Partial slabs [split][tap][ci][co].
 // ---------------------------------------------------------------------------------------------
 #define PW_RP 72  // LDS row pitch (bf16): 64 rows + 8 pad
-__global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const float* __restrict__ X,
+template <bool XB>
+__global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const void* __restrict__ Xv,
                                                        const float* __restrict__ D, int ldd, long long rows,
                                                        long long rows_per_split, float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) __bf16 Xs[2][64 * PW_RP];
@@ -364,21 +614,29 @@ __global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const float* __
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const long long row = rc + lr + 32 * u;
-      const float* xp = nullptr;
+      long long xo = -1;
       const float* dp = nullptr;
       if (row < r1) {
         const int img = (int)(row / per_img);
         const int rr = (int)(row - (long long)img * per_img);
         const int oy = rr / g.wo, ox = rr - (rr / g.wo) * g.wo;
         int iy, ix;
-        if (pc_src(g, oy, ox, ky, kx, iy, ix)) xp = X + ((long long)(img * g.hi + iy) * g.wi + ix) * g.ldx;
+        if (pc_src(g, oy, ox, ky, kx, iy, ix)) xo = ((long long)(img * g.hi + iy) * g.wi + ix) * g.ldx;
         dp = D + row * ldd;
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int c = (q0 + 8 * j) * 4;
         const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-        xv[u][j] = (xp && ci0 + c < g.cin) ? *(const f32x4*)(xp + ci0 + c) : z;
+        xv[u][j] = z;
+        if (xo >= 0 && ci0 + c < g.cin) {
+          if constexpr (XB) {
+            typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+            xv[u][j] = __builtin_convertvector(*(const bf16x4_t*)((const __bf16*)Xv + xo + ci0 + c), f32x4);
+          } else {
+            xv[u][j] = *(const f32x4*)((const float*)Xv + xo + ci0 + c);
+          }
+        }
         dv[u][j] = (dp && co0 + c < g.cout) ? *(const f32x4*)(dp + co0 + c) : z;
       }
     }
@@ -491,6 +749,81 @@ __global__ void mask_edge_kernel(float* x, long long n_rows, int per_img, int wo
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ float elu_f(float x) { return x > 0.f ? x : expm1f(x); }
 __device__ __forceinline__ float delu_f(float x) { return x > 0.f ? 1.f : expf(x); }
+
+// Vectorised forms (4 channels per thread, NL_RPB rows per block, 32-bit index math): the resnet
+// nonlinearity with the training pass's dropout fused (y = f(x) * mask, nn.py:270-274), written fp32
+// or bf16 -- bf16 when its only consumers are the bf16-MFMA convs, which round it the same way --
+// and its backward dx (+)= f'(x) * (dy * mask).
+#define NL_RPB 64
+typedef __bf16 pc_bf16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void nl_fwd4(f32x4 v, int kind, f32x4& a, f32x4& b) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (kind == 0) {
+      a[e] = fmaxf(v[e], 0.f);
+    } else {
+      a[e] = elu_f(v[e]);
+      b[e] = elu_f(-v[e]);
+    }
+  }
+}
+template <bool YB>
+__global__ __launch_bounds__(256) void nonlin4_kernel(const float* __restrict__ x, long long rows, int c, int ldx,
+                                                      int kind, const float* __restrict__ mask, void* __restrict__ y,
+                                                      int ldy) {
+  const int q = c >> 2, cy = kind == 2 ? 2 * c : c;
+  const long long r0 = (long long)blockIdx.x * NL_RPB;
+  const int nr = (int)(rows - r0 < NL_RPB ? rows - r0 : NL_RPB);
+  for (int j = threadIdx.x; j < nr * q; j += 256) {
+    const int rr = j / q;
+    const int ch = (j - rr * q) * 4;
+    const long long r = r0 + rr;
+    f32x4 a, b = {0.f, 0.f, 0.f, 0.f};
+    nl_fwd4(*(const f32x4*)(x + r * ldx + ch), kind, a, b);
+    if (mask) {
+      a *= *(const f32x4*)(mask + r * cy + ch);
+      if (kind == 2) b *= *(const f32x4*)(mask + r * cy + c + ch);
+    }
+    if constexpr (YB) {
+      __bf16* yp = (__bf16*)y + r * ldy + ch;
+      *(pc_bf16x4*)yp = __builtin_convertvector(a, pc_bf16x4);
+      if (kind == 2) *(pc_bf16x4*)(yp + c) = __builtin_convertvector(b, pc_bf16x4);
+    } else {
+      float* yp = (float*)y + r * ldy + ch;
+      *(f32x4*)yp = a;
+      if (kind == 2) *(f32x4*)(yp + c) = b;
+    }
+  }
+}
+__global__ __launch_bounds__(256) void nonlin4_bwd_kernel(const float* __restrict__ x, long long rows, int c, int ldx,
+                                                          int kind, const float* __restrict__ mask,
+                                                          const float* __restrict__ dy, int ldy, float* __restrict__ dx,
+                                                          int lddx, int accumulate) {
+  const int q = c >> 2, cy = kind == 2 ? 2 * c : c;
+  const long long r0 = (long long)blockIdx.x * NL_RPB;
+  const int nr = (int)(rows - r0 < NL_RPB ? rows - r0 : NL_RPB);
+  for (int j = threadIdx.x; j < nr * q; j += 256) {
+    const int rr = j / q;
+    const int ch = (j - rr * q) * 4;
+    const long long r = r0 + rr;
+    const f32x4 v = *(const f32x4*)(x + r * ldx + ch);
+    f32x4 g = *(const f32x4*)(dy + r * ldy + ch), g2 = {0.f, 0.f, 0.f, 0.f};
+    if (kind == 2) g2 = *(const f32x4*)(dy + r * ldy + c + ch);
+    if (mask) {
+      g *= *(const f32x4*)(mask + r * cy + ch);
+      if (kind == 2) g2 *= *(const f32x4*)(mask + r * cy + c + ch);
+    }
+    f32x4 d;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (kind == 0) d[e] = v[e] > 0.f ? g[e] : 0.f;  // tf.nn.relu: relu'(0) = 0
+      else if (kind == 1) d[e] = g[e] * delu_f(v[e]);
+      else d[e] = g[e] * delu_f(v[e]) - g2[e] * delu_f(-v[e]);
+    }
+    f32x4* p = (f32x4*)(dx + r * lddx + ch);
+    *p = accumulate ? *p + d : d;
+  }
+}
 
 __global__ void nonlin_kernel(const float* __restrict__ x, long long rows, int c, int ldx, int kind,
                               float* __restrict__ y, int ldy) {
@@ -910,32 +1243,46 @@ __global__ void ratio_kernel(const float* __restrict__ z, const float* __restric
   if (i < nimg) ratio[i] = lo + (hi - lo) * sigm(z[i] + (zb ? zb[0] : 0.f));
 }
 
-// column moments in fp64 (two-pass per column group): scratch [2][c]
-__global__ __launch_bounds__(256) void wn_init_kernel(const float* __restrict__ y, long long rows, int c, int ldy,
-                                                      float init_scale, float* g, float* b) {
+// column moments in fp64, two passes (mean, then the centred second moment) over row blocks of
+// rpb rows: block (column group of 64, row block) -> part[rb][c]; the second pass and the
+// finaliser re-derive each column's mean from part in the same fixed order (deterministic)
+#define WNI_MAXRB 512
+__device__ __forceinline__ double wni_mean(const double* part, int nrb, int c, int col, long long rows) {
+  double s = 0.0;
+  for (int k = 0; k < nrb; ++k) s += part[(long long)k * c + col];
+  return s / (double)rows;
+}
+__global__ __launch_bounds__(256) void wn_mom_kernel(const float* __restrict__ y, long long rows, int c, int ldy,
+                                                     long long rpb, int nrb, int pass, double* part) {
   __shared__ double red[4][64];
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6, t = threadIdx.x & 63;
+  __shared__ double mean_s[64];
+  const int t = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + t;
+  const long long r0 = (long long)blockIdx.y * rpb;
+  const long long r1 = r0 + rpb < rows ? r0 + rpb : rows;
+  if (pass == 1 && q == 0) mean_s[t] = col < c ? wni_mean(part, nrb, c, col, rows) : 0.0;
+  __syncthreads();
+  const double mean = pass == 1 ? mean_s[t] : 0.0;
   double s = 0.0;
   if (col < c)
-    for (long long r = q; r < rows; r += 4) s += y[r * ldy + col];
+    for (long long r = r0 + q; r < r1; r += 4) {
+      const double v = (double)y[r * ldy + col] - mean;
+      s += pass == 1 ? v * v : v;
+    }
   red[q][t] = s;
   __syncthreads();
-  const double mean = (red[0][t] + red[1][t] + red[2][t] + red[3][t]) / (double)rows;
-  __syncthreads();
-  double v = 0.0;
-  if (col < c)
-    for (long long r = q; r < rows; r += 4) {
-      const double d = y[r * ldy + col] - mean;
-      v += d * d;
-    }
-  red[q][t] = v;
-  __syncthreads();
-  if (q == 0 && col < c) {
-    const double var = (red[0][t] + red[1][t] + red[2][t] + red[3][t]) / (double)rows;
-    const double si = init_scale / sqrt(var + 1e-10);
-    g[col] = (float)(g[col] * si);
-    b[col] = (float)(b[col] - mean * si);
-  }
+  if (q == 0 && col < c)
+    part[((long long)pass * nrb + blockIdx.y) * c + col] = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+}
+__global__ void wn_init_fin_kernel(const double* part, int nrb, long long rows, int c, float init_scale, float* g,
+                                   float* b) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= c) return;
+  const double mean = wni_mean(part, nrb, c, col, rows);
+  const double var = wni_mean(part + (long long)nrb * c, nrb, c, col, rows);
+  const double si = init_scale / sqrt(var + 1e-10);
+  g[col] = (float)(g[col] * si);
+  b[col] = (float)(b[col] - mean * si);
 }
 
 __global__ void ema_kernel(float* avg, const float* p, long long n, float decay) {
@@ -987,12 +1334,13 @@ int svae_pcnn_wnorm_bwd(const float* V, const float* g, const float* norm, const
   return hipchk();
 }
 
-int svae_pcnn_conv(const float* x, int n, int hi, int wi, int cin, int ldx, const void* wk, int kpad,
+int svae_pcnn_conv(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, const void* wk, int kpad,
                    const float* bias, float* y, int ho, int wo, int cout, int ldy, int kh, int kw, int s, int pt,
                    int pl, int mode, int accumulate, int zero_edge, void* stream) {
   const PcGeom g = make_geom(n, hi, wi, cin, ldx, ho, wo, cout, kh, kw, s, pt, pl, mode);
   if (!x || !wk || !y || !geom_ok(g) || ldy < cout || kpad < cin || kpad % 16 || zero_edge < 0 || zero_edge > 2)
     return bad("pcnn_conv: bad arguments");
+  if (x_bf16 && (cin % 8 || ldx % 8 || kpad % 32)) return bad("pcnn_conv: bf16 input needs cin, ldx % 8 == 0");
   const long long rows = (long long)n * ho * wo;
   hipStream_t st = (hipStream_t)stream;
   const __bf16* w = (const __bf16*)wk;
@@ -1001,33 +1349,59 @@ int svae_pcnn_conv(const float* x, int n, int hi, int wi, int cin, int ldx, cons
     const char* v = getenv("SVAE_PC_CONV1");
     return v && v[0] == '1';
   }();
-  if (kpad % 32 == 0 && !old) {  // LDS-staged kernel, up to 160 output channels per block
+  static const int pc3 = [] {  // SVAE_PC3: 0 = stride-1 convs on pc_conv2 too; 1 / 2 = halo kernel, TM
+    const char* v = getenv("SVAE_PC3");
+    return v ? atoi(v) : 1;
+  }();
+  if (kpad % 32 == 0 && !old) {  // LDS-staged kernels, up to 160 output channels per block
     const int n32 = (cout + 31) / 32;
     const int tiles = (n32 + 4) / 5;
     const int NT = (n32 + tiles - 1) / tiles;
-    const dim3 grid(gx, tiles);
-    switch (NT) {
-      case 1: hipLaunchKernelGGL(pc_conv2_kernel<1>, grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge); break;
-      case 2: hipLaunchKernelGGL(pc_conv2_kernel<2>, grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge); break;
-      case 3: hipLaunchKernelGGL(pc_conv2_kernel<3>, grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge); break;
-      case 4: hipLaunchKernelGGL(pc_conv2_kernel<4>, grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge); break;
-      default: hipLaunchKernelGGL(pc_conv2_kernel<5>, grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge); break;
+    Pc3 h;
+    size_t lds = 0;
+    if (pc3 >= 1 && pc3 <= 2 && pc3_plan(g, kpad, pc3, &h, &lds)) {  // stride 1: one halo window per chunk
+#define PC3_NT(TMV, XBV)                                                                                \
+  switch (NT) {                                                                                         \
+    case 1: pc3_launch<1, TMV, XBV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, st); break; \
+    case 2: pc3_launch<2, TMV, XBV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, st); break; \
+    case 3: pc3_launch<3, TMV, XBV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, st); break; \
+    case 4: pc3_launch<4, TMV, XBV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, st); break; \
+    default: pc3_launch<5, TMV, XBV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, st); break; \
+  }
+      if (x_bf16) { PC3_NT(1, true) }
+      else if (pc3 == 2) { PC3_NT(2, false) }
+      else { PC3_NT(1, false) }
+#undef PC3_NT
+      return hipchk();
     }
+    const dim3 grid(gx, tiles);
+#define PC2_NT(XBV)                                                                                                   \
+  switch (NT) {                                                                                                      \
+    case 1: hipLaunchKernelGGL((pc_conv2_kernel<1, XBV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge); break; \
+    case 2: hipLaunchKernelGGL((pc_conv2_kernel<2, XBV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge); break; \
+    case 3: hipLaunchKernelGGL((pc_conv2_kernel<3, XBV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge); break; \
+    case 4: hipLaunchKernelGGL((pc_conv2_kernel<4, XBV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge); break; \
+    default: hipLaunchKernelGGL((pc_conv2_kernel<5, XBV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge); break; \
+  }
+    if (x_bf16) { PC2_NT(true) } else { PC2_NT(false) }
+#undef PC2_NT
     return hipchk();
   }
+  if (x_bf16) return bad("pcnn_conv: bf16 input on the register-direct kernel (SVAE_PC_CONV1)");
   // register-direct kernel: two 32-column subtiles per wave (wider tiles measured slower here)
+  const float* xf = (const float*)x;
   if (cout > 32)
-    hipLaunchKernelGGL(pc_conv_kernel<2>, dim3(gx, (cout + 63) / 64), dim3(256), 0, st, g, x, w, kpad, bias, y, ldy,
+    hipLaunchKernelGGL(pc_conv_kernel<2>, dim3(gx, (cout + 63) / 64), dim3(256), 0, st, g, xf, w, kpad, bias, y, ldy,
                        accumulate, zero_edge);
   else
-    hipLaunchKernelGGL(pc_conv_kernel<1>, dim3(gx, 1), dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate,
+    hipLaunchKernelGGL(pc_conv_kernel<1>, dim3(gx, 1), dim3(256), 0, st, g, xf, w, kpad, bias, y, ldy, accumulate,
                        zero_edge);
   return hipchk();
 }
 
-int svae_pcnn_conv_wgrad(const float* x, int n, int hi, int wi, int cin, int ldx, const float* dy, int ldd, int ho,
-                         int wo, int cout, int kh, int kw, int s, int pt, int pl, int mode, float* dW, float* scratch,
-                         int64_t scratch_elems, void* stream) {
+int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, const float* dy, int ldd,
+                         int ho, int wo, int cout, int kh, int kw, int s, int pt, int pl, int mode, float* dW,
+                         float* scratch, int64_t scratch_elems, void* stream) {
   const PcGeom g = make_geom(n, hi, wi, cin, ldx, ho, wo, cout, kh, kw, s, pt, pl, mode);
   if (!x || !dy || !dW || !scratch || !geom_ok(g) || ldd < cout || ldd % 4 || cout % 4)
     return bad("pcnn_wgrad: bad arguments");
@@ -1045,8 +1419,12 @@ int svae_pcnn_conv_wgrad(const float* x, int n, int hi, int wi, int cin, int ldx
   rps = (rps + 63) / 64 * 64;
   ns = (rows + rps - 1) / rps;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(pc_wgrad_kernel, dim3(tiles, taps, (unsigned)ns), dim3(256), 0, st, g, x, dy, ldd, rows, rps,
-                     scratch);
+  if (x_bf16)
+    hipLaunchKernelGGL(pc_wgrad_kernel<true>, dim3(tiles, taps, (unsigned)ns), dim3(256), 0, st, g, x, dy, ldd, rows,
+                       rps, scratch);
+  else
+    hipLaunchKernelGGL(pc_wgrad_kernel<false>, dim3(tiles, taps, (unsigned)ns), dim3(256), 0, st, g, x, dy, ldd, rows,
+                       rps, scratch);
   hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(wsz)), dim3(256), 0, st, scratch, (int)ns, wsz, dW);
   return hipchk();
 }
@@ -1076,19 +1454,41 @@ int svae_pcnn_mask_edge(float* x, int n, int ho, int wo, int c, int ldx, int mas
   return hipchk();
 }
 
-int svae_pcnn_nonlin(const float* x, int64_t rows, int c, int ldx, int kind, float* y, int ldy, void* stream) {
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+int svae_pcnn_nonlin(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, void* y, int ldy,
+                     int y_bf16, void* stream) {
   if (!x || !y || rows < 1 || c < 1 || kind < 0 || kind > 2 || ldx < c || ldy < (kind == 2 ? 2 * c : c))
     return bad("pcnn_nonlin: bad arguments");
-  hipLaunchKernelGGL(nonlin_kernel, dim3(blocks_for(rows * c)), dim3(256), 0, (hipStream_t)stream, x, (long long)rows,
-                     c, ldx, kind, y, ldy);
+  hipStream_t st = (hipStream_t)stream;
+  const bool vec = c % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && al16(x) && (!mask || al16(mask)) &&
+                   (y_bf16 ? ((uintptr_t)y & 7) == 0 : al16(y));
+  if (vec) {
+    const dim3 grid((unsigned)((rows + NL_RPB - 1) / NL_RPB));
+    if (y_bf16) hipLaunchKernelGGL(nonlin4_kernel<true>, grid, dim3(256), 0, st, x, (long long)rows, c, ldx, kind, mask, y, ldy);
+    else hipLaunchKernelGGL(nonlin4_kernel<false>, grid, dim3(256), 0, st, x, (long long)rows, c, ldx, kind, mask, y, ldy);
+    return hipchk();
+  }
+  if (mask || y_bf16) return bad("pcnn_nonlin: a mask or bf16 output needs 4-channel aligned rows");
+  hipLaunchKernelGGL(nonlin_kernel, dim3(blocks_for(rows * c)), dim3(256), 0, st, x, (long long)rows, c, ldx, kind,
+                     (float*)y, ldy);
   return hipchk();
 }
 
-int svae_pcnn_nonlin_bwd(const float* x, int64_t rows, int c, int ldx, int kind, const float* dy, int ldy, float* dx,
-                         int lddx, int accumulate, void* stream) {
+int svae_pcnn_nonlin_bwd(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, const float* dy,
+                         int ldy, float* dx, int lddx, int accumulate, void* stream) {
   if (!x || !dy || !dx || rows < 1 || c < 1 || kind < 0 || kind > 2) return bad("pcnn_nonlin_bwd: bad arguments");
-  hipLaunchKernelGGL(nonlin_bwd_kernel, dim3(blocks_for(rows * c)), dim3(256), 0, (hipStream_t)stream, x,
-                     (long long)rows, c, ldx, kind, dy, ldy, dx, lddx, accumulate);
+  hipStream_t st = (hipStream_t)stream;
+  const bool vec = c % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && lddx % 4 == 0 && al16(x) && al16(dy) && al16(dx) &&
+                   (!mask || al16(mask));
+  if (vec) {
+    hipLaunchKernelGGL(nonlin4_bwd_kernel, dim3((unsigned)((rows + NL_RPB - 1) / NL_RPB)), dim3(256), 0, st, x,
+                       (long long)rows, c, ldx, kind, mask, dy, ldy, dx, lddx, accumulate);
+    return hipchk();
+  }
+  if (mask) return bad("pcnn_nonlin_bwd: a mask needs 4-channel aligned rows");
+  hipLaunchKernelGGL(nonlin_bwd_kernel, dim3(blocks_for(rows * c)), dim3(256), 0, st, x, (long long)rows, c, ldx, kind,
+                     dy, ldy, dx, lddx, accumulate);
   return hipchk();
 }
 
@@ -1213,10 +1613,17 @@ int svae_pcnn_highway(const float* s, const float* prev, const float* z, const f
 
 int svae_pcnn_wn_init(const float* y, int64_t rows, int c, int ldy, float init_scale, float* g, float* b,
                       double* scratch, void* stream) {
-  (void)scratch;
-  if (!y || !g || !b || rows < 1 || c < 1 || ldy < c) return bad("pcnn_wn_init: bad arguments");
-  hipLaunchKernelGGL(wn_init_kernel, dim3((c + 63) / 64), dim3(256), 0, (hipStream_t)stream, y, (long long)rows, c,
-                     ldy, init_scale, g, b);
+  if (!y || !g || !b || !scratch || rows < 1 || c < 1 || ldy < c) return bad("pcnn_wn_init: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  long long nrb = (rows + 1023) / 1024;  // >= 1024 rows per block, at most WNI_MAXRB blocks per column group
+  if (nrb > WNI_MAXRB) nrb = WNI_MAXRB;
+  const long long rpb = (rows + nrb - 1) / nrb;
+  nrb = (rows + rpb - 1) / rpb;
+  const dim3 grid((c + 63) / 64, (unsigned)nrb);
+  for (int pass = 0; pass < 2; ++pass)
+    hipLaunchKernelGGL(wn_mom_kernel, grid, dim3(256), 0, st, y, (long long)rows, c, ldy, rpb, (int)nrb, pass, scratch);
+  hipLaunchKernelGGL(wn_init_fin_kernel, dim3((c + 255) / 256), dim3(256), 0, st, scratch, (int)nrb, (long long)rows, c,
+                     init_scale, g, b);
   return hipchk();
 }
 

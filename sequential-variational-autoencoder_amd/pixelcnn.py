@@ -44,7 +44,8 @@ def _r16(c):
 
 
 class Act:
-    """An NHWC activation: ``buf`` [n*h*w][ld] fp32, channels [off, off + c)."""
+    """An NHWC activation: ``buf`` [n*h*w][ld] fp32 (or bf16: a nonlinearity output read only by the
+    bf16-MFMA convs), channels [off, off + c)."""
     __slots__ = ("buf", "off", "c", "ld", "n", "h", "w")
 
     def __init__(self, buf, c, n, h, w, off=0, ld=None):
@@ -55,8 +56,12 @@ class Act:
     def rows(self):
         return self.n * self.h * self.w
 
+    @property
+    def bf(self):
+        return self.buf.dtype == torch.bfloat16
+
     def ptr(self):
-        return _p(self.buf, self.off)
+        return ctypes.c_void_p(self.buf.data_ptr() + self.buf.element_size() * self.off)
 
 
 def param_shapes(spec):
@@ -257,7 +262,7 @@ class PixelCNNpp:
         if pr:  # bench.py's live roofline probe: an event pair around this forward conv launch
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        _ck(L.svae_pcnn_conv(x.ptr(), x.n, x.h, x.w, cin, x.ld, ctypes.c_void_p(wkf.data_ptr()), kf,
+        _ck(L.svae_pcnn_conv(x.ptr(), x.n, x.h, x.w, cin, x.ld, int(x.bf), ctypes.c_void_p(wkf.data_ptr()), kf,
                              _p(self.P, off_b), out.ptr(), ho, wo, cout, out.ld, kh, kw, s, pt, pl, mode,
                              1 if acc else 0, zero_edge, st))
         if pr:
@@ -268,11 +273,11 @@ class PixelCNNpp:
             src = out
             if acc or zero_edge:
                 src = Act(self._new(x.n * ho * wo, cout), cout, x.n, ho, wo)
-                _ck(L.svae_pcnn_conv(x.ptr(), x.n, x.h, x.w, cin, x.ld, ctypes.c_void_p(wkf.data_ptr()), kf,
+                _ck(L.svae_pcnn_conv(x.ptr(), x.n, x.h, x.w, cin, x.ld, int(x.bf), ctypes.c_void_p(wkf.data_ptr()), kf,
                                      _p(self.P, off_b), src.ptr(), ho, wo, cout, cout, kh, kw, s,
                                      pt - (zero_edge == 1), pl - (zero_edge == 2), mode, 0, 0, st))
             _ck(L.svae_pcnn_wn_init(src.ptr(), src.rows, cout, src.ld, float(init_scale), _p(self.P, off_g),
-                                    _p(self.P, off_b), None, st))
+                                    _p(self.P, off_b), _p(self.scratch), st))
         if self._record:
             geo = (kh, kw, s, pt, pl, mode, zero_edge, kf, kd, off_v, off_g, off_b)
             self._tape.append(lambda: self._wconv_bwd(x, out, norm, wkd, geo))
@@ -290,15 +295,15 @@ class PixelCNNpp:
         _ck(L.svae_pcnn_colsum(_p(dy), y.rows, cout, cout, y.h, y.w, 0, _p(self.G, off_b), 0, _p(self.scratch), st))
         dW = torch.empty(taps * cin * cout, dtype=torch.float32, device=self.dev)
         sc = self.scratch
-        _ck(L.svae_pcnn_conv_wgrad(x.ptr(), x.n, x.h, x.w, cin, x.ld, _p(dy), cout, y.h, y.w, cout, kh, kw, s, pt, pl,
-                                   mode, _p(dW), _p(sc), sc.numel(), st))
+        _ck(L.svae_pcnn_conv_wgrad(x.ptr(), x.n, x.h, x.w, cin, x.ld, int(x.bf), _p(dy), cout, y.h, y.w, cout, kh, kw,
+                                   s, pt, pl, mode, _p(dW), _p(sc), sc.numel(), st))
         _ck(L.svae_pcnn_wnorm_bwd(_p(self.P, off_v), _p(self.P, off_g), _p(norm), _p(dW), taps, cin, cout,
                                   _p(self.G, off_v), _p(self.G, off_g), st))
         if id(x) in self._nograd:
             return
         dx = self._grad(x)
         # the input gradient: the transposed gather over dy with the [tap][Cin][Cout] copy
-        _ck(L.svae_pcnn_conv(_p(dy), y.n, y.h, y.w, cout, cout, ctypes.c_void_p(wkd.data_ptr()), kd, None, _p(dx),
+        _ck(L.svae_pcnn_conv(_p(dy), y.n, y.h, y.w, cout, cout, 0, ctypes.c_void_p(wkd.data_ptr()), kd, None, _p(dx),
                              x.h, x.w, cin, cin, kh, kw, s, pt, pl, 1 - mode, 1, 0, st))
 
     def _dense(self, x, name, cout, init_scale=1.0):
@@ -306,16 +311,21 @@ class PixelCNNpp:
         y = self._wconv(self._view(x, x.rows, 1, 1), name, cout, 1, 1, 1, 0, 0, init_scale=init_scale)
         return self._view(y, x.n, x.h, x.w)
 
-    def _nonlin(self, x, kind):
+    def _nonlin(self, x, kind, mask=None):
+        """y = f(x) (* the dropout keep-mask, fused).  Every nonlinearity output of the network is read
+        only by convolutions (bf16 MFMA operands), so y is stored as bf16 when its channels allow it:
+        the conv result is bitwise the one from fp32 storage (nn.py:270-274: dropout before the conv)."""
         k = NL_KIND[kind]
         c = 2 * x.c if k == 2 else x.c
-        y = Act(self._new(x.rows, c), c, x.n, x.h, x.w)
-        _ck(self.L.svae_pcnn_nonlin(x.ptr(), x.rows, x.c, x.ld, k, y.ptr(), y.ld, self._st()))
+        bf = c % 8 == 0 and x.c % 4 == 0 and x.ld % 4 == 0
+        buf = torch.empty(x.rows, c, dtype=torch.bfloat16 if bf else torch.float32, device=self.dev)
+        y = Act(buf, c, x.n, x.h, x.w)
+        _ck(self.L.svae_pcnn_nonlin(x.ptr(), x.rows, x.c, x.ld, k, _p(mask), y.ptr(), y.ld, int(bf), self._st()))
         if self._record:
             def bwd():
                 if not self._has_grad(y):
                     return
-                _ck(self.L.svae_pcnn_nonlin_bwd(x.ptr(), x.rows, x.c, x.ld, k, _p(self._grad(y)), c,
+                _ck(self.L.svae_pcnn_nonlin_bwd(x.ptr(), x.rows, x.c, x.ld, k, _p(mask), _p(self._grad(y)), c,
                                                 _p(self._grad(x)), x.c, 1, self._st()))
             self._tape.append(bwd)
         return y
@@ -374,10 +384,9 @@ class PixelCNNpp:
         c1 = self._wconv(self._nonlin(x, nl), self._nm("conv2d"), x.c, kh, kw, 1, pt, pl)
         if a is not None:
             self._dense_into(self._nonlin(a, nl), self._nm("dense"), c1)
-        t2 = self._nonlin(c1, nl)
-        mask = self._next_mask(t2.rows, t2.c)
-        if mask is not None:  # training-pass dropout (nn.py:273-274)
-            t2 = self._dropout(t2, mask)
+        # training-pass dropout (nn.py:273-274) fused into the nonlinearity
+        mask = self._next_mask(c1.rows, 2 * c1.c if nl == "concat_elu" else c1.c)
+        t2 = self._nonlin(c1, nl, mask)
         c2 = self._wconv(t2, self._nm("conv2d"), 2 * x.c, kh, kw, 1, pt, pl, init_scale=0.1)
         return self._gate(x, c2, h, self._nm("conditional_weights") + "/hw")
 
@@ -395,18 +404,6 @@ class PixelCNNpp:
             return None
         self.last_masks.append(m)
         return m
-
-    def _dropout(self, x, mask):
-        y = Act(self._new(x.rows, x.c), x.c, x.n, x.h, x.w)
-        _ck(self.L.svae_pcnn_dropout(x.ptr(), x.rows, x.c, x.ld, _p(mask), y.ptr(), y.ld, self._st()))
-        if self._record:
-            def bwd():  # x (a fresh nonlinearity output) has no other consumer: its gradient is written
-                if not self._has_grad(y):
-                    return
-                _ck(self.L.svae_pcnn_dropout(_p(self._grad(y)), x.rows, x.c, x.c, _p(mask), _p(self._grad(x)), x.c,
-                                             self._st()))
-            self._tape.append(bwd)
-        return y
 
     def _dense_into(self, x, name, out):
         self._wconv(self._view(x, x.rows, 1, 1), name, out.c, 1, 1, 1, 0, 0, out=self._view(out, out.rows, 1, 1))

@@ -1,0 +1,103 @@
+"""svae_pcnn_conv (the PixelCNN++ head's gather convolution, include/svae_pcnn.h) against a torch fp64
+reference on the same bf16-rounded operands, over the geometries the head launches: the shifted
+[2, 3] / [2, 2] / [1, 3] / [2, 1] convs (mode 0) and their input gradients (mode 1) at 64x64, 32x32,
+16x16 and 8x8 (several images per block), the 1x1 nin / dense layers, shifted outputs (zero_edge),
+accumulation, channel slices (ldx > cin), 1 - 10 column tiles, and shapes that take the fallback
+kernel (stride 2, ragged rows).  Only bf16 products summed in fp32 differ from the reference."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import pkg_mod
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(x, w, n, hi, wi, cin, ho, wo, cout, kh, kw, s, pt, pl, mode, bias, zero_edge):
+    """out(oy, ox) = sum_taps in(src(oy, ox, ky, kx)) . W[ky][kx] (svae_pcnn.h geometry), fp64."""
+    xi = x.reshape(n, hi, wi, -1)[..., :cin].permute(0, 3, 1, 2).double()
+    wt = w.double()  # [tap][cout][cin]
+    W4 = wt.reshape(kh, kw, cout, cin).permute(2, 3, 0, 1)  # [cout][cin][kh][kw]
+    if mode == 0:
+        # iy = oy*s - pt + ky: cross-correlation over the input padded by pt / pl at the top / left
+        pad_b = max(0, (ho - 1) * s - pt + kh - hi)
+        pad_r = max(0, (wo - 1) * s - pl + kw - wi)
+        xp = F.pad(xi, (pl, pad_r, pt, pad_b))
+        y = F.conv2d(xp, W4, stride=s)[:, :, :ho, :wo]
+    else:
+        assert s == 1
+        # iy = oy + pt - ky: the flipped kernel, origin oy + pt - kh + 1
+        top, left = kh - 1 - pt, kw - 1 - pl
+        pad_b = max(0, ho - 1 + pt - hi + 1)
+        pad_r = max(0, wo - 1 + pl - wi + 1)
+        xp = F.pad(xi, (max(left, 0), pad_r, max(top, 0), pad_b))
+        xp = xp[:, :, max(-top, 0):, max(-left, 0):]
+        y = F.conv2d(xp, W4.flip(2, 3))[:, :, :ho, :wo]
+    y = y.permute(0, 2, 3, 1).reshape(n * ho * wo, cout)
+    if bias is not None:
+        y = y + bias.double()
+    if zero_edge:
+        m = torch.zeros(n, ho, wo, 1, dtype=torch.bool)
+        if zero_edge == 1:
+            m[:, 0] = True
+        else:
+            m[:, :, 0] = True
+        y = torch.where(m.reshape(-1, 1), torch.zeros_like(y), y)
+    return y
+
+
+CASES = [
+    # n, hi, ho, cin, ldx, cout, kh, kw, s, pt, pl, mode, acc, zero_edge
+    (2, 64, 64, 160, 160, 160, 2, 3, 1, 1, 1, 0, 0, 0),    # u-stream resnet conv
+    (2, 64, 64, 160, 160, 320, 2, 3, 1, 1, 1, 1, 0, 0),    # its input gradient, 2 column tiles
+    (2, 32, 32, 64, 96, 96, 2, 2, 1, 1, 1, 0, 1, 0),       # ul-stream conv, channel slice, accumulate
+    (2, 32, 32, 96, 96, 64, 2, 2, 1, 1, 1, 1, 1, 0),
+    (2, 16, 16, 4, 4, 160, 2, 3, 1, 2, 1, 0, 0, 1),        # down_shift(ds_conv(x_pad)) of the input
+    (8, 8, 8, 8, 8, 8, 2, 1, 1, 1, 1, 0, 1, 2),            # right_shift(drs_conv), 4 images per block
+    (8, 8, 8, 8, 8, 8, 1, 3, 1, 1, 1, 1, 0, 0),
+    (512, 1, 1, 320, 320, 100, 1, 1, 1, 0, 0, 0, 0, 0),    # nin / dense (10 M mixture logits)
+    (2, 64, 64, 160, 160, 40, 2, 3, 1, 1, 1, 0, 0, 0),     # 2 column tiles of 32 (one partial)
+    (2, 4, 4, 8, 8, 8, 2, 3, 1, 1, 1, 0, 0, 0),            # ragged rows: fallback kernel
+    (2, 32, 16, 32, 32, 32, 2, 3, 2, 1, 1, 0, 0, 0),       # stride 2: fallback kernel
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "n%d_h%d_%dto%d_k%dx%d_s%d_m%d_a%d_z%d" % (
+    c[0], c[2], c[3], c[5], c[6], c[7], c[8], c[11], c[12], c[13]))
+def test_pcnn_conv_matches_reference(case):
+    n, hi, ho, cin, ldx, cout, kh, kw, s, pt, pl, mode, acc, zero_edge = case
+    wi, wo = hi, ho
+    L = pkg_mod("_lib")
+    rng = np.random.default_rng(hash(case) % 2 ** 32)
+    kpad = (cin + 31) // 32 * 32
+    taps = kh * kw
+    x = torch.tensor(rng.uniform(-1, 1, (n * hi * wi, ldx)), dtype=torch.float32).to(torch.bfloat16).float()
+    w = torch.tensor(rng.normal(0, 0.1, (taps, cout, cin)), dtype=torch.float32).to(torch.bfloat16)
+    wk = torch.zeros(taps, cout, kpad, dtype=torch.bfloat16)
+    wk[:, :, :cin] = w
+    bias = torch.tensor(rng.normal(0, 0.1, cout), dtype=torch.float32)
+    y0 = torch.tensor(rng.normal(0, 1, (n * ho * wo, cout)), dtype=torch.float32)
+    xd, wkd, bd = x.cuda(), wk.cuda(), bias.cuda()
+    yd = y0.clone().cuda() if acc else torch.full((n * ho * wo, cout), float("nan"), device="cuda")
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    L.check(L.lib().svae_pcnn_conv(p(xd), n, hi, wi, cin, ldx, 0, p(wkd), kpad, p(bd), p(yd), ho, wo, cout, cout, kh, kw,
+                                   s, pt, pl, mode, acc, zero_edge, L.stream_ptr()))
+    torch.cuda.synchronize()
+    ref = _ref(x, w.float(), n, hi, wi, cin, ho, wo, cout, kh, kw, s, pt, pl, mode, bias, zero_edge)
+    if acc:
+        ref = ref + y0.double()
+    got = yd.cpu().double()
+    err = float((got - ref).abs().max() / ref.abs().max())
+    print("\nconv %s: max rel err %.2e" % (case, err))
+    assert torch.isfinite(got).all()
+    assert err < 2e-5
+    if cin % 8 == 0 and ldx % 8 == 0:  # the same operand stored as bf16 (x_bf16): bitwise the same result
+        yb = y0.clone().cuda() if acc else torch.full((n * ho * wo, cout), float("nan"), device="cuda")
+        xb = xd.to(torch.bfloat16)
+        L.check(L.lib().svae_pcnn_conv(p(xb), n, hi, wi, cin, ldx, 1, p(wkd), kpad, p(bd), p(yb), ho, wo, cout, cout, kh,
+                                       kw, s, pt, pl, mode, acc, zero_edge, L.stream_ptr()))
+        torch.cuda.synchronize()
+        assert torch.equal(yb.cpu(), yd.cpu())

@@ -91,6 +91,7 @@ def test_pixelvae_step_matches_oracle():
 
 
 def test_pixelvae_train_and_generate():
+    torch.manual_seed(1234)  # the device-drawn dropout masks and sampler uniforms of train()
     pv, cd, ospec, hp, x, tgt, eps, u_mix, u_log, rng = _setup()
     p0 = pv.head.P.clone()
     losses = [pv.train(x, tgt) for _ in range(3)]
