@@ -18,6 +18,7 @@ void svae_tls_error(const std::string& msg);  // engine.cpp: svae_last_error(NUL
 namespace {
 
 typedef __bf16 pc_bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 pc_bf16x4 __attribute__((ext_vector_type(4)));
 typedef float pc_f32x8 __attribute__((ext_vector_type(8)));
 
 int bad(const char* msg) {
@@ -571,7 +572,7 @@ void pc3_launch(const PcGeom& g, const Pc3& h, const void* x, const __bf16* w, i
   const size_t lds = (size_t)(h.npix + g.kh * g.kw * 32 * NT) * PC2_P * 2;
   static bool attr = false;
   if (!attr) {  // the largest window + weight stage: 640 pixels + 6 taps x 160 rows (128 KB)
-    hipFuncSetAttribute((const void*)pc_conv3_kernel<NT, TM, XB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)pc_conv3_kernel<NT, TM, XB>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         (PC3_MAXPIX + PC3_MAXTAPS * 32 * NT) * PC2_P * 2);
     attr = true;
   }
@@ -610,6 +611,7 @@ __global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const void* __r
   // rows, the next chunk loaded into registers while the current one's MFMAs run
   const int lr = tid >> 3, q0 = tid & 7;
   f32x4 xv[2][2], dv[2][2];
+  pc_bf16x8 xb8[2];  // XB: channels 8 q0 .. 8 q0 + 7 of the row in one 16-B load
   auto load = [&](long long rc) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -624,19 +626,15 @@ __global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const void* __r
         if (pc_src(g, oy, ox, ky, kx, iy, ix)) xo = ((long long)(img * g.hi + iy) * g.wi + ix) * g.ldx;
         dp = D + row * ldd;
       }
+      if constexpr (XB) {
+        pc_bf16x8 z8 = {};
+        xb8[u] = (xo >= 0 && ci0 + 8 * q0 < g.cin) ? *(const pc_bf16x8*)((const __bf16*)Xv + xo + ci0 + 8 * q0) : z8;
+      }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int c = (q0 + 8 * j) * 4;
         const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-        xv[u][j] = z;
-        if (xo >= 0 && ci0 + c < g.cin) {
-          if constexpr (XB) {
-            typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-            xv[u][j] = __builtin_convertvector(*(const bf16x4_t*)((const __bf16*)Xv + xo + ci0 + c), f32x4);
-          } else {
-            xv[u][j] = *(const f32x4*)((const float*)Xv + xo + ci0 + c);
-          }
-        }
+        if constexpr (!XB) xv[u][j] = (xo >= 0 && ci0 + c < g.cin) ? *(const f32x4*)((const float*)Xv + xo + ci0 + c) : z;
         dv[u][j] = (dp && co0 + c < g.cout) ? *(const f32x4*)(dp + co0 + c) : z;
       }
     }
@@ -649,7 +647,8 @@ __global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const void* __r
         const int c = (q0 + 8 * j) * 4;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          Xs[buf][(c + e) * PW_RP + lr + 32 * u] = (__bf16)xv[u][j][e];
+          if constexpr (XB) Xs[buf][(8 * q0 + 4 * j + e) * PW_RP + lr + 32 * u] = xb8[u][4 * j + e];
+          else Xs[buf][(c + e) * PW_RP + lr + 32 * u] = (__bf16)xv[u][j][e];
           Ds[buf][(c + e) * PW_RP + lr + 32 * u] = (__bf16)dv[u][j][e];
         }
       }
@@ -755,7 +754,6 @@ __device__ __forceinline__ float delu_f(float x) { return x > 0.f ? 1.f : expf(x
 // or bf16 -- bf16 when its only consumers are the bf16-MFMA convs, which round it the same way --
 // and its backward dx (+)= f'(x) * (dy * mask).
 #define NL_RPB 64
-typedef __bf16 pc_bf16x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void nl_fwd4(f32x4 v, int kind, f32x4& a, f32x4& b) {
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -1408,6 +1406,7 @@ int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx,
   const long long rows = (long long)n * ho * wo;
   const int taps = kh * kw;
   const long long wsz = (long long)taps * cin * cout;
+  hipStream_t st = (hipStream_t)stream;
   const int tiles = ((cin + 63) / 64) * ((cout + 63) / 64);
   // splits: ~2048 blocks, >= 256 rows (8 chunks) per split, bounded by the scratch slabs
   long long ns = (2048 + (long long)tiles * taps - 1) / ((long long)tiles * taps);
@@ -1418,7 +1417,6 @@ int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx,
   long long rps = (rows + ns - 1) / ns;
   rps = (rps + 63) / 64 * 64;
   ns = (rows + rps - 1) / rps;
-  hipStream_t st = (hipStream_t)stream;
   if (x_bf16)
     hipLaunchKernelGGL(pc_wgrad_kernel<true>, dim3(tiles, taps, (unsigned)ns), dim3(256), 0, st, g, x, dy, ldd, rows,
                        rps, scratch);

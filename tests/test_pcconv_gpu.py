@@ -101,3 +101,54 @@ def test_pcnn_conv_matches_reference(case):
                                        kw, s, pt, pl, mode, acc, zero_edge, L.stream_ptr()))
         torch.cuda.synchronize()
         assert torch.equal(yb.cpu(), yd.cpu())
+
+
+def _gathered(x, n, hi, wi, cin, ho, wo, kh, kw, pt, pl, mode, ky, kx):
+    """X[src(p, tap)] for every output pixel p of a stride-1 conv (zero outside the image), fp64."""
+    xi = x.reshape(n, hi, wi, -1)[..., :cin].double()
+    if mode == 0:
+        top, left, oy, ox = pt, pl, ky, kx
+    else:
+        top, left, oy, ox = kh - 1 - pt, kw - 1 - pl, kh - 1 - ky, kw - 1 - kx
+    big = torch.zeros(n, ho + kh + abs(top) + hi, wo + kw + abs(left) + wi, cin, dtype=torch.float64)
+    big[:, kh + abs(top) + top - kh:, :][:, :hi, :][:, :, kw + abs(left) + left - kw:][:, :, :wi] = xi
+    y0, x0 = kh + abs(top) - kh + oy, kw + abs(left) - kw + ox
+    return big[:, y0:y0 + ho, x0:x0 + wo].reshape(n * ho * wo, cin)
+
+
+WCASES = [
+    # n, h, cin, ldx, cout, kh, kw, pt, pl, mode, x_bf16
+    (2, 64, 160, 160, 160, 2, 3, 1, 1, 0, 1),     # resnet conv, bf16 input
+    (2, 64, 160, 160, 320, 2, 2, 1, 1, 0, 1),
+    (2, 32, 64, 96, 96, 2, 3, 1, 1, 1, 0),        # mode 1, fp32 input, channel slice
+    (2, 16, 32, 32, 64, 2, 3, 2, 1, 0, 0),
+    (512, 1, 320, 320, 160, 1, 1, 0, 0, 0, 1),    # nin
+    (8, 8, 32, 32, 32, 2, 2, 1, 1, 0, 1),
+    (2, 16, 4, 4, 32, 2, 3, 2, 1, 0, 0),          # 4 input channels (x_pad)
+]
+
+
+@pytest.mark.parametrize("case", WCASES, ids=lambda c: "n%d_h%d_%dto%d_k%dx%d_m%d_xb%d" % (
+    c[0], c[1], c[2], c[4], c[5], c[6], c[9], c[10]))
+def test_pcnn_wgrad_matches_reference(case):
+    n, h, cin, ldx, cout, kh, kw, pt, pl, mode, xb = case
+    L = pkg_mod("_lib")
+    rng = np.random.default_rng(hash(case) % 2 ** 32)
+    x = torch.tensor(rng.uniform(-1, 1, (n * h * h, ldx)), dtype=torch.float32).to(torch.bfloat16).float()
+    d = torch.tensor(rng.normal(0, 1, (n * h * h, cout)), dtype=torch.float32)
+    db = d.to(torch.bfloat16).double()  # the kernels stage D as bf16
+    ref = torch.stack([_gathered(x, n, h, h, cin, h, h, kh, kw, pt, pl, mode, t // kw, t % kw).T @ db
+                       for t in range(kh * kw)])
+    xd = x.cuda().to(torch.bfloat16) if xb else x.cuda()
+    dd = d.cuda()
+    dW = torch.full((kh * kw, cin, cout), float("nan"), device="cuda")
+    sc = torch.empty(1 << 24, device="cuda")
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    L.check(L.lib().svae_pcnn_conv_wgrad(p(xd), n, h, h, cin, ldx, xb, p(dd), cout, h, h, cout, kh, kw, 1, pt, pl, mode,
+                                         p(dW), p(sc), sc.numel(), L.stream_ptr()))
+    torch.cuda.synchronize()
+    got = dW.cpu().double()
+    err = float((got - ref).abs().max() / ref.abs().max())
+    print("\nwgrad %s: max rel err %.2e" % (case, err))
+    assert torch.isfinite(got).all()
+    assert err < 1e-5

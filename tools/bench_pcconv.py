@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--xb", action="store_true", help="bf16 input for the forward (mode 0) convs")
+    ap.add_argument("--wgrad", action="store_true", help="time svae_pcnn_conv_wgrad of the forward (mode 0) shapes")
     ap.add_argument("--shape", default=None, help="only res,cin,cout,kh,kw,mode (e.g. 64,160,160,2,3,0)")
     a = ap.parse_args()
     lib = L.lib()
@@ -47,13 +48,25 @@ def main():
         x = torch.randn(rows, cin, device="cuda").to(torch.bfloat16 if xb else torch.float32)
         wk = (torch.randn(kh * kw, cout, kpad, device="cuda") * 0.05).to(torch.bfloat16)
         y = torch.empty(rows, cout, device="cuda")
-        args = (p(x), n_, hi, hi, cin, cin, int(xb), p(wk), kpad, None, p(y), ho, ho, cout, cout, kh, kw, 1, pt, pl, mode, 0, 0, st)
+        if a.wgrad:
+            if mode != 0:
+                continue
+            dy = torch.randn(rows, cout, device="cuda")
+            dW = torch.empty(kh * kw * cin * cout, device="cuda")
+            sc = torch.empty(1 << 26, device="cuda")
+            fn = lib.svae_pcnn_conv_wgrad
+            args = (p(x), n_, hi, hi, cin, cin, int(xb), p(dy), cout, ho, ho, cout, kh, kw, 1, pt, pl, mode, p(dW), p(sc),
+                    sc.numel(), st)
+        else:
+            fn = lib.svae_pcnn_conv
+            args = (p(x), n_, hi, hi, cin, cin, int(xb), p(wk), kpad, None, p(y), ho, ho, cout, cout, kh, kw, 1, pt, pl, mode,
+                    0, 0, st)
         for _ in range(2):
-            L.check(lib.svae_pcnn_conv(*args))
+            L.check(fn(*args))
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(a.reps):
-            L.check(lib.svae_pcnn_conv(*args))
+            L.check(fn(*args))
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / a.reps
@@ -62,7 +75,7 @@ def main():
         tot_f += fl
         print("res %2d %3d->%3d k%dx%d mode %d: %8.1f us  %7.1f TF/s" % (res, cin, cout, kh, kw, mode, us, fl / us / 1e6),
               flush=True)
-    print("SVAE_PC3=%s xb=%d total %.1f us, %.1f TF/s" % (os.environ.get("SVAE_PC3", "1"), int(a.xb), tot_t, tot_f / tot_t / 1e6))
+    print("%s SVAE_PC3=%s xb=%d total %.1f us, %.1f TF/s" % ("wgrad" if a.wgrad else "conv", os.environ.get("SVAE_PC3", "1"), int(a.xb), tot_t, tot_f / tot_t / 1e6))
 
 
 if __name__ == "__main__":
