@@ -32,7 +32,7 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no 2:1 s
 # wgrad_halo2_kernel) is reported as the secondary entry.
 DOMINANT_KID = "KID_HALO_KW"
 SECONDARY_KID = "KID_WHALO2_S1"
-PMC_FILE = "profiles/r03_v2_pmc_traffic.json"  # tools/gpu/r03_pmc.sh (bench command, two passes, calibrated FETCH rules)
+PMC_FILE = "profiles/r03_v3_pmc_traffic.json"  # tools/gpu/r03_final.sh (bench command, two passes, calibrated FETCH rules)
 
 
 # metric / workload per preset (BASELINE.json configs[1] is the headline: CelebA B=128)
@@ -297,7 +297,7 @@ def run_pixelvae(args, cfgmod):
         "roofline": None if ach is None else {
             "bound": "mfma", "achieved": round(ach, 3), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 5), "traffic": None,
-            "kernel": "pc_conv2_kernel (PixelCNN++ head forward convolutions, all instances)",
+            "kernel": "pc_conv3_kernel + pc_conv2_kernel (PixelCNN++ head forward convolutions, all instances)",
             "timed_launches": len(probe), "avg_launch_us": round(pms * 1e3 / max(1, len(probe)), 2),
             "step_achieved_tflops": round((head_flops + vae_flops) / (ms / 1e3) / 1e12, 3)},
         "cpu_baseline": None,
