@@ -346,9 +346,10 @@ int wgrad_halo2_enabled() {
 // Config per layer: WN = 2 where N >= 64 (one staged G window feeds 64 D columns), else the
 // 32-column tile with two K-interleaved wave sets; KYR = 4 (all 16 taps per block; the 8-tap
 // variant and the double-buffered stage were measured slower in round 2 and are not built).
-// Split count: ~target blocks over the machine (SVAE_WH2_TARGET, default 128: in the step the
-// kernel shares the GPU with the main stream, and half the splits halve the slab traffic), >= minch chunks
-// per split (SVAE_WH2_MINCH, default 4), slab within capacity.
+// Split count: ~target blocks over the machine (SVAE_WH2_TARGET, default 64: in the step the kernel
+// shares the GPU with the main stream, and every halving of the splits halves the partial-slab writes
+// and the reduce's reads; 128 -> 64 measured within noise, profiles/r03_ab2.txt), >= minch chunks per
+// split (SVAE_WH2_MINCH, default 4), slab within capacity.
 // stride 2 (SVAE_WH2_S2=0 keeps those layers on gemm_bf16.hip's generic halo weight-GEMM): 64-pixel
 // chunks (the window is ~4x the chunk's pixels), row-space widths 8 and 16
 static int wh2_cp(int WO, int S) { return S == 2 ? 64 : (WO == 32 ? 128 : 256); }
@@ -375,7 +376,7 @@ int wgrad_halo2(const WgArgs& w, int groups, float* slab, long long slab_cap, fl
   const int WO = w.g.Wo;
   const int S = w.g.stride;
   const int cp = wh2_cp(WO, S);
-  static const int target = env_int("SVAE_WH2_TARGET", 128);
+  static const int target = env_int("SVAE_WH2_TARGET", 64);
   static const int minch = env_int("SVAE_WH2_MINCH", 4);
   // SVAE_WH2_NSW=2: a 64-column block as 4 waves of two 32-column subtiles (each transposed A
   // fragment feeds two MFMAs) instead of 8 waves of one
