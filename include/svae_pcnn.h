@@ -48,10 +48,11 @@ int svae_pcnn_conv(const void* x, int n, int hi, int wi, int cin, int ldx, int x
                    int pl, int mode, int accumulate, int zero_edge, void* stream);
 /* weight gradient of that conv: dW[tap][cin][cout] = sum_rows gather(x)[row][ci] . dy[row][co]
  * (split over rows into `scratch` slabs, then a fixed-order reduce: deterministic); x fp32 or bf16
- * (x_bf16 = 1). */
+ * (x_bf16 = 1).  dbias (may be NULL): the bias gradient sum_rows dy[row][co], written, from the same
+ * pass over dy (fp32 sums). */
 int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, const float* dy, int ldd, int ho,
-                         int wo, int cout, int kh, int kw, int s, int pt, int pl, int mode, float* dW, float* scratch,
-                         int64_t scratch_elems, void* stream);
+                         int wo, int cout, int kh, int kw, int s, int pt, int pl, int mode, float* dW, float* dbias,
+                         float* scratch, int64_t scratch_elems, void* stream);
 /* column sums over rows (bias gradients): out[c] (+)= sum_r x[r][c]; mask_edge 1 / 2 skips
  * rows with oy == 0 / ox == 0 of a [n][ho][wo] row space (the zeroed shifted outputs). */
 int svae_pcnn_colsum(const float* x, int64_t rows, int c, int ldx, int ho, int wo, int mask_edge, float* out,

@@ -106,7 +106,7 @@ def lib():
         "svae_pcnn_conv": ([vp, i32, i32, i32, i32, i32, i32, vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, i32,
                             i32, i32, i32, i32, i32, vp], i32),
         "svae_pcnn_conv_wgrad": ([vp, i32, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32,
-                                  i32, vp, vp, i64, vp], i32),
+                                  i32, vp, vp, vp, i64, vp], i32),
         "svae_pcnn_colsum": ([vp, i64, i32, i32, i32, i32, i32, vp, i32, vp, vp], i32),
         "svae_pcnn_mask_edge": ([vp, i32, i32, i32, i32, i32, i32, vp], i32),
         "svae_pcnn_nonlin": ([vp, i64, i32, i32, i32, vp, vp, i32, i32, vp], i32),

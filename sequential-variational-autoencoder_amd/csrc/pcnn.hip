@@ -588,10 +588,13 @@ void pc3_launch(const PcGeom& g, const Pc3& h, const void* x, const __bf16* w, i
 // each MFMA fragment is one 16-B LDS read).  Partial slabs [split][tap][ci][co].
 // ---------------------------------------------------------------------------------------------
 #define PW_RP 72  // LDS row pitch (bf16): 64 rows + 8 pad
+// bsum != NULL: the blocks of tap 0 and the first ci tile also sum their D rows per column (fp32,
+// before the bf16 staging) into bsum[split][cout]: the conv's bias gradient without another pass over dy
 template <bool XB>
 __global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const void* __restrict__ Xv,
                                                        const float* __restrict__ D, int ldd, long long rows,
-                                                       long long rows_per_split, float* __restrict__ part) {
+                                                       long long rows_per_split, float* __restrict__ part,
+                                                       float* __restrict__ bsum) {
   __shared__ __attribute__((aligned(16))) __bf16 Xs[2][64 * PW_RP];
   __shared__ __attribute__((aligned(16))) __bf16 Ds[2][64 * PW_RP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
@@ -639,7 +642,15 @@ __global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const void* __r
       }
     }
   };
+  const bool bias_blk = bsum && tap == 0 && ci0 == 0;
+  f32x4 bacc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   auto store = [&](int buf) {
+    if (bias_blk) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bacc[j] += dv[u][j];
+    }
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -678,6 +689,19 @@ __global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const void* __r
   for (int r = 0; r < 16; ++r) {
     const int ci = ci0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
     if (ci < g.cin && co < g.cout) out[(long long)ci * g.cout + co] = acc[r];
+  }
+  if (bias_blk) {  // column sums: the 32 row lanes combined in lane order through LDS (the loop's last barrier passed)
+    float* red = (float*)Xs;  // [32][64]
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[lr * 64 + (q0 + 8 * j) * 4 + e] = bacc[j][e];
+    __syncthreads();
+    if (tid < 64 && co0 + tid < g.cout) {
+      float v = 0.f;
+      for (int i = 0; i < 32; ++i) v += red[i * 64 + tid];
+      bsum[(long long)split * g.cout + co0 + tid] = v;
+    }
   }
 }
 
@@ -1399,7 +1423,7 @@ int svae_pcnn_conv(const void* x, int n, int hi, int wi, int cin, int ldx, int x
 
 int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, const float* dy, int ldd,
                          int ho, int wo, int cout, int kh, int kw, int s, int pt, int pl, int mode, float* dW,
-                         float* scratch, int64_t scratch_elems, void* stream) {
+                         float* dbias, float* scratch, int64_t scratch_elems, void* stream) {
   const PcGeom g = make_geom(n, hi, wi, cin, ldx, ho, wo, cout, kh, kw, s, pt, pl, mode);
   if (!x || !dy || !dW || !scratch || !geom_ok(g) || ldd < cout || ldd % 4 || cout % 4)
     return bad("pcnn_wgrad: bad arguments");
@@ -1412,18 +1436,22 @@ int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx,
   long long ns = (2048 + (long long)tiles * taps - 1) / ((long long)tiles * taps);
   const long long max_rows = (rows + 255) / 256;
   if (ns > max_rows) ns = max_rows;
-  if (ns > scratch_elems / wsz) ns = scratch_elems / wsz;
+  if (ns > scratch_elems / (wsz + cout)) ns = scratch_elems / (wsz + cout);  // slabs + bias partials
   if (ns < 1) return bad("pcnn_wgrad: scratch too small");
   long long rps = (rows + ns - 1) / ns;
   rps = (rps + 63) / 64 * 64;
   ns = (rows + rps - 1) / rps;
+  float* bpart = dbias ? scratch + ns * wsz : nullptr;
   if (x_bf16)
     hipLaunchKernelGGL(pc_wgrad_kernel<true>, dim3(tiles, taps, (unsigned)ns), dim3(256), 0, st, g, x, dy, ldd, rows,
-                       rps, scratch);
+                       rps, scratch, bpart);
   else
     hipLaunchKernelGGL(pc_wgrad_kernel<false>, dim3(tiles, taps, (unsigned)ns), dim3(256), 0, st, g, x, dy, ldd, rows,
-                       rps, scratch);
+                       rps, scratch, bpart);
   hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(wsz)), dim3(256), 0, st, scratch, (int)ns, wsz, dW);
+  if (dbias)
+    hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(cout)), dim3(256), 0, st, bpart, (int)ns, (long long)cout,
+                       dbias);
   return hipchk();
 }
 

@@ -220,6 +220,30 @@ class PixelCNNpp:
             self._keep.append(a)
         return g
 
+    def _gout(self, a):
+        """(gradient buffer of ``a``, accumulate flag) for an op that adds its contribution: the first
+        contribution WRITES a fresh buffer (no zero fill, no read-modify-write), later ones accumulate."""
+        while id(a) in self._same:
+            a = self._same[id(a)]
+        g = self._g.get(id(a))
+        if g is not None:
+            return g, 1
+        g = torch.empty(a.rows, a.c, dtype=torch.float32, device=self.dev)
+        self._g[id(a)] = g
+        self._keep.append(a)
+        return g, 0
+
+    def _galias(self, a, g):
+        """Make ``g`` (a dead gradient buffer of ``a``'s shape) the gradient of ``a`` if it has none yet;
+        returns False if ``a`` already has one (the caller then accumulates into it)."""
+        while id(a) in self._same:
+            a = self._same[id(a)]
+        if id(a) in self._g or tuple(g.shape) != (a.rows, a.c):
+            return False
+        self._g[id(a)] = g
+        self._keep.append(a)
+        return True
+
     def _has_grad(self, a):
         while id(a) in self._same:
             a = self._same[id(a)]
@@ -292,19 +316,19 @@ class PixelCNNpp:
         if zero_edge:  # the zeroed shifted outputs pass no gradient
             dy = dy.clone()
             _ck(L.svae_pcnn_mask_edge(_p(dy), y.n, y.h, y.w, cout, cout, zero_edge, st))
-        _ck(L.svae_pcnn_colsum(_p(dy), y.rows, cout, cout, y.h, y.w, 0, _p(self.G, off_b), 0, _p(self.scratch), st))
         dW = torch.empty(taps * cin * cout, dtype=torch.float32, device=self.dev)
         sc = self.scratch
+        # dW and the bias gradient (written into G) from one pass over dy
         _ck(L.svae_pcnn_conv_wgrad(x.ptr(), x.n, x.h, x.w, cin, x.ld, int(x.bf), _p(dy), cout, y.h, y.w, cout, kh, kw,
-                                   s, pt, pl, mode, _p(dW), _p(sc), sc.numel(), st))
+                                   s, pt, pl, mode, _p(dW), _p(self.G, off_b), _p(sc), sc.numel(), st))
         _ck(L.svae_pcnn_wnorm_bwd(_p(self.P, off_v), _p(self.P, off_g), _p(norm), _p(dW), taps, cin, cout,
                                   _p(self.G, off_v), _p(self.G, off_g), st))
         if id(x) in self._nograd:
             return
-        dx = self._grad(x)
+        dx, dacc = self._gout(x)
         # the input gradient: the transposed gather over dy with the [tap][Cin][Cout] copy
         _ck(L.svae_pcnn_conv(_p(dy), y.n, y.h, y.w, cout, cout, 0, ctypes.c_void_p(wkd.data_ptr()), kd, None, _p(dx),
-                             x.h, x.w, cin, cin, kh, kw, s, pt, pl, 1 - mode, 1, 0, st))
+                             x.h, x.w, cin, cin, kh, kw, s, pt, pl, 1 - mode, dacc, 0, st))
 
     def _dense(self, x, name, cout, init_scale=1.0):
         """nn.nin / dense over the channel axis (nn.py:255-260): a 1x1 gather GEMM over every pixel."""
@@ -325,8 +349,9 @@ class PixelCNNpp:
             def bwd():
                 if not self._has_grad(y):
                     return
+                dx, dacc = self._gout(x)
                 _ck(self.L.svae_pcnn_nonlin_bwd(x.ptr(), x.rows, x.c, x.ld, k, _p(mask), _p(self._grad(y)), c,
-                                                _p(self._grad(x)), x.c, 1, self._st()))
+                                                _p(dx), x.c, dacc, self._st()))
             self._tape.append(bwd)
         return y
 
@@ -341,8 +366,10 @@ class PixelCNNpp:
                 if not self._has_grad(y):
                     return
                 dy = self._grad(y)
-                _ck(self.L.svae_pcnn_copy(_p(dy), c, a.rows, a.c, _p(self._grad(a)), a.c, 1, self._st()))
-                _ck(self.L.svae_pcnn_copy(_p(dy, a.c), c, b.rows, b.c, _p(self._grad(b)), b.c, 1, self._st()))
+                da, aacc = self._gout(a)
+                _ck(self.L.svae_pcnn_copy(_p(dy), c, a.rows, a.c, _p(da), a.c, aacc, self._st()))
+                db, bacc = self._gout(b)
+                _ck(self.L.svae_pcnn_copy(_p(dy, a.c), c, b.rows, b.c, _p(db), b.c, bacc, self._st()))
             self._tape.append(bwd)
         return y
 
@@ -363,9 +390,12 @@ class PixelCNNpp:
                     return
                 st2 = self._st()
                 dy = self._grad(y)
-                _ck(self.L.svae_pcnn_copy(_p(dy), F, x.rows, F, _p(self._grad(x)), F, 1, st2))
-                dc2 = self._grad(c2)
+                dc2, _ = self._gout(c2)  # (c2's only consumer: written)
                 _ck(self.L.svae_pcnn_gate_bwd(c2.ptr(), _p(hp), _p(dy), F, x.rows, x.h * x.w, F, _p(dc2), st2))
+                # the residual's gradient is dy itself: y's gradient is complete and dead after this
+                # op, so x takes the buffer over when it has no gradient yet (else one accumulating copy)
+                if not self._galias(x, dy):
+                    _ck(self.L.svae_pcnn_copy(_p(dy), F, x.rows, F, _p(self._grad(x)), F, 1, st2))
                 dhp = torch.empty(x.n, 2 * F, dtype=torch.float32, device=self.dev)
                 _ck(self.L.svae_pcnn_imgsum(_p(dc2), 2 * F, x.n, x.h * x.w, 2 * F, _p(dhp), _p(self.scratch), st2))
                 # d hw [K][2F] = h^T . dhp
@@ -483,7 +513,7 @@ class PixelCNNpp:
         l = self._run(x, h, record=backward)
         pix = l.rows
         logp = torch.empty(pix, dtype=torch.float32, device=self.dev)
-        dl = self._grad(l) if backward else None
+        dl = self._gout(l)[0] if backward else None  # (written whole by the mixture kernel)
         _ck(self.L.svae_pcnn_mixlogistic(_p(x), l.ptr(), pix, self.s["M"], _p(logp), _p(dl), float(coef), st))
         tot = torch.empty(1, dtype=torch.float64, device=self.dev)
         _ck(self.L.svae_pcnn_sum(_p(logp), pix, None, ctypes.c_void_p(tot.data_ptr()), st))
@@ -513,7 +543,7 @@ class PixelCNNpp:
         parameter's gradient is WRITTEN into ``self.G`` (zeroed first); returns d loss / d h [B, K]."""
         x, _ = self._fw_in
         self.G.zero_()
-        self._grad(self._fw_l).copy_(dl.reshape(self._fw_l.rows, self._fw_l.c))
+        self._gout(self._fw_l)[0].copy_(dl.reshape(self._fw_l.rows, self._fw_l.c))
         self._dh = torch.zeros(x.shape[0], self.s["K"], dtype=torch.float32, device=self.dev) if grad_h else None
         for fn in reversed(self._tape):
             fn()

@@ -144,11 +144,14 @@ def test_pcnn_wgrad_matches_reference(case):
     dW = torch.full((kh * kw, cin, cout), float("nan"), device="cuda")
     sc = torch.empty(1 << 24, device="cuda")
     p = lambda t: ctypes.c_void_p(t.data_ptr())
+    db = torch.full((cout,), float("nan"), device="cuda")
     L.check(L.lib().svae_pcnn_conv_wgrad(p(xd), n, h, h, cin, ldx, xb, p(dd), cout, h, h, cout, kh, kw, 1, pt, pl, mode,
-                                         p(dW), p(sc), sc.numel(), L.stream_ptr()))
+                                         p(dW), p(db), p(sc), sc.numel(), L.stream_ptr()))
     torch.cuda.synchronize()
     got = dW.cpu().double()
     err = float((got - ref).abs().max() / ref.abs().max())
-    print("\nwgrad %s: max rel err %.2e" % (case, err))
+    dbref = d.double().sum(0)  # the bias gradient: fp32 dy summed (not bf16-rounded)
+    eb = float((db.cpu().double() - dbref).abs().max() / dbref.abs().max())
+    print("\nwgrad %s: max rel err %.2e, bias %.2e" % (case, err, eb))
     assert torch.isfinite(got).all()
-    assert err < 1e-5
+    assert err < 1e-5 and eb < 1e-5

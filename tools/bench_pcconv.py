@@ -55,8 +55,9 @@ def main():
             dW = torch.empty(kh * kw * cin * cout, device="cuda")
             sc = torch.empty(1 << 26, device="cuda")
             fn = lib.svae_pcnn_conv_wgrad
-            args = (p(x), n_, hi, hi, cin, cin, int(xb), p(dy), cout, ho, ho, cout, kh, kw, 1, pt, pl, mode, p(dW), p(sc),
-                    sc.numel(), st)
+            db = torch.empty(cout, device="cuda")
+            args = (p(x), n_, hi, hi, cin, cin, int(xb), p(dy), cout, ho, ho, cout, kh, kw, 1, pt, pl, mode, p(dW), p(db),
+                    p(sc), sc.numel(), st)
         else:
             fn = lib.svae_pcnn_conv
             args = (p(x), n_, hi, hi, cin, cin, int(xb), p(wk), kpad, None, p(y), ho, ho, cout, cout, kh, kw, 1, pt, pl, mode,
