@@ -61,15 +61,19 @@ int svae_pcnn_colsum(const float* x, int64_t rows, int c, int ldx, int ho, int w
 int svae_pcnn_mask_edge(float* x, int n, int ho, int wo, int c, int ldx, int mask_edge, void* stream);
 
 /* resnet nonlinearity (model.py:24-31): kind 0 relu, 1 elu, 2 concat_elu (y has 2c channels
- * [elu(x), elu(-x)], nn.py:12-15), times the training pass's dropout keep-mask (nn.py:273-274;
- * mask [rows][cy] holding 1 / keep_prob or 0, cy = y's channels; NULL: none); y fp32 or bf16
- * (y_bf16 = 1: for a consumer that reads it as a bf16 MFMA operand).  A mask or a bf16 y needs
- * c, ldx, ldy multiples of 4 and 16-B aligned rows. */
-int svae_pcnn_nonlin(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, void* y, int ldy,
-                     int y_bf16, void* stream);
-/* its backward: dx (+)= f'(x) . (dy . mask) */
-int svae_pcnn_nonlin_bwd(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, const float* dy,
-                         int ldy, float* dx, int lddx, int accumulate, void* stream);
+ * [elu(x), elu(-x)], nn.py:12-15), times the training pass's dropout keep-mask (nn.py:273-274):
+ * mask [rows][cy] holding 1 / keep_prob or 0 (cy = y's channels), or, with mask NULL and keep < 1,
+ * the mask svae_pcnn_dropout_mask(rows * cy, keep, seed) writes, drawn inside the kernel; keep >= 1
+ * and no mask: none.  y fp32 or bf16 (y_bf16 = 1: for a consumer that reads it as a bf16 MFMA
+ * operand).  Dropout or a bf16 y needs c, ldx, ldy multiples of 4 and 16-B aligned rows. */
+int svae_pcnn_nonlin(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, float keep,
+                     uint64_t seed, void* y, int ldy, int y_bf16, void* stream);
+/* its backward: dx (+)= f'(x) . (dy . mask), the mask given or drawn as in the forward */
+int svae_pcnn_nonlin_bwd(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, float keep,
+                         uint64_t seed, const float* dy, int ldy, float* dx, int lddx, int accumulate, void* stream);
+/* the seeded dropout keep-mask: out[i] = 1 / keep with probability keep, else 0 (splitmix64 of
+ * seed + i, 24-bit uniform), i < n -- what the two calls above draw for a NULL mask. */
+int svae_pcnn_dropout_mask(int64_t n, float keep, uint64_t seed, float* out, void* stream);
 
 /* gated_resnet tail (nn.py:283-288): with c2 = [a | b] (2f channels) + hp[img] (h . hw):
  * out = x + a . sigmoid(b). */

@@ -62,7 +62,7 @@ def lib():
         raise RuntimeError("libsvae_hip.so not built (%s); run __graft_entry__.build() or "
                            "python sequential-variational-autoencoder_amd/build.py" % LIB_PATH)
     L = ctypes.CDLL(LIB_PATH)
-    vp, i32, i64, f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float
+    vp, i32, i64, f32, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_uint64
     cfgp = ctypes.POINTER(SvaeConfig)
     sig = {
         "svae_param_count": ([cfgp, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i32)], i32),
@@ -109,8 +109,9 @@ def lib():
                                   i32, vp, vp, vp, i64, vp], i32),
         "svae_pcnn_colsum": ([vp, i64, i32, i32, i32, i32, i32, vp, i32, vp, vp], i32),
         "svae_pcnn_mask_edge": ([vp, i32, i32, i32, i32, i32, i32, vp], i32),
-        "svae_pcnn_nonlin": ([vp, i64, i32, i32, i32, vp, vp, i32, i32, vp], i32),
-        "svae_pcnn_nonlin_bwd": ([vp, i64, i32, i32, i32, vp, vp, i32, vp, i32, i32, vp], i32),
+        "svae_pcnn_nonlin": ([vp, i64, i32, i32, i32, vp, f32, u64, vp, i32, i32, vp], i32),
+        "svae_pcnn_nonlin_bwd": ([vp, i64, i32, i32, i32, vp, f32, u64, vp, i32, vp, i32, i32, vp], i32),
+        "svae_pcnn_dropout_mask": ([i64, f32, u64, vp, vp], i32),
         "svae_pcnn_gate": ([vp, i32, vp, vp, i64, i32, i32, vp, i32, vp], i32),
         "svae_pcnn_gate_bwd": ([vp, vp, vp, i32, i64, i32, i32, vp, vp], i32),
         "svae_pcnn_gemm_small": ([vp, i32, i32, vp, i32, i32, vp, i32, i32, i32, i32, f32, vp], i32),
@@ -151,7 +152,8 @@ PCNN_EXPORTED = ["svae_pcnn_wnorm", "svae_pcnn_wnorm_bwd", "svae_pcnn_conv", "sv
                  "svae_pcnn_gate_bwd", "svae_pcnn_gemm_small", "svae_pcnn_imgsum", "svae_pcnn_copy",
                  "svae_pcnn_pad_ones", "svae_pcnn_mixlogistic", "svae_pcnn_sum", "svae_pcnn_sample",
                  "svae_pcnn_highway", "svae_pcnn_wn_init", "svae_pcnn_adam", "svae_pcnn_ema", "svae_pcnn_sample_bwd",
-                 "svae_pcnn_highway_bwd", "svae_pcnn_dropout", "svae_pcnn_sqerr"]
+                 "svae_pcnn_highway_bwd", "svae_pcnn_dropout", "svae_pcnn_sqerr",
+                 "svae_pcnn_dropout_mask"]
 
 # bf16 GEMM instance ids (csrc/kernels.h KernelId) for svae_probe_begin
 KID_IGEMM_BF16_256x32 = 2

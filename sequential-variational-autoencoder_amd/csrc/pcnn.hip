@@ -789,10 +789,33 @@ __device__ __forceinline__ void nl_fwd4(f32x4 v, int kind, f32x4& a, f32x4& b) {
     }
   }
 }
+// the training pass's dropout keep-mask drawn in the kernel (no mask tensor): element idx of the
+// [rows][cy] mask keeps with probability keep (splitmix64 of seed + idx, 24-bit uniform) and
+// scales by 1 / keep -- the same value in the forward, the backward and svae_pcnn_dropout_mask
+__device__ __forceinline__ float drop_scale(unsigned long long seed, unsigned long long idx, float keep, float inv) {
+  unsigned long long z = seed + idx * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.f / 16777216.f) < keep ? inv : 0.f;
+}
+__device__ __forceinline__ f32x4 drop_scale4(unsigned long long seed, unsigned long long idx, float keep, float inv) {
+  return f32x4{drop_scale(seed, idx, keep, inv), drop_scale(seed, idx + 1, keep, inv),
+               drop_scale(seed, idx + 2, keep, inv), drop_scale(seed, idx + 3, keep, inv)};
+}
+__global__ void dropout_mask_kernel(long long n, float keep, unsigned long long seed, float* __restrict__ out) {
+  const float inv = 1.f / keep;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    out[i] = drop_scale(seed, (unsigned long long)i, keep, inv);
+}
+
 template <bool YB>
 __global__ __launch_bounds__(256) void nonlin4_kernel(const float* __restrict__ x, long long rows, int c, int ldx,
-                                                      int kind, const float* __restrict__ mask, void* __restrict__ y,
-                                                      int ldy) {
+                                                      int kind, const float* __restrict__ mask, float keep,
+                                                      unsigned long long seed, void* __restrict__ y, int ldy) {
+  const bool hashed = !mask && keep < 1.f;
+  const float inv = 1.f / keep;
   const int q = c >> 2, cy = kind == 2 ? 2 * c : c;
   const long long r0 = (long long)blockIdx.x * NL_RPB;
   const int nr = (int)(rows - r0 < NL_RPB ? rows - r0 : NL_RPB);
@@ -805,6 +828,9 @@ __global__ __launch_bounds__(256) void nonlin4_kernel(const float* __restrict__ 
     if (mask) {
       a *= *(const f32x4*)(mask + r * cy + ch);
       if (kind == 2) b *= *(const f32x4*)(mask + r * cy + c + ch);
+    } else if (hashed) {
+      a *= drop_scale4(seed, (unsigned long long)(r * cy + ch), keep, inv);
+      if (kind == 2) b *= drop_scale4(seed, (unsigned long long)(r * cy + c + ch), keep, inv);
     }
     if constexpr (YB) {
       __bf16* yp = (__bf16*)y + r * ldy + ch;
@@ -818,9 +844,11 @@ __global__ __launch_bounds__(256) void nonlin4_kernel(const float* __restrict__ 
   }
 }
 __global__ __launch_bounds__(256) void nonlin4_bwd_kernel(const float* __restrict__ x, long long rows, int c, int ldx,
-                                                          int kind, const float* __restrict__ mask,
-                                                          const float* __restrict__ dy, int ldy, float* __restrict__ dx,
-                                                          int lddx, int accumulate) {
+                                                          int kind, const float* __restrict__ mask, float keep,
+                                                          unsigned long long seed, const float* __restrict__ dy,
+                                                          int ldy, float* __restrict__ dx, int lddx, int accumulate) {
+  const bool hashed = !mask && keep < 1.f;
+  const float inv = 1.f / keep;
   const int q = c >> 2, cy = kind == 2 ? 2 * c : c;
   const long long r0 = (long long)blockIdx.x * NL_RPB;
   const int nr = (int)(rows - r0 < NL_RPB ? rows - r0 : NL_RPB);
@@ -834,6 +862,9 @@ __global__ __launch_bounds__(256) void nonlin4_bwd_kernel(const float* __restric
     if (mask) {
       g *= *(const f32x4*)(mask + r * cy + ch);
       if (kind == 2) g2 *= *(const f32x4*)(mask + r * cy + c + ch);
+    } else if (hashed) {
+      g *= drop_scale4(seed, (unsigned long long)(r * cy + ch), keep, inv);
+      if (kind == 2) g2 *= drop_scale4(seed, (unsigned long long)(r * cy + c + ch), keep, inv);
     }
     f32x4 d;
 #pragma unroll
@@ -1482,8 +1513,8 @@ int svae_pcnn_mask_edge(float* x, int n, int ho, int wo, int c, int ldx, int mas
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-int svae_pcnn_nonlin(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, void* y, int ldy,
-                     int y_bf16, void* stream) {
+int svae_pcnn_nonlin(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, float keep,
+                     uint64_t seed, void* y, int ldy, int y_bf16, void* stream) {
   if (!x || !y || rows < 1 || c < 1 || kind < 0 || kind > 2 || ldx < c || ldy < (kind == 2 ? 2 * c : c))
     return bad("pcnn_nonlin: bad arguments");
   hipStream_t st = (hipStream_t)stream;
@@ -1491,28 +1522,32 @@ int svae_pcnn_nonlin(const float* x, int64_t rows, int c, int ldx, int kind, con
                    (y_bf16 ? ((uintptr_t)y & 7) == 0 : al16(y));
   if (vec) {
     const dim3 grid((unsigned)((rows + NL_RPB - 1) / NL_RPB));
-    if (y_bf16) hipLaunchKernelGGL(nonlin4_kernel<true>, grid, dim3(256), 0, st, x, (long long)rows, c, ldx, kind, mask, y, ldy);
-    else hipLaunchKernelGGL(nonlin4_kernel<false>, grid, dim3(256), 0, st, x, (long long)rows, c, ldx, kind, mask, y, ldy);
+    if (y_bf16)
+      hipLaunchKernelGGL(nonlin4_kernel<true>, grid, dim3(256), 0, st, x, (long long)rows, c, ldx, kind, mask, keep,
+                         (unsigned long long)seed, y, ldy);
+    else
+      hipLaunchKernelGGL(nonlin4_kernel<false>, grid, dim3(256), 0, st, x, (long long)rows, c, ldx, kind, mask, keep,
+                         (unsigned long long)seed, y, ldy);
     return hipchk();
   }
-  if (mask || y_bf16) return bad("pcnn_nonlin: a mask or bf16 output needs 4-channel aligned rows");
+  if (mask || keep < 1.f || y_bf16) return bad("pcnn_nonlin: dropout or a bf16 output needs 4-channel aligned rows");
   hipLaunchKernelGGL(nonlin_kernel, dim3(blocks_for(rows * c)), dim3(256), 0, st, x, (long long)rows, c, ldx, kind,
                      (float*)y, ldy);
   return hipchk();
 }
 
-int svae_pcnn_nonlin_bwd(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, const float* dy,
-                         int ldy, float* dx, int lddx, int accumulate, void* stream) {
+int svae_pcnn_nonlin_bwd(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, float keep,
+                         uint64_t seed, const float* dy, int ldy, float* dx, int lddx, int accumulate, void* stream) {
   if (!x || !dy || !dx || rows < 1 || c < 1 || kind < 0 || kind > 2) return bad("pcnn_nonlin_bwd: bad arguments");
   hipStream_t st = (hipStream_t)stream;
   const bool vec = c % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && lddx % 4 == 0 && al16(x) && al16(dy) && al16(dx) &&
                    (!mask || al16(mask));
   if (vec) {
     hipLaunchKernelGGL(nonlin4_bwd_kernel, dim3((unsigned)((rows + NL_RPB - 1) / NL_RPB)), dim3(256), 0, st, x,
-                       (long long)rows, c, ldx, kind, mask, dy, ldy, dx, lddx, accumulate);
+                       (long long)rows, c, ldx, kind, mask, keep, (unsigned long long)seed, dy, ldy, dx, lddx, accumulate);
     return hipchk();
   }
-  if (mask) return bad("pcnn_nonlin_bwd: a mask needs 4-channel aligned rows");
+  if (mask || keep < 1.f) return bad("pcnn_nonlin_bwd: dropout needs 4-channel aligned rows");
   hipLaunchKernelGGL(nonlin_bwd_kernel, dim3(blocks_for(rows * c)), dim3(256), 0, st, x, (long long)rows, c, ldx, kind,
                      dy, ldy, dx, lddx, accumulate);
   return hipchk();
@@ -1616,6 +1651,13 @@ int svae_pcnn_sqerr(const float* a, const float* t, int nimg, int64_t per_img, f
                     void* stream) {
   if (!a || !t || nimg < 1 || per_img < 1 || (!rec && !da)) return bad("pcnn_sqerr: bad arguments");
   hipLaunchKernelGGL(sqerr_kernel, dim3(nimg), dim3(256), 0, (hipStream_t)stream, a, t, (long long)per_img, coef, rec, da);
+  return hipchk();
+}
+
+int svae_pcnn_dropout_mask(int64_t n, float keep, uint64_t seed, float* out, void* stream) {
+  if (!out || n < 1 || !(keep > 0.f) || keep > 1.f) return bad("pcnn_dropout_mask: bad arguments");
+  hipLaunchKernelGGL(dropout_mask_kernel, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, (long long)n, keep,
+                     (unsigned long long)seed, out);
   return hipchk();
 }
 

@@ -43,6 +43,20 @@ def _r16(c):
     return (c + 31) // 32 * 32
 
 
+class DropMask:
+    """A dropout keep-mask drawn inside the nonlinearity kernels from (seed, keep) instead of stored:
+    ``shape`` (rows, channels); ``tensor(net)`` writes the same mask out (svae_pcnn_dropout_mask)."""
+    __slots__ = ("shape", "keep", "seed")
+
+    def __init__(self, rows, c, keep, seed):
+        self.shape, self.keep, self.seed = (rows, c), float(keep), int(seed)
+
+    def tensor(self, net):
+        m = torch.empty(self.shape, dtype=torch.float32, device=net.dev)
+        _ck(net.L.svae_pcnn_dropout_mask(m.numel(), self.keep, self.seed, _p(m), _lib.stream_ptr()))
+        return m
+
+
 class Act:
     """An NHWC activation: ``buf`` [n*h*w][ld] fp32 (or bf16: a nonlinearity output read only by the
     bf16-MFMA convs), channels [off, off + c)."""
@@ -165,6 +179,7 @@ class PixelCNNpp:
         self._tape, self._g, self._keep, self._same, self._cnt = [], {}, [], {}, {}
         self._record = self._init = False
         self._dropout_p, self._masks, self.last_masks = 0.0, None, []
+        self.keep_masks = False  # drawn masks: record their tensors in last_masks (else DropMask descriptors)
         self.probe, self.probe_cap = None, 0  # [(flops, event, event)] of timed forward conv launches
         self.conv_flops = 0.0  # running total of forward conv FLOPs (tools/bench_pcnn.py)
 
@@ -344,13 +359,17 @@ class PixelCNNpp:
         bf = c % 8 == 0 and x.c % 4 == 0 and x.ld % 4 == 0
         buf = torch.empty(x.rows, c, dtype=torch.bfloat16 if bf else torch.float32, device=self.dev)
         y = Act(buf, c, x.n, x.h, x.w)
-        _ck(self.L.svae_pcnn_nonlin(x.ptr(), x.rows, x.c, x.ld, k, _p(mask), y.ptr(), y.ld, int(bf), self._st()))
+        if isinstance(mask, DropMask):  # drawn in the kernel from (seed, keep)
+            mp, keep, seed = None, mask.keep, mask.seed
+        else:
+            mp, keep, seed = _p(mask), 1.0, 0
+        _ck(self.L.svae_pcnn_nonlin(x.ptr(), x.rows, x.c, x.ld, k, mp, keep, seed, y.ptr(), y.ld, int(bf), self._st()))
         if self._record:
             def bwd():
                 if not self._has_grad(y):
                     return
                 dx, dacc = self._gout(x)
-                _ck(self.L.svae_pcnn_nonlin_bwd(x.ptr(), x.rows, x.c, x.ld, k, _p(mask), _p(self._grad(y)), c,
+                _ck(self.L.svae_pcnn_nonlin_bwd(x.ptr(), x.rows, x.c, x.ld, k, mp, keep, seed, _p(self._grad(y)), c,
                                                 _p(dx), x.c, dacc, self._st()))
             self._tape.append(bwd)
         return y
@@ -422,14 +441,18 @@ class PixelCNNpp:
 
     def _next_mask(self, rows, c):
         """The next gated resnet's dropout mask (1 / keep_prob where kept, else 0; tf.nn.dropout,
-        nn.py:273-274): from the injected list (parity), else drawn on the device when dropout_p > 0.
-        Every mask used is appended to ``self.last_masks``."""
+        nn.py:273-274): from the injected list (parity), else, when dropout_p > 0, a DropMask the
+        nonlinearity kernels draw from a seed (the seeds come from torch's CPU generator, so
+        torch.manual_seed fixes them).  Every mask used is appended to ``self.last_masks`` (a
+        DropMask, or its tensor when ``keep_masks`` is set)."""
         if self._masks is not None:
             m = next(self._masks)
-            m = torch.as_tensor(m, dtype=torch.float32, device=self.dev).reshape(rows, c).contiguous()
+            if not isinstance(m, DropMask):
+                m = torch.as_tensor(m, dtype=torch.float32, device=self.dev).reshape(rows, c).contiguous()
         elif self._dropout_p > 0.0:
-            keep = 1.0 - self._dropout_p
-            m = (torch.rand(rows, c, device=self.dev) < keep).to(torch.float32) * (1.0 / keep)
+            m = DropMask(rows, c, 1.0 - self._dropout_p, int(torch.randint(0, 2 ** 62, (1,)).item()))
+            if self.keep_masks:
+                m = m.tensor(self)
         else:
             return None
         self.last_masks.append(m)

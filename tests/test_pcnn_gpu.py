@@ -192,3 +192,26 @@ def test_full_size_step_runs():
     bpd = nll / (2 * 64 * 64 * 3 * np.log(2))
     print("\nfull-size NLL %.1f (%.3f bits/dim at init), %d parameters" % (nll, bpd, net.n_params))
     assert np.isfinite(nll) and torch.isfinite(net.G).all() and torch.isfinite(net.P).all()
+
+
+def test_seeded_dropout_matches_explicit_mask():
+    """The training pass's dropout drawn inside the nonlinearity kernels (DropMask: seed, keep) gives
+    bitwise the output and gradients of the same mask passed as a tensor, and keeps ~1 - p."""
+    PC, spec, ospec, params, x, h = _setup(nr_filters=16)
+    net = PC.PixelCNNpp(spec, params=params)
+    torch.manual_seed(3)
+    l1 = net.forward_train(x, h, dropout_p=0.3).clone()
+    masks = list(net.last_masks)
+    assert masks and all(isinstance(m, PC.DropMask) for m in masks)
+    dl = torch.randn_like(l1)
+    net.backward_from(dl.reshape(-1, l1.shape[-1]))
+    g1 = net.G.clone()
+    tens = [m.tensor(net) for m in masks]
+    l2 = net.forward_train(x, h, masks=tens).clone()
+    net.backward_from(dl.reshape(-1, l1.shape[-1]))
+    torch.cuda.synchronize()
+    assert torch.equal(l1, l2) and torch.equal(g1, net.G)
+    kept = torch.cat([(t > 0).float().reshape(-1) for t in tens]).mean().item()
+    scale = {float(v) for t in tens for v in t.unique().tolist()}
+    print("\nseeded dropout: kept fraction %.4f, values %s" % (kept, sorted(scale)))
+    assert abs(kept - 0.7) < 0.02 and len(scale) == 2 and abs(max(scale) - 1 / 0.7) < 1e-6

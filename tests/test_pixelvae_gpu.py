@@ -117,7 +117,7 @@ def test_pixelvae_full_size_properties():
     um = rng.uniform(1e-5, 1 - 1e-5, (8, 64, 64, 10))
     ul = rng.uniform(1e-5, 1 - 1e-5, (8, 64, 64, 3))
     pv.forward(x, x, eps, 1.0, um, ul)
-    masks = [m.clone() for m in pv.head.last_masks]
+    masks = list(pv.head.last_masks)  # the seeded masks of that pass (DropMask), drawn again identically
     res = []
     for _ in range(2):
         pv.forward(x, x, eps, 1.0, um, ul, masks=masks)
