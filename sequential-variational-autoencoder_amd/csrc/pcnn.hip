@@ -583,6 +583,200 @@ void pc3_launch(const PcGeom& g, const Pc3& h, const void* x, const __bf16* w, i
 }
 
 // ---------------------------------------------------------------------------------------------
+// Tap-row weight gradient (stride 1, both modes: the resnet convs and their input gradients' nin /
+// dense layers viewed as 16-wide images): dW[tap][ci][co] = sum_p X[src(p, tap)][ci] . D[p][co].
+// Block = 64 ci x 64 co x ONE kernel row ky (its kw taps), four waves of 32 x 32 x kw taps; K = a
+// split of the output pixels in chunks of 128 (whole image rows).  Per chunk the block stages, pixel-
+// major in bf16, the chunk's X row segment for kernel row ky (R rows x (wo + kw - 1) pixels: the kw
+// taps of the row are pixel shifts of one window) and its D rows; per 16-pixel K step a wave reads
+// one transposed D fragment (ds_read_b64_tr_b16) and, per tap, one transposed X fragment at the
+// tap's shift.  Against pc_wgrad_kernel (one tap per block) X and D are read kh instead of kh x kw
+// times and each barrier covers 8 x kw MFMAs instead of 4.  bsum: the bias gradient's per-split
+// column sums (blocks of ky = 0 and the first ci tile, fp32 before the bf16 staging).
+// ---------------------------------------------------------------------------------------------
+typedef short pc_v4i16 __attribute__((ext_vector_type(4)));
+typedef short pc_v8i16 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ pc_v4i16 pc_tr16(const __bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) pc_v4i16*)(p));
+}
+__device__ __forceinline__ pc_bf16x8 pc_join(pc_v4i16 lo, pc_v4i16 hi) {
+  pc_v8i16 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(pc_bf16x8, v);
+}
+struct Pw4 {
+  int R, PC, npix;  // image rows per chunk, window pixels per row, window pixels
+  int iy_off[2];    // per kernel row: window row 0's input row relative to the chunk's first output row
+  int ix_off;       // window column 0's input column
+  int nchunk, cps;  // chunks in all, chunks per split
+};
+#define PW4_CP 128     // output pixels per chunk
+#define PW4_MAXPIX 144 // 8 rows x 18 (16-wide images, kw = 3)
+#define PW4_P 72       // LDS pixel pitch (bf16): 64 channels + 8
+template <bool XB>
+__global__ __launch_bounds__(256) void pc_wgrad4_kernel(PcGeom g, Pw4 h, const void* __restrict__ Xv,
+                                                        const float* __restrict__ D, int ldd, float* __restrict__ part,
+                                                        float* __restrict__ bsum) {
+  constexpr int WI = (PW4_MAXPIX * 8 + 255) / 256;  // window items (8 channels) per thread
+  constexpr int DI = (PW4_CP * 16 + 255) / 256;     // D items (4 columns) per thread
+  __shared__ __attribute__((aligned(16))) __bf16 smem[(PW4_MAXPIX + PW4_CP) * PW4_P];
+  __bf16* Ws = smem;                    // [npix][PW4_P]
+  __bf16* Dm = smem + h.npix * PW4_P;   // [128][PW4_P]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = lane >> 4, i16 = lane & 15, q = i16 >> 2, p4 = i16 & 3, l32 = lane & 31, hh = lane >> 5;
+  const int ci0 = blockIdx.x * 64, co0 = blockIdx.y * 64;
+  const int ky = blockIdx.z % g.kh, split = blockIdx.z / g.kh;
+  const int wm = wave & 1, wn = wave >> 1;
+  const bool live = ci0 + wm * 32 < g.cin && co0 + wn * 32 < g.cout;
+  const int per_img = g.ho * g.wo;
+  const int c_beg = split * h.cps;
+  const int c_end = c_beg + h.cps < h.nchunk ? c_beg + h.cps : h.nchunk;
+  const bool bias_blk = bsum && ky == 0 && ci0 == 0;
+  const int iy_off = h.iy_off[ky];
+
+  f32x16 acc[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  f32x4 bacc = {0.f, 0.f, 0.f, 0.f};  // bias column sums: this thread's column quad (tid & 15)
+
+  f32x4 xa[XB ? 1 : WI][2];
+  pc_bf16x8 xh[XB ? WI : 1];
+  f32x4 dv[DI];
+  auto load = [&](int c) {
+    const long long p0 = (long long)c * PW4_CP;
+    const int img = (int)(p0 / per_img);
+    const int oy0 = (int)(p0 - (long long)img * per_img) / g.wo;
+#pragma unroll
+    for (int i = 0; i < WI; ++i) {
+      const int it = tid + 256 * i;
+      const int pix = it >> 3, c8 = (it & 7) * 8;
+      long long off = -1;
+      if (it < h.npix * 8 && ci0 + c8 < g.cin) {
+        const int pr = pix / h.PC, pc = pix - pr * h.PC;
+        const int iy = oy0 + iy_off + pr, ix = h.ix_off + pc;
+        if (iy >= 0 && iy < g.hi && ix >= 0 && ix < g.wi)
+          off = ((long long)(img * g.hi + iy) * g.wi + ix) * g.ldx + ci0 + c8;
+      }
+      if constexpr (XB) {
+        pc_bf16x8 z = {};
+        xh[i] = off >= 0 ? *(const pc_bf16x8*)((const __bf16*)Xv + off) : z;
+      } else {
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        xa[i][0] = off >= 0 ? *(const f32x4*)((const float*)Xv + off) : z;
+        xa[i][1] = off >= 0 ? *(const f32x4*)((const float*)Xv + off + 4) : z;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < DI; ++i) {
+      const int it = tid + 256 * i;
+      const int k = it >> 4, c4 = (it & 15) * 4;
+      dv[i] = co0 + c4 < g.cout ? *(const f32x4*)(D + (p0 + k) * ldd + co0 + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < WI; ++i) {
+      const int it = tid + 256 * i;
+      if (it >= h.npix * 8) continue;
+      __bf16* w = Ws + (it >> 3) * PW4_P + (it & 7) * 8;
+      if constexpr (XB) {
+        *(pc_bf16x8*)w = xh[i];
+      } else {
+        const pc_f32x8 v8 = {xa[i][0][0], xa[i][0][1], xa[i][0][2], xa[i][0][3],
+                             xa[i][1][0], xa[i][1][1], xa[i][1][2], xa[i][1][3]};
+        *(pc_bf16x8*)w = __builtin_convertvector(v8, pc_bf16x8);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < DI; ++i) {
+      const int it = tid + 256 * i;
+      const int k = it >> 4, c4 = (it & 15) * 4;
+      if (bias_blk) bacc += dv[i];  // (the column quad it & 15 == tid & 15 for every i)
+      *(pc_bf16x4*)(Dm + k * PW4_P + c4) = __builtin_convertvector(dv[i], pc_bf16x4);
+    }
+  };
+
+  // lane roles of the transposed reads: pixel lk (+ 4) of a 16-pixel K step, channel / column quad
+  const int lk = 8 * (grp >> 1) + q;
+  const int cha = wm * 32 + 16 * (grp & 1) + 4 * p4;
+  const int chb = wn * 32 + 16 * (grp & 1) + 4 * p4;
+  if (c_beg < c_end) {
+    load(c_beg);
+    store();
+  }
+  __syncthreads();
+  for (int c = c_beg; c < c_end; ++c) {
+    if (c + 1 < c_end) load(c + 1);
+    if (live) {
+#pragma unroll 2
+      for (int ks = 0; ks < PW4_CP / 16; ++ks) {
+        const int k0 = ks * 16;
+        const int wrow = k0 / g.wo, wcol = k0 - wrow * g.wo;  // the step's 16 pixels share one image row
+        const int wp = wrow * h.PC + wcol + lk;
+        const pc_bf16x8 bf =
+            pc_join(pc_tr16(Dm + (k0 + lk) * PW4_P + chb), pc_tr16(Dm + (k0 + lk + 4) * PW4_P + chb));
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          if (kx < g.kw) {
+            const int sh = g.mode == 0 ? kx : g.kw - 1 - kx;
+            const __bf16* wa = Ws + (wp + sh) * PW4_P + cha;
+            const pc_bf16x8 af = pc_join(pc_tr16(wa), pc_tr16(wa + 4 * PW4_P));
+            acc[kx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc[kx], 0, 0, 0);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (c + 1 < c_end) {
+      store();
+      __syncthreads();
+    }
+  }
+  if (live) {
+    float* out = part + (long long)split * g.kh * g.kw * g.cin * g.cout;
+    const int n = co0 + wn * 32 + l32;
+    for (int kx = 0; kx < g.kw; ++kx) {
+      const int tap = ky * g.kw + kx;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = ci0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (m < g.cin && n < g.cout) out[((long long)tap * g.cin + m) * g.cout + n] = acc[kx][r];
+      }
+    }
+  }
+  if (bias_blk) {  // the 16 row lanes of each column quad combined in lane order through LDS
+    float* red = (float*)smem;  // [16 row lanes][64]
+    *(f32x4*)&red[(tid >> 4) * 64 + (tid & 15) * 4] = bacc;
+    __syncthreads();
+    if (tid < 64 && co0 + tid < g.cout) {
+      float v = 0.f;
+      for (int i = 0; i < 16; ++i) v += red[i * 64 + tid];
+      bsum[(long long)split * g.cout + co0 + tid] = v;
+    }
+  }
+}
+
+// (measured on the B = 128 head shapes: the [2, 3] convs 1.2-1.45x faster than the one-tap kernel, the
+// [2, 2] and 1x1 ones slower at two blocks per CU: kw = 3 only)
+bool pw4_plan(const PcGeom& g, long long rows, Pw4* out) {
+  if (g.s != 1 || g.kh > 2 || g.kw != 3 || g.wo % 16 || PW4_CP % g.wo || (g.ho * g.wo) % PW4_CP || rows % PW4_CP ||
+      g.ldx % 8 || g.cin % 8)
+    return false;
+  Pw4 h;
+  h.R = PW4_CP / g.wo;
+  h.PC = g.wo + g.kw - 1;
+  h.npix = h.R * h.PC;
+  if (h.npix > PW4_MAXPIX) return false;
+  for (int ky = 0; ky < 2; ++ky) h.iy_off[ky] = g.mode == 0 ? ky - g.pt : g.pt - ky;
+  h.ix_off = g.mode == 0 ? -g.pl : g.pl - (g.kw - 1);
+  h.nchunk = (int)(rows / PW4_CP);
+  h.cps = 0;
+  *out = h;
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------
 // weight gradient: block = one tap x 64 ci x 64 co (2 x 2 waves of 32 x 32), K = a split of the
 // output rows in chunks of 32, staged through LDS transposed (row-contiguous per channel, so
 // each MFMA fragment is one 16-B LDS read).  Partial slabs [split][tap][ci][co].
@@ -1462,6 +1656,38 @@ int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx,
   const int taps = kh * kw;
   const long long wsz = (long long)taps * cin * cout;
   hipStream_t st = (hipStream_t)stream;
+  static const int pw4 = [] {  // SVAE_PW4=0: every weight gradient on the one-tap kernel
+    const char* v = getenv("SVAE_PW4");
+    return v ? atoi(v) : 1;
+  }();
+  {
+    PcGeom g4 = g;
+    if (kh == 1 && kw == 1 && pt == 0 && pl == 0 && s == 1 && rows % 256 == 0) {  // 1x1: 16-wide images
+      g4.n = (int)(rows / 256);
+      g4.hi = g4.wi = g4.ho = g4.wo = 16;
+    }
+    Pw4 h;
+    if (pw4 && pw4_plan(g4, rows, &h)) {
+      const long long tiles4 = (long long)((cin + 63) / 64) * ((cout + 63) / 64) * kh;
+      long long ns = (1024 + tiles4 - 1) / tiles4;  // ~1024 blocks
+      if (ns > h.nchunk) ns = h.nchunk;
+      if (ns > scratch_elems / (wsz + cout)) ns = scratch_elems / (wsz + cout);
+      if (ns < 1) return bad("pcnn_wgrad: scratch too small");
+      h.cps = (int)((h.nchunk + ns - 1) / ns);
+      ns = (h.nchunk + h.cps - 1) / h.cps;
+      float* bpart = dbias ? scratch + ns * wsz : nullptr;
+      const dim3 grid((unsigned)((cin + 63) / 64), (unsigned)((cout + 63) / 64), (unsigned)(kh * ns));
+      if (x_bf16)
+        hipLaunchKernelGGL(pc_wgrad4_kernel<true>, grid, dim3(256), 0, st, g4, h, x, dy, ldd, scratch, bpart);
+      else
+        hipLaunchKernelGGL(pc_wgrad4_kernel<false>, grid, dim3(256), 0, st, g4, h, x, dy, ldd, scratch, bpart);
+      hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(wsz)), dim3(256), 0, st, scratch, (int)ns, wsz, dW);
+      if (dbias)
+        hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(cout)), dim3(256), 0, st, bpart, (int)ns,
+                           (long long)cout, dbias);
+      return hipchk();
+    }
+  }
   const int tiles = ((cin + 63) / 64) * ((cout + 63) / 64);
   // splits: ~2048 blocks, >= 256 rows (8 chunks) per split, bounded by the scratch slabs
   long long ns = (2048 + (long long)tiles * taps - 1) / ((long long)tiles * taps);

@@ -125,6 +125,9 @@ WCASES = [
     (512, 1, 320, 320, 160, 1, 1, 0, 0, 0, 1),    # nin
     (8, 8, 32, 32, 32, 2, 2, 1, 1, 0, 1),
     (2, 16, 4, 4, 32, 2, 3, 2, 1, 0, 0),          # 4 input channels (x_pad)
+    (4, 16, 8, 8, 16, 2, 3, 1, 1, 0, 1),          # channel counts below one 32-wide sub-tile
+    (4, 16, 16, 16, 8, 2, 3, 1, 1, 1, 0),
+    (2, 32, 96, 96, 40, 2, 3, 1, 1, 0, 1),        # partial 64-wide tiles
 ]
 
 
