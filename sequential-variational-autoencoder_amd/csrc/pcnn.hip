@@ -1602,11 +1602,23 @@ int svae_pcnn_conv(const void* x, int n, int hi, int wi, int cin, int ldx, int x
   }();
   if (kpad % 32 == 0 && !old) {  // LDS-staged kernels, up to 160 output channels per block
     const int n32 = (cout + 31) / 32;
-    const int tiles = (n32 + 4) / 5;
-    const int NT = (n32 + tiles - 1) / tiles;
+    int tiles = (n32 + 4) / 5;
+    int NT = (n32 + tiles - 1) / tiles;
     Pc3 h;
     size_t lds = 0;
     if (pc3 >= 1 && pc3 <= 2 && pc3_plan(g, kpad, pc3, &h, &lds)) {  // stride 1: one halo window per chunk
+      // widest column tile (32 x NT): 64 columns for the forward convs (bf16 input, mode 0), 160 for the
+      // input gradients (tools/bench_pcconv.py, B = 128: mode 0 0-30 % faster at NT = 2 against NT = 5,
+      // mode 1 up to 55 % slower; NT = 3 slower for both); SVAE_PC3_NT overrides
+      static const int nt_env = [] {
+        const char* v = getenv("SVAE_PC3_NT");
+        return v ? atoi(v) : 0;
+      }();
+      const int nt_max = nt_env > 0 ? nt_env : (x_bf16 && mode == 0 ? 2 : 5);
+      if (nt_max < NT) {
+        tiles = (n32 + nt_max - 1) / nt_max;
+        NT = (n32 + tiles - 1) / tiles;
+      }
 #define PC3_NT(TMV, XBV)                                                                                \
   switch (NT) {                                                                                         \
     case 1: pc3_launch<1, TMV, XBV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, st); break; \
