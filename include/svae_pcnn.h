@@ -80,9 +80,10 @@ int svae_pcnn_dropout_mask(int64_t n, float keep, uint64_t seed, float* out, voi
 int svae_pcnn_gate(const float* x, int ldx, const float* c2, const float* hp, int64_t rows, int pix_per_img, int f,
                    float* out, int ldo, void* stream);
 /* its backward from the saved c2 and hp: dc2 [rows][2f] = [dout . sig(b), dout . a . sig'(b)]
- * (the residual's gradient dx is dout itself). */
+ * (the residual's gradient dx is dout itself); dhp (may be NULL): the per-image sums of dc2,
+ * [nimg][2f] (d loss / d (h . hw)), from the same pass (scratch: rows / 64 * 2f floats). */
 int svae_pcnn_gate_bwd(const float* c2, const float* hp, const float* dout, int lddo, int64_t rows, int pix_per_img,
-                       int f, float* dc2, void* stream);
+                       int f, float* dc2, float* dhp, float* scratch, void* stream);
 
 /* small fp32 GEMM (conditioning projections, highway FC): C[m][n] = beta C + sum_k A(m,k) B(k,n),
  * A(m,k) = ta ? A[k*lda + m] : A[m*lda + k], B(k,n) = tb ? B[n*ldb + k] : B[k*ldb + n]. */

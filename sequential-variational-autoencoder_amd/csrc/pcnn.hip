@@ -1145,6 +1145,104 @@ __global__ void gate_bwd_kernel(const float* __restrict__ c2, const float* __res
   }
 }
 
+// Vectorised gated-resnet tail (4 channels per thread, GT_RPB rows of one image per block, 32-bit
+// index math).  The backward also sums dc2 over the block's rows per column (fixed order: row lanes,
+// then lanes in order) into part[block][2f]; gate_imgsum_kernel adds an image's blocks in order: the
+// per-image d(h . hw) without re-reading dc2.
+#define GT_RPB 64
+__device__ __forceinline__ f32x4 sigm4(f32x4 v) {
+  f32x4 r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) r[e] = 1.f / (1.f + expf(-v[e]));
+  return r;
+}
+__global__ __launch_bounds__(256) void gate4_kernel(const float* __restrict__ x, int ldx, const float* __restrict__ c2,
+                                                    const float* __restrict__ hp, long long rows, int per_img, int f,
+                                                    float* __restrict__ out, int ldo) {
+  const int q = f >> 2;
+  const long long r0 = (long long)blockIdx.x * GT_RPB;
+  const int nr = (int)(rows - r0 < GT_RPB ? rows - r0 : GT_RPB);
+  const long long img = r0 / per_img;  // (per_img % GT_RPB == 0: one image per block)
+  for (int j = threadIdx.x; j < nr * q; j += 256) {
+    const int rr = j / q;
+    const int ch = (j - rr * q) * 4;
+    const long long r = r0 + rr;
+    f32x4 a = *(const f32x4*)(c2 + r * 2 * f + ch), b = *(const f32x4*)(c2 + r * 2 * f + f + ch);
+    if (hp) {
+      a += *(const f32x4*)(hp + img * 2 * f + ch);
+      b += *(const f32x4*)(hp + img * 2 * f + f + ch);
+    }
+    *(f32x4*)(out + r * ldo + ch) = *(const f32x4*)(x + r * ldx + ch) + a * sigm4(b);
+  }
+}
+__global__ __launch_bounds__(256) void gate4_bwd_kernel(const float* __restrict__ c2, const float* __restrict__ hp,
+                                                        const float* __restrict__ dout, int lddo, long long rows,
+                                                        int per_img, int f, float* __restrict__ dc2,
+                                                        float* __restrict__ part) {
+  __shared__ f32x4 red[256][2];
+  const int q = f >> 2;
+  const int RL = 256 / q;  // row lanes (q <= 256)
+  const int tid = threadIdx.x, qi = tid % q, rl = tid / q;
+  const long long r0 = (long long)blockIdx.x * GT_RPB;
+  const int nr = (int)(rows - r0 < GT_RPB ? rows - r0 : GT_RPB);
+  const long long img = r0 / per_img;
+  const int ch = qi * 4;
+  f32x4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
+  if (rl < RL) {
+    f32x4 ha = {0.f, 0.f, 0.f, 0.f}, hb = {0.f, 0.f, 0.f, 0.f};
+    if (hp) {
+      ha = *(const f32x4*)(hp + img * 2 * f + ch);
+      hb = *(const f32x4*)(hp + img * 2 * f + f + ch);
+    }
+    for (int rr = rl; rr < nr; rr += RL) {
+      const long long r = r0 + rr;
+      const f32x4 a = *(const f32x4*)(c2 + r * 2 * f + ch) + ha, b = *(const f32x4*)(c2 + r * 2 * f + f + ch) + hb;
+      const f32x4 d = *(const f32x4*)(dout + r * lddo + ch), s = sigm4(b);
+      const f32x4 da = d * s, db = d * a * s * (1.f - s);
+      *(f32x4*)(dc2 + r * 2 * f + ch) = da;
+      *(f32x4*)(dc2 + r * 2 * f + f + ch) = db;
+      sa += da;
+      sb += db;
+    }
+  }
+  if (!part) return;
+  red[tid][0] = sa;
+  red[tid][1] = sb;
+  __syncthreads();
+  if (tid < q) {
+    f32x4 ta = red[tid][0], tb = red[tid][1];
+    for (int l = 1; l < RL; ++l) {
+      ta += red[l * q + tid][0];
+      tb += red[l * q + tid][1];
+    }
+    *(f32x4*)(part + (long long)blockIdx.x * 2 * f + ch) = ta;
+    *(f32x4*)(part + (long long)blockIdx.x * 2 * f + f + ch) = tb;
+  }
+}
+// out[img][c] = sum of the image's bpi blocks' partials, in block order
+__global__ void gate_imgsum_kernel(const float* __restrict__ part, int bpi, int nimg, int c, float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nimg * c) return;
+  const int img = i / c, col = i - img * c;
+  float v = 0.f;
+  for (int b = 0; b < bpi; ++b) v += part[((long long)img * bpi + b) * c + col];
+  out[i] = v;
+}
+__global__ void copy4_kernel(const float* __restrict__ x, int ldx, long long rows, int c, float* __restrict__ y, int ldy,
+                             int accumulate) {
+  const int q = c >> 2;
+  const long long r0 = (long long)blockIdx.x * GT_RPB;
+  const int nr = (int)(rows - r0 < GT_RPB ? rows - r0 : GT_RPB);
+  for (int j = threadIdx.x; j < nr * q; j += 256) {
+    const int rr = j / q;
+    const int ch = (j - rr * q) * 4;
+    const long long r = r0 + rr;
+    f32x4 v = *(const f32x4*)(x + r * ldx + ch);
+    if (accumulate) v += *(const f32x4*)(y + r * ldy + ch);
+    *(f32x4*)(y + r * ldy + ch) = v;
+  }
+}
+
 __global__ void gemm_small_kernel(const float* __restrict__ A, int lda, int ta, const float* __restrict__ B, int ldb,
                                   int tb, float* __restrict__ C, int ldc, int m, int n, int k, float beta) {
   const long long stride = (long long)gridDim.x * blockDim.x, total = (long long)m * n;
@@ -1794,17 +1892,37 @@ int svae_pcnn_nonlin_bwd(const float* x, int64_t rows, int c, int ldx, int kind,
 int svae_pcnn_gate(const float* x, int ldx, const float* c2, const float* hp, int64_t rows, int pix_per_img, int f,
                    float* out, int ldo, void* stream) {
   if (!x || !c2 || !out || rows < 1 || f < 1 || pix_per_img < 1 || rows % pix_per_img) return bad("pcnn_gate: bad arguments");
-  hipLaunchKernelGGL(gate_kernel, dim3(blocks_for(rows * f)), dim3(256), 0, (hipStream_t)stream, x, ldx, c2, hp,
-                     (long long)rows, pix_per_img, f, out, ldo);
+  hipStream_t st = (hipStream_t)stream;
+  if (f % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0 && pix_per_img % GT_RPB == 0 && al16(x) && al16(c2) && al16(out) &&
+      (!hp || al16(hp))) {
+    hipLaunchKernelGGL(gate4_kernel, dim3((unsigned)(rows / GT_RPB)), dim3(256), 0, st, x, ldx, c2, hp, (long long)rows,
+                       pix_per_img, f, out, ldo);
+    return hipchk();
+  }
+  hipLaunchKernelGGL(gate_kernel, dim3(blocks_for(rows * f)), dim3(256), 0, st, x, ldx, c2, hp, (long long)rows,
+                     pix_per_img, f, out, ldo);
   return hipchk();
 }
 
 int svae_pcnn_gate_bwd(const float* c2, const float* hp, const float* dout, int lddo, int64_t rows, int pix_per_img,
-                       int f, float* dc2, void* stream) {
-  if (!c2 || !dout || !dc2 || rows < 1 || f < 1 || pix_per_img < 1 || rows % pix_per_img)
+                       int f, float* dc2, float* dhp, float* scratch, void* stream) {
+  if (!c2 || !dout || !dc2 || rows < 1 || f < 1 || pix_per_img < 1 || rows % pix_per_img || (dhp && !scratch))
     return bad("pcnn_gate_bwd: bad arguments");
-  hipLaunchKernelGGL(gate_bwd_kernel, dim3(blocks_for(rows * f)), dim3(256), 0, (hipStream_t)stream, c2, hp, dout,
-                     lddo, (long long)rows, pix_per_img, f, dc2);
+  hipStream_t st = (hipStream_t)stream;
+  const int nimg = (int)(rows / pix_per_img);
+  if (f % 4 == 0 && f <= 1024 && lddo % 4 == 0 && pix_per_img % GT_RPB == 0 && al16(c2) && al16(dout) && al16(dc2) &&
+      (!hp || al16(hp))) {
+    const long long nb = rows / GT_RPB;
+    hipLaunchKernelGGL(gate4_bwd_kernel, dim3((unsigned)nb), dim3(256), 0, st, c2, hp, dout, lddo, (long long)rows,
+                       pix_per_img, f, dc2, dhp ? scratch : nullptr);
+    if (dhp)
+      hipLaunchKernelGGL(gate_imgsum_kernel, dim3((nimg * 2 * f + 255) / 256), dim3(256), 0, st, scratch,
+                         pix_per_img / GT_RPB, nimg, 2 * f, dhp);
+    return hipchk();
+  }
+  hipLaunchKernelGGL(gate_bwd_kernel, dim3(blocks_for(rows * f)), dim3(256), 0, st, c2, hp, dout, lddo, (long long)rows,
+                     pix_per_img, f, dc2);
+  if (dhp) return svae_pcnn_imgsum(dc2, 2 * f, nimg, pix_per_img, 2 * f, dhp, scratch, stream);
   return hipchk();
 }
 
@@ -1829,8 +1947,14 @@ int svae_pcnn_imgsum(const float* x, int ldx, int nimg, int pix_per_img, int c, 
 
 int svae_pcnn_copy(const float* x, int ldx, int64_t rows, int c, float* y, int ldy, int accumulate, void* stream) {
   if (!x || !y || rows < 1 || c < 1 || ldx < c || ldy < c) return bad("pcnn_copy: bad arguments");
-  hipLaunchKernelGGL(copy_kernel, dim3(blocks_for(rows * c)), dim3(256), 0, (hipStream_t)stream, x, ldx,
-                     (long long)rows, c, y, ldy, accumulate);
+  hipStream_t st = (hipStream_t)stream;
+  if (c % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && al16(x) && al16(y)) {
+    hipLaunchKernelGGL(copy4_kernel, dim3((unsigned)((rows + GT_RPB - 1) / GT_RPB)), dim3(256), 0, st, x, ldx,
+                       (long long)rows, c, y, ldy, accumulate);
+    return hipchk();
+  }
+  hipLaunchKernelGGL(copy_kernel, dim3(blocks_for(rows * c)), dim3(256), 0, st, x, ldx, (long long)rows, c, y, ldy,
+                     accumulate);
   return hipchk();
 }
 

@@ -410,13 +410,13 @@ class PixelCNNpp:
                 st2 = self._st()
                 dy = self._grad(y)
                 dc2, _ = self._gout(c2)  # (c2's only consumer: written)
-                _ck(self.L.svae_pcnn_gate_bwd(c2.ptr(), _p(hp), _p(dy), F, x.rows, x.h * x.w, F, _p(dc2), st2))
+                dhp = torch.empty(x.n, 2 * F, dtype=torch.float32, device=self.dev)  # per-image sums of dc2
+                _ck(self.L.svae_pcnn_gate_bwd(c2.ptr(), _p(hp), _p(dy), F, x.rows, x.h * x.w, F, _p(dc2), _p(dhp),
+                                              _p(self.scratch), st2))
                 # the residual's gradient is dy itself: y's gradient is complete and dead after this
                 # op, so x takes the buffer over when it has no gradient yet (else one accumulating copy)
                 if not self._galias(x, dy):
                     _ck(self.L.svae_pcnn_copy(_p(dy), F, x.rows, F, _p(self._grad(x)), F, 1, st2))
-                dhp = torch.empty(x.n, 2 * F, dtype=torch.float32, device=self.dev)
-                _ck(self.L.svae_pcnn_imgsum(_p(dc2), 2 * F, x.n, x.h * x.w, 2 * F, _p(dhp), _p(self.scratch), st2))
                 # d hw [K][2F] = h^T . dhp
                 _ck(self.L.svae_pcnn_gemm_small(_p(h), K, 1, _p(dhp), 2 * F, 0, _p(self.G, off_hw), 2 * F, K, 2 * F,
                                                 x.n, 0.0, st2))
