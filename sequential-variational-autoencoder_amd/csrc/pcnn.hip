@@ -1243,6 +1243,28 @@ __global__ void copy4_kernel(const float* __restrict__ x, int ldx, long long row
   }
 }
 
+// long-K form: one wave per output, lanes over K, a fixed butterfly sum (deterministic)
+__global__ __launch_bounds__(256) void gemm_small_wave_kernel(const float* __restrict__ A, int lda, int ta,
+                                                              const float* __restrict__ B, int ldb, int tb,
+                                                              float* __restrict__ C, int ldc, int m, int n, int k,
+                                                              float beta) {
+  const int lane = threadIdx.x & 63;
+  const long long o = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (o >= (long long)m * n) return;
+  const int mi = (int)(o / n), ni = (int)(o - (long long)mi * n);
+  float s = 0.f;
+  for (int kk = lane; kk < k; kk += 64) {
+    const float a = ta ? A[(long long)kk * lda + mi] : A[(long long)mi * lda + kk];
+    const float b = tb ? B[(long long)ni * ldb + kk] : B[(long long)kk * ldb + ni];
+    s = fmaf(a, b, s);
+  }
+  s = wave_sum(s);
+  if (lane == 0) {
+    float* p = C + (long long)mi * ldc + ni;
+    *p = beta != 0.f ? beta * *p + s : s;
+  }
+}
+
 __global__ void gemm_small_kernel(const float* __restrict__ A, int lda, int ta, const float* __restrict__ B, int ldb,
                                   int tb, float* __restrict__ C, int ldc, int m, int n, int k, float beta) {
   const long long stride = (long long)gridDim.x * blockDim.x, total = (long long)m * n;
@@ -1929,6 +1951,11 @@ int svae_pcnn_gate_bwd(const float* c2, const float* hp, const float* dout, int 
 int svae_pcnn_gemm_small(const float* A, int lda, int ta, const float* B, int ldb, int tb, float* C, int ldc, int m,
                          int n, int k, float beta, void* stream) {
   if (!A || !B || !C || m < 1 || n < 1 || k < 1) return bad("pcnn_gemm_small: bad arguments");
+  if (k >= 128) {  // a wave per output: the K loop of one thread would be latency-bound
+    hipLaunchKernelGGL(gemm_small_wave_kernel, dim3((unsigned)(((long long)m * n + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, A, lda, ta, B, ldb, tb, C, ldc, m, n, k, beta);
+    return hipchk();
+  }
   hipLaunchKernelGGL(gemm_small_kernel, dim3(blocks_for((long long)m * n)), dim3(256), 0, (hipStream_t)stream, A, lda,
                      ta, B, ldb, tb, C, ldc, m, n, k, beta);
   return hipchk();
