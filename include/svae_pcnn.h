@@ -46,6 +46,15 @@ int svae_pcnn_wnorm_bwd(const float* V, const float* g, const float* norm, const
 int svae_pcnn_conv(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, const void* wk, int kpad,
                    const float* bias, float* y, int ho, int wo, int cout, int ldy, int kh, int kw, int s, int pt,
                    int pl, int mode, int accumulate, int zero_edge, void* stream);
+/* the input gradient of a conv whose input is a resnet nonlinearity's output t = f(src) . mask
+ * (kind 0 relu, 1 elu; mask as svae_pcnn_nonlin: given, or drawn from keep / seed): the mode-(1-m)
+ * gather of dy (fp32, the transposed weight copy wk) with dsrc (+)= result . mask . f'(src) written
+ * in the epilogue -- d t and the nonlinearity's backward pass are never materialised.  src [rows][lds],
+ * rows = n*ho*wo of the gather's output space (= t's pixels). */
+int svae_pcnn_conv_act_bwd(const float* dy, int n, int hi, int wi, int cin, int lddy, const void* wk, int kpad,
+                           float* dsrc, int ho, int wo, int cout, int ldd, int kh, int kw, int s, int pt, int pl, int mode,
+                           int accumulate, const float* src, int lds, int kind, const float* mask, float keep,
+                           uint64_t seed, void* stream);
 /* weight gradient of that conv: dW[tap][cin][cout] = sum_rows gather(x)[row][ci] . dy[row][co]
  * (split over rows into `scratch` slabs, then a fixed-order reduce: deterministic); x fp32 or bf16
  * (x_bf16 = 1).  dbias (may be NULL): the bias gradient sum_rows dy[row][co], written, from the same

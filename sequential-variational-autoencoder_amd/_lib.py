@@ -105,6 +105,8 @@ def lib():
         "svae_pcnn_wnorm_bwd": ([vp, vp, vp, vp, i32, i32, i32, vp, vp, vp], i32),
         "svae_pcnn_conv": ([vp, i32, i32, i32, i32, i32, i32, vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, i32,
                             i32, i32, i32, i32, i32, vp], i32),
+        "svae_pcnn_conv_act_bwd": ([vp, i32, i32, i32, i32, i32, vp, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32,
+                                    i32, i32, i32, vp, i32, i32, vp, f32, u64, vp], i32),
         "svae_pcnn_conv_wgrad": ([vp, i32, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32,
                                   i32, vp, vp, vp, i64, vp], i32),
         "svae_pcnn_colsum": ([vp, i64, i32, i32, i32, i32, i32, vp, i32, vp, vp], i32),
@@ -153,7 +155,7 @@ PCNN_EXPORTED = ["svae_pcnn_wnorm", "svae_pcnn_wnorm_bwd", "svae_pcnn_conv", "sv
                  "svae_pcnn_pad_ones", "svae_pcnn_mixlogistic", "svae_pcnn_sum", "svae_pcnn_sample",
                  "svae_pcnn_highway", "svae_pcnn_wn_init", "svae_pcnn_adam", "svae_pcnn_ema", "svae_pcnn_sample_bwd",
                  "svae_pcnn_highway_bwd", "svae_pcnn_dropout", "svae_pcnn_sqerr",
-                 "svae_pcnn_dropout_mask"]
+                 "svae_pcnn_dropout_mask", "svae_pcnn_conv_act_bwd"]
 
 # bf16 GEMM instance ids (csrc/kernels.h KernelId) for svae_probe_begin
 KID_IGEMM_BF16_256x32 = 2

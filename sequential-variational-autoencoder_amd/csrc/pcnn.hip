@@ -65,6 +65,24 @@ __device__ __forceinline__ bool pc_src(const PcGeom& g, int oy, int ox, int ky, 
   return iy >= 0 && iy < g.hi && ix >= 0 && ix < g.wi;
 }
 
+// The input-gradient epilogue of a conv whose input is a resnet nonlinearity's output t = f(src) *
+// mask (relu / elu, nn.py:270-274): the conv writes d src = d t * mask * f'(src) instead of d t,
+// so the nonlinearity's backward pass (and d t's buffer) disappear.  on = 0: a plain epilogue.
+struct NlbArgs {
+  const float* src; int lds;  // the nonlinearity's input, [rows][lds]
+  int kind;                    // 0 relu, 1 elu
+  const float* mask;           // keep-mask [rows][cols], or NULL: hashed (keep, seed) / none (keep >= 1)
+  float keep; unsigned long long seed;
+  int on;
+};
+__device__ __forceinline__ float drop_scale(unsigned long long seed, unsigned long long idx, float keep, float inv);
+__device__ __forceinline__ float nlb_apply(const NlbArgs& e, long long row, int col, int cols, float g) {
+  if (e.mask) g *= e.mask[row * cols + col];
+  else if (e.keep < 1.f) g *= drop_scale(e.seed, (unsigned long long)(row * cols + col), e.keep, 1.f / e.keep);
+  const float v = e.src[row * e.lds + col];
+  return e.kind == 0 ? (v > 0.f ? g : 0.f) : g * (v > 0.f ? 1.f : expf(v));  // (relu'(0) = 0, elu' as delu_f)
+}
+
 // ---------------------------------------------------------------------------------------------
 // weight norm (nn.py:173, :201, :236)
 // ---------------------------------------------------------------------------------------------
@@ -233,7 +251,7 @@ template <int NT, bool XB>
 __global__ __launch_bounds__(256) void pc_conv2_kernel(PcGeom g, const void* __restrict__ Xv,
                                                        const __bf16* __restrict__ Wk, int kpad,
                                                        const float* __restrict__ bias, float* __restrict__ Y,
-                                                       int ldy, int accumulate, int zero_edge) {
+                                                       int ldy, int accumulate, int zero_edge, NlbArgs nlb) {
   constexpr int BR = 32 * NT;  // weight rows (output channels) per block
   __shared__ __attribute__((aligned(16))) __bf16 As[2][128 * PC2_P];
   __shared__ __attribute__((aligned(16))) __bf16 Bs[2][BR * PC2_P];
@@ -343,6 +361,7 @@ __global__ __launch_bounds__(256) void pc_conv2_kernel(PcGeom g, const void* __r
       const int n = n0 + t * 32 + l32;
       if (n >= g.cout) continue;
       float val = zero ? 0.f : acc[t][r] + (bias ? bias[n] : 0.f);
+      if (nlb.on) val = nlb_apply(nlb, mm, n, g.cout, val);
       float* p = Y + mm * ldy + n;
       if (accumulate) val += *p;
       *p = val;
@@ -373,7 +392,7 @@ template <int NT, int TM, bool XB>
 __global__ __launch_bounds__(512) void pc_conv3_kernel(PcGeom g, Pc3 h, const void* __restrict__ Xv,
                                                        const __bf16* __restrict__ Wk, int kpad,
                                                        const float* __restrict__ bias, float* __restrict__ Y,
-                                                       int ldy, int accumulate, int zero_edge) {
+                                                       int ldy, int accumulate, int zero_edge, NlbArgs nlb) {
   constexpr int BM = 256 * TM;
   constexpr int BR = 32 * NT;                                  // weight rows (output channels) per tap
   constexpr int AI = (PC3_MAXPIX * 4 + 511) / 512;             // window items (8 channels) per thread
@@ -512,6 +531,33 @@ __global__ __launch_bounds__(512) void pc_conv3_kernel(PcGeom g, Pc3 h, const vo
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
     const long long mw = m0 + wave * 32 * TM + tm * 32;
+    if (nlb.on) {  // activation-backward epilogue: per column tile, every load of the 16 rows before the stores
+      const float* __restrict__ srcp = nlb.src;
+      const float* __restrict__ mskp = nlb.mask;
+      const float inv = 1.f / nlb.keep;
+#pragma unroll
+      for (int tn = 0; tn < NT; ++tn) {
+        const int n = n0 + tn * 32 + l32;
+        if (n >= g.cout) continue;
+        float sv[16], mv[16], cv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const long long mm = mw + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          sv[r] = srcp[mm * nlb.lds + n];
+          mv[r] = mskp ? mskp[mm * g.cout + n]
+                       : (nlb.keep < 1.f ? drop_scale(nlb.seed, (unsigned long long)(mm * g.cout + n), nlb.keep, inv) : 1.f);
+          cv[r] = accumulate ? Y[mm * ldy + n] : 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const long long mm = mw + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          const float gm = acc[tm][tn][r] * mv[r];
+          const float d = nlb.kind == 0 ? (sv[r] > 0.f ? gm : 0.f) : gm * (sv[r] > 0.f ? 1.f : expf(sv[r]));
+          Y[mm * ldy + n] = accumulate ? d + cv[r] : d;
+        }
+      }
+      continue;
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const long long mm = mw + (r & 3) + 8 * (r >> 2) + 4 * hh;
@@ -568,7 +614,7 @@ bool pc3_plan(const PcGeom& g, int kpad, int TM, Pc3* out, size_t* lds) {
 
 template <int NT, int TM, bool XB>
 void pc3_launch(const PcGeom& g, const Pc3& h, const void* x, const __bf16* w, int kpad, const float* bias, float* y,
-                int ldy, int accumulate, int zero_edge, hipStream_t st) {
+                int ldy, int accumulate, int zero_edge, const NlbArgs& nlb, hipStream_t st) {
   const size_t lds = (size_t)(h.npix + g.kh * g.kw * 32 * NT) * PC2_P * 2;
   static bool attr = false;
   if (!attr) {  // the largest window + weight stage: 640 pixels + 6 taps x 160 rows (128 KB)
@@ -579,7 +625,7 @@ void pc3_launch(const PcGeom& g, const Pc3& h, const void* x, const __bf16* w, i
   const long long rows = (long long)g.n * g.ho * g.wo;
   const dim3 grid((unsigned)(rows / (256 * TM)), (unsigned)((g.cout + 32 * NT - 1) / (32 * NT)));
   hipLaunchKernelGGL((pc_conv3_kernel<NT, TM, XB>), grid, dim3(512), lds, st, g, h, x, w, kpad, bias, y, ldy, accumulate,
-                     zero_edge);
+                     zero_edge, nlb);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1701,9 +1747,31 @@ int svae_pcnn_wnorm_bwd(const float* V, const float* g, const float* norm, const
   return hipchk();
 }
 
+static int pcnn_conv_impl(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, const void* wk, int kpad,
+                          const float* bias, float* y, int ho, int wo, int cout, int ldy, int kh, int kw, int s, int pt,
+                          int pl, int mode, int accumulate, int zero_edge, const NlbArgs& nlb, void* stream);
+
 int svae_pcnn_conv(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, const void* wk, int kpad,
                    const float* bias, float* y, int ho, int wo, int cout, int ldy, int kh, int kw, int s, int pt,
                    int pl, int mode, int accumulate, int zero_edge, void* stream) {
+  NlbArgs nlb{};
+  return pcnn_conv_impl(x, n, hi, wi, cin, ldx, x_bf16, wk, kpad, bias, y, ho, wo, cout, ldy, kh, kw, s, pt, pl, mode,
+                        accumulate, zero_edge, nlb, stream);
+}
+
+int svae_pcnn_conv_act_bwd(const float* dy, int n, int hi, int wi, int cin, int lddy, const void* wk, int kpad,
+                           float* dsrc, int ho, int wo, int cout, int ldd, int kh, int kw, int s, int pt, int pl, int mode,
+                           int accumulate, const float* src, int lds, int kind, const float* mask, float keep,
+                           uint64_t seed, void* stream) {
+  if (!src || lds < cout || kind < 0 || kind > 1 || (!mask && !(keep > 0.f))) return bad("pcnn_conv_act_bwd: bad arguments");
+  NlbArgs nlb{src, lds, kind, mask, keep, (unsigned long long)seed, 1};
+  return pcnn_conv_impl(dy, n, hi, wi, cin, lddy, 0, wk, kpad, nullptr, dsrc, ho, wo, cout, ldd, kh, kw, s, pt, pl, mode,
+                        accumulate, 0, nlb, stream);
+}
+
+static int pcnn_conv_impl(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, const void* wk, int kpad,
+                          const float* bias, float* y, int ho, int wo, int cout, int ldy, int kh, int kw, int s, int pt,
+                          int pl, int mode, int accumulate, int zero_edge, const NlbArgs& nlb, void* stream) {
   const PcGeom g = make_geom(n, hi, wi, cin, ldx, ho, wo, cout, kh, kw, s, pt, pl, mode);
   if (!x || !wk || !y || !geom_ok(g) || ldy < cout || kpad < cin || kpad % 16 || zero_edge < 0 || zero_edge > 2)
     return bad("pcnn_conv: bad arguments");
@@ -1741,11 +1809,11 @@ int svae_pcnn_conv(const void* x, int n, int hi, int wi, int cin, int ldx, int x
       }
 #define PC3_NT(TMV, XBV)                                                                                \
   switch (NT) {                                                                                         \
-    case 1: pc3_launch<1, TMV, XBV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, st); break; \
-    case 2: pc3_launch<2, TMV, XBV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, st); break; \
-    case 3: pc3_launch<3, TMV, XBV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, st); break; \
-    case 4: pc3_launch<4, TMV, XBV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, st); break; \
-    default: pc3_launch<5, TMV, XBV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, st); break; \
+    case 1: pc3_launch<1, TMV, XBV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, st); break; \
+    case 2: pc3_launch<2, TMV, XBV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, st); break; \
+    case 3: pc3_launch<3, TMV, XBV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, st); break; \
+    case 4: pc3_launch<4, TMV, XBV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, st); break; \
+    default: pc3_launch<5, TMV, XBV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, st); break; \
   }
       if (x_bf16) { PC3_NT(1, true) }
       else if (pc3 == 2) { PC3_NT(2, false) }
@@ -1756,17 +1824,17 @@ int svae_pcnn_conv(const void* x, int n, int hi, int wi, int cin, int ldx, int x
     const dim3 grid(gx, tiles);
 #define PC2_NT(XBV)                                                                                                   \
   switch (NT) {                                                                                                      \
-    case 1: hipLaunchKernelGGL((pc_conv2_kernel<1, XBV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge); break; \
-    case 2: hipLaunchKernelGGL((pc_conv2_kernel<2, XBV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge); break; \
-    case 3: hipLaunchKernelGGL((pc_conv2_kernel<3, XBV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge); break; \
-    case 4: hipLaunchKernelGGL((pc_conv2_kernel<4, XBV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge); break; \
-    default: hipLaunchKernelGGL((pc_conv2_kernel<5, XBV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge); break; \
+    case 1: hipLaunchKernelGGL((pc_conv2_kernel<1, XBV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb); break; \
+    case 2: hipLaunchKernelGGL((pc_conv2_kernel<2, XBV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb); break; \
+    case 3: hipLaunchKernelGGL((pc_conv2_kernel<3, XBV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb); break; \
+    case 4: hipLaunchKernelGGL((pc_conv2_kernel<4, XBV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb); break; \
+    default: hipLaunchKernelGGL((pc_conv2_kernel<5, XBV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb); break; \
   }
     if (x_bf16) { PC2_NT(true) } else { PC2_NT(false) }
 #undef PC2_NT
     return hipchk();
   }
-  if (x_bf16) return bad("pcnn_conv: bf16 input on the register-direct kernel (SVAE_PC_CONV1)");
+  if (x_bf16 || nlb.on) return bad("pcnn_conv: bf16 input / activation epilogue on the register-direct kernel (SVAE_PC_CONV1)");
   // register-direct kernel: two 32-column subtiles per wave (wider tiles measured slower here)
   const float* xf = (const float*)x;
   if (cout > 32)

@@ -180,6 +180,11 @@ class PixelCNNpp:
         self._record = self._init = False
         self._dropout_p, self._masks, self.last_masks = 0.0, None, []
         self.keep_masks = False  # drawn masks: record their tensors in last_masks (else DropMask descriptors)
+        # relu / elu backward in the consuming conv's input-gradient epilogue (svae_pcnn_conv_act_bwd):
+        # bitwise the same gradients, but 800 -> 765 img/s on c_pixelvae (the one-block-per-CU halo conv
+        # exposes the epilogue's extra loads), so off by default
+        self.fuse_act_bwd = False
+        self._nl_src = {}
         self.probe, self.probe_cap = None, 0  # [(flops, event, event)] of timed forward conv launches
         self.conv_flops = 0.0  # running total of forward conv FLOPs (tools/bench_pcnn.py)
 
@@ -340,6 +345,17 @@ class PixelCNNpp:
                                   _p(self.G, off_v), _p(self.G, off_g), st))
         if id(x) in self._nograd:
             return
+        root = x
+        while id(root) in self._same:
+            root = self._same[id(root)]
+        nl = self._nl_src.get(id(root))
+        if nl is not None:  # x = f(src) * mask: the input gradient's epilogue writes d src (no d x, no f' pass)
+            src, k, mp, keep, seed = nl
+            ds, dacc = self._gout(src)
+            _ck(L.svae_pcnn_conv_act_bwd(_p(dy), y.n, y.h, y.w, cout, cout, ctypes.c_void_p(wkd.data_ptr()), kd, _p(ds),
+                                         x.h, x.w, cin, cin, kh, kw, s, pt, pl, 1 - mode, dacc, src.ptr(), src.ld, k, mp,
+                                         keep, seed, st))
+            return
         dx, dacc = self._gout(x)
         # the input gradient: the transposed gather over dy with the [tap][Cin][Cout] copy
         _ck(L.svae_pcnn_conv(_p(dy), y.n, y.h, y.w, cout, cout, 0, ctypes.c_void_p(wkd.data_ptr()), kd, None, _p(dx),
@@ -364,6 +380,9 @@ class PixelCNNpp:
         else:
             mp, keep, seed = _p(mask), 1.0, 0
         _ck(self.L.svae_pcnn_nonlin(x.ptr(), x.rows, x.c, x.ld, k, mp, keep, seed, y.ptr(), y.ld, int(bf), self._st()))
+        if self._record and k != 2 and self.fuse_act_bwd:  # its consuming conv applies f' (svae_pcnn_conv_act_bwd)
+            self._nl_src[id(y)] = (x, k, mp, keep, seed)
+            self._keep.append(x)
         if self._record:
             def bwd():
                 if not self._has_grad(y):
@@ -477,6 +496,7 @@ class PixelCNNpp:
         self.last_masks = []
         self._tape, self._g, self._keep, self._same, self._cnt = [], {}, [], {}, {}
         self._nograd = set()
+        self._nl_src = {}
         B, H, W = x.shape[0], s["H"], s["W"]
         F, R = s["F"], s["R"]
         rows = B * H * W
@@ -525,7 +545,7 @@ class PixelCNNpp:
         return l.buf.view(x.shape[0], self.s["H"], self.s["W"], 10 * self.s["M"])
 
     def _drop(self):
-        self._tape, self._g, self._keep, self._same = [], {}, [], {}
+        self._tape, self._g, self._keep, self._same, self._nl_src = [], {}, [], {}, {}
 
     def loss(self, x, h, backward=True, grad_h=False, coef=1.0):
         """NLL = discretized_mix_logistic_loss(x, model(x, h)) summed (nn.py:84-85).  With

@@ -215,3 +215,22 @@ def test_seeded_dropout_matches_explicit_mask():
     scale = {float(v) for t in tens for v in t.unique().tolist()}
     print("\nseeded dropout: kept fraction %.4f, values %s" % (kept, sorted(scale)))
     assert abs(kept - 0.7) < 0.02 and len(scale) == 2 and abs(max(scale) - 1 / 0.7) < 1e-6
+
+
+@pytest.mark.parametrize("nl", ["relu", "elu"])
+def test_fused_activation_backward_is_bitwise(nl):
+    """The relu / elu backward applied in the consuming conv's input-gradient epilogue
+    (svae_pcnn_conv_act_bwd) gives bitwise the gradients of the separate nonlinearity pass, with
+    seeded dropout on."""
+    PC, spec, ospec, params, x, h = _setup(nl, nr_filters=16)
+    net = PC.PixelCNNpp(spec, params=params)
+    res = []
+    for fuse in (True, False):
+        net.fuse_act_bwd = fuse
+        torch.manual_seed(5)
+        l = net.forward_train(x, h, dropout_p=0.3).clone()
+        dh = net.backward_from(torch.ones_like(l).reshape(-1, l.shape[-1]) * 0.01)
+        torch.cuda.synchronize()
+        res.append((l, net.G.clone(), dh.clone()))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
