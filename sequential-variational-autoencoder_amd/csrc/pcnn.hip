@@ -1869,7 +1869,11 @@ int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx,
     Pw4 h;
     if (pw4 && pw4_plan(g4, rows, &h)) {
       const long long tiles4 = (long long)((cin + 63) / 64) * ((cout + 63) / 64) * kh;
-      long long ns = (1024 + tiles4 - 1) / tiles4;  // ~1024 blocks
+      static const int tgt4 = [] {  // SVAE_PW4_TARGET: blocks of the tap-row kernel (default 1024)
+        const char* v = getenv("SVAE_PW4_TARGET");
+        return v ? atoi(v) : 1024;
+      }();
+      long long ns = (tgt4 + tiles4 - 1) / tiles4;
       if (ns > h.nchunk) ns = h.nchunk;
       if (ns > scratch_elems / (wsz + cout)) ns = scratch_elems / (wsz + cout);
       if (ns < 1) return bad("pcnn_wgrad: scratch too small");
@@ -1890,7 +1894,11 @@ int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx,
   }
   const int tiles = ((cin + 63) / 64) * ((cout + 63) / 64);
   // splits: ~2048 blocks, >= 256 rows (8 chunks) per split, bounded by the scratch slabs
-  long long ns = (2048 + (long long)tiles * taps - 1) / ((long long)tiles * taps);
+  static const int tgt1 = [] {  // SVAE_PW_TARGET: blocks of the one-tap kernel (default 2048)
+    const char* v = getenv("SVAE_PW_TARGET");
+    return v ? atoi(v) : 2048;
+  }();
+  long long ns = (tgt1 + (long long)tiles * taps - 1) / ((long long)tiles * taps);
   const long long max_rows = (rows + 255) / 256;
   if (ns > max_rows) ns = max_rows;
   if (ns > scratch_elems / (wsz + cout)) ns = scratch_elems / (wsz + cout);  // slabs + bias partials
