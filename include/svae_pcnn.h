@@ -57,11 +57,11 @@ int svae_pcnn_conv_act_bwd(const float* dy, int n, int hi, int wi, int cin, int 
                            uint64_t seed, void* stream);
 /* weight gradient of that conv: dW[tap][cin][cout] = sum_rows gather(x)[row][ci] . dy[row][co]
  * (split over rows into `scratch` slabs, then a fixed-order reduce: deterministic); x fp32 or bf16
- * (x_bf16 = 1).  dbias (may be NULL): the bias gradient sum_rows dy[row][co], written, from the same
- * pass over dy (fp32 sums). */
-int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, const float* dy, int ldd, int ho,
-                         int wo, int cout, int kh, int kw, int s, int pt, int pl, int mode, float* dW, float* dbias,
-                         float* scratch, int64_t scratch_elems, void* stream);
+ * (x_bf16 = 1), dy fp32 or bf16 (dy_bf16 = 1).  dbias (may be NULL, fp32 dy only): the bias gradient
+ * sum_rows dy[row][co], written, from the same pass over dy (fp32 sums). */
+int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, const void* dy, int ldd,
+                         int dy_bf16, int ho, int wo, int cout, int kh, int kw, int s, int pt, int pl, int mode, float* dW,
+                         float* dbias, float* scratch, int64_t scratch_elems, void* stream);
 /* column sums over rows (bias gradients): out[c] (+)= sum_r x[r][c]; mask_edge 1 / 2 skips
  * rows with oy == 0 / ox == 0 of a [n][ho][wo] row space (the zeroed shifted outputs). */
 int svae_pcnn_colsum(const float* x, int64_t rows, int c, int ldx, int ho, int wo, int mask_edge, float* out,
@@ -77,9 +77,13 @@ int svae_pcnn_mask_edge(float* x, int n, int ho, int wo, int c, int ldx, int mas
  * operand).  Dropout or a bf16 y needs c, ldx, ldy multiples of 4 and 16-B aligned rows. */
 int svae_pcnn_nonlin(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, float keep,
                      uint64_t seed, void* y, int ldy, int y_bf16, void* stream);
-/* its backward: dx (+)= f'(x) . (dy . mask), the mask given or drawn as in the forward */
+/* its backward: dx (+)= f'(x) . (dy . mask), the mask given or drawn as in the forward.  dx fp32, or
+ * bf16 (dx_bf16 = 1: a gradient read only as a bf16 MFMA operand); dsum (may be NULL): the column
+ * sums of the written gradient over all rows, fp32 (a conv's bias gradient), from the same pass
+ * (scratch: ceil(rows / 64) * c floats).  bf16 / dsum: kinds 0 / 1, accumulate = 0, aligned rows. */
 int svae_pcnn_nonlin_bwd(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, float keep,
-                         uint64_t seed, const float* dy, int ldy, float* dx, int lddx, int accumulate, void* stream);
+                         uint64_t seed, const float* dy, int ldy, void* dx, int lddx, int dx_bf16, int accumulate,
+                         float* dsum, float* scratch, void* stream);
 /* the seeded dropout keep-mask: out[i] = 1 / keep with probability keep, else 0 (splitmix64 of
  * seed + i, 24-bit uniform), i < n -- what the two calls above draw for a NULL mask. */
 int svae_pcnn_dropout_mask(int64_t n, float keep, uint64_t seed, float* out, void* stream);
@@ -89,10 +93,11 @@ int svae_pcnn_dropout_mask(int64_t n, float keep, uint64_t seed, float* out, voi
 int svae_pcnn_gate(const float* x, int ldx, const float* c2, const float* hp, int64_t rows, int pix_per_img, int f,
                    float* out, int ldo, void* stream);
 /* its backward from the saved c2 and hp: dc2 [rows][2f] = [dout . sig(b), dout . a . sig'(b)]
- * (the residual's gradient dx is dout itself); dhp (may be NULL): the per-image sums of dc2,
- * [nimg][2f] (d loss / d (h . hw)), from the same pass (scratch: rows / 64 * 2f floats). */
+ * (the residual's gradient dx is dout itself), fp32 or bf16 (dc2_bf16 = 1); dhp (may be NULL): the
+ * per-image sums of dc2, [nimg][2f] (d loss / d (h . hw)); dsum (may be NULL): its sums over all rows
+ * (the producing conv's bias gradient); both fp32 from the same pass (scratch: rows / 64 * 2f floats). */
 int svae_pcnn_gate_bwd(const float* c2, const float* hp, const float* dout, int lddo, int64_t rows, int pix_per_img,
-                       int f, float* dc2, float* dhp, float* scratch, void* stream);
+                       int f, void* dc2, int dc2_bf16, float* dhp, float* dsum, float* scratch, void* stream);
 
 /* small fp32 GEMM (conditioning projections, highway FC): C[m][n] = beta C + sum_k A(m,k) B(k,n),
  * A(m,k) = ta ? A[k*lda + m] : A[m*lda + k], B(k,n) = tb ? B[n*ldb + k] : B[k*ldb + n]. */

@@ -108,14 +108,14 @@ def lib():
         "svae_pcnn_conv_act_bwd": ([vp, i32, i32, i32, i32, i32, vp, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32,
                                     i32, i32, i32, vp, i32, i32, vp, f32, u64, vp], i32),
         "svae_pcnn_conv_wgrad": ([vp, i32, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32,
-                                  i32, vp, vp, vp, i64, vp], i32),
+                                  i32, i32, vp, vp, vp, i64, vp], i32),
         "svae_pcnn_colsum": ([vp, i64, i32, i32, i32, i32, i32, vp, i32, vp, vp], i32),
         "svae_pcnn_mask_edge": ([vp, i32, i32, i32, i32, i32, i32, vp], i32),
         "svae_pcnn_nonlin": ([vp, i64, i32, i32, i32, vp, f32, u64, vp, i32, i32, vp], i32),
-        "svae_pcnn_nonlin_bwd": ([vp, i64, i32, i32, i32, vp, f32, u64, vp, i32, vp, i32, i32, vp], i32),
+        "svae_pcnn_nonlin_bwd": ([vp, i64, i32, i32, i32, vp, f32, u64, vp, i32, vp, i32, i32, i32, vp, vp, vp], i32),
         "svae_pcnn_dropout_mask": ([i64, f32, u64, vp, vp], i32),
         "svae_pcnn_gate": ([vp, i32, vp, vp, i64, i32, i32, vp, i32, vp], i32),
-        "svae_pcnn_gate_bwd": ([vp, vp, vp, i32, i64, i32, i32, vp, vp, vp, vp], i32),
+        "svae_pcnn_gate_bwd": ([vp, vp, vp, i32, i64, i32, i32, vp, i32, vp, vp, vp, vp], i32),
         "svae_pcnn_gemm_small": ([vp, i32, i32, vp, i32, i32, vp, i32, i32, i32, i32, f32, vp], i32),
         "svae_pcnn_imgsum": ([vp, i32, i32, i32, i32, vp, vp, vp], i32),
         "svae_pcnn_copy": ([vp, i32, i64, i32, vp, i32, i32, vp], i32),

@@ -658,10 +658,12 @@ struct Pw4 {
 #define PW4_CP 128     // output pixels per chunk
 #define PW4_MAXPIX 144 // 8 rows x 18 (16-wide images, kw = 3)
 #define PW4_P 72       // LDS pixel pitch (bf16): 64 channels + 8
-template <bool XB>
+// DB: D (the output gradient) stored bf16 -- its MFMA precision (the bias sum is then done upstream)
+template <bool XB, bool DB>
 __global__ __launch_bounds__(256) void pc_wgrad4_kernel(PcGeom g, Pw4 h, const void* __restrict__ Xv,
-                                                        const float* __restrict__ D, int ldd, float* __restrict__ part,
+                                                        const void* __restrict__ Dv, int ldd, float* __restrict__ part,
                                                         float* __restrict__ bsum) {
+  const float* D = (const float*)Dv;
   constexpr int WI = (PW4_MAXPIX * 8 + 255) / 256;  // window items (8 channels) per thread
   constexpr int DI = (PW4_CP * 16 + 255) / 256;     // D items (4 columns) per thread
   __shared__ __attribute__((aligned(16))) __bf16 smem[(PW4_MAXPIX + PW4_CP) * PW4_P];
@@ -677,7 +679,7 @@ __global__ __launch_bounds__(256) void pc_wgrad4_kernel(PcGeom g, Pw4 h, const v
   const int c_beg = split * h.cps;
   const int c_end = c_beg + h.cps < h.nchunk ? c_beg + h.cps : h.nchunk;
   const bool bias_blk = bsum && ky == 0 && ci0 == 0;
-  const int iy_off = h.iy_off[ky];
+  const int iy_off = ky == 0 ? h.iy_off[0] : h.iy_off[1];
 
   f32x16 acc[3];
 #pragma unroll
@@ -717,7 +719,12 @@ __global__ __launch_bounds__(256) void pc_wgrad4_kernel(PcGeom g, Pw4 h, const v
     for (int i = 0; i < DI; ++i) {
       const int it = tid + 256 * i;
       const int k = it >> 4, c4 = (it & 15) * 4;
-      dv[i] = co0 + c4 < g.cout ? *(const f32x4*)(D + (p0 + k) * ldd + co0 + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (DB)
+        dv[i] = co0 + c4 < g.cout
+                    ? __builtin_convertvector(*(const pc_bf16x4*)((const __bf16*)Dv + (p0 + k) * ldd + co0 + c4), f32x4)
+                    : f32x4{0.f, 0.f, 0.f, 0.f};
+      else
+        dv[i] = co0 + c4 < g.cout ? *(const f32x4*)(D + (p0 + k) * ldd + co0 + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
   auto store = [&]() {
@@ -782,7 +789,9 @@ __global__ __launch_bounds__(256) void pc_wgrad4_kernel(PcGeom g, Pw4 h, const v
   if (live) {
     float* out = part + (long long)split * g.kh * g.kw * g.cin * g.cout;
     const int n = co0 + wn * 32 + l32;
-    for (int kx = 0; kx < g.kw; ++kx) {
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {  // (unrolled: a runtime-indexed acc would live in scratch memory)
+      if (kx >= g.kw) break;
       const int tap = ky * g.kw + kx;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -830,9 +839,9 @@ bool pw4_plan(const PcGeom& g, long long rows, Pw4* out) {
 #define PW_RP 72  // LDS row pitch (bf16): 64 rows + 8 pad
 // bsum != NULL: the blocks of tap 0 and the first ci tile also sum their D rows per column (fp32,
 // before the bf16 staging) into bsum[split][cout]: the conv's bias gradient without another pass over dy
-template <bool XB>
+template <bool XB, bool DB>
 __global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const void* __restrict__ Xv,
-                                                       const float* __restrict__ D, int ldd, long long rows,
+                                                       const void* __restrict__ Dv, int ldd, long long rows,
                                                        long long rows_per_split, float* __restrict__ part,
                                                        float* __restrict__ bsum) {
   __shared__ __attribute__((aligned(16))) __bf16 Xs[2][64 * PW_RP];
@@ -861,13 +870,15 @@ __global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const void* __r
       const long long row = rc + lr + 32 * u;
       long long xo = -1;
       const float* dp = nullptr;
+      const __bf16* dph = nullptr;
       if (row < r1) {
         const int img = (int)(row / per_img);
         const int rr = (int)(row - (long long)img * per_img);
         const int oy = rr / g.wo, ox = rr - (rr / g.wo) * g.wo;
         int iy, ix;
         if (pc_src(g, oy, ox, ky, kx, iy, ix)) xo = ((long long)(img * g.hi + iy) * g.wi + ix) * g.ldx;
-        dp = D + row * ldd;
+        if constexpr (DB) dph = (const __bf16*)Dv + row * ldd;
+        else dp = (const float*)Dv + row * ldd;
       }
       if constexpr (XB) {
         pc_bf16x8 z8 = {};
@@ -878,7 +889,10 @@ __global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const void* __r
         const int c = (q0 + 8 * j) * 4;
         const f32x4 z = {0.f, 0.f, 0.f, 0.f};
         if constexpr (!XB) xv[u][j] = (xo >= 0 && ci0 + c < g.cin) ? *(const f32x4*)((const float*)Xv + xo + ci0 + c) : z;
-        dv[u][j] = (dp && co0 + c < g.cout) ? *(const f32x4*)(dp + co0 + c) : z;
+        if constexpr (DB)
+          dv[u][j] = (dph && co0 + c < g.cout) ? __builtin_convertvector(*(const pc_bf16x4*)(dph + co0 + c), f32x4) : z;
+        else
+          dv[u][j] = (dp && co0 + c < g.cout) ? *(const f32x4*)(dp + co0 + c) : z;
       }
     }
   };
@@ -1118,6 +1132,47 @@ __global__ __launch_bounds__(256) void nonlin4_bwd_kernel(const float* __restric
   }
 }
 
+// the same backward (kinds 0 / 1, written, not accumulated) with per-block column sums of the written
+// gradient into part[block][c] (row lanes, then lanes in order: deterministic), dx fp32 or bf16
+__global__ __launch_bounds__(256) void nonlin4_bwd_cs_kernel(const float* __restrict__ x, long long rows, int c,
+                                                             int ldx, int kind, const float* __restrict__ mask,
+                                                             float keep, unsigned long long seed,
+                                                             const float* __restrict__ dy, int ldy, void* __restrict__ dxv,
+                                                             int lddx, int out_bf16, float* __restrict__ part) {
+  __shared__ f32x4 red[256];
+  const int q = c >> 2;
+  const int RL = 256 / q;
+  const int tid = threadIdx.x, qi = tid % q, rl = tid / q;
+  const long long r0 = (long long)blockIdx.x * NL_RPB;
+  const int nr = (int)(rows - r0 < NL_RPB ? rows - r0 : NL_RPB);
+  const bool hashed = !mask && keep < 1.f;
+  const float inv = 1.f / keep;
+  const int ch = qi * 4;
+  f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+  if (rl < RL) {
+    for (int rr = rl; rr < nr; rr += RL) {
+      const long long r = r0 + rr;
+      const f32x4 v = *(const f32x4*)(x + r * ldx + ch);
+      f32x4 g = *(const f32x4*)(dy + r * ldy + ch);
+      if (mask) g *= *(const f32x4*)(mask + r * c + ch);
+      else if (hashed) g *= drop_scale4(seed, (unsigned long long)(r * c + ch), keep, inv);
+      f32x4 d;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) d[e] = kind == 0 ? (v[e] > 0.f ? g[e] : 0.f) : g[e] * delu_f(v[e]);
+      if (out_bf16) *(pc_bf16x4*)((__bf16*)dxv + r * lddx + ch) = __builtin_convertvector(d, pc_bf16x4);
+      else *(f32x4*)((float*)dxv + r * lddx + ch) = d;
+      sum += d;
+    }
+  }
+  red[tid] = sum;
+  __syncthreads();
+  if (tid < q) {
+    f32x4 t = red[tid];
+    for (int l = 1; l < RL; ++l) t += red[l * q + tid];
+    *(f32x4*)(part + (long long)blockIdx.x * c + ch) = t;
+  }
+}
+
 __global__ void nonlin_kernel(const float* __restrict__ x, long long rows, int c, int ldx, int kind,
                               float* __restrict__ y, int ldy) {
   const long long stride = (long long)gridDim.x * blockDim.x, total = rows * c;
@@ -1223,7 +1278,7 @@ __global__ __launch_bounds__(256) void gate4_kernel(const float* __restrict__ x,
 }
 __global__ __launch_bounds__(256) void gate4_bwd_kernel(const float* __restrict__ c2, const float* __restrict__ hp,
                                                         const float* __restrict__ dout, int lddo, long long rows,
-                                                        int per_img, int f, float* __restrict__ dc2,
+                                                        int per_img, int f, void* __restrict__ dc2v, int out_bf16,
                                                         float* __restrict__ part) {
   __shared__ f32x4 red[256][2];
   const int q = f >> 2;
@@ -1245,8 +1300,15 @@ __global__ __launch_bounds__(256) void gate4_bwd_kernel(const float* __restrict_
       const f32x4 a = *(const f32x4*)(c2 + r * 2 * f + ch) + ha, b = *(const f32x4*)(c2 + r * 2 * f + f + ch) + hb;
       const f32x4 d = *(const f32x4*)(dout + r * lddo + ch), s = sigm4(b);
       const f32x4 da = d * s, db = d * a * s * (1.f - s);
-      *(f32x4*)(dc2 + r * 2 * f + ch) = da;
-      *(f32x4*)(dc2 + r * 2 * f + f + ch) = db;
+      if (out_bf16) {  // read only as a bf16 MFMA operand (the conv's input gradient and weight gradient)
+        __bf16* o = (__bf16*)dc2v + r * 2 * f + ch;
+        *(pc_bf16x4*)o = __builtin_convertvector(da, pc_bf16x4);
+        *(pc_bf16x4*)(o + f) = __builtin_convertvector(db, pc_bf16x4);
+      } else {
+        float* o = (float*)dc2v + r * 2 * f + ch;
+        *(f32x4*)o = da;
+        *(f32x4*)(o + f) = db;
+      }
       sa += da;
       sb += db;
     }
@@ -1846,12 +1908,13 @@ static int pcnn_conv_impl(const void* x, int n, int hi, int wi, int cin, int ldx
   return hipchk();
 }
 
-int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, const float* dy, int ldd,
-                         int ho, int wo, int cout, int kh, int kw, int s, int pt, int pl, int mode, float* dW,
+int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, const void* dy, int ldd,
+                         int dy_bf16, int ho, int wo, int cout, int kh, int kw, int s, int pt, int pl, int mode, float* dW,
                          float* dbias, float* scratch, int64_t scratch_elems, void* stream) {
   const PcGeom g = make_geom(n, hi, wi, cin, ldx, ho, wo, cout, kh, kw, s, pt, pl, mode);
   if (!x || !dy || !dW || !scratch || !geom_ok(g) || ldd < cout || ldd % 4 || cout % 4)
     return bad("pcnn_wgrad: bad arguments");
+  if (dy_bf16 && dbias) return bad("pcnn_wgrad: the bias gradient needs the fp32 dy (sum it upstream)");
   const long long rows = (long long)n * ho * wo;
   const int taps = kh * kw;
   const long long wsz = (long long)taps * cin * cout;
@@ -1881,10 +1944,10 @@ int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx,
       ns = (h.nchunk + h.cps - 1) / h.cps;
       float* bpart = dbias ? scratch + ns * wsz : nullptr;
       const dim3 grid((unsigned)((cin + 63) / 64), (unsigned)((cout + 63) / 64), (unsigned)(kh * ns));
-      if (x_bf16)
-        hipLaunchKernelGGL(pc_wgrad4_kernel<true>, grid, dim3(256), 0, st, g4, h, x, dy, ldd, scratch, bpart);
-      else
-        hipLaunchKernelGGL(pc_wgrad4_kernel<false>, grid, dim3(256), 0, st, g4, h, x, dy, ldd, scratch, bpart);
+#define PW4_L(XBV, DBV) hipLaunchKernelGGL((pc_wgrad4_kernel<XBV, DBV>), grid, dim3(256), 0, st, g4, h, x, dy, ldd, scratch, bpart)
+      if (x_bf16) { if (dy_bf16) PW4_L(true, true); else PW4_L(true, false); }
+      else { if (dy_bf16) PW4_L(false, true); else PW4_L(false, false); }
+#undef PW4_L
       hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(wsz)), dim3(256), 0, st, scratch, (int)ns, wsz, dW);
       if (dbias)
         hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(cout)), dim3(256), 0, st, bpart, (int)ns,
@@ -1907,12 +1970,11 @@ int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx,
   rps = (rps + 63) / 64 * 64;
   ns = (rows + rps - 1) / rps;
   float* bpart = dbias ? scratch + ns * wsz : nullptr;
-  if (x_bf16)
-    hipLaunchKernelGGL(pc_wgrad_kernel<true>, dim3(tiles, taps, (unsigned)ns), dim3(256), 0, st, g, x, dy, ldd, rows,
-                       rps, scratch, bpart);
-  else
-    hipLaunchKernelGGL(pc_wgrad_kernel<false>, dim3(tiles, taps, (unsigned)ns), dim3(256), 0, st, g, x, dy, ldd, rows,
-                       rps, scratch, bpart);
+#define PW1_L(XBV, DBV) hipLaunchKernelGGL((pc_wgrad_kernel<XBV, DBV>), dim3(tiles, taps, (unsigned)ns), dim3(256), 0, st, g, x, dy, \
+                                           ldd, rows, rps, scratch, bpart)
+  if (x_bf16) { if (dy_bf16) PW1_L(true, true); else PW1_L(true, false); }
+  else { if (dy_bf16) PW1_L(false, true); else PW1_L(false, false); }
+#undef PW1_L
   hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(wsz)), dim3(256), 0, st, scratch, (int)ns, wsz, dW);
   if (dbias)
     hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(cout)), dim3(256), 0, st, bpart, (int)ns, (long long)cout,
@@ -1971,19 +2033,32 @@ int svae_pcnn_nonlin(const float* x, int64_t rows, int c, int ldx, int kind, con
 }
 
 int svae_pcnn_nonlin_bwd(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, float keep,
-                         uint64_t seed, const float* dy, int ldy, float* dx, int lddx, int accumulate, void* stream) {
+                         uint64_t seed, const float* dy, int ldy, void* dx, int lddx, int dx_bf16, int accumulate,
+                         float* dsum, float* scratch, void* stream) {
   if (!x || !dy || !dx || rows < 1 || c < 1 || kind < 0 || kind > 2) return bad("pcnn_nonlin_bwd: bad arguments");
   hipStream_t st = (hipStream_t)stream;
-  const bool vec = c % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && lddx % 4 == 0 && al16(x) && al16(dy) && al16(dx) &&
-                   (!mask || al16(mask));
+  const bool vec = c % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && lddx % 4 == 0 && al16(x) && al16(dy) &&
+                   (dx_bf16 ? ((uintptr_t)dx & 7) == 0 : al16(dx)) && (!mask || al16(mask));
+  if (dx_bf16 || dsum) {  // written gradient (bf16 and / or with its column sums): relu / elu only
+    if (!vec || kind == 2 || accumulate || c > 1024 || (dsum && !scratch))
+      return bad("pcnn_nonlin_bwd: bf16 output / column sums need kind 0/1, a written aligned gradient");
+    const long long nb = (rows + NL_RPB - 1) / NL_RPB;
+    float* part = dsum ? scratch : nullptr;
+    if (!part) return bad("pcnn_nonlin_bwd: bf16 output without column sums is not built");
+    hipLaunchKernelGGL(nonlin4_bwd_cs_kernel, dim3((unsigned)nb), dim3(256), 0, st, x, (long long)rows, c, ldx, kind,
+                       mask, keep, (unsigned long long)seed, dy, ldy, dx, lddx, dx_bf16, part);
+    // the column sums of the per-block partials: the two-stage fixed-order column sum (not one thread per column)
+    return svae_pcnn_colsum(part, nb, c, c, 1, 1, 0, dsum, 0, part + nb * c, stream);
+  }
   if (vec) {
     hipLaunchKernelGGL(nonlin4_bwd_kernel, dim3((unsigned)((rows + NL_RPB - 1) / NL_RPB)), dim3(256), 0, st, x,
-                       (long long)rows, c, ldx, kind, mask, keep, (unsigned long long)seed, dy, ldy, dx, lddx, accumulate);
+                       (long long)rows, c, ldx, kind, mask, keep, (unsigned long long)seed, dy, ldy, (float*)dx, lddx,
+                       accumulate);
     return hipchk();
   }
   if (mask || keep < 1.f) return bad("pcnn_nonlin_bwd: dropout needs 4-channel aligned rows");
   hipLaunchKernelGGL(nonlin_bwd_kernel, dim3(blocks_for(rows * c)), dim3(256), 0, st, x, (long long)rows, c, ldx, kind,
-                     dy, ldy, dx, lddx, accumulate);
+                     dy, ldy, (float*)dx, lddx, accumulate);
   return hipchk();
 }
 
@@ -2003,24 +2078,28 @@ int svae_pcnn_gate(const float* x, int ldx, const float* c2, const float* hp, in
 }
 
 int svae_pcnn_gate_bwd(const float* c2, const float* hp, const float* dout, int lddo, int64_t rows, int pix_per_img,
-                       int f, float* dc2, float* dhp, float* scratch, void* stream) {
-  if (!c2 || !dout || !dc2 || rows < 1 || f < 1 || pix_per_img < 1 || rows % pix_per_img || (dhp && !scratch))
+                       int f, void* dc2, int dc2_bf16, float* dhp, float* dsum, float* scratch, void* stream) {
+  if (!c2 || !dout || !dc2 || rows < 1 || f < 1 || pix_per_img < 1 || rows % pix_per_img || ((dhp || dsum) && !scratch))
     return bad("pcnn_gate_bwd: bad arguments");
   hipStream_t st = (hipStream_t)stream;
   const int nimg = (int)(rows / pix_per_img);
-  if (f % 4 == 0 && f <= 1024 && lddo % 4 == 0 && pix_per_img % GT_RPB == 0 && al16(c2) && al16(dout) && al16(dc2) &&
-      (!hp || al16(hp))) {
+  if (f % 4 == 0 && f <= 1024 && lddo % 4 == 0 && pix_per_img % GT_RPB == 0 && al16(c2) && al16(dout) &&
+      (dc2_bf16 ? ((uintptr_t)dc2 & 7) == 0 : al16(dc2)) && (!hp || al16(hp))) {
     const long long nb = rows / GT_RPB;
+    const bool sums = dhp || dsum;
     hipLaunchKernelGGL(gate4_bwd_kernel, dim3((unsigned)nb), dim3(256), 0, st, c2, hp, dout, lddo, (long long)rows,
-                       pix_per_img, f, dc2, dhp ? scratch : nullptr);
+                       pix_per_img, f, dc2, dc2_bf16, sums ? scratch : nullptr);
     if (dhp)
       hipLaunchKernelGGL(gate_imgsum_kernel, dim3((nimg * 2 * f + 255) / 256), dim3(256), 0, st, scratch,
                          pix_per_img / GT_RPB, nimg, 2 * f, dhp);
+    if (dsum)  // the sums over all rows: the two-stage fixed-order column sum of the block partials
+      return svae_pcnn_colsum(scratch, nb, 2 * f, 2 * f, 1, 1, 0, dsum, 0, scratch + nb * 2 * f, stream);
     return hipchk();
   }
+  if (dc2_bf16 || dsum) return bad("pcnn_gate_bwd: bf16 dc2 / column sums need the vectorised path");
   hipLaunchKernelGGL(gate_bwd_kernel, dim3(blocks_for(rows * f)), dim3(256), 0, st, c2, hp, dout, lddo, (long long)rows,
-                     pix_per_img, f, dc2);
-  if (dhp) return svae_pcnn_imgsum(dc2, 2 * f, nimg, pix_per_img, 2 * f, dhp, scratch, stream);
+                     pix_per_img, f, (float*)dc2);
+  if (dhp) return svae_pcnn_imgsum((const float*)dc2, 2 * f, nimg, pix_per_img, 2 * f, dhp, scratch, stream);
   return hipchk();
 }
 

@@ -18,6 +18,7 @@ dense V [in, out], hw [K, 2F]); names follow the reference's layer counters (nn.
 """
 import ctypes
 import math
+import os
 
 import numpy as np
 import torch
@@ -184,7 +185,10 @@ class PixelCNNpp:
         # bitwise the same gradients, but 800 -> 765 img/s on c_pixelvae (the one-block-per-CU halo conv
         # exposes the epilogue's extra loads), so off by default
         self.fuse_act_bwd = False
-        self._nl_src = {}
+        # the gradients of the resnet convs' outputs, read only as bf16 MFMA operands, stored bf16 (their
+        # bias gradients summed in fp32 by the op that writes them)
+        self.bf16_grads = os.environ.get("SVAE_PC_BF16_GRADS", "0") == "1"  # opt-in: measured slower (804 vs 882 img/s)
+        self._nl_src, self._bias_of, self._bf16_grad = {}, {}, set()
         self.probe, self.probe_cap = None, 0  # [(flops, event, event)] of timed forward conv launches
         self.conv_flops = 0.0  # running total of forward conv FLOPs (tools/bench_pcnn.py)
 
@@ -239,6 +243,11 @@ class PixelCNNpp:
             self._g[id(a)] = g
             self._keep.append(a)
         return g
+
+    def _root(self, a):
+        while id(a) in self._same:
+            a = self._same[id(a)]
+        return a
 
     def _gout(self, a):
         """(gradient buffer of ``a``, accumulate flag) for an op that adds its contribution: the first
@@ -325,6 +334,7 @@ class PixelCNNpp:
         if self._record:
             geo = (kh, kw, s, pt, pl, mode, zero_edge, kf, kd, off_v, off_g, off_b)
             self._tape.append(lambda: self._wconv_bwd(x, out, norm, wkd, geo))
+            self._bias_of.setdefault(id(self._root(out)), []).append(off_b)  # (every conv summed into it)
         return out
 
     def _wconv_bwd(self, x, y, norm, wkd, geo):
@@ -333,14 +343,16 @@ class PixelCNNpp:
         kh, kw, s, pt, pl, mode, zero_edge, kf, kd, off_v, off_g, off_b = geo
         taps, cin, cout = kh * kw, x.c, y.c
         dy = self._grad(y)
+        dyb = dy.dtype == torch.bfloat16  # (its consumer wrote it bf16 and this conv's bias gradient with it)
         if zero_edge:  # the zeroed shifted outputs pass no gradient
             dy = dy.clone()
             _ck(L.svae_pcnn_mask_edge(_p(dy), y.n, y.h, y.w, cout, cout, zero_edge, st))
         dW = torch.empty(taps * cin * cout, dtype=torch.float32, device=self.dev)
         sc = self.scratch
-        # dW and the bias gradient (written into G) from one pass over dy
-        _ck(L.svae_pcnn_conv_wgrad(x.ptr(), x.n, x.h, x.w, cin, x.ld, int(x.bf), _p(dy), cout, y.h, y.w, cout, kh, kw,
-                                   s, pt, pl, mode, _p(dW), _p(self.G, off_b), _p(sc), sc.numel(), st))
+        # dW and (fp32 dy) the bias gradient, written into G, from one pass over dy
+        _ck(L.svae_pcnn_conv_wgrad(x.ptr(), x.n, x.h, x.w, cin, x.ld, int(x.bf), ctypes.c_void_p(dy.data_ptr()), cout,
+                                   int(dyb), y.h, y.w, cout, kh, kw, s, pt, pl, mode, _p(dW),
+                                   None if dyb else _p(self.G, off_b), _p(sc), sc.numel(), st))
         _ck(L.svae_pcnn_wnorm_bwd(_p(self.P, off_v), _p(self.P, off_g), _p(norm), _p(dW), taps, cin, cout,
                                   _p(self.G, off_v), _p(self.G, off_g), st))
         if id(x) in self._nograd:
@@ -348,7 +360,7 @@ class PixelCNNpp:
         root = x
         while id(root) in self._same:
             root = self._same[id(root)]
-        nl = self._nl_src.get(id(root))
+        nl = None if dyb else self._nl_src.get(id(root))
         if nl is not None:  # x = f(src) * mask: the input gradient's epilogue writes d src (no d x, no f' pass)
             src, k, mp, keep, seed = nl
             ds, dacc = self._gout(src)
@@ -358,8 +370,9 @@ class PixelCNNpp:
             return
         dx, dacc = self._gout(x)
         # the input gradient: the transposed gather over dy with the [tap][Cin][Cout] copy
-        _ck(L.svae_pcnn_conv(_p(dy), y.n, y.h, y.w, cout, cout, 0, ctypes.c_void_p(wkd.data_ptr()), kd, None, _p(dx),
-                             x.h, x.w, cin, cin, kh, kw, s, pt, pl, 1 - mode, dacc, 0, st))
+        _ck(L.svae_pcnn_conv(ctypes.c_void_p(dy.data_ptr()), y.n, y.h, y.w, cout, cout, int(dyb),
+                             ctypes.c_void_p(wkd.data_ptr()), kd, None, _p(dx), x.h, x.w, cin, cin, kh, kw, s, pt, pl,
+                             1 - mode, dacc, 0, st))
 
     def _dense(self, x, name, cout, init_scale=1.0):
         """nn.nin / dense over the channel axis (nn.py:255-260): a 1x1 gather GEMM over every pixel."""
@@ -387,9 +400,24 @@ class PixelCNNpp:
             def bwd():
                 if not self._has_grad(y):
                     return
+                rx = self._root(x)
+                if (id(rx) in self._bf16_grad and not self._has_grad(x) and k != 2 and x.c % 8 == 0
+                        and x.ld % 4 == 0):
+                    # x's only consumer: its gradient is written here whole, as bf16 (the producing convs read
+                    # it only as an MFMA operand), with the fp32 column sums = their bias gradients
+                    dx = torch.empty(x.rows, x.c, dtype=torch.bfloat16, device=self.dev)
+                    self._g[id(rx)] = dx
+                    self._keep.append(rx)
+                    offs = self._bias_of[id(rx)]
+                    _ck(self.L.svae_pcnn_nonlin_bwd(x.ptr(), x.rows, x.c, x.ld, k, mp, keep, seed, _p(self._grad(y)),
+                                                    c, ctypes.c_void_p(dx.data_ptr()), x.c, 1, 0,
+                                                    _p(self.G, offs[0]), _p(self.scratch), self._st()))
+                    for o in offs[1:]:
+                        self.G[o:o + x.c].copy_(self.G[offs[0]:offs[0] + x.c])
+                    return
                 dx, dacc = self._gout(x)
                 _ck(self.L.svae_pcnn_nonlin_bwd(x.ptr(), x.rows, x.c, x.ld, k, mp, keep, seed, _p(self._grad(y)), c,
-                                                _p(dx), x.c, dacc, self._st()))
+                                                _p(dx), x.c, 0, dacc, None, None, self._st()))
             self._tape.append(bwd)
         return y
 
@@ -428,10 +456,22 @@ class PixelCNNpp:
                     return
                 st2 = self._st()
                 dy = self._grad(y)
-                dc2, _ = self._gout(c2)  # (c2's only consumer: written)
                 dhp = torch.empty(x.n, 2 * F, dtype=torch.float32, device=self.dev)  # per-image sums of dc2
-                _ck(self.L.svae_pcnn_gate_bwd(c2.ptr(), _p(hp), _p(dy), F, x.rows, x.h * x.w, F, _p(dc2), _p(dhp),
-                                              _p(self.scratch), st2))
+                rc = self._root(c2)
+                offs = self._bias_of.get(id(rc), [])
+                if id(rc) in self._bf16_grad and len(offs) == 1 and (x.h * x.w) % 64 == 0 and F % 4 == 0:
+                    # c2's only consumer: dc2 written bf16 (its conv reads it only as an MFMA operand) with
+                    # the fp32 sums over all rows, the conv's bias gradient
+                    dc2 = torch.empty(c2.rows, c2.c, dtype=torch.bfloat16, device=self.dev)
+                    self._g[id(rc)] = dc2
+                    self._keep.append(rc)
+                    _ck(self.L.svae_pcnn_gate_bwd(c2.ptr(), _p(hp), _p(dy), F, x.rows, x.h * x.w, F,
+                                                  ctypes.c_void_p(dc2.data_ptr()), 1, _p(dhp), _p(self.G, offs[0]),
+                                                  _p(self.scratch), st2))
+                else:
+                    dc2, _ = self._gout(c2)  # (c2's only consumer: written)
+                    _ck(self.L.svae_pcnn_gate_bwd(c2.ptr(), _p(hp), _p(dy), F, x.rows, x.h * x.w, F, _p(dc2), 0,
+                                                  _p(dhp), None, _p(self.scratch), st2))
                 # the residual's gradient is dy itself: y's gradient is complete and dead after this
                 # op, so x takes the buffer over when it has no gradient yet (else one accumulating copy)
                 if not self._galias(x, dy):
@@ -456,6 +496,8 @@ class PixelCNNpp:
         mask = self._next_mask(c1.rows, 2 * c1.c if nl == "concat_elu" else c1.c)
         t2 = self._nonlin(c1, nl, mask)
         c2 = self._wconv(t2, self._nm("conv2d"), 2 * x.c, kh, kw, 1, pt, pl, init_scale=0.1)
+        if self.bf16_grads:  # c1 / c2 feed one op each: their gradients may be written bf16 by it
+            self._bf16_grad.update((id(self._root(c1)), id(self._root(c2))))
         return self._gate(x, c2, h, self._nm("conditional_weights") + "/hw")
 
     def _next_mask(self, rows, c):
@@ -496,7 +538,7 @@ class PixelCNNpp:
         self.last_masks = []
         self._tape, self._g, self._keep, self._same, self._cnt = [], {}, [], {}, {}
         self._nograd = set()
-        self._nl_src = {}
+        self._nl_src, self._bias_of, self._bf16_grad = {}, {}, set()
         B, H, W = x.shape[0], s["H"], s["W"]
         F, R = s["F"], s["R"]
         rows = B * H * W
@@ -546,6 +588,7 @@ class PixelCNNpp:
 
     def _drop(self):
         self._tape, self._g, self._keep, self._same, self._nl_src = [], {}, [], {}, {}
+        self._bias_of, self._bf16_grad = {}, set()
 
     def loss(self, x, h, backward=True, grad_h=False, coef=1.0):
         """NLL = discretized_mix_logistic_loss(x, model(x, h)) summed (nn.py:84-85).  With

@@ -148,7 +148,7 @@ def test_pcnn_wgrad_matches_reference(case):
     sc = torch.empty(1 << 24, device="cuda")
     p = lambda t: ctypes.c_void_p(t.data_ptr())
     db = torch.full((cout,), float("nan"), device="cuda")
-    L.check(L.lib().svae_pcnn_conv_wgrad(p(xd), n, h, h, cin, ldx, xb, p(dd), cout, h, h, cout, kh, kw, 1, pt, pl, mode,
+    L.check(L.lib().svae_pcnn_conv_wgrad(p(xd), n, h, h, cin, ldx, xb, p(dd), cout, 0, h, h, cout, kh, kw, 1, pt, pl, mode,
                                          p(dW), p(db), p(sc), sc.numel(), L.stream_ptr()))
     torch.cuda.synchronize()
     got = dW.cpu().double()

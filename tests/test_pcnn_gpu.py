@@ -224,6 +224,7 @@ def test_fused_activation_backward_is_bitwise(nl):
     seeded dropout on."""
     PC, spec, ospec, params, x, h = _setup(nl, nr_filters=16)
     net = PC.PixelCNNpp(spec, params=params)
+    net.bf16_grads = False  # (the fused epilogue takes the fp32 output gradients)
     res = []
     for fuse in (True, False):
         net.fuse_act_bwd = fuse
@@ -234,3 +235,25 @@ def test_fused_activation_backward_is_bitwise(nl):
         res.append((l, net.G.clone(), dh.clone()))
     assert torch.equal(res[0][0], res[1][0])
     assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
+
+
+def test_bf16_gradient_buffers_match_fp32():
+    """The resnet convs' output gradients stored bf16 (with their bias gradients summed in fp32 by the
+    op that writes them) against fp32 storage: the same forward, the weight / input gradients equal up
+    to fp32 summation order (the convs round dy to bf16 either way), the bias gradients to fp32 order."""
+    PC, spec, ospec, params, x, h = _setup("relu", nr_filters=16)
+    net = PC.PixelCNNpp(spec, params=params)
+    res = []
+    for b in (True, False):
+        net.bf16_grads = b
+        torch.manual_seed(9)
+        l = net.forward_train(x, h, dropout_p=0.3).clone()
+        dh = net.backward_from(torch.ones_like(l).reshape(-1, l.shape[-1]) * 0.01)
+        torch.cuda.synchronize()
+        res.append((l, net.grads(), dh.clone()))
+    assert torch.equal(res[0][0], res[1][0])
+    worst = max(float(np.abs(res[0][1][k] - res[1][1][k]).max() / max(np.abs(res[1][1][k]).max(), 1e-20))
+                for k in res[1][1] if np.abs(res[1][1][k]).max() > 0)
+    edh = float((res[0][2] - res[1][2]).abs().max() / res[1][2].abs().max())
+    print("\nbf16 gradient buffers vs fp32: worst per-tensor rel max err %.2e, dh %.2e" % (worst, edh))
+    assert worst < 1e-4 and edh < 1e-4

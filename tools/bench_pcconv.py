@@ -56,7 +56,7 @@ def main():
             sc = torch.empty(1 << 26, device="cuda")
             fn = lib.svae_pcnn_conv_wgrad
             db = torch.empty(cout, device="cuda")
-            args = (p(x), n_, hi, hi, cin, cin, int(xb), p(dy), cout, ho, ho, cout, kh, kw, 1, pt, pl, mode, p(dW), p(db),
+            args = (p(x), n_, hi, hi, cin, cin, int(xb), p(dy), cout, 0, ho, ho, cout, kh, kw, 1, pt, pl, mode, p(dW), p(db),
                     p(sc), sc.numel(), st)
         else:
             fn = lib.svae_pcnn_conv
