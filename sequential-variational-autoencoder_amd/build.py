@@ -19,6 +19,11 @@ HEADERS = ["common.h", "kernels.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-mcode-object-version=5",
          "-I" + INCLUDE, "-I" + CSRC, "-Wno-unused-result"]
+# A/B builds of compile-time variants: SVAE_CFLAGS="-DSVAE_WT=1" SVAE_BUILD_OUT=ab/wt.so (objects in
+# csrc/build-<name>); the default build ignores both
+EXTRA = os.environ.get("SVAE_CFLAGS", "").split()
+if os.environ.get("SVAE_BUILD_OUT"):
+    OUT = os.path.abspath(os.environ["SVAE_BUILD_OUT"])
 
 
 def _mtime(p):
@@ -26,7 +31,8 @@ def _mtime(p):
 
 
 def build(force=False, verbose=False):
-    bdir = os.path.join(CSRC, "build")
+    bdir = os.path.join(CSRC, "build" if OUT.endswith("libsvae_hip.so") and not EXTRA
+                        else "build-" + os.path.splitext(os.path.basename(OUT))[0])
     os.makedirs(bdir, exist_ok=True)
     hdr_t = max(_mtime(os.path.join(CSRC, h)) for h in HEADERS)
     hdr_t = max(hdr_t, _mtime(os.path.join(INCLUDE, "svae_hip.h")), _mtime(os.path.join(INCLUDE, "svae_pcnn.h")))
@@ -38,7 +44,7 @@ def build(force=False, verbose=False):
         objs.append(op)
         if force or _mtime(op) < max(_mtime(sp), hdr_t):
             lang = ["-x", "hip"] if src.endswith(".hip") else []
-            jobs.append([HIPCC] + FLAGS + lang + ["-c", sp, "-o", op])
+            jobs.append([HIPCC] + FLAGS + EXTRA + lang + ["-c", sp, "-o", op])
 
     def run(cmd):
         if verbose:

@@ -161,9 +161,9 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* pre, int ldp
     for (int e = 0; e < 4; ++e) y[e] = act_f(y[e], act);
     const long long o = group * out_gs + r * ldo + c;
     if (out_bf16)  // read only by bf16 GEMMs, which round it the same way while staging
-      *(bf16x4_bn*)((__bf16*)out + o) = __builtin_convertvector(y, bf16x4_bn);
+      st_out8((__bf16*)out + o, __builtin_bit_cast(u64, __builtin_convertvector(y, bf16x4_bn)));
     else
-      *(f32x4*)(out + o) = y;
+      st_out16(out, o, y);
   }
 }
 
@@ -297,9 +297,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const f32x4 dp = is * (dz - a - xh * b);
     const long long o = group * dpre_gs + r * lddp + c;
     if (dpre_bf16)  // consumed only by bf16 GEMMs, which round it the same way while staging
-      *(bf16x4_bn*)((__bf16*)dpre + o) = __builtin_convertvector(dp, bf16x4_bn);
+      st_out8((__bf16*)dpre + o, __builtin_bit_cast(u64, __builtin_convertvector(dp, bf16x4_bn)));
     else
-      *(f32x4*)(dpre + o) = dp;
+      st_out16(dpre, o, dp);
     if (dres) {
       f32x4* d = (f32x4*)(dres + r * ldres + c);
       *d = res_acc ? *d + dz : dz;

@@ -116,6 +116,37 @@ __device__ __forceinline__ void bw_term_v(float v, float pre, float m, float is,
 // Same-line atomics serialise, so producers spread over nsh (power of 2) shards by row-block
 // (shard = rb & (nsh-1), shard stride sh words); the consumer adds the shards as integers.
 typedef unsigned long long u64;
+
+// Output stores of the main-stream kernels.  SVAE_WT=1 builds store them write-through (sc1): the
+// kernel then leaves no dirty L2 lines for its end-of-kernel release to write back before the next
+// dependent launch may start (MI355X_MICROARCH.md, "boundary": + dirty bytes / 6 TB/s per boundary).
+#ifndef SVAE_WT
+#define SVAE_WT 0
+#endif
+typedef int i32x4_st __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_out(float* p, float v) {
+#if SVAE_WT
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  *p = v;
+#endif
+}
+__device__ __forceinline__ void st_out8(void* p, u64 v) {
+#if SVAE_WT
+  __hip_atomic_store((u64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  *(u64*)p = v;
+#endif
+}
+// 16-byte store at element offset `off` of a wave-uniform base (buffer descriptor from the base)
+__device__ __forceinline__ void st_out16(float* base, long long off, f32x4 v) {
+#if SVAE_WT
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_st, v), r, (int)(off * 4), 0, 16);
+#else
+  *(f32x4*)(base + off) = v;
+#endif
+}
 __device__ __forceinline__ void fx_add(u64* p, float v) {
   const double d = (double)v * 65536.0;  // exact
   const double fl = floor(d);

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <string>
 #include <vector>
@@ -494,6 +495,15 @@ struct svae_ctx {
   hipEvent_t ev_drain = nullptr;  // arena overflow: the side stream drained before reuse
   hipEvent_t ev_da_ready = nullptr, ev_da_free = nullptr, ev_start = nullptr, ev_join = nullptr;
   int ring_pos = 0, iring_pos = 0;
+  // batched hand-over to the side stream (SVAE_SIDE_BATCH = k > 1): weight-gradient work is queued
+  // and enqueued on st2 behind ONE main-stream event per k layers (and at every split-latent
+  // hand-over, which shares that event with st3).  Each event record on the main stream is a
+  // marker packet that drains the queue before the next dispatch (a 4-10 us gap per record).
+  std::vector<std::function<int()>> side_q;
+  int side_batch = 1;
+  static constexpr int NF = 4;
+  hipEvent_t ev_flush[NF] = {};
+  int flush_pos = 0;
   // backward step hook (data-parallel bucketed all-reduce): called on the host after the
   // backward of chain step t is enqueued, with the side stream ordered after all of that step's
   // work on both streams; t = -1 after the whole backward (streams joined)
@@ -749,10 +759,13 @@ struct Slot {
 };
 // next region of `n` elements of a per-pass arena; on overflow (a geometry the plan did not
 // size) the main stream waits for the side stream to drain and the arena starts over
+static int side_flush(svae_ctx* c, hipStream_t also = nullptr);
+static int side_run_queued(svae_ctx* c);
 static float* arena_next(svae_ctx* c, float* base, long long cap, long long& off, long long n,
                          bool st3_reads = false) {
   n = (n + 63) / 64 * 64;
   if (off + n > cap) {
+    side_flush(c);
     hipEvent_t ev = st3_reads ? c->ev_drain3 : c->ev_drain;
     hipEventRecord(ev, st3_reads ? c->st3 : c->st2);
     hipStreamWaitEvent(c->st, ev, 0);
@@ -776,9 +789,61 @@ static Slot idpre_next(svae_ctx* c, long long n) {
 }
 // run fn (weight-gradient launches) on the side stream after everything enqueued so far on the
 // main stream; the side stream uses its own split slab
+// enqueue the queued side-stream work behind one main-stream event; `also` (st3) waits on the
+// same event.  Returns the first error of the queued work.
+static int side_flush(svae_ctx* c, hipStream_t also) {
+  if (!c->side) return 0;
+  if (c->side_q.empty() && !also) return 0;
+  hipEvent_t ev = c->ev_flush[c->flush_pos];
+  c->flush_pos = (c->flush_pos + 1) % svae_ctx::NF;
+  hipEventRecord(ev, c->st);
+  if (also) hipStreamWaitEvent(also, ev, 0);
+  if (c->side_q.empty()) return 0;
+  hipStreamWaitEvent(c->st2, ev, 0);
+  return side_run_queued(c);
+}
+// enqueue the queued work on st2, which the caller has already ordered after the main stream
+static int side_run_queued(svae_ctx* c) {
+  if (c->side_q.empty()) return 0;
+  hipStream_t s0 = c->st;
+  float* sl0 = c->slab;
+  c->st = c->st2;
+  c->slab = c->slab2;
+  int r = 0;
+  for (auto& f : c->side_q) {
+    const int e = f();
+    if (e && !r) r = e;
+  }
+  c->side_q.clear();
+  c->st = s0;
+  c->slab = sl0;
+  return r;
+}
+// queued form of on_side for closures that capture by value (SVAE_SIDE_BATCH > 1); otherwise at once
+template <class Fn>
+static int on_side_q(svae_ctx* c, hipEvent_t ready, Fn&& fn) {
+  if (!c->side || !ready || c->side_batch <= 1) {
+    if (c->side && ready) {
+      hipEventRecord(ready, c->st);
+      hipStreamWaitEvent(c->st2, ready, 0);
+      hipStream_t s0 = c->st;
+      float* sl0 = c->slab;
+      c->st = c->st2;
+      c->slab = c->slab2;
+      const int r = fn();
+      c->st = s0;
+      c->slab = sl0;
+      return r;
+    }
+    return fn();
+  }
+  c->side_q.emplace_back(std::forward<Fn>(fn));
+  return (int)c->side_q.size() >= c->side_batch ? side_flush(c) : 0;
+}
 template <class Fn>
 static int on_side(svae_ctx* c, hipEvent_t ready, hipEvent_t freed, Fn&& fn) {
   if (!c->side || !ready) return fn();
+  if (int r = side_flush(c)) return r;  // queued work first (stream order on st2)
   hipEventRecord(ready, c->st);
   hipStreamWaitEvent(c->st2, ready, 0);
   hipStream_t s0 = c->st;
@@ -1175,10 +1240,11 @@ static int fc_bn_bwd(svae_ctx* c, const FcL& f, View in, View dy, View y, const 
   w.nsplit = 1;
   w.chunk = (B + 31) / 32 * 32;
   w.part = c->Gr + f.ow;  // single split over the batch rows: write dW [nin][nout] directly
-  on_side(c, sl.ready, sl.freed, [&] {
-    wgemm(c, w, 1);
-    return 0;
-  });
+  if ((r = on_side_q(c, sl.ready, [=] {
+         wgemm(c, w, 1);
+         return 0;
+       })))
+    return r;
   if (din.p) {
     FwdArgs a{};
     a.A = sl.p; a.lda = f.nout; a.a_bf16 = c->dbf;
@@ -1197,11 +1263,12 @@ static int fc_bn_bwd(svae_ctx* c, const FcL& f, View in, View dy, View y, const 
 // work on both streams, so a collective issued on it sees that step's complete gradients
 static void adam_range(svae_ctx* c, long long lo, long long hi, float lr, long long step, float clip, hipStream_t s);
 
-static void step_hook(svae_ctx* c, int t) {
-  if ((!c->hook && !c->fa_on) || c->m.shared) return;  // shared tensors are complete only after every step
+static int step_hook(svae_ctx* c, int t) {
+  if ((!c->hook && !c->fa_on) || c->m.shared) return 0;  // shared tensors are complete only after every step
   if (c->side) {
     hipEventRecord(c->ev_hook, c->st);
     hipStreamWaitEvent(c->st2, c->ev_hook, 0);
+    if (int r = side_run_queued(c)) return r;  // the step's queued weight gradients, before its bucket
     hipEventRecord(c->ev_j3, c->st3);  // the step's split-latent gradients
     hipStreamWaitEvent(c->st2, c->ev_j3, 0);
   }
@@ -1209,6 +1276,7 @@ static void step_hook(svae_ctx* c, int t) {
   // the bucket's update follows whatever exchange the hook ordered on the side stream; the
   // backward of steps < t reads neither theta_t nor its shadows
   if (c->fa_on) adam_range(c, c->m.step_lo[t], c->m.step_hi[t], c->fa_lr, c->fa_step, c->fa_clip, c->st2);
+  return 0;
 }
 
 // Recognition ladders of steps [t0, t0+n) (inference_ladder :1579-1630, heads :1592-1609) on
@@ -1447,6 +1515,11 @@ static int engine_forward(svae_ctx* c) {
     return v ? atoi(v) : 1;
   }();
   const bool sfc_side = sfc_mode != 0 && c->side && !g.plc && T <= 64;
+  static const bool pack_first = [] {  // SVAE_PACK_FIRST=1: output operands packed before the st3 hand-over
+    const char* e = getenv("SVAE_PACK_FIRST");
+    return e && e[0] == '1';
+  }();
+  if (pack_first) pack_out_all(c, st);
   if (sfc_side) {
     hipEventRecord(c->ev_aux, st);
     hipStreamWaitEvent(c->st3, c->ev_aux, 0);
@@ -1456,7 +1529,7 @@ static int engine_forward(svae_ctx* c) {
     }
   }
 
-  pack_out_all(c, st);
+  if (!pack_first) pack_out_all(c, st);
 
   // ---------------- the chain ----------------
   for (int t = 0; t < T; ++t) {
@@ -1611,9 +1684,13 @@ static int inference_bwd(svae_ctx* c, int t0, int n, View in0, float* dx0) {
                    bns(c->inf_bn_b[lvl], Fl), Fl, I0.b[lvl].obeta, wg, ACT_LRELU, sb.p, gs, View{}, 0, &fu_ib,
                    dpre_bf(c, I0.b[lvl]));
     if (r) return r;
-    r = on_side(c, sb.ready, sb.freed, [&] {
-      return conv_wgrad(c, I0.b[lvl], n, wg, View{act_a(lvl), Fl, gs, c->abf}, sb.p, gs, c->Gr + I0.b[lvl].ow);
-    });
+    {
+      const ConvL Lw = I0.b[lvl];
+      const View in_{act_a(lvl), Fl, gs, c->abf};
+      const float* dp = sb.p;
+      float* dW = c->Gr + Lw.ow;
+      r = on_side_q(c, sb.ready, [=] { return conv_wgrad(c, Lw, n, wg, in_, dp, gs, dW); });
+    }
     if (r) return r;
     BwFuse fu_ia = bw_fuse(c, pre_a(lvl), Fl, gs, nullptr, 0, 0, bns(c->inf_bn_a[lvl], Fl), Fl, I0.a[lvl].obeta, wg,
                            ACT_LRELU, Fl);
@@ -1625,7 +1702,12 @@ static int inference_bwd(svae_ctx* c, int t0, int n, View in0, float* dx0) {
                    dpre_bf(c, I0.a[lvl]));
     if (r) return r;
     View in = lvl == 0 ? in0 : View{act_b(lvl - 1), F[lvl], c->inf_gs[lvl - 1]};
-    r = on_side(c, sa.ready, sa.freed, [&] { return conv_wgrad(c, I0.a[lvl], n, wg, in, sa.p, gs, c->Gr + I0.a[lvl].ow); });
+    {
+      const ConvL Lw = I0.a[lvl];
+      const float* dp = sa.p;
+      float* dW = c->Gr + Lw.ow;
+      r = on_side_q(c, sa.ready, [=] { return conv_wgrad(c, Lw, n, wg, in, dp, gs, dW); });
+    }
     if (r) return r;
     if (lvl > 0) {
       const bool wrote = heads_of(lvl - 1);
@@ -1641,7 +1723,15 @@ static int inference_bwd(svae_ctx* c, int t0, int n, View in0, float* dx0) {
   return 0;
 }
 
+static int engine_backward_pass(svae_ctx* c);
+// the pass, then whatever side-stream work is still queued (early debug returns, errors)
 static int engine_backward(svae_ctx* c) {
+  const int r = engine_backward_pass(c);
+  const int r2 = side_flush(c);
+  c->side_q.clear();
+  return r ? r : r2;
+}
+static int engine_backward_pass(svae_ctx* c) {
   Model& M = c->m;
   const Geo& g = M.g;
   const int B = g.B, L = g.L, T = g.T;
@@ -1680,7 +1770,7 @@ static int engine_backward(svae_ctx* c) {
         r = inference_bwd(c, t + 1, 1, View{(float*)chain_x(c, t), g.C, 0}, c->dx[t & 1]);
         if (r) return r;
       }
-      step_hook(c, t + 1);  // step t+1's gradients are complete
+      if ((r = step_hook(c, t + 1))) return r;  // step t+1's gradients are complete
     }
     if (t < c->dbg_stop_step) return 0;  // debug: stop after step dbg_stop_step
     svae_ctx::StepBufs& s = c->sb[t];
@@ -1736,18 +1826,22 @@ static int engine_backward(svae_ctx* c) {
       else
         choose_split(w.rows, 16, (F[1] + 127) / 128, 1, 16LL * M_out * F[1], c->slab_cap, w.nsplit, w.chunk);
       w.nsp = g.split ? 2 : 1;
-      on_side(c, c->ev_da_ready, nullptr, [&] {
+      float* da = c->da;
+      const int F1 = F[1], Cc = g.C;
+      float* gout = c->Gr + G.owout;
+      float* gratio = t >= 1 ? c->Gr + G.owratio : nullptr;
+      float* gbout = c->Gr + G.obout;
+      float* gbratio = t >= 1 ? c->Gr + G.obratio : nullptr;
+      if ((r = on_side_q(c, c->ev_da_ready, [=]() mutable {
         w.part = c->slab;
         const int ns = (bfk || g.split) ? wgrad_smallc_part(w, 1, c->slab, c->slab_cap, c->st) : 0;
         if (ns) w.nsplit = ns;  // LDS im2col kernel (wgrad_smallc.hip)
         else wgemm(c, w, 1);
-        wgrad_reduce(c->slab, 0, w.nsplit, 16, M_out, F[1], c->Gr + G.owout, 0, g.C,
-                     t >= 1 ? c->Gr + G.owratio : nullptr, 0, 0, 1, c->st);
+        wgrad_reduce(c->slab, 0, w.nsplit, 16, M_out, F1, gout, 0, Cc, gratio, 0, 0, 1, c->st);
         // output / ratio bias gradients (own scratch)
-        colsum_small(c->da, C1, P0, M_out, c->cs_part, c->Gr + G.obout, g.C, t >= 1 ? c->Gr + G.obratio : nullptr,
-                     c->st);
+        colsum_small(da, C1, P0, M_out, c->cs_part, gbout, Cc, gbratio, c->st);
         return 0;
-      });
+      }))) return r;
       // d cur = conv-T dgrad (CONV gather over da with the packed [tap][C+1][F1] weights as KN)
       FwdArgs a{};
       a.A = c->da; a.lda = C1;
@@ -1773,8 +1867,13 @@ static int engine_backward(svae_ctx* c) {
                      0, l1.obeta, 0, ACT_RELU, sl.p, 0, View{}, 0, &fu_s1, dpre_bf(c, l1));
       if (r) return r;
       if (t == c->dbg_stop_step && lvl == c->dbg_stop_lvl2) { c->dbg_last = dcur; return 0; }
-      r = on_side(c, sl.ready, sl.freed,
-                  [&] { return conv_wgrad(c, l1, 1, 0, View{s.cat[lvl], 2 * Fl, 0}, sl.p, 0, c->Gr + l1.ow); });
+      {
+        const ConvL Lw = l1;
+        const View in_{s.cat[lvl], 2 * Fl, 0};
+        const float* dp = sl.p;
+        float* dW = c->Gr + Lw.ow;
+        r = on_side_q(c, sl.ready, [=] { return conv_wgrad(c, Lw, 1, 0, in_, dp, 0, dW); });
+      }
       if (r) return r;
       // s2[lvl]'s BN partials over the d-half of dcat (shortcut at t >= 1: act' from the stored y)
       BwFuse fu_s2 = bw_fuse(c, s.s2_pre[lvl], Fl, 0, t >= 1 ? s.cat[lvl] : nullptr, 2 * Fl, 0, s.s2_bn[lvl], 0,
@@ -1790,8 +1889,7 @@ static int engine_backward(svae_ctx* c) {
         for (int i = 0; i < lvl; ++i) zoff += g.D[i];
         hipStream_t ss = st;
         if (c->side) {
-          hipEventRecord(c->ev_aux, st);
-          hipStreamWaitEvent(c->st3, c->ev_aux, 0);
+          if ((r = side_flush(c, c->st3))) return r;  // one event for st3 and the queued st2 work
           ss = c->st3;
         }
         splitfc_bwd(c->z + (long long)t * B * g.Dz, g.Dz, zoff, B, g.D[lvl], c->P + f.ow, c->P + f.obeta, f.nout,
@@ -1806,7 +1904,12 @@ static int engine_backward(svae_ctx* c) {
                      s.s2_bn[lvl], 0, l2.obeta, 0, ACT_RELU, sl.p, 0, dres, 0, &fu_s2, dpre_bf(c, l2));
       if (r) return r;
       View in = lvl == L - 2 ? View{s.top_act, F[L], 0, c->abf} : View{s.s1_act[lvl + 1], F[lvl + 2], 0, c->abf};
-      r = on_side(c, sl.ready, sl.freed, [&] { return conv_wgrad(c, l2, 1, 0, in, sl.p, 0, c->Gr + l2.ow); });
+      {
+        const ConvL Lw = l2;
+        const float* dp = sl.p;
+        float* dW = c->Gr + Lw.ow;
+        r = on_side_q(c, sl.ready, [=] { return conv_wgrad(c, Lw, 1, 0, in, dp, 0, dW); });
+      }
       if (r) return r;
       if (lvl < L - 2) {  // next: s1[lvl+1] (no shortcut)
         fu_s1 = bw_fuse(c, s.s1_pre[lvl + 1], F[lvl + 2], 0, nullptr, 0, 0, s.s1_bn[lvl + 1], 0, G.s1[lvl + 1].obeta, 0,
@@ -1832,8 +1935,7 @@ static int engine_backward(svae_ctx* c) {
       const int coff = t >= 1 ? F[L] : 0;
       hipStream_t ss = st;
       if (c->side) {
-        hipEventRecord(c->ev_aux, st);
-        hipStreamWaitEvent(c->st3, c->ev_aux, 0);
+        if ((r = side_flush(c, c->st3))) return r;
         ss = c->st3;
       }
       splitfc_bwd(c->z + (long long)t * B * g.Dz, g.Dz, g.Dz - g.D[L - 1], B, g.D[L - 1], c->P + f.ow, c->P + f.obeta,
@@ -1855,9 +1957,13 @@ static int engine_backward(svae_ctx* c) {
                      F[L - 1], s.enc_bn_c, 0, E.c.obeta, 0, ACT_LRELU, sl.p, 0, View{}, 0, nullptr,
                      dpre_bf(c, E.c));
       if (r) return r;
-      r = on_side(c, sl.ready, sl.freed, [&] {
-        return conv_wgrad(c, E.c, 1, 0, View{s.enc_act_b[L - 2], F[L - 1], 0}, sl.p, 0, c->Gr + E.c.ow);
-      });
+      {
+        const ConvL Lw = E.c;
+        const View in_{s.enc_act_b[L - 2], F[L - 1], 0};
+        const float* dp = sl.p;
+        float* dW = c->Gr + Lw.ow;
+        r = on_side_q(c, sl.ready, [=] { return conv_wgrad(c, Lw, 1, 0, in_, dp, 0, dW); });
+      }
       if (r) return r;
       // E.c's input gradient accumulates last into denc[L-2] (after the decoder shortcut term)
       BwFuse fu_eb = bw_fuse(c, s.enc_pre_b[L - 2], F[L - 1], 0, nullptr, 0, 0, s.enc_bn_b[L - 2], 0, E.b[L - 2].obeta,
@@ -1872,9 +1978,13 @@ static int engine_backward(svae_ctx* c) {
                        Fl, s.enc_bn_b[lvl], 0, E.b[lvl].obeta, 0, ACT_LRELU, sb.p, 0, View{}, 0, &fu_eb,
                        dpre_bf(c, E.b[lvl]));
         if (r) return r;
-        r = on_side(c, sb.ready, sb.freed, [&] {
-          return conv_wgrad(c, E.b[lvl], 1, 0, View{s.enc_act_a[lvl], Fl, 0, c->abf}, sb.p, 0, c->Gr + E.b[lvl].ow);
-        });
+        {
+          const ConvL Lw = E.b[lvl];
+          const View in_{s.enc_act_a[lvl], Fl, 0, c->abf};
+          const float* dp = sb.p;
+          float* dW = c->Gr + Lw.ow;
+          r = on_side_q(c, sb.ready, [=] { return conv_wgrad(c, Lw, 1, 0, in_, dp, 0, dW); });
+        }
         if (r) return r;
         BwFuse fu_ea = bw_fuse(c, s.enc_pre_a[lvl], Fl, 0, nullptr, 0, 0, s.enc_bn_a[lvl], 0, E.a[lvl].obeta, 0,
                                ACT_LRELU, Fl);
@@ -1886,7 +1996,12 @@ static int engine_backward(svae_ctx* c) {
                        dpre_bf(c, E.a[lvl]));
         if (r) return r;
         View in = lvl == 0 ? View{(float*)xprev, g.C, 0} : View{s.enc_act_b[lvl - 1], F[lvl], 0};
-        r = on_side(c, sa.ready, sa.freed, [&] { return conv_wgrad(c, E.a[lvl], 1, 0, in, sa.p, 0, c->Gr + E.a[lvl].ow); });
+        {
+          const ConvL Lw = E.a[lvl];
+          const float* dp = sa.p;
+          float* dW = c->Gr + Lw.ow;
+          r = on_side_q(c, sa.ready, [=] { return conv_wgrad(c, Lw, 1, 0, in, dp, 0, dW); });
+        }
         if (r) return r;
         View din = lvl == 0 ? View{dxout, g.C, 0} : View{c->denc[lvl - 1], F[lvl], 0};
         if (lvl > 0) {  // accumulates last into denc[lvl-1]: E.b[lvl-1]'s BN partials
@@ -1903,6 +2018,7 @@ static int engine_backward(svae_ctx* c) {
     // earlier steps: q(z_t | x) needs only dz_t (inference_bwd waits on ev_dz), its weight gradients
     // go to the side stream like every other; own split slab
     if (rec_ov && t % c->rec_group == 0) {
+      if ((r = side_flush(c))) return r;
       hipStream_t s0 = c->st;
       float* sl0 = c->slab;
       c->st = c->st4;
@@ -1914,7 +2030,7 @@ static int engine_backward(svae_ctx* c) {
     }
   }
 
-  step_hook(c, 0);
+  if ((r = step_hook(c, 0))) return r;
 
   // ---------------- recognition ladders: all steps batched, or step 0 (Latent InfoMax) ----------------
   if (rec_ov) {  // joined: every recognition group was enqueued on st4 during the chain backward
@@ -1923,6 +2039,7 @@ static int engine_backward(svae_ctx* c) {
   } else if ((r = inference_bwd(c, 0, g.plc ? 1 : T, View{(float*)c->x_in, g.C, 0}, nullptr))) {
     return r;
   }
+  if ((r = side_flush(c))) return r;
   if (M.shared) {  // public gradient = fixed-order sum of the step copies (side stream joined first)
     if (c->side) {
       hipEventRecord(c->ev_join, c->st2);
@@ -2308,6 +2425,11 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
       mk(&c->ev_aux); mk(&c->ev_aux2); mk(&c->ev_dz); mk(&c->ev_j3); mk(&c->ev_j4);
       mk(&c->ev_drain3);
       for (int i = 0; i < 64; ++i) mk(&c->ev_sfc[i]);
+      for (int i = 0; i < svae_ctx::NF; ++i) mk(&c->ev_flush[i]);
+      {  // SVAE_SIDE_BATCH (read per context): weight-gradient layers per side-stream hand-over
+        const char* e = getenv("SVAE_SIDE_BATCH");
+        c->side_batch = e ? std::max(1, atoi(e)) : 1;
+      }
       c->side = ok;
     }
   }
@@ -2327,6 +2449,8 @@ int svae_destroy(svae_ctx* c) {
                         c->ev_drain3})
     if (ev) hipEventDestroy(ev);
   for (hipEvent_t ev : c->ev_sfc)
+    if (ev) hipEventDestroy(ev);
+  for (hipEvent_t ev : c->ev_flush)
     if (ev) hipEventDestroy(ev);
   for (int i = 0; i < svae_ctx::NR; ++i) {
     if (c->ev_ready[i]) hipEventDestroy(c->ev_ready[i]);

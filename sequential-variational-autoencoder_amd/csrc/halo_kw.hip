@@ -26,6 +26,9 @@ typedef float f32x8 __attribute__((ext_vector_type(8)));
 #define KW_CK 32   // channels per window stage
 #define KW_ROWP 40 // LDS pixel pitch in bf16 (80 B: conflict-free 16-B fragment reads)
 #define KW_PI 4    // window items (8 channels) per thread: npix * 4 <= 256 * KW_PI
+#ifndef KW_OCC
+#define KW_OCC 4   // waves per SIMD of the bf16-A 32-column instances (5 spills 38 VGPRs)
+#endif
 
 struct KwArgs {
   FwdArgs f;
@@ -59,7 +62,7 @@ __device__ __forceinline__ long long kw_out_row(const KwArgs& h, const ConvGeom&
 // A x B fragment pair runs the six plane products; B comes from the three shadow planes
 // PST: the persistent form (h.tpb > 1 tiles per block, 1-D grid); without it the tile loop runs once
 template <int BM, int BN, bool S2T, bool ABF, int NS = 1, bool PST = false>
-__global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64 && !PST) ? 4 : 2) void igemm_halo_kw_kernel(KwArgs h) {
+__global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64 && !PST) ? KW_OCC : 2) void igemm_halo_kw_kernel(KwArgs h) {
   static_assert(NS == 1 || (NS == 3 && !ABF), "split planes from fp32 activations only");
   constexpr int TM = BM / 32;
   constexpr int TN = BN / 32;
@@ -332,7 +335,7 @@ __global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64 && !PST) ? 4 : 2)
       if (bias) v += biasv;
       v = act_f(v, a.act);
       if (a.accumulate) v += cv[i];
-      Cp[orow[i] * a.ldc + n] = v;
+      st_out(&Cp[orow[i] * a.ldc + n], v);
       if (bwc) bw_term_v(v, pv[i], bm, bi, bb, bwy != nullptr, yv[i], a.bw.act, s1, s2);
     }
     if (a.stats) {

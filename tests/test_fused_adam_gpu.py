@@ -77,3 +77,25 @@ def test_rebind_after_external_write_rebuilds_weight_copies():
     assert a.loss_value() == b.loss_value()
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("preset,dtype,over", [
+    ("tiny", "bf16", {}),
+    ("celeba", "bf16", {}),
+    ("tiny", "bf16x6", {}),
+    ("tiny_homog", "bf16", {}),
+])
+@pytest.mark.parametrize("fused", [False, True])
+def test_batched_side_handover_is_bitwise(preset, dtype, over, fused, monkeypatch):
+    """SVAE_SIDE_BATCH = k queues the weight-gradient work of k layers behind one main-stream
+    event (engine.cpp on_side_q / side_flush): the same kernels on the same data, so losses and
+    parameters after three steps equal the per-layer hand-over bit for bit (the per-bucket Adam
+    of the fused path must still follow every weight gradient of its bucket)."""
+    monkeypatch.setenv("SVAE_SIDE_BATCH", "1")
+    p0, l0, _ = _run(preset, dtype, fused, over)
+    for k in ("3", "100"):
+        monkeypatch.setenv("SVAE_SIDE_BATCH", k)
+        p1, l1, changed = _run(preset, dtype, fused, over)
+        assert changed > 0
+        assert l0 == l1, (k, l0, l1)
+        np.testing.assert_array_equal(p0, p1)

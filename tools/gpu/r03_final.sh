@@ -26,3 +26,10 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o 
 python3 tools/prof_summary.py gpurun_out/${TAG}_prof/run_results.db > gpurun_out/${TAG}_kernel_stats.txt 2>&1 || true
 python3 tools/stream_breakdown.py gpurun_out/${TAG}_prof/run_results.db 28 20 8 > gpurun_out/${TAG}_streams.txt 2>&1 || true
 head -8 gpurun_out/${TAG}_streams.txt
+# LSUN-bedroom (BASELINE configs[2], B=256) and the parity mode's kernel stats
+timeout -k 10 300 python bench.py --config lsun --steps 10 --warmup 3 --no-cpu-baseline --no-fp32 > gpurun_out/${TAG}_lsun_bench.json.log 2>&1 || { tail -20 gpurun_out/${TAG}_lsun_bench.json.log; exit 1; }
+tail -1 gpurun_out/${TAG}_lsun_bench.json.log > gpurun_out/${TAG}_lsun_bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof6 -o run -- python3 bench.py --dtype bf16x6 --steps 6 --warmup 2 --no-cpu-baseline --no-fp32 > gpurun_out/${TAG}_prof6.log 2>&1 || exit 1
+python3 tools/prof_summary.py gpurun_out/${TAG}_prof6/run_results.db > gpurun_out/${TAG}_bf16x6_kernel_stats.txt 2>&1 || true
+python3 tools/stream_breakdown.py gpurun_out/${TAG}_prof6/run_results.db 28 6 4 > gpurun_out/${TAG}_bf16x6_streams.txt 2>&1 || true
+rm -rf gpurun_out/${TAG}_prof6
