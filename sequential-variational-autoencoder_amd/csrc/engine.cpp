@@ -1515,9 +1515,11 @@ static int engine_forward(svae_ctx* c) {
     return v ? atoi(v) : 1;
   }();
   const bool sfc_side = sfc_mode != 0 && c->side && !g.plc && T <= 64;
-  static const bool pack_first = [] {  // SVAE_PACK_FIRST=1: output operands packed before the st3 hand-over
+  // output / ratio operands packed before the split-latent hand-over to st3 (+0.5 % per step in a
+  // same-box A/B, profiles/r03_ab3.txt); SVAE_PACK_FIRST=0 packs after it (round 2's order)
+  static const bool pack_first = [] {
     const char* e = getenv("SVAE_PACK_FIRST");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   if (pack_first) pack_out_all(c, st);
   if (sfc_side) {
