@@ -482,6 +482,10 @@ struct svae_ctx {
   hipEvent_t ev_j4 = nullptr;
   float* slab4 = nullptr;
   int rec_group = 0;
+  // forward recognition split (SVAE_REC_SPLIT=1): step 0's ladder on the main stream, the batched
+  // ladders of steps 1..T-1 on st4 (own split slab), overlapping the chain's step 0
+  int rec_split = 0;
+  hipEvent_t ev_rs = nullptr, ev_rs2 = nullptr;
   float* slab2 = nullptr;
   // BN-backward outputs read by the side stream's weight GEMMs: every one of a backward pass gets
   // its own region of these arenas (bump-allocated, reset per pass), so the main stream never
@@ -1110,6 +1114,13 @@ static BwFuse bw_fuse(svae_ctx* c, const float* pre, int ldp, long long pre_gs, 
   return f;
 }
 
+static bool nofuse_out() {  // SVAE_NO_BWFUSE_OUT=1: s1[0]'s BN-backward sums in their own pass (A/B)
+  static const bool v = [] {
+    const char* e = getenv("SVAE_NO_BWFUSE_OUT");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
 static int conv_dgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, const float* dpre, long long dpre_gs,
                       View din, int accumulate, BwFuse* fu = nullptr) {
   if (fu) fu->used = false;
@@ -1279,6 +1290,15 @@ static int step_hook(svae_ctx* c, int t) {
   return 0;
 }
 
+// `off` elements into a tensor stored as fp32 or (bf) bf16, as a float* view base.  A group stride
+// of a bf16 tensor counts bf16 elements (the producing kernels index it so), so step t0's group of
+// the T-batched recognition activations starts t0 * gs bf16 elements in; float* arithmetic would
+// put it twice as far, which only the same call's own reads agree with (found by a split forward /
+// batched backward mismatch, tools/gpu/r03_recdiag.py)
+static float* elem_off(float* base, long long off, int bf) {
+  return bf ? (float*)((__bf16*)base + off) : base + off;
+}
+
 // Recognition ladders of steps [t0, t0+n) (inference_ladder :1579-1630, heads :1592-1609) on
 // input `in` (group stride in.gs), then mu / sigma / z / KL (:1022-1024, :1156-1158).
 static int inference_fwd(svae_ctx* c, int t0, int n, View in0) {
@@ -1297,10 +1317,11 @@ static int inference_fwd(svae_ctx* c, int t0, int n, View in0) {
     const long long gs = c->inf_gs[lvl];
     const int Fl = F[lvl + 1];
     View in = lvl == 0 ? in0 : View{c->inf_act_b[lvl - 1] + t0 * c->inf_gs[lvl - 1], F[lvl], c->inf_gs[lvl - 1]};
+    float* act_a = elem_off(c->inf_act_a[lvl], t0 * gs, c->abf);  // bf16 storage: step t0's group in bf16 elements
     r = conv_bn_act_fwd(c, I.a[lvl], n, wg, in, c->inf_pre_a[lvl] + t0 * gs, gs, bns(c->inf_bn_a[lvl], Fl), Fl, View{},
-                        ACT_LRELU, View{c->inf_act_a[lvl] + t0 * gs, Fl, gs, c->abf});
+                        ACT_LRELU, View{act_a, Fl, gs, c->abf});
     if (r) return r;
-    r = conv_bn_act_fwd(c, I.b[lvl], n, wg, View{c->inf_act_a[lvl] + t0 * gs, Fl, gs, c->abf}, c->inf_pre_b[lvl] + t0 * gs, gs,
+    r = conv_bn_act_fwd(c, I.b[lvl], n, wg, View{act_a, Fl, gs, c->abf}, c->inf_pre_b[lvl] + t0 * gs, gs,
                         bns(c->inf_bn_b[lvl], Fl), Fl, View{}, ACT_LRELU, View{c->inf_act_b[lvl] + t0 * gs, Fl, gs});
     if (r) return r;
     for (int hl = 0; hl < L; ++hl) {
@@ -1506,8 +1527,24 @@ static int engine_forward(svae_ctx* c) {
   c->eps_used = eps;
   // recognition: q(z_t | x) for every step at once (groups = T), or, in Latent InfoMax mode,
   // q(z_0 | x) here and q(z_t | x_{t-1}) inside the chain (create_recognition_network :1013-1027)
-  if ((r = inference_fwd(c, 0, g.plc ? 1 : T, View{(float*)c->x_in, g.C, 0}))) return r;
+  if (c->rec_split && c->st4 && !g.plc && T > 1) {
+    if ((r = inference_fwd(c, 0, 1, View{(float*)c->x_in, g.C, 0}))) return r;
+    hipEventRecord(c->ev_rs, st);
+    hipStreamWaitEvent(c->st4, c->ev_rs, 0);
+    hipStream_t s0 = c->st;
+    float* sl0 = c->slab;
+    c->st = c->st4;
+    c->slab = c->slab4;
+    r = inference_fwd(c, 1, T - 1, View{(float*)c->x_in, g.C, 0});
+    c->st = s0;
+    c->slab = sl0;
+    if (r) return r;
+    hipEventRecord(c->ev_rs2, c->st4);
+  } else if ((r = inference_fwd(c, 0, g.plc ? 1 : T, View{(float*)c->x_in, g.C, 0}))) {
+    return r;
+  }
   }  // !generative
+  const bool rsplit = c->rec_split && c->st4 && !g.plc && T > 1 && !c->generative;
   // split_latent of every step on the side stream (z is known for all steps unless Latent
   // InfoMax draws z_t inside the chain); step t's decoder waits on ev_sfc[t]
   static const int sfc_mode = [] {  // SVAE_SFC: 0 = split-latent forward on the main stream per step
@@ -1526,6 +1563,7 @@ static int engine_forward(svae_ctx* c) {
     hipEventRecord(c->ev_aux, st);
     hipStreamWaitEvent(c->st3, c->ev_aux, 0);
     for (int t = 0; t < g.Te; ++t) {
+      if (t == 1 && rsplit) hipStreamWaitEvent(c->st3, c->ev_rs2, 0);  // z_t of steps >= 1 (st4)
       split_latent_fwd(c, t, c->st3);
       hipEventRecord(c->ev_sfc[t], c->st3);
     }
@@ -1536,6 +1574,7 @@ static int engine_forward(svae_ctx* c) {
   // ---------------- the chain ----------------
   for (int t = 0; t < T; ++t) {
     svae_ctx::StepBufs& s = c->sb[t];
+    if (t == 1 && rsplit) hipStreamWaitEvent(st, c->ev_rs2, 0);  // recognition of steps >= 1 (st4)
     if (t >= g.Te) {  // external generator step: only its KL statistics here (recon 0: the caller's)
       HIPCHK(c, hipMemsetAsync(s.rec_part, 0, (size_t)B * c->out_nblk * sizeof(float), st));
       loss_reduce(s.rec_part, c->out_nblk, c->kl_img + (long long)t * B, B, g.H * g.W * g.C, s.stats, s.rec_img, st);
@@ -1657,7 +1696,7 @@ static int inference_bwd(svae_ctx* c, int t0, int n, View in0, float* dx0) {
              (long long)B * 2 * g.Dz, n, st);
   const InfStep& I0 = M.inf[t0];
   auto bns = [&](const BNS& b, int C) { return BNS{b.mean + (long long)t0 * C, b.invstd + (long long)t0 * C}; };
-  auto act_a = [&](int l) { return c->inf_act_a[l] + t0 * c->inf_gs[l]; };
+  auto act_a = [&](int l) { return elem_off(c->inf_act_a[l], t0 * c->inf_gs[l], c->abf); };
   auto act_b = [&](int l) { return c->inf_act_b[l] + t0 * c->inf_gs[l]; };
   auto pre_a = [&](int l) { return c->inf_pre_a[l] + t0 * c->inf_gs[l]; };
   auto pre_b = [&](int l) { return c->inf_pre_b[l] + t0 * c->inf_gs[l]; };
@@ -1794,6 +1833,7 @@ static int engine_backward_pass(svae_ctx* c) {
       }
     }
     float* dzt = c->dz + (long long)t * B * g.Dz;
+    BwFuse fu_s1;  // s1[lvl]'s BN partials: from the output layer's (lvl 0) / s2[lvl-1]'s input-gradient epilogue
 
     // ---- output + highway (:1720-1729)
     c->da = c->da_base + (long long)t * P0 * C1;  // own region per step: no wait for the previous reader
@@ -1852,12 +1892,28 @@ static int engine_backward_pass(svae_ctx* c) {
       a.N = F[1]; a.Cin = C1;
       a.g = ConvGeom{GM_CONV, B, g.H, g.W, S[1], S[1], 2, 1, 4};
       a.rows = B * S[1] * S[1]; a.nclass = 1;
+      // s1[0]'s BN-backward partials in this input gradient's epilogue (small-channel kernel only)
+      fu_s1 = BwFuse{};
+      if (!nofuse_out()) {
+        BwFuse f = bw_fuse(c, s.s1_pre[0], F[1], 0, nullptr, 0, 0, s.s1_bn[0], 0, G.s1[0].obeta, 0, ACT_RELU, F[1]);
+        FwdArgs t = a;
+        t.bw = f.bw;
+        t.stats = (u64*)1;  // (eligibility only)
+        if (f.bw.C % 4 == 0 && smallc_ok(t, false)) {
+          const AccR acc = acc_bn(c, 1, F[1], smallc_nrb(t));
+          if (!acc.p) return fail(c, SVAE_EBADARG, "BN accumulator arena too small");
+          a.bw = f.bw;
+          set_stats(a, acc);
+          f.acc = acc;
+          f.used = true;
+          fu_s1 = f;
+        }
+      }
       igemm_fwd(a, 1, st);
     }
     // ---- decoder levels, bottom-up (reverse of :1710-1717)
     float* dcur = c->dcur;
     float* dnext = c->dnext;
-    BwFuse fu_s1;  // s1[lvl]'s BN partials from the s2[lvl-1] input-gradient epilogue
     for (int lvl = 0; lvl <= L - 2; ++lvl) {
       const int Fl = F[lvl + 1];
       const long long rows = (long long)B * S[lvl + 1] * S[lvl + 1];
@@ -2087,7 +2143,7 @@ static bool plan(svae_ctx* c) {
   }
   int maxnin = 0;
   for (int l = 0; l < L; ++l) maxnin = std::max(maxnin, c->m.inf[0].head[l].nin);
-  c->head_nsplit = heads_splits(maxnin);
+  c->head_nsplit = heads_splits(maxnin);  // latent_fwd_kernel sums up to 32 head partials per dimension
   c->head_part = A((long long)T * c->head_nsplit * B * 2 * g.Dz);
   c->mu = A((long long)T * B * g.Dz);
   c->sig = A((long long)T * B * g.Dz);
@@ -2221,7 +2277,7 @@ static bool plan(svae_ctx* c) {
   c->slab_cap = 64LL << 20;
   c->slab = A(c->slab_cap);
   c->slab2 = A(c->slab_cap);
-  if (c->rec_group > 0) c->slab4 = A(c->slab_cap);
+  if (c->rec_group > 0 || c->rec_split) c->slab4 = A(c->slab_cap);
   c->cs_part = A(64 * 1024);
   c->zero_img = A((long long)B * g.H * g.W * g.C);
   return true;
@@ -2283,6 +2339,8 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
     const char* rg = getenv("SVAE_REC_GROUP");  // recognition-backward group size (0 = batched after the chain)
     c->rec_group = rg ? atoi(rg) : 0;
     if (c->rec_group < 0 || c->m.g.plc) c->rec_group = 0;
+    const char* rs = getenv("SVAE_REC_SPLIT");  // forward recognition of steps >= 1 on st4
+    c->rec_split = (rs && rs[0] == '1' && !c->m.g.plc && c->m.g.T > 1) ? 1 : 0;
   }
   {
     const char* v = getenv("SVAE_DPRE_F32");  // A/B: keep the BN-backward outputs in fp32
@@ -2293,6 +2351,10 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
   c->counting = true;
   c->arena_used = 0;
   plan(c);
+  if (c->head_nsplit > 32 || c->m.g.Dz > 256) {  // latent_fwd_kernel's limits
+    delete c;
+    return fail(nullptr, SVAE_EBADCONFIG, "recognition head input over 65536 features or latent over 256");
+  }
   c->arena_bytes = c->arena_used;
   c->counting = false;
   c->arena_used = 0;
@@ -2409,7 +2471,8 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
     if (!(ns && ns[0] == '1')) {
       bool ok = hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking) == hipSuccess;
       ok = ok && hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking) == hipSuccess;
-      if (c->rec_group > 0) ok = ok && hipStreamCreateWithFlags(&c->st4, hipStreamNonBlocking) == hipSuccess;
+      if (c->rec_group > 0 || c->rec_split)
+        ok = ok && hipStreamCreateWithFlags(&c->st4, hipStreamNonBlocking) == hipSuccess;
       // cross-stream ordering on this device only: no system-scope fence (a system-scope release
       // writes the L2s back for host / peer visibility, a GPU-side bubble at every record); the
       // gradient-hook event, which orders a collective's peer traffic, keeps it
@@ -2428,6 +2491,8 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
       mk(&c->ev_drain3);
       for (int i = 0; i < 64; ++i) mk(&c->ev_sfc[i]);
       for (int i = 0; i < svae_ctx::NF; ++i) mk(&c->ev_flush[i]);
+      mk(&c->ev_rs);
+      mk(&c->ev_rs2);
       {  // SVAE_SIDE_BATCH (read per context): weight-gradient layers per side-stream hand-over
         const char* e = getenv("SVAE_SIDE_BATCH");
         c->side_batch = e ? std::max(1, atoi(e)) : 1;
@@ -2453,6 +2518,8 @@ int svae_destroy(svae_ctx* c) {
   for (hipEvent_t ev : c->ev_sfc)
     if (ev) hipEventDestroy(ev);
   for (hipEvent_t ev : c->ev_flush)
+    if (ev) hipEventDestroy(ev);
+  for (hipEvent_t ev : {c->ev_rs, c->ev_rs2})
     if (ev) hipEventDestroy(ev);
   for (int i = 0; i < svae_ctx::NR; ++i) {
     if (c->ev_ready[i]) hipEventDestroy(c->ev_ready[i]);

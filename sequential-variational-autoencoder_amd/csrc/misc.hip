@@ -2,6 +2,7 @@
 // reparameterised latent + KL, small-N conv (output / layer-0 dgrad), output +
 // highway + reconstruction loss, loss reduction, clip+Adam, Philox normals.
 #include <algorithm>
+#include <cstdint>
 
 #include "common.h"
 #include "kernels.h"
@@ -205,7 +206,7 @@ void splitfc_bwd(const float* z, int ldz, int zoff, int B, int K, const float* W
 // (recognition heads K=32768 -> D=3, and dz = dpre @ W^T of split_latent)
 // ---------------------------------------------------------------------------
 #define SK_ROWS 4
-#define SK_CHUNK 4096
+#define SK_CHUNK 2048  // = HF_CHUNK: both fill heads_splits(K) partial rows
 
 template <int DM>
 // D outputs from W, and (W2 != nullptr) D more from W2 into columns coff2.. of part: the mean and
@@ -278,11 +279,99 @@ static void skinny(const float* X, int ldx, long long x_gs, int B, int K, const 
   }
 }
 
-int heads_splits(int K) { return (K + SK_CHUNK - 1) / SK_CHUNK; }
+// Narrow heads (D <= 4, the CelebA latents): both heads over 8 rows and a 2048-wide K chunk per block.
+// Each thread takes 4 consecutive k per step as one 16-byte X load per row and the matching 4*D
+// contiguous weights of each head as D 16-byte loads (reused by the block's 8 rows: W is read B/8
+// times, not B/4), then the per-thread sums go through the wave and the block in a fixed order.
+#define HF_ROWS 8
+#define HF_CHUNK 2048
+template <int D>
+__global__ __launch_bounds__(256) void heads_fwd_kernel(const float* __restrict__ X, long long x_gs, int B, int K,
+                                                        const float* __restrict__ Wm, const float* __restrict__ Ws,
+                                                        long long w_gs, float* __restrict__ part, long long p_gs,
+                                                        int pcols, int coff, int coff2) {
+  __shared__ float red[4][HF_ROWS][2 * D];
+  const int group = blockIdx.z, split = blockIdx.y, r0 = blockIdx.x * HF_ROWS;
+  X += group * x_gs;
+  Wm += group * w_gs;
+  Ws += group * w_gs;
+  float acc[HF_ROWS][2 * D];
+#pragma unroll
+  for (int r = 0; r < HF_ROWS; ++r)
+#pragma unroll
+    for (int o = 0; o < 2 * D; ++o) acc[r][o] = 0.f;
+  const int k1 = min(K, (split + 1) * HF_CHUNK);
+  for (int k = split * HF_CHUNK + 4 * threadIdx.x; k < k1; k += 1024) {
+    float wm[4 * D], ws[4 * D];  // [j][o] of k + j
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      const f32x4 a = *(const f32x4*)(Wm + (long long)k * D + 4 * i), b = *(const f32x4*)(Ws + (long long)k * D + 4 * i);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        wm[4 * i + e] = a[e];
+        ws[4 * i + e] = b[e];
+      }
+    }
+    f32x4 x[HF_ROWS];
+#pragma unroll
+    for (int r = 0; r < HF_ROWS; ++r)
+      x[r] = r0 + r < B ? *(const f32x4*)(X + (long long)(r0 + r) * K + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < HF_ROWS; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int o = 0; o < D; ++o) {
+          acc[r][o] = fmaf(x[r][j], wm[j * D + o], acc[r][o]);
+          acc[r][D + o] = fmaf(x[r][j], ws[j * D + o], acc[r][D + o]);
+        }
+  }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int r = 0; r < HF_ROWS; ++r)
+#pragma unroll
+    for (int o = 0; o < 2 * D; ++o) {
+      const float v = wave_sum(acc[r][o]);
+      if (lane == 0) red[wave][r][o] = v;
+    }
+  __syncthreads();
+  if (threadIdx.x < HF_ROWS * 2 * D) {
+    const int r = threadIdx.x / (2 * D), o = threadIdx.x % (2 * D);
+    if (r0 + r < B) {
+      const float v = red[0][r][o] + red[1][r][o] + red[2][r][o] + red[3][r][o];
+      part[group * p_gs + ((long long)split * B + r0 + r) * pcols + (o < D ? coff + o : coff2 + o - D)] = v;
+    }
+  }
+}
+
+int heads_splits(int K) { return (K + HF_CHUNK - 1) / HF_CHUNK; }
+
+static bool heads_narrow_off() {  // SVAE_HEADS_SKINNY=1: the former 4-row skinny pass (A/B)
+  static const bool v = [] {
+    const char* e = getenv("SVAE_HEADS_SKINNY");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
 
 void heads_fwd(const float* X, long long x_gs, int B, int K, const float* Wm, const float* Ws, long long w_gs, int D,
                float* part, long long part_gs, int pcols, int coff, int groups, hipStream_t s) {
   // mean and stddev heads in one pass over X (the shared recognition features)
+  const bool al = ((uintptr_t)X % 16 == 0) && ((uintptr_t)Wm % 16 == 0) && ((uintptr_t)Ws % 16 == 0) &&
+                  (x_gs % 4 == 0) && (w_gs % 4 == 0);
+  if (D <= 4 && K % 4 == 0 && al && !heads_narrow_off()) {
+    dim3 grid((B + HF_ROWS - 1) / HF_ROWS, heads_splits(K), groups);
+    const int c2 = pcols / 2 + coff;
+#define HF_L(DD) hipLaunchKernelGGL(heads_fwd_kernel<DD>, grid, dim3(256), 0, s, X, x_gs, B, K, Wm, Ws, w_gs, part, \
+                                    part_gs, pcols, coff, c2)
+    if (D == 1) HF_L(1);
+    else if (D == 2) HF_L(2);
+    else if (D == 3) HF_L(3);
+    else HF_L(4);
+#undef HF_L
+    return;
+  }
+  // the splits follow HF_CHUNK (heads_splits); skinny's chunk must match
   skinny(X, K, x_gs, B, K, Wm, D, 1, w_gs, D, part, part_gs, pcols, coff, groups, s, Ws, pcols / 2 + coff);
 }
 
@@ -307,44 +396,66 @@ void splitfc_dz_reduce(const float* dz_part, int nblk, int B, int K, float* dz, 
 // latent: mu = clip(sum + bm), sig = sigmoid(sum + bs), z = mu + sig*eps, KL per image
 // (sequential_vae.py:1592-1594, :1023, :1156-1158)
 // ---------------------------------------------------------------------------
-__global__ void latent_fwd_kernel(const float* __restrict__ part, long long part_gs, int nsplit, int B, int Dz,
-                                  LatentLvls lv, long long bias_gs, float clipv, float prior, int uniform,
-                                  const float* __restrict__ eps, long long eps_gs, float* __restrict__ mu,
-                                  float* __restrict__ sig, float* __restrict__ z, long long ms_gs,
-                                  float* __restrict__ kl_img, long long kl_gs) {
+// one thread per (image, latent dimension): the 2 x nsplit head partials of a dimension load
+// together (summed in split order), and each image's KL terms are added in dimension order from LDS
+// (the order of the former one-thread-per-image loop: bitwise the same mu, sigma, z and KL)
+__global__ __launch_bounds__(256) void latent_fwd_kernel(const float* __restrict__ part, long long part_gs,
+                                                         int nsplit, int B, int Dz, LatentLvls lv, long long bias_gs,
+                                                         float clipv, float prior, int uniform,
+                                                         const float* __restrict__ eps, long long eps_gs,
+                                                         float* __restrict__ mu, float* __restrict__ sig,
+                                                         float* __restrict__ z, long long ms_gs,
+                                                         float* __restrict__ kl_img, long long kl_gs) {
+  __shared__ float klt[256];
   const int group = blockIdx.y;
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= B) return;
-  const float* P = part + group * part_gs;
-  const float p2 = prior * prior;
-  float kl = 0.f;
-  for (int l = 0; l < lv.L; ++l) {
-    for (int d = 0; d < lv.dim[l]; ++d) {
-      const int c = lv.off[l] + d;
-      float sm = 0.f, ss = 0.f;
-#pragma unroll 8
-      for (int sp = 0; sp < nsplit; ++sp) {  // loads batched, adds in the same order
-        sm += P[((long long)sp * B + n) * 2 * Dz + c];
-        ss += P[((long long)sp * B + n) * 2 * Dz + Dz + c];
-      }
-      float m = sm + lv.bm[l][group * bias_gs + d];
-      float mc = fminf(fmaxf(m, -clipv), clipv);
-      float sg = sigmoid_f(ss + lv.bs[l][group * bias_gs + d]);
-      const long long o = group * ms_gs + (long long)n * Dz + c;
-      mu[o] = m;  // raw (pre-clip) mean; the clip mask is re-derived in latent_bwd
-      sig[o] = sg;
-      z[o] = mc + sg * eps[group * eps_gs + (long long)n * Dz + c];
-      // use_uniform_prior: reduce_mean(-log sigma) (sequential_vae.py:1159-1160)
-      kl += uniform ? -__logf(sg) : -0.5f - __logf(sg) + 0.5f * sg * sg / p2 + 0.5f * mc * mc / p2;
+  const int ipb = 256 / Dz;  // images per block
+  const int il = threadIdx.x / Dz, c = threadIdx.x - il * Dz;
+  const int n = blockIdx.x * ipb + il;
+  const bool act = il < ipb && n < B;
+  float term = 0.f;
+  if (act) {
+    int l = 0;
+    while (l + 1 < lv.L && c >= lv.off[l + 1]) ++l;
+    const int d = c - lv.off[l];
+    const float* P = part + group * part_gs;
+    float pm[32], ps[32];
+#pragma unroll
+    for (int sp = 0; sp < 32; ++sp) {
+      pm[sp] = sp < nsplit ? P[((long long)sp * B + n) * 2 * Dz + c] : 0.f;
+      ps[sp] = sp < nsplit ? P[((long long)sp * B + n) * 2 * Dz + Dz + c] : 0.f;
     }
+    float sm = 0.f, ss = 0.f;
+#pragma unroll
+    for (int sp = 0; sp < 32; ++sp)
+      if (sp < nsplit) {
+        sm += pm[sp];
+        ss += ps[sp];
+      }
+    const float p2 = prior * prior;
+    const float m = sm + lv.bm[l][group * bias_gs + d];
+    const float mc = fminf(fmaxf(m, -clipv), clipv);
+    const float sg = sigmoid_f(ss + lv.bs[l][group * bias_gs + d]);
+    const long long o = group * ms_gs + (long long)n * Dz + c;
+    mu[o] = m;  // raw (pre-clip) mean; the clip mask is re-derived in latent_bwd
+    sig[o] = sg;
+    z[o] = mc + sg * eps[group * eps_gs + (long long)n * Dz + c];
+    // use_uniform_prior: reduce_mean(-log sigma) (sequential_vae.py:1159-1160)
+    term = uniform ? -__logf(sg) : -0.5f - __logf(sg) + 0.5f * sg * sg / p2 + 0.5f * mc * mc / p2;
   }
-  kl_img[group * kl_gs + n] = kl / Dz;
+  klt[threadIdx.x] = term;
+  __syncthreads();
+  if (act && c == 0) {
+    float kl = 0.f;
+    for (int j = 0; j < Dz; ++j) kl += klt[threadIdx.x + j];
+    kl_img[group * kl_gs + n] = kl / Dz;
+  }
 }
 
 void latent_fwd(const float* part, long long part_gs, int nsplit, int B, int Dz, const LatentLvls& lv,
                 long long bias_gs, float clipv, float prior, int uniform, const float* eps, long long eps_gs, float* mu,
                 float* sig, float* z, long long ms_gs, float* kl_img, long long kl_gs, int groups, hipStream_t s) {
-  hipLaunchKernelGGL(latent_fwd_kernel, dim3((B + 127) / 128, groups), dim3(128), 0, s, part, part_gs, nsplit, B, Dz,
+  const int ipb = 256 / Dz;
+  hipLaunchKernelGGL(latent_fwd_kernel, dim3((B + ipb - 1) / ipb, groups), dim3(256), 0, s, part, part_gs, nsplit, B, Dz,
                      lv, bias_gs, clipv, prior, uniform, eps, eps_gs, mu, sig, z, ms_gs, kl_img, kl_gs);
 }
 

@@ -36,6 +36,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int SC_TM = 2;               // 32-pixel tiles per wave
 constexpr int SC_BM = 4 * 32 * SC_TM;  // output pixels per block (4 waves)
+constexpr int SC_SQ = 6;               // window items per thread (WR * WC <= 1536)
 
 template <int TN, int TM, bool BF>
 __global__ __launch_bounds__(256) void conv_smallc_kernel(FwdArgs a) {
@@ -59,19 +60,35 @@ __global__ __launch_bounds__(256) void conv_smallc_kernel(FwdArgs a) {
 
   const float* A = a.A + group * a.a_gs + (long long)img * g.Hi * g.Wi * a.lda;
 
-  // ---- stage the window (rows iy0 .. iy0+WR-1, cols -1 .. Wi), 4 channels, zeros outside
-  for (int q = tid; q < WR * WC; q += 256) {
-    const int r = q / WC, col = q - r * WC;
-    const int iy = iy0 + r, ix = col - 1;
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (iy >= 0 && iy < g.Hi && ix >= 0 && ix < g.Wi) {
-      const float* src = A + ((long long)iy * g.Wi + ix) * a.lda;
+  // ---- stage the window (rows iy0 .. iy0+WR-1, cols -1 .. Wi), 4 channels, zeros outside: every
+  //      item's loads issue before the first LDS store (one memory round trip per block, not one per
+  //      256 items; WR * WC <= 256 * SC_SQ, host-checked)
+  {
+    f32x4 sv[SC_SQ];
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
-        if (c < a.Cin) v[c] = src[c];
+    for (int i = 0; i < SC_SQ; ++i) {
+      const int q = tid + 256 * i;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (q < WR * WC) {
+        const int r = q / WC, col = q - r * WC;
+        const int iy = iy0 + r, ix = col - 1;
+        if (iy >= 0 && iy < g.Hi && ix >= 0 && ix < g.Wi) {
+          const float* src = A + ((long long)iy * g.Wi + ix) * a.lda;
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (c < a.Cin) v[c] = src[c];
+        }
+      }
+      sv[i] = v;
     }
-    if (BF) ((bf16x4*)smem)[q] = __builtin_convertvector(v, bf16x4);
-    else ((f32x4*)smem)[q] = v;
+#pragma unroll
+    for (int i = 0; i < SC_SQ; ++i) {
+      const int q = tid + 256 * i;
+      if (q < WR * WC) {
+        if (BF) ((bf16x4*)smem)[q] = __builtin_convertvector(sv[i], bf16x4);
+        else ((f32x4*)smem)[q] = sv[i];
+      }
+    }
   }
 
   // ---- B fragments (registers, once per block)
@@ -159,14 +176,43 @@ __global__ __launch_bounds__(256) void conv_smallc_kernel(FwdArgs a) {
     }
   }
 
-  // ---- epilogue
+  // ---- epilogue (optionally with the fused backward-BN partials of the layer whose dy this is:
+  //      BwStat, the halo_kw / igemm_halo contract; their pre / y rows load before any store)
   float* Cp = a.C + group * a.c_gs;
   const float* bias = a.bias ? a.bias + group * a.bias_gs : nullptr;
   float csum[TN], csq[TN];
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) { csum[tn] = 0.f; csq[tn] = 0.f; }
+  const bool bwm = a.bw.pre != nullptr;
+  float bwmean[TN], bwis[TN], bwb[TN];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    const int n = tn * 32 + l32;
+    bwmean[tn] = bwis[tn] = bwb[tn] = 0.f;
+    if (bwm && n < a.bw.C) {
+      bwmean[tn] = a.bw.mean[group * a.bw.ms_gs + n];
+      bwis[tn] = a.bw.invstd[group * a.bw.ms_gs + n];
+      bwb[tn] = a.bw.y ? 0.f : a.bw.beta[group * a.bw.beta_gs + n];
+    }
+  }
+  const float* bwpre = bwm ? a.bw.pre + group * a.bw.pre_gs : nullptr;
+  const float* bwy = (bwm && a.bw.y) ? a.bw.y + group * a.bw.y_gs : nullptr;
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
+    float pv[16][TN], yv[16][TN];
+    if (bwm) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long long m = p0 + 32 * (wave * TM + tm) + (r & 3) + 8 * (r >> 2) + 4 * h;
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+          const int n = tn * 32 + l32;
+          const bool bwc = n < a.bw.C;
+          pv[r][tn] = bwc ? bwpre[m * a.bw.ldp + n] : 0.f;
+          yv[r][tn] = (bwc && bwy) ? bwy[m * a.bw.ldy + n] : 0.f;
+        }
+      }
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const long long m = p0 + 32 * (wave * TM + tm) + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -174,13 +220,17 @@ __global__ __launch_bounds__(256) void conv_smallc_kernel(FwdArgs a) {
       for (int tn = 0; tn < TN; ++tn) {
         const int n = tn * 32 + l32;
         float v = acc[tm][tn][r];
-        csum[tn] += v;
-        csq[tn] += v * v;
+        if (!bwm) {
+          csum[tn] += v;
+          csq[tn] += v * v;
+        }
         if (bias) v += bias[n];
         v = act_f(v, a.act);
         float* dst = Cp + m * a.ldc + n;
         if (a.accumulate) v += *dst;
         *dst = v;
+        if (bwm && n < a.bw.C)
+          bw_term_v(v, pv[r][tn], bwmean[tn], bwis[tn], bwb[tn], bwy != nullptr, yv[r][tn], a.bw.act, csum[tn], csq[tn]);
       }
     }
   }
@@ -195,7 +245,7 @@ __global__ __launch_bounds__(256) void conv_smallc_kernel(FwdArgs a) {
       }
     }
     __syncthreads();
-    if (tid < N) {
+    if (tid < (bwm ? a.bw.C : N)) {
       const float s = ((red[0][0][tid] + red[0][1][tid]) + red[0][2][tid]) + red[0][3][tid];
       const float q = ((red[1][0][tid] + red[1][1][tid]) + red[1][2][tid]) + red[1][3][tid];
       stat_put(a.stats + (blockIdx.x & (a.s_nsh - 1)) * a.s_sh + group * a.s_gs, tid, s, q);
@@ -231,6 +281,7 @@ void launch_smallc(const FwdArgs& a, int groups, hipStream_t s) {
 constexpr int SN_R = 8;      // output rows per block
 constexpr int SN_PITCH = 40; // LDS pixel pitch in bf16 (32 channels + 8 pad)
 constexpr int SN_MAXT = 16;  // class-row tiles per wave: (R/2) x (Wi/16) <= 16  -> Wi <= 64
+constexpr int SN_SQ = 2;     // window staging items per thread and batch (4 cost the kernel a wave per SIMD)
 
 typedef float f32x8 __attribute__((ext_vector_type(8)));
 
@@ -260,14 +311,28 @@ __global__ __launch_bounds__(256) void convt_smalln_kernel(FwdArgs a) {
 
   for (int ch = 0; ch < a.Cin; ch += 32) {
     if (ch) __syncthreads();  // previous chunk's window fully read
-    for (int it = tid; it < PR * PC * 4; it += 256) {
-      const int pix = it >> 2, part = it & 3;
-      const int pr = pix / PC, pc = pix - pr * PC;
-      const int iy = iy0 + pr, ix = pc - 1;
-      f32x4 lo = {0.f, 0.f, 0.f, 0.f}, hi = lo;
-      if (iy >= 0 && iy < g.Hi && ix >= 0 && ix < g.Wi)
-        ld8_raw(a.A, a0 + ((long long)iy * g.Wi + ix) * a.lda + ch + part * 8, abf, lo, hi);
-      *(bf16x8*)&wsm[pix * SN_PITCH + part * 8] = raw8_bf(lo, hi, abf);
+    // batches of SN_SQ items per thread: every load of a batch issues before its LDS stores (one
+    // memory round trip per batch of 512 items)
+    for (int b0 = 0; b0 < PR * PC * 4; b0 += 256 * SN_SQ) {
+      f32x4 lo[SN_SQ], hi[SN_SQ];
+#pragma unroll
+      for (int i = 0; i < SN_SQ; ++i) {
+        const int it = b0 + tid + 256 * i;
+        lo[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        hi[i] = lo[i];
+        if (it < PR * PC * 4) {
+          const int pix = it >> 2, part = it & 3;
+          const int pr = pix / PC, pc = pix - pr * PC;
+          const int iy = iy0 + pr, ix = pc - 1;
+          if (iy >= 0 && iy < g.Hi && ix >= 0 && ix < g.Wi)
+            ld8_raw(a.A, a0 + ((long long)iy * g.Wi + ix) * a.lda + ch + part * 8, abf, lo[i], hi[i]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < SN_SQ; ++i) {
+        const int it = b0 + tid + 256 * i;
+        if (it < PR * PC * 4) *(bf16x8*)&wsm[(it >> 2) * SN_PITCH + (it & 3) * 8] = raw8_bf(lo[i], hi[i], abf);
+      }
     }
     // this class's 4 tap fragments of the chunk (columns >= N are zero)
     bf16x8 bq[4];
@@ -353,11 +418,13 @@ bool smallc_ok(const FwdArgs& a, bool bf) {
   const ConvGeom& g = a.g;
   if (smallc_disabled()) return false;
   if (g.mode != GM_CONV || g.ksz != 4 || g.stride != 2 || g.pad != 1 || a.nclass != 1) return false;
-  if (a.Cin < 1 || a.Cin > 4 || a.bw.pre) return false;
+  if (a.Cin < 1 || a.Cin > 4) return false;
+  if (a.bw.pre && (a.bw.C > a.N || !a.stats)) return false;  // fused BN-backward partials: N columns at most
   if (!(a.N == 32 || a.N == 64 || a.N == 128)) return false;
   if (g.Hi != 2 * g.Ho || g.Wi != 2 * g.Wo || g.Wo > SC_BM || SC_BM % g.Wo) return false;
   if ((g.Ho * g.Wo) % SC_BM || a.rows % SC_BM) return false;
   if (bf ? !a.Bh : !a.B) return false;
+  if ((2 * (SC_BM / g.Wo) + 2) * (g.Wi + 2) > 256 * SC_SQ) return false;  // the staging's item budget
   return smallc_lds(a, bf) <= 64 * 1024;
 }
 

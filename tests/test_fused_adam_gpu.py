@@ -99,3 +99,51 @@ def test_batched_side_handover_is_bitwise(preset, dtype, over, fused, monkeypatc
         assert changed > 0
         assert l0 == l1, (k, l0, l1)
         np.testing.assert_array_equal(p0, p1)
+
+
+def _fwd_bwd(preset, dtype, over):
+    cfgmod, SV = pkg_mod("config"), pkg_mod("sequential_vae").SequentialVAE
+    cfg = cfgmod.preset(preset, batch=4, dtype=dtype, **over)
+    net = SV(cfg, seed=0)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(11)
+    x = torch.rand(cfg.batch, cfg.height, cfg.width, cfg.channels, device="cuda", generator=g) * 2 - 1
+    eps = torch.randn(cfg.mc_steps, cfg.batch, cfg.latent_dim, device="cuda", generator=g)
+    net.forward(x, x, eps, 0.5)
+    net.backward()
+    torch.cuda.synchronize()
+    loss, gr = net.loss_value(), net.grads.cpu().numpy().copy()
+    net.close()
+    return loss, gr
+
+
+@pytest.mark.parametrize("preset,dtype,over", [
+    ("tiny", "bf16", {}),
+    ("tiny", "fp32", {}),
+    ("tiny_homog", "bf16", {}),
+])
+@pytest.mark.parametrize("knob", ["SVAE_REC_SPLIT", "SVAE_REC_GROUP"])
+def test_forward_recognition_split_matches(preset, dtype, over, knob, monkeypatch):
+    """SVAE_REC_SPLIT=1 runs step 0's recognition ladder on the main stream and the batched ladders of
+    steps 1..T-1 on a fourth stream beside the chain's step 0 (engine.cpp engine_forward).  The same
+    per-step kernels run on the same data; only launch shapes that depend on the group count
+    (split-K / tile choices of step 0's launches) may change a summation order, so the loss and the
+    gradient of one step agree to fp32 rounding (reported when bitwise).  (Compared before any Adam
+    step: Adam's first update is sign(g) * lr, which turns a rounding-level difference of a near-zero
+    gradient into a full step.)  SVAE_REC_GROUP=1 is the backward counterpart: the recognition
+    backward of each step on the fourth stream as soon as its dz is final.  Both read the bf16
+    recognition activations at a step offset, which must count bf16 elements (engine.cpp elem_off:
+    with float* arithmetic these gave steps >= 1 wrong conv weight gradients, 100-140 % off)."""
+    monkeypatch.delenv("SVAE_REC_SPLIT", raising=False)
+    monkeypatch.delenv("SVAE_REC_GROUP", raising=False)
+    l0, g0 = _fwd_bwd(preset, dtype, over)
+    monkeypatch.setenv(knob, "1")
+    l1, g1 = _fwd_bwd(preset, dtype, over)
+    gvec = float(np.linalg.norm(g1 - g0) / np.linalg.norm(g0))
+    print("rec split %s %s/%s: bitwise %s, loss rel %.2e, gradient vector rel %.2e" % (
+        knob, preset, dtype, l0 == l1 and np.array_equal(g0, g1), abs(l0 - l1) / abs(l0), gvec))
+    # these geometries launch the same kernel shapes either way: bitwise.  (At the CelebA geometry a
+    # one-group launch of step 0 may take a split-K form the batched one does not, and the chaotic
+    # B=4 chain amplifies that rounding; there the knobs run the engine parity suite instead,
+    # tools/gpu/r03_headsab.sh.)
+    assert l0 == l1 and np.array_equal(g0, g1), (l0, l1, gvec)
