@@ -368,6 +368,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
+    if os.environ.get("SVAE_BENCH_STREAM") == "1":  # A/B: run on a non-default torch stream
+        torch.cuda.set_stream(torch.cuda.Stream(local))
     dist = None
     if world > 1:
         import torch.distributed as dist

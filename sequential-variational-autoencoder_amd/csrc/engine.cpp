@@ -2469,7 +2469,23 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
   {
     const char* ns = getenv("SVAE_NO_SIDE");
     if (!(ns && ns[0] == '1')) {
-      bool ok = hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking) == hipSuccess;
+      // SVAE_SIDE_CUMASK=k (A/B): the weight-gradient stream runs on all CUs but every k-th, so the
+      // main stream's latency-bound kernels always find free CUs.  A CU-masked stream is a blocking
+      // stream (it synchronises with the NULL stream), so this is only meaningful when the caller's
+      // stream is not the NULL stream (bench.py SVAE_BENCH_STREAM=1)
+      const char* cm = getenv("SVAE_SIDE_CUMASK");
+      const int cmk = cm ? atoi(cm) : 0;
+      bool ok;
+      if (cmk >= 2) {
+        int ncu = 0;
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        for (int i = 0; i < ncu; ++i)
+          if (i % cmk != cmk - 1) mask[i / 32] |= 1u << (i % 32);
+        ok = hipExtStreamCreateWithCUMask(&c->st2, (uint32_t)mask.size(), mask.data()) == hipSuccess;
+      } else {
+        ok = hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking) == hipSuccess;
+      }
       ok = ok && hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking) == hipSuccess;
       if (c->rec_group > 0 || c->rec_split)
         ok = ok && hipStreamCreateWithFlags(&c->st4, hipStreamNonBlocking) == hipSuccess;
