@@ -32,7 +32,7 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no 2:1 s
 # wgrad_halo2_kernel) is reported as the secondary entry.
 DOMINANT_KID = "KID_HALO_KW"
 SECONDARY_KID = "KID_WHALO2_S1"
-PMC_FILE = "profiles/r03_v3_pmc_traffic.json"  # tools/gpu/r03_final.sh (bench command, two passes, calibrated FETCH rules)
+PMC_FILE = "profiles/r03_v5_pmc_traffic.json"  # tools/gpu/r03_final.sh (bench command, two passes, calibrated FETCH rules)
 
 
 # metric / workload per preset (BASELINE.json configs[1] is the headline: CelebA B=128)
