@@ -1235,10 +1235,14 @@ static int fc_bn_fwd(svae_ctx* c, const FcL& f, View in, float* pre, BNS bn, Vie
 }
 
 // dense backward: dy wrt post-act (view), y, pre -> grads; din (=) if non-null
-static int fc_bn_bwd(svae_ctx* c, const FcL& f, View in, View dy, View y, const float* pre, BNS bn, View din) {
+// fu_self: this layer's BN-backward sums were added by the producer of dy (pre-reduced);
+// fu_din: the BN layer whose dy is din, its sums fused into this layer's input-gradient GEMM when
+// that runs the split-K dense kernel (splitk_reduce carries the BwStat terms)
+static int fc_bn_bwd(svae_ctx* c, const FcL& f, View in, View dy, View y, const float* pre, BNS bn, View din,
+                     BwFuse* fu_self = nullptr, BwFuse* fu_din = nullptr) {
   const int B = c->m.g.B;
   const Slot sl = dpre_next(c, (long long)B * f.nout);
-  int r = bn_act_bwd(c, 1, B, f.nout, dy, y, pre, 0, f.nout, bn, 0, f.obeta, 0, ACT_LRELU, sl.p, 0, View{}, 0, nullptr,
+  int r = bn_act_bwd(c, 1, B, f.nout, dy, y, pre, 0, f.nout, bn, 0, f.obeta, 0, ACT_LRELU, sl.p, 0, View{}, 0, fu_self,
                      c->dbf);
   if (r) return r;
   WgArgs w{};
@@ -1265,6 +1269,26 @@ static int fc_bn_bwd(svae_ctx* c, const FcL& f, View in, View dy, View y, const 
     a.g.mode = GM_DENSE; a.g.nimg = B; a.g.ksz = 1; a.g.stride = 1;
     a.rows = B; a.nclass = 1;
     if (c->m.g.bf16) a.Bh = shadowN(c, f.ow);  // [in][out] as NK (n = in, k = out)
+    if (fu_din) fu_din->used = false;
+    static const bool fc_fuse = [] {  // SVAE_BWFUSE_FC=0: the FC BN-backward sums in their own pass (A/B)
+      const char* e = getenv("SVAE_BWFUSE_FC");
+      return !(e && e[0] == '0');
+    }();
+    if (fu_din && fu_din->bw.pre && c->m.g.bf16 && !c->m.g.split && fu_din->bw.C % 4 == 0 && fu_din->bw.C <= a.N &&
+        fc_fuse) {
+      FwdArgs t = a;
+      t.part = c->slab;
+      t.part_cap = c->slab_cap;
+      t.bw = fu_din->bw;
+      if (dense_kw_ok(t, 1) && dense_kw_ks(t) > 1) {
+        const AccR acc = acc_bn(c, 1, fu_din->bw.C, dense_kw_nrb(t));
+        if (!acc.p) return fail(c, SVAE_EBADARG, "BN accumulator arena too small");
+        a.bw = fu_din->bw;
+        set_stats(a, acc);
+        fu_din->acc = acc;
+        fu_din->used = true;
+      }
+    }
     gemm(c, a, 1);
   }
   return 0;
@@ -1985,8 +2009,14 @@ static int engine_backward_pass(svae_ctx* c) {
     // own region per pass when the side stream's split-latent backward reads it
     float* dtop = c->side ? arena_next(c, c->dtop_arena, c->dtop_cap, c->dtop_off, (long long)B * s.ktop, true)
                           : c->dtop;
+    // E.fc's BN-backward sums (t >= 1: columns [0, nout) of dtop) from the top FC's input gradient
+    BwFuse fu_efc;
+    if (t >= 1) {
+      const FcL& ef = M.enc[t].fc;
+      fu_efc = bw_fuse(c, s.encfc_pre, ef.nout, 0, nullptr, 0, 0, s.enc_bn_fc, 0, ef.obeta, 0, ACT_LRELU, ef.nout);
+    }
     r = fc_bn_bwd(c, G.top, View{s.top_cat, s.ktop, 0}, View{dcur, ntop, 0}, View{s.top_act, ntop, 0}, s.top_pre,
-                  s.top_bn, View{dtop, s.ktop, 0});
+                  s.top_bn, View{dtop, s.ktop, 0}, nullptr, t >= 1 ? &fu_efc : nullptr);
     if (r) return r;
     {
       const FcL& f = G.split[L - 1];
@@ -2007,7 +2037,7 @@ static int engine_backward_pass(svae_ctx* c) {
       const EncStep& E = M.enc[t];
       const int nc = S[L] * S[L] * F[L - 1];
       r = fc_bn_bwd(c, E.fc, View{s.enc_c_act, nc, 0, c->abf}, View{dtop, s.ktop, 0}, View{s.top_cat, s.ktop, 0},
-                    s.encfc_pre, s.enc_bn_fc, View{c->denc_c, nc, 0});
+                    s.encfc_pre, s.enc_bn_fc, View{c->denc_c, nc, 0}, fu_efc.used ? &fu_efc : nullptr);
       if (r) return r;
       const long long rc = (long long)B * S[L] * S[L];
       Slot sl = dpre_next(c, rc * F[L - 1]);
