@@ -1,4 +1,4 @@
-"""Data-parallel path on CPU (gloo, world_size 2 and 8): per-shard BN semantics + one
+"""Data-parallel path on CPU (gloo, world_size 2, 4 and 8): per-shard BN semantics + one
 all-reduce of the flat gradient (SURVEY.md §8e parity rule):
   N-rank loss  = mean over shards of the single-process loss of each shard
   N-rank grad  = mean over shards of the per-shard gradients
@@ -53,7 +53,7 @@ def _worker(rank, world, port, gx, gt, eps_all, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 4])
 def test_dp_allreduce_matches_shard_mean(tmp_path, world):
     B = 4 * world
     cd = spec.make_config("tiny", batch=B)
