@@ -1270,9 +1270,9 @@ static int fc_bn_bwd(svae_ctx* c, const FcL& f, View in, View dy, View y, const 
     a.rows = B; a.nclass = 1;
     if (c->m.g.bf16) a.Bh = shadowN(c, f.ow);  // [in][out] as NK (n = in, k = out)
     if (fu_din) fu_din->used = false;
-    static const bool fc_fuse = [] {  // SVAE_BWFUSE_FC=1: E.fc's BN-backward sums in the top FC's input
-      const char* e = getenv("SVAE_BWFUSE_FC");  // gradient (A/B; off until measured on the GPU)
-      return e && e[0] == '1';
+    static const bool fc_fuse = [] {  // E.fc's BN-backward sums in the top FC's input gradient: +0.3 %
+      const char* e = getenv("SVAE_BWFUSE_FC");  // (profiles/r03_fc_ab.txt); SVAE_BWFUSE_FC=0 restores the pass
+      return !(e && e[0] == '0');
     }();
     if (fu_din && fu_din->bw.pre && c->m.g.bf16 && !c->m.g.split && fu_din->bw.C % 4 == 0 && fu_din->bw.C <= a.N &&
         fc_fuse) {
