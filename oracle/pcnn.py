@@ -352,12 +352,14 @@ def loss_and_grads(spec, params, x, h, bf16=False):
     return float(loss), l.detach().numpy(), grads
 
 
-def data_init(spec, params, x, h):
+def data_init(spec, params, x, h, masks=None, bf16=False):
     """The init pass (model(..., init=True), pixelvae.py:103-105): new g, b of every weight-normed
-    layer in construction order, each from its own (un-normalised) output moments."""
+    layer in construction order, each from its own (un-normalised) output moments.  masks: the
+    pass's dropout keep-masks (pixelvae.py:103-105 passes dropout_p to the init model too);
+    bf16: the HIP head's operand rounding."""
     P = to_tensors(params, requires_grad=False)
-    net = Net(spec, P, init=True)
-    net.model(torch.tensor(x, dtype=DT), torch.tensor(h, dtype=DT))
+    net = Net(spec, P, bf16=bf16, init=True)
+    net.model(torch.tensor(np.asarray(x), dtype=DT), torch.tensor(np.asarray(h), dtype=DT), masks=masks)
     out = dict(params)
     for k, v in net.updates.items():
         out[k] = v.numpy()

@@ -505,6 +505,7 @@ struct svae_ctx {
   // marker packet that drains the queue before the next dispatch (a 4-10 us gap per record).
   std::vector<std::function<int()>> side_q;
   int side_batch = 1;
+  bool fc_fuse = true;  // E.fc BN-backward sums fused into the top FC's input gradient (SVAE_BWFUSE_FC)
   static constexpr int NF = 4;
   hipEvent_t ev_flush[NF] = {};
   int flush_pos = 0;
@@ -823,7 +824,15 @@ static int side_run_queued(svae_ctx* c) {
   c->slab = sl0;
   return r;
 }
-// queued form of on_side for closures that capture by value (SVAE_SIDE_BATCH > 1); otherwise at once
+// queued form of on_side for closures that capture by value (SVAE_SIDE_BATCH > 1); otherwise at once.
+// Contract of the queued form:
+//  - a closure's inputs are produced on the stream that is c->st when it is queued; the queue
+//    must be flushed (side_flush records its event on c->st) before c->st changes, so the
+//    event orders st2 after the producing stream (the st4 recognition groups flush before
+//    restoring the main stream);
+//  - there is no per-slot "freed" event: every dpre / dcat / dtop / da region lives in a per-pass
+//    arena and is never reused within a pass, so no slot waits for its reader;
+//  - c->st / c->slab are read when the closure RUNS (side_run_queued swaps in st2 / slab2).
 template <class Fn>
 static int on_side_q(svae_ctx* c, hipEvent_t ready, Fn&& fn) {
   if (!c->side || !ready || c->side_batch <= 1) {
@@ -1270,12 +1279,10 @@ static int fc_bn_bwd(svae_ctx* c, const FcL& f, View in, View dy, View y, const 
     a.rows = B; a.nclass = 1;
     if (c->m.g.bf16) a.Bh = shadowN(c, f.ow);  // [in][out] as NK (n = in, k = out)
     if (fu_din) fu_din->used = false;
-    static const bool fc_fuse = [] {  // E.fc's BN-backward sums in the top FC's input gradient: +0.3 %
-      const char* e = getenv("SVAE_BWFUSE_FC");  // (profiles/r03_fc_ab.txt); SVAE_BWFUSE_FC=0 restores the pass
-      return !(e && e[0] == '0');
-    }();
+    // E.fc's BN-backward sums in the top FC's input gradient: +0.3 % (profiles/r03_fc_ab.txt);
+    // SVAE_BWFUSE_FC=0 at svae_create restores the separate pass
     if (fu_din && fu_din->bw.pre && c->m.g.bf16 && !c->m.g.split && fu_din->bw.C % 4 == 0 && fu_din->bw.C <= a.N &&
-        fc_fuse) {
+        c->fc_fuse) {
       FwdArgs t = a;
       t.part = c->slab;
       t.part_cap = c->slab_cap;
@@ -2112,6 +2119,10 @@ static int engine_backward_pass(svae_ctx* c) {
       c->st = c->st4;
       c->slab = c->slab4;
       r = inference_bwd(c, t, std::min(c->rec_group, T - t), View{(float*)c->x_in, g.C, 0}, nullptr);
+      // the group's queued weight-gradient closures read st4's dpre: flush them behind an event
+      // recorded on st4 (side_flush records on c->st), before the main stream is restored
+      const int rf = side_flush(c);
+      if (!r) r = rf;
       c->st = s0;
       c->slab = sl0;
       if (r) return r;
@@ -2173,7 +2184,7 @@ static bool plan(svae_ctx* c) {
   }
   int maxnin = 0;
   for (int l = 0; l < L; ++l) maxnin = std::max(maxnin, c->m.inf[0].head[l].nin);
-  c->head_nsplit = heads_splits(maxnin);  // latent_fwd_kernel sums up to 32 head partials per dimension
+  c->head_nsplit = heads_splits(maxnin);  // latent_fwd_kernel sums the head partials 32 splits at a time
   c->head_part = A((long long)T * c->head_nsplit * B * 2 * g.Dz);
   c->mu = A((long long)T * B * g.Dz);
   c->sig = A((long long)T * B * g.Dz);
@@ -2381,9 +2392,9 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
   c->counting = true;
   c->arena_used = 0;
   plan(c);
-  if (c->head_nsplit > 32 || c->m.g.Dz > 256) {  // latent_fwd_kernel's limits
+  if (c->m.g.Dz > 1024) {  // latent_fwd_kernel: one image per block of up to 1024 threads
     delete c;
-    return fail(nullptr, SVAE_EBADCONFIG, "recognition head input over 65536 features or latent over 256");
+    return fail(nullptr, SVAE_EBADCONFIG, "latent over 1024 dimensions");
   }
   c->arena_bytes = c->arena_used;
   c->counting = false;
@@ -2545,6 +2556,10 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
       }
       c->side = ok;
     }
+  }
+  {
+    const char* e = getenv("SVAE_BWFUSE_FC");  // read per context (A/B and the bitwise test)
+    c->fc_fuse = !(e && e[0] == '0');
   }
   for (int i = 0; i < 64; ++i) c->reg_host[i] = 0.f;
   *out = c;

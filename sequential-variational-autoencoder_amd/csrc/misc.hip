@@ -397,18 +397,20 @@ void splitfc_dz_reduce(const float* dz_part, int nblk, int B, int K, float* dz, 
 // (sequential_vae.py:1592-1594, :1023, :1156-1158)
 // ---------------------------------------------------------------------------
 // one thread per (image, latent dimension): the 2 x nsplit head partials of a dimension load
-// together (summed in split order), and each image's KL terms are added in dimension order from LDS
-// (the order of the former one-thread-per-image loop: bitwise the same mu, sigma, z and KL)
-__global__ __launch_bounds__(256) void latent_fwd_kernel(const float* __restrict__ part, long long part_gs,
-                                                         int nsplit, int B, int Dz, LatentLvls lv, long long bias_gs,
-                                                         float clipv, float prior, int uniform,
-                                                         const float* __restrict__ eps, long long eps_gs,
-                                                         float* __restrict__ mu, float* __restrict__ sig,
-                                                         float* __restrict__ z, long long ms_gs,
-                                                         float* __restrict__ kl_img, long long kl_gs) {
-  __shared__ float klt[256];
+// together, 32 splits at a time (summed in split order for any nsplit), and each image's KL terms
+// are added in dimension order from LDS (the order of the former one-thread-per-image loop: bitwise
+// the same mu, sigma, z and KL).  Blocks of 256 threads hold 256 / Dz images; Dz > 256 takes one
+// image per block of Dz rounded up to 64 threads.
+__global__ __launch_bounds__(1024) void latent_fwd_kernel(const float* __restrict__ part, long long part_gs,
+                                                          int nsplit, int B, int Dz, LatentLvls lv, long long bias_gs,
+                                                          float clipv, float prior, int uniform,
+                                                          const float* __restrict__ eps, long long eps_gs,
+                                                          float* __restrict__ mu, float* __restrict__ sig,
+                                                          float* __restrict__ z, long long ms_gs,
+                                                          float* __restrict__ kl_img, long long kl_gs) {
+  __shared__ float klt[1024];
   const int group = blockIdx.y;
-  const int ipb = 256 / Dz;  // images per block
+  const int ipb = (int)blockDim.x / Dz;  // images per block
   const int il = threadIdx.x / Dz, c = threadIdx.x - il * Dz;
   const int n = blockIdx.x * ipb + il;
   const bool act = il < ipb && n < B;
@@ -418,19 +420,21 @@ __global__ __launch_bounds__(256) void latent_fwd_kernel(const float* __restrict
     while (l + 1 < lv.L && c >= lv.off[l + 1]) ++l;
     const int d = c - lv.off[l];
     const float* P = part + group * part_gs;
-    float pm[32], ps[32];
-#pragma unroll
-    for (int sp = 0; sp < 32; ++sp) {
-      pm[sp] = sp < nsplit ? P[((long long)sp * B + n) * 2 * Dz + c] : 0.f;
-      ps[sp] = sp < nsplit ? P[((long long)sp * B + n) * 2 * Dz + Dz + c] : 0.f;
-    }
     float sm = 0.f, ss = 0.f;
+    for (int s0 = 0; s0 < nsplit; s0 += 32) {
+      float pm[32], ps[32];
 #pragma unroll
-    for (int sp = 0; sp < 32; ++sp)
-      if (sp < nsplit) {
-        sm += pm[sp];
-        ss += ps[sp];
+      for (int sp = 0; sp < 32; ++sp) {
+        pm[sp] = s0 + sp < nsplit ? P[((long long)(s0 + sp) * B + n) * 2 * Dz + c] : 0.f;
+        ps[sp] = s0 + sp < nsplit ? P[((long long)(s0 + sp) * B + n) * 2 * Dz + Dz + c] : 0.f;
       }
+#pragma unroll
+      for (int sp = 0; sp < 32; ++sp)
+        if (s0 + sp < nsplit) {
+          sm += pm[sp];
+          ss += ps[sp];
+        }
+    }
     const float p2 = prior * prior;
     const float m = sm + lv.bm[l][group * bias_gs + d];
     const float mc = fminf(fmaxf(m, -clipv), clipv);
@@ -454,8 +458,9 @@ __global__ __launch_bounds__(256) void latent_fwd_kernel(const float* __restrict
 void latent_fwd(const float* part, long long part_gs, int nsplit, int B, int Dz, const LatentLvls& lv,
                 long long bias_gs, float clipv, float prior, int uniform, const float* eps, long long eps_gs, float* mu,
                 float* sig, float* z, long long ms_gs, float* kl_img, long long kl_gs, int groups, hipStream_t s) {
-  const int ipb = 256 / Dz;
-  hipLaunchKernelGGL(latent_fwd_kernel, dim3((B + ipb - 1) / ipb, groups), dim3(256), 0, s, part, part_gs, nsplit, B, Dz,
+  const int bs = Dz <= 256 ? 256 : (Dz + 63) / 64 * 64;  // (svae_create rejects Dz > 1024)
+  const int ipb = bs / Dz;
+  hipLaunchKernelGGL(latent_fwd_kernel, dim3((B + ipb - 1) / ipb, groups), dim3(bs), 0, s, part, part_gs, nsplit, B, Dz,
                      lv, bias_gs, clipv, prior, uniform, eps, eps_gs, mu, sig, z, ms_gs, kl_img, kl_gs);
 }
 

@@ -86,11 +86,16 @@ def test_rebind_after_external_write_rebuilds_weight_copies():
     ("tiny_homog", "bf16", {}),
 ])
 @pytest.mark.parametrize("fused", [False, True])
-def test_batched_side_handover_is_bitwise(preset, dtype, over, fused, monkeypatch):
+@pytest.mark.parametrize("rec_group", ["0", "1"])
+def test_batched_side_handover_is_bitwise(preset, dtype, over, fused, rec_group, monkeypatch):
     """SVAE_SIDE_BATCH = k queues the weight-gradient work of k layers behind one main-stream
     event (engine.cpp on_side_q / side_flush): the same kernels on the same data, so losses and
     parameters after three steps equal the per-layer hand-over bit for bit (the per-bucket Adam
-    of the fused path must still follow every weight gradient of its bucket)."""
+    of the fused path must still follow every weight gradient of its bucket).  With
+    SVAE_REC_GROUP=1 the recognition backward of each step runs on a fourth stream and queues its
+    weight gradients there: the queue must be flushed behind an event on THAT stream (ADVICE r03:
+    flushed later from the main stream, the weight-GEMMs could read dpre st4 had not written)."""
+    monkeypatch.setenv("SVAE_REC_GROUP", rec_group)
     monkeypatch.setenv("SVAE_SIDE_BATCH", "1")
     p0, l0, _ = _run(preset, dtype, fused, over)
     for k in ("3", "100"):
@@ -147,3 +152,18 @@ def test_forward_recognition_split_matches(preset, dtype, over, knob, monkeypatc
     # B=4 chain amplifies that rounding; there the knobs run the engine parity suite instead,
     # tools/gpu/r03_headsab.sh.)
     assert l0 == l1 and np.array_equal(g0, g1), (l0, l1, gvec)
+
+
+@pytest.mark.parametrize("preset", ["tiny", "celeba"])
+def test_fc_bn_backward_fusion_is_bitwise(preset, monkeypatch):
+    """bf16 default: E.fc's BN-backward sums are formed in the top FC's split-K input gradient
+    (engine.cpp fc_bn_bwd, splitk_reduce BwStat columns) instead of a bn_bwd_reduce pass.  The sums
+    are fixed-point accumulated (order-free), so three training steps must equal the unfused path
+    (SVAE_BWFUSE_FC=0) bit for bit."""
+    monkeypatch.setenv("SVAE_BWFUSE_FC", "0")
+    p0, l0, _ = _run(preset, "bf16", True, {})
+    monkeypatch.setenv("SVAE_BWFUSE_FC", "1")
+    p1, l1, changed = _run(preset, "bf16", True, {})
+    assert changed > 0
+    assert l0 == l1, (l0, l1)
+    np.testing.assert_array_equal(p0, p1)

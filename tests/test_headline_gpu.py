@@ -7,7 +7,8 @@ T=8), in both precision modes, on the same inputs and the same injected eps.
 * bf16 engine (the mode bench.py measures): loss within the documented bf16 bound of the fp32
   engine (2e-2) and within 3x (+ floor) of the error of the bf16-emulating CPU
   restatement (oracle/torch_twin.py emulate_bf16, the same operands rounded); x_hat_t within 3x
-  (+ floor) of that twin's own error.  Gradients are printed only (see the comment at the end).
+  (+ floor) of that twin's own error; the gradient vector and per-tensor median vs float64 within 2x
+  of that twin's own gradient error vs float64 (the twin's backward rounds the same legs).
 * bf16x6 engine (split-bf16 MFMA, the fp32-accurate mode bench.py reports as `parity_value`): the
   fp32 bounds -- loss within 1e-4 of float64, x_hat_0 / x_hat_1 within 1e-4, x_hat_t within
   max(1e-4, 4x the fp32 twin's own error vs float64), and the gradient vector within 4x the fp32
@@ -52,14 +53,15 @@ def test_headline_config_both_precisions():
     # the chaos scale every fp32-class gradient is measured against)
     o64 = torch_twin.Twin(cd, struct, params, dtype=torch.float64).step(x, tgt, eps, 1.0)
     t32 = torch_twin.Twin(cd, struct, params, dtype=torch.float32).step(x, tgt, eps, 1.0)
-    with torch.no_grad():
-        emul = torch_twin.Twin(cd, struct, params, dtype=torch.float32, requires_grad=False,
-                               emulate_bf16=True).step(x, tgt, eps, 1.0, backward=False)
+    # the bf16-emulating twin WITH its backward: the same operands rounded in the same legs, fp32
+    # accumulation -- its gradient error vs float64 is the scale the bf16 engine's gradient is held to
+    emul = torch_twin.Twin(cd, struct, params, dtype=torch.float32, emulate_bf16=True).step(x, tgt, eps, 1.0)
     table = pkg_mod("weights").param_table(pkg_mod("config").preset("celeba"))[0]
     live = [p for p in table if p["offset"] + p["size"] <= len(res["fp32"]["grads"])]
     flat = lambda gd: np.concatenate([np.ravel(gd[p["name"]]).astype(np.float64) for p in live])
-    g64, gt32 = flat(o64["grads"]), flat(t32["grads"])
+    g64, gt32, gem = flat(o64["grads"]), flat(t32["grads"]), flat(emul["grads"])
     e_twin = _rel(gt32, g64)
+    e_emg = _rel(gem, g64)
     L64 = o64["loss"]
     e32 = abs(res["fp32"]["loss"] - L64) / abs(L64)
     e16 = abs(res["bf16"]["loss"] - L64) / abs(L64)
@@ -74,6 +76,12 @@ def test_headline_config_both_precisions():
     gvec = _rel(g16f, g32f)
     per = [_rel(g16[p["offset"]:p["offset"] + p["size"]], g32[p["offset"]:p["offset"] + p["size"]])
            for p in live if np.linalg.norm(g32[p["offset"]:p["offset"] + p["size"]]) > 1e-7]
+    # bf16 engine and bf16-emulating twin, each vs float64: vector and per-tensor median
+    g16_64 = _rel(g16f, g64)
+    sl = lambda p: slice(p["offset"], p["offset"] + p["size"])
+    big = [p for p in live if np.linalg.norm(np.ravel(o64["grads"][p["name"]])) > 1e-7]
+    med16 = float(np.median([_rel(g16[sl(p)], o64["grads"][p["name"]]) for p in big]))
+    medem = float(np.median([_rel(emul["grads"][p["name"]], o64["grads"][p["name"]]) for p in big]))
     ex6 = abs(res["bf16x6"]["loss"] - L64) / abs(L64)
     xx6 = [_rel(res["bf16x6"]["xhat"][t], o64["xhat"][t]) for t in range(8)]
     xt32 = [_rel(t32["xhat"][t], o64["xhat"][t]) for t in range(8)]
@@ -88,6 +96,8 @@ def test_headline_config_both_precisions():
     print("       bf16 engine vs emul twin %s" % ["%.1e" % e for e in x16e])
     print("gradients bf16 vs fp32 engine: vector %.3e, per-tensor median %.3e, p90 %.3e" % (
         gvec, float(np.median(per)), float(np.percentile(per, 90))))
+    print("gradients vs float64: bf16 engine vector %.3e (median %.3e) | bf16-emulating twin vector %.3e "
+          "(median %.3e) | bound 2 x the twin's" % (g16_64, med16, e_emg, medem))
     print("per-image ELBO bf16 vs fp32: max rel %.2e" % float(
         np.max(np.abs(res["bf16"]["elbo"] - res["fp32"]["elbo"]) / np.abs(res["fp32"]["elbo"]))))
     print("bf16x6: loss %.6f (rel %.2e vs f64); x_hat_t rel L2 vs float64 %s" % (
@@ -112,9 +122,11 @@ def test_headline_config_both_precisions():
     assert e16 <= max(2e-3, 3 * eem)
     for t in range(8):
         assert x16[t] <= max(2e-3, 3 * xem[t]), (t, x16[t], xem[t])
-    # bf16 is the NON-parity throughput mode: its gradients at this geometry are printed, not
-    # bounded (bench.py labels its `value` "parity": false).  bf16 rounding of the operands (~4e-3
-    # relative) is amplified ~3-4x per chain step (tests/test_chaos.py), so x_hat_7 itself moves by
-    # tens of percent and every gradient with it; the bf16 gradient bound is checked at B=8, T=3
-    # against the bf16-emulating twin (test_engine_gpu.py::test_bf16_mode_close_to_oracle)
-    assert np.isfinite(g16).all() and gvec < 10
+    # bf16 gradients: bf16 rounding of the operands (~4e-3 relative) is
+    # amplified ~3-4x per chain step (tests/test_chaos.py), so at T=8 the gradient of ANY bf16
+    # evaluation of this graph is far from float64 -- the emulating twin's own error is that scale.
+    # The engine's gradient must be within 2x of it (vector and per-tensor median), i.e. the engine
+    # rounds no worse than the operand rounding it declares.
+    assert np.isfinite(g16).all()
+    assert g16_64 <= 2 * e_emg, (g16_64, e_emg)
+    assert med16 <= 2 * max(medem, 1e-3), (med16, medem)

@@ -129,3 +129,74 @@ def test_pixelvae_full_size_properties():
     assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
     assert torch.isfinite(res[0][1]).all() and torch.isfinite(res[0][2]).all()
     pv.close()
+
+
+def test_pixelvae_init_every_step_matches_oracle():
+    """The reference's literal train() (sequential_vae.py:1360-1362): the head's data-dependent init
+    pass (pixel_cnn/pixelvae.py:103-105, nn.py:176-180 / :206-210) runs before EVERY iteration, on the
+    ground truth and the current z_e, with the pass's dropout.  PixelVAE(init_every_step=True), two
+    train() iterations with injected eps, uniforms and keep-masks (init and training pass):
+      * each iteration's init: the head's g, b after the pass vs oracle/pcnn.data_init on the head's
+        parameters before it (same z_e, masks, bf16 operand rounding): 3e-2 rel per tensor (the
+        moments of bf16-MFMA outputs in fp32 vs fp64; test_pcnn_gpu.py::test_data_init_matches_oracle);
+      * each iteration's loss vs oracle/pixelvae.forward_backward on the engine's pre-update
+        parameters and the post-init head: 1e-4 rel (the step-parity bound above);
+      * the init really re-ran: the second iteration's g differs from the first iteration's post-Adam g."""
+    pv, cd, ospec, hp, x, tgt, eps, u_mix, u_log, rng = _setup()
+    pv.init_every_step = True
+    pv.forward(x, tgt, eps, 0.6, u_mix, u_log)      # dry pass: mask shapes
+    masks = _masks(rng, pv)
+    init_masks = _masks(rng, pv)
+    snaps = []
+    orig = pv.init_pass
+
+    def rec_init(target, masks=None):
+        before = pv.head.params()
+        z = pv.vae.latent(pkg_mod("_lib").BUF_Z, pv.e).cpu().numpy().astype(np.float64)
+        orig(target, masks)
+        torch.cuda.synchronize()
+        snaps.append((before, z, pv.head.params(), {k: v.astype(np.float64) for k, v in pv.vae.param_dict().items()}))
+    pv.init_pass = rec_init
+    post_adam_g = None
+    for it in (1, 2):
+        pv.train(x, tgt, eps=eps, u_mix=u_mix, u_log=u_log, masks=masks, init_masks=init_masks)
+        torch.cuda.synchronize()
+        assert len(snaps) == it
+        before, z, after, eng = snaps[-1]
+        ref = opc.data_init(ospec, before, tgt, z, masks=init_masks, bf16=True)
+        gb = [k for k in ref if k.endswith("/g") or k.endswith("/b")]
+        worst = max(_rel(after[k], ref[k]) for k in gb)
+        if it == 2:
+            changed = max(_rel(after[k], post_adam_g[k]) for k in post_adam_g)
+            assert changed > 1e-4, changed  # the pass re-ran on the trained weights
+        reg = 1.0 - np.exp(-it / pv.cfg.reg_coeff_rate)
+        o = opv.forward_backward(cd, eng, ospec, after, x, tgt, eps, reg, u_mix, u_log, masks)
+        el = abs(pv.loss_value() - o["loss"]) / abs(o["loss"])
+        print("\ninit_every_step iteration %d: init g/b worst rel %.2e; loss %.6f oracle %.6f (rel %.2e)" % (
+            it, worst, pv.loss_value(), o["loss"], el))
+        assert worst < 3e-2
+        assert el <= 1e-4
+        hp_now = pv.head.params()
+        post_adam_g = {k: hp_now[k] for k in gb if k.endswith("/g")}
+    assert pv.vae.adam_updates == 2 and pv.head.iteration == 2
+    pv.close()
+
+
+def test_pixelvae_full_size_train_iterations_finite():
+    """c_pixelvae at BASELINE configs[4]'s benchmarked size (64x64, B = 128, the reference head):
+    four train() iterations (the bench's step: init pass once, both forwards and backwards, Adam, EMA)
+    stay finite, in the loss and in every parameter and gradient (the bench loop at full
+    size had no test; a mid-round r03 episode went non-finite)."""
+    torch.manual_seed(7)
+    PV = pkg_mod("pixelvae").PixelVAE
+    pv = PV("c_pixelvae", batch_size=128, dtype="bf16")
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    x = torch.rand(128, 64, 64, 3, device="cuda", generator=g) * 2 - 1
+    losses = [pv.train(x, x) for _ in range(4)]
+    torch.cuda.synchronize()
+    print("\nc_pixelvae B=128 train(): %s" % ["%.5f" % v for v in losses])
+    assert all(np.isfinite(losses))
+    assert torch.isfinite(pv.vae.params).all() and torch.isfinite(pv.vae.grads).all()
+    assert torch.isfinite(pv.head.P).all() and torch.isfinite(pv.head.G).all() and torch.isfinite(pv.head.ema).all()
+    pv.close()
