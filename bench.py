@@ -258,8 +258,11 @@ def run_pixelvae(args, cfgmod):
     """BASELINE configs[4] (CelebA + pixel_cnn decoder, 1 GPU): the c_pixelvae training step
     (pixelvae.PixelVAE.train: engine forward, head training pass with dropout, sampler + highway,
     both backwards, Adam + Polyak EMA) on a synthetic batch resident in HBM.  The roofline entry is
-    the head's conv kernel (pc_conv2_kernel: every forward convolution of the head, timed live by
-    event pairs around its first --probe-launches launches inside the timed region)."""
+    the head's forward convolution kernels (pc_conv3_kernel for the stride-1 halo convs,
+    pc_conv2_kernel for the rest: every forward convolution of the head, timed live by event pairs
+    around its first --probe-launches launches inside the timed region).  The per-step head FLOPs
+    (and so step_achieved_tflops) are ESTIMATED as 3x the forward convolution FLOPs (forward +
+    input gradient + weight gradient); only the forward launches are timed."""
     PV = importlib.import_module(PKG + ".pixelvae").PixelVAE
     B = args.batch or 128
     dtype = args.dtype
@@ -294,12 +297,14 @@ def run_pixelvae(args, cfgmod):
                    "image": [c.height, c.width, c.channels], "mc_steps": c.mc_steps, "parallelism": "dp1"},
         "elbo_per_img": round(pv.loss_value(), 5),
         "head_conv_tflop_per_step": round(head_flops / 1e12, 3),
+        "head_conv_tflop_method": "estimated: 3 x the counted forward convolution FLOPs (fwd + dgrad + wgrad)",
         "roofline": None if ach is None else {
             "bound": "mfma", "achieved": round(ach, 3), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 5), "traffic": None,
             "kernel": "pc_conv3_kernel + pc_conv2_kernel (PixelCNN++ head forward convolutions, all instances)",
             "timed_launches": len(probe), "avg_launch_us": round(pms * 1e3 / max(1, len(probe)), 2),
-            "step_achieved_tflops": round((head_flops + vae_flops) / (ms / 1e3) / 1e12, 3)},
+            "step_achieved_tflops": round((head_flops + vae_flops) / (ms / 1e3) / 1e12, 3),
+            "step_achieved_method": "estimated: head FLOPs = 3 x forward convolution FLOPs"},
         "cpu_baseline": None,
     }
     if not args.no_cpu_baseline:  # the fp64 CPU restatement of the same chain on a 2-image sample
