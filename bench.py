@@ -359,6 +359,9 @@ def main():
                     help="N>1: one all-reduce after the backward instead of per-step buckets during it")
     ap.add_argument("--no-fp32", action="store_true",
                     help="skip the parity-mode throughputs (parity_value: bf16x6, fp32_value: fp32 MFMA)")
+    ap.add_argument("--no-fp32-mode", action="store_true",
+                    help="skip only the fp32-MFMA throughput (fp32_value); parity_value (bf16x6) is still measured")
+    ap.add_argument("--parity-steps", type=int, default=10, help="timed steps of the parity-mode throughputs")
     ap.add_argument("--probe-launches", type=int, default=96,
                     help="dominant-kernel launches timed with HIP event pairs inside the timed region (the first N; "
                          "0 = every launch). Each pair is two event records on the kernel's stream, so timing all "
@@ -508,8 +511,9 @@ def main():
     fp32_value = fp32_ms = par_value = par_ms = None
     if world == 1 and args.dtype == "bf16" and not args.no_fp32:
         net.close()
-        par_value, par_ms = mode_throughput(cfg, SV, "bf16x6")
-        fp32_value, fp32_ms = mode_throughput(cfg, SV, "fp32")
+        par_value, par_ms = mode_throughput(cfg, SV, "bf16x6", steps=args.parity_steps)
+        if not args.no_fp32_mode:
+            fp32_value, fp32_ms = mode_throughput(cfg, SV, "fp32", steps=args.parity_steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, cfgname)
     if rank == 0:

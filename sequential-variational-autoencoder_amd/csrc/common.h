@@ -124,15 +124,18 @@ typedef unsigned long long u64;
 #define SVAE_WT 0
 #endif
 typedef int i32x4_st __attribute__((ext_vector_type(4)));
+// SVAE_WT bits: 1 = the 16-byte stores (st_out16), 2 = the 8-byte ones (st_out8), 4 = the 4-byte ones
+// (st_out): a 16-byte write-through store costs what a plain one does, an 8-byte one 2.7x and a
+// 4-byte one ~6x per byte (MI355X_MICROARCH.md, stores of each flavour)
 __device__ __forceinline__ void st_out(float* p, float v) {
-#if SVAE_WT
+#if SVAE_WT & 4
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #else
   *p = v;
 #endif
 }
 __device__ __forceinline__ void st_out8(void* p, u64 v) {
-#if SVAE_WT
+#if SVAE_WT & 2
   __hip_atomic_store((u64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #else
   *(u64*)p = v;
@@ -140,7 +143,7 @@ __device__ __forceinline__ void st_out8(void* p, u64 v) {
 }
 // 16-byte store at element offset `off` of a wave-uniform base (buffer descriptor from the base)
 __device__ __forceinline__ void st_out16(float* base, long long off, f32x4 v) {
-#if SVAE_WT
+#if SVAE_WT & 1
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_st, v), r, (int)(off * 4), 0, 16);
 #else

@@ -882,7 +882,7 @@ static bool trace_gemm() {
 static int gemm(svae_ctx* c, FwdArgs a, int groups) {
   if (c->m.g.split && a.Bh) {
     a.nsp = 3;
-    a.b_plane = c->wplane;
+    if (!a.b_plane) a.b_plane = c->wplane;  // (the packed output weights carry their own plane stride)
     a.part = c->slab;
     a.part_cap = c->slab_cap;
     if (!igemm_split_ok(a, groups)) {  // no split kernel for this shape: the fp32 kernels
@@ -951,8 +951,14 @@ static int gemm_nrb(svae_ctx* c, FwdArgs a, int groups) {
   return nrb_of(a);
 }
 static void wgemm(svae_ctx* c, const WgArgs& w, int groups) {
-  if (!c->m.g.bf16 || c->m.g.split) {  // (split mode: the tap-merged bf16 kernel has no split form)
+  if (!c->m.g.bf16) {
     wgrad(w, groups, c->st);
+    return;
+  }
+  if (c->m.g.split) {  // the tap-merged bf16 kernel on w.nsp operand planes (wgrad_bf16_kernel NSP)
+    WgArgs ws = w;
+    if (ws.nsp < 2) ws.nsp = 2;
+    wgrad_bf16(ws, groups, c->st);
     return;
   }
   if (c->probe.kid != KID_NONE) {  // algorithmic FLOPs: 2 * taps * M * N * row pixels
@@ -1083,7 +1089,7 @@ static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, V
   }
   // image-space stride-2 conv with Cin <= 3: im2col in LDS, MFMA over pixel chunks
   if ((bfk || c->m.g.split) && wgrad_smallc(w, groups, c->slab, c->slab_cap, dW, w_gs, c->st)) return 0;
-  if (bfk)  // tap-merged tiles; longer splits (less slab traffic)
+  if (bfk || c->m.g.split)  // tap-merged tiles; longer splits (less slab traffic)
     choose_split(w.rows, 1, wgrad_bf16_tiles(w), groups, 16LL * w.M * w.N, c->slab_cap, w.nsplit, w.chunk, 2048,
                  256);
   else
@@ -1135,10 +1141,12 @@ static int conv_dgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, c
   if (fu) fu->used = false;
   const int B = c->m.g.B;
   const float* W = c->P + L.ow;
-  if (L.cin % 4 != 0 && c->m.g.bf16 && !c->m.g.split && L.cout % 32 == 0 && !L.tr) {
-    // layer-0 conv input gradient (N = image channels): bf16 halo gather (CONVT mode from dpre)
+  if (L.cin % 4 != 0 && c->m.g.bf16 && L.cout % 32 == 0 && !L.tr) {
+    // layer-0 conv input gradient (N = image channels): bf16 small-N conv-T gather (CONVT mode from
+    // dpre); split mode: the same kernel on the three planes (convt_smalln_kernel<3>)
     FwdArgs a{};
     a.A = dpre; a.a_gs = dpre_gs; a.lda = L.cout; a.a_bf16 = dpre_bf(c, L);
+    a.B = W;  // (fp32 fallback of a split-mode shape without a split kernel)
     a.Bh = shadowN(c, L.ow); a.b_nk = 1; a.ldb = L.cout; a.b_tap = (long long)L.cin * L.cout; a.b_gs = w_gs;
     a.C = din.p; a.c_gs = din.gs; a.ldc = din.ld;
     a.N = L.cin; a.Cin = L.cout;
@@ -1264,6 +1272,7 @@ static int fc_bn_bwd(svae_ctx* c, const FcL& f, View in, View dy, View y, const 
   w.nsplit = 1;
   w.chunk = (B + 31) / 32 * 32;
   w.part = c->Gr + f.ow;  // single split over the batch rows: write dW [nin][nout] directly
+  w.nsp = c->m.g.split ? 3 : 1;  // split mode: six plane products (K = the batch: short sums)
   if ((r = on_side_q(c, sl.ready, [=] {
          wgemm(c, w, 1);
          return 0;
@@ -1398,6 +1407,7 @@ static void pack_out_all(svae_ctx* c, hipStream_t st) {
     a.P = c->P;
     a.C = g.C;
     a.F1 = g.F[1];
+    a.nsp = g.split ? 3 : 1;
     for (int i = 0; i < nt; ++i) {
       const int t = t0 + i;
       const GenStep& G = M.gen[t];
@@ -1406,7 +1416,7 @@ static void pack_out_all(svae_ctx* c, hipStream_t st) {
       a.owratio[i] = t >= 1 ? G.owratio : -1;
       a.obratio[i] = t >= 1 ? G.obratio : -1;
       a.wpack[i] = c->sb[t].wpack;
-      a.wpack_h[i] = (g.bf16 && !g.split) ? (__bf16*)c->sb[t].wpack_h : nullptr;
+      a.wpack_h[i] = g.bf16 ? (__bf16*)c->sb[t].wpack_h : nullptr;
     }
     pack_out(a, nt, st);
   }
@@ -1673,13 +1683,17 @@ static int engine_forward(svae_ctx* c) {
           HIPCHK(c, hipMemcpy2DAsync(s.wpack + g.C * F1, (size_t)C1 * F1 * sizeof(float), c->P + G.owratio,
                                      (size_t)F1 * sizeof(float), (size_t)F1 * sizeof(float), 16,
                                      hipMemcpyDeviceToDevice, st));
-        if (g.bf16 && !g.split) shadow_weights(s.wpack, s.wpack_h, nullptr, 16LL * C1 * F1, nullptr, 0, nullptr, 1, 0, st);
+        if (g.bf16)
+          shadow_weights(s.wpack, s.wpack_h, nullptr, 16LL * C1 * F1, nullptr, 0, nullptr, g.split ? 3 : 1,
+                         g.split ? 16LL * C1 * F1 : 0, st);
       }
       ConvGeom og{GM_CONVT, B, S[1], S[1], g.H, g.W, 2, 1, 4};
-      if (g.bf16 && !g.split) {  // bf16 halo gather-GEMM, N = C+1 of one 32-column tile, bias in the epilogue
+      if (g.bf16) {  // small-N conv-T gather (split mode: on the three planes of the packed weights), bias in the epilogue
         FwdArgs a{};
         a.A = cur.p; a.lda = F1; a.a_bf16 = cur.bf;
+        a.B = s.wpack;  // (fp32 fallback)
         a.Bh = s.wpack_h; a.b_nk = 1; a.ldb = F1; a.b_tap = (long long)C1 * F1;
+        a.b_plane = g.split ? 16LL * C1 * F1 : 0;
         a.C = s.a_out; a.ldc = C1;
         a.N = C1; a.Cin = F1;
         a.g = og;
@@ -2226,7 +2240,7 @@ static bool plan(svae_ctx* c) {
       maxact = std::max(maxact, 2 * n);
     }
     s.wpack = A(16LL * C1 * F[1] + 4);
-    s.wpack_h = A(8LL * C1 * F[1] + 4);
+    s.wpack_h = A((g.split ? 24LL : 8LL) * C1 * F[1] + 4);  // bf16 [tap][C+1][F1] (split mode: 3 planes)
     s.a_out = A((long long)B * g.H * g.W * C1);
     s.xhat = A((long long)B * g.H * g.W * g.C);
     s.rec_part = A((long long)B * c->out_nblk);

@@ -890,15 +890,20 @@ __global__ __launch_bounds__(256, (BN == 32 && S == 1) ? 2 : 1) void wgrad_halo_
 //   part[split][r][n] = sum_{p in split} G[src(p, tap)][m] * D[p][n]
 // (small-channel layers fill all waves; one dY tile feeds every tap of the row tile)
 // ---------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, bool VECG>
+// NSP > 1 (split mode, dtype bf16x6): both operands staged as NSP bf16 planes (opload.h split4) in ONE
+// LDS buffer (two barriers per K chunk instead of double buffering), mfma_split products: the FC
+// weight gradients (K = the batch: NSP = 3, six products) and the tap-merged conv weight gradients
+// without a halo kernel (NSP = 2, three products, as wgrad_halo2 / wgrad_smallc)
+template <int BM, int BN, int WM, int WN, bool VECG, int NSP = 1>
 __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
   constexpr int TM = BM / WM / 32;
   constexpr int TN = BN / WN / 32;
   constexpr int QMc = BM / 4, QNc = BN / 4;                  // channel quads
   constexpr int UA = QMc * (BKB / 4), UB = QNc * (BKB / 4);  // 4x4 units per tile
   constexpr int RA = (UA + 255) / 256, RB = (UB + 255) / 256;
-  __shared__ __attribute__((aligned(16))) __bf16 As[2][BM * ROWP];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[2][BN * ROWP];
+  constexpr int NBUF = NSP == 1 ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) __bf16 As[NBUF][NSP][BM * ROWP];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[NBUF][NSP][BN * ROWP];
 
   const ConvGeom& g = a.g;
   const int tid = threadIdx.x;
@@ -1021,7 +1026,14 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
         const bool rg = VECG && gbf;  // raw bf16 bits (the scalar gather path holds fp32 values)
         f32x4 col = {raw4_elem(va[i][0], c, rg), raw4_elem(va[i][1], c, rg), raw4_elem(va[i][2], c, rg),
                      raw4_elem(va[i][3], c, rg)};
-        *(bf16x4*)&As[buf][(mq * 4 + c) * ROWP + pq * 4] = __builtin_convertvector(col, bf16x4);
+        if constexpr (NSP == 1) {
+          *(bf16x4*)&As[buf][0][(mq * 4 + c) * ROWP + pq * 4] = __builtin_convertvector(col, bf16x4);
+        } else {
+          bf16x4 pl[NSP];
+          split4<NSP>(col, pl);
+#pragma unroll
+          for (int q = 0; q < NSP; ++q) *(bf16x4*)&As[buf][q][(mq * 4 + c) * ROWP + pq * 4] = pl[q];
+        }
       }
     }
 #pragma unroll
@@ -1033,7 +1045,14 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
       for (int c = 0; c < 4; ++c) {
         f32x4 col = {raw4_elem(vb[i][0], c, dbf), raw4_elem(vb[i][1], c, dbf), raw4_elem(vb[i][2], c, dbf),
                      raw4_elem(vb[i][3], c, dbf)};
-        *(bf16x4*)&Bs[buf][(nq * 4 + c) * ROWP + pq * 4] = __builtin_convertvector(col, bf16x4);
+        if constexpr (NSP == 1) {
+          *(bf16x4*)&Bs[buf][0][(nq * 4 + c) * ROWP + pq * 4] = __builtin_convertvector(col, bf16x4);
+        } else {
+          bf16x4 pl[NSP];
+          split4<NSP>(col, pl);
+#pragma unroll
+          for (int q = 0; q < NSP; ++q) *(bf16x4*)&Bs[buf][q][(nq * 4 + c) * ROWP + pq * 4] = pl[q];
+        }
       }
     }
   };
@@ -1052,23 +1071,36 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
   }
   __syncthreads();
   for (int kc = 0; kc < nk; ++kc) {
-    const int cur = kc & 1;
+    const int cur = NSP == 1 ? (kc & 1) : 0;
     if (kc + 1 < nk) load_tile(kc + 1);
 #pragma unroll
     for (int ks = 0; ks < BKB / 16; ++ks) {
-      bf16x8 af[TM], bfr[TN];
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm) af[tm] = *(const bf16x8*)&As[cur][(wm0 + tm * 32 + l32) * ROWP + ks * 16 + 8 * h];
-#pragma unroll
-      for (int tn = 0; tn < TN; ++tn) bfr[tn] = *(const bf16x8*)&Bs[cur][(wn0 + tn * 32 + l32) * ROWP + ks * 16 + 8 * h];
+      bf16x8 af[TM][NSP], bfr[TN][NSP];
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-        for (int tn = 0; tn < TN; ++tn)
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm], bfr[tn], acc[tm][tn], 0, 0, 0);
+        for (int q = 0; q < NSP; ++q)
+          af[tm][q] = *(const bf16x8*)&As[cur][q][(wm0 + tm * 32 + l32) * ROWP + ks * 16 + 8 * h];
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+        for (int q = 0; q < NSP; ++q)
+          bfr[tn][q] = *(const bf16x8*)&Bs[cur][q][(wn0 + tn * 32 + l32) * ROWP + ks * 16 + 8 * h];
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_split<NSP>(af[tm], bfr[tn], acc[tm][tn]);
     }
-    if (kc + 1 < nk) store_tile(cur ^ 1);
-    __syncthreads();
+    if constexpr (NSP == 1) {
+      if (kc + 1 < nk) store_tile(cur ^ 1);
+      __syncthreads();
+    } else {  // one buffer: every wave done reading it before the next chunk is stored
+      __syncthreads();
+      if (kc + 1 < nk) {
+        store_tile(0);
+        __syncthreads();
+      }
+    }
   }
   float* P = a.part + group * a.p_gs + (long long)split * Mtot * a.N;
 #pragma unroll
@@ -1428,13 +1460,15 @@ static int pertap_plan(const FwdArgs& a, int groups, int* ksplit) {
 }
 
 bool igemm_split_ok(const FwdArgs& a, int groups) {
-  return a.Bh && !a.a_bf16 && (dense_kw_ok(a, groups) || halo_kw_plan(a, groups) > 0);
+  return a.Bh && !a.a_bf16 && (dense_kw_ok(a, groups) || halo_kw_plan(a, groups) > 0 || smalln_ok(a));
 }
 
 int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit) {
-  if (a.nsp > 1) {  // split-bf16 planes: dense_kw or halo_kw only (igemm_split_ok)
+  if (a.nsp > 1) {  // split-bf16 planes: dense_kw, halo_kw or the small-N conv-T (igemm_split_ok)
     if (ksplit) *ksplit = 1;
-    return dense_kw_ok(a, groups) ? dense_kw_nrb(a) : halo_kw_plan(a, groups);
+    if (dense_kw_ok(a, groups)) return dense_kw_nrb(a);
+    const int nrb = halo_kw_plan(a, groups);
+    return nrb > 0 ? nrb : 0;  // (convt_smalln: no statistics)
   }
   if (smallc_ok(a, true)) {
     if (ksplit) *ksplit = 1;
@@ -1531,6 +1565,11 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
     return dense_kw_nrb(a);
   }
   if (a.nsp > 1) {  // igemm_split_ok: the wave-split halo gather takes every other split shape
+    if (halo_kw_plan(a, groups) <= 0 && smalln_ok(a)) {  // the N <= 16 stride-2 conv-T (output layer, layer-0 dgrad)
+      convt_smalln(a, groups, s);
+      if (after) hipEventRecord(after, s);
+      return 0;
+    }
     const int nrb = halo_kw(a, groups, s);
     if (after) hipEventRecord(after, s);
     return nrb;
@@ -1589,8 +1628,16 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
 template <int BM, int BN, int WM, int WN>
 static void launch_wg_bf16(const WgArgs& a, int groups, bool vec, hipStream_t s) {
   dim3 grid((a.ntap * a.M + BM - 1) / BM, (a.N + BN - 1) / BN, groups * a.nsplit);
-  if (vec) hipLaunchKernelGGL((wgrad_bf16_kernel<BM, BN, WM, WN, true>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((wgrad_bf16_kernel<BM, BN, WM, WN, false>), grid, dim3(256), 0, s, a);
+  if (a.nsp == 3) {
+    if (vec) hipLaunchKernelGGL((wgrad_bf16_kernel<BM, BN, WM, WN, true, 3>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_bf16_kernel<BM, BN, WM, WN, false, 3>), grid, dim3(256), 0, s, a);
+  } else if (a.nsp == 2) {
+    if (vec) hipLaunchKernelGGL((wgrad_bf16_kernel<BM, BN, WM, WN, true, 2>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_bf16_kernel<BM, BN, WM, WN, false, 2>), grid, dim3(256), 0, s, a);
+  } else {
+    if (vec) hipLaunchKernelGGL((wgrad_bf16_kernel<BM, BN, WM, WN, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_bf16_kernel<BM, BN, WM, WN, false>), grid, dim3(256), 0, s, a);
+  }
 }
 
 // tiles of the tap-merged weight-GEMM (for the split heuristic)

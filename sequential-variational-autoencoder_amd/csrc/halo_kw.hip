@@ -29,6 +29,9 @@ typedef float f32x8 __attribute__((ext_vector_type(8)));
 #ifndef KW_OCC
 #define KW_OCC 4   // waves per SIMD of the bf16-A 32-column instances (5 spills 38 VGPRs)
 #endif
+#ifndef KW_OCC_BR
+#define KW_OCC_BR 5  // the same with the two-tap B ring
+#endif
 
 struct KwArgs {
   FwdArgs f;
@@ -41,6 +44,7 @@ struct KwArgs {
   FastDiv d_win, d_pc, d_img, d_wr, d_rimg, d_q, d_qw;  // PR*PC, PC, Hr*Wr, Wr, R*Wr, (Ho/2)*(Wo/2), Wo/2
   int ntx, nty, ntz;  // tiles along rows / columns / (groups x classes)
   int tpb;            // tiles per block: 1 = one tile per block (3-D grid); > 1 = persistent (1-D grid)
+  int vec;            // 16-byte epilogue (every epilogue operand row 16-byte aligned; SVAE_KW_VEC)
 };
 
 namespace {
@@ -55,19 +59,113 @@ __device__ __forceinline__ long long kw_out_row(const KwArgs& h, const ConvGeom&
   return m;
 }
 
+// The epilogue with 16-byte accesses (h.vec: every operand row 16-byte aligned): thread = 4
+// consecutive columns of BM / (256 / (BN / 4)) rows.  The four waves' partial tiles (red, [4][BM][BN]
+// fp32) are summed in wave order, then bias / act / accumulate, one 16-byte store per row, the
+// forward BN statistics or the fused backward-BN partials per column (row groups summed in LDS in a
+// fixed order: deterministic).  Stores go through st_out16 (write-through in SVAE_WT builds: a
+// 16-byte sc1 store costs what a plain one does, a 4-byte one six times as much per byte).
+template <int BM, int BN>
+__device__ __forceinline__ void kw_epilogue_vec(const KwArgs& h, float* red, int tid, int m0, int n0, int group, int cls) {
+  const FwdArgs& a = h.f;
+  const ConvGeom& g = a.g;
+  constexpr int TPR = BN / 4;       // threads per row
+  constexpr int NRG = 256 / TPR;    // row groups
+  constexpr int NR = BM / NRG > 0 ? BM / NRG : 1;
+  const int c4 = (tid % TPR) * 4, rg = tid / TPR;
+  const int n = n0 + c4;
+  float* Cp = a.C + group * a.c_gs;
+  const bool bwm = a.bw.pre != nullptr;
+  const bool bwc = bwm && n < a.bw.C;  // (bw.C % 4 == 0: whole quads)
+  f32x4 bm = {0.f, 0.f, 0.f, 0.f}, bi = bm, bb = bm, biasv = bm;
+  if (bwc) {
+    bm = *(const f32x4*)&a.bw.mean[group * a.bw.ms_gs + n];
+    bi = *(const f32x4*)&a.bw.invstd[group * a.bw.ms_gs + n];
+    if (!a.bw.y) bb = *(const f32x4*)&a.bw.beta[group * a.bw.beta_gs + n];
+  }
+  if (a.bias) biasv = *(const f32x4*)&a.bias[group * a.bias_gs + n];
+  const float* bwpre = bwc ? a.bw.pre + group * a.bw.pre_gs : nullptr;
+  const float* bwy = (bwc && a.bw.y) ? a.bw.y + group * a.bw.y_gs : nullptr;
+  const bool rows_ok = rg < BM;  // (NRG > BM: the extra row groups idle)
+  long long orow[NR];
+  f32x4 cv[NR], pv[NR], yv[NR];
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {  // every global load before the first store
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    cv[i] = pv[i] = yv[i] = z;
+    orow[i] = 0;
+    if (!rows_ok) continue;
+    orow[i] = kw_out_row(h, g, cls, m0 + rg + i * NRG);
+    if (a.accumulate) cv[i] = *(const f32x4*)&Cp[orow[i] * a.ldc + n];
+    if (bwpre) pv[i] = *(const f32x4*)&bwpre[orow[i] * a.bw.ldp + n];
+    if (bwy) yv[i] = *(const f32x4*)&bwy[orow[i] * a.bw.ldy + n];
+  }
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    if (!rows_ok) continue;
+    const int m = rg + i * NRG;
+    f32x4 v = *(const f32x4*)&red[(0 * BM + m) * BN + c4];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) v += *(const f32x4*)&red[(w * BM + m) * BN + c4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float x = v[j];
+      if (!bwm) {
+        s1[j] += x;
+        s2[j] += x * x;
+      }
+      if (a.bias) x += biasv[j];
+      x = act_f(x, a.act);
+      if (a.accumulate) x += cv[i][j];
+      v[j] = x;
+      if (bwc) bw_term_v(x, pv[i][j], bm[j], bi[j], bb[j], bwy != nullptr, yv[i][j], a.bw.act, s1[j], s2[j]);
+    }
+    st_out16(Cp, orow[i] * a.ldc + n, v);
+  }
+  if (a.stats) {
+    __syncthreads();  // every wave is done reading red
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      red[rg * BN + c4 + j] = s1[j];
+      red[NRG * BN + rg * BN + c4 + j] = s2[j];
+    }
+    __syncthreads();
+    if (tid < BN) {
+      const int SC = bwm ? a.bw.C : a.N;  // stats columns (row-block stride 2*SC)
+      if (n0 + tid < SC) {
+        float sa = 0.f, qa = 0.f;
+        for (int j = 0; j < NRG; ++j) {
+          sa += red[j * BN + tid];
+          qa += red[NRG * BN + j * BN + tid];
+        }
+        const int rb = cls * h.ntx + m0 / BM;
+        stat_put(a.stats + (rb & (a.s_nsh - 1)) * a.s_sh + group * a.s_gs, n0 + tid, sa, qa);
+      }
+    }
+  }
+}
+
 // bf16-A 32-column instances at 4 waves per SIMD (<= 128 VGPRs, no spills; was 132 -> 3 waves): +0.3 %
 // of the step in a same-box A/B (tools/gpu/r02_libab.sh); the fp32-A ones would spill
 // NS = 3: the split-bf16 mode (dtype bf16x6, opload.h split8 / mfma_split): the fp32 window is
 // staged as three bf16 planes (one LDS buffer, restaged under a second barrier per chunk) and every
 // A x B fragment pair runs the six plane products; B comes from the three shadow planes
 // PST: the persistent form (h.tpb > 1 tiles per block, 1-D grid); without it the tile loop runs once
-template <int BM, int BN, bool S2T, bool ABF, int NS = 1, bool PST = false>
-__global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64 && !PST) ? KW_OCC : 2) void igemm_halo_kw_kernel(KwArgs h) {
+// BR: B fragments through a two-tap register ring (tap u + 1's loads issued under tap u's MFMAs; the
+// next chunk's first tap under the last) instead of a whole chunk of taps one chunk ahead: 16-tap
+// instances only; frees (NTW - 2) x TN x 2 x NS fragment registers (split mode: 48 VGPRs)
+template <int BM, int BN, bool S2T, bool ABF, int NS = 1, bool PST = false, bool BR = false>
+__global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64 && !PST) ? (BR ? KW_OCC_BR : KW_OCC)
+                                                                         : ((NS == 3 && BR) ? 3 : 2))
+void igemm_halo_kw_kernel(KwArgs h) {
   static_assert(NS == 1 || (NS == 3 && !ABF), "split planes from fp32 activations only");
+  static_assert(!BR || (!S2T && !PST), "the B ring: 16-tap, one-tile instances");
   constexpr int TM = BM / 32;
   constexpr int TN = BN / 32;
   constexpr int NTAP = S2T ? 4 : 16;
   constexpr int NTW = NTAP / 4;  // taps per wave (and B prefetch distance: one chunk ahead)
+  constexpr int NBQ = BR ? 2 : NTW;  // B fragment slots
   extern __shared__ __attribute__((aligned(16))) __bf16 ksm[];
   const FwdArgs& a = h.f;
   const ConvGeom& g = a.g;
@@ -200,8 +298,8 @@ __global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64 && !PST) ? KW_OCC
   }
 
   // ---- this wave's taps: t = wave * NTW + u; B fragments one chunk ahead ----
-  bf16x8 bq[NTW][TN][2][NS];
-  auto load_b = [&](const TileG& q, int u, int chunk) {
+  bf16x8 bq[NBQ][TN][2][NS];
+  auto load_b = [&](const TileG& q, int slot, int u, int chunk) {
     const __bf16* bptr = (const __bf16*)a.Bh + q.group * a.b_gs + (long long)(q.n0 + l32) * a.ldb + 8 * hh;
     const int t = wave * NTW + u;
     const int tap = S2T ? q.tap0 + 8 * (t >> 1) + 2 * (t & 1) : t;
@@ -212,14 +310,18 @@ __global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64 && !PST) ? KW_OCC
       for (int kq = 0; kq < 2; ++kq)
 #pragma unroll
         for (int p = 0; p < NS; ++p)
-          bq[u][tn][kq][p] = *(const bf16x8*)(bptr + p * a.b_plane + (long long)tn * 32 * a.ldb + off + kq * 16);
+          bq[slot][tn][kq][p] = *(const bf16x8*)(bptr + p * a.b_plane + (long long)tn * 32 * a.ldb + off + kq * 16);
   };
 
   TileG cur = tile_geo(bx, by, bz);
   set_window(cur);
   load_window(cur, 0);
+  if constexpr (BR) {
+    load_b(cur, 0, 0, 0);
+  } else {
 #pragma unroll
-  for (int u = 0; u < NTW; ++u) load_b(cur, u, 0);
+    for (int u = 0; u < NTW; ++u) load_b(cur, u, u, 0);
+  }
   if constexpr (NS == 1) {
     store_window(0);
     __syncthreads();
@@ -247,15 +349,23 @@ __global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64 && !PST) ? KW_OCC
         store_window(0);
         __syncthreads();
       }
-      if (has_next) {
-        load_window(cur, c + 1);
-      } else if (has_tile) {  // the next tile's first window, under this chunk's MFMAs and the epilogue
-        set_window(nxt);
-        load_window(nxt, 0);
+      if constexpr (!BR) {
+        if (has_next) {
+          load_window(cur, c + 1);
+        } else if (has_tile) {  // the next tile's first window, under this chunk's MFMAs and the epilogue
+          set_window(nxt);
+          load_window(nxt, 0);
+        }
       }
       const __bf16* W = ksm + buf * h.npix * KW_ROWP;
 #pragma unroll
       for (int u = 0; u < NTW; ++u) {
+        if constexpr (BR) {  // the ring: the next tap's B (this chunk's, or the next chunk's first)
+          if (u + 1 < NTW) load_b(cur, (u + 1) & 1, u + 1, c);
+          else if (has_next) load_b(cur, (u + 1) & 1, 0, c + 1);
+          // the next chunk's window after tap 1's B loads (in-order vmcnt: a later B wait also waits for it)
+          if (u == 0 && has_next) load_window(cur, c + 1);
+        }
         const int t = wave * NTW + u;
         const int shift = S2T ? toff0 + tsgn * ((t >> 1) * h.PC + (t & 1)) : toff0 + tsgn * ((t >> 2) * h.PC + (t & 3));
         const int sh = shift * KW_ROWP;
@@ -269,10 +379,12 @@ __global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64 && !PST) ? KW_OCC
 #pragma unroll
           for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-            for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_split<NS>(af[tm], bq[u][tn][kq], acc[tm][tn]);
+            for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_split<NS>(af[tm], bq[BR ? (u & 1) : u][tn][kq], acc[tm][tn]);
         }
-        if (has_next) load_b(cur, u, c + 1);
-        else if (has_tile) load_b(nxt, u, 0);
+        if constexpr (!BR) {
+          if (has_next) load_b(cur, u, u, c + 1);
+          else if (has_tile) load_b(nxt, u, u, 0);
+        }
       }
       if constexpr (NS == 1) {
         if (has_next) store_window(buf ^ 1);
@@ -293,6 +405,18 @@ __global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64 && !PST) ? KW_OCC
           red[(wave * BM + m) * BN + tn * 32 + l32] = acc[tm][tn][r];
         }
     __syncthreads();
+    if (h.vec) {  // 16-byte epilogue: 4 consecutive columns per thread (write-through-friendly stores)
+      kw_epilogue_vec<BM, BN>(h, red, tid, cur.m0, cur.n0, cur.group, cur.cls);
+      if (!has_tile) break;
+      __syncthreads();
+      cur = nxt;
+      ++t_cur;
+      if constexpr (NS == 1) {
+        store_window(0);
+        __syncthreads();
+      }
+      continue;
+    }
     constexpr int NRG = 256 / BN;  // row groups
     const int col = tid % BN, rg = tid / BN;
     const int n = n0 + col;
@@ -461,6 +585,19 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
   h.nty = (int)grid.y;
   h.ntz = (int)grid.z;
   h.tpb = 1;
+  {  // SVAE_KW_VEC=1: the 16-byte epilogue where every row of C (and of the BN-backward operands) is aligned
+    static const int vec_mode = [] {
+      const char* e = getenv("SVAE_KW_VEC");
+      return e ? atoi(e) : 0;
+    }();
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    bool ok = vec_mode != 0 && a.ldc % 4 == 0 && a.c_gs % 4 == 0 && al16(a.C) && (!a.bias || (al16(a.bias) && a.bias_gs % 4 == 0));
+    if (a.bw.pre)
+      ok = ok && a.bw.C % 4 == 0 && a.bw.ldp % 4 == 0 && a.bw.pre_gs % 4 == 0 && al16(a.bw.pre) && al16(a.bw.mean) &&
+           al16(a.bw.invstd) && a.bw.ms_gs % 4 == 0 &&
+           (a.bw.y ? (a.bw.ldy % 4 == 0 && a.bw.y_gs % 4 == 0 && al16(a.bw.y)) : (al16(a.bw.beta) && a.bw.beta_gs % 4 == 0));
+    h.vec = ok ? 1 : 0;
+  }
   // persistent form (SVAE_KW_PERSIST=1): where the tiles exceed the resident blocks, each block runs
   // a contiguous run of tiles with the next tile's window / B loads under the current tile's last
   // chunk and epilogue
@@ -478,21 +615,31 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
       grid = dim3((unsigned)((ntiles + h.tpb - 1) / h.tpb), 1, 1);
     }
   }
+  // SVAE_KW_BRING: the two-tap B register ring on the 16-tap instances (bit 0: split mode, bit 1: bf16)
+  static const int bring = [] {
+    const char* e = getenv("SVAE_KW_BRING");
+    return e ? atoi(e) : 0;
+  }();
   if (a.nsp > 1) {  // split-bf16 planes (fp32 A): 64 / 32-row tiles, 32 columns
     static bool attr = false;
     if (!attr) {
       for (const void* f : {(const void*)igemm_halo_kw_kernel<64, 32, true, false, 3>,
                             (const void*)igemm_halo_kw_kernel<64, 32, false, false, 3>,
                             (const void*)igemm_halo_kw_kernel<32, 32, true, false, 3>,
-                            (const void*)igemm_halo_kw_kernel<32, 32, false, false, 3>})
+                            (const void*)igemm_halo_kw_kernel<32, 32, false, false, 3>,
+                            (const void*)igemm_halo_kw_kernel<64, 32, false, false, 3, false, true>,
+                            (const void*)igemm_halo_kw_kernel<32, 32, false, false, 3, false, true>})
         hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
       attr = true;
     }
+    const bool br = (bring & 1) != 0;
     if (bm == 64) {
       if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, true, false, 3>), grid, dim3(256), lds, s, h);
+      else if (br) hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, false, false, 3, false, true>), grid, dim3(256), lds, s, h);
       else hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, false, false, 3>), grid, dim3(256), lds, s, h);
     } else {
       if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<32, 32, true, false, 3>), grid, dim3(256), lds, s, h);
+      else if (br) hipLaunchKernelGGL((igemm_halo_kw_kernel<32, 32, false, false, 3, false, true>), grid, dim3(256), lds, s, h);
       else hipLaunchKernelGGL((igemm_halo_kw_kernel<32, 32, false, false, 3>), grid, dim3(256), lds, s, h);
     }
     return a.nclass * (a.rows / bm);
@@ -503,6 +650,8 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
     else hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, false, true, 1, true>), grid, dim3(256), lds, s, h);    \
   } else if (a.a_bf16) {                                                                                     \
     if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<BM_, BN_, true, true>), grid, dim3(256), lds, s, h);    \
+    else if ((bring & 2) && BN_ == 32 && BM_ <= 64)                                                          \
+      hipLaunchKernelGGL((igemm_halo_kw_kernel<BM_, BN_, false, true, 1, false, true>), grid, dim3(256), lds, s, h); \
     else hipLaunchKernelGGL((igemm_halo_kw_kernel<BM_, BN_, false, true>), grid, dim3(256), lds, s, h);       \
   } else {                                                                                                   \
     if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<BM_, BN_, true, false>), grid, dim3(256), lds, s, h);   \

@@ -223,6 +223,7 @@ struct PackOutArgs {
   float* wpack[PACK_MAXT];
   __bf16* wpack_h[PACK_MAXT];           // nullptr in fp32 mode
   int C, F1;
+  int nsp;                              // bf16 planes (3 in the split mode, 16 (C+1) F1 apart)
 };
 void pack_out(const PackOutArgs& a, int nt, hipStream_t s);
 void output_fwd(const float* a, int B, int HW, int C, const float* xprev, const float* target, float lo, float hi,

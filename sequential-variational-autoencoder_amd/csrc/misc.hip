@@ -1187,7 +1187,14 @@ __global__ void pack_out_kernel(PackOutArgs a) {
       const int rem = i - tap * C1 * F1;
       const int co = rem / F1, ci = rem - co * F1;
       v = co < C ? wout[((long long)tap * C + co) * F1 + ci] : (wratio ? wratio[tap * F1 + ci] : 0.f);
-      if (a.wpack_h[t]) a.wpack_h[t][i] = (__bf16)v;
+      if (a.wpack_h[t]) {  // bf16 copy; split mode: plane q = bf16(v - the earlier planes)
+        float r = v;
+        for (int q = 0; q < a.nsp; ++q) {
+          const __bf16 b = (__bf16)r;
+          a.wpack_h[t][(long long)q * nw + i] = b;
+          r -= (float)b;
+        }
+      }
     } else {
       const int j = i - nw;
       v = j < C ? a.P[a.obout[t] + j] : ((j == C && a.obratio[t] >= 0) ? a.P[a.obratio[t]] : 0.f);

@@ -285,7 +285,25 @@ constexpr int SN_SQ = 2;     // window staging items per thread and batch (4 cos
 
 typedef float f32x8 __attribute__((ext_vector_type(8)));
 
+// NS = 3 (split mode, dtype bf16x6): the fp32 window is staged as three bf16 planes (opload.h split8),
+// B comes from the three weight planes (a.b_plane apart) and every fragment pair runs the six plane
+// products (mfma_split16): an fp32-accurate conv-T on bf16 MFMA
+template <int NS>
+__device__ __forceinline__ f32x4 mfma_split16(const bf16x8 (&x)[NS], const bf16x8 (&y)[NS], f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], y[0], acc, 0, 0, 0);
+  if constexpr (NS >= 3) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], y[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[1], y[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], y[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[2], y[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[1], y[1], acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+template <int NS>
 __global__ __launch_bounds__(256) void convt_smalln_kernel(FwdArgs a) {
+  static_assert(NS == 1 || NS == 3, "one plane or the split mode's three");
   extern __shared__ __attribute__((aligned(16))) __bf16 wsm[];
   const ConvGeom& g = a.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -304,6 +322,7 @@ __global__ __launch_bounds__(256) void convt_smalln_kernel(FwdArgs a) {
   const __bf16* Bw = (const __bf16*)a.Bh + group * a.b_gs;
   const int ky0 = (cy + g.pad) & 1, kx0 = (cx + g.pad) & 1;
   const bool nvalid = r16 < a.N;
+  const int wplane = PR * PC * SN_PITCH;  // LDS elements per window plane (NS = 3)
 
   f32x4 acc[SN_MAXT];
 #pragma unroll
@@ -331,15 +350,28 @@ __global__ __launch_bounds__(256) void convt_smalln_kernel(FwdArgs a) {
 #pragma unroll
       for (int i = 0; i < SN_SQ; ++i) {
         const int it = b0 + tid + 256 * i;
-        if (it < PR * PC * 4) *(bf16x8*)&wsm[(it >> 2) * SN_PITCH + (it & 3) * 8] = raw8_bf(lo[i], hi[i], abf);
+        if (it < PR * PC * 4) {
+          const int o = (it >> 2) * SN_PITCH + (it & 3) * 8;
+          if constexpr (NS == 1) {
+            *(bf16x8*)&wsm[o] = raw8_bf(lo[i], hi[i], abf);
+          } else {
+            bf16x8 pl[NS];
+            split8<NS>(lo[i], hi[i], pl);
+#pragma unroll
+            for (int q = 0; q < NS; ++q) *(bf16x8*)&wsm[q * wplane + o] = pl[q];
+          }
+        }
       }
     }
     // this class's 4 tap fragments of the chunk (columns >= N are zero)
-    bf16x8 bq[4];
+    bf16x8 bq[4][NS];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int tap = (ky0 + 2 * (t >> 1)) * 4 + kx0 + 2 * (t & 1);
-      bq[t] = nvalid ? *(const bf16x8*)(Bw + tap * a.b_tap + (long long)r16 * a.ldb + ch + 8 * kg) : bf16x8{};
+#pragma unroll
+      for (int q = 0; q < NS; ++q)
+        bq[t][q] = nvalid ? *(const bf16x8*)(Bw + q * a.b_plane + tap * a.b_tap + (long long)r16 * a.ldb + ch + 8 * kg)
+                          : bf16x8{};
     }
     __syncthreads();
 #pragma unroll
@@ -351,8 +383,10 @@ __global__ __launch_bounds__(256) void convt_smalln_kernel(FwdArgs a) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const int ty = t >> 1, tx = t & 1;
-          const bf16x8 af = *(const bf16x8*)&wsm[((wr - ty) * PC + wc - tx) * SN_PITCH + 8 * kg];
-          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bq[t], acc[i], 0, 0, 0);
+          bf16x8 af[NS];
+#pragma unroll
+          for (int q = 0; q < NS; ++q) af[q] = *(const bf16x8*)&wsm[q * wplane + ((wr - ty) * PC + wc - tx) * SN_PITCH + 8 * kg];
+          acc[i] = mfma_split16<NS>(af, bq[t], acc[i]);
         }
       }
     }
@@ -460,13 +494,17 @@ bool smalln_ok(const FwdArgs& a) {
   if (g.Ho != 2 * g.Hi || g.Wo != 2 * g.Wi || g.Ho % SN_R || g.Wi % 16) return false;
   if ((SN_R / 2) * (g.Wi / 16) > SN_MAXT) return false;
   if (a.ldb % 8 || a.b_tap % 8 || a.lda % 4) return false;  // 16-byte fragment / staging loads
-  return (SN_R / 2 + 2) * (g.Wi + 2) * SN_PITCH * 2 <= 64 * 1024 && SN_R * g.Wo * a.N * 4 <= 64 * 1024;
+  if (a.nsp > 1 && (a.nsp != 3 || a.a_bf16 || a.b_plane % 8)) return false;  // split: fp32 A, 3 planes
+  const int planes = a.nsp > 1 ? 3 : 1;
+  return (SN_R / 2 + 2) * (g.Wi + 2) * SN_PITCH * 2 * planes <= 64 * 1024 && SN_R * g.Wo * a.N * 4 <= 64 * 1024;
 }
 
 void convt_smalln(const FwdArgs& a, int groups, hipStream_t s) {
-  const int win = (SN_R / 2 + 2) * (a.g.Wi + 2) * SN_PITCH * 2;
+  const int planes = a.nsp > 1 ? 3 : 1;
+  const int win = (SN_R / 2 + 2) * (a.g.Wi + 2) * SN_PITCH * 2 * planes;
   const int tile = a.ldc == a.N ? SN_R * a.g.Wo * a.N * 4 : 0;  // the assembled output rows
   const int lds = win > tile ? win : tile;
   dim3 grid(a.g.nimg * (a.g.Ho / SN_R), 1, groups);
-  hipLaunchKernelGGL(convt_smalln_kernel, grid, dim3(256), lds, s, a);
+  if (planes == 3) hipLaunchKernelGGL(convt_smalln_kernel<3>, grid, dim3(256), lds, s, a);
+  else hipLaunchKernelGGL(convt_smalln_kernel<1>, grid, dim3(256), lds, s, a);
 }

@@ -1,0 +1,7 @@
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+SVAE_KW_BRING=3 timeout -k 10 600 python -u -m pytest tests/test_engine_gpu.py tests/test_golden_gpu.py tests/test_headline_gpu.py -x -q -s --timeout 500 --timeout-method thread > gpurun_out/r04_ring_tests.txt 2>&1 || { tail -30 gpurun_out/r04_ring_tests.txt; exit 1; }
+tail -2 gpurun_out/r04_ring_tests.txt
+grep -A12 "headline CelebA" gpurun_out/r04_ring_tests.txt
+bash tools/gpu/r04_ab.sh SVAE_KW_BRING=1 SVAE_KW_BRING=3 SVAE_KW_BRING=3@ab/br4.so

@@ -27,6 +27,6 @@ for line in r.stderr.splitlines():
 flt = sys.argv[2] if len(sys.argv) > 2 else ""
 for d in out:
     if flt in d["name"]:
-        print("%-60s VGPR %4s AGPR %4s spill %3s/%3s occ %s LDS %s" % (
-            d["name"][:60], d.get("VGPRs"), d.get("AGPRs"), d.get("VGPRs Spill"), d.get("SGPRs Spill"),
+        print("%-90s VGPR %4s AGPR %4s spill %3s/%3s occ %s LDS %s" % (
+            d["name"][:90], d.get("VGPRs"), d.get("AGPRs"), d.get("VGPRs Spill"), d.get("SGPRs Spill"),
             d.get("Occupancy [waves/SIMD]"), d.get("LDS Size [bytes/block]")))
