@@ -29,6 +29,15 @@ __device__ __forceinline__ f32x4 bn_y(f32x4 x, f32x4 m, f32x4 is, f32x4 b) {
 // a separate finalize launch per BN layer.
 #define AP_QB 64
 
+// SVAE_BN_W8=1: bf16-output BN passes with 8 channels per thread (one 16-byte store)
+static bool bn_w8() {
+  static const bool v = [] {
+    const char* e = getenv("SVAE_BN_W8");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 // shards so that at most ~16 row-blocks add into one accumulator line
 int bn_acc_shards(long long rowblocks) {
   int n = 1;
@@ -73,9 +82,10 @@ struct ApGrid {
   dim3 grid;
   int rpb;
 };
-static ApGrid ap_grid(long long rows, int C, int groups) {
-  const int Q = C / 4;
-  const int QB = Q < AP_QB ? Q : AP_QB;
+// W = channels per thread: 4 (one 16-byte fp32 quad), or 8 for bf16 outputs (one 16-byte bf16 store)
+static ApGrid ap_grid(long long rows, int C, int groups, int W = 4) {
+  const int Q = C / W;
+  const int QB = Q < AP_QB * 4 / W ? Q : AP_QB * 4 / W;
   const int RL = 256 / QB;
   const int gx = (Q + QB - 1) / QB;
   // >= rpt rows per thread (SVAE_AP_RPT, default 2) within a budget of SVAE_AP_CAP blocks (default
@@ -101,6 +111,9 @@ static ApGrid ap_grid(long long rows, int C, int groups) {
   return g;
 }
 
+// W = 8 (bf16 output, C % 8 == 0): each thread normalises 8 consecutive channels of a row and
+// writes them as one 16-byte bf16 vector (write-through-friendly; W = 4 writes 8 bytes)
+template <int W>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const float* pre, int ldp, long long pre_gs, long long rows,
                                                        int C, const u64* acc, long long acc_gs, long long sh,
                                                        int nsh, float eps,
@@ -111,17 +124,17 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* pre, int ldp
   __shared__ __attribute__((aligned(16))) float sm[2][AP_QB * 4];
   __shared__ u64 tot[4 * AP_QB * 4];
   const int group = blockIdx.z;
-  const int Q = C >> 2;
-  const int QB = Q < AP_QB ? Q : AP_QB;
+  const int Q = C / W;
+  const int QB = Q < AP_QB * 4 / W ? Q : AP_QB * 4 / W;
   const int RL = 256 / QB;
   const int tid = threadIdx.x, qi = tid % QB, rl = tid / QB;
   const int q0 = blockIdx.x * QB;
-  const int nch = min(QB * 4, C - q0 * 4);
+  const int nch = min(QB * W, C - q0 * W);
   mean += group * ms_gs;
   invstd += group * ms_gs;
-  if (acc) acc_gather(acc + group * acc_gs, sh, nsh, q0 * 4, nch, tot);
+  if (acc) acc_gather(acc + group * acc_gs, sh, nsh, q0 * W, nch, tot);
   if (tid < nch) {
-    const int c = q0 * 4 + tid;
+    const int c = q0 * W + tid;
     {
       float m, is;
       if (acc) {
@@ -146,13 +159,39 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* pre, int ldp
   __syncthreads();
   const int q = q0 + qi;
   if (rl >= RL || q >= Q) return;
-  const int c = q * 4;
+  const int c = q * W;
   pre += group * pre_gs;
   if (res) res += group * res_gs;
-  const f32x4 m = *(const f32x4*)&sm[0][qi * 4], is = *(const f32x4*)&sm[1][qi * 4];
-  const f32x4 b = *(const f32x4*)(beta + group * beta_gs + c);
   const long long r0 = (long long)blockIdx.y * rpb;
   const long long r1 = r0 + rpb < rows ? r0 + rpb : rows;
+  if constexpr (W == 8) {  // (out_bf16)
+    const f32x4 m0 = *(const f32x4*)&sm[0][qi * 8], is0 = *(const f32x4*)&sm[1][qi * 8];
+    const f32x4 m1 = *(const f32x4*)&sm[0][qi * 8 + 4], is1 = *(const f32x4*)&sm[1][qi * 8 + 4];
+    const f32x4 b0 = *(const f32x4*)(beta + group * beta_gs + c), b1 = *(const f32x4*)(beta + group * beta_gs + c + 4);
+#pragma unroll 4
+    for (long long r = r0 + rl; r < r1; r += RL) {
+      f32x4 y0 = bn_y(*(const f32x4*)(pre + r * ldp + c), m0, is0, b0);
+      f32x4 y1 = bn_y(*(const f32x4*)(pre + r * ldp + c + 4), m1, is1, b1);
+      if (res) {
+        y0 += *(const f32x4*)(res + r * ldr + c);
+        y1 += *(const f32x4*)(res + r * ldr + c + 4);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        y0[e] = act_f(y0[e], act);
+        y1[e] = act_f(y1[e], act);
+      }
+      const long long o = group * out_gs + r * ldo + c;  // bf16 elements (a multiple of 8)
+      const bf16x4_bn h0 = __builtin_convertvector(y0, bf16x4_bn), h1 = __builtin_convertvector(y1, bf16x4_bn);
+      const u64 u0 = __builtin_bit_cast(u64, h0), u1 = __builtin_bit_cast(u64, h1);
+      const f32x4 bits = {__uint_as_float((unsigned)u0), __uint_as_float((unsigned)(u0 >> 32)),
+                          __uint_as_float((unsigned)u1), __uint_as_float((unsigned)(u1 >> 32))};
+      st_out16(out, o / 2, bits);
+    }
+    return;
+  }
+  const f32x4 m = *(const f32x4*)&sm[0][qi * 4], is = *(const f32x4*)&sm[1][qi * 4];
+  const f32x4 b = *(const f32x4*)(beta + group * beta_gs + c);
 #pragma unroll 4
   for (long long r = r0 + rl; r < r1; r += RL) {
     f32x4 y = bn_y(*(const f32x4*)(pre + r * ldp + c), m, is, b);
@@ -171,8 +210,14 @@ void bn_apply(const float* pre, int ldp, long long pre_gs, long long rows, int C
               long long sh, int nsh, float eps, float* mean, float* invstd, long long ms_gs, const float* beta, long long beta_gs,
               const float* res, int ldr, long long res_gs, int act, float* out, int ldo, long long out_gs, int groups,
               hipStream_t s, int out_bf16) {
+  if (out_bf16 && bn_w8() && C % 8 == 0 && ldo % 8 == 0 && out_gs % 8 == 0 && ((uintptr_t)out & 15) == 0) {
+    const ApGrid g = ap_grid(rows, C, groups, 8);
+    hipLaunchKernelGGL(bn_apply_kernel<8>, g.grid, dim3(256), 0, s, pre, ldp, pre_gs, rows, C, acc, acc_gs, sh, nsh, eps,
+                       mean, invstd, ms_gs, beta, beta_gs, res, ldr, res_gs, act, out, ldo, out_gs, g.rpb, out_bf16);
+    return;
+  }
   const ApGrid g = ap_grid(rows, C, groups);
-  hipLaunchKernelGGL(bn_apply_kernel, g.grid, dim3(256), 0, s, pre, ldp, pre_gs, rows, C, acc, acc_gs, sh, nsh, eps, mean,
+  hipLaunchKernelGGL(bn_apply_kernel<4>, g.grid, dim3(256), 0, s, pre, ldp, pre_gs, rows, C, acc, acc_gs, sh, nsh, eps, mean,
                      invstd, ms_gs, beta, beta_gs, res, ldr, res_gs, act, out, ldo, out_gs, g.rpb, out_bf16);
 }
 
@@ -246,6 +291,8 @@ void bn_bwd_reduce(const float* dy, int lddy, long long dy_gs, const float* y, i
                      rows, C, mean, invstd, ms_gs, beta, beta_gs, act, acc, acc_gs, sh, nsh);
 }
 
+// W = 8 (bf16 dpre, C % 8 == 0): 8 channels per thread, one 16-byte bf16 store per row
+template <int W>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const float* dy, int lddy, long long dy_gs, const float* y, int ldy, long long y_gs, const float* pre, int ldp,
     long long pre_gs, long long rows, int C, const float* mean, const float* invstd, long long ms_gs,
@@ -256,15 +303,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   __shared__ __attribute__((aligned(16))) float sm[2][AP_QB * 4];
   __shared__ u64 tot[4 * AP_QB * 4];
   const int group = blockIdx.z;
-  const int Q = C >> 2;
-  const int QB = Q < AP_QB ? Q : AP_QB;
+  const int Q = C / W;
+  const int QB = Q < AP_QB * 4 / W ? Q : AP_QB * 4 / W;
   const int RL = 256 / QB;
   const int tid = threadIdx.x, qi = tid % QB, rl = tid / QB;
   const int q0 = blockIdx.x * QB;
-  const int nch = min(QB * 4, C - q0 * 4);
-  acc_gather(acc + group * acc_gs, sh, nsh, q0 * 4, nch, tot);
+  const int nch = min(QB * W, C - q0 * W);
+  acc_gather(acc + group * acc_gs, sh, nsh, q0 * W, nch, tot);
   if (tid < nch) {
-    const int c = q0 * 4 + tid;
+    const int c = q0 * W + tid;
     {
       const double sd = fx_get(tot + 4 * tid), sx = fx_get(tot + 4 * tid + 2);
       sm[0][tid] = (float)(sd / (double)rows);  // a = mean(dz)
@@ -275,11 +322,48 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   __syncthreads();
   const int q = q0 + qi;
   if (rl >= RL || q >= Q) return;
-  const int c = q * 4;
+  const int c = q * W;
   dy += group * dy_gs;
   if (y) y += group * y_gs;
   pre += group * pre_gs;
   if (dres) dres += group * dres_gs;
+  if constexpr (W == 8) {  // (dpre_bf16)
+    const long long r0 = (long long)blockIdx.y * rpb;
+    const long long r1 = r0 + rpb < rows ? r0 + rpb : rows;
+    f32x4 mm[2], iss[2], bbb[2], aa[2], bq[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      mm[h] = *(const f32x4*)(mean + group * ms_gs + c + 4 * h);
+      iss[h] = *(const f32x4*)(invstd + group * ms_gs + c + 4 * h);
+      bbb[h] = y ? f32x4{0.f, 0.f, 0.f, 0.f} : *(const f32x4*)(beta + group * beta_gs + c + 4 * h);
+      aa[h] = *(const f32x4*)&sm[0][qi * 8 + 4 * h];
+      bq[h] = *(const f32x4*)&sm[1][qi * 8 + 4 * h];
+    }
+#pragma unroll 2
+    for (long long r = r0 + rl; r < r1; r += RL) {
+      u64 u[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 g = *(const f32x4*)(dy + r * lddy + c + 4 * h);
+        const f32x4 xp = *(const f32x4*)(pre + r * ldp + c + 4 * h);
+        const f32x4 yy = y ? *(const f32x4*)(y + r * ldy + c + 4 * h) : bn_y(xp, mm[h], iss[h], bbb[h]);
+        const f32x4 xh = (xp - mm[h]) * iss[h];
+        f32x4 dz;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dz[e] = g[e] * dact_from_y(yy[e], act);
+        const f32x4 dp = iss[h] * (dz - aa[h] - xh * bq[h]);
+        u[h] = __builtin_bit_cast(u64, __builtin_convertvector(dp, bf16x4_bn));
+        if (dres) {
+          f32x4* d = (f32x4*)(dres + r * ldres + c + 4 * h);
+          *d = res_acc ? *d + dz : dz;
+        }
+      }
+      const f32x4 bits = {__uint_as_float((unsigned)u[0]), __uint_as_float((unsigned)(u[0] >> 32)),
+                          __uint_as_float((unsigned)u[1]), __uint_as_float((unsigned)(u[1] >> 32))};
+      st_out16(dpre, (group * dpre_gs + r * lddp + c) / 2, bits);
+    }
+    return;
+  }
   const f32x4 m = *(const f32x4*)(mean + group * ms_gs + c), is = *(const f32x4*)(invstd + group * ms_gs + c);
   const f32x4 bb = y ? f32x4{0.f, 0.f, 0.f, 0.f} : *(const f32x4*)(beta + group * beta_gs + c);
   const f32x4 a = *(const f32x4*)&sm[0][qi * 4], b = *(const f32x4*)&sm[1][qi * 4];
@@ -313,8 +397,15 @@ void bn_bwd_apply(const float* dy, int lddy, long long dy_gs, const float* y, in
                   long long acc_gs, long long sh, int nsh, float* dbeta, long long dbeta_gs, int act, float* dpre, int lddp,
                   long long dpre_gs, float* dres, int ldres, long long dres_gs, int res_acc, int groups,
                   hipStream_t s, int dpre_bf16) {
+  if (dpre_bf16 && bn_w8() && C % 8 == 0 && lddp % 8 == 0 && dpre_gs % 8 == 0 && ((uintptr_t)dpre & 15) == 0) {
+    const ApGrid g = ap_grid(rows, C, groups, 8);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<8>, g.grid, dim3(256), 0, s, dy, lddy, dy_gs, y, ldy, y_gs, pre, ldp, pre_gs,
+                       rows, C, mean, invstd, ms_gs, beta, beta_gs, acc, acc_gs, sh, nsh, dbeta, dbeta_gs, act, dpre,
+                       lddp, dpre_gs, dres, ldres, dres_gs, res_acc, g.rpb, dpre_bf16);
+    return;
+  }
   const ApGrid g = ap_grid(rows, C, groups);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, g.grid, dim3(256), 0, s, dy, lddy, dy_gs, y, ldy, y_gs, pre, ldp, pre_gs,
+  hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, g.grid, dim3(256), 0, s, dy, lddy, dy_gs, y, ldy, y_gs, pre, ldp, pre_gs,
                      rows, C, mean, invstd, ms_gs, beta, beta_gs, acc, acc_gs, sh, nsh, dbeta, dbeta_gs, act, dpre, lddp,
                      dpre_gs, dres, ldres, dres_gs, res_acc, g.rpb, dpre_bf16);
 }

@@ -955,6 +955,14 @@ static void wgemm(svae_ctx* c, const WgArgs& w, int groups) {
     wgrad(w, groups, c->st);
     return;
   }
+  static const bool split_wg = [] {  // SVAE_SPLIT_WG=0: the fp32 weight-GEMM in split mode (A/B)
+    const char* e = getenv("SVAE_SPLIT_WG");
+    return !(e && e[0] == '0');
+  }();
+  if (c->m.g.split && !split_wg) {
+    wgrad(w, groups, c->st);
+    return;
+  }
   if (c->m.g.split) {  // the tap-merged bf16 kernel on w.nsp operand planes (wgrad_bf16_kernel NSP)
     WgArgs ws = w;
     if (ws.nsp < 2) ws.nsp = 2;

@@ -1531,7 +1531,9 @@ int igemm_bf16_kid(const FwdArgs& a) {
 }
 
 int wgrad_bf16_kid(const WgArgs& a) {
-  const int scalar = !((a.M % 4 == 0) && (a.ldg % 4 == 0));
+  // the vector gather decodes a quad of 4 row-space pixels once: they must lie on one image row
+  // (row-space width a multiple of 4; a 2-wide layer took pixels of the next row at the wrong place)
+  const int scalar = !((a.M % 4 == 0) && (a.ldg % 4 == 0) && (a.g.mode == GM_DENSE || a.g.Wo % 4 == 0));
   if (a.N <= 32) return KID_WGRAD_BF16_128x32 + scalar;
   if (a.N <= 64) return KID_WGRAD_BF16_128x64 + scalar;
   return KID_WGRAD_BF16_128x128 + scalar;

@@ -615,10 +615,12 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
       grid = dim3((unsigned)((ntiles + h.tpb - 1) / h.tpb), 1, 1);
     }
   }
-  // SVAE_KW_BRING: the two-tap B register ring on the 16-tap instances (bit 0: split mode, bit 1: bf16)
+  // SVAE_KW_BRING: the two-tap B register ring on the 16-tap instances (bit 0: split mode, bit 1: bf16).
+  // Default 1: the split instances go from 2 to 3 waves per SIMD (bf16x6 step 18.74 -> 18.08 ms,
+  // profiles/r04_ab1.txt); the bf16 ones would need a fifth wave and spill (8 % slower)
   static const int bring = [] {
     const char* e = getenv("SVAE_KW_BRING");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 1;
   }();
   if (a.nsp > 1) {  // split-bf16 planes (fp32 A): 64 / 32-row tiles, 32 columns
     static bool attr = false;
