@@ -474,6 +474,15 @@ struct svae_ctx {
   static constexpr int NR = 6;  // "ready" events (re-recorded in turn: each is waited on right after its record)
   bool side = false;
   hipStream_t st2 = nullptr;
+  // SVAE_SIDE2=1: a second weight-gradient stream; the conv weight-GEMMs alternate between st2 and st2b
+  // (own split slab each).  A wgrad launch holds ~64 CUs, so two run side by side where one left
+  // the rest of the machine to latency-bound main-stream kernels.  Every ordering point that
+  // follows "the side stream" first merges st2b into st2 (side_merge).
+  hipStream_t st2b = nullptr;
+  float* slab2b = nullptr;
+  hipEvent_t ev_merge = nullptr;
+  unsigned side_rr = 0;
+  bool side_pin = false;  // the closure being handed over uses shared scratch: st2 only
   hipStream_t st3 = nullptr;  // split-latent FCs (fwd up front, bwd per level): no weight-GEMM queue ahead
   hipEvent_t ev_dz = nullptr, ev_j3 = nullptr;
   // recognition backward overlapped with the chain backward: groups of rec_group steps on st4 as soon
@@ -505,6 +514,7 @@ struct svae_ctx {
   // marker packet that drains the queue before the next dispatch (a 4-10 us gap per record).
   std::vector<std::function<int()>> side_q;
   int side_batch = 1;
+  bool side2 = false;  // SVAE_SIDE2 (read at svae_create, before the arena plan)
   bool fc_fuse = true;  // E.fc BN-backward sums fused into the top FC's input gradient (SVAE_BWFUSE_FC)
   static constexpr int NF = 4;
   hipEvent_t ev_flush[NF] = {};
@@ -766,11 +776,18 @@ struct Slot {
 // size) the main stream waits for the side stream to drain and the arena starts over
 static int side_flush(svae_ctx* c, hipStream_t also = nullptr);
 static int side_run_queued(svae_ctx* c);
+// st2 after everything enqueued so far on st2b (no-op without the second side stream)
+static void side_merge(svae_ctx* c) {
+  if (!c->st2b) return;
+  hipEventRecord(c->ev_merge, c->st2b);
+  hipStreamWaitEvent(c->st2, c->ev_merge, 0);
+}
 static float* arena_next(svae_ctx* c, float* base, long long cap, long long& off, long long n,
                          bool st3_reads = false) {
   n = (n + 63) / 64 * 64;
   if (off + n > cap) {
     side_flush(c);
+    if (!st3_reads) side_merge(c);
     hipEvent_t ev = st3_reads ? c->ev_drain3 : c->ev_drain;
     hipEventRecord(ev, st3_reads ? c->st3 : c->st2);
     hipStreamWaitEvent(c->st, ev, 0);
@@ -837,12 +854,14 @@ template <class Fn>
 static int on_side_q(svae_ctx* c, hipEvent_t ready, Fn&& fn) {
   if (!c->side || !ready || c->side_batch <= 1) {
     if (c->side && ready) {
+      const bool b = c->st2b && !c->side_pin && (c->side_rr++ & 1);
+      hipStream_t sx = b ? c->st2b : c->st2;
       hipEventRecord(ready, c->st);
-      hipStreamWaitEvent(c->st2, ready, 0);
+      hipStreamWaitEvent(sx, ready, 0);
       hipStream_t s0 = c->st;
       float* sl0 = c->slab;
-      c->st = c->st2;
-      c->slab = c->slab2;
+      c->st = sx;
+      c->slab = b ? c->slab2b : c->slab2;
       const int r = fn();
       c->st = s0;
       c->slab = sl0;
@@ -980,6 +999,18 @@ static void wgemm(svae_ctx* c, const WgArgs& w, int groups) {
   wgrad_bf16(w, groups, c->st);
 }
 
+// SVAE_DBG_SKIP (timing probe, WRONG RESULTS): bit 0 skips the forward BN apply of the layers whose
+// output only bf16 GEMMs read, bit 1 the backward BN apply of the conv layers without a shortcut --
+// the step time without the passes a consumer-side fold would remove (an upper bound of its gain);
+// bit 2 every conv weight gradient (side stream), bit 3 the per-bucket Adam of the chain steps
+static int dbg_skip() {
+  static const int v = [] {
+    const char* e = getenv("SVAE_DBG_SKIP");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 // Forward conv/convT + BN + act.  in: [B,hin,hin,cin] (ld), out view gets act(BN(pre)+res)
 static int conv_bn_act_fwd(svae_ctx* c, const ConvL& L, int groups, long long w_gs, View in, float* pre,
                            long long pre_gs, BNS bn, long long bn_gs, View res, int act, View out) {
@@ -1001,6 +1032,7 @@ static int conv_bn_act_fwd(svae_ctx* c, const ConvL& L, int groups, long long w_
   set_stats(a, acc);
   gemm(c, a, groups);
   const long long rows = (long long)B * L.hout * L.hout;
+  if ((dbg_skip() & 1) && out.bf && !res.p) return 0;  // TIMING PROBE ONLY (wrong results): no apply pass
   bn_apply(pre, L.cout, pre_gs, rows, L.cout, acc.p, acc.gs, acc.sh, acc.nsh, 1e-3f, bn.mean, bn.invstd, bn_gs, c->P + L.obeta, w_gs,
            res.p, res.ld, res.gs, act, out.p, out.ld, out.gs, groups, c->st, out.bf);
   return 0;
@@ -1028,9 +1060,11 @@ static int dpre_bf(const svae_ctx* c, const ConvL& L) {
 }
 
 // weight gradient of a conv/convT layer: dpre = grad wrt pre-BN output, in = layer input
+static int dbg_skip();
 static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, View in, const float* dpre,
                       long long dpre_gs, float* dW) {
   const int B = c->m.g.B;
+  if (dbg_skip() & 4) return 0;  // TIMING PROBE ONLY (wrong results): no conv weight gradients
   WgArgs w{};
   w.g.ksz = 4;
   w.g.pad = 1;
@@ -1230,6 +1264,7 @@ static int bn_act_bwd(svae_ctx* c, int groups, long long rows, int C, View dy, V
   if (!pre_reduced)
     bn_bwd_reduce(dy.p, dy.ld, dy.gs, yp, y.ld, y.gs, pre, ldp, pre_gs, rows, C, bn.mean, bn.invstd, bn_gs, beta, w_gs,
                   act, acc.p, acc.gs, acc.sh, acc.nsh, groups, c->st);
+  if ((dbg_skip() & 2) && !dres.p && rows > c->m.g.B) return 0;  // TIMING PROBE ONLY (wrong results)
   bn_bwd_apply(dy.p, dy.ld, dy.gs, yp, y.ld, y.gs, pre, ldp, pre_gs, rows, C, bn.mean, bn.invstd, bn_gs, beta, w_gs,
                acc.p, acc.gs, acc.sh, acc.nsh, c->Gr + beta_off, w_gs, act, dpre, C, dpre_gs, dres.p, dres.ld, dres.gs, res_acc, groups,
                c->st, dpre_bf16);
@@ -1328,13 +1363,14 @@ static int step_hook(svae_ctx* c, int t) {
     hipEventRecord(c->ev_hook, c->st);
     hipStreamWaitEvent(c->st2, c->ev_hook, 0);
     if (int r = side_run_queued(c)) return r;  // the step's queued weight gradients, before its bucket
+    side_merge(c);
     hipEventRecord(c->ev_j3, c->st3);  // the step's split-latent gradients
     hipStreamWaitEvent(c->st2, c->ev_j3, 0);
   }
   if (c->hook) c->hook(c->hook_user, t);
   // the bucket's update follows whatever exchange the hook ordered on the side stream; the
   // backward of steps < t reads neither theta_t nor its shadows
-  if (c->fa_on) adam_range(c, c->m.step_lo[t], c->m.step_hi[t], c->fa_lr, c->fa_step, c->fa_clip, c->st2);
+  if (c->fa_on && !(dbg_skip() & 8)) adam_range(c, c->m.step_lo[t], c->m.step_hi[t], c->fa_lr, c->fa_step, c->fa_clip, c->st2);
   return 0;
 }
 
@@ -1852,6 +1888,7 @@ static int engine_backward_pass(svae_ctx* c) {
   if (c->side) {  // the side stream starts after the forward (and anything before it)
     hipEventRecord(c->ev_start, st);
     hipStreamWaitEvent(c->st2, c->ev_start, 0);
+    if (c->st2b) hipStreamWaitEvent(c->st2b, c->ev_start, 0);
     // re-arm the slot-free events on the main stream: the previous backward's side-stream work
     // was joined into it, so "free" holds now, and every later wait depends only on work of this
     // pass (required when the step is captured into a graph)
@@ -1927,6 +1964,7 @@ static int engine_backward_pass(svae_ctx* c) {
       float* gratio = t >= 1 ? c->Gr + G.owratio : nullptr;
       float* gbout = c->Gr + G.obout;
       float* gbratio = t >= 1 ? c->Gr + G.obratio : nullptr;
+      c->side_pin = true;  // (colsum_small's cs_part scratch is shared by every step's closure)
       if ((r = on_side_q(c, c->ev_da_ready, [=]() mutable {
         w.part = c->slab;
         const int ns = (bfk || g.split) ? wgrad_smallc_part(w, 1, c->slab, c->slab_cap, c->st) : 0;
@@ -1937,6 +1975,7 @@ static int engine_backward_pass(svae_ctx* c) {
         colsum_small(da, C1, P0, M_out, c->cs_part, gbout, Cc, gbratio, c->st);
         return 0;
       }))) return r;
+      c->side_pin = false;
       // d cur = conv-T dgrad (CONV gather over da with the packed [tap][C+1][F1] weights as KN)
       FwdArgs a{};
       a.A = c->da; a.lda = C1;
@@ -2163,7 +2202,8 @@ static int engine_backward_pass(svae_ctx* c) {
   if ((r = side_flush(c))) return r;
   if (M.shared) {  // public gradient = fixed-order sum of the step copies (side stream joined first)
     if (c->side) {
-      hipEventRecord(c->ev_join, c->st2);
+      side_merge(c);
+    hipEventRecord(c->ev_join, c->st2);
       hipStreamWaitEvent(st, c->ev_join, 0);
       hipEventRecord(c->ev_j3, c->st3);
       hipStreamWaitEvent(st, c->ev_j3, 0);
@@ -2340,6 +2380,7 @@ static bool plan(svae_ctx* c) {
   c->slab_cap = 64LL << 20;
   c->slab = A(c->slab_cap);
   c->slab2 = A(c->slab_cap);
+  if (c->side2) c->slab2b = A(c->slab_cap);
   if (c->rec_group > 0 || c->rec_split) c->slab4 = A(c->slab_cap);
   c->cs_part = A(64 * 1024);
   c->zero_img = A((long long)B * g.H * g.W * g.C);
@@ -2399,6 +2440,8 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
     return fail(nullptr, SVAE_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
   }
   {
+    const char* s2 = getenv("SVAE_SIDE2");  // a second weight-gradient stream
+    c->side2 = s2 && s2[0] == '1';
     const char* rg = getenv("SVAE_REC_GROUP");  // recognition-backward group size (0 = batched after the chain)
     c->rec_group = rg ? atoi(rg) : 0;
     if (c->rec_group < 0 || c->m.g.plc) c->rec_group = 0;
@@ -2550,6 +2593,7 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
         ok = hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking) == hipSuccess;
       }
       ok = ok && hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking) == hipSuccess;
+      if (c->side2) ok = ok && hipStreamCreateWithFlags(&c->st2b, hipStreamNonBlocking) == hipSuccess;
       if (c->rec_group > 0 || c->rec_split)
         ok = ok && hipStreamCreateWithFlags(&c->st4, hipStreamNonBlocking) == hipSuccess;
       // cross-stream ordering on this device only: no system-scope fence (a system-scope release
@@ -2572,6 +2616,7 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
       for (int i = 0; i < svae_ctx::NF; ++i) mk(&c->ev_flush[i]);
       mk(&c->ev_rs);
       mk(&c->ev_rs2);
+      if (c->side2) mk(&c->ev_merge);
       {  // SVAE_SIDE_BATCH (read per context): weight-gradient layers per side-stream hand-over
         const char* e = getenv("SVAE_SIDE_BATCH");
         c->side_batch = e ? std::max(1, atoi(e)) : 1;
@@ -2590,7 +2635,7 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
 
 int svae_destroy(svae_ctx* c) {
   if (!c) return 0;
-  for (hipStream_t sx : {c->st2, c->st3, c->st4})
+  for (hipStream_t sx : {c->st2b, c->st2, c->st3, c->st4})
     if (sx) {
       hipStreamSynchronize(sx);
       hipStreamDestroy(sx);
@@ -2602,7 +2647,7 @@ int svae_destroy(svae_ctx* c) {
     if (ev) hipEventDestroy(ev);
   for (hipEvent_t ev : c->ev_flush)
     if (ev) hipEventDestroy(ev);
-  for (hipEvent_t ev : {c->ev_rs, c->ev_rs2})
+  for (hipEvent_t ev : {c->ev_rs, c->ev_rs2, c->ev_merge})
     if (ev) hipEventDestroy(ev);
   for (int i = 0; i < svae_ctx::NR; ++i) {
     if (c->ev_ready[i]) hipEventDestroy(c->ev_ready[i]);
@@ -2736,6 +2781,7 @@ int svae_backward(svae_ctx* c, void* stream) {
   int r = engine_backward(c);
   c->ext_dx = c->ext_dz = nullptr;  // one-shot
   if (c->side) {  // join: the side stream's weight gradients are ordered before later caller work
+    side_merge(c);
     hipEventRecord(c->ev_join, c->st2);
     hipStreamWaitEvent(c->st, c->ev_join, 0);
     hipEventRecord(c->ev_j3, c->st3);
@@ -2792,6 +2838,7 @@ int svae_backward_imp(svae_ctx* c, void* stream) {
   c->Gr = c->m.shared ? c->Gimp_v : c->Gimp_pub;
   int r = engine_backward(c);
   if (c->side) {
+    side_merge(c);
     hipEventRecord(c->ev_join, c->st2);
     hipStreamWaitEvent(c->st, c->ev_join, 0);
     hipEventRecord(c->ev_j3, c->st3);

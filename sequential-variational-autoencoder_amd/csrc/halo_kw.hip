@@ -32,6 +32,9 @@ typedef float f32x8 __attribute__((ext_vector_type(8)));
 #ifndef KW_OCC_BR
 #define KW_OCC_BR 5  // the same with the two-tap B ring
 #endif
+#ifndef KW_OCC_S32
+#define KW_OCC_S32 4  // split-mode 32-row instances with the B ring
+#endif
 
 struct KwArgs {
   FwdArgs f;
@@ -155,12 +158,13 @@ __device__ __forceinline__ void kw_epilogue_vec(const KwArgs& h, float* red, int
 // BR: B fragments through a two-tap register ring (tap u + 1's loads issued under tap u's MFMAs; the
 // next chunk's first tap under the last) instead of a whole chunk of taps one chunk ahead: 16-tap
 // instances only; frees (NTW - 2) x TN x 2 x NS fragment registers (split mode: 48 VGPRs)
-template <int BM, int BN, bool S2T, bool ABF, int NS = 1, bool PST = false, bool BR = false>
+// PI: window items per thread (npix * 4 <= 256 * PI); 3 frees 8 (fp32) window registers
+template <int BM, int BN, bool S2T, bool ABF, int NS = 1, bool PST = false, bool BR = false, int PI = KW_PI>
 __global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64 && !PST) ? (BR ? KW_OCC_BR : KW_OCC)
-                                                                         : ((NS == 3 && BR) ? 3 : 2))
+                                                                         : ((NS == 3 && BR) ? (BM == 32 ? KW_OCC_S32 : 3) : 2))
 void igemm_halo_kw_kernel(KwArgs h) {
   static_assert(NS == 1 || (NS == 3 && !ABF), "split planes from fp32 activations only");
-  static_assert(!BR || (!S2T && !PST), "the B ring: 16-tap, one-tile instances");
+  static_assert(!BR || !S2T, "the B ring: 16-tap instances");
   constexpr int TM = BM / 32;
   constexpr int TN = BN / 32;
   constexpr int NTAP = S2T ? 4 : 16;
@@ -223,7 +227,7 @@ void igemm_halo_kw_kernel(KwArgs h) {
     tsgn = -1;
   }
 
-  int woff[KW_PI];
+  int woff[PI];
   auto set_window = [&](const TileG& q) {  // window item offsets of tile q (igemm_halo_kernel's origin)
     int oy_min, ox_min;
     if (S2T) {
@@ -240,7 +244,7 @@ void igemm_halo_kw_kernel(KwArgs h) {
     const int ry0 = fdiv(q.m0 - img0 * per_img, h.d_wr);
     const int iy_base = ry0 * h.sy + oy_min;
 #pragma unroll
-    for (int i = 0; i < KW_PI; ++i) {
+    for (int i = 0; i < PI; ++i) {
       const int it = tid + 256 * i;
       woff[i] = -2;  // -2: no item, -1: zero (outside the image)
       if (it < h.npix * 4) {
@@ -255,11 +259,11 @@ void igemm_halo_kw_kernel(KwArgs h) {
       }
     }
   };
-  f32x4 wv[KW_PI][2];
+  f32x4 wv[PI][2];
   auto load_window = [&](const TileG& q, int chunk) {
     const long long ac = q.group * a.a_gs + chunk * KW_CK;
 #pragma unroll
-    for (int i = 0; i < KW_PI; ++i) {
+    for (int i = 0; i < PI; ++i) {
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
       wv[i][0] = z;
       wv[i][1] = z;
@@ -270,7 +274,7 @@ void igemm_halo_kw_kernel(KwArgs h) {
   auto store_window = [&](int buf) {
     __bf16* W = ksm + buf * h.npix * KW_ROWP;
 #pragma unroll
-    for (int i = 0; i < KW_PI; ++i) {
+    for (int i = 0; i < PI; ++i) {
       const int it = tid + 256 * i;
       if (woff[i] < -1) continue;
       const int o = (it >> 2) * KW_ROWP + (it & 3) * 8;
@@ -363,8 +367,17 @@ void igemm_halo_kw_kernel(KwArgs h) {
         if constexpr (BR) {  // the ring: the next tap's B (this chunk's, or the next chunk's first)
           if (u + 1 < NTW) load_b(cur, (u + 1) & 1, u + 1, c);
           else if (has_next) load_b(cur, (u + 1) & 1, 0, c + 1);
-          // the next chunk's window after tap 1's B loads (in-order vmcnt: a later B wait also waits for it)
-          if (u == 0 && has_next) load_window(cur, c + 1);
+          else if (has_tile) load_b(nxt, (u + 1) & 1, 0, 0);  // persistent: the next tile's first tap
+          // the next chunk's (or tile's) window after tap 1's B loads (in-order vmcnt: a later B wait
+          // also waits for it)
+          if (u == 0) {
+            if (has_next) {
+              load_window(cur, c + 1);
+            } else if (has_tile) {
+              set_window(nxt);
+              load_window(nxt, 0);
+            }
+          }
         }
         const int t = wave * NTW + u;
         const int shift = S2T ? toff0 + tsgn * ((t >> 1) * h.PC + (t & 1)) : toff0 + tsgn * ((t >> 2) * h.PC + (t & 3));
@@ -504,6 +517,23 @@ static int kw_bn_mode() {  // SVAE_KW_BN: 32 (default) or 64 column tiles
   return v;
 }
 
+static bool split_pi3() {  // SVAE_KW_PI3=0: split instances keep 4 window items per thread
+  static const bool v = [] {
+    const char* e = getenv("SVAE_KW_PI3");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+// split mode: SVAE_KW_SPLIT_BM=32 takes 32-row tiles (4 waves per SIMD) instead of 64 where both fit
+static int split_bm_max() {
+  static const int v = [] {
+    const char* e = getenv("SVAE_KW_SPLIT_BM");
+    return e ? atoi(e) : 64;
+  }();
+  return v;
+}
+
 static bool kw_plan(const FwdArgs& a, int groups, KwArgs* out, int* bm_out, int* bn_out, size_t* lds_out) {
   const ConvGeom& g = a.g;
   if (g.mode == GM_DENSE || g.ksz != 4 || g.pad != 1 || !a.Bh || a.Cin % KW_CK != 0 || a.N % 32 != 0) return false;
@@ -549,7 +579,7 @@ static bool kw_plan(const FwdArgs& a, int groups, KwArgs* out, int* bm_out, int*
     *bn_out = bn;
     // NS = 1: two window buffers; NS = 3 (split planes): one buffer of three planes
     const int wbufs = a.nsp > 1 ? 3 : 2;
-    if (a.nsp > 1 && (a.a_bf16 || bm > 64)) continue;  // split instances: fp32 A, 32 / 64-row tiles
+    if (a.nsp > 1 && (a.a_bf16 || bm > 64 || bm > split_bm_max())) continue;  // split instances: fp32 A, 32 / 64-row tiles
     *lds_out = std::max((size_t)(wbufs * h.npix) * KW_ROWP * sizeof(__bf16), (size_t)4 * bm * bn * sizeof(float));
     return true;
   }
@@ -630,17 +660,44 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
                             (const void*)igemm_halo_kw_kernel<32, 32, true, false, 3>,
                             (const void*)igemm_halo_kw_kernel<32, 32, false, false, 3>,
                             (const void*)igemm_halo_kw_kernel<64, 32, false, false, 3, false, true>,
-                            (const void*)igemm_halo_kw_kernel<32, 32, false, false, 3, false, true>})
+                            (const void*)igemm_halo_kw_kernel<32, 32, false, false, 3, false, true>,
+                            (const void*)igemm_halo_kw_kernel<64, 32, false, false, 3, false, true, 3>,
+                            (const void*)igemm_halo_kw_kernel<32, 32, false, false, 3, false, true, 3>})
         hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
       attr = true;
     }
     const bool br = (bring & 1) != 0;
+    const bool pi3 = h.npix * 4 <= 256 * 3 && split_pi3();
+    // SVAE_KW_PERSIST_SPLIT=k: the 64-row split ring instances persistent over 256 x 3 x k blocks (the
+    // next tile's window and first B fragments load under the current tile's last chunk)
+    static const int persist_split = [] {
+      const char* e = getenv("SVAE_KW_PERSIST_SPLIT");
+      return e ? atoi(e) : 0;
+    }();
+    if (persist_split && br && pi3 && bm == 64 && !s2t) {
+      const long long slots = 256LL * 3 * persist_split;
+      const long long ntiles = (long long)h.ntx * h.nty * h.ntz;
+      if (ntiles > slots) {
+        h.tpb = (int)((ntiles + slots - 1) / slots);
+        grid = dim3((unsigned)((ntiles + h.tpb - 1) / h.tpb), 1, 1);
+        static bool attrp = false;
+        if (!attrp) {
+          hipFuncSetAttribute((const void*)igemm_halo_kw_kernel<64, 32, false, false, 3, true, true, 3>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+          attrp = true;
+        }
+        hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, false, false, 3, true, true, 3>), grid, dim3(256), lds, s, h);
+        return a.nclass * (a.rows / bm);
+      }
+    }
     if (bm == 64) {
       if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, true, false, 3>), grid, dim3(256), lds, s, h);
+      else if (br && pi3) hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, false, false, 3, false, true, 3>), grid, dim3(256), lds, s, h);
       else if (br) hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, false, false, 3, false, true>), grid, dim3(256), lds, s, h);
       else hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, false, false, 3>), grid, dim3(256), lds, s, h);
     } else {
       if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<32, 32, true, false, 3>), grid, dim3(256), lds, s, h);
+      else if (br && pi3) hipLaunchKernelGGL((igemm_halo_kw_kernel<32, 32, false, false, 3, false, true, 3>), grid, dim3(256), lds, s, h);
       else if (br) hipLaunchKernelGGL((igemm_halo_kw_kernel<32, 32, false, false, 3, false, true>), grid, dim3(256), lds, s, h);
       else hipLaunchKernelGGL((igemm_halo_kw_kernel<32, 32, false, false, 3>), grid, dim3(256), lds, s, h);
     }

@@ -167,3 +167,19 @@ def test_fc_bn_backward_fusion_is_bitwise(preset, monkeypatch):
     assert changed > 0
     assert l0 == l1, (l0, l1)
     np.testing.assert_array_equal(p0, p1)
+
+
+@pytest.mark.parametrize("preset,dtype", [("tiny", "bf16"), ("celeba", "bf16"), ("tiny", "bf16x6"), ("celeba", "bf16x6"),
+                                          ("tiny_homog", "bf16")])
+@pytest.mark.parametrize("fused", [False, True])
+def test_second_side_stream_is_bitwise(preset, dtype, fused, monkeypatch):
+    """SVAE_SIDE2=1 alternates the conv weight-GEMMs between two side streams (own split slab each;
+    engine.cpp side_merge orders the per-bucket Adam, the DP hook and the final join after both):
+    the same kernels on the same data, so three training steps equal the one-stream run bit for bit."""
+    monkeypatch.setenv("SVAE_SIDE2", "0")
+    p0, l0, _ = _run(preset, dtype, fused, {})
+    monkeypatch.setenv("SVAE_SIDE2", "1")
+    p1, l1, changed = _run(preset, dtype, fused, {})
+    assert changed > 0
+    assert l0 == l1, (l0, l1)
+    np.testing.assert_array_equal(p0, p1)
