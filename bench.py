@@ -32,7 +32,14 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no 2:1 s
 # wgrad_halo2_kernel) is reported as the secondary entry.
 DOMINANT_KID = "KID_HALO_KW"
 SECONDARY_KID = "KID_WHALO2_S1"
-PMC_FILE = "profiles/r03_v5_pmc_traffic.json"  # tools/gpu/r03_final.sh (bench command, two passes, calibrated FETCH rules)
+# PMC summaries (tools/pmc_traffic.py: FETCH_SIZE / WRITE_SIZE passes of the same bench command, calibrated
+# FETCH rules) per workload; a workload never borrows another's traffic (LSUN read CelebA's)
+PMC_FILES = {
+    "celeba/bf16": ["profiles/r04_final_pmc_traffic.json", "profiles/r03_v5_pmc_traffic.json"],
+    "celeba/bf16x6": ["profiles/r04_final_x6_pmc_traffic.json"],
+    "lsun/bf16": ["profiles/r04_final_lsun_pmc_traffic.json"],
+    "c_pixelvae/bf16": ["profiles/r04_final_pv_pmc_traffic.json"],
+}
 
 
 # metric / workload per preset (BASELINE.json configs[1] is the headline: CelebA B=128)
@@ -159,15 +166,14 @@ def isolated_wgrad(L, cfg, iters=20):
                        "included), same shapes and operand storage; the live figure above is the in-step one")
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, key="celeba/bf16"):
     """HBM bytes per launch of `kernel` (a family: every template instance whose name starts with
-    the kernel's base name, weighted by dispatch count) from the newest committed PMC summary
-    (tools/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of the bench command,
-    the gfx950 FETCH correction per kernel as recorded there), or (None, None)."""
-    import glob
+    the kernel's base name, weighted by dispatch count) from the committed PMC summary of this
+    workload (`key` = config/dtype; tools/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE rocprofv3
+    passes of the bench command, the gfx950 FETCH correction per kernel as recorded there), or
+    (None, None) when that workload has none."""
     base = kernel.split("<")[0].split(" ")[0]
-    # the PMC passes of this bench command at the current code first, then any other summary
-    paths = [os.path.join(ROOT, PMC_FILE)] + sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True)
+    paths = [os.path.join(ROOT, p) for p in PMC_FILES.get(key, [])]
     for path in paths:
         try:
             with open(path) as f:
@@ -231,11 +237,14 @@ def cpu_baseline(cfg, cfgname, target_sec=20.0, max_steps=3):
                                                 os.environ.get("OMP_NUM_THREADS", "unset")))
 
 
-def mode_throughput(cfg, SV, dtype, steps=10, warmup=3):
+def mode_throughput(cfg, SV, dtype, steps=10, warmup=3, probe_kid=None, probe_launches=96):
     """images/sec of the same training step in another precision mode: "fp32" (fp32 MFMA) or
     "bf16x6" (split-bf16 MFMA, the fp32-accurate mode held to the fp32 parity bounds in
-    tests/test_headline_gpu.py)."""
+    tests/test_headline_gpu.py).  probe_kid: the first probe_launches launches of that kernel family
+    inside the timed steps are bracketed by HIP event pairs (svae_probe_begin); returns
+    (images/s, ms/step, probe dict or None)."""
     from dataclasses import replace
+    L = importlib.import_module(PKG + "._lib")
     c32 = replace(cfg, dtype=dtype)
     net = SV(c32, seed=0)
     g = torch.Generator(device="cuda")
@@ -245,13 +254,24 @@ def mode_throughput(cfg, SV, dtype, steps=10, warmup=3):
     for it in range(1, warmup + steps + 1):
         if it == warmup + 1:
             torch.cuda.synchronize()
+            if probe_kid is not None:
+                L.check(L.lib().svae_probe_begin(net.ctx, probe_kid, probe_launches), net.ctx)
             t0 = time.perf_counter()
         net.forward(x, x, None, 1.0 - math.exp(-it / c32.reg_coeff_rate))
         net.backward_apply(c32.learning_rate, it)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    probe = None
+    if probe_kid is not None:
+        n, nt = ctypes.c_int64(), ctypes.c_int64()
+        fl, ms_k = ctypes.c_double(), ctypes.c_double()
+        L.check(L.lib().svae_probe_end(net.ctx, ctypes.byref(n), ctypes.byref(nt), ctypes.byref(fl),
+                                       ctypes.byref(ms_k)), net.ctx)
+        if nt.value > 0:
+            probe = dict(kernel=L.lib().svae_kernel_name(probe_kid).decode(), launches_per_step=n.value / steps,
+                         timed=nt.value, flops=fl.value, ms=ms_k.value)
     net.close()
-    return c32.batch * steps / dt, dt / steps * 1e3
+    return c32.batch * steps / dt, dt / steps * 1e3, probe
 
 
 def run_pixelvae(args, cfgmod):
@@ -460,7 +480,7 @@ def main():
                                        ctypes.byref(ms_k)), net.ctx)
         if nt.value > 0:
             ach2 = fl.value / (ms_k.value / 1e3) / 1e12
-            tr2, tsrc2 = pmc_traffic(L.lib().svae_kernel_name(kid2).decode())
+            tr2, tsrc2 = pmc_traffic(L.lib().svae_kernel_name(kid2).decode(), args.config + "/" + args.dtype)
             probe2 = dict(kernel=L.lib().svae_kernel_name(kid2).decode(), achieved=round(ach2, 3),
                           frac=round(ach2 / BF16_MFMA_PEAK_TFLOPS, 5), launches_per_step=n.value / 2,
                           avg_launch_us=round(ms_k.value * 1e3 / nt.value, 2), timed_launches=nt.value,
@@ -486,7 +506,7 @@ def main():
         # (2*taps*M*N*pixels) / sum of per-launch event durations
         ach = probe["flops"] / (probe["ms"] / 1e3) / 1e12
         avg_us = probe["ms"] * 1e3 / probe["timed"]
-        traffic, tsrc = pmc_traffic(probe["kernel"])
+        traffic, tsrc = pmc_traffic(probe["kernel"], args.config + "/" + args.dtype)
         roof = dict(bound="mfma", achieved=round(ach, 3), peak=BF16_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
                     frac=round(ach / BF16_MFMA_PEAK_TFLOPS, 5), traffic=traffic,
                     kernel=probe["kernel"], launches_per_step=probe["launches"] / args.steps,
@@ -508,12 +528,27 @@ def main():
     if rank == 0 and roof is not None and probe2 is not None:
         probe2["isolated"] = isolated_wgrad(L, cfg) if args.dtype == "bf16" else None
         roof["secondary"] = probe2
-    fp32_value = fp32_ms = par_value = par_ms = None
+    fp32_value = fp32_ms = par_value = par_ms = par_roof = None
     if world == 1 and args.dtype == "bf16" and not args.no_fp32:
         net.close()
-        par_value, par_ms = mode_throughput(cfg, SV, "bf16x6", steps=args.parity_steps)
+        par_value, par_ms, par_probe = mode_throughput(cfg, SV, "bf16x6", steps=args.parity_steps,
+                                                       probe_kid=getattr(L, DOMINANT_KID),
+                                                       probe_launches=args.probe_launches or 96)
+        if par_probe is not None:  # the split gather: useful (algorithmic) and issued (6 products) MFMA rates
+            use = par_probe["flops"] / (par_probe["ms"] / 1e3) / 1e12
+            tr_x6, tsrc_x6 = pmc_traffic(par_probe["kernel"], args.config + "/bf16x6")
+            par_roof = {"bound": "mfma", "kernel": par_probe["kernel"] + " (split planes: 6 bf16 MFMAs per fragment pair)",
+                        "achieved": round(use, 3), "issued": round(6 * use, 3), "peak": BF16_MFMA_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(use / BF16_MFMA_PEAK_TFLOPS, 5),
+                        "frac_issued": round(6 * use / BF16_MFMA_PEAK_TFLOPS, 5),
+                        "launches_per_step": par_probe["launches_per_step"], "timed_launches": par_probe["timed"],
+                        "avg_launch_us": round(par_probe["ms"] * 1e3 / par_probe["timed"], 2),
+                        "flops_per_launch": round(par_probe["flops"] / par_probe["timed"]),
+                        "traffic": tr_x6, "traffic_source": tsrc_x6,
+                        "step_achieved_tflops": round(flops_img * par_value / 1e12, 3),
+                        "step_frac": round(flops_img * par_value / 1e12 / BF16_MFMA_PEAK_TFLOPS, 5)}
         if not args.no_fp32_mode:
-            fp32_value, fp32_ms = mode_throughput(cfg, SV, "fp32", steps=args.parity_steps)
+            fp32_value, fp32_ms, _ = mode_throughput(cfg, SV, "fp32", steps=args.parity_steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, cfgname)
     if rank == 0:
@@ -542,6 +577,7 @@ def main():
             "parity_value": None if par_value is None else round(par_value, 2),
             "parity_ms_per_step": None if par_ms is None else round(par_ms, 3),
             "parity_dtype": "bf16x6" if par_value is not None else None,
+            "parity_roofline": par_roof,
             "fp32_value": None if fp32_value is None else round(fp32_value, 2),
             "fp32_ms_per_step": None if fp32_ms is None else round(fp32_ms, 3),
             "flops_per_img": flops_img,

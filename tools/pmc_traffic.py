@@ -115,8 +115,10 @@ def main():
                           fetch_bytes_per_launch=round(fetch), write_bytes_per_launch=round(write),
                           hbm_bytes_per_launch=round(fetch + write))
     doc = dict(label=label, source="rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), csv",
-               correction="per kernel (fetch_rule): FETCH_SIZE x2 only for 16 B/lane loads (gfx950 half-count), "
-                          "x1 otherwise (uncalibrated); KiB->bytes x1024",
+               correction="per kernel (fetch_rule, calibrated on known byte counts: tools/calib/fetch_calib.hip, "
+                          "profiles/r03_fetch_calib.txt): FETCH_SIZE x2 where the operand rows are whole 128-B lines "
+                          "(counted half), x1 for 64-B line halves (counted exactly), byte-weighted mixes for the "
+                          "weight-GEMMs; each kernel's fetch_rule names its factor; KiB->bytes x1024",
                kernels=kernels)
     with open(out, "w") as fh:
         json.dump(doc, fh, indent=1, sort_keys=True)
