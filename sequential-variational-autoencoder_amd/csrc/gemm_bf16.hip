@@ -1464,6 +1464,10 @@ bool igemm_split_ok(const FwdArgs& a, int groups) {
 }
 
 int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit) {
+  if (a.ain.acc) {  // consumer-side BN of A: the wave-split halo gather only
+    if (ksplit) *ksplit = 1;
+    return halo_kw_plan(a, groups);
+  }
   if (a.nsp > 1) {  // split-bf16 planes: dense_kw, halo_kw or the small-N conv-T (igemm_split_ok)
     if (ksplit) *ksplit = 1;
     if (dense_kw_ok(a, groups)) return dense_kw_nrb(a);
@@ -1518,6 +1522,7 @@ const char* kernel_name(int kid) {
 }
 
 int igemm_bf16_kid(const FwdArgs& a) {
+  if (a.ain.acc) return halo_kw_plan(a, 1) > 0 ? KID_HALO_KW : KID_NONE;
   if (a.nsp > 1) return (!dense_kw_ok(a, 1) && halo_kw_plan(a, 1) > 0) ? KID_HALO_KW : KID_NONE;
   if (!halo_disabled()) {
     const HaloPlan hp = halo_plan(a, 1);
@@ -1544,6 +1549,11 @@ int igemm_bf16(FwdArgs a, int groups, hipStream_t s, hipEvent_t after) {
 }
 
 int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t after) {
+  if (a.ain.acc) {  // consumer-side BN of A (the caller checked halo_kw_plan)
+    const int nrb = halo_kw(a, groups, s);
+    if (after) hipEventRecord(after, s);
+    return nrb;
+  }
   if (a.nsp > 1 && !igemm_split_ok(a, groups)) return -2;  // no split kernel for this shape
   if (path == 2 && a.nsp <= 1 && smallc_ok(a, true)) {
     conv_smallc(a, groups, true, s);

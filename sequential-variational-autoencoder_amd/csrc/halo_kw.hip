@@ -33,7 +33,7 @@ typedef float f32x8 __attribute__((ext_vector_type(8)));
 #define KW_OCC_BR 5  // the same with the two-tap B ring
 #endif
 #ifndef KW_OCC_S32
-#define KW_OCC_S32 4  // split-mode 32-row instances with the B ring
+#define KW_OCC_S32 3  // split-mode 32-row instances with the B ring (4 spills 17-18 VGPRs)
 #endif
 
 struct KwArgs {
@@ -48,6 +48,7 @@ struct KwArgs {
   int ntx, nty, ntz;  // tiles along rows / columns / (groups x classes)
   int tpb;            // tiles per block: 1 = one tile per block (3-D grid); > 1 = persistent (1-D grid)
   int vec;            // 16-byte epilogue (every epilogue operand row 16-byte aligned; SVAE_KW_VEC)
+  int ain_off;        // byte offset of the consumer-side BN table [3][Cin] in dynamic LDS (f.ain.acc != nullptr)
 };
 
 namespace {
@@ -270,13 +271,29 @@ void igemm_halo_kw_kernel(KwArgs h) {
       if (woff[i] >= 0) ld8_raw(a.A, ac + woff[i], abf, wv[i][0], wv[i][1]);
     }
   };
+  // consumer-side BN (a.ain): a = act(bn_y(pre)) of the chunk's 8 channels of this thread (every item of
+  // a thread has the same channel part tid & 3), table [mean | invstd | beta][Cin] in LDS
+  const bool ain = a.ain.acc != nullptr;
+  const float* ain_tbl = (const float*)((const char*)ksm + h.ain_off);
+  auto ain_apply = [&](f32x4& lo, f32x4& hi, int chunk) {
+    const int c0 = chunk * KW_CK + (tid & 3) * 8;
+    const f32x4 m0 = *(const f32x4*)&ain_tbl[c0], m1 = *(const f32x4*)&ain_tbl[c0 + 4];
+    const f32x4 s0 = *(const f32x4*)&ain_tbl[a.Cin + c0], s1 = *(const f32x4*)&ain_tbl[a.Cin + c0 + 4];
+    const f32x4 b0 = *(const f32x4*)&ain_tbl[2 * a.Cin + c0], b1 = *(const f32x4*)&ain_tbl[2 * a.Cin + c0 + 4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      lo[j] = act_f(bn_y1(lo[j], m0[j], s0[j], b0[j]), a.ain.act);
+      hi[j] = act_f(bn_y1(hi[j], m1[j], s1[j], b1[j]), a.ain.act);
+    }
+  };
   // NS == 1: buffer `buf` of two; NS == 3: plane p of the one buffer at p * npix * KW_ROWP
-  auto store_window = [&](int buf) {
+  auto store_window = [&](int buf, int chunk) {
     __bf16* W = ksm + buf * h.npix * KW_ROWP;
 #pragma unroll
     for (int i = 0; i < PI; ++i) {
       const int it = tid + 256 * i;
       if (woff[i] < -1) continue;
+      if (!ABF && ain && woff[i] >= 0) ain_apply(wv[i][0], wv[i][1], chunk);  // (padding stays 0)
       const int o = (it >> 2) * KW_ROWP + (it & 3) * 8;
       if constexpr (NS == 1) {
         *(bf16x8*)&W[o] = raw8_bf(wv[i][0], wv[i][1], abf);
@@ -318,6 +335,30 @@ void igemm_halo_kw_kernel(KwArgs h) {
   };
 
   TileG cur = tile_geo(bx, by, bz);
+  if (!ABF && ain) {  // finalise the producer's statistics of every input channel (bn_apply's expression)
+    float* tbl = (float*)((char*)ksm + h.ain_off);
+    const int g = cur.group;
+    for (int c = tid; c < a.Cin; c += 256) {
+      const u64* base = a.ain.acc + g * a.ain.acc_gs + 4LL * c;
+      u64 t[4] = {0, 0, 0, 0};
+      for (int k = 0; k < a.ain.nsh; ++k)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) t[w] += base[k * a.ain.sh + w];
+      const double cnt = (double)a.ain.rows;
+      const double md = fx_get(t) / cnt;
+      double var = fx_get(t + 2) / cnt - md * md;
+      if (var < 0.0) var = 0.0;
+      const float m = (float)md, is = (float)(1.0 / sqrt(var + (double)a.ain.eps));
+      tbl[c] = m;
+      tbl[a.Cin + c] = is;
+      tbl[2 * a.Cin + c] = a.ain.beta[g * a.ain.beta_gs + c];
+      if (bx == 0 && by == 0 && a.ain.mean) {
+        a.ain.mean[g * a.ain.ms_gs + c] = m;
+        a.ain.invstd[g * a.ain.ms_gs + c] = is;
+      }
+    }
+    __syncthreads();
+  }
   set_window(cur);
   load_window(cur, 0);
   if constexpr (BR) {
@@ -327,7 +368,7 @@ void igemm_halo_kw_kernel(KwArgs h) {
     for (int u = 0; u < NTW; ++u) load_b(cur, u, u, 0);
   }
   if constexpr (NS == 1) {
-    store_window(0);
+    store_window(0, 0);
     __syncthreads();
   }
   for (;;) {
@@ -350,7 +391,7 @@ void igemm_halo_kw_kernel(KwArgs h) {
       const int buf = NS == 1 ? (c & 1) : 0;
       const bool has_next = c + 1 < nchunk;
       if constexpr (NS > 1) {  // one buffer of NS planes: stage chunk c, then prefetch c + 1
-        store_window(0);
+        store_window(0, c);
         __syncthreads();
       }
       if constexpr (!BR) {
@@ -400,7 +441,7 @@ void igemm_halo_kw_kernel(KwArgs h) {
         }
       }
       if constexpr (NS == 1) {
-        if (has_next) store_window(buf ^ 1);
+        if (has_next) store_window(buf ^ 1, c + 1);
       }
       __syncthreads();
     }
@@ -425,7 +466,7 @@ void igemm_halo_kw_kernel(KwArgs h) {
       cur = nxt;
       ++t_cur;
       if constexpr (NS == 1) {
-        store_window(0);
+        store_window(0, 0);
         __syncthreads();
       }
       continue;
@@ -500,7 +541,7 @@ void igemm_halo_kw_kernel(KwArgs h) {
     cur = nxt;
     ++t_cur;
     if constexpr (NS == 1) {
-      store_window(0);
+      store_window(0, 0);
       __syncthreads();
     }
   }
@@ -596,6 +637,7 @@ static bool kw_disabled() {
 
 int halo_kw_plan(const FwdArgs& a, int groups) {
   if (kw_disabled()) return 0;
+  if (a.ain.acc && (a.a_bf16 || a.Cin % 8)) return 0;  // consumer-side BN: fp32 A (the pre-BN tensor)
   KwArgs h;
   int bm, bn;
   size_t lds;
@@ -615,6 +657,12 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
   h.nty = (int)grid.y;
   h.ntz = (int)grid.z;
   h.tpb = 1;
+  h.ain_off = 0;
+  if (a.ain.acc) {  // the consumer-side BN table [3][Cin] after the window / reduction region
+    if (a.a_bf16 || a.Cin % 8) return -1;
+    h.ain_off = (int)((lds + 15) / 16 * 16);
+    lds = (size_t)h.ain_off + 3 * (size_t)a.Cin * sizeof(float);
+  }
   {  // SVAE_KW_VEC=1: the 16-byte epilogue where every row of C (and of the BN-backward operands) is aligned
     static const int vec_mode = [] {
       const char* e = getenv("SVAE_KW_VEC");
@@ -635,7 +683,7 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
     const char* e = getenv("SVAE_KW_PERSIST");
     return e ? atoi(e) : 0;
   }();
-  if (persist && a.nsp <= 1 && a.a_bf16 && bn == 32 && bm == 64) {  // the persistent instances
+  if (persist && a.nsp <= 1 && a.a_bf16 && bn == 32 && bm == 64 && !a.ain.acc) {  // the persistent instances
     const int occ_w = 2;
     const int occ_l = (int)std::max<size_t>(1, (size_t)163840 / std::max<size_t>(lds, 1));
     const long long slots = 256LL * std::min(occ_w, occ_l) * (persist > 1 ? persist : 1);
@@ -663,7 +711,7 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
                             (const void*)igemm_halo_kw_kernel<32, 32, false, false, 3, false, true>,
                             (const void*)igemm_halo_kw_kernel<64, 32, false, false, 3, false, true, 3>,
                             (const void*)igemm_halo_kw_kernel<32, 32, false, false, 3, false, true, 3>})
-        hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 98304);
       attr = true;
     }
     const bool br = (bring & 1) != 0;
@@ -674,7 +722,7 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
       const char* e = getenv("SVAE_KW_PERSIST_SPLIT");
       return e ? atoi(e) : 0;
     }();
-    if (persist_split && br && pi3 && bm == 64 && !s2t) {
+    if (persist_split && br && pi3 && bm == 64 && !s2t && !a.ain.acc) {
       const long long slots = 256LL * 3 * persist_split;
       const long long ntiles = (long long)h.ntx * h.nty * h.ntz;
       if (ntiles > slots) {
@@ -683,7 +731,7 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
         static bool attrp = false;
         if (!attrp) {
           hipFuncSetAttribute((const void*)igemm_halo_kw_kernel<64, 32, false, false, 3, true, true, 3>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 98304);
           attrp = true;
         }
         hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, false, false, 3, true, true, 3>), grid, dim3(256), lds, s, h);
@@ -723,7 +771,7 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
                             (const void*)igemm_halo_kw_kernel<128, 32, false, false>,
                             (const void*)igemm_halo_kw_kernel<128, 32, true, true>,
                             (const void*)igemm_halo_kw_kernel<128, 32, false, true>})
-        hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 98304);
       attr = true;
     }
     KW_LAUNCH(128, 32)
@@ -734,7 +782,7 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
                             (const void*)igemm_halo_kw_kernel<64, 64, false, false>,
                             (const void*)igemm_halo_kw_kernel<64, 64, true, true>,
                             (const void*)igemm_halo_kw_kernel<64, 64, false, true>})
-        hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 98304);
       attr = true;
     }
     KW_LAUNCH(64, 64)

@@ -14,6 +14,18 @@ struct BwStat {
   int act, C;
 };
 
+// Consumer-side BN(+act) of the A operand (the wave-split halo gather only): A holds the producing
+// layer's pre-BN output and the gather stages a = act(bn_y(pre)) -- the expression of bn_apply, from
+// the same fixed-point accumulators finalised the same way, so bitwise the applied tensor.  The block
+// at tile (0, 0) of each group stores mean / invstd for the backward.
+struct AinBN {
+  const u64* acc; long long acc_gs, sh; int nsh;  // the producer's statistics accumulators (acc == nullptr: off)
+  long long rows;                                  // rows the statistics cover
+  const float* beta; long long beta_gs;
+  float* mean; float* invstd; long long ms_gs;
+  int act; float eps;
+};
+
 // gather-GEMM  C[p][n] (+)= act(bias + sum_{tap,k} A[src(p,tap)][k] * B[tap][k|n][n|k])
 struct FwdArgs {
   const float* A; long long a_gs; int lda;
@@ -36,6 +48,7 @@ struct FwdArgs {
   // split-bf16 mode (dtype = bf16x6, opload.h split8): A and B as nsp bf16 planes each (1 = plain
   // bf16); B plane p at Bh + p * b_plane elements.  Only kernels that implement it accept nsp > 1
   int nsp; long long b_plane;
+  AinBN ain;    // consumer-side BN of A (halo_kw only)
 };
 
 // weight-GEMM  part[split][tap][m][n] = sum_{p in split} G[src(p,tap)][m] * D[p][n]

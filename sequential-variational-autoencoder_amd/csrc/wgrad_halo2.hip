@@ -375,7 +375,11 @@ int wgrad_halo2(const WgArgs& w, int groups, float* slab, long long slab_cap, fl
   if (!wgrad_halo2_ok(w)) return 0;
   const int WO = w.g.Wo;
   const int S = w.g.stride;
-  const int cp = wh2_cp(WO, S);
+  // split mode (NSP = 2, fp32 operands): 128-pixel chunks for the 8- and 16-wide layers halve the
+  // staging registers (256 VGPRs + spills at 256-pixel chunks; SVAE_WH2_SPLIT_CP=256 restores them)
+  static const int split_cp = env_int("SVAE_WH2_SPLIT_CP", 128);
+  const bool sp128 = w.nsp > 1 && S == 1 && WO <= 16 && split_cp == 128 && w.rows % 128 == 0;
+  const int cp = sp128 ? 128 : wh2_cp(WO, S);
   static const int target = env_int("SVAE_WH2_TARGET", 64);
   static const int minch = env_int("SVAE_WH2_MINCH", 4);
   // SVAE_WH2_NSW=2: a 64-column block as 4 waves of two 32-column subtiles (each transposed A
@@ -409,7 +413,15 @@ int wgrad_halo2(const WgArgs& w, int groups, float* slab, long long slab_cap, fl
   if (wn == 2 && nsw == 2) { wh2_launch<WOV, CPV, 4, 1, 1, false, 2>(a, groups, s); } \
   else if (wn == 2) { WH2(WOV, CPV, 4, 2, 1); }                                     \
   else { WH2(WOV, CPV, 4, 1, 2); }
-  if (S == 2) {  // 64-pixel chunks: WN = 2 where N >= 64, else two K-interleaved wave sets
+  if (sp128) {  // split planes, 128-pixel chunks
+    if (WO == 16) {
+      if (wn == 2) wh2_launch_op<16, 128, 4, 2, 1, false, 0, 1, 1, 1, 2>(a, groups, s);
+      else wh2_launch_op<16, 128, 4, 1, 2, false, 0, 1, 1, 1, 2>(a, groups, s);
+    } else {
+      if (wn == 2) wh2_launch_op<8, 128, 4, 2, 1, false, 0, 1, 1, 1, 2>(a, groups, s);
+      else wh2_launch_op<8, 128, 4, 1, 2, false, 0, 1, 1, 1, 2>(a, groups, s);
+    }
+  } else if (S == 2) {  // 64-pixel chunks: WN = 2 where N >= 64, else two K-interleaved wave sets
     if (WO == 16) {
       if (wn == 2) wh2_launch<16, 64, 4, 2, 1, false, 1, 2>(a, groups, s);
       else wh2_launch<16, 64, 4, 1, 2, false, 1, 2>(a, groups, s);
