@@ -446,11 +446,13 @@ void svae_tls_error(const std::string& msg) { g_tls_err = msg; }
 // ============================================================================
 // engine context
 // ============================================================================
+struct Defer;
 struct View {
   float* p = nullptr;
   int ld = 0;
   long long gs = 0;
   int bf = 0;  // stored as bf16 (element ld / gs unchanged): only bf16 GEMMs read it (opload.h)
+  const Defer* dfr = nullptr;  // the tensor's BN apply was deferred to the side stream (SVAE_FOLD)
 };
 
 struct BNS {  // per-layer BN statistics (mean / invstd), groups x C
@@ -516,6 +518,15 @@ struct svae_ctx {
   int side_batch = 1;
   bool side2 = false;  // SVAE_SIDE2 (read at svae_create, before the arena plan)
   bool fc_fuse = true;  // E.fc BN-backward sums fused into the top FC's input gradient (SVAE_BWFUSE_FC)
+  // SVAE_FOLD=1: the forward BN apply of a layer whose only main-stream consumer is a wave-split halo
+  // gather runs on st2 (for the backward's weight gradients), and the gather stages act(bn_y(pre))
+  // itself (FwdArgs::ain): the apply leaves the critical path.  Bitwise the same tensors.
+  bool fold = false;
+  static constexpr int NFOLD = 32;
+  hipEvent_t ev_fold[NFOLD] = {};
+  int fold_pos = 0;
+  bool fold_used = false;
+  hipEvent_t ev_fold_join = nullptr;
   static constexpr int NF = 4;
   hipEvent_t ev_flush[NF] = {};
   int flush_pos = 0;
@@ -695,6 +706,21 @@ static AccR acc_bn(svae_ctx* c, int groups, int C, long long rowblocks) {
   r.p = acc_take(c, r.sh * r.nsh);
   return r;
 }
+// a BN(+act) apply deferred to the side stream: what a consumer needs to stage it from pre
+struct Defer {
+  const float* pre = nullptr;
+  int ld = 0;
+  long long gs = 0;
+  AccR acc;
+  long long rows = 0;
+  const float* beta = nullptr;
+  long long beta_gs = 0;
+  BNS bn;
+  long long bn_gs = 0;
+  int act = 0;
+  hipEvent_t applied = nullptr;  // on st2, after the apply
+};
+
 static void set_stats(FwdArgs& a, const AccR& r) {
   a.stats = r.p;
   a.s_gs = r.gs;
@@ -1011,9 +1037,23 @@ static int dbg_skip() {
   return v;
 }
 
-// Forward conv/convT + BN + act.  in: [B,hin,hin,cin] (ld), out view gets act(BN(pre)+res)
+// the consumer-side BN gather is available for this launch (the wave-split halo gather takes it)
+static bool ain_ok(svae_ctx* c, const FwdArgs& t, int groups) {
+  if (!c->m.g.bf16 || !t.Bh) return false;
+  FwdArgs u = t;
+  if (c->m.g.split) {
+    u.nsp = 3;
+    u.b_plane = c->wplane;
+  }
+  return halo_kw_plan(u, groups) > 0;
+}
+
+// Forward conv/convT + BN + act.  in: [B,hin,hin,cin] (ld), out view gets act(BN(pre)+res).
+// in.dfr: the input's BN apply was deferred (its gather stages act(bn_y(pre)), or waits for the apply
+// where it cannot); dfr_out: defer this layer's apply to st2 when SVAE_FOLD is on (no residual)
 static int conv_bn_act_fwd(svae_ctx* c, const ConvL& L, int groups, long long w_gs, View in, float* pre,
-                           long long pre_gs, BNS bn, long long bn_gs, View res, int act, View out) {
+                           long long pre_gs, BNS bn, long long bn_gs, View res, int act, View out,
+                           Defer* dfr_out = nullptr) {
   const int B = c->m.g.B;
   FwdArgs a = fwd_args_conv(L, B, c->P + L.ow, w_gs);
   a.A = in.p;
@@ -1027,12 +1067,49 @@ static int conv_bn_act_fwd(svae_ctx* c, const ConvL& L, int groups, long long w_
     a.Bh = L.tr ? shadowN(c, L.ow) : shadowT(c, L.ow);
     a.ldb = L.cin;
   }
+  if (in.dfr) {
+    const Defer& d = *in.dfr;
+    FwdArgs t = a;
+    t.A = d.pre;
+    t.a_gs = d.gs;
+    t.lda = d.ld;
+    t.a_bf16 = 0;
+    t.ain = AinBN{d.acc.p, d.acc.gs, d.acc.sh, d.acc.nsh, d.rows, d.beta, d.beta_gs, d.bn.mean, d.bn.invstd, d.bn_gs,
+                  d.act, 1e-3f};
+    if (ain_ok(c, t, groups)) a = t;
+    else hipStreamWaitEvent(c->st, d.applied, 0);  // stage the applied tensor
+  }
   const AccR acc = acc_bn(c, groups, L.cout, gemm_nrb(c, a, groups));
   if (!acc.p) return fail(c, SVAE_EBADARG, "BN accumulator arena too small");
   set_stats(a, acc);
   gemm(c, a, groups);
   const long long rows = (long long)B * L.hout * L.hout;
   if ((dbg_skip() & 1) && out.bf && !res.p) return 0;  // TIMING PROBE ONLY (wrong results): no apply pass
+  if (dfr_out && c->fold && c->side && !res.p) {  // the apply on st2, off the critical path
+    hipEvent_t ready = c->ev_fold[c->fold_pos];
+    hipEvent_t applied = c->ev_fold[c->fold_pos + 1];
+    c->fold_pos = (c->fold_pos + 2) % svae_ctx::NFOLD;
+    hipEventRecord(ready, c->st);
+    hipStreamWaitEvent(c->st2, ready, 0);
+    bn_apply(pre, L.cout, pre_gs, rows, L.cout, acc.p, acc.gs, acc.sh, acc.nsh, 1e-3f, bn.mean, bn.invstd, bn_gs,
+             c->P + L.obeta, w_gs, nullptr, 0, 0, act, out.p, out.ld, out.gs, groups, c->st2, out.bf);
+    hipEventRecord(applied, c->st2);
+    c->fold_used = true;
+    Defer& d = *dfr_out;
+    d.pre = pre;
+    d.ld = L.cout;
+    d.gs = pre_gs;
+    d.acc = acc;
+    d.rows = rows;
+    d.beta = c->P + L.obeta;
+    d.beta_gs = w_gs;
+    d.bn = bn;
+    d.bn_gs = bn_gs;
+    d.act = act;
+    d.applied = applied;
+    return 0;
+  }
+  if (dfr_out) *dfr_out = Defer{};
   bn_apply(pre, L.cout, pre_gs, rows, L.cout, acc.p, acc.gs, acc.sh, acc.nsh, 1e-3f, bn.mean, bn.invstd, bn_gs, c->P + L.obeta, w_gs,
            res.p, res.ld, res.gs, act, out.p, out.ld, out.gs, groups, c->st, out.bf);
   return 0;
@@ -1402,10 +1479,11 @@ static int inference_fwd(svae_ctx* c, int t0, int n, View in0) {
     const int Fl = F[lvl + 1];
     View in = lvl == 0 ? in0 : View{c->inf_act_b[lvl - 1] + t0 * c->inf_gs[lvl - 1], F[lvl], c->inf_gs[lvl - 1]};
     float* act_a = elem_off(c->inf_act_a[lvl], t0 * gs, c->abf);  // bf16 storage: step t0's group in bf16 elements
+    Defer da;  // conv a's apply deferred to st2 (SVAE_FOLD): conv b's gather stages it from pre
     r = conv_bn_act_fwd(c, I.a[lvl], n, wg, in, c->inf_pre_a[lvl] + t0 * gs, gs, bns(c->inf_bn_a[lvl], Fl), Fl, View{},
-                        ACT_LRELU, View{act_a, Fl, gs, c->abf});
+                        ACT_LRELU, View{act_a, Fl, gs, c->abf}, &da);
     if (r) return r;
-    r = conv_bn_act_fwd(c, I.b[lvl], n, wg, View{act_a, Fl, gs, c->abf}, c->inf_pre_b[lvl] + t0 * gs, gs,
+    r = conv_bn_act_fwd(c, I.b[lvl], n, wg, View{act_a, Fl, gs, c->abf, da.pre ? &da : nullptr}, c->inf_pre_b[lvl] + t0 * gs, gs,
                         bns(c->inf_bn_b[lvl], Fl), Fl, View{}, ACT_LRELU, View{c->inf_act_b[lvl] + t0 * gs, Fl, gs});
     if (r) return r;
     for (int hl = 0; hl < L; ++hl) {
@@ -1675,10 +1753,11 @@ static int engine_forward(svae_ctx* c) {
       View in{(float*)xprev, g.C, 0};
       for (int lvl = 0; lvl < L - 1; ++lvl) {
         const int Fl = F[lvl + 1];
+        Defer da;  // conv a's apply deferred to st2 (SVAE_FOLD): conv b's gather stages it from pre
         r = conv_bn_act_fwd(c, E.a[lvl], 1, 0, in, s.enc_pre_a[lvl], 0, s.enc_bn_a[lvl], 0, View{}, ACT_LRELU,
-                            View{s.enc_act_a[lvl], Fl, 0, c->abf});
+                            View{s.enc_act_a[lvl], Fl, 0, c->abf}, &da);
         if (r) return r;
-        r = conv_bn_act_fwd(c, E.b[lvl], 1, 0, View{s.enc_act_a[lvl], Fl, 0, c->abf}, s.enc_pre_b[lvl], 0, s.enc_bn_b[lvl], 0,
+        r = conv_bn_act_fwd(c, E.b[lvl], 1, 0, View{s.enc_act_a[lvl], Fl, 0, c->abf, da.pre ? &da : nullptr}, s.enc_pre_b[lvl], 0, s.enc_bn_b[lvl], 0,
                             View{}, ACT_LRELU, View{s.enc_act_b[lvl], Fl, 0});
         if (r) return r;
         in = View{s.enc_act_b[lvl], Fl, 0};
@@ -1697,6 +1776,7 @@ static int engine_forward(svae_ctx* c) {
     r = fc_bn_fwd(c, G.top, View{s.top_cat, s.ktop, 0}, s.top_pre, s.top_bn, View{s.top_act, S[L] * S[L] * F[L], 0, c->abf});
     if (r) return r;
     View cur{s.top_act, F[L], 0, c->abf};
+    Defer ds1;  // s1[lvl >= 1]'s apply deferred to st2 (SVAE_FOLD): s2[lvl-1]'s conv-T gather stages it
     for (int lvl = L - 2; lvl >= 0; --lvl) {
       const int Fl = F[lvl + 1];
       View res = t >= 1 ? View{s.enc_act_b[lvl], Fl, 0} : View{};
@@ -1704,9 +1784,9 @@ static int engine_forward(svae_ctx* c) {
                           View{s.cat[lvl], 2 * Fl, 0});
       if (r) return r;
       r = conv_bn_act_fwd(c, G.s1[lvl], 1, 0, View{s.cat[lvl], 2 * Fl, 0}, s.s1_pre[lvl], 0, s.s1_bn[lvl], 0, View{},
-                          ACT_RELU, View{s.s1_act[lvl], Fl, 0, c->abf});
+                          ACT_RELU, View{s.s1_act[lvl], Fl, 0, c->abf}, lvl >= 1 ? &ds1 : nullptr);
       if (r) return r;
-      cur = View{s.s1_act[lvl], Fl, 0, c->abf};
+      cur = View{s.s1_act[lvl], Fl, 0, c->abf, (lvl >= 1 && ds1.pre) ? &ds1 : nullptr};
     }
     // output + ratio conv-T (:1720, :1727) as one 4-channel small-N gather
     {
@@ -1759,6 +1839,11 @@ static int engine_forward(svae_ctx* c) {
       if (g.imp && t >= 1)  // ||mle_t - mle_{t-1}||^2 per image (:1190-1191)
         sqdiff_img(s.xhat, c->sb[t - 1].xhat, B, (long long)g.H * g.W * g.C, c->imp_img + (long long)t * B, st);
     }
+  }
+  if (c->fold_used) {  // the deferred applies (st2) before anything after the forward
+    hipEventRecord(c->ev_fold_join, c->st2);
+    hipStreamWaitEvent(st, c->ev_fold_join, 0);
+    c->fold_used = false;
   }
   return 0;
 }
@@ -2440,6 +2525,8 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
     return fail(nullptr, SVAE_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
   }
   {
+    const char* fo = getenv("SVAE_FOLD");  // forward BN applies of gather-only tensors on st2
+    c->fold = fo && fo[0] == '1';
     const char* s2 = getenv("SVAE_SIDE2");  // a second weight-gradient stream
     c->side2 = s2 && s2[0] == '1';
     const char* rg = getenv("SVAE_REC_GROUP");  // recognition-backward group size (0 = batched after the chain)
@@ -2617,6 +2704,8 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
       mk(&c->ev_rs);
       mk(&c->ev_rs2);
       if (c->side2) mk(&c->ev_merge);
+      for (int i = 0; i < svae_ctx::NFOLD; ++i) mk(&c->ev_fold[i]);
+      mk(&c->ev_fold_join);
       {  // SVAE_SIDE_BATCH (read per context): weight-gradient layers per side-stream hand-over
         const char* e = getenv("SVAE_SIDE_BATCH");
         c->side_batch = e ? std::max(1, atoi(e)) : 1;
@@ -2647,7 +2736,9 @@ int svae_destroy(svae_ctx* c) {
     if (ev) hipEventDestroy(ev);
   for (hipEvent_t ev : c->ev_flush)
     if (ev) hipEventDestroy(ev);
-  for (hipEvent_t ev : {c->ev_rs, c->ev_rs2, c->ev_merge})
+  for (hipEvent_t ev : {c->ev_rs, c->ev_rs2, c->ev_merge, c->ev_fold_join})
+    if (ev) hipEventDestroy(ev);
+  for (hipEvent_t ev : c->ev_fold)
     if (ev) hipEventDestroy(ev);
   for (int i = 0; i < svae_ctx::NR; ++i) {
     if (c->ev_ready[i]) hipEventDestroy(c->ev_ready[i]);

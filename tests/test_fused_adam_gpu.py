@@ -183,3 +183,23 @@ def test_second_side_stream_is_bitwise(preset, dtype, fused, monkeypatch):
     assert changed > 0
     assert l0 == l1, (l0, l1)
     np.testing.assert_array_equal(p0, p1)
+
+
+@pytest.mark.parametrize("preset,dtype,over", [
+    ("tiny", "bf16", {}), ("celeba", "bf16", {}), ("tiny", "bf16x6", {}), ("celeba", "bf16x6", {}),
+    ("tiny_homog", "bf16", {}), ("tiny", "bf16", {"predict_latent_code": True}),
+])
+@pytest.mark.parametrize("fused", [False, True])
+def test_forward_bn_fold_is_bitwise(preset, dtype, over, fused, monkeypatch):
+    """SVAE_FOLD=1: the forward BN apply of the recognition / encoder conv-a and decoder s1 (level >= 1)
+    outputs runs on the side stream, and the next layer's wave-split gather stages act(bn_y(pre)) from
+    the pre-BN tensor itself with the statistics finalised as bn_apply does (engine.cpp
+    conv_bn_act_fwd, halo_kw.hip ain): the same values, so three training steps are bitwise the
+    unfolded run's."""
+    monkeypatch.setenv("SVAE_FOLD", "0")
+    p0, l0, _ = _run(preset, dtype, fused, over)
+    monkeypatch.setenv("SVAE_FOLD", "1")
+    p1, l1, changed = _run(preset, dtype, fused, over)
+    assert changed > 0
+    assert l0 == l1, (l0, l1)
+    np.testing.assert_array_equal(p0, p1)
