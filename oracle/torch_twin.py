@@ -7,6 +7,7 @@ flatten order for every FC input.  Used (a) to cross-check oracle/model.py and
 the reference's own TF-CPU path cannot run here (no TensorFlow).
 """
 import math
+import os
 
 import torch
 import torch.nn.functional as Fn
@@ -52,6 +53,20 @@ def _x3(f, a, b):
     ah, al = _split(a)
     bh, bl = _split(b)
     return f(ah, bh) + f(ah, bl) + f(al, bh)
+
+
+class _RoundSTE(torch.autograd.Function):
+    """bf16 storage of a pre-BN conv output (the engine's bf16 mode, DESIGN §5 "bf16 pre"): the value is
+    rounded (RNE) where the GEMM epilogue stores it; the gradient passes unchanged (the engine's dpre is
+    the gradient at the stored tensor and flows into the conv's backward as is)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return _bf(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
 
 
 class _RoundedOp(torch.autograd.Function):
@@ -118,12 +133,16 @@ def nhwc_unflatten(x, S, C):
 
 class Twin:
     def __init__(self, cfg, struct, params, dtype=torch.float32, requires_grad=True, emulate_bf16=False,
-                 emulate_split=False):
+                 emulate_split=False, pre_bf16=None):
         self.cfg, self.struct = cfg, struct
         self.P = {k: torch.tensor(v, dtype=dtype, requires_grad=requires_grad) for k, v in params.items()}
         self.dtype = dtype
         self.bf16 = emulate_bf16 or emulate_split
         self.split = emulate_split  # dtype='bf16x3': every rounded leg as hi/lo split products
+        # bf16 mode stores every conv layer's pre-BN output as bf16 (the engine's SVAE_PRE_F32=1 keeps fp32)
+        if pre_bf16 is None:
+            pre_bf16 = emulate_bf16 and not emulate_split and os.environ.get("SVAE_PRE_F32", "0") != "1"
+        self.pre_bf16 = pre_bf16
 
     def _op(self, fn, x, w, rf=True, rd=True, rw=True):
         if not self.bf16:
@@ -139,6 +158,8 @@ class Twin:
     def _cba(self, x, lay, s, act, transpose=False, residual=None):
         P = self.P
         y = self._conv(x, P[lay["w"]], s, transpose)
+        if self.pre_bf16:
+            y = _RoundSTE.apply(y)
         y = y + P[lay["b"]].view(1, -1, 1, 1)
         y = bn_train(y, P[lay["beta"]])
         if residual is not None:

@@ -113,7 +113,8 @@ static ApGrid ap_grid(long long rows, int C, int groups, int W = 4) {
 
 // W = 8 (bf16 output, C % 8 == 0): each thread normalises 8 consecutive channels of a row and
 // writes them as one 16-byte bf16 vector (write-through-friendly; W = 4 writes 8 bytes)
-template <int W>
+// PB: pre is stored as bf16 (common.h pf_ld4)
+template <int W, bool PB>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const float* pre, int ldp, long long pre_gs, long long rows,
                                                        int C, const u64* acc, long long acc_gs, long long sh,
                                                        int nsh, float eps,
@@ -160,7 +161,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* pre, int ldp
   const int q = q0 + qi;
   if (rl >= RL || q >= Q) return;
   const int c = q * W;
-  pre += group * pre_gs;
+  pre = pf_at(pre, group * pre_gs, PB);
   if (res) res += group * res_gs;
   const long long r0 = (long long)blockIdx.y * rpb;
   const long long r1 = r0 + rpb < rows ? r0 + rpb : rows;
@@ -170,8 +171,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* pre, int ldp
     const f32x4 b0 = *(const f32x4*)(beta + group * beta_gs + c), b1 = *(const f32x4*)(beta + group * beta_gs + c + 4);
 #pragma unroll 4
     for (long long r = r0 + rl; r < r1; r += RL) {
-      f32x4 y0 = bn_y(*(const f32x4*)(pre + r * ldp + c), m0, is0, b0);
-      f32x4 y1 = bn_y(*(const f32x4*)(pre + r * ldp + c + 4), m1, is1, b1);
+      f32x4 y0 = bn_y(pf_ld4(pre, r * ldp + c, PB), m0, is0, b0);
+      f32x4 y1 = bn_y(pf_ld4(pre, r * ldp + c + 4, PB), m1, is1, b1);
       if (res) {
         y0 += *(const f32x4*)(res + r * ldr + c);
         y1 += *(const f32x4*)(res + r * ldr + c + 4);
@@ -194,7 +195,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* pre, int ldp
   const f32x4 b = *(const f32x4*)(beta + group * beta_gs + c);
 #pragma unroll 4
   for (long long r = r0 + rl; r < r1; r += RL) {
-    f32x4 y = bn_y(*(const f32x4*)(pre + r * ldp + c), m, is, b);
+    f32x4 y = bn_y(pf_ld4(pre, r * ldp + c, PB), m, is, b);
     if (res) y += *(const f32x4*)(res + r * ldr + c);
 #pragma unroll
     for (int e = 0; e < 4; ++e) y[e] = act_f(y[e], act);
@@ -209,22 +210,31 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* pre, int ldp
 void bn_apply(const float* pre, int ldp, long long pre_gs, long long rows, int C, const u64* acc, long long acc_gs,
               long long sh, int nsh, float eps, float* mean, float* invstd, long long ms_gs, const float* beta, long long beta_gs,
               const float* res, int ldr, long long res_gs, int act, float* out, int ldo, long long out_gs, int groups,
-              hipStream_t s, int out_bf16) {
+              hipStream_t s, int out_bf16, int pre_bf16) {
   if (out_bf16 && bn_w8() && C % 8 == 0 && ldo % 8 == 0 && out_gs % 8 == 0 && ((uintptr_t)out & 15) == 0) {
     const ApGrid g = ap_grid(rows, C, groups, 8);
-    hipLaunchKernelGGL(bn_apply_kernel<8>, g.grid, dim3(256), 0, s, pre, ldp, pre_gs, rows, C, acc, acc_gs, sh, nsh, eps,
-                       mean, invstd, ms_gs, beta, beta_gs, res, ldr, res_gs, act, out, ldo, out_gs, g.rpb, out_bf16);
+    if (pre_bf16)
+      hipLaunchKernelGGL((bn_apply_kernel<8, true>), g.grid, dim3(256), 0, s, pre, ldp, pre_gs, rows, C, acc, acc_gs, sh, nsh,
+                         eps, mean, invstd, ms_gs, beta, beta_gs, res, ldr, res_gs, act, out, ldo, out_gs, g.rpb, out_bf16);
+    else
+      hipLaunchKernelGGL((bn_apply_kernel<8, false>), g.grid, dim3(256), 0, s, pre, ldp, pre_gs, rows, C, acc, acc_gs, sh, nsh,
+                         eps, mean, invstd, ms_gs, beta, beta_gs, res, ldr, res_gs, act, out, ldo, out_gs, g.rpb, out_bf16);
     return;
   }
   const ApGrid g = ap_grid(rows, C, groups);
-  hipLaunchKernelGGL(bn_apply_kernel<4>, g.grid, dim3(256), 0, s, pre, ldp, pre_gs, rows, C, acc, acc_gs, sh, nsh, eps, mean,
-                     invstd, ms_gs, beta, beta_gs, res, ldr, res_gs, act, out, ldo, out_gs, g.rpb, out_bf16);
+  if (pre_bf16)
+    hipLaunchKernelGGL((bn_apply_kernel<4, true>), g.grid, dim3(256), 0, s, pre, ldp, pre_gs, rows, C, acc, acc_gs, sh, nsh,
+                       eps, mean, invstd, ms_gs, beta, beta_gs, res, ldr, res_gs, act, out, ldo, out_gs, g.rpb, out_bf16);
+  else
+    hipLaunchKernelGGL((bn_apply_kernel<4, false>), g.grid, dim3(256), 0, s, pre, ldp, pre_gs, rows, C, acc, acc_gs, sh, nsh,
+                       eps, mean, invstd, ms_gs, beta, beta_gs, res, ldr, res_gs, act, out, ldo, out_gs, g.rpb, out_bf16);
 }
 
 #define BWD_RPB 256  // rows per row-block of the backward reduction
 int bn_bwd_rowblocks(long long rows) { return (int)((rows + BWD_RPB - 1) / BWD_RPB); }
 
 // y == nullptr: act' from the recomputed pre-activation bn_y(pre) (layers without a shortcut add)
+template <bool PB>
 __global__ void bn_bwd_reduce_kernel(const float* dy, int lddy, long long dy_gs, const float* y, int ldy,
                                      long long y_gs, const float* pre, int ldp, long long pre_gs, long long rows,
                                      int C, const float* mean, const float* invstd, long long ms_gs, const float* beta,
@@ -241,7 +251,7 @@ __global__ void bn_bwd_reduce_kernel(const float* dy, int lddy, long long dy_gs,
   const bool active = rl < RL && q < Q;
   dy += group * dy_gs;
   if (y) y += group * y_gs;
-  pre += group * pre_gs;
+  pre = pf_at(pre, group * pre_gs, PB);
   mean += group * ms_gs;
   invstd += group * ms_gs;
   f32x4 sd = {0.f, 0.f, 0.f, 0.f}, sx = {0.f, 0.f, 0.f, 0.f};
@@ -254,7 +264,7 @@ __global__ void bn_bwd_reduce_kernel(const float* dy, int lddy, long long dy_gs,
 #pragma unroll 4
     for (long long r = r0 + rl; r < r1; r += RL) {
       f32x4 g = *(const f32x4*)(dy + r * lddy + c);
-      const f32x4 xp = *(const f32x4*)(pre + r * ldp + c);
+      const f32x4 xp = pf_ld4(pre, r * ldp + c, PB);
       f32x4 yy = y ? *(const f32x4*)(y + r * ldy + c) : bn_y(xp, m, is, bb);
       f32x4 xh = (xp - m) * is;
 #pragma unroll
@@ -283,23 +293,27 @@ __global__ void bn_bwd_reduce_kernel(const float* dy, int lddy, long long dy_gs,
 void bn_bwd_reduce(const float* dy, int lddy, long long dy_gs, const float* y, int ldy, long long y_gs,
                    const float* pre, int ldp, long long pre_gs, long long rows, int C, const float* mean,
                    const float* invstd, long long ms_gs, const float* beta, long long beta_gs, int act, u64* acc,
-                   long long acc_gs, long long sh, int nsh, int groups, hipStream_t s) {
+                   long long acc_gs, long long sh, int nsh, int groups, hipStream_t s, int pre_bf16) {
   const int Q = C / 4;
   const int QB = Q < 16 ? Q : 16;
   dim3 grid((Q + QB - 1) / QB, (unsigned)bn_bwd_rowblocks(rows), groups);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, grid, dim3(256), 0, s, dy, lddy, dy_gs, y, ldy, y_gs, pre, ldp, pre_gs,
-                     rows, C, mean, invstd, ms_gs, beta, beta_gs, act, acc, acc_gs, sh, nsh);
+  if (pre_bf16)
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, grid, dim3(256), 0, s, dy, lddy, dy_gs, y, ldy, y_gs, pre, ldp, pre_gs,
+                       rows, C, mean, invstd, ms_gs, beta, beta_gs, act, acc, acc_gs, sh, nsh);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, grid, dim3(256), 0, s, dy, lddy, dy_gs, y, ldy, y_gs, pre, ldp, pre_gs,
+                       rows, C, mean, invstd, ms_gs, beta, beta_gs, act, acc, acc_gs, sh, nsh);
 }
 
 // W = 8 (bf16 dpre, C % 8 == 0): 8 channels per thread, one 16-byte bf16 store per row
-template <int W>
+template <int W, bool PB>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const float* dy, int lddy, long long dy_gs, const float* y, int ldy, long long y_gs, const float* pre, int ldp,
     long long pre_gs, long long rows, int C, const float* mean, const float* invstd, long long ms_gs,
     const float* beta, long long beta_gs, const u64* acc, long long acc_gs, long long sh, int nsh, float* dbeta,
     long long dbeta_gs, int act,
     float* dpre, int lddp, long long dpre_gs, float* dres, int ldres, long long dres_gs, int res_acc, int rpb,
-    int dpre_bf16) {
+    int dpre_bf16, const float* ab) {
   __shared__ __attribute__((aligned(16))) float sm[2][AP_QB * 4];
   __shared__ u64 tot[4 * AP_QB * 4];
   const int group = blockIdx.z;
@@ -309,8 +323,16 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   const int tid = threadIdx.x, qi = tid % QB, rl = tid / QB;
   const int q0 = blockIdx.x * QB;
   const int nch = min(QB * W, C - q0 * W);
-  acc_gather(acc + group * acc_gs, sh, nsh, q0 * W, nch, tot);
-  if (tid < nch) {
+  if (ab) {  // finalised by the producer's last block (BnFin mode 1; dbeta written there)
+    if (tid < nch) {
+      const int c = q0 * W + tid;
+      sm[0][tid] = ab[group * 2LL * C + c];
+      sm[1][tid] = ab[group * 2LL * C + C + c];
+    }
+  } else {
+    acc_gather(acc + group * acc_gs, sh, nsh, q0 * W, nch, tot);
+  }
+  if (tid < nch && !ab) {
     const int c = q0 * W + tid;
     {
       const double sd = fx_get(tot + 4 * tid), sx = fx_get(tot + 4 * tid + 2);
@@ -325,7 +347,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   const int c = q * W;
   dy += group * dy_gs;
   if (y) y += group * y_gs;
-  pre += group * pre_gs;
+  pre = pf_at(pre, group * pre_gs, PB);
   if (dres) dres += group * dres_gs;
   if constexpr (W == 8) {  // (dpre_bf16)
     const long long r0 = (long long)blockIdx.y * rpb;
@@ -345,7 +367,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const f32x4 g = *(const f32x4*)(dy + r * lddy + c + 4 * h);
-        const f32x4 xp = *(const f32x4*)(pre + r * ldp + c + 4 * h);
+        const f32x4 xp = pf_ld4(pre, r * ldp + c + 4 * h, PB);
         const f32x4 yy = y ? *(const f32x4*)(y + r * ldy + c + 4 * h) : bn_y(xp, mm[h], iss[h], bbb[h]);
         const f32x4 xh = (xp - mm[h]) * iss[h];
         f32x4 dz;
@@ -372,7 +394,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
 #pragma unroll 2
   for (long long r = r0 + rl; r < r1; r += RL) {
     const f32x4 g = *(const f32x4*)(dy + r * lddy + c);
-    const f32x4 xp = *(const f32x4*)(pre + r * ldp + c);
+    const f32x4 xp = pf_ld4(pre, r * ldp + c, PB);
     const f32x4 yy = y ? *(const f32x4*)(y + r * ldy + c) : bn_y(xp, m, is, bb);
     const f32x4 xh = (xp - m) * is;
     f32x4 dz;
@@ -396,16 +418,22 @@ void bn_bwd_apply(const float* dy, int lddy, long long dy_gs, const float* y, in
                   const float* invstd, long long ms_gs, const float* beta, long long beta_gs, const u64* acc,
                   long long acc_gs, long long sh, int nsh, float* dbeta, long long dbeta_gs, int act, float* dpre, int lddp,
                   long long dpre_gs, float* dres, int ldres, long long dres_gs, int res_acc, int groups,
-                  hipStream_t s, int dpre_bf16) {
+                  hipStream_t s, int dpre_bf16, int pre_bf16, const float* ab) {
+#define BWA_LAUNCH(W_, G_)                                                                                          \
+  if (pre_bf16)                                                                                                    \
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<W_, true>), G_.grid, dim3(256), 0, s, dy, lddy, dy_gs, y, ldy, y_gs, pre, ldp, \
+                       pre_gs, rows, C, mean, invstd, ms_gs, beta, beta_gs, acc, acc_gs, sh, nsh, dbeta, dbeta_gs, act, \
+                       dpre, lddp, dpre_gs, dres, ldres, dres_gs, res_acc, G_.rpb, dpre_bf16, ab);                    \
+  else                                                                                                             \
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<W_, false>), G_.grid, dim3(256), 0, s, dy, lddy, dy_gs, y, ldy, y_gs, pre,   \
+                       ldp, pre_gs, rows, C, mean, invstd, ms_gs, beta, beta_gs, acc, acc_gs, sh, nsh, dbeta, dbeta_gs, \
+                       act, dpre, lddp, dpre_gs, dres, ldres, dres_gs, res_acc, G_.rpb, dpre_bf16, ab);
   if (dpre_bf16 && bn_w8() && C % 8 == 0 && lddp % 8 == 0 && dpre_gs % 8 == 0 && ((uintptr_t)dpre & 15) == 0) {
     const ApGrid g = ap_grid(rows, C, groups, 8);
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<8>, g.grid, dim3(256), 0, s, dy, lddy, dy_gs, y, ldy, y_gs, pre, ldp, pre_gs,
-                       rows, C, mean, invstd, ms_gs, beta, beta_gs, acc, acc_gs, sh, nsh, dbeta, dbeta_gs, act, dpre,
-                       lddp, dpre_gs, dres, ldres, dres_gs, res_acc, g.rpb, dpre_bf16);
+    BWA_LAUNCH(8, g)
     return;
   }
   const ApGrid g = ap_grid(rows, C, groups);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, g.grid, dim3(256), 0, s, dy, lddy, dy_gs, y, ldy, y_gs, pre, ldp, pre_gs,
-                     rows, C, mean, invstd, ms_gs, beta, beta_gs, acc, acc_gs, sh, nsh, dbeta, dbeta_gs, act, dpre, lddp,
-                     dpre_gs, dres, ldres, dres_gs, res_acc, g.rpb, dpre_bf16);
+  BWA_LAUNCH(4, g)
+#undef BWA_LAUNCH
 }

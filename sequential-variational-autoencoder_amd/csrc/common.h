@@ -150,6 +150,21 @@ __device__ __forceinline__ void st_out16(float* base, long long off, f32x4 v) {
   *(f32x4*)(base + off) = v;
 #endif
 }
+// Pre-BN conv outputs stored as bf16 (bf16 mode, DESIGN §5 "bf16 pre"): the producing epilogue rounds
+// the fp32 sum (RNE) before it takes the BN statistics and stores 2 bytes; every reader widens.  Offsets
+// and strides stay in elements of the storage type (a bf16 tensor's group g starts g * gs bf16 elements in)
+typedef __bf16 pf_bf16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float bf_rnd(float v) { return (float)(__bf16)v; }
+__device__ __forceinline__ const float* pf_at(const float* p, long long off, bool bf) {
+  return bf ? (const float*)((const __bf16*)p + off) : p + off;
+}
+__device__ __forceinline__ float pf_ld(const float* p, long long i, bool bf) {
+  return bf ? (float)((const __bf16*)p)[i] : p[i];
+}
+__device__ __forceinline__ f32x4 pf_ld4(const float* p, long long i, bool bf) {  // i % 4 == 0
+  if (bf) return __builtin_convertvector(*(const pf_bf16x4*)((const __bf16*)p + i), f32x4);
+  return *(const f32x4*)(p + i);
+}
 __device__ __forceinline__ void fx_add(u64* p, float v) {
   const double d = (double)v * 65536.0;  // exact
   const double fl = floor(d);
@@ -162,6 +177,63 @@ __device__ __forceinline__ double fx_get(const u64* p) {
 __device__ __forceinline__ void stat_put(u64* acc, int c, float s, float q) {
   fx_add(acc + 4 * c, s);
   fx_add(acc + 4 * c + 2, q);
+}
+
+// Last-arriver finalisation of forward BN statistics (FwdArgs::fin): after a producer block has added its
+// column partials (stat_put), it counts itself in on the group's arrival counter; the block that arrives
+// last -- every other block's atomics are then complete -- sums the accumulator shards of all C columns as
+// integers and writes mean / invstd with bn_apply's own fp64 expression (bitwise what bn_apply would
+// compute), so the apply pass reads two floats per channel instead of gathering nsh x 4 words per channel
+// in every block (that gather, served from the memory side since the atomics bypass the XCD L2s, cost
+// 2.5 % of the bf16 step and 7 % of the bf16x6 step: SVAE_DBG_SKIP=16 probe)
+struct BnFin {
+  u64* cnt;            // arrival counters [group] (zeroed with the accumulators once per pass); nullptr: off
+  int nblk;            // producer blocks (tiles) per group: set by the launcher
+  const u64* acc; long long acc_gs, sh; int nsh;
+  int C;
+  long long rows; float eps;
+  float* mean; float* invstd; long long ms_gs;  // mode 1: a = mean(dz) into mean, b = mean(dz * xhat) into invstd
+  int mode;            // 0: forward (mean, invstd); 1: backward sums (a, b, and dbeta = sum dz)
+  float* dbeta; long long dbeta_gs;
+};
+// Ordering without agent-scope fences: those write back the whole XCD L2 on gfx950 (buffer_wbl2), per block
+// -- 2.3x the step.  The statistics and the counter are device-scope atomics, performed where every XCD
+// sees them; a thread waits for its own statistics atomics to be acknowledged (s_waitcnt) before the
+// block counts itself in, and the last block reads the accumulators with device-scope atomic loads.
+__device__ __forceinline__ void bn_fin_arrive(const BnFin& f, int group, int* flag) {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_s_waitcnt(0);  // this thread's stat_put atomics are performed
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const u64 prev = __hip_atomic_fetch_add(f.cnt + group, 1ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = prev == (u64)(f.nblk - 1) ? 1 : 0;
+  }
+  __syncthreads();
+  const int last = *flag;
+  __syncthreads();  // (flag may live in a region the caller reuses)
+  if (!last) return;
+  const u64* acc = f.acc + group * f.acc_gs;
+  for (int c = threadIdx.x; c < f.C; c += blockDim.x) {
+    u64 t[4] = {0, 0, 0, 0};
+    for (int k = 0; k < f.nsh; ++k)
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+        t[w] += __hip_atomic_load(acc + k * f.sh + 4LL * c + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const double cnt = (double)f.rows;
+    if (f.mode == 1) {  // bn_bwd_apply's expressions
+      const double sd = fx_get(t), sx = fx_get(t + 2);
+      f.mean[group * f.ms_gs + c] = (float)(sd / cnt);
+      f.invstd[group * f.ms_gs + c] = (float)(sx / cnt);
+      if (f.dbeta) f.dbeta[group * f.dbeta_gs + c] = (float)sd;
+      continue;
+    }
+    const double md = fx_get(t) / cnt;
+    double var = fx_get(t + 2) / cnt - md * md;
+    if (var < 0.0) var = 0.0;
+    f.mean[group * f.ms_gs + c] = (float)md;
+    f.invstd[group * f.ms_gs + c] = (float)(1.0 / sqrt(var + (double)f.eps));
+  }
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

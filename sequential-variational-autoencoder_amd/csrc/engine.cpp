@@ -623,6 +623,13 @@ struct svae_ctx {
   // wgrad GEMMs, round them identically while staging (opload.h)
   int dbf = 0;
   int abf = 0;  // bf16 mode: the post-activation tensors read only by bf16 GEMMs are stored as bf16
+  // bf16 mode: every conv layer's pre-BN output is stored as bf16 by its GEMM epilogue (the BN statistics
+  // of the stored values); the BN apply / backward passes and the fused backward-BN epilogues widen it
+  int pbf = 0;
+  // conv BN statistics finalised by the producing halo_kw launch's last block (common.h BnFin): the apply
+  // passes read mean / invstd (bit 0, forward) or a, b (bit 1, the fused backward sums) instead of every
+  // block finalising its channels (SVAE_BN_LAF; bitwise, but off: 9.5 % / 16 % slower, profiles/r04_laf_ab.txt)
+  int laf = 0;
   float* Gimp_pub = nullptr;         // caller's improvement-loss gradient (svae_bind_imp)
   float* Gimp_v = nullptr;           // its virtual copy under weight sharing
   // BN statistics: fixed-point column accumulators (common.h stat_put), one region per BN
@@ -718,6 +725,7 @@ struct Defer {
   BNS bn;
   long long bn_gs = 0;
   int act = 0;
+  bool fin = false;              // mean / invstd finalised by the producer's last block (BnFin)
   hipEvent_t applied = nullptr;  // on st2, after the apply
 };
 
@@ -1028,7 +1036,9 @@ static void wgemm(svae_ctx* c, const WgArgs& w, int groups) {
 // SVAE_DBG_SKIP (timing probe, WRONG RESULTS): bit 0 skips the forward BN apply of the layers whose
 // output only bf16 GEMMs read, bit 1 the backward BN apply of the conv layers without a shortcut --
 // the step time without the passes a consumer-side fold would remove (an upper bound of its gain);
-// bit 2 every conv weight gradient (side stream), bit 3 the per-bucket Adam of the chain steps
+// bit 2 every conv weight gradient (side stream), bit 3 the per-bucket Adam of the chain steps; bit 4 makes
+// the conv layers' forward BN apply read last step's mean / invstd instead of finalising the statistics
+// accumulators per block (the gain a producer-side finalise could bring)
 static int dbg_skip() {
   static const int v = [] {
     const char* e = getenv("SVAE_DBG_SKIP");
@@ -1073,17 +1083,35 @@ static int conv_bn_act_fwd(svae_ctx* c, const ConvL& L, int groups, long long w_
     t.A = d.pre;
     t.a_gs = d.gs;
     t.lda = d.ld;
-    t.a_bf16 = 0;
+    t.a_bf16 = c->pbf;  // the pre-BN tensor's storage
     t.ain = AinBN{d.acc.p, d.acc.gs, d.acc.sh, d.acc.nsh, d.rows, d.beta, d.beta_gs, d.bn.mean, d.bn.invstd, d.bn_gs,
-                  d.act, 1e-3f};
+                  d.act, 1e-3f, d.fin ? 1 : 0};
     if (ain_ok(c, t, groups)) a = t;
     else hipStreamWaitEvent(c->st, d.applied, 0);  // stage the applied tensor
   }
   const AccR acc = acc_bn(c, groups, L.cout, gemm_nrb(c, a, groups));
   if (!acc.p) return fail(c, SVAE_EBADARG, "BN accumulator arena too small");
   set_stats(a, acc);
-  gemm(c, a, groups);
+  if (c->pbf) {  // every conv BN layer: its readers in the backward take the same flag (c->pbf)
+    if (!igemm_c_bf16_ok(a, groups)) return fail(c, SVAE_EBADARG, "bf16 pre-BN output: no kernel for this launch");
+    a.c_bf16 = 1;
+  }
   const long long rows = (long long)B * L.hout * L.hout;
+  bool fin = false;  // mean / invstd finalised by the producer's last block
+  if ((c->laf & 1) && c->m.g.bf16 && a.Bh) {
+    FwdArgs u = a;
+    if (c->m.g.split) {
+      u.nsp = 3;
+      u.b_plane = c->wplane;
+    }
+    if (igemm_fin_ok(u, groups)) {
+      u64* cnt = acc_take(c, groups);
+      if (!cnt) return fail(c, SVAE_EBADARG, "BN accumulator arena too small");
+      a.fin = BnFin{cnt, 0, acc.p, acc.gs, acc.sh, acc.nsh, L.cout, rows, 1e-3f, bn.mean, bn.invstd, bn_gs, 0, nullptr, 0};
+      fin = true;
+    }
+  }
+  gemm(c, a, groups);
   if ((dbg_skip() & 1) && out.bf && !res.p) return 0;  // TIMING PROBE ONLY (wrong results): no apply pass
   if (dfr_out && c->fold && c->side && !res.p) {  // the apply on st2, off the critical path
     hipEvent_t ready = c->ev_fold[c->fold_pos];
@@ -1091,8 +1119,8 @@ static int conv_bn_act_fwd(svae_ctx* c, const ConvL& L, int groups, long long w_
     c->fold_pos = (c->fold_pos + 2) % svae_ctx::NFOLD;
     hipEventRecord(ready, c->st);
     hipStreamWaitEvent(c->st2, ready, 0);
-    bn_apply(pre, L.cout, pre_gs, rows, L.cout, acc.p, acc.gs, acc.sh, acc.nsh, 1e-3f, bn.mean, bn.invstd, bn_gs,
-             c->P + L.obeta, w_gs, nullptr, 0, 0, act, out.p, out.ld, out.gs, groups, c->st2, out.bf);
+    bn_apply(pre, L.cout, pre_gs, rows, L.cout, fin ? nullptr : acc.p, acc.gs, acc.sh, acc.nsh, 1e-3f, bn.mean, bn.invstd,
+             bn_gs, c->P + L.obeta, w_gs, nullptr, 0, 0, act, out.p, out.ld, out.gs, groups, c->st2, out.bf, c->pbf);
     hipEventRecord(applied, c->st2);
     c->fold_used = true;
     Defer& d = *dfr_out;
@@ -1106,12 +1134,14 @@ static int conv_bn_act_fwd(svae_ctx* c, const ConvL& L, int groups, long long w_
     d.bn = bn;
     d.bn_gs = bn_gs;
     d.act = act;
+    d.fin = fin;
     d.applied = applied;
     return 0;
   }
   if (dfr_out) *dfr_out = Defer{};
-  bn_apply(pre, L.cout, pre_gs, rows, L.cout, acc.p, acc.gs, acc.sh, acc.nsh, 1e-3f, bn.mean, bn.invstd, bn_gs, c->P + L.obeta, w_gs,
-           res.p, res.ld, res.gs, act, out.p, out.ld, out.gs, groups, c->st, out.bf);
+  bn_apply(pre, L.cout, pre_gs, rows, L.cout, (fin || (dbg_skip() & 16)) ? nullptr : acc.p, acc.gs, acc.sh, acc.nsh, 1e-3f, bn.mean,
+           bn.invstd, bn_gs, c->P + L.obeta, w_gs, res.p, res.ld, res.gs, act, out.p, out.ld, out.gs, groups, c->st, out.bf,
+           c->pbf);
   return 0;
 }
 
@@ -1236,15 +1266,21 @@ struct BwFuse {
   BwStat bw{};
   AccR acc;  // accumulators the fused epilogue adds into
   bool used = false;
+  float* dbeta = nullptr;   // the layer's beta gradient
+  long long dbeta_gs = 0;
+  float* ab = nullptr;      // a, b finalised by the producing launch's last block ([group][2C]; BnFin mode 1)
 };
 static BwFuse bw_fuse(svae_ctx* c, const float* pre, int ldp, long long pre_gs, const float* y, int ldy, long long y_gs,
-                      BNS bn, long long bn_gs, long long beta_off, long long w_gs, int act, int C) {
+                      BNS bn, long long bn_gs, long long beta_off, long long w_gs, int act, int C, int pre_bf16) {
   BwFuse f;
   f.bw.pre = pre; f.bw.ldp = ldp; f.bw.pre_gs = pre_gs;
   f.bw.y = y; f.bw.ldy = ldy; f.bw.y_gs = y_gs;
   f.bw.mean = bn.mean; f.bw.invstd = bn.invstd; f.bw.ms_gs = bn_gs;
   f.bw.beta = c->P + beta_off; f.bw.beta_gs = w_gs;
   f.bw.act = act; f.bw.C = C;
+  f.bw.pre_bf16 = pre_bf16;
+  f.dbeta = c->Gr ? c->Gr + beta_off : nullptr;
+  f.dbeta_gs = w_gs;
   return f;
 }
 
@@ -1322,6 +1358,21 @@ static int conv_dgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, c
       set_stats(a, acc);
       fu->acc = acc;
       fu->used = true;
+      fu->ab = nullptr;
+      FwdArgs u = a;
+      if (c->m.g.split) {
+        u.nsp = 3;
+        u.b_plane = c->wplane;
+      }
+      if ((c->laf & 2) && fu->dbeta && igemm_fin_ok(u, groups)) {  // a, b, dbeta by the last block
+        const int C = fu->bw.C;
+        u64* cnt = acc_take(c, groups);
+        float* ab = (float*)acc_take(c, (long long)groups * C);  // [group][2C] floats
+        if (!cnt || !ab) return fail(c, SVAE_EBADARG, "BN accumulator arena too small");
+        a.fin = BnFin{cnt, 0, acc.p, acc.gs, acc.sh, acc.nsh, C, (long long)B * L.hin * L.hin, 1e-3f, ab, ab + C,
+                      2LL * C, 1, fu->dbeta, fu->dbeta_gs};
+        fu->ab = ab;
+      }
     }
   }
   gemm(c, a, groups);
@@ -1331,7 +1382,8 @@ static int conv_dgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, c
 // BN(+act) backward: dy (grad wrt post-act out y) -> dpre; dbeta into grads; optional dres
 static int bn_act_bwd(svae_ctx* c, int groups, long long rows, int C, View dy, View y, const float* pre, long long pre_gs,
                       int ldp, BNS bn, long long bn_gs, long long beta_off, long long w_gs, int act, float* dpre,
-                      long long dpre_gs, View dres, int res_acc, const BwFuse* fu = nullptr, int dpre_bf16 = 0) {
+                      long long dpre_gs, View dres, int res_acc, const BwFuse* fu = nullptr, int dpre_bf16 = 0,
+                      int pre_bf16 = 0) {
   const bool pre_reduced = fu && fu->used;  // sums already added by the fused dgrad epilogue
   const AccR acc = pre_reduced ? fu->acc : acc_bn(c, groups, C, bn_bwd_rowblocks(rows));
   if (!acc.p) return fail(c, SVAE_EBADARG, "BN accumulator arena too small");
@@ -1340,11 +1392,11 @@ static int bn_act_bwd(svae_ctx* c, int groups, long long rows, int C, View dy, V
   const float* beta = c->P + beta_off;
   if (!pre_reduced)
     bn_bwd_reduce(dy.p, dy.ld, dy.gs, yp, y.ld, y.gs, pre, ldp, pre_gs, rows, C, bn.mean, bn.invstd, bn_gs, beta, w_gs,
-                  act, acc.p, acc.gs, acc.sh, acc.nsh, groups, c->st);
+                  act, acc.p, acc.gs, acc.sh, acc.nsh, groups, c->st, pre_bf16);
   if ((dbg_skip() & 2) && !dres.p && rows > c->m.g.B) return 0;  // TIMING PROBE ONLY (wrong results)
   bn_bwd_apply(dy.p, dy.ld, dy.gs, yp, y.ld, y.gs, pre, ldp, pre_gs, rows, C, bn.mean, bn.invstd, bn_gs, beta, w_gs,
                acc.p, acc.gs, acc.sh, acc.nsh, c->Gr + beta_off, w_gs, act, dpre, C, dpre_gs, dres.p, dres.ld, dres.gs, res_acc, groups,
-               c->st, dpre_bf16);
+               c->st, dpre_bf16, pre_bf16, pre_reduced ? fu->ab : nullptr);
   return 0;
 }
 
@@ -1480,10 +1532,11 @@ static int inference_fwd(svae_ctx* c, int t0, int n, View in0) {
     View in = lvl == 0 ? in0 : View{c->inf_act_b[lvl - 1] + t0 * c->inf_gs[lvl - 1], F[lvl], c->inf_gs[lvl - 1]};
     float* act_a = elem_off(c->inf_act_a[lvl], t0 * gs, c->abf);  // bf16 storage: step t0's group in bf16 elements
     Defer da;  // conv a's apply deferred to st2 (SVAE_FOLD): conv b's gather stages it from pre
-    r = conv_bn_act_fwd(c, I.a[lvl], n, wg, in, c->inf_pre_a[lvl] + t0 * gs, gs, bns(c->inf_bn_a[lvl], Fl), Fl, View{},
+    r = conv_bn_act_fwd(c, I.a[lvl], n, wg, in, elem_off(c->inf_pre_a[lvl], t0 * gs, c->pbf), gs, bns(c->inf_bn_a[lvl], Fl), Fl, View{},
                         ACT_LRELU, View{act_a, Fl, gs, c->abf}, &da);
     if (r) return r;
-    r = conv_bn_act_fwd(c, I.b[lvl], n, wg, View{act_a, Fl, gs, c->abf, da.pre ? &da : nullptr}, c->inf_pre_b[lvl] + t0 * gs, gs,
+    r = conv_bn_act_fwd(c, I.b[lvl], n, wg, View{act_a, Fl, gs, c->abf, da.pre ? &da : nullptr},
+                        elem_off(c->inf_pre_b[lvl], t0 * gs, c->pbf), gs,
                         bns(c->inf_bn_b[lvl], Fl), Fl, View{}, ACT_LRELU, View{c->inf_act_b[lvl] + t0 * gs, Fl, gs});
     if (r) return r;
     for (int hl = 0; hl < L; ++hl) {
@@ -1872,8 +1925,8 @@ static int inference_bwd(svae_ctx* c, int t0, int n, View in0, float* dx0) {
   auto bns = [&](const BNS& b, int C) { return BNS{b.mean + (long long)t0 * C, b.invstd + (long long)t0 * C}; };
   auto act_a = [&](int l) { return elem_off(c->inf_act_a[l], t0 * c->inf_gs[l], c->abf); };
   auto act_b = [&](int l) { return c->inf_act_b[l] + t0 * c->inf_gs[l]; };
-  auto pre_a = [&](int l) { return c->inf_pre_a[l] + t0 * c->inf_gs[l]; };
-  auto pre_b = [&](int l) { return c->inf_pre_b[l] + t0 * c->inf_gs[l]; };
+  auto pre_a = [&](int l) { return elem_off(c->inf_pre_a[l], t0 * c->inf_gs[l], c->pbf); };
+  auto pre_b = [&](int l) { return elem_off(c->inf_pre_b[l], t0 * c->inf_gs[l], c->pbf); };
   // heads of ladder level l -> idb (first write), l's own conv-a input gradient (level l+1) after them
   auto heads_of = [&](int l) {
     bool first = true;
@@ -1897,7 +1950,7 @@ static int inference_bwd(svae_ctx* c, int t0, int n, View in0, float* dx0) {
     Slot sb = idpre_next(c, n * gs);
     r = bn_act_bwd(c, n, rows, Fl, View{c->idb, Fl, gs}, View{act_b(lvl), Fl, gs}, pre_b(lvl), gs, Fl,
                    bns(c->inf_bn_b[lvl], Fl), Fl, I0.b[lvl].obeta, wg, ACT_LRELU, sb.p, gs, View{}, 0, &fu_ib,
-                   dpre_bf(c, I0.b[lvl]));
+                   dpre_bf(c, I0.b[lvl]), c->pbf);
     if (r) return r;
     {
       const ConvL Lw = I0.b[lvl];
@@ -1908,13 +1961,13 @@ static int inference_bwd(svae_ctx* c, int t0, int n, View in0, float* dx0) {
     }
     if (r) return r;
     BwFuse fu_ia = bw_fuse(c, pre_a(lvl), Fl, gs, nullptr, 0, 0, bns(c->inf_bn_a[lvl], Fl), Fl, I0.a[lvl].obeta, wg,
-                           ACT_LRELU, Fl);
+                           ACT_LRELU, Fl, c->pbf);
     r = conv_dgrad(c, I0.b[lvl], n, wg, sb.p, gs, View{c->ida, Fl, gs}, 0, &fu_ia);
     if (r) return r;
     Slot sa = idpre_next(c, n * gs);
     r = bn_act_bwd(c, n, rows, Fl, View{c->ida, Fl, gs}, View{act_a(lvl), Fl, gs}, pre_a(lvl), gs, Fl,
                    bns(c->inf_bn_a[lvl], Fl), Fl, I0.a[lvl].obeta, wg, ACT_LRELU, sa.p, gs, View{}, 0, &fu_ia,
-                   dpre_bf(c, I0.a[lvl]));
+                   dpre_bf(c, I0.a[lvl]), c->pbf);
     if (r) return r;
     View in = lvl == 0 ? in0 : View{act_b(lvl - 1), F[lvl], c->inf_gs[lvl - 1]};
     {
@@ -1927,7 +1980,7 @@ static int inference_bwd(svae_ctx* c, int t0, int n, View in0, float* dx0) {
     if (lvl > 0) {
       const bool wrote = heads_of(lvl - 1);
       fu_ib = bw_fuse(c, pre_b(lvl - 1), F[lvl], c->inf_gs[lvl - 1], nullptr, 0, 0, bns(c->inf_bn_b[lvl - 1], F[lvl]), F[lvl],
-                      I0.b[lvl - 1].obeta, wg, ACT_LRELU, F[lvl]);
+                      I0.b[lvl - 1].obeta, wg, ACT_LRELU, F[lvl], c->pbf);
       r = conv_dgrad(c, I0.a[lvl], n, wg, sa.p, gs, View{c->idb, F[lvl], c->inf_gs[lvl - 1]}, wrote ? 1 : 0, &fu_ib);
       if (r) return r;
     } else if (dx0) {  // Latent InfoMax: d loss / d x_{t-1} through q(z_t | x_{t-1})
@@ -2072,7 +2125,7 @@ static int engine_backward_pass(svae_ctx* c) {
       // s1[0]'s BN-backward partials in this input gradient's epilogue (small-channel kernel only)
       fu_s1 = BwFuse{};
       if (!nofuse_out()) {
-        BwFuse f = bw_fuse(c, s.s1_pre[0], F[1], 0, nullptr, 0, 0, s.s1_bn[0], 0, G.s1[0].obeta, 0, ACT_RELU, F[1]);
+        BwFuse f = bw_fuse(c, s.s1_pre[0], F[1], 0, nullptr, 0, 0, s.s1_bn[0], 0, G.s1[0].obeta, 0, ACT_RELU, F[1], c->pbf);
         FwdArgs t = a;
         t.bw = f.bw;
         t.stats = (u64*)1;  // (eligibility only)
@@ -2099,7 +2152,7 @@ static int engine_backward_pass(svae_ctx* c) {
       // s1: relu(BN(convT_s1(cat)))
       Slot sl = dpre_next(c, rows * Fl);
       r = bn_act_bwd(c, 1, rows, Fl, View{dcur, Fl, 0}, View{s.s1_act[lvl], Fl, 0}, s.s1_pre[lvl], 0, Fl, s.s1_bn[lvl],
-                     0, l1.obeta, 0, ACT_RELU, sl.p, 0, View{}, 0, &fu_s1, dpre_bf(c, l1));
+                     0, l1.obeta, 0, ACT_RELU, sl.p, 0, View{}, 0, &fu_s1, dpre_bf(c, l1), c->pbf);
       if (r) return r;
       if (t == c->dbg_stop_step && lvl == c->dbg_stop_lvl2) { c->dbg_last = dcur; return 0; }
       {
@@ -2112,7 +2165,7 @@ static int engine_backward_pass(svae_ctx* c) {
       if (r) return r;
       // s2[lvl]'s BN partials over the d-half of dcat (shortcut at t >= 1: act' from the stored y)
       BwFuse fu_s2 = bw_fuse(c, s.s2_pre[lvl], Fl, 0, t >= 1 ? s.cat[lvl] : nullptr, 2 * Fl, 0, s.s2_bn[lvl], 0,
-                             l2.obeta, 0, ACT_RELU, Fl);
+                             l2.obeta, 0, ACT_RELU, Fl, c->pbf);
       // dcat: its own region per pass when the split-latent backward reads it on the side stream
       float* dcat = c->side ? arena_next(c, c->dcat_arena, c->dcat_cap, c->dcat_off, rows * 2 * Fl, true) : c->dcat;
       r = conv_dgrad(c, l1, 1, 0, sl.p, 0, View{dcat, 2 * Fl, 0}, 0, &fu_s2);
@@ -2136,7 +2189,7 @@ static int engine_backward_pass(svae_ctx* c) {
       View dres = t >= 1 ? View{c->denc[lvl], Fl, 0} : View{};
       sl = dpre_next(c, rows * Fl);
       r = bn_act_bwd(c, 1, rows, Fl, View{dcat, 2 * Fl, 0}, View{s.cat[lvl], 2 * Fl, 0}, s.s2_pre[lvl], 0, Fl,
-                     s.s2_bn[lvl], 0, l2.obeta, 0, ACT_RELU, sl.p, 0, dres, 0, &fu_s2, dpre_bf(c, l2));
+                     s.s2_bn[lvl], 0, l2.obeta, 0, ACT_RELU, sl.p, 0, dres, 0, &fu_s2, dpre_bf(c, l2), c->pbf);
       if (r) return r;
       View in = lvl == L - 2 ? View{s.top_act, F[L], 0, c->abf} : View{s.s1_act[lvl + 1], F[lvl + 2], 0, c->abf};
       {
@@ -2148,7 +2201,7 @@ static int engine_backward_pass(svae_ctx* c) {
       if (r) return r;
       if (lvl < L - 2) {  // next: s1[lvl+1] (no shortcut)
         fu_s1 = bw_fuse(c, s.s1_pre[lvl + 1], F[lvl + 2], 0, nullptr, 0, 0, s.s1_bn[lvl + 1], 0, G.s1[lvl + 1].obeta, 0,
-                        ACT_RELU, F[lvl + 2]);
+                        ACT_RELU, F[lvl + 2], c->pbf);
         r = conv_dgrad(c, l2, 1, 0, sl.p, 0, View{dnext, in.ld, 0}, 0, &fu_s1);
       } else {
         r = conv_dgrad(c, l2, 1, 0, sl.p, 0, View{dnext, in.ld, 0}, 0);
@@ -2166,7 +2219,7 @@ static int engine_backward_pass(svae_ctx* c) {
     BwFuse fu_efc;
     if (t >= 1) {
       const FcL& ef = M.enc[t].fc;
-      fu_efc = bw_fuse(c, s.encfc_pre, ef.nout, 0, nullptr, 0, 0, s.enc_bn_fc, 0, ef.obeta, 0, ACT_LRELU, ef.nout);
+      fu_efc = bw_fuse(c, s.encfc_pre, ef.nout, 0, nullptr, 0, 0, s.enc_bn_fc, 0, ef.obeta, 0, ACT_LRELU, ef.nout, 0);
     }
     r = fc_bn_bwd(c, G.top, View{s.top_cat, s.ktop, 0}, View{dcur, ntop, 0}, View{s.top_act, ntop, 0}, s.top_pre,
                   s.top_bn, View{dtop, s.ktop, 0}, nullptr, t >= 1 ? &fu_efc : nullptr);
@@ -2196,7 +2249,7 @@ static int engine_backward_pass(svae_ctx* c) {
       Slot sl = dpre_next(c, rc * F[L - 1]);
       r = bn_act_bwd(c, 1, rc, F[L - 1], View{c->denc_c, F[L - 1], 0}, View{s.enc_c_act, F[L - 1], 0}, s.enc_c_pre, 0,
                      F[L - 1], s.enc_bn_c, 0, E.c.obeta, 0, ACT_LRELU, sl.p, 0, View{}, 0, nullptr,
-                     dpre_bf(c, E.c));
+                     dpre_bf(c, E.c), c->pbf);
       if (r) return r;
       {
         const ConvL Lw = E.c;
@@ -2208,7 +2261,7 @@ static int engine_backward_pass(svae_ctx* c) {
       if (r) return r;
       // E.c's input gradient accumulates last into denc[L-2] (after the decoder shortcut term)
       BwFuse fu_eb = bw_fuse(c, s.enc_pre_b[L - 2], F[L - 1], 0, nullptr, 0, 0, s.enc_bn_b[L - 2], 0, E.b[L - 2].obeta,
-                             0, ACT_LRELU, F[L - 1]);
+                             0, ACT_LRELU, F[L - 1], c->pbf);
       r = conv_dgrad(c, E.c, 1, 0, sl.p, 0, View{c->denc[L - 2], F[L - 1], 0}, 1, &fu_eb);
       if (r) return r;
       for (int lvl = L - 2; lvl >= 0; --lvl) {
@@ -2217,7 +2270,7 @@ static int engine_backward_pass(svae_ctx* c) {
         Slot sb = dpre_next(c, rows * Fl);
         r = bn_act_bwd(c, 1, rows, Fl, View{c->denc[lvl], Fl, 0}, View{s.enc_act_b[lvl], Fl, 0}, s.enc_pre_b[lvl], 0,
                        Fl, s.enc_bn_b[lvl], 0, E.b[lvl].obeta, 0, ACT_LRELU, sb.p, 0, View{}, 0, &fu_eb,
-                       dpre_bf(c, E.b[lvl]));
+                       dpre_bf(c, E.b[lvl]), c->pbf);
         if (r) return r;
         {
           const ConvL Lw = E.b[lvl];
@@ -2228,13 +2281,13 @@ static int engine_backward_pass(svae_ctx* c) {
         }
         if (r) return r;
         BwFuse fu_ea = bw_fuse(c, s.enc_pre_a[lvl], Fl, 0, nullptr, 0, 0, s.enc_bn_a[lvl], 0, E.a[lvl].obeta, 0,
-                               ACT_LRELU, Fl);
+                               ACT_LRELU, Fl, c->pbf);
         r = conv_dgrad(c, E.b[lvl], 1, 0, sb.p, 0, View{c->dcur, Fl, 0}, 0, &fu_ea);
         if (r) return r;
         Slot sa = dpre_next(c, rows * Fl);
         r = bn_act_bwd(c, 1, rows, Fl, View{c->dcur, Fl, 0}, View{s.enc_act_a[lvl], Fl, 0}, s.enc_pre_a[lvl], 0, Fl,
                        s.enc_bn_a[lvl], 0, E.a[lvl].obeta, 0, ACT_LRELU, sa.p, 0, View{}, 0, &fu_ea,
-                       dpre_bf(c, E.a[lvl]));
+                       dpre_bf(c, E.a[lvl]), c->pbf);
         if (r) return r;
         View in = lvl == 0 ? View{(float*)xprev, g.C, 0} : View{s.enc_act_b[lvl - 1], F[lvl], 0};
         {
@@ -2247,7 +2300,7 @@ static int engine_backward_pass(svae_ctx* c) {
         View din = lvl == 0 ? View{dxout, g.C, 0} : View{c->denc[lvl - 1], F[lvl], 0};
         if (lvl > 0) {  // accumulates last into denc[lvl-1]: E.b[lvl-1]'s BN partials
           fu_eb = bw_fuse(c, s.enc_pre_b[lvl - 1], F[lvl], 0, nullptr, 0, 0, s.enc_bn_b[lvl - 1], 0, E.b[lvl - 1].obeta,
-                          0, ACT_LRELU, F[lvl]);
+                          0, ACT_LRELU, F[lvl], c->pbf);
           r = conv_dgrad(c, E.a[lvl], 1, 0, sa.p, 0, din, 1, &fu_eb);
         } else {
           r = conv_dgrad(c, E.a[lvl], 1, 0, sa.p, 0, din, 1);
@@ -2540,6 +2593,10 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
     c->dbf = (c->m.g.bf16 && !c->m.g.split && !(v && v[0] == '1')) ? 1 : 0;
     const char* va = getenv("SVAE_ACT_F32");  // A/B: keep every activation in fp32
     c->abf = (c->m.g.bf16 && !c->m.g.split && !(va && va[0] == '1')) ? 1 : 0;
+    const char* vl = getenv("SVAE_BN_LAF");
+    c->laf = vl ? atoi(vl) : 0;
+    const char* vp = getenv("SVAE_PRE_F32");  // A/B: keep the conv layers' pre-BN outputs in fp32
+    c->pbf = (c->m.g.bf16 && !c->m.g.split && !(vp && vp[0] == '1')) ? 1 : 0;
   }
   c->counting = true;
   c->arena_used = 0;
@@ -3062,13 +3119,13 @@ int svae_copy_out(svae_ctx* c, int which, int step, float* dst, int64_t n, void*
     case 102: c->dbg_stop_lvl = step; return 0;                                     // debug: stop level
     case 103: src = c->dcur; cnt = n; break;                                        // debug: raw scratch
     case 104: src = c->dnext; cnt = n; break;
-    case 105: src = c->sb[c->dbg_stop_step].s1_pre[step]; cnt = n; break;           // debug: saved tensors
+    case 105: src = c->sb[c->dbg_stop_step].s1_pre[step]; cnt = n; src_bf16 = c->pbf; break;  // debug: saved tensors
     case 109: src = c->dpre; cnt = n; break;
     case 110: src = c->dbg_last; cnt = n; break;
     case 111: c->dbg_stop_lvl2 = step; return 0;
-    case 113: src = c->inf_pre_a[step]; cnt = n; break;   // debug: inference level `step`, all T groups
+    case 113: src = c->inf_pre_a[step]; cnt = n; src_bf16 = c->pbf; break;  // debug: inference level `step`, all T groups
     case 114: src = c->inf_act_a[step]; cnt = n; src_bf16 = c->abf; break;
-    case 115: src = c->inf_pre_b[step]; cnt = n; break;
+    case 115: src = c->inf_pre_b[step]; cnt = n; src_bf16 = c->pbf; break;
     case 116: src = c->inf_act_b[step]; cnt = n; break;
     case 106: src = c->sb[c->dbg_stop_step].s1_act[step]; cnt = n; src_bf16 = c->abf; break;
     case 107: src = c->sb[c->dbg_stop_step].s1_bn[step].mean; cnt = n; break;

@@ -291,7 +291,8 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
     const int n = n0 + wn0 + tn * 32 + l32;
     biasv[tn] = (bias && n < a.N) ? bias[n] : 0.f;
   }
-  const float* bwpre = bwm ? a.bw.pre + group * a.bw.pre_gs : nullptr;
+  const bool pbf = a.bw.pre_bf16 != 0;
+  const float* bwpre = bwm ? pf_at(a.bw.pre, group * a.bw.pre_gs, pbf) : nullptr;
   const float* bwy = (bwm && a.bw.y) ? a.bw.y + group * a.bw.y_gs : nullptr;
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
@@ -312,7 +313,7 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
           const bool ok = mok[i] && n < a.N;
           const bool bwc = ok && bwm && n < a.bw.C;
           cv[i][tn] = (ok && a.accumulate) ? Cp[orow[i] * a.ldc + n] : 0.f;
-          pv[i][tn] = bwc ? bwpre[orow[i] * a.bw.ldp + n] : 0.f;
+          pv[i][tn] = bwc ? pf_ld(bwpre, orow[i] * a.bw.ldp + n, pbf) : 0.f;
           yv[i][tn] = (bwc && bwy) ? bwy[orow[i] * a.bw.ldy + n] : 0.f;
         }
       }
@@ -324,6 +325,7 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
           const int n = n0 + wn0 + tn * 32 + l32;
           if (n >= a.N) continue;
           float v = acc[tm][tn][rb + i];
+          if (a.c_bf16) v = bf_rnd(v);  // bf16-stored pre-BN output: the statistics of the stored values
           if (!bwm) {
             csum[tn] += v;
             csq[tn] += v * v;
@@ -331,7 +333,8 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
           if (bias) v += biasv[tn];
           v = act_f(v, a.act);
           if (a.accumulate) v += cv[i][tn];
-          Cp[orow[i] * a.ldc + n] = v;
+          if (a.c_bf16) ((__bf16*)a.C)[group * a.c_gs + orow[i] * a.ldc + n] = (__bf16)v;
+          else Cp[orow[i] * a.ldc + n] = v;
           if (bwm && n < a.bw.C)
             bw_term_v(v, pv[i][tn], bwmean[tn], bwis[tn], bwb[tn], bwy != nullptr, yv[i][tn], a.bw.act, csum[tn],
                       csq[tn]);
@@ -631,7 +634,8 @@ __global__ __launch_bounds__(256, (ABF && BN * BM <= 8192) ? 4 : 2) void igemm_h
     const int n = n0 + wn0 + tn * 32 + l32;
     biasv[tn] = (bias && nok[tn] && n < a.N) ? bias[n] : 0.f;
   }
-  const float* bwpre = bwm ? a.bw.pre + group * a.bw.pre_gs : nullptr;
+  const bool pbf = a.bw.pre_bf16 != 0;
+  const float* bwpre = bwm ? pf_at(a.bw.pre, group * a.bw.pre_gs, pbf) : nullptr;
   const float* bwy = (bwm && a.bw.y) ? a.bw.y + group * a.bw.y_gs : nullptr;
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
@@ -650,7 +654,7 @@ __global__ __launch_bounds__(256, (ABF && BN * BM <= 8192) ? 4 : 2) void igemm_h
           const bool ok = nok[tn] && n < a.N;
           const bool bwc = ok && bwm && n < a.bw.C;
           cv[i][tn] = (ok && a.accumulate) ? Cp[orow[i] * a.ldc + n] : 0.f;
-          pv[i][tn] = bwc ? bwpre[orow[i] * a.bw.ldp + n] : 0.f;
+          pv[i][tn] = bwc ? pf_ld(bwpre, orow[i] * a.bw.ldp + n, pbf) : 0.f;
           yv[i][tn] = (bwc && bwy) ? bwy[orow[i] * a.bw.ldy + n] : 0.f;
         }
       }
@@ -661,6 +665,7 @@ __global__ __launch_bounds__(256, (ABF && BN * BM <= 8192) ? 4 : 2) void igemm_h
           const int n = n0 + wn0 + tn * 32 + l32;
           if (!nok[tn] || n >= a.N) continue;
           float v = acc[tm][tn][rb + i];
+          if (a.c_bf16) v = bf_rnd(v);  // bf16-stored pre-BN output: the statistics of the stored values
           if (!bwm) {
             csum[tn] += v;
             csq[tn] += v * v;
@@ -668,7 +673,8 @@ __global__ __launch_bounds__(256, (ABF && BN * BM <= 8192) ? 4 : 2) void igemm_h
           if (bias) v += biasv[tn];
           v = act_f(v, a.act);
           if (a.accumulate) v += cv[i][tn];
-          Cp[orow[i] * a.ldc + n] = v;
+          if (a.c_bf16) ((__bf16*)a.C)[group * a.c_gs + orow[i] * a.ldc + n] = (__bf16)v;
+          else Cp[orow[i] * a.ldc + n] = v;
           if (bwm && n < a.bw.C)
             bw_term_v(v, pv[i][tn], bwmean[tn], bwis[tn], bwb[tn], bwy != nullptr, yv[i][tn], a.bw.act, csum[tn],
                       csq[tn]);
@@ -1182,7 +1188,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* part, i
                                                             float* C, long long c_gs, int ldc, const float* bias,
                                                             long long bias_gs, int act, int accumulate, u64* stats,
                                                             long long s_gs, long long s_sh, int s_nsh, BwStat bw,
-                                                            int rpb) {
+                                                            int rpb, int c_bf16) {
   __shared__ f32x4 red[2][256];
   const int group = blockIdx.z;
   const int qi = threadIdx.x & 15, rl = threadIdx.x >> 4;
@@ -1217,7 +1223,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* part, i
 #pragma unroll 8
       for (int k = 1; k < ks; ++k) v[i] += *(const f32x4*)(P + k * slab + (long long)r * N + n);
       if (bwq) {
-        pr[i] = *(const f32x4*)(bw.pre + group * bw.pre_gs + (long long)r * bw.ldp + n);
+        pr[i] = pf_ld4(bw.pre, group * bw.pre_gs + (long long)r * bw.ldp + n, bw.pre_bf16 != 0);
         if (bw.y) yr[i] = *(const f32x4*)(bw.y + group * bw.y_gs + (long long)r * bw.ldy + n);
       }
     }
@@ -1232,6 +1238,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* part, i
       const int r = r0 + rl + 16 * i;
       if (r >= r1) continue;
       f32x4 w = v[i];
+      if (c_bf16) {  // bf16-stored pre-BN output: the statistics of the stored values
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = bf_rnd(w[e]);
+      }
       if (!bw.pre) {
         s1 += w;
         s2 += w * w;
@@ -1240,7 +1250,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* part, i
 #pragma unroll
       for (int e = 0; e < 4; ++e) w[e] = act_f(w[e], act);
       if (accumulate) w += cv[i];
-      *(f32x4*)(Cg + (long long)r * ldc + n) = w;
+      if (c_bf16)
+        *(pf_bf16x4*)((__bf16*)C + group * c_gs + (long long)r * ldc + n) = __builtin_convertvector(w, pf_bf16x4);
+      else
+        *(f32x4*)(Cg + (long long)r * ldc + n) = w;
       if (bwq) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1463,6 +1476,26 @@ bool igemm_split_ok(const FwdArgs& a, int groups) {
   return a.Bh && !a.a_bf16 && (dense_kw_ok(a, groups) || halo_kw_plan(a, groups) > 0 || smalln_ok(a));
 }
 
+// bf16-stored pre-BN outputs (FwdArgs::c_bf16): every bf16 launch path of a BN-statistics GEMM implements
+// them (wave-split / tiled halo, per-tap, their split-K reduce, the small-channel conv) except dense_kw
+// (FC layers keep fp32 pre); the consumer-side BN launches run on halo_kw, which implements them too
+bool igemm_c_bf16_ok(const FwdArgs& a, int groups) {
+  if (a.nsp > 1 || !a.stats || a.bias || a.act != ACT_NONE || a.accumulate || a.bw.pre) return false;
+  if (a.ldc % 4 || a.c_gs % 4 || ((uintptr_t)a.C & 7)) return false;
+  if (a.ain.acc) return halo_kw_plan(a, groups) > 0;  // (the consumer-side BN launch: halo_kw only)
+  return !dense_kw_ok(a, groups);
+}
+
+// the launch runs on halo_kw (igemm_bf16_path's choice), whose epilogue implements FwdArgs::fin
+bool igemm_fin_ok(const FwdArgs& a, int groups) {
+  if (!a.stats) return false;
+  if (a.ain.acc) return halo_kw_plan(a, groups) > 0;
+  if (a.nsp > 1) return !dense_kw_ok(a, groups) && halo_kw_plan(a, groups) > 0;
+  if (smallc_ok(a, true) || dense_kw_ok(a, groups) || halo_disabled()) return false;
+  const HaloPlan hp = halo_plan(a, groups);
+  return hp.ok && kw_first(a, hp) && halo_kw_plan(a, groups) > 0;
+}
+
 int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit) {
   if (a.ain.acc) {  // consumer-side BN of A: the wave-split halo gather only
     if (ksplit) *ksplit = 1;
@@ -1572,7 +1605,7 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
       const int rpb = dense_kw_rpb(a);
       dim3 grid((a.N + 63) / 64, (a.rows + rpb - 1) / rpb, 1);
       hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, s, a.part, ks, a.rows, a.N, a.C, a.c_gs, a.ldc,
-                         a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs, a.s_sh, a.s_nsh, a.bw, rpb);
+                         a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs, a.s_sh, a.s_nsh, a.bw, rpb, a.c_bf16);
     }
     return dense_kw_nrb(a);
   }
@@ -1612,7 +1645,7 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
       if (hp.ks > 1) {
         dim3 grid((a.N + 63) / 64, hp.nrb, groups);
         hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, s, a.part, hp.ks, a.rows_total, a.N, a.C, a.c_gs,
-                           a.ldc, a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs, a.s_sh, a.s_nsh, a.bw, SKR_ROWS);
+                           a.ldc, a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs, a.s_sh, a.s_nsh, a.bw, SKR_ROWS, a.c_bf16);
       }
       return hp.nrb;
     }
@@ -1632,7 +1665,7 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
   if (ks > 1) {
     dim3 grid((a.N + 63) / 64, nrb, groups);
     hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, s, a.part, ks, a.rows_total, a.N, a.C, a.c_gs, a.ldc,
-                       a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs, a.s_sh, a.s_nsh, a.bw, SKR_ROWS);
+                       a.bias, a.bias_gs, a.act, a.accumulate, a.stats, a.s_gs, a.s_sh, a.s_nsh, a.bw, SKR_ROWS, a.c_bf16);
   }
   return nrb;
 }

@@ -69,7 +69,7 @@ __device__ __forceinline__ long long kw_out_row(const KwArgs& h, const ConvGeom&
 // forward BN statistics or the fused backward-BN partials per column (row groups summed in LDS in a
 // fixed order: deterministic).  Stores go through st_out16 (write-through in SVAE_WT builds: a
 // 16-byte sc1 store costs what a plain one does, a 4-byte one six times as much per byte).
-template <int BM, int BN>
+template <int BM, int BN, bool PB>
 __device__ __forceinline__ void kw_epilogue_vec(const KwArgs& h, float* red, int tid, int m0, int n0, int group, int cls) {
   const FwdArgs& a = h.f;
   const ConvGeom& g = a.g;
@@ -88,7 +88,8 @@ __device__ __forceinline__ void kw_epilogue_vec(const KwArgs& h, float* red, int
     if (!a.bw.y) bb = *(const f32x4*)&a.bw.beta[group * a.bw.beta_gs + n];
   }
   if (a.bias) biasv = *(const f32x4*)&a.bias[group * a.bias_gs + n];
-  const float* bwpre = bwc ? a.bw.pre + group * a.bw.pre_gs : nullptr;
+  constexpr bool pbf = PB;  // (compile-time: a run-time choice per load serialises the batch's loads)
+  const float* bwpre = bwc ? pf_at(a.bw.pre, group * a.bw.pre_gs, pbf) : nullptr;
   const float* bwy = (bwc && a.bw.y) ? a.bw.y + group * a.bw.y_gs : nullptr;
   const bool rows_ok = rg < BM;  // (NRG > BM: the extra row groups idle)
   long long orow[NR];
@@ -101,7 +102,7 @@ __device__ __forceinline__ void kw_epilogue_vec(const KwArgs& h, float* red, int
     if (!rows_ok) continue;
     orow[i] = kw_out_row(h, g, cls, m0 + rg + i * NRG);
     if (a.accumulate) cv[i] = *(const f32x4*)&Cp[orow[i] * a.ldc + n];
-    if (bwpre) pv[i] = *(const f32x4*)&bwpre[orow[i] * a.bw.ldp + n];
+    if (bwpre) pv[i] = pf_ld4(bwpre, orow[i] * a.bw.ldp + n, pbf);
     if (bwy) yv[i] = *(const f32x4*)&bwy[orow[i] * a.bw.ldy + n];
   }
   float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
@@ -112,6 +113,10 @@ __device__ __forceinline__ void kw_epilogue_vec(const KwArgs& h, float* red, int
     f32x4 v = *(const f32x4*)&red[(0 * BM + m) * BN + c4];
 #pragma unroll
     for (int w = 1; w < 4; ++w) v += *(const f32x4*)&red[(w * BM + m) * BN + c4];
+    if (a.c_bf16) {  // bf16-stored pre-BN output: the statistics of the stored values
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = bf_rnd(v[j]);
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float x = v[j];
@@ -125,7 +130,10 @@ __device__ __forceinline__ void kw_epilogue_vec(const KwArgs& h, float* red, int
       v[j] = x;
       if (bwc) bw_term_v(x, pv[i][j], bm[j], bi[j], bb[j], bwy != nullptr, yv[i][j], a.bw.act, s1[j], s2[j]);
     }
-    st_out16(Cp, orow[i] * a.ldc + n, v);
+    if (a.c_bf16)
+      st_out8((__bf16*)a.C + group * a.c_gs + orow[i] * a.ldc + n, __builtin_bit_cast(u64, __builtin_convertvector(v, pf_bf16x4)));
+    else
+      st_out16(Cp, orow[i] * a.ldc + n, v);
   }
   if (a.stats) {
     __syncthreads();  // every wave is done reading red
@@ -147,6 +155,7 @@ __device__ __forceinline__ void kw_epilogue_vec(const KwArgs& h, float* red, int
         stat_put(a.stats + (rb & (a.s_nsh - 1)) * a.s_sh + group * a.s_gs, n0 + tid, sa, qa);
       }
     }
+    if (a.fin.cnt) bn_fin_arrive(a.fin, group, (int*)red);
   }
 }
 
@@ -160,8 +169,11 @@ __device__ __forceinline__ void kw_epilogue_vec(const KwArgs& h, float* red, int
 // next chunk's first tap under the last) instead of a whole chunk of taps one chunk ahead: 16-tap
 // instances only; frees (NTW - 2) x TN x 2 x NS fragment registers (split mode: 48 VGPRs)
 // PI: window items per thread (npix * 4 <= 256 * PI); 3 frees 8 (fp32) window registers
-template <int BM, int BN, bool S2T, bool ABF, int NS = 1, bool PST = false, bool BR = false, int PI = KW_PI>
-__global__ __launch_bounds__(256, (ABF && BN == 32 && BM <= 64 && !PST) ? (BR ? KW_OCC_BR : KW_OCC)
+// AIN: the bf16-A instances that take the consumer-side BN (a bf16-stored pre-BN tensor); the fp32-A ones
+// take it at run time (in the bf16-A ones it would cost the default instances 12-15 spilled VGPRs)
+template <int BM, int BN, bool S2T, bool ABF, int NS = 1, bool PST = false, bool BR = false, int PI = KW_PI,
+          bool AIN = false>
+__global__ __launch_bounds__(256, AIN ? (S2T ? 4 : 3) : (ABF && BN == 32 && BM <= 64 && !PST) ? ((BR || S2T) ? KW_OCC_BR : KW_OCC)
                                                                          : ((NS == 3 && BR) ? (BM == 32 ? KW_OCC_S32 : 3) : 2))
 void igemm_halo_kw_kernel(KwArgs h) {
   static_assert(NS == 1 || (NS == 3 && !ABF), "split planes from fp32 activations only");
@@ -273,7 +285,7 @@ void igemm_halo_kw_kernel(KwArgs h) {
   };
   // consumer-side BN (a.ain): a = act(bn_y(pre)) of the chunk's 8 channels of this thread (every item of
   // a thread has the same channel part tid & 3), table [mean | invstd | beta][Cin] in LDS
-  const bool ain = a.ain.acc != nullptr;
+  const bool ain = (!ABF || AIN) && a.ain.acc != nullptr;
   const float* ain_tbl = (const float*)((const char*)ksm + h.ain_off);
   auto ain_apply = [&](f32x4& lo, f32x4& hi, int chunk) {
     const int c0 = chunk * KW_CK + (tid & 3) * 8;
@@ -293,7 +305,16 @@ void igemm_halo_kw_kernel(KwArgs h) {
     for (int i = 0; i < PI; ++i) {
       const int it = tid + 256 * i;
       if (woff[i] < -1) continue;
-      if (!ABF && ain && woff[i] >= 0) ain_apply(wv[i][0], wv[i][1], chunk);  // (padding stays 0)
+      if (ain && woff[i] >= 0) {  // (padding stays 0)
+        if constexpr (ABF) {  // bf16-stored pre: widen, apply, round back (bn_apply's bf16 output, bitwise)
+          const ol_f32x8 w8 = __builtin_convertvector(__builtin_bit_cast(bf16x8, wv[i][0]), ol_f32x8);
+          f32x4 lo = {w8[0], w8[1], w8[2], w8[3]}, hi = {w8[4], w8[5], w8[6], w8[7]};
+          ain_apply(lo, hi, chunk);
+          wv[i][0] = __builtin_bit_cast(f32x4, raw8_bf(lo, hi, false));
+        } else {
+          ain_apply(wv[i][0], wv[i][1], chunk);
+        }
+      }
       const int o = (it >> 2) * KW_ROWP + (it & 3) * 8;
       if constexpr (NS == 1) {
         *(bf16x8*)&W[o] = raw8_bf(wv[i][0], wv[i][1], abf);
@@ -335,10 +356,16 @@ void igemm_halo_kw_kernel(KwArgs h) {
   };
 
   TileG cur = tile_geo(bx, by, bz);
-  if (!ABF && ain) {  // finalise the producer's statistics of every input channel (bn_apply's expression)
+  if (ain) {  // finalise the producer's statistics of every input channel (bn_apply's expression)
     float* tbl = (float*)((char*)ksm + h.ain_off);
     const int g = cur.group;
     for (int c = tid; c < a.Cin; c += 256) {
+      if (a.ain.fin) {  // the producer's last block finalised them (BnFin)
+        tbl[c] = a.ain.mean[g * a.ain.ms_gs + c];
+        tbl[a.Cin + c] = a.ain.invstd[g * a.ain.ms_gs + c];
+        tbl[2 * a.Cin + c] = a.ain.beta[g * a.ain.beta_gs + c];
+        continue;
+      }
       const u64* base = a.ain.acc + g * a.ain.acc_gs + 4LL * c;
       u64 t[4] = {0, 0, 0, 0};
       for (int k = 0; k < a.ain.nsh; ++k)
@@ -460,7 +487,8 @@ void igemm_halo_kw_kernel(KwArgs h) {
         }
     __syncthreads();
     if (h.vec) {  // 16-byte epilogue: 4 consecutive columns per thread (write-through-friendly stores)
-      kw_epilogue_vec<BM, BN>(h, red, tid, cur.m0, cur.n0, cur.group, cur.cls);
+      if (a.bw.pre_bf16) kw_epilogue_vec<BM, BN, true>(h, red, tid, cur.m0, cur.n0, cur.group, cur.cls);
+      else kw_epilogue_vec<BM, BN, false>(h, red, tid, cur.m0, cur.n0, cur.group, cur.cls);
       if (!has_tile) break;
       __syncthreads();
       cur = nxt;
@@ -490,14 +518,15 @@ void igemm_halo_kw_kernel(KwArgs h) {
     constexpr int NR = BM / NRG;
     long long orow[NR];
     float cv[NR], pv[NR], yv[NR];
-    const float* bwpre = bwc ? a.bw.pre + group * a.bw.pre_gs : nullptr;
+    const bool pbf = a.bw.pre_bf16 != 0;
+    const float* bwpre = bwc ? pf_at(a.bw.pre, group * a.bw.pre_gs, pbf) : nullptr;
     const float* bwy = (bwc && a.bw.y) ? a.bw.y + group * a.bw.y_gs : nullptr;
     const float biasv = bias ? bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
       orow[i] = kw_out_row(h, g, cls, m0 + rg + i * NRG);
       cv[i] = a.accumulate ? Cp[orow[i] * a.ldc + n] : 0.f;
-      pv[i] = bwpre ? bwpre[orow[i] * a.bw.ldp + n] : 0.f;
+      pv[i] = bwpre ? pf_ld(bwpre, orow[i] * a.bw.ldp + n, pbf) : 0.f;
       yv[i] = bwy ? bwy[orow[i] * a.bw.ldy + n] : 0.f;
     }
 #pragma unroll
@@ -506,6 +535,7 @@ void igemm_halo_kw_kernel(KwArgs h) {
       float v = red[(0 * BM + m) * BN + col];
 #pragma unroll
       for (int w = 1; w < 4; ++w) v += red[(w * BM + m) * BN + col];
+      if (a.c_bf16) v = bf_rnd(v);  // bf16-stored pre-BN output: the statistics of the stored values
       if (!bwm) {
         s1 += v;
         s2 += v * v;
@@ -513,7 +543,8 @@ void igemm_halo_kw_kernel(KwArgs h) {
       if (bias) v += biasv;
       v = act_f(v, a.act);
       if (a.accumulate) v += cv[i];
-      st_out(&Cp[orow[i] * a.ldc + n], v);
+      if (a.c_bf16) ((__bf16*)a.C)[group * a.c_gs + orow[i] * a.ldc + n] = (__bf16)v;
+      else st_out(&Cp[orow[i] * a.ldc + n], v);
       if (bwc) bw_term_v(v, pv[i], bm, bi, bb, bwy != nullptr, yv[i], a.bw.act, s1, s2);
     }
     if (a.stats) {
@@ -534,6 +565,7 @@ void igemm_halo_kw_kernel(KwArgs h) {
           stat_put(a.stats + (rb & (a.s_nsh - 1)) * a.s_sh + group * a.s_gs, n0 + tid, s, q);
         }
       }
+      if (a.fin.cnt) bn_fin_arrive(a.fin, group, (int*)red);
     }
     if (!has_tile) break;
     // ---- the next tile: its window (prefetched above) into LDS once every wave is done with red ----
@@ -637,11 +669,12 @@ static bool kw_disabled() {
 
 int halo_kw_plan(const FwdArgs& a, int groups) {
   if (kw_disabled()) return 0;
-  if (a.ain.acc && (a.a_bf16 || a.Cin % 8)) return 0;  // consumer-side BN: fp32 A (the pre-BN tensor)
+  if (a.ain.acc && a.Cin % 8) return 0;  // consumer-side BN: A is the pre-BN tensor (fp32, or bf16-stored)
   KwArgs h;
   int bm, bn;
   size_t lds;
   if (!kw_plan(a, groups, &h, &bm, &bn, &lds)) return 0;
+  if (a.ain.acc && a.a_bf16 && (bn != 32 || bm > 64)) return 0;  // the AIN instances
   return a.nclass * (a.rows / bm);
 }
 
@@ -653,13 +686,14 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
   h.f = a;
   const bool s2t = a.g.mode == GM_CONVT && a.g.stride == 2;
   dim3 grid(a.rows / bm, a.N / bn, groups * a.nclass);
+  h.f.fin.nblk = (a.rows / bm) * (a.N / bn) * a.nclass;  // tiles per group (last-arriver finalisation)
   h.ntx = (int)grid.x;
   h.nty = (int)grid.y;
   h.ntz = (int)grid.z;
   h.tpb = 1;
   h.ain_off = 0;
   if (a.ain.acc) {  // the consumer-side BN table [3][Cin] after the window / reduction region
-    if (a.a_bf16 || a.Cin % 8) return -1;
+    if (a.Cin % 8) return -1;
     h.ain_off = (int)((lds + 15) / 16 * 16);
     lds = (size_t)h.ain_off + 3 * (size_t)a.Cin * sizeof(float);
   }
@@ -669,7 +703,9 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
       return e ? atoi(e) : 0;
     }();
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-    bool ok = vec_mode != 0 && a.ldc % 4 == 0 && a.c_gs % 4 == 0 && al16(a.C) && (!a.bias || (al16(a.bias) && a.bias_gs % 4 == 0));
+    // bf16-stored pre (written, or read by the fused backward-BN terms): always the 8-byte vector form
+    const bool pbf = a.c_bf16 || (a.bw.pre && a.bw.pre_bf16);
+    bool ok = (vec_mode != 0 || pbf) && a.ldc % 4 == 0 && a.c_gs % 4 == 0 && al16(a.C) && (!a.bias || (al16(a.bias) && a.bias_gs % 4 == 0));
     if (a.bw.pre)
       ok = ok && a.bw.C % 4 == 0 && a.bw.ldp % 4 == 0 && a.bw.pre_gs % 4 == 0 && al16(a.bw.pre) && al16(a.bw.mean) &&
            al16(a.bw.invstd) && a.bw.ms_gs % 4 == 0 &&
@@ -755,6 +791,9 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
   if (h.tpb > 1 && a.a_bf16 && BN_ == 32 && BM_ == 64) {  /* persistent: the bf16-A 64x32 instances */     \
     if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, true, true, 1, true>), grid, dim3(256), lds, s, h); \
     else hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, false, true, 1, true>), grid, dim3(256), lds, s, h);    \
+  } else if (a.a_bf16 && a.ain.acc) {  /* consumer-side BN of a bf16 pre-BN tensor (halo_kw_plan: BN 32, BM <= 64) */ \
+    if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<BM_, BN_, true, true, 1, false, false, KW_PI, true>), grid, dim3(256), lds, s, h); \
+    else hipLaunchKernelGGL((igemm_halo_kw_kernel<BM_, BN_, false, true, 1, false, false, KW_PI, true>), grid, dim3(256), lds, s, h); \
   } else if (a.a_bf16) {                                                                                     \
     if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<BM_, BN_, true, true>), grid, dim3(256), lds, s, h);    \
     else if ((bring & 2) && BN_ == 32 && BM_ <= 64)                                                          \

@@ -12,6 +12,7 @@ struct BwStat {
   const float* mean; const float* invstd; long long ms_gs;
   const float* beta; long long beta_gs;
   int act, C;
+  int pre_bf16;                                 // pre is stored as bf16 (common.h pf_ld)
 };
 
 // Consumer-side BN(+act) of the A operand (the wave-split halo gather only): A holds the producing
@@ -24,6 +25,7 @@ struct AinBN {
   const float* beta; long long beta_gs;
   float* mean; float* invstd; long long ms_gs;
   int act; float eps;
+  int fin;                                         // mean / invstd already finalised (BnFin): read them
 };
 
 // gather-GEMM  C[p][n] (+)= act(bias + sum_{tap,k} A[src(p,tap)][k] * B[tap][k|n][n|k])
@@ -49,6 +51,10 @@ struct FwdArgs {
   // bf16); B plane p at Bh + p * b_plane elements.  Only kernels that implement it accept nsp > 1
   int nsp; long long b_plane;
   AinBN ain;    // consumer-side BN of A (halo_kw only)
+  // forward BN producers (bf16 mode): store C as bf16, the statistics taken from the rounded values;
+  // only with stats, no bias / act / accumulate / bw (igemm_c_bf16_ok)
+  int c_bf16;
+  BnFin fin;    // last-arriver BN finalisation (common.h; halo_kw only: igemm_fin_ok)
 };
 
 // weight-GEMM  part[split][tap][m][n] = sum_{p in split} G[src(p,tap)][m] * D[p][n]
@@ -115,6 +121,10 @@ int halo_kw_plan(const FwdArgs& a, int groups);
 // the split-bf16 (nsp = 3) gather-GEMMs: does a launch of this shape have a split kernel (halo_kw,
 // dense_kw)?  Shapes without one run the fp32 kernels (igemm_fwd) in that mode.
 bool igemm_split_ok(const FwdArgs& a, int groups);
+// a BN-statistics launch (a.stats set) whose kernel can store C as bf16 (FwdArgs::c_bf16)
+bool igemm_c_bf16_ok(const FwdArgs& a, int groups);
+// a BN-statistics launch that runs on halo_kw, whose epilogue implements FwdArgs::fin
+bool igemm_fin_ok(const FwdArgs& a, int groups);
 int halo_kw(const FwdArgs& a, int groups, hipStream_t s);
 void wgrad_bf16(WgArgs a, int groups, hipStream_t s, hipEvent_t after = nullptr);  // taps merged into M (part [split][tap*M+m][n])
 int wgrad_bf16_tiles(const WgArgs& a);
@@ -166,12 +176,13 @@ int bn_acc_shards(long long rowblocks);
 void bn_apply(const float* pre, int ldp, long long pre_gs, long long rows, int C, const u64* acc, long long acc_gs,
               long long sh, int nsh, float eps, float* mean, float* invstd, long long ms_gs, const float* beta, long long beta_gs,
               const float* res, int ldr, long long res_gs, int act, float* out, int ldo, long long out_gs, int groups,
-              hipStream_t s, int out_bf16 = 0);  // out_bf16: write the activation as bf16 (RNE)
+              hipStream_t s, int out_bf16 = 0,   // out_bf16: write the activation as bf16 (RNE)
+              int pre_bf16 = 0);                 // pre_bf16: pre is stored as bf16
 // sums of dz and dz*xhat, dz = dy*act'(y)   -> added into acc[group][4*C]
 void bn_bwd_reduce(const float* dy, int lddy, long long dy_gs, const float* y, int ldy, long long y_gs,
                    const float* pre, int ldp, long long pre_gs, long long rows, int C, const float* mean,
                    const float* invstd, long long ms_gs, const float* beta, long long beta_gs, int act, u64* acc,
-                   long long acc_gs, long long sh, int nsh, int groups, hipStream_t s);
+                   long long acc_gs, long long sh, int nsh, int groups, hipStream_t s, int pre_bf16 = 0);
 int bn_bwd_rowblocks(long long rows);
 // dpre = invstd*(dz - a - xhat*b), a = sum(dz)/n, b = sum(dz*xhat)/n from acc; dbeta = sum(dz);
 // optional dres (+)= dz
@@ -180,7 +191,9 @@ void bn_bwd_apply(const float* dy, int lddy, long long dy_gs, const float* y, in
                   const float* invstd, long long ms_gs, const float* beta, long long beta_gs, const u64* acc,
                   long long acc_gs, long long sh, int nsh, float* dbeta, long long dbeta_gs, int act, float* dpre, int lddp,
                   long long dpre_gs, float* dres, int ldres, long long dres_gs, int res_acc, int groups,
-                  hipStream_t s, int dpre_bf16 = 0);  // dpre_bf16: write dpre as bf16 (RNE)
+                  hipStream_t s, int dpre_bf16 = 0,  // dpre_bf16: write dpre as bf16 (RNE)
+                  int pre_bf16 = 0,
+                  const float* ab = nullptr);  // a, b finalised by the producer (BnFin mode 1): [group][2C]
 
 // ---- split_latent FC(K=Dl) + BN over batch + lrelu, fused (sequential_vae.py:1801-1806) ----
 // out[n][j] written at out + n*o_n + (j / F)*ldo + (j % F)

@@ -38,7 +38,9 @@ constexpr int SC_TM = 2;               // 32-pixel tiles per wave
 constexpr int SC_BM = 4 * 32 * SC_TM;  // output pixels per block (4 waves)
 constexpr int SC_SQ = 6;               // window items per thread (WR * WC <= 1536)
 
-template <int TN, int TM, bool BF>
+// PB: the fused backward-BN partials read a bf16-stored pre (a.bw.pre_bf16; compile-time: a run-time
+// choice per load cost the output layer's input gradient 75 %)
+template <int TN, int TM, bool BF, bool PB = false>
 __global__ __launch_bounds__(256) void conv_smallc_kernel(FwdArgs a) {
   constexpr int BM = 128 * TM;
   // window: BF 8 B per pixel (4 x bf16), fp32 16 B per pixel; sized by the host (dynamic LDS)
@@ -195,7 +197,8 @@ __global__ __launch_bounds__(256) void conv_smallc_kernel(FwdArgs a) {
       bwb[tn] = a.bw.y ? 0.f : a.bw.beta[group * a.bw.beta_gs + n];
     }
   }
-  const float* bwpre = bwm ? a.bw.pre + group * a.bw.pre_gs : nullptr;
+  constexpr bool pbf = PB;
+  const float* bwpre = bwm ? pf_at(a.bw.pre, group * a.bw.pre_gs, pbf) : nullptr;
   const float* bwy = (bwm && a.bw.y) ? a.bw.y + group * a.bw.y_gs : nullptr;
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
@@ -208,7 +211,7 @@ __global__ __launch_bounds__(256) void conv_smallc_kernel(FwdArgs a) {
         for (int tn = 0; tn < TN; ++tn) {
           const int n = tn * 32 + l32;
           const bool bwc = n < a.bw.C;
-          pv[r][tn] = bwc ? bwpre[m * a.bw.ldp + n] : 0.f;
+          pv[r][tn] = bwc ? pf_ld(bwpre, m * a.bw.ldp + n, pbf) : 0.f;
           yv[r][tn] = (bwc && bwy) ? bwy[m * a.bw.ldy + n] : 0.f;
         }
       }
@@ -220,12 +223,17 @@ __global__ __launch_bounds__(256) void conv_smallc_kernel(FwdArgs a) {
       for (int tn = 0; tn < TN; ++tn) {
         const int n = tn * 32 + l32;
         float v = acc[tm][tn][r];
+        if (a.c_bf16) v = bf_rnd(v);  // bf16-stored pre-BN output: the statistics of the stored values
         if (!bwm) {
           csum[tn] += v;
           csq[tn] += v * v;
         }
         if (bias) v += bias[n];
         v = act_f(v, a.act);
+        if (a.c_bf16) {
+          ((__bf16*)a.C)[group * a.c_gs + m * a.ldc + n] = (__bf16)v;
+          continue;
+        }
         float* dst = Cp + m * a.ldc + n;
         if (a.accumulate) v += *dst;
         *dst = v;
@@ -261,7 +269,10 @@ int smallc_lds(const FwdArgs& a, bool bf) {
 template <int TN, bool BF>
 void launch_smallc(const FwdArgs& a, int groups, hipStream_t s) {
   dim3 grid(a.rows / SC_BM, 1, groups);
-  hipLaunchKernelGGL((conv_smallc_kernel<TN, SC_TM, BF>), grid, dim3(256), smallc_lds(a, BF), s, a);
+  if (a.bw.pre && a.bw.pre_bf16)
+    hipLaunchKernelGGL((conv_smallc_kernel<TN, SC_TM, BF, true>), grid, dim3(256), smallc_lds(a, BF), s, a);
+  else
+    hipLaunchKernelGGL((conv_smallc_kernel<TN, SC_TM, BF>), grid, dim3(256), smallc_lds(a, BF), s, a);
 }
 
 // ---------------------------------------------------------------------------
@@ -301,9 +312,13 @@ __device__ __forceinline__ f32x4 mfma_split16(const bf16x8 (&x)[NS], const bf16x
   return acc;
 }
 
-template <int NS>
+// MT: class-row tiles per wave the kernel is compiled for (8: input rows up to 32 wide -- the 64x64 output
+// layer; 16: up to 64).  The accumulators and the unrolled tile loop scale with it: at 16 the split
+// instance needed 256 VGPRs + 91 AGPRs (one wave per SIMD)
+template <int NS, int MT = SN_MAXT>
 __global__ __launch_bounds__(256) void convt_smalln_kernel(FwdArgs a) {
   static_assert(NS == 1 || NS == 3, "one plane or the split mode's three");
+  static_assert(MT <= SN_MAXT, "tiles per wave");
   extern __shared__ __attribute__((aligned(16))) __bf16 wsm[];
   const ConvGeom& g = a.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -324,9 +339,9 @@ __global__ __launch_bounds__(256) void convt_smalln_kernel(FwdArgs a) {
   const bool nvalid = r16 < a.N;
   const int wplane = PR * PC * SN_PITCH;  // LDS elements per window plane (NS = 3)
 
-  f32x4 acc[SN_MAXT];
+  f32x4 acc[MT];
 #pragma unroll
-  for (int i = 0; i < SN_MAXT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   for (int ch = 0; ch < a.Cin; ch += 32) {
     if (ch) __syncthreads();  // previous chunk's window fully read
@@ -375,7 +390,7 @@ __global__ __launch_bounds__(256) void convt_smalln_kernel(FwdArgs a) {
     }
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < SN_MAXT; ++i) {
+    for (int i = 0; i < MT; ++i) {
       if (i < ntile) {
         const int j = i / WT, hseg = i - j * WT;
         // class pixel (qy, qx) = (Y0/2 + j, 16*hseg + r16): window row qy + cy - ty - iy0
@@ -401,7 +416,7 @@ __global__ __launch_bounds__(256) void convt_smalln_kernel(FwdArgs a) {
     float* ot = (float*)wsm;  // [SN_R][Wo][N]
     if (nvalid) {
 #pragma unroll
-      for (int i = 0; i < SN_MAXT; ++i) {
+      for (int i = 0; i < MT; ++i) {
         if (i < ntile) {
           const int j = i / WT, hseg = i - j * WT;
           const int y = 2 * j + cy;
@@ -429,7 +444,7 @@ __global__ __launch_bounds__(256) void convt_smalln_kernel(FwdArgs a) {
   }
   if (!nvalid) return;
 #pragma unroll
-  for (int i = 0; i < SN_MAXT; ++i) {
+  for (int i = 0; i < MT; ++i) {
     if (i < ntile) {
       const int j = i / WT, hseg = i - j * WT;
       const int Y = Y0 + 2 * j + cy;
@@ -505,6 +520,12 @@ void convt_smalln(const FwdArgs& a, int groups, hipStream_t s) {
   const int tile = a.ldc == a.N ? SN_R * a.g.Wo * a.N * 4 : 0;  // the assembled output rows
   const int lds = win > tile ? win : tile;
   dim3 grid(a.g.nimg * (a.g.Ho / SN_R), 1, groups);
-  if (planes == 3) hipLaunchKernelGGL(convt_smalln_kernel<3>, grid, dim3(256), lds, s, a);
-  else hipLaunchKernelGGL(convt_smalln_kernel<1>, grid, dim3(256), lds, s, a);
+  const bool small = (SN_R / 2) * (a.g.Wi / 16) <= 8;
+  if (planes == 3) {
+    if (small) hipLaunchKernelGGL((convt_smalln_kernel<3, 8>), grid, dim3(256), lds, s, a);
+    else hipLaunchKernelGGL((convt_smalln_kernel<3>), grid, dim3(256), lds, s, a);
+  } else {
+    if (small) hipLaunchKernelGGL((convt_smalln_kernel<1, 8>), grid, dim3(256), lds, s, a);
+    else hipLaunchKernelGGL((convt_smalln_kernel<1>), grid, dim3(256), lds, s, a);
+  }
 }
