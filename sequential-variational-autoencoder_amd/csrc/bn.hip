@@ -39,9 +39,17 @@ static bool bn_w8() {
 }
 
 // shards so that at most ~16 row-blocks add into one accumulator line
-int bn_acc_shards(long long rowblocks) {
+// cap: 16 (bf16 mode) or 32 (split mode: +0.8 % there, -1 % in bf16; profiles/r04_shards_ab.txt); the
+// apply blocks each gather nsh x 4 words per channel, the producers' atomics contend with fewer (SVAE_BN_SHMAX
+// overrides: 8 -3 %, 4 -13 %)
+int bn_acc_shards(long long rowblocks, int cap) {
+  static const int over = [] {
+    const char* e = getenv("SVAE_BN_SHMAX");
+    return e ? atoi(e) : 0;
+  }();
+  if (over > 0) cap = over;
   int n = 1;
-  while (n < 16 && (long long)n * 16 < rowblocks) n *= 2;
+  while (n < cap && (long long)n * 16 < rowblocks) n *= 2;
   return n;
 }
 

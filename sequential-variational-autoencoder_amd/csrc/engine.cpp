@@ -707,7 +707,7 @@ struct AccR {
 };
 static AccR acc_bn(svae_ctx* c, int groups, int C, long long rowblocks) {
   AccR r;
-  r.nsh = bn_acc_shards(rowblocks);
+  r.nsh = bn_acc_shards(rowblocks, c->m.g.split ? 32 : 16);
   r.gs = 4LL * C;
   r.sh = ((long long)groups * r.gs + 31) / 32 * 32;
   r.p = acc_take(c, r.sh * r.nsh);

@@ -172,7 +172,7 @@ void wgrad_reduce(const float* part, long long p_gs, int nsplit, int ntap, int M
 // out = act((pre - mean)*invstd + beta [+ res]).  acc != nullptr: mean/invstd are computed from
 // acc (count rows, eps) and written to mean/invstd for the backward; acc == nullptr: read them.
 // Accumulators: acc[shard][group][4*C], shard stride sh words, nsh shards.
-int bn_acc_shards(long long rowblocks);
+int bn_acc_shards(long long rowblocks, int cap = 16);
 void bn_apply(const float* pre, int ldp, long long pre_gs, long long rows, int C, const u64* acc, long long acc_gs,
               long long sh, int nsh, float eps, float* mean, float* invstd, long long ms_gs, const float* beta, long long beta_gs,
               const float* res, int ldr, long long res_gs, int act, float* out, int ldo, long long out_gs, int groups,
