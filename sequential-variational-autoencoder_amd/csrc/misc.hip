@@ -563,9 +563,116 @@ __global__ __launch_bounds__(256) void heads_bwd_kernel(const float* __restrict_
     }
 }
 
+// The same with the batch rows split over HR_RG thread groups of a block (64 k per block): a thread walks
+// B / HR_RG rows instead of all B (4 dependent load batches instead of 16 at B = 128: the one-k-per-thread
+// form is latency-bound at ~1.7 TB/s), and the RG partial weight-gradient sums of a k are added in LDS
+// in row-group order (deterministic; a different summation order from heads_bwd_kernel)
+#define HR_RG 4
+template <int DM>
+__global__ __launch_bounds__(256) void heads_bwd_rg_kernel(const float* __restrict__ X, long long x_gs,
+                                                           float* __restrict__ dX, long long dx_gs, int B, int K,
+                                                           const float* __restrict__ Wm, const float* __restrict__ Ws,
+                                                           long long w_gs, int D, const float* __restrict__ dhead,
+                                                           long long dh_gs, int dcols, int coff, float* __restrict__ dWm,
+                                                           float* __restrict__ dWs, float* __restrict__ dbm,
+                                                           float* __restrict__ dbs, int accumulate) {
+  extern __shared__ float dh[];  // [B][2*D], then the partial sums [2 * DM][HR_RG][64]
+  float* red = dh + B * 2 * D;
+  const int group = blockIdx.y;
+  X += group * x_gs;
+  dX += group * dx_gs;
+  Wm += group * w_gs;
+  Ws += group * w_gs;
+  dhead += group * dh_gs;
+  for (int i = threadIdx.x; i < B * 2 * D; i += blockDim.x) {
+    const int n = i / (2 * D), o = i % (2 * D);
+    dh[i] = dhead[(long long)n * dcols + (o < D ? coff + o : dcols / 2 + coff + o - D)];
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x < 2 * D) {
+    float s = 0.f;
+    for (int n = 0; n < B; ++n) s += dh[n * 2 * D + threadIdx.x];
+    if (threadIdx.x < D) dbm[group * w_gs + threadIdx.x] = s;
+    else dbs[group * w_gs + threadIdx.x - D] = s;
+  }
+  const int kl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + kl;
+  const bool kv = k < K;
+  float wm[DM], ws[DM], gm[DM], gs[DM];
+#pragma unroll
+  for (int o = 0; o < DM; ++o) {
+    wm[o] = (kv && o < D) ? Wm[(long long)k * D + o] : 0.f;
+    ws[o] = (kv && o < D) ? Ws[(long long)k * D + o] : 0.f;
+    gm[o] = gs[o] = 0.f;
+  }
+  const int rows = B / HR_RG, r0 = rg * rows;
+  constexpr int RB = 8;
+  if (kv) {
+    for (int n0 = r0; n0 < r0 + rows; n0 += RB) {
+      float xs[RB], old[RB];
+#pragma unroll
+      for (int j = 0; j < RB; ++j) {
+        const int n = n0 + j;
+        const bool ok = n < r0 + rows;
+        xs[j] = ok ? X[(long long)n * K + k] : 0.f;
+        old[j] = (accumulate && ok) ? dX[(long long)n * K + k] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < RB; ++j) {
+        const int n = n0 + j;
+        if (n >= r0 + rows) break;
+        float dx = 0.f;
+#pragma unroll
+        for (int o = 0; o < DM; ++o) {
+          if (o < D) {
+            const float a = dh[n * 2 * D + o], b = dh[n * 2 * D + D + o];
+            dx = fmaf(a, wm[o], fmaf(b, ws[o], dx));
+            gm[o] = fmaf(xs[j], a, gm[o]);
+            gs[o] = fmaf(xs[j], b, gs[o]);
+          }
+        }
+        dX[(long long)n * K + k] = accumulate ? old[j] + dx : dx;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < DM; ++o) {
+    red[((2 * o) * HR_RG + rg) * 64 + kl] = gm[o];
+    red[((2 * o + 1) * HR_RG + rg) * 64 + kl] = gs[o];
+  }
+  __syncthreads();
+  if (rg == 0 && kv) {
+#pragma unroll
+    for (int o = 0; o < DM; ++o)
+      if (o < D) {
+        float sm = 0.f, ss = 0.f;
+#pragma unroll
+        for (int g = 0; g < HR_RG; ++g) {
+          sm += red[((2 * o) * HR_RG + g) * 64 + kl];
+          ss += red[((2 * o + 1) * HR_RG + g) * 64 + kl];
+        }
+        dWm[group * w_gs + (long long)k * D + o] = sm;
+        dWs[group * w_gs + (long long)k * D + o] = ss;
+      }
+  }
+}
+
 void heads_bwd(const float* X, long long x_gs, float* dX, long long dx_gs, int B, int K, const float* Wm,
                const float* Ws, long long w_gs, int D, const float* dhead, long long dh_gs, int dcols, int coff,
                float* dWm, float* dWs, float* dbm, float* dbs, int accumulate, int groups, hipStream_t s) {
+  const char* rge = getenv("SVAE_HEADS_RG");  // =0: one thread per k over all rows (round 3); read per call (A/B tests)
+  const bool rg_on = !(rge && rge[0] == '0');
+  if (rg_on && B % (HR_RG * 8) == 0 && D <= 8) {
+    dim3 grid((K + 63) / 64, groups);
+    size_t lds = (size_t)B * 2 * D * sizeof(float) + (size_t)2 * 8 * HR_RG * 64 * sizeof(float);
+    if (D <= 4)
+      hipLaunchKernelGGL(heads_bwd_rg_kernel<4>, grid, dim3(256), lds, s, X, x_gs, dX, dx_gs, B, K, Wm, Ws, w_gs, D,
+                         dhead, dh_gs, dcols, coff, dWm, dWs, dbm, dbs, accumulate);
+    else
+      hipLaunchKernelGGL(heads_bwd_rg_kernel<8>, grid, dim3(256), lds, s, X, x_gs, dX, dx_gs, B, K, Wm, Ws, w_gs, D,
+                         dhead, dh_gs, dcols, coff, dWm, dWs, dbm, dbs, accumulate);
+    return;
+  }
   dim3 grid((K + 255) / 256, groups);
   size_t lds = (size_t)B * 2 * D * sizeof(float);
   if (D <= 4)
