@@ -63,13 +63,28 @@ __device__ __forceinline__ float ld1(const void* base, long long off, bool bf) {
 //   NS = 2:  a0 b0 + a0 b1 + a1 b0                         (3 MFMAs, ~2^-17 relative per product)
 //   NS = 3:  a0 b0 + a0 b1 + a1 b0 + a0 b2 + a2 b0 + a1 b1  (6 MFMAs, below fp32 rounding)
 // with fp32 accumulation, so a split GEMM is an fp32 GEMM to within fp32 summation error.
+// In value pairs: one v_cvt_pk_bf16_f32 rounds a pair, the pair widens back with a shift and a mask, and the
+// residuals are packed fp32 subtractions (v_pk_add_f32): 38 VALU per 8 values at NS = 3 where the
+// vector form compiled to 62 (a single-value conversion and a shift per element to widen).  The same
+// roundings and exact residuals: bitwise the same planes.
+typedef __bf16 ol_bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int ol_u32x4 __attribute__((ext_vector_type(4)));
 template <int NS>
 __device__ __forceinline__ void split8(f32x4 lo, f32x4 hi, ol_bf16x8 (&p)[NS]) {
-  ol_f32x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  ol_f32x2 v[4] = {{lo[0], lo[1]}, {lo[2], lo[3]}, {hi[0], hi[1]}, {hi[2], hi[3]}};
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    p[s] = __builtin_convertvector(v, ol_bf16x8);
-    if (s + 1 < NS) v = v - __builtin_convertvector(p[s], ol_f32x8);
+    ol_u32x4 w;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const unsigned b = __builtin_bit_cast(unsigned, __builtin_convertvector(v[j], ol_bf16x2));
+      w[j] = b;
+      if (s + 1 < NS) {
+        const ol_f32x2 r = {__uint_as_float(b << 16), __uint_as_float(b & 0xffff0000u)};
+        v[j] = v[j] - r;
+      }
+    }
+    p[s] = __builtin_bit_cast(ol_bf16x8, w);
   }
 }
 template <int NS>
