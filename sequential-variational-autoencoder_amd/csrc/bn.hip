@@ -242,7 +242,7 @@ void bn_apply(const float* pre, int ldp, long long pre_gs, long long rows, int C
 int bn_bwd_rowblocks(long long rows) { return (int)((rows + BWD_RPB - 1) / BWD_RPB); }
 
 // y == nullptr: act' from the recomputed pre-activation bn_y(pre) (layers without a shortcut add)
-template <bool PB>
+template <bool PB, bool YB>
 __global__ void bn_bwd_reduce_kernel(const float* dy, int lddy, long long dy_gs, const float* y, int ldy,
                                      long long y_gs, const float* pre, int ldp, long long pre_gs, long long rows,
                                      int C, const float* mean, const float* invstd, long long ms_gs, const float* beta,
@@ -258,7 +258,7 @@ __global__ void bn_bwd_reduce_kernel(const float* dy, int lddy, long long dy_gs,
   const int q = blockIdx.x * QB + qi;
   const bool active = rl < RL && q < Q;
   dy += group * dy_gs;
-  if (y) y += group * y_gs;
+  if (y) y = pf_at(y, group * y_gs, YB);
   pre = pf_at(pre, group * pre_gs, PB);
   mean += group * ms_gs;
   invstd += group * ms_gs;
@@ -273,7 +273,7 @@ __global__ void bn_bwd_reduce_kernel(const float* dy, int lddy, long long dy_gs,
     for (long long r = r0 + rl; r < r1; r += RL) {
       f32x4 g = *(const f32x4*)(dy + r * lddy + c);
       const f32x4 xp = pf_ld4(pre, r * ldp + c, PB);
-      f32x4 yy = y ? *(const f32x4*)(y + r * ldy + c) : bn_y(xp, m, is, bb);
+      f32x4 yy = y ? pf_ld4(y, r * ldy + c, YB) : bn_y(xp, m, is, bb);
       f32x4 xh = (xp - m) * is;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -301,20 +301,26 @@ __global__ void bn_bwd_reduce_kernel(const float* dy, int lddy, long long dy_gs,
 void bn_bwd_reduce(const float* dy, int lddy, long long dy_gs, const float* y, int ldy, long long y_gs,
                    const float* pre, int ldp, long long pre_gs, long long rows, int C, const float* mean,
                    const float* invstd, long long ms_gs, const float* beta, long long beta_gs, int act, u64* acc,
-                   long long acc_gs, long long sh, int nsh, int groups, hipStream_t s, int pre_bf16) {
+                   long long acc_gs, long long sh, int nsh, int groups, hipStream_t s, int pre_bf16, int y_bf16) {
   const int Q = C / 4;
   const int QB = Q < 16 ? Q : 16;
   dim3 grid((Q + QB - 1) / QB, (unsigned)bn_bwd_rowblocks(rows), groups);
-  if (pre_bf16)
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, grid, dim3(256), 0, s, dy, lddy, dy_gs, y, ldy, y_gs, pre, ldp, pre_gs,
-                       rows, C, mean, invstd, ms_gs, beta, beta_gs, act, acc, acc_gs, sh, nsh);
-  else
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, grid, dim3(256), 0, s, dy, lddy, dy_gs, y, ldy, y_gs, pre, ldp, pre_gs,
-                       rows, C, mean, invstd, ms_gs, beta, beta_gs, act, acc, acc_gs, sh, nsh);
+#define BWR_LAUNCH(PB_, YB_)                                                                                 \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<PB_, YB_>), grid, dim3(256), 0, s, dy, lddy, dy_gs, y, ldy, y_gs, pre, ldp, \
+                     pre_gs, rows, C, mean, invstd, ms_gs, beta, beta_gs, act, acc, acc_gs, sh, nsh)
+  const bool yb = y && y_bf16;
+  if (pre_bf16) {
+    if (yb) BWR_LAUNCH(true, true);
+    else BWR_LAUNCH(true, false);
+  } else {
+    if (yb) BWR_LAUNCH(false, true);
+    else BWR_LAUNCH(false, false);
+  }
+#undef BWR_LAUNCH
 }
 
 // W = 8 (bf16 dpre, C % 8 == 0): 8 channels per thread, one 16-byte bf16 store per row
-template <int W, bool PB>
+template <int W, bool PB, bool YB>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const float* dy, int lddy, long long dy_gs, const float* y, int ldy, long long y_gs, const float* pre, int ldp,
     long long pre_gs, long long rows, int C, const float* mean, const float* invstd, long long ms_gs,
@@ -354,7 +360,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   if (rl >= RL || q >= Q) return;
   const int c = q * W;
   dy += group * dy_gs;
-  if (y) y += group * y_gs;
+  if (y) y = pf_at(y, group * y_gs, YB);
   pre = pf_at(pre, group * pre_gs, PB);
   if (dres) dres += group * dres_gs;
   if constexpr (W == 8) {  // (dpre_bf16)
@@ -376,7 +382,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       for (int h = 0; h < 2; ++h) {
         const f32x4 g = *(const f32x4*)(dy + r * lddy + c + 4 * h);
         const f32x4 xp = pf_ld4(pre, r * ldp + c + 4 * h, PB);
-        const f32x4 yy = y ? *(const f32x4*)(y + r * ldy + c + 4 * h) : bn_y(xp, mm[h], iss[h], bbb[h]);
+        const f32x4 yy = y ? pf_ld4(y, r * ldy + c + 4 * h, YB) : bn_y(xp, mm[h], iss[h], bbb[h]);
         const f32x4 xh = (xp - mm[h]) * iss[h];
         f32x4 dz;
 #pragma unroll
@@ -403,7 +409,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   for (long long r = r0 + rl; r < r1; r += RL) {
     const f32x4 g = *(const f32x4*)(dy + r * lddy + c);
     const f32x4 xp = pf_ld4(pre, r * ldp + c, PB);
-    const f32x4 yy = y ? *(const f32x4*)(y + r * ldy + c) : bn_y(xp, m, is, bb);
+    const f32x4 yy = y ? pf_ld4(y, r * ldy + c, YB) : bn_y(xp, m, is, bb);
     const f32x4 xh = (xp - m) * is;
     f32x4 dz;
 #pragma unroll
@@ -426,16 +432,20 @@ void bn_bwd_apply(const float* dy, int lddy, long long dy_gs, const float* y, in
                   const float* invstd, long long ms_gs, const float* beta, long long beta_gs, const u64* acc,
                   long long acc_gs, long long sh, int nsh, float* dbeta, long long dbeta_gs, int act, float* dpre, int lddp,
                   long long dpre_gs, float* dres, int ldres, long long dres_gs, int res_acc, int groups,
-                  hipStream_t s, int dpre_bf16, int pre_bf16, const float* ab) {
+                  hipStream_t s, int dpre_bf16, int pre_bf16, const float* ab, int y_bf16) {
+  const bool yb = y && y_bf16;
+#define BWA_ONE(W_, PB_, YB_, G_)                                                                                  \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<W_, PB_, YB_>), G_.grid, dim3(256), 0, s, dy, lddy, dy_gs, y, ldy, y_gs, pre, \
+                     ldp, pre_gs, rows, C, mean, invstd, ms_gs, beta, beta_gs, acc, acc_gs, sh, nsh, dbeta, dbeta_gs, act, \
+                     dpre, lddp, dpre_gs, dres, ldres, dres_gs, res_acc, G_.rpb, dpre_bf16, ab)
 #define BWA_LAUNCH(W_, G_)                                                                                          \
-  if (pre_bf16)                                                                                                    \
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<W_, true>), G_.grid, dim3(256), 0, s, dy, lddy, dy_gs, y, ldy, y_gs, pre, ldp, \
-                       pre_gs, rows, C, mean, invstd, ms_gs, beta, beta_gs, acc, acc_gs, sh, nsh, dbeta, dbeta_gs, act, \
-                       dpre, lddp, dpre_gs, dres, ldres, dres_gs, res_acc, G_.rpb, dpre_bf16, ab);                    \
-  else                                                                                                             \
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<W_, false>), G_.grid, dim3(256), 0, s, dy, lddy, dy_gs, y, ldy, y_gs, pre,   \
-                       ldp, pre_gs, rows, C, mean, invstd, ms_gs, beta, beta_gs, acc, acc_gs, sh, nsh, dbeta, dbeta_gs, \
-                       act, dpre, lddp, dpre_gs, dres, ldres, dres_gs, res_acc, G_.rpb, dpre_bf16, ab);
+  if (pre_bf16) {                                                                                                  \
+    if (yb) BWA_ONE(W_, true, true, G_);                                                                           \
+    else BWA_ONE(W_, true, false, G_);                                                                             \
+  } else {                                                                                                         \
+    if (yb) BWA_ONE(W_, false, true, G_);                                                                          \
+    else BWA_ONE(W_, false, false, G_);                                                                            \
+  }
   if (dpre_bf16 && bn_w8() && C % 8 == 0 && lddp % 8 == 0 && dpre_gs % 8 == 0 && ((uintptr_t)dpre & 15) == 0) {
     const ApGrid g = ap_grid(rows, C, groups, 8);
     BWA_LAUNCH(8, g)
@@ -444,4 +454,5 @@ void bn_bwd_apply(const float* dy, int lddy, long long dy_gs, const float* y, in
   const ApGrid g = ap_grid(rows, C, groups);
   BWA_LAUNCH(4, g)
 #undef BWA_LAUNCH
+#undef BWA_ONE
 }

@@ -626,6 +626,10 @@ struct svae_ctx {
   // bf16 mode: every conv layer's pre-BN output is stored as bf16 by its GEMM epilogue (the BN statistics
   // of the stored values); the BN apply / backward passes and the fused backward-BN epilogues widen it
   int pbf = 0;
+  // bf16 mode: the decoder concat buffers [s2 output | split latent] are stored as bf16 -- read only by the
+  // s1 gather and weight-GEMM (which round them the same way) and, for the s2 BN backward, by act' (the
+  // sign of y, which bf16 rounding keeps): bitwise the fp32-stored step (SVAE_CAT_F32=1)
+  int cbf = 0;
   // conv BN statistics finalised by the producing halo_kw launch's last block (common.h BnFin): the apply
   // passes read mean / invstd (bit 0, forward) or a, b (bit 1, the fused backward sums) instead of every
   // block finalising its channels (SVAE_BN_LAF; bitwise, but off: 9.5 % / 16 % slower, profiles/r04_laf_ab.txt)
@@ -1392,11 +1396,11 @@ static int bn_act_bwd(svae_ctx* c, int groups, long long rows, int C, View dy, V
   const float* beta = c->P + beta_off;
   if (!pre_reduced)
     bn_bwd_reduce(dy.p, dy.ld, dy.gs, yp, y.ld, y.gs, pre, ldp, pre_gs, rows, C, bn.mean, bn.invstd, bn_gs, beta, w_gs,
-                  act, acc.p, acc.gs, acc.sh, acc.nsh, groups, c->st, pre_bf16);
+                  act, acc.p, acc.gs, acc.sh, acc.nsh, groups, c->st, pre_bf16, yp ? y.bf : 0);
   if ((dbg_skip() & 2) && !dres.p && rows > c->m.g.B) return 0;  // TIMING PROBE ONLY (wrong results)
   bn_bwd_apply(dy.p, dy.ld, dy.gs, yp, y.ld, y.gs, pre, ldp, pre_gs, rows, C, bn.mean, bn.invstd, bn_gs, beta, w_gs,
                acc.p, acc.gs, acc.sh, acc.nsh, c->Gr + beta_off, w_gs, act, dpre, C, dpre_gs, dres.p, dres.ld, dres.gs, res_acc, groups,
-               c->st, dpre_bf16, pre_bf16, pre_reduced ? fu->ab : nullptr);
+               c->st, dpre_bf16, pre_bf16, pre_reduced ? fu->ab : nullptr, yp ? y.bf : 0);
   return 0;
 }
 
@@ -1611,7 +1615,8 @@ static void split_latent_fwd(svae_ctx* c, int t, hipStream_t stream) {
     const FcL& f = G.split[i];
     if (i < L - 1) {
       splitfc_fwd(zt, g.Dz, zoff, B, g.D[i], c->P + f.ow, c->P + f.obeta, f.nout, s.split_mean[i], s.split_inv[i],
-                  s.cat[i] + F[i + 1], (long long)S[i + 1] * S[i + 1] * 2 * F[i + 1], F[i + 1], 2 * F[i + 1], stream);
+                  elem_off(s.cat[i], F[i + 1], c->cbf), (long long)S[i + 1] * S[i + 1] * 2 * F[i + 1], F[i + 1],
+                  2 * F[i + 1], stream, c->cbf);
     } else {
       const int coff = t >= 1 ? F[L] : 0;
       splitfc_fwd(zt, g.Dz, zoff, B, g.D[i], c->P + f.ow, c->P + f.obeta, f.nout, s.split_mean[i], s.split_inv[i],
@@ -1834,9 +1839,9 @@ static int engine_forward(svae_ctx* c) {
       const int Fl = F[lvl + 1];
       View res = t >= 1 ? View{s.enc_act_b[lvl], Fl, 0} : View{};
       r = conv_bn_act_fwd(c, G.s2[lvl], 1, 0, cur, s.s2_pre[lvl], 0, s.s2_bn[lvl], 0, res, ACT_RELU,
-                          View{s.cat[lvl], 2 * Fl, 0});
+                          View{s.cat[lvl], 2 * Fl, 0, c->cbf});
       if (r) return r;
-      r = conv_bn_act_fwd(c, G.s1[lvl], 1, 0, View{s.cat[lvl], 2 * Fl, 0}, s.s1_pre[lvl], 0, s.s1_bn[lvl], 0, View{},
+      r = conv_bn_act_fwd(c, G.s1[lvl], 1, 0, View{s.cat[lvl], 2 * Fl, 0, c->cbf}, s.s1_pre[lvl], 0, s.s1_bn[lvl], 0, View{},
                           ACT_RELU, View{s.s1_act[lvl], Fl, 0, c->abf}, lvl >= 1 ? &ds1 : nullptr);
       if (r) return r;
       cur = View{s.s1_act[lvl], Fl, 0, c->abf, (lvl >= 1 && ds1.pre) ? &ds1 : nullptr};
@@ -2157,7 +2162,7 @@ static int engine_backward_pass(svae_ctx* c) {
       if (t == c->dbg_stop_step && lvl == c->dbg_stop_lvl2) { c->dbg_last = dcur; return 0; }
       {
         const ConvL Lw = l1;
-        const View in_{s.cat[lvl], 2 * Fl, 0};
+        const View in_{s.cat[lvl], 2 * Fl, 0, c->cbf};
         const float* dp = sl.p;
         float* dW = c->Gr + Lw.ow;
         r = on_side_q(c, sl.ready, [=] { return conv_wgrad(c, Lw, 1, 0, in_, dp, 0, dW); });
@@ -2166,6 +2171,7 @@ static int engine_backward_pass(svae_ctx* c) {
       // s2[lvl]'s BN partials over the d-half of dcat (shortcut at t >= 1: act' from the stored y)
       BwFuse fu_s2 = bw_fuse(c, s.s2_pre[lvl], Fl, 0, t >= 1 ? s.cat[lvl] : nullptr, 2 * Fl, 0, s.s2_bn[lvl], 0,
                              l2.obeta, 0, ACT_RELU, Fl, c->pbf);
+      fu_s2.bw.y_bf16 = t >= 1 ? c->cbf : 0;
       // dcat: its own region per pass when the split-latent backward reads it on the side stream
       float* dcat = c->side ? arena_next(c, c->dcat_arena, c->dcat_cap, c->dcat_off, rows * 2 * Fl, true) : c->dcat;
       r = conv_dgrad(c, l1, 1, 0, sl.p, 0, View{dcat, 2 * Fl, 0}, 0, &fu_s2);
@@ -2188,7 +2194,7 @@ static int engine_backward_pass(svae_ctx* c) {
       // s2: relu(BN(convT_s2(cur)) + enc_{lvl+1})
       View dres = t >= 1 ? View{c->denc[lvl], Fl, 0} : View{};
       sl = dpre_next(c, rows * Fl);
-      r = bn_act_bwd(c, 1, rows, Fl, View{dcat, 2 * Fl, 0}, View{s.cat[lvl], 2 * Fl, 0}, s.s2_pre[lvl], 0, Fl,
+      r = bn_act_bwd(c, 1, rows, Fl, View{dcat, 2 * Fl, 0}, View{s.cat[lvl], 2 * Fl, 0, c->cbf}, s.s2_pre[lvl], 0, Fl,
                      s.s2_bn[lvl], 0, l2.obeta, 0, ACT_RELU, sl.p, 0, dres, 0, &fu_s2, dpre_bf(c, l2), c->pbf);
       if (r) return r;
       View in = lvl == L - 2 ? View{s.top_act, F[L], 0, c->abf} : View{s.s1_act[lvl + 1], F[lvl + 2], 0, c->abf};
@@ -2593,6 +2599,8 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
     c->dbf = (c->m.g.bf16 && !c->m.g.split && !(v && v[0] == '1')) ? 1 : 0;
     const char* va = getenv("SVAE_ACT_F32");  // A/B: keep every activation in fp32
     c->abf = (c->m.g.bf16 && !c->m.g.split && !(va && va[0] == '1')) ? 1 : 0;
+    const char* vc = getenv("SVAE_CAT_F32");
+    c->cbf = (c->abf && !(vc && vc[0] == '1')) ? 1 : 0;
     const char* vl = getenv("SVAE_BN_LAF");
     c->laf = vl ? atoi(vl) : 0;
     const char* vp = getenv("SVAE_PRE_F32");  // A/B: keep the conv layers' pre-BN outputs in fp32

@@ -293,7 +293,8 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
   }
   const bool pbf = a.bw.pre_bf16 != 0;
   const float* bwpre = bwm ? pf_at(a.bw.pre, group * a.bw.pre_gs, pbf) : nullptr;
-  const float* bwy = (bwm && a.bw.y) ? a.bw.y + group * a.bw.y_gs : nullptr;
+  const bool ybf = a.bw.y_bf16 != 0;
+  const float* bwy = (bwm && a.bw.y) ? pf_at(a.bw.y, group * a.bw.y_gs, ybf) : nullptr;
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
 #pragma unroll
@@ -314,7 +315,7 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(FwdArgs a) {
           const bool bwc = ok && bwm && n < a.bw.C;
           cv[i][tn] = (ok && a.accumulate) ? Cp[orow[i] * a.ldc + n] : 0.f;
           pv[i][tn] = bwc ? pf_ld(bwpre, orow[i] * a.bw.ldp + n, pbf) : 0.f;
-          yv[i][tn] = (bwc && bwy) ? bwy[orow[i] * a.bw.ldy + n] : 0.f;
+          yv[i][tn] = (bwc && bwy) ? pf_ld(bwy, orow[i] * a.bw.ldy + n, ybf) : 0.f;
         }
       }
 #pragma unroll
@@ -636,7 +637,8 @@ __global__ __launch_bounds__(256, (ABF && BN * BM <= 8192) ? 4 : 2) void igemm_h
   }
   const bool pbf = a.bw.pre_bf16 != 0;
   const float* bwpre = bwm ? pf_at(a.bw.pre, group * a.bw.pre_gs, pbf) : nullptr;
-  const float* bwy = (bwm && a.bw.y) ? a.bw.y + group * a.bw.y_gs : nullptr;
+  const bool ybf = a.bw.y_bf16 != 0;
+  const float* bwy = (bwm && a.bw.y) ? pf_at(a.bw.y, group * a.bw.y_gs, ybf) : nullptr;
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
 #pragma unroll
@@ -655,7 +657,7 @@ __global__ __launch_bounds__(256, (ABF && BN * BM <= 8192) ? 4 : 2) void igemm_h
           const bool bwc = ok && bwm && n < a.bw.C;
           cv[i][tn] = (ok && a.accumulate) ? Cp[orow[i] * a.ldc + n] : 0.f;
           pv[i][tn] = bwc ? pf_ld(bwpre, orow[i] * a.bw.ldp + n, pbf) : 0.f;
-          yv[i][tn] = (bwc && bwy) ? bwy[orow[i] * a.bw.ldy + n] : 0.f;
+          yv[i][tn] = (bwc && bwy) ? pf_ld(bwy, orow[i] * a.bw.ldy + n, ybf) : 0.f;
         }
       }
 #pragma unroll
@@ -1224,7 +1226,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* part, i
       for (int k = 1; k < ks; ++k) v[i] += *(const f32x4*)(P + k * slab + (long long)r * N + n);
       if (bwq) {
         pr[i] = pf_ld4(bw.pre, group * bw.pre_gs + (long long)r * bw.ldp + n, bw.pre_bf16 != 0);
-        if (bw.y) yr[i] = *(const f32x4*)(bw.y + group * bw.y_gs + (long long)r * bw.ldy + n);
+        if (bw.y) yr[i] = pf_ld4(bw.y, group * bw.y_gs + (long long)r * bw.ldy + n, bw.y_bf16 != 0);
       }
     }
     f32x4 cv[NRT];

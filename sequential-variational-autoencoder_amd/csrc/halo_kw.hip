@@ -69,7 +69,7 @@ __device__ __forceinline__ long long kw_out_row(const KwArgs& h, const ConvGeom&
 // forward BN statistics or the fused backward-BN partials per column (row groups summed in LDS in a
 // fixed order: deterministic).  Stores go through st_out16 (write-through in SVAE_WT builds: a
 // 16-byte sc1 store costs what a plain one does, a 4-byte one six times as much per byte).
-template <int BM, int BN, bool PB>
+template <int BM, int BN, bool PB, bool YB>
 __device__ __forceinline__ void kw_epilogue_vec(const KwArgs& h, float* red, int tid, int m0, int n0, int group, int cls) {
   const FwdArgs& a = h.f;
   const ConvGeom& g = a.g;
@@ -90,7 +90,7 @@ __device__ __forceinline__ void kw_epilogue_vec(const KwArgs& h, float* red, int
   if (a.bias) biasv = *(const f32x4*)&a.bias[group * a.bias_gs + n];
   constexpr bool pbf = PB;  // (compile-time: a run-time choice per load serialises the batch's loads)
   const float* bwpre = bwc ? pf_at(a.bw.pre, group * a.bw.pre_gs, pbf) : nullptr;
-  const float* bwy = (bwc && a.bw.y) ? a.bw.y + group * a.bw.y_gs : nullptr;
+  const float* bwy = (bwc && a.bw.y) ? pf_at(a.bw.y, group * a.bw.y_gs, YB) : nullptr;
   const bool rows_ok = rg < BM;  // (NRG > BM: the extra row groups idle)
   long long orow[NR];
   f32x4 cv[NR], pv[NR], yv[NR];
@@ -103,7 +103,7 @@ __device__ __forceinline__ void kw_epilogue_vec(const KwArgs& h, float* red, int
     orow[i] = kw_out_row(h, g, cls, m0 + rg + i * NRG);
     if (a.accumulate) cv[i] = *(const f32x4*)&Cp[orow[i] * a.ldc + n];
     if (bwpre) pv[i] = pf_ld4(bwpre, orow[i] * a.bw.ldp + n, pbf);
-    if (bwy) yv[i] = *(const f32x4*)&bwy[orow[i] * a.bw.ldy + n];
+    if (bwy) yv[i] = pf_ld4(bwy, orow[i] * a.bw.ldy + n, YB);
   }
   float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -487,8 +487,13 @@ void igemm_halo_kw_kernel(KwArgs h) {
         }
     __syncthreads();
     if (h.vec) {  // 16-byte epilogue: 4 consecutive columns per thread (write-through-friendly stores)
-      if (a.bw.pre_bf16) kw_epilogue_vec<BM, BN, true>(h, red, tid, cur.m0, cur.n0, cur.group, cur.cls);
-      else kw_epilogue_vec<BM, BN, false>(h, red, tid, cur.m0, cur.n0, cur.group, cur.cls);
+      if (a.bw.pre_bf16) {
+        if (a.bw.y_bf16) kw_epilogue_vec<BM, BN, true, true>(h, red, tid, cur.m0, cur.n0, cur.group, cur.cls);
+        else kw_epilogue_vec<BM, BN, true, false>(h, red, tid, cur.m0, cur.n0, cur.group, cur.cls);
+      } else {
+        if (a.bw.y_bf16) kw_epilogue_vec<BM, BN, false, true>(h, red, tid, cur.m0, cur.n0, cur.group, cur.cls);
+        else kw_epilogue_vec<BM, BN, false, false>(h, red, tid, cur.m0, cur.n0, cur.group, cur.cls);
+      }
       if (!has_tile) break;
       __syncthreads();
       cur = nxt;
@@ -520,14 +525,15 @@ void igemm_halo_kw_kernel(KwArgs h) {
     float cv[NR], pv[NR], yv[NR];
     const bool pbf = a.bw.pre_bf16 != 0;
     const float* bwpre = bwc ? pf_at(a.bw.pre, group * a.bw.pre_gs, pbf) : nullptr;
-    const float* bwy = (bwc && a.bw.y) ? a.bw.y + group * a.bw.y_gs : nullptr;
+    const bool ybf = a.bw.y_bf16 != 0;
+    const float* bwy = (bwc && a.bw.y) ? pf_at(a.bw.y, group * a.bw.y_gs, ybf) : nullptr;
     const float biasv = bias ? bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
       orow[i] = kw_out_row(h, g, cls, m0 + rg + i * NRG);
       cv[i] = a.accumulate ? Cp[orow[i] * a.ldc + n] : 0.f;
       pv[i] = bwpre ? pf_ld(bwpre, orow[i] * a.bw.ldp + n, pbf) : 0.f;
-      yv[i] = bwy ? bwy[orow[i] * a.bw.ldy + n] : 0.f;
+      yv[i] = bwy ? pf_ld(bwy, orow[i] * a.bw.ldy + n, ybf) : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < NR; ++i) {

@@ -13,6 +13,7 @@ struct BwStat {
   const float* beta; long long beta_gs;
   int act, C;
   int pre_bf16;                                 // pre is stored as bf16 (common.h pf_ld)
+  int y_bf16;                                   // y is stored as bf16 (only its sign is used: act')
 };
 
 // Consumer-side BN(+act) of the A operand (the wave-split halo gather only): A holds the producing
@@ -182,7 +183,8 @@ void bn_apply(const float* pre, int ldp, long long pre_gs, long long rows, int C
 void bn_bwd_reduce(const float* dy, int lddy, long long dy_gs, const float* y, int ldy, long long y_gs,
                    const float* pre, int ldp, long long pre_gs, long long rows, int C, const float* mean,
                    const float* invstd, long long ms_gs, const float* beta, long long beta_gs, int act, u64* acc,
-                   long long acc_gs, long long sh, int nsh, int groups, hipStream_t s, int pre_bf16 = 0);
+                   long long acc_gs, long long sh, int nsh, int groups, hipStream_t s, int pre_bf16 = 0,
+                   int y_bf16 = 0);
 int bn_bwd_rowblocks(long long rows);
 // dpre = invstd*(dz - a - xhat*b), a = sum(dz)/n, b = sum(dz*xhat)/n from acc; dbeta = sum(dz);
 // optional dres (+)= dz
@@ -193,12 +195,14 @@ void bn_bwd_apply(const float* dy, int lddy, long long dy_gs, const float* y, in
                   long long dpre_gs, float* dres, int ldres, long long dres_gs, int res_acc, int groups,
                   hipStream_t s, int dpre_bf16 = 0,  // dpre_bf16: write dpre as bf16 (RNE)
                   int pre_bf16 = 0,
-                  const float* ab = nullptr);  // a, b finalised by the producer (BnFin mode 1): [group][2C]
+                  const float* ab = nullptr,   // a, b finalised by the producer (BnFin mode 1): [group][2C]
+                  int y_bf16 = 0);             // y stored as bf16 (act' needs its sign only)
 
 // ---- split_latent FC(K=Dl) + BN over batch + lrelu, fused (sequential_vae.py:1801-1806) ----
 // out[n][j] written at out + n*o_n + (j / F)*ldo + (j % F)
 void splitfc_fwd(const float* z, int ldz, int zoff, int B, int K, const float* W, const float* beta, int J,
-                 float* mean, float* invstd, float* out, long long o_n, int F, int ldo, hipStream_t s);
+                 float* mean, float* invstd, float* out, long long o_n, int F, int ldo, hipStream_t s,
+                 int out_bf16 = 0);  // out_bf16: the concat buffer is stored as bf16 (offsets in bf16 elements)
 // writes dW [K][J], dbeta [J] and dz_part [splitfc_blocks(J)][B][K]
 void splitfc_bwd(const float* z, int ldz, int zoff, int B, int K, const float* W, const float* beta, int J,
                  const float* mean, const float* invstd, const float* dout, long long o_n, int F, int ldo, float* dW,

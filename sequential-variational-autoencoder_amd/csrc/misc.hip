@@ -25,7 +25,8 @@ static int ew_blocks(long long work, int per = 256, int cap = 4096) {
 template <int KM>
 __global__ __launch_bounds__(256) void splitfc_fwd_kernel(const float* z, int ldz, int zoff, int B, int K,
                                                           const float* W, const float* beta, int J, float* mean,
-                                                          float* invstd, float* out, long long o_n, int F, int ldo) {
+                                                          float* invstd, float* out, long long o_n, int F, int ldo,
+                                                          int out_bf16) {
   extern __shared__ float zs[];  // [B][KM], zero padded past K
   __shared__ float red[SFC_RG][SFC_COLS];
   for (int i = threadIdx.x; i < B * KM; i += blockDim.x) {
@@ -65,26 +66,32 @@ __global__ __launch_bounds__(256) void splitfc_fwd_kernel(const float* z, int ld
     invstd[j] = is;
   }
   const float b = beta[j];
-  float* dst = out + (long long)(j / F) * ldo + (j % F);
+  const long long o0 = (long long)(j / F) * ldo + (j % F);
+  if (out_bf16) {  // read only by bf16 GEMMs (the s1 gather and weight gradient round it the same way)
+    __bf16* dh = (__bf16*)out + o0;
+    for (int n = rg; n < B; n += SFC_RG) dh[n * o_n] = (__bf16)lrelu_f((pre(n) - m) * is + b);
+    return;
+  }
+  float* dst = out + o0;
   for (int n = rg; n < B; n += SFC_RG) dst[n * o_n] = lrelu_f((pre(n) - m) * is + b);
 }
 
 static int sfc_km(int K) { return K <= 4 ? 4 : (K <= 8 ? 8 : 32); }
 
 void splitfc_fwd(const float* z, int ldz, int zoff, int B, int K, const float* W, const float* beta, int J,
-                 float* mean, float* invstd, float* out, long long o_n, int F, int ldo, hipStream_t s) {
+                 float* mean, float* invstd, float* out, long long o_n, int F, int ldo, hipStream_t s, int out_bf16) {
   const int km = sfc_km(K);
   dim3 g((J + SFC_COLS - 1) / SFC_COLS);
   const size_t lds = (size_t)B * km * sizeof(float);
   if (km == 4)
     hipLaunchKernelGGL(splitfc_fwd_kernel<4>, g, dim3(256), lds, s, z, ldz, zoff, B, K, W, beta, J, mean, invstd, out,
-                       o_n, F, ldo);
+                       o_n, F, ldo, out_bf16);
   else if (km == 8)
     hipLaunchKernelGGL(splitfc_fwd_kernel<8>, g, dim3(256), lds, s, z, ldz, zoff, B, K, W, beta, J, mean, invstd, out,
-                       o_n, F, ldo);
+                       o_n, F, ldo, out_bf16);
   else
     hipLaunchKernelGGL(splitfc_fwd_kernel<32>, g, dim3(256), lds, s, z, ldz, zoff, B, K, W, beta, J, mean, invstd,
-                       out, o_n, F, ldo);
+                       out, o_n, F, ldo, out_bf16);
 }
 
 int splitfc_blocks(int J) { return (J + SFC_COLS - 1) / SFC_COLS; }

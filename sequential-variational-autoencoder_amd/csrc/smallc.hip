@@ -199,7 +199,8 @@ __global__ __launch_bounds__(256) void conv_smallc_kernel(FwdArgs a) {
   }
   constexpr bool pbf = PB;
   const float* bwpre = bwm ? pf_at(a.bw.pre, group * a.bw.pre_gs, pbf) : nullptr;
-  const float* bwy = (bwm && a.bw.y) ? a.bw.y + group * a.bw.y_gs : nullptr;
+  const bool ybf = a.bw.y_bf16 != 0;
+  const float* bwy = (bwm && a.bw.y) ? pf_at(a.bw.y, group * a.bw.y_gs, ybf) : nullptr;
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
     float pv[16][TN], yv[16][TN];
@@ -212,7 +213,7 @@ __global__ __launch_bounds__(256) void conv_smallc_kernel(FwdArgs a) {
           const int n = tn * 32 + l32;
           const bool bwc = n < a.bw.C;
           pv[r][tn] = bwc ? pf_ld(bwpre, m * a.bw.ldp + n, pbf) : 0.f;
-          yv[r][tn] = (bwc && bwy) ? bwy[m * a.bw.ldy + n] : 0.f;
+          yv[r][tn] = (bwc && bwy) ? pf_ld(bwy, m * a.bw.ldy + n, ybf) : 0.f;
         }
       }
     }

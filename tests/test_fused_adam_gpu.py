@@ -227,3 +227,22 @@ def test_bn_last_arriver_finalisation_is_bitwise(preset, dtype, batch, fused, mo
     assert changed > 0
     assert l0 == l1, (l0, l1)
     np.testing.assert_array_equal(p0, p1)
+
+
+@pytest.mark.parametrize("preset,dtype,batch,over", [
+    ("tiny", "bf16", 4, {}), ("celeba", "bf16", 128, {}), ("tiny_homog", "bf16", 4, {}),
+    ("tiny", "bf16", 4, {"predict_latent_code": True}),
+])
+@pytest.mark.parametrize("fused", [False, True])
+def test_bf16_concat_storage_is_bitwise(preset, dtype, batch, over, fused, monkeypatch):
+    """bf16 mode stores the decoder concat buffers [s2 output | split latent] as bf16 (engine.cpp cbf):
+    their readers round them to bf16 anyway (the s1 gather and weight-GEMM) or use only the sign of the
+    s2 output (act' in its BN backward), so three training steps are bitwise the fp32-stored ones
+    (SVAE_CAT_F32=1)."""
+    monkeypatch.setenv("SVAE_CAT_F32", "1")
+    p0, l0, _ = _run(preset, dtype, fused, over, batch=batch)
+    monkeypatch.setenv("SVAE_CAT_F32", "0")
+    p1, l1, changed = _run(preset, dtype, fused, over, batch=batch)
+    assert changed > 0
+    assert l0 == l1, (l0, l1)
+    np.testing.assert_array_equal(p0, p1)
