@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256) void splitfc_fwd_kernel(const float* z, int ld
                                                           const float* W, const float* beta, int J, float* mean,
                                                           float* invstd, float* out, long long o_n, int F, int ldo,
                                                           int out_bf16) {
-  extern __shared__ float zs[];  // [B][KM], zero padded past K
+  extern __shared__ __attribute__((aligned(16))) float zs[];  // [B][KM], zero padded past K
   __shared__ float red[SFC_RG][SFC_COLS];
   for (int i = threadIdx.x; i < B * KM; i += blockDim.x) {
     const int d = i % KM;
@@ -40,10 +40,14 @@ __global__ __launch_bounds__(256) void splitfc_fwd_kernel(const float* z, int ld
   float w[KM];
 #pragma unroll
   for (int d = 0; d < KM; ++d) w[d] = (ok && d < K) ? W[(long long)d * J + j] : 0.f;
-  auto pre = [&](int n) {
+  auto pre = [&](int n) {  // (16-byte LDS reads of the z row, the same fma order)
     float s = 0.f;
 #pragma unroll
-    for (int d = 0; d < KM; ++d) s = fmaf(zs[n * KM + d], w[d], s);
+    for (int d4 = 0; d4 < KM; d4 += 4) {
+      const f32x4 zv = *(const f32x4*)&zs[n * KM + d4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s = fmaf(zv[e], w[d4 + e], s);
+    }
     return s;
   };
   float s = 0.f;
@@ -99,18 +103,18 @@ int splitfc_blocks(int J) { return (J + SFC_COLS - 1) / SFC_COLS; }
 // backward: dW [K][J], dbeta [J], and per-block partial dz: dz_part[blk][n][d] = sum_{j in blk} dpre[n][j] W[d][j].
 // dpre rows are staged in LDS (pitch 65: conflict-free column reads) and the dz partials are then
 // formed by plain per-thread dot products over the block's 64 features.
-#define SFC_PITCH (SFC_COLS + 1)
+#define SFC_PITCH (SFC_COLS + 4)  // (a multiple of 4: 16-byte row reads in the dz pass; column accesses are per wave)
 template <int KM>
 __global__ __launch_bounds__(256) void splitfc_bwd_kernel(const float* z, int ldz, int zoff, int B, int K,
                                                           const float* W, const float* beta, int J,
                                                           const float* mean, const float* invstd, const float* dout,
                                                           long long o_n, int F, int ldo, float* dW, float* dbeta,
                                                           float* dz_part) {
-  extern __shared__ float sm[];
+  extern __shared__ __attribute__((aligned(16))) float sm[];
   float* zs = sm;                 // [B][KM]
   float* dps = sm + B * KM;       // [B][SFC_PITCH]
   __shared__ float red[2][SFC_RG][SFC_COLS];
-  __shared__ float ws[KM][SFC_COLS];
+  __shared__ __attribute__((aligned(16))) float ws[KM][SFC_COLS];
   for (int i = threadIdx.x; i < B * KM; i += blockDim.x) {
     const int d = i % KM;
     zs[i] = d < K ? z[(i / KM) * ldz + zoff + d] : 0.f;
@@ -131,10 +135,14 @@ __global__ __launch_bounds__(256) void splitfc_bwd_kernel(const float* z, int ld
 #pragma unroll 32
   for (int n = rg; n < B; n += SFC_RG) dps[n * SFC_PITCH + c] = ok ? src[n * o_n] : 0.f;
   __syncthreads();
-  auto xhat = [&](int n) {
+  auto xhat = [&](int n) {  // (16-byte LDS reads of the z row: a quarter of the LDS instructions, same fma order)
     float s = 0.f;
 #pragma unroll
-    for (int d = 0; d < KM; ++d) s = fmaf(zs[n * KM + d], w[d], s);
+    for (int d4 = 0; d4 < KM; d4 += 4) {
+      const f32x4 zv = *(const f32x4*)&zs[n * KM + d4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s = fmaf(zv[e], w[d4 + e], s);
+    }
     return (s - m) * is;
   };
   float sd = 0.f, sx = 0.f;
@@ -158,7 +166,11 @@ __global__ __launch_bounds__(256) void splitfc_bwd_kernel(const float* z, int ld
     const float dp = ok ? is * (dps[n * SFC_PITCH + c] - a - xhat(n) * cc) : 0.f;
     dps[n * SFC_PITCH + c] = dp;
 #pragma unroll
-    for (int d = 0; d < KM; ++d) gw[d] = fmaf(zs[n * KM + d], dp, gw[d]);
+    for (int d4 = 0; d4 < KM; d4 += 4) {
+      const f32x4 zv = *(const f32x4*)&zs[n * KM + d4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gw[d4 + e] = fmaf(zv[e], dp, gw[d4 + e]);
+    }
   }
   __syncthreads();
   float* P = dz_part + (long long)blockIdx.x * B * K;
@@ -166,8 +178,12 @@ __global__ __launch_bounds__(256) void splitfc_bwd_kernel(const float* z, int ld
     const int n = p / K, d = p - n * K;
     const float* row = dps + n * SFC_PITCH;
     float s = 0.f;
-#pragma unroll 16
-    for (int q = 0; q < SFC_COLS; ++q) s = fmaf(row[q], ws[d][q], s);
+#pragma unroll 4
+    for (int q = 0; q < SFC_COLS; q += 4) {
+      const f32x4 rv = *(const f32x4*)&row[q], wv = *(const f32x4*)&ws[d][q];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s = fmaf(rv[e], wv[e], s);
+    }
     P[p] = s;
   }
   __syncthreads();  // dps reused below as the dW reduction buffer
@@ -361,6 +377,77 @@ static bool heads_narrow_off() {  // SVAE_HEADS_SKINNY=1: the former 4-row skinn
   return v;
 }
 
+// Wide heads (4 < D <= 32, e.g. LSUN's 20-30 latents per level): a block owns 64 batch rows x both heads'
+// 2D outputs (padded to 64) over one HF_CHUNK split of K, staged through LDS 32 k at a time; each thread
+// keeps a 4 x 4 output tile.  The weights of a split are read once per 64 rows (skinny_kernel<32> read
+// them once per 4 rows and spilled: 3.9 GB of L2 traffic and 630 us per LSUN level-0 launch).
+#define HT_KS 32
+__global__ __launch_bounds__(256) void heads_tile_fwd_kernel(const float* __restrict__ X, long long x_gs, int B, int K,
+                                                             const float* __restrict__ Wm, const float* __restrict__ Ws,
+                                                             long long w_gs, int D, float* __restrict__ part,
+                                                             long long p_gs, int pcols, int coff, int coff2) {
+  __shared__ float xs[64][HT_KS + 1];
+  __shared__ __attribute__((aligned(16))) float ws[HT_KS][64];
+  const int group = blockIdx.z, split = blockIdx.y, r0 = blockIdx.x * 64;
+  X += group * x_gs;
+  Wm += group * w_gs;
+  Ws += group * w_gs;
+  const int tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
+  float acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  const int k0 = split * HF_CHUNK, k1 = min(K, k0 + HF_CHUNK);
+  for (int kb = k0; kb < k1; kb += HT_KS) {
+    {  // X: 64 rows x 32 k, 8 consecutive k per thread
+      const int row = tid >> 2, kp = (tid & 3) * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k = kb + kp + e;
+        xs[row][kp + e] = (r0 + row < B && k < k1) ? X[(long long)(r0 + row) * K + k] : 0.f;
+      }
+    }
+    {  // W: 32 k x [mean D | std D | 0 ...], 8 columns per thread
+      const int kk = tid >> 3, c0 = (tid & 7) * 8;
+      const int k = kb + kk;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = c0 + e;
+        float w = 0.f;
+        if (k < k1) {
+          if (c < D) w = Wm[(long long)k * D + c];
+          else if (c < 2 * D) w = Ws[(long long)k * D + c - D];
+        }
+        ws[kk][c] = w;
+      }
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int kk = 0; kk < HT_KS; ++kk) {
+      const f32x4 w = *(const f32x4*)&ws[kk][4 * tc];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float x = xs[4 * tr + i][kk];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(x, w[j], acc[i][j]);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = r0 + 4 * tr + i;
+    if (r >= B) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int o = 4 * tc + j;
+      if (o < 2 * D)
+        part[group * p_gs + ((long long)split * B + r) * pcols + (o < D ? coff + o : coff2 + o - D)] = acc[i][j];
+    }
+  }
+}
+
 void heads_fwd(const float* X, long long x_gs, int B, int K, const float* Wm, const float* Ws, long long w_gs, int D,
                float* part, long long part_gs, int pcols, int coff, int groups, hipStream_t s) {
   // mean and stddev heads in one pass over X (the shared recognition features)
@@ -376,6 +463,14 @@ void heads_fwd(const float* X, long long x_gs, int B, int K, const float* Wm, co
     else if (D == 3) HF_L(3);
     else HF_L(4);
 #undef HF_L
+    return;
+  }
+  const char* te = getenv("SVAE_HEADS_TILE");  // bit 0 off: the skinny pass for the wide heads (A/B; read per call)
+  const bool tile_off = te && !(atoi(te) & 1);
+  if (D > 4 && D <= 32 && !tile_off) {
+    dim3 grid((B + 63) / 64, heads_splits(K), groups);
+    hipLaunchKernelGGL(heads_tile_fwd_kernel, grid, dim3(256), 0, s, X, x_gs, B, K, Wm, Ws, w_gs, D, part, part_gs, pcols,
+                       coff, pcols / 2 + coff);
     return;
   }
   // the splits follow HF_CHUNK (heads_splits); skinny's chunk must match
@@ -664,9 +759,112 @@ __global__ __launch_bounds__(256) void heads_bwd_rg_kernel(const float* __restri
   }
 }
 
+// Wide heads backward (8 < D <= 32): a block owns 64 k columns over all B rows, 32 rows at a time through
+// LDS: dW[k][o] = sum_n X[n][k] dh[n][o] (a 4 k x 4 o tile per thread, accumulated over the row steps in
+// row order) and dX[n][k] (+)= sum_o dh[n][o] W[k][o] (2 rows x 4 k per thread) with the block's weights
+// held in LDS transposed [o][k].  heads_bwd_kernel<32> (one k per thread over every row, 188 VGPRs) took
+// 1.2 ms per LSUN level-0 launch.
+__global__ __launch_bounds__(256) void heads_tile_bwd_kernel(const float* __restrict__ X, long long x_gs,
+                                                             float* __restrict__ dX, long long dx_gs, int B, int K,
+                                                             const float* __restrict__ Wm, const float* __restrict__ Ws,
+                                                             long long w_gs, int D, const float* __restrict__ dhead,
+                                                             long long dh_gs, int dcols, int coff, float* __restrict__ dWm,
+                                                             float* __restrict__ dWs, float* __restrict__ dbm,
+                                                             float* __restrict__ dbs, int accumulate) {
+  __shared__ __attribute__((aligned(16))) float wt[64][64];   // [o][k]
+  __shared__ __attribute__((aligned(16))) float xs[32][64];   // [n][k]
+  __shared__ __attribute__((aligned(16))) float dhs[32][68];  // [n][o] (pitch 68: the dX loop's 4 rows per wave in 4 banks)
+  const int group = blockIdx.y, k0 = blockIdx.x * 64, tid = threadIdx.x;
+  X += group * x_gs;
+  dX += group * dx_gs;
+  Wm += group * w_gs;
+  Ws += group * w_gs;
+  dhead += group * dh_gs;
+  auto dh_at = [&](int n, int o) -> float {
+    return o < D ? dhead[(long long)n * dcols + coff + o] : (o < 2 * D ? dhead[(long long)n * dcols + dcols / 2 + coff + o - D] : 0.f);
+  };
+  if (blockIdx.x == 0 && tid < 2 * D) {  // bias gradients (row order)
+    float sb = 0.f;
+    for (int n = 0; n < B; ++n) sb += dh_at(n, tid);
+    if (tid < D) dbm[group * w_gs + tid] = sb;
+    else dbs[group * w_gs + tid - D] = sb;
+  }
+  for (int i = tid; i < 64 * 64; i += 256) {
+    const int kk = i >> 6, o = i & 63, k = k0 + kk;
+    float w = 0.f;
+    if (k < K) {
+      if (o < D) w = Wm[(long long)k * D + o];
+      else if (o < 2 * D) w = Ws[(long long)k * D + o - D];
+    }
+    wt[o][kk] = w;
+  }
+  const int tk = tid >> 4, tq = tid & 15;  // dW: k = 4 tk .. + 3, o = 4 tq .. + 3;  dX: rows 2 tk, 2 tk + 1, k = 4 tq ..
+  float gw[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) gw[i][j] = 0.f;
+  for (int n0 = 0; n0 < B; n0 += 32) {
+    __syncthreads();  // (wt written; the previous step's xs / dhs read)
+    for (int i = tid; i < 32 * 64; i += 256) {
+      const int r = i >> 6, c = i & 63, n = n0 + r, k = k0 + c;
+      xs[r][c] = (n < B && k < K) ? X[(long long)n * K + k] : 0.f;
+      dhs[r][c] = n < B ? dh_at(n, c) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int r = 0; r < 32; ++r) {
+      const f32x4 x = *(const f32x4*)&xs[r][4 * tk];
+      const f32x4 g = *(const f32x4*)&dhs[r][4 * tq];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) gw[i][j] = fmaf(x[i], g[j], gw[i][j]);
+    }
+    f32x4 dx[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll 8
+    for (int o = 0; o < 64; ++o) {
+      const f32x4 w = *(const f32x4*)&wt[o][4 * tq];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) dx[h] += dhs[2 * tk + h][o] * w;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int n = n0 + 2 * tk + h;
+      if (n >= B) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = k0 + 4 * tq + e;
+        if (k >= K) continue;
+        float* d = dX + (long long)n * K + k;
+        *d = accumulate ? *d + dx[h][e] : dx[h][e];
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = k0 + 4 * tk + i;
+    if (k >= K) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int o = 4 * tq + j;
+      if (o < D) dWm[group * w_gs + (long long)k * D + o] = gw[i][j];
+      else if (o < 2 * D) dWs[group * w_gs + (long long)k * D + o - D] = gw[i][j];
+    }
+  }
+}
+
 void heads_bwd(const float* X, long long x_gs, float* dX, long long dx_gs, int B, int K, const float* Wm,
                const float* Ws, long long w_gs, int D, const float* dhead, long long dh_gs, int dcols, int coff,
                float* dWm, float* dWs, float* dbm, float* dbs, int accumulate, int groups, hipStream_t s) {
+  const char* te = getenv("SVAE_HEADS_TILE");  // bit 1 off: heads_bwd_kernel<32> for the wide heads (A/B; per call)
+  const bool tile_off = te && !(atoi(te) & 2);
+  if (D > 8 && D <= 32 && !tile_off) {
+    dim3 grid((K + 63) / 64, groups);
+    hipLaunchKernelGGL(heads_tile_bwd_kernel, grid, dim3(256), 0, s, X, x_gs, dX, dx_gs, B, K, Wm, Ws, w_gs, D, dhead,
+                       dh_gs, dcols, coff, dWm, dWs, dbm, dbs, accumulate);
+    return;
+  }
   const char* rge = getenv("SVAE_HEADS_RG");  // =0: one thread per k over all rows (round 3); read per call (A/B tests)
   const bool rg_on = !(rge && rge[0] == '0');
   if (rg_on && B % (HR_RG * 8) == 0 && D <= 8) {
