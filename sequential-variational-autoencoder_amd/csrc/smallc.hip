@@ -224,14 +224,14 @@ __global__ __launch_bounds__(256) void conv_smallc_kernel(FwdArgs a) {
       for (int tn = 0; tn < TN; ++tn) {
         const int n = tn * 32 + l32;
         float v = acc[tm][tn][r];
-        if (a.c_bf16) v = bf_rnd(v);  // bf16-stored pre-BN output: the statistics of the stored values
+        if (BF && a.c_bf16) v = bf_rnd(v);  // bf16-stored pre-BN output: the statistics of the stored values (bf16 model only)
         if (!bwm) {
           csum[tn] += v;
           csq[tn] += v * v;
         }
         if (bias) v += bias[n];
         v = act_f(v, a.act);
-        if (a.c_bf16) {
+        if (BF && a.c_bf16) {
           ((__bf16*)a.C)[group * a.c_gs + m * a.ldc + n] = (__bf16)v;
           continue;
         }
