@@ -386,7 +386,7 @@ __global__ __launch_bounds__(256) void heads_tile_fwd_kernel(const float* __rest
                                                              const float* __restrict__ Wm, const float* __restrict__ Ws,
                                                              long long w_gs, int D, float* __restrict__ part,
                                                              long long p_gs, int pcols, int coff, int coff2) {
-  __shared__ float xs[64][HT_KS + 1];
+  __shared__ __attribute__((aligned(16))) float xs[64][HT_KS + 4];  // pitch 36: 16-byte row reads, 4 rows per wave in 4 banks
   __shared__ __attribute__((aligned(16))) float ws[HT_KS][64];
   const int group = blockIdx.z, split = blockIdx.y, r0 = blockIdx.x * 64;
   X += group * x_gs;
@@ -423,15 +423,19 @@ __global__ __launch_bounds__(256) void heads_tile_fwd_kernel(const float* __rest
       }
     }
     __syncthreads();
-#pragma unroll 8
-    for (int kk = 0; kk < HT_KS; ++kk) {
-      const f32x4 w = *(const f32x4*)&ws[kk][4 * tc];
+#pragma unroll 2
+    for (int kk = 0; kk < HT_KS; kk += 4) {  // 4 k per step: 8 16-byte LDS reads for 64 fma (same order per output)
+      f32x4 x[4], w[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float x = xs[4 * tr + i][kk];
+      for (int i = 0; i < 4; ++i) x[i] = *(const f32x4*)&xs[4 * tr + i][kk];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(x, w[j], acc[i][j]);
-      }
+      for (int q = 0; q < 4; ++q) w[q] = *(const f32x4*)&ws[kk + q][4 * tc];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(x[i][q], w[q][j], acc[i][j]);
     }
     __syncthreads();
   }
@@ -822,11 +826,17 @@ __global__ __launch_bounds__(256) void heads_tile_bwd_kernel(const float* __rest
         for (int j = 0; j < 4; ++j) gw[i][j] = fmaf(x[i], g[j], gw[i][j]);
     }
     f32x4 dx[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-#pragma unroll 8
-    for (int o = 0; o < 64; ++o) {
-      const f32x4 w = *(const f32x4*)&wt[o][4 * tq];
+#pragma unroll 2
+    for (int o = 0; o < 64; o += 4) {  // 4 o per step: 6 16-byte LDS reads for 32 fma (same order per output)
+      f32x4 w[4];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) dx[h] += dhs[2 * tk + h][o] * w;
+      for (int q = 0; q < 4; ++q) w[q] = *(const f32x4*)&wt[o + q][4 * tq];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 d = *(const f32x4*)&dhs[2 * tk + h][o];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dx[h] += d[q] * w[q];
+      }
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
