@@ -381,9 +381,10 @@ int wgrad_halo2(const WgArgs& w, int groups, float* slab, long long slab_cap, fl
   const bool sp128 = w.nsp > 1 && S == 1 && WO <= 16 && split_cp == 128 && w.rows % 128 == 0;
   const int cp = sp128 ? 128 : wh2_cp(WO, S);
   // split mode: 128 (its weight-GEMMs are 3x the MFMA work, so more splits spread the side stream: parity
-  // mode +1.9 %, profiles/r04_knobs_ab.txt); bf16: 64.  SVAE_WH2_TARGET overrides both
+  // mode +1.9 %, profiles/r04_knobs_ab.txt); bf16: 96 (+0.6 %, profiles/r04_knobs2_ab.txt).  SVAE_WH2_TARGET
+  // overrides both
   static const int target_env = env_int("SVAE_WH2_TARGET", 0);
-  const int target = target_env > 0 ? target_env : (w.nsp > 1 ? 128 : 64);
+  const int target = target_env > 0 ? target_env : (w.nsp > 1 ? 128 : 96);
   static const int minch = env_int("SVAE_WH2_MINCH", 4);
   // SVAE_WH2_NSW=2: a 64-column block as 4 waves of two 32-column subtiles (each transposed A
   // fragment feeds two MFMAs) instead of 8 waves of one
