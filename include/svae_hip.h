@@ -209,7 +209,10 @@ int svae_op_conv(const float* x, int n, int h, int cin, const float* w, int cout
  * (transpose=1) of fp32 NHWC x with bf16 weights already in the engine's NK shadow layout
  * w_nk[tap][cout][cin] (tap = ky*4+kx); x is rounded to bf16 while staged, fp32 accumulate.
  * path: 0 per-tap gather kernel, 1 halo-tile kernel (SVAE_EBADARG if the shape does not
- * qualify), 2 automatic.  scratch (optional) enables split-K. */
+ * qualify), 2 automatic.  scratch (optional) enables split-K.  path | 16: the split-bf16 mode
+ * (dtype bf16x6): w_nk holds three planes of 16*cin*cout elements each (x = p0 + p1 + p2); path | 48:
+ * two more planes follow, the scaled fp16 pair fp16(w * 2^10), fp16(w * 2^10 - h0) that the
+ * wave-split gathers use in that mode. */
 int svae_op_gather_bf16(const float* x, int n, int h, int cin, const void* w_nk, int cout, int stride, int transpose,
                         int path, float* y, void* scratch, int64_t scratch_bytes, void* stream);
 /* bf16 weight gradient of a conv (transpose=0) / conv-T (transpose=1) layer: dw in TF layout

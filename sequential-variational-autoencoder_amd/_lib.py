@@ -5,6 +5,7 @@ resolves to the HIP runtime torch already mapped (one runtime per process: devic
 pointers from torch tensors are valid inside the library).  There is no fallback:
 if the library is missing or fails to load, every entry point raises.
 """
+import contextlib
 import ctypes
 import os
 
@@ -13,6 +14,8 @@ import torch  # noqa: F401  (must be imported before the HIP library is mapped)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # SVAE_LIB: another build of the library (A/B runs of compile-time variants)
 LIB_PATH = os.environ.get("SVAE_LIB") or os.path.join(_HERE, "libsvae_hip.so")
+# the -DSVAE_KNOBS build (csrc/knobs.h): the A/B tuning switches read from the environment
+KNOBS_PATH = os.path.join(_HERE, "libsvae_hip_knobs.so")
 
 _c_float_p = ctypes.POINTER(ctypes.c_float)
 
@@ -53,15 +56,38 @@ _lib = None
 STEP_HOOK = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int)
 
 
+_loaded = {}
+
+
 def lib():
     """Load (once) and return the library; raises if it is absent."""
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise RuntimeError("libsvae_hip.so not built (%s); run __graft_entry__.build() or "
-                           "python sequential-variational-autoencoder_amd/build.py" % LIB_PATH)
-    L = ctypes.CDLL(LIB_PATH)
+    _lib = _load(LIB_PATH)
+    return _lib
+
+
+@contextlib.contextmanager
+def knob_build():
+    """Within the block, lib() is the -DSVAE_KNOBS build (the tests that hold an A/B switch of
+    csrc/knobs.h bitwise to the default path set SVAE_* and create their networks inside it)."""
+    global _lib
+    prev = lib()
+    _lib = _load(KNOBS_PATH)
+    try:
+        yield _lib
+    finally:
+        _lib = prev
+
+
+def _load(path):
+    if path in _loaded:
+        return _loaded[path]
+    if not os.path.exists(path):
+        raise RuntimeError("%s not built; run __graft_entry__.build() or "
+                           "python sequential-variational-autoencoder_amd/build.py" % path)
+    L = ctypes.CDLL(path)
     vp, i32, i64, f32, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_uint64
     cfgp = ctypes.POINTER(SvaeConfig)
     sig = {
@@ -136,7 +162,7 @@ def lib():
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
-    _lib = L
+    _loaded[path] = L
     return L
 
 

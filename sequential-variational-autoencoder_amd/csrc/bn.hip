@@ -9,6 +9,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "knobs.h"
 #include "kernels.h"
 
 typedef __bf16 bf16x4_bn __attribute__((ext_vector_type(4)));
@@ -31,10 +32,7 @@ __device__ __forceinline__ f32x4 bn_y(f32x4 x, f32x4 m, f32x4 is, f32x4 b) {
 
 // SVAE_BN_W8=1: bf16-output BN passes with 8 channels per thread (one 16-byte store)
 static bool bn_w8() {
-  static const bool v = [] {
-    const char* e = getenv("SVAE_BN_W8");
-    return e && e[0] == '1';
-  }();
+  static const bool v = svae_knob("SVAE_BN_W8", 0) == 1;
   return v;
 }
 
@@ -43,10 +41,7 @@ static bool bn_w8() {
 // apply blocks each gather nsh x 4 words per channel, the producers' atomics contend with fewer (SVAE_BN_SHMAX
 // overrides: 8 -3 %, 4 -13 %)
 int bn_acc_shards(long long rowblocks, int cap) {
-  static const int over = [] {
-    const char* e = getenv("SVAE_BN_SHMAX");
-    return e ? atoi(e) : 0;
-  }();
+  static const int over = svae_knob("SVAE_BN_SHMAX", 0);
   if (over > 0) cap = over;
   int n = 1;
   while (n < cap && (long long)n * 16 < rowblocks) n *= 2;
@@ -100,15 +95,9 @@ static ApGrid ap_grid(long long rows, int C, int groups, int W = 4) {
   // 4096): these latency-bound passes want blocks even though every block re-finalises its channels'
   // statistics (tools/gpu/r02_rpt.sh: 2 / 4096 is 1 % faster per step than round 1's 4 / 2048; 8, 16,
   // 32 rows per thread 3, 10, 25 % slower)
-  static const int rpt = [] {
-    const char* v = getenv("SVAE_AP_RPT");
-    return v ? atoi(v) : 2;
-  }();
+  static const int rpt = svae_knob("SVAE_AP_RPT", 2);
   long long want = (rows + (long long)rpt * RL - 1) / ((long long)rpt * RL);
-  static const int capb = [] {  // SVAE_AP_CAP: block budget of one pass
-    const char* v = getenv("SVAE_AP_CAP");
-    return v ? atoi(v) : 4096;
-  }();
+  static const int capb = svae_knob("SVAE_AP_CAP", 4096);  // block budget of one pass
   long long cap = capb / ((long long)gx * groups);
   if (cap < 1) cap = 1;
   long long ry = want < cap ? want : cap;

@@ -6,6 +6,17 @@
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// The split mode's scaled fp16 weight planes (opload.h split8_h16 / mfma_h16): planes 3 and 4 of the
+// bf16 weight shadows hold h0 = fp16(w * 2^H16_WS), h1 = fp16(w * 2^H16_WS - h0).  |w| < 64 fits fp16
+// and |w| >= 2^-13 keeps every bit (22-23 of them); the model's weights are O(0.01-1).
+#define H16_WS 10
+#define H16_PLANE 3
+__device__ __forceinline__ void h16_pair(float w, _Float16& h0, _Float16& h1) {
+  const float s = w * (float)(1 << H16_WS);
+  h0 = (_Float16)s;
+  h1 = (_Float16)(s - (float)h0);
+}
+
 #define SVAE_WAVE 64
 
 enum SvaeAct { ACT_NONE = 0, ACT_RELU = 1, ACT_LRELU = 2, ACT_SIGMOID = 3 };

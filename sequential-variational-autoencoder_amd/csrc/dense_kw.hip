@@ -13,6 +13,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "knobs.h"
 #include "kernels.h"
 #include "opload.h"
 
@@ -136,10 +137,7 @@ __global__ __launch_bounds__(256) void dense_kw_kernel(FwdArgs a) {
 }
 
 bool dkw_disabled() {
-  static const bool v = [] {
-    const char* e = getenv("SVAE_NO_DKW");
-    return e && e[0] == '1';
-  }();
+  static const bool v = svae_knob("SVAE_NO_DKW", 0) == 1;
   return v;
 }
 
@@ -147,8 +145,7 @@ bool dkw_disabled() {
 
 static int dkw_wk() {  // SVAE_DKW_WK: 4 (32-row blocks), 2 or 1 (128-row blocks)
   static const int v = [] {
-    const char* e = getenv("SVAE_DKW_WK");
-    const int w = e ? atoi(e) : 4;
+    const int w = svae_knob("SVAE_DKW_WK", 4);
     return (w == 1 || w == 2) ? w : 4;
   }();
   return v;
@@ -165,8 +162,8 @@ static long long dkw_blocks(const FwdArgs& a) {
 int dense_kw_ks(const FwdArgs& a) {
   const long long blocks = dkw_blocks(a);
   const int nks = a.Cin / 16;
-  static const int tgt = [] { const char* e = getenv("SVAE_DKW_TGT"); return e ? atoi(e) : 512; }();
-  static const int mink = [] { const char* e = getenv("SVAE_DKW_MINK"); return e ? atoi(e) : 8; }();
+  static const int tgt = svae_knob("SVAE_DKW_TGT", 512);
+  static const int mink = svae_knob("SVAE_DKW_MINK", 8);
   int ks = 1;
   if (!a.part || a.ldc % 4) return 1;
   while (blocks * ks < tgt && nks / (2 * ks) >= mink && (long long)(2 * ks) * a.rows * a.N <= a.part_cap) ks *= 2;

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "kernels.h"
+#include "knobs.h"
 #include "svae_hip.h"
 
 namespace {
@@ -930,16 +931,16 @@ static int on_side(svae_ctx* c, hipEvent_t ready, hipEvent_t freed, Fn&& fn) {
 // SVAE_TRACE_GEMM=1: every main-stream gather-GEMM timed alone (the stream is drained around
 // it) and printed with its shape -- a per-layer breakdown for tuning, not for measurement runs
 static bool trace_gemm() {
-  static const bool v = [] {
-    const char* e = getenv("SVAE_TRACE_GEMM");
-    return e && e[0] == '1';
-  }();
+  static const bool v = svae_knob("SVAE_TRACE_GEMM", 0) == 1;
   return v;
 }
 static int gemm(svae_ctx* c, FwdArgs a, int groups) {
   if (c->m.g.split && a.Bh) {
     a.nsp = 3;
-    if (!a.b_plane) a.b_plane = c->wplane;  // (the packed output weights carry their own plane stride)
+    if (!a.b_plane) {  // (the packed output weights carry their own plane stride and no fp16 planes)
+      a.b_plane = c->wplane;
+      a.h16 = 1;  // a weight shadow: the fp16 planes H16_PLANE.. follow the bf16 ones
+    }
     a.part = c->slab;
     a.part_cap = c->slab_cap;
     if (!igemm_split_ok(a, groups)) {  // no split kernel for this shape: the fp32 kernels
@@ -1012,10 +1013,7 @@ static void wgemm(svae_ctx* c, const WgArgs& w, int groups) {
     wgrad(w, groups, c->st);
     return;
   }
-  static const bool split_wg = [] {  // SVAE_SPLIT_WG=0: the fp32 weight-GEMM in split mode (A/B)
-    const char* e = getenv("SVAE_SPLIT_WG");
-    return !(e && e[0] == '0');
-  }();
+  static const bool split_wg = svae_knob("SVAE_SPLIT_WG", 1) != 0;  // 0: the fp32 weight-GEMM in split mode
   if (c->m.g.split && !split_wg) {
     wgrad(w, groups, c->st);
     return;
@@ -1042,7 +1040,9 @@ static void wgemm(svae_ctx* c, const WgArgs& w, int groups) {
 // the step time without the passes a consumer-side fold would remove (an upper bound of its gain);
 // bit 2 every conv weight gradient (side stream), bit 3 the per-bucket Adam of the chain steps; bit 4 makes
 // the conv layers' forward BN apply read last step's mean / invstd instead of finalising the statistics
-// accumulators per block (the gain a producer-side finalise could bring)
+// accumulators per block (the gain a producer-side finalise could bring).  Compiled only into a
+// -DSVAE_DEBUG_PROBES build: the shipping library ignores the variable (tests/test_knobs.py)
+#ifdef SVAE_DEBUG_PROBES
 static int dbg_skip() {
   static const int v = [] {
     const char* e = getenv("SVAE_DBG_SKIP");
@@ -1050,6 +1050,9 @@ static int dbg_skip() {
   }();
   return v;
 }
+#else
+static inline int dbg_skip() { return 0; }
+#endif
 
 // the consumer-side BN gather is available for this launch (the wave-split halo gather takes it)
 static bool ain_ok(svae_ctx* c, const FwdArgs& t, int groups) {
@@ -1058,6 +1061,7 @@ static bool ain_ok(svae_ctx* c, const FwdArgs& t, int groups) {
   if (c->m.g.split) {
     u.nsp = 3;
     u.b_plane = c->wplane;
+    u.h16 = 1;
   }
   return halo_kw_plan(u, groups) > 0;
 }
@@ -1107,6 +1111,7 @@ static int conv_bn_act_fwd(svae_ctx* c, const ConvL& L, int groups, long long w_
     if (c->m.g.split) {
       u.nsp = 3;
       u.b_plane = c->wplane;
+      u.h16 = 1;
     }
     if (igemm_fin_ok(u, groups)) {
       u64* cnt = acc_take(c, groups);
@@ -1171,7 +1176,6 @@ static int dpre_bf(const svae_ctx* c, const ConvL& L) {
 }
 
 // weight gradient of a conv/convT layer: dpre = grad wrt pre-BN output, in = layer input
-static int dbg_skip();
 static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, View in, const float* dpre,
                       long long dpre_gs, float* dW) {
   const int B = c->m.g.B;
@@ -1217,8 +1221,8 @@ static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, V
       const long long per = 16LL * w.M * w.N;
       // ~wh_target blocks, but >= wh_minch chunks per block: every split writes (and the reduce
       // reads) a full 16*M*N partial, so short splits cost more partial traffic than they save
-      static const int wh_target = getenv("SVAE_WH_TARGET") ? atoi(getenv("SVAE_WH_TARGET")) : 256;
-      static const int wh_minch = getenv("SVAE_WH_MINCH") ? atoi(getenv("SVAE_WH_MINCH")) : 8;
+      static const int wh_target = svae_knob("SVAE_WH_TARGET", 256);
+      static const int wh_minch = svae_knob("SVAE_WH_MINCH", 8);
       long long ns = (wh_target + (long long)pl.tiles * groups - 1) / ((long long)pl.tiles * groups);
       ns = std::min<long long>(ns, std::max<long long>(1, pl.h.nchunk / wh_minch));
       ns = std::min<long long>(ns, std::max<long long>(1, c->slab_cap / (per * groups)));
@@ -1289,10 +1293,7 @@ static BwFuse bw_fuse(svae_ctx* c, const float* pre, int ldp, long long pre_gs, 
 }
 
 static bool nofuse_out() {  // SVAE_NO_BWFUSE_OUT=1: s1[0]'s BN-backward sums in their own pass (A/B)
-  static const bool v = [] {
-    const char* e = getenv("SVAE_NO_BWFUSE_OUT");
-    return e && e[0] == '1';
-  }();
+  static const bool v = svae_knob("SVAE_NO_BWFUSE_OUT", 0) == 1;
   return v;
 }
 static int conv_dgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, const float* dpre, long long dpre_gs,
@@ -1348,10 +1349,7 @@ static int conv_dgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, c
   if (c->m.g.bf16 && c->wN) {  // NK bf16 [tap][ci][co]: conv -> N copy, conv-T -> T copy
     a.Bh = L.tr ? shadowT(c, L.ow) : shadowN(c, L.ow);
     a.ldb = L.cout;
-    static const int nofuse = [] {
-      const char* v = getenv("SVAE_NO_BWFUSE");
-      return (v && v[0] == '1') ? 1 : 0;
-    }();
+    static const int nofuse = svae_knob("SVAE_NO_BWFUSE", 0) == 1;
     FwdArgs sa = a;  // split mode: the fused partials need the split kernel (the fp32 one has none)
     sa.nsp = 3;
     const bool fuse_ok = !c->m.g.split || igemm_split_ok(sa, groups);
@@ -1367,6 +1365,7 @@ static int conv_dgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, c
       if (c->m.g.split) {
         u.nsp = 3;
         u.b_plane = c->wplane;
+        u.h16 = 1;
       }
       if ((c->laf & 2) && fu->dbeta && igemm_fin_ok(u, groups)) {  // a, b, dbeta by the last block
         const int C = fu->bw.C;
@@ -1569,10 +1568,7 @@ static int inference_fwd(svae_ctx* c, int t0, int n, View in0) {
 // The output / ratio conv-T operands of every step, PACK_MAXT steps per launch (misc.hip
 // pack_out_kernel): [tap][C+1][F1] weights (ratio row zero at t = 0), 4 bias floats, bf16 copy.
 static bool pack_step_mode() {
-  static const bool v = [] {
-    const char* e = getenv("SVAE_PACK_STEP");
-    return e && e[0] == '1';
-  }();
+  static const bool v = svae_knob("SVAE_PACK_STEP", 0) == 1;
   return v;
 }
 
@@ -1768,17 +1764,11 @@ static int engine_forward(svae_ctx* c) {
   const bool rsplit = c->rec_split && c->st4 && !g.plc && T > 1 && !c->generative;
   // split_latent of every step on the side stream (z is known for all steps unless Latent
   // InfoMax draws z_t inside the chain); step t's decoder waits on ev_sfc[t]
-  static const int sfc_mode = [] {  // SVAE_SFC: 0 = split-latent forward on the main stream per step
-    const char* v = getenv("SVAE_SFC");
-    return v ? atoi(v) : 1;
-  }();
+  static const int sfc_mode = svae_knob("SVAE_SFC", 1);  // 0 = split-latent forward on the main stream per step
   const bool sfc_side = sfc_mode != 0 && c->side && !g.plc && T <= 64;
   // output / ratio operands packed before the split-latent hand-over to st3 (+0.5 % per step in a
   // same-box A/B, profiles/r03_ab3.txt); SVAE_PACK_FIRST=0 packs after it (round 2's order)
-  static const bool pack_first = [] {
-    const char* e = getenv("SVAE_PACK_FIRST");
-    return !(e && e[0] == '0');
-  }();
+  static const bool pack_first = svae_knob("SVAE_PACK_FIRST", 1) != 0;
   if (pack_first) pack_out_all(c, st);
   if (sfc_side) {
     hipEventRecord(c->ev_aux, st);
@@ -2584,34 +2574,27 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
     return fail(nullptr, SVAE_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
   }
   {
-    const char* fo = getenv("SVAE_FOLD");  // forward BN applies of gather-only tensors on st2
-    c->fold = fo && fo[0] == '1';
-    const char* s2 = getenv("SVAE_SIDE2");  // a second weight-gradient stream
-    c->side2 = s2 && s2[0] == '1';
-    const char* rg = getenv("SVAE_REC_GROUP");  // recognition-backward group size (0 = batched after the chain)
-    c->rec_group = rg ? atoi(rg) : 0;
+    // measured-slower alternatives, reachable only in a -DSVAE_KNOBS build, read per context
+    c->fold = svae_knob("SVAE_FOLD", 0) == 1;          // forward BN applies of gather-only tensors on st2
+    c->side2 = svae_knob("SVAE_SIDE2", 0) == 1;        // a second weight-gradient stream
+    c->rec_group = svae_knob("SVAE_REC_GROUP", 0);     // recognition-backward group size (0 = batched after the chain)
     if (c->rec_group < 0 || c->m.g.plc) c->rec_group = 0;
-    const char* rs = getenv("SVAE_REC_SPLIT");  // forward recognition of steps >= 1 on st4
-    c->rec_split = (rs && rs[0] == '1' && !c->m.g.plc && c->m.g.T > 1) ? 1 : 0;
+    c->rec_split = (svae_knob("SVAE_REC_SPLIT", 0) == 1 && !c->m.g.plc && c->m.g.T > 1) ? 1 : 0;  // forward recognition of steps >= 1 on st4
   }
   {
-    const char* v = getenv("SVAE_DPRE_F32");  // A/B: keep the BN-backward outputs in fp32
-    c->dbf = (c->m.g.bf16 && !c->m.g.split && !(v && v[0] == '1')) ? 1 : 0;
-    const char* va = getenv("SVAE_ACT_F32");  // A/B: keep every activation in fp32
-    c->abf = (c->m.g.bf16 && !c->m.g.split && !(va && va[0] == '1')) ? 1 : 0;
-    const char* vc = getenv("SVAE_CAT_F32");
-    c->cbf = (c->abf && !(vc && vc[0] == '1')) ? 1 : 0;
-    const char* vl = getenv("SVAE_BN_LAF");
-    c->laf = vl ? atoi(vl) : 0;
-    const char* vp = getenv("SVAE_PRE_F32");  // A/B: keep the conv layers' pre-BN outputs in fp32
-    c->pbf = (c->m.g.bf16 && !c->m.g.split && !(vp && vp[0] == '1')) ? 1 : 0;
+    // operand storage in bf16 mode; the fp32 alternatives are bitwise A/B checks (knob builds)
+    c->dbf = (c->m.g.bf16 && !c->m.g.split && svae_knob("SVAE_DPRE_F32", 0) != 1) ? 1 : 0;  // BN-backward outputs
+    c->abf = (c->m.g.bf16 && !c->m.g.split && svae_knob("SVAE_ACT_F32", 0) != 1) ? 1 : 0;   // GEMM-only activations
+    c->cbf = (c->abf && svae_knob("SVAE_CAT_F32", 0) != 1) ? 1 : 0;                        // decoder concat buffers
+    c->laf = svae_knob("SVAE_BN_LAF", 0);  // last-arriver BN finalisation (experimental: off)
+    c->pbf = (c->m.g.bf16 && !c->m.g.split && svae_knob("SVAE_PRE_F32", 0) != 1) ? 1 : 0;   // conv pre-BN outputs
   }
   c->counting = true;
   c->arena_used = 0;
   plan(c);
-  if (c->m.g.Dz > 1024) {  // latent_fwd_kernel: one image per block of up to 1024 threads
+  if (c->m.g.Dz > 256) {  // latent_fwd_kernel: whole images per 256-thread block (unreachable: make_geo caps Dz)
     delete c;
-    return fail(nullptr, SVAE_EBADCONFIG, "latent over 1024 dimensions");
+    return fail(nullptr, SVAE_EBADCONFIG, "latent over 256 dimensions");
   }
   c->arena_bytes = c->arena_used;
   c->counting = false;
@@ -2671,7 +2654,8 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
     // split mode: three planes (hi / mid / lo, opload.h split8) of wplane elements each
     c->nsp = c->m.g.split ? 3 : 1;
     c->wplane = ((long long)nl + 127) / 128 * 128;
-    const size_t sbytes = (size_t)c->nsp * c->wplane * 2;
+    // (split mode: + the two scaled fp16 planes H16_PLANE, H16_PLANE + 1 that the wave-split gathers read)
+    const size_t sbytes = (size_t)(c->nsp == 3 ? H16_PLANE + 2 : c->nsp) * c->wplane * 2;
     e = hipMalloc(&c->wN, sbytes);
     if (e == hipSuccess) e = hipMalloc(&c->wT, sbytes);
     if (e != hipSuccess) {
@@ -2725,14 +2709,12 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
   }
   hipHostMalloc((void**)&c->reg_host, 64 * sizeof(float), hipHostMallocDefault);
   {
-    const char* ns = getenv("SVAE_NO_SIDE");
-    if (!(ns && ns[0] == '1')) {
+    if (svae_knob("SVAE_NO_SIDE", 0) != 1) {
       // SVAE_SIDE_CUMASK=k (A/B): the weight-gradient stream runs on all CUs but every k-th, so the
       // main stream's latency-bound kernels always find free CUs.  A CU-masked stream is a blocking
       // stream (it synchronises with the NULL stream), so this is only meaningful when the caller's
       // stream is not the NULL stream (bench.py SVAE_BENCH_STREAM=1)
-      const char* cm = getenv("SVAE_SIDE_CUMASK");
-      const int cmk = cm ? atoi(cm) : 0;
+      const int cmk = svae_knob("SVAE_SIDE_CUMASK", 0);
       bool ok;
       if (cmk >= 2) {
         int ncu = 0;
@@ -2752,10 +2734,7 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
       // writes the L2s back for host / peer visibility, a GPU-side bubble at every record); the
       // gradient-hook event, which orders a collective's peer traffic, keeps it
       // (SVAE_EV_SYSFENCE=1: every event with the system fence)
-      static const bool sysf = [] {
-        const char* e = getenv("SVAE_EV_SYSFENCE");
-        return e && e[0] == '1';
-      }();
+      static const bool sysf = svae_knob("SVAE_EV_SYSFENCE", 0) == 1;
       const unsigned evf = hipEventDisableTiming | (sysf ? 0u : (unsigned)hipEventDisableSystemFence);
       auto mk = [&](hipEvent_t* ev) { ok = ok && hipEventCreateWithFlags(ev, evf) == hipSuccess; };
       for (int i = 0; i < svae_ctx::NR; ++i) { mk(&c->ev_ready[i]); mk(&c->ev_iready[i]); }
@@ -2772,15 +2751,13 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
       for (int i = 0; i < svae_ctx::NFOLD; ++i) mk(&c->ev_fold[i]);
       mk(&c->ev_fold_join);
       {  // SVAE_SIDE_BATCH (read per context): weight-gradient layers per side-stream hand-over
-        const char* e = getenv("SVAE_SIDE_BATCH");
-        c->side_batch = e ? std::max(1, atoi(e)) : 1;
+        c->side_batch = std::max(1, svae_knob("SVAE_SIDE_BATCH", 1));
       }
       c->side = ok;
     }
   }
   {
-    const char* e = getenv("SVAE_BWFUSE_FC");  // read per context (A/B and the bitwise test)
-    c->fc_fuse = !(e && e[0] == '0');
+    c->fc_fuse = svae_knob("SVAE_BWFUSE_FC", 1) != 0;  // read per context (A/B and the bitwise test)
   }
   for (int i = 0; i < 64; ++i) c->reg_host[i] = 0.f;
   *out = c;
@@ -3173,6 +3150,9 @@ int svae_op_conv(const float* x, int n, int h, int cin, const float* w, int cout
 
 int svae_op_gather_bf16(const float* x, int n, int h, int cin, const void* w_nk, int cout, int stride, int transpose,
                         int path, float* y, void* scratch, int64_t scratch_bytes, void* stream) {
+  const int split = (path >> 4) & 1;  // bit 4: split-bf16 planes (dtype bf16x6): w_nk holds 3 planes
+  const int path_in = path;
+  path &= 15;
   if (!x || !w_nk || !y || (stride != 1 && stride != 2) || path < 0 || path > 2)
     return fail(nullptr, SVAE_EBADARG, "bad op args");
   ConvL L;
@@ -3184,6 +3164,11 @@ int svae_op_gather_bf16(const float* x, int n, int h, int cin, const void* w_nk,
   a.C = y; a.ldc = cout;
   a.part = (float*)scratch;
   a.part_cap = scratch ? scratch_bytes / (int64_t)sizeof(float) : 0;
+  if (split) {
+    a.nsp = 3;
+    a.b_plane = 16LL * cin * cout;
+    a.h16 = (path_in >> 5) & 1;  // bit 5: w_nk also holds the scaled fp16 planes (5 planes in all)
+  }
   if (igemm_bf16_path(a, 1, path, (hipStream_t)stream) < 0)
     return fail(nullptr, SVAE_EBADARG, "shape does not qualify for the halo-tile kernel");
   hipError_t e = hipGetLastError();

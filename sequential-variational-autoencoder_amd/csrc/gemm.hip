@@ -16,6 +16,7 @@
 // The epilogue optionally emits per-column partial (sum, sum^2) for the
 // following training-mode BatchNorm, so BN statistics cost no extra HBM pass.
 #include "common.h"
+#include "knobs.h"
 #include "kernels.h"
 
 #define BK 32
@@ -610,8 +611,8 @@ void wgrad_reduce(const float* part, long long p_gs, int nsplit, int ntap, int M
   const long long nq = per / 4;
   // split lanes: enough blocks to stream the slab at full bandwidth even for small outputs
   // SVAE_WRED_SLMAX / SVAE_WRED_BLOCKS: split-lane cap and block target (A/B knobs)
-  static const int sl_max = getenv("SVAE_WRED_SLMAX") ? atoi(getenv("SVAE_WRED_SLMAX")) : 16;
-  static const int blk_target = getenv("SVAE_WRED_BLOCKS") ? atoi(getenv("SVAE_WRED_BLOCKS")) : 1024;
+  static const int sl_max = svae_knob("SVAE_WRED_SLMAX", 16);
+  static const int blk_target = svae_knob("SVAE_WRED_BLOCKS", 1024);
   int sl = 1;
   while (sl < sl_max && sl < nsplit && (nq * sl) / 256 * groups < blk_target) sl *= 4;
   const int qb = 256 / sl;

@@ -11,6 +11,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "knobs.h"
 #include "kernels.h"
 #include "opload.h"
 
@@ -1134,6 +1135,14 @@ __global__ void shadow_n_kernel(const float* w, __bf16* out, long long n, int ns
        i += (long long)gridDim.x * blockDim.x * 4) {
     if (i + 3 < n) {
       f32x4 v = *(const f32x4*)(w + i);
+      if (nsp == 3) {  // split mode: the fp16 planes too
+        _Float16 h0[4], h1[4];
+        for (int e = 0; e < 4; ++e) h16_pair(v[e], h0[e], h1[e]);
+        for (int e = 0; e < 4; ++e) {
+          ((_Float16*)out)[H16_PLANE * plane + i + e] = h0[e];
+          ((_Float16*)out)[(H16_PLANE + 1) * plane + i + e] = h1[e];
+        }
+      }
       for (int p = 0; p < nsp; ++p) {
         const bf16x4 h = __builtin_convertvector(v, bf16x4);
         *(bf16x4*)(out + p * plane + i) = h;
@@ -1142,6 +1151,7 @@ __global__ void shadow_n_kernel(const float* w, __bf16* out, long long n, int ns
     } else {
       for (long long j = i; j < n; ++j) {
         float v = w[j];
+        if (nsp == 3) h16_pair(v, ((_Float16*)out)[H16_PLANE * plane + j], ((_Float16*)out)[(H16_PLANE + 1) * plane + j]);
         for (int p = 0; p < nsp; ++p) {
           const __bf16 h = (__bf16)v;
           out[p * plane + j] = h;
@@ -1171,6 +1181,9 @@ __global__ __launch_bounds__(256) void shadow_t_kernel(const float* w, __bf16* o
     int c = d.w + i, r = d.z + tx;
     if (r < R && c < Cc) {
       float v = t[tx][i];
+      if (nsp == 3)  // split mode: the fp16 planes too
+        h16_pair(v, ((_Float16*)dst)[H16_PLANE * plane + (long long)c * R + r],
+                 ((_Float16*)dst)[(H16_PLANE + 1) * plane + (long long)c * R + r]);
       for (int p = 0; p < nsp; ++p) {
         const __bf16 h = (__bf16)v;
         dst[p * plane + (long long)c * R + r] = h;
@@ -1317,10 +1330,7 @@ struct HaloPlan {
 // the large tile is kept only when it fills this many blocks; below it the smaller tile (no or
 // less split-K) wins (tools/bench_gather.py: 16x16 / 8x8 conv-T layers).  SVAE_HALO_FILL overrides.
 static int halo_fill() {
-  static const int v = [] {
-    const char* e = getenv("SVAE_HALO_FILL");
-    return e ? atoi(e) : 512;
-  }();
+  static const int v = svae_knob("SVAE_HALO_FILL", 512);
   return v;
 }
 
@@ -1343,10 +1353,7 @@ static HaloPlan halo_plan(const FwdArgs& a, int groups) {
   // the smaller tile of the two (128x32 / 64x64 / 64x128) by default since the gather-GEMMs run at
   // 4 waves per SIMD (v42: +0.8 % of the step over 4 same-box rounds); SVAE_HALO_SMALL=0 restores the
   // larger tile where it fills halo_fill() blocks
-  static const bool small_only = [] {
-    const char* v = getenv("SVAE_HALO_SMALL");
-    return !(v && v[0] == '0');
-  }();
+  static const bool small_only = svae_knob("SVAE_HALO_SMALL", 1) != 0;
   for (int ci = small_only ? 1 : 0; ci < 2; ++ci) {
     const int bm = cands[ci];
     if (bm % Wr != 0 || a.rows % bm != 0) continue;
@@ -1390,10 +1397,7 @@ static HaloPlan halo_plan(const FwdArgs& a, int groups) {
     p.ks = ks;
     // a split of one chunk never prefetches a second window: one LDS buffer, so that three blocks
     // (the register limit) instead of two fit a CU and hide each other's window-load latency
-    static const bool two_buf = [] {
-      const char* v = getenv("SVAE_HALO_1BUF");
-      return v && v[0] == '0';
-    }();
+    static const bool two_buf = svae_knob("SVAE_HALO_1BUF", 1) == 0;
     if (!two_buf && (nchunk + ks - 1) / ks <= 1) p.lds = (size_t)h.npix * ROWP * sizeof(__bf16);
     p.nrb = ks == 1 ? a.nclass * (a.rows / bm) : (int)(((long long)a.rows * a.nclass + SKR_ROWS - 1) / SKR_ROWS);
     if (bn == 32) p.kid = bm == 256 ? KID_HALO_256x32 : KID_HALO_128x32;
@@ -1436,21 +1440,14 @@ static void launch_halo(const HaloArgs& h, int groups, size_t lds, hipStream_t s
 // per launch there); at 4 waves per SIMD (v41) the wave split on every layer is 2.3 % faster per
 // step (v43, same-box A/B).  SVAE_KW: 0 = only instead of split-K, 1 = layers with >= 2 chunks
 static bool kw_first(const FwdArgs& a, const HaloPlan& hp) {
-  static const int mode = [] {  // SVAE_KW: 0 = only instead of split-K, 2 = wherever it fits (default)
-    const char* v = getenv("SVAE_KW");
-    return v ? atoi(v) : 2;
-  }();
+  static const int mode = svae_knob("SVAE_KW", 2);  // 0 = only instead of split-K, 2 = wherever it fits
   if (hp.ks > 1) return true;
   if (mode == 2) return true;
   return mode == 1 && a.Cin >= 2 * HALO_CK;
 }
 
 static int halo_disabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("SVAE_NO_HALO");
-    v = (e && e[0] == '1') ? 1 : 0;
-  }
+  static const int v = svae_knob("SVAE_NO_HALO", 0) == 1;
   return v;
 }
 
@@ -1755,11 +1752,7 @@ int wgrad_halo_plan(const WgArgs& a, int groups, WHaloPlanOut* out) {
 }
 
 static int wgrad_halo_disabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("SVAE_NO_HALO");
-    v = (e && e[0] == '1') ? 1 : 0;
-  }
+  static const int v = svae_knob("SVAE_NO_HALO", 0) == 1;
   return v;
 }
 int wgrad_halo_enabled() { return !wgrad_halo_disabled(); }

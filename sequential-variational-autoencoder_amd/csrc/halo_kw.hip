@@ -18,6 +18,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "knobs.h"
 #include "opload.h"
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -31,6 +32,15 @@ typedef float f32x8 __attribute__((ext_vector_type(8)));
 #endif
 #ifndef KW_OCC_BR
 #define KW_OCC_BR 5  // the same with the two-tap B ring
+#endif
+#ifndef KW_OCC_H16
+#define KW_OCC_H16 4  // the split mode's fp16-plane instances (two planes: ~24 VGPRs fewer than three)
+#endif
+#ifndef KW_OCC_H16_64
+#define KW_OCC_H16_64 3  // (4 spills 8-26 VGPRs)
+#endif
+#ifndef KW_OCC_H16_128
+#define KW_OCC_H16_128 2
 #endif
 #ifndef KW_OCC_S32
 #define KW_OCC_S32 3  // split-mode 32-row instances with the B ring (4 spills 17-18 VGPRs)
@@ -49,6 +59,7 @@ struct KwArgs {
   int tpb;            // tiles per block: 1 = one tile per block (3-D grid); > 1 = persistent (1-D grid)
   int vec;            // 16-byte epilogue (every epilogue operand row 16-byte aligned; SVAE_KW_VEC)
   int ain_off;        // byte offset of the consumer-side BN table [3][Cin] in dynamic LDS (f.ain.acc != nullptr)
+  int slot_off;       // NS = 2: byte offset of the [2][4] wave maxima of |A| in dynamic LDS
 };
 
 namespace {
@@ -174,10 +185,12 @@ __device__ __forceinline__ void kw_epilogue_vec(const KwArgs& h, float* red, int
 template <int BM, int BN, bool S2T, bool ABF, int NS = 1, bool PST = false, bool BR = false, int PI = KW_PI,
           bool AIN = false>
 __global__ __launch_bounds__(256, AIN ? (S2T ? 4 : 3) : (ABF && BN == 32 && BM <= 64 && !PST) ? ((BR || S2T) ? KW_OCC_BR : KW_OCC)
-                                                                         : ((NS == 3 && BR) ? (BM == 32 ? KW_OCC_S32 : 3) : 2))
+                                                                         : NS == 2 ? (BM == 128 ? KW_OCC_H16_128 : BM == 64 ? KW_OCC_H16_64 : KW_OCC_H16)
+                                                                         : ((NS == 3 && BR) ? (BM == 32 ? KW_OCC_S32 : (BM == 128 ? 2 : 3)) : 2))
 void igemm_halo_kw_kernel(KwArgs h) {
-  static_assert(NS == 1 || (NS == 3 && !ABF), "split planes from fp32 activations only");
+  static_assert(NS == 1 || ((NS == 2 || NS == 3) && !ABF), "split planes from fp32 activations only");
   static_assert(!BR || !S2T, "the B ring: 16-tap instances");
+  static_assert(!(PST && NS == 2), "the fp16 planes' running exponent is per tile");
   constexpr int TM = BM / 32;
   constexpr int TN = BN / 32;
   constexpr int NTAP = S2T ? 4 : 16;
@@ -191,6 +204,14 @@ void igemm_halo_kw_kernel(KwArgs h) {
   const int lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
   constexpr bool abf = ABF;
+#ifdef SVAE_EXP_STAMPS  // timing experiment: per-wave phase stamps (s_memtime) into the split-K scratch
+  unsigned long long* stamp_p = (unsigned long long*)a.part +
+      ((long long)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 4 + wave) * 16;
+#define KW_STAMP(i) do { if (lane == 0 && (i) < 16) stamp_p[(i)] = __builtin_readcyclecounter(); } while (0)
+#else
+#define KW_STAMP(i) do {} while (0)
+#endif
+  KW_STAMP(0);
   const int nchunk = a.Cin / KW_CK;
   const int per_img = h.Hr * h.Wr;
 
@@ -298,7 +319,31 @@ void igemm_halo_kw_kernel(KwArgs h) {
       hi[j] = act_f(bn_y1(hi[j], m1[j], s1[j], b1[j]), a.ain.act);
     }
   };
-  // NS == 1: buffer `buf` of two; NS == 3: plane p of the one buffer at p * npix * KW_ROWP
+  // NS == 2 (scaled fp16 planes): the block-wide running max of |A| over the chunks staged so far and
+  // its exponent hs (A is staged as A * 2^hs; every wave's accumulator is kept in the current units and
+  // shrunk by the exponent step when a chunk raises the max, exact powers of two)
+  [[maybe_unused]] int hs = 0;
+  [[maybe_unused]] float hmax = 0.f;
+  [[maybe_unused]] float* hslot = (float*)((char*)ksm + h.slot_off);
+  auto wave_max_put = [&](int parity) {  // this wave's max |A| of the registers holding the next chunk
+    float m = 0.f;
+#pragma unroll
+    for (int i = 0; i < PI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) m = fmaxf(m, fmaxf(fabsf(wv[i][0][j]), fabsf(wv[i][1][j])));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if (lane == 0) hslot[parity * 4 + wave] = m;
+  };
+  auto take_scale = [&](int parity) {  // (after a barrier) the new exponent; returns the step (<= 0)
+    const float m = fmaxf(fmaxf(hslot[parity * 4], hslot[parity * 4 + 1]), fmaxf(hslot[parity * 4 + 2], hslot[parity * 4 + 3]));
+    hmax = fmaxf(hmax, m);
+    const int ns = h16_exp(hmax);
+    const int d = ns - hs;
+    hs = ns;
+    return d;
+  };
+  // NS == 1: buffer `buf` of two; NS == 3 / 2: plane p of the one buffer at p * npix * KW_ROWP
   auto store_window = [&](int buf, int chunk) {
     __bf16* W = ksm + buf * h.npix * KW_ROWP;
 #pragma unroll
@@ -320,7 +365,13 @@ void igemm_halo_kw_kernel(KwArgs h) {
         *(bf16x8*)&W[o] = raw8_bf(wv[i][0], wv[i][1], abf);
       } else {
         bf16x8 pl[NS];
-        split8<NS>(wv[i][0], wv[i][1], pl);
+#ifdef SVAE_EXP_NOSPLIT  // timing experiment (wrong results): one conversion, copied to every plane
+        pl[0] = raw8_bf(wv[i][0], wv[i][1], false);
+        for (int p = 1; p < NS; ++p) pl[p] = pl[0];
+#else
+        if constexpr (NS == 2) split8_h16(wv[i][0], wv[i][1], hs, pl);
+        else split8<NS>(wv[i][0], wv[i][1], pl);
+#endif
 #pragma unroll
         for (int p = 0; p < NS; ++p) *(bf16x8*)&ksm[p * h.npix * KW_ROWP + o] = pl[p];
       }
@@ -345,7 +396,11 @@ void igemm_halo_kw_kernel(KwArgs h) {
     const __bf16* bptr = (const __bf16*)a.Bh + q.group * a.b_gs + (long long)(q.n0 + l32) * a.ldb + 8 * hh;
     const int t = wave * NTW + u;
     const int tap = S2T ? q.tap0 + 8 * (t >> 1) + 2 * (t & 1) : t;
+#ifdef SVAE_EXP_BL1  // timing experiment (wrong results): every B fragment from one L1-resident tap / chunk
+    const long long off = 0 * (tap + chunk);
+#else
     const long long off = (long long)tap * a.b_tap + chunk * KW_CK;
+#endif
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
@@ -398,6 +453,11 @@ void igemm_halo_kw_kernel(KwArgs h) {
     store_window(0, 0);
     __syncthreads();
   }
+  if constexpr (NS == 2) {
+    wave_max_put(0);
+    __syncthreads();
+  }
+  KW_STAMP(1);
   for (;;) {
     // the next tile of this block (persistent form)
     const bool has_tile = PST && t_cur + 1 < t_end;
@@ -418,9 +478,21 @@ void igemm_halo_kw_kernel(KwArgs h) {
       const int buf = NS == 1 ? (c & 1) : 0;
       const bool has_next = c + 1 < nchunk;
       if constexpr (NS > 1) {  // one buffer of NS planes: stage chunk c, then prefetch c + 1
+        if constexpr (NS == 2) {
+          const int d = take_scale(c & 1);
+          if (d != 0) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+              for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = __builtin_ldexpf(acc[i][j][r], d);
+          }
+        }
         store_window(0, c);
         __syncthreads();
       }
+      if (c < 4) KW_STAMP(2 + 2 * c);
       if constexpr (!BR) {
         if (has_next) {
           load_window(cur, c + 1);
@@ -460,18 +532,26 @@ void igemm_halo_kw_kernel(KwArgs h) {
 #pragma unroll
           for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-            for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_split<NS>(af[tm], bq[BR ? (u & 1) : u][tn][kq], acc[tm][tn]);
+            for (int tn = 0; tn < TN; ++tn) {
+              if constexpr (NS == 2) acc[tm][tn] = mfma_h16(af[tm], bq[BR ? (u & 1) : u][tn][kq], acc[tm][tn]);
+              else acc[tm][tn] = mfma_split<NS>(af[tm], bq[BR ? (u & 1) : u][tn][kq], acc[tm][tn]);
+            }
         }
         if constexpr (!BR) {
           if (has_next) load_b(cur, u, u, c + 1);
           else if (has_tile) load_b(nxt, u, u, 0);
         }
       }
+      if (c < 4) KW_STAMP(3 + 2 * c);
       if constexpr (NS == 1) {
         if (has_next) store_window(buf ^ 1, c + 1);
       }
+      if constexpr (NS == 2) {
+        if (has_next) wave_max_put((c + 1) & 1);
+      }
       __syncthreads();
     }
+    KW_STAMP(10);
 
     // ---- sum the four waves' partial tiles in LDS (fixed order), then one epilogue ----
     const int m0 = cur.m0, n0 = cur.n0, group = cur.group, cls = cur.cls;
@@ -483,9 +563,10 @@ void igemm_halo_kw_kernel(KwArgs h) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int m = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          red[(wave * BM + m) * BN + tn * 32 + l32] = acc[tm][tn][r];
+          red[(wave * BM + m) * BN + tn * 32 + l32] = NS == 2 ? __builtin_ldexpf(acc[tm][tn][r], -(hs + H16_WS)) : acc[tm][tn][r];
         }
     __syncthreads();
+    KW_STAMP(11);
     if (h.vec) {  // 16-byte epilogue: 4 consecutive columns per thread (write-through-friendly stores)
       if (a.bw.pre_bf16) {
         if (a.bw.y_bf16) kw_epilogue_vec<BM, BN, true, true>(h, red, tid, cur.m0, cur.n0, cur.group, cur.cls);
@@ -494,6 +575,7 @@ void igemm_halo_kw_kernel(KwArgs h) {
         if (a.bw.y_bf16) kw_epilogue_vec<BM, BN, false, true>(h, red, tid, cur.m0, cur.n0, cur.group, cur.cls);
         else kw_epilogue_vec<BM, BN, false, false>(h, red, tid, cur.m0, cur.n0, cur.group, cur.cls);
       }
+      KW_STAMP(12);
       if (!has_tile) break;
       __syncthreads();
       cur = nxt;
@@ -573,6 +655,7 @@ void igemm_halo_kw_kernel(KwArgs h) {
       }
       if (a.fin.cnt) bn_fin_arrive(a.fin, group, (int*)red);
     }
+    KW_STAMP(12);
     if (!has_tile) break;
     // ---- the next tile: its window (prefetched above) into LDS once every wave is done with red ----
     __syncthreads();
@@ -589,27 +672,21 @@ void igemm_halo_kw_kernel(KwArgs h) {
 
 // ---- planner: eligible shapes, BM, window geometry, LDS, stats row-blocks ----
 static int kw_bn_mode() {  // SVAE_KW_BN: 32 (default) or 64 column tiles
-  static const int v = [] {
-    const char* e = getenv("SVAE_KW_BN");
-    return e ? atoi(e) : 32;
-  }();
+  static const int v = svae_knob("SVAE_KW_BN", 32);
   return v;
 }
 
 static bool split_pi3() {  // SVAE_KW_PI3=0: split instances keep 4 window items per thread
-  static const bool v = [] {
-    const char* e = getenv("SVAE_KW_PI3");
-    return !(e && e[0] == '0');
-  }();
+  static const bool v = svae_knob("SVAE_KW_PI3", 1) != 0;
   return v;
 }
 
 // split mode: SVAE_KW_SPLIT_BM=32 takes 32-row tiles (4 waves per SIMD) instead of 64 where both fit
 static int split_bm_max() {
-  static const int v = [] {
-    const char* e = getenv("SVAE_KW_SPLIT_BM");
-    return e ? atoi(e) : 64;
-  }();
+#ifndef KW_SPLIT_BM_DEFAULT
+#define KW_SPLIT_BM_DEFAULT 64
+#endif
+  static const int v = svae_knob("SVAE_KW_SPLIT_BM", KW_SPLIT_BM_DEFAULT);
   return v;
 }
 
@@ -622,12 +699,9 @@ static bool kw_plan(const FwdArgs& a, int groups, KwArgs* out, int* bm_out, int*
   const int sy = g.mode == GM_CONV ? g.stride : 1;
   const int span = s2t ? 2 : 4;
   const int per_img = Hr * Wr;
-  static const int bm_max = [] {  // SVAE_KW_BM: largest row tile (32, 64 = default, 128)
-    const char* e = getenv("SVAE_KW_BM");
-    return e ? atoi(e) : 64;
-  }();
+  static const int bm_max = svae_knob("SVAE_KW_BM", 64);  // (bf16 instances; the split ones: split_bm_max())
   for (int bm : {128, 64, 32}) {
-    if (bm > bm_max) continue;
+    if (bm > (a.nsp > 1 ? split_bm_max() : bm_max)) continue;
     if (bm % Wr != 0 || a.rows % bm != 0) continue;
     if (!(per_img % bm == 0 || bm % per_img == 0)) continue;
     KwArgs h;
@@ -657,8 +731,8 @@ static bool kw_plan(const FwdArgs& a, int groups, KwArgs* out, int* bm_out, int*
     *bm_out = bm;
     *bn_out = bn;
     // NS = 1: two window buffers; NS = 3 (split planes): one buffer of three planes
-    const int wbufs = a.nsp > 1 ? 3 : 2;
-    if (a.nsp > 1 && (a.a_bf16 || bm > 64 || bm > split_bm_max())) continue;  // split instances: fp32 A, 32 / 64-row tiles
+    const int wbufs = a.nsp > 1 ? (a.h16 ? 2 : 3) : 2;  // (h16: one buffer of two fp16 planes)
+    if (a.nsp > 1 && (a.a_bf16 || bm > split_bm_max())) continue;  // split instances: fp32 A
     *lds_out = std::max((size_t)(wbufs * h.npix) * KW_ROWP * sizeof(__bf16), (size_t)4 * bm * bn * sizeof(float));
     return true;
   }
@@ -666,10 +740,7 @@ static bool kw_plan(const FwdArgs& a, int groups, KwArgs* out, int* bm_out, int*
 }
 
 static bool kw_disabled() {
-  static const bool v = [] {
-    const char* e = getenv("SVAE_NO_KW");
-    return e && e[0] == '1';
-  }();
+  static const bool v = svae_knob("SVAE_NO_KW", 0) == 1;
   return v;
 }
 
@@ -698,16 +769,14 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
   h.ntz = (int)grid.z;
   h.tpb = 1;
   h.ain_off = 0;
+  h.slot_off = 0;
   if (a.ain.acc) {  // the consumer-side BN table [3][Cin] after the window / reduction region
     if (a.Cin % 8) return -1;
     h.ain_off = (int)((lds + 15) / 16 * 16);
     lds = (size_t)h.ain_off + 3 * (size_t)a.Cin * sizeof(float);
   }
   {  // SVAE_KW_VEC=1: the 16-byte epilogue where every row of C (and of the BN-backward operands) is aligned
-    static const int vec_mode = [] {
-      const char* e = getenv("SVAE_KW_VEC");
-      return e ? atoi(e) : 0;
-    }();
+    static const int vec_mode = svae_knob("SVAE_KW_VEC", 0);
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     // bf16-stored pre (written, or read by the fused backward-BN terms): always the 8-byte vector form
     const bool pbf = a.c_bf16 || (a.bw.pre && a.bw.pre_bf16);
@@ -721,10 +790,7 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
   // persistent form (SVAE_KW_PERSIST=1): where the tiles exceed the resident blocks, each block runs
   // a contiguous run of tiles with the next tile's window / B loads under the current tile's last
   // chunk and epilogue
-  static const int persist = [] {
-    const char* e = getenv("SVAE_KW_PERSIST");
-    return e ? atoi(e) : 0;
-  }();
+  static const int persist = svae_knob("SVAE_KW_PERSIST", 0);
   if (persist && a.nsp <= 1 && a.a_bf16 && bn == 32 && bm == 64 && !a.ain.acc) {  // the persistent instances
     const int occ_w = 2;
     const int occ_l = (int)std::max<size_t>(1, (size_t)163840 / std::max<size_t>(lds, 1));
@@ -738,10 +804,39 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
   // SVAE_KW_BRING: the two-tap B register ring on the 16-tap instances (bit 0: split mode, bit 1: bf16).
   // Default 1: the split instances go from 2 to 3 waves per SIMD (bf16x6 step 18.74 -> 18.08 ms,
   // profiles/r04_ab1.txt); the bf16 ones would need a fifth wave and spill (8 % slower)
-  static const int bring = [] {
-    const char* e = getenv("SVAE_KW_BRING");
-    return e ? atoi(e) : 1;
-  }();
+  static const int bring = svae_knob("SVAE_KW_BRING", 1);
+  if (a.nsp > 1 && a.h16) {  // split mode, scaled fp16 planes (opload.h split8_h16 / mfma_h16): 3 MFMAs per pair
+    static bool attr = false;
+    if (!attr) {
+      for (const void* f : {(const void*)igemm_halo_kw_kernel<64, 32, true, false, 2>,
+                            (const void*)igemm_halo_kw_kernel<32, 32, true, false, 2>,
+                            (const void*)igemm_halo_kw_kernel<128, 32, true, false, 2>,
+                            (const void*)igemm_halo_kw_kernel<64, 32, false, false, 2, false, true, 3>,
+                            (const void*)igemm_halo_kw_kernel<32, 32, false, false, 2, false, true, 3>,
+                            (const void*)igemm_halo_kw_kernel<64, 32, false, false, 2, false, true>,
+                            (const void*)igemm_halo_kw_kernel<32, 32, false, false, 2, false, true>,
+                            (const void*)igemm_halo_kw_kernel<128, 32, false, false, 2, false, true>})
+        hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 98304);
+      attr = true;
+    }
+    h.f.Bh = (const __bf16*)a.Bh + 3 * a.b_plane;  // the fp16 planes
+    h.slot_off = (int)((lds + 15) / 16 * 16);
+    lds = (size_t)h.slot_off + 8 * sizeof(float);
+    const bool pi3 = h.npix * 4 <= 256 * 3;
+    if (bm == 128) {
+      if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<128, 32, true, false, 2>), grid, dim3(256), lds, s, h);
+      else hipLaunchKernelGGL((igemm_halo_kw_kernel<128, 32, false, false, 2, false, true>), grid, dim3(256), lds, s, h);
+    } else if (bm == 64) {
+      if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, true, false, 2>), grid, dim3(256), lds, s, h);
+      else if (pi3) hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, false, false, 2, false, true, 3>), grid, dim3(256), lds, s, h);
+      else hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, false, false, 2, false, true>), grid, dim3(256), lds, s, h);
+    } else {
+      if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<32, 32, true, false, 2>), grid, dim3(256), lds, s, h);
+      else if (pi3) hipLaunchKernelGGL((igemm_halo_kw_kernel<32, 32, false, false, 2, false, true, 3>), grid, dim3(256), lds, s, h);
+      else hipLaunchKernelGGL((igemm_halo_kw_kernel<32, 32, false, false, 2, false, true>), grid, dim3(256), lds, s, h);
+    }
+    return a.nclass * (a.rows / bm);
+  }
   if (a.nsp > 1) {  // split-bf16 planes (fp32 A): 64 / 32-row tiles, 32 columns
     static bool attr = false;
     if (!attr) {
@@ -752,7 +847,9 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
                             (const void*)igemm_halo_kw_kernel<64, 32, false, false, 3, false, true>,
                             (const void*)igemm_halo_kw_kernel<32, 32, false, false, 3, false, true>,
                             (const void*)igemm_halo_kw_kernel<64, 32, false, false, 3, false, true, 3>,
-                            (const void*)igemm_halo_kw_kernel<32, 32, false, false, 3, false, true, 3>})
+                            (const void*)igemm_halo_kw_kernel<32, 32, false, false, 3, false, true, 3>,
+                            (const void*)igemm_halo_kw_kernel<128, 32, true, false, 3>,
+                            (const void*)igemm_halo_kw_kernel<128, 32, false, false, 3, false, true>})
         hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 98304);
       attr = true;
     }
@@ -760,10 +857,7 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
     const bool pi3 = h.npix * 4 <= 256 * 3 && split_pi3();
     // SVAE_KW_PERSIST_SPLIT=k: the 64-row split ring instances persistent over 256 x 3 x k blocks (the
     // next tile's window and first B fragments load under the current tile's last chunk)
-    static const int persist_split = [] {
-      const char* e = getenv("SVAE_KW_PERSIST_SPLIT");
-      return e ? atoi(e) : 0;
-    }();
+    static const int persist_split = svae_knob("SVAE_KW_PERSIST_SPLIT", 0);
     if (persist_split && br && pi3 && bm == 64 && !s2t && !a.ain.acc) {
       const long long slots = 256LL * 3 * persist_split;
       const long long ntiles = (long long)h.ntx * h.nty * h.ntz;
@@ -780,7 +874,10 @@ int halo_kw(const FwdArgs& a, int groups, hipStream_t s) {
         return a.nclass * (a.rows / bm);
       }
     }
-    if (bm == 64) {
+    if (bm == 128) {  // 128-row tiles: each B fragment serves four row fragments
+      if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<128, 32, true, false, 3>), grid, dim3(256), lds, s, h);
+      else hipLaunchKernelGGL((igemm_halo_kw_kernel<128, 32, false, false, 3, false, true>), grid, dim3(256), lds, s, h);
+    } else if (bm == 64) {
       if (s2t) hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, true, false, 3>), grid, dim3(256), lds, s, h);
       else if (br && pi3) hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, false, false, 3, false, true, 3>), grid, dim3(256), lds, s, h);
       else if (br) hipLaunchKernelGGL((igemm_halo_kw_kernel<64, 32, false, false, 3, false, true>), grid, dim3(256), lds, s, h);

@@ -51,6 +51,9 @@ struct FwdArgs {
   // split-bf16 mode (dtype = bf16x6, opload.h split8): A and B as nsp bf16 planes each (1 = plain
   // bf16); B plane p at Bh + p * b_plane elements.  Only kernels that implement it accept nsp > 1
   int nsp; long long b_plane;
+  // split mode: B also holds two scaled fp16 planes (w * 2^H16_WS, opload.h) at planes 3 and 4; the
+  // wave-split halo gather then runs the three-product fp16 form (halo_kw NS = 2)
+  int h16;
   AinBN ain;    // consumer-side BN of A (halo_kw only)
   // forward BN producers (bf16 mode): store C as bf16, the statistics taken from the rounded values;
   // only with stats, no bias / act / accumulate / bw (igemm_c_bf16_ok)

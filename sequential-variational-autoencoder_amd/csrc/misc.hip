@@ -5,6 +5,7 @@
 #include <cstdint>
 
 #include "common.h"
+#include "knobs.h"
 #include "kernels.h"
 
 #define KMAX 32  // max latent dims per level handled in registers (LSUN: 30)
@@ -370,10 +371,7 @@ __global__ __launch_bounds__(256) void heads_fwd_kernel(const float* __restrict_
 int heads_splits(int K) { return (K + HF_CHUNK - 1) / HF_CHUNK; }
 
 static bool heads_narrow_off() {  // SVAE_HEADS_SKINNY=1: the former 4-row skinny pass (A/B)
-  static const bool v = [] {
-    const char* e = getenv("SVAE_HEADS_SKINNY");
-    return e && e[0] == '1';
-  }();
+  static const bool v = svae_knob("SVAE_HEADS_SKINNY", 0) == 1;
   return v;
 }
 
@@ -469,8 +467,8 @@ void heads_fwd(const float* X, long long x_gs, int B, int K, const float* Wm, co
 #undef HF_L
     return;
   }
-  const char* te = getenv("SVAE_HEADS_TILE");  // bit 0 off: the skinny pass for the wide heads (A/B; read per call)
-  const bool tile_off = te && !(atoi(te) & 1);
+  // SVAE_HEADS_TILE bit 0 off: the skinny pass for the wide heads (knob builds read it per call: the A/B tests)
+  const bool tile_off = !(svae_knob("SVAE_HEADS_TILE", 3) & 1);
   if (D > 4 && D <= 32 && !tile_off) {
     dim3 grid((B + 63) / 64, heads_splits(K), groups);
     hipLaunchKernelGGL(heads_tile_fwd_kernel, grid, dim3(256), 0, s, X, x_gs, B, K, Wm, Ws, w_gs, D, part, part_gs, pcols,
@@ -505,9 +503,9 @@ void splitfc_dz_reduce(const float* dz_part, int nblk, int B, int K, float* dz, 
 // one thread per (image, latent dimension): the 2 x nsplit head partials of a dimension load
 // together, 32 splits at a time (summed in split order for any nsplit), and each image's KL terms
 // are added in dimension order from LDS (the order of the former one-thread-per-image loop: bitwise
-// the same mu, sigma, z and KL).  Blocks of 256 threads hold 256 / Dz images; Dz > 256 takes one
-// image per block of Dz rounded up to 64 threads.
-__global__ __launch_bounds__(1024) void latent_fwd_kernel(const float* __restrict__ part, long long part_gs,
+// the same mu, sigma, z and KL).  Blocks of 256 threads hold 256 / Dz images (Dz <= 256: make_geo caps
+// the latent at 8 levels x 32 dimensions and svae_create rejects more).
+__global__ __launch_bounds__(256) void latent_fwd_kernel(const float* __restrict__ part, long long part_gs,
                                                           int nsplit, int B, int Dz, LatentLvls lv, long long bias_gs,
                                                           float clipv, float prior, int uniform,
                                                           const float* __restrict__ eps, long long eps_gs,
@@ -564,7 +562,7 @@ __global__ __launch_bounds__(1024) void latent_fwd_kernel(const float* __restric
 void latent_fwd(const float* part, long long part_gs, int nsplit, int B, int Dz, const LatentLvls& lv,
                 long long bias_gs, float clipv, float prior, int uniform, const float* eps, long long eps_gs, float* mu,
                 float* sig, float* z, long long ms_gs, float* kl_img, long long kl_gs, int groups, hipStream_t s) {
-  const int bs = Dz <= 256 ? 256 : (Dz + 63) / 64 * 64;  // (svae_create rejects Dz > 1024)
+  const int bs = 256;  // (svae_create rejects Dz > 256)
   const int ipb = bs / Dz;
   hipLaunchKernelGGL(latent_fwd_kernel, dim3((B + ipb - 1) / ipb, groups), dim3(bs), 0, s, part, part_gs, nsplit, B, Dz,
                      lv, bias_gs, clipv, prior, uniform, eps, eps_gs, mu, sig, z, ms_gs, kl_img, kl_gs);
@@ -867,16 +865,16 @@ __global__ __launch_bounds__(256) void heads_tile_bwd_kernel(const float* __rest
 void heads_bwd(const float* X, long long x_gs, float* dX, long long dx_gs, int B, int K, const float* Wm,
                const float* Ws, long long w_gs, int D, const float* dhead, long long dh_gs, int dcols, int coff,
                float* dWm, float* dWs, float* dbm, float* dbs, int accumulate, int groups, hipStream_t s) {
-  const char* te = getenv("SVAE_HEADS_TILE");  // bit 1 off: heads_bwd_kernel<32> for the wide heads (A/B; per call)
-  const bool tile_off = te && !(atoi(te) & 2);
+  // SVAE_HEADS_TILE bit 1 off: heads_bwd_kernel<32> for the wide heads (knob builds: per call)
+  const bool tile_off = !(svae_knob("SVAE_HEADS_TILE", 3) & 2);
   if (D > 8 && D <= 32 && !tile_off) {
     dim3 grid((K + 63) / 64, groups);
     hipLaunchKernelGGL(heads_tile_bwd_kernel, grid, dim3(256), 0, s, X, x_gs, dX, dx_gs, B, K, Wm, Ws, w_gs, D, dhead,
                        dh_gs, dcols, coff, dWm, dWs, dbm, dbs, accumulate);
     return;
   }
-  const char* rge = getenv("SVAE_HEADS_RG");  // =0: one thread per k over all rows (round 3); read per call (A/B tests)
-  const bool rg_on = !(rge && rge[0] == '0');
+  // SVAE_HEADS_RG=0: one thread per k over all rows (round 3; knob builds: per call)
+  const bool rg_on = svae_knob("SVAE_HEADS_RG", 1) != 0;
   if (rg_on && B % (HR_RG * 8) == 0 && D <= 8) {
     dim3 grid((K + 63) / 64, groups);
     size_t lds = (size_t)B * 2 * D * sizeof(float) + (size_t)2 * 8 * HR_RG * 64 * sizeof(float);
@@ -1320,6 +1318,7 @@ __device__ __forceinline__ void adam1(float& w, float g, float& m, float& v, flo
 // 16-B vectors (w/g/m/v 16-B aligned: ranges start on a multiple of 4 elements); wn != nullptr
 // also writes the bf16 copy of the updated weights (the GEMMs' N-layout shadow, shadow_n_kernel's
 // rounding), which saves the next forward's separate conversion pass over the live region
+typedef _Float16 ol4h __attribute__((ext_vector_type(4)));
 __global__ void adam_kernel(float* w, const float* g, float* m, float* v, __bf16* wn, long long n, float lr_t, float b1,
                             float b2, float eps, float clipv, int nsp, long long plane) {
   const long long stride = (long long)gridDim.x * blockDim.x;
@@ -1338,7 +1337,13 @@ __global__ void adam_kernel(float* w, const float* g, float* m, float* v, __bf16
     ((f32x4*)m)[q] = mm;
     ((f32x4*)v)[q] = vv;
     ((f32x4*)w)[q] = ww;
-    if (wn) {  // the bf16 N-layout copy (split mode: nsp planes, opload.h split4)
+    if (wn) {  // the bf16 N-layout copy (split mode: nsp planes, opload.h split4; and the fp16 planes)
+      if (nsp == 3) {
+        _Float16 h0[4], h1[4];
+        for (int e = 0; e < 4; ++e) h16_pair(ww[e], h0[e], h1[e]);
+        *(ol4h*)((_Float16*)wn + H16_PLANE * plane + 4 * q) = ol4h{h0[0], h0[1], h0[2], h0[3]};
+        *(ol4h*)((_Float16*)wn + (H16_PLANE + 1) * plane + 4 * q) = ol4h{h1[0], h1[1], h1[2], h1[3]};
+      }
       for (int p = 0; p < nsp; ++p) {
         const bf16x4_t h = __builtin_convertvector(ww, bf16x4_t);
         *(bf16x4_t*)(wn + p * plane + 4 * q) = h;
@@ -1350,6 +1355,7 @@ __global__ void adam_kernel(float* w, const float* g, float* m, float* v, __bf16
     adam1(w[i], g[i], m[i], v[i], lr_t, b1, b2, eps, clipv);
     if (wn) {
       float x = w[i];
+      if (nsp == 3) h16_pair(x, ((_Float16*)wn)[H16_PLANE * plane + i], ((_Float16*)wn)[(H16_PLANE + 1) * plane + i]);
       for (int p = 0; p < nsp; ++p) {
         const __bf16 h = (__bf16)x;
         wn[p * plane + i] = h;

@@ -109,3 +109,42 @@ __device__ __forceinline__ f32x16 mfma_split(const ol_bf16x8 (&a)[NS], const ol_
   }
   return acc;
 }
+
+// ---- scaled fp16 hi/lo operands (the split mode's gathers, halo_kw NS = 2) ----
+// x' = x * 2^s (exact), h0 = fp16(x'), h1 = fp16(x' - h0) (the residual is exact in fp32): 22-23 bits of
+// x for |x'| >= 2^-3, an absolute error <= 2^-25 * 2^-s below (subnormal h1).  A product is summed as
+// a0 b0 + a0 b1 + a1 b0 (3 fp16 MFMAs: each fp16 x fp16 product is exact in fp32; the dropped a1 b1 is
+// <= 2^-22 |ab|), fp32 accumulation.  Activations take a block-wide running exponent per window chunk
+// (max |x| * 2^s in [2^14, 2^15)), weights the fixed H16_WS below.  CPU emulation of the whole CelebA
+// T=8 step: x_hat_t error vs float64 below the fp32 twin's at every t.
+typedef _Float16 ol_f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 ol_f16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void split8_h16(f32x4 lo, f32x4 hi, int s, ol_bf16x8 (&p)[2]) {
+  ol_f32x8 v = {__builtin_ldexpf(lo[0], s), __builtin_ldexpf(lo[1], s), __builtin_ldexpf(lo[2], s),
+                __builtin_ldexpf(lo[3], s), __builtin_ldexpf(hi[0], s), __builtin_ldexpf(hi[1], s),
+                __builtin_ldexpf(hi[2], s), __builtin_ldexpf(hi[3], s)};
+  const ol_f16x8 h0 = __builtin_convertvector(v, ol_f16x8);
+  v = v - __builtin_convertvector(h0, ol_f32x8);
+  const ol_f16x8 h1 = __builtin_convertvector(v, ol_f16x8);
+  p[0] = __builtin_bit_cast(ol_bf16x8, h0);
+  p[1] = __builtin_bit_cast(ol_bf16x8, h1);
+}
+__device__ __forceinline__ void split4_h16(f32x4 x, int s, ol_f16x4 (&p)[2]) {
+  const f32x4 v = {__builtin_ldexpf(x[0], s), __builtin_ldexpf(x[1], s), __builtin_ldexpf(x[2], s),
+                   __builtin_ldexpf(x[3], s)};
+  p[0] = __builtin_convertvector(v, ol_f16x4);
+  p[1] = __builtin_convertvector(v - __builtin_convertvector(p[0], f32x4), ol_f16x4);
+}
+__device__ __forceinline__ f32x16 mfma_h16(const ol_bf16x8 (&a)[2], const ol_bf16x8 (&b)[2], f32x16 acc) {
+  const ol_f16x8 a0 = __builtin_bit_cast(ol_f16x8, a[0]), a1 = __builtin_bit_cast(ol_f16x8, a[1]);
+  const ol_f16x8 b0 = __builtin_bit_cast(ol_f16x8, b[0]), b1 = __builtin_bit_cast(ol_f16x8, b[1]);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, acc, 0, 0, 0);
+  return acc;
+}
+// exponent s with max * 2^s in [2^14, 2^15) for a non-negative finite max (0: s = 0)
+__device__ __forceinline__ int h16_exp(float mx) {
+  const int e = (int)((__float_as_uint(mx) >> 23) & 0xff);
+  return mx > 0.f ? 14 - (e - 127) : 0;
+}

@@ -9,6 +9,7 @@
 #include <string>
 
 #include "common.h"
+#include "knobs.h"
 #include "kernels.h"
 #include "svae_hip.h"
 #include "svae_pcnn.h"
@@ -1842,14 +1843,8 @@ static int pcnn_conv_impl(const void* x, int n, int hi, int wi, int cin, int ldx
   hipStream_t st = (hipStream_t)stream;
   const __bf16* w = (const __bf16*)wk;
   const unsigned gx = (unsigned)((rows + 127) / 128);
-  static const bool old = [] {
-    const char* v = getenv("SVAE_PC_CONV1");
-    return v && v[0] == '1';
-  }();
-  static const int pc3 = [] {  // SVAE_PC3: 0 = stride-1 convs on pc_conv2 too; 1 / 2 = halo kernel, TM
-    const char* v = getenv("SVAE_PC3");
-    return v ? atoi(v) : 1;
-  }();
+  static const bool old = svae_knob("SVAE_PC_CONV1", 0) == 1;
+  static const int pc3 = svae_knob("SVAE_PC3", 1);  // 0 = stride-1 convs on pc_conv2 too; 1 / 2 = halo kernel, TM
   if (kpad % 32 == 0 && !old) {  // LDS-staged kernels, up to 160 output channels per block
     const int n32 = (cout + 31) / 32;
     int tiles = (n32 + 4) / 5;
@@ -1860,10 +1855,7 @@ static int pcnn_conv_impl(const void* x, int n, int hi, int wi, int cin, int ldx
       // widest column tile (32 x NT): 64 columns for the forward convs (bf16 input, mode 0), 160 for the
       // input gradients (tools/bench_pcconv.py, B = 128: mode 0 0-30 % faster at NT = 2 against NT = 5,
       // mode 1 up to 55 % slower; NT = 3 slower for both); SVAE_PC3_NT overrides
-      static const int nt_env = [] {
-        const char* v = getenv("SVAE_PC3_NT");
-        return v ? atoi(v) : 0;
-      }();
+      static const int nt_env = svae_knob("SVAE_PC3_NT", 0);
       const int nt_max = nt_env > 0 ? nt_env : (x_bf16 && mode == 0 ? 2 : 5);
       if (nt_max < NT) {
         tiles = (n32 + nt_max - 1) / nt_max;
@@ -1919,10 +1911,7 @@ int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx,
   const int taps = kh * kw;
   const long long wsz = (long long)taps * cin * cout;
   hipStream_t st = (hipStream_t)stream;
-  static const int pw4 = [] {  // SVAE_PW4=0: every weight gradient on the one-tap kernel
-    const char* v = getenv("SVAE_PW4");
-    return v ? atoi(v) : 1;
-  }();
+  static const int pw4 = svae_knob("SVAE_PW4", 1);  // 0: every weight gradient on the one-tap kernel
   {
     PcGeom g4 = g;
     if (kh == 1 && kw == 1 && pt == 0 && pl == 0 && s == 1 && rows % 256 == 0) {  // 1x1: 16-wide images
@@ -1932,10 +1921,7 @@ int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx,
     Pw4 h;
     if (pw4 && pw4_plan(g4, rows, &h)) {
       const long long tiles4 = (long long)((cin + 63) / 64) * ((cout + 63) / 64) * kh;
-      static const int tgt4 = [] {  // SVAE_PW4_TARGET: blocks of the tap-row kernel (default 1024)
-        const char* v = getenv("SVAE_PW4_TARGET");
-        return v ? atoi(v) : 1024;
-      }();
+      static const int tgt4 = svae_knob("SVAE_PW4_TARGET", 1024);  // blocks of the tap-row kernel
       long long ns = (tgt4 + tiles4 - 1) / tiles4;
       if (ns > h.nchunk) ns = h.nchunk;
       if (ns > scratch_elems / (wsz + cout)) ns = scratch_elems / (wsz + cout);
@@ -1957,10 +1943,7 @@ int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx,
   }
   const int tiles = ((cin + 63) / 64) * ((cout + 63) / 64);
   // splits: ~2048 blocks, >= 256 rows (8 chunks) per split, bounded by the scratch slabs
-  static const int tgt1 = [] {  // SVAE_PW_TARGET: blocks of the one-tap kernel (default 2048)
-    const char* v = getenv("SVAE_PW_TARGET");
-    return v ? atoi(v) : 2048;
-  }();
+  static const int tgt1 = svae_knob("SVAE_PW_TARGET", 2048);  // blocks of the one-tap kernel
   long long ns = (tgt1 + (long long)tiles * taps - 1) / ((long long)tiles * taps);
   const long long max_rows = (rows + 255) / 256;
   if (ns > max_rows) ns = max_rows;

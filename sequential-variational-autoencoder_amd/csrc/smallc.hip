@@ -25,6 +25,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "knobs.h"
 #include "kernels.h"
 #include "opload.h"
 
@@ -481,10 +482,7 @@ bool smallc_ok(const FwdArgs& a, bool bf) {
 int smallc_nrb(const FwdArgs& a) { return a.rows / SC_BM; }
 
 bool smallc_disabled() {
-  static const int off = [] {
-    const char* e = getenv("SVAE_NO_SMALLC");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
+  static const int off = svae_knob("SVAE_NO_SMALLC", 0) == 1;
   return off != 0;
 }
 

@@ -22,6 +22,7 @@
 // Window pitch 64 B (32 G channels) and the D row XOR swizzle (WN = 2) keep the
 // ds_read_b64_tr_b16 reads conflict-free (same layouts as gemm_bf16.hip's halo weight-GEMM).
 #include "common.h"
+#include "knobs.h"
 #include "kernels.h"
 #include "opload.h"
 
@@ -330,10 +331,7 @@ void wh2_launch(const WH2Args& a, int groups, hipStream_t s) {
   }
 }
 
-int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return (v && *v) ? atoi(v) : dflt;
-}
+int env_int(const char* name, int dflt) { return svae_knob(name, dflt); }
 
 }  // namespace
 

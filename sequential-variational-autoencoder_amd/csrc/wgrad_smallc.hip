@@ -25,6 +25,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "knobs.h"
 #include "kernels.h"
 #include "opload.h"
 
@@ -246,10 +247,7 @@ __global__ __launch_bounds__(256) void wgrad_smallc_kernel(SCArgs a) {
 }  // namespace
 
 int wgrad_smallc_disabled() {
-  static const int v = [] {
-    const char* e = getenv("SVAE_NO_WSC");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
+  static const int v = svae_knob("SVAE_NO_WSC", 0) == 1;
   return v;
 }
 

@@ -35,3 +35,12 @@ def built_lib():
 def gpu_available():
     import torch
     return torch.cuda.is_available()
+
+
+@pytest.fixture
+def knob_lib():
+    """Networks created inside the test use the -DSVAE_KNOBS build (libsvae_hip_knobs.so), which reads
+    the A/B switches of csrc/knobs.h (SVAE_*) that the shipping library compiles to their defaults."""
+    L = pkg_mod("_lib")
+    with L.knob_build() as lib:
+        yield lib

@@ -87,7 +87,7 @@ def test_rebind_after_external_write_rebuilds_weight_copies():
 ])
 @pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("rec_group", ["0", "1"])
-def test_batched_side_handover_is_bitwise(preset, dtype, over, fused, rec_group, monkeypatch):
+def test_batched_side_handover_is_bitwise(preset, dtype, over, fused, rec_group, monkeypatch, knob_lib):
     """SVAE_SIDE_BATCH = k queues the weight-gradient work of k layers behind one main-stream
     event (engine.cpp on_side_q / side_flush): the same kernels on the same data, so losses and
     parameters after three steps equal the per-layer hand-over bit for bit (the per-bucket Adam
@@ -128,7 +128,7 @@ def _fwd_bwd(preset, dtype, over):
     ("tiny_homog", "bf16", {}),
 ])
 @pytest.mark.parametrize("knob", ["SVAE_REC_SPLIT", "SVAE_REC_GROUP"])
-def test_forward_recognition_split_matches(preset, dtype, over, knob, monkeypatch):
+def test_forward_recognition_split_matches(preset, dtype, over, knob, monkeypatch, knob_lib):
     """SVAE_REC_SPLIT=1 runs step 0's recognition ladder on the main stream and the batched ladders of
     steps 1..T-1 on a fourth stream beside the chain's step 0 (engine.cpp engine_forward).  The same
     per-step kernels run on the same data; only launch shapes that depend on the group count
@@ -155,7 +155,7 @@ def test_forward_recognition_split_matches(preset, dtype, over, knob, monkeypatc
 
 
 @pytest.mark.parametrize("preset", ["tiny", "celeba"])
-def test_fc_bn_backward_fusion_is_bitwise(preset, monkeypatch):
+def test_fc_bn_backward_fusion_is_bitwise(preset, monkeypatch, knob_lib):
     """bf16 default: E.fc's BN-backward sums are formed in the top FC's split-K input gradient
     (engine.cpp fc_bn_bwd, splitk_reduce BwStat columns) instead of a bn_bwd_reduce pass.  The sums
     are fixed-point accumulated (order-free), so three training steps must equal the unfused path
@@ -172,7 +172,7 @@ def test_fc_bn_backward_fusion_is_bitwise(preset, monkeypatch):
 @pytest.mark.parametrize("preset,dtype", [("tiny", "bf16"), ("celeba", "bf16"), ("tiny", "bf16x6"), ("celeba", "bf16x6"),
                                           ("tiny_homog", "bf16")])
 @pytest.mark.parametrize("fused", [False, True])
-def test_second_side_stream_is_bitwise(preset, dtype, fused, monkeypatch):
+def test_second_side_stream_is_bitwise(preset, dtype, fused, monkeypatch, knob_lib):
     """SVAE_SIDE2=1 alternates the conv weight-GEMMs between two side streams (own split slab each;
     engine.cpp side_merge orders the per-bucket Adam, the DP hook and the final join after both):
     the same kernels on the same data, so three training steps equal the one-stream run bit for bit."""
@@ -191,7 +191,7 @@ def test_second_side_stream_is_bitwise(preset, dtype, fused, monkeypatch):
 ])
 @pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("pre_f32", ["0", "1"])
-def test_forward_bn_fold_is_bitwise(preset, dtype, over, fused, pre_f32, monkeypatch):
+def test_forward_bn_fold_is_bitwise(preset, dtype, over, fused, pre_f32, monkeypatch, knob_lib):
     """SVAE_FOLD=1: the forward BN apply of the recognition / encoder conv-a and decoder s1 (level >= 1)
     outputs runs on the side stream, and the next layer's wave-split gather stages act(bn_y(pre)) from
     the pre-BN tensor itself with the statistics finalised as bn_apply does (engine.cpp
@@ -214,7 +214,7 @@ def test_forward_bn_fold_is_bitwise(preset, dtype, over, fused, pre_f32, monkeyp
     ("tiny", "bf16", 4), ("celeba", "bf16", 128), ("celeba", "bf16x6", 128), ("tiny_homog", "bf16", 4),
 ])
 @pytest.mark.parametrize("fused", [False, True])
-def test_bn_last_arriver_finalisation_is_bitwise(preset, dtype, batch, fused, monkeypatch):
+def test_bn_last_arriver_finalisation_is_bitwise(preset, dtype, batch, fused, monkeypatch, knob_lib):
     """SVAE_BN_LAF: the last block of each halo_kw BN producer turns the fixed-point accumulators into
     mean / invstd (forward) or the backward sums a, b and dbeta (common.h bn_fin_arrive) with the apply
     passes' own expressions, ordered by device-scope atomics alone.  Three training steps at the headline
@@ -234,7 +234,7 @@ def test_bn_last_arriver_finalisation_is_bitwise(preset, dtype, batch, fused, mo
     ("tiny", "bf16", 4, {"predict_latent_code": True}),
 ])
 @pytest.mark.parametrize("fused", [False, True])
-def test_bf16_concat_storage_is_bitwise(preset, dtype, batch, over, fused, monkeypatch):
+def test_bf16_concat_storage_is_bitwise(preset, dtype, batch, over, fused, monkeypatch, knob_lib):
     """bf16 mode stores the decoder concat buffers [s2 output | split latent] as bf16 (engine.cpp cbf):
     their readers round them to bf16 anyway (the s1 gather and weight-GEMM) or use only the sign of the
     s2 output (act' in its BN backward), so three training steps are bitwise the fp32-stored ones

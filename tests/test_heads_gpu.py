@@ -28,7 +28,7 @@ def _grads(monkeypatch, rg):
     return out
 
 
-def test_heads_row_groups_match(monkeypatch):
+def test_heads_row_groups_match(monkeypatch, knob_lib):
     g0 = _grads(monkeypatch, "0")
     g1 = _grads(monkeypatch, "1")
     differing = []
@@ -63,7 +63,7 @@ def _lsun(monkeypatch, tile):
     return mus, out
 
 
-def test_wide_heads_tiles_match(monkeypatch):
+def test_wide_heads_tiles_match(monkeypatch, knob_lib):
     """LSUN (B = 256, 20-30 latents per level), one chain step, fp32: the tiled wide-heads forward
     (misc.hip heads_tile_fwd_kernel) against the skinny forward (SVAE_HEADS_TILE=2 vs 3): latent means /
     stddevs within 1e-5; the tiled backward (heads_tile_bwd_kernel) against the one-k-per-thread kernel
