@@ -366,7 +366,7 @@ def _spawn_ranks(n):
     return subprocess.call(cmd)
 
 
-def main():
+def make_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -393,7 +393,24 @@ def main():
                     help="dominant-kernel launches timed with HIP event pairs inside the timed region (the first N; "
                          "0 = every launch). Each pair is two event records on the kernel's stream, so timing all "
                          "~1000 launches of a 20-step run costs the step itself ~2 %%")
-    args = ap.parse_args()
+    return ap
+
+
+def init_distributed(args, world, local):
+    """The N>1 process group: RCCL (backend "nccl", one rank per GPU) unless --dist-backend gloo;
+    returns torch.distributed, or None at N=1."""
+    if world <= 1:
+        return None
+    import torch.distributed as dist
+    if args.dist_backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group("gloo")
+    return dist
+
+
+def main():
+    args = make_parser().parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(_spawn_ranks(args.gpus))
@@ -410,13 +427,7 @@ def main():
     torch.cuda.set_device(local)
     if os.environ.get("SVAE_BENCH_STREAM") == "1":  # A/B: run on a non-default torch stream
         torch.cuda.set_stream(torch.cuda.Stream(local))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group("gloo")
+    dist = init_distributed(args, world, local)
 
     cfgmod = importlib.import_module(PKG + ".config")
     if args.config == "c_pixelvae":
