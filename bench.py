@@ -31,6 +31,8 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no 2:1 s
 # stream, the critical path; csrc/halo_kw.hip).  The stride-1 halo weight-GEMM (side stream,
 # wgrad_halo2_kernel) is reported as the secondary entry.
 DOMINANT_KID = "KID_HALO_KW"
+# the parity-grade (bf16x6) step's dominant kernel: the fp16-plane wave-split gather (csrc/halo_x3.hip)
+DOMINANT_KID_SPLIT = "KID_HALO_X3"
 SECONDARY_KID = "KID_WHALO2_S1"
 # PMC summaries (tools/pmc_traffic.py: FETCH_SIZE / WRITE_SIZE passes of the same bench command, calibrated
 # FETCH rules) per workload; a workload never borrows another's traffic (LSUN read CelebA's)
@@ -461,7 +463,7 @@ def main():
         net.forward(x, tgt, None, reg)
         net.backward_apply(cfg.learning_rate, it)  # backward + clip/Adam per chain-step bucket
 
-    probe_kid = getattr(L, DOMINANT_KID) if args.dtype in ("bf16", "bf16x6") else None
+    probe_kid = getattr(L, DOMINANT_KID if args.dtype == "bf16" else DOMINANT_KID_SPLIT) if args.dtype in ("bf16", "bf16x6") else None
     it = 0
     for _ in range(args.warmup):
         it += 1
@@ -527,7 +529,7 @@ def main():
 
     roof = None
     cpu = None
-    nprod = 6 if args.dtype == "bf16x6" else 1  # MFMAs issued per useful one (split planes: six products)
+    nprod = 3 if args.dtype == "bf16x6" else 1  # MFMAs issued per useful one (fp16 hi/lo planes: three products)
     if rank == 0 and probe is not None and probe["timed"] > 0:
         # dominant kernel, timed live in the timed region: sum of per-launch algorithmic FLOPs
         # (2*taps*M*N*pixels) / sum of per-launch event durations
@@ -536,7 +538,7 @@ def main():
         traffic, tsrc = pmc_traffic(probe["kernel"], args.config + "/" + args.dtype)
         roof = dict(bound="mfma", achieved=round(ach, 3), peak=BF16_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
                     frac=round(ach / BF16_MFMA_PEAK_TFLOPS, 5), traffic=traffic,
-                    kernel=probe["kernel"] + (" (split planes: 6 bf16 MFMAs per fragment pair)" if nprod > 1 else ""),
+                    kernel=probe["kernel"] + (" (scaled fp16 hi/lo planes: 3 MFMAs per fragment pair)" if nprod > 1 else ""),
                     launches_per_step=probe["launches"] / args.steps,
                     avg_launch_us=round(avg_us, 2), timed_launches=probe["timed"],
                     flops_per_launch=round(probe["flops"] / probe["timed"]),
@@ -564,11 +566,11 @@ def main():
     if world == 1 and args.dtype in ("bf16", "bf16x6") and not args.no_fp32 and not args.no_secondary:
         net.close()
         alt_value, alt_ms, alt_probe = mode_throughput(cfg, SV, alt, steps=args.parity_steps,
-                                                       probe_kid=getattr(L, DOMINANT_KID),
+                                                       probe_kid=getattr(L, DOMINANT_KID if alt == "bf16" else DOMINANT_KID_SPLIT),
                                                        probe_launches=args.probe_launches or 96)
-        if alt_probe is not None:  # useful (algorithmic) and, for bf16x6, issued (6 products) MFMA rates
+        if alt_probe is not None:  # useful (algorithmic) and, for bf16x6, issued (3 products) MFMA rates
             use = alt_probe["flops"] / (alt_probe["ms"] / 1e3) / 1e12
-            k = 6 if alt == "bf16x6" else 1
+            k = 3 if alt == "bf16x6" else 1
             tr_a, tsrc_a = pmc_traffic(alt_probe["kernel"], args.config + "/" + alt)
             alt_roof = {"bound": "mfma", "kernel": alt_probe["kernel"],
                         "achieved": round(use, 3), "issued": round(k * use, 3), "peak": BF16_MFMA_PEAK_TFLOPS,

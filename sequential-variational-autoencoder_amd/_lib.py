@@ -200,6 +200,7 @@ KID_WHALO_32_S2 = 23
 KID_WHALO2_S1 = 26   # wgrad_halo2_kernel<...>: every instance of the stride-1 halo weight-GEMM
 KID_HALO_KW = 27     # igemm_halo_kw_kernel<...>: the wave-split gather-GEMM (main stream)
 KID_WHALO2_S2 = 28   # wgrad_halo2_kernel<..., S = 2>: the stride-2 instances
+KID_HALO_X3 = 29     # gather_x3_kernel<...>: the split mode's fp16-plane wave-split gather (main stream)
 
 
 def check(rc, ctx=None):

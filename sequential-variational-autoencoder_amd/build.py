@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 OUT = os.path.join(HERE, "libsvae_hip.so")
-SOURCES = ["gemm.hip", "gemm_bf16.hip", "wgrad_halo2.hip", "wgrad_smallc.hip", "smallc.hip", "bn.hip", "misc.hip", "chain.hip", "halo_kw.hip", "dense_kw.hip", "pcnn.hip", "engine.cpp"]
+SOURCES = ["gemm.hip", "gemm_bf16.hip", "wgrad_halo2.hip", "wgrad_smallc.hip", "smallc.hip", "bn.hip", "misc.hip", "chain.hip", "halo_kw.hip", "halo_x3.hip", "dense_kw.hip", "pcnn.hip", "engine.cpp"]
 HEADERS = ["common.h", "kernels.h", "knobs.h", "opload.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-mcode-object-version=5",

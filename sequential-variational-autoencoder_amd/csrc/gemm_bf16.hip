@@ -1472,7 +1472,8 @@ static int pertap_plan(const FwdArgs& a, int groups, int* ksplit) {
 }
 
 bool igemm_split_ok(const FwdArgs& a, int groups) {
-  return a.Bh && !a.a_bf16 && (dense_kw_ok(a, groups) || halo_kw_plan(a, groups) > 0 || smalln_ok(a));
+  return a.Bh && !a.a_bf16 &&
+         (dense_kw_ok(a, groups) || halo_x3_plan(a, groups) > 0 || halo_kw_plan(a, groups) > 0 || smalln_ok(a));
 }
 
 // bf16-stored pre-BN outputs (FwdArgs::c_bf16): every bf16 launch path of a BN-statistics GEMM implements
@@ -1503,6 +1504,8 @@ int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit) {
   if (a.nsp > 1) {  // split-bf16 planes: dense_kw, halo_kw or the small-N conv-T (igemm_split_ok)
     if (ksplit) *ksplit = 1;
     if (dense_kw_ok(a, groups)) return dense_kw_nrb(a);
+    const int nx3 = halo_x3_plan(a, groups);  // the fp16-plane gather (halo_x3.hip) first
+    if (nx3 > 0) return nx3;
     const int nrb = halo_kw_plan(a, groups);
     return nrb > 0 ? nrb : 0;  // (convt_smalln: no statistics)
   }
@@ -1549,13 +1552,18 @@ const char* kernel_name(int kid) {
       "wgrad_halo_kernel<32, 1>", "wgrad_halo_kernel<32, 2>", "wgrad_halo_kernel<64, 1>", "wgrad_halo_kernel<64, 2>",
       "wgrad_halo2_kernel (stride-1 halo weight-GEMM, all S = 1 instances)",
       "igemm_halo_kw_kernel (small-image gather-GEMM, K split over waves, all instances)",
-      "wgrad_halo2_kernel (stride-2 halo weight-GEMM, all instances)"};
+      "wgrad_halo2_kernel (stride-2 halo weight-GEMM, all instances)",
+      "gather_x3_kernel (split mode: fp16-plane wave-split gather, all instances)"};
   return (kid >= 0 && kid < KID_COUNT) ? names[kid] : "none";
 }
 
 int igemm_bf16_kid(const FwdArgs& a) {
   if (a.ain.acc) return halo_kw_plan(a, 1) > 0 ? KID_HALO_KW : KID_NONE;
-  if (a.nsp > 1) return (!dense_kw_ok(a, 1) && halo_kw_plan(a, 1) > 0) ? KID_HALO_KW : KID_NONE;
+  if (a.nsp > 1) {
+    if (dense_kw_ok(a, 1)) return KID_NONE;
+    if (halo_x3_plan(a, 1) > 0) return KID_HALO_X3;
+    return halo_kw_plan(a, 1) > 0 ? KID_HALO_KW : KID_NONE;
+  }
   if (!halo_disabled()) {
     const HaloPlan hp = halo_plan(a, 1);
     if (hp.ok) return (kw_first(a, hp) && halo_kw_plan(a, 1)) ? KID_HALO_KW : hp.kid;
@@ -1609,12 +1617,13 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
     return dense_kw_nrb(a);
   }
   if (a.nsp > 1) {  // igemm_split_ok: the wave-split halo gather takes every other split shape
-    if (halo_kw_plan(a, groups) <= 0 && smalln_ok(a)) {  // the N <= 16 stride-2 conv-T (output layer, layer-0 dgrad)
+    if (halo_x3_plan(a, groups) <= 0 && halo_kw_plan(a, groups) <= 0 && smalln_ok(a)) {  // the N <= 16 stride-2 conv-T (output layer, layer-0 dgrad)
       convt_smalln(a, groups, s);
       if (after) hipEventRecord(after, s);
       return 0;
     }
-    const int nrb = halo_kw(a, groups, s);
+    int nrb = halo_x3(a, groups, s);  // the fp16-plane gather (halo_x3.hip) where it fits
+    if (nrb < 0) nrb = halo_kw(a, groups, s);
     if (after) hipEventRecord(after, s);
     return nrb;
   }

@@ -441,6 +441,7 @@ void igemm_halo_kw_kernel(KwArgs h) {
     }
     __syncthreads();
   }
+  KW_STAMP(13);
   set_window(cur);
   load_window(cur, 0);
   if constexpr (BR) {
@@ -453,6 +454,7 @@ void igemm_halo_kw_kernel(KwArgs h) {
     store_window(0, 0);
     __syncthreads();
   }
+  KW_STAMP(14);
   if constexpr (NS == 2) {
     wave_max_put(0);
     __syncthreads();
@@ -632,9 +634,14 @@ void igemm_halo_kw_kernel(KwArgs h) {
       v = act_f(v, a.act);
       if (a.accumulate) v += cv[i];
       if (a.c_bf16) ((__bf16*)a.C)[group * a.c_gs + orow[i] * a.ldc + n] = (__bf16)v;
+#ifdef SVAE_EXP_NOSTORE  // timing experiment (wrong results): the epilogue without its stores
+      else if (v != v) st_out(&Cp[orow[i] * a.ldc + n], v);
+#else
       else st_out(&Cp[orow[i] * a.ldc + n], v);
+#endif
       if (bwc) bw_term_v(v, pv[i], bm, bi, bb, bwy != nullptr, yv[i], a.bw.act, s1, s2);
     }
+    KW_STAMP(15);
     if (a.stats) {
       __syncthreads();  // every wave is done reading red
       red[tid] = s1;

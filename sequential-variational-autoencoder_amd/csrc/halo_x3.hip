@@ -1,0 +1,435 @@
+// The split mode's wave-split halo gather on scaled fp16 hi/lo planes (dtype bf16x6; opload.h
+// split8_h16 / mfma_h16): every conv / conv-T forward and input gradient with >= 1 channel chunk of 32
+// and 32-column output tiles.
+//
+// A block owns BM output rows x 32 columns and all of K.  Per 32-channel chunk it stages the input
+// window of its rows (plus the 4x4 halo) in LDS once, as the two fp16 planes of A * 2^hs (hs: the
+// block's running exponent, below), and its four waves run the MFMAs against that window:
+//   16-tap layers (conv s1 / s2, conv-T s1): wave w takes kernel row ky = w (four taps); the four
+//       partial tiles are summed in LDS in wave order before one epilogue (deterministic).
+//   stride-2 conv-T: the block covers all four output-parity classes of its rows, wave w the class
+//       (cy, cx) = (w >> 1, w & 1) with that class's four taps over one union window; the waves' tiles
+//       are disjoint, so there is no reduction (halo_kw.hip ran one class per block, one tap per wave).
+// B (the weights) comes from the two scaled fp16 weight planes H16_PLANE.. of the engine's shadows,
+// one tap of fragments ahead in registers.
+//
+// Scaling: fp16 has 11 significant bits and a narrow exponent range, so the block scales A by a power
+// of two 2^hs with max|A| * 2^hs in [2^14, 2^15) over the chunks staged so far (the running maximum
+// only grows, so hs only falls; the accumulators are rescaled by the same exact power of two when it
+// does).  Weights carry the fixed 2^H16_WS.  The epilogue multiplies by 2^-(hs + H16_WS).
+#include "common.h"
+#include "kernels.h"
+#include "opload.h"
+
+typedef __bf16 x3_16x8 __attribute__((ext_vector_type(8)));  // 8 raw 16-bit lanes (fp16 bits)
+
+#define X3_CK 32    // channels per window stage
+#define X3_ROWP 40  // LDS pixel pitch in 16-bit elements (80 B: conflict-free 16-B fragment reads)
+
+struct X3Args {
+  const float* A; long long a_gs; int lda;
+  const __bf16* Bh; long long b_gs; int ldb; long long b_tap, b_plane;  // fp16 plane h0 at Bh, h1 at Bh + b_plane
+  float* C; long long c_gs; int ldc;
+  u64* stats; long long s_gs, s_sh; int s_nsh;
+  const float* bias; long long bias_gs;
+  BwStat bw;
+  int Cin, act, accumulate;
+  int mode;          // GM_CONV / GM_CONVT
+  int Hi, Wi, Ho, Wo;
+  int Hr, Wr;        // row space per class
+  int R, PR, PC, sy, npix;
+  int oy0, ox0;      // window origin (conv-T stride 2: the union of the four classes' windows)
+  int toff0, tsgn;   // tap shift: window offset of tap t = toff0 + tsgn * (row(t) * PC + col(t))
+  FastDiv d_win, d_pc, d_img, d_wr, d_rimg;
+  int slot_off;      // byte offset of the [2][4] wave maxima of |A| in dynamic LDS
+};
+
+namespace {
+
+template <int BM, bool CPW, int PI>
+__global__ __launch_bounds__(256, BM == 64 ? 3 : 4) void gather_x3_kernel(X3Args h) {
+  constexpr int TM = BM / 32;
+  extern __shared__ __attribute__((aligned(16))) __bf16 xsm[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const BlockXYZ blk = xcd_block();
+  const int m0 = blk.x * BM, n0 = blk.y * 32, group = blk.z;
+  const int nchunk = h.Cin / X3_CK;
+  const int per_img = h.Hr * h.Wr;
+
+  // ---- window items: PI per thread, 8 channels each (item it = pixel it / 4, channel part it % 4) ----
+  int woff[PI];
+  {
+    const int img0 = fdiv(m0, h.d_img);
+    const int ry0 = fdiv(m0 - img0 * per_img, h.d_wr);
+    const int iy_base = ry0 * h.sy + h.oy0;
+#pragma unroll
+    for (int i = 0; i < PI; ++i) {
+      const int it = tid + 256 * i;
+      woff[i] = -2;  // -2: no item, -1: zero (outside the image)
+      if (it < h.npix * 4) {
+        const int pix = it >> 2, part = it & 3;
+        const int il = fdiv(pix, h.d_win);
+        const int r2 = pix - il * h.PR * h.PC;
+        const int pr = fdiv(r2, h.d_pc), pc = r2 - pr * h.PC;
+        const int iy = iy_base + pr, ix = h.ox0 + pc;
+        woff[i] = (iy >= 0 && iy < h.Hi && ix >= 0 && ix < h.Wi) ? (((img0 + il) * h.Hi + iy) * h.Wi + ix) * h.lda + part * 8
+                                                                 : -1;
+      }
+    }
+  }
+  f32x4 wv[PI][2];
+  const float* Ag = h.A + group * h.a_gs;
+  auto load_window = [&](int chunk) {
+#pragma unroll
+    for (int i = 0; i < PI; ++i) {
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      wv[i][0] = z;
+      wv[i][1] = z;
+      if (woff[i] >= 0) {
+        const float* p = Ag + woff[i] + chunk * X3_CK;
+        wv[i][0] = *(const f32x4*)p;
+        wv[i][1] = *(const f32x4*)(p + 4);
+      }
+    }
+  };
+
+  // ---- the block's running max |A| and exponent hs (A staged as A * 2^hs) ----
+  int hs = 0;
+  float hmax = 0.f;
+  float* hslot = (float*)((char*)xsm + h.slot_off);
+  auto wave_max_put = [&](int parity) {  // this wave's max |A| over the registers holding the next chunk
+    float m = 0.f;
+#pragma unroll
+    for (int i = 0; i < PI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) m = fmaxf(m, fmaxf(fabsf(wv[i][0][j]), fabsf(wv[i][1][j])));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if (lane == 0) hslot[parity * 4 + wave] = m;
+  };
+  auto store_window = [&]() {
+#pragma unroll
+    for (int i = 0; i < PI; ++i) {
+      const int it = tid + 256 * i;
+      if (woff[i] < -1) continue;
+      x3_16x8 pl[2];
+      split8_h16(wv[i][0], wv[i][1], hs, pl);
+      const int o = (it >> 2) * X3_ROWP + (it & 3) * 8;
+      *(x3_16x8*)&xsm[o] = pl[0];
+      *(x3_16x8*)&xsm[h.npix * X3_ROWP + o] = pl[1];
+    }
+  };
+
+  // ---- A fragment bases (this wave's class offset for the stride-2 conv-T) ----
+  const int cls = CPW ? wave : 0;
+  const int cyo = CPW ? (wave >> 1) : 0, cxo = CPW ? (wave & 1) : 0;
+  int abase[TM];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const int ml = tm * 32 + l32;
+    const int rows_img = h.R * h.Wr;
+    const int il = fdiv(ml, h.d_rimg);
+    const int rem = ml - il * rows_img;
+    const int ryl = fdiv(rem, h.d_wr), rx = rem - ryl * h.Wr;
+    abase[tm] = ((il * h.PR + ryl * h.sy + cyo) * h.PC + rx * h.sy + cxo) * X3_ROWP + 8 * hh;
+  }
+  // this wave's taps u = 0..3: 16-tap layers kernel row ky = wave; conv-T stride 2 class `cls`'s 2 x 2
+  auto tap_of = [&](int u) {
+    if constexpr (CPW) {
+      const int cy = cls >> 1, cx = cls & 1;
+      return ((cy + 1) & 1) * 4 + ((cx + 1) & 1) + 8 * (u >> 1) + 2 * (u & 1);  // (pad 1)
+    } else {
+      return wave * 4 + u;
+    }
+  };
+  auto shift_of = [&](int u) {
+    if constexpr (CPW) return h.toff0 + h.tsgn * ((u >> 1) * h.PC + (u & 1));
+    else return h.toff0 + h.tsgn * (wave * h.PC + u);
+  };
+  x3_16x8 bq[2][2][2];  // [ring slot][kq][plane]
+  const __bf16* bbase = h.Bh + group * h.b_gs + (long long)(n0 + l32) * h.ldb + 8 * hh;
+  auto load_b = [&](int slot, int u, int chunk) {
+    const __bf16* p = bbase + (long long)tap_of(u) * h.b_tap + chunk * X3_CK;
+#pragma unroll
+    for (int kq = 0; kq < 2; ++kq) {
+      bq[slot][kq][0] = *(const x3_16x8*)(p + kq * 16);
+      bq[slot][kq][1] = *(const x3_16x8*)(p + h.b_plane + kq * 16);
+    }
+  };
+
+  load_window(0);
+  load_b(0, 0, 0);
+  wave_max_put(0);
+  __syncthreads();
+
+  f32x16 acc[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+
+  for (int c = 0; c < nchunk; ++c) {
+    const bool has_next = c + 1 < nchunk;
+    {  // the chunk's exponent (the running max only grows: a step d <= 0 shrinks the accumulators exactly)
+      const float* sl = hslot + (c & 1) * 4;
+      hmax = fmaxf(hmax, fmaxf(fmaxf(sl[0], sl[1]), fmaxf(sl[2], sl[3])));
+      const int ns = h16_exp(hmax);
+      const int d = ns - hs;
+      hs = ns;
+      if (d != 0) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][r] = __builtin_ldexpf(acc[i][r], d);
+      }
+    }
+    store_window();
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      // the ring: the next tap's B (this chunk's, or the next chunk's first)
+      if (u + 1 < 4) load_b((u + 1) & 1, u + 1, c);
+      else if (has_next) load_b(0, 0, c + 1);
+      // the next chunk's window after tap 1's B loads (in-order vmcnt: a later B wait also waits for it)
+      if (u == 0 && has_next) load_window(c + 1);
+      const int sh = shift_of(u) * X3_ROWP;
+#pragma unroll
+      for (int kq = 0; kq < 2; ++kq) {
+        x3_16x8 af[TM][2];
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+          af[tm][0] = *(const x3_16x8*)&xsm[abase[tm] + sh + kq * 16];
+          af[tm][1] = *(const x3_16x8*)&xsm[h.npix * X3_ROWP + abase[tm] + sh + kq * 16];
+        }
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) acc[tm] = mfma_h16(af[tm], bq[u & 1][kq], acc[tm]);
+      }
+    }
+    if (has_next) wave_max_put((c + 1) & 1);
+    __syncthreads();
+  }
+
+  // ---- the waves' tiles into LDS (in the units of C), then one epilogue over the block ----
+  float* red = (float*)xsm;  // [4][BM][32]
+  const int usc = -(hs + H16_WS);
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      red[(wave * BM + m) * 32 + l32] = __builtin_ldexpf(acc[tm][r], usc);
+    }
+  __syncthreads();
+
+  // 16-byte epilogue: thread = 4 consecutive columns x rows rg, rg + 32, ... (8 threads per 128-B row)
+  constexpr int ROWS = CPW ? 4 * BM : BM;  // output rows of the block (CPW: the four classes' tiles)
+  constexpr int NR = ROWS / 32;
+  const int c4 = (tid & 7) * 4, rg = tid >> 3;
+  const int n = n0 + c4;
+  float* Cp = h.C + group * h.c_gs;
+  const bool bwm = h.bw.pre != nullptr;
+  const bool bwc = bwm && n < h.bw.C;
+  f32x4 bm = {0.f, 0.f, 0.f, 0.f}, bi = bm, bb = bm, biasv = bm;
+  if (bwc) {
+    bm = *(const f32x4*)&h.bw.mean[group * h.bw.ms_gs + n];
+    bi = *(const f32x4*)&h.bw.invstd[group * h.bw.ms_gs + n];
+    if (!h.bw.y) bb = *(const f32x4*)&h.bw.beta[group * h.bw.beta_gs + n];
+  }
+  if (h.bias) biasv = *(const f32x4*)&h.bias[group * h.bias_gs + n];
+  const float* bwpre = bwc ? h.bw.pre + group * h.bw.pre_gs : nullptr;
+  const float* bwy = (bwc && h.bw.y) ? h.bw.y + group * h.bw.y_gs : nullptr;
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  constexpr int NB = NR < 2 ? NR : 2;  // rows per batch: every global load of a batch before its first store
+  static_assert(NR % NB == 0, "row batches");
+#pragma unroll
+  for (int i0 = 0; i0 < NR; i0 += NB) {
+    long long orow[NB];
+    f32x4 cv[NB], pv[NB], yv[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int vr = rg + 32 * (i0 + b);
+      if constexpr (CPW) {  // class k = (cy, cx), row m -> output pixel (2 qy + cy, 2 qx + cx)
+        const int k = vr / BM;
+        const int row = m0 + vr % BM;
+        const int img = fdiv(row, h.d_img);
+        const int r2 = row - img * per_img;
+        const int qy = fdiv(r2, h.d_wr), qx = r2 - qy * h.Wr;
+        orow[b] = ((long long)img * h.Ho + 2 * qy + (k >> 1)) * h.Wo + 2 * qx + (k & 1);
+      } else {
+        orow[b] = m0 + vr;
+      }
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      cv[b] = pv[b] = yv[b] = z;
+      if (h.accumulate) cv[b] = *(const f32x4*)&Cp[orow[b] * h.ldc + n];
+      if (bwpre) pv[b] = *(const f32x4*)&bwpre[orow[b] * h.bw.ldp + n];
+      if (bwy) yv[b] = *(const f32x4*)&bwy[orow[b] * h.bw.ldy + n];
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int vr = rg + 32 * (i0 + b);
+      f32x4 v = *(const f32x4*)&red[vr * 32 + c4];
+      if constexpr (!CPW) {
+#pragma unroll
+        for (int w = 1; w < 4; ++w) v += *(const f32x4*)&red[(w * BM + vr) * 32 + c4];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float x = v[j];
+        if (!bwm) {
+          s1[j] += x;
+          s2[j] += x * x;
+        }
+        if (h.bias) x += biasv[j];
+        x = act_f(x, h.act);
+        if (h.accumulate) x += cv[b][j];
+        v[j] = x;
+        if (bwc) bw_term_v(x, pv[b][j], bm[j], bi[j], bb[j], bwy != nullptr, yv[b][j], h.bw.act, s1[j], s2[j]);
+      }
+      *(f32x4*)&Cp[orow[b] * h.ldc + n] = v;
+    }
+  }
+  if (h.stats) {
+    __syncthreads();  // every wave is done reading red
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      red[rg * 32 + c4 + j] = s1[j];
+      red[32 * 32 + rg * 32 + c4 + j] = s2[j];
+    }
+    __syncthreads();
+    if (tid < 32) {
+      const int SC = bwm ? h.bw.C : 0x7fffffff;  // stats columns
+      if (n0 + tid < SC) {
+        float sa = 0.f, qa = 0.f;
+        for (int j = 0; j < 32; ++j) {  // fixed order: deterministic
+          sa += red[j * 32 + tid];
+          qa += red[32 * 32 + j * 32 + tid];
+        }
+        const int rb = blk.x;
+        stat_put(h.stats + (rb & (h.s_nsh - 1)) * h.s_sh + group * h.s_gs, n0 + tid, sa, qa);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// ---- planner / launcher ----
+// Eligible: 4x4 pad-1 conv (stride 1 / 2) and conv-T (stride 1 / 2) with Cin % 32 == 0, N % 32 == 0, fp32
+// A and C, the fp16 weight planes (a.h16), 16-byte aligned epilogue operands, no consumer-side BN.
+struct X3Plan {
+  X3Args h;
+  int bm, pi;
+  bool cpw;
+  size_t lds;
+  dim3 grid;
+};
+
+static bool x3_plan(const FwdArgs& a, int groups, X3Plan* out) {
+  const ConvGeom& g = a.g;
+  if (a.nsp < 2 || !a.h16 || !a.Bh || a.a_bf16 || a.c_bf16 || a.ain.acc || a.fin.cnt) return false;
+  if (g.mode == GM_DENSE || g.ksz != 4 || g.pad != 1 || a.Cin % X3_CK != 0 || a.N % 32 != 0) return false;
+  if (g.mode == GM_CONVT && g.stride > 2) return false;
+  if (a.bw.pre && (a.bw.pre_bf16 || a.bw.y_bf16)) return false;
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (a.ldc % 4 || a.c_gs % 4 || !al16(a.C) || (a.bias && (!al16(a.bias) || a.bias_gs % 4))) return false;
+  if (a.bw.pre && (a.bw.C % 4 || a.bw.ldp % 4 || a.bw.pre_gs % 4 || !al16(a.bw.pre) || !al16(a.bw.mean) ||
+                   !al16(a.bw.invstd) || a.bw.ms_gs % 4 ||
+                   (a.bw.y ? (a.bw.ldy % 4 || a.bw.y_gs % 4 || !al16(a.bw.y)) : (!al16(a.bw.beta) || a.bw.beta_gs % 4))))
+    return false;
+  const bool s2t = g.mode == GM_CONVT && g.stride == 2;
+  const int Hr = s2t ? g.Ho / 2 : g.Ho, Wr = s2t ? g.Wo / 2 : g.Wo;
+  const int sy = g.mode == GM_CONV ? g.stride : 1;
+  const int span = s2t ? 3 : 4;  // window rows beyond R - 1 (conv-T stride 2: the classes' union)
+  const int per_img = Hr * Wr;
+  for (int bm : {64, 32}) {
+    if (bm % Wr != 0 || a.rows % bm != 0) continue;
+    if (!(per_img % bm == 0 || bm % per_img == 0)) continue;
+    X3Args& h = out->h;
+    h.Hr = Hr;
+    h.Wr = Wr;
+    h.R = bm >= per_img ? Hr : bm / Wr;
+    const int nimg = bm >= per_img ? bm / per_img : 1;
+    h.sy = sy;
+    h.PR = (h.R - 1) * sy + span;
+    h.PC = (Wr - 1) * sy + span;
+    h.npix = nimg * h.PR * h.PC;
+    const int pi = (h.npix * 4 + 255) / 256;
+    if (pi > 4) continue;
+    const long long blocks = (long long)(a.rows / bm) * (a.N / 32) * groups;
+    if (blocks < 256 && bm > 32) continue;
+    // stride-2 conv-T: one block per 4 classes' tiles; the 4x4-input levels give too few blocks
+    // (halo_kw's one class per block, four times the blocks, is faster there: 29 vs 40 us, 14 vs 17 us)
+    if (s2t && blocks < 512) return false;
+    h.d_win = make_fastdiv(h.PR * h.PC);
+    h.d_pc = make_fastdiv(h.PC);
+    h.d_img = make_fastdiv(per_img);
+    h.d_wr = make_fastdiv(Wr);
+    h.d_rimg = make_fastdiv(h.R * Wr);
+    if (s2t) {  // union origin of the four classes (pad 1: class 0 starts one row / column up)
+      h.oy0 = h.ox0 = -1;
+      h.toff0 = h.PC + 1;
+      h.tsgn = -1;
+    } else if (g.mode == GM_CONV) {
+      h.oy0 = h.ox0 = -g.pad;
+      h.toff0 = 0;
+      h.tsgn = 1;
+    } else {
+      h.oy0 = h.ox0 = g.pad - 3;
+      h.toff0 = 3 * h.PC + 3;
+      h.tsgn = -1;
+    }
+    out->bm = bm;
+    out->pi = pi <= 3 ? 3 : 4;
+    out->cpw = s2t;
+    const size_t win = (size_t)2 * h.npix * X3_ROWP * 2;
+    const size_t red = (size_t)4 * bm * 32 * 4;
+    h.slot_off = (int)((std::max(win, red) + 15) / 16 * 16);
+    out->lds = (size_t)h.slot_off + 8 * sizeof(float);
+    out->grid = dim3(a.rows / bm, a.N / 32, groups);
+    return true;
+  }
+  return false;
+}
+
+int halo_x3_plan(const FwdArgs& a, int groups) {
+  X3Plan p;
+  if (!x3_plan(a, groups, &p)) return 0;
+  return a.rows / p.bm;  // stats row-blocks (per group)
+}
+
+int halo_x3(const FwdArgs& a, int groups, hipStream_t s) {
+  X3Plan p;
+  if (!x3_plan(a, groups, &p)) return -1;
+  X3Args& h = p.h;
+  h.A = a.A; h.a_gs = a.a_gs; h.lda = a.lda;
+  h.Bh = (const __bf16*)a.Bh + H16_PLANE * a.b_plane;  // the fp16 planes of the shadow
+  h.b_gs = a.b_gs; h.ldb = a.ldb; h.b_tap = a.b_tap; h.b_plane = a.b_plane;
+  h.C = a.C; h.c_gs = a.c_gs; h.ldc = a.ldc;
+  h.stats = a.stats; h.s_gs = a.s_gs; h.s_sh = a.s_sh; h.s_nsh = a.s_nsh;
+  h.bias = a.bias; h.bias_gs = a.bias_gs;
+  h.bw = a.bw;
+  h.Cin = a.Cin; h.act = a.act; h.accumulate = a.accumulate;
+  h.mode = a.g.mode;
+  h.Hi = a.g.Hi; h.Wi = a.g.Wi; h.Ho = a.g.Ho; h.Wo = a.g.Wo;
+  static bool attr = false;
+  if (!attr) {
+    for (const void* f : {(const void*)gather_x3_kernel<64, false, 3>, (const void*)gather_x3_kernel<64, false, 4>,
+                          (const void*)gather_x3_kernel<32, false, 3>, (const void*)gather_x3_kernel<32, false, 4>,
+                          (const void*)gather_x3_kernel<64, true, 3>, (const void*)gather_x3_kernel<64, true, 4>,
+                          (const void*)gather_x3_kernel<32, true, 3>, (const void*)gather_x3_kernel<32, true, 4>})
+      hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 98304);
+    attr = true;
+  }
+#define X3_LAUNCH(BM_, CPW_, PI_) hipLaunchKernelGGL((gather_x3_kernel<BM_, CPW_, PI_>), p.grid, dim3(256), p.lds, s, h)
+  if (p.bm == 64) {
+    if (p.cpw) { if (p.pi == 3) X3_LAUNCH(64, true, 3); else X3_LAUNCH(64, true, 4); }
+    else { if (p.pi == 3) X3_LAUNCH(64, false, 3); else X3_LAUNCH(64, false, 4); }
+  } else {
+    if (p.cpw) { if (p.pi == 3) X3_LAUNCH(32, true, 3); else X3_LAUNCH(32, true, 4); }
+    else { if (p.pi == 3) X3_LAUNCH(32, false, 3); else X3_LAUNCH(32, false, 4); }
+  }
+#undef X3_LAUNCH
+  return a.rows / p.bm;
+}

@@ -108,7 +108,8 @@ enum KernelId {
   KID_WHALO2_S1 = 26,  // wgrad_halo2_kernel<...> (all instances: stride-1 halo weight-GEMM, wgrad_halo2.hip)
   KID_HALO_KW = 27,    // igemm_halo_kw_kernel<...> (all instances: small-image gather, K over waves, halo_kw.hip)
   KID_WHALO2_S2 = 28, // wgrad_halo2_kernel<..., S = 2> (stride-2 instances, separate from KID_WHALO_32_S2)
-  KID_COUNT = 29
+  KID_HALO_X3 = 29,    // gather_x3_kernel<...> (all instances: the split mode's fp16-plane gather, halo_x3.hip)
+  KID_COUNT = 30
 };
 const char* kernel_name(int kid);
 int igemm_bf16_kid(const FwdArgs& a);
@@ -121,6 +122,9 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
 int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit);
 // small-image halo gather-GEMM with K split over the block's waves (halo_kw.hip), used where the
 // tiled halo kernel would split K over the grid: stats row-blocks (0 = shape not eligible) / launch
+// the split mode's fp16-plane wave-split gather (halo_x3.hip): stats row-blocks (0: not eligible) / launch (-1)
+int halo_x3_plan(const FwdArgs& a, int groups);
+int halo_x3(const FwdArgs& a, int groups, hipStream_t s);
 int halo_kw_plan(const FwdArgs& a, int groups);
 // the split-bf16 (nsp = 3) gather-GEMMs: does a launch of this shape have a split kernel (halo_kw,
 // dense_kw)?  Shapes without one run the fp32 kernels (igemm_fwd) in that mode.

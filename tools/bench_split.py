@@ -113,16 +113,16 @@ def stamps(names):
         span = t[:, :, 12].max() - t0
         print("%s %s: %d blocks, span %.0f clk" % (name, (n, h, cin, cout, s, tr), nblk, span))
         names_ = {1: "prologue", 2: "stage0", 3: "mfma0", 4: "stage1", 5: "mfma1", 6: "stage2", 7: "mfma2",
-                  8: "stage3", 9: "mfma3", 10: "loopend", 11: "red", 12: "epi"}
-        prev = t[:, :, 0]
-        for i in range(1, 13):
+                  8: "stage3", 9: "mfma3", 10: "loopend", 11: "red", 12: "epi", 13: "args", 14: "issued",
+                  15: "stores"}
+        rows = []
+        for i in range(1, 16):
             cur = t[:, :, i]
             ok = cur > 0
-            if not ok.any():
-                continue
-            d = (cur - prev)[ok]
-            print("  %-9s mean %8.0f  p10 %8.0f  p90 %8.0f" % (names_[i], d.mean(), np.percentile(d, 10), np.percentile(d, 90)))
-            prev = np.where(ok, cur, prev)
+            if ok.any():
+                rows.append(((cur - t[:, :, 0])[ok].mean(), i))
+        for off, i in sorted(rows):
+            print("  %-9s at %8.0f clk after entry" % (names_[i], off))
         life = (t[:, :, 12] - t[:, :, 0]).mean()
         starts = np.sort(t[:, 0, 0] - t0)
         print("  lifetime mean %.0f clk; block starts p25/p50/p75 %.0f/%.0f/%.0f" % (
