@@ -29,7 +29,10 @@ typedef __bf16 dk_bf16x8 __attribute__((ext_vector_type(8)));
 // WK = 4: 32-row blocks, K over the waves.  WK = 1: 128-row blocks (the whole batch), every wave
 // its own 32 rows over the split's full K range, so each weight column is read by one block.
 // NS = 3: split-bf16 planes (dtype bf16x6, opload.h): A split in registers, B from the three
-// shadow planes, six MFMAs per fragment pair
+// shadow planes, six MFMAs per fragment pair.  NS = 2: the split mode's scaled fp16 hi/lo planes
+// (opload.h split8_h16 / mfma_h16, three MFMAs): A * 2^hs with a per-wave running exponent over the
+// wave's K batches (the accumulators shrink by the exact power of two when it falls), B the shadow's
+// fp16 planes (w * 2^H16_WS); each wave's partial tile is unscaled before the LDS sum
 template <int TN, bool ABF, int WK, int NS = 1>
 __global__ __launch_bounds__(256) void dense_kw_kernel(FwdArgs a) {
   constexpr int BN = 32 * TN, BMR = 32 * (4 / WK);
@@ -44,18 +47,22 @@ __global__ __launch_bounds__(256) void dense_kw_kernel(FwdArgs a) {
   const int j0 = (int)((long long)nks * z / ks), j1 = (int)((long long)nks * (z + 1) / ks);
   const int m = m0 + wr * 32 + l32;
   const bool mv = m < a.rows;
-  const __bf16* Bw = (const __bf16*)a.Bh;
+  const __bf16* Bw = (const __bf16*)a.Bh;  // (NS = 2: advanced to the fp16 planes below)
   f32x16 acc[TN];
 #pragma unroll
   for (int t = 0; t < TN; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
   const long long arow = (long long)m * a.lda;
+  [[maybe_unused]] int hs = 0;
+  [[maybe_unused]] float hmax = 0.f;
+  if constexpr (NS == 2) Bw += H16_PLANE * a.b_plane;  // the fp16 planes of the shadow
   // DKW_U K steps per batch, all loads of a batch issued before its MFMAs (the per-wave chain is
   // latency-bound: a handful of K steps per wave, few waves per CU); steps past the split's end
   // load zero fragments
   for (int jb = j0 + wk; jb < j1; jb += WK * DKW_U) {
     dk_bf16x8 af[DKW_U][NS], bf[DKW_U][TN][NS];
+    [[maybe_unused]] f32x4 alo[DKW_U], ahi[DKW_U];
 #pragma unroll
     for (int u = 0; u < DKW_U; ++u) {
       const int j = jb + WK * u;
@@ -63,7 +70,10 @@ __global__ __launch_bounds__(256) void dense_kw_kernel(FwdArgs a) {
       f32x4 lo = {0.f, 0.f, 0.f, 0.f}, hi = lo;
       if (mv && j < j1) ld8_raw(a.A, arow + k, ABF, lo, hi);
       if constexpr (NS == 1) af[u][0] = raw8_bf(lo, hi, ABF);
-      else split8<NS>(lo, hi, af[u]);
+      else if constexpr (NS == 2) {
+        alo[u] = lo;
+        ahi[u] = hi;
+      } else split8<NS>(lo, hi, af[u]);
 #pragma unroll
       for (int t = 0; t < TN; ++t) {
         const int n = n0 + t * 32 + l32;
@@ -74,10 +84,41 @@ __global__ __launch_bounds__(256) void dense_kw_kernel(FwdArgs a) {
         }
       }
     }
+    if constexpr (NS == 2) {  // the batch's max |A| over the wave, the running exponent, then the planes
+      float mx = 0.f;
 #pragma unroll
-    for (int u = 0; u < DKW_U; ++u)
+      for (int u = 0; u < DKW_U; ++u)
 #pragma unroll
-      for (int t = 0; t < TN; ++t) acc[t] = mfma_split<NS>(af[u], bf[u][t], acc[t]);
+        for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fmaxf(fabsf(alo[u][e]), fabsf(ahi[u][e])));
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+      hmax = fmaxf(hmax, mx);
+      const int ns = h16_exp(hmax);
+      if (ns != hs) {
+#pragma unroll
+        for (int t = 0; t < TN; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[t][r] = __builtin_ldexpf(acc[t][r], ns - hs);
+        hs = ns;
+      }
+#pragma unroll
+      for (int u = 0; u < DKW_U; ++u) split8_h16(alo[u], ahi[u], hs, af[u]);
+#pragma unroll
+      for (int u = 0; u < DKW_U; ++u)
+#pragma unroll
+        for (int t = 0; t < TN; ++t) acc[t] = mfma_h16(af[u], bf[u][t], acc[t]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < DKW_U; ++u)
+#pragma unroll
+        for (int t = 0; t < TN; ++t) acc[t] = mfma_split<NS>(af[u], bf[u][t], acc[t]);
+    }
+  }
+  if constexpr (NS == 2) {  // back to the units of C
+#pragma unroll
+    for (int t = 0; t < TN; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = __builtin_ldexpf(acc[t][r], -(hs + H16_WS));
   }
   // ---- the WK waves' partial tiles, summed in a fixed order ----
 #pragma unroll
@@ -195,7 +236,10 @@ int dense_kw(const FwdArgs& a, int ks, hipStream_t s) {
 #define DKW_L(TN_, WK_)                                                                         \
   if (a.a_bf16) hipLaunchKernelGGL((dense_kw_kernel<TN_, true, WK_>), grid, dim3(256), 0, s, a); \
   else hipLaunchKernelGGL((dense_kw_kernel<TN_, false, WK_>), grid, dim3(256), 0, s, a);
-  if (a.nsp > 1) {  // split-bf16 planes: fp32 A, 32-row blocks with K over the waves
+  if (a.nsp > 1 && a.h16) {  // split mode, scaled fp16 planes: fp32 A, 32-row blocks with K over the waves
+    if (tn == 2) hipLaunchKernelGGL((dense_kw_kernel<2, false, 4, 2>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((dense_kw_kernel<1, false, 4, 2>), grid, dim3(256), 0, s, a);
+  } else if (a.nsp > 1) {  // split-bf16 planes: fp32 A, 32-row blocks with K over the waves
     if (tn == 2) hipLaunchKernelGGL((dense_kw_kernel<2, false, 4, 3>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((dense_kw_kernel<1, false, 4, 3>), grid, dim3(256), 0, s, a);
   } else if (tn == 2) {

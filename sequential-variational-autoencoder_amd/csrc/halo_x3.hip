@@ -25,6 +25,9 @@ typedef __bf16 x3_16x8 __attribute__((ext_vector_type(8)));  // 8 raw 16-bit lan
 
 #define X3_CK 32    // channels per window stage
 #define X3_ROWP 40  // LDS pixel pitch in 16-bit elements (80 B: conflict-free 16-B fragment reads)
+#ifndef X3_BMMAX
+#define X3_BMMAX 128  // largest row tile (16-tap layers; the stride-2 conv-T takes <= 64: four classes per block)
+#endif
 
 struct X3Args {
   const float* A; long long a_gs; int lda;
@@ -42,17 +45,26 @@ struct X3Args {
   int toff0, tsgn;   // tap shift: window offset of tap t = toff0 + tsgn * (row(t) * PC + col(t))
   FastDiv d_win, d_pc, d_img, d_wr, d_rimg;
   int slot_off;      // byte offset of the [2][4] wave maxima of |A| in dynamic LDS
+  void* stamps;      // (SVAE_EXP_STAMPS builds: the phase stamps, in the split-K scratch)
 };
 
 namespace {
 
 template <int BM, bool CPW, int PI>
-__global__ __launch_bounds__(256, BM == 64 ? 3 : 4) void gather_x3_kernel(X3Args h) {
+__global__ __launch_bounds__(256, BM == 128 ? 2 : BM == 64 ? 3 : 4) void gather_x3_kernel(X3Args h) {
   constexpr int TM = BM / 32;
   extern __shared__ __attribute__((aligned(16))) __bf16 xsm[];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
+#ifdef SVAE_EXP_STAMPS  // timing experiment: per-wave phase stamps (s_memtime) into the split-K scratch
+  unsigned long long* stamp_p = (unsigned long long*)h.stamps +
+      ((long long)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 4 + wave) * 16;
+#define X3_STAMP(i) do { if (lane == 0 && (i) < 16) stamp_p[(i)] = __builtin_readcyclecounter(); } while (0)
+#else
+#define X3_STAMP(i) do {} while (0)
+#endif
+  X3_STAMP(0);
   const BlockXYZ blk = xcd_block();
   const int m0 = blk.x * BM, n0 = blk.y * 32, group = blk.z;
   const int nchunk = h.Cin / X3_CK;
@@ -159,10 +171,13 @@ __global__ __launch_bounds__(256, BM == 64 ? 3 : 4) void gather_x3_kernel(X3Args
     }
   };
 
+  X3_STAMP(13);
   load_window(0);
   load_b(0, 0, 0);
+  X3_STAMP(14);
   wave_max_put(0);
   __syncthreads();
+  X3_STAMP(1);
 
   f32x16 acc[TM];
 #pragma unroll
@@ -187,6 +202,7 @@ __global__ __launch_bounds__(256, BM == 64 ? 3 : 4) void gather_x3_kernel(X3Args
     }
     store_window();
     __syncthreads();
+    if (c < 4) X3_STAMP(2 + 2 * c);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       // the ring: the next tap's B (this chunk's, or the next chunk's first)
@@ -207,9 +223,11 @@ __global__ __launch_bounds__(256, BM == 64 ? 3 : 4) void gather_x3_kernel(X3Args
         for (int tm = 0; tm < TM; ++tm) acc[tm] = mfma_h16(af[tm], bq[u & 1][kq], acc[tm]);
       }
     }
+    if (c < 4) X3_STAMP(3 + 2 * c);
     if (has_next) wave_max_put((c + 1) & 1);
     __syncthreads();
   }
+  X3_STAMP(10);
 
   // ---- the waves' tiles into LDS (in the units of C), then one epilogue over the block ----
   float* red = (float*)xsm;  // [4][BM][32]
@@ -222,6 +240,7 @@ __global__ __launch_bounds__(256, BM == 64 ? 3 : 4) void gather_x3_kernel(X3Args
       red[(wave * BM + m) * 32 + l32] = __builtin_ldexpf(acc[tm][r], usc);
     }
   __syncthreads();
+  X3_STAMP(11);
 
   // 16-byte epilogue: thread = 4 consecutive columns x rows rg, rg + 32, ... (8 threads per 128-B row)
   constexpr int ROWS = CPW ? 4 * BM : BM;  // output rows of the block (CPW: the four classes' tiles)
@@ -290,6 +309,7 @@ __global__ __launch_bounds__(256, BM == 64 ? 3 : 4) void gather_x3_kernel(X3Args
       *(f32x4*)&Cp[orow[b] * h.ldc + n] = v;
     }
   }
+  X3_STAMP(15);
   if (h.stats) {
     __syncthreads();  // every wave is done reading red
 #pragma unroll
@@ -311,6 +331,7 @@ __global__ __launch_bounds__(256, BM == 64 ? 3 : 4) void gather_x3_kernel(X3Args
       }
     }
   }
+  X3_STAMP(12);
 }
 
 }  // namespace
@@ -343,7 +364,11 @@ static bool x3_plan(const FwdArgs& a, int groups, X3Plan* out) {
   const int sy = g.mode == GM_CONV ? g.stride : 1;
   const int span = s2t ? 3 : 4;  // window rows beyond R - 1 (conv-T stride 2: the classes' union)
   const int per_img = Hr * Wr;
-  for (int bm : {64, 32}) {
+  // 128-row tiles on the 16-tap layers (the fixed per-block costs -- window prologue, epilogue -- over twice
+  // the MFMA work: 0.74-0.97 of the 64-row time on those shapes, profiles/r05_m1_x3.txt); the stride-2
+  // conv-T keeps <= 64 (its block already covers four classes: 128 rows left too few blocks, 1.6x)
+  for (int bm : {128, 64, 32}) {
+    if (bm > X3_BMMAX || (bm == 128 && s2t)) continue;
     if (bm % Wr != 0 || a.rows % bm != 0) continue;
     if (!(per_img % bm == 0 || bm % per_img == 0)) continue;
     X3Args& h = out->h;
@@ -413,6 +438,7 @@ int halo_x3(const FwdArgs& a, int groups, hipStream_t s) {
   h.Cin = a.Cin; h.act = a.act; h.accumulate = a.accumulate;
   h.mode = a.g.mode;
   h.Hi = a.g.Hi; h.Wi = a.g.Wi; h.Ho = a.g.Ho; h.Wo = a.g.Wo;
+  h.stamps = a.part;
   static bool attr = false;
   if (!attr) {
     for (const void* f : {(const void*)gather_x3_kernel<64, false, 3>, (const void*)gather_x3_kernel<64, false, 4>,
@@ -420,9 +446,20 @@ int halo_x3(const FwdArgs& a, int groups, hipStream_t s) {
                           (const void*)gather_x3_kernel<64, true, 3>, (const void*)gather_x3_kernel<64, true, 4>,
                           (const void*)gather_x3_kernel<32, true, 3>, (const void*)gather_x3_kernel<32, true, 4>})
       hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 98304);
+#if X3_BMMAX >= 128
+    for (const void* f : {(const void*)gather_x3_kernel<128, false, 3>, (const void*)gather_x3_kernel<128, false, 4>,
+                          (const void*)gather_x3_kernel<128, true, 3>, (const void*)gather_x3_kernel<128, true, 4>})
+      hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 98304);
+#endif
     attr = true;
   }
 #define X3_LAUNCH(BM_, CPW_, PI_) hipLaunchKernelGGL((gather_x3_kernel<BM_, CPW_, PI_>), p.grid, dim3(256), p.lds, s, h)
+#if X3_BMMAX >= 128
+  if (p.bm == 128) {
+    if (p.cpw) { if (p.pi == 3) X3_LAUNCH(128, true, 3); else X3_LAUNCH(128, true, 4); }
+    else { if (p.pi == 3) X3_LAUNCH(128, false, 3); else X3_LAUNCH(128, false, 4); }
+  } else
+#endif
   if (p.bm == 64) {
     if (p.cpw) { if (p.pi == 3) X3_LAUNCH(64, true, 3); else X3_LAUNCH(64, true, 4); }
     else { if (p.pi == 3) X3_LAUNCH(64, false, 3); else X3_LAUNCH(64, false, 4); }
