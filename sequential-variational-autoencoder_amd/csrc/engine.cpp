@@ -1056,7 +1056,9 @@ static inline int dbg_skip() { return 0; }
 
 // the consumer-side BN gather is available for this launch (the wave-split halo gather takes it)
 static bool ain_ok(svae_ctx* c, const FwdArgs& t, int groups) {
-  if (!c->m.g.bf16 || !t.Bh) return false;
+  // (the split mode's gathers scale their staged window by its running maximum, taken before a
+  // consumer-side BN could be applied: the knob-only fold runs in the bf16 mode alone)
+  if (!c->m.g.bf16 || !t.Bh || c->m.g.split) return false;
   FwdArgs u = t;
   if (c->m.g.split) {
     u.nsp = 3;

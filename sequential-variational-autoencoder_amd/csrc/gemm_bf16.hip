@@ -1519,6 +1519,13 @@ int igemm_bf16_plan(const FwdArgs& a, int groups, int* ksplit) {
   }
   // (no shortcut for convt_smalln: it only takes launches without stats, and the plan is asked
   //  before a.stats is set -- a BN layer must plan as the kernel that will carry its stats)
+  {
+    const int nx3 = halo_x3_plan(a, groups);  // the lean wave-split gather (halo_x3.hip) first
+    if (nx3 > 0) {
+      if (ksplit) *ksplit = 1;
+      return nx3;
+    }
+  }
   if (!halo_disabled()) {
     const HaloPlan hp = halo_plan(a, groups);
     if (hp.ok) {
@@ -1564,6 +1571,7 @@ int igemm_bf16_kid(const FwdArgs& a) {
     if (halo_x3_plan(a, 1) > 0) return KID_HALO_X3;
     return halo_kw_plan(a, 1) > 0 ? KID_HALO_KW : KID_NONE;
   }
+  if (halo_x3_plan(a, 1) > 0) return KID_HALO_X3;
   if (!halo_disabled()) {
     const HaloPlan hp = halo_plan(a, 1);
     if (hp.ok) return (kw_first(a, hp) && halo_kw_plan(a, 1)) ? KID_HALO_KW : hp.kid;
@@ -1626,6 +1634,13 @@ int igemm_bf16_path(FwdArgs a, int groups, int path, hipStream_t s, hipEvent_t a
     if (nrb < 0) nrb = halo_kw(a, groups, s);
     if (after) hipEventRecord(after, s);
     return nrb;
+  }
+  if (path == 2) {  // the lean wave-split gather (halo_x3.hip) where it fits
+    const int nrb = halo_x3(a, groups, s);
+    if (nrb >= 0) {
+      if (after) hipEventRecord(after, s);
+      return nrb;
+    }
   }
   if (path == 1 || (path == 2 && !halo_disabled())) {
     HaloPlan hp = halo_plan(a, groups);

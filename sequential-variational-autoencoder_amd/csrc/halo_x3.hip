@@ -19,12 +19,14 @@
 // does).  Weights carry the fixed 2^H16_WS.  The epilogue multiplies by 2^-(hs + H16_WS).
 #include "common.h"
 #include "kernels.h"
+#include "knobs.h"
 #include "opload.h"
 
 typedef __bf16 x3_16x8 __attribute__((ext_vector_type(8)));  // 8 raw 16-bit lanes (fp16 bits)
 
 #define X3_CK 32    // channels per window stage
 #define X3_ROWP 40  // LDS pixel pitch in 16-bit elements (80 B: conflict-free 16-B fragment reads)
+#define X3_OCC(BM, NP) ((NP) == 2 ? ((BM) == 128 ? 2 : (BM) == 64 ? 3 : 4) : ((BM) == 128 ? 2 : 4))
 #ifndef X3_BMMAX
 #define X3_BMMAX 128  // largest row tile (16-tap layers; the stride-2 conv-T takes <= 64: four classes per block)
 #endif
@@ -37,6 +39,7 @@ struct X3Args {
   const float* bias; long long bias_gs;
   BwStat bw;
   int Cin, act, accumulate;
+  int c_bf16;        // (bf16 mode) C is the bf16-stored pre-BN output
   int mode;          // GM_CONV / GM_CONVT
   int Hi, Wi, Ho, Wo;
   int Hr, Wr;        // row space per class
@@ -50,8 +53,13 @@ struct X3Args {
 
 namespace {
 
-template <int BM, bool CPW, int PI>
-__global__ __launch_bounds__(256, BM == 128 ? 2 : BM == 64 ? 3 : 4) void gather_x3_kernel(X3Args h) {
+// NP = 2: the split mode (fp32 A, scaled fp16 hi/lo planes, three MFMAs per fragment pair).
+// NP = 1: the bf16 mode (A fp32 or, ABF, stored bf16; one bf16 plane; bf16-stored pre-BN outputs c_bf16 and
+//         the fused backward-BN terms on bf16-stored pre / y).
+template <int BM, bool CPW, int PI, int NP = 2, bool ABF = false>
+__global__ __launch_bounds__(256, X3_OCC(BM, NP)) void gather_x3_kernel(X3Args h) {
+  static_assert(NP == 2 || NP == 1, "fp16 hi/lo planes or one bf16 plane");
+  static_assert(NP == 1 || !ABF, "the split planes come from fp32 activations");
   constexpr int TM = BM / 32;
   extern __shared__ __attribute__((aligned(16))) __bf16 xsm[];
   const int tid = threadIdx.x;
@@ -92,18 +100,14 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : BM == 64 ? 3 : 4) void gather_
     }
   }
   f32x4 wv[PI][2];
-  const float* Ag = h.A + group * h.a_gs;
+  const float* Ag = ABF ? (const float*)((const __bf16*)h.A + group * h.a_gs) : h.A + group * h.a_gs;
   auto load_window = [&](int chunk) {
 #pragma unroll
     for (int i = 0; i < PI; ++i) {
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
       wv[i][0] = z;
       wv[i][1] = z;
-      if (woff[i] >= 0) {
-        const float* p = Ag + woff[i] + chunk * X3_CK;
-        wv[i][0] = *(const f32x4*)p;
-        wv[i][1] = *(const f32x4*)(p + 4);
-      }
+      if (woff[i] >= 0) ld8_raw(Ag, woff[i] + chunk * X3_CK, ABF, wv[i][0], wv[i][1]);
     }
   };
 
@@ -126,11 +130,15 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : BM == 64 ? 3 : 4) void gather_
     for (int i = 0; i < PI; ++i) {
       const int it = tid + 256 * i;
       if (woff[i] < -1) continue;
-      x3_16x8 pl[2];
-      split8_h16(wv[i][0], wv[i][1], hs, pl);
       const int o = (it >> 2) * X3_ROWP + (it & 3) * 8;
-      *(x3_16x8*)&xsm[o] = pl[0];
-      *(x3_16x8*)&xsm[h.npix * X3_ROWP + o] = pl[1];
+      if constexpr (NP == 2) {
+        x3_16x8 pl[2];
+        split8_h16(wv[i][0], wv[i][1], hs, pl);
+        *(x3_16x8*)&xsm[o] = pl[0];
+        *(x3_16x8*)&xsm[h.npix * X3_ROWP + o] = pl[1];
+      } else {
+        *(x3_16x8*)&xsm[o] = raw8_bf(wv[i][0], wv[i][1], ABF);
+      }
     }
   };
 
@@ -160,14 +168,14 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : BM == 64 ? 3 : 4) void gather_
     if constexpr (CPW) return h.toff0 + h.tsgn * ((u >> 1) * h.PC + (u & 1));
     else return h.toff0 + h.tsgn * (wave * h.PC + u);
   };
-  x3_16x8 bq[2][2][2];  // [ring slot][kq][plane]
+  x3_16x8 bq[2][2][NP];  // [ring slot][kq][plane]
   const __bf16* bbase = h.Bh + group * h.b_gs + (long long)(n0 + l32) * h.ldb + 8 * hh;
   auto load_b = [&](int slot, int u, int chunk) {
     const __bf16* p = bbase + (long long)tap_of(u) * h.b_tap + chunk * X3_CK;
 #pragma unroll
     for (int kq = 0; kq < 2; ++kq) {
       bq[slot][kq][0] = *(const x3_16x8*)(p + kq * 16);
-      bq[slot][kq][1] = *(const x3_16x8*)(p + h.b_plane + kq * 16);
+      if constexpr (NP == 2) bq[slot][kq][1] = *(const x3_16x8*)(p + h.b_plane + kq * 16);
     }
   };
 
@@ -175,8 +183,10 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : BM == 64 ? 3 : 4) void gather_
   load_window(0);
   load_b(0, 0, 0);
   X3_STAMP(14);
-  wave_max_put(0);
-  __syncthreads();
+  if constexpr (NP == 2) {
+    wave_max_put(0);
+    __syncthreads();
+  }
   X3_STAMP(1);
 
   f32x16 acc[TM];
@@ -187,7 +197,7 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : BM == 64 ? 3 : 4) void gather_
 
   for (int c = 0; c < nchunk; ++c) {
     const bool has_next = c + 1 < nchunk;
-    {  // the chunk's exponent (the running max only grows: a step d <= 0 shrinks the accumulators exactly)
+    if constexpr (NP == 2) {  // the chunk's exponent (the running max only grows: a step d <= 0 shrinks the accumulators exactly)
       const float* sl = hslot + (c & 1) * 4;
       hmax = fmaxf(hmax, fmaxf(fmaxf(sl[0], sl[1]), fmaxf(sl[2], sl[3])));
       const int ns = h16_exp(hmax);
@@ -213,31 +223,36 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : BM == 64 ? 3 : 4) void gather_
       const int sh = shift_of(u) * X3_ROWP;
 #pragma unroll
       for (int kq = 0; kq < 2; ++kq) {
-        x3_16x8 af[TM][2];
+        x3_16x8 af[TM][NP];
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
           af[tm][0] = *(const x3_16x8*)&xsm[abase[tm] + sh + kq * 16];
-          af[tm][1] = *(const x3_16x8*)&xsm[h.npix * X3_ROWP + abase[tm] + sh + kq * 16];
+          if constexpr (NP == 2) af[tm][1] = *(const x3_16x8*)&xsm[h.npix * X3_ROWP + abase[tm] + sh + kq * 16];
         }
 #pragma unroll
-        for (int tm = 0; tm < TM; ++tm) acc[tm] = mfma_h16(af[tm], bq[u & 1][kq], acc[tm]);
+        for (int tm = 0; tm < TM; ++tm) {
+          if constexpr (NP == 2) acc[tm] = mfma_h16(af[tm], bq[u & 1][kq], acc[tm]);
+          else acc[tm] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm][0], bq[u & 1][kq][0], acc[tm], 0, 0, 0);
+        }
       }
     }
     if (c < 4) X3_STAMP(3 + 2 * c);
-    if (has_next) wave_max_put((c + 1) & 1);
+    if constexpr (NP == 2) {
+      if (has_next) wave_max_put((c + 1) & 1);
+    }
     __syncthreads();
   }
   X3_STAMP(10);
 
   // ---- the waves' tiles into LDS (in the units of C), then one epilogue over the block ----
   float* red = (float*)xsm;  // [4][BM][32]
-  const int usc = -(hs + H16_WS);
+  const int usc = NP == 2 ? -(hs + H16_WS) : 0;
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int m = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-      red[(wave * BM + m) * 32 + l32] = __builtin_ldexpf(acc[tm][r], usc);
+      red[(wave * BM + m) * 32 + l32] = NP == 2 ? __builtin_ldexpf(acc[tm][r], usc) : acc[tm][r];
     }
   __syncthreads();
   X3_STAMP(11);
@@ -257,8 +272,10 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : BM == 64 ? 3 : 4) void gather_
     if (!h.bw.y) bb = *(const f32x4*)&h.bw.beta[group * h.bw.beta_gs + n];
   }
   if (h.bias) biasv = *(const f32x4*)&h.bias[group * h.bias_gs + n];
-  const float* bwpre = bwc ? h.bw.pre + group * h.bw.pre_gs : nullptr;
-  const float* bwy = (bwc && h.bw.y) ? h.bw.y + group * h.bw.y_gs : nullptr;
+  // bf16-stored pre / y (bf16 mode): compile-time per instance only where NP == 1 (h.bw.*_bf16 checked by the plan)
+  const bool pbf = NP == 1 && h.bw.pre_bf16, ybf = NP == 1 && h.bw.y_bf16;
+  const float* bwpre = bwc ? pf_at(h.bw.pre, group * h.bw.pre_gs, pbf) : nullptr;
+  const float* bwy = (bwc && h.bw.y) ? pf_at(h.bw.y, group * h.bw.y_gs, ybf) : nullptr;
   float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
   constexpr int NB = NR < 2 ? NR : 2;  // rows per batch: every global load of a batch before its first store
   static_assert(NR % NB == 0, "row batches");
@@ -282,8 +299,8 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : BM == 64 ? 3 : 4) void gather_
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
       cv[b] = pv[b] = yv[b] = z;
       if (h.accumulate) cv[b] = *(const f32x4*)&Cp[orow[b] * h.ldc + n];
-      if (bwpre) pv[b] = *(const f32x4*)&bwpre[orow[b] * h.bw.ldp + n];
-      if (bwy) yv[b] = *(const f32x4*)&bwy[orow[b] * h.bw.ldy + n];
+      if (bwpre) pv[b] = pf_ld4(bwpre, orow[b] * h.bw.ldp + n, pbf);
+      if (bwy) yv[b] = pf_ld4(bwy, orow[b] * h.bw.ldy + n, ybf);
     }
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -292,6 +309,10 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : BM == 64 ? 3 : 4) void gather_
       if constexpr (!CPW) {
 #pragma unroll
         for (int w = 1; w < 4; ++w) v += *(const f32x4*)&red[(w * BM + vr) * 32 + c4];
+      }
+      if (NP == 1 && h.c_bf16) {  // bf16-stored pre-BN output: the statistics of the stored values
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = bf_rnd(v[j]);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -306,7 +327,10 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : BM == 64 ? 3 : 4) void gather_
         v[j] = x;
         if (bwc) bw_term_v(x, pv[b][j], bm[j], bi[j], bb[j], bwy != nullptr, yv[b][j], h.bw.act, s1[j], s2[j]);
       }
-      *(f32x4*)&Cp[orow[b] * h.ldc + n] = v;
+      if (NP == 1 && h.c_bf16)
+        *(u64*)((__bf16*)h.C + group * h.c_gs + orow[b] * h.ldc + n) = __builtin_bit_cast(u64, __builtin_convertvector(v, pf_bf16x4));
+      else
+        *(f32x4*)&Cp[orow[b] * h.ldc + n] = v;
     }
   }
   X3_STAMP(15);
@@ -347,17 +371,28 @@ struct X3Plan {
   dim3 grid;
 };
 
+// (knob builds read these per call: the bitwise tests switch them between networks of one process)
+static bool x3_bf16_on() { return svae_knob("SVAE_X3_BF16", 1) != 0; }  // 0: the bf16 mode's gathers on halo_kw
+// SVAE_X3=0: every gather on halo_kw (the knob-only consumer-side BN / last-arriver paths' bitwise tests
+// compare halo_kw with halo_kw)
+static bool x3_on() { return svae_knob("SVAE_X3", 1) != 0; }
+
 static bool x3_plan(const FwdArgs& a, int groups, X3Plan* out) {
   const ConvGeom& g = a.g;
-  if (a.nsp < 2 || !a.h16 || !a.Bh || a.a_bf16 || a.c_bf16 || a.ain.acc || a.fin.cnt) return false;
+  if (!x3_on() || !a.Bh || a.ain.acc || a.fin.cnt) return false;
+  const bool split = a.nsp > 1;
+  if (split ? (!a.h16 || a.a_bf16 || a.c_bf16) : !x3_bf16_on()) return false;
+  if (a.c_bf16 && (a.accumulate || a.bias || a.act != ACT_NONE || ((uintptr_t)a.C & 7))) return false;
   if (g.mode == GM_DENSE || g.ksz != 4 || g.pad != 1 || a.Cin % X3_CK != 0 || a.N % 32 != 0) return false;
   if (g.mode == GM_CONVT && g.stride > 2) return false;
-  if (a.bw.pre && (a.bw.pre_bf16 || a.bw.y_bf16)) return false;
+  if (split && a.bw.pre && (a.bw.pre_bf16 || a.bw.y_bf16)) return false;
   auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  if (a.ldc % 4 || a.c_gs % 4 || !al16(a.C) || (a.bias && (!al16(a.bias) || a.bias_gs % 4))) return false;
-  if (a.bw.pre && (a.bw.C % 4 || a.bw.ldp % 4 || a.bw.pre_gs % 4 || !al16(a.bw.pre) || !al16(a.bw.mean) ||
-                   !al16(a.bw.invstd) || a.bw.ms_gs % 4 ||
-                   (a.bw.y ? (a.bw.ldy % 4 || a.bw.y_gs % 4 || !al16(a.bw.y)) : (!al16(a.bw.beta) || a.bw.beta_gs % 4))))
+  auto al8 = [](const void* p) { return ((uintptr_t)p & 7) == 0; };
+  if (a.ldc % 4 || a.c_gs % 4 || (!a.c_bf16 && !al16(a.C)) || (a.bias && (!al16(a.bias) || a.bias_gs % 4))) return false;
+  if (a.bw.pre && (a.bw.C % 4 || a.bw.ldp % 4 || a.bw.pre_gs % 4 || !(a.bw.pre_bf16 ? al8(a.bw.pre) : al16(a.bw.pre)) ||
+                   !al16(a.bw.mean) || !al16(a.bw.invstd) || a.bw.ms_gs % 4 ||
+                   (a.bw.y ? (a.bw.ldy % 4 || a.bw.y_gs % 4 || !(a.bw.y_bf16 ? al8(a.bw.y) : al16(a.bw.y)))
+                           : (!al16(a.bw.beta) || a.bw.beta_gs % 4))))
     return false;
   const bool s2t = g.mode == GM_CONVT && g.stride == 2;
   const int Hr = s2t ? g.Ho / 2 : g.Ho, Wr = s2t ? g.Wo / 2 : g.Wo;
@@ -408,7 +443,7 @@ static bool x3_plan(const FwdArgs& a, int groups, X3Plan* out) {
     out->bm = bm;
     out->pi = pi <= 3 ? 3 : 4;
     out->cpw = s2t;
-    const size_t win = (size_t)2 * h.npix * X3_ROWP * 2;
+    const size_t win = (size_t)(split ? 2 : 1) * h.npix * X3_ROWP * 2;  // NP planes
     const size_t red = (size_t)4 * bm * 32 * 4;
     h.slot_off = (int)((std::max(win, red) + 15) / 16 * 16);
     out->lds = (size_t)h.slot_off + 8 * sizeof(float);
@@ -429,44 +464,51 @@ int halo_x3(const FwdArgs& a, int groups, hipStream_t s) {
   if (!x3_plan(a, groups, &p)) return -1;
   X3Args& h = p.h;
   h.A = a.A; h.a_gs = a.a_gs; h.lda = a.lda;
-  h.Bh = (const __bf16*)a.Bh + H16_PLANE * a.b_plane;  // the fp16 planes of the shadow
+  const bool split = a.nsp > 1;
+  h.Bh = (const __bf16*)a.Bh + (split ? H16_PLANE * a.b_plane : 0);  // split: the fp16 planes of the shadow
   h.b_gs = a.b_gs; h.ldb = a.ldb; h.b_tap = a.b_tap; h.b_plane = a.b_plane;
   h.C = a.C; h.c_gs = a.c_gs; h.ldc = a.ldc;
   h.stats = a.stats; h.s_gs = a.s_gs; h.s_sh = a.s_sh; h.s_nsh = a.s_nsh;
   h.bias = a.bias; h.bias_gs = a.bias_gs;
   h.bw = a.bw;
   h.Cin = a.Cin; h.act = a.act; h.accumulate = a.accumulate;
+  h.c_bf16 = a.c_bf16;
   h.mode = a.g.mode;
   h.Hi = a.g.Hi; h.Wi = a.g.Wi; h.Ho = a.g.Ho; h.Wo = a.g.Wo;
   h.stamps = a.part;
   static bool attr = false;
-  if (!attr) {
-    for (const void* f : {(const void*)gather_x3_kernel<64, false, 3>, (const void*)gather_x3_kernel<64, false, 4>,
-                          (const void*)gather_x3_kernel<32, false, 3>, (const void*)gather_x3_kernel<32, false, 4>,
-                          (const void*)gather_x3_kernel<64, true, 3>, (const void*)gather_x3_kernel<64, true, 4>,
-                          (const void*)gather_x3_kernel<32, true, 3>, (const void*)gather_x3_kernel<32, true, 4>})
-      hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 98304);
-#if X3_BMMAX >= 128
-    for (const void* f : {(const void*)gather_x3_kernel<128, false, 3>, (const void*)gather_x3_kernel<128, false, 4>,
-                          (const void*)gather_x3_kernel<128, true, 3>, (const void*)gather_x3_kernel<128, true, 4>})
-      hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 98304);
-#endif
+  if (!attr) {  // (LDS above the 64 KB default: the 128-row reduction tile)
+#define X3_ATTR(BM_, CPW_, PI_, NP_, ABF_) \
+    hipFuncSetAttribute((const void*)gather_x3_kernel<BM_, CPW_, PI_, NP_, ABF_>, hipFuncAttributeMaxDynamicSharedMemorySize, 98304);
+    X3_ATTR(128, false, 3, 2, false) X3_ATTR(128, false, 4, 2, false) X3_ATTR(64, false, 3, 2, false)
+    X3_ATTR(64, false, 4, 2, false) X3_ATTR(32, false, 3, 2, false) X3_ATTR(32, false, 4, 2, false)
+    X3_ATTR(64, true, 3, 2, false) X3_ATTR(64, true, 4, 2, false) X3_ATTR(32, true, 3, 2, false)
+    X3_ATTR(32, true, 4, 2, false)
+    X3_ATTR(128, false, 4, 1, false) X3_ATTR(128, false, 4, 1, true) X3_ATTR(64, false, 4, 1, false)
+    X3_ATTR(64, false, 4, 1, true) X3_ATTR(32, false, 4, 1, false) X3_ATTR(32, false, 4, 1, true)
+    X3_ATTR(64, true, 4, 1, false) X3_ATTR(64, true, 4, 1, true) X3_ATTR(32, true, 4, 1, false)
+    X3_ATTR(32, true, 4, 1, true)
+#undef X3_ATTR
     attr = true;
   }
-#define X3_LAUNCH(BM_, CPW_, PI_) hipLaunchKernelGGL((gather_x3_kernel<BM_, CPW_, PI_>), p.grid, dim3(256), p.lds, s, h)
-#if X3_BMMAX >= 128
+#define X3_LAUNCH(BM_, CPW_, PI_, NP_, ABF_) \
+  hipLaunchKernelGGL((gather_x3_kernel<BM_, CPW_, PI_, NP_, ABF_>), p.grid, dim3(256), p.lds, s, h)
+  // the bf16 mode (NP = 1): four window items per thread (registers to spare), A fp32 or bf16-stored
+#define X3_BF(BM_, CPW_) \
+  if (a.a_bf16) X3_LAUNCH(BM_, CPW_, 4, 1, true); else X3_LAUNCH(BM_, CPW_, 4, 1, false);
+#define X3_SP(BM_, CPW_) \
+  if (p.pi == 3) X3_LAUNCH(BM_, CPW_, 3, 2, false); else X3_LAUNCH(BM_, CPW_, 4, 2, false);
   if (p.bm == 128) {
-    if (p.cpw) { if (p.pi == 3) X3_LAUNCH(128, true, 3); else X3_LAUNCH(128, true, 4); }
-    else { if (p.pi == 3) X3_LAUNCH(128, false, 3); else X3_LAUNCH(128, false, 4); }
-  } else
-#endif
-  if (p.bm == 64) {
-    if (p.cpw) { if (p.pi == 3) X3_LAUNCH(64, true, 3); else X3_LAUNCH(64, true, 4); }
-    else { if (p.pi == 3) X3_LAUNCH(64, false, 3); else X3_LAUNCH(64, false, 4); }
+    if (split) { X3_SP(128, false) } else { X3_BF(128, false) }
+  } else if (p.bm == 64) {
+    if (p.cpw) { if (split) { X3_SP(64, true) } else { X3_BF(64, true) } }
+    else { if (split) { X3_SP(64, false) } else { X3_BF(64, false) } }
   } else {
-    if (p.cpw) { if (p.pi == 3) X3_LAUNCH(32, true, 3); else X3_LAUNCH(32, true, 4); }
-    else { if (p.pi == 3) X3_LAUNCH(32, false, 3); else X3_LAUNCH(32, false, 4); }
+    if (p.cpw) { if (split) { X3_SP(32, true) } else { X3_BF(32, true) } }
+    else { if (split) { X3_SP(32, false) } else { X3_BF(32, false) } }
   }
+#undef X3_SP
+#undef X3_BF
 #undef X3_LAUNCH
   return a.rows / p.bm;
 }

@@ -186,20 +186,22 @@ def test_second_side_stream_is_bitwise(preset, dtype, fused, monkeypatch, knob_l
 
 
 @pytest.mark.parametrize("preset,dtype,over", [
-    ("tiny", "bf16", {}), ("celeba", "bf16", {}), ("tiny", "bf16x6", {}), ("celeba", "bf16x6", {}),
+    ("tiny", "bf16", {}), ("celeba", "bf16", {}),
     ("tiny_homog", "bf16", {}), ("tiny", "bf16", {"predict_latent_code": True}),
 ])
 @pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("pre_f32", ["0", "1"])
 def test_forward_bn_fold_is_bitwise(preset, dtype, over, fused, pre_f32, monkeypatch, knob_lib):
-    """SVAE_FOLD=1: the forward BN apply of the recognition / encoder conv-a and decoder s1 (level >= 1)
+    """(Knob-only, measured slower: DESIGN §9.)  SVAE_FOLD=1: the forward BN apply of the recognition / encoder conv-a and decoder s1 (level >= 1)
     outputs runs on the side stream, and the next layer's wave-split gather stages act(bn_y(pre)) from
     the pre-BN tensor itself with the statistics finalised as bn_apply does (engine.cpp
     conv_bn_act_fwd, halo_kw.hip ain): the same values, so three training steps are bitwise the
     unfolded run's.  In bf16 mode the pre-BN tensor is stored bf16 (widened, applied and rounded back
-    while staging) or fp32 (SVAE_PRE_F32=1)."""
+    while staging) or fp32 (SVAE_PRE_F32=1).  Not in the split mode (engine.cpp ain_ok): its gathers
+    scale the staged window by a maximum taken before the consumer-side BN would apply."""
     if pre_f32 == "1" and dtype != "bf16":
         pytest.skip("fp32 / split modes store pre-BN tensors in fp32 either way")
+    monkeypatch.setenv("SVAE_X3", "0")  # the fold runs on halo_kw: compare halo_kw with halo_kw
     monkeypatch.setenv("SVAE_PRE_F32", pre_f32)
     monkeypatch.setenv("SVAE_FOLD", "0")
     p0, l0, _ = _run(preset, dtype, fused, over)
@@ -215,11 +217,12 @@ def test_forward_bn_fold_is_bitwise(preset, dtype, over, fused, pre_f32, monkeyp
 ])
 @pytest.mark.parametrize("fused", [False, True])
 def test_bn_last_arriver_finalisation_is_bitwise(preset, dtype, batch, fused, monkeypatch, knob_lib):
-    """SVAE_BN_LAF: the last block of each halo_kw BN producer turns the fixed-point accumulators into
+    """(Knob-only, measured slower: DESIGN §9.)  SVAE_BN_LAF: the last block of each halo_kw BN producer turns the fixed-point accumulators into
     mean / invstd (forward) or the backward sums a, b and dbeta (common.h bn_fin_arrive) with the apply
     passes' own expressions, ordered by device-scope atomics alone.  Three training steps at the headline
     batch (thousands of producer blocks on every XCD) are bitwise the per-block finalisation's: a block
     whose statistics the last arriver missed would move mean / invstd."""
+    monkeypatch.setenv("SVAE_X3", "0")  # the finalisation runs on halo_kw: compare halo_kw with halo_kw
     monkeypatch.setenv("SVAE_BN_LAF", "0")
     p0, l0, _ = _run(preset, dtype, fused, {}, batch=batch)
     monkeypatch.setenv("SVAE_BN_LAF", "3")
