@@ -174,7 +174,7 @@ def pmc_traffic(kernel, key="celeba/bf16"):
     workload (`key` = config/dtype; tools/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE rocprofv3
     passes of the bench command, the gfx950 FETCH correction per kernel as recorded there), or
     (None, None) when that workload has none."""
-    base = kernel.split("<")[0].split(" ")[0]
+    bases = [k.strip().split("<")[0].split(" ")[0] for k in kernel.split(" + ")]  # "a + b": both families
     paths = [os.path.join(ROOT, p) for p in PMC_FILES.get(key, [])]
     for path in paths:
         try:
@@ -184,11 +184,11 @@ def pmc_traffic(kernel, key="celeba/bf16"):
             continue
         tot = n = 0
         for k, v in d.get("kernels", {}).items():
-            if base == "wgrad_halo2_kernel" and "<" in k:  # the stride-1 instances (last template argument S)
+            if "wgrad_halo2_kernel" in bases and "<" in k:  # the stride-1 instances (last template argument S)
                 targs = k[k.index("<") + 1:k.rindex(">")].split(",")
                 if len(targs) >= 10 and targs[9].strip() != "1":
                     continue
-            if k.split("<")[0] == base and v.get("hbm_bytes_per_launch"):
+            if k.split("<")[0] in bases and v.get("hbm_bytes_per_launch"):
                 tot += v["hbm_bytes_per_launch"] * v["dispatches_fetch_pass"]
                 n += v["dispatches_fetch_pass"]
         if n:
@@ -276,57 +276,105 @@ def mode_throughput(cfg, SV, dtype, steps=10, warmup=3, probe_kid=None, probe_la
     return c32.batch * steps / dt, dt / steps * 1e3, probe
 
 
-def run_pixelvae(args, cfgmod):
-    """BASELINE configs[4] (CelebA + pixel_cnn decoder, 1 GPU): the c_pixelvae training step
-    (pixelvae.PixelVAE.train: engine forward, head training pass with dropout, sampler + highway,
-    both backwards, Adam + Polyak EMA) on a synthetic batch resident in HBM.  The roofline entry is
-    the head's forward convolution kernels (pc_conv3_kernel for the stride-1 halo convs,
-    pc_conv2_kernel for the rest: every forward convolution of the head, timed live by event pairs
-    around its first --probe-launches launches inside the timed region).  The per-step head FLOPs
-    (and so step_achieved_tflops) are ESTIMATED as 3x the forward convolution FLOPs (forward +
-    input gradient + weight gradient); only the forward launches are timed."""
-    PV = importlib.import_module(PKG + ".pixelvae").PixelVAE
-    B = args.batch or 128
-    dtype = args.dtype
+def _pv_throughput(PV, B, dtype, steps, warmup, probe_cap):
+    """Time `steps` c_pixelvae training steps in `dtype` (the head in its split mode for "bf16x6" / "fp32",
+    bf16 MFMA for "bf16"): (images/sec, ms/step, forward-conv probe, elbo, head conv FLOPs per step, pv)."""
     pv = PV("c_pixelvae", batch_size=B, dtype=dtype)
     c = pv.cfg
     g = torch.Generator(device="cuda")
     g.manual_seed(1234)
     x = (torch.rand(B, c.height, c.width, c.channels, device="cuda", generator=g) * 2 - 1).contiguous()
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         pv.train(x, x)
     torch.cuda.synchronize()
-    pv.head.probe, pv.head.probe_cap = [], args.probe_launches or 96
+    pv.head.probe, pv.head.probe_cap = [], probe_cap
     pv.head.conv_flops = 0.0
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         pv.train(x, x)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     probe, pv.head.probe = pv.head.probe, None
+    head_flops = 3.0 * pv.head.conv_flops / steps  # forward + input gradient + weight gradient
+    return B * steps / dt, dt / steps * 1e3, probe, pv.loss_value(), head_flops, pv, x
+
+
+def _pv_roofline(probe, planes, head_flops, vae_flops, ms, key):
+    """The head's forward convolutions (event pairs around each probed launch): algorithmic FLOPs per
+    second; in the split mode one algorithmic conv is 6 plane-product launches (issued = 6 x achieved)."""
     pflops = sum(f for f, _, _ in probe)
     pms = sum(e0.elapsed_time(e1) for _, e0, e1 in probe)
-    ach = pflops / (pms / 1e3) / 1e12 if pms > 0 else None
-    head_flops = 3.0 * pv.head.conv_flops / args.steps  # forward + input gradient + weight gradient
+    if pms <= 0:
+        return None
+    ach = pflops / (pms / 1e3) / 1e12
+    nprod = planes * (planes + 1) // 2
+    kern = "pc_conv3_kernel + pc_conv2_kernel"
+    traffic, tsrc = pmc_traffic(kern, key)
+    return {"bound": "mfma", "achieved": round(ach, 3), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 5), "traffic": traffic, "traffic_source": tsrc,
+            "traffic_unit": "HBM bytes per launch (PMC, family average)",
+            "kernel": kern + " (PixelCNN++ head forward convolutions, all instances%s)"
+                      % (", %d plane-product launches per conv" % nprod if nprod > 1 else ""),
+            "issued": round(ach * nprod, 3), "frac_issued": round(ach * nprod / BF16_MFMA_PEAK_TFLOPS, 5),
+            "timed_convs": len(probe), "avg_conv_us": round(pms * 1e3 / max(1, len(probe)), 2),
+            "step_achieved_tflops": round((head_flops + vae_flops) / (ms / 1e3) / 1e12, 3),
+            "step_achieved_method": "estimated: head FLOPs = 3 x forward convolution FLOPs"}
+
+
+def run_pixelvae(args, cfgmod):
+    """BASELINE configs[4] (CelebA + pixel_cnn decoder, 1 GPU): the c_pixelvae training step
+    (pixelvae.PixelVAE.train: engine forward, head training pass with dropout, sampler + highway,
+    both backwards, Adam + Polyak EMA) on a synthetic batch resident in HBM.  `value` is the
+    --dtype step (default bf16x6: the engine's split mode and the head's 3-plane split mode, the
+    fp32-grade step of tests/test_pixelvae_gpu.py); the bf16 step is reported beside it.  The
+    roofline entry is the head's forward convolution kernels (pc_conv3_kernel for the stride-1 halo
+    convs, pc_conv2_kernel for the rest: every forward convolution of the head, timed live by event
+    pairs around its first --probe-launches convolutions inside the timed region).  The per-step head
+    FLOPs (and so step_achieved_tflops) are ESTIMATED as 3x the forward convolution FLOPs (forward +
+    input gradient + weight gradient); only the forward launches are timed."""
+    PV = importlib.import_module(PKG + ".pixelvae").PixelVAE
+    B = args.batch or 128
+    dtype = args.dtype
+    cap = args.probe_launches or 96
+    value, ms, probe, elbo, head_flops, pv, x = _pv_throughput(PV, B, dtype, args.steps, args.warmup, cap)
+    c = pv.cfg
+    planes = pv.head.planes
     vae_flops = conv_flops_per_img(c) * B  # the engine's part (both steps' recognition + step 0 ladder)
-    ms = dt / args.steps * 1e3
+    alt = "bf16" if dtype != "bf16" else "bf16x6"
+    alt_value = alt_ms = alt_roof = None
+    if not args.no_secondary:
+        pv.close()
+        del pv
+        torch.cuda.empty_cache()
+        av, am, ap_, _, ahf, apv, _ = _pv_throughput(PV, B, alt, args.parity_steps, 2, cap)
+        alt_value, alt_ms = av, am
+        alt_roof = _pv_roofline(ap_, apv.head.planes, ahf, vae_flops, am, "c_pixelvae/" + alt)
+        apv.close()
+        del apv
+        torch.cuda.empty_cache()
+        pv = PV("c_pixelvae", batch_size=B, dtype=dtype)  # (for the CPU baseline's parameters)
+    parity = dtype != "bf16"
     line = {
-        "metric": METRIC["c_pixelvae"][0], "value": round(B * args.steps / dt, 2), "unit": "images/sec", "n_gpus": 1,
+        "metric": METRIC["c_pixelvae"][0], "value": round(value, 2), "unit": "images/sec", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": dtype + " engine, bf16-MFMA head",
+        "scaling": "weak", "vs_baseline": None,
+        "dtype": dtype + (" engine, 3-plane split head (6 bf16-MFMA products per GEMM)" if planes > 1
+                          else " engine, bf16-MFMA head"),
         "data": "synthetic U[-1,1] NHWC batch, target=input, eps / sampler uniforms / dropout masks on device",
         "config": {"workload": METRIC["c_pixelvae"][1], "model": "c_pixelvae", "global_batch": B, "per_gpu_batch": B,
                    "image": [c.height, c.width, c.channels], "mc_steps": c.mc_steps, "parallelism": "dp1"},
-        "elbo_per_img": round(pv.loss_value(), 5),
+        "elbo_per_img": round(elbo, 5),
+        "parity": parity,
+        "parity_value": round(value, 2) if parity else (None if alt_value is None else round(alt_value, 2)),
+        "parity_ms_per_step": round(ms, 3) if parity else (None if alt_ms is None else round(alt_ms, 3)),
+        "parity_dtype": dtype if parity else (alt if alt_value is not None else None),
+        "parity_roofline": None if parity else alt_roof,
+        "bf16_value": None if alt != "bf16" or alt_value is None else round(alt_value, 2),
+        "bf16_ms_per_step": None if alt != "bf16" or alt_ms is None else round(alt_ms, 3),
+        "bf16_roofline": alt_roof if alt == "bf16" else None,
         "head_conv_tflop_per_step": round(head_flops / 1e12, 3),
         "head_conv_tflop_method": "estimated: 3 x the counted forward convolution FLOPs (fwd + dgrad + wgrad)",
-        "roofline": None if ach is None else {
-            "bound": "mfma", "achieved": round(ach, 3), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 5), "traffic": None,
-            "kernel": "pc_conv3_kernel + pc_conv2_kernel (PixelCNN++ head forward convolutions, all instances)",
-            "timed_launches": len(probe), "avg_launch_us": round(pms * 1e3 / max(1, len(probe)), 2),
-            "step_achieved_tflops": round((head_flops + vae_flops) / (ms / 1e3) / 1e12, 3),
-            "step_achieved_method": "estimated: head FLOPs = 3 x forward convolution FLOPs"},
+        "roofline": _pv_roofline(probe, planes, head_flops, vae_flops, ms, "c_pixelvae/" + dtype),
         "cpu_baseline": None,
     }
     if not args.no_cpu_baseline:  # the fp64 CPU restatement of the same chain on a 2-image sample

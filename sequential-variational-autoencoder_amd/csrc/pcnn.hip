@@ -32,6 +32,8 @@ int hipchk() {
   svae_tls_error(std::string("HIP: ") + hipGetErrorString(e));
   return SVAE_EHIP;
 }
+#define PC_MAXPLANES 3  // operand planes of the split mode (svae_pcnn_*_planes)
+
 int blocks_for(long long n, int per = 256, int cap = 16384) {
   long long b = (n + per - 1) / per;
   if (b < 1) b = 1;
@@ -112,10 +114,19 @@ __global__ __launch_bounds__(256) void wn_norm_kernel(const float* __restrict__ 
   if (threadIdx.x == 0) norm[c] = (float)sqrt(s);
 }
 
-// W = g / norm * V -> wk_f [tap][co][kf] (K = ci) and wk_d [tap][ci][kd] (K = co), zero padded
+// W = g / norm * V -> wk_f [tap][co][kf] (K = ci) and wk_d [tap][ci][kd] (K = co), zero padded.
+// planes > 1 (the head's split mode): `planes` bf16 planes per copy, plane p at p * (copy size), with
+// W = sum_p plane_p up to the last plane's rounding (plane p = bf16 of what planes 0..p-1 left)
+__device__ __forceinline__ void wn_put(__bf16* w, long long i, long long pstride, int planes, float v) {
+  for (int p = 0; p < planes; ++p) {
+    const __bf16 b = (__bf16)v;
+    w[i + p * pstride] = b;
+    v -= (float)b;
+  }
+}
 __global__ void wn_apply_kernel(const float* __restrict__ V, const float* __restrict__ g,
                                 const float* __restrict__ norm, int taps, int cin, int cout, __bf16* wk_f, int kf,
-                                __bf16* wk_d, int kd) {
+                                __bf16* wk_d, int kd, int planes) {
   const long long nf = wk_f ? (long long)taps * cout * kf : 0, nd = wk_d ? (long long)taps * cin * kd : 0;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nf + nd; i += stride) {
@@ -125,7 +136,7 @@ __global__ void wn_apply_kernel(const float* __restrict__ V, const float* __rest
       const int co = (int)(r % cout), tap = (int)(r / cout);
       float w = 0.f;
       if (ci < cin) w = V[((long long)tap * cin + ci) * cout + co] * (g[co] / norm[co]);
-      wk_f[i] = (__bf16)w;
+      wn_put(wk_f, i, nf, planes, w);
     } else {
       const long long j = i - nf;
       const int co = (int)(j % kd);
@@ -133,7 +144,7 @@ __global__ void wn_apply_kernel(const float* __restrict__ V, const float* __rest
       const int ci = (int)(r % cin), tap = (int)(r / cin);
       float w = 0.f;
       if (co < cout) w = V[((long long)tap * cin + ci) * cout + co] * (g[co] / norm[co]);
-      wk_d[j] = (__bf16)w;
+      wn_put(wk_d, j, nd, planes, w);
     }
   }
 }
@@ -1790,13 +1801,19 @@ extern "C" {
 
 int svae_pcnn_wnorm(const float* V, const float* g, int taps, int cin, int cout, float* norm, void* wk_f, int kf,
                     void* wk_d, int kd, void* stream) {
-  if (!V || !g || !norm || taps < 1 || cin < 1 || cout < 1) return bad("pcnn_wnorm: bad arguments");
+  return svae_pcnn_wnorm_planes(V, g, taps, cin, cout, norm, wk_f, kf, wk_d, kd, 1, stream);
+}
+
+int svae_pcnn_wnorm_planes(const float* V, const float* g, int taps, int cin, int cout, float* norm, void* wk_f,
+                           int kf, void* wk_d, int kd, int planes, void* stream) {
+  if (!V || !g || !norm || taps < 1 || cin < 1 || cout < 1 || planes < 1 || planes > PC_MAXPLANES)
+    return bad("pcnn_wnorm: bad arguments");
   if ((wk_f && (kf < cin || kf % 16)) || (wk_d && (kd < cout || kd % 16))) return bad("pcnn_wnorm: bad padding");
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(wn_norm_kernel, dim3(cout), dim3(256), 0, s, V, taps * cin, cout, norm);
   const long long n = (wk_f ? (long long)taps * cout * kf : 0) + (wk_d ? (long long)taps * cin * kd : 0);
   if (n) hipLaunchKernelGGL(wn_apply_kernel, dim3(blocks_for(n)), dim3(256), 0, s, V, g, norm, taps, cin, cout,
-                            (__bf16*)wk_f, kf, (__bf16*)wk_d, kd);
+                            (__bf16*)wk_f, kf, (__bf16*)wk_d, kd, planes);
   return hipchk();
 }
 
@@ -1900,13 +1917,20 @@ static int pcnn_conv_impl(const void* x, int n, int hi, int wi, int cin, int ldx
   return hipchk();
 }
 
-int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, const void* dy, int ldd,
-                         int dy_bf16, int ho, int wo, int cout, int kh, int kw, int s, int pt, int pl, int mode, float* dW,
-                         float* dbias, float* scratch, int64_t scratch_elems, void* stream) {
+// The weight gradient as a sum of nprod operand products sum_p gather(xs[p])^T ds[p] (one product: the
+// plain bf16 gradient; the split mode's plane products, svae_pcnn_conv_wgrad_planes): every product's
+// launch writes its own ns partial slabs and ONE fixed-order reduce adds all nprod * ns of them.
+static int pcnn_wgrad_impl(const void* const* xs, const void* const* ds, int nprod, int n, int hi, int wi, int cin,
+                           int ldx, int x_bf16, int ldd, int dy_bf16, int ho, int wo, int cout, int kh, int kw, int s,
+                           int pt, int pl, int mode, float* dW, float* dbias, float* scratch, int64_t scratch_elems,
+                           void* stream) {
   const PcGeom g = make_geom(n, hi, wi, cin, ldx, ho, wo, cout, kh, kw, s, pt, pl, mode);
-  if (!x || !dy || !dW || !scratch || !geom_ok(g) || ldd < cout || ldd % 4 || cout % 4)
+  bool ok = nprod >= 1 && nprod <= PC_MAXPLANES * (PC_MAXPLANES + 1) / 2;
+  for (int p = 0; ok && p < nprod; ++p) ok = xs[p] && ds[p];
+  if (!ok || !dW || !scratch || !geom_ok(g) || ldd < cout || ldd % 4 || cout % 4)
     return bad("pcnn_wgrad: bad arguments");
   if (dy_bf16 && dbias) return bad("pcnn_wgrad: the bias gradient needs the fp32 dy (sum it upstream)");
+  if (dbias && nprod > 1) return bad("pcnn_wgrad: the bias gradient of a plane product (sum it upstream)");
   const long long rows = (long long)n * ho * wo;
   const int taps = kh * kw;
   const long long wsz = (long long)taps * cin * cout;
@@ -1924,17 +1948,23 @@ int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx,
       static const int tgt4 = svae_knob("SVAE_PW4_TARGET", 1024);  // blocks of the tap-row kernel
       long long ns = (tgt4 + tiles4 - 1) / tiles4;
       if (ns > h.nchunk) ns = h.nchunk;
-      if (ns > scratch_elems / (wsz + cout)) ns = scratch_elems / (wsz + cout);
+      if (ns > scratch_elems / (nprod * wsz + cout)) ns = scratch_elems / (nprod * wsz + cout);
       if (ns < 1) return bad("pcnn_wgrad: scratch too small");
       h.cps = (int)((h.nchunk + ns - 1) / ns);
       ns = (h.nchunk + h.cps - 1) / h.cps;
-      float* bpart = dbias ? scratch + ns * wsz : nullptr;
+      float* bpart = dbias ? scratch + nprod * ns * wsz : nullptr;
       const dim3 grid((unsigned)((cin + 63) / 64), (unsigned)((cout + 63) / 64), (unsigned)(kh * ns));
-#define PW4_L(XBV, DBV) hipLaunchKernelGGL((pc_wgrad4_kernel<XBV, DBV>), grid, dim3(256), 0, st, g4, h, x, dy, ldd, scratch, bpart)
-      if (x_bf16) { if (dy_bf16) PW4_L(true, true); else PW4_L(true, false); }
-      else { if (dy_bf16) PW4_L(false, true); else PW4_L(false, false); }
+      for (int p = 0; p < nprod; ++p) {
+        const void* x = xs[p];
+        const void* dy = ds[p];
+        float* slab = scratch + p * ns * wsz;
+#define PW4_L(XBV, DBV) hipLaunchKernelGGL((pc_wgrad4_kernel<XBV, DBV>), grid, dim3(256), 0, st, g4, h, x, dy, ldd, slab, bpart)
+        if (x_bf16) { if (dy_bf16) PW4_L(true, true); else PW4_L(true, false); }
+        else { if (dy_bf16) PW4_L(false, true); else PW4_L(false, false); }
 #undef PW4_L
-      hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(wsz)), dim3(256), 0, st, scratch, (int)ns, wsz, dW);
+      }
+      hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(wsz)), dim3(256), 0, st, scratch, (int)(nprod * ns),
+                         wsz, dW);
       if (dbias)
         hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(cout)), dim3(256), 0, st, bpart, (int)ns,
                            (long long)cout, dbias);
@@ -1947,21 +1977,113 @@ int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx,
   long long ns = (tgt1 + (long long)tiles * taps - 1) / ((long long)tiles * taps);
   const long long max_rows = (rows + 255) / 256;
   if (ns > max_rows) ns = max_rows;
-  if (ns > scratch_elems / (wsz + cout)) ns = scratch_elems / (wsz + cout);  // slabs + bias partials
+  if (ns > scratch_elems / (nprod * wsz + cout)) ns = scratch_elems / (nprod * wsz + cout);  // slabs + bias partials
   if (ns < 1) return bad("pcnn_wgrad: scratch too small");
   long long rps = (rows + ns - 1) / ns;
   rps = (rps + 63) / 64 * 64;
   ns = (rows + rps - 1) / rps;
-  float* bpart = dbias ? scratch + ns * wsz : nullptr;
+  float* bpart = dbias ? scratch + nprod * ns * wsz : nullptr;
+  for (int p = 0; p < nprod; ++p) {
+    const void* x = xs[p];
+    const void* dy = ds[p];
+    float* slab = scratch + p * ns * wsz;
 #define PW1_L(XBV, DBV) hipLaunchKernelGGL((pc_wgrad_kernel<XBV, DBV>), dim3(tiles, taps, (unsigned)ns), dim3(256), 0, st, g, x, dy, \
-                                           ldd, rows, rps, scratch, bpart)
-  if (x_bf16) { if (dy_bf16) PW1_L(true, true); else PW1_L(true, false); }
-  else { if (dy_bf16) PW1_L(false, true); else PW1_L(false, false); }
+                                           ldd, rows, rps, slab, bpart)
+    if (x_bf16) { if (dy_bf16) PW1_L(true, true); else PW1_L(true, false); }
+    else { if (dy_bf16) PW1_L(false, true); else PW1_L(false, false); }
 #undef PW1_L
-  hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(wsz)), dim3(256), 0, st, scratch, (int)ns, wsz, dW);
+  }
+  hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(wsz)), dim3(256), 0, st, scratch, (int)(nprod * ns), wsz,
+                     dW);
   if (dbias)
     hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(cout)), dim3(256), 0, st, bpart, (int)ns, (long long)cout,
                        dbias);
+  return hipchk();
+}
+
+int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, const void* dy, int ldd,
+                         int dy_bf16, int ho, int wo, int cout, int kh, int kw, int s, int pt, int pl, int mode, float* dW,
+                         float* dbias, float* scratch, int64_t scratch_elems, void* stream) {
+  return pcnn_wgrad_impl(&x, &dy, 1, n, hi, wi, cin, ldx, x_bf16, ldd, dy_bf16, ho, wo, cout, kh, kw, s, pt, pl, mode,
+                         dW, dbias, scratch, scratch_elems, stream);
+}
+
+// the split mode's products (i, j), i + j < planes, largest first: (0,0) (0,1) (1,0) (0,2) (1,1) (2,0)
+static int pc_products(int planes, int* pi, int* pj) {
+  int k = 0;
+  for (int d = 0; d < planes; ++d)
+    for (int i = 0; i <= d; ++i) {
+      pi[k] = i;
+      pj[k] = d - i;
+      ++k;
+    }
+  return k;
+}
+
+int svae_pcnn_conv_wgrad_planes(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, int64_t x_pstride,
+                                const void* dy, int ldd, int dy_bf16, int64_t dy_pstride, int planes, int ho, int wo,
+                                int cout, int kh, int kw, int s, int pt, int pl, int mode, float* dW, float* scratch,
+                                int64_t scratch_elems, void* stream) {
+  if (!x || !dy || planes < 1 || planes > PC_MAXPLANES || x_pstride < 0 || dy_pstride < 0)
+    return bad("pcnn_wgrad_planes: bad arguments");
+  int pi[PC_MAXPLANES * PC_MAXPLANES], pj[PC_MAXPLANES * PC_MAXPLANES];
+  const int np = pc_products(planes, pi, pj);
+  const void* xs[PC_MAXPLANES * PC_MAXPLANES];
+  const void* ds[PC_MAXPLANES * PC_MAXPLANES];
+  for (int p = 0; p < np; ++p) {  // (the X plane against the D plane: products (i, j) pair x_i with dy_j)
+    xs[p] = (const char*)x + (x_bf16 ? 2 : 4) * x_pstride * pi[p];
+    ds[p] = (const char*)dy + (dy_bf16 ? 2 : 4) * dy_pstride * pj[p];
+  }
+  return pcnn_wgrad_impl(xs, ds, np, n, hi, wi, cin, ldx, x_bf16, ldd, dy_bf16, ho, wo, cout, kh, kw, s, pt, pl, mode,
+                         dW, nullptr, scratch, scratch_elems, stream);
+}
+
+int svae_pcnn_conv_planes(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, int64_t x_pstride,
+                          const void* wk, int kpad, int planes, const float* bias, float* y, int ho, int wo, int cout,
+                          int ldy, int kh, int kw, int s, int pt, int pl, int mode, int accumulate, int zero_edge,
+                          void* stream) {
+  if (!x || !wk || planes < 1 || planes > PC_MAXPLANES || x_pstride < 0) return bad("pcnn_conv_planes: bad arguments");
+  int pi[PC_MAXPLANES * PC_MAXPLANES], pj[PC_MAXPLANES * PC_MAXPLANES];
+  const int np = pc_products(planes, pi, pj);
+  const long long wst = (long long)kh * kw * cout * kpad;  // one weight plane (wk [tap][cout][kpad])
+  NlbArgs nlb{};
+  for (int p = 0; p < np; ++p) {  // the first product writes (or accumulates) with the bias, the rest add
+    const void* xp = (const char*)x + (x_bf16 ? 2 : 4) * x_pstride * pi[p];
+    const __bf16* wp = (const __bf16*)wk + wst * pj[p];
+    const int rc = pcnn_conv_impl(xp, n, hi, wi, cin, ldx, x_bf16, wp, kpad, p ? nullptr : bias, y, ho, wo, cout, ldy,
+                                  kh, kw, s, pt, pl, mode, p ? 1 : accumulate, zero_edge, nlb, stream);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+// x [rows][ldx] fp32 -> `planes` planes [rows][ldo] (plane p at p * rows * ldo, fp32 or bf16): plane p = bf16
+// of what planes 0..p-1 left of x; stored fp32, the last plane keeps the exact remainder (a kernel that
+// reads it as an MFMA operand rounds it to bf16 itself)
+__global__ void split_planes_kernel(const float* __restrict__ x, long long rows, int c, int ldx, int planes,
+                                    void* __restrict__ out, int ldo, int out_bf16) {
+  const long long n = rows * c, pst = rows * ldo;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const long long r = i / c;
+    const int ch = (int)(i - r * c);
+    float v = x[r * ldx + ch];
+    const long long o = r * ldo + ch;
+    for (int p = 0; p < planes; ++p) {
+      const __bf16 b = (__bf16)v;
+      if (out_bf16) ((__bf16*)out)[o + p * pst] = b;
+      else ((float*)out)[o + p * pst] = p == planes - 1 ? v : (float)b;
+      v -= (float)b;
+    }
+  }
+}
+
+int svae_pcnn_split_planes(const float* x, int64_t rows, int c, int ldx, int planes, void* out, int ldo, int out_bf16,
+                           void* stream) {
+  if (!x || !out || rows < 1 || c < 1 || ldx < c || ldo < c || planes < 1 || planes > PC_MAXPLANES)
+    return bad("pcnn_split_planes: bad arguments");
+  hipLaunchKernelGGL(split_planes_kernel, dim3(blocks_for(rows * c)), dim3(256), 0, (hipStream_t)stream, x,
+                     (long long)rows, c, ldx, planes, out, ldo, out_bf16);
   return hipchk();
 }
 

@@ -152,7 +152,7 @@ class PixelCNNpp:
     """Conditional PixelCNN++ on libsvae_hip.so.  One instance owns its parameters, gradients,
     Adam moments and Polyak averages (flat fp32 device buffers)."""
 
-    def __init__(self, spec, params=None, seed=0, device="cuda", scratch_elems=1 << 26):
+    def __init__(self, spec, params=None, seed=0, device="cuda", scratch_elems=1 << 26, planes=1):
         if not torch.cuda.is_available():
             raise RuntimeError("PixelCNNpp needs a GPU (HIP kernels in libsvae_hip.so); there is no CPU fallback")
         self.s = spec
@@ -189,6 +189,13 @@ class PixelCNNpp:
         # bias gradients summed in fp32 by the op that writes them)
         self.bf16_grads = os.environ.get("SVAE_PC_BF16_GRADS", "0") == "1"  # opt-in: measured slower (804 vs 882 img/s)
         self._nl_src, self._bias_of, self._bf16_grad = {}, {}, set()
+        # operand planes of the conv / nin GEMMs: 1 = bf16 MFMA operands; 3 = the split mode (include/svae_pcnn.h:
+        # every operand a sum of 3 bf16 planes, 6 plane products per GEMM: fp32-grade, nn.py:189-252 in fp32)
+        if planes not in (1, 2, 3):
+            raise ValueError("planes must be 1 (bf16), 2 or 3 (split)")
+        self.planes = planes
+        if planes > 1:  # every activation and gradient stays fp32 (split into planes at each GEMM)
+            self.bf16_grads = False
         self.probe, self.probe_cap = None, 0  # [(flops, event, event)] of timed forward conv launches
         self.conv_flops = 0.0  # running total of forward conv FLOPs (tools/bench_pcnn.py)
 
@@ -299,11 +306,13 @@ class PixelCNNpp:
         off_g, _, _ = self.table[name + "/g"]
         off_b, _, _ = self.table[name + "/b"]
         kf, kd = _r16(cin), _r16(cout)
+        P = self.planes
         norm = torch.empty(cout, dtype=torch.float32, device=self.dev)
-        wkf = torch.empty(taps * cout * kf, dtype=torch.bfloat16, device=self.dev)
-        wkd = torch.empty(taps * cin * kd, dtype=torch.bfloat16, device=self.dev)
-        _ck(L.svae_pcnn_wnorm(_p(self.P, off_v), _p(self.P, off_g), taps, cin, cout, _p(norm), _p(wkf), kf,
-                              ctypes.c_void_p(wkd.data_ptr()), kd, st))
+        wkf = torch.empty(P * taps * cout * kf, dtype=torch.bfloat16, device=self.dev)
+        wkd = torch.empty(P * taps * cin * kd, dtype=torch.bfloat16, device=self.dev)
+        _ck(L.svae_pcnn_wnorm_planes(_p(self.P, off_v), _p(self.P, off_g), taps, cin, cout, _p(norm), _p(wkf), kf,
+                                     ctypes.c_void_p(wkd.data_ptr()), kd, P, st))
+        xs = self._planes(x) if P > 1 else None  # (the split mode's operand planes of x, kept for the backward)
         if ho is None:
             ho, wo = (x.h - 1) // s + 1, (x.w - 1) // s + 1
         # algorithmic FLOPs of the forward gather GEMM (valid taps only for the stride-2 deconvs)
@@ -315,9 +324,8 @@ class PixelCNNpp:
         if pr:  # bench.py's live roofline probe: an event pair around this forward conv launch
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        _ck(L.svae_pcnn_conv(x.ptr(), x.n, x.h, x.w, cin, x.ld, int(x.bf), ctypes.c_void_p(wkf.data_ptr()), kf,
-                             _p(self.P, off_b), out.ptr(), ho, wo, cout, out.ld, kh, kw, s, pt, pl, mode,
-                             1 if acc else 0, zero_edge, st))
+        self._conv(x, xs, wkf, kf, _p(self.P, off_b), out.ptr(), ho, wo, cout, out.ld, kh, kw, s, pt, pl, mode,
+                   1 if acc else 0, zero_edge)
         if pr:
             e1.record()
             self.probe.append((2.0 * x.n * ho * wo * cout * cin * taps / (s * s if mode == 1 else 1), e0, e1))
@@ -326,18 +334,43 @@ class PixelCNNpp:
             src = out
             if acc or zero_edge:
                 src = Act(self._new(x.n * ho * wo, cout), cout, x.n, ho, wo)
-                _ck(L.svae_pcnn_conv(x.ptr(), x.n, x.h, x.w, cin, x.ld, int(x.bf), ctypes.c_void_p(wkf.data_ptr()), kf,
-                                     _p(self.P, off_b), src.ptr(), ho, wo, cout, cout, kh, kw, s,
-                                     pt - (zero_edge == 1), pl - (zero_edge == 2), mode, 0, 0, st))
+                self._conv(x, xs, wkf, kf, _p(self.P, off_b), src.ptr(), ho, wo, cout, cout, kh, kw, s,
+                           pt - (zero_edge == 1), pl - (zero_edge == 2), mode, 0, 0)
             _ck(L.svae_pcnn_wn_init(src.ptr(), src.rows, cout, src.ld, float(init_scale), _p(self.P, off_g),
                                     _p(self.P, off_b), _p(self.scratch), st))
         if self._record:
             geo = (kh, kw, s, pt, pl, mode, zero_edge, kf, kd, off_v, off_g, off_b)
-            self._tape.append(lambda: self._wconv_bwd(x, out, norm, wkd, geo))
+            self._tape.append(lambda: self._wconv_bwd(x, out, norm, wkd, geo, xs))
             self._bias_of.setdefault(id(self._root(out)), []).append(off_b)  # (every conv summed into it)
         return out
 
-    def _wconv_bwd(self, x, y, norm, wkd, geo):
+    def _planes(self, a):
+        """The split mode's operand planes of activation (or [rows][c] gradient) ``a``: (buffer, ld, bf16 flag,
+        plane stride) -- bf16 planes where the bf16-operand kernels take them (c % 8 == 0), else fp32 ones."""
+        if isinstance(a, Act):
+            assert not a.bf, "split mode: activations are fp32"
+            src, rows, c, ld = a.ptr(), a.rows, a.c, a.ld
+        else:
+            assert a.dtype == torch.float32 and a.is_contiguous()
+            src, rows, c, ld = _p(a), a.shape[0], a.shape[1], a.shape[1]
+        bf = c % 8 == 0
+        out = torch.empty(self.planes * rows * c, dtype=torch.bfloat16 if bf else torch.float32, device=self.dev)
+        _ck(self.L.svae_pcnn_split_planes(src, rows, c, ld, self.planes, ctypes.c_void_p(out.data_ptr()), c, int(bf),
+                                          self._st()))
+        return out, c, int(bf), rows * c
+
+    def _conv(self, x, xs, wk, kpad, bias, y, ho, wo, cout, ldy, kh, kw, s, pt, pl, mode, acc, zero_edge):
+        """One gather conv of ``x`` (an Act; ``xs`` its split-mode planes, or None) with the weight copy ``wk``."""
+        if xs is None:
+            _ck(self.L.svae_pcnn_conv(x.ptr(), x.n, x.h, x.w, x.c, x.ld, int(x.bf), ctypes.c_void_p(wk.data_ptr()), kpad,
+                                      bias, y, ho, wo, cout, ldy, kh, kw, s, pt, pl, mode, acc, zero_edge, self._st()))
+            return
+        buf, ld, bf, pst = xs
+        _ck(self.L.svae_pcnn_conv_planes(ctypes.c_void_p(buf.data_ptr()), x.n, x.h, x.w, x.c, ld, bf, pst,
+                                         ctypes.c_void_p(wk.data_ptr()), kpad, self.planes, bias, y, ho, wo, cout, ldy,
+                                         kh, kw, s, pt, pl, mode, acc, zero_edge, self._st()))
+
+    def _wconv_bwd(self, x, y, norm, wkd, geo, xs=None):
         L = self.L
         st = self._st()
         kh, kw, s, pt, pl, mode, zero_edge, kf, kd, off_v, off_g, off_b = geo
@@ -349,6 +382,9 @@ class PixelCNNpp:
             _ck(L.svae_pcnn_mask_edge(_p(dy), y.n, y.h, y.w, cout, cout, zero_edge, st))
         dW = torch.empty(taps * cin * cout, dtype=torch.float32, device=self.dev)
         sc = self.scratch
+        if xs is not None:
+            self._wconv_bwd_split(x, y, dy, norm, wkd, geo, xs, dW)
+            return
         # dW and (fp32 dy) the bias gradient, written into G, from one pass over dy
         _ck(L.svae_pcnn_conv_wgrad(x.ptr(), x.n, x.h, x.w, cin, x.ld, int(x.bf), ctypes.c_void_p(dy.data_ptr()), cout,
                                    int(dyb), y.h, y.w, cout, kh, kw, s, pt, pl, mode, _p(dW),
@@ -374,6 +410,29 @@ class PixelCNNpp:
                              ctypes.c_void_p(wkd.data_ptr()), kd, None, _p(dx), x.h, x.w, cin, cin, kh, kw, s, pt, pl,
                              1 - mode, dacc, 0, st))
 
+    def _wconv_bwd_split(self, x, y, dy, norm, wkd, geo, xs, dW):
+        """_wconv_bwd in the split mode: dW and the input gradient as plane-product sums over the planes of x
+        and of dy (fp32; the bias gradient its column sums)."""
+        L = self.L
+        st = self._st()
+        kh, kw, s, pt, pl, mode, zero_edge, kf, kd, off_v, off_g, off_b = geo
+        taps, cin, cout = kh * kw, x.c, y.c
+        ds, dld, dbf, dpst = self._planes(dy)
+        xb, xld, xbf, xpst = xs
+        sc = self.scratch
+        _ck(L.svae_pcnn_colsum(_p(dy), y.rows, cout, cout, 0, 0, 0, _p(self.G, off_b), 0, _p(sc), st))
+        _ck(L.svae_pcnn_conv_wgrad_planes(ctypes.c_void_p(xb.data_ptr()), x.n, x.h, x.w, cin, xld, xbf, xpst,
+                                          ctypes.c_void_p(ds.data_ptr()), dld, dbf, dpst, self.planes, y.h, y.w, cout,
+                                          kh, kw, s, pt, pl, mode, _p(dW), _p(sc), sc.numel(), st))
+        _ck(L.svae_pcnn_wnorm_bwd(_p(self.P, off_v), _p(self.P, off_g), _p(norm), _p(dW), taps, cin, cout,
+                                  _p(self.G, off_v), _p(self.G, off_g), st))
+        if id(x) in self._nograd:
+            return
+        dx, dacc = self._gout(x)
+        _ck(L.svae_pcnn_conv_planes(ctypes.c_void_p(ds.data_ptr()), y.n, y.h, y.w, cout, dld, dbf, dpst,
+                                    ctypes.c_void_p(wkd.data_ptr()), kd, self.planes, None, _p(dx), x.h, x.w, cin, cin,
+                                    kh, kw, s, pt, pl, 1 - mode, dacc, 0, st))
+
     def _dense(self, x, name, cout, init_scale=1.0):
         """nn.nin / dense over the channel axis (nn.py:255-260): a 1x1 gather GEMM over every pixel."""
         y = self._wconv(self._view(x, x.rows, 1, 1), name, cout, 1, 1, 1, 0, 0, init_scale=init_scale)
@@ -385,7 +444,7 @@ class PixelCNNpp:
         the conv result is bitwise the one from fp32 storage (nn.py:270-274: dropout before the conv)."""
         k = NL_KIND[kind]
         c = 2 * x.c if k == 2 else x.c
-        bf = c % 8 == 0 and x.c % 4 == 0 and x.ld % 4 == 0
+        bf = self.planes == 1 and c % 8 == 0 and x.c % 4 == 0 and x.ld % 4 == 0
         buf = torch.empty(x.rows, c, dtype=torch.bfloat16 if bf else torch.float32, device=self.dev)
         y = Act(buf, c, x.n, x.h, x.w)
         if isinstance(mask, DropMask):  # drawn in the kernel from (seed, keep)
@@ -393,7 +452,7 @@ class PixelCNNpp:
         else:
             mp, keep, seed = _p(mask), 1.0, 0
         _ck(self.L.svae_pcnn_nonlin(x.ptr(), x.rows, x.c, x.ld, k, mp, keep, seed, y.ptr(), y.ld, int(bf), self._st()))
-        if self._record and k != 2 and self.fuse_act_bwd:  # its consuming conv applies f' (svae_pcnn_conv_act_bwd)
+        if self._record and k != 2 and self.fuse_act_bwd and self.planes == 1:  # its consuming conv applies f' (svae_pcnn_conv_act_bwd)
             self._nl_src[id(y)] = (x, k, mp, keep, seed)
             self._keep.append(x)
         if self._record:

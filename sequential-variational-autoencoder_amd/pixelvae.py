@@ -42,7 +42,7 @@ from .sequential_vae import SequentialVAE
 
 class PixelVAE:
     def __init__(self, config="c_pixelvae", batch_size=None, seed=0, head=None, dropout_p=0.3, polyak_decay=0.9995,
-                 init_every_step=False, **over):
+                 init_every_step=False, head_planes=None, **over):
         cfg = preset(config, **over) if isinstance(config, str) else config
         if batch_size is not None:
             cfg = replace(cfg, batch=batch_size)
@@ -55,7 +55,12 @@ class PixelVAE:
         self.vae = SequentialVAE(cfg, seed=seed)
         hs = dict(nr_resnet=3, nr_filters=160, nr_mix=10, nonlinearity="relu")  # pixelvae.py:54-63
         hs.update(head or {})
-        self.head = PixelCNNpp(make_spec(H=cfg.height, W=cfg.width, C=3, K=cfg.latent_dim, **hs), seed=seed + 1)
+        # the head's GEMM operands: bf16 (1 plane), or the split mode's 3 bf16 planes (fp32-grade) -- by default
+        # the split mode with the engine's split dtype, so dtype "bf16x6" is an fp32-accurate step end to end
+        if head_planes is None:
+            head_planes = 3 if cfg.dtype == "bf16x6" else 1
+        self.head = PixelCNNpp(make_spec(H=cfg.height, W=cfg.width, C=3, K=cfg.latent_dim, **hs), seed=seed + 1,
+                               planes=head_planes)
         self.L = self.vae.L
         self.dev = self.vae.device
         self.e = e

@@ -4,8 +4,9 @@ PARITY UNPINNED: the reference glue cannot run, see that module's header).
 
 Small geometry (16x16, a 4-level ladder, a 1-resnet 8-filter head with 2 mixtures), B = 4, T = 2,
 shared theta / phi, injected eps, sampler uniforms and dropout keep-masks (p = 0.3).  The engine
-runs fp32 (parity mode); the head is bf16 MFMA (its only mode), compared against the oracle with
-the same bf16 operand rounding.  Bounds:
+runs fp32 (parity mode); the head runs bf16 MFMA, compared against the oracle with the same bf16
+operand rounding, and (test_pixelvae_split_head_matches_fp64) in its fp32-grade split mode against the
+unrounded fp64 oracle.  Bounds of the bf16 head:
   loss, step-0 recon / KL, x_hat_0          : 1e-4 rel (the engine's fp32 bounds)
   x_hat_1 (the head's highway output)         : 1e-3 rel L2
   engine gradients (via d/dz_1, d/dx_hat_0)   : vector 2e-2, per-tensor median 1e-2 (the head's
@@ -31,9 +32,9 @@ def _rel(a, b):
     return float(np.linalg.norm(np.ravel(a) - np.ravel(b)) / max(np.linalg.norm(np.ravel(b)), 1e-30))
 
 
-def _setup(dtype="fp32", seed=0):
+def _setup(dtype="fp32", seed=0, head_planes=1):
     PV = pkg_mod("pixelvae").PixelVAE
-    pv = PV("c_pixelvae", head=HEAD, seed=seed, dtype=dtype, **GEO)
+    pv = PV("c_pixelvae", head=HEAD, seed=seed, dtype=dtype, head_planes=head_planes, **GEO)
     c = pv.cfg
     cd = spec.make_config("tiny", H=16, W=16, C=3, levels=4, filter_sizes=GEO["filter_sizes"],
                           latent_dims=GEO["latent_dims"], mc_steps=2, batch=4, latent_mean_clip=4.0,
@@ -87,6 +88,40 @@ def test_pixelvae_step_matches_oracle():
     names = [p["name"] for p in pv.vae.table]
     assert not any("encoder" in n or "generative_network" in n for n in names)
     assert any(n.startswith("phi/inference_network/") for n in names)
+    pv.close()
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16x6"])
+def test_pixelvae_split_head_matches_fp64(dtype):
+    """The head's split mode (3 bf16 planes per operand, 6 plane products: include/svae_pcnn.h) with an
+    fp32-grade engine (fp32, or bf16x6 whose default head is the split one) against the UNROUNDED fp64
+    oracle (bf16_head=False): x_hat_1 <= 1e-4 and the head gradients <= 1e-3, the
+    engine gradients <= 1e-3 (they now see an fp32-grade d/dz_1)."""
+    pv, cd, ospec, hp, x, tgt, eps, u_mix, u_log, rng = _setup(dtype=dtype, head_planes=3 if dtype == "fp32" else None)
+    assert pv.head.planes == 3
+    pv.forward(x, tgt, eps, 0.6, u_mix, u_log)
+    masks = _masks(rng, pv)
+    pv.forward(x, tgt, eps, 0.6, u_mix, u_log, masks=masks)
+    pv.backward()
+    torch.cuda.synchronize()
+    loss = pv.loss_value()
+    x0, x1 = pv.xhat(0).cpu().numpy(), pv.xhat(1).cpu().numpy()
+    g_eng = pv.vae.grad_dict()
+    g_head = pv.head.grads()
+    o = opv.forward_backward(cd, pv.vae.param_dict(), ospec, hp, x, tgt, eps, 0.6, u_mix, u_log, masks,
+                             bf16_head=False)
+    el = abs(loss - o["loss"]) / abs(o["loss"])
+    e0, e1 = _rel(x0, o["xhat"][0]), _rel(x1, o["xhat"][1])
+    live = [k for k, v in o["grads"].items() if np.linalg.norm(v) > 1e-7]
+    cat = lambda d, ks: np.concatenate([np.ravel(d[k]) for k in ks])
+    gv = _rel(cat(g_eng, live), cat(o["grads"], live))
+    hlive = [k for k, v in o["head_grads"].items() if np.linalg.norm(v) > 1e-9]
+    hv = _rel(cat(g_head, hlive), cat(o["head_grads"], hlive))
+    hw = max(_rel(g_head[k], o["head_grads"][k]) for k in hlive)
+    print("\nc_pixelvae split head (%s engine): loss rel %.2e; x_hat_0 %.2e x_hat_1 %.2e; engine grads %.2e; head "
+          "grads vector %.2e worst tensor %.2e" % (dtype, el, e0, e1, gv, hv, hw))
+    assert el <= 1e-5 and e0 <= 1e-4 and e1 <= 1e-4
+    assert gv <= 1e-3 and hv <= 1e-3
     pv.close()
 
 
