@@ -26,21 +26,22 @@ PKG = "sequential-variational-autoencoder_amd"
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no 2:1 sparsity)
-# dominant kernel of the bf16 step (profiles/r0*_kernel_stats.txt: the largest total time): the
-# wave-split halo gather-GEMM igemm_halo_kw_kernel (every forward / input-gradient conv of the main
-# stream, the critical path; csrc/halo_kw.hip).  The stride-1 halo weight-GEMM (side stream,
-# wgrad_halo2_kernel) is reported as the secondary entry.
-DOMINANT_KID = "KID_HALO_KW"
-# the parity-grade (bf16x6) step's dominant kernel: the fp16-plane wave-split gather (csrc/halo_x3.hip)
+# dominant kernel of both steps (profiles/r05_f6_kernel_stats.txt, r05_fbf_kernel_stats.txt: the largest
+# total time): the wave-split halo gather gather_x3_kernel (csrc/halo_x3.hip; every forward / input-gradient
+# conv with >= 1 channel chunk on the main stream, the critical path) -- on scaled fp16 hi/lo planes in the
+# split mode, bf16 in the bf16 mode.  The stride-1 halo weight-GEMM (side stream, wgrad_halo2_kernel) is
+# reported as the secondary entry.
+DOMINANT_KID = "KID_HALO_X3"
 DOMINANT_KID_SPLIT = "KID_HALO_X3"
 SECONDARY_KID = "KID_WHALO2_S1"
 # PMC summaries (tools/pmc_traffic.py: FETCH_SIZE / WRITE_SIZE passes of the same bench command, calibrated
 # FETCH rules) per workload; a workload never borrows another's traffic (LSUN read CelebA's)
 PMC_FILES = {
-    "celeba/bf16": ["profiles/r04_final_pmc_traffic.json", "profiles/r04_v1_pmc_traffic.json", "profiles/r03_v5_pmc_traffic.json"],
-    "celeba/bf16x6": ["profiles/r04_final_x6_pmc_traffic.json", "profiles/r04_v1_x6_pmc_traffic.json"],
+    "celeba/bf16": ["profiles/r05_fbf_pmc_traffic.json", "profiles/r04_final_pmc_traffic.json"],
+    "celeba/bf16x6": ["profiles/r05_f6_pmc_traffic.json", "profiles/r04_final_x6_pmc_traffic.json"],
     "lsun/bf16": ["profiles/r04_final_lsun_pmc_traffic.json", "profiles/r04_v1_lsun_pmc_traffic.json"],
     "c_pixelvae/bf16": ["profiles/r04_final_pv_pmc_traffic.json", "profiles/r04_v1_pv_pmc_traffic.json"],
+    "c_pixelvae/bf16x6": ["profiles/r05_fpv_pmc_traffic.json"],
 }
 
 
@@ -302,20 +303,21 @@ def _pv_throughput(PV, B, dtype, steps, warmup, probe_cap):
 def _pv_roofline(probe, planes, head_flops, vae_flops, ms, key):
     """The head's forward convolutions (event pairs around each probed launch): algorithmic FLOPs per
     second; in the split mode one algorithmic conv is 6 plane-product launches (issued = 6 x achieved)."""
-    pflops = sum(f for f, _, _ in probe)
-    pms = sum(e0.elapsed_time(e1) for _, e0, e1 in probe)
+    pflops = sum(f for f, _, _, _ in probe)
+    iflops = sum(f * k for f, _, _, k in probe)  # the MFMA work the plane products really run
+    pms = sum(e0.elapsed_time(e1) for _, e0, e1, _ in probe)
     if pms <= 0:
         return None
     ach = pflops / (pms / 1e3) / 1e12
-    nprod = planes * (planes + 1) // 2
     kern = "pc_conv3_kernel + pc_conv2_kernel"
     traffic, tsrc = pmc_traffic(kern, key)
     return {"bound": "mfma", "achieved": round(ach, 3), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 5), "traffic": traffic, "traffic_source": tsrc,
             "traffic_unit": "HBM bytes per launch (PMC, family average)",
             "kernel": kern + " (PixelCNN++ head forward convolutions, all instances%s)"
-                      % (", %d plane-product launches per conv" % nprod if nprod > 1 else ""),
-            "issued": round(ach * nprod, 3), "frac_issued": round(ach * nprod / BF16_MFMA_PEAK_TFLOPS, 5),
+                      % (", split mode: 3 fp16 plane products per conv (6 bf16 ones where channels %% 8 != 0)"
+                         if planes > 1 else ""),
+            "issued": round(ach * iflops / pflops, 3), "frac_issued": round(ach * iflops / pflops / BF16_MFMA_PEAK_TFLOPS, 5),
             "timed_convs": len(probe), "avg_conv_us": round(pms * 1e3 / max(1, len(probe)), 2),
             "step_achieved_tflops": round((head_flops + vae_flops) / (ms / 1e3) / 1e12, 3),
             "step_achieved_method": "estimated: head FLOPs = 3 x forward convolution FLOPs"}
@@ -358,7 +360,7 @@ def run_pixelvae(args, cfgmod):
         "metric": METRIC["c_pixelvae"][0], "value": round(value, 2), "unit": "images/sec", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
-        "dtype": dtype + (" engine, 3-plane split head (6 bf16-MFMA products per GEMM)" if planes > 1
+        "dtype": dtype + (" engine, split head (scaled fp16 hi/lo planes: 3 fp16-MFMA products per GEMM)" if planes > 1
                           else " engine, bf16-MFMA head"),
         "data": "synthetic U[-1,1] NHWC batch, target=input, eps / sampler uniforms / dropout masks on device",
         "config": {"workload": METRIC["c_pixelvae"][1], "model": "c_pixelvae", "global_batch": B, "per_gpu_batch": B,

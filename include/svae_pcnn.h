@@ -62,34 +62,38 @@ int svae_pcnn_conv_act_bwd(const float* dy, int n, int hi, int wi, int cin, int 
 int svae_pcnn_conv_wgrad(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, const void* dy, int ldd,
                          int dy_bf16, int ho, int wo, int cout, int kh, int kw, int s, int pt, int pl, int mode, float* dW,
                          float* dbias, float* scratch, int64_t scratch_elems, void* stream);
-/* ---- split mode (fp32-grade head, pixelvae dtype "bf16x6"): operands as sums of bf16 planes ----
- * A value v is held as `planes` bf16 planes p_0 + p_1 + ... (p_k = bf16 of what p_0..p_{k-1} left of v:
- * 8 more mantissa bits per plane; 3 planes hold an fp32 value to its last bit or two).  A product
- * x . w is the sum of the plane products x_i . w_j with i + j < planes (3 planes: 6 products, the
- * dropped terms below 2^-24 of the result), each a bf16-MFMA launch of the kernels above (fp32
- * accumulate), largest first.  Replaces the fp32 tf.nn.conv2d / conv2d_transpose / matmul of
- * nn.py:189-252 to fp32 accuracy.
+/* ---- split mode (fp32-grade head, pixelvae dtype "bf16x6"): operands as sums of 16-bit planes ----
+ * Two plane formats replace the fp32 tf.nn.conv2d / conv2d_transpose / matmul of nn.py:189-252:
+ *  - fp16 (h16_scale / x_scale / w_scale given, planes = 2): a tensor scaled by 2^s (s: max|v| 2^s in
+ *    [2^14, 2^15), computed on the device) as h0 = fp16(v 2^s), h1 = fp16(v 2^s - h0): 22 significant
+ *    bits; a product is h0.h0' + h0.h1' + h1.h0' (3 fp16-MFMA launches) times 2^-(s + s').  A scale
+ *    buffer is 2 floats: [0] <- 2^-s, [1] scratch (max|v|).  Needs 16-bit storage (channels % 8 == 0).
+ *  - bf16 (no scales, planes 1..3): p_k = bf16 of what p_0..p_{k-1} left of v (8 bits per plane); a
+ *    product is the sum over i + j < planes of x_i . w_j (3 planes: 6 launches, fp32-grade).  Any shape.
+ * Every launch is one of the bf16 / fp16-MFMA kernels above (fp32 accumulate), largest product first.
  * svae_pcnn_wnorm_planes: svae_pcnn_wnorm writing `planes` planes per copy (plane p of wk_f at
- *   p * taps*cout*kf, of wk_d at p * taps*cin*kd). */
+ *   p * taps*cout*kf, of wk_d at p * taps*cin*kd); h16_scale: the fp16 format (planes = 2). */
 int svae_pcnn_wnorm_planes(const float* V, const float* g, int taps, int cin, int cout, float* norm, void* wk_f,
-                           int kf, void* wk_d, int kd, int planes, void* stream);
-/* x [rows][ldx] fp32 -> planes [rows][ldo] at plane stride rows*ldo, bf16 (out_bf16 = 1) or fp32 (the
- * last fp32 plane keeps the exact remainder, which the consuming kernel rounds to bf16). */
+                           int kf, void* wk_d, int kd, int planes, float* h16_scale, void* stream);
+/* x [rows][ldx] fp32 -> planes [rows][ldo] at plane stride rows*ldo: bf16 (out_bf16 = 1) or fp32 (the last
+ * fp32 plane keeps the exact remainder, which the consuming kernel rounds to bf16); h16_scale: the two
+ * scaled fp16 planes (planes = 2, out_bf16 = 1: 16-bit storage). */
 int svae_pcnn_split_planes(const float* x, int64_t rows, int c, int ldx, int planes, void* out, int ldo, int out_bf16,
-                           void* stream);
-/* svae_pcnn_conv over plane operands: x planes at x_pstride elements apart (fp32, or bf16 with x_bf16),
- * wk `planes` planes of [tap][cout][kpad]; the products (i, j), i + j < planes, accumulate into y. */
+                           float* h16_scale, void* stream);
+/* svae_pcnn_conv over plane operands: x planes at x_pstride elements apart (fp32, or 16-bit with x_bf16),
+ * wk `planes` planes of [tap][cout][kpad]; x_scale / w_scale (both or neither): the fp16 format. */
 int svae_pcnn_conv_planes(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, int64_t x_pstride,
-                          const void* wk, int kpad, int planes, const float* bias, float* y, int ho, int wo, int cout,
-                          int ldy, int kh, int kw, int s, int pt, int pl, int mode, int accumulate, int zero_edge,
-                          void* stream);
-/* svae_pcnn_conv_wgrad over plane operands (x planes x_pstride apart, dy planes dy_pstride apart): every
- * product's partial slabs go to scratch and one fixed-order reduce writes dW.  No bias gradient (its
- * column sum is svae_pcnn_colsum of the fp32 dy). */
+                          const void* wk, int kpad, int planes, const float* x_scale, const float* w_scale,
+                          const float* bias, float* y, int ho, int wo, int cout, int ldy, int kh, int kw, int s, int pt,
+                          int pl, int mode, int accumulate, int zero_edge, void* stream);
+/* svae_pcnn_conv_wgrad over plane operands (x planes x_pstride apart, dy planes dy_pstride apart; x_scale /
+ * dy_scale: the fp16 format): every product's partial slabs go to scratch and one fixed-order reduce
+ * writes dW.  No bias gradient (its column sum is svae_pcnn_colsum of the fp32 dy). */
 int svae_pcnn_conv_wgrad_planes(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, int64_t x_pstride,
-                                const void* dy, int ldd, int dy_bf16, int64_t dy_pstride, int planes, int ho, int wo,
-                                int cout, int kh, int kw, int s, int pt, int pl, int mode, float* dW, float* scratch,
-                                int64_t scratch_elems, void* stream);
+                                const void* dy, int ldd, int dy_bf16, int64_t dy_pstride, int planes,
+                                const float* x_scale, const float* dy_scale, int ho, int wo, int cout, int kh, int kw,
+                                int s, int pt, int pl, int mode, float* dW, float* scratch, int64_t scratch_elems,
+                                void* stream);
 /* column sums over rows (bias gradients): out[c] (+)= sum_r x[r][c]; mask_edge 1 / 2 skips
  * rows with oy == 0 / ox == 0 of a [n][ho][wo] row space (the zeroed shifted outputs). */
 int svae_pcnn_colsum(const float* x, int64_t rows, int c, int ldx, int ho, int wo, int mask_edge, float* out,

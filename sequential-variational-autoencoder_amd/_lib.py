@@ -135,12 +135,12 @@ def _load(path):
                                     i32, i32, i32, vp, i32, i32, vp, f32, u64, vp], i32),
         "svae_pcnn_conv_wgrad": ([vp, i32, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32,
                                   i32, i32, vp, vp, vp, i64, vp], i32),
-        "svae_pcnn_wnorm_planes": ([vp, vp, i32, i32, i32, vp, vp, i32, vp, i32, i32, vp], i32),
-        "svae_pcnn_split_planes": ([vp, i64, i32, i32, i32, vp, i32, i32, vp], i32),
-        "svae_pcnn_conv_planes": ([vp, i32, i32, i32, i32, i32, i32, i64, vp, i32, i32, vp, vp, i32, i32, i32, i32,
-                                   i32, i32, i32, i32, i32, i32, i32, i32, vp], i32),
-        "svae_pcnn_conv_wgrad_planes": ([vp, i32, i32, i32, i32, i32, i32, i64, vp, i32, i32, i64, i32, i32, i32,
-                                         i32, i32, i32, i32, i32, i32, i32, vp, vp, i64, vp], i32),
+        "svae_pcnn_wnorm_planes": ([vp, vp, i32, i32, i32, vp, vp, i32, vp, i32, i32, vp, vp], i32),
+        "svae_pcnn_split_planes": ([vp, i64, i32, i32, i32, vp, i32, i32, vp, vp], i32),
+        "svae_pcnn_conv_planes": ([vp, i32, i32, i32, i32, i32, i32, i64, vp, i32, i32, vp, vp, vp, vp, i32, i32,
+                                   i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp], i32),
+        "svae_pcnn_conv_wgrad_planes": ([vp, i32, i32, i32, i32, i32, i32, i64, vp, i32, i32, i64, i32, vp, vp, i32,
+                                         i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, i64, vp], i32),
         "svae_pcnn_colsum": ([vp, i64, i32, i32, i32, i32, i32, vp, i32, vp, vp], i32),
         "svae_pcnn_mask_edge": ([vp, i32, i32, i32, i32, i32, i32, vp], i32),
         "svae_pcnn_nonlin": ([vp, i64, i32, i32, i32, vp, f32, u64, vp, i32, i32, vp], i32),

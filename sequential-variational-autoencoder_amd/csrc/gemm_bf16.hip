@@ -1560,7 +1560,7 @@ const char* kernel_name(int kid) {
       "wgrad_halo2_kernel (stride-1 halo weight-GEMM, all S = 1 instances)",
       "igemm_halo_kw_kernel (small-image gather-GEMM, K split over waves, all instances)",
       "wgrad_halo2_kernel (stride-2 halo weight-GEMM, all instances)",
-      "gather_x3_kernel (split mode: fp16-plane wave-split gather, all instances)"};
+      "gather_x3_kernel (wave-split halo gather: fp16 hi/lo planes in split mode, bf16 in bf16 mode; all instances)"};
   return (kid >= 0 && kid < KID_COUNT) ? names[kid] : "none";
 }
 

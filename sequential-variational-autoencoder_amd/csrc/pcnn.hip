@@ -21,6 +21,24 @@ namespace {
 typedef __bf16 pc_bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 pc_bf16x4 __attribute__((ext_vector_type(4)));
 typedef float pc_f32x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 pc_f16x8 __attribute__((ext_vector_type(8)));
+
+// H: the 16-bit operand lanes hold fp16 bits (the split mode's scaled hi / lo planes), else bf16
+template <bool H>
+__device__ __forceinline__ f32x16 pc_mfma(pc_bf16x8 a, pc_bf16x8 b, f32x16 c) {
+  if constexpr (H)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(pc_f16x8, a), __builtin_bit_cast(pc_f16x8, b), c,
+                                                  0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+// the fp16 planes' inverse scales (svae_pcnn.h: a[0] of the x planes, b[0] of the weight / dy planes):
+// a product of two scaled fp16 operands is multiplied by a[0] * b[0] (exact powers of two)
+struct PcScale {
+  const float* a;
+  const float* b;
+};
+__device__ __forceinline__ float pc_alpha(const PcScale& sc) { return sc.a ? sc.a[0] * sc.b[0] : 1.f; }
 
 int bad(const char* msg) {
   svae_tls_error(msg);
@@ -117,6 +135,51 @@ __global__ __launch_bounds__(256) void wn_norm_kernel(const float* __restrict__ 
 // W = g / norm * V -> wk_f [tap][co][kf] (K = ci) and wk_d [tap][ci][kd] (K = co), zero padded.
 // planes > 1 (the head's split mode): `planes` bf16 planes per copy, plane p at p * (copy size), with
 // W = sum_p plane_p up to the last plane's rounding (plane p = bf16 of what planes 0..p-1 left)
+// The split mode's fp16 planes: a tensor scaled by 2^s, s such that max|v| * 2^s is in [2^14, 2^15) (fp16's
+// top binade: 11 significant bits per plane, no overflow), held as h0 = fp16(v 2^s), h1 = fp16(v 2^s - h0):
+// 22 significant bits down to fp16's subnormal floor, 2^-24 * 2^-s, i.e. 2^-39 of the tensor's maximum.
+// `mx` holds the bits of max|v| (non-negative floats order as unsigned ints).
+__device__ __forceinline__ int h16_shift(unsigned mx) {
+  const float m = __uint_as_float(mx);
+  if (!(m > 0.f)) return 0;
+  int e;
+  (void)frexpf(m, &e);  // m = f 2^e, f in [0.5, 1)
+  const int sh = 15 - e;
+  return sh < -60 ? -60 : (sh > 60 ? 60 : sh);  // (two inverse scales multiply: keep their product normal)
+}
+__device__ __forceinline__ void h16_put(__bf16* w, long long i, long long pstride, float v, int sh) {
+  const float x = ldexpf(v, sh);
+  const _Float16 h0 = (_Float16)x;
+  const _Float16 h1 = (_Float16)(x - (float)h0);
+  w[i] = __builtin_bit_cast(__bf16, h0);
+  w[i + pstride] = __builtin_bit_cast(__bf16, h1);
+}
+// max |v| over a block into *mx (one device-scope atomic per block, integer max of the float bits)
+__device__ __forceinline__ void block_absmax_put(float v, unsigned* mx) {
+  __shared__ unsigned red[8];
+  unsigned b = __float_as_uint(fabsf(v));
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned t = __shfl_xor(b, o);
+    b = t > b ? t : b;
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = b;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned m = 0;
+    for (int w = 0; w < (int)(blockDim.x + 63) / 64; ++w) m = red[w] > m ? red[w] : m;
+    atomicMax(mx, m);
+  }
+}
+// max |W| = max_co max_k |V[k][co]| * |g[co] / norm[co]| (the product apply forms: monotone in |V|) into *mx
+__global__ __launch_bounds__(256) void wn_absmax_kernel(const float* __restrict__ V, const float* __restrict__ g,
+                                                        const float* __restrict__ norm, int K, int cout,
+                                                        unsigned* __restrict__ mx) {
+  const int c = blockIdx.x;
+  float m = 0.f;
+  for (int k = threadIdx.x; k < K; k += 256) m = fmaxf(m, fabsf(V[(long long)k * cout + c]));
+  block_absmax_put(m * fabsf(g[c] / norm[c]), mx);
+}
+
 __device__ __forceinline__ void wn_put(__bf16* w, long long i, long long pstride, int planes, float v) {
   for (int p = 0; p < planes; ++p) {
     const __bf16 b = (__bf16)v;
@@ -124,10 +187,13 @@ __device__ __forceinline__ void wn_put(__bf16* w, long long i, long long pstride
     v -= (float)b;
   }
 }
+// h16 != NULL: the two scaled fp16 planes (h16[1] = the bits of max|W|, h16[0] <- the inverse scale)
 __global__ void wn_apply_kernel(const float* __restrict__ V, const float* __restrict__ g,
                                 const float* __restrict__ norm, int taps, int cin, int cout, __bf16* wk_f, int kf,
-                                __bf16* wk_d, int kd, int planes) {
+                                __bf16* wk_d, int kd, int planes, float* h16) {
   const long long nf = wk_f ? (long long)taps * cout * kf : 0, nd = wk_d ? (long long)taps * cin * kd : 0;
+  const int sh = h16 ? h16_shift(__float_as_uint(h16[1])) : 0;
+  if (h16 && blockIdx.x == 0 && threadIdx.x == 0) h16[0] = ldexpf(1.f, -sh);
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nf + nd; i += stride) {
     if (i < nf) {
@@ -136,7 +202,8 @@ __global__ void wn_apply_kernel(const float* __restrict__ V, const float* __rest
       const int co = (int)(r % cout), tap = (int)(r / cout);
       float w = 0.f;
       if (ci < cin) w = V[((long long)tap * cin + ci) * cout + co] * (g[co] / norm[co]);
-      wn_put(wk_f, i, nf, planes, w);
+      if (h16) h16_put(wk_f, i, nf, w, sh);
+      else wn_put(wk_f, i, nf, planes, w);
     } else {
       const long long j = i - nf;
       const int co = (int)(j % kd);
@@ -144,7 +211,8 @@ __global__ void wn_apply_kernel(const float* __restrict__ V, const float* __rest
       const int ci = (int)(r % cin), tap = (int)(r / cin);
       float w = 0.f;
       if (co < cout) w = V[((long long)tap * cin + ci) * cout + co] * (g[co] / norm[co]);
-      wn_put(wk_d, j, nd, planes, w);
+      if (h16) h16_put(wk_d, j, nd, w, sh);
+      else wn_put(wk_d, j, nd, planes, w);
     }
   }
 }
@@ -259,11 +327,13 @@ __global__ __launch_bounds__(256) void pc_conv_kernel(PcGeom g, const float* __r
 // % 32 == 0.
 // ---------------------------------------------------------------------------------------------
 #define PC2_P 40  // LDS row pitch (bf16)
-template <int NT, bool XB>
+template <int NT, bool XB, bool H = false>
 __global__ __launch_bounds__(256) void pc_conv2_kernel(PcGeom g, const void* __restrict__ Xv,
                                                        const __bf16* __restrict__ Wk, int kpad,
                                                        const float* __restrict__ bias, float* __restrict__ Y,
-                                                       int ldy, int accumulate, int zero_edge, NlbArgs nlb) {
+                                                       int ldy, int accumulate, int zero_edge, NlbArgs nlb,
+                                                       PcScale sc) {
+  static_assert(XB || !H, "fp16 planes are stored 16-bit");
   constexpr int BR = 32 * NT;  // weight rows (output channels) per block
   __shared__ __attribute__((aligned(16))) __bf16 As[2][128 * PC2_P];
   __shared__ __attribute__((aligned(16))) __bf16 Bs[2][BR * PC2_P];
@@ -352,13 +422,14 @@ __global__ __launch_bounds__(256) void pc_conv2_kernel(PcGeom g, const void* __r
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const pc_bf16x8 bf = *(const pc_bf16x8*)&Bs[buf][(t * 32 + l32) * PC2_P + kq * 16 + 8 * h];
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc[t], 0, 0, 0);
+        acc[t] = pc_mfma<H>(af, bf, acc[t]);
       }
     }
     if (c + 1 < nchunk) store(buf ^ 1);
     __syncthreads();
   }
   const long long mw = m0 + wave * 32;
+  const float al = H ? pc_alpha(sc) : 1.f;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const long long mm = mw + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -372,7 +443,7 @@ __global__ __launch_bounds__(256) void pc_conv2_kernel(PcGeom g, const void* __r
     for (int t = 0; t < NT; ++t) {
       const int n = n0 + t * 32 + l32;
       if (n >= g.cout) continue;
-      float val = zero ? 0.f : acc[t][r] + (bias ? bias[n] : 0.f);
+      float val = zero ? 0.f : (H ? acc[t][r] * al : acc[t][r]) + (bias ? bias[n] : 0.f);
       if (nlb.on) val = nlb_apply(nlb, mm, n, g.cout, val);
       float* p = Y + mm * ldy + n;
       if (accumulate) val += *p;
@@ -400,11 +471,13 @@ struct Pc3 {
 #define PC3_MAXPIX 640
 #define PC3_MAXTAPS 6
 // XB: X stored as bf16 (a nonlinearity output the head writes in the conv's operand precision)
-template <int NT, int TM, bool XB>
+template <int NT, int TM, bool XB, bool H = false>
 __global__ __launch_bounds__(512) void pc_conv3_kernel(PcGeom g, Pc3 h, const void* __restrict__ Xv,
                                                        const __bf16* __restrict__ Wk, int kpad,
                                                        const float* __restrict__ bias, float* __restrict__ Y,
-                                                       int ldy, int accumulate, int zero_edge, NlbArgs nlb) {
+                                                       int ldy, int accumulate, int zero_edge, NlbArgs nlb,
+                                                       PcScale sc) {
+  static_assert(XB || !H, "fp16 planes are stored 16-bit");
   constexpr int BM = 256 * TM;
   constexpr int BR = 32 * NT;                                  // weight rows (output channels) per tap
   constexpr int AI = (PC3_MAXPIX * 4 + 511) / 512;             // window items (8 channels) per thread
@@ -530,7 +603,7 @@ __global__ __launch_bounds__(512) void pc_conv3_kernel(PcGeom g, Pc3 h, const vo
         for (int tn = 0; tn < NT; ++tn) {
           const pc_bf16x8 bf = *(const pc_bf16x8*)(bt + tn * 32 * PC2_P + kq * 16);
 #pragma unroll
-          for (int tm = 0; tm < TM; ++tm) acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm], bf, acc[tm][tn], 0, 0, 0);
+          for (int tm = 0; tm < TM; ++tm) acc[tm][tn] = pc_mfma<H>(af[tm], bf, acc[tm][tn]);
         }
       }
     }
@@ -539,6 +612,15 @@ __global__ __launch_bounds__(512) void pc_conv3_kernel(PcGeom g, Pc3 h, const vo
       store();
       __syncthreads();
     }
+  }
+  if constexpr (H) {  // the fp16 planes' scales, once (the activation epilogue below then sees true values)
+    const float al = pc_alpha(sc);
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < NT; ++tn)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[tm][tn][r] *= al;
   }
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
@@ -624,20 +706,20 @@ bool pc3_plan(const PcGeom& g, int kpad, int TM, Pc3* out, size_t* lds) {
   return true;
 }
 
-template <int NT, int TM, bool XB>
+template <int NT, int TM, bool XB, bool H = false>
 void pc3_launch(const PcGeom& g, const Pc3& h, const void* x, const __bf16* w, int kpad, const float* bias, float* y,
-                int ldy, int accumulate, int zero_edge, const NlbArgs& nlb, hipStream_t st) {
+                int ldy, int accumulate, int zero_edge, const NlbArgs& nlb, const PcScale& sc, hipStream_t st) {
   const size_t lds = (size_t)(h.npix + g.kh * g.kw * 32 * NT) * PC2_P * 2;
   static bool attr = false;
   if (!attr) {  // the largest window + weight stage: 640 pixels + 6 taps x 160 rows (128 KB)
-    (void)hipFuncSetAttribute((const void*)pc_conv3_kernel<NT, TM, XB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)pc_conv3_kernel<NT, TM, XB, H>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         (PC3_MAXPIX + PC3_MAXTAPS * 32 * NT) * PC2_P * 2);
     attr = true;
   }
   const long long rows = (long long)g.n * g.ho * g.wo;
   const dim3 grid((unsigned)(rows / (256 * TM)), (unsigned)((g.cout + 32 * NT - 1) / (32 * NT)));
-  hipLaunchKernelGGL((pc_conv3_kernel<NT, TM, XB>), grid, dim3(512), lds, st, g, h, x, w, kpad, bias, y, ldy, accumulate,
-                     zero_edge, nlb);
+  hipLaunchKernelGGL((pc_conv3_kernel<NT, TM, XB, H>), grid, dim3(512), lds, st, g, h, x, w, kpad, bias, y, ldy,
+                     accumulate, zero_edge, nlb, sc);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -671,7 +753,7 @@ struct Pw4 {
 #define PW4_MAXPIX 144 // 8 rows x 18 (16-wide images, kw = 3)
 #define PW4_P 72       // LDS pixel pitch (bf16): 64 channels + 8
 // DB: D (the output gradient) stored bf16 -- its MFMA precision (the bias sum is then done upstream)
-template <bool XB, bool DB>
+template <bool XB, bool DB, bool H = false>
 __global__ __launch_bounds__(256) void pc_wgrad4_kernel(PcGeom g, Pw4 h, const void* __restrict__ Xv,
                                                         const void* __restrict__ Dv, int ldd, float* __restrict__ part,
                                                         float* __restrict__ bsum) {
@@ -787,7 +869,7 @@ __global__ __launch_bounds__(256) void pc_wgrad4_kernel(PcGeom g, Pw4 h, const v
             const int sh = g.mode == 0 ? kx : g.kw - 1 - kx;
             const __bf16* wa = Ws + (wp + sh) * PW4_P + cha;
             const pc_bf16x8 af = pc_join(pc_tr16(wa), pc_tr16(wa + 4 * PW4_P));
-            acc[kx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc[kx], 0, 0, 0);
+            acc[kx] = pc_mfma<H>(af, bf, acc[kx]);
           }
         }
       }
@@ -851,7 +933,7 @@ bool pw4_plan(const PcGeom& g, long long rows, Pw4* out) {
 #define PW_RP 72  // LDS row pitch (bf16): 64 rows + 8 pad
 // bsum != NULL: the blocks of tap 0 and the first ci tile also sum their D rows per column (fp32,
 // before the bf16 staging) into bsum[split][cout]: the conv's bias gradient without another pass over dy
-template <bool XB, bool DB>
+template <bool XB, bool DB, bool H = false>
 __global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const void* __restrict__ Xv,
                                                        const void* __restrict__ Dv, int ldd, long long rows,
                                                        long long rows_per_split, float* __restrict__ part,
@@ -943,7 +1025,7 @@ __global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const void* __r
     for (int kq = 0; kq < 4; ++kq) {
       const pc_bf16x8 af = *(const pc_bf16x8*)&Xs[buf][(wm * 32 + l32) * PW_RP + kq * 16 + 8 * h];
       const pc_bf16x8 bf = *(const pc_bf16x8*)&Ds[buf][(wn * 32 + l32) * PW_RP + kq * 16 + 8 * h];
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc, 0, 0, 0);
+      acc = pc_mfma<H>(af, bf, acc);
     }
     if (more) store(buf ^ 1);
     __syncthreads();
@@ -971,12 +1053,15 @@ __global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const void* __r
   }
 }
 
-__global__ void split_reduce_kernel(const float* __restrict__ part, int nsplit, long long n, float* __restrict__ out) {
+// sc.a != NULL: the slabs are fp16-plane products, the sum is scaled by their inverse scales (exact)
+__global__ void split_reduce_kernel(const float* __restrict__ part, int nsplit, long long n, float* __restrict__ out,
+                                    PcScale sc = PcScale{nullptr, nullptr}) {
   const long long stride = (long long)gridDim.x * blockDim.x;
+  const float al = pc_alpha(sc);
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     float s = 0.f;
     for (int k = 0; k < nsplit; ++k) s += part[(long long)k * n + i];
-    out[i] = s;
+    out[i] = s * al;
   }
 }
 
@@ -1801,19 +1886,25 @@ extern "C" {
 
 int svae_pcnn_wnorm(const float* V, const float* g, int taps, int cin, int cout, float* norm, void* wk_f, int kf,
                     void* wk_d, int kd, void* stream) {
-  return svae_pcnn_wnorm_planes(V, g, taps, cin, cout, norm, wk_f, kf, wk_d, kd, 1, stream);
+  return svae_pcnn_wnorm_planes(V, g, taps, cin, cout, norm, wk_f, kf, wk_d, kd, 1, nullptr, stream);
 }
 
 int svae_pcnn_wnorm_planes(const float* V, const float* g, int taps, int cin, int cout, float* norm, void* wk_f,
-                           int kf, void* wk_d, int kd, int planes, void* stream) {
-  if (!V || !g || !norm || taps < 1 || cin < 1 || cout < 1 || planes < 1 || planes > PC_MAXPLANES)
+                           int kf, void* wk_d, int kd, int planes, float* h16_scale, void* stream) {
+  if (!V || !g || !norm || taps < 1 || cin < 1 || cout < 1 || planes < 1 || planes > PC_MAXPLANES ||
+      (h16_scale && planes != 2))
     return bad("pcnn_wnorm: bad arguments");
   if ((wk_f && (kf < cin || kf % 16)) || (wk_d && (kd < cout || kd % 16))) return bad("pcnn_wnorm: bad padding");
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(wn_norm_kernel, dim3(cout), dim3(256), 0, s, V, taps * cin, cout, norm);
+  if (h16_scale) {  // max |W| for the fp16 planes' scale
+    if (hipMemsetAsync(h16_scale + 1, 0, sizeof(float), s) != hipSuccess) return hipchk();
+    hipLaunchKernelGGL(wn_absmax_kernel, dim3(cout), dim3(256), 0, s, V, g, norm, taps * cin, cout,
+                       (unsigned*)(h16_scale + 1));
+  }
   const long long n = (wk_f ? (long long)taps * cout * kf : 0) + (wk_d ? (long long)taps * cin * kd : 0);
   if (n) hipLaunchKernelGGL(wn_apply_kernel, dim3(blocks_for(n)), dim3(256), 0, s, V, g, norm, taps, cin, cout,
-                            (__bf16*)wk_f, kf, (__bf16*)wk_d, kd, planes);
+                            (__bf16*)wk_f, kf, (__bf16*)wk_d, kd, planes, h16_scale);
   return hipchk();
 }
 
@@ -1829,7 +1920,8 @@ int svae_pcnn_wnorm_bwd(const float* V, const float* g, const float* norm, const
 
 static int pcnn_conv_impl(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, const void* wk, int kpad,
                           const float* bias, float* y, int ho, int wo, int cout, int ldy, int kh, int kw, int s, int pt,
-                          int pl, int mode, int accumulate, int zero_edge, const NlbArgs& nlb, void* stream);
+                          int pl, int mode, int accumulate, int zero_edge, const NlbArgs& nlb, void* stream,
+                          const PcScale& sc = PcScale{nullptr, nullptr});
 
 int svae_pcnn_conv(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, const void* wk, int kpad,
                    const float* bias, float* y, int ho, int wo, int cout, int ldy, int kh, int kw, int s, int pt,
@@ -1851,8 +1943,11 @@ int svae_pcnn_conv_act_bwd(const float* dy, int n, int hi, int wi, int cin, int 
 
 static int pcnn_conv_impl(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, const void* wk, int kpad,
                           const float* bias, float* y, int ho, int wo, int cout, int ldy, int kh, int kw, int s, int pt,
-                          int pl, int mode, int accumulate, int zero_edge, const NlbArgs& nlb, void* stream) {
+                          int pl, int mode, int accumulate, int zero_edge, const NlbArgs& nlb, void* stream,
+                          const PcScale& sc) {
   const PcGeom g = make_geom(n, hi, wi, cin, ldx, ho, wo, cout, kh, kw, s, pt, pl, mode);
+  const bool H = sc.a != nullptr;  // fp16 planes (the split mode): 16-bit storage only
+  if (H && (!x_bf16 || !sc.b || nlb.on)) return bad("pcnn_conv: fp16 planes need 16-bit x and both scales");
   if (!x || !wk || !y || !geom_ok(g) || ldy < cout || kpad < cin || kpad % 16 || zero_edge < 0 || zero_edge > 2)
     return bad("pcnn_conv: bad arguments");
   if (x_bf16 && (cin % 8 || ldx % 8 || kpad % 32)) return bad("pcnn_conv: bf16 input needs cin, ldx % 8 == 0");
@@ -1878,34 +1973,35 @@ static int pcnn_conv_impl(const void* x, int n, int hi, int wi, int cin, int ldx
         tiles = (n32 + nt_max - 1) / nt_max;
         NT = (n32 + tiles - 1) / tiles;
       }
-#define PC3_NT(TMV, XBV)                                                                                \
-  switch (NT) {                                                                                         \
-    case 1: pc3_launch<1, TMV, XBV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, st); break; \
-    case 2: pc3_launch<2, TMV, XBV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, st); break; \
-    case 3: pc3_launch<3, TMV, XBV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, st); break; \
-    case 4: pc3_launch<4, TMV, XBV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, st); break; \
-    default: pc3_launch<5, TMV, XBV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, st); break; \
+#define PC3_NT(TMV, XBV, HV)                                                                                \
+  switch (NT) {                                                                                             \
+    case 1: pc3_launch<1, TMV, XBV, HV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, sc, st); break; \
+    case 2: pc3_launch<2, TMV, XBV, HV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, sc, st); break; \
+    case 3: pc3_launch<3, TMV, XBV, HV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, sc, st); break; \
+    case 4: pc3_launch<4, TMV, XBV, HV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, sc, st); break; \
+    default: pc3_launch<5, TMV, XBV, HV>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, sc, st); break; \
   }
-      if (x_bf16) { PC3_NT(1, true) }
-      else if (pc3 == 2) { PC3_NT(2, false) }
-      else { PC3_NT(1, false) }
+      if (H) { PC3_NT(1, true, true) }
+      else if (x_bf16) { PC3_NT(1, true, false) }
+      else if (pc3 == 2) { PC3_NT(2, false, false) }
+      else { PC3_NT(1, false, false) }
 #undef PC3_NT
       return hipchk();
     }
     const dim3 grid(gx, tiles);
-#define PC2_NT(XBV)                                                                                                   \
+#define PC2_NT(XBV, HV)                                                                                               \
   switch (NT) {                                                                                                      \
-    case 1: hipLaunchKernelGGL((pc_conv2_kernel<1, XBV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb); break; \
-    case 2: hipLaunchKernelGGL((pc_conv2_kernel<2, XBV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb); break; \
-    case 3: hipLaunchKernelGGL((pc_conv2_kernel<3, XBV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb); break; \
-    case 4: hipLaunchKernelGGL((pc_conv2_kernel<4, XBV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb); break; \
-    default: hipLaunchKernelGGL((pc_conv2_kernel<5, XBV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb); break; \
+    case 1: hipLaunchKernelGGL((pc_conv2_kernel<1, XBV, HV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, sc); break; \
+    case 2: hipLaunchKernelGGL((pc_conv2_kernel<2, XBV, HV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, sc); break; \
+    case 3: hipLaunchKernelGGL((pc_conv2_kernel<3, XBV, HV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, sc); break; \
+    case 4: hipLaunchKernelGGL((pc_conv2_kernel<4, XBV, HV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, sc); break; \
+    default: hipLaunchKernelGGL((pc_conv2_kernel<5, XBV, HV>), grid, dim3(256), 0, st, g, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, sc); break; \
   }
-    if (x_bf16) { PC2_NT(true) } else { PC2_NT(false) }
+    if (H) { PC2_NT(true, true) } else if (x_bf16) { PC2_NT(true, false) } else { PC2_NT(false, false) }
 #undef PC2_NT
     return hipchk();
   }
-  if (x_bf16 || nlb.on) return bad("pcnn_conv: bf16 input / activation epilogue on the register-direct kernel (SVAE_PC_CONV1)");
+  if (x_bf16 || nlb.on || H) return bad("pcnn_conv: bf16 input / activation epilogue on the register-direct kernel (SVAE_PC_CONV1)");
   // register-direct kernel: two 32-column subtiles per wave (wider tiles measured slower here)
   const float* xf = (const float*)x;
   if (cout > 32)
@@ -1923,7 +2019,9 @@ static int pcnn_conv_impl(const void* x, int n, int hi, int wi, int cin, int ldx
 static int pcnn_wgrad_impl(const void* const* xs, const void* const* ds, int nprod, int n, int hi, int wi, int cin,
                            int ldx, int x_bf16, int ldd, int dy_bf16, int ho, int wo, int cout, int kh, int kw, int s,
                            int pt, int pl, int mode, float* dW, float* dbias, float* scratch, int64_t scratch_elems,
-                           void* stream) {
+                           void* stream, const PcScale& sc = PcScale{nullptr, nullptr}) {
+  const bool H = sc.a != nullptr;  // fp16 planes: both operands 16-bit, the reduce applies the scales
+  if (H && (!x_bf16 || !dy_bf16 || !sc.b || dbias)) return bad("pcnn_wgrad: fp16 planes need 16-bit x and dy");
   const PcGeom g = make_geom(n, hi, wi, cin, ldx, ho, wo, cout, kh, kw, s, pt, pl, mode);
   bool ok = nprod >= 1 && nprod <= PC_MAXPLANES * (PC_MAXPLANES + 1) / 2;
   for (int p = 0; ok && p < nprod; ++p) ok = xs[p] && ds[p];
@@ -1959,15 +2057,17 @@ static int pcnn_wgrad_impl(const void* const* xs, const void* const* ds, int npr
         const void* dy = ds[p];
         float* slab = scratch + p * ns * wsz;
 #define PW4_L(XBV, DBV) hipLaunchKernelGGL((pc_wgrad4_kernel<XBV, DBV>), grid, dim3(256), 0, st, g4, h, x, dy, ldd, slab, bpart)
-        if (x_bf16) { if (dy_bf16) PW4_L(true, true); else PW4_L(true, false); }
+        if (H) hipLaunchKernelGGL((pc_wgrad4_kernel<true, true, true>), grid, dim3(256), 0, st, g4, h, x, dy, ldd, slab,
+                                  bpart);
+        else if (x_bf16) { if (dy_bf16) PW4_L(true, true); else PW4_L(true, false); }
         else { if (dy_bf16) PW4_L(false, true); else PW4_L(false, false); }
 #undef PW4_L
       }
       hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(wsz)), dim3(256), 0, st, scratch, (int)(nprod * ns),
-                         wsz, dW);
+                         wsz, dW, sc);
       if (dbias)
         hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(cout)), dim3(256), 0, st, bpart, (int)ns,
-                           (long long)cout, dbias);
+                           (long long)cout, dbias, PcScale{nullptr, nullptr});
       return hipchk();
     }
   }
@@ -1989,15 +2089,17 @@ static int pcnn_wgrad_impl(const void* const* xs, const void* const* ds, int npr
     float* slab = scratch + p * ns * wsz;
 #define PW1_L(XBV, DBV) hipLaunchKernelGGL((pc_wgrad_kernel<XBV, DBV>), dim3(tiles, taps, (unsigned)ns), dim3(256), 0, st, g, x, dy, \
                                            ldd, rows, rps, slab, bpart)
-    if (x_bf16) { if (dy_bf16) PW1_L(true, true); else PW1_L(true, false); }
+    if (H) hipLaunchKernelGGL((pc_wgrad_kernel<true, true, true>), dim3(tiles, taps, (unsigned)ns), dim3(256), 0, st, g, x,
+                              dy, ldd, rows, rps, slab, bpart);
+    else if (x_bf16) { if (dy_bf16) PW1_L(true, true); else PW1_L(true, false); }
     else { if (dy_bf16) PW1_L(false, true); else PW1_L(false, false); }
 #undef PW1_L
   }
   hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(wsz)), dim3(256), 0, st, scratch, (int)(nprod * ns), wsz,
-                     dW);
+                     dW, sc);
   if (dbias)
     hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(cout)), dim3(256), 0, st, bpart, (int)ns, (long long)cout,
-                       dbias);
+                       dbias, PcScale{nullptr, nullptr});
   return hipchk();
 }
 
@@ -2021,10 +2123,12 @@ static int pc_products(int planes, int* pi, int* pj) {
 }
 
 int svae_pcnn_conv_wgrad_planes(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, int64_t x_pstride,
-                                const void* dy, int ldd, int dy_bf16, int64_t dy_pstride, int planes, int ho, int wo,
-                                int cout, int kh, int kw, int s, int pt, int pl, int mode, float* dW, float* scratch,
-                                int64_t scratch_elems, void* stream) {
-  if (!x || !dy || planes < 1 || planes > PC_MAXPLANES || x_pstride < 0 || dy_pstride < 0)
+                                const void* dy, int ldd, int dy_bf16, int64_t dy_pstride, int planes,
+                                const float* x_scale, const float* dy_scale, int ho, int wo, int cout, int kh, int kw,
+                                int s, int pt, int pl, int mode, float* dW, float* scratch, int64_t scratch_elems,
+                                void* stream) {
+  if (!x || !dy || planes < 1 || planes > PC_MAXPLANES || x_pstride < 0 || dy_pstride < 0 ||
+      (!x_scale != !dy_scale) || (x_scale && planes != 2))
     return bad("pcnn_wgrad_planes: bad arguments");
   int pi[PC_MAXPLANES * PC_MAXPLANES], pj[PC_MAXPLANES * PC_MAXPLANES];
   const int np = pc_products(planes, pi, pj);
@@ -2035,14 +2139,17 @@ int svae_pcnn_conv_wgrad_planes(const void* x, int n, int hi, int wi, int cin, i
     ds[p] = (const char*)dy + (dy_bf16 ? 2 : 4) * dy_pstride * pj[p];
   }
   return pcnn_wgrad_impl(xs, ds, np, n, hi, wi, cin, ldx, x_bf16, ldd, dy_bf16, ho, wo, cout, kh, kw, s, pt, pl, mode,
-                         dW, nullptr, scratch, scratch_elems, stream);
+                         dW, nullptr, scratch, scratch_elems, stream, PcScale{x_scale, dy_scale});
 }
 
 int svae_pcnn_conv_planes(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, int64_t x_pstride,
-                          const void* wk, int kpad, int planes, const float* bias, float* y, int ho, int wo, int cout,
-                          int ldy, int kh, int kw, int s, int pt, int pl, int mode, int accumulate, int zero_edge,
-                          void* stream) {
-  if (!x || !wk || planes < 1 || planes > PC_MAXPLANES || x_pstride < 0) return bad("pcnn_conv_planes: bad arguments");
+                          const void* wk, int kpad, int planes, const float* x_scale, const float* w_scale,
+                          const float* bias, float* y, int ho, int wo, int cout, int ldy, int kh, int kw, int s, int pt,
+                          int pl, int mode, int accumulate, int zero_edge, void* stream) {
+  if (!x || !wk || planes < 1 || planes > PC_MAXPLANES || x_pstride < 0 || (!x_scale != !w_scale) ||
+      (x_scale && planes != 2))
+    return bad("pcnn_conv_planes: bad arguments");
+  const PcScale sc{x_scale, w_scale};
   int pi[PC_MAXPLANES * PC_MAXPLANES], pj[PC_MAXPLANES * PC_MAXPLANES];
   const int np = pc_products(planes, pi, pj);
   const long long wst = (long long)kh * kw * cout * kpad;  // one weight plane (wk [tap][cout][kpad])
@@ -2051,7 +2158,7 @@ int svae_pcnn_conv_planes(const void* x, int n, int hi, int wi, int cin, int ldx
     const void* xp = (const char*)x + (x_bf16 ? 2 : 4) * x_pstride * pi[p];
     const __bf16* wp = (const __bf16*)wk + wst * pj[p];
     const int rc = pcnn_conv_impl(xp, n, hi, wi, cin, ldx, x_bf16, wp, kpad, p ? nullptr : bias, y, ho, wo, cout, ldy,
-                                  kh, kw, s, pt, pl, mode, p ? 1 : accumulate, zero_edge, nlb, stream);
+                                  kh, kw, s, pt, pl, mode, p ? 1 : accumulate, zero_edge, nlb, stream, sc);
     if (rc) return rc;
   }
   return 0;
@@ -2078,12 +2185,48 @@ __global__ void split_planes_kernel(const float* __restrict__ x, long long rows,
   }
 }
 
+__global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x, long long rows, int c, int ldx,
+                                                     unsigned* __restrict__ mx) {
+  const long long n = rows * c;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  float m = 0.f;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const long long r = i / c;
+    m = fmaxf(m, fabsf(x[r * ldx + (i - r * c)]));
+  }
+  block_absmax_put(m, mx);
+}
+
+// the two scaled fp16 planes of x (h16[1]: the bits of max|x|; h16[0] <- the inverse scale)
+__global__ void split_h16_kernel(const float* __restrict__ x, long long rows, int c, int ldx, __bf16* __restrict__ out,
+                                 int ldo, float* h16) {
+  const long long n = rows * c, pst = rows * ldo;
+  const int sh = h16_shift(__float_as_uint(h16[1]));
+  if (blockIdx.x == 0 && threadIdx.x == 0) h16[0] = ldexpf(1.f, -sh);
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const long long r = i / c;
+    const int ch = (int)(i - r * c);
+    h16_put(out, r * ldo + ch, pst, x[r * ldx + ch], sh);
+  }
+}
+
 int svae_pcnn_split_planes(const float* x, int64_t rows, int c, int ldx, int planes, void* out, int ldo, int out_bf16,
-                           void* stream) {
-  if (!x || !out || rows < 1 || c < 1 || ldx < c || ldo < c || planes < 1 || planes > PC_MAXPLANES)
+                           float* h16_scale, void* stream) {
+  if (!x || !out || rows < 1 || c < 1 || ldx < c || ldo < c || planes < 1 || planes > PC_MAXPLANES ||
+      (h16_scale && (planes != 2 || !out_bf16)))
     return bad("pcnn_split_planes: bad arguments");
-  hipLaunchKernelGGL(split_planes_kernel, dim3(blocks_for(rows * c)), dim3(256), 0, (hipStream_t)stream, x,
-                     (long long)rows, c, ldx, planes, out, ldo, out_bf16);
+  hipStream_t st = (hipStream_t)stream;
+  if (h16_scale) {
+    if (hipMemsetAsync(h16_scale + 1, 0, sizeof(float), st) != hipSuccess) return hipchk();
+    hipLaunchKernelGGL(absmax_kernel, dim3(blocks_for(rows * c, 256, 2048)), dim3(256), 0, st, x, (long long)rows, c,
+                       ldx, (unsigned*)(h16_scale + 1));
+    hipLaunchKernelGGL(split_h16_kernel, dim3(blocks_for(rows * c)), dim3(256), 0, st, x, (long long)rows, c, ldx,
+                       (__bf16*)out, ldo, h16_scale);
+    return hipchk();
+  }
+  hipLaunchKernelGGL(split_planes_kernel, dim3(blocks_for(rows * c)), dim3(256), 0, st, x, (long long)rows, c, ldx,
+                     planes, out, ldo, out_bf16);
   return hipchk();
 }
 
@@ -2228,7 +2371,8 @@ int svae_pcnn_imgsum(const float* x, int ldx, int nimg, int pix_per_img, int c, 
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(imgsum_kernel, dim3((c + 63) / 64, nimg, ps), dim3(256), 0, st, x, ldx, pix_per_img, c, scratch);
   const long long n = (long long)nimg * c;
-  hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(n)), dim3(256), 0, st, scratch, ps, n, out);
+  hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(n)), dim3(256), 0, st, scratch, ps, n, out,
+                     PcScale{nullptr, nullptr});
   return hipchk();
 }
 

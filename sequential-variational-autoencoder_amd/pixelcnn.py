@@ -189,11 +189,13 @@ class PixelCNNpp:
         # bias gradients summed in fp32 by the op that writes them)
         self.bf16_grads = os.environ.get("SVAE_PC_BF16_GRADS", "0") == "1"  # opt-in: measured slower (804 vs 882 img/s)
         self._nl_src, self._bias_of, self._bf16_grad = {}, {}, set()
-        # operand planes of the conv / nin GEMMs: 1 = bf16 MFMA operands; 3 = the split mode (include/svae_pcnn.h:
-        # every operand a sum of 3 bf16 planes, 6 plane products per GEMM: fp32-grade, nn.py:189-252 in fp32)
+        # operand planes of the conv / nin GEMMs: 1 = bf16 MFMA operands; 3 = the split mode (include/svae_pcnn.h):
+        # fp32-grade products, nn.py:189-252 in fp32 -- two scaled fp16 planes per operand (3 fp16-MFMA
+        # products) for the layers whose channel counts allow 16-bit storage (h16), else 3 bf16 planes (6)
         if planes not in (1, 2, 3):
             raise ValueError("planes must be 1 (bf16), 2 or 3 (split)")
         self.planes = planes
+        self.h16 = True
         if planes > 1:  # every activation and gradient stays fp32 (split into planes at each GEMM)
             self.bf16_grads = False
         self.probe, self.probe_cap = None, 0  # [(flops, event, event)] of timed forward conv launches
@@ -306,13 +308,15 @@ class PixelCNNpp:
         off_g, _, _ = self.table[name + "/g"]
         off_b, _, _ = self.table[name + "/b"]
         kf, kd = _r16(cin), _r16(cout)
-        P = self.planes
+        h16 = self.planes > 1 and self.h16 and cin % 8 == 0 and cout % 8 == 0  # this layer's plane format
+        P = 2 if h16 else self.planes
         norm = torch.empty(cout, dtype=torch.float32, device=self.dev)
         wkf = torch.empty(P * taps * cout * kf, dtype=torch.bfloat16, device=self.dev)
         wkd = torch.empty(P * taps * cin * kd, dtype=torch.bfloat16, device=self.dev)
+        wsc = torch.empty(2, dtype=torch.float32, device=self.dev) if h16 else None  # [2^-s, max|W|]
         _ck(L.svae_pcnn_wnorm_planes(_p(self.P, off_v), _p(self.P, off_g), taps, cin, cout, _p(norm), _p(wkf), kf,
-                                     ctypes.c_void_p(wkd.data_ptr()), kd, P, st))
-        xs = self._planes(x) if P > 1 else None  # (the split mode's operand planes of x, kept for the backward)
+                                     ctypes.c_void_p(wkd.data_ptr()), kd, P, _p(wsc), st))
+        xs = self._planes(x, h16) if self.planes > 1 else None  # (the split mode's planes of x, kept for the backward)
         if ho is None:
             ho, wo = (x.h - 1) // s + 1, (x.w - 1) // s + 1
         # algorithmic FLOPs of the forward gather GEMM (valid taps only for the stride-2 deconvs)
@@ -324,53 +328,58 @@ class PixelCNNpp:
         if pr:  # bench.py's live roofline probe: an event pair around this forward conv launch
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        self._conv(x, xs, wkf, kf, _p(self.P, off_b), out.ptr(), ho, wo, cout, out.ld, kh, kw, s, pt, pl, mode,
+        self._conv(x, xs, wkf, kf, wsc, _p(self.P, off_b), out.ptr(), ho, wo, cout, out.ld, kh, kw, s, pt, pl, mode,
                    1 if acc else 0, zero_edge)
         if pr:
             e1.record()
-            self.probe.append((2.0 * x.n * ho * wo * cout * cin * taps / (s * s if mode == 1 else 1), e0, e1))
+            nprod = 1 if xs is None else xs[4] * (xs[4] + 1) // 2  # MFMA launches per algorithmic product
+            self.probe.append((2.0 * x.n * ho * wo * cout * cin * taps / (s * s if mode == 1 else 1), e0, e1, nprod))
         if self._init:  # data-dependent init: this layer's g, b from the moments of its own output
             # (before any shift or sum), which is passed on un-normalised (tf.identity of the old x)
             src = out
             if acc or zero_edge:
                 src = Act(self._new(x.n * ho * wo, cout), cout, x.n, ho, wo)
-                self._conv(x, xs, wkf, kf, _p(self.P, off_b), src.ptr(), ho, wo, cout, cout, kh, kw, s,
+                self._conv(x, xs, wkf, kf, wsc, _p(self.P, off_b), src.ptr(), ho, wo, cout, cout, kh, kw, s,
                            pt - (zero_edge == 1), pl - (zero_edge == 2), mode, 0, 0)
             _ck(L.svae_pcnn_wn_init(src.ptr(), src.rows, cout, src.ld, float(init_scale), _p(self.P, off_g),
                                     _p(self.P, off_b), _p(self.scratch), st))
         if self._record:
             geo = (kh, kw, s, pt, pl, mode, zero_edge, kf, kd, off_v, off_g, off_b)
-            self._tape.append(lambda: self._wconv_bwd(x, out, norm, wkd, geo, xs))
+            self._tape.append(lambda: self._wconv_bwd(x, out, norm, wkd, geo, xs, wsc))
             self._bias_of.setdefault(id(self._root(out)), []).append(off_b)  # (every conv summed into it)
         return out
 
-    def _planes(self, a):
-        """The split mode's operand planes of activation (or [rows][c] gradient) ``a``: (buffer, ld, bf16 flag,
-        plane stride) -- bf16 planes where the bf16-operand kernels take them (c % 8 == 0), else fp32 ones."""
+    def _planes(self, a, h16):
+        """The split mode's operand planes of activation (or [rows][c] gradient) ``a``: (buffer, ld, 16-bit flag,
+        plane stride, planes, scale) -- the two scaled fp16 planes (h16; scale = [2^-s, max|a|]), else
+        ``self.planes`` bf16 planes (16-bit where the bf16-operand kernels take them: c % 8 == 0, else fp32)."""
         if isinstance(a, Act):
             assert not a.bf, "split mode: activations are fp32"
             src, rows, c, ld = a.ptr(), a.rows, a.c, a.ld
         else:
             assert a.dtype == torch.float32 and a.is_contiguous()
             src, rows, c, ld = _p(a), a.shape[0], a.shape[1], a.shape[1]
-        bf = c % 8 == 0
-        out = torch.empty(self.planes * rows * c, dtype=torch.bfloat16 if bf else torch.float32, device=self.dev)
-        _ck(self.L.svae_pcnn_split_planes(src, rows, c, ld, self.planes, ctypes.c_void_p(out.data_ptr()), c, int(bf),
+        bf = h16 or c % 8 == 0
+        P = 2 if h16 else self.planes
+        out = torch.empty(P * rows * c, dtype=torch.bfloat16 if bf else torch.float32, device=self.dev)
+        sc = torch.empty(2, dtype=torch.float32, device=self.dev) if h16 else None
+        _ck(self.L.svae_pcnn_split_planes(src, rows, c, ld, P, ctypes.c_void_p(out.data_ptr()), c, int(bf), _p(sc),
                                           self._st()))
-        return out, c, int(bf), rows * c
+        return out, c, int(bf), rows * c, P, sc
 
-    def _conv(self, x, xs, wk, kpad, bias, y, ho, wo, cout, ldy, kh, kw, s, pt, pl, mode, acc, zero_edge):
-        """One gather conv of ``x`` (an Act; ``xs`` its split-mode planes, or None) with the weight copy ``wk``."""
+    def _conv(self, x, xs, wk, kpad, wsc, bias, y, ho, wo, cout, ldy, kh, kw, s, pt, pl, mode, acc, zero_edge):
+        """One gather conv of ``x`` (an Act; ``xs`` its split-mode planes, or None) with the weight copy ``wk``
+        (``wsc``: its fp16 planes' scale)."""
         if xs is None:
             _ck(self.L.svae_pcnn_conv(x.ptr(), x.n, x.h, x.w, x.c, x.ld, int(x.bf), ctypes.c_void_p(wk.data_ptr()), kpad,
                                       bias, y, ho, wo, cout, ldy, kh, kw, s, pt, pl, mode, acc, zero_edge, self._st()))
             return
-        buf, ld, bf, pst = xs
+        buf, ld, bf, pst, P, xsc = xs
         _ck(self.L.svae_pcnn_conv_planes(ctypes.c_void_p(buf.data_ptr()), x.n, x.h, x.w, x.c, ld, bf, pst,
-                                         ctypes.c_void_p(wk.data_ptr()), kpad, self.planes, bias, y, ho, wo, cout, ldy,
-                                         kh, kw, s, pt, pl, mode, acc, zero_edge, self._st()))
+                                         ctypes.c_void_p(wk.data_ptr()), kpad, P, _p(xsc), _p(wsc), bias, y, ho, wo,
+                                         cout, ldy, kh, kw, s, pt, pl, mode, acc, zero_edge, self._st()))
 
-    def _wconv_bwd(self, x, y, norm, wkd, geo, xs=None):
+    def _wconv_bwd(self, x, y, norm, wkd, geo, xs=None, wsc=None):
         L = self.L
         st = self._st()
         kh, kw, s, pt, pl, mode, zero_edge, kf, kd, off_v, off_g, off_b = geo
@@ -383,7 +392,7 @@ class PixelCNNpp:
         dW = torch.empty(taps * cin * cout, dtype=torch.float32, device=self.dev)
         sc = self.scratch
         if xs is not None:
-            self._wconv_bwd_split(x, y, dy, norm, wkd, geo, xs, dW)
+            self._wconv_bwd_split(x, y, dy, norm, wkd, geo, xs, wsc, dW)
             return
         # dW and (fp32 dy) the bias gradient, written into G, from one pass over dy
         _ck(L.svae_pcnn_conv_wgrad(x.ptr(), x.n, x.h, x.w, cin, x.ld, int(x.bf), ctypes.c_void_p(dy.data_ptr()), cout,
@@ -410,28 +419,28 @@ class PixelCNNpp:
                              ctypes.c_void_p(wkd.data_ptr()), kd, None, _p(dx), x.h, x.w, cin, cin, kh, kw, s, pt, pl,
                              1 - mode, dacc, 0, st))
 
-    def _wconv_bwd_split(self, x, y, dy, norm, wkd, geo, xs, dW):
+    def _wconv_bwd_split(self, x, y, dy, norm, wkd, geo, xs, wsc, dW):
         """_wconv_bwd in the split mode: dW and the input gradient as plane-product sums over the planes of x
-        and of dy (fp32; the bias gradient its column sums)."""
+        and of dy (fp32, split in the layer's plane format; the bias gradient its column sums)."""
         L = self.L
         st = self._st()
         kh, kw, s, pt, pl, mode, zero_edge, kf, kd, off_v, off_g, off_b = geo
         taps, cin, cout = kh * kw, x.c, y.c
-        ds, dld, dbf, dpst = self._planes(dy)
-        xb, xld, xbf, xpst = xs
+        xb, xld, xbf, xpst, P, xsc = xs
+        ds, dld, dbf, dpst, _, dsc = self._planes(dy, xsc is not None)
         sc = self.scratch
         _ck(L.svae_pcnn_colsum(_p(dy), y.rows, cout, cout, 0, 0, 0, _p(self.G, off_b), 0, _p(sc), st))
         _ck(L.svae_pcnn_conv_wgrad_planes(ctypes.c_void_p(xb.data_ptr()), x.n, x.h, x.w, cin, xld, xbf, xpst,
-                                          ctypes.c_void_p(ds.data_ptr()), dld, dbf, dpst, self.planes, y.h, y.w, cout,
-                                          kh, kw, s, pt, pl, mode, _p(dW), _p(sc), sc.numel(), st))
+                                          ctypes.c_void_p(ds.data_ptr()), dld, dbf, dpst, P, _p(xsc), _p(dsc), y.h, y.w,
+                                          cout, kh, kw, s, pt, pl, mode, _p(dW), _p(sc), sc.numel(), st))
         _ck(L.svae_pcnn_wnorm_bwd(_p(self.P, off_v), _p(self.P, off_g), _p(norm), _p(dW), taps, cin, cout,
                                   _p(self.G, off_v), _p(self.G, off_g), st))
         if id(x) in self._nograd:
             return
         dx, dacc = self._gout(x)
         _ck(L.svae_pcnn_conv_planes(ctypes.c_void_p(ds.data_ptr()), y.n, y.h, y.w, cout, dld, dbf, dpst,
-                                    ctypes.c_void_p(wkd.data_ptr()), kd, self.planes, None, _p(dx), x.h, x.w, cin, cin,
-                                    kh, kw, s, pt, pl, 1 - mode, dacc, 0, st))
+                                    ctypes.c_void_p(wkd.data_ptr()), kd, P, _p(dsc), _p(wsc), None, _p(dx), x.h, x.w,
+                                    cin, cin, kh, kw, s, pt, pl, 1 - mode, dacc, 0, st))
 
     def _dense(self, x, name, cout, init_scale=1.0):
         """nn.nin / dense over the channel axis (nn.py:255-260): a 1x1 gather GEMM over every pixel."""

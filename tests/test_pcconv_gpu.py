@@ -160,94 +160,114 @@ def test_pcnn_wgrad_matches_reference(case):
     assert err < 1e-5 and eb < 1e-5
 
 
-# ---------------- the split mode (3 bf16 planes per operand, 6 plane products: fp32-grade) ----------------
-def _planes(L, t, planes, bf):
-    """svae_pcnn_split_planes of fp32 [rows][c] ``t`` (device): [planes][rows][c] bf16 or fp32."""
+# ---------------- the split mode: operands as sums of 16-bit planes (include/svae_pcnn.h) ----------------
+# fmt "bf16": 3 bf16 planes, 6 products; fmt "h16": two scaled fp16 planes, 3 products (16-bit storage only)
+def _planes(L, t, fmt, bf=1):
+    """svae_pcnn_split_planes of fp32 [rows][c] ``t`` (device): ([planes][rows][c] planes, scale or None)."""
     rows, c = t.shape
-    out = torch.empty(planes, rows, c, dtype=torch.bfloat16 if bf else torch.float32, device="cuda")
-    L.check(L.lib().svae_pcnn_split_planes(ctypes.c_void_p(t.data_ptr()), rows, c, c, planes,
-                                           ctypes.c_void_p(out.data_ptr()), c, int(bf), L.stream_ptr()))
-    return out
+    h16 = fmt == "h16"
+    P = 2 if h16 else 3
+    out = torch.empty(P, rows, c, dtype=torch.bfloat16 if (bf or h16) else torch.float32, device="cuda")
+    sc = torch.empty(2, device="cuda") if h16 else None
+    L.check(L.lib().svae_pcnn_split_planes(ctypes.c_void_p(t.data_ptr()), rows, c, c, P,
+                                           ctypes.c_void_p(out.data_ptr()), c, int(bf or h16),
+                                           None if sc is None else ctypes.c_void_p(sc.data_ptr()), L.stream_ptr()))
+    return out, sc
 
 
-def _wn_planes(L, V, g, taps, cin, cout, planes):
-    """svae_pcnn_wnorm_planes: the forward copy's planes [planes][tap][cout][kf] and the fp64 W [tap][cout][cin]."""
+def _wn_planes(L, V, g, taps, cin, cout, fmt):
+    """svae_pcnn_wnorm_planes: the forward copy's planes [planes][tap][cout][kf], its scale, the fp64 W [tap][cout][cin]."""
+    h16 = fmt == "h16"
+    P = 2 if h16 else 3
     kf, kd = (cin + 31) // 32 * 32, (cout + 31) // 32 * 32
     norm = torch.empty(cout, device="cuda")
-    wkf = torch.empty(planes * taps * cout * kf, dtype=torch.bfloat16, device="cuda")
-    wkd = torch.empty(planes * taps * cin * kd, dtype=torch.bfloat16, device="cuda")
+    wkf = torch.empty(P * taps * cout * kf, dtype=torch.bfloat16, device="cuda")
+    wkd = torch.empty(P * taps * cin * kd, dtype=torch.bfloat16, device="cuda")
+    sc = torch.empty(2, device="cuda") if h16 else None
     Vd, gd = V.cuda(), g.cuda()
-    p = lambda t: ctypes.c_void_p(t.data_ptr())
-    L.check(L.lib().svae_pcnn_wnorm_planes(p(Vd), p(gd), taps, cin, cout, p(norm), p(wkf), kf, p(wkd), kd, planes,
+    p = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())
+    L.check(L.lib().svae_pcnn_wnorm_planes(p(Vd), p(gd), taps, cin, cout, p(norm), p(wkf), kf, p(wkd), kd, P, p(sc),
                                            L.stream_ptr()))
     V64 = V.double().reshape(taps, cin, cout)
     W = V64 * (g.double() / V64.pow(2).sum((0, 1)).sqrt())
-    return wkf, kf, W.permute(0, 2, 1).contiguous()
+    return wkf, kf, sc, W.permute(0, 2, 1).contiguous()
+
+
+def _fmts(c):
+    return ["bf16", "h16"] if c % 8 == 0 else ["bf16"]
 
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "n%d_h%d_%dto%d_k%dx%d_s%d_m%d_a%d_z%d" % (
     c[0], c[2], c[3], c[5], c[6], c[7], c[8], c[11], c[12], c[13]))
 def test_pcnn_conv_planes_is_fp32_grade(case):
-    """svae_pcnn_conv_planes over unrounded fp32 operands (x split by svae_pcnn_split_planes, fp32 planes and,
-    where cin allows, bf16 planes; W by svae_pcnn_wnorm_planes) against fp64: the fp32 bounds of
-    tests/test_split_gather_gpu.py (2e-6 relative L2, 2e-5 of max|ref| pointwise)."""
+    """svae_pcnn_conv_planes over unrounded fp32 operands (x split by svae_pcnn_split_planes, W by
+    svae_pcnn_wnorm_planes) in both plane formats -- 3 bf16 planes (fp32 and bf16 storage) and, where cin
+    allows, two scaled fp16 planes -- against fp64: the fp32 bounds of tests/test_split_gather_gpu.py
+    (2e-6 relative L2, 2e-5 of max|ref| pointwise).  The input is scaled by 1e-3 so the fp16 planes'
+    scale is exercised away from 1."""
     n, hi, ho, cin, ldx, cout, kh, kw, s, pt, pl, mode, acc, zero_edge = case
     wi, wo = hi, ho
     L = pkg_mod("_lib")
     rng = np.random.default_rng(hash(case) % 2 ** 32 + 1)
     taps = kh * kw
-    x = torch.tensor(rng.uniform(-1, 1, (n * hi * wi, cin)), dtype=torch.float32)
+    x = torch.tensor(rng.uniform(-1, 1, (n * hi * wi, cin)) * 1e-3, dtype=torch.float32)
     V = torch.tensor(rng.normal(0, 0.05, (taps, cin, cout)), dtype=torch.float32)
     g = torch.tensor(rng.uniform(0.5, 2.0, cout), dtype=torch.float32)
-    bias = torch.tensor(rng.normal(0, 0.1, cout), dtype=torch.float32)
-    y0 = torch.tensor(rng.normal(0, 1, (n * ho * wo, cout)), dtype=torch.float32)
-    wkf, kf, W = _wn_planes(L, V, g, taps, cin, cout, 3)
-    ref = _ref(x, W, n, hi, wi, cin, ho, wo, cout, kh, kw, s, pt, pl, mode, bias, zero_edge)
-    if acc:
-        ref = ref + y0.double()
-    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    bias = torch.tensor(rng.normal(0, 1e-4, cout), dtype=torch.float32)
+    y0 = torch.tensor(rng.normal(0, 1e-3, (n * ho * wo, cout)), dtype=torch.float32)
+    p = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())
     xd, bd = x.cuda(), bias.cuda()
-    for bf in ([0, 1] if cin % 8 == 0 else [0]):
-        xs = _planes(L, xd, 3, bf)
-        yd = y0.clone().cuda() if acc else torch.full((n * ho * wo, cout), float("nan"), device="cuda")
-        L.check(L.lib().svae_pcnn_conv_planes(p(xs), n, hi, wi, cin, cin, bf, n * hi * wi * cin, p(wkf), kf, 3, p(bd),
-                                              p(yd), ho, wo, cout, cout, kh, kw, s, pt, pl, mode, acc, zero_edge,
-                                              L.stream_ptr()))
-        torch.cuda.synchronize()
-        got = yd.cpu().double()
-        rel = float((got - ref).norm() / ref.norm())
-        mx = float((got - ref).abs().max() / ref.abs().max())
-        print("\nconv planes %s bf%d: rel %.2e max %.2e" % (case, bf, rel, mx))
-        assert torch.isfinite(got).all()
-        assert rel <= 2e-6 and mx <= 2e-5
+    for fmt in _fmts(cin):
+        wkf, kf, wsc, W = _wn_planes(L, V, g, taps, cin, cout, fmt)
+        ref = _ref(x, W, n, hi, wi, cin, ho, wo, cout, kh, kw, s, pt, pl, mode, bias, zero_edge)
+        if acc:
+            ref = ref + y0.double()
+        for bf in ([1] if fmt == "h16" else ([0, 1] if cin % 8 == 0 else [0])):
+            xs, xsc = _planes(L, xd, fmt, bf)
+            P = xs.shape[0]
+            yd = y0.clone().cuda() if acc else torch.full((n * ho * wo, cout), float("nan"), device="cuda")
+            L.check(L.lib().svae_pcnn_conv_planes(p(xs), n, hi, wi, cin, cin, bf, n * hi * wi * cin, p(wkf), kf, P,
+                                                  p(xsc), p(wsc), p(bd), p(yd), ho, wo, cout, cout, kh, kw, s, pt, pl,
+                                                  mode, acc, zero_edge, L.stream_ptr()))
+            torch.cuda.synchronize()
+            got = yd.cpu().double()
+            rel = float((got - ref).norm() / ref.norm())
+            mx = float((got - ref).abs().max() / ref.abs().max())
+            print("\nconv planes %s %s bf%d: rel %.2e max %.2e" % (case, fmt, bf, rel, mx))
+            assert torch.isfinite(got).all()
+            assert rel <= 2e-6 and mx <= 2e-5
 
 
 @pytest.mark.parametrize("case", WCASES, ids=lambda c: "n%d_h%d_%dto%d_k%dx%d_m%d_xb%d" % (
     c[0], c[1], c[2], c[4], c[5], c[6], c[9], c[10]))
 def test_pcnn_wgrad_planes_is_fp32_grade(case):
-    """svae_pcnn_conv_wgrad_planes: the 6 plane products' slabs and one reduce, against fp64 on the
-    unrounded operands (x planes bf16 where cin allows, dy planes fp32)."""
+    """svae_pcnn_conv_wgrad_planes: every product's slabs and one reduce, against fp64 on the unrounded
+    operands, in both plane formats (fp16 where cin and cout allow; dy spans 6 decades to exercise the
+    fp16 planes' floor)."""
     n, h, cin, ldx, cout, kh, kw, pt, pl, mode, xb = case
-    xb = xb if cin % 8 == 0 else 0
     L = pkg_mod("_lib")
     rng = np.random.default_rng(hash(case) % 2 ** 32 + 2)
     x = torch.tensor(rng.uniform(-1, 1, (n * h * h, cin)), dtype=torch.float32)
-    d = torch.tensor(rng.normal(0, 1, (n * h * h, cout)), dtype=torch.float32)
+    d = torch.tensor(rng.normal(0, 1, (n * h * h, cout)) * 10.0 ** rng.uniform(-6, 0, (n * h * h, 1)),
+                     dtype=torch.float32)
     ref = torch.stack([_gathered(x, n, h, h, cin, h, h, kh, kw, pt, pl, mode, t // kw, t % kw).T @ d.double()
                        for t in range(kh * kw)])
-    xs = _planes(L, x.cuda(), 3, xb)
-    ds = _planes(L, d.cuda(), 3, 0)
-    dW = torch.full((kh * kw, cin, cout), float("nan"), device="cuda")
-    sc = torch.empty(1 << 24, device="cuda")
-    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    p = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())
     rows = n * h * h
-    L.check(L.lib().svae_pcnn_conv_wgrad_planes(p(xs), n, h, h, cin, cin, xb, rows * cin, p(ds), cout, 0, rows * cout, 3,
-                                                h, h, cout, kh, kw, 1, pt, pl, mode, p(dW), p(sc), sc.numel(),
-                                                L.stream_ptr()))
-    torch.cuda.synchronize()
-    got = dW.cpu().double()
-    rel = float((got - ref).norm() / ref.norm())
-    mx = float((got - ref).abs().max() / ref.abs().max())
-    print("\nwgrad planes %s: rel %.2e max %.2e" % (case, rel, mx))
-    assert torch.isfinite(got).all()
-    assert rel <= 2e-6 and mx <= 2e-5
+    for fmt in (["bf16", "h16"] if cin % 8 == 0 and cout % 8 == 0 else ["bf16"]):
+        xbf = 1 if fmt == "h16" else (xb if cin % 8 == 0 else 0)
+        xs, xsc = _planes(L, x.cuda(), fmt, xbf)
+        ds, dsc = _planes(L, d.cuda(), fmt, 1 if fmt == "h16" else 0)
+        dbf = 1 if fmt == "h16" else 0
+        dW = torch.full((kh * kw, cin, cout), float("nan"), device="cuda")
+        sc = torch.empty(1 << 24, device="cuda")
+        L.check(L.lib().svae_pcnn_conv_wgrad_planes(p(xs), n, h, h, cin, cin, xbf, rows * cin, p(ds), cout, dbf,
+                                                    rows * cout, xs.shape[0], p(xsc), p(dsc), h, h, cout, kh, kw, 1,
+                                                    pt, pl, mode, p(dW), p(sc), sc.numel(), L.stream_ptr()))
+        torch.cuda.synchronize()
+        got = dW.cpu().double()
+        rel = float((got - ref).norm() / ref.norm())
+        mx = float((got - ref).abs().max() / ref.abs().max())
+        print("\nwgrad planes %s %s: rel %.2e max %.2e" % (case, fmt, rel, mx))
+        assert torch.isfinite(got).all()
+        assert rel <= 2e-6 and mx <= 2e-5
