@@ -40,6 +40,7 @@ PMC_FILES = {
     "celeba/bf16": ["profiles/r05_fbf_pmc_traffic.json", "profiles/r04_final_pmc_traffic.json"],
     "celeba/bf16x6": ["profiles/r05_f6_pmc_traffic.json", "profiles/r04_final_x6_pmc_traffic.json"],
     "lsun/bf16": ["profiles/r04_final_lsun_pmc_traffic.json", "profiles/r04_v1_lsun_pmc_traffic.json"],
+    "lsun/bf16x6": ["profiles/r05_fl6_pmc_traffic.json"],
     "c_pixelvae/bf16": ["profiles/r04_final_pv_pmc_traffic.json", "profiles/r04_v1_pv_pmc_traffic.json"],
     "c_pixelvae/bf16x6": ["profiles/r05_fpv_pmc_traffic.json"],
 }
