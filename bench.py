@@ -316,7 +316,7 @@ def _pv_roofline(probe, planes, head_flops, vae_flops, ms, key):
             "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 5), "traffic": traffic, "traffic_source": tsrc,
             "traffic_unit": "HBM bytes per launch (PMC, family average)",
             "kernel": kern + " (PixelCNN++ head forward convolutions, all instances%s)"
-                      % (", split mode: 3 fp16 plane products per conv (6 bf16 ones where channels %% 8 != 0)"
+                      % (", split mode: 3 fp16 plane products per conv (6 bf16 ones where channels % 8 != 0)"
                          if planes > 1 else ""),
             "issued": round(ach * iflops / pflops, 3), "frac_issued": round(ach * iflops / pflops / BF16_MFMA_PEAK_TFLOPS, 5),
             "timed_convs": len(probe), "avg_conv_us": round(pms * 1e3 / max(1, len(probe)), 2),
