@@ -26,7 +26,10 @@ typedef __bf16 x3_16x8 __attribute__((ext_vector_type(8)));  // 8 raw 16-bit lan
 
 #define X3_CK 32    // channels per window stage
 #define X3_ROWP 40  // LDS pixel pitch in 16-bit elements (80 B: conflict-free 16-B fragment reads)
-#define X3_OCC(BM, NP) ((NP) == 2 ? ((BM) == 128 ? 2 : (BM) == 64 ? 3 : 4) : ((BM) == 128 ? 2 : 4))
+#ifndef X3_OCC_S32
+#define X3_OCC_S32 3  // 32-row split instances: 3 waves per SIMD (at 4 the PI = 4 instance spilt 20 VGPRs; 14.93 vs 15.04 ms, profiles/r05_x3_occ_ab.txt)
+#endif
+#define X3_OCC(BM, NP) ((NP) == 2 ? ((BM) == 128 ? 2 : (BM) == 64 ? 3 : X3_OCC_S32) : ((BM) == 128 ? 2 : 4))
 #ifndef X3_BMMAX
 #define X3_BMMAX 128  // largest row tile (16-tap layers; the stride-2 conv-T takes <= 64: four classes per block)
 #endif
