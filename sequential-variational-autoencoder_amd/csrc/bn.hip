@@ -227,6 +227,41 @@ void bn_apply(const float* pre, int ldp, long long pre_gs, long long rows, int C
                        eps, mean, invstd, ms_gs, beta, beta_gs, res, ldr, res_gs, act, out, ldo, out_gs, g.rpb, out_bf16);
 }
 
+// Statistics finalised ONCE per BN layer (svae_ctx::bnfin): one thread per channel sums the accumulator
+// shards and writes what every apply block would otherwise compute from its own gather (the same fp64
+// expressions: bitwise the per-block path).  The apply passes then read two floats per channel.
+// Forward: mean, invstd.  Backward: ab = [a = mean(dz) | b = mean(dz xhat)] per group, and dbeta.
+__global__ __launch_bounds__(256) void bn_fin_kernel(const u64* acc, long long acc_gs, long long sh, int nsh,
+                                                     long long rows, int C, float eps, float* mean, float* invstd,
+                                                     long long ms_gs, float* ab, float* dbeta, long long dbeta_gs) {
+  const int c = blockIdx.x * 256 + threadIdx.x, group = blockIdx.y;
+  if (c >= C) return;
+  const u64* base = acc + group * acc_gs + 4LL * c;
+  u64 t[4] = {0, 0, 0, 0};
+  for (int k = 0; k < nsh; ++k)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) t[w] += base[k * sh + w];
+  const double cnt = (double)rows;
+  if (ab) {  // backward (bn_bwd_apply_kernel's expressions)
+    const double sd = fx_get(t), sx = fx_get(t + 2);
+    ab[group * 2LL * C + c] = (float)(sd / cnt);
+    ab[group * 2LL * C + C + c] = (float)(sx / cnt);
+    if (dbeta) dbeta[group * dbeta_gs + c] = (float)sd;
+    return;
+  }
+  const double md = fx_get(t) / cnt;  // (bn_apply_kernel's expressions)
+  double var = fx_get(t + 2) / cnt - md * md;
+  if (var < 0.0) var = 0.0;
+  mean[group * ms_gs + c] = (float)md;
+  invstd[group * ms_gs + c] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+void bn_finalize(const u64* acc, long long acc_gs, long long sh, int nsh, long long rows, int C, float eps, float* mean,
+                 float* invstd, long long ms_gs, float* ab, float* dbeta, long long dbeta_gs, int groups, hipStream_t s) {
+  hipLaunchKernelGGL(bn_fin_kernel, dim3((C + 255) / 256, groups), dim3(256), 0, s, acc, acc_gs, sh, nsh, rows, C, eps,
+                     mean, invstd, ms_gs, ab, dbeta, dbeta_gs);
+}
+
 #define BWD_RPB 256  // rows per row-block of the backward reduction
 int bn_bwd_rowblocks(long long rows) { return (int)((rows + BWD_RPB - 1) / BWD_RPB); }
 

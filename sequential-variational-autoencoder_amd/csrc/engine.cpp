@@ -635,6 +635,9 @@ struct svae_ctx {
   // passes read mean / invstd (bit 0, forward) or a, b (bit 1, the fused backward sums) instead of every
   // block finalising its channels (SVAE_BN_LAF; bitwise, but off: 9.5 % / 16 % slower, profiles/r04_laf_ab.txt)
   int laf = 0;
+  // BN statistics finalised by one small launch per layer and pass (SVAE_BN_FIN) instead of by every apply
+  // block from the accumulator shards
+  int bnfin = 0;
   float* Gimp_pub = nullptr;         // caller's improvement-loss gradient (svae_bind_imp)
   float* Gimp_v = nullptr;           // its virtual copy under weight sharing
   // BN statistics: fixed-point column accumulators (common.h stat_put), one region per BN
@@ -1150,6 +1153,11 @@ static int conv_bn_act_fwd(svae_ctx* c, const ConvL& L, int groups, long long w_
     return 0;
   }
   if (dfr_out) *dfr_out = Defer{};
+  if (c->bnfin && !fin && !(dbg_skip() & 16)) {  // the statistics finalised once, read by every apply block
+    bn_finalize(acc.p, acc.gs, acc.sh, acc.nsh, rows, L.cout, 1e-3f, bn.mean, bn.invstd, bn_gs, nullptr, nullptr, 0,
+                groups, c->st);
+    fin = true;
+  }
   bn_apply(pre, L.cout, pre_gs, rows, L.cout, (fin || (dbg_skip() & 16)) ? nullptr : acc.p, acc.gs, acc.sh, acc.nsh, 1e-3f, bn.mean,
            bn.invstd, bn_gs, c->P + L.obeta, w_gs, res.p, res.ld, res.gs, act, out.p, out.ld, out.gs, groups, c->st, out.bf,
            c->pbf);
@@ -1399,9 +1407,17 @@ static int bn_act_bwd(svae_ctx* c, int groups, long long rows, int C, View dy, V
     bn_bwd_reduce(dy.p, dy.ld, dy.gs, yp, y.ld, y.gs, pre, ldp, pre_gs, rows, C, bn.mean, bn.invstd, bn_gs, beta, w_gs,
                   act, acc.p, acc.gs, acc.sh, acc.nsh, groups, c->st, pre_bf16, yp ? y.bf : 0);
   if ((dbg_skip() & 2) && !dres.p && rows > c->m.g.B) return 0;  // TIMING PROBE ONLY (wrong results)
+  const float* ab = pre_reduced ? fu->ab : nullptr;
+  if (c->bnfin && !ab) {  // a, b and dbeta finalised once, read by every apply block
+    float* t = (float*)acc_take(c, (long long)groups * C);  // [group][2C] floats
+    if (!t) return fail(c, SVAE_EBADARG, "BN accumulator arena too small");
+    bn_finalize(acc.p, acc.gs, acc.sh, acc.nsh, rows, C, 1e-3f, nullptr, nullptr, 0, t, c->Gr + beta_off, w_gs, groups,
+                c->st);
+    ab = t;
+  }
   bn_bwd_apply(dy.p, dy.ld, dy.gs, yp, y.ld, y.gs, pre, ldp, pre_gs, rows, C, bn.mean, bn.invstd, bn_gs, beta, w_gs,
                acc.p, acc.gs, acc.sh, acc.nsh, c->Gr + beta_off, w_gs, act, dpre, C, dpre_gs, dres.p, dres.ld, dres.gs, res_acc, groups,
-               c->st, dpre_bf16, pre_bf16, pre_reduced ? fu->ab : nullptr, yp ? y.bf : 0);
+               c->st, dpre_bf16, pre_bf16, ab, yp ? y.bf : 0);
   return 0;
 }
 
@@ -2589,6 +2605,7 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
     c->abf = (c->m.g.bf16 && !c->m.g.split && svae_knob("SVAE_ACT_F32", 0) != 1) ? 1 : 0;   // GEMM-only activations
     c->cbf = (c->abf && svae_knob("SVAE_CAT_F32", 0) != 1) ? 1 : 0;                        // decoder concat buffers
     c->laf = svae_knob("SVAE_BN_LAF", 0);  // last-arriver BN finalisation (experimental: off)
+    c->bnfin = svae_knob("SVAE_BN_FIN", 0);
     c->pbf = (c->m.g.bf16 && !c->m.g.split && svae_knob("SVAE_PRE_F32", 0) != 1) ? 1 : 0;   // conv pre-BN outputs
   }
   c->counting = true;

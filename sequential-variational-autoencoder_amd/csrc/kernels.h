@@ -187,6 +187,9 @@ void bn_apply(const float* pre, int ldp, long long pre_gs, long long rows, int C
               hipStream_t s, int out_bf16 = 0,   // out_bf16: write the activation as bf16 (RNE)
               int pre_bf16 = 0);                 // pre_bf16: pre is stored as bf16
 // sums of dz and dz*xhat, dz = dy*act'(y)   -> added into acc[group][4*C]
+// the layer's statistics finalised once (forward: mean / invstd; backward, ab != NULL: [a | b] per group and dbeta)
+void bn_finalize(const u64* acc, long long acc_gs, long long sh, int nsh, long long rows, int C, float eps, float* mean,
+                 float* invstd, long long ms_gs, float* ab, float* dbeta, long long dbeta_gs, int groups, hipStream_t s);
 void bn_bwd_reduce(const float* dy, int lddy, long long dy_gs, const float* y, int ldy, long long y_gs,
                    const float* pre, int ldp, long long pre_gs, long long rows, int C, const float* mean,
                    const float* invstd, long long ms_gs, const float* beta, long long beta_gs, int act, u64* acc,

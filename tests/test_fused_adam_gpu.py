@@ -232,6 +232,24 @@ def test_bn_last_arriver_finalisation_is_bitwise(preset, dtype, batch, fused, mo
     np.testing.assert_array_equal(p0, p1)
 
 
+@pytest.mark.parametrize("preset,dtype,batch", [
+    ("tiny", "fp32", 4), ("tiny", "bf16", 4), ("celeba", "bf16", 128), ("celeba", "bf16x6", 128),
+    ("tiny_homog", "bf16x6", 4),
+])
+@pytest.mark.parametrize("fused", [False, True])
+def test_bn_finalise_once_is_bitwise(preset, dtype, batch, fused, monkeypatch, knob_lib):
+    """SVAE_BN_FIN: each conv BN layer's statistics (forward mean / invstd, backward a, b, dbeta) finalised by
+    one small launch (bn.hip bn_fin_kernel) instead of by every apply block from the accumulator shards --
+    the same fp64 expressions over the same integer sums, so three training steps are bitwise equal."""
+    monkeypatch.setenv("SVAE_BN_FIN", "0")
+    p0, l0, _ = _run(preset, dtype, fused, {}, batch=batch)
+    monkeypatch.setenv("SVAE_BN_FIN", "1")
+    p1, l1, changed = _run(preset, dtype, fused, {}, batch=batch)
+    assert changed > 0
+    assert l0 == l1, (l0, l1)
+    np.testing.assert_array_equal(p0, p1)
+
+
 @pytest.mark.parametrize("preset,dtype,batch,over", [
     ("tiny", "bf16", 4, {}), ("celeba", "bf16", 128, {}), ("tiny_homog", "bf16", 4, {}),
     ("tiny", "bf16", 4, {"predict_latent_code": True}),
