@@ -941,11 +941,16 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
     rc.img = n * g.Hi * g.Wi;
     return rc;
   };
+  // staging unit u -> (channel quad, pixel quad): eight consecutive lanes take the eight pixel quads of one
+  // channel quad, so the transposed 8-byte LDS stores of 32 lanes (4 channel quads x 8 pixel quads, rows 4
+  // apart at an 80-B pitch) hit 64 distinct banks (u % QMc put 32 channel quads of one pixel quad on 4 bank
+  // offsets: 8-way conflicts); the global loads still use whole 128-B lines (8 channel quads x 8 pixels)
+  constexpr int PQ = BKB / 4;  // pixel quads per K chunk
   // per-unit (tap, channel) of the A rows this thread stages (fixed over the K loop)
   int utap[RA], um[RA], uky[RA], ukx[RA];
 #pragma unroll
   for (int i = 0; i < RA; ++i) {
-    const int r = r0 + ((tid + 256 * i) % QMc) * 4;
+    const int r = r0 + ((tid + 256 * i) / PQ) * 4;
     utap[i] = r / a.M;
     um[i] = r - utap[i] * a.M;
     uky[i] = utap[i] / g.ksz;
@@ -957,8 +962,8 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
 #pragma unroll
     for (int i = 0; i < RA; ++i) {
       const int u = tid + 256 * i;
-      const int pq = u / QMc;
-      const int r = r0 + (u % QMc) * 4;
+      const int pq = u % PQ;
+      const int r = r0 + (u / PQ) * 4;
       if (VECG) {
         // a quad of 4 row-space pixels never crosses an image row (chunks are 32-aligned and
         // every row-space width is a multiple of 4): decode it once, step x by the stride
@@ -1013,7 +1018,7 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
 #pragma unroll
     for (int i = 0; i < RB; ++i) {
       const int u = tid + 256 * i;
-      const int nq = u % QNc, pq = u / QNc;
+      const int nq = u / PQ, pq = u % PQ;
       const int nc = n0 + nq * 4;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -1029,7 +1034,7 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
     for (int i = 0; i < RA; ++i) {
       const int u = tid + 256 * i;
       if (u >= UA) continue;
-      const int mq = u % QMc, pq = u / QMc;
+      const int mq = u / PQ, pq = u % PQ;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const bool rg = VECG && gbf;  // raw bf16 bits (the scalar gather path holds fp32 values)
@@ -1049,7 +1054,7 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
     for (int i = 0; i < RB; ++i) {
       const int u = tid + 256 * i;
       if (u >= UB) continue;
-      const int nq = u % QNc, pq = u / QNc;
+      const int nq = u / PQ, pq = u % PQ;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         f32x4 col = {raw4_elem(vb[i][0], c, dbf), raw4_elem(vb[i][1], c, dbf), raw4_elem(vb[i][2], c, dbf),
