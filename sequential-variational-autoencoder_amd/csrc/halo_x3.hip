@@ -29,7 +29,11 @@ typedef __bf16 x3_16x8 __attribute__((ext_vector_type(8)));  // 8 raw 16-bit lan
 #ifndef X3_OCC_S32
 #define X3_OCC_S32 3  // 32-row split instances: 3 waves per SIMD (at 4 the PI = 4 instance spilt 20 VGPRs; 14.93 vs 15.04 ms, profiles/r05_x3_occ_ab.txt)
 #endif
-#define X3_OCC(BM, NP) ((NP) == 2 ? ((BM) == 128 ? 2 : (BM) == 64 ? 3 : X3_OCC_S32) : ((BM) == 128 ? 2 : 4))
+#define X3_OCC(BM, NP, PI) \
+  ((PI) > 4 ? 2 : (NP) == 2 ? ((BM) == 128 ? 2 : (BM) == 64 ? 3 : X3_OCC_S32) : ((BM) == 128 ? 2 : 4))
+#ifndef X3_PI8
+#define X3_PI8 1  // 64-row tiles of the stride-2 convs with 8 window items per thread (their windows are 4x)
+#endif
 #ifndef X3_BMMAX
 #define X3_BMMAX 128  // largest row tile (16-tap layers; the stride-2 conv-T takes <= 64: four classes per block)
 #endif
@@ -60,7 +64,7 @@ namespace {
 // NP = 1: the bf16 mode (A fp32 or, ABF, stored bf16; one bf16 plane; bf16-stored pre-BN outputs c_bf16 and
 //         the fused backward-BN terms on bf16-stored pre / y).
 template <int BM, bool CPW, int PI, int NP = 2, bool ABF = false>
-__global__ __launch_bounds__(256, X3_OCC(BM, NP)) void gather_x3_kernel(X3Args h) {
+__global__ __launch_bounds__(256, X3_OCC(BM, NP, PI)) void gather_x3_kernel(X3Args h) {
   static_assert(NP == 2 || NP == 1, "fp16 hi/lo planes or one bf16 plane");
   static_assert(NP == 1 || !ABF, "the split planes come from fp32 activations");
   constexpr int TM = BM / 32;
@@ -419,7 +423,9 @@ static bool x3_plan(const FwdArgs& a, int groups, X3Plan* out) {
     h.PC = (Wr - 1) * sy + span;
     h.npix = nimg * h.PR * h.PC;
     const int pi = (h.npix * 4 + 255) / 256;
-    if (pi > 4) continue;
+    // the stride-2 convs' windows are four times a stride-1 one per output row: 64-row tiles take 8 items per
+    // thread there (the 32-row tiles they fell back to ran 24 MFMAs per wave between two barriers)
+    if (pi > ((X3_PI8 && bm == 64 && !s2t) ? 8 : 4)) continue;
     const long long blocks = (long long)(a.rows / bm) * (a.N / 32) * groups;
     if (blocks < 256 && bm > 32) continue;
     // stride-2 conv-T: one block per 4 classes' tiles; the 4x4-input levels give too few blocks
@@ -444,7 +450,7 @@ static bool x3_plan(const FwdArgs& a, int groups, X3Plan* out) {
       h.tsgn = -1;
     }
     out->bm = bm;
-    out->pi = pi <= 3 ? 3 : 4;
+    out->pi = pi <= 3 ? 3 : (pi <= 4 ? 4 : 8);
     out->cpw = s2t;
     const size_t win = (size_t)(split ? 2 : 1) * h.npix * X3_ROWP * 2;  // NP planes
     const size_t red = (size_t)4 * bm * 32 * 4;
@@ -491,6 +497,7 @@ int halo_x3(const FwdArgs& a, int groups, hipStream_t s) {
     X3_ATTR(64, false, 4, 1, true) X3_ATTR(32, false, 4, 1, false) X3_ATTR(32, false, 4, 1, true)
     X3_ATTR(64, true, 4, 1, false) X3_ATTR(64, true, 4, 1, true) X3_ATTR(32, true, 4, 1, false)
     X3_ATTR(32, true, 4, 1, true)
+    X3_ATTR(64, false, 8, 2, false) X3_ATTR(64, false, 8, 1, false) X3_ATTR(64, false, 8, 1, true)
 #undef X3_ATTR
     attr = true;
   }
@@ -501,6 +508,12 @@ int halo_x3(const FwdArgs& a, int groups, hipStream_t s) {
   if (a.a_bf16) X3_LAUNCH(BM_, CPW_, 4, 1, true); else X3_LAUNCH(BM_, CPW_, 4, 1, false);
 #define X3_SP(BM_, CPW_) \
   if (p.pi == 3) X3_LAUNCH(BM_, CPW_, 3, 2, false); else X3_LAUNCH(BM_, CPW_, 4, 2, false);
+  if (p.pi == 8) {  // (64-row tiles of the stride-2 convs only)
+    if (split) X3_LAUNCH(64, false, 8, 2, false);
+    else if (a.a_bf16) X3_LAUNCH(64, false, 8, 1, true);
+    else X3_LAUNCH(64, false, 8, 1, false);
+    return a.rows / p.bm;
+  }
   if (p.bm == 128) {
     if (split) { X3_SP(128, false) } else { X3_BF(128, false) }
   } else if (p.bm == 64) {

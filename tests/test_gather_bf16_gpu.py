@@ -33,6 +33,8 @@ SHAPES = [
     # CelebA B=128 small-image layers: path 2 runs them on the wave-split kernel (csrc/halo_kw.hip)
     # with 64-row tiles instead of grid split-K
     (128, 8, 256, 128, 1, 1), (128, 4, 384, 128, 2, 1), (128, 8, 128, 128, 1, 0), (128, 8, 128, 64, 2, 1),
+    # stride-2 convs at B = 128: halo_x3's 64-row tiles with 8 window items per thread
+    (128, 32, 32, 64, 2, 0), (128, 16, 64, 128, 2, 0),
 ]
 
 

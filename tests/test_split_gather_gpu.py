@@ -24,6 +24,7 @@ SHAPES = [
     (128, 16, 64, 32, 2, 1), (128, 8, 128, 64, 2, 1),                        # conv-T s2: class per wave
     (128, 4, 384, 128, 2, 1), (16, 8, 128, 64, 2, 1),                        # conv-T s2: the halo_kw fallback
     (8, 16, 64, 32, 1, 0), (8, 32, 32, 64, 1, 0),                            # input-gradient shapes
+    (128, 32, 32, 64, 2, 0), (128, 16, 64, 128, 2, 0),                       # conv s2: 64-row tiles, 8 items
 ]
 
 

@@ -35,6 +35,17 @@ for lo, hi in bins:
     sel = [g for g in gaps if lo <= g < hi]
     print("  gap [%g, %g) us: %4d gaps, %8.1f us" % (lo, hi, len(sel), sum(sel)))
 name = lambda n: n.replace('void ', '').replace('(anonymous namespace)::', '').split('(')[0][:40]
+# which transitions the 4-10 us gaps follow (launch boundaries after event records vs plain dependencies)
+mid = collections.Counter()
+mid_t = collections.defaultdict(float)
+for i, gp in enumerate(gaps):
+    if 4 <= gp < 10:
+        k = "%s -> %s" % (name(ms[i][0]).split('<')[0], name(ms[i + 1][0]).split('<')[0])
+        mid[k] += 1
+        mid_t[k] += gp
+print("  4-10 us gaps by transition:")
+for k, v in mid.most_common(14):
+    print("    %4d %8.1f us  %s" % (v, mid_t[k], k))
 order = sorted(range(len(gaps)), key=lambda i: -gaps[i])[:int(sys.argv[3]) if len(sys.argv) > 3 else 20]
 for i in sorted(order):
     print("  %7.1f us after %-40s before %-40s" % (gaps[i], name(ms[i][0]), name(ms[i + 1][0])))
