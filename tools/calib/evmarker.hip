@@ -40,8 +40,8 @@ int main() {
   hipEventCreate(&t0);
   hipEventCreate(&t1);
   int *flags, *bad;
-  void* seq;  // mode 7's sequence word (host-visible: the stream value ops want signal-capable memory)
-  if (hipExtMallocWithFlags(&seq, 64, hipMallocSignalMemory) != hipSuccess) return 1;
+  void* seq;  // mode 7's sequence word
+  if (hipMalloc(&seq, 64) != hipSuccess) return 2;
   float* buf;
   const long long nfloat = 1LL << 20;  // 4 MB written per kernel
   if (hipMalloc(&flags, K * sizeof(int)) != hipSuccess || hipMalloc(&bad, sizeof(int)) != hipSuccess ||
