@@ -210,7 +210,7 @@ __global__ __launch_bounds__(256, X3_OCC(BM, NP, PI)) void gather_x3_kernel(X3Ar
       const int ns = h16_exp(hmax);
       const int d = ns - hs;
       hs = ns;
-      if (d != 0) {
+      if (d != 0 && c > 0) {  // (before the first chunk the accumulators are zero)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -253,13 +253,15 @@ __global__ __launch_bounds__(256, X3_OCC(BM, NP, PI)) void gather_x3_kernel(X3Ar
 
   // ---- the waves' tiles into LDS (in the units of C), then one epilogue over the block ----
   float* red = (float*)xsm;  // [4][BM][32]
+  // (the split mode's tiles in units of 2^(hs + H16_WS), shared by the block's waves: the reduced sums are
+  // unscaled below -- exact, as every partial carries the same power of two)
   const int usc = NP == 2 ? -(hs + H16_WS) : 0;
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int m = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-      red[(wave * BM + m) * 32 + l32] = NP == 2 ? __builtin_ldexpf(acc[tm][r], usc) : acc[tm][r];
+      red[(wave * BM + m) * 32 + l32] = acc[tm][r];
     }
   __syncthreads();
   X3_STAMP(11);
@@ -316,6 +318,10 @@ __global__ __launch_bounds__(256, X3_OCC(BM, NP, PI)) void gather_x3_kernel(X3Ar
       if constexpr (!CPW) {
 #pragma unroll
         for (int w = 1; w < 4; ++w) v += *(const f32x4*)&red[(w * BM + vr) * 32 + c4];
+      }
+      if constexpr (NP == 2) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = __builtin_ldexpf(v[j], usc);
       }
       if (NP == 1 && h.c_bf16) {  // bf16-stored pre-BN output: the statistics of the stored values
 #pragma unroll

@@ -119,10 +119,12 @@ __device__ __forceinline__ f32x16 mfma_split(const ol_bf16x8 (&a)[NS], const ol_
 // T=8 step: x_hat_t error vs float64 below the fp32 twin's at every t.
 typedef _Float16 ol_f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 ol_f16x4 __attribute__((ext_vector_type(4)));
+// (x * 2^s as a multiply by the exact power of two -- packed v_pk_mul_f32, correctly rounded like ldexp;
+// h16_exp keeps s within the normal exponent range)
 __device__ __forceinline__ void split8_h16(f32x4 lo, f32x4 hi, int s, ol_bf16x8 (&p)[2]) {
-  ol_f32x8 v = {__builtin_ldexpf(lo[0], s), __builtin_ldexpf(lo[1], s), __builtin_ldexpf(lo[2], s),
-                __builtin_ldexpf(lo[3], s), __builtin_ldexpf(hi[0], s), __builtin_ldexpf(hi[1], s),
-                __builtin_ldexpf(hi[2], s), __builtin_ldexpf(hi[3], s)};
+  const float sc = __uint_as_float((unsigned)(s + 127) << 23);
+  ol_f32x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  v *= sc;
   const ol_f16x8 h0 = __builtin_convertvector(v, ol_f16x8);
   v = v - __builtin_convertvector(h0, ol_f32x8);
   const ol_f16x8 h1 = __builtin_convertvector(v, ol_f16x8);
@@ -146,5 +148,6 @@ __device__ __forceinline__ f32x16 mfma_h16(const ol_bf16x8 (&a)[2], const ol_bf1
 // exponent s with max * 2^s in [2^14, 2^15) for a non-negative finite max (0: s = 0)
 __device__ __forceinline__ int h16_exp(float mx) {
   const int e = (int)((__float_as_uint(mx) >> 23) & 0xff);
-  return mx > 0.f ? 14 - (e - 127) : 0;
+  const int s = mx > 0.f ? 14 - (e - 127) : 0;
+  return s < 126 ? s : 126;  // (a maximum below 2^-112: the planes then sit below the top binade)
 }
