@@ -471,20 +471,24 @@ struct Pc3 {
 #define PC3_MAXPIX 640
 #define PC3_MAXTAPS 6
 // XB: X stored as bf16 (a nonlinearity output the head writes in the conv's operand precision)
-template <int NT, int TM, bool XB, bool H = false>
+// HP (with H): both fp16 planes of x (xpst elements apart) and of the weights (wpst apart) staged per chunk, the
+// three plane products h0 h0' + h0 h1' + h1 h0' per fragment pair in ONE launch (svae_pcnn_conv_planes)
+template <int NT, int TM, bool XB, bool H = false, bool HP = false>
 __global__ __launch_bounds__(512) void pc_conv3_kernel(PcGeom g, Pc3 h, const void* __restrict__ Xv,
                                                        const __bf16* __restrict__ Wk, int kpad,
                                                        const float* __restrict__ bias, float* __restrict__ Y,
                                                        int ldy, int accumulate, int zero_edge, NlbArgs nlb,
-                                                       PcScale sc) {
+                                                       PcScale sc, long long xpst, long long wpst) {
   static_assert(XB || !H, "fp16 planes are stored 16-bit");
+  static_assert(H || !HP, "fused planes are the fp16 ones");
+  constexpr int NPL = HP ? 2 : 1;
   constexpr int BM = 256 * TM;
   constexpr int BR = 32 * NT;                                  // weight rows (output channels) per tap
   constexpr int AI = (PC3_MAXPIX * 4 + 511) / 512;             // window items (8 channels) per thread
   constexpr int BI = (PC3_MAXTAPS * BR * 4 + 511) / 512;       // 16-B weight items per thread
   extern __shared__ __attribute__((aligned(16))) __bf16 pc3s[];
-  __bf16* As = pc3s;                    // [npix][PC2_P]
-  __bf16* Bs = pc3s + h.npix * PC2_P;   // [tap][BR][PC2_P]
+  __bf16* As = pc3s;                          // [plane][npix][PC2_P]
+  __bf16* Bs = pc3s + NPL * h.npix * PC2_P;   // [plane][tap][BR][PC2_P]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hh = lane >> 5;
   const int taps = g.kh * g.kw;
   const int per_img = g.ho * g.wo;
@@ -514,8 +518,8 @@ __global__ __launch_bounds__(512) void pc_conv3_kernel(PcGeom g, Pc3 h, const vo
   const float* X = (const float*)Xv;
   const __bf16* Xh = (const __bf16*)Xv;
   f32x4 ra[XB ? 1 : AI][2];
-  pc_bf16x8 rh[XB ? AI : 1];
-  pc_bf16x8 rb[BI];
+  pc_bf16x8 rh[XB ? AI : 1], rh1[HP ? AI : 1];
+  pc_bf16x8 rb[BI], rb1[HP ? BI : 1];
   const int nb = taps * BR;  // staged weight rows
   auto load = [&](int c) {
     const int k0 = c * 32;
@@ -524,7 +528,9 @@ __global__ __launch_bounds__(512) void pc_conv3_kernel(PcGeom g, Pc3 h, const vo
       const int ci = k0 + ((tid + 512 * i) & 3) * 8;
       if constexpr (XB) {  // 8 channels = one 16-B load (cin % 8 == 0)
         pc_bf16x8 z = {};
-        rh[i] = (aoff[i] >= 0 && ci < g.cin) ? *(const pc_bf16x8*)(Xh + aoff[i] + k0) : z;
+        const bool ok = aoff[i] >= 0 && ci < g.cin;
+        rh[i] = ok ? *(const pc_bf16x8*)(Xh + aoff[i] + k0) : z;
+        if constexpr (HP) rh1[i] = ok ? *(const pc_bf16x8*)(Xh + xpst + aoff[i] + k0) : z;
       } else {
         const f32x4 z = {0.f, 0.f, 0.f, 0.f};
         ra[i][0] = z;
@@ -541,8 +547,10 @@ __global__ __launch_bounds__(512) void pc_conv3_kernel(PcGeom g, Pc3 h, const vo
       const int it = tid + 512 * i, row = it >> 2, q = it & 3;
       const int t = row / BR, n = row - t * BR;
       pc_bf16x8 z = {};
-      rb[i] = (row < nb && n0 + n < g.cout) ? *(const pc_bf16x8*)(Wk + ((long long)t * g.cout + n0 + n) * kpad + k0 + q * 8)
-                                            : z;
+      const bool ok = row < nb && n0 + n < g.cout;
+      const long long wo = ((long long)t * g.cout + n0 + n) * kpad + k0 + q * 8;
+      rb[i] = ok ? *(const pc_bf16x8*)(Wk + wo) : z;
+      if constexpr (HP) rb1[i] = ok ? *(const pc_bf16x8*)(Wk + wpst + wo) : z;
     }
   };
   auto store = [&]() {
@@ -552,6 +560,7 @@ __global__ __launch_bounds__(512) void pc_conv3_kernel(PcGeom g, Pc3 h, const vo
       const int it = tid + 512 * i;
       if constexpr (XB) {
         *(pc_bf16x8*)&As[(it >> 2) * PC2_P + (it & 3) * 8] = rh[i];
+        if constexpr (HP) *(pc_bf16x8*)&As[(h.npix + (it >> 2)) * PC2_P + (it & 3) * 8] = rh1[i];
       } else {
         const pc_f32x8 v8 = {ra[i][0][0], ra[i][0][1], ra[i][0][2], ra[i][0][3],
                              ra[i][1][0], ra[i][1][1], ra[i][1][2], ra[i][1][3]};
@@ -561,7 +570,10 @@ __global__ __launch_bounds__(512) void pc_conv3_kernel(PcGeom g, Pc3 h, const vo
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
       const int it = tid + 512 * i, row = it >> 2, q = it & 3;
-      if (row < nb) *(pc_bf16x8*)&Bs[row * PC2_P + q * 8] = rb[i];
+      if (row < nb) {
+        *(pc_bf16x8*)&Bs[row * PC2_P + q * 8] = rb[i];
+        if constexpr (HP) *(pc_bf16x8*)&Bs[(nb + row) * PC2_P + q * 8] = rb1[i];
+      }
     }
   };
 
@@ -596,14 +608,27 @@ __global__ __launch_bounds__(512) void pc_conv3_kernel(PcGeom g, Pc3 h, const vo
       const __bf16* bt = Bs + (t * BR + l32) * PC2_P + 8 * hh;
 #pragma unroll
       for (int kq = 0; kq < 2; ++kq) {
-        pc_bf16x8 af[TM];
+        pc_bf16x8 af[TM], af1[HP ? TM : 1];
 #pragma unroll
-        for (int tm = 0; tm < TM; ++tm) af[tm] = *(const pc_bf16x8*)&As[abase[tm] + toff + kq * 16];
+        for (int tm = 0; tm < TM; ++tm) {
+          af[tm] = *(const pc_bf16x8*)&As[abase[tm] + toff + kq * 16];
+          if constexpr (HP) af1[tm] = *(const pc_bf16x8*)&As[h.npix * PC2_P + abase[tm] + toff + kq * 16];
+        }
 #pragma unroll
         for (int tn = 0; tn < NT; ++tn) {
           const pc_bf16x8 bf = *(const pc_bf16x8*)(bt + tn * 32 * PC2_P + kq * 16);
+          if constexpr (HP) {  // h0 h0' + h0 h1' + h1 h0'
+            const pc_bf16x8 bf1 = *(const pc_bf16x8*)(bt + (nb + tn * 32) * PC2_P + kq * 16);
 #pragma unroll
-          for (int tm = 0; tm < TM; ++tm) acc[tm][tn] = pc_mfma<H>(af[tm], bf, acc[tm][tn]);
+            for (int tm = 0; tm < TM; ++tm) {
+              acc[tm][tn] = pc_mfma<true>(af[tm], bf, acc[tm][tn]);
+              acc[tm][tn] = pc_mfma<true>(af[tm], bf1, acc[tm][tn]);
+              acc[tm][tn] = pc_mfma<true>(af1[tm], bf, acc[tm][tn]);
+            }
+          } else {
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) acc[tm][tn] = pc_mfma<H>(af[tm], bf, acc[tm][tn]);
+          }
         }
       }
     }
@@ -706,20 +731,22 @@ bool pc3_plan(const PcGeom& g, int kpad, int TM, Pc3* out, size_t* lds) {
   return true;
 }
 
-template <int NT, int TM, bool XB, bool H = false>
+template <int NT, int TM, bool XB, bool H = false, bool HP = false>
 void pc3_launch(const PcGeom& g, const Pc3& h, const void* x, const __bf16* w, int kpad, const float* bias, float* y,
-                int ldy, int accumulate, int zero_edge, const NlbArgs& nlb, const PcScale& sc, hipStream_t st) {
-  const size_t lds = (size_t)(h.npix + g.kh * g.kw * 32 * NT) * PC2_P * 2;
+                int ldy, int accumulate, int zero_edge, const NlbArgs& nlb, const PcScale& sc, hipStream_t st,
+                long long xpst = 0, long long wpst = 0) {
+  const size_t lds = (size_t)(h.npix + g.kh * g.kw * 32 * NT) * PC2_P * 2 * (HP ? 2 : 1);
   static bool attr = false;
-  if (!attr) {  // the largest window + weight stage: 640 pixels + 6 taps x 160 rows (128 KB)
-    (void)hipFuncSetAttribute((const void*)pc_conv3_kernel<NT, TM, XB, H>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (PC3_MAXPIX + PC3_MAXTAPS * 32 * NT) * PC2_P * 2);
+  if (!attr) {  // the largest window + weight stage: 640 pixels + 6 taps x 160 rows (128 KB); HP: the 160 KB cap
+    const int mx = (PC3_MAXPIX + PC3_MAXTAPS * 32 * NT) * PC2_P * 2 * (HP ? 2 : 1);
+    (void)hipFuncSetAttribute((const void*)pc_conv3_kernel<NT, TM, XB, H, HP>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, mx < 160 * 1024 ? mx : 160 * 1024);
     attr = true;
   }
   const long long rows = (long long)g.n * g.ho * g.wo;
   const dim3 grid((unsigned)(rows / (256 * TM)), (unsigned)((g.cout + 32 * NT - 1) / (32 * NT)));
-  hipLaunchKernelGGL((pc_conv3_kernel<NT, TM, XB, H>), grid, dim3(512), lds, st, g, h, x, w, kpad, bias, y, ldy,
-                     accumulate, zero_edge, nlb, sc);
+  hipLaunchKernelGGL((pc_conv3_kernel<NT, TM, XB, H, HP>), grid, dim3(512), lds, st, g, h, x, w, kpad, bias, y, ldy,
+                     accumulate, zero_edge, nlb, sc, xpst, wpst);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2142,6 +2169,30 @@ int svae_pcnn_conv_wgrad_planes(const void* x, int n, int hi, int wi, int cin, i
                          dW, nullptr, scratch, scratch_elems, stream, PcScale{x_scale, dy_scale});
 }
 
+// The fp16-plane conv in ONE launch of the halo kernel with both planes staged (pc_conv3 HP): 1 if the launch is
+// not eligible (stride 2, a window or stage beyond the LDS budget) -- the caller then runs the three products
+static int pcnn_conv_hp(const void* x, int n, int hi, int wi, int cin, int ldx, long long xpst, const void* wk, int kpad,
+                        long long wpst, const PcScale& sc, const float* bias, float* y, int ho, int wo, int cout, int ldy,
+                        int kh, int kw, int s, int pt, int pl, int mode, int accumulate, int zero_edge, void* stream) {
+  const PcGeom g = make_geom(n, hi, wi, cin, ldx, ho, wo, cout, kh, kw, s, pt, pl, mode);
+  if (!geom_ok(g) || cin % 8 || ldx % 8 || kpad % 32 || ldy < cout) return 1;
+  if (svae_knob("SVAE_PC_HP", 1) == 0) return 1;
+  Pc3 h;
+  size_t lds0 = 0;
+  if (!pc3_plan(g, kpad, 1, &h, &lds0)) return 1;
+  const int n32 = (cout + 31) / 32;
+  int tiles = (n32 + 1) / 2;  // at most 64 columns per block: two planes of window and weights in LDS
+  const int NT = (n32 + tiles - 1) / tiles;
+  const size_t lds = (size_t)(h.npix + kh * kw * 32 * NT) * PC2_P * 2 * 2;
+  if (lds > 160 * 1024) return 1;
+  NlbArgs nlb{};
+  const __bf16* w = (const __bf16*)wk;
+  hipStream_t st = (hipStream_t)stream;
+  if (NT == 1) pc3_launch<1, 1, true, true, true>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, sc, st, xpst, wpst);
+  else pc3_launch<2, 1, true, true, true>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, sc, st, xpst, wpst);
+  return hipchk();
+}
+
 int svae_pcnn_conv_planes(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, int64_t x_pstride,
                           const void* wk, int kpad, int planes, const float* x_scale, const float* w_scale,
                           const float* bias, float* y, int ho, int wo, int cout, int ldy, int kh, int kw, int s, int pt,
@@ -2150,6 +2201,11 @@ int svae_pcnn_conv_planes(const void* x, int n, int hi, int wi, int cin, int ldx
       (x_scale && planes != 2))
     return bad("pcnn_conv_planes: bad arguments");
   const PcScale sc{x_scale, w_scale};
+  if (x_scale && x_bf16) {  // the fp16 planes: all three products in one launch where the halo kernel takes it
+    const int rc = pcnn_conv_hp(x, n, hi, wi, cin, ldx, x_pstride, wk, kpad, (long long)kh * kw * cout * kpad, sc, bias,
+                                y, ho, wo, cout, ldy, kh, kw, s, pt, pl, mode, accumulate, zero_edge, stream);
+    if (rc <= 0) return rc;
+  }
   int pi[PC_MAXPLANES * PC_MAXPLANES], pj[PC_MAXPLANES * PC_MAXPLANES];
   const int np = pc_products(planes, pi, pj);
   const long long wst = (long long)kh * kw * cout * kpad;  // one weight plane (wk [tap][cout][kpad])
