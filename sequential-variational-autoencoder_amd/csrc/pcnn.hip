@@ -780,16 +780,21 @@ struct Pw4 {
 #define PW4_MAXPIX 144 // 8 rows x 18 (16-wide images, kw = 3)
 #define PW4_P 72       // LDS pixel pitch (bf16): 64 channels + 8
 // DB: D (the output gradient) stored bf16 -- its MFMA precision (the bias sum is then done upstream)
-template <bool XB, bool DB, bool H = false>
+// HP (with H): both fp16 planes of x and dy staged (xpst / dpst apart), three products per fragment pair
+template <bool XB, bool DB, bool H = false, bool HP = false>
 __global__ __launch_bounds__(256) void pc_wgrad4_kernel(PcGeom g, Pw4 h, const void* __restrict__ Xv,
                                                         const void* __restrict__ Dv, int ldd, float* __restrict__ part,
-                                                        float* __restrict__ bsum) {
+                                                        float* __restrict__ bsum, long long xpst = 0,
+                                                        long long dpst = 0) {
+  static_assert(!HP || (XB && DB && H), "fused planes: 16-bit fp16 x and dy");
   const float* D = (const float*)Dv;
   constexpr int WI = (PW4_MAXPIX * 8 + 255) / 256;  // window items (8 channels) per thread
   constexpr int DI = (PW4_CP * 16 + 255) / 256;     // D items (4 columns) per thread
-  __shared__ __attribute__((aligned(16))) __bf16 smem[(PW4_MAXPIX + PW4_CP) * PW4_P];
+  __shared__ __attribute__((aligned(16))) __bf16 smem[(HP ? 2 : 1) * (PW4_MAXPIX + PW4_CP) * PW4_P];
   __bf16* Ws = smem;                    // [npix][PW4_P]
   __bf16* Dm = smem + h.npix * PW4_P;   // [128][PW4_P]
+  __bf16* Ws1 = Dm + PW4_CP * PW4_P;    // HP: the second planes
+  __bf16* Dm1 = Ws1 + h.npix * PW4_P;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int grp = lane >> 4, i16 = lane & 15, q = i16 >> 2, p4 = i16 & 3, l32 = lane & 31, hh = lane >> 5;
   const int ci0 = blockIdx.x * 64, co0 = blockIdx.y * 64;
@@ -810,8 +815,9 @@ __global__ __launch_bounds__(256) void pc_wgrad4_kernel(PcGeom g, Pw4 h, const v
   f32x4 bacc = {0.f, 0.f, 0.f, 0.f};  // bias column sums: this thread's column quad (tid & 15)
 
   f32x4 xa[XB ? 1 : WI][2];
-  pc_bf16x8 xh[XB ? WI : 1];
+  pc_bf16x8 xh[XB ? WI : 1], xh1[HP ? WI : 1];
   f32x4 dv[DI];
+  pc_bf16x4 dr[HP ? DI : 1], dr1[HP ? DI : 1];  // HP: dy's raw 16-bit lanes
   auto load = [&](int c) {
     const long long p0 = (long long)c * PW4_CP;
     const int img = (int)(p0 / per_img);
@@ -830,6 +836,7 @@ __global__ __launch_bounds__(256) void pc_wgrad4_kernel(PcGeom g, Pw4 h, const v
       if constexpr (XB) {
         pc_bf16x8 z = {};
         xh[i] = off >= 0 ? *(const pc_bf16x8*)((const __bf16*)Xv + off) : z;
+        if constexpr (HP) xh1[i] = off >= 0 ? *(const pc_bf16x8*)((const __bf16*)Xv + xpst + off) : z;
       } else {
         const f32x4 z = {0.f, 0.f, 0.f, 0.f};
         xa[i][0] = off >= 0 ? *(const f32x4*)((const float*)Xv + off) : z;
@@ -840,7 +847,12 @@ __global__ __launch_bounds__(256) void pc_wgrad4_kernel(PcGeom g, Pw4 h, const v
     for (int i = 0; i < DI; ++i) {
       const int it = tid + 256 * i;
       const int k = it >> 4, c4 = (it & 15) * 4;
-      if constexpr (DB)
+      if constexpr (HP) {
+        const pc_bf16x4 z4 = {};
+        const __bf16* dp = (const __bf16*)Dv + (p0 + k) * ldd + co0 + c4;
+        dr[i] = co0 + c4 < g.cout ? *(const pc_bf16x4*)dp : z4;
+        dr1[i] = co0 + c4 < g.cout ? *(const pc_bf16x4*)(dp + dpst) : z4;
+      } else if constexpr (DB)
         dv[i] = co0 + c4 < g.cout
                     ? __builtin_convertvector(*(const pc_bf16x4*)((const __bf16*)Dv + (p0 + k) * ldd + co0 + c4), f32x4)
                     : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -856,6 +868,7 @@ __global__ __launch_bounds__(256) void pc_wgrad4_kernel(PcGeom g, Pw4 h, const v
       __bf16* w = Ws + (it >> 3) * PW4_P + (it & 7) * 8;
       if constexpr (XB) {
         *(pc_bf16x8*)w = xh[i];
+        if constexpr (HP) *(pc_bf16x8*)(Ws1 + (it >> 3) * PW4_P + (it & 7) * 8) = xh1[i];
       } else {
         const pc_f32x8 v8 = {xa[i][0][0], xa[i][0][1], xa[i][0][2], xa[i][0][3],
                              xa[i][1][0], xa[i][1][1], xa[i][1][2], xa[i][1][3]};
@@ -866,6 +879,11 @@ __global__ __launch_bounds__(256) void pc_wgrad4_kernel(PcGeom g, Pw4 h, const v
     for (int i = 0; i < DI; ++i) {
       const int it = tid + 256 * i;
       const int k = it >> 4, c4 = (it & 15) * 4;
+      if constexpr (HP) {
+        *(pc_bf16x4*)(Dm + k * PW4_P + c4) = dr[i];
+        *(pc_bf16x4*)(Dm1 + k * PW4_P + c4) = dr1[i];
+        continue;
+      }
       if (bias_blk) bacc += dv[i];  // (the column quad it & 15 == tid & 15 for every i)
       *(pc_bf16x4*)(Dm + k * PW4_P + c4) = __builtin_convertvector(dv[i], pc_bf16x4);
     }
@@ -890,6 +908,9 @@ __global__ __launch_bounds__(256) void pc_wgrad4_kernel(PcGeom g, Pw4 h, const v
         const int wp = wrow * h.PC + wcol + lk;
         const pc_bf16x8 bf =
             pc_join(pc_tr16(Dm + (k0 + lk) * PW4_P + chb), pc_tr16(Dm + (k0 + lk + 4) * PW4_P + chb));
+        pc_bf16x8 bf1 = {};
+        if constexpr (HP)
+          bf1 = pc_join(pc_tr16(Dm1 + (k0 + lk) * PW4_P + chb), pc_tr16(Dm1 + (k0 + lk + 4) * PW4_P + chb));
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
           if (kx < g.kw) {
@@ -897,6 +918,12 @@ __global__ __launch_bounds__(256) void pc_wgrad4_kernel(PcGeom g, Pw4 h, const v
             const __bf16* wa = Ws + (wp + sh) * PW4_P + cha;
             const pc_bf16x8 af = pc_join(pc_tr16(wa), pc_tr16(wa + 4 * PW4_P));
             acc[kx] = pc_mfma<H>(af, bf, acc[kx]);
+            if constexpr (HP) {
+              const __bf16* wa1 = Ws1 + (wp + sh) * PW4_P + cha;
+              const pc_bf16x8 af1 = pc_join(pc_tr16(wa1), pc_tr16(wa1 + 4 * PW4_P));
+              acc[kx] = pc_mfma<true>(af, bf1, acc[kx]);
+              acc[kx] = pc_mfma<true>(af1, bf, acc[kx]);
+            }
           }
         }
       }
@@ -960,13 +987,18 @@ bool pw4_plan(const PcGeom& g, long long rows, Pw4* out) {
 #define PW_RP 72  // LDS row pitch (bf16): 64 rows + 8 pad
 // bsum != NULL: the blocks of tap 0 and the first ci tile also sum their D rows per column (fp32,
 // before the bf16 staging) into bsum[split][cout]: the conv's bias gradient without another pass over dy
-template <bool XB, bool DB, bool H = false>
+// HP (with H): both fp16 planes of x (xpst apart) and of dy (dpst apart) staged, h0 d0 + h0 d1 + h1 d0 per fragment
+// pair in ONE launch (svae_pcnn_conv_wgrad_planes); dy's 16-bit lanes are staged as raw bits
+template <bool XB, bool DB, bool H = false, bool HP = false>
 __global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const void* __restrict__ Xv,
                                                        const void* __restrict__ Dv, int ldd, long long rows,
                                                        long long rows_per_split, float* __restrict__ part,
-                                                       float* __restrict__ bsum) {
-  __shared__ __attribute__((aligned(16))) __bf16 Xs[2][64 * PW_RP];
-  __shared__ __attribute__((aligned(16))) __bf16 Ds[2][64 * PW_RP];
+                                                       float* __restrict__ bsum, long long xpst = 0,
+                                                       long long dpst = 0) {
+  static_assert(!HP || (XB && DB && H), "fused planes: 16-bit fp16 x and dy");
+  constexpr int NPL = HP ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) __bf16 Xs[NPL][2][64 * PW_RP];
+  __shared__ __attribute__((aligned(16))) __bf16 Ds[NPL][2][64 * PW_RP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int nci = (g.cin + 63) / 64;
   const int ci0 = (blockIdx.x % nci) * 64, co0 = (blockIdx.x / nci) * 64;
@@ -984,7 +1016,8 @@ __global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const void* __r
   // rows, the next chunk loaded into registers while the current one's MFMAs run
   const int lr = tid >> 3, q0 = tid & 7;
   f32x4 xv[2][2], dv[2][2];
-  pc_bf16x8 xb8[2];  // XB: channels 8 q0 .. 8 q0 + 7 of the row in one 16-B load
+  pc_bf16x8 xb8[2], xb81[2];  // XB: channels 8 q0 .. 8 q0 + 7 of the row in one 16-B load
+  pc_bf16x4 dh[HP ? 2 : 1][2][2];  // HP: dy's raw 16-bit lanes, both planes
   auto load = [&](long long rc) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -1003,14 +1036,21 @@ __global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const void* __r
       }
       if constexpr (XB) {
         pc_bf16x8 z8 = {};
-        xb8[u] = (xo >= 0 && ci0 + 8 * q0 < g.cin) ? *(const pc_bf16x8*)((const __bf16*)Xv + xo + ci0 + 8 * q0) : z8;
+        const bool ok = xo >= 0 && ci0 + 8 * q0 < g.cin;
+        xb8[u] = ok ? *(const pc_bf16x8*)((const __bf16*)Xv + xo + ci0 + 8 * q0) : z8;
+        if constexpr (HP) xb81[u] = ok ? *(const pc_bf16x8*)((const __bf16*)Xv + xpst + xo + ci0 + 8 * q0) : z8;
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int c = (q0 + 8 * j) * 4;
         const f32x4 z = {0.f, 0.f, 0.f, 0.f};
         if constexpr (!XB) xv[u][j] = (xo >= 0 && ci0 + c < g.cin) ? *(const f32x4*)((const float*)Xv + xo + ci0 + c) : z;
-        if constexpr (DB)
+        if constexpr (HP) {
+          const pc_bf16x4 z4 = {};
+          const bool ok = dph && co0 + c < g.cout;
+          dh[0][u][j] = ok ? *(const pc_bf16x4*)(dph + co0 + c) : z4;
+          dh[1][u][j] = ok ? *(const pc_bf16x4*)(dph + dpst + co0 + c) : z4;
+        } else if constexpr (DB)
           dv[u][j] = (dph && co0 + c < g.cout) ? __builtin_convertvector(*(const pc_bf16x4*)(dph + co0 + c), f32x4) : z;
         else
           dv[u][j] = (dp && co0 + c < g.cout) ? *(const f32x4*)(dp + co0 + c) : z;
@@ -1033,9 +1073,15 @@ __global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const void* __r
         const int c = (q0 + 8 * j) * 4;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          if constexpr (XB) Xs[buf][(8 * q0 + 4 * j + e) * PW_RP + lr + 32 * u] = xb8[u][4 * j + e];
-          else Xs[buf][(c + e) * PW_RP + lr + 32 * u] = (__bf16)xv[u][j][e];
-          Ds[buf][(c + e) * PW_RP + lr + 32 * u] = (__bf16)dv[u][j][e];
+          if constexpr (XB) Xs[0][buf][(8 * q0 + 4 * j + e) * PW_RP + lr + 32 * u] = xb8[u][4 * j + e];
+          else Xs[0][buf][(c + e) * PW_RP + lr + 32 * u] = (__bf16)xv[u][j][e];
+          if constexpr (HP) {
+            Xs[NPL - 1][buf][(8 * q0 + 4 * j + e) * PW_RP + lr + 32 * u] = xb81[u][4 * j + e];
+            Ds[0][buf][(c + e) * PW_RP + lr + 32 * u] = dh[0][u][j][e];
+            Ds[NPL - 1][buf][(c + e) * PW_RP + lr + 32 * u] = dh[HP ? 1 : 0][u][j][e];
+          } else {
+            Ds[0][buf][(c + e) * PW_RP + lr + 32 * u] = (__bf16)dv[u][j][e];
+          }
         }
       }
   };
@@ -1050,9 +1096,15 @@ __global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const void* __r
     if (more) load(rc + 64);
 #pragma unroll
     for (int kq = 0; kq < 4; ++kq) {
-      const pc_bf16x8 af = *(const pc_bf16x8*)&Xs[buf][(wm * 32 + l32) * PW_RP + kq * 16 + 8 * h];
-      const pc_bf16x8 bf = *(const pc_bf16x8*)&Ds[buf][(wn * 32 + l32) * PW_RP + kq * 16 + 8 * h];
+      const pc_bf16x8 af = *(const pc_bf16x8*)&Xs[0][buf][(wm * 32 + l32) * PW_RP + kq * 16 + 8 * h];
+      const pc_bf16x8 bf = *(const pc_bf16x8*)&Ds[0][buf][(wn * 32 + l32) * PW_RP + kq * 16 + 8 * h];
       acc = pc_mfma<H>(af, bf, acc);
+      if constexpr (HP) {
+        const pc_bf16x8 af1 = *(const pc_bf16x8*)&Xs[NPL - 1][buf][(wm * 32 + l32) * PW_RP + kq * 16 + 8 * h];
+        const pc_bf16x8 bf1 = *(const pc_bf16x8*)&Ds[NPL - 1][buf][(wn * 32 + l32) * PW_RP + kq * 16 + 8 * h];
+        acc = pc_mfma<true>(af, bf1, acc);
+        acc = pc_mfma<true>(af1, bf, acc);
+      }
     }
     if (more) store(buf ^ 1);
     __syncthreads();
@@ -1066,7 +1118,7 @@ __global__ __launch_bounds__(256) void pc_wgrad_kernel(PcGeom g, const void* __r
     if (ci < g.cin && co < g.cout) out[(long long)ci * g.cout + co] = acc[r];
   }
   if (bias_blk) {  // column sums: the 32 row lanes combined in lane order through LDS (the loop's last barrier passed)
-    float* red = (float*)Xs;  // [32][64]
+    float* red = (float*)&Xs[0][0][0];  // [32][64]
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -2046,8 +2098,10 @@ static int pcnn_conv_impl(const void* x, int n, int hi, int wi, int cin, int ldx
 static int pcnn_wgrad_impl(const void* const* xs, const void* const* ds, int nprod, int n, int hi, int wi, int cin,
                            int ldx, int x_bf16, int ldd, int dy_bf16, int ho, int wo, int cout, int kh, int kw, int s,
                            int pt, int pl, int mode, float* dW, float* dbias, float* scratch, int64_t scratch_elems,
-                           void* stream, const PcScale& sc = PcScale{nullptr, nullptr}) {
+                           void* stream, const PcScale& sc = PcScale{nullptr, nullptr}, long long xpst = -1,
+                           long long dpst = -1) {
   const bool H = sc.a != nullptr;  // fp16 planes: both operands 16-bit, the reduce applies the scales
+  const bool HP = H && xpst >= 0;  // ... both planes of each in one launch (the three products fused)
   if (H && (!x_bf16 || !dy_bf16 || !sc.b || dbias)) return bad("pcnn_wgrad: fp16 planes need 16-bit x and dy");
   const PcGeom g = make_geom(n, hi, wi, cin, ldx, ho, wo, cout, kh, kw, s, pt, pl, mode);
   bool ok = nprod >= 1 && nprod <= PC_MAXPLANES * (PC_MAXPLANES + 1) / 2;
@@ -2083,9 +2137,11 @@ static int pcnn_wgrad_impl(const void* const* xs, const void* const* ds, int npr
         const void* x = xs[p];
         const void* dy = ds[p];
         float* slab = scratch + p * ns * wsz;
-#define PW4_L(XBV, DBV) hipLaunchKernelGGL((pc_wgrad4_kernel<XBV, DBV>), grid, dim3(256), 0, st, g4, h, x, dy, ldd, slab, bpart)
-        if (H) hipLaunchKernelGGL((pc_wgrad4_kernel<true, true, true>), grid, dim3(256), 0, st, g4, h, x, dy, ldd, slab,
-                                  bpart);
+#define PW4_L(XBV, DBV) hipLaunchKernelGGL((pc_wgrad4_kernel<XBV, DBV>), grid, dim3(256), 0, st, g4, h, x, dy, ldd, slab, bpart, 0LL, 0LL)
+        if (HP) hipLaunchKernelGGL((pc_wgrad4_kernel<true, true, true, true>), grid, dim3(256), 0, st, g4, h, x, dy, ldd,
+                                   slab, bpart, xpst, dpst);
+        else if (H) hipLaunchKernelGGL((pc_wgrad4_kernel<true, true, true>), grid, dim3(256), 0, st, g4, h, x, dy, ldd,
+                                       slab, bpart, 0LL, 0LL);
         else if (x_bf16) { if (dy_bf16) PW4_L(true, true); else PW4_L(true, false); }
         else { if (dy_bf16) PW4_L(false, true); else PW4_L(false, false); }
 #undef PW4_L
@@ -2115,9 +2171,11 @@ static int pcnn_wgrad_impl(const void* const* xs, const void* const* ds, int npr
     const void* dy = ds[p];
     float* slab = scratch + p * ns * wsz;
 #define PW1_L(XBV, DBV) hipLaunchKernelGGL((pc_wgrad_kernel<XBV, DBV>), dim3(tiles, taps, (unsigned)ns), dim3(256), 0, st, g, x, dy, \
-                                           ldd, rows, rps, slab, bpart)
-    if (H) hipLaunchKernelGGL((pc_wgrad_kernel<true, true, true>), dim3(tiles, taps, (unsigned)ns), dim3(256), 0, st, g, x,
-                              dy, ldd, rows, rps, slab, bpart);
+                                           ldd, rows, rps, slab, bpart, 0LL, 0LL)
+    if (HP) hipLaunchKernelGGL((pc_wgrad_kernel<true, true, true, true>), dim3(tiles, taps, (unsigned)ns), dim3(256), 0, st,
+                               g, x, dy, ldd, rows, rps, slab, bpart, xpst, dpst);
+    else if (H) hipLaunchKernelGGL((pc_wgrad_kernel<true, true, true>), dim3(tiles, taps, (unsigned)ns), dim3(256), 0, st,
+                                   g, x, dy, ldd, rows, rps, slab, bpart, 0LL, 0LL);
     else if (x_bf16) { if (dy_bf16) PW1_L(true, true); else PW1_L(true, false); }
     else { if (dy_bf16) PW1_L(false, true); else PW1_L(false, false); }
 #undef PW1_L
@@ -2157,6 +2215,9 @@ int svae_pcnn_conv_wgrad_planes(const void* x, int n, int hi, int wi, int cin, i
   if (!x || !dy || planes < 1 || planes > PC_MAXPLANES || x_pstride < 0 || dy_pstride < 0 ||
       (!x_scale != !dy_scale) || (x_scale && planes != 2))
     return bad("pcnn_wgrad_planes: bad arguments");
+  if (x_scale && x_bf16 && dy_bf16 && svae_knob("SVAE_PC_HP", 1) != 0)  // the fp16 planes: one launch per slab set
+    return pcnn_wgrad_impl(&x, &dy, 1, n, hi, wi, cin, ldx, x_bf16, ldd, dy_bf16, ho, wo, cout, kh, kw, s, pt, pl, mode,
+                           dW, nullptr, scratch, scratch_elems, stream, PcScale{x_scale, dy_scale}, x_pstride, dy_pstride);
   int pi[PC_MAXPLANES * PC_MAXPLANES], pj[PC_MAXPLANES * PC_MAXPLANES];
   const int np = pc_products(planes, pi, pj);
   const void* xs[PC_MAXPLANES * PC_MAXPLANES];
