@@ -962,8 +962,9 @@ __global__ __launch_bounds__(256) void pc_wgrad4_kernel(PcGeom g, Pw4 h, const v
 
 // (measured on the B = 128 head shapes: the [2, 3] convs 1.2-1.45x faster than the one-tap kernel, the
 // [2, 2] and 1x1 ones slower at two blocks per CU: kw = 3 only)
-bool pw4_plan(const PcGeom& g, long long rows, Pw4* out) {
-  if (g.s != 1 || g.kh > 2 || g.kw != 3 || g.wo % 16 || PW4_CP % g.wo || (g.ho * g.wo) % PW4_CP || rows % PW4_CP ||
+// any_kw: every kernel width (the fused-plane weight gradients, where a one-tap launch re-reads x and dy per tap)
+bool pw4_plan(const PcGeom& g, long long rows, Pw4* out, bool any_kw = false) {
+  if (g.s != 1 || g.kh > 2 || (any_kw ? g.kw > 3 : g.kw != 3) || g.wo % 16 || PW4_CP % g.wo || (g.ho * g.wo) % PW4_CP || rows % PW4_CP ||
       g.ldx % 8 || g.cin % 8)
     return false;
   Pw4 h;
@@ -2122,7 +2123,8 @@ static int pcnn_wgrad_impl(const void* const* xs, const void* const* ds, int npr
       g4.hi = g4.wi = g4.ho = g4.wo = 16;
     }
     Pw4 h;
-    if (pw4 && pw4_plan(g4, rows, &h)) {
+    static const bool allkw = svae_knob("SVAE_PW4_ALLKW", 1) != 0;  // fused planes: [2, 2] / 1x1 on the tap-row kernel too (387 -> 440 img/s)
+    if (pw4 && pw4_plan(g4, rows, &h, HP && allkw)) {
       const long long tiles4 = (long long)((cin + 63) / 64) * ((cout + 63) / 64) * kh;
       static const int tgt4 = svae_knob("SVAE_PW4_TARGET", 1024);  // blocks of the tap-row kernel
       long long ns = (tgt4 + tiles4 - 1) / tiles4;
