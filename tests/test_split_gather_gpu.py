@@ -25,6 +25,8 @@ SHAPES = [
     (128, 4, 384, 128, 2, 1), (16, 8, 128, 64, 2, 1),                        # conv-T s2: the halo_kw fallback
     (8, 16, 64, 32, 1, 0), (8, 32, 32, 64, 1, 0),                            # input-gradient shapes
     (128, 32, 32, 64, 2, 0), (128, 16, 64, 128, 2, 0),                       # conv s2: 64-row tiles, 8 items
+    (128, 32, 64, 64, 1, 0), (128, 8, 256, 128, 1, 0), (32, 64, 32, 32, 1, 0),  # conv s1: 128-row tiles
+    (128, 16, 128, 128, 1, 1),                                               # conv-T s1: 128-row tiles
 ]
 
 
@@ -88,7 +90,7 @@ def test_split_gather_matches_float64(shape):
 
 
 @pytest.mark.parametrize("shape", [(16, 32, 64, 32, 1, 1), (8, 8, 256, 128, 1, 1), (128, 16, 64, 32, 2, 1),
-                                   (8, 16, 64, 128, 2, 0)])
+                                   (8, 16, 64, 128, 2, 0), (128, 8, 256, 128, 1, 0)])
 def test_split_gather_chunk_ranges(shape):
     """Chunks of 32 channels at magnitudes 1e-3, 1e+3, 0 and 1 in turn: the running exponent rises and
     the accumulators are rescaled; an all-zero chunk leaves it; small chunks after a large one keep
