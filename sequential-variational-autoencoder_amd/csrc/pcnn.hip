@@ -2330,6 +2330,43 @@ __global__ void split_h16_kernel(const float* __restrict__ x, long long rows, in
   }
 }
 
+// 4-channel vector forms (c, ldx, ldo % 4 == 0, 16-B x, 8-B out; rows * c / 4 < 2^31): one 16-byte load and one
+// 8-byte store per plane for four elements, the row by a multiply-shift -- the same per-element arithmetic as
+// absmax_kernel / split_h16_kernel above (bitwise), which ran at 1.5-2.5 TB/s on their 64-bit divisions and
+// 2-byte stores (the c_pixelvae split head calls them once per conv input: 11 % of its step, r05_gpv)
+__global__ __launch_bounds__(256) void absmax4_kernel(const float* __restrict__ x, int n4, int c4, FastDiv dc4, int ldx,
+                                                      unsigned* __restrict__ mx) {
+  float m = 0.f;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    const int r = fdiv(i, dc4);
+    const f32x4 v = *(const f32x4*)&x[(long long)r * ldx + 4 * (i - r * c4)];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+  }
+  block_absmax_put(m, mx);
+}
+__global__ __launch_bounds__(256) void split_h16x4_kernel(const float* __restrict__ x, int n4, int c4, FastDiv dc4,
+                                                          int ldx, __bf16* __restrict__ out, int ldo, long long pst,
+                                                          float* h16) {
+  const int sh = h16_shift(__float_as_uint(h16[1]));
+  if (blockIdx.x == 0 && threadIdx.x == 0) h16[0] = ldexpf(1.f, -sh);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    const int r = fdiv(i, dc4), q = i - r * c4;
+    const f32x4 v = *(const f32x4*)&x[(long long)r * ldx + 4 * q];
+    unsigned short h0[4], h1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float t = ldexpf(v[j], sh);
+      const _Float16 a = (_Float16)t;
+      const _Float16 b = (_Float16)(t - (float)a);
+      h0[j] = __builtin_bit_cast(unsigned short, a);
+      h1[j] = __builtin_bit_cast(unsigned short, b);
+    }
+    const long long o = (long long)r * ldo + 4 * q;
+    *(u64*)(out + o) = (u64)h0[0] | ((u64)h0[1] << 16) | ((u64)h0[2] << 32) | ((u64)h0[3] << 48);
+    *(u64*)(out + o + pst) = (u64)h1[0] | ((u64)h1[1] << 16) | ((u64)h1[2] << 32) | ((u64)h1[3] << 48);
+  }
+}
+
 int svae_pcnn_split_planes(const float* x, int64_t rows, int c, int ldx, int planes, void* out, int ldo, int out_bf16,
                            float* h16_scale, void* stream) {
   if (!x || !out || rows < 1 || c < 1 || ldx < c || ldo < c || planes < 1 || planes > PC_MAXPLANES ||
@@ -2338,6 +2375,17 @@ int svae_pcnn_split_planes(const float* x, int64_t rows, int c, int ldx, int pla
   hipStream_t st = (hipStream_t)stream;
   if (h16_scale) {
     if (hipMemsetAsync(h16_scale + 1, 0, sizeof(float), st) != hipSuccess) return hipchk();
+    static const bool vec = svae_knob("SVAE_PC_SPLIT4", 1) != 0;
+    if (vec && c % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)out & 7) == 0 &&
+        rows * (long long)c / 4 < (1LL << 31)) {
+      const int c4 = c / 4, n4 = (int)(rows * c4);
+      const FastDiv dc4 = make_fastdiv(c4);
+      hipLaunchKernelGGL(absmax4_kernel, dim3(blocks_for(n4, 256, 4096)), dim3(256), 0, st, x, n4, c4, dc4, ldx,
+                         (unsigned*)(h16_scale + 1));
+      hipLaunchKernelGGL(split_h16x4_kernel, dim3(blocks_for(n4)), dim3(256), 0, st, x, n4, c4, dc4, ldx,
+                         (__bf16*)out, ldo, (long long)rows * ldo, h16_scale);
+      return hipchk();
+    }
     hipLaunchKernelGGL(absmax_kernel, dim3(blocks_for(rows * c, 256, 2048)), dim3(256), 0, st, x, (long long)rows, c,
                        ldx, (unsigned*)(h16_scale + 1));
     hipLaunchKernelGGL(split_h16_kernel, dim3(blocks_for(rows * c)), dim3(256), 0, st, x, (long long)rows, c, ldx,

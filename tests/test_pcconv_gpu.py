@@ -175,6 +175,32 @@ def _planes(L, t, fmt, bf=1):
     return out, sc
 
 
+@pytest.mark.parametrize("rows,c,ld", [(4096, 160, 160), (1000, 12, 12), (777, 6, 6), (2048, 64, 80), (5, 4, 4)])
+def test_pcnn_split_h16_is_exact(rows, c, ld):
+    """The scaled fp16 pair of svae_pcnn_split_planes (the 4-channel vector kernels where c, ld % 4 == 0, the
+    element loop else) bit for bit against torch: s = 15 - e (max|x| = f 2^e, f in [0.5, 1)), hi = fp16(x 2^s),
+    lo = fp16(x 2^s - hi), scale[0] = 2^-s; a strided source (ld > c) and magnitudes over 2^-30 .. 2^20."""
+    L = pkg_mod("_lib")
+    g = torch.Generator(device="cuda").manual_seed(rows * 131 + c)
+    src = torch.randn(rows, ld, device="cuda", generator=g) * torch.exp2(
+        torch.randint(-30, 20, (rows, 1), device="cuda", generator=g).float())
+    x = src[:, :c]
+    out = torch.empty(2, rows, c, dtype=torch.bfloat16, device="cuda")
+    sc = torch.empty(2, device="cuda")
+    L.check(L.lib().svae_pcnn_split_planes(ctypes.c_void_p(src.data_ptr()), rows, c, ld, 2,
+                                           ctypes.c_void_p(out.data_ptr()), c, 1, ctypes.c_void_p(sc.data_ptr()),
+                                           L.stream_ptr()))
+    torch.cuda.synchronize()
+    e = int(torch.frexp(x.abs().max()).exponent)
+    s = max(-60, min(60, 15 - e))
+    t = torch.ldexp(x, torch.tensor(float(s), device="cuda"))
+    hi = t.half()
+    lo = (t - hi.float()).half()
+    assert float(sc[0]) == 2.0 ** -s and float(sc[1]) == float(x.abs().max())
+    assert torch.equal(out[0].view(torch.int16), hi.view(torch.int16))
+    assert torch.equal(out[1].view(torch.int16), lo.view(torch.int16))
+
+
 def _wn_planes(L, V, g, taps, cin, cout, fmt):
     """svae_pcnn_wnorm_planes: the forward copy's planes [planes][tap][cout][kf], its scale, the fp64 W [tap][cout][cin]."""
     h16 = fmt == "h16"
