@@ -1145,6 +1145,26 @@ __global__ void split_reduce_kernel(const float* __restrict__ part, int nsplit, 
   }
 }
 
+// (n % 4 == 0, 16-B part / out: four elements per thread, the same k order -- bitwise)
+__global__ void split_reduce4_kernel(const float* __restrict__ part, int nsplit, long long n, float* __restrict__ out,
+                                     PcScale sc) {
+  const long long stride = (long long)gridDim.x * blockDim.x * 4;
+  const float al = pc_alpha(sc);
+  for (long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += stride) {
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < nsplit; ++k) s += *(const f32x4*)&part[(long long)k * n + i];
+    *(f32x4*)&out[i] = s * al;
+  }
+}
+// the weight-gradient split-K partials into dW (scaled by the split mode's alpha)
+static void split_reduce(const float* part, int nsplit, long long n, float* out, PcScale sc, hipStream_t st) {
+  static const bool vec = svae_knob("SVAE_PC_SRED4", 1) != 0;
+  if (vec && n % 4 == 0 && ((uintptr_t)part & 15) == 0 && ((uintptr_t)out & 15) == 0)
+    hipLaunchKernelGGL(split_reduce4_kernel, dim3(blocks_for(n / 4)), dim3(256), 0, st, part, nsplit, n, out, sc);
+  else
+    hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(n)), dim3(256), 0, st, part, nsplit, n, out, sc);
+}
+
 // ---------------------------------------------------------------------------------------------
 // column sums (bias gradients) and edge masks
 // ---------------------------------------------------------------------------------------------
@@ -1171,6 +1191,57 @@ __global__ __launch_bounds__(256) void colsum_part_kernel_pc(const float* __rest
   if (q == 0 && col < c)
     part[(long long)blockIdx.y * c + col] =
         red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+// stage 1, 4-column vector form (c, ldx % 4 == 0, 16-B x / part, rows < 2^31): 64 columns x 16 row lanes per
+// block, one 16-byte load per row and lane, the lanes combined in a fixed order (the element form above runs at
+// ~1 TB/s on its 4-byte loads and 64-bit row modulo)
+__global__ __launch_bounds__(256) void colsum_part4_kernel_pc(const float* __restrict__ x, int rows, int c, int ldx,
+                                                              int per_img, FastDiv dimg, int wo, FastDiv dwo,
+                                                              int mask_edge, int rows_per_split,
+                                                              float* __restrict__ part) {
+  __shared__ f32x4 red[16][16];
+  const int cq = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int col = blockIdx.x * 64 + cq * 4;
+  const int r0 = blockIdx.y * rows_per_split;
+  const int r1 = r0 + rows_per_split < rows ? r0 + rows_per_split : rows;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (col < c)
+    for (int r = r0 + rl; r < r1; r += 16) {
+      if (mask_edge) {
+        const int rr = r - fdiv(r, dimg) * per_img;
+        const int y = fdiv(rr, dwo);
+        if (mask_edge == 1 ? (y == 0) : (rr - y * wo == 0)) continue;
+      }
+      s += *(const f32x4*)&x[(long long)r * ldx + col];
+    }
+  red[rl][cq] = s;
+  __syncthreads();
+  if (rl == 0 && col < c) {
+    f32x4 t = red[0][cq];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) t += red[j][cq];
+    *(f32x4*)&part[(long long)blockIdx.y * c + col] = t;
+  }
+}
+// stage 2, 4-column form (with the vector stage 1): 64 columns x 16 split lanes per block, one 16-byte load per
+// split and lane (the element form's 4 lanes looped ns / 4 = 128-256 dependent loads: 39 us per call, r05_gpv)
+__global__ __launch_bounds__(256) void colsum_fin4_kernel_pc(const float* __restrict__ part, int nsplit, int c,
+                                                             float* __restrict__ out, int accumulate) {
+  __shared__ f32x4 red[16][16];
+  const int cq = threadIdx.x & 15, q = threadIdx.x >> 4;
+  const int col = blockIdx.x * 64 + cq * 4;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (col < c)
+    for (int k = q; k < nsplit; k += 16) s += *(const f32x4*)&part[(long long)k * c + col];
+  red[q][cq] = s;
+  __syncthreads();
+  if (q == 0 && col < c) {
+    f32x4 t = red[0][cq];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) t += red[j][cq];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) out[col + j] = accumulate ? out[col + j] + t[j] : t[j];
+  }
 }
 // stage 2: 64 columns per block, 4 split-lanes, fixed-order combine
 __global__ __launch_bounds__(256) void colsum_fin_kernel_pc(const float* __restrict__ part, int nsplit, int c,
@@ -2148,8 +2219,7 @@ static int pcnn_wgrad_impl(const void* const* xs, const void* const* ds, int npr
         else { if (dy_bf16) PW4_L(false, true); else PW4_L(false, false); }
 #undef PW4_L
       }
-      hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(wsz)), dim3(256), 0, st, scratch, (int)(nprod * ns),
-                         wsz, dW, sc);
+      split_reduce(scratch, (int)(nprod * ns), wsz, dW, sc, st);
       if (dbias)
         hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(cout)), dim3(256), 0, st, bpart, (int)ns,
                            (long long)cout, dbias, PcScale{nullptr, nullptr});
@@ -2182,8 +2252,7 @@ static int pcnn_wgrad_impl(const void* const* xs, const void* const* ds, int npr
     else { if (dy_bf16) PW1_L(false, true); else PW1_L(false, false); }
 #undef PW1_L
   }
-  hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(wsz)), dim3(256), 0, st, scratch, (int)(nprod * ns), wsz,
-                     dW, sc);
+  split_reduce(scratch, (int)(nprod * ns), wsz, dW, sc, st);
   if (dbias)
     hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks_for(cout)), dim3(256), 0, st, bpart, (int)ns, (long long)cout,
                        dbias, PcScale{nullptr, nullptr});
@@ -2406,6 +2475,15 @@ int svae_pcnn_colsum(const float* x, int64_t rows, int c, int ldx, int ho, int w
   if (ns * c > (1LL << 24)) ns = ((1LL << 24) / c > 0) ? (1LL << 24) / c : 1;
   const long long rps = (rows + ns - 1) / ns;
   hipStream_t st = (hipStream_t)stream;
+  static const bool vec = svae_knob("SVAE_PC_COLSUM4", 1) != 0;
+  if (vec && c % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)scratch & 15) == 0 &&
+      rows < (1LL << 31) - rps) {
+    hipLaunchKernelGGL(colsum_part4_kernel_pc, dim3((c + 63) / 64, (unsigned)ns), dim3(256), 0, st, x, (int)rows, c,
+                       ldx, ho * wo, make_fastdiv(ho * wo), wo, make_fastdiv(wo), mask_edge, (int)rps, scratch);
+    hipLaunchKernelGGL(colsum_fin4_kernel_pc, dim3((c + 63) / 64), dim3(256), 0, st, scratch, (int)ns, c, out,
+                       accumulate);
+    return hipchk();
+  }
   hipLaunchKernelGGL(colsum_part_kernel_pc, dim3((c + 63) / 64, (unsigned)ns), dim3(256), 0, st, x, (long long)rows, c,
                      ldx, ho * wo, wo, mask_edge, rps, scratch);
   hipLaunchKernelGGL(colsum_fin_kernel_pc, dim3((c + 63) / 64), dim3(256), 0, st, scratch, (int)ns, c, out,

@@ -201,6 +201,33 @@ def test_pcnn_split_h16_is_exact(rows, c, ld):
     assert torch.equal(out[1].view(torch.int16), lo.view(torch.int16))
 
 
+@pytest.mark.parametrize("n,ho,wo,c,ld,mask,acc", [(16, 32, 32, 160, 160, 0, 0), (16, 32, 32, 160, 160, 1, 1),
+                                                   (8, 16, 16, 64, 96, 2, 0), (4, 8, 8, 6, 6, 1, 0),
+                                                   (3, 7, 5, 12, 12, 2, 1), (128, 32, 32, 80, 80, 0, 0)])
+def test_pcnn_colsum_matches_float64(n, ho, wo, c, ld, mask, acc):
+    """svae_pcnn_colsum (the conv bias gradients: column sums over [rows][c], optionally without each image's first
+    output row (mask 1) or column (mask 2), added to ``out`` with acc) against a float64 sum: the 4-column vector
+    partials where c, ld % 4 == 0, the element ones else."""
+    L = pkg_mod("_lib")
+    g = torch.Generator(device="cuda").manual_seed(n * 1000 + c + mask)
+    rows = n * ho * wo
+    src = torch.randn(rows, ld, device="cuda", generator=g)
+    out = torch.randn(c, device="cuda", generator=g)
+    ref = src[:, :c].double().view(n, ho, wo, c)
+    if mask == 1:
+        ref = ref[:, 1:]
+    elif mask == 2:
+        ref = ref[:, :, 1:]
+    ref = ref.sum((0, 1, 2)) + (out.double() if acc else 0)
+    scratch = torch.empty(1 << 22, device="cuda")
+    L.check(L.lib().svae_pcnn_colsum(ctypes.c_void_p(src.data_ptr()), rows, c, ld, ho, wo, mask,
+                                     ctypes.c_void_p(out.data_ptr()), acc, ctypes.c_void_p(scratch.data_ptr()),
+                                     L.stream_ptr()))
+    torch.cuda.synchronize()
+    err = float((out.double() - ref).abs().max() / (ref.abs().max() + 1.0))
+    assert err < 1e-5, err
+
+
 def _wn_planes(L, V, g, taps, cin, cout, fmt):
     """svae_pcnn_wnorm_planes: the forward copy's planes [planes][tap][cout][kf], its scale, the fp64 W [tap][cout][cin]."""
     h16 = fmt == "h16"
