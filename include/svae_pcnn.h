@@ -80,6 +80,9 @@ int svae_pcnn_wnorm_planes(const float* V, const float* g, int taps, int cin, in
  * scaled fp16 planes (planes = 2, out_bf16 = 1: 16-bit storage). */
 int svae_pcnn_split_planes(const float* x, int64_t rows, int c, int ldx, int planes, void* out, int ldo, int out_bf16,
                            float* h16_scale, void* stream);
+/* the fp16 format's split with max|x| already in h16_scale[1] (svae_pcnn_nonlin_absmax wrote it). */
+int svae_pcnn_split_h16_premax(const float* x, int64_t rows, int c, int ldx, void* out, int ldo, float* h16_scale,
+                               void* stream);
 /* svae_pcnn_conv over plane operands: x planes at x_pstride elements apart (fp32, or 16-bit with x_bf16),
  * wk `planes` planes of [tap][cout][kpad]; x_scale / w_scale (both or neither): the fp16 format. */
 int svae_pcnn_conv_planes(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, int64_t x_pstride,
@@ -109,6 +112,10 @@ int svae_pcnn_mask_edge(float* x, int n, int ho, int wo, int c, int ldx, int mas
  * operand).  Dropout or a bf16 y needs c, ldx, ldy multiples of 4 and 16-B aligned rows. */
 int svae_pcnn_nonlin(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, float keep,
                      uint64_t seed, void* y, int ldy, int y_bf16, void* stream);
+/* svae_pcnn_nonlin with fp32 y that also leaves max|y| in h16_scale[1] (the split mode's scale of the
+ * conv input y, for svae_pcnn_split_h16_premax).  Needs the aligned 4-channel rows of dropout. */
+int svae_pcnn_nonlin_absmax(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, float keep,
+                            uint64_t seed, float* y, int ldy, float* h16_scale, void* stream);
 /* its backward: dx (+)= f'(x) . (dy . mask), the mask given or drawn as in the forward.  dx fp32, or
  * bf16 (dx_bf16 = 1: a gradient read only as a bf16 MFMA operand); dsum (may be NULL): the column
  * sums of the written gradient over all rows, fp32 (a conv's bias gradient), from the same pass

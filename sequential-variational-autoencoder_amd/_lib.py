@@ -137,6 +137,7 @@ def _load(path):
                                   i32, i32, vp, vp, vp, i64, vp], i32),
         "svae_pcnn_wnorm_planes": ([vp, vp, i32, i32, i32, vp, vp, i32, vp, i32, i32, vp, vp], i32),
         "svae_pcnn_split_planes": ([vp, i64, i32, i32, i32, vp, i32, i32, vp, vp], i32),
+        "svae_pcnn_split_h16_premax": ([vp, i64, i32, i32, vp, i32, vp, vp], i32),
         "svae_pcnn_conv_planes": ([vp, i32, i32, i32, i32, i32, i32, i64, vp, i32, i32, vp, vp, vp, vp, i32, i32,
                                    i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp], i32),
         "svae_pcnn_conv_wgrad_planes": ([vp, i32, i32, i32, i32, i32, i32, i64, vp, i32, i32, i64, i32, vp, vp, i32,
@@ -144,6 +145,7 @@ def _load(path):
         "svae_pcnn_colsum": ([vp, i64, i32, i32, i32, i32, i32, vp, i32, vp, vp], i32),
         "svae_pcnn_mask_edge": ([vp, i32, i32, i32, i32, i32, i32, vp], i32),
         "svae_pcnn_nonlin": ([vp, i64, i32, i32, i32, vp, f32, u64, vp, i32, i32, vp], i32),
+        "svae_pcnn_nonlin_absmax": ([vp, i64, i32, i32, i32, vp, f32, u64, vp, i32, vp, vp], i32),
         "svae_pcnn_nonlin_bwd": ([vp, i64, i32, i32, i32, vp, f32, u64, vp, i32, vp, i32, i32, i32, vp, vp, vp], i32),
         "svae_pcnn_dropout_mask": ([i64, f32, u64, vp, vp], i32),
         "svae_pcnn_gate": ([vp, i32, vp, vp, i64, i32, i32, vp, i32, vp], i32),
@@ -188,7 +190,8 @@ PCNN_EXPORTED = ["svae_pcnn_wnorm", "svae_pcnn_wnorm_bwd", "svae_pcnn_conv", "sv
                  "svae_pcnn_highway", "svae_pcnn_wn_init", "svae_pcnn_adam", "svae_pcnn_ema", "svae_pcnn_sample_bwd",
                  "svae_pcnn_highway_bwd", "svae_pcnn_dropout", "svae_pcnn_sqerr",
                  "svae_pcnn_dropout_mask", "svae_pcnn_conv_act_bwd", "svae_pcnn_wnorm_planes",
-                 "svae_pcnn_split_planes", "svae_pcnn_conv_planes", "svae_pcnn_conv_wgrad_planes"]
+                 "svae_pcnn_split_planes", "svae_pcnn_conv_planes", "svae_pcnn_conv_wgrad_planes",
+                 "svae_pcnn_split_h16_premax", "svae_pcnn_nonlin_absmax"]
 
 # bf16 GEMM instance ids (csrc/kernels.h KernelId) for svae_probe_begin
 KID_IGEMM_BF16_256x32 = 2

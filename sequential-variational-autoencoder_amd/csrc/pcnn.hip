@@ -167,7 +167,9 @@ __device__ __forceinline__ void block_absmax_put(float v, unsigned* mx) {
   if (threadIdx.x == 0) {
     unsigned m = 0;
     for (int w = 0; w < (int)(blockDim.x + 63) / 64; ++w) m = red[w] > m ? red[w] : m;
-    atomicMax(mx, m);
+    // (one contended address for thousands of blocks: most find the maximum already at least theirs, and a
+    // plain read of it spares them the serialised atomic -- 70 us of a 25 us pass, r05_hpv)
+    if (m > __hip_atomic_load(mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(mx, m);
   }
 }
 // max |W| = max_co max_k |V[k][co]| * |g[co] / norm[co]| (the product apply forms: monotone in |V|) into *mx
@@ -1313,9 +1315,13 @@ __global__ void dropout_mask_kernel(long long n, float keep, unsigned long long 
 }
 
 template <bool YB>
+// amax != NULL: max |y| over the block into *amax (the split mode's absmax of this conv input, fused: bitwise the
+// separate pass over y)
 __global__ __launch_bounds__(256) void nonlin4_kernel(const float* __restrict__ x, long long rows, int c, int ldx,
                                                       int kind, const float* __restrict__ mask, float keep,
-                                                      unsigned long long seed, void* __restrict__ y, int ldy) {
+                                                      unsigned long long seed, void* __restrict__ y, int ldy,
+                                                      unsigned* __restrict__ amax) {
+  float am = 0.f;
   const bool hashed = !mask && keep < 1.f;
   const float inv = 1.f / keep;
   const int q = c >> 2, cy = kind == 2 ? 2 * c : c;
@@ -1342,8 +1348,12 @@ __global__ __launch_bounds__(256) void nonlin4_kernel(const float* __restrict__ 
       float* yp = (float*)y + r * ldy + ch;
       *(f32x4*)yp = a;
       if (kind == 2) *(f32x4*)(yp + c) = b;
+      if (amax)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) am = fmaxf(am, fmaxf(fabsf(a[j]), fabsf(b[j])));  // (b = 0 unless kind 2)
     }
   }
+  if (!YB && amax) block_absmax_put(am, amax);
 }
 __global__ __launch_bounds__(256) void nonlin4_bwd_kernel(const float* __restrict__ x, long long rows, int c, int ldx,
                                                           int kind, const float* __restrict__ mask, float keep,
@@ -2436,27 +2446,29 @@ __global__ __launch_bounds__(256) void split_h16x4_kernel(const float* __restric
   }
 }
 
-int svae_pcnn_split_planes(const float* x, int64_t rows, int c, int ldx, int planes, void* out, int ldo, int out_bf16,
-                           float* h16_scale, void* stream) {
+static int pcnn_split(const float* x, int64_t rows, int c, int ldx, int planes, void* out, int ldo, int out_bf16,
+                      float* h16_scale, bool premax, void* stream) {
   if (!x || !out || rows < 1 || c < 1 || ldx < c || ldo < c || planes < 1 || planes > PC_MAXPLANES ||
       (h16_scale && (planes != 2 || !out_bf16)))
     return bad("pcnn_split_planes: bad arguments");
   hipStream_t st = (hipStream_t)stream;
   if (h16_scale) {
-    if (hipMemsetAsync(h16_scale + 1, 0, sizeof(float), st) != hipSuccess) return hipchk();
+    if (!premax && hipMemsetAsync(h16_scale + 1, 0, sizeof(float), st) != hipSuccess) return hipchk();
     static const bool vec = svae_knob("SVAE_PC_SPLIT4", 1) != 0;
     if (vec && c % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)out & 7) == 0 &&
         rows * (long long)c / 4 < (1LL << 31)) {
       const int c4 = c / 4, n4 = (int)(rows * c4);
       const FastDiv dc4 = make_fastdiv(c4);
-      hipLaunchKernelGGL(absmax4_kernel, dim3(blocks_for(n4, 256, 4096)), dim3(256), 0, st, x, n4, c4, dc4, ldx,
-                         (unsigned*)(h16_scale + 1));
+      if (!premax)
+        hipLaunchKernelGGL(absmax4_kernel, dim3(blocks_for(n4, 256, 1024)), dim3(256), 0, st, x, n4, c4, dc4, ldx,
+                           (unsigned*)(h16_scale + 1));
       hipLaunchKernelGGL(split_h16x4_kernel, dim3(blocks_for(n4)), dim3(256), 0, st, x, n4, c4, dc4, ldx,
                          (__bf16*)out, ldo, (long long)rows * ldo, h16_scale);
       return hipchk();
     }
-    hipLaunchKernelGGL(absmax_kernel, dim3(blocks_for(rows * c, 256, 2048)), dim3(256), 0, st, x, (long long)rows, c,
-                       ldx, (unsigned*)(h16_scale + 1));
+    if (!premax)
+      hipLaunchKernelGGL(absmax_kernel, dim3(blocks_for(rows * c, 256, 2048)), dim3(256), 0, st, x, (long long)rows, c,
+                         ldx, (unsigned*)(h16_scale + 1));
     hipLaunchKernelGGL(split_h16_kernel, dim3(blocks_for(rows * c)), dim3(256), 0, st, x, (long long)rows, c, ldx,
                        (__bf16*)out, ldo, h16_scale);
     return hipchk();
@@ -2464,6 +2476,15 @@ int svae_pcnn_split_planes(const float* x, int64_t rows, int c, int ldx, int pla
   hipLaunchKernelGGL(split_planes_kernel, dim3(blocks_for(rows * c)), dim3(256), 0, st, x, (long long)rows, c, ldx,
                      planes, out, ldo, out_bf16);
   return hipchk();
+}
+int svae_pcnn_split_planes(const float* x, int64_t rows, int c, int ldx, int planes, void* out, int ldo, int out_bf16,
+                           float* h16_scale, void* stream) {
+  return pcnn_split(x, rows, c, ldx, planes, out, ldo, out_bf16, h16_scale, false, stream);
+}
+int svae_pcnn_split_h16_premax(const float* x, int64_t rows, int c, int ldx, void* out, int ldo, float* h16_scale,
+                               void* stream) {
+  if (!h16_scale) return bad("pcnn_split_h16_premax: bad arguments");
+  return pcnn_split(x, rows, c, ldx, 2, out, ldo, 1, h16_scale, true, stream);
 }
 
 int svae_pcnn_colsum(const float* x, int64_t rows, int c, int ldx, int ho, int wo, int mask_edge, float* out,
@@ -2502,27 +2523,39 @@ int svae_pcnn_mask_edge(float* x, int n, int ho, int wo, int c, int ldx, int mas
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-int svae_pcnn_nonlin(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, float keep,
-                     uint64_t seed, void* y, int ldy, int y_bf16, void* stream) {
+static int pcnn_nonlin(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, float keep,
+                       uint64_t seed, void* y, int ldy, int y_bf16, float* h16_scale, void* stream) {
   if (!x || !y || rows < 1 || c < 1 || kind < 0 || kind > 2 || ldx < c || ldy < (kind == 2 ? 2 * c : c))
     return bad("pcnn_nonlin: bad arguments");
   hipStream_t st = (hipStream_t)stream;
+  unsigned* amax = h16_scale ? (unsigned*)(h16_scale + 1) : nullptr;
+  if (amax && hipMemsetAsync(amax, 0, sizeof(float), st) != hipSuccess) return hipchk();
   const bool vec = c % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && al16(x) && (!mask || al16(mask)) &&
                    (y_bf16 ? ((uintptr_t)y & 7) == 0 : al16(y));
   if (vec) {
     const dim3 grid((unsigned)((rows + NL_RPB - 1) / NL_RPB));
     if (y_bf16)
       hipLaunchKernelGGL(nonlin4_kernel<true>, grid, dim3(256), 0, st, x, (long long)rows, c, ldx, kind, mask, keep,
-                         (unsigned long long)seed, y, ldy);
+                         (unsigned long long)seed, y, ldy, nullptr);
     else
       hipLaunchKernelGGL(nonlin4_kernel<false>, grid, dim3(256), 0, st, x, (long long)rows, c, ldx, kind, mask, keep,
-                         (unsigned long long)seed, y, ldy);
+                         (unsigned long long)seed, y, ldy, amax);
     return hipchk();
   }
   if (mask || keep < 1.f || y_bf16) return bad("pcnn_nonlin: dropout or a bf16 output needs 4-channel aligned rows");
+  if (amax) return bad("pcnn_nonlin_absmax: needs 4-channel aligned fp32 rows");
   hipLaunchKernelGGL(nonlin_kernel, dim3(blocks_for(rows * c)), dim3(256), 0, st, x, (long long)rows, c, ldx, kind,
                      (float*)y, ldy);
   return hipchk();
+}
+int svae_pcnn_nonlin(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, float keep,
+                     uint64_t seed, void* y, int ldy, int y_bf16, void* stream) {
+  return pcnn_nonlin(x, rows, c, ldx, kind, mask, keep, seed, y, ldy, y_bf16, nullptr, stream);
+}
+int svae_pcnn_nonlin_absmax(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, float keep,
+                            uint64_t seed, float* y, int ldy, float* h16_scale, void* stream) {
+  if (!h16_scale) return bad("pcnn_nonlin_absmax: bad arguments");
+  return pcnn_nonlin(x, rows, c, ldx, kind, mask, keep, seed, y, ldy, 0, h16_scale, stream);
 }
 
 int svae_pcnn_nonlin_bwd(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, float keep,

@@ -61,11 +61,12 @@ class DropMask:
 class Act:
     """An NHWC activation: ``buf`` [n*h*w][ld] fp32 (or bf16: a nonlinearity output read only by the
     bf16-MFMA convs), channels [off, off + c)."""
-    __slots__ = ("buf", "off", "c", "ld", "n", "h", "w")
+    __slots__ = ("buf", "off", "c", "ld", "n", "h", "w", "amax")
 
-    def __init__(self, buf, c, n, h, w, off=0, ld=None):
+    def __init__(self, buf, c, n, h, w, off=0, ld=None, amax=None):
         self.buf, self.c, self.n, self.h, self.w, self.off = buf, c, n, h, w, off
         self.ld = c if ld is None else ld
+        self.amax = amax  # (split mode) [2] floats, [1] = max|this activation| from its producer, or None
 
     @property
     def rows(self):
@@ -196,6 +197,9 @@ class PixelCNNpp:
             raise ValueError("planes must be 1 (bf16), 2 or 3 (split)")
         self.planes = planes
         self.h16 = True
+        # (split mode) the nonlinearity kernels also leave max|y| of their outputs, which are conv inputs, so
+        # the fp16-plane split skips its absmax pass (bitwise; SVAE_PC_FUSE_AMAX=0: the separate pass)
+        self.fuse_absmax = os.environ.get("SVAE_PC_FUSE_AMAX", "1") == "1"
         if planes > 1:  # every activation and gradient stays fp32 (split into planes at each GEMM)
             self.bf16_grads = False
         self.probe, self.probe_cap = None, 0  # [(flops, event, event)] of timed forward conv launches
@@ -289,7 +293,7 @@ class PixelCNNpp:
 
     def _view(self, a, n, h, w):
         """``a`` reshaped to another row space (same buffer and gradient)."""
-        v = Act(a.buf, a.c, n, h, w, a.off, a.ld)
+        v = Act(a.buf, a.c, n, h, w, a.off, a.ld, a.amax if n * h * w == a.rows else None)
         self._same[id(v)] = a
         self._keep.append(v)
         return v
@@ -356,6 +360,11 @@ class PixelCNNpp:
         if isinstance(a, Act):
             assert not a.bf, "split mode: activations are fp32"
             src, rows, c, ld = a.ptr(), a.rows, a.c, a.ld
+            if h16 and a.amax is not None:  # its producer left max|a| (svae_pcnn_nonlin_absmax): no absmax pass
+                out = torch.empty(2 * rows * c, dtype=torch.bfloat16, device=self.dev)
+                _ck(self.L.svae_pcnn_split_h16_premax(src, rows, c, ld, ctypes.c_void_p(out.data_ptr()), c,
+                                                      _p(a.amax), self._st()))
+                return out, c, 1, rows * c, 2, a.amax
         else:
             assert a.dtype == torch.float32 and a.is_contiguous()
             src, rows, c, ld = _p(a), a.shape[0], a.shape[1], a.shape[1]
@@ -460,7 +469,15 @@ class PixelCNNpp:
             mp, keep, seed = None, mask.keep, mask.seed
         else:
             mp, keep, seed = _p(mask), 1.0, 0
-        _ck(self.L.svae_pcnn_nonlin(x.ptr(), x.rows, x.c, x.ld, k, mp, keep, seed, y.ptr(), y.ld, int(bf), self._st()))
+        if (self.planes > 1 and self.h16 and self.fuse_absmax and c % 8 == 0 and x.c % 4 == 0 and x.ld % 4 == 0
+                and x.buf.dtype == torch.float32):
+            # the split mode's conv input: the kernel also leaves max|y| for its fp16 planes (bitwise the pass)
+            y.amax = torch.empty(2, dtype=torch.float32, device=self.dev)
+            _ck(self.L.svae_pcnn_nonlin_absmax(x.ptr(), x.rows, x.c, x.ld, k, mp, keep, seed, y.ptr(), y.ld,
+                                               _p(y.amax), self._st()))
+        else:
+            _ck(self.L.svae_pcnn_nonlin(x.ptr(), x.rows, x.c, x.ld, k, mp, keep, seed, y.ptr(), y.ld, int(bf),
+                                        self._st()))
         if self._record and k != 2 and self.fuse_act_bwd and self.planes == 1:  # its consuming conv applies f' (svae_pcnn_conv_act_bwd)
             self._nl_src[id(y)] = (x, k, mp, keep, seed)
             self._keep.append(x)

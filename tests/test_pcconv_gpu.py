@@ -228,6 +228,32 @@ def test_pcnn_colsum_matches_float64(n, ho, wo, c, ld, mask, acc):
     assert err < 1e-5, err
 
 
+@pytest.mark.parametrize("kind,keep", [(2, 1.0), (1, 0.5), (0, 1.0)])
+def test_pcnn_nonlin_absmax_then_premax_split_is_the_two_pass_split(kind, keep):
+    """svae_pcnn_nonlin_absmax (the nonlinearity leaving max|y|) + svae_pcnn_split_h16_premax bit for bit the
+    plain nonlinearity + svae_pcnn_split_planes' absmax and split passes (the split head's fused path)."""
+    L = pkg_mod("_lib")
+    rows, c = 3000, 40
+    g = torch.Generator(device="cuda").manual_seed(kind)
+    x = torch.randn(rows, c, device="cuda", generator=g) * 3
+    cy = 2 * c if kind == 2 else c
+    y0 = torch.empty(rows, cy, device="cuda")
+    y1 = torch.empty(rows, cy, device="cuda")
+    sc = torch.empty(2, device="cuda")
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())
+    L.check(L.lib().svae_pcnn_nonlin(vp(x), rows, c, c, kind, None, keep, 99, vp(y0), cy, 0, L.stream_ptr()))
+    L.check(L.lib().svae_pcnn_nonlin_absmax(vp(x), rows, c, c, kind, None, keep, 99, vp(y1), cy, vp(sc),
+                                            L.stream_ptr()))
+    p1 = torch.empty(2, rows, cy, dtype=torch.bfloat16, device="cuda")
+    L.check(L.lib().svae_pcnn_split_h16_premax(vp(y1), rows, cy, cy, vp(p1), cy, vp(sc), L.stream_ptr()))
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1)
+    assert float(sc[1]) == float(y0.abs().max())
+    p0, sc0 = _planes(L, y0, "h16")
+    torch.cuda.synchronize()
+    assert torch.equal(p0.view(torch.int16), p1.view(torch.int16)) and torch.equal(sc0, sc)
+
+
 def _wn_planes(L, V, g, taps, cin, cout, fmt):
     """svae_pcnn_wnorm_planes: the forward copy's planes [planes][tap][cout][kf], its scale, the fp64 W [tap][cout][cin]."""
     h16 = fmt == "h16"
