@@ -324,6 +324,46 @@ def _pv_roofline(probe, planes, head_flops, vae_flops, ms, key):
             "step_achieved_method": "estimated: head FLOPs = 3 x forward convolution FLOPs"}
 
 
+def pixelvae_cpu_baseline(pv, x, c, nb):
+    """The same c_pixelvae training step (both chain steps, the head's training pass WITH dropout 0.3, the
+    mixture draw, highway, 16 MSE + KL, backward through everything) in fp32 torch on the host cores:
+    oracle/pixelvae.py at dtype float32 -- the fp32 counterpart of the fp32-grade split step, on a batch
+    sample of nb images (the timing is per image; one untimed step first, then steps until >= 10 s)."""
+    from oracle import pcnn as opc, pixelvae as opv, spec as ospec_mod
+    threads, phys, avail = _cpu_threads()
+    torch.set_num_threads(threads)
+    cd = ospec_mod.make_config("celeba", batch=nb, mc_steps=2, latent_dims=list(c.latent_dims),
+                               filter_sizes=list(c.filter_sizes), latent_mean_clip=c.latent_mean_clip,
+                               min_highway=c.min_highway, max_highway=c.max_highway, regularized_steps=(0,),
+                               first_step_loss_coeff=c.first_step_loss_coeff)
+    cd["share_theta"] = cd["share_phi"] = True
+    hs = opc.make_spec(H=64, W=64, K=c.latent_dim)
+    rng = np.random.default_rng(7)
+    xs = x[:nb].cpu().numpy()
+    eps = rng.standard_normal((2, nb, c.latent_dim)).astype(np.float32)
+    um = rng.uniform(1e-5, 1 - 1e-5, (nb, 64, 64, hs["M"])).astype(np.float32)
+    ul = rng.uniform(1e-5, 1 - 1e-5, (nb, 64, 64, 3)).astype(np.float32)
+    keep = 0.7  # dropout_p 0.3 (pixelvae.py:54-63) in every gated resnet: one keep-mask per resnet, in call order
+    R, F = hs["R"], hs["F"]
+    res = [64] * (2 * R) + [32] * (2 * R) + [16] * (2 * R) + [16] * (2 * R) + [32] * (2 * R + 2) + [64] * (2 * R + 2)
+    masks = [(rng.uniform(size=(nb, r, r, F)) < keep).astype(np.float32) / keep for r in res]
+    pub, hp = pv.vae.param_dict(), pv.head.params()
+    run = lambda: opv.forward_backward(cd, pub, hs, hp, xs, xs, eps, 1.0, um, ul, masks, bf16_head=False,
+                                       dtype=torch.float32)
+    run()
+    n, t0 = 0, time.perf_counter()
+    while True:
+        run()
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= 10.0 or n >= 20:
+            break
+    return dict(value=round(nb * n / dt, 4), unit="images/sec", cores=threads, kind="port",
+                sample="%d fwd+bwd steps of %d images of the c_pixelvae chain (oracle/pixelvae.py in fp32 torch CPU, "
+                       "dropout 0.3 on, 1 untimed step first) on %d threads (host: %d physical cores)"
+                       % (n, nb, threads, phys))
+
+
 def run_pixelvae(args, cfgmod):
     """BASELINE configs[4] (CelebA + pixel_cnn decoder, 1 GPU): the c_pixelvae training step
     (pixelvae.PixelVAE.train: engine forward, head training pass with dropout, sampler + highway,
@@ -380,28 +420,8 @@ def run_pixelvae(args, cfgmod):
         "roofline": _pv_roofline(probe, planes, head_flops, vae_flops, ms, "c_pixelvae/" + dtype),
         "cpu_baseline": None,
     }
-    if not args.no_cpu_baseline:  # the fp64 CPU restatement of the same chain on a 2-image sample
-        from oracle import pcnn as opc, pixelvae as opv, spec as ospec_mod
-        threads, phys, avail = _cpu_threads()
-        torch.set_num_threads(threads)
-        cd = ospec_mod.make_config("celeba", batch=2, mc_steps=2, latent_dims=list(c.latent_dims),
-                                   filter_sizes=list(c.filter_sizes), latent_mean_clip=c.latent_mean_clip,
-                                   min_highway=c.min_highway, max_highway=c.max_highway, regularized_steps=(0,),
-                                   first_step_loss_coeff=c.first_step_loss_coeff)
-        cd["share_theta"] = cd["share_phi"] = True
-        hs = opc.make_spec(H=64, W=64, K=c.latent_dim)
-        xs = x[:2].cpu().numpy()
-        eps = np.random.default_rng(1).standard_normal((2, 2, c.latent_dim))
-        um = np.random.default_rng(2).uniform(1e-5, 1 - 1e-5, (2, 64, 64, 10))
-        ul = np.random.default_rng(3).uniform(1e-5, 1 - 1e-5, (2, 64, 64, 3))
-        pub, hp = pv.vae.param_dict(), pv.head.params()
-        t0 = time.perf_counter()
-        opv.forward_backward(cd, pub, hs, hp, xs, xs, eps, 1.0, um, ul, None, bf16_head=False)
-        cdt = time.perf_counter() - t0
-        line["cpu_baseline"] = dict(value=round(2 / cdt, 4), unit="images/sec", cores=threads, kind="port",
-                                    sample="1 fwd+bwd of 2 images of the c_pixelvae chain with oracle/pixelvae.py "
-                                           "(fp64 torch CPU, dropout off) on %d threads (host: %d physical cores)"
-                                           % (threads, phys))
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = pixelvae_cpu_baseline(pv, x, c, args.cpu_batch)
     print(json.dumps(line), flush=True)
     pv.close()
 
@@ -424,6 +444,9 @@ def make_parser():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup-seconds", type=float, default=1.0,
+                    help="after the --warmup steps, more untimed steps until this much warm-up has run (0: off); "
+                         "--steps and what is timed are unchanged")
     ap.add_argument("--config", default="celeba")
     ap.add_argument("--batch", type=int, default=None)
     # bf16x6 (split-bf16 MFMA, held to the fp32 parity bounds in tests/test_headline_gpu.py) is the
@@ -435,6 +458,7 @@ def make_parser():
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip every leg after the timed region (secondary kernel probe, other precision modes)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=8, help="c_pixelvae: images per CPU-baseline step (a sample)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N>1: one all-reduce after the backward instead of per-step buckets during it")
     ap.add_argument("--no-fp32", action="store_true",
@@ -516,10 +540,25 @@ def main():
 
     probe_kid = getattr(L, DOMINANT_KID if args.dtype == "bf16" else DOMINANT_KID_SPLIT) if args.dtype in ("bf16", "bf16x6") else None
     it = 0
+    tw = time.perf_counter()
     for _ in range(args.warmup):
         it += 1
         step(it)
     torch.cuda.synchronize()
+    # time-based warm-up: keep stepping until --warmup-seconds of warm-up have run, so the
+    # clock and caches settle before the timed region; every rank runs the same count (each step all-reduces)
+    wdt = time.perf_counter() - tw
+    per = wdt / max(1, args.warmup)
+    extra = max(0, int(math.ceil((args.warmup_seconds - wdt) / max(per, 1e-4)))) if args.warmup_seconds > 0 else 0
+    if dist:
+        te = torch.tensor([extra], device="cuda", dtype=torch.int64)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        extra = int(te.item())
+    for _ in range(extra):
+        it += 1
+        step(it)
+    torch.cuda.synchronize()
+    warm_s = time.perf_counter() - tw
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -645,6 +684,8 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_extra_steps": extra,
+            "warmup_s": round(warm_s, 3),
             "ms_per_step": round(ms, 3),
             "higher_is_better": True,
             "scaling": "weak",

@@ -115,6 +115,10 @@ enum svae_buffer {
   SVAE_BUF_IMP_IMG = 10  /* [B] ||mle_t - mle_{t-1}||^2 per image (improvement loss, t >= 1) */
 };
 
+/* Hash (16 hex digits) of the sources this library was compiled from (build.py src_hash); the
+ * Python mirror refuses a library whose hash differs from its tree's.  No reference counterpart. */
+const char* svae_build_hash(void);
+
 /* Parameter table (pure host; callable without a GPU).  Live (trainable, non-zero-grad)
  * tensors occupy [0, n_live); dead / pre-BN-bias tensors the tail [n_live, n_total). */
 int svae_param_count(const svae_config* cfg, int64_t* n_total, int64_t* n_live, int32_t* n_tensors);

@@ -24,10 +24,13 @@ import torch
 from . import pcnn, spec, torch_twin
 
 
-def forward_backward(cd, pub, head_spec, head_params, x, tgt, eps, reg, u_mix, u_log, masks, bf16_head=True):
+def forward_backward(cd, pub, head_spec, head_params, x, tgt, eps, reg, u_mix, u_log, masks, bf16_head=True,
+                     dtype=torch.float64):
     """cd: spec.make_config dict of the chain (mc_steps = e + 1, share_theta / share_phi, ...);
     pub: the engine's public parameters (name -> array); head_params: the head's (name -> array).
-    Returns dict(loss, xhat [per step], rec, kl, grads (public names), head_grads, l)."""
+    dtype: float64 (the parity oracle) or float32 (bench.py's like-for-like CPU baseline of the fp32-grade
+    step).  Returns dict(loss, xhat [per step], rec, kl, grads (public names), head_grads, l)."""
+    DT = dtype
     T = cd["mc_steps"]
     e = T - 1
     sh_t, sh_p = cd.get("share_theta", True), cd.get("share_phi", True)
@@ -38,12 +41,12 @@ def forward_backward(cd, pub, head_spec, head_params, x, tgt, eps, reg, u_mix, u
         k = spec.shared_name(p["name"], sh_t, sh_p, False)
         if k in pub:
             per[p["name"]] = np.asarray(pub[k], np.float64)
-    tw = torch_twin.Twin(cd, struct, per, dtype=torch.float64)
-    Ph = pcnn.to_tensors({k: np.asarray(v, np.float64) for k, v in head_params.items()})
-    xt = torch.as_tensor(np.asarray(x), dtype=torch.float64).permute(0, 3, 1, 2)
-    tg = torch.as_tensor(np.asarray(tgt), dtype=torch.float64)
+    tw = torch_twin.Twin(cd, struct, per, dtype=DT)
+    Ph = {k: torch.tensor(np.asarray(v, np.float64), dtype=DT, requires_grad=True) for k, v in head_params.items()}
+    xt = torch.as_tensor(np.asarray(x), dtype=DT).permute(0, 3, 1, 2)
+    tg = torch.as_tensor(np.asarray(tgt), dtype=DT)
     tgc = tg.permute(0, 3, 1, 2)
-    ep = torch.as_tensor(np.asarray(eps), dtype=torch.float64)
+    ep = torch.as_tensor(np.asarray(eps), dtype=DT)
     p2 = cd["latent_prior_stddev"] ** 2
     loss, xh, recs, kls = 0.0, [], [], []
     prev = None
@@ -57,8 +60,7 @@ def forward_backward(cd, pub, head_spec, head_params, x, tgt, eps, reg, u_mix, u
         else:
             net = pcnn.Net(head_spec, Ph, bf16=bf16_head)
             l = net.model(tg, z, masks=masks)
-            smp = pcnn.mix_logistic_sample(l, torch.as_tensor(u_mix, dtype=torch.float64),
-                                           torch.as_tensor(u_log, dtype=torch.float64))
+            smp = pcnn.mix_logistic_sample(l, torch.as_tensor(u_mix, dtype=DT), torch.as_tensor(u_log, dtype=DT))
             o, _ = pcnn.highway_mix(smp, prev.permute(0, 2, 3, 1), z, Ph["highway/W"], Ph["highway/b"],
                                     cd["min_highway"], cd["max_highway"])
             out = o.permute(0, 3, 1, 2)

@@ -88,6 +88,17 @@ def _load(path):
         raise RuntimeError("%s not built; run __graft_entry__.build() or "
                            "python sequential-variational-autoencoder_amd/build.py" % path)
     L = ctypes.CDLL(path)
+    L.svae_build_hash.argtypes = []
+    L.svae_build_hash.restype = ctypes.c_char_p
+    built = (L.svae_build_hash() or b"").decode()
+    # the library must be built from this tree's sources (a stale binary shipped with a newer tree is never
+    # run); SVAE_LIB variant builds (A/B of modified copies) are exempt
+    if not os.environ.get("SVAE_LIB"):
+        from . import build as _build
+        want = _build.src_hash()
+        if built != want:
+            raise RuntimeError("%s was built from other sources (hash %s, tree %s); run __graft_entry__.build()"
+                               % (path, built, want))
     vp, i32, i64, f32, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_uint64
     cfgp = ctypes.POINTER(SvaeConfig)
     sig = {
@@ -181,7 +192,7 @@ EXPORTED = ["svae_param_count", "svae_param_layout", "svae_create", "svae_destro
             "svae_op_gather_bf16", "svae_op_wgrad_bf16", "svae_generate", "svae_set_backward_hook",
             "svae_hook_stream", "svae_adam_range", "svae_backward_adam", "svae_adam_state",
             "svae_set_chain_noise", "svae_bind_imp", "svae_backward_imp", "svae_adam_imp", "svae_imp_range",
-            "svae_set_external_grads"]
+            "svae_set_external_grads", "svae_build_hash"]
 # include/svae_pcnn.h (the PixelCNN++ head)
 PCNN_EXPORTED = ["svae_pcnn_wnorm", "svae_pcnn_wnorm_bwd", "svae_pcnn_conv", "svae_pcnn_conv_wgrad", "svae_pcnn_colsum",
                  "svae_pcnn_mask_edge", "svae_pcnn_nonlin", "svae_pcnn_nonlin_bwd", "svae_pcnn_gate",

@@ -8,6 +8,7 @@ Objects go to csrc/build/, the shared library to the package directory, so the
 library with the A/B tuning switches of csrc/knobs.h read from the environment; only the
 tests that hold an alternative path bitwise to the default and tools/gpu/ab.sh load it.
 """
+import hashlib
 import os
 import subprocess
 import sys
@@ -34,8 +35,38 @@ def _mtime(p):
     return os.path.getmtime(p) if os.path.exists(p) else 0.0
 
 
+def src_hash():
+    """sha256 (16 hex digits) of every source and header the library is compiled from, in a fixed order.
+    engine.cpp embeds it (svae_build_hash(), and the literal "SVAE_SRC_HASH=<hash>" in the binary), so
+    _lib refuses a library built from other sources and build() skips a library that is already current."""
+    h = hashlib.sha256()
+    for name in SOURCES + HEADERS:
+        with open(os.path.join(CSRC, name), "rb") as f:
+            h.update(name.encode() + b"\0" + f.read() + b"\0")
+    for name in ("svae_hip.h", "svae_pcnn.h"):
+        with open(os.path.join(INCLUDE, name), "rb") as f:
+            h.update(name.encode() + b"\0" + f.read() + b"\0")
+    return h.hexdigest()[:16]
+
+
+def embedded_hash(path):
+    """The SVAE_SRC_HASH literal a built library carries (None: absent / unreadable)."""
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    i = data.find(b"SVAE_SRC_HASH=")
+    return data[i + 14:i + 30].decode("ascii", "replace") if i >= 0 else None
+
+
 def build(force=False, verbose=False, knobs=False):
     out, extra = (KNOBS_OUT, ["-DSVAE_KNOBS"]) if knobs else (OUT, EXTRA)
+    sh = src_hash()
+    # a library built from exactly these sources is current whatever the object files' state (they do
+    # not travel to the GPU box: the library itself is checked there, and rebuilt only if it is stale)
+    if not force and not EXTRA and embedded_hash(out) == sh:
+        return out
     bdir = os.path.join(CSRC, "build" if out.endswith("libsvae_hip.so") and not extra
                         else "build-" + os.path.splitext(os.path.basename(out))[0].replace("libsvae_hip_", ""))
     os.makedirs(bdir, exist_ok=True)
@@ -47,9 +78,12 @@ def build(force=False, verbose=False, knobs=False):
         sp = os.path.join(CSRC, src)
         op = os.path.join(bdir, os.path.splitext(src)[0] + ".o")
         objs.append(op)
-        if force or _mtime(op) < max(_mtime(sp), hdr_t):
+        # engine.cpp carries the source hash: recompiled whenever any source changed
+        stale = _mtime(op) < max(_mtime(sp), hdr_t) or (src == "engine.cpp" and embedded_hash(op) != sh)
+        if force or stale:
             lang = ["-x", "hip"] if src.endswith(".hip") else []
-            jobs.append([HIPCC] + FLAGS + extra + lang + ["-c", sp, "-o", op])
+            defs = ['-DSVAE_SRC_HASH="%s"' % sh] if src == "engine.cpp" else []
+            jobs.append([HIPCC] + FLAGS + extra + defs + lang + ["-c", sp, "-o", op])
 
     def run(cmd):
         if verbose:
@@ -62,7 +96,7 @@ def build(force=False, verbose=False, knobs=False):
     if jobs:
         with ThreadPoolExecutor(max_workers=min(len(jobs), 8)) as ex:
             list(ex.map(run, jobs))
-    if jobs or force or _mtime(out) < max(_mtime(o) for o in objs):
+    if jobs or force or _mtime(out) < max(_mtime(o) for o in objs) or embedded_hash(out) != sh:
         run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out] + objs)
     return out
 

@@ -7,14 +7,30 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // The split mode's scaled fp16 weight planes (opload.h split8_h16 / mfma_h16): planes 3 and 4 of the
-// bf16 weight shadows hold h0 = fp16(w * 2^H16_WS), h1 = fp16(w * 2^H16_WS - h0).  |w| < 64 fits fp16
-// and |w| >= 2^-13 keeps every bit (22-23 of them); the model's weights are O(0.01-1).
+// bf16 weight shadows hold h0 = fp16(w * 2^e), h1 = fp16(w * 2^e - h0) with a per-tensor exponent e
+// (the engine's exponent table, one entry per 64-float block of the parameter buffer: every tensor
+// starts on a 64-float boundary).  e puts the tensor's max |w| in [2^H16_WTOP, 2^(H16_WTOP + 1)): 22-23
+// significant bits for every weight down to 2^-(H16_WTOP + 3) of that maximum, and 2^(15 - H16_WTOP)x of
+// headroom below fp16's largest finite value for the weights to grow before the planes are re-made
+// (svae_* Adam flags a weight past 2^15 in its tensor's units; the next forward re-derives the exponent
+// and the planes of every tensor before any GEMM reads them).  H16_WS: the exponent of shadows made
+// without a table (operator-level test entry points, the knob-only packed output weights).
 #define H16_WS 10
+#define H16_WTOP 10
+#define H16_WOVF 32768.f
 #define H16_PLANE 3
-__device__ __forceinline__ void h16_pair(float w, _Float16& h0, _Float16& h1) {
-  const float s = w * (float)(1 << H16_WS);
+__device__ __forceinline__ void h16_pair(float w, int e, _Float16& h0, _Float16& h1) {
+  const float s = w * __uint_as_float((unsigned)(e + 127) << 23);  // (exact power of two; |e| <= 126)
   h0 = (_Float16)s;
   h1 = (_Float16)(s - (float)h0);
+}
+// the exponent for a tensor whose max |w| is wmax (0 or non-finite: H16_WS)
+__host__ __device__ __forceinline__ int h16_wexp(float wmax) {
+  if (!(wmax > 0.f) || !(wmax < 3.0e38f)) return H16_WS;
+  int ex = 0;
+  frexpf(wmax, &ex);  // wmax = f * 2^ex, f in [0.5, 1): max * 2^(H16_WTOP + 1 - ex) in [2^H16_WTOP, 2^(H16_WTOP + 1))
+  const int e = H16_WTOP + 1 - ex;
+  return e < -100 ? -100 : (e > 100 ? 100 : e);
 }
 
 #define SVAE_WAVE 64

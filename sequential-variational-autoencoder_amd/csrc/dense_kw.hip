@@ -32,7 +32,7 @@ typedef __bf16 dk_bf16x8 __attribute__((ext_vector_type(8)));
 // shadow planes, six MFMAs per fragment pair.  NS = 2: the split mode's scaled fp16 hi/lo planes
 // (opload.h split8_h16 / mfma_h16, three MFMAs): A * 2^hs with a per-wave running exponent over the
 // wave's K batches (the accumulators shrink by the exact power of two when it falls), B the shadow's
-// fp16 planes (w * 2^H16_WS); each wave's partial tile is unscaled before the LDS sum
+// fp16 planes (w * 2^e, e the tensor's exponent); each wave's partial tile is unscaled before the LDS sum
 template <int TN, bool ABF, int WK, int NS = 1>
 __global__ __launch_bounds__(256) void dense_kw_kernel(FwdArgs a) {
   constexpr int BN = 32 * TN, BMR = 32 * (4 / WK);
@@ -48,6 +48,7 @@ __global__ __launch_bounds__(256) void dense_kw_kernel(FwdArgs a) {
   const int m = m0 + wr * 32 + l32;
   const bool mv = m < a.rows;
   const __bf16* Bw = (const __bf16*)a.Bh;  // (NS = 2: advanced to the fp16 planes below)
+  [[maybe_unused]] const int wex = (NS == 2 && a.wexp) ? a.wexp[0] : H16_WS;
   f32x16 acc[TN];
 #pragma unroll
   for (int t = 0; t < TN; ++t)
@@ -114,11 +115,11 @@ __global__ __launch_bounds__(256) void dense_kw_kernel(FwdArgs a) {
         for (int t = 0; t < TN; ++t) acc[t] = mfma_split<NS>(af[u], bf[u][t], acc[t]);
     }
   }
-  if constexpr (NS == 2) {  // back to the units of C
+  if constexpr (NS == 2) {  // back to the units of C (the weight planes carry their tensor's exponent)
 #pragma unroll
     for (int t = 0; t < TN; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[t][r] = __builtin_ldexpf(acc[t][r], -(hs + H16_WS));
+      for (int r = 0; r < 16; ++r) acc[t][r] = __builtin_ldexpf(acc[t][r], -(hs + wex));
   }
   // ---- the WK waves' partial tiles, summed in a fixed order ----
 #pragma unroll

@@ -651,6 +651,12 @@ struct svae_ctx {
   int ntiles = 0;
   std::vector<long long> tile_off;  // tiles sorted by tensor offset: each tile's tensor offset
   long long fresh = 0;  // live elements whose bf16 shadows an Adam update refreshed since the last forward
+  // split mode: the fp16 weight planes' exponent per 64-float block (common.h h16_pair), the GEMM weight
+  // tensors {offset, elements, R, Cc} it is derived over, and the Adam overflow flag (wexp_fixup)
+  int* wtab = nullptr;
+  long long* winfo_d = nullptr;
+  int nwinfo = 0;
+  int* wovf = nullptr;
   // svae_backward_adam: clip + Adam of each step's bucket inside the backward (side stream)
   bool fa_on = false;
   float fa_lr = 0.f, fa_clip = 0.f;
@@ -943,6 +949,16 @@ static int gemm(svae_ctx* c, FwdArgs a, int groups) {
     if (!a.b_plane) {  // (the packed output weights carry their own plane stride and no fp16 planes)
       a.b_plane = c->wplane;
       a.h16 = 1;  // a weight shadow: the fp16 planes H16_PLANE.. follow the bf16 ones
+      // ... at its tensor's exponent: the table entry of the weight's offset in the shadow, per group
+      const __bf16* b = (const __bf16*)a.Bh;
+      const __bf16* bn = (const __bf16*)c->wN;
+      const __bf16* bt = (const __bf16*)c->wT;
+      long long off = -1;
+      if (b >= bn && b < bn + c->wplane) off = b - bn;
+      else if (b >= bt && b < bt + c->wplane) off = b - bt;
+      if (off < 0 || (off & 63) || (a.b_gs & 63) || !c->wtab) return fail(c, SVAE_EBADARG, "weight outside the shadows");
+      a.wexp = c->wtab + (off >> 6);
+      a.wexp_gs = a.b_gs >> 6;
     }
     a.part = c->slab;
     a.part_cap = c->slab_cap;
@@ -1062,13 +1078,7 @@ static bool ain_ok(svae_ctx* c, const FwdArgs& t, int groups) {
   // (the split mode's gathers scale their staged window by its running maximum, taken before a
   // consumer-side BN could be applied: the knob-only fold runs in the bf16 mode alone)
   if (!c->m.g.bf16 || !t.Bh || c->m.g.split) return false;
-  FwdArgs u = t;
-  if (c->m.g.split) {
-    u.nsp = 3;
-    u.b_plane = c->wplane;
-    u.h16 = 1;
-  }
-  return halo_kw_plan(u, groups) > 0;
+  return halo_kw_plan(t, groups) > 0;
 }
 
 // Forward conv/convT + BN + act.  in: [B,hin,hin,cin] (ld), out view gets act(BN(pre)+res).
@@ -1221,7 +1231,11 @@ static int conv_wgrad(svae_ctx* c, const ConvL& L, int groups, long long w_gs, V
     hipEvent_t* ev = nullptr;
     if (c->probe.kid != KID_NONE)
       ev = probe_pair(c, w.g.stride == 1 ? KID_WHALO2_S1 : KID_WHALO2_S2, 2.0 * 16 * (double)w.M * w.N * w.rows * groups);
-    if (wgrad_halo2(w, groups, c->slab, c->slab_cap, dW, w_gs, c->st, ev ? ev[1] : nullptr)) return 0;
+    // the T-batched recognition layers (groups > 1) run after the chain backward, beside the recognition
+    // input gradients and then alone: twice the default split target (SVAE_WH2_GTARGET, 0 = the default)
+    static const int gtarget = svae_knob("SVAE_WH2_GTARGET", 256);
+    if (wgrad_halo2(w, groups, c->slab, c->slab_cap, dW, w_gs, c->st, ev ? ev[1] : nullptr, groups > 1 ? gtarget : 0))
+      return 0;
   }
   const bool bfk = c->m.g.bf16 && !c->m.g.split;  // plain-bf16 weight-GEMM kernels
   if (bfk && c->wg_path != 0 && wgrad_halo_enabled()) {
@@ -1615,6 +1629,50 @@ static void pack_out_all(svae_ctx* c, hipStream_t st) {
   }
 }
 
+// split_latent of every step, one launch per level over all steps (splitfc_fwd_steps, grid.y = step), top
+// level first: ev_top after it (the top FC of step 0 waits only on that), ev_all after the rest
+static void split_latent_fwd_all(svae_ctx* c, hipStream_t stream, hipEvent_t ev_top, hipEvent_t ev_all) {
+  const Model& M = c->m;
+  const Geo& g = M.g;
+  const int B = g.B, L = g.L;
+  const int* F = g.F;
+  const int* S = g.S;
+  int zoff[8] = {};
+  for (int i = 1; i < L; ++i) zoff[i] = zoff[i - 1] + g.D[i - 1];
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int i = pass == 0 ? L - 1 : 0; i < (pass == 0 ? L : L - 1); ++i) {
+      for (int t0 = 0; t0 < g.Te; t0 += SFC_MAXT) {
+        const int nt = std::min(SFC_MAXT, g.Te - t0);
+        SfcSteps a{};
+        for (int k = 0; k < nt; ++k) {
+          const int t = t0 + k;
+          svae_ctx::StepBufs& s = c->sb[t];
+          const FcL& f = M.gen[t].split[i];
+          a.W[k] = c->P + f.ow;
+          a.beta[k] = c->P + f.obeta;
+          a.mean[k] = s.split_mean[i];
+          a.invstd[k] = s.split_inv[i];
+          if (i < L - 1) {
+            a.out[k] = elem_off(s.cat[i], F[i + 1], c->cbf);
+            a.o_n[k] = (long long)S[i + 1] * S[i + 1] * 2 * F[i + 1];
+          } else {
+            a.out[k] = s.top_cat + (t >= 1 ? F[L] : 0);
+            a.o_n[k] = s.ktop;
+          }
+        }
+        const int J = M.gen[t0].split[i].nout;
+        const float* z0 = c->z + (long long)t0 * B * g.Dz;
+        if (i < L - 1)
+          splitfc_fwd_steps(z0, (long long)B * g.Dz, g.Dz, zoff[i], B, g.D[i], J, F[i + 1], 2 * F[i + 1], c->cbf, a, nt,
+                            stream);
+        else
+          splitfc_fwd_steps(z0, (long long)B * g.Dz, g.Dz, zoff[i], B, g.D[i], J, J, 0, 0, a, nt, stream);
+      }
+    }
+    hipEventRecord(pass == 0 ? ev_top : ev_all, stream);
+  }
+}
+
 static void split_latent_fwd(svae_ctx* c, int t, hipStream_t stream) {
   const Model& M = c->m;
   const Geo& g = M.g;
@@ -1727,8 +1785,15 @@ static int engine_forward(svae_ctx* c) {
   if ((r = acc_reset(c))) return r;
   if (M.shared) share_broadcast(c->Ppub, c->Pv, c->share_seg, c->share_nseg, st);
   // the shadows are current when the last Adam updates covered the whole live region
-  if (g.bf16 && !(c->fresh == M.n_live && !M.shared))
-    shadow_weights(c->P, c->wN, c->wT, M.n_live, c->tiles_d, c->ntiles, c->offs_d, c->nsp, c->wplane, st);
+  if (g.bf16 && !(c->fresh == M.n_live && !M.shared)) {
+    // split mode: every tensor's fp16-plane exponent from its max |w| first (clears the overflow flag)
+    if (g.split) wexp_refresh(c->P, c->winfo_d, c->nwinfo, c->wtab, c->wovf, st);
+    shadow_weights(c->P, c->wN, c->wT, M.n_live, c->tiles_d, c->ntiles, c->offs_d, c->nsp, c->wplane, st, c->wtab);
+  } else if (g.split) {
+    // the planes the Adam updates wrote: re-made at fresh exponents if a weight outgrew its tensor's
+    // (one block that returns at once unless the flag is up)
+    wexp_fixup(c->P, c->winfo_d, c->nwinfo, c->wtab, c->wovf, c->wN, c->wT, c->wplane, st);
+  }
   c->fresh = 0;
   if (g.noisy) {  // chain noise N(0,1) [T,B,H,W,C] (tf.random_normal(image_batch_shape), :1090)
     const long long n = (long long)T * B * g.H * g.W * g.C;
@@ -1788,13 +1853,21 @@ static int engine_forward(svae_ctx* c) {
   // same-box A/B, profiles/r03_ab3.txt); SVAE_PACK_FIRST=0 packs after it (round 2's order)
   static const bool pack_first = svae_knob("SVAE_PACK_FIRST", 1) != 0;
   if (pack_first) pack_out_all(c, st);
+  // every step's split-latent forward batched per level (SVAE_SFC_STEPS=0: one launch per level and step, the
+  // round-5 schedule); not with the knob-only recognition split, whose z_t of steps >= 1 arrive later
+  static const bool sfc_steps = svae_knob("SVAE_SFC_STEPS", 1) != 0;
+  const bool sfc_all = sfc_side && sfc_steps && !rsplit;
   if (sfc_side) {
     hipEventRecord(c->ev_aux, st);
     hipStreamWaitEvent(c->st3, c->ev_aux, 0);
-    for (int t = 0; t < g.Te; ++t) {
-      if (t == 1 && rsplit) hipStreamWaitEvent(c->st3, c->ev_rs2, 0);  // z_t of steps >= 1 (st4)
-      split_latent_fwd(c, t, c->st3);
-      hipEventRecord(c->ev_sfc[t], c->st3);
+    if (sfc_all) {
+      split_latent_fwd_all(c, c->st3, c->ev_sfc[0], c->ev_sfc[1]);
+    } else {
+      for (int t = 0; t < g.Te; ++t) {
+        if (t == 1 && rsplit) hipStreamWaitEvent(c->st3, c->ev_rs2, 0);  // z_t of steps >= 1 (st4)
+        split_latent_fwd(c, t, c->st3);
+        hipEventRecord(c->ev_sfc[t], c->st3);
+      }
     }
   }
 
@@ -1836,8 +1909,13 @@ static int engine_forward(svae_ctx* c) {
       if (r) return r;
     }
     // split_latent (:1796-1806): ladder_i straight into the concat buffers
-    if (sfc_side) hipStreamWaitEvent(st, c->ev_sfc[t], 0);
-    else split_latent_fwd(c, t, st);
+    if (sfc_all) {
+      if (t == 0) hipStreamWaitEvent(st, c->ev_sfc[0], 0);  // the top level of every step
+    } else if (sfc_side) {
+      hipStreamWaitEvent(st, c->ev_sfc[t], 0);
+    } else {
+      split_latent_fwd(c, t, st);
+    }
     // generator_ladder decoder (:1695-1721)
     r = fc_bn_fwd(c, G.top, View{s.top_cat, s.ktop, 0}, s.top_pre, s.top_bn, View{s.top_act, S[L] * S[L] * F[L], 0, c->abf});
     if (r) return r;
@@ -1849,6 +1927,7 @@ static int engine_forward(svae_ctx* c) {
       r = conv_bn_act_fwd(c, G.s2[lvl], 1, 0, cur, s.s2_pre[lvl], 0, s.s2_bn[lvl], 0, res, ACT_RELU,
                           View{s.cat[lvl], 2 * Fl, 0, c->cbf});
       if (r) return r;
+      if (sfc_all && t == 0 && lvl == L - 2) hipStreamWaitEvent(st, c->ev_sfc[1], 0);  // the other levels, every step
       r = conv_bn_act_fwd(c, G.s1[lvl], 1, 0, View{s.cat[lvl], 2 * Fl, 0, c->cbf}, s.s1_pre[lvl], 0, s.s1_bn[lvl], 0, View{},
                           ACT_RELU, View{s.s1_act[lvl], Fl, 0, c->abf}, lvl >= 1 ? &ds1 : nullptr);
       if (r) return r;
@@ -1987,7 +2066,14 @@ static int inference_bwd(svae_ctx* c, int t0, int n, View in0, float* dx0) {
       const ConvL Lw = I0.a[lvl];
       const float* dp = sa.p;
       float* dW = c->Gr + Lw.ow;
-      r = on_side_q(c, sa.ready, [=] { return conv_wgrad(c, Lw, n, wg, in, dp, gs, dW); });
+      // the backward's last weight gradient (the image conv of every step's ladder) on the main stream,
+      // which has nothing left to run: it overlaps the side stream's backlog instead of queueing behind it
+      // (SVAE_TAIL_MAIN=0: the side stream, round 5)
+      static const bool tail_main = svae_knob("SVAE_TAIL_MAIN", 1) != 0;
+      if (lvl == 0 && !dx0 && tail_main && c->side)
+        r = conv_wgrad(c, Lw, n, wg, in, dp, gs, dW);
+      else
+        r = on_side_q(c, sa.ready, [=] { return conv_wgrad(c, Lw, n, wg, in, dp, gs, dW); });
     }
     if (r) return r;
     if (lvl > 0) {
@@ -2544,6 +2630,13 @@ static bool plan(svae_ctx* c) {
 // ============================================================================
 extern "C" {
 
+#ifndef SVAE_SRC_HASH
+#define SVAE_SRC_HASH "unknown"
+#endif
+// build.py's hash of the sources this library was compiled from (the literal stays in the binary)
+static const char kSrcHash[] = "SVAE_SRC_HASH=" SVAE_SRC_HASH;
+const char* svae_build_hash(void) { return kSrcHash + 14; }
+
 int svae_param_count(const svae_config* cfg, int64_t* n_total, int64_t* n_live, int32_t* n_tensors) {
   Model m;
   std::string err;
@@ -2725,6 +2818,25 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
     }
     hipMemcpy(c->tiles_d, tiles.data(), tiles.size() * sizeof(int), hipMemcpyHostToDevice);
     hipMemcpy(c->offs_d, offs.data(), offs.size() * sizeof(long long), hipMemcpyHostToDevice);
+    if (c->m.g.split) {  // the fp16 weight planes' exponent table (H16_WS until the first shadow refresh)
+      std::vector<long long> info;
+      for (const TT& x : tt) {
+        info.push_back(x.off); info.push_back((long long)x.taps * x.R * x.Cc); info.push_back(x.R); info.push_back(x.Cc);
+      }
+      c->nwinfo = (int)tt.size();
+      const long long nb = c->wplane / 64 + 1;
+      e = hipMalloc(&c->wtab, nb * sizeof(int));
+      if (e == hipSuccess) e = hipMalloc(&c->winfo_d, std::max<size_t>(1, info.size()) * sizeof(long long));
+      if (e == hipSuccess) e = hipMalloc(&c->wovf, sizeof(int));
+      if (e != hipSuccess) {
+        svae_destroy(c);
+        return fail(nullptr, SVAE_ENOMEM, std::string("hipMalloc exponent table: ") + hipGetErrorString(e));
+      }
+      std::vector<int> w0((size_t)nb, H16_WS);
+      hipMemcpy(c->wtab, w0.data(), nb * sizeof(int), hipMemcpyHostToDevice);
+      if (!info.empty()) hipMemcpy(c->winfo_d, info.data(), info.size() * sizeof(long long), hipMemcpyHostToDevice);
+      hipMemset(c->wovf, 0, sizeof(int));
+    }
   }
   hipHostMalloc((void**)&c->reg_host, 64 * sizeof(float), hipHostMallocDefault);
   {
@@ -2814,6 +2926,9 @@ int svae_destroy(svae_ctx* c) {
   if (c->wT) hipFree(c->wT);
   if (c->tiles_d) hipFree(c->tiles_d);
   if (c->offs_d) hipFree(c->offs_d);
+  if (c->wtab) hipFree(c->wtab);
+  if (c->winfo_d) hipFree(c->winfo_d);
+  if (c->wovf) hipFree(c->wovf);
   if (c->Pv) hipFree(c->Pv);
   if (c->Gimp_v) hipFree(c->Gimp_v);
   if (c->share_seg) hipFree(c->share_seg);
@@ -3024,11 +3139,12 @@ static void adam_range(svae_ctx* c, long long lo, long long hi, float lr, long l
   const double lr_t = lr * std::sqrt(1.0 - std::pow(b2, (double)step)) / (1.0 - std::pow(b1, (double)step));
   const bool sh = c->m.g.bf16 && !c->m.shared && c->wN;
   adam_step(c->Ppub + lo, c->Gpub + lo, c->adam_m + lo, c->adam_v + lo, sh ? (void*)((__bf16*)c->wN + lo) : nullptr,
-            hi - lo, (float)lr_t, (float)b1, (float)b2, 1e-8f, clip, c->nsp, c->wplane, s);
+            hi - lo, (float)lr_t, (float)b1, (float)b2, 1e-8f, clip, c->nsp, c->wplane, s, c->wtab, lo, c->wovf);
   if (sh) {
     const long long tb = std::lower_bound(c->tile_off.begin(), c->tile_off.end(), lo) - c->tile_off.begin();
     const long long te = std::lower_bound(c->tile_off.begin(), c->tile_off.end(), hi) - c->tile_off.begin();
-    shadow_t_tiles(c->Ppub, c->wT, (const int*)c->tiles_d + 4 * tb, (int)(te - tb), c->offs_d, c->nsp, c->wplane, s);
+    shadow_t_tiles(c->Ppub, c->wT, (const int*)c->tiles_d + 4 * tb, (int)(te - tb), c->offs_d, c->nsp, c->wplane, s,
+                   c->wtab);
     c->fresh += hi - lo;
   }
 }

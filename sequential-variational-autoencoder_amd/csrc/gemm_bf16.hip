@@ -1135,14 +1135,15 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgArgs a) {
 // bf16 weight shadows: N = plain conversion; T = per-tap transpose of [rows][cols]
 // ---------------------------------------------------------------------------
 // split mode (nsp planes): plane p holds bf16(w - sum of the earlier planes) (opload.h split4)
-__global__ void shadow_n_kernel(const float* w, __bf16* out, long long n, int nsp, long long plane) {
+__global__ void shadow_n_kernel(const float* w, __bf16* out, long long n, int nsp, long long plane, const int* wtab) {
   for (long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n;
        i += (long long)gridDim.x * blockDim.x * 4) {
     if (i + 3 < n) {
       f32x4 v = *(const f32x4*)(w + i);
       if (nsp == 3) {  // split mode: the fp16 planes too
         _Float16 h0[4], h1[4];
-        for (int e = 0; e < 4; ++e) h16_pair(v[e], h0[e], h1[e]);
+        const int ex = wtab ? wtab[i >> 6] : H16_WS;
+        for (int e = 0; e < 4; ++e) h16_pair(v[e], ex, h0[e], h1[e]);
         for (int e = 0; e < 4; ++e) {
           ((_Float16*)out)[H16_PLANE * plane + i + e] = h0[e];
           ((_Float16*)out)[(H16_PLANE + 1) * plane + i + e] = h1[e];
@@ -1156,7 +1157,9 @@ __global__ void shadow_n_kernel(const float* w, __bf16* out, long long n, int ns
     } else {
       for (long long j = i; j < n; ++j) {
         float v = w[j];
-        if (nsp == 3) h16_pair(v, ((_Float16*)out)[H16_PLANE * plane + j], ((_Float16*)out)[(H16_PLANE + 1) * plane + j]);
+        if (nsp == 3)
+          h16_pair(v, wtab ? wtab[j >> 6] : H16_WS, ((_Float16*)out)[H16_PLANE * plane + j],
+                   ((_Float16*)out)[(H16_PLANE + 1) * plane + j]);
         for (int p = 0; p < nsp; ++p) {
           const __bf16 h = (__bf16)v;
           out[p * plane + j] = h;
@@ -1169,7 +1172,7 @@ __global__ void shadow_n_kernel(const float* w, __bf16* out, long long n, int ns
 
 // one 32x32 tile per block; tiles enumerated by the host table (tensor, tap, r0, c0)
 __global__ __launch_bounds__(256) void shadow_t_kernel(const float* w, __bf16* out, const int4* tiles,
-                                                       const long long* offs, int nsp, long long plane) {
+                                                       const long long* offs, int nsp, long long plane, const int* wtab) {
   __shared__ float t[32][33];
   const int4 d = tiles[blockIdx.x];  // x: tensor index, y: tap, z: r0, w: c0
   const long long off = offs[3 * d.x];
@@ -1177,6 +1180,7 @@ __global__ __launch_bounds__(256) void shadow_t_kernel(const float* w, __bf16* o
   const float* src = w + off + (long long)d.y * R * Cc;
   __bf16* dst = out + off + (long long)d.y * R * Cc;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int ex = (nsp == 3 && wtab) ? wtab[off >> 6] : H16_WS;
   for (int i = ty; i < 32; i += 8) {
     int r = d.z + i, c = d.w + tx;
     t[i][tx] = (r < R && c < Cc) ? src[(long long)r * Cc + c] : 0.f;
@@ -1187,7 +1191,7 @@ __global__ __launch_bounds__(256) void shadow_t_kernel(const float* w, __bf16* o
     if (r < R && c < Cc) {
       float v = t[tx][i];
       if (nsp == 3)  // split mode: the fp16 planes too
-        h16_pair(v, ((_Float16*)dst)[H16_PLANE * plane + (long long)c * R + r],
+        h16_pair(v, ex, ((_Float16*)dst)[H16_PLANE * plane + (long long)c * R + r],
                  ((_Float16*)dst)[(H16_PLANE + 1) * plane + (long long)c * R + r]);
       for (int p = 0; p < nsp; ++p) {
         const __bf16 h = (__bf16)v;
@@ -1808,18 +1812,82 @@ void wgrad_halo(const WHaloPlanOut& pl, const WgArgs& a, int groups, hipStream_t
 }
 
 void shadow_weights(const float* w, void* wn, void* wt, long long n, const void* tiles, int ntiles, const void* offs,
-                    int nsp, long long plane, hipStream_t s) {
+                    int nsp, long long plane, hipStream_t s, const int* wtab) {
   long long q = (n + 3) / 4;
   int blocks = (int)std::min<long long>((q + 255) / 256, 8192);
-  hipLaunchKernelGGL(shadow_n_kernel, dim3(blocks), dim3(256), 0, s, w, (__bf16*)wn, n, nsp, plane);
+  hipLaunchKernelGGL(shadow_n_kernel, dim3(blocks), dim3(256), 0, s, w, (__bf16*)wn, n, nsp, plane, wtab);
   if (ntiles > 0)
     hipLaunchKernelGGL(shadow_t_kernel, dim3(ntiles), dim3(256), 0, s, w, (__bf16*)wt, (const int4*)tiles,
-                       (const long long*)offs, nsp, plane);
+                       (const long long*)offs, nsp, plane, wtab);
 }
 
 void shadow_t_tiles(const float* w, void* wt, const void* tiles, int ntiles, const void* offs, int nsp, long long plane,
-                    hipStream_t s) {
+                    hipStream_t s, const int* wtab) {
   if (ntiles > 0)
     hipLaunchKernelGGL(shadow_t_kernel, dim3(ntiles), dim3(256), 0, s, w, (__bf16*)wt, (const int4*)tiles,
-                       (const long long*)offs, nsp, plane);
+                       (const long long*)offs, nsp, plane, wtab);
+}
+
+// ---------------------------------------------------------------------------
+// the fp16 weight planes' per-tensor exponents (common.h h16_wexp): max |w| per tensor -> exponent table
+// ---------------------------------------------------------------------------
+__device__ float wexp_block_max(const float* w, long long n) {  // max |w[0..n)| over the block (256 threads)
+  __shared__ float wm[4];
+  float m = 0.f;
+  for (long long i = threadIdx.x; i < n; i += blockDim.x) m = fmaxf(m, fabsf(w[i]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  return fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+}
+
+// one block per tensor: its exponent into every 64-float block entry the tensor covers
+__device__ int wexp_set(const float* w, const long long* info, int t, int* wtab) {
+  const long long off = info[4 * t], n = info[4 * t + 1];
+  const int e = h16_wexp(wexp_block_max(w + off, n));
+  for (long long b = (off >> 6) + threadIdx.x; b < ((off + n + 63) >> 6); b += blockDim.x) wtab[b] = e;
+  return e;
+}
+
+__global__ __launch_bounds__(256) void wexp_refresh_kernel(const float* w, const long long* info, int* wtab, int* ovf) {
+  wexp_set(w, info, blockIdx.x, wtab);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ovf = 0;  // the shadow pass that follows rewrites every plane
+}
+
+// one block (runs in every split-mode forward; returns at once unless an Adam update raised the flag)
+__global__ __launch_bounds__(256) void wexp_fixup_kernel(const float* w, const long long* info, int ntensor, int* wtab,
+                                                         int* ovf, _Float16* wn, _Float16* wt, long long plane) {
+  if (*ovf == 0) return;
+  for (int t = 0; t < ntensor; ++t) {
+    const int e = wexp_set(w, info, t, wtab);
+    const long long off = info[4 * t], n = info[4 * t + 1];
+    const int R = (int)info[4 * t + 2], Cc = (int)info[4 * t + 3];
+    const long long per = (long long)R * Cc;
+    for (long long i = threadIdx.x; i < n; i += blockDim.x) {
+      _Float16 h0, h1;
+      h16_pair(w[off + i], e, h0, h1);
+      wn[H16_PLANE * plane + off + i] = h0;  // N layout
+      wn[(H16_PLANE + 1) * plane + off + i] = h1;
+      const long long tap = i / per, rc = i - tap * per;  // per-tap transpose: [tap][r][c] -> [tap][c][r]
+      const int r = (int)(rc / Cc), c = (int)(rc - (long long)r * Cc);
+      const long long j = off + tap * per + (long long)c * R + r;
+      wt[H16_PLANE * plane + j] = h0;
+      wt[(H16_PLANE + 1) * plane + j] = h1;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *ovf = 0;
+}
+
+void wexp_refresh(const float* w, const long long* info, int ntensor, int* wtab, int* ovf, hipStream_t s) {
+  if (ntensor > 0) hipLaunchKernelGGL(wexp_refresh_kernel, dim3(ntensor), dim3(256), 0, s, w, info, wtab, ovf);
+}
+
+void wexp_fixup(const float* w, const long long* info, int ntensor, int* wtab, int* ovf, void* wn, void* wt,
+                long long plane, hipStream_t s) {
+  if (ntensor > 0)
+    hipLaunchKernelGGL(wexp_fixup_kernel, dim3(1), dim3(256), 0, s, w, info, ntensor, wtab, ovf, (_Float16*)wn,
+                       (_Float16*)wt, plane);
 }

@@ -558,6 +558,8 @@ void igemm_halo_kw_kernel(KwArgs h) {
     // ---- sum the four waves' partial tiles in LDS (fixed order), then one epilogue ----
     const int m0 = cur.m0, n0 = cur.n0, group = cur.group, cls = cur.cls;
     float* red = (float*)ksm;  // [4][BM][BN]
+    [[maybe_unused]] int wex = H16_WS;  // the weight planes' exponent (split mode)
+    if constexpr (NS == 2) wex = a.wexp ? a.wexp[group * a.wexp_gs] : H16_WS;
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -565,7 +567,7 @@ void igemm_halo_kw_kernel(KwArgs h) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int m = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          red[(wave * BM + m) * BN + tn * 32 + l32] = NS == 2 ? __builtin_ldexpf(acc[tm][tn][r], -(hs + H16_WS)) : acc[tm][tn][r];
+          red[(wave * BM + m) * BN + tn * 32 + l32] = NS == 2 ? __builtin_ldexpf(acc[tm][tn][r], -(hs + wex)) : acc[tm][tn][r];
         }
     __syncthreads();
     KW_STAMP(11);

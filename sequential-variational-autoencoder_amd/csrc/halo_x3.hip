@@ -16,7 +16,7 @@
 // Scaling: fp16 has 11 significant bits and a narrow exponent range, so the block scales A by a power
 // of two 2^hs with max|A| * 2^hs in [2^14, 2^15) over the chunks staged so far (the running maximum
 // only grows, so hs only falls; the accumulators are rescaled by the same exact power of two when it
-// does).  Weights carry the fixed 2^H16_WS.  The epilogue multiplies by 2^-(hs + H16_WS).
+// does).  Weights carry their tensor's exponent 2^e (common.h h16_pair).  The epilogue multiplies by 2^-(hs + e).
 #include "common.h"
 #include "kernels.h"
 #include "knobs.h"
@@ -33,6 +33,9 @@ typedef __bf16 x3_16x8 __attribute__((ext_vector_type(8)));  // 8 raw 16-bit lan
   ((PI) > 4 ? 2 : (NP) == 2 ? ((BM) == 128 ? 2 : (BM) == 64 ? 3 : X3_OCC_S32) : ((BM) == 128 ? 2 : 4))
 #ifndef X3_PI8
 #define X3_PI8 1  // 64-row tiles of the stride-2 convs with 8 window items per thread (their windows are 4x)
+#endif
+#ifndef X3_PERM
+#define X3_PERM 1  // the conflict-free window image (x3_lane_pix); 0: round 5's pixel-order lanes, compact rows
 #endif
 #ifndef X3_BMMAX
 #define X3_BMMAX 128  // largest row tile (16-tap layers; the stride-2 conv-T takes <= 64: four classes per block)
@@ -51,20 +54,60 @@ struct X3Args {
   int Hi, Wi, Ho, Wo;
   int Hr, Wr;        // row space per class
   int R, PR, PC, sy, npix;
+  // LDS image of the window (conflict-free A-fragment reads, x3_lane_pix): row pitch PCP >= PC pixels, nlds
+  // pixels in all; dint: the stride-2 convs' window columns de-interleaved (even columns, then from PCh the odd
+  // ones); pm: the lane -> output pixel order of a 32-row tile (0 identity, 1 16-wide rows, 2 8-wide rows)
+  int PCP, PCh, nlds, dint, pm;
   int oy0, ox0;      // window origin (conv-T stride 2: the union of the four classes' windows)
-  int toff0, tsgn;   // tap shift: window offset of tap t = toff0 + tsgn * (row(t) * PC + col(t))
+  int toff0, tsgn;   // tap shift: LDS pixel offset of tap t = toff0 + tsgn * (row(t) * PCP + col(t))
   FastDiv d_win, d_pc, d_img, d_wr, d_rimg;
   int slot_off;      // byte offset of the [2][4] wave maxima of |A| in dynamic LDS
   void* stamps;      // (SVAE_EXP_STAMPS builds: the phase stamps, in the split-K scratch)
+  const int* wexp; long long wexp_gs;  // the weight planes' exponent of group g (nullptr: H16_WS)
 };
 
 namespace {
 
+// Conflict-free A-fragment reads.  A ds_read_b128 serves its 64 lanes in four groups of 16 lanes, {0-3, 12-15,
+// 20-27} and {4-11, 16-19, 28-31} of each half-wave; a group is conflict-free when its 16 pixels hit 16 distinct
+// 16-byte bank slots, which at the 80-B pixel pitch (slot = 5 * pixel mod 16) means 16 distinct pixel positions
+// mod 16.  A 32-row tile of a 32-wide row space is 32 consecutive pixels of one row: every group reads 16
+// consecutive positions.  In 16- and 8-wide row spaces the tile's rows jump by the window pitch and groups
+// collided (2-3 way; 5.9 conflict cycles per LDS instruction on the 8x8 layers, profiles/r06_p1_sq.txt).  So
+// the lanes take the tile's pixels in a group-aware order: pm 1 (16-wide) gives each group one row of 16
+// consecutive pixels; pm 2 (8-wide) gives each group 4 rows x 4 columns, with the LDS row pitch PCP = 12 (stride
+// 1 / conv-T) or 18 (stride-2 conv, whose de-interleaved rows are 2 * 18 = 4 mod 16 apart), so its rows sit
+// 0 / 4 / 8 / 12 slots apart.  The output pixel of accumulator row m is then x3_lane_pix(m); the epilogue reads
+// the reduced tile through the inverse (x3_pix_lane).  Bitwise the same results (every output element sums the
+// same products in the same order).
+__device__ __forceinline__ int x3_rank_lane(int g, int k) {  // the lane of rank k (0..15) in group g
+  return g == 0 ? (k < 4 ? k : (k < 8 ? k + 8 : k + 12)) : (k < 8 ? k + 4 : (k < 12 ? k + 8 : k + 16));
+}
+__device__ __forceinline__ int x3_lane_pix(int l, int pm) {  // tile-local output pixel of lane l (0..31)
+  if (pm == 0) return l;
+  const int g = (l < 4 || (l >= 12 && l < 16) || (l >= 20 && l < 28)) ? 0 : 1;
+  const int k = g == 0 ? (l < 4 ? l : (l < 16 ? l - 8 : l - 12)) : (l < 12 ? l - 4 : (l < 20 ? l - 8 : l - 16));
+  return pm == 1 ? g * 16 + k : (k >> 2) * 8 + g * 4 + (k & 3);
+}
+__device__ __forceinline__ int x3_pix_lane(int p, int pm) {  // inverse: the lane (accumulator row) of pixel p
+  if (pm == 0) return p;
+  const int g = pm == 1 ? (p >> 4) : ((p >> 2) & 1);
+  const int k = pm == 1 ? (p & 15) : ((p >> 3) * 4 + (p & 3));
+  return x3_rank_lane(g, k);
+}
+
 // NP = 2: the split mode (fp32 A, scaled fp16 hi/lo planes, three MFMAs per fragment pair).
 // NP = 1: the bf16 mode (A fp32 or, ABF, stored bf16; one bf16 plane; bf16-stored pre-BN outputs c_bf16 and
 //         the fused backward-BN terms on bf16-stored pre / y).
-template <int BM, bool CPW, int PI, int NP = 2, bool ABF = false>
-__global__ __launch_bounds__(256, X3_OCC(BM, NP, PI)) void gather_x3_kernel(X3Args h) {
+// RD: the B (weight) fragment ring.  2: two taps of fragments, the next tap's loaded while the current one's
+// MFMAs run (the next chunk's window loaded after tap 1's).  4 (the split mode, one block per CU): a slot per
+// tap of the wave's kernel row, refilled with the same tap of the NEXT chunk right after its MFMAs, and the
+// next chunk's window loaded right after the barrier, before those refills -- every tap's fragments are then
+// a whole chunk ahead, and (vmcnt counts in issue order) no tap's wait includes the window's loads.  32 more
+// VGPRs: one wave per SIMD, for the launches whose grid is one block per CU anyway.
+template <int BM, bool CPW, int PI, int NP = 2, bool ABF = false, int RD = 2>
+__global__ __launch_bounds__(256, RD == 4 ? 1 : X3_OCC(BM, NP, PI)) void gather_x3_kernel(X3Args h) {
+  static_assert(RD == 2 || (RD == 4 && NP == 2), "the full-chunk ring: split mode");
   static_assert(NP == 2 || NP == 1, "fp16 hi/lo planes or one bf16 plane");
   static_assert(NP == 1 || !ABF, "the split planes come from fp32 activations");
   constexpr int TM = BM / 32;
@@ -83,10 +126,12 @@ __global__ __launch_bounds__(256, X3_OCC(BM, NP, PI)) void gather_x3_kernel(X3Ar
   const BlockXYZ blk = xcd_block();
   const int m0 = blk.x * BM, n0 = blk.y * 32, group = blk.z;
   const int nchunk = h.Cin / X3_CK;
+  [[maybe_unused]] int wex = H16_WS;  // the split mode's weight-plane exponent (the epilogue's unscale)
+  if constexpr (NP == 2) wex = h.wexp ? h.wexp[group * h.wexp_gs] : H16_WS;
   const int per_img = h.Hr * h.Wr;
 
   // ---- window items: PI per thread, 8 channels each (item it = pixel it / 4, channel part it % 4) ----
-  int woff[PI];
+  int woff[PI], wpos[PI];  // global element offset; LDS element offset (the pixel's slot in the window image)
   {
     const int img0 = fdiv(m0, h.d_img);
     const int ry0 = fdiv(m0 - img0 * per_img, h.d_wr);
@@ -103,6 +148,8 @@ __global__ __launch_bounds__(256, X3_OCC(BM, NP, PI)) void gather_x3_kernel(X3Ar
         const int iy = iy_base + pr, ix = h.ox0 + pc;
         woff[i] = (iy >= 0 && iy < h.Hi && ix >= 0 && ix < h.Wi) ? (((img0 + il) * h.Hi + iy) * h.Wi + ix) * h.lda + part * 8
                                                                  : -1;
+        const int cs = h.dint ? ((pc & 1) ? h.PCh + (pc >> 1) : (pc >> 1)) : pc;
+        wpos[i] = ((il * h.PR + pr) * h.PCP + cs) * X3_ROWP + part * 8;
       }
     }
   }
@@ -135,14 +182,13 @@ __global__ __launch_bounds__(256, X3_OCC(BM, NP, PI)) void gather_x3_kernel(X3Ar
   auto store_window = [&]() {
 #pragma unroll
     for (int i = 0; i < PI; ++i) {
-      const int it = tid + 256 * i;
       if (woff[i] < -1) continue;
-      const int o = (it >> 2) * X3_ROWP + (it & 3) * 8;
+      const int o = wpos[i];
       if constexpr (NP == 2) {
         x3_16x8 pl[2];
         split8_h16(wv[i][0], wv[i][1], hs, pl);
         *(x3_16x8*)&xsm[o] = pl[0];
-        *(x3_16x8*)&xsm[h.npix * X3_ROWP + o] = pl[1];
+        *(x3_16x8*)&xsm[h.nlds * X3_ROWP + o] = pl[1];
       } else {
         *(x3_16x8*)&xsm[o] = raw8_bf(wv[i][0], wv[i][1], ABF);
       }
@@ -155,12 +201,13 @@ __global__ __launch_bounds__(256, X3_OCC(BM, NP, PI)) void gather_x3_kernel(X3Ar
   int abase[TM];
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
-    const int ml = tm * 32 + l32;
+    const int ml = tm * 32 + x3_lane_pix(l32, h.pm);
     const int rows_img = h.R * h.Wr;
     const int il = fdiv(ml, h.d_rimg);
     const int rem = ml - il * rows_img;
     const int ryl = fdiv(rem, h.d_wr), rx = rem - ryl * h.Wr;
-    abase[tm] = ((il * h.PR + ryl * h.sy + cyo) * h.PC + rx * h.sy + cxo) * X3_ROWP + 8 * hh;
+    // (de-interleaved stride-2 windows: output column rx reads slot rx + the tap's column slot)
+    abase[tm] = ((il * h.PR + ryl * h.sy + cyo) * h.PCP + (h.dint ? rx : rx * h.sy + cxo)) * X3_ROWP + 8 * hh;
   }
   // this wave's taps u = 0..3: 16-tap layers kernel row ky = wave; conv-T stride 2 class `cls`'s 2 x 2
   auto tap_of = [&](int u) {
@@ -172,10 +219,10 @@ __global__ __launch_bounds__(256, X3_OCC(BM, NP, PI)) void gather_x3_kernel(X3Ar
     }
   };
   auto shift_of = [&](int u) {
-    if constexpr (CPW) return h.toff0 + h.tsgn * ((u >> 1) * h.PC + (u & 1));
-    else return h.toff0 + h.tsgn * (wave * h.PC + u);
+    if constexpr (CPW) return h.toff0 + h.tsgn * ((u >> 1) * h.PCP + (u & 1));
+    else return h.dint ? wave * h.PCP + ((u & 1) ? h.PCh + (u >> 1) : (u >> 1)) : h.toff0 + h.tsgn * (wave * h.PCP + u);
   };
-  x3_16x8 bq[2][2][NP];  // [ring slot][kq][plane]
+  x3_16x8 bq[RD][2][NP];  // [ring slot][kq][plane]
   const __bf16* bbase = h.Bh + group * h.b_gs + (long long)(n0 + l32) * h.ldb + 8 * hh;
   auto load_b = [&](int slot, int u, int chunk) {
     const __bf16* p = bbase + (long long)tap_of(u) * h.b_tap + chunk * X3_CK;
@@ -188,7 +235,12 @@ __global__ __launch_bounds__(256, X3_OCC(BM, NP, PI)) void gather_x3_kernel(X3Ar
 
   X3_STAMP(13);
   load_window(0);
-  load_b(0, 0, 0);
+  if constexpr (RD == 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) load_b(u, u, 0);
+  } else {
+    load_b(0, 0, 0);
+  }
   X3_STAMP(14);
   if constexpr (NP == 2) {
     wave_max_put(0);
@@ -220,13 +272,17 @@ __global__ __launch_bounds__(256, X3_OCC(BM, NP, PI)) void gather_x3_kernel(X3Ar
     store_window();
     __syncthreads();
     if (c < 4) X3_STAMP(2 + 2 * c);
+    if (RD == 4 && has_next) load_window(c + 1);  // (older than this chunk's B refills)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      // the ring: the next tap's B (this chunk's, or the next chunk's first)
-      if (u + 1 < 4) load_b((u + 1) & 1, u + 1, c);
-      else if (has_next) load_b(0, 0, c + 1);
-      // the next chunk's window after tap 1's B loads (in-order vmcnt: a later B wait also waits for it)
-      if (u == 0 && has_next) load_window(c + 1);
+      if constexpr (RD == 2) {
+        // the ring: the next tap's B (this chunk's, or the next chunk's first)
+        if (u + 1 < 4) load_b((u + 1) & 1, u + 1, c);
+        else if (has_next) load_b(0, 0, c + 1);
+        // the next chunk's window after tap 1's B loads (in-order vmcnt: a later B wait also waits for it)
+        if (u == 0 && has_next) load_window(c + 1);
+      }
+      const int slot = RD == 4 ? u : (u & 1);
       const int sh = shift_of(u) * X3_ROWP;
 #pragma unroll
       for (int kq = 0; kq < 2; ++kq) {
@@ -234,14 +290,15 @@ __global__ __launch_bounds__(256, X3_OCC(BM, NP, PI)) void gather_x3_kernel(X3Ar
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
           af[tm][0] = *(const x3_16x8*)&xsm[abase[tm] + sh + kq * 16];
-          if constexpr (NP == 2) af[tm][1] = *(const x3_16x8*)&xsm[h.npix * X3_ROWP + abase[tm] + sh + kq * 16];
+          if constexpr (NP == 2) af[tm][1] = *(const x3_16x8*)&xsm[h.nlds * X3_ROWP + abase[tm] + sh + kq * 16];
         }
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
-          if constexpr (NP == 2) acc[tm] = mfma_h16(af[tm], bq[u & 1][kq], acc[tm]);
-          else acc[tm] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm][0], bq[u & 1][kq][0], acc[tm], 0, 0, 0);
+          if constexpr (NP == 2) acc[tm] = mfma_h16(af[tm], bq[slot][kq], acc[tm]);
+          else acc[tm] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm][0], bq[slot][kq][0], acc[tm], 0, 0, 0);
         }
       }
+      if (RD == 4 && has_next) load_b(slot, u, c + 1);  // this tap of the next chunk, a whole chunk ahead
     }
     if (c < 4) X3_STAMP(3 + 2 * c);
     if constexpr (NP == 2) {
@@ -255,7 +312,7 @@ __global__ __launch_bounds__(256, X3_OCC(BM, NP, PI)) void gather_x3_kernel(X3Ar
   float* red = (float*)xsm;  // [4][BM][32]
   // (the split mode's tiles in units of 2^(hs + H16_WS), shared by the block's waves: the reduced sums are
   // unscaled below -- exact, as every partial carries the same power of two)
-  const int usc = NP == 2 ? -(hs + H16_WS) : 0;
+  const int usc = NP == 2 ? -(hs + wex) : 0;
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -314,10 +371,11 @@ __global__ __launch_bounds__(256, X3_OCC(BM, NP, PI)) void gather_x3_kernel(X3Ar
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const int vr = rg + 32 * (i0 + b);
-      f32x4 v = *(const f32x4*)&red[vr * 32 + c4];
+      const int vq = (vr & ~31) | x3_pix_lane(vr & 31, h.pm);  // the accumulator row of output row vr
+      f32x4 v = *(const f32x4*)&red[vq * 32 + c4];
       if constexpr (!CPW) {
 #pragma unroll
-        for (int w = 1; w < 4; ++w) v += *(const f32x4*)&red[(w * BM + vr) * 32 + c4];
+        for (int w = 1; w < 4; ++w) v += *(const f32x4*)&red[(w * BM + vq) * 32 + c4];
       }
       if constexpr (NP == 2) {
 #pragma unroll
@@ -376,9 +434,14 @@ __global__ __launch_bounds__(256, X3_OCC(BM, NP, PI)) void gather_x3_kernel(X3Ar
 // ---- planner / launcher ----
 // Eligible: 4x4 pad-1 conv (stride 1 / 2) and conv-T (stride 1 / 2) with Cin % 32 == 0, N % 32 == 0, fp32
 // A and C, the fp16 weight planes (a.h16), 16-byte aligned epilogue operands, no consumer-side BN.
+// the full-chunk B ring (RD = 4): 0 never, 1 where the grid is at most one block per CU (the occupancy the
+// ring's registers cost is then not there to lose), 2 every split launch of 64 / 128 rows
+#ifndef X3_RD_MODE
+#define X3_RD_MODE 1
+#endif
 struct X3Plan {
   X3Args h;
-  int bm, pi;
+  int bm, pi, rd;
   bool cpw;
   size_t lds;
   dim3 grid;
@@ -428,6 +491,14 @@ static bool x3_plan(const FwdArgs& a, int groups, X3Plan* out) {
     h.PR = (h.R - 1) * sy + span;
     h.PC = (Wr - 1) * sy + span;
     h.npix = nimg * h.PR * h.PC;
+    // the conflict-free window image (x3_lane_pix): lane order and row pitch by row-space width
+    h.dint = (X3_PERM && sy == 2) ? 1 : 0;
+    h.PCh = (h.PC + 1) / 2;
+    h.pm = !X3_PERM ? 0 : Wr == 16 ? 1 : Wr == 8 ? 2 : 0;
+    h.PCP = h.PC;
+    if (h.pm == 2 && sy == 1) h.PCP = 12;                        // (PC = 11 / 10: rows 12 = -4 mod 16 slots apart)
+    if (h.pm == 2 && sy == 2 && (2 * h.PC) % 16 != 4) h.pm = 0;  // (PC = 18: de-interleaved rows 36 = 4 mod 16 apart)
+    h.nlds = nimg * h.PR * h.PCP;
     const int pi = (h.npix * 4 + 255) / 256;
     // the stride-2 convs' windows are four times a stride-1 one per output row: 64-row tiles take 8 items per
     // thread there (the 32-row tiles they fell back to ran 24 MFMAs per wave between two barriers)
@@ -444,7 +515,7 @@ static bool x3_plan(const FwdArgs& a, int groups, X3Plan* out) {
     h.d_rimg = make_fastdiv(h.R * Wr);
     if (s2t) {  // union origin of the four classes (pad 1: class 0 starts one row / column up)
       h.oy0 = h.ox0 = -1;
-      h.toff0 = h.PC + 1;
+      h.toff0 = h.PCP + 1;
       h.tsgn = -1;
     } else if (g.mode == GM_CONV) {
       h.oy0 = h.ox0 = -g.pad;
@@ -452,13 +523,14 @@ static bool x3_plan(const FwdArgs& a, int groups, X3Plan* out) {
       h.tsgn = 1;
     } else {
       h.oy0 = h.ox0 = g.pad - 3;
-      h.toff0 = 3 * h.PC + 3;
+      h.toff0 = 3 * h.PCP + 3;
       h.tsgn = -1;
     }
     out->bm = bm;
     out->pi = pi <= 3 ? 3 : (pi <= 4 ? 4 : 8);
     out->cpw = s2t;
-    const size_t win = (size_t)(split ? 2 : 1) * h.npix * X3_ROWP * 2;  // NP planes
+    out->rd = (split && bm >= 64 && (X3_RD_MODE == 2 || (X3_RD_MODE == 1 && blocks <= 256))) ? 4 : 2;
+    const size_t win = (size_t)(split ? 2 : 1) * h.nlds * X3_ROWP * 2;  // NP planes
     const size_t red = (size_t)4 * bm * 32 * 4;
     h.slot_off = (int)((std::max(win, red) + 15) / 16 * 16);
     out->lds = (size_t)h.slot_off + 8 * sizeof(float);
@@ -491,10 +563,12 @@ int halo_x3(const FwdArgs& a, int groups, hipStream_t s) {
   h.mode = a.g.mode;
   h.Hi = a.g.Hi; h.Wi = a.g.Wi; h.Ho = a.g.Ho; h.Wo = a.g.Wo;
   h.stamps = a.part;
+  h.wexp = a.wexp; h.wexp_gs = a.wexp_gs;
   static bool attr = false;
   if (!attr) {  // (LDS above the 64 KB default: the 128-row reduction tile)
 #define X3_ATTR(BM_, CPW_, PI_, NP_, ABF_) \
-    hipFuncSetAttribute((const void*)gather_x3_kernel<BM_, CPW_, PI_, NP_, ABF_>, hipFuncAttributeMaxDynamicSharedMemorySize, 98304);
+    hipFuncSetAttribute((const void*)gather_x3_kernel<BM_, CPW_, PI_, NP_, ABF_>, hipFuncAttributeMaxDynamicSharedMemorySize, 98304); \
+    if (NP_ == 2 && BM_ >= 64) hipFuncSetAttribute((const void*)gather_x3_kernel<BM_, CPW_, PI_, 2, false, (NP_ == 2 && BM_ >= 64) ? 4 : 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 98304);
     X3_ATTR(128, false, 3, 2, false) X3_ATTR(128, false, 4, 2, false) X3_ATTR(64, false, 3, 2, false)
     X3_ATTR(64, false, 4, 2, false) X3_ATTR(32, false, 3, 2, false) X3_ATTR(32, false, 4, 2, false)
     X3_ATTR(64, true, 3, 2, false) X3_ATTR(64, true, 4, 2, false) X3_ATTR(32, true, 3, 2, false)
@@ -507,8 +581,11 @@ int halo_x3(const FwdArgs& a, int groups, hipStream_t s) {
 #undef X3_ATTR
     attr = true;
   }
-#define X3_LAUNCH(BM_, CPW_, PI_, NP_, ABF_) \
-  hipLaunchKernelGGL((gather_x3_kernel<BM_, CPW_, PI_, NP_, ABF_>), p.grid, dim3(256), p.lds, s, h)
+#define X3_LAUNCH(BM_, CPW_, PI_, NP_, ABF_) do { \
+  if (NP_ == 2 && BM_ >= 64 && p.rd == 4) \
+    hipLaunchKernelGGL((gather_x3_kernel<BM_, CPW_, PI_, 2, false, (NP_ == 2 && BM_ >= 64) ? 4 : 2>), p.grid, dim3(256), p.lds, s, h); \
+  else \
+    hipLaunchKernelGGL((gather_x3_kernel<BM_, CPW_, PI_, NP_, ABF_>), p.grid, dim3(256), p.lds, s, h); } while (0)
   // the bf16 mode (NP = 1): four window items per thread (registers to spare), A fp32 or bf16-stored
 #define X3_BF(BM_, CPW_) \
   if (a.a_bf16) X3_LAUNCH(BM_, CPW_, 4, 1, true); else X3_LAUNCH(BM_, CPW_, 4, 1, false);

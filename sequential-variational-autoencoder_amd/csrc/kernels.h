@@ -54,6 +54,8 @@ struct FwdArgs {
   // split mode: B also holds two scaled fp16 planes (w * 2^H16_WS, opload.h) at planes 3 and 4; the
   // wave-split halo gather then runs the three-product fp16 form (halo_kw NS = 2)
   int h16;
+  // the fp16 planes' per-tensor exponent (common.h h16_pair): group g's at wexp[g * wexp_gs]; nullptr: H16_WS
+  const int* wexp; long long wexp_gs;
   AinBN ain;    // consumer-side BN of A (halo_kw only)
   // forward BN producers (bf16 mode): store C as bf16, the statistics taken from the rounded values;
   // only with stats, no bias / act / accumulate / bw (igemm_c_bf16_ok)
@@ -159,15 +161,25 @@ int wgrad_halo_enabled();
 int wgrad_halo2_enabled();
 int wgrad_halo2_ok(const WgArgs& w);
 int wgrad_halo2(const WgArgs& w, int groups, float* slab, long long slab_cap, float* dW, long long w_gs,
-                hipStream_t s, hipEvent_t after = nullptr);
+                hipStream_t s, hipEvent_t after = nullptr, int target_blocks = 0);  // 0: the default split target
 void wgrad_halo(const WHaloPlanOut& pl, const WgArgs& a, int groups, hipStream_t s, hipEvent_t after = nullptr);
 // bf16 weight shadows: wn = bf16(w) for [0,n); wt = per-tap transposes listed in tiles/offs.
 // nsp > 1 (split mode): plane p (at p * plane elements) holds the p-th bf16 term of opload.h split8
+// wtab: the split mode's fp16-plane exponent per 64-float block (nullptr: H16_WS)
 void shadow_weights(const float* w, void* wn, void* wt, long long n, const void* tiles, int ntiles, const void* offs,
-                    int nsp, long long plane, hipStream_t s);
+                    int nsp, long long plane, hipStream_t s, const int* wtab = nullptr);
 // per-tap transposed bf16 shadow of the ntiles tiles starting at `tiles` only
 void shadow_t_tiles(const float* w, void* wt, const void* tiles, int ntiles, const void* offs, int nsp, long long plane,
-                    hipStream_t s);
+                    hipStream_t s, const int* wtab = nullptr);
+// The per-tensor exponents of the fp16 weight planes (common.h h16_wexp).  info: per GEMM weight tensor
+// {offset, elements, R, Cc} (R x Cc per tap; taps = elements / (R Cc)); wtab: one exponent per 64-float
+// block; ovf: the overflow flag the Adam kernels raise.
+// refresh: every tensor's exponent from its max |w| (one block per tensor; clears ovf), before a full
+// shadow_weights pass.  fixup: one block; when ovf is set, re-derives every exponent and rewrites the fp16
+// planes of both shadows (N at wn, per-tap transposes at wt), then clears ovf -- otherwise returns at once
+void wexp_refresh(const float* w, const long long* info, int ntensor, int* wtab, int* ovf, hipStream_t s);
+void wexp_fixup(const float* w, const long long* info, int ntensor, int* wtab, int* ovf, void* wn, void* wt,
+                long long plane, hipStream_t s);
 void igemm_fwd(FwdArgs a, int groups, hipStream_t s);
 void wgrad(WgArgs a, int groups, hipStream_t s);
 void wgrad_reduce(const float* part, long long p_gs, int nsplit, int ntap, int M, int N, float* out0,
@@ -213,6 +225,19 @@ void bn_bwd_apply(const float* dy, int lddy, long long dy_gs, const float* y, in
 void splitfc_fwd(const float* z, int ldz, int zoff, int B, int K, const float* W, const float* beta, int J,
                  float* mean, float* invstd, float* out, long long o_n, int F, int ldo, hipStream_t s,
                  int out_bf16 = 0);  // out_bf16: the concat buffer is stored as bf16 (offsets in bf16 elements)
+// one level for up to SFC_MAXT chain steps (grid.y = step; z_t at z + t * z_ts): per-step weights, beta,
+// statistics and output (o_n per step: the top concat's row pitch differs at t = 0)
+#define SFC_MAXT 16
+struct SfcSteps {
+  const float* W[SFC_MAXT];
+  const float* beta[SFC_MAXT];
+  float* mean[SFC_MAXT];
+  float* invstd[SFC_MAXT];
+  float* out[SFC_MAXT];
+  long long o_n[SFC_MAXT];
+};
+void splitfc_fwd_steps(const float* z, long long z_ts, int ldz, int zoff, int B, int K, int J, int F, int ldo,
+                       int out_bf16, const SfcSteps& a, int nt, hipStream_t s);
 // writes dW [K][J], dbeta [J] and dz_part [splitfc_blocks(J)][B][K]
 void splitfc_bwd(const float* z, int ldz, int zoff, int B, int K, const float* W, const float* beta, int J,
                  const float* mean, const float* invstd, const float* dout, long long o_n, int F, int ldo, float* dW,
@@ -278,8 +303,11 @@ void loss_reduce(const float* rec_part, int nblk, const float* kl_img, int B, in
 // ---- optimizer: clip(+-c) + TF Adam (sequential_vae.py:1267-1276) ----
 // clip + TF Adam on n elements; wn != nullptr: also the bf16 copy of the updated weights (nsp planes
 // of the split mode at wn + p * plane)
+// wtab / ovf (split mode): the fp16 planes' exponent per 64-float block of the parameter buffer (element i of
+// this range is element wbase + i there) and the overflow flag
 void adam_step(float* w, const float* g, float* m, float* v, void* wn, long long n, float lr_t, float b1, float b2,
-               float eps, float clipv, int nsp, long long plane, hipStream_t s);
+               float eps, float clipv, int nsp, long long plane, hipStream_t s, const int* wtab = nullptr,
+               long long wbase = 0, int* ovf = nullptr);
 
 // ---- weight sharing (homogeneous chain): virtual per-step copies <-> public tensors ----
 // Pv[v + i] = P[p + i] for every segment {v, p, size} of seg[nseg][3]

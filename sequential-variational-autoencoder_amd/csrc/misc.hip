@@ -24,11 +24,9 @@ static int ew_blocks(long long work, int per = 256, int cap = 4096) {
 #define SFC_RG 4
 
 template <int KM>
-__global__ __launch_bounds__(256) void splitfc_fwd_kernel(const float* z, int ldz, int zoff, int B, int K,
-                                                          const float* W, const float* beta, int J, float* mean,
-                                                          float* invstd, float* out, long long o_n, int F, int ldo,
-                                                          int out_bf16) {
-  extern __shared__ __attribute__((aligned(16))) float zs[];  // [B][KM], zero padded past K
+__device__ __forceinline__ void splitfc_fwd_body(const float* z, int ldz, int zoff, int B, int K, const float* W,
+                                                 const float* beta, int J, float* mean, float* invstd, float* out,
+                                                 long long o_n, int F, int ldo, int out_bf16, float* zs) {
   __shared__ float red[SFC_RG][SFC_COLS];
   for (int i = threadIdx.x; i < B * KM; i += blockDim.x) {
     const int d = i % KM;
@@ -81,6 +79,28 @@ __global__ __launch_bounds__(256) void splitfc_fwd_kernel(const float* z, int ld
   for (int n = rg; n < B; n += SFC_RG) dst[n * o_n] = lrelu_f((pre(n) - m) * is + b);
 }
 
+template <int KM>
+__global__ __launch_bounds__(256) void splitfc_fwd_kernel(const float* z, int ldz, int zoff, int B, int K,
+                                                          const float* W, const float* beta, int J, float* mean,
+                                                          float* invstd, float* out, long long o_n, int F, int ldo,
+                                                          int out_bf16) {
+  extern __shared__ __attribute__((aligned(16))) float zs[];  // [B][KM], zero padded past K
+  splitfc_fwd_body<KM>(z, ldz, zoff, B, K, W, beta, J, mean, invstd, out, o_n, F, ldo, out_bf16, zs);
+}
+
+// one level of split_latent for the chain steps t0 .. t0 + nt - 1 in one launch (grid.y = step): every
+// z_t is known after the T-batched recognition, so the forward of all steps is one launch per level
+// instead of one per (level, step) -- the same block body, bitwise the per-step launches
+template <int KM>
+__global__ __launch_bounds__(256) void splitfc_fwd_steps_kernel(const float* z, long long z_ts, int ldz, int zoff,
+                                                                int B, int K, int J, int F, int ldo, int out_bf16,
+                                                                SfcSteps a) {
+  extern __shared__ __attribute__((aligned(16))) float zs[];
+  const int i = blockIdx.y;
+  splitfc_fwd_body<KM>(z + i * z_ts, ldz, zoff, B, K, a.W[i], a.beta[i], J, a.mean[i], a.invstd[i], a.out[i], a.o_n[i], F,
+                       ldo, out_bf16, zs);
+}
+
 static int sfc_km(int K) { return K <= 4 ? 4 : (K <= 8 ? 8 : 32); }
 
 void splitfc_fwd(const float* z, int ldz, int zoff, int B, int K, const float* W, const float* beta, int J,
@@ -100,6 +120,20 @@ void splitfc_fwd(const float* z, int ldz, int zoff, int B, int K, const float* W
 }
 
 int splitfc_blocks(int J) { return (J + SFC_COLS - 1) / SFC_COLS; }
+
+void splitfc_fwd_steps(const float* z, long long z_ts, int ldz, int zoff, int B, int K, int J, int F, int ldo,
+                       int out_bf16, const SfcSteps& a, int nt, hipStream_t s) {
+  const int km = sfc_km(K);
+  dim3 g((J + SFC_COLS - 1) / SFC_COLS, nt);
+  const size_t lds = (size_t)B * km * sizeof(float);
+  if (km == 4)
+    hipLaunchKernelGGL(splitfc_fwd_steps_kernel<4>, g, dim3(256), lds, s, z, z_ts, ldz, zoff, B, K, J, F, ldo, out_bf16, a);
+  else if (km == 8)
+    hipLaunchKernelGGL(splitfc_fwd_steps_kernel<8>, g, dim3(256), lds, s, z, z_ts, ldz, zoff, B, K, J, F, ldo, out_bf16, a);
+  else
+    hipLaunchKernelGGL(splitfc_fwd_steps_kernel<32>, g, dim3(256), lds, s, z, z_ts, ldz, zoff, B, K, J, F, ldo, out_bf16, a);
+}
+
 
 // backward: dW [K][J], dbeta [J], and per-block partial dz: dz_part[blk][n][d] = sum_{j in blk} dpre[n][j] W[d][j].
 // dpre rows are staged in LDS (pitch 65: conflict-free column reads) and the dz partials are then
@@ -1319,8 +1353,17 @@ __device__ __forceinline__ void adam1(float& w, float g, float& m, float& v, flo
 // also writes the bf16 copy of the updated weights (the GEMMs' N-layout shadow, shadow_n_kernel's
 // rounding), which saves the next forward's separate conversion pass over the live region
 typedef _Float16 ol4h __attribute__((ext_vector_type(4)));
+// split mode: the fp16 planes at the tensor's exponent wtab[(wbase + i) / 64] (H16_WS without a table); a
+// weight at or past 2^15 in those units raises *ovf, and the next forward re-makes every tensor's planes
+// (wexp_fixup) before a GEMM reads them
+__device__ __forceinline__ void adam_h16(float w, int e, _Float16& h0, _Float16& h1, bool& ovf) {
+  h16_pair(w, e, h0, h1);
+  ovf |= !(fabsf(w * __uint_as_float((unsigned)(e + 127) << 23)) < H16_WOVF);
+}
 __global__ void adam_kernel(float* w, const float* g, float* m, float* v, __bf16* wn, long long n, float lr_t, float b1,
-                            float b2, float eps, float clipv, int nsp, long long plane) {
+                            float b2, float eps, float clipv, int nsp, long long plane, const int* wtab, long long wbase,
+                            int* ovf_flag) {
+  bool ovf = false;
   const long long stride = (long long)gridDim.x * blockDim.x;
   const long long nq = n >> 2;
   for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += stride) {
@@ -1340,7 +1383,8 @@ __global__ void adam_kernel(float* w, const float* g, float* m, float* v, __bf16
     if (wn) {  // the bf16 N-layout copy (split mode: nsp planes, opload.h split4; and the fp16 planes)
       if (nsp == 3) {
         _Float16 h0[4], h1[4];
-        for (int e = 0; e < 4; ++e) h16_pair(ww[e], h0[e], h1[e]);
+        const int ex = wtab ? wtab[(wbase + 4 * q) >> 6] : H16_WS;
+        for (int e = 0; e < 4; ++e) adam_h16(ww[e], ex, h0[e], h1[e], ovf);
         *(ol4h*)((_Float16*)wn + H16_PLANE * plane + 4 * q) = ol4h{h0[0], h0[1], h0[2], h0[3]};
         *(ol4h*)((_Float16*)wn + (H16_PLANE + 1) * plane + 4 * q) = ol4h{h1[0], h1[1], h1[2], h1[3]};
       }
@@ -1355,7 +1399,9 @@ __global__ void adam_kernel(float* w, const float* g, float* m, float* v, __bf16
     adam1(w[i], g[i], m[i], v[i], lr_t, b1, b2, eps, clipv);
     if (wn) {
       float x = w[i];
-      if (nsp == 3) h16_pair(x, ((_Float16*)wn)[H16_PLANE * plane + i], ((_Float16*)wn)[(H16_PLANE + 1) * plane + i]);
+      if (nsp == 3)
+        adam_h16(x, wtab ? wtab[(wbase + i) >> 6] : H16_WS, ((_Float16*)wn)[H16_PLANE * plane + i],
+                 ((_Float16*)wn)[(H16_PLANE + 1) * plane + i], ovf);
       for (int p = 0; p < nsp; ++p) {
         const __bf16 h = (__bf16)x;
         wn[p * plane + i] = h;
@@ -1363,13 +1409,15 @@ __global__ void adam_kernel(float* w, const float* g, float* m, float* v, __bf16
       }
     }
   }
+  if (ovf && ovf_flag) *ovf_flag = 1;  // (a plain store: every writer stores the same value)
 }
 
 void adam_step(float* w, const float* g, float* m, float* v, void* wn, long long n, float lr_t, float b1, float b2,
-               float eps, float clipv, int nsp, long long plane, hipStream_t s) {
+               float eps, float clipv, int nsp, long long plane, hipStream_t s, const int* wtab, long long wbase,
+               int* ovf) {
   if (n <= 0) return;
   hipLaunchKernelGGL(adam_kernel, dim3(ew_blocks((n + 3) / 4, 256, 8192)), dim3(256), 0, s, w, g, m, v, (__bf16*)wn,
-                     n, lr_t, b1, b2, eps, clipv, nsp, plane);
+                     n, lr_t, b1, b2, eps, clipv, nsp, plane, wtab, wbase, ovf);
 }
 
 __global__ void bf16_to_f32_kernel(const __bf16* src, float* dst, long long n) {

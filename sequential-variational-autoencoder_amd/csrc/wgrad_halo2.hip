@@ -369,7 +369,7 @@ int wgrad_halo2_ok(const WgArgs& w) {
 }
 
 int wgrad_halo2(const WgArgs& w, int groups, float* slab, long long slab_cap, float* dW, long long w_gs,
-                hipStream_t s, hipEvent_t after) {
+                hipStream_t s, hipEvent_t after, int target_blocks) {
   if (!wgrad_halo2_ok(w)) return 0;
   const int WO = w.g.Wo;
   const int S = w.g.stride;
@@ -382,7 +382,7 @@ int wgrad_halo2(const WgArgs& w, int groups, float* slab, long long slab_cap, fl
   // mode +1.9 %, profiles/r04_knobs_ab.txt); bf16: 96 (+0.6 %, profiles/r04_knobs2_ab.txt).  SVAE_WH2_TARGET
   // overrides both
   static const int target_env = env_int("SVAE_WH2_TARGET", 0);
-  const int target = target_env > 0 ? target_env : (w.nsp > 1 ? 128 : 96);
+  const int target = target_env > 0 ? target_env : target_blocks > 0 ? target_blocks : (w.nsp > 1 ? 128 : 96);
   static const int minch = env_int("SVAE_WH2_MINCH", 4);
   // SVAE_WH2_NSW=2: a 64-column block as 4 waves of two 32-column subtiles (each transposed A
   // fragment feeds two MFMAs) instead of 8 waves of one

@@ -18,7 +18,6 @@ dense V [in, out], hw [K, 2F]); names follow the reference's layer counters (nn.
 """
 import ctypes
 import math
-import os
 
 import numpy as np
 import torch
@@ -153,7 +152,8 @@ class PixelCNNpp:
     """Conditional PixelCNN++ on libsvae_hip.so.  One instance owns its parameters, gradients,
     Adam moments and Polyak averages (flat fp32 device buffers)."""
 
-    def __init__(self, spec, params=None, seed=0, device="cuda", scratch_elems=1 << 26, planes=1):
+    def __init__(self, spec, params=None, seed=0, device="cuda", scratch_elems=1 << 26, planes=1, bf16_grads=False,
+                 fuse_absmax=True):
         if not torch.cuda.is_available():
             raise RuntimeError("PixelCNNpp needs a GPU (HIP kernels in libsvae_hip.so); there is no CPU fallback")
         self.s = spec
@@ -188,18 +188,20 @@ class PixelCNNpp:
         self.fuse_act_bwd = False
         # the gradients of the resnet convs' outputs, read only as bf16 MFMA operands, stored bf16 (their
         # bias gradients summed in fp32 by the op that writes them)
-        self.bf16_grads = os.environ.get("SVAE_PC_BF16_GRADS", "0") == "1"  # opt-in: measured slower (804 vs 882 img/s)
+        # (opt-in: measured slower, 804 vs 882 img/s; bf16 head only)
+        self.bf16_grads = bool(bf16_grads)
         self._nl_src, self._bias_of, self._bf16_grad = {}, {}, set()
         # operand planes of the conv / nin GEMMs: 1 = bf16 MFMA operands; 3 = the split mode (include/svae_pcnn.h):
         # fp32-grade products, nn.py:189-252 in fp32 -- two scaled fp16 planes per operand (3 fp16-MFMA
         # products) for the layers whose channel counts allow 16-bit storage (h16), else 3 bf16 planes (6)
-        if planes not in (1, 2, 3):
-            raise ValueError("planes must be 1 (bf16), 2 or 3 (split)")
+        # (2 bf16 planes would be neither the bf16 head nor fp32-grade on the layers without fp16 planes)
+        if planes not in (1, 3):
+            raise ValueError("planes must be 1 (bf16 MFMA operands) or 3 (the fp32-grade split mode)")
         self.planes = planes
         self.h16 = True
         # (split mode) the nonlinearity kernels also leave max|y| of their outputs, which are conv inputs, so
-        # the fp16-plane split skips its absmax pass (bitwise; SVAE_PC_FUSE_AMAX=0: the separate pass)
-        self.fuse_absmax = os.environ.get("SVAE_PC_FUSE_AMAX", "1") == "1"
+        # the fp16-plane split skips its absmax pass (bitwise; fuse_absmax=False: the separate pass, for A/Bs)
+        self.fuse_absmax = bool(fuse_absmax)
         if planes > 1:  # every activation and gradient stays fp32 (split into planes at each GEMM)
             self.bf16_grads = False
         self.probe, self.probe_cap = None, 0  # [(flops, event, event)] of timed forward conv launches

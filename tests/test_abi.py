@@ -26,6 +26,36 @@ def test_library_exports_header_symbols(built_lib):
     assert sorted(pkg_mod("_lib").EXPORTED) == syms
 
 
+def test_library_embeds_its_source_hash(built_lib):
+    """the library carries the hash of the sources it was compiled from (build.py
+    src_hash over csrc/* and include/*), as svae_build_hash() and as the literal build() reads from the
+    file; _lib refuses a library whose hash is not the tree's, so no stale binary is ever tested."""
+    build = pkg_mod("build")
+    want = build.src_hash()
+    assert re.fullmatch(r"[0-9a-f]{16}", want)
+    assert build.embedded_hash(built_lib) == want
+    lib = ctypes.CDLL(built_lib)
+    lib.svae_build_hash.restype = ctypes.c_char_p
+    assert lib.svae_build_hash().decode() == want
+    knobs = build.build(knobs=True)
+    assert build.embedded_hash(knobs) == want
+
+
+def test_loader_refuses_a_library_from_other_sources(built_lib, tmp_path, monkeypatch):
+    """A copy of the library whose embedded hash differs from the tree's does not load through _lib."""
+    L = pkg_mod("_lib")
+    data = open(built_lib, "rb").read()
+    i = data.find(b"SVAE_SRC_HASH=")
+    assert i >= 0
+    old = data[i + 14:i + 30]
+    bad = bytes(ord("0") if c != ord("0") else ord("1") for c in old)
+    stale = tmp_path / "libsvae_hip.so"
+    stale.write_bytes(data[:i + 14] + bad + data[i + 30:])
+    monkeypatch.delenv("SVAE_LIB", raising=False)
+    with pytest.raises(RuntimeError, match="built from other sources"):
+        L._load(str(stale))
+
+
 def test_library_exports_pcnn_symbols(built_lib):
     """include/svae_pcnn.h (the PixelCNN++ head): every entry point is exported and
     has a ctypes signature."""

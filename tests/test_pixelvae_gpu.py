@@ -32,20 +32,20 @@ def _rel(a, b):
     return float(np.linalg.norm(np.ravel(a) - np.ravel(b)) / max(np.linalg.norm(np.ravel(b)), 1e-30))
 
 
-def _setup(dtype="fp32", seed=0, head_planes=1):
+def _setup(dtype="fp32", seed=0, head_planes=1, head=HEAD):
     PV = pkg_mod("pixelvae").PixelVAE
-    pv = PV("c_pixelvae", head=HEAD, seed=seed, dtype=dtype, head_planes=head_planes, **GEO)
+    pv = PV("c_pixelvae", head=head, seed=seed, dtype=dtype, head_planes=head_planes, **GEO)
     c = pv.cfg
     cd = spec.make_config("tiny", H=16, W=16, C=3, levels=4, filter_sizes=GEO["filter_sizes"],
                           latent_dims=GEO["latent_dims"], mc_steps=2, batch=4, latent_mean_clip=4.0,
                           min_highway=0.2, max_highway=0.8, regularized_steps=(0,), first_step_loss_coeff=2.0)
     cd["share_theta"] = cd["share_phi"] = True
-    ospec = opc.make_spec(H=16, W=16, K=c.latent_dim, **HEAD)
+    ospec = opc.make_spec(H=16, W=16, K=c.latent_dim, **head)
     hp = opc.init_params(ospec, seed + 11)
     pv.head.set_params(hp)
     x, tgt, eps = spec.make_inputs(cd, batch=4)
     rng = np.random.default_rng(seed + 5)
-    u_mix = rng.uniform(1e-5, 1 - 1e-5, (4, 16, 16, HEAD["nr_mix"]))
+    u_mix = rng.uniform(1e-5, 1 - 1e-5, (4, 16, 16, head["nr_mix"]))
     u_log = rng.uniform(1e-5, 1 - 1e-5, (4, 16, 16, 3))
     return pv, cd, ospec, hp, x, tgt, eps, u_mix, u_log, rng
 
@@ -91,13 +91,19 @@ def test_pixelvae_step_matches_oracle():
     pv.close()
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16x6"])
-def test_pixelvae_split_head_matches_fp64(dtype):
-    """The head's split mode (3 bf16 planes per operand, 6 plane products: include/svae_pcnn.h) with an
-    fp32-grade engine (fp32, or bf16x6 whose default head is the split one) against the UNROUNDED fp64
-    oracle (bf16_head=False): x_hat_1 <= 1e-4 and the head gradients <= 1e-3, the
-    engine gradients <= 1e-3 (they now see an fp32-grade d/dz_1)."""
-    pv, cd, ospec, hp, x, tgt, eps, u_mix, u_log, rng = _setup(dtype=dtype, head_planes=3 if dtype == "fp32" else None)
+@pytest.mark.parametrize("dtype,head", [("fp32", HEAD), ("bf16x6", HEAD),
+                                        ("bf16x6", dict(nr_resnet=2, nr_filters=64, nr_mix=2))])
+def test_pixelvae_split_head_matches_fp64(dtype, head):
+    """The head's split mode (include/svae_pcnn.h): every layer whose channel counts are multiples of 8 on
+    two scaled fp16 planes per operand (3 fp16-MFMA products; the fused halo conv and the premax split of
+    the nonlinearity outputs), the 4-channel input convs and the 10 M-channel output nin on 3 bf16 planes
+    (6 products), with an fp32-grade engine (fp32, or bf16x6 whose default head is the split one) against
+    the UNROUNDED fp64 oracle (bf16_head=False): x_hat_1 <= 1e-4 and the head gradients <= 1e-3 (VERDICT r04
+    item 7), the engine gradients <= 1e-3 (they now see an fp32-grade d/dz_1).  The 64-filter, 2-resnet head
+     runs the fp16-plane GEMMs over several 32-channel K chunks (the concatenated 2F = 128
+    inputs of the up-pass resnets: four), which the 8-filter head's single chunk does not."""
+    pv, cd, ospec, hp, x, tgt, eps, u_mix, u_log, rng = _setup(dtype=dtype, head_planes=3 if dtype == "fp32" else None,
+                                                               head=head)
     assert pv.head.planes == 3
     pv.forward(x, tgt, eps, 0.6, u_mix, u_log)
     masks = _masks(rng, pv)
@@ -118,8 +124,9 @@ def test_pixelvae_split_head_matches_fp64(dtype):
     hlive = [k for k, v in o["head_grads"].items() if np.linalg.norm(v) > 1e-9]
     hv = _rel(cat(g_head, hlive), cat(o["head_grads"], hlive))
     hw = max(_rel(g_head[k], o["head_grads"][k]) for k in hlive)
-    print("\nc_pixelvae split head (%s engine): loss rel %.2e; x_hat_0 %.2e x_hat_1 %.2e; engine grads %.2e; head "
-          "grads vector %.2e worst tensor %.2e" % (dtype, el, e0, e1, gv, hv, hw))
+    print("\nc_pixelvae split head (%s engine, %d filters x %d resnets): loss rel %.2e; x_hat_0 %.2e x_hat_1 %.2e; "
+          "engine grads %.2e; head grads vector %.2e worst tensor %.2e"
+          % (dtype, head["nr_filters"], head["nr_resnet"], el, e0, e1, gv, hv, hw))
     assert el <= 1e-5 and e0 <= 1e-4 and e1 <= 1e-4
     assert gv <= 1e-3 and hv <= 1e-3
     pv.close()
