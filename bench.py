@@ -17,6 +17,12 @@ import os
 import sys
 import time
 
+# Hardware queues per process, before anything initialises HIP: the engine's three streams plus RCCL's own
+# (N > 1) share HIP's default 4 queues, and streams sharing a queue serialise.  Measured with an RCCL process
+# group in the process (tools/dist_overhead.py, profiles/r06_d_overhead.txt): 19.30 ms/step at 4 queues,
+# 15.48 at 8 (15.54 / 15.50 without a process group: N = 1 is unaffected)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 import numpy as np
 import torch
 
@@ -685,6 +691,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "warmup_extra_steps": extra,
+            "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
             "warmup_s": round(warm_s, 3),
             "ms_per_step": round(ms, 3),
             "higher_is_better": True,

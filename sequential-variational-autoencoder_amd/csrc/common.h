@@ -24,6 +24,14 @@ __device__ __forceinline__ void h16_pair(float w, int e, _Float16& h0, _Float16&
   h0 = (_Float16)s;
   h1 = (_Float16)(s - (float)h0);
 }
+// An exponent-table entry: the exponent in the low 16 bits (signed); bit 16 set where the tensor's three bf16
+// planes are read too (split mode: only the small-N conv-T of the image-channel convs' input gradients reads
+// them; every other GEMM there takes the fp16 pair, so the shadow and Adam kernels skip the bf16 planes of
+// the rest -- 6 bytes per weight and layout)
+#define WTAB_BF16 (1 << 16)
+__host__ __device__ __forceinline__ int wtab_exp(int v) { return (int)(short)(v & 0xffff); }
+__host__ __device__ __forceinline__ bool wtab_bf16(int v) { return (v & WTAB_BF16) != 0; }
+
 // the exponent for a tensor whose max |w| is wmax (0 or non-finite: H16_WS)
 __host__ __device__ __forceinline__ int h16_wexp(float wmax) {
   if (!(wmax > 0.f) || !(wmax < 3.0e38f)) return H16_WS;

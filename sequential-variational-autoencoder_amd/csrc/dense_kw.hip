@@ -48,7 +48,7 @@ __global__ __launch_bounds__(256) void dense_kw_kernel(FwdArgs a) {
   const int m = m0 + wr * 32 + l32;
   const bool mv = m < a.rows;
   const __bf16* Bw = (const __bf16*)a.Bh;  // (NS = 2: advanced to the fp16 planes below)
-  [[maybe_unused]] const int wex = (NS == 2 && a.wexp) ? a.wexp[0] : H16_WS;
+  [[maybe_unused]] const int wex = (NS == 2 && a.wexp) ? wtab_exp(a.wexp[0]) : H16_WS;
   f32x16 acc[TN];
 #pragma unroll
   for (int t = 0; t < TN; ++t)

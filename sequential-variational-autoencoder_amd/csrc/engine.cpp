@@ -546,7 +546,8 @@ struct svae_ctx {
   hipEvent_t ev_sfc[64] = {};
   svae_step_hook hook = nullptr;
   void* hook_user = nullptr;
-  hipEvent_t ev_hook = nullptr;
+  hipEvent_t ev_hook = nullptr;     // (system-scope release: a collective's peers read the bucket)
+  hipEvent_t ev_hook_dev = nullptr; // the same hand-over without a hook (fused Adam only): device scope
   float* cs_part = nullptr;  // output-bias column-sum partials (side stream)
   bool generative = false;   // svae_generate: chain on caller / prior latents, no recognition
   float* zero_img = nullptr; // [B,H,W,C] zeros: reconstruction target of the generative chain
@@ -1524,8 +1525,11 @@ static void adam_range(svae_ctx* c, long long lo, long long hi, float lr, long l
 static int step_hook(svae_ctx* c, int t) {
   if ((!c->hook && !c->fa_on) || c->m.shared) return 0;  // shared tensors are complete only after every step
   if (c->side) {
-    hipEventRecord(c->ev_hook, c->st);
-    hipStreamWaitEvent(c->st2, c->ev_hook, 0);
+    // the system-scope release only where a collective reads the bucket (8 per step otherwise: each writes the
+    // L2s back on the main stream for no reader outside this device)
+    hipEvent_t ev = c->hook ? c->ev_hook : c->ev_hook_dev;
+    hipEventRecord(ev, c->st);
+    hipStreamWaitEvent(c->st2, ev, 0);
     if (int r = side_run_queued(c)) return r;  // the step's queued weight gradients, before its bucket
     side_merge(c);
     hipEventRecord(c->ev_j3, c->st3);  // the step's split-latent gradients
@@ -2832,7 +2836,14 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
         svae_destroy(c);
         return fail(nullptr, SVAE_ENOMEM, std::string("hipMalloc exponent table: ") + hipGetErrorString(e));
       }
-      std::vector<int> w0((size_t)nb, H16_WS);
+      // exponent H16_WS until the first shadow refresh; the bf16-planes flag on the tensors a small-N conv-T
+      // may read (a side under 32 channels: the image-channel convs, whose input gradients run on
+      // convt_smalln's 3 bf16 planes); every other split-mode GEMM reads the fp16 pair only (halo_x3,
+      // halo_kw and dense_kw take the shadows with FwdArgs::h16 set)
+      std::vector<int> w0((size_t)nb, H16_WS & 0xffff);
+      for (const TT& x : tt)
+        if (x.taps == 16 && (x.R < 32 || x.Cc < 32))
+          for (long long b = x.off >> 6; b < (x.off + (long long)x.taps * x.R * x.Cc + 63) >> 6; ++b) w0[b] |= WTAB_BF16;
       hipMemcpy(c->wtab, w0.data(), nb * sizeof(int), hipMemcpyHostToDevice);
       if (!info.empty()) hipMemcpy(c->winfo_d, info.data(), info.size() * sizeof(long long), hipMemcpyHostToDevice);
       hipMemset(c->wovf, 0, sizeof(int));
@@ -2872,6 +2883,7 @@ int svae_create(const svae_config* cfg, int device, svae_ctx** out) {
       mk(&c->ev_drain);
       mk(&c->ev_da_ready); mk(&c->ev_da_free); mk(&c->ev_start); mk(&c->ev_join);
       ok = ok && hipEventCreateWithFlags(&c->ev_hook, hipEventDisableTiming) == hipSuccess;
+      mk(&c->ev_hook_dev);
       mk(&c->ev_aux); mk(&c->ev_aux2); mk(&c->ev_dz); mk(&c->ev_j3); mk(&c->ev_j4);
       mk(&c->ev_drain3);
       for (int i = 0; i < 64; ++i) mk(&c->ev_sfc[i]);
@@ -2902,7 +2914,7 @@ int svae_destroy(svae_ctx* c) {
       hipStreamSynchronize(sx);
       hipStreamDestroy(sx);
     }
-  for (hipEvent_t ev : {c->ev_da_ready, c->ev_da_free, c->ev_start, c->ev_join, c->ev_hook, c->ev_aux, c->ev_aux2, c->ev_dz, c->ev_j3, c->ev_j4,
+  for (hipEvent_t ev : {c->ev_da_ready, c->ev_da_free, c->ev_start, c->ev_join, c->ev_hook, c->ev_hook_dev, c->ev_aux, c->ev_aux2, c->ev_dz, c->ev_j3, c->ev_j4,
                         c->ev_drain3})
     if (ev) hipEventDestroy(ev);
   for (hipEvent_t ev : c->ev_sfc)

@@ -1140,15 +1140,18 @@ __global__ void shadow_n_kernel(const float* w, __bf16* out, long long n, int ns
        i += (long long)gridDim.x * blockDim.x * 4) {
     if (i + 3 < n) {
       f32x4 v = *(const f32x4*)(w + i);
+      bool bfp = true;  // the bf16 planes (split mode: only the tensors flagged in the table)
       if (nsp == 3) {  // split mode: the fp16 planes too
         _Float16 h0[4], h1[4];
-        const int ex = wtab ? wtab[i >> 6] : H16_WS;
-        for (int e = 0; e < 4; ++e) h16_pair(v[e], ex, h0[e], h1[e]);
+        const int tv = wtab ? wtab[i >> 6] : (H16_WS | WTAB_BF16);
+        bfp = wtab_bf16(tv);
+        for (int e = 0; e < 4; ++e) h16_pair(v[e], wtab_exp(tv), h0[e], h1[e]);
         for (int e = 0; e < 4; ++e) {
           ((_Float16*)out)[H16_PLANE * plane + i + e] = h0[e];
           ((_Float16*)out)[(H16_PLANE + 1) * plane + i + e] = h1[e];
         }
       }
+      if (bfp)
       for (int p = 0; p < nsp; ++p) {
         const bf16x4 h = __builtin_convertvector(v, bf16x4);
         *(bf16x4*)(out + p * plane + i) = h;
@@ -1157,9 +1160,10 @@ __global__ void shadow_n_kernel(const float* w, __bf16* out, long long n, int ns
     } else {
       for (long long j = i; j < n; ++j) {
         float v = w[j];
+        const int tv = wtab ? wtab[j >> 6] : (H16_WS | WTAB_BF16);
         if (nsp == 3)
-          h16_pair(v, wtab ? wtab[j >> 6] : H16_WS, ((_Float16*)out)[H16_PLANE * plane + j],
-                   ((_Float16*)out)[(H16_PLANE + 1) * plane + j]);
+          h16_pair(v, wtab_exp(tv), ((_Float16*)out)[H16_PLANE * plane + j], ((_Float16*)out)[(H16_PLANE + 1) * plane + j]);
+        if (nsp != 3 || wtab_bf16(tv))
         for (int p = 0; p < nsp; ++p) {
           const __bf16 h = (__bf16)v;
           out[p * plane + j] = h;
@@ -1180,7 +1184,9 @@ __global__ __launch_bounds__(256) void shadow_t_kernel(const float* w, __bf16* o
   const float* src = w + off + (long long)d.y * R * Cc;
   __bf16* dst = out + off + (long long)d.y * R * Cc;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  const int ex = (nsp == 3 && wtab) ? wtab[off >> 6] : H16_WS;
+  const int tv = (nsp == 3 && wtab) ? wtab[off >> 6] : (H16_WS | WTAB_BF16);
+  const int ex = wtab_exp(tv);
+  const int np = (nsp != 3 || wtab_bf16(tv)) ? nsp : 0;  // bf16 planes written (split mode: flagged tensors)
   for (int i = ty; i < 32; i += 8) {
     int r = d.z + i, c = d.w + tx;
     t[i][tx] = (r < R && c < Cc) ? src[(long long)r * Cc + c] : 0.f;
@@ -1193,7 +1199,7 @@ __global__ __launch_bounds__(256) void shadow_t_kernel(const float* w, __bf16* o
       if (nsp == 3)  // split mode: the fp16 planes too
         h16_pair(v, ex, ((_Float16*)dst)[H16_PLANE * plane + (long long)c * R + r],
                  ((_Float16*)dst)[(H16_PLANE + 1) * plane + (long long)c * R + r]);
-      for (int p = 0; p < nsp; ++p) {
+      for (int p = 0; p < np; ++p) {
         const __bf16 h = (__bf16)v;
         dst[p * plane + (long long)c * R + r] = h;
         v -= (float)h;
@@ -1847,7 +1853,8 @@ __device__ float wexp_block_max(const float* w, long long n) {  // max |w[0..n)|
 __device__ int wexp_set(const float* w, const long long* info, int t, int* wtab) {
   const long long off = info[4 * t], n = info[4 * t + 1];
   const int e = h16_wexp(wexp_block_max(w + off, n));
-  for (long long b = (off >> 6) + threadIdx.x; b < ((off + n + 63) >> 6); b += blockDim.x) wtab[b] = e;
+  for (long long b = (off >> 6) + threadIdx.x; b < ((off + n + 63) >> 6); b += blockDim.x)
+    wtab[b] = (wtab[b] & ~0xffff) | (e & 0xffff);  // (the bf16-planes flag stays)
   return e;
 }
 

@@ -559,7 +559,7 @@ void igemm_halo_kw_kernel(KwArgs h) {
     const int m0 = cur.m0, n0 = cur.n0, group = cur.group, cls = cur.cls;
     float* red = (float*)ksm;  // [4][BM][BN]
     [[maybe_unused]] int wex = H16_WS;  // the weight planes' exponent (split mode)
-    if constexpr (NS == 2) wex = a.wexp ? a.wexp[group * a.wexp_gs] : H16_WS;
+    if constexpr (NS == 2) wex = a.wexp ? wtab_exp(a.wexp[group * a.wexp_gs]) : H16_WS;
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm)
 #pragma unroll

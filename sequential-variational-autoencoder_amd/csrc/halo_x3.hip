@@ -127,7 +127,7 @@ __global__ __launch_bounds__(256, RD == 4 ? 1 : X3_OCC(BM, NP, PI)) void gather_
   const int m0 = blk.x * BM, n0 = blk.y * 32, group = blk.z;
   const int nchunk = h.Cin / X3_CK;
   [[maybe_unused]] int wex = H16_WS;  // the split mode's weight-plane exponent (the epilogue's unscale)
-  if constexpr (NP == 2) wex = h.wexp ? h.wexp[group * h.wexp_gs] : H16_WS;
+  if constexpr (NP == 2) wex = h.wexp ? wtab_exp(h.wexp[group * h.wexp_gs]) : H16_WS;
   const int per_img = h.Hr * h.Wr;
 
   // ---- window items: PI per thread, 8 channels each (item it = pixel it / 4, channel part it % 4) ----

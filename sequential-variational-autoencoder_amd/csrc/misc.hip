@@ -1381,13 +1381,16 @@ __global__ void adam_kernel(float* w, const float* g, float* m, float* v, __bf16
     ((f32x4*)v)[q] = vv;
     ((f32x4*)w)[q] = ww;
     if (wn) {  // the bf16 N-layout copy (split mode: nsp planes, opload.h split4; and the fp16 planes)
+      bool bfp = true;  // the bf16 planes (split mode: only the tensors flagged in the table)
       if (nsp == 3) {
         _Float16 h0[4], h1[4];
-        const int ex = wtab ? wtab[(wbase + 4 * q) >> 6] : H16_WS;
-        for (int e = 0; e < 4; ++e) adam_h16(ww[e], ex, h0[e], h1[e], ovf);
+        const int tv = wtab ? wtab[(wbase + 4 * q) >> 6] : (H16_WS | WTAB_BF16);
+        bfp = wtab_bf16(tv);
+        for (int e = 0; e < 4; ++e) adam_h16(ww[e], wtab_exp(tv), h0[e], h1[e], ovf);
         *(ol4h*)((_Float16*)wn + H16_PLANE * plane + 4 * q) = ol4h{h0[0], h0[1], h0[2], h0[3]};
         *(ol4h*)((_Float16*)wn + (H16_PLANE + 1) * plane + 4 * q) = ol4h{h1[0], h1[1], h1[2], h1[3]};
       }
+      if (bfp)
       for (int p = 0; p < nsp; ++p) {
         const bf16x4_t h = __builtin_convertvector(ww, bf16x4_t);
         *(bf16x4_t*)(wn + p * plane + 4 * q) = h;
@@ -1399,9 +1402,10 @@ __global__ void adam_kernel(float* w, const float* g, float* m, float* v, __bf16
     adam1(w[i], g[i], m[i], v[i], lr_t, b1, b2, eps, clipv);
     if (wn) {
       float x = w[i];
+      const int tv = wtab ? wtab[(wbase + i) >> 6] : (H16_WS | WTAB_BF16);
       if (nsp == 3)
-        adam_h16(x, wtab ? wtab[(wbase + i) >> 6] : H16_WS, ((_Float16*)wn)[H16_PLANE * plane + i],
-                 ((_Float16*)wn)[(H16_PLANE + 1) * plane + i], ovf);
+        adam_h16(x, wtab_exp(tv), ((_Float16*)wn)[H16_PLANE * plane + i], ((_Float16*)wn)[(H16_PLANE + 1) * plane + i], ovf);
+      if (nsp != 3 || wtab_bf16(tv))
       for (int p = 0; p < nsp; ++p) {
         const __bf16 h = (__bf16)x;
         wn[p * plane + i] = h;

@@ -3,7 +3,8 @@ averaged gradient per iteration (parallel.py).
 
 Eight ranks share the one GPU of the test box (spawned before any GPU call; gloo over device
 tensors -- RCCL refuses several ranks on one device, and the driver's 8-GPU bench covers RCCL over
-xGMI).  Each rank runs the bf16 engine at B = 128 on its contiguous shard of one 1024-image batch
+xGMI).  Each rank runs the engine at B = 128 -- in the bench's headline mode bf16x6 (the fp32-grade split
+step) and in bf16 -- on its contiguous shard of one 1024-image batch
 through the bench's DP path: OverlappedAllReduce (per-step buckets exchanged from inside the
 backward) + backward_apply (each bucket's clip + Adam right after its exchange).  Checked:
   * every rank's exchanged gradient equals the float64 mean of the 8 per-shard engine gradients to
@@ -47,13 +48,13 @@ def _global_batch(cfg):
     return x, eps
 
 
-def _worker(rank, port, out_dir):
+def _worker(rank, port, out_dir, dtype):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
     cfgmod, SV, par = pkg_mod("config"), pkg_mod("sequential_vae").SequentialVAE, pkg_mod("parallel")
-    cfg = cfgmod.preset("celeba", batch=PER, dtype="bf16")
+    cfg = cfgmod.preset("celeba", batch=PER, dtype=dtype)
     xg, eg = _global_batch(cfg)
     x = par.shard(xg, rank, WORLD).cuda().contiguous()
     eps = eg[:, rank * PER:(rank + 1) * PER].cuda().contiguous()
@@ -127,11 +128,12 @@ def _worker(rank, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_dp8_celeba_1024_sharded_on_engine(tmp_path):
-    mp.spawn(_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+@pytest.mark.parametrize("dtype", ["bf16x6", "bf16"])
+def test_dp8_celeba_1024_sharded_on_engine(tmp_path, dtype):
+    mp.spawn(_worker, args=(_free_port(), str(tmp_path), dtype), nprocs=WORLD, join=True)
     rs = [json.loads((tmp_path / ("r%d.json" % r)).read_text()) for r in range(WORLD)]
     r0 = rs[0]
-    print("\nDP8 CelebA 1024 = 8 x 128 (bf16 engine, overlapped exchange + per-bucket Adam):")
+    print("\nDP8 CelebA 1024 = 8 x 128 (%s engine, overlapped exchange + per-bucket Adam):" % dtype)
     for r in rs:
         print("  rank %d: loss %.6f (DP step %.6f); exchanged vs float64 mean: rel L2 %.2e, max |d| / (2e-6 mean|g|) "
               "%.3f; bitwise as rank 0: grad %s params %s" % (r["rank"], r["loss_plain"], r["loss_dp"], r["rel"],
