@@ -126,8 +126,16 @@ __global__ __launch_bounds__(256, RD == 4 ? 1 : X3_OCC(BM, NP, PI)) void gather_
   const BlockXYZ blk = xcd_block();
   const int m0 = blk.x * BM, n0 = blk.y * 32, group = blk.z;
   const int nchunk = h.Cin / X3_CK;
-  [[maybe_unused]] int wex = H16_WS;  // the split mode's weight-plane exponent (the epilogue's unscale)
-  if constexpr (NP == 2) wex = h.wexp ? wtab_exp(h.wexp[group * h.wexp_gs]) : H16_WS;
+  // the split mode's weight-plane exponent (the epilogue's unscale), read with a vector-memory load whose
+  // value is first used in the epilogue: a scalar load would be waited for before the window's addresses are
+  // even computed (lgkmcnt is not in order), this one completes under the window's own wait (num_records 0
+  // without a table: the load returns 0, decoded as H16_WS below)
+  [[maybe_unused]] int wraw = 0;
+  if constexpr (NP == 2) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(h.wexp ? h.wexp + group * h.wexp_gs : nullptr), (short)0, h.wexp ? 4 : 0, 0x00020000);
+    wraw = __builtin_amdgcn_raw_buffer_load_b32(r, 0, 0, 0);
+  }
   const int per_img = h.Hr * h.Wr;
 
   // ---- window items: PI per thread, 8 channels each (item it = pixel it / 4, channel part it % 4) ----
@@ -308,21 +316,8 @@ __global__ __launch_bounds__(256, RD == 4 ? 1 : X3_OCC(BM, NP, PI)) void gather_
   }
   X3_STAMP(10);
 
-  // ---- the waves' tiles into LDS (in the units of C), then one epilogue over the block ----
-  float* red = (float*)xsm;  // [4][BM][32]
-  // (the split mode's tiles in units of 2^(hs + H16_WS), shared by the block's waves: the reduced sums are
-  // unscaled below -- exact, as every partial carries the same power of two)
-  const int usc = NP == 2 ? -(hs + wex) : 0;
-#pragma unroll
-  for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-      red[(wave * BM + m) * 32 + l32] = acc[tm][r];
-    }
-  __syncthreads();
-  X3_STAMP(11);
-
+  // ---- epilogue operands (independent of the accumulators): set up, and the first row batch's loads issued
+  // before the tiles go through LDS, so their latency runs under the reduction ----
   // 16-byte epilogue: thread = 4 consecutive columns x rows rg, rg + 32, ... (8 threads per 128-B row)
   constexpr int ROWS = CPW ? 4 * BM : BM;  // output rows of the block (CPW: the four classes' tiles)
   constexpr int NR = ROWS / 32;
@@ -342,13 +337,11 @@ __global__ __launch_bounds__(256, RD == 4 ? 1 : X3_OCC(BM, NP, PI)) void gather_
   const bool pbf = NP == 1 && h.bw.pre_bf16, ybf = NP == 1 && h.bw.y_bf16;
   const float* bwpre = bwc ? pf_at(h.bw.pre, group * h.bw.pre_gs, pbf) : nullptr;
   const float* bwy = (bwc && h.bw.y) ? pf_at(h.bw.y, group * h.bw.y_gs, ybf) : nullptr;
-  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
-  constexpr int NB = NR < 2 ? NR : 2;  // rows per batch: every global load of a batch before its first store
+  constexpr int NB = NR < 4 ? NR : 4;  // rows per batch: every global load of a batch before its first store
   static_assert(NR % NB == 0, "row batches");
-#pragma unroll
-  for (int i0 = 0; i0 < NR; i0 += NB) {
-    long long orow[NB];
-    f32x4 cv[NB], pv[NB], yv[NB];
+  long long orow[NB];
+  f32x4 cv[NB], pv[NB], yv[NB];
+  auto fetch = [&](int i0) {
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const int vr = rg + 32 * (i0 + b);
@@ -368,6 +361,28 @@ __global__ __launch_bounds__(256, RD == 4 ? 1 : X3_OCC(BM, NP, PI)) void gather_
       if (bwpre) pv[b] = pf_ld4(bwpre, orow[b] * h.bw.ldp + n, pbf);
       if (bwy) yv[b] = pf_ld4(bwy, orow[b] * h.bw.ldy + n, ybf);
     }
+  };
+  fetch(0);
+
+  // ---- the waves' tiles into LDS (in the units of C), then one epilogue over the block ----
+  float* red = (float*)xsm;  // [4][BM][32]
+  // (the split mode's tiles in units of 2^(hs + H16_WS), shared by the block's waves: the reduced sums are
+  // unscaled below -- exact, as every partial carries the same power of two)
+  const int usc = NP == 2 ? -(hs + (h.wexp ? wtab_exp(wraw) : H16_WS)) : 0;
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      red[(wave * BM + m) * 32 + l32] = acc[tm][r];
+    }
+  __syncthreads();
+  X3_STAMP(11);
+
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i0 = 0; i0 < NR; i0 += NB) {
+    if (i0 > 0) fetch(i0);
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const int vr = rg + 32 * (i0 + b);
