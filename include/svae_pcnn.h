@@ -101,6 +101,11 @@ int svae_pcnn_conv_wgrad_planes(const void* x, int n, int hi, int wi, int cin, i
  * rows with oy == 0 / ox == 0 of a [n][ho][wo] row space (the zeroed shifted outputs). */
 int svae_pcnn_colsum(const float* x, int64_t rows, int c, int ldx, int ho, int wo, int mask_edge, float* out,
                      int accumulate, float* scratch, void* stream);
+/* The split mode's gradient operand prologue in one pass over x (fp32 [rows][c], ld ldx): its column sums into
+ * out (as svae_pcnn_colsum, mask_edge 0: bitwise) and max|x| into h16_scale[1] (as the absmax pass of
+ * svae_pcnn_split_planes), after which svae_pcnn_split_h16_premax writes the two fp16 planes. */
+int svae_pcnn_colsum_absmax(const float* x, int64_t rows, int c, int ldx, float* out, int accumulate, float* scratch,
+                            float* h16_scale, void* stream);
 /* zero the rows / columns a zero_edge conv wrote as 0 (its output gradient there is dead). */
 int svae_pcnn_mask_edge(float* x, int n, int ho, int wo, int c, int ldx, int mask_edge, void* stream);
 

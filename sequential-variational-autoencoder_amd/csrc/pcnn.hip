@@ -752,6 +752,206 @@ void pc3_launch(const PcGeom& g, const Pc3& h, const void* x, const __bf16* w, i
 }
 
 // ---------------------------------------------------------------------------------------------
+// Row-staged halo conv of the split mode (both fp16 planes, three products per fragment pair): the
+// block covers up to 160 output channels (NT = 5 column tiles) so the input window -- 4 B per element
+// in two planes -- is staged ONCE per chunk for all of them (pc_conv3 HP holds every tap's weight rows
+// in LDS, which caps it at 64 columns: the window was re-read by 3 / 5 column blocks of the 160 / 320-
+// channel convs and the 160-channel ones computed 192).  Per 32-channel chunk the window stays in LDS
+// while the weight rows of ONE kernel row (kw taps x 32 NT rows, both planes) at a time pass through
+// it: per row phase each wave runs kw x 2 x NT x 3 MFMAs (90 for the [2, 3] convs at NT = 5) and the
+// next phase's operands (the next row's weights, or the next chunk's window and row 0) load into
+// registers meanwhile.  Bitwise the same sums as pc_conv3 HP per output (same K order: chunk, tap,
+// k step, product order).
+// ---------------------------------------------------------------------------------------------
+#define PC3R_MAXPIX 384  // window pixels of a row-staged block (the head's shapes: 306-330)
+template <int NT>
+__global__ __launch_bounds__(512) void pc_conv3r_kernel(PcGeom g, Pc3 h, const __bf16* __restrict__ Xh,
+                                                        const __bf16* __restrict__ Wk, int kpad,
+                                                        const float* __restrict__ bias, float* __restrict__ Y, int ldy,
+                                                        int accumulate, int zero_edge, PcScale sc, long long xpst,
+                                                        long long wpst) {
+  constexpr int BM = 256;
+  constexpr int BR = 32 * NT;                                  // output channels per block
+  constexpr int AI = (PC3R_MAXPIX * 4 + 511) / 512;            // window items (8 channels) per thread
+  constexpr int BI = (3 * BR * 4 + 511) / 512;                 // 16-B weight items of one kernel row (kw <= 3)
+  extern __shared__ __attribute__((aligned(16))) __bf16 pc3s[];
+  __bf16* As = pc3s;                          // [plane][npix][PC2_P]
+  __bf16* Bs = pc3s + 2 * h.npix * PC2_P;     // [plane][kw][BR][PC2_P]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hh = lane >> 5;
+  const int per_img = g.ho * g.wo;
+  const long long m0 = (long long)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BR;
+  const int img0 = (int)(m0 / per_img);
+  const int oy0 = (int)(m0 - (long long)img0 * per_img) / g.wo;
+  const int iy0 = oy0 + h.oy_off, ix0 = h.ox_off;
+  const int nbr = g.kw * BR;  // staged weight rows of one kernel row
+
+  int aoff[AI];  // (element offsets: the head's activations hold < 2^31 elements, pc3r_ok)
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int it = tid + 512 * i;
+    aoff[i] = -2;
+    if (it < h.npix * 4) {
+      const int pix = it >> 2, part = it & 3;
+      const int il = pix / (h.PR * h.PC);
+      const int r2 = pix - il * h.PR * h.PC;
+      const int pr = r2 / h.PC, pc = r2 - pr * h.PC;
+      const int iy = iy0 + pr, ix = ix0 + pc;
+      aoff[i] = (iy >= 0 && iy < g.hi && ix >= 0 && ix < g.wi)
+                    ? ((((img0 + il) * g.hi + iy) * g.wi + ix) * g.ldx + part * 8)
+                    : -1;
+    }
+  }
+  pc_bf16x8 rh[AI], rh1[AI], rb[BI], rb1[BI];
+  auto load_window = [&](int c) {
+    const int k0 = c * 32;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int ci = k0 + ((tid + 512 * i) & 3) * 8;
+      const pc_bf16x8 z = {};
+      const bool ok = aoff[i] >= 0 && ci < g.cin;
+      rh[i] = ok ? *(const pc_bf16x8*)(Xh + aoff[i] + k0) : z;
+      rh1[i] = ok ? *(const pc_bf16x8*)(Xh + xpst + aoff[i] + k0) : z;
+    }
+  };
+  auto load_row = [&](int c, int ky) {  // kernel row ky's kw taps, chunk c
+    const int k0 = c * 32;
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int it = tid + 512 * i, row = it >> 2, q = it & 3;
+      const int kx = row / BR, n = row - kx * BR;
+      const pc_bf16x8 z = {};
+      const bool ok = row < nbr && n0 + n < g.cout;
+      const long long wo = ((long long)(ky * g.kw + kx) * g.cout + n0 + n) * kpad + k0 + q * 8;
+      rb[i] = ok ? *(const pc_bf16x8*)(Wk + wo) : z;
+      rb1[i] = ok ? *(const pc_bf16x8*)(Wk + wpst + wo) : z;
+    }
+  };
+  auto store_window = [&]() {
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      if (aoff[i] < -1) continue;
+      const int it = tid + 512 * i;
+      *(pc_bf16x8*)&As[(it >> 2) * PC2_P + (it & 3) * 8] = rh[i];
+      *(pc_bf16x8*)&As[(h.npix + (it >> 2)) * PC2_P + (it & 3) * 8] = rh1[i];
+    }
+  };
+  auto store_row = [&]() {
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int it = tid + 512 * i, row = it >> 2, q = it & 3;
+      if (row < nbr) {
+        *(pc_bf16x8*)&Bs[row * PC2_P + q * 8] = rb[i];
+        *(pc_bf16x8*)&Bs[(nbr + row) * PC2_P + q * 8] = rb1[i];
+      }
+    }
+  };
+
+  int abase;
+  {
+    const int rows_img = h.R * g.wo;
+    const int ml = wave * 32 + l32;
+    const int il = ml / rows_img;
+    const int rem = ml - il * rows_img;
+    const int ry = rem / g.wo, rx = rem - ry * g.wo;
+    abase = ((il * h.PR + ry) * h.PC + rx) * PC2_P + 8 * hh;
+  }
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  const int nchunk = kpad / 32;
+  load_window(0);
+  load_row(0, 0);
+  store_window();
+  store_row();
+  __syncthreads();
+  for (int c = 0; c < nchunk; ++c) {
+    for (int ky = 0; ky < g.kh; ++ky) {
+      const bool last_row = ky + 1 == g.kh;
+      const bool more = !last_row || c + 1 < nchunk;
+      if (!last_row) {
+        load_row(c, ky + 1);
+      } else if (c + 1 < nchunk) {
+        load_window(c + 1);
+        load_row(c + 1, 0);
+      }
+      for (int kx = 0; kx < g.kw; ++kx) {
+        const int toff = (g.mode == 0 ? ky * h.PC + kx : (g.kh - 1 - ky) * h.PC + (g.kw - 1 - kx)) * PC2_P;
+        const __bf16* bt = Bs + (kx * BR + l32) * PC2_P + 8 * hh;
+#pragma unroll
+        for (int kq = 0; kq < 2; ++kq) {
+          const pc_bf16x8 af = *(const pc_bf16x8*)&As[abase + toff + kq * 16];
+          const pc_bf16x8 af1 = *(const pc_bf16x8*)&As[h.npix * PC2_P + abase + toff + kq * 16];
+#pragma unroll
+          for (int tn = 0; tn < NT; ++tn) {
+            const pc_bf16x8 bf = *(const pc_bf16x8*)(bt + tn * 32 * PC2_P + kq * 16);
+            const pc_bf16x8 bf1 = *(const pc_bf16x8*)(bt + (nbr + tn * 32) * PC2_P + kq * 16);
+            acc[tn] = pc_mfma<true>(af, bf, acc[tn]);  // h0 h0' + h0 h1' + h1 h0' (pc_conv3 HP's order)
+            acc[tn] = pc_mfma<true>(af, bf1, acc[tn]);
+            acc[tn] = pc_mfma<true>(af1, bf, acc[tn]);
+          }
+        }
+      }
+      __syncthreads();  // every wave is done with this row's weights (and, after the last row, the window)
+      if (more) {
+        if (last_row) store_window();
+        store_row();
+        __syncthreads();
+      }
+    }
+  }
+  const float al = pc_alpha(sc);
+  const long long mw = m0 + wave * 32;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const long long mm = mw + (r & 3) + 8 * (r >> 2) + 4 * hh;
+    bool zero = false;
+    if (zero_edge) {
+      const int rr = (int)(mm % per_img);
+      zero = zero_edge == 1 ? (rr / g.wo == 0) : (rr % g.wo == 0);
+    }
+#pragma unroll
+    for (int tn = 0; tn < NT; ++tn) {
+      const int n = n0 + tn * 32 + l32;
+      if (n >= g.cout) continue;
+      float val = zero ? 0.f : acc[tn][r] * al + (bias ? bias[n] : 0.f);
+      float* p = Y + mm * ldy + n;
+      if (accumulate) val += *p;
+      *p = val;
+    }
+  }
+}
+
+// LDS of a row-staged launch (the window's and one kernel row's weights, both planes)
+size_t pc3r_lds(const PcGeom& g, const Pc3& h, int NT) {
+  return (size_t)(h.npix + g.kw * 32 * NT) * PC2_P * 2 * 2;
+}
+bool pc3r_ok(const PcGeom& g, const Pc3& h, int NT) {
+  return g.kw <= 3 && h.npix <= PC3R_MAXPIX && (long long)g.n * g.hi * g.wi * g.ldx < (1LL << 31) &&
+         pc3r_lds(g, h, NT) <= 160 * 1024;
+}
+
+template <int NT>
+void pc3r_launch(const PcGeom& g, const Pc3& h, const __bf16* x, const __bf16* w, int kpad, const float* bias, float* y,
+                 int ldy, int accumulate, int zero_edge, const PcScale& sc, hipStream_t st, long long xpst,
+                 long long wpst) {
+  static bool attr = false;
+  if (!attr) {
+    const int mx = (PC3R_MAXPIX + 3 * 32 * NT) * PC2_P * 2 * 2;
+    (void)hipFuncSetAttribute((const void*)pc_conv3r_kernel<NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              mx < 160 * 1024 ? mx : 160 * 1024);
+    attr = true;
+  }
+  const long long rows = (long long)g.n * g.ho * g.wo;
+  const dim3 grid((unsigned)(rows / 256), (unsigned)((g.cout + 32 * NT - 1) / (32 * NT)));
+  hipLaunchKernelGGL((pc_conv3r_kernel<NT>), grid, dim3(512), pc3r_lds(g, h, NT), st, g, h, x, w, kpad, bias, y, ldy,
+                     accumulate, zero_edge, sc, xpst, wpst);
+}
+
+// ---------------------------------------------------------------------------------------------
 // Tap-row weight gradient (stride 1, both modes: the resnet convs and their input gradients' nin /
 // dense layers viewed as 16-wide images): dW[tap][ci][co] = sum_p X[src(p, tap)][ci] . D[p][co].
 // Block = 64 ci x 64 co x ONE kernel row ky (its kw taps), four waves of 32 x 32 x kw taps; K = a
@@ -1217,6 +1417,34 @@ __global__ __launch_bounds__(256) void colsum_part4_kernel_pc(const float* __res
       s += *(const f32x4*)&x[(long long)r * ldx + col];
     }
   red[rl][cq] = s;
+  __syncthreads();
+  if (rl == 0 && col < c) {
+    f32x4 t = red[0][cq];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) t += red[j][cq];
+    *(f32x4*)&part[(long long)blockIdx.y * c + col] = t;
+  }
+}
+// stage 1 with max |x| (the split mode's gradient planes, svae_pcnn_colsum_absmax): the bias gradient's column
+// partials and the fp16 planes' scale from ONE pass over dy (were colsum_part4 + absmax4: two reads of it)
+__global__ __launch_bounds__(256) void colsum_amax4_kernel_pc(const float* __restrict__ x, int rows, int c, int ldx,
+                                                              int rows_per_split, float* __restrict__ part,
+                                                              unsigned* __restrict__ mx) {
+  __shared__ f32x4 red[16][16];
+  const int cq = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int col = blockIdx.x * 64 + cq * 4;
+  const int r0 = blockIdx.y * rows_per_split;
+  const int r1 = r0 + rows_per_split < rows ? r0 + rows_per_split : rows;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  float m = 0.f;
+  if (col < c)
+    for (int r = r0 + rl; r < r1; r += 16) {
+      const f32x4 v = *(const f32x4*)&x[(long long)r * ldx + col];
+      s += v;
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+    }
+  red[rl][cq] = s;
+  block_absmax_put(m, mx);  // (its barrier also orders red's stores before the reads below)
   __syncthreads();
   if (rl == 0 && col < c) {
     f32x4 t = red[0][cq];
@@ -2323,13 +2551,31 @@ static int pcnn_conv_hp(const void* x, int n, int hi, int wi, int cin, int ldx, 
   size_t lds0 = 0;
   if (!pc3_plan(g, kpad, 1, &h, &lds0)) return 1;
   const int n32 = (cout + 31) / 32;
+  const __bf16* w = (const __bf16*)wk;
+  hipStream_t st = (hipStream_t)stream;
+  if (svae_knob("SVAE_PC_RS", 1) != 0) {  // row-staged: up to 160 columns per block, one window per chunk
+    const int rtiles = (n32 + 4) / 5;
+    const int RNT = (n32 + rtiles - 1) / rtiles;
+    // (a grid under one block per CU keeps the 64-column tiles: 16 x 16 x 160 at B = 128 has 128 row blocks,
+    //  60 us on pc_conv3 HP's 384 blocks against 65 us on 128; tools/bench_pcconv_hp.py)
+    const long long rblocks = (long long)g.n * g.ho * g.wo / 256 * rtiles;
+    if (rblocks >= 256 && pc3r_ok(g, h, RNT)) {
+      const __bf16* xh = (const __bf16*)x;
+      switch (RNT) {
+        case 1: pc3r_launch<1>(g, h, xh, w, kpad, bias, y, ldy, accumulate, zero_edge, sc, st, xpst, wpst); break;
+        case 2: pc3r_launch<2>(g, h, xh, w, kpad, bias, y, ldy, accumulate, zero_edge, sc, st, xpst, wpst); break;
+        case 3: pc3r_launch<3>(g, h, xh, w, kpad, bias, y, ldy, accumulate, zero_edge, sc, st, xpst, wpst); break;
+        case 4: pc3r_launch<4>(g, h, xh, w, kpad, bias, y, ldy, accumulate, zero_edge, sc, st, xpst, wpst); break;
+        default: pc3r_launch<5>(g, h, xh, w, kpad, bias, y, ldy, accumulate, zero_edge, sc, st, xpst, wpst); break;
+      }
+      return hipchk();
+    }
+  }
   int tiles = (n32 + 1) / 2;  // at most 64 columns per block: two planes of window and weights in LDS
   const int NT = (n32 + tiles - 1) / tiles;
   const size_t lds = (size_t)(h.npix + kh * kw * 32 * NT) * PC2_P * 2 * 2;
   if (lds > 160 * 1024) return 1;
   NlbArgs nlb{};
-  const __bf16* w = (const __bf16*)wk;
-  hipStream_t st = (hipStream_t)stream;
   if (NT == 1) pc3_launch<1, 1, true, true, true>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, sc, st, xpst, wpst);
   else pc3_launch<2, 1, true, true, true>(g, h, x, w, kpad, bias, y, ldy, accumulate, zero_edge, nlb, sc, st, xpst, wpst);
   return hipchk();
@@ -2509,6 +2755,31 @@ int svae_pcnn_colsum(const float* x, int64_t rows, int c, int ldx, int ho, int w
                      ldx, ho * wo, wo, mask_edge, rps, scratch);
   hipLaunchKernelGGL(colsum_fin_kernel_pc, dim3((c + 63) / 64), dim3(256), 0, st, scratch, (int)ns, c, out,
                      accumulate);
+  return hipchk();
+}
+
+int svae_pcnn_colsum_absmax(const float* x, int64_t rows, int c, int ldx, float* out, int accumulate, float* scratch,
+                            float* h16_scale, void* stream) {
+  if (!x || !out || !scratch || !h16_scale || rows < 1 || c < 1 || ldx < c) return bad("pcnn_colsum_absmax: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(h16_scale + 1, 0, sizeof(float), st) != hipSuccess) return hipchk();
+  long long ns = (rows + 255) / 256;  // (svae_pcnn_colsum's split: the same column partials, bitwise)
+  if (ns > 1024) ns = 1024;
+  if (ns * c > (1LL << 24)) ns = ((1LL << 24) / c > 0) ? (1LL << 24) / c : 1;
+  const long long rps = (rows + ns - 1) / ns;
+  static const bool vec = svae_knob("SVAE_PC_COLSUM4", 1) != 0 && svae_knob("SVAE_PC_CSAMAX", 1) != 0;
+  if (vec && c % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)scratch & 15) == 0 &&
+      rows < (1LL << 31) - rps) {
+    hipLaunchKernelGGL(colsum_amax4_kernel_pc, dim3((c + 63) / 64, (unsigned)ns), dim3(256), 0, st, x, (int)rows, c,
+                       ldx, (int)rps, scratch, (unsigned*)(h16_scale + 1));
+    hipLaunchKernelGGL(colsum_fin4_kernel_pc, dim3((c + 63) / 64), dim3(256), 0, st, scratch, (int)ns, c, out,
+                       accumulate);
+    return hipchk();
+  }
+  const int rc = svae_pcnn_colsum(x, rows, c, ldx, 1, 1, 0, out, accumulate, scratch, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(absmax_kernel, dim3(blocks_for(rows * c, 256, 2048)), dim3(256), 0, st, x, (long long)rows, c, ldx,
+                     (unsigned*)(h16_scale + 1));
   return hipchk();
 }
 

@@ -438,9 +438,18 @@ class PixelCNNpp:
         kh, kw, s, pt, pl, mode, zero_edge, kf, kd, off_v, off_g, off_b = geo
         taps, cin, cout = kh * kw, x.c, y.c
         xb, xld, xbf, xpst, P, xsc = xs
-        ds, dld, dbf, dpst, _, dsc = self._planes(dy, xsc is not None)
         sc = self.scratch
-        _ck(L.svae_pcnn_colsum(_p(dy), y.rows, cout, cout, 0, 0, 0, _p(self.G, off_b), 0, _p(sc), st))
+        if xsc is not None and self.fuse_absmax and cout % 4 == 0 and dy.dtype == torch.float32:
+            # the fp16 planes of dy: the bias gradient's column sums and max|dy| from one pass, then the premax split
+            dsc = torch.empty(2, dtype=torch.float32, device=self.dev)
+            _ck(L.svae_pcnn_colsum_absmax(_p(dy), y.rows, cout, cout, _p(self.G, off_b), 0, _p(sc), _p(dsc), st))
+            ds = torch.empty(2 * y.rows * cout, dtype=torch.bfloat16, device=self.dev)
+            _ck(L.svae_pcnn_split_h16_premax(_p(dy), y.rows, cout, cout, ctypes.c_void_p(ds.data_ptr()), cout, _p(dsc),
+                                             st))
+            dld, dbf, dpst = cout, 1, y.rows * cout
+        else:
+            ds, dld, dbf, dpst, _, dsc = self._planes(dy, xsc is not None)
+            _ck(L.svae_pcnn_colsum(_p(dy), y.rows, cout, cout, 0, 0, 0, _p(self.G, off_b), 0, _p(sc), st))
         _ck(L.svae_pcnn_conv_wgrad_planes(ctypes.c_void_p(xb.data_ptr()), x.n, x.h, x.w, cin, xld, xbf, xpst,
                                           ctypes.c_void_p(ds.data_ptr()), dld, dbf, dpst, P, _p(xsc), _p(dsc), y.h, y.w,
                                           cout, kh, kw, s, pt, pl, mode, _p(dW), _p(sc), sc.numel(), st))

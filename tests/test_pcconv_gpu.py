@@ -350,3 +350,32 @@ def test_pcnn_wgrad_planes_is_fp32_grade(case):
         print("\nwgrad planes %s %s: rel %.2e max %.2e" % (case, fmt, rel, mx))
         assert torch.isfinite(got).all()
         assert rel <= 2e-6 and mx <= 2e-5
+
+
+@pytest.mark.parametrize("rows,c,ld,acc", [(131072, 160, 160, 0), (32768, 320, 320, 1), (3000, 40, 48, 0),
+                                           (777, 6, 6, 1)])
+def test_pcnn_colsum_absmax_is_colsum_plus_the_absmax_pass(rows, c, ld, acc):
+    """svae_pcnn_colsum_absmax (the split head's gradient prologue: bias-gradient column sums and max|dy| in one
+    pass) bit for bit svae_pcnn_colsum + the absmax pass of svae_pcnn_split_planes, and the premax split after it
+    the planes of svae_pcnn_split_planes (the 4-column vector kernel where c, ld % 4 == 0, the two passes else)."""
+    L = pkg_mod("_lib")
+    g = torch.Generator(device="cuda").manual_seed(rows + c)
+    src = torch.randn(rows, ld, device="cuda", generator=g) * 1e-3
+    out0 = torch.randn(c, device="cuda", generator=g)
+    out1 = out0.clone()
+    scratch = torch.empty(1 << 22, device="cuda")
+    sc = torch.empty(2, device="cuda")
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())
+    L.check(L.lib().svae_pcnn_colsum(vp(src), rows, c, ld, 1, 1, 0, vp(out0), acc, vp(scratch), L.stream_ptr()))
+    L.check(L.lib().svae_pcnn_colsum_absmax(vp(src), rows, c, ld, vp(out1), acc, vp(scratch), vp(sc), L.stream_ptr()))
+    torch.cuda.synchronize()
+    assert torch.equal(out0, out1)
+    assert float(sc[1]) == float(src[:, :c].abs().max())
+    if c % 4 == 0:
+        dense = src[:, :c].contiguous()
+        p1 = torch.empty(2, rows, c, dtype=torch.bfloat16, device="cuda")
+        L.check(L.lib().svae_pcnn_colsum_absmax(vp(dense), rows, c, c, vp(out1), 0, vp(scratch), vp(sc), L.stream_ptr()))
+        L.check(L.lib().svae_pcnn_split_h16_premax(vp(dense), rows, c, c, vp(p1), c, vp(sc), L.stream_ptr()))
+        p0, sc0 = _planes(L, dense, "h16")
+        torch.cuda.synchronize()
+        assert torch.equal(p0.view(torch.int16), p1.view(torch.int16)) and torch.equal(sc0, sc)
