@@ -106,6 +106,13 @@ int svae_pcnn_colsum(const float* x, int64_t rows, int c, int ldx, int ho, int w
  * svae_pcnn_split_planes), after which svae_pcnn_split_h16_premax writes the two fp16 planes. */
 int svae_pcnn_colsum_absmax(const float* x, int64_t rows, int c, int ldx, float* out, int accumulate, float* scratch,
                             float* h16_scale, void* stream);
+/* im2col of a stride-1 mode-0 conv input x ([n][hi][wi][cin], ld ldx, fp32) as the two scaled fp16 planes of a
+ * [n*ho*wo][kc] operand (planes kc * rows elements apart; h16_scale as svae_pcnn_split_planes: [2^-s, max|x|]):
+ * column (ky * kw + kx) * cin + ci holds x at (oy - pt + ky, ox - pl + kx), 0 outside the image and for columns
+ * >= kh * kw * cin.  The conv is then the 1x1 svae_pcnn_conv_planes over it with the [1][cout][kc] weight copy
+ * of V viewed as [kh * kw * cin][cout] (svae_pcnn_wnorm_planes with taps 1). */
+int svae_pcnn_im2col_h16(const float* x, int n, int hi, int wi, int cin, int ldx, int ho, int wo, int kh, int kw, int pt,
+                         int pl, void* out, int kc, float* h16_scale, void* stream);
 /* zero the rows / columns a zero_edge conv wrote as 0 (its output gradient there is dead). */
 int svae_pcnn_mask_edge(float* x, int n, int ho, int wo, int c, int ldx, int mask_edge, void* stream);
 

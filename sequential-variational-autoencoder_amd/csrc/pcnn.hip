@@ -2758,6 +2758,49 @@ int svae_pcnn_colsum(const float* x, int64_t rows, int c, int ldx, int ho, int w
   return hipchk();
 }
 
+// im2col of a small-channel stride-1 mode-0 conv's input as the two scaled fp16 planes of a [rows][kc] operand:
+// column k = (ky * kw + kx) * cin + ci holds x[img][oy - pt + ky][ox - pl + kx][ci] (0 outside the image and for
+// k >= kh * kw * cin), so the conv runs as a 1x1 conv with K = kc (the head's 4-channel input convs: K = 8-24 in
+// one 32-wide chunk instead of 32 per tap, and 2 planes / 3 products instead of 3 bf16 planes / 6 launches)
+__global__ __launch_bounds__(256) void im2col_h16_kernel(const float* __restrict__ x, int hi, int wi, int cin, int ldx,
+                                                         int ho, int wo, int kw, int pt, int pl, int kreal, long long rows,
+                                                         int kc, __bf16* __restrict__ out, float* h16) {
+  const int sh = h16_shift(__float_as_uint(h16[1]));
+  if (blockIdx.x == 0 && threadIdx.x == 0) h16[0] = ldexpf(1.f, -sh);
+  const long long n = rows * kc, pst = rows * kc;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / kc;
+    const int k = (int)(i - r * kc);
+    float v = 0.f;
+    if (k < kreal) {
+      const int tap = k / cin, ci = k - tap * cin;
+      const int ky = tap / kw, kx = tap - ky * kw;
+      const int img = (int)(r / ((long long)ho * wo));
+      const int rr = (int)(r - (long long)img * ho * wo);
+      const int oy = rr / wo, ox = rr - oy * wo;
+      const int iy = oy - pt + ky, ix = ox - pl + kx;
+      if (iy >= 0 && iy < hi && ix >= 0 && ix < wi) v = x[((long long)(img * hi + iy) * wi + ix) * ldx + ci];
+    }
+    h16_put(out, i, pst, v, sh);
+  }
+}
+
+int svae_pcnn_im2col_h16(const float* x, int n, int hi, int wi, int cin, int ldx, int ho, int wo, int kh, int kw, int pt,
+                         int pl, void* out, int kc, float* h16_scale, void* stream) {
+  if (!x || !out || !h16_scale || n < 1 || hi < 1 || wi < 1 || cin < 1 || ldx < cin || ho < 1 || wo < 1 || kh < 1 ||
+      kw < 1 || kc < kh * kw * cin || kc % 32)
+    return bad("pcnn_im2col_h16: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  const long long rows = (long long)n * ho * wo;
+  if (hipMemsetAsync(h16_scale + 1, 0, sizeof(float), st) != hipSuccess) return hipchk();
+  // the planes' scale from max|x| (>= max over the gathered columns: every value fits)
+  hipLaunchKernelGGL(absmax_kernel, dim3(blocks_for((long long)n * hi * wi * cin, 256, 2048)), dim3(256), 0, st, x,
+                     (long long)n * hi * wi, cin, ldx, (unsigned*)(h16_scale + 1));
+  hipLaunchKernelGGL(im2col_h16_kernel, dim3(blocks_for(rows * kc)), dim3(256), 0, st, x, hi, wi, cin, ldx, ho, wo, kw,
+                     pt, pl, kh * kw * cin, rows, kc, (__bf16*)out, h16_scale);
+  return hipchk();
+}
+
 int svae_pcnn_colsum_absmax(const float* x, int64_t rows, int c, int ldx, float* out, int accumulate, float* scratch,
                             float* h16_scale, void* stream) {
   if (!x || !out || !scratch || !h16_scale || rows < 1 || c < 1 || ldx < c) return bad("pcnn_colsum_absmax: bad arguments");

@@ -153,7 +153,7 @@ class PixelCNNpp:
     Adam moments and Polyak averages (flat fp32 device buffers)."""
 
     def __init__(self, spec, params=None, seed=0, device="cuda", scratch_elems=1 << 26, planes=1, bf16_grads=False,
-                 fuse_absmax=True):
+                 fuse_absmax=True, im2col=True):
         if not torch.cuda.is_available():
             raise RuntimeError("PixelCNNpp needs a GPU (HIP kernels in libsvae_hip.so); there is no CPU fallback")
         self.s = spec
@@ -202,6 +202,8 @@ class PixelCNNpp:
         # (split mode) the nonlinearity kernels also leave max|y| of their outputs, which are conv inputs, so
         # the fp16-plane split skips its absmax pass (bitwise; fuse_absmax=False: the separate pass, for A/Bs)
         self.fuse_absmax = bool(fuse_absmax)
+        # the split mode's small-channel input convs as 1x1 convs over their im2col (K = kh * kw * cin <= 32)
+        self.im2col = bool(im2col)
         if planes > 1:  # every activation and gradient stays fp32 (split into planes at each GEMM)
             self.bf16_grads = False
         self.probe, self.probe_cap = None, 0  # [(flops, event, event)] of timed forward conv launches
@@ -314,6 +316,9 @@ class PixelCNNpp:
         off_g, _, _ = self.table[name + "/g"]
         off_b, _, _ = self.table[name + "/b"]
         kf, kd = _r16(cin), _r16(cout)
+        if (self.planes > 1 and self.h16 and self.im2col and cin % 8 and cout % 8 == 0 and s == 1 and mode == 0
+                and taps * cin <= 32 and not self._init and id(x) in self._nograd and not x.bf):
+            return self._wconv_col(x, name, cout, kh, kw, pt, pl, zero_edge, out)
         h16 = self.planes > 1 and self.h16 and cin % 8 == 0 and cout % 8 == 0  # this layer's plane format
         P = 2 if h16 else self.planes
         norm = torch.empty(cout, dtype=torch.float32, device=self.dev)
@@ -350,9 +355,54 @@ class PixelCNNpp:
             _ck(L.svae_pcnn_wn_init(src.ptr(), src.rows, cout, src.ld, float(init_scale), _p(self.P, off_g),
                                     _p(self.P, off_b), _p(self.scratch), st))
         if self._record:
-            geo = (kh, kw, s, pt, pl, mode, zero_edge, kf, kd, off_v, off_g, off_b)
+            geo = (kh, kw, s, pt, pl, mode, zero_edge, kf, kd, off_v, off_g, off_b, (taps, cin))
             self._tape.append(lambda: self._wconv_bwd(x, out, norm, wkd, geo, xs, wsc))
             self._bias_of.setdefault(id(self._root(out)), []).append(off_b)  # (every conv summed into it)
+        return out
+
+    def _wconv_col(self, x, name, cout, kh, kw, pt, pl, zero_edge, out):
+        """A small-channel stride-1 conv of the split mode (the head's 4-channel input convs, no input gradient) as
+        the 1x1 fp16-plane conv of its im2col: K = kh * kw * cin columns in one 32-wide chunk (svae_pcnn_im2col_h16,
+        the weights V viewed as [kh * kw * cin][cout]); the weight gradient is the 1x1 one over the same planes."""
+        L = self.L
+        st = self._st()
+        taps, cin = kh * kw, x.c
+        K = taps * cin
+        off_v, _, _ = self.table[name + "/V"]
+        off_g, _, _ = self.table[name + "/g"]
+        off_b, _, _ = self.table[name + "/b"]
+        ho, wo = x.h, x.w
+        rows = x.n * ho * wo
+        norm = torch.empty(cout, dtype=torch.float32, device=self.dev)
+        wkf = torch.empty(2 * cout * 32, dtype=torch.bfloat16, device=self.dev)
+        wsc = torch.empty(2, dtype=torch.float32, device=self.dev)
+        _ck(L.svae_pcnn_wnorm_planes(_p(self.P, off_v), _p(self.P, off_g), 1, K, cout, _p(norm), _p(wkf), 32, None, 0, 2,
+                                     _p(wsc), st))
+        xcol = torch.empty(2 * rows * 32, dtype=torch.bfloat16, device=self.dev)
+        xsc = torch.empty(2, dtype=torch.float32, device=self.dev)
+        _ck(L.svae_pcnn_im2col_h16(x.ptr(), x.n, x.h, x.w, cin, x.ld, ho, wo, kh, kw, pt, pl,
+                                   ctypes.c_void_p(xcol.data_ptr()), 32, _p(xsc), st))
+        xc = Act(xcol, 32, x.n, ho, wo)  # (the planes' operand as the 1x1 conv's input: x.c = 32 columns)
+        self._nograd.add(id(xc))
+        self._keep.append(xc)
+        xs = (xcol, 32, 1, rows * 32, 2, xsc)
+        self.conv_flops += 2.0 * rows * cout * cin * taps
+        acc = out is not None
+        if out is None:
+            out = Act(self._new(rows, cout), cout, x.n, ho, wo)
+        pr = self.probe is not None and len(self.probe) < self.probe_cap
+        if pr:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        self._conv(xc, xs, wkf, 32, wsc, _p(self.P, off_b), out.ptr(), ho, wo, cout, out.ld, 1, 1, 1, 0, 0, 0,
+                   1 if acc else 0, zero_edge)
+        if pr:
+            e1.record()
+            self.probe.append((2.0 * rows * cout * cin * taps, e0, e1, 3))
+        if self._record:
+            geo = (1, 1, 1, 0, 0, 0, zero_edge, 32, 0, off_v, off_g, off_b, (1, K))
+            self._tape.append(lambda: self._wconv_bwd(xc, out, norm, None, geo, xs, wsc))
+            self._bias_of.setdefault(id(self._root(out)), []).append(off_b)
         return out
 
     def _planes(self, a, h16):
@@ -393,7 +443,7 @@ class PixelCNNpp:
     def _wconv_bwd(self, x, y, norm, wkd, geo, xs=None, wsc=None):
         L = self.L
         st = self._st()
-        kh, kw, s, pt, pl, mode, zero_edge, kf, kd, off_v, off_g, off_b = geo
+        kh, kw, s, pt, pl, mode, zero_edge, kf, kd, off_v, off_g, off_b, _ = geo
         taps, cin, cout = kh * kw, x.c, y.c
         dy = self._grad(y)
         dyb = dy.dtype == torch.bfloat16  # (its consumer wrote it bf16 and this conv's bias gradient with it)
@@ -435,7 +485,7 @@ class PixelCNNpp:
         and of dy (fp32, split in the layer's plane format; the bias gradient its column sums)."""
         L = self.L
         st = self._st()
-        kh, kw, s, pt, pl, mode, zero_edge, kf, kd, off_v, off_g, off_b = geo
+        kh, kw, s, pt, pl, mode, zero_edge, kf, kd, off_v, off_g, off_b, (wn_taps, wn_cin) = geo
         taps, cin, cout = kh * kw, x.c, y.c
         xb, xld, xbf, xpst, P, xsc = xs
         sc = self.scratch
@@ -453,7 +503,8 @@ class PixelCNNpp:
         _ck(L.svae_pcnn_conv_wgrad_planes(ctypes.c_void_p(xb.data_ptr()), x.n, x.h, x.w, cin, xld, xbf, xpst,
                                           ctypes.c_void_p(ds.data_ptr()), dld, dbf, dpst, P, _p(xsc), _p(dsc), y.h, y.w,
                                           cout, kh, kw, s, pt, pl, mode, _p(dW), _p(sc), sc.numel(), st))
-        _ck(L.svae_pcnn_wnorm_bwd(_p(self.P, off_v), _p(self.P, off_g), _p(norm), _p(dW), taps, cin, cout,
+        # (an im2col layer, _wconv_col: dW's first wn_taps * wn_cin rows are the [tap][cin] ones of V)
+        _ck(L.svae_pcnn_wnorm_bwd(_p(self.P, off_v), _p(self.P, off_g), _p(norm), _p(dW), wn_taps, wn_cin, cout,
                                   _p(self.G, off_v), _p(self.G, off_g), st))
         if id(x) in self._nograd:
             return
