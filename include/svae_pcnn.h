@@ -113,6 +113,20 @@ int svae_pcnn_colsum_absmax(const float* x, int64_t rows, int c, int ldx, float*
  * of V viewed as [kh * kw * cin][cout] (svae_pcnn_wnorm_planes with taps 1). */
 int svae_pcnn_im2col_h16(const float* x, int n, int hi, int wi, int cin, int ldx, int ho, int wo, int kh, int kw, int pt,
                          int pl, void* out, int kc, float* h16_scale, void* stream);
+/* svae_pcnn_conv_planes that also leaves max |y| (after the accumulate) in y_scale[1]: the bound the consuming
+ * svae_pcnn_nonlin_h16 takes. */
+int svae_pcnn_conv_planes_amax(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, int64_t x_pstride,
+                               const void* wk, int kpad, int planes, const float* x_scale, const float* w_scale,
+                               const float* bias, float* y, int ho, int wo, int cout, int ldy, int kh, int kw, int s,
+                               int pt, int pl, int mode, int accumulate, int zero_edge, float* y_scale, void* stream);
+/* svae_pcnn_nonlin with the dropout (a mask tensor [rows][cy] whose largest value is mask_max, or, mask NULL,
+ * the in-kernel one of keep, seed; keep 1: none) writing y only as the two scaled fp16 planes [2][rows][ldo] of
+ * the consuming conv (planes rows * ldo elements apart), at the exponent of a bound on max |y| known before the
+ * pass: x_scale[1] (= max |x|, from x's producer; at least 1 for elu / concat_elu) times the dropout's largest
+ * factor.  h16_scale <- [2^-s, the bound].  Needs c, ldx, ldo % 4 == 0, 16-B x and mask, 8-B out. */
+int svae_pcnn_nonlin_h16(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, float mask_max,
+                         float keep, uint64_t seed, const float* x_scale, void* out, int ldo, float* h16_scale,
+                         void* stream);
 /* zero the rows / columns a zero_edge conv wrote as 0 (its output gradient there is dead). */
 int svae_pcnn_mask_edge(float* x, int n, int ho, int wo, int c, int ldx, int mask_edge, void* stream);
 

@@ -769,7 +769,7 @@ __global__ __launch_bounds__(512) void pc_conv3r_kernel(PcGeom g, Pc3 h, const _
                                                         const __bf16* __restrict__ Wk, int kpad,
                                                         const float* __restrict__ bias, float* __restrict__ Y, int ldy,
                                                         int accumulate, int zero_edge, PcScale sc, long long xpst,
-                                                        long long wpst) {
+                                                        long long wpst, unsigned* __restrict__ amax) {
   constexpr int BM = 256;
   constexpr int BR = 32 * NT;                                  // output channels per block
   constexpr int AI = (PC3R_MAXPIX * 4 + 511) / 512;            // window items (8 channels) per thread
@@ -905,6 +905,7 @@ __global__ __launch_bounds__(512) void pc_conv3r_kernel(PcGeom g, Pc3 h, const _
   }
   const float al = pc_alpha(sc);
   const long long mw = m0 + wave * 32;
+  float am = 0.f;  // (amax: max |y| of the block's outputs, after the accumulate)
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const long long mm = mw + (r & 3) + 8 * (r >> 2) + 4 * hh;
@@ -921,8 +922,10 @@ __global__ __launch_bounds__(512) void pc_conv3r_kernel(PcGeom g, Pc3 h, const _
       float* p = Y + mm * ldy + n;
       if (accumulate) val += *p;
       *p = val;
+      am = fmaxf(am, fabsf(val));
     }
   }
+  if (amax) block_absmax_put(am, amax);
 }
 
 // LDS of a row-staged launch (the window's and one kernel row's weights, both planes)
@@ -937,7 +940,7 @@ bool pc3r_ok(const PcGeom& g, const Pc3& h, int NT) {
 template <int NT>
 void pc3r_launch(const PcGeom& g, const Pc3& h, const __bf16* x, const __bf16* w, int kpad, const float* bias, float* y,
                  int ldy, int accumulate, int zero_edge, const PcScale& sc, hipStream_t st, long long xpst,
-                 long long wpst) {
+                 long long wpst, unsigned* amax) {
   static bool attr = false;
   if (!attr) {
     const int mx = (PC3R_MAXPIX + 3 * 32 * NT) * PC2_P * 2 * 2;
@@ -948,7 +951,7 @@ void pc3r_launch(const PcGeom& g, const Pc3& h, const __bf16* x, const __bf16* w
   const long long rows = (long long)g.n * g.ho * g.wo;
   const dim3 grid((unsigned)(rows / 256), (unsigned)((g.cout + 32 * NT - 1) / (32 * NT)));
   hipLaunchKernelGGL((pc_conv3r_kernel<NT>), grid, dim3(512), pc3r_lds(g, h, NT), st, g, h, x, w, kpad, bias, y, ldy,
-                     accumulate, zero_edge, sc, xpst, wpst);
+                     accumulate, zero_edge, sc, xpst, wpst, amax);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2541,9 +2544,11 @@ int svae_pcnn_conv_wgrad_planes(const void* x, int n, int hi, int wi, int cin, i
 
 // The fp16-plane conv in ONE launch of the halo kernel with both planes staged (pc_conv3 HP): 1 if the launch is
 // not eligible (stride 2, a window or stage beyond the LDS budget) -- the caller then runs the three products
+// amax != NULL: max |y| into *amax where the row-staged kernel runs (*done set); the caller takes a pass otherwise
 static int pcnn_conv_hp(const void* x, int n, int hi, int wi, int cin, int ldx, long long xpst, const void* wk, int kpad,
                         long long wpst, const PcScale& sc, const float* bias, float* y, int ho, int wo, int cout, int ldy,
-                        int kh, int kw, int s, int pt, int pl, int mode, int accumulate, int zero_edge, void* stream) {
+                        int kh, int kw, int s, int pt, int pl, int mode, int accumulate, int zero_edge, void* stream,
+                        unsigned* amax = nullptr, bool* done = nullptr) {
   const PcGeom g = make_geom(n, hi, wi, cin, ldx, ho, wo, cout, kh, kw, s, pt, pl, mode);
   if (!geom_ok(g) || cin % 8 || ldx % 8 || kpad % 32 || ldy < cout) return 1;
   if (svae_knob("SVAE_PC_HP", 1) == 0) return 1;
@@ -2562,12 +2567,13 @@ static int pcnn_conv_hp(const void* x, int n, int hi, int wi, int cin, int ldx, 
     if (rblocks >= 256 && pc3r_ok(g, h, RNT)) {
       const __bf16* xh = (const __bf16*)x;
       switch (RNT) {
-        case 1: pc3r_launch<1>(g, h, xh, w, kpad, bias, y, ldy, accumulate, zero_edge, sc, st, xpst, wpst); break;
-        case 2: pc3r_launch<2>(g, h, xh, w, kpad, bias, y, ldy, accumulate, zero_edge, sc, st, xpst, wpst); break;
-        case 3: pc3r_launch<3>(g, h, xh, w, kpad, bias, y, ldy, accumulate, zero_edge, sc, st, xpst, wpst); break;
-        case 4: pc3r_launch<4>(g, h, xh, w, kpad, bias, y, ldy, accumulate, zero_edge, sc, st, xpst, wpst); break;
-        default: pc3r_launch<5>(g, h, xh, w, kpad, bias, y, ldy, accumulate, zero_edge, sc, st, xpst, wpst); break;
+        case 1: pc3r_launch<1>(g, h, xh, w, kpad, bias, y, ldy, accumulate, zero_edge, sc, st, xpst, wpst, amax); break;
+        case 2: pc3r_launch<2>(g, h, xh, w, kpad, bias, y, ldy, accumulate, zero_edge, sc, st, xpst, wpst, amax); break;
+        case 3: pc3r_launch<3>(g, h, xh, w, kpad, bias, y, ldy, accumulate, zero_edge, sc, st, xpst, wpst, amax); break;
+        case 4: pc3r_launch<4>(g, h, xh, w, kpad, bias, y, ldy, accumulate, zero_edge, sc, st, xpst, wpst, amax); break;
+        default: pc3r_launch<5>(g, h, xh, w, kpad, bias, y, ldy, accumulate, zero_edge, sc, st, xpst, wpst, amax); break;
       }
+      if (done) *done = true;
       return hipchk();
     }
   }
@@ -2690,6 +2696,37 @@ __global__ __launch_bounds__(256) void split_h16x4_kernel(const float* __restric
     *(u64*)(out + o) = (u64)h0[0] | ((u64)h0[1] << 16) | ((u64)h0[2] << 32) | ((u64)h0[3] << 48);
     *(u64*)(out + o + pst) = (u64)h1[0] | ((u64)h1[1] << 16) | ((u64)h1[2] << 32) | ((u64)h1[3] << 48);
   }
+}
+
+// svae_pcnn_conv_planes leaving max |y| in y_scale[1] (the consumer nonlinearity's fp16-plane bound): fused into
+// the row-staged kernel's epilogue, else a pass over y after the conv
+int svae_pcnn_conv_planes_amax(const void* x, int n, int hi, int wi, int cin, int ldx, int x_bf16, int64_t x_pstride,
+                               const void* wk, int kpad, int planes, const float* x_scale, const float* w_scale,
+                               const float* bias, float* y, int ho, int wo, int cout, int ldy, int kh, int kw, int s,
+                               int pt, int pl, int mode, int accumulate, int zero_edge, float* y_scale, void* stream) {
+  if (!y_scale || !y) return bad("pcnn_conv_planes_amax: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(y_scale + 1, 0, sizeof(float), st) != hipSuccess) return hipchk();
+  bool done = false;
+  if (x && wk && x_scale && w_scale && x_bf16 && planes == 2 && x_pstride >= 0) {
+    const PcScale sc{x_scale, w_scale};
+    const int rc = pcnn_conv_hp(x, n, hi, wi, cin, ldx, x_pstride, wk, kpad, (long long)kh * kw * cout * kpad, sc, bias,
+                                y, ho, wo, cout, ldy, kh, kw, s, pt, pl, mode, accumulate, zero_edge, stream,
+                                (unsigned*)(y_scale + 1), &done);
+    if (rc < 0) return rc;
+    if (rc == 0 && done) return 0;
+    if (rc == 0) {  // (ran on pc_conv3 HP: the pass below)
+      hipLaunchKernelGGL(absmax_kernel, dim3(blocks_for((long long)n * ho * wo * cout, 256, 2048)), dim3(256), 0, st, y,
+                         (long long)n * ho * wo, cout, ldy, (unsigned*)(y_scale + 1));
+      return hipchk();
+    }
+  }
+  const int rc = svae_pcnn_conv_planes(x, n, hi, wi, cin, ldx, x_bf16, x_pstride, wk, kpad, planes, x_scale, w_scale,
+                                       bias, y, ho, wo, cout, ldy, kh, kw, s, pt, pl, mode, accumulate, zero_edge, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(absmax_kernel, dim3(blocks_for((long long)n * ho * wo * cout, 256, 2048)), dim3(256), 0, st, y,
+                     (long long)n * ho * wo, cout, ldy, (unsigned*)(y_scale + 1));
+  return hipchk();
 }
 
 static int pcnn_split(const float* x, int64_t rows, int c, int ldx, int planes, void* out, int ldo, int out_bf16,
@@ -2870,6 +2907,77 @@ int svae_pcnn_nonlin_absmax(const float* x, int64_t rows, int c, int ldx, int ki
                             uint64_t seed, float* y, int ldy, float* h16_scale, void* stream) {
   if (!h16_scale) return bad("pcnn_nonlin_absmax: bad arguments");
   return pcnn_nonlin(x, rows, c, ldx, kind, mask, keep, seed, y, ldy, 0, h16_scale, stream);
+}
+
+// the nonlinearity (with the seeded dropout) writing its output straight as the two scaled fp16 planes of the
+// consuming conv's operand: the planes' exponent from a bound on max |y| known before the pass -- max |x| (left
+// by x's producer, x_scale[1]), 1 for elu / concat_elu, over keep -- instead of the fp32 output, its absmax and a
+// split pass.  h16_scale <- [2^-s, the bound]
+__global__ __launch_bounds__(256) void nonlin4_h16_kernel(const float* __restrict__ x, long long rows, int c, int ldx,
+                                                          int kind, const float* __restrict__ mask, float keep,
+                                                          unsigned long long seed, float mask_max,
+                                                          const float* __restrict__ x_scale, __bf16* __restrict__ out,
+                                                          int ldo, float* h16) {
+  const bool hashed = !mask && keep < 1.f;
+  const float inv = 1.f / keep;
+  float bound = x_scale[1];
+  if (kind != 0) bound = fmaxf(bound, 1.f);
+  bound = bound * mask_max * (1.f + 0x1p-20f);  // (rounded up: every |y| <= bound)
+  const int sh = h16_shift(__float_as_uint(bound));
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    h16[0] = ldexpf(1.f, -sh);
+    h16[1] = bound;
+  }
+  const int q = c >> 2, cy = kind == 2 ? 2 * c : c;
+  const long long pst = rows * ldo;
+  const long long r0 = (long long)blockIdx.x * NL_RPB;
+  const int nr = (int)(rows - r0 < NL_RPB ? rows - r0 : NL_RPB);
+  for (int j = threadIdx.x; j < nr * q; j += 256) {
+    const int rr = j / q;
+    const int ch = (j - rr * q) * 4;
+    const long long r = r0 + rr;
+    f32x4 a, b = {0.f, 0.f, 0.f, 0.f};
+    nl_fwd4(*(const f32x4*)(x + r * ldx + ch), kind, a, b);
+    if (mask) {
+      a *= *(const f32x4*)(mask + r * cy + ch);
+      if (kind == 2) b *= *(const f32x4*)(mask + r * cy + c + ch);
+    } else if (hashed) {
+      a *= drop_scale4(seed, (unsigned long long)(r * cy + ch), keep, inv);
+      if (kind == 2) b *= drop_scale4(seed, (unsigned long long)(r * cy + c + ch), keep, inv);
+    }
+    for (int half = 0; half < (kind == 2 ? 2 : 1); ++half) {
+      const f32x4 v = half ? b : a;
+      unsigned short h0[4], h1[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float t = ldexpf(v[e], sh);
+        const _Float16 u = (_Float16)t;
+        const _Float16 l = (_Float16)(t - (float)u);
+        h0[e] = __builtin_bit_cast(unsigned short, u);
+        h1[e] = __builtin_bit_cast(unsigned short, l);
+      }
+      const long long o = r * ldo + ch + half * c;
+      *(u64*)(out + o) = (u64)h0[0] | ((u64)h0[1] << 16) | ((u64)h0[2] << 32) | ((u64)h0[3] << 48);
+      *(u64*)(out + o + pst) = (u64)h1[0] | ((u64)h1[1] << 16) | ((u64)h1[2] << 32) | ((u64)h1[3] << 48);
+    }
+  }
+}
+
+int svae_pcnn_nonlin_h16(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, float mask_max,
+                         float keep, uint64_t seed, const float* x_scale, void* out, int ldo, float* h16_scale,
+                         void* stream) {
+  const int cy = kind == 2 ? 2 * c : c;
+  if (!x || !x_scale || !out || !h16_scale || rows < 1 || c < 1 || kind < 0 || kind > 2 || ldx < c || ldo < cy ||
+      !(keep > 0.f) || keep > 1.f || c % 4 || ldx % 4 || ldo % 4 || !al16(x) || ((uintptr_t)out & 7) ||
+      (mask && (!al16(mask) || !(mask_max >= 0.f))))
+    return bad("pcnn_nonlin_h16: bad arguments");
+  // the largest factor the dropout applies: the mask tensor's maximum, or 1 / keep for the in-kernel mask
+  const float mmax = mask ? (mask_max > 0.f ? mask_max : 1.f) : 1.f / keep;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(nonlin4_h16_kernel, dim3((unsigned)((rows + NL_RPB - 1) / NL_RPB)), dim3(256), 0, st, x,
+                     (long long)rows, c, ldx, kind, mask, keep, (unsigned long long)seed, mmax, x_scale, (__bf16*)out,
+                     ldo, h16_scale);
+  return hipchk();
 }
 
 int svae_pcnn_nonlin_bwd(const float* x, int64_t rows, int c, int ldx, int kind, const float* mask, float keep,

@@ -60,12 +60,13 @@ class DropMask:
 class Act:
     """An NHWC activation: ``buf`` [n*h*w][ld] fp32 (or bf16: a nonlinearity output read only by the
     bf16-MFMA convs), channels [off, off + c)."""
-    __slots__ = ("buf", "off", "c", "ld", "n", "h", "w", "amax")
+    __slots__ = ("buf", "off", "c", "ld", "n", "h", "w", "amax", "planes")
 
     def __init__(self, buf, c, n, h, w, off=0, ld=None, amax=None):
         self.buf, self.c, self.n, self.h, self.w, self.off = buf, c, n, h, w, off
         self.ld = c if ld is None else ld
         self.amax = amax  # (split mode) [2] floats, [1] = max|this activation| from its producer, or None
+        self.planes = None  # (split mode) its fp16 planes written by its producer (PixelCNNpp._planes' tuple)
 
     @property
     def rows(self):
@@ -191,6 +192,7 @@ class PixelCNNpp:
         # (opt-in: measured slower, 804 vs 882 img/s; bf16 head only)
         self.bf16_grads = bool(bf16_grads)
         self._nl_src, self._bias_of, self._bf16_grad = {}, {}, set()
+        self._mask_max = {}
         # operand planes of the conv / nin GEMMs: 1 = bf16 MFMA operands; 3 = the split mode (include/svae_pcnn.h):
         # fp32-grade products, nn.py:189-252 in fp32 -- two scaled fp16 planes per operand (3 fp16-MFMA
         # products) for the layers whose channel counts allow 16-bit storage (h16), else 3 bf16 planes (6)
@@ -306,7 +308,7 @@ class PixelCNNpp:
         return _lib.stream_ptr()
 
     def _wconv(self, x, name, cout, kh, kw, s, pt, pl, mode=0, ho=None, wo=None, zero_edge=0, out=None,
-               init_scale=1.0):
+               init_scale=1.0, amax=False):
         """Weight-normed conv / deconv / dense (nn.py:160-252) as a gather GEMM; returns the output Act
         (or accumulates into ``out``, whose existing values it adds to)."""
         L = self.L
@@ -339,8 +341,17 @@ class PixelCNNpp:
         if pr:  # bench.py's live roofline probe: an event pair around this forward conv launch
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        self._conv(x, xs, wkf, kf, wsc, _p(self.P, off_b), out.ptr(), ho, wo, cout, out.ld, kh, kw, s, pt, pl, mode,
-                   1 if acc else 0, zero_edge)
+        if amax and xs is not None and wsc is not None and out.off == 0:
+            # (the last writer of an activation a split-mode nonlinearity reads: max |out| for its planes' bound)
+            out.amax = torch.empty(2, dtype=torch.float32, device=self.dev)
+            buf, ld, bf, pst, P_, xsc = xs
+            _ck(L.svae_pcnn_conv_planes_amax(ctypes.c_void_p(buf.data_ptr()), x.n, x.h, x.w, x.c, ld, bf, pst,
+                                             ctypes.c_void_p(wkf.data_ptr()), kf, P_, _p(xsc), _p(wsc),
+                                             _p(self.P, off_b), out.ptr(), ho, wo, cout, out.ld, kh, kw, s, pt, pl, mode,
+                                             1 if acc else 0, zero_edge, _p(out.amax), st))
+        else:
+            self._conv(x, xs, wkf, kf, wsc, _p(self.P, off_b), out.ptr(), ho, wo, cout, out.ld, kh, kw, s, pt, pl, mode,
+                       1 if acc else 0, zero_edge)
         if pr:
             e1.record()
             nprod = 1 if xs is None else xs[4] * (xs[4] + 1) // 2  # MFMA launches per algorithmic product
@@ -410,6 +421,8 @@ class PixelCNNpp:
         plane stride, planes, scale) -- the two scaled fp16 planes (h16; scale = [2^-s, max|a|]), else
         ``self.planes`` bf16 planes (16-bit where the bf16-operand kernels take them: c % 8 == 0, else fp32)."""
         if isinstance(a, Act):
+            if a.planes is not None:  # written as planes by its producer (svae_pcnn_nonlin_h16)
+                return a.planes
             assert not a.bf, "split mode: activations are fp32"
             src, rows, c, ld = a.ptr(), a.rows, a.c, a.ld
             if h16 and a.amax is not None:  # its producer left max|a| (svae_pcnn_nonlin_absmax): no absmax pass
@@ -525,13 +538,30 @@ class PixelCNNpp:
         k = NL_KIND[kind]
         c = 2 * x.c if k == 2 else x.c
         bf = self.planes == 1 and c % 8 == 0 and x.c % 4 == 0 and x.ld % 4 == 0
-        buf = torch.empty(x.rows, c, dtype=torch.bfloat16 if bf else torch.float32, device=self.dev)
-        y = Act(buf, c, x.n, x.h, x.w)
         if isinstance(mask, DropMask):  # drawn in the kernel from (seed, keep)
             mp, keep, seed = None, mask.keep, mask.seed
         else:
             mp, keep, seed = _p(mask), 1.0, 0
-        if (self.planes > 1 and self.h16 and self.fuse_absmax and c % 8 == 0 and x.c % 4 == 0 and x.ld % 4 == 0
+        if (self.planes > 1 and self.h16 and self.fuse_absmax and x.amax is not None and c % 8 == 0 and x.c % 4 == 0
+                and x.ld % 4 == 0 and x.buf.dtype == torch.float32 and not self._init
+                and x.buf.data_ptr() % 16 == 0 and x.off % 4 == 0):
+            # the split mode's conv input straight as its fp16 planes: the exponent from x's producer's max |x|
+            # (no fp32 y, no absmax, no split pass; y is read only by the consuming conv)
+            pl = torch.empty(2 * x.rows * c, dtype=torch.bfloat16, device=self.dev)
+            psc = torch.empty(2, dtype=torch.float32, device=self.dev)
+            mmax = self._mask_max.get(id(mask), 0.0) if mp is not None else 0.0
+            _ck(self.L.svae_pcnn_nonlin_h16(x.ptr(), x.rows, x.c, x.ld, k, mp, float(mmax), keep, seed, _p(x.amax),
+                                            ctypes.c_void_p(pl.data_ptr()), c, _p(psc), self._st()))
+            y = Act(pl, c, x.n, x.h, x.w)
+            y.planes = (pl, c, 1, x.rows * c, 2, psc)
+            self._keep.append(y)
+            buf = None
+        else:
+            buf = torch.empty(x.rows, c, dtype=torch.bfloat16 if bf else torch.float32, device=self.dev)
+            y = Act(buf, c, x.n, x.h, x.w)
+        if buf is None:
+            pass
+        elif (self.planes > 1 and self.h16 and self.fuse_absmax and c % 8 == 0 and x.c % 4 == 0 and x.ld % 4 == 0
                 and x.buf.dtype == torch.float32):
             # the split mode's conv input: the kernel also leaves max|y| for its fp16 planes (bitwise the pass)
             y.amax = torch.empty(2, dtype=torch.float32, device=self.dev)
@@ -636,9 +666,12 @@ class PixelCNNpp:
     def _gated_resnet(self, x, h, kh, kw, a=None):
         nl = self.s["nl"]
         pt, pl = kh - 1, (kw - 1) // 2 if kw == 3 else kw - 1
-        c1 = self._wconv(self._nonlin(x, nl), self._nm("conv2d"), x.c, kh, kw, 1, pt, pl)
+        # (the split mode: c1's last writer leaves max |c1|, so the dropout nonlinearity below writes its fp16
+        #  planes directly, svae_pcnn_nonlin_h16)
+        c1 = self._wconv(self._nonlin(x, nl), self._nm("conv2d"), x.c, kh, kw, 1, pt, pl, amax=a is None)
         if a is not None:
-            self._dense_into(self._nonlin(a, nl), self._nm("dense"), c1)
+            v = self._dense_into(self._nonlin(a, nl), self._nm("dense"), c1, amax=True)
+            c1.amax = v.amax
         # training-pass dropout (nn.py:273-274) fused into the nonlinearity
         mask = self._next_mask(c1.rows, 2 * c1.c if nl == "concat_elu" else c1.c)
         t2 = self._nonlin(c1, nl, mask)
@@ -656,7 +689,9 @@ class PixelCNNpp:
         if self._masks is not None:
             m = next(self._masks)
             if not isinstance(m, DropMask):
+                mx = float(np.max(m)) if isinstance(m, np.ndarray) else float(torch.as_tensor(m).max())
                 m = torch.as_tensor(m, dtype=torch.float32, device=self.dev).reshape(rows, c).contiguous()
+                self._mask_max[id(m)] = mx  # (its largest factor: the planes' bound of svae_pcnn_nonlin_h16)
         elif self._dropout_p > 0.0:
             m = DropMask(rows, c, 1.0 - self._dropout_p, int(torch.randint(0, 2 ** 62, (1,)).item()))
             if self.keep_masks:
@@ -666,8 +701,10 @@ class PixelCNNpp:
         self.last_masks.append(m)
         return m
 
-    def _dense_into(self, x, name, out):
-        self._wconv(self._view(x, x.rows, 1, 1), name, out.c, 1, 1, 1, 0, 0, out=self._view(out, out.rows, 1, 1))
+    def _dense_into(self, x, name, out, amax=False):
+        v = self._view(out, out.rows, 1, 1)
+        self._wconv(self._view(x, x.rows, 1, 1), name, out.c, 1, 1, 1, 0, 0, out=v, amax=amax)
+        return v
 
     def _nm(self, kind):
         i = self._cnt.get(kind, 0)
@@ -686,6 +723,7 @@ class PixelCNNpp:
         self._tape, self._g, self._keep, self._same, self._cnt = [], {}, [], {}, {}
         self._nograd = set()
         self._nl_src, self._bias_of, self._bf16_grad = {}, {}, set()
+        self._mask_max = {}
         B, H, W = x.shape[0], s["H"], s["W"]
         F, R = s["F"], s["R"]
         rows = B * H * W

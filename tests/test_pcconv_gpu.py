@@ -379,3 +379,36 @@ def test_pcnn_colsum_absmax_is_colsum_plus_the_absmax_pass(rows, c, ld, acc):
         p0, sc0 = _planes(L, dense, "h16")
         torch.cuda.synchronize()
         assert torch.equal(p0.view(torch.int16), p1.view(torch.int16)) and torch.equal(sc0, sc)
+
+
+@pytest.mark.parametrize("kind,keep,tensor_mask", [(0, 1.0, False), (0, 0.7, False), (0, 0.7, True), (1, 0.7, False),
+                                                   (2, 1.0, False)])
+def test_pcnn_nonlin_h16_planes_hold_the_nonlinearity(kind, keep, tensor_mask):
+    """svae_pcnn_nonlin_h16 (the split head's conv input written straight as fp16 planes, the exponent from a bound
+    on max|y| known before the pass): the planes sum to svae_pcnn_nonlin's fp32 output within 2^-21 of the bound
+    (two fp16 planes: 22 bits of the scaled value) and the bound covers max|y| -- for the in-kernel seeded dropout
+    and for a mask tensor."""
+    L = pkg_mod("_lib")
+    rows, c = 4096, 40
+    g = torch.Generator(device="cuda").manual_seed(kind * 10 + int(keep * 10))
+    x = torch.randn(rows, c, device="cuda", generator=g) * 3
+    cy = 2 * c if kind == 2 else c
+    vp = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())
+    mask = None
+    if tensor_mask:
+        mask = (torch.rand(rows, cy, device="cuda", generator=g) < keep).float() / keep
+    y = torch.empty(rows, cy, device="cuda")
+    L.check(L.lib().svae_pcnn_nonlin(vp(x), rows, c, c, kind, vp(mask), 1.0 if tensor_mask else keep, 77, vp(y), cy, 0,
+                                     L.stream_ptr()))
+    xs = torch.tensor([0.0, float(x.abs().max())], device="cuda")
+    pl = torch.empty(2, rows, cy, dtype=torch.float16, device="cuda")
+    sc = torch.empty(2, device="cuda")
+    mmax = float(mask.max()) if tensor_mask else 0.0
+    L.check(L.lib().svae_pcnn_nonlin_h16(vp(x), rows, c, c, kind, vp(mask), mmax, 1.0 if tensor_mask else keep, 77,
+                                         vp(xs), vp(pl), cy, vp(sc), L.stream_ptr()))
+    torch.cuda.synchronize()
+    bound = float(sc[1])
+    assert bound >= float(y.abs().max())
+    rec = (pl[0].double() + pl[1].double()) * float(sc[0])
+    err = float((rec - y.double()).abs().max())
+    assert err <= bound * 2.0 ** -21, (err, bound)
