@@ -157,6 +157,9 @@ int svae_pcnn_dropout_mask(int64_t n, float keep, uint64_t seed, float* out, voi
  * out = x + a . sigmoid(b). */
 int svae_pcnn_gate(const float* x, int ldx, const float* c2, const float* hp, int64_t rows, int pix_per_img, int f,
                    float* out, int ldo, void* stream);
+/* svae_pcnn_gate leaving max |out| in out_scale[1] (the bound svae_pcnn_nonlin_h16 takes for out's planes). */
+int svae_pcnn_gate_amax(const float* x, int ldx, const float* c2, const float* hp, int64_t rows, int pix_per_img, int f,
+                        float* out, int ldo, float* out_scale, void* stream);
 /* its backward from the saved c2 and hp: dc2 [rows][2f] = [dout . sig(b), dout . a . sig'(b)]
  * (the residual's gradient dx is dout itself), fp32 or bf16 (dc2_bf16 = 1); dhp (may be NULL): the
  * per-image sums of dc2, [nimg][2f] (d loss / d (h . hw)); dsum (may be NULL): its sums over all rows

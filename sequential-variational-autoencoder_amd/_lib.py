@@ -165,6 +165,7 @@ def _load(path):
         "svae_pcnn_nonlin_bwd": ([vp, i64, i32, i32, i32, vp, f32, u64, vp, i32, vp, i32, i32, i32, vp, vp, vp], i32),
         "svae_pcnn_dropout_mask": ([i64, f32, u64, vp, vp], i32),
         "svae_pcnn_gate": ([vp, i32, vp, vp, i64, i32, i32, vp, i32, vp], i32),
+        "svae_pcnn_gate_amax": ([vp, i32, vp, vp, i64, i32, i32, vp, i32, vp, vp], i32),
         "svae_pcnn_gate_bwd": ([vp, vp, vp, i32, i64, i32, i32, vp, i32, vp, vp, vp, vp], i32),
         "svae_pcnn_gemm_small": ([vp, i32, i32, vp, i32, i32, vp, i32, i32, i32, i32, f32, vp], i32),
         "svae_pcnn_imgsum": ([vp, i32, i32, i32, i32, vp, vp, vp], i32),
@@ -201,7 +202,7 @@ EXPORTED = ["svae_param_count", "svae_param_layout", "svae_create", "svae_destro
 # include/svae_pcnn.h (the PixelCNN++ head)
 PCNN_EXPORTED = ["svae_pcnn_wnorm", "svae_pcnn_wnorm_bwd", "svae_pcnn_conv", "svae_pcnn_conv_wgrad", "svae_pcnn_colsum",
                  "svae_pcnn_colsum_absmax", "svae_pcnn_im2col_h16", "svae_pcnn_conv_planes_amax",
-                 "svae_pcnn_nonlin_h16",
+                 "svae_pcnn_nonlin_h16", "svae_pcnn_gate_amax",
                  "svae_pcnn_mask_edge", "svae_pcnn_nonlin", "svae_pcnn_nonlin_bwd", "svae_pcnn_gate",
                  "svae_pcnn_gate_bwd", "svae_pcnn_gemm_small", "svae_pcnn_imgsum", "svae_pcnn_copy",
                  "svae_pcnn_pad_ones", "svae_pcnn_mixlogistic", "svae_pcnn_sum", "svae_pcnn_sample",

@@ -1746,9 +1746,11 @@ __device__ __forceinline__ f32x4 sigm4(f32x4 v) {
   for (int e = 0; e < 4; ++e) r[e] = 1.f / (1.f + expf(-v[e]));
   return r;
 }
+// amax != NULL: max |out| into *amax (the bound of the next split-mode nonlinearity's fp16 planes)
 __global__ __launch_bounds__(256) void gate4_kernel(const float* __restrict__ x, int ldx, const float* __restrict__ c2,
                                                     const float* __restrict__ hp, long long rows, int per_img, int f,
-                                                    float* __restrict__ out, int ldo) {
+                                                    float* __restrict__ out, int ldo, unsigned* __restrict__ amax) {
+  float am = 0.f;
   const int q = f >> 2;
   const long long r0 = (long long)blockIdx.x * GT_RPB;
   const int nr = (int)(rows - r0 < GT_RPB ? rows - r0 : GT_RPB);
@@ -1762,8 +1764,11 @@ __global__ __launch_bounds__(256) void gate4_kernel(const float* __restrict__ x,
       a += *(const f32x4*)(hp + img * 2 * f + ch);
       b += *(const f32x4*)(hp + img * 2 * f + f + ch);
     }
-    *(f32x4*)(out + r * ldo + ch) = *(const f32x4*)(x + r * ldx + ch) + a * sigm4(b);
+    const f32x4 o = *(const f32x4*)(x + r * ldx + ch) + a * sigm4(b);
+    *(f32x4*)(out + r * ldo + ch) = o;
+    am = fmaxf(am, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
   }
+  if (amax) block_absmax_put(am, amax);
 }
 __global__ __launch_bounds__(256) void gate4_bwd_kernel(const float* __restrict__ c2, const float* __restrict__ hp,
                                                         const float* __restrict__ dout, int lddo, long long rows,
@@ -3010,19 +3015,33 @@ int svae_pcnn_nonlin_bwd(const float* x, int64_t rows, int c, int ldx, int kind,
   return hipchk();
 }
 
-int svae_pcnn_gate(const float* x, int ldx, const float* c2, const float* hp, int64_t rows, int pix_per_img, int f,
-                   float* out, int ldo, void* stream) {
+static int pcnn_gate(const float* x, int ldx, const float* c2, const float* hp, int64_t rows, int pix_per_img, int f,
+                     float* out, int ldo, float* out_scale, void* stream) {
   if (!x || !c2 || !out || rows < 1 || f < 1 || pix_per_img < 1 || rows % pix_per_img) return bad("pcnn_gate: bad arguments");
   hipStream_t st = (hipStream_t)stream;
+  unsigned* amax = out_scale ? (unsigned*)(out_scale + 1) : nullptr;
+  if (amax && hipMemsetAsync(amax, 0, sizeof(float), st) != hipSuccess) return hipchk();
   if (f % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0 && pix_per_img % GT_RPB == 0 && al16(x) && al16(c2) && al16(out) &&
       (!hp || al16(hp))) {
     hipLaunchKernelGGL(gate4_kernel, dim3((unsigned)(rows / GT_RPB)), dim3(256), 0, st, x, ldx, c2, hp, (long long)rows,
-                       pix_per_img, f, out, ldo);
+                       pix_per_img, f, out, ldo, amax);
     return hipchk();
   }
   hipLaunchKernelGGL(gate_kernel, dim3(blocks_for(rows * f)), dim3(256), 0, st, x, ldx, c2, hp, (long long)rows,
                      pix_per_img, f, out, ldo);
+  if (amax)
+    hipLaunchKernelGGL(absmax_kernel, dim3(blocks_for(rows * f, 256, 2048)), dim3(256), 0, st, out, (long long)rows, f,
+                       ldo, amax);
   return hipchk();
+}
+int svae_pcnn_gate(const float* x, int ldx, const float* c2, const float* hp, int64_t rows, int pix_per_img, int f,
+                   float* out, int ldo, void* stream) {
+  return pcnn_gate(x, ldx, c2, hp, rows, pix_per_img, f, out, ldo, nullptr, stream);
+}
+int svae_pcnn_gate_amax(const float* x, int ldx, const float* c2, const float* hp, int64_t rows, int pix_per_img, int f,
+                        float* out, int ldo, float* out_scale, void* stream) {
+  if (!out_scale) return bad("pcnn_gate_amax: bad arguments");
+  return pcnn_gate(x, ldx, c2, hp, rows, pix_per_img, f, out, ldo, out_scale, stream);
 }
 
 int svae_pcnn_gate_bwd(const float* c2, const float* hp, const float* dout, int lddo, int64_t rows, int pix_per_img,

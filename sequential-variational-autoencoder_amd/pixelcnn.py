@@ -300,6 +300,8 @@ class PixelCNNpp:
     def _view(self, a, n, h, w):
         """``a`` reshaped to another row space (same buffer and gradient)."""
         v = Act(a.buf, a.c, n, h, w, a.off, a.ld, a.amax if n * h * w == a.rows else None)
+        if n * h * w == a.rows:
+            v.planes = a.planes  # (the same [rows][c] planes)
         self._same[id(v)] = a
         self._keep.append(v)
         return v
@@ -626,7 +628,12 @@ class PixelCNNpp:
         _ck(self.L.svae_pcnn_gemm_small(_p(h), K, 0, _p(self.P, off_hw), 2 * F, 0, _p(hp), 2 * F, x.n, 2 * F, K, 0.0,
                                         st))
         y = Act(self._new(x.rows, F), F, x.n, x.h, x.w)
-        _ck(self.L.svae_pcnn_gate(x.ptr(), x.ld, c2.ptr(), _p(hp), x.rows, x.h * x.w, F, y.ptr(), F, st))
+        if self.planes > 1 and self.h16 and self.fuse_absmax:  # max |y|: the next nonlinearity writes fp16 planes
+            y.amax = torch.empty(2, dtype=torch.float32, device=self.dev)
+            _ck(self.L.svae_pcnn_gate_amax(x.ptr(), x.ld, c2.ptr(), _p(hp), x.rows, x.h * x.w, F, y.ptr(), F,
+                                           _p(y.amax), st))
+        else:
+            _ck(self.L.svae_pcnn_gate(x.ptr(), x.ld, c2.ptr(), _p(hp), x.rows, x.h * x.w, F, y.ptr(), F, st))
         if self._record:
             def bwd():
                 if not self._has_grad(y):
