@@ -309,14 +309,15 @@ def _pv_throughput(PV, B, dtype, steps, warmup, probe_cap):
 
 def _pv_roofline(probe, planes, head_flops, vae_flops, ms, key):
     """The head's forward convolutions (event pairs around each probed launch): algorithmic FLOPs per
-    second; in the split mode one algorithmic conv is 6 plane-product launches (issued = 6 x achieved)."""
+    second; in the split mode one algorithmic conv is 3 fp16 plane products in one launch (issued = 3 x achieved;
+    6 bf16 ones where channels % 8 != 0)."""
     pflops = sum(f for f, _, _, _ in probe)
     iflops = sum(f * k for f, _, _, k in probe)  # the MFMA work the plane products really run
     pms = sum(e0.elapsed_time(e1) for _, e0, e1, _ in probe)
     if pms <= 0:
         return None
     ach = pflops / (pms / 1e3) / 1e12
-    kern = "pc_conv3_kernel + pc_conv2_kernel"
+    kern = "pc_conv3r_kernel + pc_conv3_kernel + pc_conv2_kernel"
     traffic, tsrc = pmc_traffic(kern, key)
     return {"bound": "mfma", "achieved": round(ach, 3), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 5), "traffic": traffic, "traffic_source": tsrc,
