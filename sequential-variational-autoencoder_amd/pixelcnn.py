@@ -424,6 +424,8 @@ class PixelCNNpp:
         ``self.planes`` bf16 planes (16-bit where the bf16-operand kernels take them: c % 8 == 0, else fp32)."""
         if isinstance(a, Act):
             if a.planes is not None:  # written as planes by its producer (svae_pcnn_nonlin_h16)
+                if not h16:
+                    raise RuntimeError("an fp16-plane activation read by a non-fp16-plane layer")
                 return a.planes
             assert not a.bf, "split mode: activations are fp32"
             src, rows, c, ld = a.ptr(), a.rows, a.c, a.ld
@@ -533,7 +535,7 @@ class PixelCNNpp:
         y = self._wconv(self._view(x, x.rows, 1, 1), name, cout, 1, 1, 1, 0, 0, init_scale=init_scale)
         return self._view(y, x.n, x.h, x.w)
 
-    def _nonlin(self, x, kind, mask=None):
+    def _nonlin(self, x, kind, mask=None, planes_out=False):
         """y = f(x) (* the dropout keep-mask, fused).  Every nonlinearity output of the network is read
         only by convolutions (bf16 MFMA operands), so y is stored as bf16 when its channels allow it:
         the conv result is bitwise the one from fp32 storage (nn.py:270-274: dropout before the conv)."""
@@ -544,7 +546,10 @@ class PixelCNNpp:
             mp, keep, seed = None, mask.keep, mask.seed
         else:
             mp, keep, seed = _p(mask), 1.0, 0
-        if (self.planes > 1 and self.h16 and self.fuse_absmax and x.amax is not None and c % 8 == 0 and x.c % 4 == 0
+        # planes_out: the caller's consumer is an fp16-plane conv (channels % 8 == 0 both ways), so y may exist as
+        # its planes only
+        if (planes_out and self.planes > 1 and self.h16 and self.fuse_absmax and x.amax is not None and c % 8 == 0
+                and x.c % 4 == 0
                 and x.ld % 4 == 0 and x.buf.dtype == torch.float32 and not self._init
                 and x.buf.data_ptr() % 16 == 0 and x.off % 4 == 0):
             # the split mode's conv input straight as its fp16 planes: the exponent from x's producer's max |x|
@@ -675,13 +680,15 @@ class PixelCNNpp:
         pt, pl = kh - 1, (kw - 1) // 2 if kw == 3 else kw - 1
         # (the split mode: c1's last writer leaves max |c1|, so the dropout nonlinearity below writes its fp16
         #  planes directly, svae_pcnn_nonlin_h16)
-        c1 = self._wconv(self._nonlin(x, nl), self._nm("conv2d"), x.c, kh, kw, 1, pt, pl, amax=a is None)
+        hp = x.c % 8 == 0  # (every conv of the resnet on fp16 planes: F and 2F channels)
+        c1 = self._wconv(self._nonlin(x, nl, planes_out=hp), self._nm("conv2d"), x.c, kh, kw, 1, pt, pl,
+                         amax=a is None)
         if a is not None:
-            v = self._dense_into(self._nonlin(a, nl), self._nm("dense"), c1, amax=True)
+            v = self._dense_into(self._nonlin(a, nl, planes_out=hp), self._nm("dense"), c1, amax=True)
             c1.amax = v.amax
         # training-pass dropout (nn.py:273-274) fused into the nonlinearity
         mask = self._next_mask(c1.rows, 2 * c1.c if nl == "concat_elu" else c1.c)
-        t2 = self._nonlin(c1, nl, mask)
+        t2 = self._nonlin(c1, nl, mask, planes_out=hp)
         c2 = self._wconv(t2, self._nm("conv2d"), 2 * x.c, kh, kw, 1, pt, pl, init_scale=0.1)
         if self.bf16_grads:  # c1 / c2 feed one op each: their gradients may be written bf16 by it
             self._bf16_grad.update((id(self._root(c1)), id(self._root(c2))))
