@@ -48,7 +48,7 @@ PMC_FILES = {
     "lsun/bf16": ["profiles/r04_final_lsun_pmc_traffic.json", "profiles/r04_v1_lsun_pmc_traffic.json"],
     "lsun/bf16x6": ["profiles/r05_fl6_pmc_traffic.json"],
     "c_pixelvae/bf16": ["profiles/r04_final_pv_pmc_traffic.json", "profiles/r04_v1_pv_pmc_traffic.json"],
-    "c_pixelvae/bf16x6": ["profiles/r05_gpv_pmc_traffic.json", "profiles/r05_fpv_pmc_traffic.json"],
+    "c_pixelvae/bf16x6": ["profiles/r06_gpv_pmc_traffic.json", "profiles/r05_gpv_pmc_traffic.json"],
 }
 
 
