@@ -20,8 +20,13 @@ import time
 # Hardware queues per process, before anything initialises HIP: the engine's three streams plus RCCL's own
 # (N > 1) share HIP's default 4 queues, and streams sharing a queue serialise.  Measured with an RCCL process
 # group in the process (tools/dist_overhead.py, profiles/r06_d_overhead.txt): 19.30 ms/step at 4 queues,
-# 15.48 at 8 (15.54 / 15.50 without a process group: N = 1 is unaffected)
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# 15.48 at 8 (15.54 / 15.50 without a process group: N = 1 is unaffected).  At least 8: the GPU boxes export 4
+try:
+    _hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
+except ValueError:
+    _hwq = 0
+if _hwq < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 import numpy as np
 import torch
