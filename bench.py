@@ -49,7 +49,7 @@ SECONDARY_KID = "KID_WHALO2_S1"
 # FETCH rules) per workload; a workload never borrows another's traffic (LSUN read CelebA's)
 PMC_FILES = {
     "celeba/bf16": ["profiles/r05_gbf_pmc_traffic.json", "profiles/r05_fbf_pmc_traffic.json"],
-    "celeba/bf16x6": ["profiles/r06_g_pmc_traffic.json", "profiles/r05_g6_pmc_traffic.json"],
+    "celeba/bf16x6": ["profiles/r06_h_pmc_traffic.json", "profiles/r06_g_pmc_traffic.json"],
     "lsun/bf16": ["profiles/r04_final_lsun_pmc_traffic.json", "profiles/r04_v1_lsun_pmc_traffic.json"],
     "lsun/bf16x6": ["profiles/r05_fl6_pmc_traffic.json"],
     "c_pixelvae/bf16": ["profiles/r04_final_pv_pmc_traffic.json", "profiles/r04_v1_pv_pmc_traffic.json"],
