@@ -559,17 +559,26 @@ def main():
     torch.cuda.synchronize()
     # time-based warm-up: keep stepping until --warmup-seconds of warm-up have run, so the
     # clock and caches settle before the timed region; every rank runs the same count (each step all-reduces)
-    wdt = time.perf_counter() - tw
-    per = wdt / max(1, args.warmup)
-    extra = max(0, int(math.ceil((args.warmup_seconds - wdt) / max(per, 1e-4)))) if args.warmup_seconds > 0 else 0
-    if dist:
-        te = torch.tensor([extra], device="cuda", dtype=torch.int64)
-        dist.all_reduce(te, op=dist.ReduceOp.MAX)
-        extra = int(te.item())
-    for _ in range(extra):
-        it += 1
-        step(it)
-    torch.cuda.synchronize()
+    # (rounds of steps sized from the last round's per-step time -- the first steps run slower -- until the
+    # target is reached; each round's count is the MAX over ranks)
+    per = (time.perf_counter() - tw) / max(1, args.warmup)
+    extra = 0
+    for _round in range(8):
+        wdt = time.perf_counter() - tw
+        need = max(0, int(math.ceil((args.warmup_seconds - wdt) / max(per, 1e-4)))) if args.warmup_seconds > 0 else 0
+        if dist:
+            te = torch.tensor([need], device="cuda", dtype=torch.int64)
+            dist.all_reduce(te, op=dist.ReduceOp.MAX)
+            need = int(te.item())
+        if need == 0:
+            break
+        t0r = time.perf_counter()
+        for _ in range(need):
+            it += 1
+            step(it)
+        torch.cuda.synchronize()
+        per = (time.perf_counter() - t0r) / need
+        extra += need
     warm_s = time.perf_counter() - tw
     if dist:
         dist.barrier()
